@@ -1,0 +1,137 @@
+#!/usr/bin/env python3
+"""Headline benchmark: UNet 512x512 bf16 training throughput (images/s, whole job).
+
+Metric/config from BASELINE.json: "images/sec (whole node) UNet 512x512 bf16 at 1/2/4/8 MI355X".
+Model: the reference 4-level UNet (base 32, 7,760,097 params, random init), full training step
+(forward, BCE - log Dice loss, backward, RCCL gradient all-reduce for N>1, fused Adam step) through
+the framework's own strategy classes.  Data: synthetic images/masks generated on the GPU (a pool
+of distinct batches cycled every step; the reference's CPU JPEG decode is not part of the step).
+
+    python bench.py                                  # N=1, defaults finish in ~1-2 min
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 --master-port P \
+        bench.py --gpus N --steps K --warmup W      # one rank per GPU over RCCL (DDP)
+
+Timing: W untimed warm-up steps; then barrier + device sync, K timed steps, barrier + device sync;
+elapsed = MAX over ranks.  value = N * per_gpu_batch * K / elapsed (weak scaling).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+BASELINE_METRIC = "images/sec (whole node) UNet 512x512 bf16 at 1/2/4/8 MI355X; Dice parity"
+# measured stock PyTorch-ROCm (MIOpen, bf16 autocast, channels_last) img/s per GPU on MI355X for
+# this exact config, recorded in BASELINE.md; the reference itself publishes no number.
+STOCK_BASELINE_PER_GPU = None
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=32, help="images per GPU per step")
+    ap.add_argument("--img", type=int, default=512)
+    ap.add_argument("--backend", choices=["hip", "torch", "auto"], default="auto")
+    ap.add_argument("--model", default="unet")
+    ap.add_argument("--bucket-mb", type=float, default=8.0)
+    ap.add_argument("--pool", type=int, default=2, help="distinct synthetic batches cycled")
+    ap.add_argument("--out", default=None, help="also append the JSON line to this file")
+    return ap.parse_args()
+
+
+def main():
+    a = parse()
+    import torch
+    import torch.distributed as dist
+
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != a.gpus and rank == 0:
+        print(f"[bench] note: WORLD_SIZE={world} but --gpus={a.gpus}", file=sys.stderr)
+    torch.cuda.set_device(local)
+    device = torch.device(f"cuda:{local}")
+    if world > 1:
+        dist.init_process_group("nccl", init_method="env://", device_id=device)
+
+    from distributedpytorch_amd.config import TrainConfig
+    from distributedpytorch_amd.data.synthetic import synthetic_batch
+    from distributedpytorch_amd.models.unet import build_model, count_params
+    from distributedpytorch_amd.trainer import DDPStrategy, SingleDevice
+    from distributedpytorch_amd.compute import resolve_backend
+    from distributedpytorch_amd.utils import set_seed
+
+    set_seed(1234)
+    cfg = TrainConfig(train_method="DDP" if world > 1 else "singleGPU", batch_size=a.batch,
+                      img_size=(a.img, a.img), dtype="bf16", backend=a.backend, model=a.model,
+                      bucket_mb=a.bucket_mb, lr=1e-4)
+    model = build_model(a.model)
+    nparams = count_params(model)
+    strat = DDPStrategy(cfg, model, device) if world > 1 else SingleDevice(cfg, model, device)
+    backend = resolve_backend(a.backend, device)
+
+    pool = []
+    for i in range(a.pool):
+        img, mask = synthetic_batch(a.batch, a.img, a.img, 3, seed=1000 * rank + i, device=device)
+        pool.append((img, mask.float().unsqueeze(1)))
+
+    def step(i):
+        x, t = pool[i % len(pool)]
+        return strat.train_step(x, t)
+
+    t_w0 = time.perf_counter()
+    loss = None
+    for i in range(a.warmup):
+        loss = step(i)
+    torch.cuda.synchronize()
+    warm_s = time.perf_counter() - t_w0
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        loss = step(a.warmup + i)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    el = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    elapsed = float(el.item())
+    final_loss = float(loss.item()) if loss is not None else float("nan")
+
+    imgs = a.batch * world * a.steps
+    value = imgs / elapsed
+    ms = 1000.0 * elapsed / a.steps
+    vs = None
+    if STOCK_BASELINE_PER_GPU:
+        vs = round(value / (STOCK_BASELINE_PER_GPU * world), 4)
+    out = {
+        "metric": BASELINE_METRIC, "value": round(value, 2), "unit": "images/s", "n_gpus": world,
+        "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": vs, "dtype": "bf16",
+        "data": "synthetic (GPU-generated images + ellipse masks), random-init weights",
+        "config": {"model": f"{a.model} (reference 4-level UNet, base 32, {nparams} params)" if a.model == "unet"
+                   else a.model, "global_batch": a.batch * world, "per_gpu_batch": a.batch,
+                   "seq_len": a.img * a.img, "image_hw": [a.img, a.img],
+                   "parallelism": f"dp{world}", "backend": backend, "bucket_mb": a.bucket_mb},
+        "final_loss": round(final_loss, 5), "warmup_s": round(warm_s, 2),
+        "peak_mem_gb": round(torch.cuda.max_memory_allocated(device) / 2 ** 30, 2),
+    }
+    if rank == 0:
+        line = json.dumps(out)
+        print(line, flush=True)
+        if a.out:
+            with open(a.out, "a") as f:
+                f.write(line + "\n")
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

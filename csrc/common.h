@@ -1,0 +1,39 @@
+// Shared helpers for the gfx950 (MI355X / CDNA4) kernels of distributedpytorch_amd.
+// Every launcher is extern "C", takes raw device pointers + a hipStream_t, and returns hipError_t.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <stdint.h>
+
+#define DPA_API extern "C" __attribute__((visibility("default")))
+
+typedef __attribute__((ext_vector_type(8))) short bf16x8_t;   // 8 bf16 = one MFMA A/B fragment
+typedef __attribute__((ext_vector_type(4))) float f32x4_t;    // 16x16 MFMA accumulator
+typedef __attribute__((ext_vector_type(16))) float f32x16_t;  // 32x32 MFMA accumulator
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4_t;
+typedef __attribute__((ext_vector_type(2))) unsigned int u32x2_t;
+
+static __device__ __forceinline__ float bf2f(unsigned short h) {
+  return __uint_as_float(((unsigned int)h) << 16);
+}
+// round-to-nearest-even f32 -> bf16 (NaN-preserving cast; hipcc lowers to v_cvt_pk_bf16_f32)
+static __device__ __forceinline__ unsigned short f2bf(float f) {
+  __hip_bfloat16 b = __float2bfloat16(f);
+  return *reinterpret_cast<unsigned short*>(&b);
+}
+static __device__ __forceinline__ unsigned int pack_bf2(float lo, float hi) {
+  return (unsigned int)f2bf(lo) | ((unsigned int)f2bf(hi) << 16);
+}
+
+static __device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+static inline int dpa_grid(long long n, int block, int cap = 2048) {
+  long long g = (n + block - 1) / block;
+  if (g > cap) g = cap;
+  if (g < 1) g = 1;
+  return (int)g;
+}

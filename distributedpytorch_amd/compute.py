@@ -1,0 +1,77 @@
+"""Per-device forward "compute" backends and the sum-decomposed loss.
+
+The reference loss (``utils/utils.py:14-25``) is a function of four global sums over the batch:
+
+    S = [sum BCE(p,t), sum p*[t==1], sum p, sum [t==1]],   N = #pixels
+    loss = S0/N - log(2*S1 / (S2 + S3 + 1e-15))
+
+so every parallel strategy computes *partial* sums where its data lives and combines them:
+DP adds the per-device S on device 0 (= the reference's loss on the gathered batch), the pipeline
+adds per-microbatch S on the last stage (= the loss on the whole batch, like the reference MP),
+DDP uses its local S (reference per-rank semantics) or all-reduces it (``--global-dice``).
+
+Backends (block implementations, ``models.blocks``):
+* ``torch`` - stock PyTorch ops (MIOpen convs), bf16 autocast + channels_last activations.  This is
+  the measured "stock PyTorch-ROCm" baseline of BASELINE.md and the CPU path.
+* ``hip`` (``models.hip_unet.HipBlocks``) - hand-written gfx950 kernels, NHWC bf16.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from .loss import EPS
+
+
+def loss_partials_from_probs(p: torch.Tensor, t: torch.Tensor) -> torch.Tensor:
+    p = p.float()
+    t = t.float()
+    dt = (t == 1).float()
+    bce = F.binary_cross_entropy(p, t, reduction="sum")
+    return torch.stack([bce, (p * dt).sum(), p.sum(), dt.sum()])
+
+
+def loss_from_partials(S: torch.Tensor, n: int, dice: bool = True) -> torch.Tensor:
+    loss = S[0] / n
+    if dice:
+        loss = loss - torch.log(2 * S[1] / (S[2] + S[3] + EPS))
+    return loss
+
+
+class Compute:
+    """Whole-model forward on one device through a block backend (see ``models.blocks``)."""
+
+    def __init__(self, model: torch.nn.Module, blocks):
+        self.model = model
+        self.blocks = blocks
+        self.depth = model.cfg.depth
+        self.name = blocks.name
+
+    def forward_partials(self, x: torch.Tensor, t: torch.Tensor) -> torch.Tensor:
+        from .models.blocks import run_segment, n_blocks
+        return run_segment(self.blocks, 0, n_blocks(self.depth), self.depth, {"x": x}, t)["partials"]
+
+    def probs(self, x: torch.Tensor) -> torch.Tensor:
+        from .models.blocks import run_segment, n_blocks
+        return run_segment(self.blocks, 0, n_blocks(self.depth), self.depth, {"x": x}, want="probs")["probs"]
+
+
+def resolve_backend(backend: str, device) -> str:
+    device = torch.device(device)
+    if backend == "auto":
+        return "hip" if device.type == "cuda" else "torch"
+    return backend
+
+
+def make_blocks(model, backend: str = "auto", dtype: str = "bf16"):
+    dev = next(model.parameters()).device
+    backend = resolve_backend(backend, dev)
+    if backend == "hip":
+        from .models.hip_unet import HipBlocks
+        return HipBlocks(model, dtype=dtype)
+    from .models.blocks import TorchBlocks
+    return TorchBlocks(model, dtype=dtype)
+
+
+def make_compute(model, backend: str = "auto", dtype: str = "bf16") -> Compute:
+    return Compute(model, make_blocks(model, backend, dtype))

@@ -1,0 +1,121 @@
+"""Configuration + CLI.
+
+The eight reference flags are kept verbatim (reference ``train.py:15-26``):
+``-t/--train-method`` ``-v/--validation`` ``-l/--load`` ``-e/--epochs`` ``--lr/--learning-rate``
+``-b/--batch-size`` ``-c/--checkpoint`` ``-s/--seed``.  Additions (SURVEY §5 "Config / flag
+system"): image size, dtype, synthetic data, data dirs, backend (hip|torch), model preset,
+pipeline stages/microbatches, all-reduce bucket size, global-Dice option, step limits.
+
+``-t`` accepts ``singleGPU | DP | DDP | MP`` like the reference; an unknown value is an error
+(the reference silently did nothing).
+"""
+from __future__ import annotations
+
+import argparse
+import os
+from dataclasses import dataclass, field, asdict
+from typing import Optional, Tuple
+
+METHODS = ("singleGPU", "DP", "DDP", "MP")
+
+
+@dataclass
+class TrainConfig:
+    train_method: str = "singleGPU"
+    val: float = 10.0
+    load: Optional[str] = None
+    epochs: int = 10
+    lr: float = 1e-4
+    batch_size: int = 4
+    checkpoint: Optional[str] = None
+    seed: int = 42
+    # --- additions ---
+    img_size: Tuple[int, int] = (640, 960)          # (H, W); reference newsize=[960, 640] (W, H)
+    dtype: str = "bf16"                              # compute dtype: bf16 | fp32
+    backend: str = "auto"                            # hip | torch | auto
+    model: str = "unet"                              # preset name (models.unet.PRESETS)
+    synthetic: bool = False
+    synthetic_len: int = 64
+    data_dir: str = "./data"
+    out_dir: str = "."
+    device: Optional[str] = None
+    stages: int = 2                                  # pipeline stages for -t MP
+    microbatches: int = 2                            # reference MP: split_size=B/2 -> 2 microbatches
+    bucket_mb: float = 8.0                           # DDP/DP all-reduce bucket size (MiB of fp32 grads)
+    global_dice: bool = False                        # DDP: Dice over the global batch (all-reduced sums)
+    loss_scale_by_batch: bool = True                 # reference multiplies loss by batch size (A11)
+    max_steps: int = 0                               # stop after N optimizer steps (0 = full epochs)
+    num_workers: int = 0
+    log_every: int = 10
+    weight_decay: float = 1e-8
+    patience: int = 2
+    save_every_epoch: bool = True
+    resume: bool = False
+    profile: bool = False
+    cuda_graph: bool = False
+
+    def to_dict(self):
+        return asdict(self)
+
+
+def build_parser() -> argparse.ArgumentParser:
+    p = argparse.ArgumentParser(description="Train UNet on images and target masks (MI355X-native)")
+    p.add_argument("--train-method", "-t", type=str, default="singleGPU", help="singleGPU | DP | DDP | MP")
+    p.add_argument("--validation", "-v", dest="val", type=float, default=10.0,
+                   help="Percentage of data used as validation")
+    p.add_argument("--load", "-l", type=str, default=None,
+                   help="Load model from a .pth file path (the reference parsed but ignored this)")
+    p.add_argument("--epochs", "-e", type=int, default=10, help="Number of epochs")
+    p.add_argument("--learning-rate", "--lr", type=float, default=1e-4, help="Learning rate", dest="lr")
+    p.add_argument("--batch-size", "-b", type=int, default=4, help="Batch size (per process for DDP)")
+    p.add_argument("--checkpoint", "-c", type=str, default=None,
+                   help="Name (without .pth) of a checkpoint under checkpoints/ to load")
+    p.add_argument("--seed", "-s", type=int, default=42, help="Set seed for reproducibility")
+    # additions
+    p.add_argument("--img-size", type=int, nargs="+", default=[640, 960], help="H [W] of the training images")
+    p.add_argument("--dtype", choices=["bf16", "fp32"], default="bf16")
+    p.add_argument("--backend", choices=["auto", "hip", "torch"], default="auto",
+                   help="hip = hand-written MI355X kernels; torch = stock PyTorch ops")
+    p.add_argument("--model", type=str, default="unet", help="model preset: unet | unet-xl | unet-bn64 | unet-tiny")
+    p.add_argument("--synthetic", action="store_true", help="use synthetic images/masks instead of data/")
+    p.add_argument("--synthetic-len", type=int, default=64)
+    p.add_argument("--data-dir", type=str, default="./data")
+    p.add_argument("--out-dir", type=str, default=".")
+    p.add_argument("--device", type=str, default=None)
+    p.add_argument("--stages", type=int, default=2)
+    p.add_argument("--microbatches", type=int, default=2)
+    p.add_argument("--bucket-mb", type=float, default=8.0)
+    p.add_argument("--global-dice", action="store_true")
+    p.add_argument("--no-batch-loss-scale", dest="loss_scale_by_batch", action="store_false")
+    p.add_argument("--max-steps", type=int, default=0)
+    p.add_argument("--num-workers", type=int, default=0)
+    p.add_argument("--log-every", type=int, default=10)
+    p.add_argument("--resume", action="store_true", help="resume from checkpoints/<method>_last.pt")
+    p.add_argument("--profile", action="store_true", help="torch.profiler trace of a few steps")
+    p.add_argument("--cuda-graph", action="store_true", help="capture the training step in a HIP graph")
+    return p
+
+
+def parse_args(argv=None) -> TrainConfig:
+    a = build_parser().parse_args(argv)
+    if a.train_method not in METHODS:
+        raise SystemExit(f"unknown --train-method {a.train_method!r}; choose from {METHODS}")
+    size = a.img_size
+    img_size = (size[0], size[0]) if len(size) == 1 else (size[0], size[1])
+    cfg = TrainConfig(
+        train_method=a.train_method, val=a.val, load=a.load, epochs=a.epochs, lr=a.lr,
+        batch_size=a.batch_size, checkpoint=a.checkpoint, seed=a.seed, img_size=img_size,
+        dtype=a.dtype, backend=a.backend, model=a.model, synthetic=a.synthetic,
+        synthetic_len=a.synthetic_len, data_dir=a.data_dir, out_dir=a.out_dir, device=a.device,
+        stages=a.stages, microbatches=a.microbatches, bucket_mb=a.bucket_mb, global_dice=a.global_dice,
+        loss_scale_by_batch=a.loss_scale_by_batch, max_steps=a.max_steps, num_workers=a.num_workers,
+        log_every=a.log_every, resume=a.resume, profile=a.profile, cuda_graph=a.cuda_graph)
+    return cfg
+
+
+def dist_env():
+    """(rank, local_rank, world_size) from torchrun's environment (torch/distributed/run.py:191-232)."""
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    return rank, local, world

@@ -1,0 +1,220 @@
+"""UNet family with the reference's parameter names and semantics.
+
+Parity target: reference ``model/unet_parts.py:6-77`` and ``model/unet_model.py:4-62``.
+
+* ``ConvBlock`` == reference ``conv_block`` (unet_parts.py:6-17): two 3x3 pad-1 convs with bias,
+  each followed by ReLU, no BatchNorm by default.  State-dict keys ``conv_block.{0,2}.*``.
+* ``Encoder`` == unet_parts.py:19-41: ``conv1..convD`` + one shared 2x2 max-pool; returns
+  ``(pooled, skip_D, ..., skip_1)`` (deepest skip first, unet_parts.py:41).
+* ``Decoder`` == unet_parts.py:43-77: per level ConvTranspose2d(k2,s2) -> center-crop of the
+  skip -> ``cat((skip, up), 1)`` (skip first) -> ConvBlock.
+* ``UNet`` == unet_model.py:4-21: encoder -> mid -> decoder -> 1x1 ``segmap`` -> sigmoid.
+
+The default configuration (in=3, out=1, base=32, depth=4, no BN, transposed-conv up path)
+reproduces the reference's 46 tensors / 7,760,097 parameters and its exact key names,
+so checkpoints round-trip with the reference.  Variants (base width, depth, BatchNorm, bilinear
+up-sampling, the ``xl`` preset used for the 1024^2 pipeline config) are additions.
+
+This module is the *reference-semantics* implementation on stock torch ops (CPU and GPU).  The
+MI355X fast path is :mod:`distributedpytorch_amd.models.engine`, which runs the same parameters
+through hand-written HIP kernels in NHWC bf16 with an explicit backward schedule.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, asdict
+from typing import List, Sequence, Tuple
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+
+@dataclass(frozen=True)
+class UNetConfig:
+    in_channels: int = 3
+    out_channels: int = 1
+    base: int = 32
+    depth: int = 4
+    batchnorm: bool = False
+    bilinear: bool = False
+
+    @property
+    def widths(self) -> List[int]:
+        return [self.base * (2 ** i) for i in range(self.depth)]
+
+    @property
+    def mid_width(self) -> int:
+        return self.base * (2 ** self.depth)
+
+    def to_dict(self):
+        return asdict(self)
+
+
+PRESETS = {
+    # reference architecture (model/modelsummary.txt:1-72)
+    "unet": UNetConfig(),
+    # larger model used by the 1024x1024 8-stage pipeline config (BASELINE.json configs[4])
+    "unet-xl": UNetConfig(base=64, depth=5),
+    # milesial-style variant listed in model/modelsummary.txt:153-247 (BN, base 64)
+    "unet-bn64": UNetConfig(base=64, batchnorm=True),
+    # tiny config for fast CPU tests
+    "unet-tiny": UNetConfig(base=8, depth=2),
+}
+
+
+def center_crop(t: torch.Tensor, h: int, w: int) -> torch.Tensor:
+    """torchvision ``CenterCrop((h, w))`` semantics for h<=H, w<=W (unet_parts.py:58)."""
+    H, W = t.shape[-2], t.shape[-1]
+    if H == h and W == w:
+        return t
+    top = int(round((H - h) / 2.0))
+    left = int(round((W - w) / 2.0))
+    return t[..., top:top + h, left:left + w]
+
+
+class ConvBlock(nn.Module):
+    """conv3x3(+BN)+ReLU, twice.  Keys ``conv_block.{0,2}`` (no BN) / ``{0,1,3,4}`` (BN)."""
+
+    def __init__(self, insize: int, outsize: int, batchnorm: bool = False):
+        super().__init__()
+        layers: List[nn.Module] = []
+        for cin in (insize, outsize):
+            layers.append(nn.Conv2d(cin, outsize, kernel_size=3, padding=1))
+            if batchnorm:
+                layers.append(nn.BatchNorm2d(outsize))
+            layers.append(nn.ReLU())
+        self.conv_block = nn.Sequential(*layers)
+        self.batchnorm = batchnorm
+
+    def convs(self) -> List[nn.Conv2d]:
+        return [m for m in self.conv_block if isinstance(m, nn.Conv2d)]
+
+    def bns(self) -> List[nn.BatchNorm2d]:
+        return [m for m in self.conv_block if isinstance(m, nn.BatchNorm2d)]
+
+    def forward(self, x):
+        return self.conv_block(x)
+
+
+class Encoder(nn.Module):
+    def __init__(self, cfg: UNetConfig):
+        super().__init__()
+        cin = cfg.in_channels
+        for i, w in enumerate(cfg.widths):
+            setattr(self, f"conv{i + 1}", ConvBlock(cin, w, cfg.batchnorm))
+            cin = w
+        self.depth = cfg.depth
+        self.maxpool = nn.MaxPool2d(2, 2)
+
+    def blocks(self) -> List[ConvBlock]:
+        return [getattr(self, f"conv{i + 1}") for i in range(self.depth)]
+
+    def forward(self, x) -> Tuple[torch.Tensor, ...]:
+        skips = []
+        for blk in self.blocks():
+            x = blk(x)
+            skips.append(x)
+            x = self.maxpool(x)
+        return (x, *reversed(skips))
+
+
+class Up(nn.Module):
+    """Bilinear x2 up-sampling followed by a 1x1 conv halving the channels (variant only)."""
+
+    def __init__(self, cin: int, cout: int):
+        super().__init__()
+        self.proj = nn.Conv2d(cin, cout, kernel_size=1)
+
+    def forward(self, x):
+        return self.proj(F.interpolate(x, scale_factor=2, mode="bilinear", align_corners=False))
+
+
+class Decoder(nn.Module):
+    def __init__(self, cfg: UNetConfig):
+        super().__init__()
+        widths = list(reversed(cfg.widths))  # 256,128,64,32
+        cin = cfg.mid_width
+        for i, w in enumerate(widths):
+            setattr(self, f"conv{i + 1}", ConvBlock(2 * w, w, cfg.batchnorm))
+        for i, w in enumerate(widths):
+            up = Up(cin, w) if cfg.bilinear else nn.ConvTranspose2d(cin, w, 2, 2)
+            setattr(self, f"deconv{i + 1}", up)
+            cin = w
+        self.depth = cfg.depth
+
+    def blocks(self) -> List[ConvBlock]:
+        return [getattr(self, f"conv{i + 1}") for i in range(self.depth)]
+
+    def ups(self) -> List[nn.Module]:
+        return [getattr(self, f"deconv{i + 1}") for i in range(self.depth)]
+
+    def level(self, i: int, x, skip):
+        out = self.ups()[i](x)
+        skip = center_crop(skip, out.shape[2], out.shape[3])
+        return self.blocks()[i](torch.cat((skip, out), dim=1))
+
+    def forward(self, x, *skips):
+        for i, skip in enumerate(skips):
+            x = self.level(i, x, skip)
+        return x
+
+
+class UNet(nn.Module):
+    """Reference-parity UNet (unet_model.py:4-62).  ``forward(x[B,C,H,W]) -> probs[B,1,H,W]``.
+
+    The reference's ``pipe=True`` (2-GPU placement + microbatch loop inside ``forward``,
+    unet_model.py:14-53) is provided by :class:`distributedpytorch_amd.parallel.pipeline.GPipe`
+    instead of being baked into the model.
+    """
+
+    def __init__(self, cfg: UNetConfig | None = None, **kw):
+        super().__init__()
+        cfg = cfg or UNetConfig(**kw)
+        self.cfg = cfg
+        self.encoder = Encoder(cfg)
+        self.mid = ConvBlock(cfg.widths[-1], cfg.mid_width, cfg.batchnorm)
+        self.decoder = Decoder(cfg)
+        self.segmap = nn.Conv2d(cfg.base, cfg.out_channels, 1)
+        self.sigmoid = nn.Sigmoid()
+
+    def logits(self, x):
+        x, *skips = self.encoder(x)
+        x = self.mid(x)
+        x = self.decoder(x, *skips)
+        return self.segmap(x)
+
+    def forward(self, x):
+        return self.sigmoid(self.logits(x))
+
+    # ---- introspection used by the engine / pipeline partitioner ----
+    def conv_blocks(self) -> List[ConvBlock]:
+        return self.encoder.blocks() + [self.mid] + self.decoder.blocks()
+
+
+def build_model(name: str = "unet", **overrides) -> UNet:
+    cfg = PRESETS[name]
+    if overrides:
+        cfg = UNetConfig(**{**cfg.to_dict(), **overrides})
+    return UNet(cfg)
+
+
+def count_params(model: nn.Module) -> int:
+    return sum(p.numel() for p in model.parameters())
+
+
+def forward_flops(cfg: UNetConfig, h: int, w: int) -> float:
+    """Forward FLOPs per image (2*MACs) over conv / deconv layers (96.6 GF @ 512^2)."""
+    fl = 0.0
+    H, W, cin = h, w, cfg.in_channels
+    for wd in cfg.widths:
+        fl += 2 * H * W * 9 * (cin * wd + wd * wd)
+        H, W, cin = H // 2, W // 2, wd
+    fl += 2 * H * W * 9 * (cin * cfg.mid_width + cfg.mid_width ** 2)
+    cin = cfg.mid_width
+    for wd in reversed(cfg.widths):
+        fl += 2 * H * W * cin * wd * 4  # deconv: every input pixel -> 2x2 outputs
+        H, W = H * 2, W * 2
+        fl += 2 * H * W * 9 * (2 * wd * wd + wd * wd)
+        cin = wd
+    fl += 2 * H * W * cfg.base * cfg.out_channels
+    return fl

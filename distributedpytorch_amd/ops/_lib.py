@@ -1,0 +1,73 @@
+"""Loader for the in-tree HIP kernel library ``distributedpytorch_amd/_C/libdpa_hip.so``.
+
+The library is plain HIP C++ (``csrc/*.hip``) compiled by ``hipcc --offload-arch=gfx950`` with
+``extern "C"`` launchers; it links the *same* ``libamdhip64.so.7`` that torch already loaded
+(identical SONAME, rpath -> torch/lib), so the ``hipStream_t`` handles we pass from
+``torch.cuda.current_stream().cuda_stream`` are valid in it.  Calls go through ctypes: no torch
+headers, seconds to rebuild, and every launcher takes raw device pointers + the stream.
+
+On a machine with a GPU the library is REQUIRED: ``lib()`` raises if it is missing instead of
+silently falling back to eager torch ops.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+
+_HERE = Path(__file__).resolve().parent.parent
+LIB_PATH = _HERE / "_C" / "libdpa_hip.so"
+_lib = None
+_err = None
+
+
+def _load():
+    global _lib, _err
+    if _lib is not None or _err is not None:
+        return _lib
+    try:
+        import torch  # noqa: F401  (must be loaded first so the HIP runtime is torch's)
+        _lib = ctypes.CDLL(str(LIB_PATH), mode=ctypes.RTLD_GLOBAL)
+        _declare(_lib)
+    except OSError as e:  # missing or unloadable
+        _err = e
+        _lib = None
+    return _lib
+
+
+def available() -> bool:
+    return _load() is not None
+
+
+def lib():
+    L = _load()
+    if L is None:
+        raise RuntimeError(
+            f"HIP kernel library not available ({LIB_PATH}): {_err}. Build it with "
+            f"`python -c 'import __graft_entry__ as g; g.build()'` or `python tools/build_hip.py`.")
+    return L
+
+
+def _declare(L):
+    c_void_p, c_int, c_float, c_long = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_int64
+    sigs = getattr(L, "dpa_signatures", None)
+    # every launcher returns int (hipError_t); argtypes are declared in ops modules lazily
+    L.dpa_version.restype = c_int
+    del sigs, c_void_p, c_int, c_float, c_long
+
+
+def check(err: int, name: str):
+    if err != 0:
+        L = lib()
+        L.dpa_error_string.restype = ctypes.c_char_p
+        msg = L.dpa_error_string(err).decode()
+        raise RuntimeError(f"{name} failed: hip error {err} ({msg})")
+
+
+def stream_ptr(device=None) -> int:
+    import torch
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def ptr(t) -> ctypes.c_void_p:
+    return ctypes.c_void_p(t.data_ptr())

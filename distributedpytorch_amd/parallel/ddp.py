@@ -1,0 +1,124 @@
+"""Data-parallel gradient all-reduce over RCCL (xGMI) with bucketing sized for point-to-point links.
+
+Replaces torch DDP (reference ``utils/train_utils.py:195-196``).
+
+Design (MI355X-first, not a translation of torch's C++ Reducer):
+* Gradients live in ONE flat fp32 buffer in backward order (:class:`..optim.FlatParameterSpace`).
+  A bucket is a contiguous slice of it -> the all-reduce runs in place on the slice, no
+  flatten/unflatten copies.
+* Buckets are cut at ``bucket_mb`` (default 8 MiB): 29.6 MiB of UNet grads -> 4 buckets plus a small
+  first one, so the collective for the deepest (largest) layers starts while the full-resolution
+  backward layers (the long tail of the step) are still running.  On 8 GPUs with 7 xGMI links
+  each, RCCL's ring/tree channels spread an 8 MiB message over all links; smaller buckets only
+  add per-collective latency (measured sweep in BASELINE.md).
+* Buckets are launched strictly in index order, as soon as every gradient in it and in all
+  earlier buckets has been produced -> identical collective order on every rank (no deadlock even
+  if autograd finishes parameters in a different order) and overlap with the rest of backward.
+* ``op=AVG`` on RCCL (ncclAvg) so no separate divide kernel; gloo (CPU tests) uses SUM + scale.
+* Initial parameters are broadcast from rank 0 in one collective over the flat buffer
+  (torch DDP's ``_sync_module_states``, N3).
+"""
+from __future__ import annotations
+
+from typing import List, Optional
+
+import torch
+import torch.distributed as dist
+
+from ..optim import FlatParameterSpace
+
+
+class BucketedAllReduce:
+    def __init__(self, space: FlatParameterSpace, bucket_mb: float = 8.0, first_bucket_mb: float = 1.0,
+                 group=None, average: bool = True, scale: float = 1.0):
+        self.space = space
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.average = average
+        self.scale = scale
+        self.nccl = dist.get_backend(group) == "nccl"
+        cap = int(bucket_mb * 2 ** 20 / 4)
+        first = int(first_bucket_mb * 2 ** 20 / 4)
+        self.buckets: List[tuple] = []   # (start, end, first_param, last_param_exclusive)
+        self.bucket_of: List[int] = []
+        start_p = 0
+        start = 0
+        limit = first if first > 0 else cap
+        for i, n in enumerate(space.numels):
+            end = space.offsets[i + 1]
+            self.bucket_of.append(len(self.buckets))
+            if end - start >= limit or i == len(space.numels) - 1:
+                self.buckets.append((start, end, start_p, i + 1))
+                start, start_p, limit = end, i + 1, cap
+        self.expected = [b[3] - b[2] for b in self.buckets]
+        self._hooks = []
+        self.reset()
+
+    # ---------------- hooks ----------------
+    def register_hooks(self):
+        idx = {id(p): i for i, p in enumerate(self.space.params)}
+        for p in self.space.params:
+            i = idx[id(p)]
+            self._hooks.append(p.register_post_accumulate_grad_hook(lambda _p, i=i: self.mark_ready(i)))
+        return self
+
+    def remove_hooks(self):
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []
+
+    def reset(self):
+        self.pending = list(self.expected)
+        self.next_launch = 0
+        self.works = []
+
+    def mark_ready(self, param_index: int):
+        b = self.bucket_of[param_index]
+        self.pending[b] -= 1
+        while self.next_launch < len(self.buckets) and self.pending[self.next_launch] == 0:
+            self._launch(self.next_launch)
+            self.next_launch += 1
+
+    def _launch(self, b: int):
+        s, e, _, _ = self.buckets[b]
+        t = self.space.grad[s:e]
+        if self.nccl and self.average and self.scale == 1.0:
+            w = dist.all_reduce(t, op=dist.ReduceOp.AVG, group=self.group, async_op=True)
+        else:
+            if self.average or self.scale != 1.0:
+                t.mul_((1.0 / self.world if self.average else 1.0) * self.scale)
+            w = dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+        self.works.append(w)
+
+    def finish(self):
+        """Launch any bucket whose grads never arrived (unused params) and wait for all collectives."""
+        while self.next_launch < len(self.buckets):
+            self._launch(self.next_launch)
+            self.next_launch += 1
+        for w in self.works:
+            w.wait()
+        self.reset()
+
+    def all_reduce_now(self):
+        """No-hook path: reduce the whole flat buffer bucket by bucket (used after a fused backward)."""
+        for b in range(len(self.buckets)):
+            self._launch(b)
+        self.next_launch = len(self.buckets)
+        self.finish()
+
+
+def broadcast_parameters(space: FlatParameterSpace, src: int = 0, group=None):
+    dist.broadcast(space.data, src=src, group=group)
+
+
+def sync_buffers(module: torch.nn.Module, src: int = 0, group=None):
+    for b in module.buffers():
+        if b.is_floating_point() or b.dtype in (torch.int64, torch.int32):
+            dist.broadcast(b, src=src, group=group)
+
+
+def all_reduce_mean(values: torch.Tensor, group=None) -> torch.Tensor:
+    if not (dist.is_initialized() and dist.get_world_size(group) > 1):
+        return values
+    dist.all_reduce(values, op=dist.ReduceOp.SUM, group=group)
+    return values / dist.get_world_size(group)

@@ -1,0 +1,356 @@
+"""GPipe pipeline model parallelism for the UNet (``-t MP``).
+
+Reference: a hand-written 2-stage, 2-microbatch pipeline inside ``UNet.forward``
+(``model/unet_model.py:14-53``): encoder+mid on cuda:0, decoder+head on
+cuda:1, the bottleneck and all four skips copied with ``.to('cuda:1')`` per microbatch, overlap
+only from async launch order, backward via plain autograd.
+
+Here, generalised to N stages x M microbatches (GPipe: all forwards, then all backwards):
+
+* :class:`GPipeDist` - one process per GPU (torchrun), the MI355X-native form.  Each rank owns one
+  contiguous block range (:func:`..models.blocks.partition`, FLOP-balanced, or the reference cut).
+  Activations AND skip tensors go *directly* from producer to consumer stage with RCCL
+  ``isend/irecv`` (one xGMI hop on the fully connected MI355X mesh - skips never relay through
+  intermediate stages), sent in the compute dtype (bf16: half the reference's bytes).  P2P runs on
+  RCCL's per-peer streams, so transfers overlap with the next microbatch's compute; receives are
+  posted one microbatch ahead.  The last stage sums the per-microbatch loss partial sums, which
+  gives exactly the reference's full-batch loss (global Dice), then back-propagates microbatch by
+  microbatch so gradients start flowing upstream immediately.
+* :class:`GPipeLocal` - single process, N local devices (the reference's own form, kept for
+  ``python train.py -t MP`` without torchrun): stages issued in wavefront order so stage s works
+  on microbatch m while stage s+1 works on microbatch m-1; cross-device copies are peer copies.
+
+Both are numerically transparent: pipelined forward == plain forward (SURVEY §3.4 probe7), checked
+by the tests against a single-device run.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Optional, Sequence
+
+import torch
+import torch.distributed as dist
+
+from ..compute import loss_from_partials, make_blocks
+from ..models.blocks import boundary_names, block_kind, n_blocks, partition, run_segment, skip_name
+from ..optim import FlatParameterSpace
+
+
+def _block_param_prefixes(idx: int, depth: int) -> List[str]:
+    kind, i = block_kind(idx, depth)
+    if kind == "enc":
+        return [f"encoder.conv{i + 1}."]
+    if kind == "mid":
+        return ["mid."]
+    if kind == "dec":
+        return [f"decoder.conv{i + 1}.", f"decoder.deconv{i + 1}."]
+    return ["segmap."]
+
+
+def stage_param_names(model, start: int, end: int) -> List[str]:
+    depth = model.cfg.depth
+    prefixes = [p for idx in range(start, end) for p in _block_param_prefixes(idx, depth)]
+    return [n for n, _ in model.named_parameters() if any(n.startswith(p) for p in prefixes)]
+
+
+def _tensor_producer(name: str, cut_start: int, cuts: Sequence[int], depth: int) -> int:
+    """Stage that produces boundary tensor ``name`` entering the stage starting at ``cut_start``."""
+    if name == "x":
+        return cuts.index(cut_start) - 1
+    lvl = int(name[len("skip"):])
+    for s in range(len(cuts) - 1):
+        if cuts[s] <= lvl < cuts[s + 1]:
+            return s
+    raise ValueError(name)
+
+
+def _stage_of_block(idx: int, cuts: Sequence[int]) -> int:
+    for s in range(len(cuts) - 1):
+        if cuts[s] <= idx < cuts[s + 1]:
+            return s
+    raise ValueError(idx)
+
+
+def stage_io(cuts: Sequence[int], depth: int):
+    """Per stage: ``recv`` list of (name, src_stage) and ``send`` list of (name, dst_stage)."""
+    S = len(cuts) - 1
+    recv = [[] for _ in range(S)]
+    send = [[] for _ in range(S)]
+    for s in range(1, S):
+        # x comes from the previous stage
+        recv[s].append(("x", s - 1))
+        send[s - 1].append(("x", s))
+    for lvl in range(depth):
+        p = _stage_of_block(lvl, cuts)
+        c = _stage_of_block(depth + 1 + (depth - 1 - lvl), cuts)
+        if p != c:
+            recv[c].append((skip_name(lvl), p))
+            send[p].append((skip_name(lvl), c))
+    return recv, send
+
+
+def infer_shapes(cfg, microbatch: int, h: int, w: int) -> Dict[str, tuple]:
+    """Shapes (NCHW) of every boundary tensor for one microbatch, by arithmetic (no tracing)."""
+    shapes = {}
+    H, W = h, w
+    for lvl, wd in enumerate(cfg.widths):
+        shapes[skip_name(lvl)] = (microbatch, wd, H, W)
+        H, W = H // 2, W // 2
+    return shapes
+
+
+class _Stage:
+    def __init__(self, model, blocks, start, end, depth):
+        self.model, self.blocks, self.start, self.end, self.depth = model, blocks, start, end, depth
+
+    def forward(self, env, target=None, want="partials"):
+        return run_segment(self.blocks, self.start, self.end, self.depth, env, target, want)
+
+
+class GPipeDist:
+    """Multi-process GPipe over a process group whose size == number of stages."""
+
+    def __init__(self, model, microbatches: int, backend: str = "auto", dtype: str = "bf16",
+                 group=None, cuts: Optional[List[int]] = None, img_hw=(512, 512), mode: str = "balanced"):
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.S = dist.get_world_size(group)
+        self.M = microbatches
+        self.model = model
+        self.depth = model.cfg.depth
+        self.cuts = cuts or partition(model.cfg, self.S, img_hw[0], img_hw[1], mode=mode)
+        assert len(self.cuts) == self.S + 1
+        self.start, self.end = self.cuts[self.rank], self.cuts[self.rank + 1]
+        self.recv_spec, self.send_spec = stage_io(self.cuts, self.depth)
+        self.device = next(model.parameters()).device
+        names = set(stage_param_names(model, self.start, self.end))
+        own = [(n, p) for n, p in model.named_parameters() if n in names]
+        for n, p in model.named_parameters():
+            if n not in names:
+                p.requires_grad_(False)
+        self.space = FlatParameterSpace(own, device=self.device)
+        self.blocks = make_blocks(model, backend, dtype)
+        self.stage = _Stage(model, self.blocks, self.start, self.end, self.depth)
+        self.comm_dtype = torch.bfloat16 if (dtype == "bf16" and self.device.type == "cuda") else torch.float32
+        self.is_first = self.rank == 0
+        self.is_last = self.rank == self.S - 1
+        self._glob = lambda s: dist.get_global_rank(group, s) if group is not None else s
+
+    # shapes of the boundary tensors for this microbatch size
+    def _shape(self, name, mb, h, w):
+        cfg = self.model.cfg
+        if name.startswith("skip"):
+            return infer_shapes(cfg, mb, h, w)[name]
+        # "x" entering block `cut`
+        cut = self.start
+        kind, i = block_kind(cut, self.depth)
+        H, W = h, w
+        if kind == "enc":
+            c = cfg.widths[i - 1]
+            return (mb, c, H >> i, W >> i)
+        if kind == "mid":
+            return (mb, cfg.widths[-1], H >> self.depth, W >> self.depth)
+        if kind == "dec":
+            c = cfg.mid_width if i == 0 else cfg.widths[self.depth - i]
+            return (mb, c, H >> (self.depth - i), W >> (self.depth - i))
+        return (mb, cfg.base, H, W)
+
+    def _recv_layout(self):
+        """channels_last on GPU (matches what the backends produce)."""
+        return torch.channels_last if self.device.type == "cuda" else torch.contiguous_format
+
+    def _irecv(self, mb, h, w):
+        bufs, works = {}, []
+        for name, src in self.recv_spec[self.rank]:
+            shp = self._shape(name, mb, h, w)
+            t = torch.empty(shp, dtype=self.comm_dtype, device=self.device, memory_format=self._recv_layout())
+            works.append(dist.irecv(t, src=self._glob(src), group=self.group))
+            bufs[name] = t
+        return bufs, works
+
+    def train_step(self, images: Optional[torch.Tensor], targets: Optional[torch.Tensor], batch: int,
+                   hw, dice: bool = True, loss_scale: float = 1.0):
+        """One GPipe step. Returns the (full-batch) loss on the last stage, None elsewhere."""
+        h, w = hw
+        M = self.M
+        assert batch % M == 0, f"batch {batch} must be divisible by microbatches {M}"
+        mb = batch // M
+        xs = images.chunk(M) if self.is_first else [None] * M
+        ts = targets.chunk(M) if self.is_last else [None] * M
+        saved_in, saved_out, pending_sends = [], [], []
+        partials = []
+        nxt = self._irecv(mb, h, w) if not self.is_first else None
+        for m in range(M):
+            if self.is_first:
+                env = {"x": xs[m]}
+                leaves = {}
+            else:
+                bufs, works = nxt
+                for wk in works:
+                    wk.wait()
+                if m + 1 < M:
+                    nxt = self._irecv(mb, h, w)
+                leaves = {k: v.detach().requires_grad_(True) for k, v in bufs.items()}
+                env = dict(leaves)
+            out = self.stage.forward(env, ts[m], "partials")
+            saved_in.append(leaves)
+            if self.is_last:
+                partials.append(out["partials"])
+                saved_out.append({})
+            else:
+                sends = {}
+                for name, dst in self.send_spec[self.rank]:
+                    t = out[name]
+                    sends[name] = t
+                    buf = t.detach().to(self.comm_dtype)
+                    pending_sends.append((dist.isend(buf, dst=self._glob(dst), group=self.group), buf))
+                saved_out.append(sends)
+
+        # ---------------- backward (microbatches in reverse order) ----------------
+        loss = None
+        if self.is_last:
+            P = torch.stack([p.detach() for p in partials]).requires_grad_(True)
+            loss = loss_from_partials(P.sum(0), targets.numel(), dice)
+            (loss * loss_scale).backward()
+            dP = P.grad
+        for m in reversed(range(M)):
+            if self.is_last:
+                torch.autograd.backward(partials[m], dP[m])
+            else:
+                outs, grads, works = [], [], []
+                for name, dst in self.send_spec[self.rank]:
+                    t = saved_out[m][name]
+                    g = torch.empty(t.shape, dtype=self.comm_dtype, device=self.device,
+                                    memory_format=self._recv_layout())
+                    works.append(dist.irecv(g, src=self._glob(dst), group=self.group))
+                    outs.append(t)
+                    grads.append(g)
+                for wk in works:
+                    wk.wait()
+                torch.autograd.backward(outs, [g.to(o.dtype) for o, g in zip(outs, grads)])
+            if not self.is_first:
+                for name, src in self.recv_spec[self.rank]:
+                    gr = saved_in[m][name].grad
+                    if gr is None:
+                        gr = torch.zeros_like(saved_in[m][name])
+                    buf = gr.to(self.comm_dtype).contiguous(memory_format=self._recv_layout())
+                    pending_sends.append((dist.isend(buf, dst=self._glob(src), group=self.group), buf))
+        for wk, _ in pending_sends:
+            wk.wait()
+        return loss
+
+    @torch.no_grad()
+    def eval_probs(self, images, batch, hw):
+        """Inference through the pipeline (one microbatch = whole batch); probs on the last stage."""
+        h, w = hw
+        if self.is_first:
+            env = {"x": images}
+        else:
+            bufs, works = self._irecv(batch, h, w)
+            for wk in works:
+                wk.wait()
+            env = dict(bufs)
+        out = self.stage.forward(env, None, "probs")
+        sends = []
+        if not self.is_last:
+            for name, dst in self.send_spec[self.rank]:
+                buf = out[name].to(self.comm_dtype).contiguous(memory_format=self._recv_layout())
+                sends.append(dist.isend(buf, dst=self._glob(dst), group=self.group))
+        for wk in sends:
+            wk.wait()
+        return out.get("probs")
+
+    def gather_state_dict(self):
+        """Full model state dict on stage 0 (other stages send their parameters)."""
+        names = stage_param_names(self.model, self.start, self.end)
+        params = dict(self.model.named_parameters())
+        all_cuts = self.cuts
+        sd = {}
+        for s in range(self.S):
+            snames = stage_param_names(self.model, all_cuts[s], all_cuts[s + 1])
+            for n in snames:
+                if s == 0:
+                    if self.rank == 0:
+                        sd[n] = params[n].detach().clone()
+                elif self.rank == s:
+                    dist.send(params[n].detach().contiguous(), dst=self._glob(0), group=self.group)
+                elif self.rank == 0:
+                    t = torch.empty_like(params[n])
+                    dist.recv(t, src=self._glob(s), group=self.group)
+                    sd[n] = t
+        del names
+        if self.rank == 0:
+            full = self.model.state_dict()
+            return {k: sd.get(k, v) for k, v in full.items()}
+        return None
+
+
+class GPipeLocal:
+    """Single-process pipeline over local devices (reference MP form, N stages x M microbatches)."""
+
+    def __init__(self, model, devices: Sequence, microbatches: int, backend: str = "auto", dtype: str = "bf16",
+                 cuts: Optional[List[int]] = None, img_hw=(512, 512), mode: str = "balanced"):
+        self.devices = [torch.device(d) for d in devices]
+        self.S = len(self.devices)
+        self.M = microbatches
+        self.model = model
+        self.depth = model.cfg.depth
+        self.cuts = cuts or partition(model.cfg, self.S, img_hw[0], img_hw[1], mode=mode)
+        # place each block's parameters on its stage's device
+        for s in range(self.S):
+            for n in stage_param_names(model, self.cuts[s], self.cuts[s + 1]):
+                mod_name, _, pname = n.rpartition(".")
+                mod = model.get_submodule(mod_name)
+                setattr(mod, pname, torch.nn.Parameter(getattr(mod, pname).detach().to(self.devices[s])))
+        self.spaces = []
+        for s in range(self.S):
+            names = set(stage_param_names(model, self.cuts[s], self.cuts[s + 1]))
+            own = [(n, p) for n, p in model.named_parameters() if n in names]
+            self.spaces.append(FlatParameterSpace(own, device=self.devices[s]))
+        self.stage_blocks = [make_blocks(model, backend, dtype) for _ in range(self.S)]
+        for s, b in enumerate(self.stage_blocks):
+            b.device = self.devices[s]
+
+    def _run(self, s, env, target, want):
+        dev = self.devices[s]
+        env = {k: v.to(dev, non_blocking=True) for k, v in env.items()}
+        if target is not None:
+            target = target.to(dev, non_blocking=True)
+        ctx = torch.cuda.device(dev) if dev.type == "cuda" else _Null()
+        with ctx:
+            return run_segment(self.stage_blocks[s], self.cuts[s], self.cuts[s + 1], self.depth, env, target, want)
+
+    def forward_partials(self, images, targets):
+        M, S = self.M, self.S
+        xs, ts = images.chunk(M), targets.chunk(M)
+        envs = [{"x": x} for x in xs]
+        partials = [None] * M
+        # wavefront order: at tick k, stages S-1..0 run microbatch k-s (later stages issued first,
+        # like unet_model.py:33-44, so the downstream device never waits behind upstream launches)
+        for k in range(M + S - 1):
+            for s in reversed(range(S)):
+                m = k - s
+                if 0 <= m < M:
+                    out = self._run(s, envs[m], ts[m] if s == S - 1 else None, "partials")
+                    if s == S - 1:
+                        partials[m] = out["partials"].to(self.devices[0])
+                    else:
+                        envs[m] = out
+        return sum(partials)
+
+    def forward_loss(self, images, targets, dice=True):
+        return loss_from_partials(self.forward_partials(images, targets), targets.numel(), dice)
+
+    @torch.no_grad()
+    def probs(self, images):
+        env = {"x": images}
+        for s in range(self.S):
+            env = self._run(s, env, None, "probs" if s == self.S - 1 else "partials")
+        return env["probs"].to(self.devices[0])
+
+
+class _Null:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False

@@ -1,0 +1,426 @@
+"""One training loop parametrised by strategy (the reference copy-pasted it three times:
+``utils/train_utils.py:22-92`` fit, ``:95-167`` fit_DP, ``:170-248`` fit_DDP).
+
+Per step (reference hot loop ``:59-79``): H2D (prefetched on a side stream), forward to the loss
+partial sums, ``(batch_size * loss).backward()`` (A11 kept, switchable), gradient all-reduce
+(strategy specific, overlapped with backward), one fused Adam launch, metrics every ``log_every``
+steps without a per-step host sync (A17).  Per epoch: sharded evaluation (loss + Dice),
+``ReduceLROnPlateau`` stepped identically on all ranks (A5), a checkpoint of the full training
+state.  At the end: ``checkpoints/<method>.pth`` (reference keys; ``module.`` prefix for DP/DDP as
+the reference wrote them) and ``loss/<method>/{train,val}_loss.pkl``.
+"""
+from __future__ import annotations
+
+import logging
+import os
+import time
+from typing import Optional
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from .compute import loss_from_partials, make_compute, resolve_backend
+from .config import TrainConfig, dist_env
+from .data import CarvanaDataset, SyntheticSegmentation, build_loaders, split_dataset
+from .data.loaders import DeviceBatcher
+from .loss import dice_score
+from .models.unet import build_model
+from .optim import FlatParameterSpace, FusedAdam, make_plateau, plateau_step
+from .parallel.ddp import BucketedAllReduce, broadcast_parameters
+from .parallel.dp import ReplicatedDataParallel
+from .parallel.pipeline import GPipeDist, GPipeLocal
+from .utils import LossCurves, MetricsLogger, load_model_state, save_model, set_seed
+from .utils.checkpoint import load_training_state, save_training_state
+
+log = logging.getLogger("dpa")
+
+
+# ============================================================================ strategies
+class Strategy:
+    name = "base"
+    module_prefix = False
+
+    def __init__(self, cfg: TrainConfig):
+        self.cfg = cfg
+        self.rank, self.local_rank, self.world = 0, 0, 1
+        self.is_main = True
+        self.device = torch.device("cpu")
+
+    # must set self.model, self.optimizer
+    def train_step(self, images, targets) -> Optional[torch.Tensor]:
+        raise NotImplementedError
+
+    def eval_batch(self, images, targets):
+        """-> (loss, dice) device tensors or None on ranks without outputs."""
+        raise NotImplementedError
+
+    def state_dict(self):
+        return self.model.state_dict()
+
+    def reduce_eval(self, vals: torch.Tensor) -> torch.Tensor:
+        return vals
+
+    def barrier(self):
+        pass
+
+    def lr_scale(self) -> float:
+        return 1.0
+
+
+def _loss_scale(cfg, batch):
+    return float(batch) if cfg.loss_scale_by_batch else 1.0
+
+
+class SingleDevice(Strategy):
+    name = "singleGPU"
+
+    def __init__(self, cfg, model, device):
+        super().__init__(cfg)
+        self.device = torch.device(device)
+        self.model = model.to(self.device)
+        self.space = FlatParameterSpace(self.model, device=self.device)
+        self.compute = make_compute(self.model, cfg.backend, cfg.dtype)
+        self.optimizer = FusedAdam(self.space, lr=cfg.lr * self.lr_scale(), weight_decay=cfg.weight_decay)
+
+    def forward_loss(self, images, targets):
+        S = self.compute.forward_partials(images, targets)
+        return loss_from_partials(S, targets.numel())
+
+    def train_step(self, images, targets):
+        self.optimizer.zero_grad()
+        loss = self.forward_loss(images, targets)
+        (loss * _loss_scale(self.cfg, images.shape[0])).backward()
+        self.optimizer.step()
+        return loss.detach()
+
+    @torch.no_grad()
+    def eval_batch(self, images, targets):
+        p = self.compute.probs(images)
+        S = _partials(p, targets)
+        return loss_from_partials(S, targets.numel()), dice_score(p, targets)
+
+
+def _partials(p, t):
+    from .compute import loss_partials_from_probs
+    return loss_partials_from_probs(p, t)
+
+
+class DDPStrategy(SingleDevice):
+    name = "DDP"
+    module_prefix = True
+
+    def __init__(self, cfg, model, device):
+        self.rank, self.local_rank, self.world = dist.get_rank(), dist_env()[1], dist.get_world_size()
+        super().__init__(cfg, model, device)
+        self.rank, self.local_rank, self.world = dist.get_rank(), dist_env()[1], dist.get_world_size()
+        self.is_main = self.rank == 0
+        broadcast_parameters(self.space, src=0)
+        scale = float(self.world) if cfg.global_dice else 1.0
+        self.reducer = BucketedAllReduce(self.space, bucket_mb=cfg.bucket_mb, scale=scale).register_hooks()
+
+    def lr_scale(self):
+        # reference: Adam(lr * world_size) (utils/train_utils.py:199) - with the real world size (A6)
+        return float(dist.get_world_size())
+
+    def forward_loss(self, images, targets):
+        S = self.compute.forward_partials(images, targets)
+        n = targets.numel()
+        if self.cfg.global_dice:
+            S = _all_reduce_sum_autograd(S)
+            n = n * self.world
+        return loss_from_partials(S, n)
+
+    def train_step(self, images, targets):
+        self.optimizer.zero_grad()
+        loss = self.forward_loss(images, targets)
+        (loss * _loss_scale(self.cfg, images.shape[0])).backward()
+        self.reducer.finish()
+        self.optimizer.step()
+        return loss.detach()
+
+    def reduce_eval(self, vals):
+        dist.all_reduce(vals, op=dist.ReduceOp.SUM)
+        return vals
+
+    def barrier(self):
+        dist.barrier()
+
+
+class _AllReduceSum(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        y = x.clone()
+        dist.all_reduce(y, op=dist.ReduceOp.SUM)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        # every rank holds the same global loss; d(global)/d(local) = 1 -> pass the grad through
+        return g
+
+
+def _all_reduce_sum_autograd(x):
+    return _AllReduceSum.apply(x)
+
+
+class DPStrategy(Strategy):
+    name = "DP"
+    module_prefix = True
+
+    def __init__(self, cfg, model, devices):
+        super().__init__(cfg)
+        self.dp = ReplicatedDataParallel(model, devices, cfg.backend, cfg.dtype)
+        self.device = self.dp.devices[0]
+        self.model = self.dp.module
+        self.optimizer = FusedAdam(self.dp.spaces, lr=cfg.lr, weight_decay=cfg.weight_decay)
+
+    def train_step(self, images, targets):
+        self.optimizer.zero_grad()
+        loss = self.dp.forward_loss(images, targets)
+        (loss * _loss_scale(self.cfg, images.shape[0])).backward()
+        self.dp.all_reduce_grads()
+        self.optimizer.step()
+        return loss.detach()
+
+    @torch.no_grad()
+    def eval_batch(self, images, targets):
+        p = self.dp.probs(images)
+        t = targets.to(p.device)
+        return loss_from_partials(_partials(p, t), t.numel()), dice_score(p, t)
+
+
+class PipelineLocalStrategy(Strategy):
+    name = "MP"
+
+    def __init__(self, cfg, model, devices):
+        super().__init__(cfg)
+        H, W = cfg.img_size
+        self.pipe = GPipeLocal(model, devices, cfg.microbatches, cfg.backend, cfg.dtype, img_hw=(H, W),
+                               mode="reference" if len(devices) == 2 else "balanced")
+        self.model = model
+        self.device = self.pipe.devices[0]
+        self.optimizer = FusedAdam(self.pipe.spaces, lr=cfg.lr, weight_decay=cfg.weight_decay)
+
+    def train_step(self, images, targets):
+        self.optimizer.zero_grad()
+        loss = self.pipe.forward_loss(images, targets)
+        (loss * _loss_scale(self.cfg, images.shape[0])).backward()
+        self.optimizer.step()
+        return loss.detach()
+
+    @torch.no_grad()
+    def eval_batch(self, images, targets):
+        p = self.pipe.probs(images)
+        t = targets.to(p.device)
+        return loss_from_partials(_partials(p, t), t.numel()), dice_score(p, t)
+
+
+class PipelineDistStrategy(Strategy):
+    name = "MP"
+
+    def __init__(self, cfg, model, device):
+        super().__init__(cfg)
+        self.rank, self.local_rank, self.world = dist.get_rank(), dist_env()[1], dist.get_world_size()
+        self.device = torch.device(device)
+        self.model = model.to(self.device)
+        H, W = cfg.img_size
+        self.pipe = GPipeDist(self.model, cfg.microbatches, cfg.backend, cfg.dtype, img_hw=(H, W),
+                              mode="reference" if self.world == 2 else "balanced")
+        self.is_main = self.pipe.is_last  # the last stage owns the loss; rank 0 saves
+        self.optimizer = FusedAdam(self.pipe.space, lr=cfg.lr, weight_decay=cfg.weight_decay)
+
+    def train_step(self, images, targets):
+        self.optimizer.zero_grad()
+        B = images.shape[0]
+        loss = self.pipe.train_step(images, targets, B, self.cfg.img_size,
+                                    loss_scale=_loss_scale(self.cfg, B))
+        self.optimizer.step()
+        return loss
+
+    @torch.no_grad()
+    def eval_batch(self, images, targets):
+        p = self.pipe.eval_probs(images, images.shape[0], self.cfg.img_size)
+        if p is None:
+            return None
+        return loss_from_partials(_partials(p, targets), targets.numel()), dice_score(p, targets)
+
+    def state_dict(self):
+        return self.pipe.gather_state_dict()
+
+    def barrier(self):
+        dist.barrier()
+
+
+# ============================================================================ driver
+def _devices_for(cfg, n_needed=None):
+    if torch.cuda.is_available():
+        n = torch.cuda.device_count()
+        return [torch.device(f"cuda:{i}") for i in range(n if n_needed is None else n_needed)]
+    return [torch.device("cpu")] * (n_needed or 2)
+
+
+def build_strategy(cfg: TrainConfig, model) -> Strategy:
+    m = cfg.train_method
+    rank, local, world = dist_env()
+    if m in ("DDP",) or (m == "MP" and world > 1):
+        if not dist.is_initialized():
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+            if backend == "nccl":
+                torch.cuda.set_device(local)   # A15: bind each rank to its own GPU
+            dist.init_process_group(backend=backend, init_method="env://")
+        device = torch.device(f"cuda:{local}") if torch.cuda.is_available() else torch.device("cpu")
+        return DDPStrategy(cfg, model, device) if m == "DDP" else PipelineDistStrategy(cfg, model, device)
+    if m == "singleGPU":
+        dev = cfg.device or ("cuda:0" if torch.cuda.is_available() else "cpu")
+        return SingleDevice(cfg, model, dev)
+    if m == "DP":
+        devs = _devices_for(cfg)
+        if torch.cuda.is_available():
+            assert len(devs) >= 2, f"Requires at least 2 GPUs to run, but got {len(devs)}"
+        return DPStrategy(cfg, model, devs)
+    if m == "MP":
+        devs = _devices_for(cfg, cfg.stages)
+        if torch.cuda.is_available():
+            assert torch.cuda.device_count() >= cfg.stages, "not enough GPUs for the pipeline stages"
+        return PipelineLocalStrategy(cfg, model, devs)
+    raise ValueError(m)
+
+
+def build_datasets(cfg: TrainConfig):
+    H, W = cfg.img_size
+    if cfg.synthetic:
+        ds = SyntheticSegmentation(cfg.synthetic_len, (H, W), 3, seed=cfg.seed)
+    else:
+        root = cfg.data_dir
+        ds = CarvanaDataset(os.path.join(root, "train_hq"), os.path.join(root, "train_masks"), newsize=(W, H))
+    return split_dataset(ds, cfg.val, seed=0)
+
+
+def _setup_logging(cfg, rank):
+    os.makedirs(os.path.join(cfg.out_dir, "logs"), exist_ok=True)
+    # one log file per rank (the reference had all DDP ranks append to one file)
+    suffix = "" if rank == 0 else f".rank{rank}"
+    path = os.path.join(cfg.out_dir, "logs", f"{cfg.train_method}{suffix}.log")
+    handler = logging.FileHandler(path, mode="a")
+    handler.setFormatter(logging.Formatter("%(message)s"))
+    log.handlers[:] = [handler]
+    log.setLevel(logging.INFO)
+    log.propagate = False
+
+
+def train(cfg: TrainConfig):
+    rank, local, world = dist_env()
+    set_seed(cfg.seed)
+    _setup_logging(cfg, rank)
+    log.info("UNet for Carvana Image Masking (Segmentation)")
+    log.info(f"config: {cfg.to_dict()}")
+    model = build_model(cfg.model)
+    if cfg.checkpoint is not None:
+        load_model_state(model, os.path.join(cfg.out_dir, "checkpoints", f"{cfg.checkpoint}.pth"))
+    if cfg.load:
+        load_model_state(model, cfg.load)
+    strat = build_strategy(cfg, model)
+    log.info(f"strategy={strat.name} backend={resolve_backend(cfg.backend, strat.device)} device={strat.device}")
+
+    train_set, val_set = build_datasets(cfg)
+    dp_ranks = world if strat.name == "DDP" else 1
+    dp_rank = strat.rank if strat.name == "DDP" else 0
+    train_loader, val_loader, sampler = build_loaders(
+        train_set, val_set, cfg.batch_size, rank=dp_rank, world_size=dp_ranks, num_workers=cfg.num_workers,
+        pin_memory=strat.device.type == "cuda", seed=cfg.seed, drop_last=strat.name in ("MP",))
+    scheduler = make_plateau(strat.optimizer, cfg.patience)
+    metrics = MetricsLogger(os.path.join(cfg.out_dir, "logs", f"{cfg.train_method}.jsonl"), strat.is_main)
+    curves = LossCurves()
+    last_path = os.path.join(cfg.out_dir, "checkpoints", f"{cfg.train_method}_last.pt")
+    start_epoch, step = 0, 0
+    if cfg.resume and os.path.exists(last_path):
+        start_epoch, step = load_training_state(last_path, model=strat.model, optimizer=strat.optimizer,
+                                                scheduler=scheduler)
+        log.info(f"resumed from {last_path} at epoch {start_epoch} step {step}")
+
+    t_start = time.time()
+    pending = []
+    for epoch in range(start_epoch, cfg.epochs):
+        if sampler is not None:
+            sampler.set_epoch(epoch)  # A7
+        n_img, t_ep = 0, time.perf_counter()
+        for images, targets in DeviceBatcher(train_loader, strat.device):
+            loss = strat.train_step(images, targets)
+            step += 1
+            n_img += images.shape[0]
+            if loss is not None:
+                pending.append(loss)
+            if step % cfg.log_every == 0 and pending:
+                vals = torch.stack([p.float().to("cpu") for p in pending]).numpy()
+                mean_loss = float(np.mean(vals[-10:]))
+                pending = []
+                curves.add_train(step, time.time() - t_start, mean_loss)
+                metrics.log(kind="train", step=step, epoch=epoch, loss=mean_loss,
+                            lr=strat.optimizer.param_groups[0]["lr"])
+                if strat.is_main:
+                    log.info(f"step {step} loss {mean_loss:.5f}")
+            if cfg.max_steps and step >= cfg.max_steps:
+                break
+        ep_time = time.perf_counter() - t_ep
+        val_loss, val_dice = evaluate(strat, val_loader)
+        curves.add_val(step, time.time() - t_start, val_loss)
+        plateau_step(scheduler, val_loss)
+        metrics.log(kind="epoch", epoch=epoch, step=step, val_loss=val_loss, val_dice=val_dice,
+                    img_per_s=n_img * max(1, strat.world if strat.name == "DDP" else 1) / max(ep_time, 1e-9),
+                    peak_mem_gb=(torch.cuda.max_memory_allocated(strat.device) / 2 ** 30
+                                 if strat.device.type == "cuda" else 0.0))
+        if strat.is_main:
+            log.info(f"epoch {epoch}: val_loss {val_loss:.5f} val_dice {val_dice:.4f}")
+            print(f"epoch {epoch + 1}/{cfg.epochs} step {step} val_loss {val_loss:.5f} dice {val_dice:.4f} "
+                  f"({n_img / max(ep_time, 1e-9):.1f} img/s/rank)", flush=True)
+        if cfg.save_every_epoch:
+            sd_model = strat.state_dict()
+            if strat.rank == 0 and sd_model is not None:
+                save_training_state(last_path, model=_SD(sd_model), optimizer=strat.optimizer,
+                                    scheduler=scheduler, epoch=epoch + 1, step=step)
+        if cfg.max_steps and step >= cfg.max_steps:
+            break
+
+    sd = strat.state_dict()
+    paths = {}
+    if strat.rank == 0 and sd is not None:
+        ck = os.path.join(cfg.out_dir, "checkpoints", f"{cfg.train_method}.pth")
+        save_model(_SD(sd), ck, module_prefix=strat.module_prefix)
+        paths["checkpoint"] = ck
+    if strat.is_main:
+        paths["loss"] = curves.save(cfg.out_dir, cfg.train_method)
+    strat.barrier()
+    return {"step": step, "paths": paths, "curves": curves, "strategy": strat}
+
+
+class _SD:
+    """Adapter so checkpoint helpers can take a plain state dict."""
+
+    def __init__(self, sd):
+        self._sd = sd
+
+    def state_dict(self):
+        return self._sd
+
+
+@torch.no_grad()
+def evaluate(strat: Strategy, val_loader):
+    """Reference ``evaluate.py:6-25`` (mean per-batch loss) + Dice; sharded and all-reduced."""
+    tot = torch.zeros(3, dtype=torch.float64)
+    for images, targets in DeviceBatcher(val_loader, strat.device):
+        r = strat.eval_batch(images, targets)
+        if r is not None:
+            loss, dice = r
+            tot += torch.tensor([float(loss), float(dice), 1.0], dtype=torch.float64)
+    if strat.name == "DDP":
+        t = tot.to(strat.device) if strat.device.type == "cuda" else tot
+        tot = strat.reduce_eval(t).cpu()
+    elif strat.name == "MP" and isinstance(strat, PipelineDistStrategy):
+        # the last stage holds the outputs; share the result with every stage
+        t = tot.to(strat.device) if strat.device.type == "cuda" else tot
+        dist.broadcast(t, src=strat.world - 1)
+        tot = t.cpu()
+    if tot[2] == 0:
+        return float("nan"), float("nan")
+    return float(tot[0] / tot[2]), float(tot[1] / tot[2])
