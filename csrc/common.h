@@ -7,11 +7,15 @@
 
 #define DPA_API extern "C" __attribute__((visibility("default")))
 
-typedef __attribute__((ext_vector_type(8))) short bf16x8_t;   // 8 bf16 = one MFMA A/B fragment
-typedef __attribute__((ext_vector_type(4))) float f32x4_t;    // 16x16 MFMA accumulator
-typedef __attribute__((ext_vector_type(16))) float f32x16_t;  // 32x32 MFMA accumulator
+typedef unsigned short bf16_t;                                     // raw bf16 storage
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;      // MFMA 16x16x32 A/B fragment
+typedef __attribute__((ext_vector_type(4))) short s16x4_t;        // ds_read_b64_tr_b16 result
+typedef __attribute__((ext_vector_type(4))) float f32x4_t;        // 16x16 MFMA accumulator
+typedef __attribute__((ext_vector_type(16))) float f32x16_t;      // 32x32 MFMA accumulator
 typedef __attribute__((ext_vector_type(4))) unsigned int u32x4_t;
 typedef __attribute__((ext_vector_type(2))) unsigned int u32x2_t;
+
+#define LDS_PTR(T, p) ((__attribute__((address_space(3))) T*)(p))
 
 static __device__ __forceinline__ float bf2f(unsigned short h) {
   return __uint_as_float(((unsigned int)h) << 16);
@@ -24,11 +28,30 @@ static __device__ __forceinline__ unsigned short f2bf(float f) {
 static __device__ __forceinline__ unsigned int pack_bf2(float lo, float hi) {
   return (unsigned int)f2bf(lo) | ((unsigned int)f2bf(hi) << 16);
 }
+static __device__ __forceinline__ float lo_bf(unsigned int u) { return __uint_as_float(u << 16); }
+static __device__ __forceinline__ float hi_bf(unsigned int u) { return __uint_as_float(u & 0xffff0000u); }
 
 static __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
+}
+
+// block-wide sum for 256-thread blocks; `red` must hold >= 4 floats of LDS. Result valid in all threads.
+static __device__ __forceinline__ float block_sum_256(float v, float* red) {
+  v = wave_sum(v);
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[w] = v;
+  __syncthreads();
+  return red[0] + red[1] + red[2] + red[3];
+}
+
+// Bijective XCD-aware remap (MI355X: 8 XCDs, hardware deals blocks round-robin): consecutive
+// *logical* ids land on the same XCD, so neighbouring tiles share that XCD's L2.
+static __device__ __forceinline__ int xcd_remap(int hw, int nwg) {
+  const int q = nwg >> 3, r = nwg & 7, xcd = hw & 7, slot = hw >> 3;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + slot;
 }
 
 static inline int dpa_grid(long long n, int block, int cap = 2048) {

@@ -1,0 +1,240 @@
+// Implicit-GEMM convolution on MFMA (gfx950), NHWC bf16 activations, fp32 accumulation.
+//
+// One kernel family covers every "k-contiguous" conv-shaped product of the UNet step
+// (SURVEY §2.5 K1, K2, K6 fwd/dgrad; reference model/unet_parts.py:10-12,51-54):
+//   * conv3x3 forward          y[p][co]  = relu(b + sum_{tap,ci} x[p+off(tap)][ci] * W[co][tap][ci])
+//   * conv3x3 dgrad            dx[p][ci] = (sum_{tap,co} g[p+off(tap)][co] * Wflip[ci][tap][co]) * (x>0)
+//   * transposed-conv forward  y[2h+i][2w+j][co] = b + sum_ci x[h][w][ci] * W[ci][co][i][j]  (scatter)
+//   * transposed-conv dgrad    dx[h][w][ci] = (sum_{i,j,co} g[2h+i][2w+j][co] * W[ci][co][i][j]) * (x>0)
+//
+// GEMM view: M = output pixels (gathered rows of the source tensor, zero padding by predication),
+// N = output channels (rows of the packed weight matrix), K = taps x source channels.  Both
+// operands are K-contiguous in memory, staged global -> registers -> LDS (double buffered, one
+// barrier per K-step; the next tile's loads are issued before this tile's MFMAs) with an XOR
+// swizzle that makes every ds_read_b128 fragment read conflict-free (see tools/lds_banks.py).
+// MFMA: v_mfma_f32_16x16x32_bf16 with A = weights (rows = out channels) and B = pixels, so each
+// lane ends with 4 consecutive channels of one pixel -> 8-byte bf16 stores.  Epilogue fuses bias,
+// ReLU, the ReLU-backward mask of the *next* tensor, accumulation and the transposed-conv scatter.
+// Block -> tile mapping is XCD-aware (channel tiles of one pixel tile share an XCD's L2).
+#include "common.h"
+
+struct IgemmArgs {
+  const bf16_t* x;      // source activations [N][Hs][Ws][ldx] (channel offset folded into the pointer)
+  const bf16_t* w;      // packed weights [Ngemm][Kpad] bf16
+  const float* bias;    // [Cout] fp32 or null
+  bf16_t* y;            // output (channel offset folded into the pointer)
+  const bf16_t* mask;   // ReLU-backward mask source (same pixel grid as y, mode 0) or null
+  int ldx, ldy, ldm, mask_ch;
+  int N, Ho, Wo;        // GEMM-M pixel grid
+  int Hs, Ws, Cs;       // source grid and channels gathered per tap (Cs % 8 == 0)
+  int KH, KW, stride, pad;
+  int Ngemm, Kpad;      // GEMM N, K padded to a multiple of BK (packed weights zero-filled)
+  int mode;             // 0: y[m][n]   1: transposed-conv 2x2/s2 scatter, n = (2i+j)*Cout + co
+  int relu, accumulate, Cout;
+};
+
+template <int BK>
+__device__ __forceinline__ int swz_nk(int row, int chunk) {
+  if constexpr (BK == 32) return chunk ^ ((row >> 1) & 3);
+  else return chunk ^ (row & 7);
+}
+
+template <int BP, int BC, int BK, int WP, int WC>
+__global__ __launch_bounds__(256) void igemm_kernel(IgemmArgs a) {
+  constexpr int CPR = BK / 8;               // 16-byte chunks per LDS row
+  constexpr int RPP = 256 / CPR;            // rows covered by one pass of 256 threads
+  constexpr int LP = (BP + RPP - 1) / RPP;  // pixel-row loads per thread
+  constexpr int LW = (BC + RPP - 1) / RPP;  // weight-row loads per thread
+  constexpr int NWC = BC / WC;
+  constexpr int NWP = BP / WP;
+  static_assert(NWC * NWP == 4, "4 waves per block");
+  constexpr int TP = WP / 16, TC = WC / 16;
+  constexpr int RB = BK * 2;                // LDS row bytes
+  __shared__ __attribute__((aligned(16))) char lds[2][(BP + BC) * RB];
+
+  const int M = a.N * a.Ho * a.Wo;
+  const int nct = a.Ngemm / BC;
+  const int npt = (M + BP - 1) / BP;
+  const int bid = xcd_remap(blockIdx.x, npt * nct);
+  const int pt = bid / nct, ct = bid - pt * nct;
+  const int m0 = pt * BP, c0 = ct * BC;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wp = wid / NWC, wc = wid - wp * NWC;
+  const int lchunk = tid % CPR;
+  const int lrow = tid / CPR;
+
+  // per-thread pixel rows of the loader: decode (n, h, w) once
+  int pn[LP], ph[LP], pw[LP];
+  bool pok[LP];
+#pragma unroll
+  for (int i = 0; i < LP; ++i) {
+    const int r = lrow + i * RPP;
+    const int m = m0 + r;
+    pok[i] = (r < BP) && (m < M);
+    const int mm = pok[i] ? m : 0;
+    const int hw = a.Ho * a.Wo;
+    pn[i] = mm / hw;
+    const int rem = mm - pn[i] * hw;
+    ph[i] = rem / a.Wo;
+    pw[i] = rem - ph[i] * a.Wo;
+  }
+  const int taps = a.KH * a.KW;
+  const int S = a.Kpad / BK;
+  uint4 pr[LP], wr[LW];
+
+  auto gload = [&](int s) {
+    const int k0 = (s * CPR + lchunk) * 8;
+    const int tap = k0 / a.Cs;
+    const int ci = k0 - tap * a.Cs;
+    const int kh = tap / a.KW, kw = tap - (tap / a.KW) * a.KW;
+    const bool tok = tap < taps;
+#pragma unroll
+    for (int i = 0; i < LP; ++i) {
+      const int ih = ph[i] * a.stride + kh - a.pad;
+      const int iw = pw[i] * a.stride + kw - a.pad;
+      const bool ok = pok[i] && tok && ih >= 0 && ih < a.Hs && iw >= 0 && iw < a.Ws;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (ok) v = *reinterpret_cast<const uint4*>(a.x + ((long)(pn[i] * a.Hs + ih) * a.Ws + iw) * a.ldx + ci);
+      pr[i] = v;
+    }
+#pragma unroll
+    for (int i = 0; i < LW; ++i) {
+      const int r = lrow + i * RPP;
+      if (r < BC)
+        wr[i] = *reinterpret_cast<const uint4*>(a.w + (long)(c0 + r) * a.Kpad + s * BK + lchunk * 8);
+    }
+  };
+  auto lstore = [&](int buf) {
+    char* P = lds[buf];
+    char* Wt = lds[buf] + BP * RB;
+#pragma unroll
+    for (int i = 0; i < LP; ++i) {
+      const int r = lrow + i * RPP;
+      if (r < BP) *reinterpret_cast<uint4*>(P + r * RB + swz_nk<BK>(r, lchunk) * 16) = pr[i];
+    }
+#pragma unroll
+    for (int i = 0; i < LW; ++i) {
+      const int r = lrow + i * RPP;
+      if (r < BC) *reinterpret_cast<uint4*>(Wt + r * RB + swz_nk<BK>(r, lchunk) * 16) = wr[i];
+    }
+  };
+
+  f32x4_t acc[TC][TP];
+#pragma unroll
+  for (int ic = 0; ic < TC; ++ic)
+#pragma unroll
+    for (int ip = 0; ip < TP; ++ip) acc[ic][ip] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  gload(0);
+  lstore(0);
+  __syncthreads();
+  for (int s = 0; s < S; ++s) {
+    const int buf = s & 1;
+    if (s + 1 < S) gload(s + 1);
+    const char* P = lds[buf];
+    const char* Wt = lds[buf] + BP * RB;
+#pragma unroll
+    for (int kk = 0; kk < BK / 32; ++kk) {
+      const int chunk = kk * 4 + (lane >> 4);
+      bf16x8_t af[TC], bfr[TP];
+#pragma unroll
+      for (int ic = 0; ic < TC; ++ic) {
+        const int row = wc * WC + ic * 16 + (lane & 15);
+        af[ic] = *reinterpret_cast<const bf16x8_t*>(Wt + row * RB + swz_nk<BK>(row, chunk) * 16);
+      }
+#pragma unroll
+      for (int ip = 0; ip < TP; ++ip) {
+        const int row = wp * WP + ip * 16 + (lane & 15);
+        bfr[ip] = *reinterpret_cast<const bf16x8_t*>(P + row * RB + swz_nk<BK>(row, chunk) * 16);
+      }
+#pragma unroll
+      for (int ic = 0; ic < TC; ++ic)
+#pragma unroll
+        for (int ip = 0; ip < TP; ++ip)
+          acc[ic][ip] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ic], bfr[ip], acc[ic][ip], 0, 0, 0);
+    }
+    if (s + 1 < S) lstore(buf ^ 1);
+    __syncthreads();
+  }
+
+  // ------------------------------------------------------------------ epilogue
+#pragma unroll
+  for (int ip = 0; ip < TP; ++ip) {
+    const int m = m0 + wp * WP + ip * 16 + (lane & 15);
+    if (m >= M) continue;
+    long ybase;
+    if (a.mode == 0) {
+      ybase = (long)m * a.ldy;
+    } else {
+      const int hw = a.Ho * a.Wo;
+      const int n = m / hw, rem = m - n * hw, h = rem / a.Wo, w = rem - (rem / a.Wo) * a.Wo;
+      ybase = ((long)(n * 2 * a.Ho + 2 * h) * (2 * a.Wo) + 2 * w) * a.ldy;
+    }
+#pragma unroll
+    for (int ic = 0; ic < TC; ++ic) {
+      const int nidx = c0 + wc * WC + ic * 16 + 4 * (lane >> 4);
+      int co = nidx;
+      long off = ybase + nidx;
+      if (a.mode == 1) {
+        const int ij = nidx / a.Cout;
+        co = nidx - ij * a.Cout;
+        off = ybase + ((long)(ij >> 1) * (2 * a.Wo) + (ij & 1)) * a.ldy + co;
+      }
+      float v0 = acc[ic][ip][0], v1 = acc[ic][ip][1], v2 = acc[ic][ip][2], v3 = acc[ic][ip][3];
+      if (a.bias) {
+        const float* b = a.bias + co;   // views into the flat fp32 buffer: only 4-byte aligned
+        v0 += b[0]; v1 += b[1]; v2 += b[2]; v3 += b[3];
+      }
+      if (a.relu) {
+        v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f);
+      }
+      if (a.mask && co < a.mask_ch) {
+        const uint2 mk = *reinterpret_cast<const uint2*>(a.mask + (long)m * a.ldm + co);
+        v0 = lo_bf(mk.x) > 0.f ? v0 : 0.f;
+        v1 = hi_bf(mk.x) > 0.f ? v1 : 0.f;
+        v2 = lo_bf(mk.y) > 0.f ? v2 : 0.f;
+        v3 = hi_bf(mk.y) > 0.f ? v3 : 0.f;
+      }
+      uint2* dst = reinterpret_cast<uint2*>(a.y + off);
+      if (a.accumulate) {
+        const uint2 o = *dst;
+        v0 += lo_bf(o.x); v1 += hi_bf(o.x); v2 += lo_bf(o.y); v3 += hi_bf(o.y);
+      }
+      *dst = make_uint2(pack_bf2(v0, v1), pack_bf2(v2, v3));
+    }
+  }
+}
+
+template <int BP, int BC, int BK, int WP, int WC>
+static int launch_igemm(const IgemmArgs& a, hipStream_t st) {
+  const int M = a.N * a.Ho * a.Wo;
+  const int grid = ((M + BP - 1) / BP) * (a.Ngemm / BC);
+  hipLaunchKernelGGL((igemm_kernel<BP, BC, BK, WP, WC>), dim3(grid), dim3(256), 0, st, a);
+  return (int)hipGetLastError();
+}
+
+// cfg: 0 = auto.  Tile families (BP x BC x BK): 1: 128x128x32  2: 128x128x64  3: 128x64x32
+//      4: 128x64x64  5: 256x32x32  6: 256x32x64  7: 64x128x64 (small-M deep layers)
+DPA_API int dpa_igemm(const IgemmArgs* args, int cfg, hipStream_t st) {
+  IgemmArgs a = *args;
+  if ((a.Cs & 7) || (a.ldx & 7) || (a.ldy & 3) || (a.Kpad & 31) || (a.Ngemm & 31)) return (int)hipErrorInvalidValue;
+  if (a.mode == 1 && (a.Cout & 3)) return (int)hipErrorInvalidValue;
+  if (cfg == 0) {
+    const long M = (long)a.N * a.Ho * a.Wo;
+    const bool k64 = (a.Kpad % 64) == 0;
+    if (a.Ngemm % 128 == 0) cfg = (M <= 16384 && a.Ngemm >= 256) ? (k64 ? 7 : 1) : (k64 ? 2 : 1);
+    else if (a.Ngemm % 64 == 0) cfg = k64 ? 4 : 3;
+    else cfg = k64 ? 6 : 5;
+  }
+  switch (cfg) {
+    case 1: if (a.Ngemm % 128) break; return launch_igemm<128, 128, 32, 64, 64>(a, st);
+    case 2: if (a.Ngemm % 128 || a.Kpad % 64) break; return launch_igemm<128, 128, 64, 64, 64>(a, st);
+    case 3: if (a.Ngemm % 64) break; return launch_igemm<128, 64, 32, 64, 32>(a, st);
+    case 4: if (a.Ngemm % 64 || a.Kpad % 64) break; return launch_igemm<128, 64, 64, 64, 32>(a, st);
+    case 5: return launch_igemm<256, 32, 32, 64, 32>(a, st);
+    case 6: if (a.Kpad % 64) break; return launch_igemm<256, 32, 64, 64, 32>(a, st);
+    case 7: if (a.Ngemm % 128 || a.Kpad % 64) break; return launch_igemm<64, 128, 64, 32, 64>(a, st);
+    default: break;
+  }
+  return (int)hipErrorInvalidValue;
+}

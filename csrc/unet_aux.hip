@@ -1,0 +1,352 @@
+// Memory-bound UNet kernels for gfx950 (everything that is not a GEMM), all NHWC bf16, 16-byte
+// vector accesses (8 channels per lane), fp32 math:
+//   * input conversion fp32 NCHW [B,3,H,W] -> bf16 NHWC8 (zero channels 3..7)  
+//   * 2x2/s2 max-pool, reading the skip from the decoder's concat buffer        (K5 fwd)
+//   * fused max-pool backward + skip-gradient add + ReLU-backward mask          (K5 bwd + K7 + K4 bwd)
+//   * batched weight packing fp32 PyTorch layout -> bf16 GEMM layouts (one launch per step)
+//   * fused 1x1 segmap + sigmoid + BCE + Dice partial sums, and its fused backward (K8-K11)
+// Reference semantics: model/unet_parts.py:26-41 (MaxPool2d(2,2)), model/unet_model.py:10-11
+// (segmap, Sigmoid), utils/utils.py:9-25 (BCE - log Dice, global over the batch).
+#include "common.h"
+
+// ------------------------------------------------------------------------------ input conversion
+__global__ __launch_bounds__(256) void nchw3_to_nhwc8_kernel(const float* __restrict__ x, bf16_t* __restrict__ y, int B,
+                                                             int C, int HW) {
+  const long tot = (long)B * HW;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < tot; i += (long)gridDim.x * blockDim.x) {
+    const long b = i / HW, p = i - b * HW;
+    float v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int c = 0; c < C && c < 8; ++c) v[c] = x[(b * C + c) * HW + p];
+    uint4 o = make_uint4(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]), pack_bf2(v[4], v[5]), pack_bf2(v[6], v[7]));
+    *reinterpret_cast<uint4*>(y + i * 8) = o;
+  }
+}
+DPA_API int dpa_input_nhwc8(const float* x, bf16_t* y, int B, int C, int H, int W, hipStream_t st) {
+  if (C > 8) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(nchw3_to_nhwc8_kernel, dim3(dpa_grid((long)B * H * W, 256, 8192)), dim3(256), 0, st, x, y, B, C, H * W);
+  return (int)hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------ max-pool 2x2 / s2
+// Floor semantics (nn.MaxPool2d(2,2)); first maximum in scan order wins (matches PyTorch).
+__global__ __launch_bounds__(256) void maxpool2_kernel(const bf16_t* __restrict__ x, int ldx, bf16_t* __restrict__ y, int ldy,
+                                                       int N, int H, int W, int C) {
+  const int Ho = H / 2, Wo = W / 2, CC = C / 8;
+  const long tot = (long)N * Ho * Wo * CC;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < tot; i += (long)gridDim.x * blockDim.x) {
+    const int cc = (int)(i % CC);
+    const long op = i / CC;
+    const int ow = (int)(op % Wo);
+    const long t = op / Wo;
+    const int oh = (int)(t % Ho);
+    const int n = (int)(t / Ho);
+    const long p00 = ((long)(n * H + 2 * oh) * W + 2 * ow);
+    const uint4 a = *reinterpret_cast<const uint4*>(x + p00 * ldx + cc * 8);
+    const uint4 b = *reinterpret_cast<const uint4*>(x + (p00 + 1) * ldx + cc * 8);
+    const uint4 c = *reinterpret_cast<const uint4*>(x + (p00 + W) * ldx + cc * 8);
+    const uint4 d = *reinterpret_cast<const uint4*>(x + (p00 + W + 1) * ldx + cc * 8);
+    const unsigned int* pa = &a.x; const unsigned int* pb = &b.x; const unsigned int* pc = &c.x; const unsigned int* pd = &d.x;
+    unsigned int o[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float l = fmaxf(fmaxf(lo_bf(pa[k]), lo_bf(pb[k])), fmaxf(lo_bf(pc[k]), lo_bf(pd[k])));
+      float h = fmaxf(fmaxf(hi_bf(pa[k]), hi_bf(pb[k])), fmaxf(hi_bf(pc[k]), hi_bf(pd[k])));
+      o[k] = pack_bf2(l, h);
+    }
+    *reinterpret_cast<uint4*>(y + op * ldy + cc * 8) = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+}
+DPA_API int dpa_maxpool2(const bf16_t* x, int ldx, bf16_t* y, int ldy, int N, int H, int W, int C, hipStream_t st) {
+  if ((C & 7) || (ldx & 7) || (ldy & 7)) return (int)hipErrorInvalidValue;
+  const long tot = (long)N * (H / 2) * (W / 2) * (C / 8);
+  hipLaunchKernelGGL(maxpool2_kernel, dim3(dpa_grid(tot, 256, 8192)), dim3(256), 0, st, x, ldx, y, ldy, N, H, W, C);
+  return (int)hipGetLastError();
+}
+
+// g[p][c] = (dskip[p][c] + (p is the window argmax ? dpool[p/2][c] : 0)) * (skip[p][c] > 0)
+// dskip may be null (no decoder contribution).  Pixels outside the pooled area (odd H/W) get only dskip.
+__global__ __launch_bounds__(256) void pool_bwd_kernel(const bf16_t* __restrict__ skip, int lds, const bf16_t* __restrict__ dskip,
+                                                       int ldd, const bf16_t* __restrict__ dpool, int ldp, bf16_t* __restrict__ g,
+                                                       int ldg, int N, int H, int W, int C) {
+  const int Ho = H / 2, Wo = W / 2, CC = C / 8;
+  const int Hw = (H + 1) / 2, Ww = (W + 1) / 2;   // windows covering every pixel
+  const long tot = (long)N * Hw * Ww * CC;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < tot; i += (long)gridDim.x * blockDim.x) {
+    const int cc = (int)(i % CC);
+    const long op = i / CC;
+    const int ow = (int)(op % Ww);
+    const long t = op / Ww;
+    const int oh = (int)(t % Hw);
+    const int n = (int)(t / Hw);
+    const bool pooled = oh < Ho && ow < Wo;
+    float dp[8];
+    if (pooled) {
+      const uint4 v = *reinterpret_cast<const uint4*>(dpool + ((long)(n * Ho + oh) * Wo + ow) * ldp + cc * 8);
+      const unsigned int* pv = &v.x;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) { dp[2 * k] = lo_bf(pv[k]); dp[2 * k + 1] = hi_bf(pv[k]); }
+    }
+    float sv[4][8];
+    long pix[4];
+    bool in[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int h = 2 * oh + (q >> 1), w = 2 * ow + (q & 1);
+      in[q] = h < H && w < W;
+      pix[q] = ((long)(n * H + h) * W + w);
+      if (in[q]) {
+        const uint4 v = *reinterpret_cast<const uint4*>(skip + pix[q] * lds + cc * 8);
+        const unsigned int* pv = &v.x;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) { sv[q][2 * k] = lo_bf(pv[k]); sv[q][2 * k + 1] = hi_bf(pv[k]); }
+      } else {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) sv[q][k] = 0.f;
+      }
+    }
+    int am[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      int best = 0;
+      float bv = sv[0][k];
+#pragma unroll
+      for (int q = 1; q < 4; ++q)
+        if (sv[q][k] > bv) { bv = sv[q][k]; best = q; }
+      am[k] = best;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (!in[q]) continue;
+      float o[8];
+      if (dskip) {
+        const uint4 v = *reinterpret_cast<const uint4*>(dskip + pix[q] * ldd + cc * 8);
+        const unsigned int* pv = &v.x;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) { o[2 * k] = lo_bf(pv[k]); o[2 * k + 1] = hi_bf(pv[k]); }
+      } else {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) o[k] = 0.f;
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        if (pooled && am[k] == q) o[k] += dp[k];
+        if (!(sv[q][k] > 0.f)) o[k] = 0.f;
+      }
+      *reinterpret_cast<uint4*>(g + pix[q] * ldg + cc * 8) =
+          make_uint4(pack_bf2(o[0], o[1]), pack_bf2(o[2], o[3]), pack_bf2(o[4], o[5]), pack_bf2(o[6], o[7]));
+    }
+  }
+}
+DPA_API int dpa_pool_bwd(const bf16_t* skip, int lds, const bf16_t* dskip, int ldd, const bf16_t* dpool, int ldp, bf16_t* g,
+                         int ldg, int N, int H, int W, int C, hipStream_t st) {
+  if ((C & 7) || (lds & 7) || (ldd & 7) || (ldp & 7) || (ldg & 7)) return (int)hipErrorInvalidValue;
+  const long tot = (long)N * ((H + 1) / 2) * ((W + 1) / 2) * (C / 8);
+  hipLaunchKernelGGL(pool_bwd_kernel, dim3(dpa_grid(tot, 256, 8192)), dim3(256), 0, st, skip, lds, dskip, ldd, dpool, ldp, g, ldg,
+                     N, H, W, C);
+  return (int)hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------ weight packing
+// One launch packs every layer: blockIdx.y selects a descriptor.
+//   mode 0: Conv2d fwd     dst[co][tap*Cs + ci]      = W[co][ci][tap]          (Ngemm=Cout, K=9*Cs)
+//   mode 1: Conv2d dgrad   dst[ci][tap*Cout + co]    = W[co][ci][8-tap]        (Ngemm=Cin,  K=9*Cout)
+//   mode 2: ConvT fwd      dst[(2i+j)*Cout+co][ci]   = W[ci][co][i][j]         (Ngemm=4*Cout, K=Cin)
+//   mode 3: ConvT dgrad    dst[ci][(2i+j)*Cout+co]   = W[ci][co][i][j]         (Ngemm=Cin, K=4*Cout)
+// k >= K (padding to Kpad) and ci >= Cin (first-layer channel padding) are zero.
+struct PackDesc {
+  long long src;   // element offset of W in the flat fp32 parameter buffer
+  long long dst;   // element offset in the packed bf16 buffer
+  int mode, Cout, Cin, Cs, Ngemm, Kpad;
+};
+__global__ __launch_bounds__(256) void pack_kernel(const float* __restrict__ flat, bf16_t* __restrict__ packed,
+                                                   const PackDesc* __restrict__ descs) {
+  const PackDesc d = descs[blockIdx.y];
+  const long tot = (long)d.Ngemm * d.Kpad;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < tot; i += (long)gridDim.x * blockDim.x) {
+    const int n = (int)(i / d.Kpad), k = (int)(i - (long)n * d.Kpad);
+    float v = 0.f;
+    const float* W = flat + d.src;
+    if (d.mode == 0) {
+      const int tap = k / d.Cs, ci = k - tap * d.Cs;
+      if (tap < 9 && ci < d.Cin) v = W[((long)n * d.Cin + ci) * 9 + tap];
+    } else if (d.mode == 1) {
+      const int tap = k / d.Cout, co = k - tap * d.Cout;
+      if (tap < 9) v = W[((long)co * d.Cin + n) * 9 + (8 - tap)];
+    } else if (d.mode == 2) {
+      const int ij = n / d.Cout, co = n - ij * d.Cout;
+      if (k < d.Cin) v = W[((long)k * d.Cout + co) * 4 + ij];
+    } else {
+      const int ij = k / d.Cout, co = k - ij * d.Cout;
+      if (ij < 4) v = W[((long)n * d.Cout + co) * 4 + ij];
+    }
+    packed[d.dst + i] = f2bf(v);
+  }
+}
+DPA_API int dpa_pack_weights(const float* flat, bf16_t* packed, const void* descs, int ndesc, long long max_elems,
+                             hipStream_t st) {
+  if (ndesc <= 0) return 0;
+  dim3 grid(dpa_grid(max_elems, 256, 1024), ndesc);
+  hipLaunchKernelGGL(pack_kernel, grid, dim3(256), 0, st, flat, packed, reinterpret_cast<const PackDesc*>(descs));
+  return (int)hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------ head + loss
+// z = b + sum_c y[p][c] w[c];  p = sigmoid(z);  BCE with log clamped at -100 (torch.nn.BCELoss);
+// partial sums S = [sum BCE, sum p*[t==1], sum p, sum [t==1]] per block -> slab [grid][4].
+// If probs != null, p is also written (inference).
+#define HEAD_MAXC 64
+template <int C>
+__device__ __forceinline__ void load_row(const bf16_t* y, float* v) {
+#pragma unroll
+  for (int k = 0; k < C / 8; ++k) {
+    const uint4 u = *reinterpret_cast<const uint4*>(y + k * 8);
+    const unsigned int* pu = &u.x;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { v[8 * k + 2 * e] = lo_bf(pu[e]); v[8 * k + 2 * e + 1] = hi_bf(pu[e]); }
+  }
+}
+
+template <int C>
+__global__ __launch_bounds__(256) void head_fwd_kernel(const bf16_t* __restrict__ y, int ldy, const float* __restrict__ w,
+                                                       const float* __restrict__ b, const float* __restrict__ t,
+                                                       float* __restrict__ slab, float* __restrict__ probs, long P) {
+  __shared__ float red[4];
+  float wv[C];
+#pragma unroll
+  for (int c = 0; c < C; ++c) wv[c] = w[c];
+  const float bias = b[0];
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < P; i += (long)gridDim.x * blockDim.x) {
+    float v[C];
+    load_row<C>(y + i * ldy, v);
+    float z = bias;
+#pragma unroll
+    for (int c = 0; c < C; ++c) z = fmaf(v[c], wv[c], z);
+    const float p = 1.f / (1.f + __expf(-z));
+    if (probs) probs[i] = p;
+    if (t) {
+      const float tt = t[i];
+      const float lp = fmaxf(__logf(p), -100.f), l1p = fmaxf(__logf(1.f - p), -100.f);
+      s0 -= tt * lp + (1.f - tt) * l1p;
+      const float one = tt == 1.f ? 1.f : 0.f;
+      s1 += p * one;
+      s2 += p;
+      s3 += one;
+    }
+  }
+  if (!slab) return;
+  s0 = block_sum_256(s0, red);
+  s1 = block_sum_256(s1, red);
+  s2 = block_sum_256(s2, red);
+  s3 = block_sum_256(s3, red);
+  if (threadIdx.x == 0) {
+    float* o = slab + 4 * (long)blockIdx.x;
+    o[0] = s0; o[1] = s1; o[2] = s2; o[3] = s3;
+  }
+}
+
+// deterministic sum of the [nblk][K] slab into out[K] (one block)
+__global__ __launch_bounds__(256) void slab_sum_kernel(const float* __restrict__ slab, int nblk, int K, float* __restrict__ out,
+                                                       int accumulate) {
+  __shared__ float red[4];
+  for (int k = 0; k < K; ++k) {
+    float s = 0.f;
+    for (int i = threadIdx.x; i < nblk; i += blockDim.x) s += slab[(long)i * K + k];
+    s = block_sum_256(s, red);
+    if (threadIdx.x == 0) out[k] = accumulate ? out[k] + s : s;
+  }
+}
+
+static int head_grid(long P) { return dpa_grid(P, 256, 2048); }
+
+DPA_API int dpa_head_fwd(const bf16_t* y, int ldy, int C, const float* w, const float* b, const float* t, float* slab,
+                         float* S, float* probs, long long P, hipStream_t st) {
+  const int grid = head_grid(P);
+  if (ldy & 7) return (int)hipErrorInvalidValue;
+  switch (C) {
+    case 8: hipLaunchKernelGGL(head_fwd_kernel<8>, dim3(grid), dim3(256), 0, st, y, ldy, w, b, t, slab, probs, (long)P); break;
+    case 16: hipLaunchKernelGGL(head_fwd_kernel<16>, dim3(grid), dim3(256), 0, st, y, ldy, w, b, t, slab, probs, (long)P); break;
+    case 32: hipLaunchKernelGGL(head_fwd_kernel<32>, dim3(grid), dim3(256), 0, st, y, ldy, w, b, t, slab, probs, (long)P); break;
+    case 64: hipLaunchKernelGGL(head_fwd_kernel<64>, dim3(grid), dim3(256), 0, st, y, ldy, w, b, t, slab, probs, (long)P); break;
+    default: return (int)hipErrorInvalidValue;
+  }
+  if (slab && S) hipLaunchKernelGGL(slab_sum_kernel, dim3(1), dim3(256), 0, st, slab, grid, 4, S, 0);
+  return (int)hipGetLastError();
+}
+
+// Backward.  dS[4] = dLoss/dS (from autograd).  Per pixel (torch formulas: BCE backward
+// (p - t) / max(p(1-p), 1e-12), sigmoid backward g*p*(1-p)):
+//   dp = dS0 * (p-t)/max(p(1-p),1e-12) + dS1*[t==1] + dS2 ;  dz = dp * p * (1-p)
+//   gy[p][c] = dz * w[c] * (y[p][c] > 0)      (ReLU backward of the last decoder conv)
+//   dw[c] += dz * y[p][c] ;  db += dz          (block partials -> slab [grid][C+1])
+template <int C>
+__global__ __launch_bounds__(256) void head_bwd_kernel(const bf16_t* __restrict__ y, int ldy, const float* __restrict__ w,
+                                                       const float* __restrict__ b, const float* __restrict__ t,
+                                                       const float* __restrict__ dS, bf16_t* __restrict__ gy, int ldg,
+                                                       float* __restrict__ slab, long P) {
+  __shared__ float red[4];
+  float wv[C], dw[C];
+#pragma unroll
+  for (int c = 0; c < C; ++c) { wv[c] = w[c]; dw[c] = 0.f; }
+  const float bias = b[0];
+  const float d0 = dS[0], d1 = dS[1], d2 = dS[2];
+  float db = 0.f;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < P; i += (long)gridDim.x * blockDim.x) {
+    float v[C];
+    load_row<C>(y + i * ldy, v);
+    float z = bias;
+#pragma unroll
+    for (int c = 0; c < C; ++c) z = fmaf(v[c], wv[c], z);
+    const float p = 1.f / (1.f + __expf(-z));
+    const float tt = t[i];
+    const float one = tt == 1.f ? 1.f : 0.f;
+    const float dp = d0 * (p - tt) / fmaxf((1.f - p) * p, 1e-12f) + d1 * one + d2;
+    const float dz = dp * (1.f - p) * p;
+    db += dz;
+    unsigned int o[C / 2];
+#pragma unroll
+    for (int c = 0; c < C; c += 2) {
+      dw[c] = fmaf(dz, v[c], dw[c]);
+      dw[c + 1] = fmaf(dz, v[c + 1], dw[c + 1]);
+      const float g0 = v[c] > 0.f ? dz * wv[c] : 0.f;
+      const float g1 = v[c + 1] > 0.f ? dz * wv[c + 1] : 0.f;
+      o[c / 2] = pack_bf2(g0, g1);
+    }
+#pragma unroll
+    for (int k = 0; k < C / 8; ++k)
+      *reinterpret_cast<uint4*>(gy + i * ldg + 8 * k) = make_uint4(o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]);
+  }
+  float* out = slab + (long)blockIdx.x * (C + 1);
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    const float s = block_sum_256(dw[c], red);
+    if (threadIdx.x == 0) out[c] = s;
+  }
+  const float s = block_sum_256(db, red);
+  if (threadIdx.x == 0) out[C] = s;
+}
+
+// gw: segmap weight grad [C] (+=), gb: bias grad [1] (+=); contiguous in the flat buffer is not assumed.
+__global__ void head_grad_finish(const float* __restrict__ tmp, float* __restrict__ gw, float* __restrict__ gb, int C) {
+  const int c = threadIdx.x;
+  if (c < C) gw[c] += tmp[c];
+  if (c == C) gb[0] += tmp[C];
+}
+
+DPA_API int dpa_head_bwd(const bf16_t* y, int ldy, int C, const float* w, const float* b, const float* t, const float* dS,
+                         bf16_t* gy, int ldg, float* slab, float* tmp, float* gw, float* gb, long long P, hipStream_t st) {
+  const int grid = head_grid(P);
+  if ((ldy & 7) || (ldg & 7)) return (int)hipErrorInvalidValue;
+  switch (C) {
+    case 8: hipLaunchKernelGGL(head_bwd_kernel<8>, dim3(grid), dim3(256), 0, st, y, ldy, w, b, t, dS, gy, ldg, slab, (long)P); break;
+    case 16: hipLaunchKernelGGL(head_bwd_kernel<16>, dim3(grid), dim3(256), 0, st, y, ldy, w, b, t, dS, gy, ldg, slab, (long)P); break;
+    case 32: hipLaunchKernelGGL(head_bwd_kernel<32>, dim3(grid), dim3(256), 0, st, y, ldy, w, b, t, dS, gy, ldg, slab, (long)P); break;
+    case 64: hipLaunchKernelGGL(head_bwd_kernel<64>, dim3(grid), dim3(256), 0, st, y, ldy, w, b, t, dS, gy, ldg, slab, (long)P); break;
+    default: return (int)hipErrorInvalidValue;
+  }
+  hipLaunchKernelGGL(slab_sum_kernel, dim3(1), dim3(256), 0, st, slab, grid, C + 1, tmp, 0);
+  hipLaunchKernelGGL(head_grad_finish, dim3(1), dim3(128), 0, st, tmp, gw, gb, C);
+  return (int)hipGetLastError();
+}
+
+DPA_API int dpa_head_slab_blocks(long long P) { return head_grid(P); }

@@ -1,0 +1,288 @@
+// Weight gradients of the UNet convolutions on MFMA (gfx950): split-K over pixels, all taps of a
+// tile inside one block, deterministic two-stage reduction (reference
+// layers model/unet_parts.py:10-12 Conv2d, :51-54 ConvTranspose2d).
+//
+//   out[tap][m][n] = sum_{p in pixel grid} A[srcA(p,tap)][m] * B[srcB(p,tap)][n]
+//     conv3x3   : A = grad of conv output g[p][co] (tap independent), B = conv input x shifted by the
+//                 tap (zero padded)                 -> dW[co][ci][kh][kw]
+//     convT 2x2 : A = grad of the upsampled output gathered at (2h+i, 2w+j), B = input x[p][ci]
+//                 -> dW[ci][co][i][j]
+//
+// GEMM K is the pixel dimension (up to N*H*W = 8.4M at 512^2, batch 32), so each block handles one
+// (m-tile, n-tile) pair for ALL taps over a contiguous range of pixels (its split) and writes an fp32
+// slab; `dpa_wgrad_reduce` sums the slabs in a fixed order (bitwise reproducible, no atomics) and
+// accumulates into the flat fp32 gradient buffer in the PyTorch parameter layout.
+//
+// Both operands are channel-contiguous in memory with K (=pixels) as the row index, so tiles are
+// staged as [32 pixels][channels] LDS images (16-B chunks, XOR swizzled) and fragments are read with
+// the gfx950 transposed LDS read ds_read_b64_tr_b16, conflict-free for 64/128/256-byte rows.
+// The tap-independent operand is staged once per pixel chunk and reused by all taps (9 for conv).
+// Bias gradients (sum of A over pixels) come from the n-tile-0 blocks' LDS images.
+#include "common.h"
+
+struct WgradArgs {
+  const bf16_t* A; const bf16_t* B;
+  float* slab;          // [splits][T][M][Nc]
+  float* bslab;         // [splits][M] or null (bias gradient partials)
+  int lda, ldb;
+  int N, Hg, Wg;        // pixel grid p = (n, h, w)
+  int HA, WA, HB, WB;   // spatial dims of A and B tensors
+  int M, Nc;            // channels of A (GEMM rows) and B (GEMM cols, may be < tile width: zero filled)
+  int s, pad, KW;       // tap-dependent operand is read at (h*s + kh - pad, w*s + kw - pad)
+  int pix_per_split, splits;
+};
+
+template <int RB>
+__device__ __forceinline__ int swz_kk(int r) {
+  if constexpr (RB == 64) return ((r >> 3) & 1) * 2;
+  else if constexpr (RB == 128) return (((r >> 1) & 1) * 2) ^ (((r >> 3) & 1) * 4);
+  else if constexpr (RB == 256) return ((r & 1) * 2) ^ (((r >> 1) & 1) * 4) ^ (((r >> 3) & 1) * 8);
+  else return 0;
+}
+
+// 8 consecutive k (pixel rows 8g..8g+7 of a [32][RB] image) for the 16 columns starting at col0
+template <int RB>
+__device__ __forceinline__ bf16x8_t tr_frag(const char* img, int col0, int lane) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int col = col0 + 4 * p;
+  const int ch = col >> 3, hb = (col & 7) * 2;
+  const int r0 = 8 * g + q, r1 = r0 + 4;
+  const char* a0 = img + r0 * RB + ((ch ^ swz_kk<RB>(r0)) << 4) + hb;
+  const char* a1 = img + r1 * RB + ((ch ^ swz_kk<RB>(r1)) << 4) + hb;
+  s16x4_t v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4_t, a0));
+  s16x4_t v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4_t, a1));
+  typedef __attribute__((ext_vector_type(8))) short s16x8_t;
+  s16x8_t v = __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8_t, v);
+}
+
+template <int BM, int BN, int WM, int WN, int T, bool TAPA>
+__global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void wgrad_kernel(WgradArgs a) {
+  constexpr int NWN = BN / WN, NW = (BM / WM) * NWN, NT = 64 * NW;
+  constexpr int TA = TAPA ? T : 1, TB = TAPA ? 1 : T;
+  constexpr int CPRA = BM / 8, CPRB = BN / 8, RBA = BM * 2, RBB = BN * 2;
+  constexpr int IMGA = 32 * RBA, IMGB = 32 * RBB;
+  constexpr int CHA = TA * CPRA, CH = CHA + TB * CPRB;   // 16-B chunks per pixel per stage
+  constexpr int SLOTS = NT / 32;
+  constexpr int L = (CH + SLOTS - 1) / SLOTS;
+  constexpr int TM = WM / 16, TN = WN / 16;
+  __shared__ __attribute__((aligned(16))) char lds[TA * IMGA + TB * IMGB];
+
+  const int nmt = a.M / BM;
+  const int nnt = (a.Nc + BN - 1) / BN;
+  const int tiles = nmt * nnt;
+  const int bid = xcd_remap(blockIdx.x, tiles * a.splits);
+  const int split = bid / tiles, tile = bid - split * tiles;
+  const int mt = tile / nnt, nt = tile - mt * nnt;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const long P = (long)a.N * a.Hg * a.Wg;
+  const long pbeg = (long)split * a.pix_per_split;
+  long pend = pbeg + a.pix_per_split;
+  if (pend > P) pend = P;
+  const int nst = (int)((pend - pbeg + 31) / 32);
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / NWN, wn = wid - wm * NWN;
+  const int lpx = tid / SLOTS, lslot = tid - lpx * SLOTS;
+  const bool do_bias = a.bslab != nullptr && nt == 0;
+
+  uint4 reg[L];
+  auto gload = [&](int st) {
+    const long p = pbeg + (long)st * 32 + lpx;
+    const bool pok = p < pend;
+    int n = 0, h = 0, w = 0;
+    if (pok) {
+      const int hw = a.Hg * a.Wg;
+      n = (int)(p / hw);
+      const int rem = (int)(p - (long)n * hw);
+      h = rem / a.Wg;
+      w = rem - h * a.Wg;
+    }
+#pragma unroll
+    for (int j = 0; j < L; ++j) {
+      const int c = lslot + j * SLOTS;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (c < CH && pok) {
+        const bool isA = c < CHA;
+        const int cl = isA ? c : c - CHA;
+        const int cpr = isA ? CPRA : CPRB;
+        const int tap = cl / cpr, cc = cl - tap * cpr;
+        const bool dep = (isA == TAPA);
+        int ih = h, iw = w, H = isA ? a.HA : a.HB, W = isA ? a.WA : a.WB;
+        if (dep) {
+          const int kh = tap / a.KW, kw = tap - (tap / a.KW) * a.KW;
+          ih = h * a.s + kh - a.pad;
+          iw = w * a.s + kw - a.pad;
+        }
+        const int ch = (isA ? m0 : n0) + cc * 8;
+        const int nch = isA ? a.M : a.Nc;
+        if (ih >= 0 && ih < H && iw >= 0 && iw < W && ch < nch) {
+          const bf16_t* src = isA ? a.A : a.B;
+          const int ld = isA ? a.lda : a.ldb;
+          v = *reinterpret_cast<const uint4*>(src + ((long)(n * H + ih) * W + iw) * ld + ch);
+        }
+      }
+      reg[j] = v;
+    }
+  };
+  auto lstore = [&]() {
+#pragma unroll
+    for (int j = 0; j < L; ++j) {
+      const int c = lslot + j * SLOTS;
+      if (c < CH) {
+        if (c < CHA) {
+          const int tap = c / CPRA, cc = c - tap * CPRA;
+          *reinterpret_cast<uint4*>(lds + tap * IMGA + lpx * RBA + ((cc ^ swz_kk<RBA>(lpx)) << 4)) = reg[j];
+        } else {
+          const int cl = c - CHA, tap = cl / CPRB, cc = cl - tap * CPRB;
+          *reinterpret_cast<uint4*>(lds + TA * IMGA + tap * IMGB + lpx * RBB + ((cc ^ swz_kk<RBB>(lpx)) << 4)) = reg[j];
+        }
+      }
+    }
+  };
+
+  f32x4_t acc[T][TM][TN];
+#pragma unroll
+  for (int t = 0; t < T; ++t)
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[t][i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  float bsum = 0.f;
+
+  if (nst > 0) {
+    gload(0);
+    lstore();
+  }
+  __syncthreads();
+  for (int st = 0; st < nst; ++st) {
+    if (st + 1 < nst) gload(st + 1);
+    if constexpr (TAPA) {
+      bf16x8_t bf[TN];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bf[j] = tr_frag<RBB>(lds + TA * IMGA, wn * WN + j * 16, lane);
+#pragma unroll
+      for (int t = 0; t < T; ++t) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const bf16x8_t af = tr_frag<RBA>(lds + t * IMGA, wm * WM + i * 16, lane);
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[t][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf[j], acc[t][i][j], 0, 0, 0);
+        }
+      }
+    } else {
+      bf16x8_t af[TM];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[i] = tr_frag<RBA>(lds, wm * WM + i * 16, lane);
+#pragma unroll
+      for (int t = 0; t < T; ++t) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const bf16x8_t bf = tr_frag<RBB>(lds + TA * IMGA + t * IMGB, wn * WN + j * 16, lane);
+#pragma unroll
+          for (int i = 0; i < TM; ++i) acc[t][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf, acc[t][i][j], 0, 0, 0);
+        }
+      }
+    }
+    if (do_bias && tid < BM) {
+      const int ch = tid >> 3, e = tid & 7;
+#pragma unroll
+      for (int t = 0; t < TA; ++t)
+        for (int r = 0; r < 32; ++r) {
+          const bf16_t v = *reinterpret_cast<const bf16_t*>(lds + t * IMGA + r * RBA + ((ch ^ swz_kk<RBA>(r)) << 4) + e * 2);
+          bsum += bf2f(v);
+        }
+    }
+    __syncthreads();
+    if (st + 1 < nst) {
+      lstore();
+      __syncthreads();
+    }
+  }
+
+  // epilogue: fp32 partial slab for this split
+#pragma unroll
+  for (int t = 0; t < T; ++t)
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int n = n0 + wn * WN + j * 16 + (lane & 15);
+        if (n >= a.Nc) continue;
+        const int mb = m0 + wm * WM + i * 16 + 4 * (lane >> 4);
+        float* dst = a.slab + (((long)split * T + t) * a.M + mb) * a.Nc + n;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) dst[(long)r * a.Nc] = acc[t][i][j][r];
+      }
+  if (do_bias && tid < BM) a.bslab[(long)split * a.M + m0 + tid] = bsum;
+}
+
+template <int BM, int BN, int WM, int WN, int T, bool TAPA>
+static int launch_wgrad(const WgradArgs& a, hipStream_t st) {
+  const int tiles = (a.M / BM) * ((a.Nc + BN - 1) / BN);
+  constexpr int NT = 64 * (BM / WM) * (BN / WN);
+  hipLaunchKernelGGL((wgrad_kernel<BM, BN, WM, WN, T, TAPA>), dim3(tiles * a.splits), dim3(NT), 0, st, a);
+  return (int)hipGetLastError();
+}
+
+// kind: 0 = conv3x3 (T=9, B tap-dependent), 1 = transposed conv 2x2/s2 (T=4, A tap-dependent).
+// cfg: 0 = auto; otherwise a tile id (see switch).  M % BM == 0 is required.
+DPA_API int dpa_wgrad(const WgradArgs* args, int kind, int cfg, hipStream_t st) {
+  const WgradArgs& a = *args;
+  if ((a.M & 31) || (a.lda & 7) || (a.ldb & 7) || (a.pix_per_split & 31) || a.splits < 1) return (int)hipErrorInvalidValue;
+  if (cfg == 0) {
+    if (kind == 0) cfg = (a.Nc <= 16) ? 1 : (a.M >= 64 && a.Nc >= 32) ? 3 : 2;
+    else cfg = (a.M >= 64 && a.Nc >= 64) ? 12 : 11;
+  }
+  if (kind == 0) {
+    switch (cfg) {
+      case 1: if (a.M % 32) break; return launch_wgrad<32, 16, 16, 16, 9, false>(a, st);   // first layer (Cin<=16)
+      case 2: if (a.M % 32) break; return launch_wgrad<32, 32, 16, 16, 9, false>(a, st);
+      case 3: if (a.M % 64) break; return launch_wgrad<64, 32, 32, 16, 9, false>(a, st);
+      case 4: if (a.M % 64) break; return launch_wgrad<64, 64, 32, 32, 9, false>(a, st);
+      default: break;
+    }
+  } else {
+    switch (cfg) {
+      case 11: if (a.M % 32) break; return launch_wgrad<32, 32, 16, 16, 4, true>(a, st);
+      case 12: if (a.M % 64) break; return launch_wgrad<64, 64, 32, 32, 4, true>(a, st);
+      default: break;
+    }
+  }
+  return (int)hipErrorInvalidValue;
+}
+
+// Sum the split slabs and accumulate into the PyTorch-layout fp32 gradient:
+//   mode 0 (Conv2d OIHW):          gw[m][n][tap]          (m = out ch, n = in ch < Nreal)
+//   mode 1 (ConvTranspose2d IOHW): gw[n][m][tap]          (n = in ch, m = out ch)
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ slab, const float* __restrict__ bslab,
+                                                           float* __restrict__ gw, float* __restrict__ gb, int splits, int T,
+                                                           int M, int Nc, int Nreal, int mode) {
+  const long tot = (long)T * M * Nc;
+  const long stride = (long)gridDim.x * blockDim.x;
+  for (long idx = (long)blockIdx.x * blockDim.x + threadIdx.x; idx < tot; idx += stride) {
+    const int n = (int)(idx % Nc);
+    const int m = (int)((idx / Nc) % M);
+    const int t = (int)(idx / ((long)Nc * M));
+    if (n >= Nreal) continue;
+    float s = 0.f;
+    for (int k = 0; k < splits; ++k) s += slab[(long)k * tot + idx];
+    const long dst = mode == 0 ? ((long)m * Nreal + n) * T + t : ((long)n * M + m) * T + t;
+    gw[dst] += s;
+  }
+  if (bslab && gb) {
+    for (long m = (long)blockIdx.x * blockDim.x + threadIdx.x; m < M; m += stride) {
+      float s = 0.f;
+      for (int k = 0; k < splits; ++k) s += bslab[(long)k * M + m];
+      gb[m] += s;
+    }
+  }
+}
+
+DPA_API int dpa_wgrad_reduce(const float* slab, const float* bslab, float* gw, float* gb, int splits, int T, int M, int Nc,
+                             int Nreal, int mode, hipStream_t st) {
+  const long tot = (long)T * M * Nc;
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(dpa_grid(tot, 256, 4096)), dim3(256), 0, st, slab, bslab, gw, gb, splits, T,
+                     M, Nc, Nreal, mode);
+  return (int)hipGetLastError();
+}

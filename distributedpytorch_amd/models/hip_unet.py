@@ -1,0 +1,343 @@
+"""MI355X block backend: the UNet blocks on hand-written gfx950 kernels (NHWC bf16, fp32 accumulate).
+
+Implements the block API of :mod:`.blocks` (``prep / enc / mid / dec / head_partials / head_probs``)
+so every strategy (single device, DDP, DP, GPipe stages) runs the same kernels.  Each block is one
+``torch.autograd.Function`` whose backward is an explicit, fused schedule:
+
+* forward  conv3x3+bias+ReLU (``igemm``), the encoder's second conv writes straight into the first
+  half of the decoder's concat buffer and the transposed conv into its second half, so the
+  reference's ``torch.cat((skip, up), 1)`` (model/unet_parts.py:59-74) costs nothing;
+* backward dgrad convs carry the ReLU-backward mask of their *input* in the epilogue, max-pool
+  backward + skip-gradient add + mask is one kernel, weight gradients are split-K MFMA kernels that
+  accumulate straight into the flat fp32 gradient buffer (:class:`..optim.FlatParameterSpace`) in
+  PyTorch layout, and each block announces the parameters whose gradients are final
+  (``space.notify_ready``) so the data-parallel all-reduce of that bucket starts while the rest of
+  the backward runs.
+
+Gradient convention between blocks: the gradient a block's backward *receives* for its (ReLU)
+output is already multiplied by the ReLU mask (the consumer applies it in its own fused epilogue);
+for the encoder skip, whose two consumers (pool, decoder concat) add up, the mask is applied once in
+the fused pool-backward kernel.  Parameters stay fp32 (master weights); a single batched kernel
+repacks them to bf16 GEMM layouts whenever they changed (``space.version``).
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Dict, List
+
+import torch
+
+from ..ops import kernels as K
+from ..optim import FlatParameterSpace
+from .unet import UNet
+
+
+class _Conv:
+    """Packing bookkeeping for one Conv2d(3x3, pad 1) layer."""
+
+    def __init__(self, mod: torch.nn.Conv2d, cin_pad: int, need_dgrad: bool):
+        self.mod = mod
+        self.Cout, self.Cin = mod.out_channels, mod.in_channels
+        self.Cs = cin_pad
+        self.Kf = K.round_up(9 * self.Cs, 32)        # fwd: K = 9*Cs
+        self.Kd = K.round_up(9 * self.Cout, 32)      # dgrad: K = 9*Cout
+        self.need_dgrad = need_dgrad
+        self.off_f = self.off_d = 0
+
+
+class _Deconv:
+    def __init__(self, mod: torch.nn.ConvTranspose2d):
+        self.mod = mod
+        self.Cin, self.Cout = mod.in_channels, mod.out_channels
+        self.Kf = K.round_up(self.Cin, 32)
+        self.Kd = K.round_up(4 * self.Cout, 32)
+        self.off_f = self.off_d = 0
+
+
+class HipBlocks:
+    name = "hip"
+
+    def __init__(self, model: UNet, dtype: str = "bf16", space: FlatParameterSpace = None):
+        cfg = model.cfg
+        if cfg.batchnorm or cfg.bilinear:
+            raise NotImplementedError("hip backend: BatchNorm / bilinear UNet variants run on --backend torch")
+        if dtype != "bf16":
+            raise NotImplementedError("hip backend computes in bf16 (fp32 accumulate); use --backend torch for fp32")
+        self.model = model
+        self.cfg = cfg
+        self.depth = cfg.depth
+        self.device = next(model.parameters()).device
+        assert self.device.type == "cuda", "HipBlocks needs a GPU"
+        self.space = space if space is not None else getattr(model, "_flat_space", None)
+        if self.space is None:
+            self.space = FlatParameterSpace(model, device=self.device)
+        self.anchor = torch.zeros(1, device=self.device, requires_grad=True)
+        self.enc_convs = [[_Conv(c, K.round_up(c.in_channels, 8) if (l == 0 and j == 0) else c.in_channels,
+                                 need_dgrad=not (l == 0 and j == 0))
+                           for j, c in enumerate(b.convs())] for l, b in enumerate(model.encoder.blocks())]
+        self.mid_convs = [_Conv(c, c.in_channels, True) for c in model.mid.convs()]
+        self.dec_convs = [[_Conv(c, c.in_channels, True) for c in b.convs()] for b in model.decoder.blocks()]
+        self.deconvs = [_Deconv(m) for m in model.decoder.ups()]
+        for convs in self.enc_convs + [self.mid_convs] + self.dec_convs:
+            for c in convs:
+                assert c.Cout % 32 == 0 and c.Cs % 8 == 0, "hip backend needs channel widths divisible by 32"
+        self._build_packing()
+        self._packed_version = None
+        self._cats: Dict[int, torch.Tensor] = {}
+
+    # ------------------------------------------------------------------ weight packing
+    def _src(self, p: torch.Tensor) -> int:
+        base = self.space.data.data_ptr()
+        off = (p.data_ptr() - base) // 4
+        assert 0 <= off < self.space.numel and p.is_contiguous()
+        return off
+
+    def _build_packing(self):
+        descs: List[K.PackDesc] = []
+        off = 0
+        max_elems = 0
+
+        def add(mode, src, cout, cin, cs, ngemm, kpad):
+            nonlocal off, max_elems
+            descs.append(K.PackDesc(src, off, mode, cout, cin, cs, ngemm, kpad))
+            start = off
+            off = K.round_up(off + ngemm * kpad, 64)
+            max_elems = max(max_elems, ngemm * kpad)
+            return start
+
+        for c in [c for cs in self.enc_convs for c in cs] + self.mid_convs + [c for cs in self.dec_convs for c in cs]:
+            src = self._src(c.mod.weight)
+            c.off_f = add(0, src, c.Cout, c.Cin, c.Cs, c.Cout, c.Kf)
+            if c.need_dgrad:
+                c.off_d = add(1, src, c.Cout, c.Cin, c.Cout, c.Cin, c.Kd)
+        for d in self.deconvs:
+            src = self._src(d.mod.weight)
+            d.off_f = add(2, src, d.Cout, d.Cin, d.Cin, 4 * d.Cout, d.Kf)
+            d.off_d = add(3, src, d.Cout, d.Cin, d.Cout, d.Cin, d.Kd)
+        self.packed = torch.zeros(off, dtype=torch.bfloat16, device=self.device)
+        raw = (K.PackDesc * len(descs))(*descs)
+        host = torch.frombuffer(bytearray(bytes(raw)), dtype=torch.uint8)
+        self.descs_dev = host.to(self.device)
+        self.ndesc = len(descs)
+        self.max_elems = max_elems
+
+    def ensure_packed(self):
+        v = self.space.version
+        if self._packed_version != v:
+            K.pack_weights(self.space.data, self.packed, self.descs_dev, self.ndesc, self.max_elems)
+            self._packed_version = v
+
+    def wf(self, c):
+        return self.packed[c.off_f:c.off_f + (c.Cout if isinstance(c, _Conv) else 4 * c.Cout) * c.Kf]
+
+    def wd(self, c):
+        return self.packed[c.off_d:c.off_d + c.Cin * c.Kd]
+
+    # ------------------------------------------------------------------ primitive launches
+    def conv_fwd(self, c: _Conv, x: torch.Tensor, y: torch.Tensor = None):
+        N, H, W = x.shape[:3]
+        if y is None:
+            y = torch.empty(N, H, W, c.Cout, dtype=torch.bfloat16, device=x.device)
+        K.igemm(x, self.wf(c), y, Ngemm=c.Cout, Kpad=c.Kf, KH=3, KW=3, stride=1, pad=1, Cs=c.Cs, out_grid=(N, H, W),
+                bias=c.mod.bias, relu=True)
+        return y
+
+    def conv_dgrad(self, c: _Conv, g: torch.Tensor, mask: torch.Tensor = None, out: torch.Tensor = None):
+        N, H, W = g.shape[:3]
+        if out is None:
+            out = torch.empty(N, H, W, c.Cin, dtype=torch.bfloat16, device=g.device)
+        K.igemm(g, self.wd(c), out, Ngemm=c.Cin, Kpad=c.Kd, KH=3, KW=3, stride=1, pad=1, Cs=c.Cout,
+                out_grid=(N, H, W), mask=mask)
+        return out
+
+    def conv_wgrad(self, c: _Conv, g: torch.Tensor, x: torch.Tensor):
+        N, H, W = g.shape[:3]
+        gw, gb = _grad(c.mod.weight), _grad(c.mod.bias)
+        K.wgrad(g, x, kind=0, grid=(N, H, W), M=c.Cout, Nc=c.Cs, s=1, pad=1, KW=3, gw=gw.view(-1), gb=gb,
+                Nreal=c.Cin)
+
+    def deconv_fwd(self, d: _Deconv, x: torch.Tensor, out: torch.Tensor):
+        N, h, w = x.shape[:3]
+        K.igemm(x, self.wf(d), out, Ngemm=4 * d.Cout, Kpad=d.Kf, KH=1, KW=1, stride=1, pad=0, Cs=d.Cin,
+                out_grid=(N, h, w), bias=d.mod.bias, mode=1, Cout=d.Cout)
+
+    def deconv_dgrad(self, d: _Deconv, gup: torch.Tensor, x: torch.Tensor):
+        N, h, w = x.shape[:3]
+        dx = torch.empty(N, h, w, d.Cin, dtype=torch.bfloat16, device=x.device)
+        K.igemm(gup, self.wd(d), dx, Ngemm=d.Cin, Kpad=d.Kd, KH=2, KW=2, stride=2, pad=0, Cs=d.Cout,
+                out_grid=(N, h, w), mask=x)
+        return dx
+
+    def deconv_wgrad(self, d: _Deconv, gup: torch.Tensor, x: torch.Tensor):
+        N, h, w = x.shape[:3]
+        K.wgrad(gup, x, kind=1, grid=(N, h, w), M=d.Cout, Nc=d.Cin, s=2, pad=0, KW=2, gw=_grad(d.mod.weight).view(-1),
+                gb=_grad(d.mod.bias), Nreal=d.Cin)
+
+    def ready(self, mods):
+        self.space.notify_ready([p for m in mods for p in (m.weight, m.bias)])
+
+    # ------------------------------------------------------------------ block API
+    def prep(self, x: torch.Tensor) -> torch.Tensor:
+        if x.dtype == torch.bfloat16 and x.dim() == 4 and x.shape[-1] == 8:
+            return x   # already NHWC8 (pipeline stages re-entering)
+        return K.input_nhwc8(x.float())
+
+    def enc(self, l: int, x):
+        self.ensure_packed()
+        return _EncFn.apply(self.anchor, x, self, l)
+
+    def mid(self, x):
+        self.ensure_packed()
+        return _MidFn.apply(self.anchor, x, self)
+
+    def dec(self, i: int, x, skip):
+        self.ensure_packed()
+        return _DecFn.apply(self.anchor, x, skip, self, i)
+
+    def head_partials(self, x, t):
+        t = t.float().contiguous()
+        return _HeadFn.apply(self.anchor, x, t, self)
+
+    @torch.no_grad()
+    def head_probs(self, x):
+        seg = self.model.segmap
+        _, probs = K.head_fwd(x, seg.weight, seg.bias, None, want_probs=True)
+        return probs.unsqueeze(1)
+
+    # concat buffers: the encoder allocates [N,H,W,2C] and returns its first half as the skip
+    def new_cat(self, N, H, W, C):
+        cat = torch.empty(N, H, W, 2 * C, dtype=torch.bfloat16, device=self.device)
+        self._cats[cat.data_ptr()] = cat
+        return cat
+
+    def cat_for(self, skip: torch.Tensor) -> torch.Tensor:
+        N, H, W, C = skip.shape
+        cat = self._cats.pop(skip.data_ptr(), None)
+        if cat is not None and tuple(cat.shape) == (N, H, W, 2 * C) and skip.stride(2) == 2 * C:
+            return cat
+        cat = torch.empty(N, H, W, 2 * C, dtype=torch.bfloat16, device=self.device)
+        cat[..., :C].copy_(skip)
+        return cat
+
+
+def _grad(p: torch.nn.Parameter) -> torch.Tensor:
+    if p.grad is None:
+        p.grad = torch.zeros_like(p)
+    g = p.grad
+    assert g.dtype == torch.float32 and g.is_contiguous()
+    return g
+
+
+class _EncFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, anchor, x, B: HipBlocks, l: int):
+        c1, c2 = B.enc_convs[l]
+        N, H, W = x.shape[:3]
+        a = B.conv_fwd(c1, x)
+        cat = B.new_cat(N, H, W, c2.Cout)
+        skip = cat[..., :c2.Cout]
+        B.conv_fwd(c2, a, skip)
+        pooled = torch.empty(N, H // 2, W // 2, c2.Cout, dtype=torch.bfloat16, device=x.device)
+        K.maxpool2(skip, pooled)
+        ctx.B, ctx.l = B, l
+        ctx.x_needs_grad = l > 0
+        ctx.save_for_backward(x, a, cat)
+        return skip, pooled
+
+    @staticmethod
+    def backward(ctx, dskip, dpooled):
+        B, l = ctx.B, ctx.l
+        x, a, cat = ctx.saved_tensors
+        c1, c2 = B.enc_convs[l]
+        C = c2.Cout
+        skip = cat[..., :C]
+        if dpooled is None:
+            dpooled = torch.zeros(x.shape[0], x.shape[1] // 2, x.shape[2] // 2, C, dtype=torch.bfloat16, device=x.device)
+        g2 = torch.empty_like(a)
+        K.pool_bwd(skip, dskip, dpooled, g2)
+        g1 = B.conv_dgrad(c2, g2, mask=a)
+        B.conv_wgrad(c2, g2, a)
+        B.ready([c2.mod])
+        gx = B.conv_dgrad(c1, g1) if ctx.x_needs_grad else None
+        B.conv_wgrad(c1, g1, x)
+        B.ready([c1.mod])
+        return None, gx, None, None
+
+
+class _MidFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, anchor, x, B: HipBlocks):
+        c1, c2 = B.mid_convs
+        a = B.conv_fwd(c1, x)
+        y = B.conv_fwd(c2, a)
+        ctx.B = B
+        ctx.save_for_backward(x, a)
+        return y
+
+    @staticmethod
+    def backward(ctx, g2):
+        B = ctx.B
+        x, a = ctx.saved_tensors
+        c1, c2 = B.mid_convs
+        g2 = g2.contiguous()
+        g1 = B.conv_dgrad(c2, g2, mask=a)
+        B.conv_wgrad(c2, g2, a)
+        B.ready([c2.mod])
+        gx = B.conv_dgrad(c1, g1)
+        B.conv_wgrad(c1, g1, x)
+        B.ready([c1.mod])
+        return None, gx, None
+
+
+class _DecFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, anchor, x, skip, B: HipBlocks, i: int):
+        d = B.deconvs[i]
+        c1, c2 = B.dec_convs[i]
+        C = d.Cout
+        cat = B.cat_for(skip)
+        B.deconv_fwd(d, x, cat[..., C:])
+        a = B.conv_fwd(c1, cat)
+        y = B.conv_fwd(c2, a)
+        ctx.B, ctx.i = B, i
+        ctx.save_for_backward(x, cat, a)
+        return y
+
+    @staticmethod
+    def backward(ctx, g2):
+        B, i = ctx.B, ctx.i
+        x, cat, a = ctx.saved_tensors
+        d = B.deconvs[i]
+        c1, c2 = B.dec_convs[i]
+        C = d.Cout
+        g2 = g2.contiguous()
+        g1 = B.conv_dgrad(c2, g2, mask=a)
+        B.conv_wgrad(c2, g2, a)
+        B.ready([c2.mod])
+        dcat = B.conv_dgrad(c1, g1)
+        B.conv_wgrad(c1, g1, cat)
+        B.ready([c1.mod])
+        gup = dcat[..., C:]
+        dx = B.deconv_dgrad(d, gup, x)
+        B.deconv_wgrad(d, gup, x)
+        B.ready([d.mod])
+        return None, dx, dcat[..., :C], None, None
+
+
+class _HeadFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, anchor, y, t, B: HipBlocks):
+        seg = B.model.segmap
+        S, _ = K.head_fwd(y, seg.weight, seg.bias, t)
+        ctx.B = B
+        ctx.save_for_backward(y, t)
+        return S.clone()
+
+    @staticmethod
+    def backward(ctx, dS):
+        B = ctx.B
+        y, t = ctx.saved_tensors
+        seg = B.model.segmap
+        gy = K.head_bwd(y, seg.weight, seg.bias, t, dS, _grad(seg.weight).view(-1), _grad(seg.bias))
+        B.ready([seg])
+        return None, gy, None, None

@@ -49,17 +49,17 @@ def lib():
 
 
 def _declare(L):
-    c_void_p, c_int, c_float, c_long = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_int64
-    sigs = getattr(L, "dpa_signatures", None)
-    # every launcher returns int (hipError_t); argtypes are declared in ops modules lazily
-    L.dpa_version.restype = c_int
-    del sigs, c_void_p, c_int, c_float, c_long
+    for name in ("dpa_version", "dpa_igemm", "dpa_wgrad", "dpa_wgrad_reduce", "dpa_input_nhwc8", "dpa_maxpool2",
+                 "dpa_pool_bwd", "dpa_pack_weights", "dpa_head_fwd", "dpa_head_bwd", "dpa_adam_flat"):
+        getattr(L, name).restype = ctypes.c_int
+    L.dpa_head_slab_blocks.restype = ctypes.c_int
+    L.dpa_head_slab_blocks.argtypes = [ctypes.c_longlong]
+    L.dpa_error_string.restype = ctypes.c_char_p
 
 
 def check(err: int, name: str):
     if err != 0:
         L = lib()
-        L.dpa_error_string.restype = ctypes.c_char_p
         msg = L.dpa_error_string(err).decode()
         raise RuntimeError(f"{name} failed: hip error {err} ({msg})")
 

@@ -1,0 +1,208 @@
+"""ctypes bindings of the gfx950 kernels in ``csrc/*.hip`` (``_C/libdpa_hip.so``).
+
+Every wrapper takes torch tensors (NHWC bf16 activations, fp32 parameters/gradients), checks the
+shape/stride/alignment assumptions its kernel makes on the host *before* launching (a bad launch
+can fault the GPU), and launches on the current HIP stream of the tensor's device.  There is no
+fallback: on a GPU the library must be present (``_lib.lib()`` raises otherwise).
+
+Kernel map:  conv3x3 fwd / dgrad, convT fwd / dgrad -> ``igemm``;  conv / convT
+weight gradients -> ``wgrad`` + ``wgrad_reduce``;  max-pool (K5) -> ``maxpool2`` / ``pool_bwd``;
+segmap + sigmoid + BCE + Dice (K8-K11) -> ``head_fwd`` / ``head_bwd``;  Adam (K13) -> ``adam_step``.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional
+
+import torch
+
+from . import _lib
+
+c_int, c_ll, c_void_p = ctypes.c_int, ctypes.c_longlong, ctypes.c_void_p
+
+
+class IgemmArgs(ctypes.Structure):
+    _fields_ = [("x", c_void_p), ("w", c_void_p), ("bias", c_void_p), ("y", c_void_p), ("mask", c_void_p)] + \
+               [(n, c_int) for n in ("ldx", "ldy", "ldm", "mask_ch", "N", "Ho", "Wo", "Hs", "Ws", "Cs", "KH", "KW",
+                                     "stride", "pad", "Ngemm", "Kpad", "mode", "relu", "accumulate", "Cout")]
+
+
+class WgradArgs(ctypes.Structure):
+    _fields_ = [("A", c_void_p), ("B", c_void_p), ("slab", c_void_p), ("bslab", c_void_p)] + \
+               [(n, c_int) for n in ("lda", "ldb", "N", "Hg", "Wg", "HA", "WA", "HB", "WB", "M", "Nc", "s", "pad",
+                                     "KW", "pix_per_split", "splits")]
+
+
+class PackDesc(ctypes.Structure):
+    _fields_ = [("src", c_ll), ("dst", c_ll), ("mode", c_int), ("Cout", c_int), ("Cin", c_int), ("Cs", c_int),
+                ("Ngemm", c_int), ("Kpad", c_int)]
+
+
+def _p(t: Optional[torch.Tensor]):
+    return None if t is None else c_void_p(t.data_ptr())
+
+
+def _stream(t: torch.Tensor):
+    return c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def _check(err, name):
+    _lib.check(int(err), name)
+
+
+def _nhwc(t: torch.Tensor, name: str):
+    """(N, H, W, C, ld) of an NHWC bf16 tensor whose channel slice may be strided (concat halves)."""
+    assert t.dtype == torch.bfloat16 and t.dim() == 4 and t.is_cuda, f"{name}: need cuda bf16 NHWC, got {t.dtype} {tuple(t.shape)}"
+    N, H, W, C = t.shape
+    sN, sH, sW, sC = t.stride()
+    ld = sW
+    assert sC == 1 and sH == W * ld and (N == 1 or sN == H * W * ld), f"{name}: unsupported strides {t.stride()}"
+    assert ld % 8 == 0 and t.data_ptr() % 16 == 0, f"{name}: ld {ld} / pointer not 16-byte aligned"
+    return N, H, W, C, ld
+
+
+def round_up(x: int, m: int) -> int:
+    return (x + m - 1) // m * m
+
+
+# ------------------------------------------------------------------------------------------ igemm
+def igemm(x: torch.Tensor, wpacked: torch.Tensor, y: torch.Tensor, *, Ngemm: int, Kpad: int, KH: int, KW: int,
+          stride: int, pad: int, Cs: int, out_grid, bias: Optional[torch.Tensor] = None, relu: bool = False,
+          mask: Optional[torch.Tensor] = None, mode: int = 0, Cout: int = 0, accumulate: bool = False, cfg: int = 0):
+    """Implicit-GEMM conv (see csrc/igemm.hip).  ``out_grid`` = (N, Ho, Wo) pixel grid of GEMM-M."""
+    N, Hs, Ws, Cx, ldx = _nhwc(x, "igemm.x")
+    _, _, _, Cy, ldy = _nhwc(y, "igemm.y")
+    No, Ho, Wo = out_grid
+    assert No == N and Cs <= Cx and Cs % 8 == 0 and Kpad % 32 == 0 and Ngemm % 32 == 0
+    assert wpacked.dtype == torch.bfloat16 and wpacked.numel() >= Ngemm * Kpad
+    assert Kpad >= KH * KW * Cs
+    if mode == 0:
+        assert tuple(y.shape[:3]) == (N, Ho, Wo) and Cy >= Ngemm, (tuple(y.shape), out_grid, Ngemm)
+    else:
+        assert tuple(y.shape[:3]) == (N, 2 * Ho, 2 * Wo) and Cy >= Cout and Ngemm == 4 * Cout
+    # gathered source extent must stay inside x
+    assert (Ho - 1) * stride + KH - 1 - pad <= Hs - 1 + pad and (Wo - 1) * stride + KW - 1 - pad <= Ws - 1 + pad
+    ldm = mch = 0
+    if mask is not None:
+        Nm, Hm, Wm, Cm, ldm = _nhwc(mask, "igemm.mask")
+        assert (Nm, Hm, Wm) == (N, Ho, Wo) and mode == 0
+        mch = min(Cm, Ngemm)
+    if bias is not None:
+        assert bias.dtype == torch.float32 and bias.is_contiguous() and bias.numel() >= (Cout or Ngemm)
+    a = IgemmArgs(_p(x).value, _p(wpacked).value, None if bias is None else bias.data_ptr(), y.data_ptr(),
+                  None if mask is None else mask.data_ptr(), ldx, ldy, ldm, mch, N, Ho, Wo, Hs, Ws, Cs, KH, KW,
+                  stride, pad, Ngemm, Kpad, mode, int(relu), int(accumulate), Cout)
+    _check(_lib.lib().dpa_igemm(ctypes.byref(a), c_int(cfg), _stream(y)), "igemm")
+
+
+# ------------------------------------------------------------------------------------------ wgrad
+def wgrad_splits(P: int, tiles: int, target_blocks: int = 1024, min_pix: int = 512):
+    splits = max(1, min(target_blocks // max(tiles, 1), P // min_pix))
+    pps = round_up(-(-P // splits), 32)
+    splits = -(-P // pps)
+    return splits, pps
+
+
+def wgrad(A: torch.Tensor, B: torch.Tensor, *, kind: int, grid, M: int, Nc: int, s: int, pad: int, KW: int,
+          gw: torch.Tensor, gb: Optional[torch.Tensor], Nreal: int, cfg: int = 0, target_blocks: int = 1024):
+    """Weight (+bias) gradient of a conv3x3 (kind 0) or transposed conv 2x2/s2 (kind 1); accumulates into gw/gb."""
+    NA, HA, WA, CA, lda = _nhwc(A, "wgrad.A")
+    NB, HB, WB, CB, ldb = _nhwc(B, "wgrad.B")
+    N, Hg, Wg = grid
+    assert NA == NB == N and CA >= M and CB >= Nc and M % 32 == 0
+    T = 9 if kind == 0 else 4
+    if kind == 0:
+        assert (HA, WA) == (Hg, Wg) and (HB, WB) == (Hg, Wg)
+    else:
+        assert (HA, WA) == (2 * Hg, 2 * Wg) and (HB, WB) == (Hg, Wg)
+    if cfg == 0:
+        if kind == 0:
+            cfg = 1 if Nc <= 16 else (3 if M % 64 == 0 else 2)
+        else:
+            cfg = 12 if (M % 64 == 0 and Nc >= 64) else 11
+    bm, bn = {1: (32, 16), 2: (32, 32), 3: (64, 32), 4: (64, 64), 11: (32, 32), 12: (64, 64)}[cfg]
+    tiles = (M // bm) * (-(-Nc // bn))
+    P = N * Hg * Wg
+    splits, pps = wgrad_splits(P, tiles, target_blocks)
+    slab = torch.empty(splits * T * M * Nc + splits * M, dtype=torch.float32, device=A.device)
+    bslab = slab[splits * T * M * Nc:] if gb is not None else None
+    assert gw.dtype == torch.float32 and gw.is_contiguous() and gw.numel() == M * Nreal * T
+    a = WgradArgs(A.data_ptr(), B.data_ptr(), slab.data_ptr(), None if bslab is None else bslab.data_ptr(),
+                  lda, ldb, N, Hg, Wg, HA, WA, HB, WB, M, Nc, s, pad, KW, pps, splits)
+    L = _lib.lib()
+    st = _stream(A)
+    _check(L.dpa_wgrad(ctypes.byref(a), c_int(kind), c_int(cfg), st), "wgrad")
+    _check(L.dpa_wgrad_reduce(_p(slab), _p(bslab), _p(gw), _p(gb), c_int(splits), c_int(T), c_int(M), c_int(Nc),
+                              c_int(Nreal), c_int(kind), st), "wgrad_reduce")
+
+
+# ------------------------------------------------------------------------------------------ aux
+def input_nhwc8(x: torch.Tensor) -> torch.Tensor:
+    assert x.dtype == torch.float32 and x.dim() == 4 and x.shape[1] <= 8
+    x = x.contiguous()
+    B, C, H, W = x.shape
+    y = torch.empty(B, H, W, 8, dtype=torch.bfloat16, device=x.device)
+    _check(_lib.lib().dpa_input_nhwc8(_p(x), _p(y), c_int(B), c_int(C), c_int(H), c_int(W), _stream(x)), "input_nhwc8")
+    return y
+
+
+def maxpool2(x: torch.Tensor, y: torch.Tensor):
+    N, H, W, C, ldx = _nhwc(x, "maxpool.x")
+    _, Ho, Wo, Cy, ldy = _nhwc(y, "maxpool.y")
+    assert (Ho, Wo) == (H // 2, W // 2) and Cy == C and C % 8 == 0
+    _check(_lib.lib().dpa_maxpool2(_p(x), c_int(ldx), _p(y), c_int(ldy), c_int(N), c_int(H), c_int(W), c_int(C),
+                                   _stream(x)), "maxpool2")
+
+
+def pool_bwd(skip: torch.Tensor, dskip: Optional[torch.Tensor], dpool: torch.Tensor, g: torch.Tensor):
+    N, H, W, C, lds = _nhwc(skip, "pool_bwd.skip")
+    ldd = 8
+    if dskip is not None:
+        Nd, Hd, Wd, Cd, ldd = _nhwc(dskip, "pool_bwd.dskip")
+        assert (Nd, Hd, Wd, Cd) == (N, H, W, C)
+    Np, Hp, Wp, Cp, ldp = _nhwc(dpool, "pool_bwd.dpool")
+    assert (Np, Hp, Wp, Cp) == (N, H // 2, W // 2, C)
+    _, Hg, Wg, Cg, ldg = _nhwc(g, "pool_bwd.g")
+    assert (Hg, Wg, Cg) == (H, W, C)
+    _check(_lib.lib().dpa_pool_bwd(_p(skip), c_int(lds), _p(dskip), c_int(ldd), _p(dpool), c_int(ldp), _p(g), c_int(ldg),
+                                   c_int(N), c_int(H), c_int(W), c_int(C), _stream(skip)), "pool_bwd")
+
+
+def pack_weights(flat: torch.Tensor, packed: torch.Tensor, descs_dev: torch.Tensor, ndesc: int, max_elems: int):
+    assert flat.dtype == torch.float32 and packed.dtype == torch.bfloat16
+    _check(_lib.lib().dpa_pack_weights(_p(flat), _p(packed), _p(descs_dev), c_int(ndesc), c_ll(max_elems),
+                                       _stream(flat)), "pack_weights")
+
+
+def head_fwd(y: torch.Tensor, w: torch.Tensor, b: torch.Tensor, t: Optional[torch.Tensor], want_probs: bool = False):
+    """-> (S[4] fp32 or None, probs[N,H,W] fp32 or None)."""
+    N, H, W, C, ldy = _nhwc(y, "head.y")
+    P = N * H * W
+    L = _lib.lib()
+    nblk = L.dpa_head_slab_blocks(c_ll(P))
+    S = slab = None
+    if t is not None:
+        assert t.dtype == torch.float32 and t.is_contiguous() and t.numel() == P
+        slab = torch.empty(nblk * 4 + 4, dtype=torch.float32, device=y.device)
+        S = slab[nblk * 4:]
+    probs = torch.empty(N, H, W, dtype=torch.float32, device=y.device) if want_probs else None
+    wf = w.reshape(-1).contiguous()
+    _check(L.dpa_head_fwd(_p(y), c_int(ldy), c_int(C), _p(wf), _p(b), _p(t), _p(slab), _p(S), _p(probs), c_ll(P),
+                          _stream(y)), "head_fwd")
+    return S, probs
+
+
+def head_bwd(y: torch.Tensor, w: torch.Tensor, b: torch.Tensor, t: torch.Tensor, dS: torch.Tensor,
+             gw: torch.Tensor, gb: torch.Tensor) -> torch.Tensor:
+    N, H, W, C, ldy = _nhwc(y, "head_bwd.y")
+    P = N * H * W
+    L = _lib.lib()
+    nblk = L.dpa_head_slab_blocks(c_ll(P))
+    gy = torch.empty(N, H, W, C, dtype=torch.bfloat16, device=y.device)
+    slab = torch.empty(nblk * (C + 1) + C + 1, dtype=torch.float32, device=y.device)
+    tmp = slab[nblk * (C + 1):]
+    dS = dS.float().contiguous()
+    assert gw.is_contiguous() and gw.numel() == C and gb.numel() == 1
+    _check(L.dpa_head_bwd(_p(y), c_int(ldy), c_int(C), _p(w.reshape(-1).contiguous()), _p(b), _p(t), _p(dS), _p(gy),
+                          c_int(C), _p(slab), _p(tmp), _p(gw), _p(gb), c_ll(P), _stream(y)), "head_bwd")
+    return gy

@@ -48,16 +48,34 @@ class FlatParameterSpace:
             self.data[o:o + n].copy_(p.detach().reshape(-1))
             p.data = self.data[o:o + n].view_as(p)
             p.grad = self.grad[o:o + n].view_as(p)
+        self._index = {id(p): i for i, p in enumerate(self.params)}
+        self.version = 0                 # bumped whenever parameter values change (optimizer, sync, load)
+        self._ready_listeners = []       # called with param indices whose gradient is final
+        if isinstance(module, nn.Module):
+            module._flat_space = self
+
+    def touch(self):
+        """Record that parameter values changed (kernels that cache packed weights re-pack)."""
+        self.version += 1
+
+    def add_ready_listener(self, fn):
+        self._ready_listeners.append(fn)
+
+    def notify_ready(self, params):
+        """Explicit-backward engines announce finished gradients (replaces autograd hooks)."""
+        if not self._ready_listeners:
+            return
+        idx = [self._index[id(p)] for p in params if id(p) in self._index]
+        for fn in self._ready_listeners:
+            for i in idx:
+                fn(i)
 
     @property
     def numel(self) -> int:
         return self.offsets[-1]
 
     def index_of(self, p: torch.Tensor) -> int:
-        for i, q in enumerate(self.params):
-            if q is p:
-                return i
-        raise KeyError("parameter not in flat space")
+        return self._index[id(p)]
 
     def slice_of(self, i: int):
         return self.offsets[i], self.offsets[i + 1]
@@ -74,6 +92,7 @@ class FlatParameterSpace:
             if p.data.data_ptr() != self.data[o:o + n].data_ptr():
                 self.data[o:o + n].copy_(p.data.reshape(-1))
                 p.data = self.data[o:o + n].view_as(p)
+        self.touch()
 
 
 def spaces_by_device(module: nn.Module) -> List[FlatParameterSpace]:
@@ -123,6 +142,7 @@ class FusedAdam(torch.optim.Optimizer):
         bc1 = 1 - b1 ** self.step_count
         bc2 = 1 - b2 ** self.step_count
         for s, m, v in zip(self.spaces, self.exp_avg, self.exp_avg_sq):
+            s.touch()
             use_k = s.data.is_cuda if self.use_kernel is None else self.use_kernel
             if use_k:
                 from . import ops

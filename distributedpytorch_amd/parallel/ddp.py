@@ -56,10 +56,13 @@ class BucketedAllReduce:
 
     # ---------------- hooks ----------------
     def register_hooks(self):
+        """Autograd post-accumulate hooks (torch-op backend) + the flat space's explicit readiness
+        notifications (HIP engine, whose backward writes gradients in place without autograd)."""
         idx = {id(p): i for i, p in enumerate(self.space.params)}
         for p in self.space.params:
             i = idx[id(p)]
             self._hooks.append(p.register_post_accumulate_grad_hook(lambda _p, i=i: self.mark_ready(i)))
+        self.space.add_ready_listener(self.mark_ready)
         return self
 
     def remove_hooks(self):
@@ -109,6 +112,7 @@ class BucketedAllReduce:
 
 def broadcast_parameters(space: FlatParameterSpace, src: int = 0, group=None):
     dist.broadcast(space.data, src=src, group=group)
+    space.touch()
 
 
 def sync_buffers(module: torch.nn.Module, src: int = 0, group=None):

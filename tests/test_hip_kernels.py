@@ -1,0 +1,244 @@
+"""Numerics of every gfx950 kernel against a plain PyTorch fp32 CPU reference of the same op.
+
+Inputs are rounded to bf16 first (the kernels' storage type), so the only differences left are the
+fp32-accumulation order and the final bf16 rounding of the outputs -> tolerances ~1e-2 relative to
+the output's max magnitude.  Shapes cover the first layer (3 -> padded 8 channels), odd spatial
+sizes (partial tiles, zero padding), concat-buffer strides and every tile family.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(a, b):
+    a, b = a.double().cpu(), b.double().cpu()
+    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-12)).item()
+
+
+def _bf(t):
+    return t.to(torch.bfloat16).float()
+
+
+def _nhwc(x):   # NCHW fp32 -> NHWC bf16 cuda
+    return x.permute(0, 2, 3, 1).contiguous().to("cuda", torch.bfloat16)
+
+
+def _nchw(y):   # NHWC cuda -> NCHW fp32 cpu
+    return y.float().permute(0, 3, 1, 2).cpu()
+
+
+def _pack_one(mode, w, cin_pad=None):
+    """Pack a single fp32 weight with the production pack kernel."""
+    from distributedpytorch_amd.ops import kernels as K
+    flat = w.reshape(-1).float().cuda().contiguous()
+    if mode in (0, 1):
+        Cout, Cin = w.shape[:2]
+        Cs = cin_pad or Cin
+        if mode == 0:
+            ngemm, kpad, cs = Cout, K.round_up(9 * Cs, 32), Cs
+        else:
+            ngemm, kpad, cs = Cin, K.round_up(9 * Cout, 32), Cout
+    else:
+        Cin, Cout = w.shape[:2]
+        if mode == 2:
+            ngemm, kpad, cs = 4 * Cout, K.round_up(Cin, 32), Cin
+        else:
+            ngemm, kpad, cs = Cin, K.round_up(4 * Cout, 32), Cout
+    d = K.PackDesc(0, 0, mode, Cout, Cin, cs, ngemm, kpad)
+    descs = torch.frombuffer(bytearray(bytes(d)), dtype=torch.uint8).cuda()
+    packed = torch.empty(ngemm * kpad, dtype=torch.bfloat16, device="cuda")
+    K.pack_weights(flat, packed, descs, 1, ngemm * kpad)
+    return packed, ngemm, kpad
+
+
+@pytest.mark.parametrize("N,H,W,Cin,Cout,cfg", [
+    (2, 17, 23, 3, 32, 0),      # first layer: 3 -> padded 8 input channels, partial tiles
+    (2, 16, 16, 32, 64, 0),
+    (1, 12, 20, 64, 128, 0),
+    (1, 8, 8, 128, 256, 0),
+    (1, 8, 8, 256, 256, 7),
+    (2, 16, 16, 64, 32, 5),
+    (2, 16, 16, 64, 32, 6),
+    (1, 16, 16, 64, 128, 1),
+    (1, 16, 16, 64, 128, 2),
+    (1, 16, 16, 64, 64, 3),
+    (1, 16, 16, 64, 64, 4),
+])
+def test_conv3x3_fwd(hip_lib, N, H, W, Cin, Cout, cfg):
+    from distributedpytorch_amd.ops import kernels as K
+    torch.manual_seed(0)
+    x = _bf(torch.randn(N, Cin, H, W))
+    w = _bf(torch.randn(Cout, Cin, 3, 3) * (2.0 / (9 * Cin)) ** 0.5)
+    b = torch.randn(Cout) * 0.1
+    ref = F.relu(F.conv2d(x, w, b, padding=1))
+    Cs = K.round_up(Cin, 8)
+    xin = torch.zeros(N, Cs, H, W)
+    xin[:, :Cin] = x
+    packed, ng, kp = _pack_one(0, w, Cs)
+    y = torch.empty(N, H, W, Cout, dtype=torch.bfloat16, device="cuda")
+    K.igemm(_nhwc(xin), packed, y, Ngemm=ng, Kpad=kp, KH=3, KW=3, stride=1, pad=1, Cs=Cs, out_grid=(N, H, W),
+            bias=b.cuda(), relu=True, cfg=cfg)
+    torch.cuda.synchronize()
+    assert _rel(_nchw(y), ref) < 2e-2
+
+
+@pytest.mark.parametrize("N,H,W,Cin,Cout", [(2, 13, 18, 32, 64), (1, 8, 8, 256, 128), (2, 16, 16, 64, 32)])
+def test_conv3x3_dgrad_masked(hip_lib, N, H, W, Cin, Cout):
+    from distributedpytorch_amd.ops import kernels as K
+    torch.manual_seed(1)
+    x = _bf(F.relu(torch.randn(N, Cin, H, W)))          # a ReLU output -> mask source
+    w = _bf(torch.randn(Cout, Cin, 3, 3) * 0.05)
+    g = _bf(torch.randn(N, Cout, H, W))
+    xr = x.clone().requires_grad_(True)
+    F.conv2d(xr, w, padding=1).backward(g)
+    ref = xr.grad * (x > 0)
+    packed, ng, kp = _pack_one(1, w)
+    out = torch.empty(N, H, W, Cin, dtype=torch.bfloat16, device="cuda")
+    K.igemm(_nhwc(g), packed, out, Ngemm=ng, Kpad=kp, KH=3, KW=3, stride=1, pad=1, Cs=Cout, out_grid=(N, H, W),
+            mask=_nhwc(x))
+    torch.cuda.synchronize()
+    assert _rel(_nchw(out), ref) < 2e-2
+
+
+@pytest.mark.parametrize("N,h,w,Cin,Cout", [(2, 5, 7, 64, 32), (1, 4, 4, 512, 256), (2, 8, 8, 128, 64)])
+def test_deconv_fwd_into_concat(hip_lib, N, h, w, Cin, Cout):
+    from distributedpytorch_amd.ops import kernels as K
+    torch.manual_seed(2)
+    x = _bf(torch.randn(N, Cin, h, w))
+    wt = _bf(torch.randn(Cin, Cout, 2, 2) * 0.05)
+    b = torch.randn(Cout) * 0.1
+    ref = F.conv_transpose2d(x, wt, b, stride=2)
+    packed, ng, kp = _pack_one(2, wt)
+    cat = torch.full((N, 2 * h, 2 * w, 2 * Cout), 7.0, dtype=torch.bfloat16, device="cuda")
+    K.igemm(_nhwc(x), packed, cat[..., Cout:], Ngemm=ng, Kpad=kp, KH=1, KW=1, stride=1, pad=0, Cs=Cin,
+            out_grid=(N, h, w), bias=b.cuda(), mode=1, Cout=Cout)
+    torch.cuda.synchronize()
+    assert _rel(_nchw(cat[..., Cout:]), ref) < 2e-2
+    assert (cat[..., :Cout] == 7.0).all()              # skip half untouched
+
+
+@pytest.mark.parametrize("N,h,w,Cin,Cout", [(2, 5, 7, 64, 32), (1, 4, 4, 512, 256)])
+def test_deconv_dgrad_from_concat(hip_lib, N, h, w, Cin, Cout):
+    from distributedpytorch_amd.ops import kernels as K
+    torch.manual_seed(3)
+    x = _bf(F.relu(torch.randn(N, Cin, h, w)))
+    wt = _bf(torch.randn(Cin, Cout, 2, 2) * 0.05)
+    gup = _bf(torch.randn(N, Cout, 2 * h, 2 * w))
+    xr = x.clone().requires_grad_(True)
+    F.conv_transpose2d(xr, wt, stride=2).backward(gup)
+    ref = xr.grad * (x > 0)
+    packed, ng, kp = _pack_one(3, wt)
+    dcat = torch.zeros(N, 2 * h, 2 * w, 2 * Cout, dtype=torch.bfloat16, device="cuda")
+    dcat[..., Cout:] = _nhwc(gup)
+    out = torch.empty(N, h, w, Cin, dtype=torch.bfloat16, device="cuda")
+    K.igemm(dcat[..., Cout:], packed, out, Ngemm=ng, Kpad=kp, KH=2, KW=2, stride=2, pad=0, Cs=Cout,
+            out_grid=(N, h, w), mask=_nhwc(x))
+    torch.cuda.synchronize()
+    assert _rel(_nchw(out), ref) < 2e-2
+
+
+@pytest.mark.parametrize("N,H,W,Cin,Cout,cin_pad", [
+    (2, 19, 21, 3, 32, 8), (2, 16, 16, 32, 32, None), (1, 12, 16, 64, 128, None), (2, 8, 8, 128, 64, None)])
+def test_conv3x3_wgrad(hip_lib, N, H, W, Cin, Cout, cin_pad):
+    from distributedpytorch_amd.ops import kernels as K
+    torch.manual_seed(4)
+    x = _bf(torch.randn(N, Cin, H, W))
+    g = _bf(torch.randn(N, Cout, H, W))
+    wr = torch.zeros(Cout, Cin, 3, 3, requires_grad=True)
+    br = torch.zeros(Cout, requires_grad=True)
+    F.conv2d(x, wr, br, padding=1).backward(g)
+    Cs = cin_pad or Cin
+    xin = torch.zeros(N, Cs, H, W)
+    xin[:, :Cin] = x
+    gw = torch.full((Cout, Cin, 3, 3), 0.5, device="cuda")    # accumulates on top
+    gb = torch.full((Cout,), 0.5, device="cuda")
+    K.wgrad(_nhwc(g), _nhwc(xin), kind=0, grid=(N, H, W), M=Cout, Nc=Cs, s=1, pad=1, KW=3, gw=gw.view(-1), gb=gb,
+            Nreal=Cin)
+    torch.cuda.synchronize()
+    assert _rel(gw.cpu() - 0.5, wr.grad) < 1e-2
+    assert _rel(gb.cpu() - 0.5, br.grad) < 1e-2
+
+
+@pytest.mark.parametrize("N,h,w,Cin,Cout", [(2, 5, 7, 64, 32), (1, 4, 4, 512, 256), (2, 8, 8, 128, 64)])
+def test_deconv_wgrad(hip_lib, N, h, w, Cin, Cout):
+    from distributedpytorch_amd.ops import kernels as K
+    torch.manual_seed(5)
+    x = _bf(torch.randn(N, Cin, h, w))
+    gup = _bf(torch.randn(N, Cout, 2 * h, 2 * w))
+    wr = torch.zeros(Cin, Cout, 2, 2, requires_grad=True)
+    br = torch.zeros(Cout, requires_grad=True)
+    F.conv_transpose2d(x, wr, br, stride=2).backward(gup)
+    dcat = torch.zeros(N, 2 * h, 2 * w, 2 * Cout, dtype=torch.bfloat16, device="cuda")
+    dcat[..., Cout:] = _nhwc(gup)
+    gw = torch.zeros(Cin, Cout, 2, 2, device="cuda")
+    gb = torch.zeros(Cout, device="cuda")
+    K.wgrad(dcat[..., Cout:], _nhwc(x), kind=1, grid=(N, h, w), M=Cout, Nc=Cin, s=2, pad=0, KW=2, gw=gw.view(-1),
+            gb=gb, Nreal=Cin)
+    torch.cuda.synchronize()
+    assert _rel(gw.cpu(), wr.grad) < 1e-2
+    assert _rel(gb.cpu(), br.grad) < 1e-2
+
+
+@pytest.mark.parametrize("N,H,W,C", [(2, 16, 16, 32), (1, 9, 11, 64)])
+def test_maxpool_and_backward(hip_lib, N, H, W, C):
+    from distributedpytorch_amd.ops import kernels as K
+    torch.manual_seed(6)
+    s = _bf(F.relu(torch.randn(N, C, H, W)))
+    cat = torch.zeros(N, H, W, 2 * C, dtype=torch.bfloat16, device="cuda")
+    cat[..., :C] = _nhwc(s)
+    pooled = torch.empty(N, H // 2, W // 2, C, dtype=torch.bfloat16, device="cuda")
+    K.maxpool2(cat[..., :C], pooled)
+    sr = s.clone().requires_grad_(True)
+    pr = F.max_pool2d(sr, 2, 2)
+    assert _rel(_nchw(pooled), pr.detach()) == 0.0
+    dpool = _bf(torch.randn_like(pr))
+    dskip = _bf(torch.randn(N, C, H, W))
+    pr.backward(dpool)
+    ref = (sr.grad + dskip) * (s > 0)
+    dcat = torch.zeros(N, H, W, 2 * C, dtype=torch.bfloat16, device="cuda")
+    dcat[..., :C] = _nhwc(dskip)
+    g = torch.empty(N, H, W, C, dtype=torch.bfloat16, device="cuda")
+    K.pool_bwd(cat[..., :C], dcat[..., :C], _nhwc(dpool), g)
+    torch.cuda.synchronize()
+    assert _rel(_nchw(g), ref) < 1e-2
+
+
+def test_head_loss_fwd_bwd(hip_lib):
+    from distributedpytorch_amd.ops import kernels as K
+    from distributedpytorch_amd.loss import bce_dice_from_probs
+    torch.manual_seed(7)
+    N, H, W, C = 2, 33, 40, 32
+    y = _bf(F.relu(torch.randn(N, C, H, W)))
+    w = torch.randn(1, C, 1, 1) * 0.2
+    b = torch.randn(1) * 0.1
+    t = (torch.rand(N, 1, H, W) > 0.6).float()
+    yr, wr, br = y.clone().requires_grad_(True), w.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    loss = bce_dice_from_probs(torch.sigmoid(F.conv2d(yr, wr, br)), t)
+    (3.0 * loss).backward()
+    wc, bc, tc = w.cuda(), b.cuda(), t.cuda().contiguous()
+    S, probs = K.head_fwd(_nhwc(y), wc, bc, tc, want_probs=True)
+    n = t.numel()
+    Sc = S.detach().clone().requires_grad_(True)
+    loss_k = Sc[0] / n - torch.log(2 * Sc[1] / (Sc[2] + Sc[3] + 1e-15))
+    (3.0 * loss_k).backward()
+    assert abs(loss_k.item() - loss.item()) < 1e-4 * max(1.0, abs(loss.item()))
+    gw = torch.zeros(C, device="cuda")
+    gb = torch.zeros(1, device="cuda")
+    gy = K.head_bwd(_nhwc(y), wc, bc, tc, Sc.grad, gw, gb)
+    torch.cuda.synchronize()
+    assert _rel(gw.cpu(), wr.grad.view(-1)) < 1e-3
+    assert _rel(gb.cpu(), br.grad) < 1e-3
+    assert _rel(_nchw(gy), yr.grad * (y > 0)) < 1e-2
+    assert _rel(probs.cpu(), torch.sigmoid(F.conv2d(y, w, b))[:, 0]) < 1e-5
+
+
+def test_input_conversion(hip_lib):
+    from distributedpytorch_amd.ops import kernels as K
+    x = torch.rand(2, 3, 7, 9)
+    y = K.input_nhwc8(x.cuda())
+    torch.cuda.synchronize()
+    assert tuple(y.shape) == (2, 7, 9, 8)
+    assert (y[..., 3:] == 0).all()
+    assert _rel(_nchw(y[..., :3].contiguous()), _bf(x)) == 0.0
