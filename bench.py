@@ -87,6 +87,10 @@ def main():
     loss = None
     for i in range(a.warmup):
         loss = step(i)
+        if rank == 0:
+            torch.cuda.synchronize()
+            print(f"[bench] warmup step {i + 1}/{a.warmup} done at {time.perf_counter() - t_w0:.1f}s", file=sys.stderr,
+                  flush=True)
     torch.cuda.synchronize()
     warm_s = time.perf_counter() - t_w0
     if world > 1:
