@@ -14,6 +14,10 @@ so every strategy (single device, DDP, DP, GPipe stages) runs the same kernels. 
   (``space.notify_ready``) so the data-parallel all-reduce of that bucket starts while the rest of
   the backward runs.
 
+Tensor interface: activations cross block boundaries as *logical NCHW, channels_last* bf16 tensors
+(memory = NHWC), exactly what the stock-op backend produces, so the pipeline send/recv code and any
+torch op work on them unchanged; internally the kernels see the NHWC view (``permute(0, 2, 3, 1)``).
+
 Gradient convention between blocks: the gradient a block's backward *receives* for its (ReLU)
 output is already multiplied by the ReLU mask (the consumer applies it in its own fused epilogue);
 for the encoder skip, whose two consumers (pool, decoder concat) add up, the mask is applied once in
@@ -178,9 +182,9 @@ class HipBlocks:
 
     # ------------------------------------------------------------------ block API
     def prep(self, x: torch.Tensor) -> torch.Tensor:
-        if x.dtype == torch.bfloat16 and x.dim() == 4 and x.shape[-1] == 8:
-            return x   # already NHWC8 (pipeline stages re-entering)
-        return K.input_nhwc8(x.float())
+        if x.dtype == torch.bfloat16 and x.dim() == 4 and x.shape[1] == 8:
+            return x   # already converted (logical NCHW8, channels_last)
+        return _o(K.input_nhwc8(x.float()))
 
     def enc(self, l: int, x):
         self.ensure_packed()
@@ -201,7 +205,7 @@ class HipBlocks:
     @torch.no_grad()
     def head_probs(self, x):
         seg = self.model.segmap
-        _, probs = K.head_fwd(x, seg.weight, seg.bias, None, want_probs=True)
+        _, probs = K.head_fwd(_v(x), seg.weight, seg.bias, None, want_probs=True)
         return probs.unsqueeze(1)
 
     # concat buffers: the encoder allocates [N,H,W,2C] and returns its first half as the skip
@@ -211,6 +215,8 @@ class HipBlocks:
         return cat
 
     def cat_for(self, skip: torch.Tensor) -> torch.Tensor:
+        """NHWC concat buffer whose first half holds ``skip`` (an NHWC view): zero-copy when ``skip``
+        came from this engine's encoder, one copy when it arrived from elsewhere (pipeline recv)."""
         N, H, W, C = skip.shape
         cat = self._cats.pop(skip.data_ptr(), None)
         if cat is not None and tuple(cat.shape) == (N, H, W, 2 * C) and skip.stride(2) == 2 * C:
@@ -218,6 +224,18 @@ class HipBlocks:
         cat = torch.empty(N, H, W, 2 * C, dtype=torch.bfloat16, device=self.device)
         cat[..., :C].copy_(skip)
         return cat
+
+
+def _v(t: torch.Tensor) -> torch.Tensor:
+    """logical-NCHW channels_last -> NHWC view (copies only if the layout is something else)."""
+    if t.dim() == 4 and t.stride(1) != 1:
+        t = t.contiguous(memory_format=torch.channels_last)
+    return t.permute(0, 2, 3, 1)
+
+
+def _o(t: torch.Tensor) -> torch.Tensor:
+    """NHWC -> logical-NCHW view (channels_last strides)."""
+    return t.permute(0, 3, 1, 2)
 
 
 def _grad(p: torch.nn.Parameter) -> torch.Tensor:
@@ -232,6 +250,7 @@ class _EncFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, anchor, x, B: HipBlocks, l: int):
         c1, c2 = B.enc_convs[l]
+        x = _v(x)
         N, H, W = x.shape[:3]
         a = B.conv_fwd(c1, x)
         cat = B.new_cat(N, H, W, c2.Cout)
@@ -242,7 +261,7 @@ class _EncFn(torch.autograd.Function):
         ctx.B, ctx.l = B, l
         ctx.x_needs_grad = l > 0
         ctx.save_for_backward(x, a, cat)
-        return skip, pooled
+        return _o(skip), _o(pooled)
 
     @staticmethod
     def backward(ctx, dskip, dpooled):
@@ -253,6 +272,9 @@ class _EncFn(torch.autograd.Function):
         skip = cat[..., :C]
         if dpooled is None:
             dpooled = torch.zeros(x.shape[0], x.shape[1] // 2, x.shape[2] // 2, C, dtype=torch.bfloat16, device=x.device)
+        else:
+            dpooled = _v(dpooled)
+        dskip = None if dskip is None else _v(dskip)
         g2 = torch.empty_like(a)
         K.pool_bwd(skip, dskip, dpooled, g2)
         g1 = B.conv_dgrad(c2, g2, mask=a)
@@ -261,32 +283,33 @@ class _EncFn(torch.autograd.Function):
         gx = B.conv_dgrad(c1, g1) if ctx.x_needs_grad else None
         B.conv_wgrad(c1, g1, x)
         B.ready([c1.mod])
-        return None, gx, None, None
+        return None, (None if gx is None else _o(gx)), None, None
 
 
 class _MidFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, anchor, x, B: HipBlocks):
         c1, c2 = B.mid_convs
+        x = _v(x)
         a = B.conv_fwd(c1, x)
         y = B.conv_fwd(c2, a)
         ctx.B = B
         ctx.save_for_backward(x, a)
-        return y
+        return _o(y)
 
     @staticmethod
     def backward(ctx, g2):
         B = ctx.B
         x, a = ctx.saved_tensors
         c1, c2 = B.mid_convs
-        g2 = g2.contiguous()
+        g2 = _v(g2)
         g1 = B.conv_dgrad(c2, g2, mask=a)
         B.conv_wgrad(c2, g2, a)
         B.ready([c2.mod])
         gx = B.conv_dgrad(c1, g1)
         B.conv_wgrad(c1, g1, x)
         B.ready([c1.mod])
-        return None, gx, None
+        return None, _o(gx), None
 
 
 class _DecFn(torch.autograd.Function):
@@ -295,13 +318,14 @@ class _DecFn(torch.autograd.Function):
         d = B.deconvs[i]
         c1, c2 = B.dec_convs[i]
         C = d.Cout
-        cat = B.cat_for(skip)
+        x = _v(x)
+        cat = B.cat_for(_v(skip))
         B.deconv_fwd(d, x, cat[..., C:])
         a = B.conv_fwd(c1, cat)
         y = B.conv_fwd(c2, a)
         ctx.B, ctx.i = B, i
         ctx.save_for_backward(x, cat, a)
-        return y
+        return _o(y)
 
     @staticmethod
     def backward(ctx, g2):
@@ -310,7 +334,7 @@ class _DecFn(torch.autograd.Function):
         d = B.deconvs[i]
         c1, c2 = B.dec_convs[i]
         C = d.Cout
-        g2 = g2.contiguous()
+        g2 = _v(g2)
         g1 = B.conv_dgrad(c2, g2, mask=a)
         B.conv_wgrad(c2, g2, a)
         B.ready([c2.mod])
@@ -321,13 +345,14 @@ class _DecFn(torch.autograd.Function):
         dx = B.deconv_dgrad(d, gup, x)
         B.deconv_wgrad(d, gup, x)
         B.ready([d.mod])
-        return None, dx, dcat[..., :C], None, None
+        return None, _o(dx), _o(dcat[..., :C]), None, None
 
 
 class _HeadFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, anchor, y, t, B: HipBlocks):
         seg = B.model.segmap
+        y = _v(y)
         S, _ = K.head_fwd(y, seg.weight, seg.bias, t)
         ctx.B = B
         ctx.save_for_backward(y, t)
@@ -340,4 +365,4 @@ class _HeadFn(torch.autograd.Function):
         seg = B.model.segmap
         gy = K.head_bwd(y, seg.weight, seg.bias, t, dS, _grad(seg.weight).view(-1), _grad(seg.bias))
         B.ready([seg])
-        return None, gy, None, None
+        return None, _o(gy), None, None

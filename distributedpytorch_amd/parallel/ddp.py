@@ -38,7 +38,7 @@ class BucketedAllReduce:
         self.scale = scale
         self.nccl = dist.get_backend(group) == "nccl"
         cap = int(bucket_mb * 2 ** 20 / 4)
-        first = int(first_bucket_mb * 2 ** 20 / 4)
+        first = int(min(first_bucket_mb, bucket_mb) * 2 ** 20 / 4)
         self.buckets: List[tuple] = []   # (start, end, first_param, last_param_exclusive)
         self.bucket_of: List[int] = []
         start_p = 0
