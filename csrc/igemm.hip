@@ -31,6 +31,7 @@ struct IgemmArgs {
   int Ngemm, Kpad;      // GEMM N, K padded to a multiple of BK (packed weights zero-filled)
   int mode;             // 0: y[m][n]   1: transposed-conv 2x2/s2 scatter, n = (2i+j)*Cout + co
   int relu, accumulate, Cout;
+  unsigned xbytes;      // bytes addressable from x (< 2^31; the host splits larger batches by image)
 };
 
 template <int BK>
@@ -48,6 +49,7 @@ __global__ __launch_bounds__(256) void igemm_kernel(IgemmArgs a) {
   constexpr int NWC = BC / WC;
   constexpr int NWP = BP / WP;
   static_assert(NWC * NWP == 4, "4 waves per block");
+  static_assert(BP % RPP == 0 && (BC % RPP == 0 || (BC * CPR) % 64 == 0), "loader tiling");
   constexpr int TP = WP / 16, TC = WC / 16;
   constexpr int RB = BK * 2;                // LDS row bytes
   __shared__ __attribute__((aligned(16))) char lds[2][(BP + BC) * RB];
@@ -80,8 +82,12 @@ __global__ __launch_bounds__(256) void igemm_kernel(IgemmArgs a) {
   }
   const int taps = a.KH * a.KW;
   const int S = a.Kpad / BK;
-  uint4 pr[LP], wr[LW];
+  u32x4_t pr[LP], wr[LW];
 
+  // Zero padding by the buffer unit's range check: an out-of-image tap gets an offset beyond
+  // num_records and reads 0 -- no branch, no select, every load issued back to back (a branch
+  // around each load makes hipcc wait vmcnt(0) per load: guide §5 ".s traps" (c)).
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, 0, (int)a.xbytes, 0x00020000);
   auto gload = [&](int s) {
     const int k0 = (s * CPR + lchunk) * 8;
     const int tap = k0 / a.Cs;
@@ -93,15 +99,14 @@ __global__ __launch_bounds__(256) void igemm_kernel(IgemmArgs a) {
       const int ih = ph[i] * a.stride + kh - a.pad;
       const int iw = pw[i] * a.stride + kw - a.pad;
       const bool ok = pok[i] && tok && ih >= 0 && ih < a.Hs && iw >= 0 && iw < a.Ws;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (ok) v = *reinterpret_cast<const uint4*>(a.x + ((long)(pn[i] * a.Hs + ih) * a.Ws + iw) * a.ldx + ci);
-      pr[i] = v;
+      const unsigned off = ok ? (unsigned)((((pn[i] * a.Hs + ih) * a.Ws + iw) * a.ldx + ci) * 2) : 0x80000000u;
+      pr[i] = __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0);
     }
 #pragma unroll
     for (int i = 0; i < LW; ++i) {
       const int r = lrow + i * RPP;
-      if (r < BC)
-        wr[i] = *reinterpret_cast<const uint4*>(a.w + (long)(c0 + r) * a.Kpad + s * BK + lchunk * 8);
+      if (BC % RPP == 0 || tid < BC * CPR)
+        wr[i] = *reinterpret_cast<const u32x4_t*>(a.w + (long)(c0 + r) * a.Kpad + s * BK + lchunk * 8);
     }
   };
   auto lstore = [&](int buf) {
@@ -110,12 +115,12 @@ __global__ __launch_bounds__(256) void igemm_kernel(IgemmArgs a) {
 #pragma unroll
     for (int i = 0; i < LP; ++i) {
       const int r = lrow + i * RPP;
-      if (r < BP) *reinterpret_cast<uint4*>(P + r * RB + swz_nk<BK>(r, lchunk) * 16) = pr[i];
+      *reinterpret_cast<u32x4_t*>(P + r * RB + swz_nk<BK>(r, lchunk) * 16) = pr[i];
     }
 #pragma unroll
     for (int i = 0; i < LW; ++i) {
       const int r = lrow + i * RPP;
-      if (r < BC) *reinterpret_cast<uint4*>(Wt + r * RB + swz_nk<BK>(r, lchunk) * 16) = wr[i];
+      if (BC % RPP == 0 || tid < BC * CPR) *reinterpret_cast<u32x4_t*>(Wt + r * RB + swz_nk<BK>(r, lchunk) * 16) = wr[i];
     }
   };
 
@@ -131,6 +136,9 @@ __global__ __launch_bounds__(256) void igemm_kernel(IgemmArgs a) {
   for (int s = 0; s < S; ++s) {
     const int buf = s & 1;
     if (s + 1 < S) gload(s + 1);
+    // keep the prefetch issue above and the LDS stores below the MFMAs: without the fences hipcc
+    // hoists the next tile's ds_writes (and so their vmcnt waits) in front of this tile's MFMAs
+    __builtin_amdgcn_sched_barrier(0);
     const char* P = lds[buf];
     const char* Wt = lds[buf] + BP * RB;
 #pragma unroll
@@ -153,6 +161,7 @@ __global__ __launch_bounds__(256) void igemm_kernel(IgemmArgs a) {
         for (int ip = 0; ip < TP; ++ip)
           acc[ic][ip] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ic], bfr[ip], acc[ic][ip], 0, 0, 0);
     }
+    __builtin_amdgcn_sched_barrier(0);
     if (s + 1 < S) lstore(buf ^ 1);
     __syncthreads();
   }

@@ -30,6 +30,7 @@ struct WgradArgs {
   int M, Nc;            // channels of A (GEMM rows) and B (GEMM cols, may be < tile width: zero filled)
   int s, pad, KW;       // tap-dependent operand is read at (h*s + kh - pad, w*s + kw - pad)
   int pix_per_split, splits;
+  unsigned abytes, bbytes;  // addressable bytes of A / B (< 2^31; the host splits larger batches)
 };
 
 template <int RB>
@@ -86,29 +87,33 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void wgrad_kernel(Wgrad
   const int lpx = tid / SLOTS, lslot = tid - lpx * SLOTS;
   const bool do_bias = a.bslab != nullptr && nt == 0;
 
-  uint4 reg[L];
+  u32x4_t reg[L];
+  // zero padding / channel tails via the buffer range check (no branch per load, see igemm.hip)
+  const __amdgpu_buffer_rsrc_t ar = __builtin_amdgcn_make_buffer_rsrc((void*)a.A, 0, (int)a.abytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t br = __builtin_amdgcn_make_buffer_rsrc((void*)a.B, 0, (int)a.bbytes, 0x00020000);
   auto gload = [&](int st) {
     const long p = pbeg + (long)st * 32 + lpx;
     const bool pok = p < pend;
     int n = 0, h = 0, w = 0;
-    if (pok) {
+    {
       const int hw = a.Hg * a.Wg;
-      n = (int)(p / hw);
-      const int rem = (int)(p - (long)n * hw);
+      const int pp = pok ? (int)p : 0;
+      n = pp / hw;
+      const int rem = pp - n * hw;
       h = rem / a.Wg;
       w = rem - h * a.Wg;
     }
 #pragma unroll
     for (int j = 0; j < L; ++j) {
       const int c = lslot + j * SLOTS;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (c < CH && pok) {
+      if (c < CH) {
         const bool isA = c < CHA;
         const int cl = isA ? c : c - CHA;
         const int cpr = isA ? CPRA : CPRB;
         const int tap = cl / cpr, cc = cl - tap * cpr;
         const bool dep = (isA == TAPA);
-        int ih = h, iw = w, H = isA ? a.HA : a.HB, W = isA ? a.WA : a.WB;
+        int ih = h, iw = w;
+        const int H = isA ? a.HA : a.HB, W = isA ? a.WA : a.WB;
         if (dep) {
           const int kh = tap / a.KW, kw = tap - (tap / a.KW) * a.KW;
           ih = h * a.s + kh - a.pad;
@@ -116,13 +121,11 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void wgrad_kernel(Wgrad
         }
         const int ch = (isA ? m0 : n0) + cc * 8;
         const int nch = isA ? a.M : a.Nc;
-        if (ih >= 0 && ih < H && iw >= 0 && iw < W && ch < nch) {
-          const bf16_t* src = isA ? a.A : a.B;
-          const int ld = isA ? a.lda : a.ldb;
-          v = *reinterpret_cast<const uint4*>(src + ((long)(n * H + ih) * W + iw) * ld + ch);
-        }
+        const bool ok = pok && ih >= 0 && ih < H && iw >= 0 && iw < W && ch < nch;
+        const int ld = isA ? a.lda : a.ldb;
+        const unsigned off = ok ? (unsigned)((((n * H + ih) * W + iw) * ld + ch) * 2) : 0x80000000u;
+        reg[j] = isA ? __builtin_amdgcn_raw_buffer_load_b128(ar, off, 0, 0) : __builtin_amdgcn_raw_buffer_load_b128(br, off, 0, 0);
       }
-      reg[j] = v;
     }
   };
   auto lstore = [&]() {
@@ -132,10 +135,10 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void wgrad_kernel(Wgrad
       if (c < CH) {
         if (c < CHA) {
           const int tap = c / CPRA, cc = c - tap * CPRA;
-          *reinterpret_cast<uint4*>(lds + tap * IMGA + lpx * RBA + ((cc ^ swz_kk<RBA>(lpx)) << 4)) = reg[j];
+          *reinterpret_cast<u32x4_t*>(lds + tap * IMGA + lpx * RBA + ((cc ^ swz_kk<RBA>(lpx)) << 4)) = reg[j];
         } else {
           const int cl = c - CHA, tap = cl / CPRB, cc = cl - tap * CPRB;
-          *reinterpret_cast<uint4*>(lds + TA * IMGA + tap * IMGB + lpx * RBB + ((cc ^ swz_kk<RBB>(lpx)) << 4)) = reg[j];
+          *reinterpret_cast<u32x4_t*>(lds + TA * IMGA + tap * IMGB + lpx * RBB + ((cc ^ swz_kk<RBB>(lpx)) << 4)) = reg[j];
         }
       }
     }
@@ -157,6 +160,7 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void wgrad_kernel(Wgrad
   __syncthreads();
   for (int st = 0; st < nst; ++st) {
     if (st + 1 < nst) gload(st + 1);
+    __builtin_amdgcn_sched_barrier(0);
     if constexpr (TAPA) {
       bf16x8_t bf[TN];
 #pragma unroll
@@ -193,6 +197,7 @@ __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void wgrad_kernel(Wgrad
           bsum += bf2f(v);
         }
     }
+    __builtin_amdgcn_sched_barrier(0);
     __syncthreads();
     if (st + 1 < nst) {
       lstore();
@@ -255,34 +260,53 @@ DPA_API int dpa_wgrad(const WgradArgs* args, int kind, int cfg, hipStream_t st) 
 // Sum the split slabs and accumulate into the PyTorch-layout fp32 gradient:
 //   mode 0 (Conv2d OIHW):          gw[m][n][tap]          (m = out ch, n = in ch < Nreal)
 //   mode 1 (ConvTranspose2d IOHW): gw[n][m][tap]          (n = in ch, m = out ch)
+// Block = 32 consecutive slab elements x 8 split groups (coalesced 128-B rows, 8 independent load
+// streams per element), partial sums combined through LDS in a fixed order -> deterministic.
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ slab, const float* __restrict__ bslab,
                                                            float* __restrict__ gw, float* __restrict__ gb, int splits, int T,
                                                            int M, int Nc, int Nreal, int mode) {
+  __shared__ float part[8][33];
   const long tot = (long)T * M * Nc;
-  const long stride = (long)gridDim.x * blockDim.x;
-  for (long idx = (long)blockIdx.x * blockDim.x + threadIdx.x; idx < tot; idx += stride) {
-    const int n = (int)(idx % Nc);
-    const int m = (int)((idx / Nc) % M);
-    const int t = (int)(idx / ((long)Nc * M));
-    if (n >= Nreal) continue;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  const long nblk_w = (tot + 31) / 32;
+  for (long b = blockIdx.x; b < nblk_w + (bslab ? (M + 31) / 32 : 0); b += gridDim.x) {
+    const bool isb = b >= nblk_w;
+    const long idx = isb ? (b - nblk_w) * 32 + tx : b * 32 + tx;
+    const long lim = isb ? M : tot;
+    const float* src = isb ? bslab : slab;
+    const long stride = isb ? M : tot;
     float s = 0.f;
-    for (int k = 0; k < splits; ++k) s += slab[(long)k * tot + idx];
-    const long dst = mode == 0 ? ((long)m * Nreal + n) * T + t : ((long)n * M + m) * T + t;
-    gw[dst] += s;
-  }
-  if (bslab && gb) {
-    for (long m = (long)blockIdx.x * blockDim.x + threadIdx.x; m < M; m += stride) {
-      float s = 0.f;
-      for (int k = 0; k < splits; ++k) s += bslab[(long)k * M + m];
-      gb[m] += s;
+    if (idx < lim) {
+#pragma unroll 8
+      for (int k = ty; k < splits; k += 8) s += src[(long)k * stride + idx];
     }
+    part[ty][tx] = s;
+    __syncthreads();
+    if (ty == 0 && idx < lim) {
+      float r = 0.f;
+#pragma unroll
+      for (int g = 0; g < 8; ++g) r += part[g][tx];
+      if (isb) {
+        gb[idx] += r;
+      } else {
+        const int n = (int)(idx % Nc);
+        const int m = (int)((idx / Nc) % M);
+        const int t = (int)(idx / ((long)Nc * M));
+        if (n < Nreal) {
+          const long dst = mode == 0 ? ((long)m * Nreal + n) * T + t : ((long)n * M + m) * T + t;
+          gw[dst] += r;
+        }
+      }
+    }
+    __syncthreads();
   }
 }
 
 DPA_API int dpa_wgrad_reduce(const float* slab, const float* bslab, float* gw, float* gb, int splits, int T, int M, int Nc,
                              int Nreal, int mode, hipStream_t st) {
   const long tot = (long)T * M * Nc;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(dpa_grid(tot, 256, 4096)), dim3(256), 0, st, slab, bslab, gw, gb, splits, T,
-                     M, Nc, Nreal, mode);
+  const long nb = (tot + 31) / 32 + (bslab ? (M + 31) / 32 : 0);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)(nb < 8192 ? nb : 8192)), dim3(256), 0, st, slab, bslab, gw, gb,
+                     splits, T, M, Nc, Nreal, mode);
   return (int)hipGetLastError();
 }

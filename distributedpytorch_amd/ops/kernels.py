@@ -24,13 +24,15 @@ c_int, c_ll, c_void_p = ctypes.c_int, ctypes.c_longlong, ctypes.c_void_p
 class IgemmArgs(ctypes.Structure):
     _fields_ = [("x", c_void_p), ("w", c_void_p), ("bias", c_void_p), ("y", c_void_p), ("mask", c_void_p)] + \
                [(n, c_int) for n in ("ldx", "ldy", "ldm", "mask_ch", "N", "Ho", "Wo", "Hs", "Ws", "Cs", "KH", "KW",
-                                     "stride", "pad", "Ngemm", "Kpad", "mode", "relu", "accumulate", "Cout")]
+                                     "stride", "pad", "Ngemm", "Kpad", "mode", "relu", "accumulate", "Cout")] + \
+               [("xbytes", ctypes.c_uint)]
 
 
 class WgradArgs(ctypes.Structure):
     _fields_ = [("A", c_void_p), ("B", c_void_p), ("slab", c_void_p), ("bslab", c_void_p)] + \
                [(n, c_int) for n in ("lda", "ldb", "N", "Hg", "Wg", "HA", "WA", "HB", "WB", "M", "Nc", "s", "pad",
-                                     "KW", "pix_per_split", "splits")]
+                                     "KW", "pix_per_split", "splits")] + \
+               [("abytes", ctypes.c_uint), ("bbytes", ctypes.c_uint)]
 
 
 class PackDesc(ctypes.Structure):
@@ -65,6 +67,19 @@ def round_up(x: int, m: int) -> int:
     return (x + m - 1) // m * m
 
 
+_MAX_BYTES = 2 ** 31 - 1024   # kernels address activations through 32-bit buffer offsets
+
+
+def _extent_bytes(N, H, W, C, ld):
+    return ((N * H * W - 1) * ld + C) * 2
+
+
+def _image_chunks(N: int, per_image_bytes: int):
+    """Split a batch so every launch addresses < 2 GiB per tensor (buffer-descriptor range)."""
+    per = max(1, _MAX_BYTES // max(per_image_bytes, 1))
+    return [(i, min(N, i + per)) for i in range(0, N, per)]
+
+
 # ------------------------------------------------------------------------------------------ igemm
 def igemm(x: torch.Tensor, wpacked: torch.Tensor, y: torch.Tensor, *, Ngemm: int, Kpad: int, KH: int, KW: int,
           stride: int, pad: int, Cs: int, out_grid, bias: Optional[torch.Tensor] = None, relu: bool = False,
@@ -89,10 +104,16 @@ def igemm(x: torch.Tensor, wpacked: torch.Tensor, y: torch.Tensor, *, Ngemm: int
         mch = min(Cm, Ngemm)
     if bias is not None:
         assert bias.dtype == torch.float32 and bias.is_contiguous() and bias.numel() >= (Cout or Ngemm)
-    a = IgemmArgs(_p(x).value, _p(wpacked).value, None if bias is None else bias.data_ptr(), y.data_ptr(),
-                  None if mask is None else mask.data_ptr(), ldx, ldy, ldm, mch, N, Ho, Wo, Hs, Ws, Cs, KH, KW,
-                  stride, pad, Ngemm, Kpad, mode, int(relu), int(accumulate), Cout)
-    _check(_lib.lib().dpa_igemm(ctypes.byref(a), c_int(cfg), _stream(y)), "igemm")
+    L = _lib.lib()
+    st = _stream(y)
+    for n0, n1 in _image_chunks(N, max(Hs * Ws * ldx, (4 if mode else 1) * Ho * Wo * ldy) * 2):
+        xs, ys = x[n0:n1], y[n0:n1]
+        nb = n1 - n0
+        a = IgemmArgs(xs.data_ptr(), _p(wpacked).value, None if bias is None else bias.data_ptr(), ys.data_ptr(),
+                      None if mask is None else mask[n0:n1].data_ptr(), ldx, ldy, ldm, mch, nb, Ho, Wo, Hs, Ws, Cs,
+                      KH, KW, stride, pad, Ngemm, Kpad, mode, int(relu), int(accumulate), Cout,
+                      _extent_bytes(nb, Hs, Ws, Cx, ldx))
+        _check(L.dpa_igemm(ctypes.byref(a), c_int(cfg), st), "igemm")
 
 
 # ------------------------------------------------------------------------------------------ wgrad
@@ -122,18 +143,21 @@ def wgrad(A: torch.Tensor, B: torch.Tensor, *, kind: int, grid, M: int, Nc: int,
             cfg = 12 if (M % 64 == 0 and Nc >= 64) else 11
     bm, bn = {1: (32, 16), 2: (32, 32), 3: (64, 32), 4: (64, 64), 11: (32, 32), 12: (64, 64)}[cfg]
     tiles = (M // bm) * (-(-Nc // bn))
-    P = N * Hg * Wg
-    splits, pps = wgrad_splits(P, tiles, target_blocks)
-    slab = torch.empty(splits * T * M * Nc + splits * M, dtype=torch.float32, device=A.device)
-    bslab = slab[splits * T * M * Nc:] if gb is not None else None
     assert gw.dtype == torch.float32 and gw.is_contiguous() and gw.numel() == M * Nreal * T
-    a = WgradArgs(A.data_ptr(), B.data_ptr(), slab.data_ptr(), None if bslab is None else bslab.data_ptr(),
-                  lda, ldb, N, Hg, Wg, HA, WA, HB, WB, M, Nc, s, pad, KW, pps, splits)
     L = _lib.lib()
     st = _stream(A)
-    _check(L.dpa_wgrad(ctypes.byref(a), c_int(kind), c_int(cfg), st), "wgrad")
-    _check(L.dpa_wgrad_reduce(_p(slab), _p(bslab), _p(gw), _p(gb), c_int(splits), c_int(T), c_int(M), c_int(Nc),
-                              c_int(Nreal), c_int(kind), st), "wgrad_reduce")
+    for n0, n1 in _image_chunks(N, max(HA * WA * lda, HB * WB * ldb) * 2):
+        nb = n1 - n0
+        P = nb * Hg * Wg
+        splits, pps = wgrad_splits(P, tiles, target_blocks)
+        slab = torch.empty(splits * T * M * Nc + splits * M, dtype=torch.float32, device=A.device)
+        bslab = slab[splits * T * M * Nc:] if gb is not None else None
+        a = WgradArgs(A[n0:n1].data_ptr(), B[n0:n1].data_ptr(), slab.data_ptr(),
+                      None if bslab is None else bslab.data_ptr(), lda, ldb, nb, Hg, Wg, HA, WA, HB, WB, M, Nc, s,
+                      pad, KW, pps, splits, _extent_bytes(nb, HA, WA, CA, lda), _extent_bytes(nb, HB, WB, CB, ldb))
+        _check(L.dpa_wgrad(ctypes.byref(a), c_int(kind), c_int(cfg), st), "wgrad")
+        _check(L.dpa_wgrad_reduce(_p(slab), _p(bslab), _p(gw), _p(gb), c_int(splits), c_int(T), c_int(M), c_int(Nc),
+                                  c_int(Nreal), c_int(kind), st), "wgrad_reduce")
 
 
 # ------------------------------------------------------------------------------------------ aux
