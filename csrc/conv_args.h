@@ -1,0 +1,66 @@
+// Argument blocks and LDS helpers shared by the convolution kernels (igemm.hip, wgrad.hip, halo.hip).
+#pragma once
+#include "common.h"
+
+struct IgemmArgs {
+  const bf16_t* x;      // source activations [N][Hs][Ws][ldx] (channel offset folded into the pointer)
+  const bf16_t* w;      // packed weights [Ngemm][Kpad] bf16
+  const float* bias;    // [Cout] fp32 or null
+  bf16_t* y;            // output (channel offset folded into the pointer)
+  const bf16_t* mask;   // ReLU-backward mask source (same pixel grid as y, mode 0) or null
+  int ldx, ldy, ldm, mask_ch;
+  int N, Ho, Wo;        // GEMM-M pixel grid
+  int Hs, Ws, Cs;       // source grid and channels gathered per tap (Cs % 8 == 0)
+  int KH, KW, stride, pad;
+  int Ngemm, Kpad;      // GEMM N, K padded to a multiple of BK (packed weights zero-filled)
+  int mode;             // 0: y[m][n]   1: transposed-conv 2x2/s2 scatter, n = (2i+j)*Cout + co
+  int relu, accumulate, Cout;
+  unsigned xbytes;      // bytes addressable from x (< 2^31; the host splits larger batches by image)
+};
+
+struct WgradArgs {
+  const bf16_t* A; const bf16_t* B;
+  float* slab;          // [splits][T][M][Nc]
+  float* bslab;         // [splits][M] or null (bias gradient partials)
+  int lda, ldb;
+  int N, Hg, Wg;        // pixel grid p = (n, h, w)
+  int HA, WA, HB, WB;   // spatial dims of A and B tensors
+  int M, Nc;            // channels of A (GEMM rows) and B (GEMM cols, may be < tile width: zero filled)
+  int s, pad, KW;       // tap-dependent operand is read at (h*s + kh - pad, w*s + kw - pad)
+  int pix_per_split, splits;
+  unsigned abytes, bbytes;  // addressable bytes of A / B (< 2^31; the host splits larger batches)
+};
+
+// nk images ([rows][BK] bf16, 16-B chunks): conflict-free ds_read_b128 fragment reads for any
+// 16 consecutive rows (tools/lds_banks.py)
+template <int BK>
+__device__ __forceinline__ int swz_nk(int row, int chunk) {
+  if constexpr (BK == 32) return chunk ^ ((row >> 1) & 3);
+  else return chunk ^ (row & 7);
+}
+
+// kk images ([pixel rows][channels] bf16, RB bytes per row) read with ds_read_b64_tr_b16
+template <int RB>
+__device__ __forceinline__ int swz_kk(int r) {
+  if constexpr (RB == 64) return ((r >> 3) & 1) * 2;
+  else if constexpr (RB == 128) return (((r >> 1) & 1) * 2) ^ (((r >> 3) & 1) * 4);
+  else if constexpr (RB == 256) return ((r & 1) * 2) ^ (((r >> 1) & 1) * 4) ^ (((r >> 3) & 1) * 8);
+  else return 0;
+}
+
+// 8 consecutive k (pixel rows 8g..8g+7 of a [32][RB] image) for the 16 columns starting at col0
+template <int RB>
+__device__ __forceinline__ bf16x8_t tr_frag(const char* img, int col0, int lane, int roff = 0) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int col = col0 + 4 * p;
+  const int ch = col >> 3, hb = (col & 7) * 2;
+  const int r0 = roff + 8 * g + q, r1 = r0 + 4;
+  const char* a0 = img + r0 * RB + ((ch ^ swz_kk<RB>(r0)) << 4) + hb;
+  const char* a1 = img + r1 * RB + ((ch ^ swz_kk<RB>(r1)) << 4) + hb;
+  s16x4_t v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4_t, a0));
+  s16x4_t v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4_t, a1));
+  typedef __attribute__((ext_vector_type(8))) short s16x8_t;
+  s16x8_t v = __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8_t, v);
+}
+

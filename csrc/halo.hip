@@ -1,0 +1,329 @@
+// Row-halo variants of the 3x3 convolution kernels for the full-resolution, low-channel layers of
+// the UNet (SURVEY §7.4 "Conv kernels on gfx950: MFMA efficiency collapses for C=32/64 full-res
+// layers ... you need NHWC tiles that reuse the 3x3 halo from LDS").
+//
+// The generic kernels (igemm.hip, wgrad.hip) gather every tap separately, so each input pixel is
+// fetched 9 times through L2; at 32-64 channels that traffic, not the MFMAs, sets the speed.  Here a
+// tile is a run of consecutive pixels of ONE image row; the three input rows it touches (plus one
+// pixel of halo on each side) are staged once into LDS and all 9 taps read shifted windows of them:
+// 3*(BP+2)/BP ~= 3x the tile instead of 9x.
+//
+//   igemm_halo : conv3x3 s1 p1 forward / dgrad (mode 0 epilogue: bias, ReLU, ReLU-mask, accumulate)
+//                K loop = 32-channel slices of the source (Cs % 32 == 0), 9 taps per slice from LDS.
+//   wgrad_halo : conv3x3 weight gradient; the B operand (layer input) is staged as 3 images of
+//                34 rows (kh = 0..2, w0-1 .. w0+32) and tap (kh, kw) reads rows kw .. kw+31.
+// Both require the tile to stay inside one image row (W % tile == 0), checked on the host.
+#include "conv_args.h"
+
+// ------------------------------------------------------------------------------------ igemm_halo
+template <int BP, int BC, int WP, int WC>
+__global__ __launch_bounds__(256) void igemm_halo_kernel(IgemmArgs a) {
+  constexpr int HR = BP + 2;              // pixels per halo row
+  constexpr int PROWS = 3 * HR;           // staged pixel rows (64 B = 32 channels each)
+  constexpr int PBYTES = PROWS * 64;
+  constexpr int WRB = 9 * 64;             // weight row bytes: 9 taps x 32 channels (576 = 64 mod 256)
+  constexpr int NWC = BC / WC, NWP = BP / WP;
+  static_assert(NWC * NWP == 4, "4 waves");
+  constexpr int TP = WP / 16, TC = WC / 16;
+  constexpr int PCH = PROWS * 4, WCH = BC * 36, CH = PCH + WCH;   // 16-B chunks per slice
+  constexpr int L = (CH + 255) / 256;
+  __shared__ __attribute__((aligned(16))) char lds[PBYTES + BC * WRB];
+  char* const Pimg = lds;
+  char* const Wimg = lds + PBYTES;
+
+  const int tilesPerRow = a.Wo / BP;
+  const int npt = a.N * a.Ho * tilesPerRow;
+  const int nct = a.Ngemm / BC;
+  const int bid = xcd_remap(blockIdx.x, npt * nct);
+  const int pt = bid / nct, ct = bid - pt * nct;
+  const int c0 = ct * BC;
+  const int rowid = pt / tilesPerRow;               // n * Ho + h (uniform)
+  const int w0 = (pt - rowid * tilesPerRow) * BP;
+  const int n = rowid / a.Ho, h = rowid - n * a.Ho;
+  const long m0 = (long)rowid * a.Wo + w0;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wp = wid / NWC, wc = wid - wp * NWC;
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, 0, (int)a.xbytes, 0x00020000);
+
+  f32x4_t acc[TC][TP];
+#pragma unroll
+  for (int ic = 0; ic < TC; ++ic)
+#pragma unroll
+    for (int ip = 0; ip < TP; ++ip) acc[ic][ip] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  const int S = a.Cs / 32;
+  for (int s = 0; s < S; ++s) {
+    // ---- stage slice s: halo pixels (zero padded by the buffer range check) + weights
+    u32x4_t reg[L];
+#pragma unroll
+    for (int j = 0; j < L; ++j) {
+      const int c = tid + j * 256;
+      if (c < PCH) {
+        const int row = c >> 2, cc = c & 3;
+        const int kh = row / HR, col = row - kh * HR;
+        const int ih = h + kh - 1, iw = w0 + col - 1;
+        const bool ok = ih >= 0 && ih < a.Hs && iw >= 0 && iw < a.Ws;
+        const unsigned off = ok ? (unsigned)((((n * a.Hs + ih) * a.Ws + iw) * a.ldx + s * 32 + cc * 8) * 2) : 0x80000000u;
+        reg[j] = __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0);
+      } else if (c < CH) {
+        const int cw = c - PCH, r = cw / 36, k = cw - r * 36;     // k = tap*4 + chunk
+        const int tap = k >> 2, cc = k & 3;
+        reg[j] = *reinterpret_cast<const u32x4_t*>(a.w + (long)(c0 + r) * a.Kpad + tap * a.Cs + s * 32 + cc * 8);
+      }
+    }
+    if (s > 0) __syncthreads();          // previous slice fully consumed
+#pragma unroll
+    for (int j = 0; j < L; ++j) {
+      const int c = tid + j * 256;
+      if (c < PCH) {
+        const int row = c >> 2, cc = c & 3;
+        *reinterpret_cast<u32x4_t*>(Pimg + row * 64 + (swz_nk<32>(row, cc) << 4)) = reg[j];
+      } else if (c < CH) {
+        const int cw = c - PCH, r = cw / 36, k = cw - r * 36;
+        const int tap = k >> 2, cc = k & 3;
+        *reinterpret_cast<u32x4_t*>(Wimg + r * WRB + tap * 64 + (swz_nk<32>(r, cc) << 4)) = reg[j];
+      }
+    }
+    __syncthreads();
+    // ---- 9 taps x (TC x TP) MFMAs from LDS
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      const int kh = tap / 3, kw = tap - kh * 3;
+      const int chunk = lane >> 4;
+      bf16x8_t af[TC], bfr[TP];
+#pragma unroll
+      for (int ic = 0; ic < TC; ++ic) {
+        const int r = wc * WC + ic * 16 + (lane & 15);
+        af[ic] = *reinterpret_cast<const bf16x8_t*>(Wimg + r * WRB + tap * 64 + (swz_nk<32>(r, chunk) << 4));
+      }
+#pragma unroll
+      for (int ip = 0; ip < TP; ++ip) {
+        const int r = kh * HR + wp * WP + ip * 16 + (lane & 15) + kw;
+        bfr[ip] = *reinterpret_cast<const bf16x8_t*>(Pimg + r * 64 + (swz_nk<32>(r, chunk) << 4));
+      }
+#pragma unroll
+      for (int ic = 0; ic < TC; ++ic)
+#pragma unroll
+        for (int ip = 0; ip < TP; ++ip)
+          acc[ic][ip] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ic], bfr[ip], acc[ic][ip], 0, 0, 0);
+    }
+  }
+
+  // ---- epilogue (mode 0): bias, ReLU, ReLU-backward mask, accumulate; 8-byte bf16 stores
+#pragma unroll
+  for (int ip = 0; ip < TP; ++ip) {
+    const long m = m0 + wp * WP + ip * 16 + (lane & 15);
+#pragma unroll
+    for (int ic = 0; ic < TC; ++ic) {
+      const int co = c0 + wc * WC + ic * 16 + 4 * (lane >> 4);
+      float v0 = acc[ic][ip][0], v1 = acc[ic][ip][1], v2 = acc[ic][ip][2], v3 = acc[ic][ip][3];
+      if (a.bias) {
+        const float* b = a.bias + co;
+        v0 += b[0]; v1 += b[1]; v2 += b[2]; v3 += b[3];
+      }
+      if (a.relu) {
+        v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f);
+      }
+      if (a.mask && co < a.mask_ch) {
+        const uint2 mk = *reinterpret_cast<const uint2*>(a.mask + m * a.ldm + co);
+        v0 = lo_bf(mk.x) > 0.f ? v0 : 0.f;
+        v1 = hi_bf(mk.x) > 0.f ? v1 : 0.f;
+        v2 = lo_bf(mk.y) > 0.f ? v2 : 0.f;
+        v3 = hi_bf(mk.y) > 0.f ? v3 : 0.f;
+      }
+      uint2* dst = reinterpret_cast<uint2*>(a.y + m * a.ldy + co);
+      if (a.accumulate) {
+        const uint2 o = *dst;
+        v0 += lo_bf(o.x); v1 += hi_bf(o.x); v2 += lo_bf(o.y); v3 += hi_bf(o.y);
+      }
+      *dst = make_uint2(pack_bf2(v0, v1), pack_bf2(v2, v3));
+    }
+  }
+}
+
+template <int BP, int BC, int WP, int WC>
+static int launch_igemm_halo(const IgemmArgs& a, hipStream_t st) {
+  const int grid = a.N * a.Ho * (a.Wo / BP) * (a.Ngemm / BC);
+  hipLaunchKernelGGL((igemm_halo_kernel<BP, BC, WP, WC>), dim3(grid), dim3(256), 0, st, a);
+  return (int)hipGetLastError();
+}
+
+// Returns hipErrorInvalidValue (nothing launched) when the shape is not eligible; the caller then
+// uses dpa_igemm.  cfg: 0 auto, 1: 256x32, 2: 128x64, 3: 128x32
+DPA_API int dpa_igemm_halo(const IgemmArgs* args, int cfg, hipStream_t st) {
+  const IgemmArgs& a = *args;
+  if (a.mode != 0 || a.KH != 3 || a.KW != 3 || a.stride != 1 || a.pad != 1 || (a.Cs % 32) || (a.ldx & 7) ||
+      (a.ldy & 3) || a.Hs != a.Ho || a.Ws != a.Wo || a.Kpad < 9 * a.Cs)
+    return (int)hipErrorInvalidValue;
+  if (cfg == 0) {
+    if (a.Ngemm == 32 && a.Wo % 256 == 0) cfg = 1;
+    else if (a.Ngemm % 64 == 0 && a.Ngemm <= 128 && a.Wo % 128 == 0) cfg = 2;
+    else if (a.Ngemm % 32 == 0 && a.Ngemm <= 64 && a.Wo % 128 == 0) cfg = 3;
+    else return (int)hipErrorInvalidValue;
+  }
+  switch (cfg) {
+    case 1: if (a.Wo % 256 || a.Ngemm % 32) break; return launch_igemm_halo<256, 32, 64, 32>(a, st);
+    case 2: if (a.Wo % 128 || a.Ngemm % 64) break; return launch_igemm_halo<128, 64, 64, 32>(a, st);
+    case 3: if (a.Wo % 128 || a.Ngemm % 32) break; return launch_igemm_halo<128, 32, 32, 32>(a, st);
+    default: break;
+  }
+  return (int)hipErrorInvalidValue;
+}
+
+// ------------------------------------------------------------------------------------ wgrad_halo
+// conv3x3 weight gradient, pixel chunks of 32 inside one row.  out[tap][m][n] as in wgrad.hip.
+template <int BM, int BN, int WM, int WN>
+__global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void wgrad_halo_kernel(WgradArgs a) {
+  constexpr int NWN = BN / WN, NW = (BM / WM) * NWN, NT = 64 * NW;
+  constexpr int CPRA = BM / 8, CPRB = BN / 8, RBA = BM * 2, RBB = BN * 2;
+  constexpr int BR = 34;                                   // B rows per kh image
+  constexpr int IMGA = 32 * RBA, IMGB = BR * RBB;
+  constexpr int CHA = 32 * CPRA, CH = CHA + 3 * BR * CPRB;
+  constexpr int L = (CH + NT - 1) / NT;
+  constexpr int TM = WM / 16, TN = WN / 16;
+  __shared__ __attribute__((aligned(16))) char lds[IMGA + 3 * IMGB];
+
+  const int nmt = a.M / BM;
+  const int nnt = (a.Nc + BN - 1) / BN;
+  const int tiles = nmt * nnt;
+  const int bid = xcd_remap(blockIdx.x, tiles * a.splits);
+  const int split = bid / tiles, tile = bid - split * tiles;
+  const int mt = tile / nnt, nt = tile - mt * nnt;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const long P = (long)a.N * a.Hg * a.Wg;
+  const long pbeg = (long)split * a.pix_per_split;
+  long pend = pbeg + a.pix_per_split;
+  if (pend > P) pend = P;
+  const int nst = (int)((pend - pbeg) / 32);            // P % 32 == 0 (host check)
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / NWN, wn = wid - wm * NWN;
+  const bool do_bias = a.bslab != nullptr && nt == 0;
+  const __amdgpu_buffer_rsrc_t ar = __builtin_amdgcn_make_buffer_rsrc((void*)a.A, 0, (int)a.abytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t br = __builtin_amdgcn_make_buffer_rsrc((void*)a.B, 0, (int)a.bbytes, 0x00020000);
+
+  u32x4_t reg[L];
+  auto gload = [&](int st) {
+    const int p0 = (int)(pbeg + (long)st * 32);           // 32 pixels of one row
+    const int hw = a.Hg * a.Wg;
+    const int n = p0 / hw, rem = p0 - n * hw, h = rem / a.Wg, w0 = rem - h * a.Wg;
+#pragma unroll
+    for (int j = 0; j < L; ++j) {
+      const int c = tid + j * NT;
+      if (c < CH) {
+        if (c < CHA) {
+          const int r = c / CPRA, cc = c - r * CPRA;
+          const int ch = m0 + cc * 8;
+          const bool ok = ch < a.M;
+          const unsigned off = ok ? (unsigned)((((n * a.HA + h) * a.WA + w0 + r) * a.lda + ch) * 2) : 0x80000000u;
+          reg[j] = __builtin_amdgcn_raw_buffer_load_b128(ar, off, 0, 0);
+        } else {
+          const int cl = c - CHA, img = cl / (BR * CPRB), rr = cl - img * (BR * CPRB);
+          const int r = rr / CPRB, cc = rr - r * CPRB;
+          const int ih = h + img - 1, iw = w0 + r - 1, ch = n0 + cc * 8;
+          const bool ok = ih >= 0 && ih < a.HB && iw >= 0 && iw < a.WB && ch < a.Nc;
+          const unsigned off = ok ? (unsigned)((((n * a.HB + ih) * a.WB + iw) * a.ldb + ch) * 2) : 0x80000000u;
+          reg[j] = __builtin_amdgcn_raw_buffer_load_b128(br, off, 0, 0);
+        }
+      }
+    }
+  };
+  auto lstore = [&]() {
+#pragma unroll
+    for (int j = 0; j < L; ++j) {
+      const int c = tid + j * NT;
+      if (c < CH) {
+        if (c < CHA) {
+          const int r = c / CPRA, cc = c - r * CPRA;
+          *reinterpret_cast<u32x4_t*>(lds + r * RBA + ((cc ^ swz_kk<RBA>(r)) << 4)) = reg[j];
+        } else {
+          const int cl = c - CHA, img = cl / (BR * CPRB), rr = cl - img * (BR * CPRB);
+          const int r = rr / CPRB, cc = rr - r * CPRB;
+          *reinterpret_cast<u32x4_t*>(lds + IMGA + img * IMGB + r * RBB + ((cc ^ swz_kk<RBB>(r)) << 4)) = reg[j];
+        }
+      }
+    }
+  };
+
+  f32x4_t acc[9][TM][TN];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[t][i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  float bsum = 0.f;
+
+  if (nst > 0) {
+    gload(0);
+    lstore();
+  }
+  __syncthreads();
+  for (int st = 0; st < nst; ++st) {
+    if (st + 1 < nst) gload(st + 1);
+    __builtin_amdgcn_sched_barrier(0);
+    bf16x8_t af[TM];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) af[i] = tr_frag<RBA>(lds, wm * WM + i * 16, lane);
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int kh = t / 3, kw = t - kh * 3;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const bf16x8_t bf = tr_frag<RBB>(lds + IMGA + kh * IMGB, wn * WN + j * 16, lane, kw);
+#pragma unroll
+        for (int i = 0; i < TM; ++i) acc[t][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf, acc[t][i][j], 0, 0, 0);
+      }
+    }
+    if (do_bias && tid < BM) {
+      const int ch = tid >> 3, e = tid & 7;
+      for (int r = 0; r < 32; ++r)
+        bsum += bf2f(*reinterpret_cast<const bf16_t*>(lds + r * RBA + ((ch ^ swz_kk<RBA>(r)) << 4) + e * 2));
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    __syncthreads();
+    if (st + 1 < nst) {
+      lstore();
+      __syncthreads();
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int nn = n0 + wn * WN + j * 16 + (lane & 15);
+        if (nn >= a.Nc) continue;
+        const int mb = m0 + wm * WM + i * 16 + 4 * (lane >> 4);
+        float* dst = a.slab + (((long)split * 9 + t) * a.M + mb) * a.Nc + nn;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) dst[(long)r * a.Nc] = acc[t][i][j][r];
+      }
+  if (do_bias && tid < BM) a.bslab[(long)split * a.M + m0 + tid] = bsum;
+}
+
+template <int BM, int BN, int WM, int WN>
+static int launch_wgrad_halo(const WgradArgs& a, hipStream_t st) {
+  const int tiles = (a.M / BM) * ((a.Nc + BN - 1) / BN);
+  constexpr int NT = 64 * (BM / WM) * (BN / WN);
+  hipLaunchKernelGGL((wgrad_halo_kernel<BM, BN, WM, WN>), dim3(tiles * a.splits), dim3(NT), 0, st, a);
+  return (int)hipGetLastError();
+}
+
+// cfg: 1: 32x32 (4 waves of 16x16)  2: 64x32  3: 32x64  4: 64x64;  0 = auto
+DPA_API int dpa_wgrad_halo(const WgradArgs* args, int cfg, hipStream_t st) {
+  const WgradArgs& a = *args;
+  if ((a.M & 31) || (a.lda & 7) || (a.ldb & 7) || (a.pix_per_split & 31) || (a.Wg & 31) || a.splits < 1 || a.s != 1 ||
+      a.pad != 1 || a.KW != 3 || a.HA != a.Hg || a.WA != a.Wg || a.HB != a.Hg || a.WB != a.Wg || (a.Nc & 31))
+    return (int)hipErrorInvalidValue;
+  if (cfg == 0) cfg = (a.M % 64 == 0) ? (a.Nc % 64 == 0 ? 4 : 2) : (a.Nc % 64 == 0 ? 3 : 1);
+  switch (cfg) {
+    case 1: return launch_wgrad_halo<32, 32, 16, 16>(a, st);
+    case 2: if (a.M % 64) break; return launch_wgrad_halo<64, 32, 32, 16>(a, st);
+    case 3: return launch_wgrad_halo<32, 64, 16, 32>(a, st);
+    case 4: if (a.M % 64) break; return launch_wgrad_halo<64, 64, 32, 32>(a, st);
+    default: break;
+  }
+  return (int)hipErrorInvalidValue;
+}

@@ -18,27 +18,7 @@
 // Block -> tile mapping is XCD-aware (channel tiles of one pixel tile share an XCD's L2).
 #include "common.h"
 
-struct IgemmArgs {
-  const bf16_t* x;      // source activations [N][Hs][Ws][ldx] (channel offset folded into the pointer)
-  const bf16_t* w;      // packed weights [Ngemm][Kpad] bf16
-  const float* bias;    // [Cout] fp32 or null
-  bf16_t* y;            // output (channel offset folded into the pointer)
-  const bf16_t* mask;   // ReLU-backward mask source (same pixel grid as y, mode 0) or null
-  int ldx, ldy, ldm, mask_ch;
-  int N, Ho, Wo;        // GEMM-M pixel grid
-  int Hs, Ws, Cs;       // source grid and channels gathered per tap (Cs % 8 == 0)
-  int KH, KW, stride, pad;
-  int Ngemm, Kpad;      // GEMM N, K padded to a multiple of BK (packed weights zero-filled)
-  int mode;             // 0: y[m][n]   1: transposed-conv 2x2/s2 scatter, n = (2i+j)*Cout + co
-  int relu, accumulate, Cout;
-  unsigned xbytes;      // bytes addressable from x (< 2^31; the host splits larger batches by image)
-};
-
-template <int BK>
-__device__ __forceinline__ int swz_nk(int row, int chunk) {
-  if constexpr (BK == 32) return chunk ^ ((row >> 1) & 3);
-  else return chunk ^ (row & 7);
-}
+#include "conv_args.h"
 
 template <int BP, int BC, int BK, int WP, int WC>
 __global__ __launch_bounds__(256) void igemm_kernel(IgemmArgs a) {

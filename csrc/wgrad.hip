@@ -18,44 +18,9 @@
 // the gfx950 transposed LDS read ds_read_b64_tr_b16, conflict-free for 64/128/256-byte rows.
 // The tap-independent operand is staged once per pixel chunk and reused by all taps (9 for conv).
 // Bias gradients (sum of A over pixels) come from the n-tile-0 blocks' LDS images.
-#include "common.h"
+#include "conv_args.h"
 
-struct WgradArgs {
-  const bf16_t* A; const bf16_t* B;
-  float* slab;          // [splits][T][M][Nc]
-  float* bslab;         // [splits][M] or null (bias gradient partials)
-  int lda, ldb;
-  int N, Hg, Wg;        // pixel grid p = (n, h, w)
-  int HA, WA, HB, WB;   // spatial dims of A and B tensors
-  int M, Nc;            // channels of A (GEMM rows) and B (GEMM cols, may be < tile width: zero filled)
-  int s, pad, KW;       // tap-dependent operand is read at (h*s + kh - pad, w*s + kw - pad)
-  int pix_per_split, splits;
-  unsigned abytes, bbytes;  // addressable bytes of A / B (< 2^31; the host splits larger batches)
-};
 
-template <int RB>
-__device__ __forceinline__ int swz_kk(int r) {
-  if constexpr (RB == 64) return ((r >> 3) & 1) * 2;
-  else if constexpr (RB == 128) return (((r >> 1) & 1) * 2) ^ (((r >> 3) & 1) * 4);
-  else if constexpr (RB == 256) return ((r & 1) * 2) ^ (((r >> 1) & 1) * 4) ^ (((r >> 3) & 1) * 8);
-  else return 0;
-}
-
-// 8 consecutive k (pixel rows 8g..8g+7 of a [32][RB] image) for the 16 columns starting at col0
-template <int RB>
-__device__ __forceinline__ bf16x8_t tr_frag(const char* img, int col0, int lane) {
-  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
-  const int col = col0 + 4 * p;
-  const int ch = col >> 3, hb = (col & 7) * 2;
-  const int r0 = 8 * g + q, r1 = r0 + 4;
-  const char* a0 = img + r0 * RB + ((ch ^ swz_kk<RB>(r0)) << 4) + hb;
-  const char* a1 = img + r1 * RB + ((ch ^ swz_kk<RB>(r1)) << 4) + hb;
-  s16x4_t v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4_t, a0));
-  s16x4_t v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4_t, a1));
-  typedef __attribute__((ext_vector_type(8))) short s16x8_t;
-  s16x8_t v = __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7);
-  return __builtin_bit_cast(bf16x8_t, v);
-}
 
 template <int BM, int BN, int WM, int WN, int T, bool TAPA>
 __global__ __launch_bounds__(64 * (BM / WM) * (BN / WN)) void wgrad_kernel(WgradArgs a) {

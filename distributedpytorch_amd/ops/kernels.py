@@ -12,6 +12,7 @@ segmap + sigmoid + BCE + Dice (K8-K11) -> ``head_fwd`` / ``head_bwd``;  Adam (K1
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import Optional
 
 import torch
@@ -68,6 +69,8 @@ def round_up(x: int, m: int) -> int:
 
 
 _MAX_BYTES = 2 ** 31 - 1024   # kernels address activations through 32-bit buffer offsets
+# row-halo kernels (csrc/halo.hip) for full-resolution low-channel convs; DPA_NO_HALO=1 disables
+USE_HALO = os.environ.get("DPA_NO_HALO", "0") != "1"
 
 
 def _extent_bytes(N, H, W, C, ld):
@@ -113,6 +116,9 @@ def igemm(x: torch.Tensor, wpacked: torch.Tensor, y: torch.Tensor, *, Ngemm: int
                       None if mask is None else mask[n0:n1].data_ptr(), ldx, ldy, ldm, mch, nb, Ho, Wo, Hs, Ws, Cs,
                       KH, KW, stride, pad, Ngemm, Kpad, mode, int(relu), int(accumulate), Cout,
                       _extent_bytes(nb, Hs, Ws, Cx, ldx))
+        if USE_HALO and mode == 0 and KH == 3 and stride == 1 and Cs % 32 == 0 and Ngemm <= 128 and cfg == 0:
+            if L.dpa_igemm_halo(ctypes.byref(a), c_int(0), st) == 0:
+                continue
         _check(L.dpa_igemm(ctypes.byref(a), c_int(cfg), st), "igemm")
 
 
@@ -136,12 +142,17 @@ def wgrad(A: torch.Tensor, B: torch.Tensor, *, kind: int, grid, M: int, Nc: int,
         assert (HA, WA) == (Hg, Wg) and (HB, WB) == (Hg, Wg)
     else:
         assert (HA, WA) == (2 * Hg, 2 * Wg) and (HB, WB) == (Hg, Wg)
-    if cfg == 0:
-        if kind == 0:
-            cfg = 1 if Nc <= 16 else (3 if M % 64 == 0 else 2)
-        else:
-            cfg = 12 if (M % 64 == 0 and Nc >= 64) else 11
-    bm, bn = {1: (32, 16), 2: (32, 32), 3: (64, 32), 4: (64, 64), 11: (32, 32), 12: (64, 64)}[cfg]
+    halo = (USE_HALO and kind == 0 and cfg == 0 and Wg % 32 == 0 and Nc % 32 == 0 and M % 32 == 0)
+    if halo:
+        hcfg = 2 if M % 64 == 0 else (3 if Nc % 64 == 0 else 1)
+        bm, bn = {1: (32, 32), 2: (64, 32), 3: (32, 64), 4: (64, 64)}[hcfg]
+    else:
+        if cfg == 0:
+            if kind == 0:
+                cfg = 1 if Nc <= 16 else (3 if M % 64 == 0 else 2)
+            else:
+                cfg = 12 if (M % 64 == 0 and Nc >= 64) else 11
+        bm, bn = {1: (32, 16), 2: (32, 32), 3: (64, 32), 4: (64, 64), 11: (32, 32), 12: (64, 64)}[cfg]
     tiles = (M // bm) * (-(-Nc // bn))
     assert gw.dtype == torch.float32 and gw.is_contiguous() and gw.numel() == M * Nreal * T
     L = _lib.lib()
@@ -155,7 +166,10 @@ def wgrad(A: torch.Tensor, B: torch.Tensor, *, kind: int, grid, M: int, Nc: int,
         a = WgradArgs(A[n0:n1].data_ptr(), B[n0:n1].data_ptr(), slab.data_ptr(),
                       None if bslab is None else bslab.data_ptr(), lda, ldb, nb, Hg, Wg, HA, WA, HB, WB, M, Nc, s,
                       pad, KW, pps, splits, _extent_bytes(nb, HA, WA, CA, lda), _extent_bytes(nb, HB, WB, CB, ldb))
-        _check(L.dpa_wgrad(ctypes.byref(a), c_int(kind), c_int(cfg), st), "wgrad")
+        if halo:
+            _check(L.dpa_wgrad_halo(ctypes.byref(a), c_int(hcfg), st), "wgrad_halo")
+        else:
+            _check(L.dpa_wgrad(ctypes.byref(a), c_int(kind), c_int(cfg), st), "wgrad")
         _check(L.dpa_wgrad_reduce(_p(slab), _p(bslab), _p(gw), _p(gb), c_int(splits), c_int(T), c_int(M), c_int(Nc),
                                   c_int(Nreal), c_int(kind), st), "wgrad_reduce")
 

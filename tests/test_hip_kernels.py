@@ -65,6 +65,11 @@ def _pack_one(mode, w, cin_pad=None):
     (1, 16, 16, 64, 128, 2),
     (1, 16, 16, 64, 64, 3),
     (1, 16, 16, 64, 64, 4),
+    # row-halo kernels (W a multiple of the 256/128-pixel tile)
+    (2, 3, 256, 32, 32, 0),
+    (1, 4, 256, 64, 32, 0),
+    (1, 3, 128, 32, 64, 0),
+    (2, 2, 128, 64, 128, 0),
 ])
 def test_conv3x3_fwd(hip_lib, N, H, W, Cin, Cout, cfg):
     from distributedpytorch_amd.ops import kernels as K
@@ -84,7 +89,8 @@ def test_conv3x3_fwd(hip_lib, N, H, W, Cin, Cout, cfg):
     assert _rel(_nchw(y), ref) < 2e-2
 
 
-@pytest.mark.parametrize("N,H,W,Cin,Cout", [(2, 13, 18, 32, 64), (1, 8, 8, 256, 128), (2, 16, 16, 64, 32)])
+@pytest.mark.parametrize("N,H,W,Cin,Cout", [(2, 13, 18, 32, 64), (1, 8, 8, 256, 128), (2, 16, 16, 64, 32),
+                                            (2, 3, 256, 32, 32), (1, 3, 256, 64, 32), (1, 2, 128, 32, 64)])
 def test_conv3x3_dgrad_masked(hip_lib, N, H, W, Cin, Cout):
     from distributedpytorch_amd.ops import kernels as K
     torch.manual_seed(1)
@@ -140,7 +146,10 @@ def test_deconv_dgrad_from_concat(hip_lib, N, h, w, Cin, Cout):
 
 
 @pytest.mark.parametrize("N,H,W,Cin,Cout,cin_pad", [
-    (2, 19, 21, 3, 32, 8), (2, 16, 16, 32, 32, None), (1, 12, 16, 64, 128, None), (2, 8, 8, 128, 64, None)])
+    (2, 19, 21, 3, 32, 8), (2, 16, 16, 32, 32, None), (1, 12, 16, 64, 128, None), (2, 8, 8, 128, 64, None),
+    # row-halo wgrad (W % 32 == 0)
+    (2, 5, 32, 32, 32, None), (1, 4, 64, 64, 32, None), (2, 3, 32, 32, 64, None), (1, 4, 32, 128, 64, None),
+    (2, 4, 32, 3, 32, 8)])
 def test_conv3x3_wgrad(hip_lib, N, H, W, Cin, Cout, cin_pad):
     from distributedpytorch_amd.ops import kernels as K
     torch.manual_seed(4)
