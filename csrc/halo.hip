@@ -327,3 +327,177 @@ DPA_API int dpa_wgrad_halo(const WgradArgs* args, int cfg, hipStream_t st) {
   }
   return (int)hipErrorInvalidValue;
 }
+
+// ------------------------------------------------------------------------------------ igemm_stream
+// Row-streaming conv3x3 (s1 p1) for Ngemm, Cs in {32, 64}: one block owns an image column strip
+// [w0, w0+BP) x rows [h0, h0+RH) and ALL output channels.  The packed weights stay resident in LDS
+// for the block's lifetime; input rows stream through a 4-slot LDS ring (3 rows in use + 1 being
+// prefetched), so every input pixel is read from HBM ~once ((RH+2)/RH x (BP+2)/BP) and every
+// output pixel written once: the layer runs at streaming bandwidth instead of gathering each
+// pixel 9 times through L2.
+// LDS images are [.. ][rows][32 channels] 64-B-row nk images (swz_nk<32>, conflict-free).
+template <int BP, int NG, int CS, int RH>
+__global__ __launch_bounds__(256) void igemm_stream_kernel(IgemmArgs a) {
+  constexpr int HR = BP + 2;                  // pixels per staged input row
+  constexpr int KS = CS / 32;                 // 32-channel slices
+  constexpr int WBYTES = 9 * KS * NG * 64;    // [tap][ks][NG][32]
+  constexpr int SLOT = KS * HR * 64;          // one input row: [ks][HR][32]
+  constexpr int WP = BP / 4, TP = WP / 16, TC = NG / 16;
+  constexpr int RCH = KS * HR * 4;            // 16-B chunks per input row
+  constexpr int LR = (RCH + 255) / 256;
+  __shared__ __attribute__((aligned(16))) char lds[WBYTES + 4 * SLOT];
+  char* const Wimg = lds;
+  char* const Ring = lds + WBYTES;
+
+  const int stripsW = a.Wo / BP;
+  const int segsH = (a.Ho + RH - 1) / RH;
+  const int bid = blockIdx.x;                               // streaming: no L2 reuse to chase
+  const int n = bid / (segsH * stripsW);
+  const int rem = bid - n * segsH * stripsW;
+  const int hs = rem / stripsW;
+  const int w0 = (rem - hs * stripsW) * BP;
+  const int h0 = hs * RH;
+  const int tid = threadIdx.x, lane = tid & 63, wp = tid >> 6;
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, 0, (int)a.xbytes, 0x00020000);
+
+  // resident weights: packed [NG][Kpad] with k = tap*CS + ci
+  for (int c = tid; c < 9 * KS * NG * 4; c += 256) {
+    const int cc = c & 3, row = (c >> 2) % NG, tk = (c >> 2) / NG;       // tk = tap*KS + ks
+    const int tap = tk / KS, ks = tk - tap * KS;
+    const u32x4_t v = *reinterpret_cast<const u32x4_t*>(a.w + (long)row * a.Kpad + tap * CS + ks * 32 + cc * 8);
+    *reinterpret_cast<u32x4_t*>(Wimg + (tk * NG + row) * 64 + (swz_nk<32>(row, cc) << 4)) = v;
+  }
+  u32x4_t reg[LR];
+  auto rload = [&](int ih) {
+#pragma unroll
+    for (int j = 0; j < LR; ++j) {
+      const int c = tid + j * 256;
+      if (c < RCH) {
+        const int cc = c & 3, px = (c >> 2) % HR, ks = (c >> 2) / HR;
+        const int iw = w0 + px - 1;
+        const bool ok = ih >= 0 && ih < a.Hs && iw >= 0 && iw < a.Ws;
+        const unsigned off = ok ? (unsigned)((((n * a.Hs + ih) * a.Ws + iw) * a.ldx + ks * 32 + cc * 8) * 2) : 0x80000000u;
+        reg[j] = __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0);
+      }
+    }
+  };
+  auto rstore = [&](int slot) {
+#pragma unroll
+    for (int j = 0; j < LR; ++j) {
+      const int c = tid + j * 256;
+      if (c < RCH) {
+        const int cc = c & 3, px = (c >> 2) % HR, ks = (c >> 2) / HR;
+        *reinterpret_cast<u32x4_t*>(Ring + slot * SLOT + (ks * HR + px) * 64 + (swz_nk<32>(px, cc) << 4)) = reg[j];
+      }
+    }
+  };
+  // prologue: input rows h0-1, h0, h0+1 -> slots 0, 1, 2
+#pragma unroll 1
+  for (int j = 0; j < 3; ++j) {
+    rload(h0 - 1 + j);
+    rstore(j);
+  }
+  __syncthreads();
+
+  const int nrows = min(RH, a.Ho - h0);
+#pragma unroll 1
+  for (int r = 0; r < nrows; ++r) {
+    if (r + 1 < nrows) rload(h0 + r + 2);                  // prefetch into registers
+    __builtin_amdgcn_sched_barrier(0);
+    f32x4_t acc[TC][TP];
+#pragma unroll
+    for (int ic = 0; ic < TC; ++ic)
+#pragma unroll
+      for (int ip = 0; ip < TP; ++ip) acc[ic][ip] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh) {
+      const char* S = Ring + ((r + kh) & 3) * SLOT;
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          const int tk = (kh * 3 + kw) * KS + ks;
+          const int chunk = lane >> 4;
+          bf16x8_t af[TC], bfr[TP];
+#pragma unroll
+          for (int ic = 0; ic < TC; ++ic) {
+            const int row = ic * 16 + (lane & 15);
+            af[ic] = *reinterpret_cast<const bf16x8_t*>(Wimg + (tk * NG + row) * 64 + (swz_nk<32>(row, chunk) << 4));
+          }
+#pragma unroll
+          for (int ip = 0; ip < TP; ++ip) {
+            const int px = wp * WP + ip * 16 + (lane & 15) + kw;
+            bfr[ip] = *reinterpret_cast<const bf16x8_t*>(S + (ks * HR + px) * 64 + (swz_nk<32>(px, chunk) << 4));
+          }
+#pragma unroll
+          for (int ic = 0; ic < TC; ++ic)
+#pragma unroll
+            for (int ip = 0; ip < TP; ++ip)
+              acc[ic][ip] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ic], bfr[ip], acc[ic][ip], 0, 0, 0);
+        }
+      }
+    }
+    // epilogue for output row h0 + r
+    const long mrow = ((long)n * a.Ho + h0 + r) * a.Wo + w0;
+#pragma unroll
+    for (int ip = 0; ip < TP; ++ip) {
+      const long m = mrow + wp * WP + ip * 16 + (lane & 15);
+#pragma unroll
+      for (int ic = 0; ic < TC; ++ic) {
+        const int co = ic * 16 + 4 * (lane >> 4);
+        float v0 = acc[ic][ip][0], v1 = acc[ic][ip][1], v2 = acc[ic][ip][2], v3 = acc[ic][ip][3];
+        if (a.bias) {
+          const float* b = a.bias + co;
+          v0 += b[0]; v1 += b[1]; v2 += b[2]; v3 += b[3];
+        }
+        if (a.relu) {
+          v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f);
+        }
+        if (a.mask && co < a.mask_ch) {
+          const uint2 mk = *reinterpret_cast<const uint2*>(a.mask + m * a.ldm + co);
+          v0 = lo_bf(mk.x) > 0.f ? v0 : 0.f;
+          v1 = hi_bf(mk.x) > 0.f ? v1 : 0.f;
+          v2 = lo_bf(mk.y) > 0.f ? v2 : 0.f;
+          v3 = hi_bf(mk.y) > 0.f ? v3 : 0.f;
+        }
+        uint2* dst = reinterpret_cast<uint2*>(a.y + m * a.ldy + co);
+        if (a.accumulate) {
+          const uint2 o = *dst;
+          v0 += lo_bf(o.x); v1 += hi_bf(o.x); v2 += lo_bf(o.y); v3 += hi_bf(o.y);
+        }
+        *dst = make_uint2(pack_bf2(v0, v1), pack_bf2(v2, v3));
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if (r + 1 < nrows) rstore((r + 3) & 3);
+    __syncthreads();
+  }
+}
+
+template <int BP, int NG, int CS, int RH>
+static int launch_igemm_stream(const IgemmArgs& a, hipStream_t st) {
+  const int grid = a.N * ((a.Ho + RH - 1) / RH) * (a.Wo / BP);
+  hipLaunchKernelGGL((igemm_stream_kernel<BP, NG, CS, RH>), dim3(grid), dim3(256), 0, st, a);
+  return (int)hipGetLastError();
+}
+
+// Eligible: conv3x3 s1 p1 mode 0, Ngemm and Cs in {32, 64}, Wo % 128 == 0, Ho >= 1.
+DPA_API int dpa_igemm_stream(const IgemmArgs* args, int rh, hipStream_t st) {
+  const IgemmArgs& a = *args;
+  if (a.mode != 0 || a.KH != 3 || a.KW != 3 || a.stride != 1 || a.pad != 1 || (a.ldx & 7) || (a.ldy & 3) ||
+      a.Hs != a.Ho || a.Ws != a.Wo || a.Wo % 128 || a.Kpad < 9 * a.Cs)
+    return (int)hipErrorInvalidValue;
+  const long blocks32 = (long)a.N * ((a.Ho + 31) / 32) * (a.Wo / 128);
+  if (rh == 0) rh = blocks32 >= 1024 ? 32 : 16;
+#define DPA_STREAM(NGv, CSv)                                                                     \
+  if (a.Ngemm == NGv && a.Cs == CSv) {                                                          \
+    if (rh == 32) return launch_igemm_stream<128, NGv, CSv, 32>(a, st);                         \
+    if (rh == 16) return launch_igemm_stream<128, NGv, CSv, 16>(a, st);                         \
+  }
+  DPA_STREAM(32, 32)
+  DPA_STREAM(32, 64)
+  DPA_STREAM(64, 32)
+  DPA_STREAM(64, 64)
+#undef DPA_STREAM
+  return (int)hipErrorInvalidValue;
+}

@@ -71,6 +71,8 @@ def round_up(x: int, m: int) -> int:
 _MAX_BYTES = 2 ** 31 - 1024   # kernels address activations through 32-bit buffer offsets
 # row-halo kernels (csrc/halo.hip) for full-resolution low-channel convs; DPA_NO_HALO=1 disables
 USE_HALO = os.environ.get("DPA_NO_HALO", "0") != "1"
+# row-streaming conv3x3 (weights resident, 4-row LDS ring); DPA_NO_STREAM=1 disables
+USE_STREAM = os.environ.get("DPA_NO_STREAM", "0") != "1"
 
 
 def _extent_bytes(N, H, W, C, ld):
@@ -86,8 +88,13 @@ def _image_chunks(N: int, per_image_bytes: int):
 # ------------------------------------------------------------------------------------------ igemm
 def igemm(x: torch.Tensor, wpacked: torch.Tensor, y: torch.Tensor, *, Ngemm: int, Kpad: int, KH: int, KW: int,
           stride: int, pad: int, Cs: int, out_grid, bias: Optional[torch.Tensor] = None, relu: bool = False,
-          mask: Optional[torch.Tensor] = None, mode: int = 0, Cout: int = 0, accumulate: bool = False, cfg: int = 0):
-    """Implicit-GEMM conv (see csrc/igemm.hip).  ``out_grid`` = (N, Ho, Wo) pixel grid of GEMM-M."""
+          mask: Optional[torch.Tensor] = None, mode: int = 0, Cout: int = 0, accumulate: bool = False, cfg: int = 0,
+          path: str = "auto"):
+    """Implicit-GEMM conv.  ``out_grid`` = (N, Ho, Wo) pixel grid of GEMM-M.
+
+    ``path``: ``auto`` picks, for a conv3x3, the row-streaming kernel (Ngemm, Cs in {32, 64}), then the
+    row-halo kernel (Cs % 32 == 0, Ngemm <= 128), then the generic gather kernel (csrc/igemm.hip);
+    ``stream`` / ``halo`` / ``generic`` force one (tests, A/B)."""
     N, Hs, Ws, Cx, ldx = _nhwc(x, "igemm.x")
     _, _, _, Cy, ldy = _nhwc(y, "igemm.y")
     No, Ho, Wo = out_grid
@@ -116,9 +123,19 @@ def igemm(x: torch.Tensor, wpacked: torch.Tensor, y: torch.Tensor, *, Ngemm: int
                       None if mask is None else mask[n0:n1].data_ptr(), ldx, ldy, ldm, mch, nb, Ho, Wo, Hs, Ws, Cs,
                       KH, KW, stride, pad, Ngemm, Kpad, mode, int(relu), int(accumulate), Cout,
                       _extent_bytes(nb, Hs, Ws, Cx, ldx))
-        if USE_HALO and mode == 0 and KH == 3 and stride == 1 and Cs % 32 == 0 and Ngemm <= 128 and cfg == 0:
-            if L.dpa_igemm_halo(ctypes.byref(a), c_int(0), st) == 0:
+        conv3 = mode == 0 and KH == 3 and stride == 1 and cfg == 0
+        if path == "stream" or (path == "auto" and USE_STREAM and conv3 and Ngemm in (32, 64) and Cs in (32, 64)):
+            err = L.dpa_igemm_stream(ctypes.byref(a), c_int(0), st)
+            if err == 0:
                 continue
+            if path == "stream":
+                _check(err, "igemm_stream")
+        if path == "halo" or (path == "auto" and USE_HALO and conv3 and Cs % 32 == 0 and Ngemm <= 128):
+            err = L.dpa_igemm_halo(ctypes.byref(a), c_int(0), st)
+            if err == 0:
+                continue
+            if path == "halo":
+                _check(err, "igemm_halo")
         _check(L.dpa_igemm(ctypes.byref(a), c_int(cfg), st), "igemm")
 
 

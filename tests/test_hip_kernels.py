@@ -65,11 +65,12 @@ def _pack_one(mode, w, cin_pad=None):
     (1, 16, 16, 64, 128, 2),
     (1, 16, 16, 64, 64, 3),
     (1, 16, 16, 64, 64, 4),
-    # row-halo kernels (W a multiple of the 256/128-pixel tile)
-    (2, 3, 256, 32, 32, 0),
-    (1, 4, 256, 64, 32, 0),
-    (1, 3, 128, 32, 64, 0),
-    (2, 2, 128, 64, 128, 0),
+    # row-streaming / row-halo kernels (W a multiple of the 128/256-pixel tile)
+    (2, 3, 256, 32, 32, "stream"), (2, 3, 256, 32, 32, "halo"),
+    (1, 37, 128, 64, 32, "stream"), (1, 4, 256, 64, 32, "halo"),
+    (1, 3, 128, 32, 64, "stream"), (1, 3, 128, 32, 64, "halo"),
+    (2, 20, 128, 64, 64, "stream"),
+    (2, 2, 128, 64, 128, "auto"),
 ])
 def test_conv3x3_fwd(hip_lib, N, H, W, Cin, Cout, cfg):
     from distributedpytorch_amd.ops import kernels as K
@@ -83,15 +84,19 @@ def test_conv3x3_fwd(hip_lib, N, H, W, Cin, Cout, cfg):
     xin[:, :Cin] = x
     packed, ng, kp = _pack_one(0, w, Cs)
     y = torch.empty(N, H, W, Cout, dtype=torch.bfloat16, device="cuda")
+    path = cfg if isinstance(cfg, str) else "auto"
+    cfg = cfg if isinstance(cfg, int) else 0
     K.igemm(_nhwc(xin), packed, y, Ngemm=ng, Kpad=kp, KH=3, KW=3, stride=1, pad=1, Cs=Cs, out_grid=(N, H, W),
-            bias=b.cuda(), relu=True, cfg=cfg)
+            bias=b.cuda(), relu=True, cfg=cfg, path=path)
     torch.cuda.synchronize()
     assert _rel(_nchw(y), ref) < 2e-2
 
 
-@pytest.mark.parametrize("N,H,W,Cin,Cout", [(2, 13, 18, 32, 64), (1, 8, 8, 256, 128), (2, 16, 16, 64, 32),
-                                            (2, 3, 256, 32, 32), (1, 3, 256, 64, 32), (1, 2, 128, 32, 64)])
-def test_conv3x3_dgrad_masked(hip_lib, N, H, W, Cin, Cout):
+@pytest.mark.parametrize("N,H,W,Cin,Cout,path", [
+    (2, 13, 18, 32, 64, "auto"), (1, 8, 8, 256, 128, "auto"), (2, 16, 16, 64, 32, "auto"),
+    (2, 3, 256, 32, 32, "stream"), (1, 3, 256, 64, 32, "halo"), (1, 2, 128, 32, 64, "stream"),
+    (1, 35, 128, 64, 64, "stream"), (2, 3, 256, 32, 32, "generic")])
+def test_conv3x3_dgrad_masked(hip_lib, N, H, W, Cin, Cout, path):
     from distributedpytorch_amd.ops import kernels as K
     torch.manual_seed(1)
     x = _bf(F.relu(torch.randn(N, Cin, H, W)))          # a ReLU output -> mask source
@@ -103,7 +108,7 @@ def test_conv3x3_dgrad_masked(hip_lib, N, H, W, Cin, Cout):
     packed, ng, kp = _pack_one(1, w)
     out = torch.empty(N, H, W, Cin, dtype=torch.bfloat16, device="cuda")
     K.igemm(_nhwc(g), packed, out, Ngemm=ng, Kpad=kp, KH=3, KW=3, stride=1, pad=1, Cs=Cout, out_grid=(N, H, W),
-            mask=_nhwc(x))
+            mask=_nhwc(x), path=path)
     torch.cuda.synchronize()
     assert _rel(_nchw(out), ref) < 2e-2
 
