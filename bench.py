@@ -53,10 +53,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != a.gpus and rank == 0:
         print(f"[bench] note: WORLD_SIZE={world} but --gpus={a.gpus}", file=sys.stderr)
+    # DPA_SAME_DEVICE=1 + DPA_DIST_BACKEND=gloo rehearse the multi-rank path on a one-GPU box
+    if os.environ.get("DPA_SAME_DEVICE", "0") == "1":
+        local = 0
     torch.cuda.set_device(local)
     device = torch.device(f"cuda:{local}")
     if world > 1:
-        dist.init_process_group("nccl", init_method="env://", device_id=device)
+        backend = os.environ.get("DPA_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", init_method="env://", device_id=device)
+        else:
+            dist.init_process_group(backend, init_method="env://")
 
     from distributedpytorch_amd.config import TrainConfig
     from distributedpytorch_amd.data.synthetic import synthetic_batch

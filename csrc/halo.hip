@@ -367,8 +367,7 @@ __global__ __launch_bounds__(256) void igemm_stream_kernel(IgemmArgs a) {
     const u32x4_t v = *reinterpret_cast<const u32x4_t*>(a.w + (long)row * a.Kpad + tap * CS + ks * 32 + cc * 8);
     *reinterpret_cast<u32x4_t*>(Wimg + (tk * NG + row) * 64 + (swz_nk<32>(row, cc) << 4)) = v;
   }
-  u32x4_t reg[LR];
-  auto rload = [&](int ih) {
+  auto rload = [&](u32x4_t (&reg)[LR], int ih) {
 #pragma unroll
     for (int j = 0; j < LR; ++j) {
       const int c = tid + j * 256;
@@ -381,7 +380,7 @@ __global__ __launch_bounds__(256) void igemm_stream_kernel(IgemmArgs a) {
       }
     }
   };
-  auto rstore = [&](int slot) {
+  auto rstore = [&](const u32x4_t (&reg)[LR], int slot) {
 #pragma unroll
     for (int j = 0; j < LR; ++j) {
       const int c = tid + j * 256;
@@ -391,18 +390,21 @@ __global__ __launch_bounds__(256) void igemm_stream_kernel(IgemmArgs a) {
       }
     }
   };
-  // prologue: input rows h0-1, h0, h0+1 -> slots 0, 1, 2
+  const int nrows = min(RH, a.Ho - h0);
+  // Input row j (image row h0-1+j) lives in ring slot j&3; output row r reads j = r, r+1, r+2.
+  // Loads run TWO rows ahead through two register sets (HBM latency ~ two row-computations):
+  // iteration r issues j = r+4 into set (r&1) and stores j = r+3 (issued at r-1) from set (r+1)&1.
+  u32x4_t regA[LR], regB[LR];
 #pragma unroll 1
   for (int j = 0; j < 3; ++j) {
-    rload(h0 - 1 + j);
-    rstore(j);
+    rload(regA, h0 - 1 + j);
+    rstore(regA, j);
   }
+  if (3 <= nrows + 1) rload(regB, h0 + 2);
   __syncthreads();
 
-  const int nrows = min(RH, a.Ho - h0);
-#pragma unroll 1
-  for (int r = 0; r < nrows; ++r) {
-    if (r + 1 < nrows) rload(h0 + r + 2);                  // prefetch into registers
+  auto row_step = [&](int r, u32x4_t (&issue)[LR], u32x4_t (&ready)[LR]) {
+    if (r + 4 <= nrows + 1) rload(issue, h0 - 1 + r + 4);
     __builtin_amdgcn_sched_barrier(0);
     f32x4_t acc[TC][TP];
 #pragma unroll
@@ -469,8 +471,13 @@ __global__ __launch_bounds__(256) void igemm_stream_kernel(IgemmArgs a) {
       }
     }
     __builtin_amdgcn_sched_barrier(0);
-    if (r + 1 < nrows) rstore((r + 3) & 3);
+    if (r + 3 <= nrows + 1) rstore(ready, (r + 3) & 3);
     __syncthreads();
+  };
+#pragma unroll 1
+  for (int r = 0; r < nrows; r += 2) {
+    row_step(r, regA, regB);
+    if (r + 1 < nrows) row_step(r + 1, regB, regA);
   }
 }
 

@@ -264,9 +264,13 @@ def build_strategy(cfg: TrainConfig, model) -> Strategy:
     m = cfg.train_method
     rank, local, world = dist_env()
     if m in ("DDP",) or (m == "MP" and world > 1):
+        # DPA_SAME_DEVICE=1 maps every rank to cuda:0 (rehearsal of the multi-rank path on one GPU;
+        # use with DPA_DIST_BACKEND=gloo, RCCL refuses two ranks on one device)
+        if os.environ.get("DPA_SAME_DEVICE", "0") == "1":
+            local = 0
         if not dist.is_initialized():
-            backend = "nccl" if torch.cuda.is_available() else "gloo"
-            if backend == "nccl":
+            backend = os.environ.get("DPA_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
+            if torch.cuda.is_available():
                 torch.cuda.set_device(local)   # A15: bind each rank to its own GPU
             dist.init_process_group(backend=backend, init_method="env://")
         device = torch.device(f"cuda:{local}") if torch.cuda.is_available() else torch.device("cpu")
