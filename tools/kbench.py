@@ -1,0 +1,83 @@
+#!/usr/bin/env python3
+"""Per-layer kernel micro-benchmark on one MI355X: times every conv path (stream / halo / generic,
+fwd + dgrad) and the weight-gradient kernels for the UNet layer shapes at a given batch/resolution,
+all variants interleaved in one process (guide §5.4 rule 24).  Prints one line per (layer, path):
+microseconds and TFLOP/s.  Usage: python tools/kbench.py [--batch 32] [--img 512] [--reps 10]"""
+import argparse
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from distributedpytorch_amd.ops import kernels as K  # noqa: E402
+
+
+def timeit(fn, reps):
+    fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ts = []
+    for _ in range(reps):
+        s.record()
+        fn()
+        e.record()
+        torch.cuda.synchronize()
+        ts.append(s.elapsed_time(e) * 1e3)
+    ts.sort()
+    return ts[len(ts) // 2]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--img", type=int, default=512)
+    ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--only", default="")
+    a = ap.parse_args()
+    dev = torch.device("cuda:0")
+    B, S = a.batch, a.img
+    # (name, H, Cin, Cout)
+    layers = [("L0 32->32", S, 32, 32), ("L0 64->32", S, 64, 32), ("L1 32->64", S // 2, 32, 64),
+              ("L1 64->64", S // 2, 64, 64), ("L1 128->64", S // 2, 128, 64), ("L2 64->128", S // 4, 64, 128),
+              ("L2 128->128", S // 4, 128, 128), ("L3 256->256", S // 8, 256, 256), ("L3 512->256", S // 8, 512, 256),
+              ("mid 512->512", S // 16, 512, 512)]
+    for name, H, Cin, Cout in layers:
+        if a.only and a.only not in name:
+            continue
+        x = torch.randn(B, H, H, Cin, device=dev).to(torch.bfloat16)
+        g = torch.randn(B, H, H, Cout, device=dev).to(torch.bfloat16)
+        y = torch.empty(B, H, H, Cout, device=dev, dtype=torch.bfloat16)
+        dx = torch.empty(B, H, H, Cin, device=dev, dtype=torch.bfloat16)
+        kf, kd = K.round_up(9 * Cin, 32), K.round_up(9 * Cout, 32)
+        wf = (torch.randn(Cout * kf, device=dev) * 0.05).to(torch.bfloat16)
+        wd = (torch.randn(Cin * kd, device=dev) * 0.05).to(torch.bfloat16)
+        bias = torch.zeros(Cout, device=dev)
+        flops = 2.0 * B * H * H * Cin * Cout * 9
+        for path in ("stream", "halo", "generic"):
+            try:
+                t = timeit(lambda: K.igemm(x, wf, y, Ngemm=Cout, Kpad=kf, KH=3, KW=3, stride=1, pad=1, Cs=Cin,
+                                           out_grid=(B, H, H), bias=bias, relu=True, path=path), a.reps)
+                print(f"{name:14s} fwd   {path:8s} {t:9.1f} us {flops / t / 1e6:7.1f} TF", flush=True)
+            except Exception as e:  # path not eligible for this shape
+                print(f"{name:14s} fwd   {path:8s}  n/a ({str(e)[:40]})", flush=True)
+            try:
+                t = timeit(lambda: K.igemm(g, wd, dx, Ngemm=Cin, Kpad=kd, KH=3, KW=3, stride=1, pad=1, Cs=Cout,
+                                           out_grid=(B, H, H), mask=x, path=path), a.reps)
+                print(f"{name:14s} dgrad {path:8s} {t:9.1f} us {flops / t / 1e6:7.1f} TF", flush=True)
+            except Exception as e:
+                print(f"{name:14s} dgrad {path:8s}  n/a ({str(e)[:40]})", flush=True)
+        gw = torch.zeros(Cout * Cin * 9, device=dev)
+        gb = torch.zeros(Cout, device=dev)
+        for halo in (True, False):
+            K.USE_HALO = halo
+            t = timeit(lambda: K.wgrad(g, x, kind=0, grid=(B, H, H), M=Cout, Nc=Cin, s=1, pad=1, KW=3, gw=gw, gb=gb,
+                                       Nreal=Cin), a.reps)
+            print(f"{name:14s} wgrad {'halo' if halo else 'generic':8s} {t:9.1f} us {flops / t / 1e6:7.1f} TF",
+                  flush=True)
+        K.USE_HALO = True
+        del x, g, y, dx
+
+
+if __name__ == "__main__":
+    main()
