@@ -333,8 +333,12 @@ DPA_API int dpa_wgrad_halo(const WgradArgs* args, int cfg, hipStream_t st) {
 // [w0, w0+BP) x rows [h0, h0+RH) and ALL output channels.  The packed weights stay resident in LDS
 // for the block's lifetime; input rows stream through a 4-slot LDS ring (3 rows in use + 1 being
 // prefetched), so every input pixel is read from HBM ~once ((RH+2)/RH x (BP+2)/BP) and every
-// output pixel written once: the layer runs at streaming bandwidth instead of gathering each
+// output pixel written once: the layer runs near streaming bandwidth instead of gathering each
 // pixel 9 times through L2.
+// At K = 9*32 an output tile gets only 9 MFMAs, so the VALU work around them (addresses, epilogue)
+// decides the speed: every per-lane byte offset (loader, LDS fragments, output, mask) is computed
+// once per block in 32 bits, rows only add a wave-uniform scalar, and all global traffic goes
+// through buffer instructions (32-bit offsets, range-checked zero padding, no 64-bit math).
 // LDS images are [.. ][rows][32 channels] 64-B-row nk images (swz_nk<32>, conflict-free).
 template <int BP, int NG, int CS, int RH>
 __global__ __launch_bounds__(256) void igemm_stream_kernel(IgemmArgs a) {
@@ -359,6 +363,8 @@ __global__ __launch_bounds__(256) void igemm_stream_kernel(IgemmArgs a) {
   const int h0 = hs * RH;
   const int tid = threadIdx.x, lane = tid & 63, wp = tid >> 6;
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, 0, (int)a.xbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc((void*)a.y, 0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t mr = __builtin_amdgcn_make_buffer_rsrc((void*)(a.mask ? a.mask : a.y), 0, 0x7fffffff, 0x00020000);
 
   // resident weights: packed [NG][Kpad] with k = tap*CS + ci
   for (int c = tid; c < 9 * KS * NG * 4; c += 256) {
@@ -367,44 +373,77 @@ __global__ __launch_bounds__(256) void igemm_stream_kernel(IgemmArgs a) {
     const u32x4_t v = *reinterpret_cast<const u32x4_t*>(a.w + (long)row * a.Kpad + tap * CS + ks * 32 + cc * 8);
     *reinterpret_cast<u32x4_t*>(Wimg + (tk * NG + row) * 64 + (swz_nk<32>(row, cc) << 4)) = v;
   }
-  auto rload = [&](u32x4_t (&reg)[LR], int ih) {
+  // ---- per-thread loader constants (row-invariant)
+  unsigned loff[LR];
+  int lsto[LR];
+  bool lok[LR];
+#pragma unroll
+  for (int j = 0; j < LR; ++j) {
+    const int c = tid + j * 256;
+    const int cc = c & 3, px = (c >> 2) % HR, ks = (c >> 2) / HR;
+    const int iw = w0 + px - 1;
+    lok[j] = c < RCH && iw >= 0 && iw < a.Ws;
+    loff[j] = (unsigned)((iw * a.ldx + ks * 32 + cc * 8) * 2);
+    lsto[j] = c < RCH ? (ks * HR + px) * 64 + (swz_nk<32>(px, cc) << 4) : -1;
+  }
+  const unsigned rowbytes_x = (unsigned)(a.Ws * a.ldx * 2);
+  u32x4_t reg[LR];
+  auto rload = [&](int ih) {
+    const bool rok = ih >= 0 && ih < a.Hs;                     // wave-uniform
+    const unsigned rbase = (unsigned)(n * a.Hs + ih) * rowbytes_x;
 #pragma unroll
     for (int j = 0; j < LR; ++j) {
-      const int c = tid + j * 256;
-      if (c < RCH) {
-        const int cc = c & 3, px = (c >> 2) % HR, ks = (c >> 2) / HR;
-        const int iw = w0 + px - 1;
-        const bool ok = ih >= 0 && ih < a.Hs && iw >= 0 && iw < a.Ws;
-        const unsigned off = ok ? (unsigned)((((n * a.Hs + ih) * a.Ws + iw) * a.ldx + ks * 32 + cc * 8) * 2) : 0x80000000u;
-        reg[j] = __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0);
-      }
+      const unsigned off = (rok && lok[j]) ? rbase + loff[j] : 0x80000000u;
+      reg[j] = __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0);
     }
   };
-  auto rstore = [&](const u32x4_t (&reg)[LR], int slot) {
+  auto rstore = [&](int slot) {
 #pragma unroll
-    for (int j = 0; j < LR; ++j) {
-      const int c = tid + j * 256;
-      if (c < RCH) {
-        const int cc = c & 3, px = (c >> 2) % HR, ks = (c >> 2) / HR;
-        *reinterpret_cast<u32x4_t*>(Ring + slot * SLOT + (ks * HR + px) * 64 + (swz_nk<32>(px, cc) << 4)) = reg[j];
-      }
-    }
+    for (int j = 0; j < LR; ++j)
+      if (lsto[j] >= 0) *reinterpret_cast<u32x4_t*>(Ring + slot * SLOT + lsto[j]) = reg[j];
   };
-  const int nrows = min(RH, a.Ho - h0);
-  // Input row j (image row h0-1+j) lives in ring slot j&3; output row r reads j = r, r+1, r+2.
-  // Loads run TWO rows ahead through two register sets (HBM latency ~ two row-computations):
-  // iteration r issues j = r+4 into set (r&1) and stores j = r+3 (issued at r-1) from set (r+1)&1.
-  u32x4_t regA[LR], regB[LR];
+  // ---- per-lane LDS fragment offsets and epilogue constants
+  const int chunk = lane >> 4;
+  int aoff[TC];
+#pragma unroll
+  for (int ic = 0; ic < TC; ++ic) {
+    const int row = ic * 16 + (lane & 15);
+    aoff[ic] = row * 64 + (swz_nk<32>(row, chunk) << 4);
+  }
+  int boff[TP][3];
+#pragma unroll
+  for (int ip = 0; ip < TP; ++ip)
+#pragma unroll
+    for (int kw = 0; kw < 3; ++kw) {
+      const int px = wp * WP + ip * 16 + (lane & 15) + kw;
+      boff[ip][kw] = px * 64 + (swz_nk<32>(px, chunk) << 4);
+    }
+  float bias[TC][4];
+#pragma unroll
+  for (int ic = 0; ic < TC; ++ic)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) bias[ic][e] = a.bias ? a.bias[ic * 16 + 4 * chunk + e] : 0.f;
+  unsigned yl[TP], ml[TP];
+#pragma unroll
+  for (int ip = 0; ip < TP; ++ip) {
+    const int pl = w0 + wp * WP + ip * 16 + (lane & 15);
+    yl[ip] = (unsigned)((pl * a.ldy + 4 * chunk) * 2);
+    ml[ip] = (unsigned)((pl * a.ldm + 4 * chunk) * 2);
+  }
+  const bool has_mask = a.mask != nullptr;
+
+  // prologue: input rows h0-1, h0, h0+1 -> slots 0, 1, 2
 #pragma unroll 1
   for (int j = 0; j < 3; ++j) {
-    rload(regA, h0 - 1 + j);
-    rstore(regA, j);
+    rload(h0 - 1 + j);
+    rstore(j);
   }
-  if (3 <= nrows + 1) rload(regB, h0 + 2);
   __syncthreads();
 
-  auto row_step = [&](int r, u32x4_t (&issue)[LR], u32x4_t (&ready)[LR]) {
-    if (r + 4 <= nrows + 1) rload(issue, h0 - 1 + r + 4);
+  const int nrows = min(RH, a.Ho - h0);
+#pragma unroll 1
+  for (int r = 0; r < nrows; ++r) {
+    if (r + 1 < nrows) rload(h0 + r + 2);                  // prefetch into registers
     __builtin_amdgcn_sched_barrier(0);
     f32x4_t acc[TC][TP];
 #pragma unroll
@@ -419,18 +458,13 @@ __global__ __launch_bounds__(256) void igemm_stream_kernel(IgemmArgs a) {
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
           const int tk = (kh * 3 + kw) * KS + ks;
-          const int chunk = lane >> 4;
           bf16x8_t af[TC], bfr[TP];
 #pragma unroll
-          for (int ic = 0; ic < TC; ++ic) {
-            const int row = ic * 16 + (lane & 15);
-            af[ic] = *reinterpret_cast<const bf16x8_t*>(Wimg + (tk * NG + row) * 64 + (swz_nk<32>(row, chunk) << 4));
-          }
+          for (int ic = 0; ic < TC; ++ic)
+            af[ic] = *reinterpret_cast<const bf16x8_t*>(Wimg + tk * NG * 64 + aoff[ic]);
 #pragma unroll
-          for (int ip = 0; ip < TP; ++ip) {
-            const int px = wp * WP + ip * 16 + (lane & 15) + kw;
-            bfr[ip] = *reinterpret_cast<const bf16x8_t*>(S + (ks * HR + px) * 64 + (swz_nk<32>(px, chunk) << 4));
-          }
+          for (int ip = 0; ip < TP; ++ip)
+            bfr[ip] = *reinterpret_cast<const bf16x8_t*>(S + ks * HR * 64 + boff[ip][kw]);
 #pragma unroll
           for (int ic = 0; ic < TC; ++ic)
 #pragma unroll
@@ -439,45 +473,43 @@ __global__ __launch_bounds__(256) void igemm_stream_kernel(IgemmArgs a) {
         }
       }
     }
-    // epilogue for output row h0 + r
-    const long mrow = ((long)n * a.Ho + h0 + r) * a.Wo + w0;
+    // epilogue for output row h0 + r: 32-bit buffer offsets = per-lane constant + uniform row base
+    const int orow = n * a.Ho + h0 + r;
+    const unsigned ybase = (unsigned)orow * (unsigned)(a.Wo * a.ldy * 2);
+    const unsigned mbase = (unsigned)orow * (unsigned)(a.Wo * a.ldm * 2);
 #pragma unroll
     for (int ip = 0; ip < TP; ++ip) {
-      const long m = mrow + wp * WP + ip * 16 + (lane & 15);
+      u32x2_t mk[TC];
+      if (has_mask) {
+#pragma unroll
+        for (int ic = 0; ic < TC; ++ic)
+          mk[ic] = (ic * 16 < a.mask_ch) ? __builtin_amdgcn_raw_buffer_load_b64(mr, mbase + ml[ip] + ic * 32, 0, 0)
+                                         : u32x2_t{0x3f803f80u, 0x3f803f80u};
+      }
 #pragma unroll
       for (int ic = 0; ic < TC; ++ic) {
-        const int co = ic * 16 + 4 * (lane >> 4);
-        float v0 = acc[ic][ip][0], v1 = acc[ic][ip][1], v2 = acc[ic][ip][2], v3 = acc[ic][ip][3];
-        if (a.bias) {
-          const float* b = a.bias + co;
-          v0 += b[0]; v1 += b[1]; v2 += b[2]; v3 += b[3];
-        }
+        float v0 = acc[ic][ip][0] + bias[ic][0], v1 = acc[ic][ip][1] + bias[ic][1];
+        float v2 = acc[ic][ip][2] + bias[ic][2], v3 = acc[ic][ip][3] + bias[ic][3];
         if (a.relu) {
           v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f);
         }
-        if (a.mask && co < a.mask_ch) {
-          const uint2 mk = *reinterpret_cast<const uint2*>(a.mask + m * a.ldm + co);
-          v0 = lo_bf(mk.x) > 0.f ? v0 : 0.f;
-          v1 = hi_bf(mk.x) > 0.f ? v1 : 0.f;
-          v2 = lo_bf(mk.y) > 0.f ? v2 : 0.f;
-          v3 = hi_bf(mk.y) > 0.f ? v3 : 0.f;
+        if (has_mask) {
+          v0 = lo_bf(mk[ic].x) > 0.f ? v0 : 0.f;
+          v1 = hi_bf(mk[ic].x) > 0.f ? v1 : 0.f;
+          v2 = lo_bf(mk[ic].y) > 0.f ? v2 : 0.f;
+          v3 = hi_bf(mk[ic].y) > 0.f ? v3 : 0.f;
         }
-        uint2* dst = reinterpret_cast<uint2*>(a.y + m * a.ldy + co);
+        const unsigned yo = ybase + yl[ip] + ic * 32;
         if (a.accumulate) {
-          const uint2 o = *dst;
+          const u32x2_t o = __builtin_amdgcn_raw_buffer_load_b64(yr, yo, 0, 0);
           v0 += lo_bf(o.x); v1 += hi_bf(o.x); v2 += lo_bf(o.y); v3 += hi_bf(o.y);
         }
-        *dst = make_uint2(pack_bf2(v0, v1), pack_bf2(v2, v3));
+        __builtin_amdgcn_raw_buffer_store_b64(u32x2_t{pack_bf2(v0, v1), pack_bf2(v2, v3)}, yr, yo, 0, 0);
       }
     }
     __builtin_amdgcn_sched_barrier(0);
-    if (r + 3 <= nrows + 1) rstore(ready, (r + 3) & 3);
+    if (r + 1 < nrows) rstore((r + 3) & 3);
     __syncthreads();
-  };
-#pragma unroll 1
-  for (int r = 0; r < nrows; r += 2) {
-    row_step(r, regA, regB);
-    if (r + 1 < nrows) row_step(r + 1, regB, regA);
   }
 }
 
