@@ -154,18 +154,18 @@ DPA_API int dpa_pool_bwd(const bf16_t* skip, int lds, const bf16_t* dskip, int l
 //   mode 3: ConvT dgrad    dst[ci][(2i+j)*Cout+co]   = W[ci][co][i][j]         (Ngemm=Cin, K=4*Cout)
 // k >= K (padding to Kpad) and ci >= Cin (first-layer channel padding) are zero.
 struct PackDesc {
-  long long src;   // element offset of W in the flat fp32 parameter buffer
+  long long src;   // device address of the fp32 weight (PyTorch layout)
   long long dst;   // element offset in the packed bf16 buffer
   int mode, Cout, Cin, Cs, Ngemm, Kpad;
 };
-__global__ __launch_bounds__(256) void pack_kernel(const float* __restrict__ flat, bf16_t* __restrict__ packed,
+__global__ __launch_bounds__(256) void pack_kernel(bf16_t* __restrict__ packed,
                                                    const PackDesc* __restrict__ descs) {
   const PackDesc d = descs[blockIdx.y];
   const long tot = (long)d.Ngemm * d.Kpad;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < tot; i += (long)gridDim.x * blockDim.x) {
     const int n = (int)(i / d.Kpad), k = (int)(i - (long)n * d.Kpad);
     float v = 0.f;
-    const float* W = flat + d.src;
+    const float* W = reinterpret_cast<const float*>(d.src);
     if (d.mode == 0) {
       const int tap = k / d.Cs, ci = k - tap * d.Cs;
       if (tap < 9 && ci < d.Cin) v = W[((long)n * d.Cin + ci) * 9 + tap];
@@ -186,7 +186,8 @@ DPA_API int dpa_pack_weights(const float* flat, bf16_t* packed, const void* desc
                              hipStream_t st) {
   if (ndesc <= 0) return 0;
   dim3 grid(dpa_grid(max_elems, 256, 1024), ndesc);
-  hipLaunchKernelGGL(pack_kernel, grid, dim3(256), 0, st, flat, packed, reinterpret_cast<const PackDesc*>(descs));
+  (void)flat;
+  hipLaunchKernelGGL(pack_kernel, grid, dim3(256), 0, st, packed, reinterpret_cast<const PackDesc*>(descs));
   return (int)hipGetLastError();
 }
 

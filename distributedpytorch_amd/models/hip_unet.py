@@ -61,7 +61,7 @@ class _Deconv:
 class HipBlocks:
     name = "hip"
 
-    def __init__(self, model: UNet, dtype: str = "bf16", space: FlatParameterSpace = None):
+    def __init__(self, model: UNet, dtype: str = "bf16", device=None):
         cfg = model.cfg
         if cfg.batchnorm or cfg.bilinear:
             raise NotImplementedError("hip backend: BatchNorm / bilinear UNet variants run on --backend torch")
@@ -70,11 +70,10 @@ class HipBlocks:
         self.model = model
         self.cfg = cfg
         self.depth = cfg.depth
-        self.device = next(model.parameters()).device
+        self.device = torch.device(device) if device is not None else next(model.parameters()).device
         assert self.device.type == "cuda", "HipBlocks needs a GPU"
-        self.space = space if space is not None else getattr(model, "_flat_space", None)
-        if self.space is None:
-            self.space = FlatParameterSpace(model, device=self.device)
+        if not any(hasattr(p, "_dpa_space") for p in model.parameters()):
+            FlatParameterSpace(model, device=self.device)     # standalone use: flatten here
         self.anchor = torch.zeros(1, device=self.device, requires_grad=True)
         self.enc_convs = [[_Conv(c, K.round_up(c.in_channels, 8) if (l == 0 and j == 0) else c.in_channels,
                                  need_dgrad=not (l == 0 and j == 0))
@@ -90,45 +89,52 @@ class HipBlocks:
         self._cats: Dict[int, torch.Tensor] = {}
 
     # ------------------------------------------------------------------ weight packing
-    def _src(self, p: torch.Tensor) -> int:
-        base = self.space.data.data_ptr()
-        off = (p.data_ptr() - base) // 4
-        assert 0 <= off < self.space.numel and p.is_contiguous()
-        return off
-
     def _build_packing(self):
+        """One descriptor per (layer, layout) for the layers whose weights live on this device (a
+        pipeline stage packs only its own); the pack kernel reads the fp32 weights in place."""
         descs: List[K.PackDesc] = []
         off = 0
         max_elems = 0
+        spaces = {}
 
-        def add(mode, src, cout, cin, cs, ngemm, kpad):
+        def add(mode, w, cout, cin, cs, ngemm, kpad):
             nonlocal off, max_elems
-            descs.append(K.PackDesc(src, off, mode, cout, cin, cs, ngemm, kpad))
+            assert w.dtype == torch.float32 and w.is_contiguous()
+            descs.append(K.PackDesc(w.data_ptr(), off, mode, cout, cin, cs, ngemm, kpad))
+            sp = getattr(w, "_dpa_space", None)
+            if sp is not None:
+                spaces[id(sp)] = sp
             start = off
             off = K.round_up(off + ngemm * kpad, 64)
             max_elems = max(max_elems, ngemm * kpad)
             return start
 
+        here = lambda m: m.weight.device == self.device   # noqa: E731
         for c in [c for cs in self.enc_convs for c in cs] + self.mid_convs + [c for cs in self.dec_convs for c in cs]:
-            src = self._src(c.mod.weight)
-            c.off_f = add(0, src, c.Cout, c.Cin, c.Cs, c.Cout, c.Kf)
+            if not here(c.mod):
+                continue
+            c.off_f = add(0, c.mod.weight, c.Cout, c.Cin, c.Cs, c.Cout, c.Kf)
             if c.need_dgrad:
-                c.off_d = add(1, src, c.Cout, c.Cin, c.Cout, c.Cin, c.Kd)
+                c.off_d = add(1, c.mod.weight, c.Cout, c.Cin, c.Cout, c.Cin, c.Kd)
         for d in self.deconvs:
-            src = self._src(d.mod.weight)
-            d.off_f = add(2, src, d.Cout, d.Cin, d.Cin, 4 * d.Cout, d.Kf)
-            d.off_d = add(3, src, d.Cout, d.Cin, d.Cout, d.Cin, d.Kd)
-        self.packed = torch.zeros(off, dtype=torch.bfloat16, device=self.device)
+            if not here(d.mod):
+                continue
+            d.off_f = add(2, d.mod.weight, d.Cout, d.Cin, d.Cin, 4 * d.Cout, d.Kf)
+            d.off_d = add(3, d.mod.weight, d.Cout, d.Cin, d.Cout, d.Cin, d.Kd)
+        self.packed = torch.zeros(max(off, 64), dtype=torch.bfloat16, device=self.device)
         raw = (K.PackDesc * len(descs))(*descs)
         host = torch.frombuffer(bytearray(bytes(raw)), dtype=torch.uint8)
         self.descs_dev = host.to(self.device)
         self.ndesc = len(descs)
         self.max_elems = max_elems
+        self.spaces = list(spaces.values())
+        # parameter data pointers the descriptors captured (re-pack layout if a param is re-bound)
+        self._ptrs = [d.src for d in descs]
 
     def ensure_packed(self):
-        v = self.space.version
+        v = sum(s.version for s in self.spaces)
         if self._packed_version != v:
-            K.pack_weights(self.space.data, self.packed, self.descs_dev, self.ndesc, self.max_elems)
+            K.pack_weights(self.packed, self.descs_dev, self.ndesc, self.max_elems)
             self._packed_version = v
 
     def wf(self, c):
@@ -178,7 +184,14 @@ class HipBlocks:
                 gb=_grad(d.mod.bias), Nreal=d.Cin)
 
     def ready(self, mods):
-        self.space.notify_ready([p for m in mods for p in (m.weight, m.bias)])
+        by_space = {}
+        for m in mods:
+            for p in (m.weight, m.bias):
+                sp = getattr(p, "_dpa_space", None)
+                if sp is not None:
+                    by_space.setdefault(id(sp), (sp, []))[1].append(p)
+        for sp, ps in by_space.values():
+            sp.notify_ready(ps)
 
     # ------------------------------------------------------------------ block API
     def prep(self, x: torch.Tensor) -> torch.Tensor:

@@ -223,10 +223,11 @@ def pool_bwd(skip: torch.Tensor, dskip: Optional[torch.Tensor], dpool: torch.Ten
                                    c_int(N), c_int(H), c_int(W), c_int(C), _stream(skip)), "pool_bwd")
 
 
-def pack_weights(flat: torch.Tensor, packed: torch.Tensor, descs_dev: torch.Tensor, ndesc: int, max_elems: int):
-    assert flat.dtype == torch.float32 and packed.dtype == torch.bfloat16
-    _check(_lib.lib().dpa_pack_weights(_p(flat), _p(packed), _p(descs_dev), c_int(ndesc), c_ll(max_elems),
-                                       _stream(flat)), "pack_weights")
+def pack_weights(packed: torch.Tensor, descs_dev: torch.Tensor, ndesc: int, max_elems: int):
+    """Batched fp32 -> bf16 GEMM-layout packing; each descriptor holds its weight's device address."""
+    assert packed.dtype == torch.bfloat16
+    _check(_lib.lib().dpa_pack_weights(None, _p(packed), _p(descs_dev), c_int(ndesc), c_ll(max_elems),
+                                       _stream(packed)), "pack_weights")
 
 
 def head_fwd(y: torch.Tensor, w: torch.Tensor, b: torch.Tensor, t: Optional[torch.Tensor], want_probs: bool = False):

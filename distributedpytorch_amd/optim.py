@@ -49,6 +49,8 @@ class FlatParameterSpace:
             p.data = self.data[o:o + n].view_as(p)
             p.grad = self.grad[o:o + n].view_as(p)
         self._index = {id(p): i for i, p in enumerate(self.params)}
+        for p in self.params:
+            p._dpa_space = self          # lets kernel engines find the space owning a parameter
         self.version = 0                 # bumped whenever parameter values change (optimizer, sync, load)
         self._ready_listeners = []       # called with param indices whose gradient is final
         if isinstance(module, nn.Module):

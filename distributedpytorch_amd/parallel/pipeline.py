@@ -306,7 +306,7 @@ class GPipeLocal:
             names = set(stage_param_names(model, self.cuts[s], self.cuts[s + 1]))
             own = [(n, p) for n, p in model.named_parameters() if n in names]
             self.spaces.append(FlatParameterSpace(own, device=self.devices[s]))
-        self.stage_blocks = [make_blocks(model, backend, dtype) for _ in range(self.S)]
+        self.stage_blocks = [make_blocks(model, backend, dtype, device=self.devices[s]) for s in range(self.S)]
         for s, b in enumerate(self.stage_blocks):
             b.device = self.devices[s]
 

@@ -46,10 +46,10 @@ def _pack_one(mode, w, cin_pad=None):
             ngemm, kpad, cs = 4 * Cout, K.round_up(Cin, 32), Cin
         else:
             ngemm, kpad, cs = Cin, K.round_up(4 * Cout, 32), Cout
-    d = K.PackDesc(0, 0, mode, Cout, Cin, cs, ngemm, kpad)
+    d = K.PackDesc(flat.data_ptr(), 0, mode, Cout, Cin, cs, ngemm, kpad)
     descs = torch.frombuffer(bytearray(bytes(d)), dtype=torch.uint8).cuda()
     packed = torch.empty(ngemm * kpad, dtype=torch.bfloat16, device="cuda")
-    K.pack_weights(flat, packed, descs, 1, ngemm * kpad)
+    K.pack_weights(packed, descs, 1, ngemm * kpad)
     return packed, ngemm, kpad
 
 

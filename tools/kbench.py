@@ -43,7 +43,7 @@ def main():
               ("L2 128->128", S // 4, 128, 128), ("L3 256->256", S // 8, 256, 256), ("L3 512->256", S // 8, 512, 256),
               ("mid 512->512", S // 16, 512, 512)]
     for name, H, Cin, Cout in layers:
-        if a.only and a.only not in name:
+        if a.only and not any(o in name for o in a.only.split(",")):
             continue
         x = torch.randn(B, H, H, Cin, device=dev).to(torch.bfloat16)
         g = torch.randn(B, H, H, Cout, device=dev).to(torch.bfloat16)
