@@ -444,6 +444,19 @@ __global__ __launch_bounds__(256) void igemm_stream_kernel(IgemmArgs a) {
 #pragma unroll 1
   for (int r = 0; r < nrows; ++r) {
     if (r + 1 < nrows) rload(h0 + r + 2);                  // prefetch into registers
+    const int orow = n * a.Ho + h0 + r;
+    const unsigned ybase = (unsigned)orow * (unsigned)(a.Wo * a.ldy * 2);
+    const unsigned mbase = (unsigned)orow * (unsigned)(a.Wo * a.ldm * 2);
+    // ReLU-mask of this output row: issued before the MFMAs so its latency hides under them
+    u32x2_t mk[TP][TC];
+    if (has_mask) {
+#pragma unroll
+      for (int ip = 0; ip < TP; ++ip)
+#pragma unroll
+        for (int ic = 0; ic < TC; ++ic)
+          mk[ip][ic] = (ic * 16 < a.mask_ch) ? __builtin_amdgcn_raw_buffer_load_b64(mr, mbase + ml[ip] + ic * 32, 0, 0)
+                                             : u32x2_t{0x3f803f80u, 0x3f803f80u};
+    }
     __builtin_amdgcn_sched_barrier(0);
     f32x4_t acc[TC][TP];
 #pragma unroll
@@ -474,18 +487,8 @@ __global__ __launch_bounds__(256) void igemm_stream_kernel(IgemmArgs a) {
       }
     }
     // epilogue for output row h0 + r: 32-bit buffer offsets = per-lane constant + uniform row base
-    const int orow = n * a.Ho + h0 + r;
-    const unsigned ybase = (unsigned)orow * (unsigned)(a.Wo * a.ldy * 2);
-    const unsigned mbase = (unsigned)orow * (unsigned)(a.Wo * a.ldm * 2);
 #pragma unroll
     for (int ip = 0; ip < TP; ++ip) {
-      u32x2_t mk[TC];
-      if (has_mask) {
-#pragma unroll
-        for (int ic = 0; ic < TC; ++ic)
-          mk[ic] = (ic * 16 < a.mask_ch) ? __builtin_amdgcn_raw_buffer_load_b64(mr, mbase + ml[ip] + ic * 32, 0, 0)
-                                         : u32x2_t{0x3f803f80u, 0x3f803f80u};
-      }
 #pragma unroll
       for (int ic = 0; ic < TC; ++ic) {
         float v0 = acc[ic][ip][0] + bias[ic][0], v1 = acc[ic][ip][1] + bias[ic][1];
@@ -494,10 +497,10 @@ __global__ __launch_bounds__(256) void igemm_stream_kernel(IgemmArgs a) {
           v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f);
         }
         if (has_mask) {
-          v0 = lo_bf(mk[ic].x) > 0.f ? v0 : 0.f;
-          v1 = hi_bf(mk[ic].x) > 0.f ? v1 : 0.f;
-          v2 = lo_bf(mk[ic].y) > 0.f ? v2 : 0.f;
-          v3 = hi_bf(mk[ic].y) > 0.f ? v3 : 0.f;
+          v0 = lo_bf(mk[ip][ic].x) > 0.f ? v0 : 0.f;
+          v1 = hi_bf(mk[ip][ic].x) > 0.f ? v1 : 0.f;
+          v2 = lo_bf(mk[ip][ic].y) > 0.f ? v2 : 0.f;
+          v3 = hi_bf(mk[ip][ic].y) > 0.f ? v3 : 0.f;
         }
         const unsigned yo = ybase + yl[ip] + ic * 32;
         if (a.accumulate) {
@@ -538,5 +541,203 @@ DPA_API int dpa_igemm_stream(const IgemmArgs* args, int rh, hipStream_t st) {
   DPA_STREAM(64, 32)
   DPA_STREAM(64, 64)
 #undef DPA_STREAM
+  return (int)hipErrorInvalidValue;
+}
+
+// ------------------------------------------------------------------------------------ wgrad_stream
+// Row-streaming conv3x3 weight gradient.  A block owns one (BM out-ch x BN in-ch) tile and an
+// image strip [w0, w0+BP) x rows [h0, h0+RH) (its split).  Per output row it stages the gradient
+// row g[h][w0..w0+BP) (A) and streams the layer-input rows through a 4-slot ring (B, BP+2 pixels
+// incl. halo), so every input/gradient pixel is read ~once.  Three waves, one per kernel row kh:
+// wave kh accumulates the taps (kh, 0..2) against ring slot (r + kh) with a pixel shift kw, i.e.
+// dW[co][kh][kw][ci] += sum_px g[h][px][co] * x[h+kh-1][px+kw-1][ci].  Fragments come from the
+// [pixel][channel] LDS images through ds_read_b64_tr_b16 (conflict-free swizzles, any row shift).
+// Bias gradient: the loader threads sum the gradient chunks they stage, reduced once per block.
+template <int BM, int BN, int BP, int RH>
+__global__ __launch_bounds__(192) void wgrad_stream_kernel(WgradArgs a) {
+  constexpr int NT = 192;
+  constexpr int HR = BP + 2;
+  constexpr int CPRA = BM / 8, CPRB = BN / 8, RBA = BM * 2, RBB = BN * 2;
+  constexpr int IMGA = BP * RBA, SLOTB = HR * RBB;
+  constexpr int CHA = BP * CPRA, CHB = HR * CPRB;
+  constexpr int LA = (CHA + NT - 1) / NT, LB = (CHB + NT - 1) / NT;
+  constexpr int TM = BM / 16, TN = BN / 16;
+  __shared__ __attribute__((aligned(16))) char lds[2 * IMGA + 4 * SLOTB];
+  __shared__ float bred[BM];
+  char* const Aimg = lds;
+  char* const Ring = lds + 2 * IMGA;
+
+  const int nmt = a.M / BM, nnt = a.Nc / BN, tiles = nmt * nnt;
+  const int stripsW = a.Wg / BP, segsH = (a.Hg + RH - 1) / RH;
+  const int bid = xcd_remap(blockIdx.x, tiles * a.splits);
+  const int split = bid / tiles, tile = bid - split * tiles;     // split = (n, hs, ws)
+  const int mt = tile / nnt, nt = tile - mt * nnt;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int n = split / (segsH * stripsW);
+  const int rem = split - n * segsH * stripsW;
+  const int hs = rem / stripsW;
+  const int w0 = (rem - hs * stripsW) * BP, h0 = hs * RH;
+  const int nrows = min(RH, a.Hg - h0);
+  const int tid = threadIdx.x, lane = tid & 63, kh = tid >> 6;
+  const bool do_bias = a.bslab != nullptr && nt == 0;
+  const __amdgpu_buffer_rsrc_t ar = __builtin_amdgcn_make_buffer_rsrc((void*)a.A, 0, (int)a.abytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t br = __builtin_amdgcn_make_buffer_rsrc((void*)a.B, 0, (int)a.bbytes, 0x00020000);
+
+  // per-thread loader constants
+  unsigned aoff[LA], boff[LB];
+  int asto[LA], bsto[LB];
+  bool bok[LB];
+#pragma unroll
+  for (int j = 0; j < LA; ++j) {
+    const int c = tid + j * NT, px = c / CPRA, cc = c - px * CPRA;
+    aoff[j] = (unsigned)(((w0 + px) * a.lda + m0 + cc * 8) * 2);
+    asto[j] = c < CHA ? px * RBA + ((cc ^ swz_kk<RBA>(px)) << 4) : -1;
+  }
+#pragma unroll
+  for (int j = 0; j < LB; ++j) {
+    const int c = tid + j * NT, px = c / CPRB, cc = c - px * CPRB;
+    const int iw = w0 + px - 1;
+    bok[j] = c < CHB && iw >= 0 && iw < a.WB;
+    boff[j] = (unsigned)((iw * a.ldb + n0 + cc * 8) * 2);
+    bsto[j] = c < CHB ? px * RBB + ((cc ^ swz_kk<RBB>(px)) << 4) : -1;
+  }
+  const unsigned arow = (unsigned)(a.WA * a.lda * 2), brow = (unsigned)(a.WB * a.ldb * 2);
+  u32x4_t ra[LA], rb[LB];
+  auto load_a = [&](int h) {
+    const unsigned base = (unsigned)(n * a.HA + h) * arow;
+#pragma unroll
+    for (int j = 0; j < LA; ++j) ra[j] = __builtin_amdgcn_raw_buffer_load_b128(ar, asto[j] >= 0 ? base + aoff[j] : 0x80000000u, 0, 0);
+  };
+  auto load_b = [&](int ih) {
+    const bool rok = ih >= 0 && ih < a.HB;
+    const unsigned base = (unsigned)(n * a.HB + ih) * brow;
+#pragma unroll
+    for (int j = 0; j < LB; ++j)
+      rb[j] = __builtin_amdgcn_raw_buffer_load_b128(br, (rok && bok[j]) ? base + boff[j] : 0x80000000u, 0, 0);
+  };
+  // bias gradient: wave 0 sums the staged gradient row from LDS; lane owns channel chunk lane % CPRA
+  float bsum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  auto store_a = [&](int buf) {
+#pragma unroll
+    for (int j = 0; j < LA; ++j)
+      if (asto[j] >= 0) *reinterpret_cast<u32x4_t*>(Aimg + buf * IMGA + asto[j]) = ra[j];
+  };
+  auto store_b = [&](int slot) {
+#pragma unroll
+    for (int j = 0; j < LB; ++j)
+      if (bsto[j] >= 0) *reinterpret_cast<u32x4_t*>(Ring + slot * SLOTB + bsto[j]) = rb[j];
+  };
+
+  f32x4_t acc[3][TM][TN];
+#pragma unroll
+  for (int kw = 0; kw < 3; ++kw)
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[kw][i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  // prologue: input rows h0-1, h0, h0+1 -> ring slots 0..2; gradient row h0 -> A buffer 0
+  if (nrows > 0) {
+#pragma unroll 1
+    for (int j = 0; j < 3; ++j) {
+      load_b(h0 - 1 + j);
+      store_b(j);
+    }
+    load_a(h0);
+    store_a(0);
+  }
+  __syncthreads();
+#pragma unroll 1
+  for (int r = 0; r < nrows; ++r) {
+    const bool more = r + 1 < nrows;
+    if (more) {
+      load_a(h0 + r + 1);
+      load_b(h0 + r + 2);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    const char* Ai = Aimg + (r & 1) * IMGA;
+    const char* Bi = Ring + ((r + kh) & 3) * SLOTB;
+#pragma unroll
+    for (int ks = 0; ks < BP / 32; ++ks) {
+      bf16x8_t af[TM];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[i] = tr_frag<RBA>(Ai, i * 16, lane, ks * 32);
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const bf16x8_t bf = tr_frag<RBB>(Bi, j * 16, lane, ks * 32 + kw);
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+            acc[kw][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf, acc[kw][i][j], 0, 0, 0);
+        }
+    }
+    if (do_bias && kh == 0) {
+#pragma unroll
+      for (int c = lane; c < CHA; c += 64) {
+        const int px = c / CPRA, cc = c - px * CPRA;
+        const u32x4_t v = *reinterpret_cast<const u32x4_t*>(Ai + px * RBA + ((cc ^ swz_kk<RBA>(px)) << 4));
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          bsum[2 * e] += lo_bf(v[e]);
+          bsum[2 * e + 1] += hi_bf(v[e]);
+        }
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if (more) {
+      store_a((r + 1) & 1);
+      store_b((r + 3) & 3);
+    }
+    __syncthreads();
+  }
+  // epilogue: this split's partial dW for taps (kh, 0..2)
+#pragma unroll
+  for (int kw = 0; kw < 3; ++kw)
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int nn = n0 + j * 16 + (lane & 15);
+        const int mb = m0 + i * 16 + 4 * (lane >> 4);
+        float* dst = a.slab + (((long)split * 9 + kh * 3 + kw) * a.M + mb) * a.Nc + nn;
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) dst[(long)rr * a.Nc] = acc[kw][i][j][rr];
+      }
+  if (do_bias) {
+    for (int c = tid; c < BM; c += NT) bred[c] = 0.f;
+    __syncthreads();
+    if (kh == 0) {
+      const int cc = lane % CPRA;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) atomicAdd(&bred[cc * 8 + e], bsum[e]);
+    }
+    __syncthreads();
+    for (int c = tid; c < BM; c += NT) a.bslab[(long)split * a.M + m0 + c] = bred[c];
+  }
+}
+
+template <int BM, int BN, int BP, int RH>
+static int launch_wgrad_stream(const WgradArgs& a, hipStream_t st) {
+  const int tiles = (a.M / BM) * (a.Nc / BN);
+  hipLaunchKernelGGL((wgrad_stream_kernel<BM, BN, BP, RH>), dim3(tiles * a.splits), dim3(192), 0, st, a);
+  return (int)hipGetLastError();
+}
+
+// splits must equal N * ceil(Hg/RH) * (Wg/BP); cfg picks (BM, BN): 1: 32x32  2: 64x32  3: 32x64
+DPA_API int dpa_wgrad_stream(const WgradArgs* args, int cfg, int bp, int rh, hipStream_t st) {
+  const WgradArgs& a = *args;
+  if ((a.lda & 7) || (a.ldb & 7) || a.s != 1 || a.pad != 1 || a.KW != 3 || a.HA != a.Hg || a.WA != a.Wg ||
+      a.HB != a.Hg || a.WB != a.Wg || a.Wg % bp || a.splits != a.N * ((a.Hg + rh - 1) / rh) * (a.Wg / bp))
+    return (int)hipErrorInvalidValue;
+#define DPA_WS(C, BMv, BNv, BPv, RHv)                                                              \
+  if (cfg == C && bp == BPv && rh == RHv && a.M % BMv == 0 && a.Nc % BNv == 0) return launch_wgrad_stream<BMv, BNv, BPv, RHv>(a, st);
+  DPA_WS(1, 32, 32, 64, 64)
+  DPA_WS(2, 64, 32, 64, 64)
+  DPA_WS(3, 32, 64, 64, 64)
+  DPA_WS(1, 32, 32, 64, 32)
+  DPA_WS(2, 64, 32, 64, 32)
+  DPA_WS(3, 32, 64, 64, 32)
+#undef DPA_WS
   return (int)hipErrorInvalidValue;
 }

@@ -148,8 +148,17 @@ def wgrad_splits(P: int, tiles: int, target_blocks: int = 1024, min_pix: int = 5
 
 
 def wgrad(A: torch.Tensor, B: torch.Tensor, *, kind: int, grid, M: int, Nc: int, s: int, pad: int, KW: int,
-          gw: torch.Tensor, gb: Optional[torch.Tensor], Nreal: int, cfg: int = 0, target_blocks: int = 1024):
-    """Weight (+bias) gradient of a conv3x3 (kind 0) or transposed conv 2x2/s2 (kind 1); accumulates into gw/gb."""
+          gw: torch.Tensor, gb: Optional[torch.Tensor], Nreal: int, cfg: int = 0, target_blocks: int = 1024,
+          path: str = "auto"):
+    """Weight (+bias) gradient of a conv3x3 (kind 0) or transposed conv 2x2/s2 (kind 1); accumulates into gw/gb.
+
+    ``path``: ``auto`` = row-streaming kernel when W % 64 == 0, else row-halo (W % 32 == 0), else the
+    generic per-tap gather kernel; ``stream`` / ``halo`` / ``generic`` force one."""
+    if path in ("auto", "stream") and kind == 0 and cfg == 0 and (USE_STREAM or path == "stream") \
+            and grid[2] % 64 == 0 and M % 32 == 0 and Nc % 32 == 0:
+        return _wgrad_stream(A, B, grid=grid, M=M, Nc=Nc, gw=gw, gb=gb, Nreal=Nreal)
+    if path == "stream":
+        raise RuntimeError("wgrad stream path not eligible for this shape")
     NA, HA, WA, CA, lda = _nhwc(A, "wgrad.A")
     NB, HB, WB, CB, ldb = _nhwc(B, "wgrad.B")
     N, Hg, Wg = grid
@@ -159,7 +168,8 @@ def wgrad(A: torch.Tensor, B: torch.Tensor, *, kind: int, grid, M: int, Nc: int,
         assert (HA, WA) == (Hg, Wg) and (HB, WB) == (Hg, Wg)
     else:
         assert (HA, WA) == (2 * Hg, 2 * Wg) and (HB, WB) == (Hg, Wg)
-    halo = (USE_HALO and kind == 0 and cfg == 0 and Wg % 32 == 0 and Nc % 32 == 0 and M % 32 == 0)
+    halo = ((USE_HALO or path == "halo") and path != "generic" and kind == 0 and cfg == 0 and Wg % 32 == 0
+            and Nc % 32 == 0 and M % 32 == 0)
     if halo:
         hcfg = 2 if M % 64 == 0 else (3 if Nc % 64 == 0 else 1)
         bm, bn = {1: (32, 32), 2: (64, 32), 3: (32, 64), 4: (64, 64)}[hcfg]
@@ -189,6 +199,31 @@ def wgrad(A: torch.Tensor, B: torch.Tensor, *, kind: int, grid, M: int, Nc: int,
             _check(L.dpa_wgrad(ctypes.byref(a), c_int(kind), c_int(cfg), st), "wgrad")
         _check(L.dpa_wgrad_reduce(_p(slab), _p(bslab), _p(gw), _p(gb), c_int(splits), c_int(T), c_int(M), c_int(Nc),
                                   c_int(Nreal), c_int(kind), st), "wgrad_reduce")
+
+
+def _wgrad_stream(A, B, *, grid, M, Nc, gw, gb, Nreal):
+    NA, HA, WA, CA, lda = _nhwc(A, "wgrad.A")
+    NB, HB, WB, CB, ldb = _nhwc(B, "wgrad.B")
+    N, Hg, Wg = grid
+    assert (HA, WA) == (Hg, Wg) == (HB, WB) and NA == NB == N and CA >= M and CB >= Nc
+    assert gw.dtype == torch.float32 and gw.is_contiguous() and gw.numel() == M * Nreal * 9
+    hcfg = 2 if M % 64 == 0 else (3 if Nc % 64 == 0 else 1)
+    bm, bn = {1: (32, 32), 2: (64, 32), 3: (32, 64)}[hcfg]
+    tiles = (M // bm) * (Nc // bn)
+    L = _lib.lib()
+    st = _stream(A)
+    for n0, n1 in _image_chunks(N, max(HA * WA * lda, HB * WB * ldb) * 2):
+        nb = n1 - n0
+        rh = 64 if nb * -(-Hg // 64) * (Wg // 64) * tiles >= 1024 else 32
+        splits = nb * -(-Hg // rh) * (Wg // 64)
+        slab = torch.empty(splits * 9 * M * Nc + splits * M, dtype=torch.float32, device=A.device)
+        bslab = slab[splits * 9 * M * Nc:] if gb is not None else None
+        a = WgradArgs(A[n0:n1].data_ptr(), B[n0:n1].data_ptr(), slab.data_ptr(),
+                      None if bslab is None else bslab.data_ptr(), lda, ldb, nb, Hg, Wg, HA, WA, HB, WB, M, Nc, 1,
+                      1, 3, 0, splits, _extent_bytes(nb, HA, WA, CA, lda), _extent_bytes(nb, HB, WB, CB, ldb))
+        _check(L.dpa_wgrad_stream(ctypes.byref(a), c_int(hcfg), c_int(64), c_int(rh), st), "wgrad_stream")
+        _check(L.dpa_wgrad_reduce(_p(slab), _p(bslab), _p(gw), _p(gb), c_int(splits), c_int(9), c_int(M), c_int(Nc),
+                                  c_int(Nreal), c_int(0), st), "wgrad_reduce")
 
 
 # ------------------------------------------------------------------------------------------ aux

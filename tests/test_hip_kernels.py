@@ -150,12 +150,16 @@ def test_deconv_dgrad_from_concat(hip_lib, N, h, w, Cin, Cout):
     assert _rel(_nchw(out), ref) < 2e-2
 
 
-@pytest.mark.parametrize("N,H,W,Cin,Cout,cin_pad", [
-    (2, 19, 21, 3, 32, 8), (2, 16, 16, 32, 32, None), (1, 12, 16, 64, 128, None), (2, 8, 8, 128, 64, None),
+@pytest.mark.parametrize("N,H,W,Cin,Cout,cin_pad,path", [
+    (2, 19, 21, 3, 32, 8, "auto"), (2, 16, 16, 32, 32, None, "auto"), (1, 12, 16, 64, 128, None, "auto"),
+    (2, 8, 8, 128, 64, None, "auto"),
     # row-halo wgrad (W % 32 == 0)
-    (2, 5, 32, 32, 32, None), (1, 4, 64, 64, 32, None), (2, 3, 32, 32, 64, None), (1, 4, 32, 128, 64, None),
-    (2, 4, 32, 3, 32, 8)])
-def test_conv3x3_wgrad(hip_lib, N, H, W, Cin, Cout, cin_pad):
+    (2, 5, 32, 32, 32, None, "halo"), (1, 4, 64, 64, 32, None, "halo"), (2, 3, 32, 32, 64, None, "halo"),
+    (1, 4, 32, 128, 64, None, "halo"), (2, 4, 32, 3, 32, 8, "auto"),
+    # row-streaming wgrad (W % 64 == 0), odd row counts -> partial row segments
+    (2, 5, 64, 32, 32, None, "stream"), (1, 37, 64, 64, 32, None, "stream"), (2, 3, 128, 32, 64, None, "stream"),
+    (1, 70, 64, 128, 64, None, "stream"), (1, 4, 64, 64, 128, None, "generic")])
+def test_conv3x3_wgrad(hip_lib, N, H, W, Cin, Cout, cin_pad, path):
     from distributedpytorch_amd.ops import kernels as K
     torch.manual_seed(4)
     x = _bf(torch.randn(N, Cin, H, W))
@@ -169,7 +173,7 @@ def test_conv3x3_wgrad(hip_lib, N, H, W, Cin, Cout, cin_pad):
     gw = torch.full((Cout, Cin, 3, 3), 0.5, device="cuda")    # accumulates on top
     gb = torch.full((Cout,), 0.5, device="cuda")
     K.wgrad(_nhwc(g), _nhwc(xin), kind=0, grid=(N, H, W), M=Cout, Nc=Cs, s=1, pad=1, KW=3, gw=gw.view(-1), gb=gb,
-            Nreal=Cin)
+            Nreal=Cin, path=path)
     torch.cuda.synchronize()
     assert _rel(gw.cpu() - 0.5, wr.grad) < 1e-2
     assert _rel(gb.cpu() - 0.5, br.grad) < 1e-2

@@ -69,13 +69,13 @@ def main():
                 print(f"{name:14s} dgrad {path:8s}  n/a ({str(e)[:40]})", flush=True)
         gw = torch.zeros(Cout * Cin * 9, device=dev)
         gb = torch.zeros(Cout, device=dev)
-        for halo in (True, False):
-            K.USE_HALO = halo
-            t = timeit(lambda: K.wgrad(g, x, kind=0, grid=(B, H, H), M=Cout, Nc=Cin, s=1, pad=1, KW=3, gw=gw, gb=gb,
-                                       Nreal=Cin), a.reps)
-            print(f"{name:14s} wgrad {'halo' if halo else 'generic':8s} {t:9.1f} us {flops / t / 1e6:7.1f} TF",
-                  flush=True)
-        K.USE_HALO = True
+        for path in ("stream", "halo", "generic"):
+            try:
+                t = timeit(lambda: K.wgrad(g, x, kind=0, grid=(B, H, H), M=Cout, Nc=Cin, s=1, pad=1, KW=3, gw=gw,
+                                           gb=gb, Nreal=Cin, path=path), a.reps)
+                print(f"{name:14s} wgrad {path:8s} {t:9.1f} us {flops / t / 1e6:7.1f} TF", flush=True)
+            except Exception as e:
+                print(f"{name:14s} wgrad {path:8s}  n/a ({str(e)[:40]})", flush=True)
         del x, g, y, dx
 
 
