@@ -16,6 +16,8 @@ struct IgemmArgs {
   int mode;             // 0: y[m][n]   1: transposed-conv 2x2/s2 scatter, n = (2i+j)*Cout + co
   int relu, accumulate, Cout;
   unsigned xbytes;      // bytes addressable from x (< 2^31; the host splits larger batches by image)
+  bf16_t* pool;         // optional fused 2x2/s2 max-pool output [N][Ho/2][Wo/2][ldp] (stream kernels)
+  int ldp;
 };
 
 struct WgradArgs {

@@ -431,6 +431,11 @@ __global__ __launch_bounds__(256) void igemm_stream_kernel(IgemmArgs a) {
     ml[ip] = (unsigned)((pl * a.ldm + 4 * chunk) * 2);
   }
   const bool has_mask = a.mask != nullptr;
+  // fused 2x2 max-pool (encoder conv2 -> next level input): even rows keep their horizontally
+  // max-reduced values in registers, odd rows finish the window and write the pooled pixel.
+  const bool do_pool = a.pool != nullptr;
+  const __amdgpu_buffer_rsrc_t pr = __builtin_amdgcn_make_buffer_rsrc((void*)(do_pool ? a.pool : a.y), 0, 0x7fffffff, 0x00020000);
+  float pkeep[TP][TC][4];
 
   // prologue: input rows h0-1, h0, h0+1 -> slots 0, 1, 2
 #pragma unroll 1
@@ -507,13 +512,147 @@ __global__ __launch_bounds__(256) void igemm_stream_kernel(IgemmArgs a) {
           const u32x2_t o = __builtin_amdgcn_raw_buffer_load_b64(yr, yo, 0, 0);
           v0 += lo_bf(o.x); v1 += hi_bf(o.x); v2 += lo_bf(o.y); v3 += hi_bf(o.y);
         }
-        __builtin_amdgcn_raw_buffer_store_b64(u32x2_t{pack_bf2(v0, v1), pack_bf2(v2, v3)}, yr, yo, 0, 0);
+        const u32x2_t packed = u32x2_t{pack_bf2(v0, v1), pack_bf2(v2, v3)};
+        __builtin_amdgcn_raw_buffer_store_b64(packed, yr, yo, 0, 0);
+        if (do_pool) {
+          // pool the STORED (bf16-rounded) values: identical to max-pooling the tensor afterwards
+          float q[4] = {lo_bf(packed.x), hi_bf(packed.x), lo_bf(packed.y), hi_bf(packed.y)};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) q[e] = fmaxf(q[e], __shfl_xor(q[e], 1, 64));   // pixel pair (w, w+1)
+          const int hrow = h0 + r;
+          if ((hrow & 1) == 0) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) pkeep[ip][ic][e] = q[e];
+          } else if (hrow < 2 * (a.Ho >> 1) && (lane & 1) == 0) {
+            const int pw = (w0 + wp * WP + ip * 16 + (lane & 15)) >> 1;
+            const unsigned po = (unsigned)((((n * (a.Ho >> 1) + (hrow >> 1)) * (a.Wo >> 1) + pw) * a.ldp +
+                                            ic * 16 + 4 * chunk) * 2);
+            __builtin_amdgcn_raw_buffer_store_b64(
+                u32x2_t{pack_bf2(fmaxf(q[0], pkeep[ip][ic][0]), fmaxf(q[1], pkeep[ip][ic][1])),
+                        pack_bf2(fmaxf(q[2], pkeep[ip][ic][2]), fmaxf(q[3], pkeep[ip][ic][3]))},
+                pr, po, 0, 0);
+          }
+        }
       }
     }
     __builtin_amdgcn_sched_barrier(0);
     if (r + 1 < nrows) rstore((r + 3) & 3);
     __syncthreads();
   }
+}
+
+// First layer (Cin = 3 padded to 8): K = 9 taps x 8 channels.  A 32-deep MFMA k-step covers 4 taps,
+// one per 16-lane group, so each lane reads its tap's 16 bytes straight from the row ring at pixel
+// (p + kw) of slot (r + kh): no im2col, 3 k-steps (taps 9..11 have zero weights).
+template <int BP, int RH>
+__global__ __launch_bounds__(256) void igemm_stream8_kernel(IgemmArgs a) {
+  constexpr int NG = 32, HR = BP + 2, SLOT = HR * 16;
+  constexpr int WP = BP / 4, TP = WP / 16, TC = NG / 16;
+  __shared__ __attribute__((aligned(16))) char lds[3 * NG * 64 + 4 * SLOT];
+  char* const Wimg = lds;
+  char* const Ring = lds + 3 * NG * 64;
+  const int stripsW = a.Wo / BP, segsH = (a.Ho + RH - 1) / RH;
+  const int bid = blockIdx.x;
+  const int n = bid / (segsH * stripsW);
+  const int rem = bid - n * segsH * stripsW;
+  const int hs = rem / stripsW;
+  const int w0 = (rem - hs * stripsW) * BP, h0 = hs * RH;
+  const int tid = threadIdx.x, lane = tid & 63, wp = tid >> 6;
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, 0, (int)a.xbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc((void*)a.y, 0, 0x7fffffff, 0x00020000);
+  // weights [co][96] -> [kstep][co][64 B] (swz_nk<32>)
+  for (int c = tid; c < 3 * NG * 4; c += 256) {
+    const int cc = c & 3, row = (c >> 2) % NG, s = (c >> 2) / NG;
+    const u32x4_t v = (s * 32 + cc * 8 < a.Kpad) ? *reinterpret_cast<const u32x4_t*>(a.w + (long)row * a.Kpad + s * 32 + cc * 8)
+                                                 : u32x4_t{0u, 0u, 0u, 0u};
+    *reinterpret_cast<u32x4_t*>(Wimg + (s * NG + row) * 64 + (swz_nk<32>(row, cc) << 4)) = v;
+  }
+  const int iw_l = w0 + tid - 1;
+  const bool lcol = tid < HR && iw_l >= 0 && iw_l < a.Ws;
+  const unsigned rowbytes = (unsigned)(a.Ws * a.ldx * 2);
+  u32x4_t reg;
+  auto rload = [&](int ih) {
+    const bool ok = lcol && ih >= 0 && ih < a.Hs;
+    reg = __builtin_amdgcn_raw_buffer_load_b128(xr, ok ? (unsigned)(n * a.Hs + ih) * rowbytes + (unsigned)(iw_l * a.ldx * 2)
+                                                       : 0x80000000u, 0, 0);
+  };
+  auto rstore = [&](int slot) {
+    if (tid < HR) *reinterpret_cast<u32x4_t*>(Ring + slot * SLOT + tid * 16) = reg;
+  };
+  const int chunk = lane >> 4;
+  int aoff[TC];
+#pragma unroll
+  for (int ic = 0; ic < TC; ++ic) {
+    const int row = ic * 16 + (lane & 15);
+    aoff[ic] = row * 64 + (swz_nk<32>(row, chunk) << 4);
+  }
+  float bias[TC][4];
+#pragma unroll
+  for (int ic = 0; ic < TC; ++ic)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) bias[ic][e] = a.bias ? a.bias[ic * 16 + 4 * chunk + e] : 0.f;
+  unsigned yl[TP];
+#pragma unroll
+  for (int ip = 0; ip < TP; ++ip) yl[ip] = (unsigned)(((w0 + wp * WP + ip * 16 + (lane & 15)) * a.ldy + 4 * chunk) * 2);
+#pragma unroll 1
+  for (int j = 0; j < 3; ++j) {
+    rload(h0 - 1 + j);
+    rstore(j);
+  }
+  __syncthreads();
+  const int nrows = min(RH, a.Ho - h0);
+#pragma unroll 1
+  for (int r = 0; r < nrows; ++r) {
+    if (r + 1 < nrows) rload(h0 + r + 2);
+    __builtin_amdgcn_sched_barrier(0);
+    f32x4_t acc[TC][TP];
+#pragma unroll
+    for (int ic = 0; ic < TC; ++ic)
+#pragma unroll
+      for (int ip = 0; ip < TP; ++ip) acc[ic][ip] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 3; ++s) {
+      const int tap = 4 * s + chunk;                     // this lane group's tap
+      const int kh = tap / 3, kw = tap - kh * 3;
+      const bool real = tap < 9;
+      bf16x8_t af[TC], bfr[TP];
+#pragma unroll
+      for (int ic = 0; ic < TC; ++ic) af[ic] = *reinterpret_cast<const bf16x8_t*>(Wimg + s * NG * 64 + aoff[ic]);
+      const char* S = Ring + ((r + (real ? kh : 0)) & 3) * SLOT;
+#pragma unroll
+      for (int ip = 0; ip < TP; ++ip) {
+        const int px = wp * WP + ip * 16 + (lane & 15) + (real ? kw : 0);
+        bfr[ip] = *reinterpret_cast<const bf16x8_t*>(S + px * 16);   // weights of taps >= 9 are zero
+      }
+#pragma unroll
+      for (int ic = 0; ic < TC; ++ic)
+#pragma unroll
+        for (int ip = 0; ip < TP; ++ip)
+          acc[ic][ip] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ic], bfr[ip], acc[ic][ip], 0, 0, 0);
+    }
+    const unsigned ybase = (unsigned)(n * a.Ho + h0 + r) * (unsigned)(a.Wo * a.ldy * 2);
+#pragma unroll
+    for (int ip = 0; ip < TP; ++ip)
+#pragma unroll
+      for (int ic = 0; ic < TC; ++ic) {
+        float v0 = acc[ic][ip][0] + bias[ic][0], v1 = acc[ic][ip][1] + bias[ic][1];
+        float v2 = acc[ic][ip][2] + bias[ic][2], v3 = acc[ic][ip][3] + bias[ic][3];
+        if (a.relu) {
+          v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f);
+        }
+        __builtin_amdgcn_raw_buffer_store_b64(u32x2_t{pack_bf2(v0, v1), pack_bf2(v2, v3)}, yr, ybase + yl[ip] + ic * 32, 0, 0);
+      }
+    __builtin_amdgcn_sched_barrier(0);
+    if (r + 1 < nrows) rstore((r + 3) & 3);
+    __syncthreads();
+  }
+}
+
+template <int BP, int RH>
+static int launch_igemm_stream8(const IgemmArgs& a, hipStream_t st) {
+  const int grid = a.N * ((a.Ho + RH - 1) / RH) * (a.Wo / BP);
+  hipLaunchKernelGGL((igemm_stream8_kernel<BP, RH>), dim3(grid), dim3(256), 0, st, a);
+  return (int)hipGetLastError();
 }
 
 template <int BP, int NG, int CS, int RH>
@@ -524,11 +663,13 @@ static int launch_igemm_stream(const IgemmArgs& a, hipStream_t st) {
 }
 
 // Eligible: conv3x3 s1 p1 mode 0, Ngemm and Cs in {32, 64}, Wo % 128 == 0, Ho >= 1.
+// With a.pool set the kernel also writes the 2x2/s2 max-pool of y (floor semantics).
 DPA_API int dpa_igemm_stream(const IgemmArgs* args, int rh, hipStream_t st) {
   const IgemmArgs& a = *args;
   if (a.mode != 0 || a.KH != 3 || a.KW != 3 || a.stride != 1 || a.pad != 1 || (a.ldx & 7) || (a.ldy & 3) ||
-      a.Hs != a.Ho || a.Ws != a.Wo || a.Wo % 128 || a.Kpad < 9 * a.Cs)
+      a.Hs != a.Ho || a.Ws != a.Wo || a.Wo % 128 || a.Kpad < 9 * a.Cs || (a.pool && (a.ldp & 3)))
     return (int)hipErrorInvalidValue;
+  if (a.Cs == 8 && a.Ngemm == 32 && !a.pool) return launch_igemm_stream8<128, 32>(a, st);
   const long blocks32 = (long)a.N * ((a.Ho + 31) / 32) * (a.Wo / 128);
   if (rh == 0) rh = blocks32 >= 1024 ? 32 : 16;
 #define DPA_STREAM(NGv, CSv)                                                                     \

@@ -144,12 +144,12 @@ class HipBlocks:
         return self.packed[c.off_d:c.off_d + c.Cin * c.Kd]
 
     # ------------------------------------------------------------------ primitive launches
-    def conv_fwd(self, c: _Conv, x: torch.Tensor, y: torch.Tensor = None):
+    def conv_fwd(self, c: _Conv, x: torch.Tensor, y: torch.Tensor = None, pool: torch.Tensor = None):
         N, H, W = x.shape[:3]
         if y is None:
             y = torch.empty(N, H, W, c.Cout, dtype=torch.bfloat16, device=x.device)
         K.igemm(x, self.wf(c), y, Ngemm=c.Cout, Kpad=c.Kf, KH=3, KW=3, stride=1, pad=1, Cs=c.Cs, out_grid=(N, H, W),
-                bias=c.mod.bias, relu=True)
+                bias=c.mod.bias, relu=True, pool=pool)
         return y
 
     def conv_dgrad(self, c: _Conv, g: torch.Tensor, mask: torch.Tensor = None, out: torch.Tensor = None):
@@ -268,9 +268,8 @@ class _EncFn(torch.autograd.Function):
         a = B.conv_fwd(c1, x)
         cat = B.new_cat(N, H, W, c2.Cout)
         skip = cat[..., :c2.Cout]
-        B.conv_fwd(c2, a, skip)
         pooled = torch.empty(N, H // 2, W // 2, c2.Cout, dtype=torch.bfloat16, device=x.device)
-        K.maxpool2(skip, pooled)
+        B.conv_fwd(c2, a, skip, pool=pooled)          # max-pool fused into the conv epilogue when streaming
         ctx.B, ctx.l = B, l
         ctx.x_needs_grad = l > 0
         ctx.save_for_backward(x, a, cat)

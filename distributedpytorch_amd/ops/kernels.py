@@ -26,7 +26,7 @@ class IgemmArgs(ctypes.Structure):
     _fields_ = [("x", c_void_p), ("w", c_void_p), ("bias", c_void_p), ("y", c_void_p), ("mask", c_void_p)] + \
                [(n, c_int) for n in ("ldx", "ldy", "ldm", "mask_ch", "N", "Ho", "Wo", "Hs", "Ws", "Cs", "KH", "KW",
                                      "stride", "pad", "Ngemm", "Kpad", "mode", "relu", "accumulate", "Cout")] + \
-               [("xbytes", ctypes.c_uint)]
+               [("xbytes", ctypes.c_uint), ("pool", c_void_p), ("ldp", c_int)]
 
 
 class WgradArgs(ctypes.Structure):
@@ -89,12 +89,13 @@ def _image_chunks(N: int, per_image_bytes: int):
 def igemm(x: torch.Tensor, wpacked: torch.Tensor, y: torch.Tensor, *, Ngemm: int, Kpad: int, KH: int, KW: int,
           stride: int, pad: int, Cs: int, out_grid, bias: Optional[torch.Tensor] = None, relu: bool = False,
           mask: Optional[torch.Tensor] = None, mode: int = 0, Cout: int = 0, accumulate: bool = False, cfg: int = 0,
-          path: str = "auto"):
+          path: str = "auto", pool: Optional[torch.Tensor] = None):
     """Implicit-GEMM conv.  ``out_grid`` = (N, Ho, Wo) pixel grid of GEMM-M.
 
     ``path``: ``auto`` picks, for a conv3x3, the row-streaming kernel (Ngemm, Cs in {32, 64}), then the
     row-halo kernel (Cs % 32 == 0, Ngemm <= 128), then the generic gather kernel (csrc/igemm.hip);
-    ``stream`` / ``halo`` / ``generic`` force one (tests, A/B)."""
+    ``stream`` / ``halo`` / ``generic`` force one (tests, A/B).  ``pool``: also produce the 2x2/s2
+    max-pool of ``y`` (fused into the streaming kernel's epilogue, else a separate pass)."""
     N, Hs, Ws, Cx, ldx = _nhwc(x, "igemm.x")
     _, _, _, Cy, ldy = _nhwc(y, "igemm.y")
     No, Ho, Wo = out_grid
@@ -114,22 +115,32 @@ def igemm(x: torch.Tensor, wpacked: torch.Tensor, y: torch.Tensor, *, Ngemm: int
         mch = min(Cm, Ngemm)
     if bias is not None:
         assert bias.dtype == torch.float32 and bias.is_contiguous() and bias.numel() >= (Cout or Ngemm)
+    ldp = 0
+    if pool is not None:
+        Np, Hp, Wp, Cp, ldp = _nhwc(pool, "igemm.pool")
+        assert (Np, Hp, Wp) == (N, Ho // 2, Wo // 2) and Cp >= Ngemm and mode == 0
     L = _lib.lib()
     st = _stream(y)
+    pool_done = True
     for n0, n1 in _image_chunks(N, max(Hs * Ws * ldx, (4 if mode else 1) * Ho * Wo * ldy) * 2):
         xs, ys = x[n0:n1], y[n0:n1]
         nb = n1 - n0
         a = IgemmArgs(xs.data_ptr(), _p(wpacked).value, None if bias is None else bias.data_ptr(), ys.data_ptr(),
                       None if mask is None else mask[n0:n1].data_ptr(), ldx, ldy, ldm, mch, nb, Ho, Wo, Hs, Ws, Cs,
                       KH, KW, stride, pad, Ngemm, Kpad, mode, int(relu), int(accumulate), Cout,
-                      _extent_bytes(nb, Hs, Ws, Cx, ldx))
+                      _extent_bytes(nb, Hs, Ws, Cx, ldx), None, 0)
         conv3 = mode == 0 and KH == 3 and stride == 1 and cfg == 0
-        if path == "stream" or (path == "auto" and USE_STREAM and conv3 and Ngemm in (32, 64) and Cs in (32, 64)):
+        stream_ok = (Ngemm in (32, 64) and Cs in (32, 64)) or (Ngemm == 32 and Cs == 8 and pool is None)
+        if path == "stream" or (path == "auto" and USE_STREAM and conv3 and stream_ok):
+            if pool is not None:
+                a.pool, a.ldp = pool[n0:n1].data_ptr(), ldp
             err = L.dpa_igemm_stream(ctypes.byref(a), c_int(0), st)
             if err == 0:
                 continue
+            a.pool, a.ldp = None, 0
             if path == "stream":
                 _check(err, "igemm_stream")
+        pool_done = False
         if path == "halo" or (path == "auto" and USE_HALO and conv3 and Cs % 32 == 0 and Ngemm <= 128):
             err = L.dpa_igemm_halo(ctypes.byref(a), c_int(0), st)
             if err == 0:
@@ -137,6 +148,8 @@ def igemm(x: torch.Tensor, wpacked: torch.Tensor, y: torch.Tensor, *, Ngemm: int
             if path == "halo":
                 _check(err, "igemm_halo")
         _check(L.dpa_igemm(ctypes.byref(a), c_int(cfg), st), "igemm")
+    if pool is not None and not pool_done:
+        maxpool2(y, pool)
 
 
 # ------------------------------------------------------------------------------------------ wgrad

@@ -71,6 +71,8 @@ def _pack_one(mode, w, cin_pad=None):
     (1, 3, 128, 32, 64, "stream"), (1, 3, 128, 32, 64, "halo"),
     (2, 20, 128, 64, 64, "stream"),
     (2, 2, 128, 64, 128, "auto"),
+    (2, 5, 128, 3, 32, "stream"),          # first layer (8 padded channels) streaming kernel
+    (1, 34, 256, 3, 32, "auto"),
 ])
 def test_conv3x3_fwd(hip_lib, N, H, W, Cin, Cout, cfg):
     from distributedpytorch_amd.ops import kernels as K
@@ -260,3 +262,22 @@ def test_input_conversion(hip_lib):
     assert tuple(y.shape) == (2, 7, 9, 8)
     assert (y[..., 3:] == 0).all()
     assert _rel(_nchw(y[..., :3].contiguous()), _bf(x)) == 0.0
+
+
+@pytest.mark.parametrize("N,H,W,Cin,Cout", [(2, 34, 128, 32, 32), (1, 9, 128, 64, 64), (1, 6, 256, 32, 64)])
+def test_conv_fused_maxpool(hip_lib, N, H, W, Cin, Cout):
+    """Encoder conv2 writes its output into the concat buffer AND its 2x2 max-pool in one pass."""
+    from distributedpytorch_amd.ops import kernels as K
+    torch.manual_seed(8)
+    x = _bf(torch.randn(N, Cin, H, W))
+    w = _bf(torch.randn(Cout, Cin, 3, 3) * (2.0 / (9 * Cin)) ** 0.5)
+    b = torch.randn(Cout) * 0.1
+    packed, ng, kp = _pack_one(0, w)
+    cat = torch.zeros(N, H, W, 2 * Cout, dtype=torch.bfloat16, device="cuda")
+    pooled = torch.empty(N, H // 2, W // 2, Cout, dtype=torch.bfloat16, device="cuda")
+    K.igemm(_nhwc(x), packed, cat[..., :Cout], Ngemm=ng, Kpad=kp, KH=3, KW=3, stride=1, pad=1, Cs=Cin,
+            out_grid=(N, H, W), bias=b.cuda(), relu=True, pool=pooled)
+    torch.cuda.synchronize()
+    y = _nchw(cat[..., :Cout])
+    assert _rel(y, F.relu(F.conv2d(x, w, b, padding=1))) < 2e-2
+    assert torch.equal(_nchw(pooled), F.max_pool2d(y, 2, 2))      # pool of the stored values, exactly
