@@ -43,8 +43,25 @@ def parse():
     return ap.parse_args()
 
 
+def _heartbeat(period: float = 60.0):
+    """Print a line every ``period`` s (first-iteration kernel compilation in stock MIOpen can take
+    minutes; a silent process looks hung to job supervisors)."""
+    import threading
+
+    t0 = time.time()
+    stop = threading.Event()
+
+    def run():
+        while not stop.wait(period):
+            print(f"[bench] alive {time.time() - t0:.0f}s", file=sys.stderr, flush=True)
+
+    threading.Thread(target=run, daemon=True).start()
+    return stop
+
+
 def main():
     a = parse()
+    hb = _heartbeat()
     import torch
     import torch.distributed as dist
 
@@ -140,6 +157,7 @@ def main():
         if a.out:
             with open(a.out, "a") as f:
                 f.write(line + "\n")
+    hb.set()
     if world > 1:
         dist.destroy_process_group()
 

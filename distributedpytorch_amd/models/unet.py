@@ -218,3 +218,12 @@ def forward_flops(cfg: UNetConfig, h: int, w: int) -> float:
         cin = wd
     fl += 2 * H * W * cfg.base * cfg.out_channels
     return fl
+
+
+if __name__ == "__main__":   # reference smoke self-test (model/unet_model.py:64-67)
+    import sys
+
+    name = sys.argv[1] if len(sys.argv) > 1 else "unet"
+    m = build_model(name)
+    with torch.no_grad():
+        print(m(torch.rand(1, 3, 640, 960)).shape)

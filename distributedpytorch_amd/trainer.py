@@ -345,13 +345,18 @@ def train(cfg: TrainConfig):
 
     t_start = time.time()
     pending = []
+    prof = _Profiler(cfg, strat) if cfg.profile else None
     for epoch in range(start_epoch, cfg.epochs):
         if sampler is not None:
             sampler.set_epoch(epoch)  # A7
         n_img, t_ep = 0, time.perf_counter()
         for images, targets in DeviceBatcher(train_loader, strat.device):
+            if prof is not None:
+                prof.before(step)
             loss = strat.train_step(images, targets)
             step += 1
+            if prof is not None:
+                prof.after(step)
             n_img += images.shape[0]
             if loss is not None:
                 pending.append(loss)
@@ -396,6 +401,37 @@ def train(cfg: TrainConfig):
         paths["loss"] = curves.save(cfg.out_dir, cfg.train_method)
     strat.barrier()
     return {"step": step, "paths": paths, "curves": curves, "strategy": strat}
+
+
+class _Profiler:
+    """``--profile``: torch.profiler (CPU + HIP kernel activity via roctracer) over steps 3..7 of the
+    run; writes a Chrome trace ``logs/<method>_rank<r>_trace.json`` and a per-kernel table
+    ``logs/<method>_rank<r>_kernels.txt``.  For counters use rocprofv3 (see README)."""
+
+    def __init__(self, cfg, strat, start: int = 3, steps: int = 5):
+        self.cfg, self.strat, self.start, self.stop = cfg, strat, start, start + steps
+        self.prof = None
+
+    def before(self, step):
+        if step == self.start and self.prof is None:
+            from torch.profiler import ProfilerActivity, profile
+            acts = [ProfilerActivity.CPU] + ([ProfilerActivity.CUDA] if self.strat.device.type == "cuda" else [])
+            self.prof = profile(activities=acts, record_shapes=False)
+            self.prof.__enter__()
+
+    def after(self, step):
+        if self.prof is not None and step >= self.stop:
+            if self.strat.device.type == "cuda":
+                torch.cuda.synchronize(self.strat.device)
+            self.prof.__exit__(None, None, None)
+            base = os.path.join(self.cfg.out_dir, "logs", f"{self.cfg.train_method}_rank{self.strat.rank}")
+            self.prof.export_chrome_trace(base + "_trace.json")
+            sort = "self_cuda_time_total" if self.strat.device.type == "cuda" else "self_cpu_time_total"
+            with open(base + "_kernels.txt", "w") as f:
+                f.write(self.prof.key_averages().table(sort_by=sort, row_limit=40))
+            log.info(f"profile written to {base}_trace.json")
+            self.prof = None
+            self.start = 1 << 60
 
 
 class _SD:
