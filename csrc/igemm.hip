@@ -21,14 +21,15 @@
 #include "conv_args.h"
 
 template <int BP, int BC, int BK, int WP, int WC>
-__global__ __launch_bounds__(256) void igemm_kernel(IgemmArgs a) {
+__global__ __launch_bounds__(64 * (BP / WP) * (BC / WC)) void igemm_kernel(IgemmArgs a) {
+  constexpr int NT = 64 * (BP / WP) * (BC / WC);   // 4 or 8 waves
   constexpr int CPR = BK / 8;               // 16-byte chunks per LDS row
-  constexpr int RPP = 256 / CPR;            // rows covered by one pass of 256 threads
+  constexpr int RPP = NT / CPR;             // rows covered by one pass of the block
   constexpr int LP = (BP + RPP - 1) / RPP;  // pixel-row loads per thread
   constexpr int LW = (BC + RPP - 1) / RPP;  // weight-row loads per thread
   constexpr int NWC = BC / WC;
   constexpr int NWP = BP / WP;
-  static_assert(NWC * NWP == 4, "4 waves per block");
+  static_assert(NWC * NWP == 4 || NWC * NWP == 8, "4 or 8 waves per block");
   static_assert(BP % RPP == 0 && (BC % RPP == 0 || (BC * CPR) % 64 == 0), "loader tiling");
   constexpr int TP = WP / 16, TC = WC / 16;
   constexpr int RB = BK * 2;                // LDS row bytes
@@ -198,12 +199,13 @@ template <int BP, int BC, int BK, int WP, int WC>
 static int launch_igemm(const IgemmArgs& a, hipStream_t st) {
   const int M = a.N * a.Ho * a.Wo;
   const int grid = ((M + BP - 1) / BP) * (a.Ngemm / BC);
-  hipLaunchKernelGGL((igemm_kernel<BP, BC, BK, WP, WC>), dim3(grid), dim3(256), 0, st, a);
+  hipLaunchKernelGGL((igemm_kernel<BP, BC, BK, WP, WC>), dim3(grid), dim3(64 * (BP / WP) * (BC / WC)), 0, st, a);
   return (int)hipGetLastError();
 }
 
 // cfg: 0 = auto.  Tile families (BP x BC x BK): 1: 128x128x32  2: 128x128x64  3: 128x64x32
 //      4: 128x64x64  5: 256x32x32  6: 256x32x64  7: 64x128x64 (small-M deep layers)
+//      8: 256x128x64 (8 waves)  9: 128x256x64 (8 waves)
 DPA_API int dpa_igemm(const IgemmArgs* args, int cfg, hipStream_t st) {
   IgemmArgs a = *args;
   if ((a.Cs & 7) || (a.ldx & 7) || (a.ldy & 3) || (a.Kpad & 31) || (a.Ngemm & 31)) return (int)hipErrorInvalidValue;
@@ -223,6 +225,8 @@ DPA_API int dpa_igemm(const IgemmArgs* args, int cfg, hipStream_t st) {
     case 5: return launch_igemm<256, 32, 32, 64, 32>(a, st);
     case 6: if (a.Kpad % 64) break; return launch_igemm<256, 32, 64, 64, 32>(a, st);
     case 7: if (a.Ngemm % 128 || a.Kpad % 64) break; return launch_igemm<64, 128, 64, 32, 64>(a, st);
+    case 8: if (a.Ngemm % 128 || a.Kpad % 64) break; return launch_igemm<256, 128, 64, 64, 64>(a, st);   // 8 waves
+    case 9: if (a.Ngemm % 256 || a.Kpad % 64) break; return launch_igemm<128, 256, 64, 64, 64>(a, st);   // 8 waves
     default: break;
   }
   return (int)hipErrorInvalidValue;

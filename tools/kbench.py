@@ -34,6 +34,8 @@ def main():
     ap.add_argument("--img", type=int, default=512)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--only", default="")
+    ap.add_argument("--cfgs", type=int, nargs="*", default=[], help="extra generic tile configs to time")
+    ap.add_argument("--no-wgrad", action="store_true")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     B, S = a.batch, a.img
@@ -54,22 +56,24 @@ def main():
         wd = (torch.randn(Cin * kd, device=dev) * 0.05).to(torch.bfloat16)
         bias = torch.zeros(Cout, device=dev)
         flops = 2.0 * B * H * H * Cin * Cout * 9
-        for path in ("stream", "halo", "generic"):
+        variants = [("stream", 0), ("halo", 0), ("generic", 0)] + [("generic", c) for c in a.cfgs]
+        for path, cfg in variants:
+            label = path if cfg == 0 else f"gen.c{cfg}"
             try:
                 t = timeit(lambda: K.igemm(x, wf, y, Ngemm=Cout, Kpad=kf, KH=3, KW=3, stride=1, pad=1, Cs=Cin,
-                                           out_grid=(B, H, H), bias=bias, relu=True, path=path), a.reps)
-                print(f"{name:14s} fwd   {path:8s} {t:9.1f} us {flops / t / 1e6:7.1f} TF", flush=True)
+                                           out_grid=(B, H, H), bias=bias, relu=True, path=path, cfg=cfg), a.reps)
+                print(f"{name:14s} fwd   {label:8s} {t:9.1f} us {flops / t / 1e6:7.1f} TF", flush=True)
             except Exception as e:  # path not eligible for this shape
-                print(f"{name:14s} fwd   {path:8s}  n/a ({str(e)[:40]})", flush=True)
+                print(f"{name:14s} fwd   {label:8s}  n/a ({str(e)[:40]})", flush=True)
             try:
                 t = timeit(lambda: K.igemm(g, wd, dx, Ngemm=Cin, Kpad=kd, KH=3, KW=3, stride=1, pad=1, Cs=Cout,
-                                           out_grid=(B, H, H), mask=x, path=path), a.reps)
-                print(f"{name:14s} dgrad {path:8s} {t:9.1f} us {flops / t / 1e6:7.1f} TF", flush=True)
+                                           out_grid=(B, H, H), mask=x, path=path, cfg=cfg), a.reps)
+                print(f"{name:14s} dgrad {label:8s} {t:9.1f} us {flops / t / 1e6:7.1f} TF", flush=True)
             except Exception as e:
-                print(f"{name:14s} dgrad {path:8s}  n/a ({str(e)[:40]})", flush=True)
+                print(f"{name:14s} dgrad {label:8s}  n/a ({str(e)[:40]})", flush=True)
         gw = torch.zeros(Cout * Cin * 9, device=dev)
         gb = torch.zeros(Cout, device=dev)
-        for path in ("stream", "halo", "generic"):
+        for path in (() if a.no_wgrad else ("stream", "halo", "generic")):
             try:
                 t = timeit(lambda: K.wgrad(g, x, kind=0, grid=(B, H, H), M=Cout, Nc=Cin, s=1, pad=1, KW=3, gw=gw,
                                            gb=gb, Nreal=Cin, path=path), a.reps)
