@@ -23,9 +23,9 @@ import sys
 import time
 
 BASELINE_METRIC = "images/sec (whole node) UNet 512x512 bf16 at 1/2/4/8 MI355X; Dice parity"
-# measured stock PyTorch-ROCm (MIOpen, bf16 autocast, channels_last) img/s per GPU on MI355X for
-# this exact config, recorded in BASELINE.md; the reference itself publishes no number.
-STOCK_BASELINE_PER_GPU = None
+# measured stock PyTorch-ROCm (MIOpen convs, bf16 autocast, channels_last) img/s per GPU on MI355X for
+# this model at 512x512 (per-GPU batch 8), recorded in BASELINE.md; the reference publishes no number.
+STOCK_BASELINE_PER_GPU = 758.32
 
 
 def parse():
