@@ -46,48 +46,68 @@ __global__ __launch_bounds__(64 * (BP / WP) * (BC / WC)) void igemm_kernel(Igemm
   const int lchunk = tid % CPR;
   const int lrow = tid / CPR;
 
-  // per-thread pixel rows of the loader: decode (n, h, w) once
-  int pn[LP], ph[LP], pw[LP];
-  bool pok[LP];
+  // Per-thread loader state, computed ONCE: each pixel row's byte offset at tap (0,0) and a bit mask
+  // of the taps that land inside the image (zero padding).  When a K-step never straddles a tap
+  // (Cs % BK == 0, every layer except tiny ones) the tap is wave-uniform, so a K-step costs one
+  // scalar division and ~4 VALU per row (the old per-lane divisions and bounds math made the loader
+  // VALU-bound beside the MFMAs).
+  unsigned pbase[LP];
+  unsigned tmask[LP];
+  const int taps = a.KH * a.KW;
 #pragma unroll
   for (int i = 0; i < LP; ++i) {
     const int r = lrow + i * RPP;
     const int m = m0 + r;
-    pok[i] = (r < BP) && (m < M);
-    const int mm = pok[i] ? m : 0;
+    const bool pok = (r < BP) && (m < M);
+    const int mm = pok ? m : 0;
     const int hw = a.Ho * a.Wo;
-    pn[i] = mm / hw;
-    const int rem = mm - pn[i] * hw;
-    ph[i] = rem / a.Wo;
-    pw[i] = rem - ph[i] * a.Wo;
+    const int pn = mm / hw;
+    const int rem = mm - pn * hw;
+    const int ph = rem / a.Wo, pw = rem - (rem / a.Wo) * a.Wo;
+    const int h0 = ph * a.stride - a.pad, w0 = pw * a.stride - a.pad;
+    unsigned msk = 0;
+    for (int t = 0; t < taps; ++t) {
+      const int kh = t / a.KW, kw = t - (t / a.KW) * a.KW;
+      const int ih = h0 + kh, iw = w0 + kw;
+      if (pok && ih >= 0 && ih < a.Hs && iw >= 0 && iw < a.Ws) msk |= 1u << t;
+    }
+    tmask[i] = msk;
+    // offset of (h0, w0) may be "negative" (padding): unsigned wrap-around is undone by the tap delta
+    pbase[i] = (unsigned)((((pn * a.Hs + h0) * a.Ws + w0) * a.ldx) * 2);
   }
-  const int taps = a.KH * a.KW;
   const int S = a.Kpad / BK;
+  const bool uniform_tap = (a.Cs % BK) == 0;
   u32x4_t pr[LP], wr[LW];
 
   // Zero padding by the buffer unit's range check: an out-of-image tap gets an offset beyond
   // num_records and reads 0 -- no branch, no select, every load issued back to back (a branch
   // around each load makes hipcc wait vmcnt(0) per load: guide §5 ".s traps" (c)).
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, 0, (int)a.xbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc((void*)a.w, 0, 0x7fffffff, 0x00020000);
+  unsigned woff[LW];
+#pragma unroll
+  for (int i = 0; i < LW; ++i) woff[i] = (unsigned)(((c0 + lrow + i * RPP) * a.Kpad + lchunk * 8) * 2);
   auto gload = [&](int s) {
-    const int k0 = (s * CPR + lchunk) * 8;
-    const int tap = k0 / a.Cs;
-    const int ci = k0 - tap * a.Cs;
+    int tap, ci;
+    if (uniform_tap) {
+      tap = (s * BK) / a.Cs;                           // wave-uniform (scalar)
+      ci = s * BK - tap * a.Cs + lchunk * 8;
+    } else {
+      const int k0 = (s * CPR + lchunk) * 8;
+      tap = k0 / a.Cs;
+      ci = k0 - tap * a.Cs;
+    }
     const int kh = tap / a.KW, kw = tap - (tap / a.KW) * a.KW;
-    const bool tok = tap < taps;
+    const unsigned delta = (unsigned)(((kh * a.Ws + kw) * a.ldx + ci) * 2);
 #pragma unroll
     for (int i = 0; i < LP; ++i) {
-      const int ih = ph[i] * a.stride + kh - a.pad;
-      const int iw = pw[i] * a.stride + kw - a.pad;
-      const bool ok = pok[i] && tok && ih >= 0 && ih < a.Hs && iw >= 0 && iw < a.Ws;
-      const unsigned off = ok ? (unsigned)((((pn[i] * a.Hs + ih) * a.Ws + iw) * a.ldx + ci) * 2) : 0x80000000u;
-      pr[i] = __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0);
+      const bool ok = tap < taps && ((tmask[i] >> tap) & 1u);
+      pr[i] = __builtin_amdgcn_raw_buffer_load_b128(xr, ok ? pbase[i] + delta : 0x80000000u, 0, 0);
     }
 #pragma unroll
     for (int i = 0; i < LW; ++i) {
-      const int r = lrow + i * RPP;
       if (BC % RPP == 0 || tid < BC * CPR)
-        wr[i] = *reinterpret_cast<const u32x4_t*>(a.w + (long)(c0 + r) * a.Kpad + s * BK + lchunk * 8);
+        wr[i] = __builtin_amdgcn_raw_buffer_load_b128(wrs, woff[i] + s * BK * 2, 0, 0);
     }
   };
   auto lstore = [&](int buf) {
