@@ -168,27 +168,30 @@ __global__ __launch_bounds__(64 * (BP / WP) * (BC / WC)) void igemm_kernel(Igemm
   }
 
   // ------------------------------------------------------------------ epilogue
+  // 32-bit buffer addressing (extents < 2 GiB per launch): no 64-bit pointer math per element.
+  const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc((void*)a.y, 0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t mr = __builtin_amdgcn_make_buffer_rsrc((void*)(a.mask ? a.mask : a.y), 0, 0x7fffffff, 0x00020000);
 #pragma unroll
   for (int ip = 0; ip < TP; ++ip) {
     const int m = m0 + wp * WP + ip * 16 + (lane & 15);
     if (m >= M) continue;
-    long ybase;
+    unsigned ybase;
     if (a.mode == 0) {
-      ybase = (long)m * a.ldy;
+      ybase = (unsigned)m * (unsigned)a.ldy;
     } else {
       const int hw = a.Ho * a.Wo;
       const int n = m / hw, rem = m - n * hw, h = rem / a.Wo, w = rem - (rem / a.Wo) * a.Wo;
-      ybase = ((long)(n * 2 * a.Ho + 2 * h) * (2 * a.Wo) + 2 * w) * a.ldy;
+      ybase = (unsigned)(((n * 2 * a.Ho + 2 * h) * (2 * a.Wo) + 2 * w) * a.ldy);
     }
 #pragma unroll
     for (int ic = 0; ic < TC; ++ic) {
       const int nidx = c0 + wc * WC + ic * 16 + 4 * (lane >> 4);
       int co = nidx;
-      long off = ybase + nidx;
+      unsigned off = ybase + nidx;
       if (a.mode == 1) {
         const int ij = nidx / a.Cout;
         co = nidx - ij * a.Cout;
-        off = ybase + ((long)(ij >> 1) * (2 * a.Wo) + (ij & 1)) * a.ldy + co;
+        off = ybase + (unsigned)(((ij >> 1) * (2 * a.Wo) + (ij & 1)) * a.ldy + co);
       }
       float v0 = acc[ic][ip][0], v1 = acc[ic][ip][1], v2 = acc[ic][ip][2], v3 = acc[ic][ip][3];
       if (a.bias) {
@@ -199,18 +202,17 @@ __global__ __launch_bounds__(64 * (BP / WP) * (BC / WC)) void igemm_kernel(Igemm
         v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f);
       }
       if (a.mask && co < a.mask_ch) {
-        const uint2 mk = *reinterpret_cast<const uint2*>(a.mask + (long)m * a.ldm + co);
+        const u32x2_t mk = __builtin_amdgcn_raw_buffer_load_b64(mr, ((unsigned)m * (unsigned)a.ldm + co) * 2, 0, 0);
         v0 = lo_bf(mk.x) > 0.f ? v0 : 0.f;
         v1 = hi_bf(mk.x) > 0.f ? v1 : 0.f;
         v2 = lo_bf(mk.y) > 0.f ? v2 : 0.f;
         v3 = hi_bf(mk.y) > 0.f ? v3 : 0.f;
       }
-      uint2* dst = reinterpret_cast<uint2*>(a.y + off);
       if (a.accumulate) {
-        const uint2 o = *dst;
+        const u32x2_t o = __builtin_amdgcn_raw_buffer_load_b64(yr, off * 2, 0, 0);
         v0 += lo_bf(o.x); v1 += hi_bf(o.x); v2 += lo_bf(o.y); v3 += hi_bf(o.y);
       }
-      *dst = make_uint2(pack_bf2(v0, v1), pack_bf2(v2, v3));
+      __builtin_amdgcn_raw_buffer_store_b64(u32x2_t{pack_bf2(v0, v1), pack_bf2(v2, v3)}, yr, off * 2, 0, 0);
     }
   }
 }
