@@ -191,6 +191,27 @@ class UNet(nn.Module):
         return self.encoder.blocks() + [self.mid] + self.decoder.blocks()
 
 
+def backward_param_order(model: "UNet") -> List[str]:
+    """Parameter names in the order their gradients become final during backward (head first, then
+    each decoder level conv2 -> conv1 -> up-conv, the bottleneck, the encoder deepest first).
+
+    :class:`..optim.FlatParameterSpace` lays the flat gradient buffer out in this order, so the
+    data-parallel buckets (contiguous slices) complete one after another while the backward is
+    still running; with plain reversed-registration order the decoder's up-convs (registered
+    after all decoder convs) would hold the first buckets back until the decoder had finished."""
+    names = [n for n, _ in model.named_parameters()]
+    order = [n for n in names if n.startswith("segmap.")]
+    for i in range(model.cfg.depth, 0, -1):
+        blk = [n for n in names if n.startswith(f"decoder.conv{i}.")]
+        order += list(reversed(blk))                       # conv_block.2 before conv_block.0 (+BN)
+        order += [n for n in names if n.startswith(f"decoder.deconv{i}.")]
+    order += list(reversed([n for n in names if n.startswith("mid.")]))
+    for i in range(model.cfg.depth, 0, -1):
+        order += list(reversed([n for n in names if n.startswith(f"encoder.conv{i}.")]))
+    rest = [n for n in names if n not in set(order)]
+    return order + rest
+
+
 def build_model(name: str = "unet", **overrides) -> UNet:
     cfg = PRESETS[name]
     if overrides:

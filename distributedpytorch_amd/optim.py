@@ -33,7 +33,12 @@ class FlatParameterSpace:
         else:  # iterable of (name, param)
             named = [(n, p) for n, p in module if p.requires_grad]
         if order == "backward":
-            named = list(reversed(named))
+            if isinstance(module, nn.Module) and hasattr(module, "cfg") and hasattr(module, "decoder"):
+                from .models.unet import backward_param_order
+                rank = {n: i for i, n in enumerate(backward_param_order(module))}
+                named = sorted(named, key=lambda kv: rank.get(kv[0], len(rank)))
+            else:
+                named = list(reversed(named))
         self.names = [n for n, _ in named]
         self.params: List[nn.Parameter] = [p for _, p in named]
         device = torch.device(device) if device is not None else self.params[0].device

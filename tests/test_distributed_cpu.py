@@ -55,7 +55,8 @@ def _ddp_worker(rank, world, port, bucket_mb, q):
     plain = build_model("unet-tiny")
     plain.load_state_dict(st.model.state_dict())
     (bce_dice_from_probs(plain(x), t) * x.shape[0]).backward()
-    local = torch.cat([p.grad.reshape(-1) for p in reversed(list(plain.parameters()))])
+    pg = dict(plain.named_parameters())
+    local = torch.cat([pg[n].grad.reshape(-1) for n in st.space.names])     # flat-buffer layout order
     allg = [torch.zeros_like(local) for _ in range(world)]
     dist.all_gather(allg, local)
     expect = sum(allg) / world
