@@ -340,15 +340,17 @@ DPA_API int dpa_wgrad_halo(const WgradArgs* args, int cfg, hipStream_t st) {
 // once per block in 32 bits, rows only add a wave-uniform scalar, and all global traffic goes
 // through buffer instructions (32-bit offsets, range-checked zero padding, no 64-bit math).
 // LDS images are [.. ][rows][32 channels] 64-B-row nk images (swz_nk<32>, conflict-free).
-template <int BP, int NG, int CS, int RH>
-__global__ __launch_bounds__(256) void igemm_stream_kernel(IgemmArgs a) {
+template <int BP, int NG, int CS, int RH, int WCS>
+__global__ __launch_bounds__(256 * WCS) void igemm_stream_kernel(IgemmArgs a) {
+  constexpr int NT = 256 * WCS;               // 4 waves along the pixels x WCS along the channels
   constexpr int HR = BP + 2;                  // pixels per staged input row
   constexpr int KS = CS / 32;                 // 32-channel slices
   constexpr int WBYTES = 9 * KS * NG * 64;    // [tap][ks][NG][32]
   constexpr int SLOT = KS * HR * 64;          // one input row: [ks][HR][32]
-  constexpr int WP = BP / 4, TP = WP / 16, TC = NG / 16;
+  constexpr int WP = BP / 4, TP = WP / 16, WCN = NG / WCS, TC = WCN / 16;
+  static_assert(TP >= 1 && TC >= 1, "tile");
   constexpr int RCH = KS * HR * 4;            // 16-B chunks per input row
-  constexpr int LR = (RCH + 255) / 256;
+  constexpr int LR = (RCH + NT - 1) / NT;
   __shared__ __attribute__((aligned(16))) char lds[WBYTES + 4 * SLOT];
   char* const Wimg = lds;
   char* const Ring = lds + WBYTES;
@@ -361,13 +363,13 @@ __global__ __launch_bounds__(256) void igemm_stream_kernel(IgemmArgs a) {
   const int hs = rem / stripsW;
   const int w0 = (rem - hs * stripsW) * BP;
   const int h0 = hs * RH;
-  const int tid = threadIdx.x, lane = tid & 63, wp = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wp = (tid >> 6) & 3, wc = tid >> 8;
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, 0, (int)a.xbytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc((void*)a.y, 0, 0x7fffffff, 0x00020000);
   const __amdgpu_buffer_rsrc_t mr = __builtin_amdgcn_make_buffer_rsrc((void*)(a.mask ? a.mask : a.y), 0, 0x7fffffff, 0x00020000);
 
   // resident weights: packed [NG][Kpad] with k = tap*CS + ci
-  for (int c = tid; c < 9 * KS * NG * 4; c += 256) {
+  for (int c = tid; c < 9 * KS * NG * 4; c += NT) {
     const int cc = c & 3, row = (c >> 2) % NG, tk = (c >> 2) / NG;       // tk = tap*KS + ks
     const int tap = tk / KS, ks = tk - tap * KS;
     const u32x4_t v = *reinterpret_cast<const u32x4_t*>(a.w + (long)row * a.Kpad + tap * CS + ks * 32 + cc * 8);
@@ -379,7 +381,7 @@ __global__ __launch_bounds__(256) void igemm_stream_kernel(IgemmArgs a) {
   bool lok[LR];
 #pragma unroll
   for (int j = 0; j < LR; ++j) {
-    const int c = tid + j * 256;
+    const int c = tid + j * NT;
     const int cc = c & 3, px = (c >> 2) % HR, ks = (c >> 2) / HR;
     const int iw = w0 + px - 1;
     lok[j] = c < RCH && iw >= 0 && iw < a.Ws;
@@ -407,7 +409,7 @@ __global__ __launch_bounds__(256) void igemm_stream_kernel(IgemmArgs a) {
   int aoff[TC];
 #pragma unroll
   for (int ic = 0; ic < TC; ++ic) {
-    const int row = ic * 16 + (lane & 15);
+    const int row = wc * WCN + ic * 16 + (lane & 15);
     aoff[ic] = row * 64 + (swz_nk<32>(row, chunk) << 4);
   }
   int boff[TP][3];
@@ -422,13 +424,13 @@ __global__ __launch_bounds__(256) void igemm_stream_kernel(IgemmArgs a) {
 #pragma unroll
   for (int ic = 0; ic < TC; ++ic)
 #pragma unroll
-    for (int e = 0; e < 4; ++e) bias[ic][e] = a.bias ? a.bias[ic * 16 + 4 * chunk + e] : 0.f;
+    for (int e = 0; e < 4; ++e) bias[ic][e] = a.bias ? a.bias[wc * WCN + ic * 16 + 4 * chunk + e] : 0.f;
   unsigned yl[TP], ml[TP];
 #pragma unroll
   for (int ip = 0; ip < TP; ++ip) {
     const int pl = w0 + wp * WP + ip * 16 + (lane & 15);
-    yl[ip] = (unsigned)((pl * a.ldy + 4 * chunk) * 2);
-    ml[ip] = (unsigned)((pl * a.ldm + 4 * chunk) * 2);
+    yl[ip] = (unsigned)((pl * a.ldy + wc * WCN + 4 * chunk) * 2);
+    ml[ip] = (unsigned)((pl * a.ldm + wc * WCN + 4 * chunk) * 2);
   }
   const bool has_mask = a.mask != nullptr;
   // fused 2x2 max-pool (encoder conv2 -> next level input): even rows keep their horizontally
@@ -459,7 +461,7 @@ __global__ __launch_bounds__(256) void igemm_stream_kernel(IgemmArgs a) {
       for (int ip = 0; ip < TP; ++ip)
 #pragma unroll
         for (int ic = 0; ic < TC; ++ic)
-          mk[ip][ic] = (ic * 16 < a.mask_ch) ? __builtin_amdgcn_raw_buffer_load_b64(mr, mbase + ml[ip] + ic * 32, 0, 0)
+          mk[ip][ic] = (wc * WCN + ic * 16 < a.mask_ch) ? __builtin_amdgcn_raw_buffer_load_b64(mr, mbase + ml[ip] + ic * 32, 0, 0)
                                              : u32x2_t{0x3f803f80u, 0x3f803f80u};
     }
     __builtin_amdgcn_sched_barrier(0);
@@ -526,7 +528,7 @@ __global__ __launch_bounds__(256) void igemm_stream_kernel(IgemmArgs a) {
           } else if (hrow < 2 * (a.Ho >> 1) && (lane & 1) == 0) {
             const int pw = (w0 + wp * WP + ip * 16 + (lane & 15)) >> 1;
             const unsigned po = (unsigned)((((n * (a.Ho >> 1) + (hrow >> 1)) * (a.Wo >> 1) + pw) * a.ldp +
-                                            ic * 16 + 4 * chunk) * 2);
+                                            wc * WCN + ic * 16 + 4 * chunk) * 2);
             __builtin_amdgcn_raw_buffer_store_b64(
                 u32x2_t{pack_bf2(fmaxf(q[0], pkeep[ip][ic][0]), fmaxf(q[1], pkeep[ip][ic][1])),
                         pack_bf2(fmaxf(q[2], pkeep[ip][ic][2]), fmaxf(q[3], pkeep[ip][ic][3]))},
@@ -655,27 +657,46 @@ static int launch_igemm_stream8(const IgemmArgs& a, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
-template <int BP, int NG, int CS, int RH>
+template <int BP, int NG, int CS, int RH, int WCS>
 static int launch_igemm_stream(const IgemmArgs& a, hipStream_t st) {
   const int grid = a.N * ((a.Ho + RH - 1) / RH) * (a.Wo / BP);
-  hipLaunchKernelGGL((igemm_stream_kernel<BP, NG, CS, RH>), dim3(grid), dim3(256), 0, st, a);
+  hipLaunchKernelGGL((igemm_stream_kernel<BP, NG, CS, RH, WCS>), dim3(grid), dim3(256 * WCS), 0, st, a);
   return (int)hipGetLastError();
 }
 
-// Eligible: conv3x3 s1 p1 mode 0, Ngemm and Cs in {32, 64}, Wo % 128 == 0, Ho >= 1.
+// Eligible: conv3x3 s1 p1 mode 0, Ngemm and Cs in {32, 64}, Wo % 64 == 0, Ho >= 1.
 // With a.pool set the kernel also writes the 2x2/s2 max-pool of y (floor semantics).
-DPA_API int dpa_igemm_stream(const IgemmArgs* args, int rh, hipStream_t st) {
+// variant: 0 auto, 1: BP128 x 4 waves, 2: BP64 x 4 waves, 3: BP128 x 8 waves, 4: BP64 x 8 waves
+DPA_API int dpa_igemm_stream(const IgemmArgs* args, int variant, hipStream_t st) {
   const IgemmArgs& a = *args;
   if (a.mode != 0 || a.KH != 3 || a.KW != 3 || a.stride != 1 || a.pad != 1 || (a.ldx & 7) || (a.ldy & 3) ||
-      a.Hs != a.Ho || a.Ws != a.Wo || a.Wo % 128 || a.Kpad < 9 * a.Cs || (a.pool && (a.ldp & 3)))
+      a.Hs != a.Ho || a.Ws != a.Wo || a.Wo % 64 || a.Kpad < 9 * a.Cs || (a.pool && (a.ldp & 3)))
     return (int)hipErrorInvalidValue;
-  if (a.Cs == 8 && a.Ngemm == 32 && !a.pool) return launch_igemm_stream8<128, 32>(a, st);
-  const long blocks32 = (long)a.N * ((a.Ho + 31) / 32) * (a.Wo / 128);
-  if (rh == 0) rh = blocks32 >= 1024 ? 32 : 16;
-#define DPA_STREAM(NGv, CSv)                                                                     \
-  if (a.Ngemm == NGv && a.Cs == CSv) {                                                          \
-    if (rh == 32) return launch_igemm_stream<128, NGv, CSv, 32>(a, st);                         \
-    if (rh == 16) return launch_igemm_stream<128, NGv, CSv, 16>(a, st);                         \
+  if (a.Cs == 8 && a.Ngemm == 32 && !a.pool && a.Wo % 128 == 0) return launch_igemm_stream8<128, 32>(a, st);
+  if (variant == 0) {
+    // LDS decides the occupancy: CS=64 rings are twice as large -> narrower strips / more waves
+    if (a.Cs == 32 && a.Ngemm == 32) variant = 1;
+    else if (a.Cs == 64 && a.Ngemm == 32) variant = 2;
+    else if (a.Cs == 32 && a.Ngemm == 64) variant = 3;
+    else variant = 4;
+  }
+  const int bp = (variant == 1 || variant == 3) ? 128 : 64;
+  if (a.Wo % bp) return (int)hipErrorInvalidValue;
+  const long blocks32 = (long)a.N * ((a.Ho + 31) / 32) * (a.Wo / bp);
+  const int rh = blocks32 >= 1024 ? 32 : 16;
+#define DPA_STREAM(NGv, CSv)                                                                               \
+  if (a.Ngemm == NGv && a.Cs == CSv) {                                                                    \
+    switch (variant * 100 + rh) {                                                                         \
+      case 132: return launch_igemm_stream<128, NGv, CSv, 32, 1>(a, st);                                  \
+      case 116: return launch_igemm_stream<128, NGv, CSv, 16, 1>(a, st);                                  \
+      case 232: return launch_igemm_stream<64, NGv, CSv, 32, 1>(a, st);                                   \
+      case 216: return launch_igemm_stream<64, NGv, CSv, 16, 1>(a, st);                                   \
+      case 332: if (NGv % 32) break; return launch_igemm_stream<128, NGv, CSv, 32, 2>(a, st);             \
+      case 316: if (NGv % 32) break; return launch_igemm_stream<128, NGv, CSv, 16, 2>(a, st);             \
+      case 432: if (NGv % 32) break; return launch_igemm_stream<64, NGv, CSv, 32, 2>(a, st);              \
+      case 416: if (NGv % 32) break; return launch_igemm_stream<64, NGv, CSv, 16, 2>(a, st);              \
+      default: break;                                                                                     \
+    }                                                                                                     \
   }
   DPA_STREAM(32, 32)
   DPA_STREAM(32, 64)

@@ -89,7 +89,7 @@ def _image_chunks(N: int, per_image_bytes: int):
 def igemm(x: torch.Tensor, wpacked: torch.Tensor, y: torch.Tensor, *, Ngemm: int, Kpad: int, KH: int, KW: int,
           stride: int, pad: int, Cs: int, out_grid, bias: Optional[torch.Tensor] = None, relu: bool = False,
           mask: Optional[torch.Tensor] = None, mode: int = 0, Cout: int = 0, accumulate: bool = False, cfg: int = 0,
-          path: str = "auto", pool: Optional[torch.Tensor] = None):
+          path: str = "auto", pool: Optional[torch.Tensor] = None, variant: int = 0):
     """Implicit-GEMM conv.  ``out_grid`` = (N, Ho, Wo) pixel grid of GEMM-M.
 
     ``path``: ``auto`` picks, for a conv3x3, the row-streaming kernel (Ngemm, Cs in {32, 64}), then the
@@ -134,7 +134,7 @@ def igemm(x: torch.Tensor, wpacked: torch.Tensor, y: torch.Tensor, *, Ngemm: int
         if path == "stream" or (path == "auto" and USE_STREAM and conv3 and stream_ok):
             if pool is not None:
                 a.pool, a.ldp = pool[n0:n1].data_ptr(), ldp
-            err = L.dpa_igemm_stream(ctypes.byref(a), c_int(0), st)
+            err = L.dpa_igemm_stream(ctypes.byref(a), c_int(variant), st)
             if err == 0:
                 continue
             a.pool, a.ldp = None, 0

@@ -36,6 +36,7 @@ def main():
     ap.add_argument("--only", default="")
     ap.add_argument("--cfgs", type=int, nargs="*", default=[], help="extra generic tile configs to time")
     ap.add_argument("--no-wgrad", action="store_true")
+    ap.add_argument("--svar", type=int, nargs="*", default=[], help="streaming-conv variants to time")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     B, S = a.batch, a.img
@@ -56,18 +57,21 @@ def main():
         wd = (torch.randn(Cin * kd, device=dev) * 0.05).to(torch.bfloat16)
         bias = torch.zeros(Cout, device=dev)
         flops = 2.0 * B * H * H * Cin * Cout * 9
-        variants = [("stream", 0), ("halo", 0), ("generic", 0)] + [("generic", c) for c in a.cfgs]
+        variants = [("stream", 0), ("halo", 0), ("generic", 0)] + [("generic", c) for c in a.cfgs] + \
+            [("stream", -v) for v in a.svar]
         for path, cfg in variants:
-            label = path if cfg == 0 else f"gen.c{cfg}"
+            label = path if cfg == 0 else (f"gen.c{cfg}" if cfg > 0 else f"strm.v{-cfg}")
+            var = -cfg if cfg < 0 else 0
+            cfg = max(cfg, 0)
             try:
                 t = timeit(lambda: K.igemm(x, wf, y, Ngemm=Cout, Kpad=kf, KH=3, KW=3, stride=1, pad=1, Cs=Cin,
-                                           out_grid=(B, H, H), bias=bias, relu=True, path=path, cfg=cfg), a.reps)
+                                           out_grid=(B, H, H), bias=bias, relu=True, path=path, cfg=cfg, variant=var), a.reps)
                 print(f"{name:14s} fwd   {label:8s} {t:9.1f} us {flops / t / 1e6:7.1f} TF", flush=True)
             except Exception as e:  # path not eligible for this shape
                 print(f"{name:14s} fwd   {label:8s}  n/a ({str(e)[:40]})", flush=True)
             try:
                 t = timeit(lambda: K.igemm(g, wd, dx, Ngemm=Cin, Kpad=kd, KH=3, KW=3, stride=1, pad=1, Cs=Cout,
-                                           out_grid=(B, H, H), mask=x, path=path, cfg=cfg), a.reps)
+                                           out_grid=(B, H, H), mask=x, path=path, cfg=cfg, variant=var), a.reps)
                 print(f"{name:14s} dgrad {label:8s} {t:9.1f} us {flops / t / 1e6:7.1f} TF", flush=True)
             except Exception as e:
                 print(f"{name:14s} dgrad {label:8s}  n/a ({str(e)[:40]})", flush=True)
