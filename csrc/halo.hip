@@ -51,40 +51,56 @@ __global__ __launch_bounds__(256) void igemm_halo_kernel(IgemmArgs a) {
 #pragma unroll
     for (int ip = 0; ip < TP; ++ip) acc[ic][ip] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
+  // per-thread staging plan, computed once: global byte offsets (slice 0) + LDS offsets
+  const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)a.w, 0, 0x7fffffff, 0x00020000);
+  unsigned goff[L];
+  int lsto[L];
+  bool isw[L], gok[L];
+#pragma unroll
+  for (int j = 0; j < L; ++j) {
+    const int c = tid + j * 256;
+    isw[j] = c >= PCH;
+    if (c < PCH) {
+      const int row = c >> 2, cc = c & 3;
+      const int kh = row / HR, col = row - kh * HR;
+      const int ih = h + kh - 1, iw = w0 + col - 1;
+      gok[j] = ih >= 0 && ih < a.Hs && iw >= 0 && iw < a.Ws;
+      goff[j] = (unsigned)((((n * a.Hs + ih) * a.Ws + iw) * a.ldx + cc * 8) * 2);
+      lsto[j] = row * 64 + (swz_nk<32>(row, cc) << 4);
+    } else {
+      const int cw = c - PCH, r = cw / 36, k = cw - r * 36;     // k = tap*4 + chunk
+      const int tap = k >> 2, cc = k & 3;
+      gok[j] = c < CH;
+      goff[j] = (unsigned)(((c0 + r) * a.Kpad + tap * a.Cs + cc * 8) * 2);
+      lsto[j] = c < CH ? PBYTES + r * WRB + tap * 64 + (swz_nk<32>(r, cc) << 4) : -1;
+    }
+  }
+  u32x4_t reg[L];
+  auto sload = [&](int s) {
+#pragma unroll
+    for (int j = 0; j < L; ++j) {
+      if (isw[j]) {
+        if (gok[j]) reg[j] = __builtin_amdgcn_raw_buffer_load_b128(wr, goff[j] + s * 64, 0, 0);
+      } else {
+        reg[j] = __builtin_amdgcn_raw_buffer_load_b128(xr, gok[j] ? goff[j] + s * 64 : 0x80000000u, 0, 0);
+      }
+    }
+  };
+  auto sstore = [&]() {
+#pragma unroll
+    for (int j = 0; j < L; ++j)
+      if (lsto[j] >= 0) *reinterpret_cast<u32x4_t*>(lds + lsto[j]) = reg[j];
+  };
+
+  // slices of 32 source channels; slice s+1 is fetched into registers while slice s computes
   const int S = a.Cs / 32;
+  sload(0);
   for (int s = 0; s < S; ++s) {
-    // ---- stage slice s: halo pixels (zero padded by the buffer range check) + weights
-    u32x4_t reg[L];
-#pragma unroll
-    for (int j = 0; j < L; ++j) {
-      const int c = tid + j * 256;
-      if (c < PCH) {
-        const int row = c >> 2, cc = c & 3;
-        const int kh = row / HR, col = row - kh * HR;
-        const int ih = h + kh - 1, iw = w0 + col - 1;
-        const bool ok = ih >= 0 && ih < a.Hs && iw >= 0 && iw < a.Ws;
-        const unsigned off = ok ? (unsigned)((((n * a.Hs + ih) * a.Ws + iw) * a.ldx + s * 32 + cc * 8) * 2) : 0x80000000u;
-        reg[j] = __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0);
-      } else if (c < CH) {
-        const int cw = c - PCH, r = cw / 36, k = cw - r * 36;     // k = tap*4 + chunk
-        const int tap = k >> 2, cc = k & 3;
-        reg[j] = *reinterpret_cast<const u32x4_t*>(a.w + (long)(c0 + r) * a.Kpad + tap * a.Cs + s * 32 + cc * 8);
-      }
-    }
-    if (s > 0) __syncthreads();          // previous slice fully consumed
-#pragma unroll
-    for (int j = 0; j < L; ++j) {
-      const int c = tid + j * 256;
-      if (c < PCH) {
-        const int row = c >> 2, cc = c & 3;
-        *reinterpret_cast<u32x4_t*>(Pimg + row * 64 + (swz_nk<32>(row, cc) << 4)) = reg[j];
-      } else if (c < CH) {
-        const int cw = c - PCH, r = cw / 36, k = cw - r * 36;
-        const int tap = k >> 2, cc = k & 3;
-        *reinterpret_cast<u32x4_t*>(Wimg + r * WRB + tap * 64 + (swz_nk<32>(r, cc) << 4)) = reg[j];
-      }
-    }
+    if (s > 0) __syncthreads();          // slice s-1 fully consumed
+    sstore();
     __syncthreads();
+    if (s + 1 < S) sload(s + 1);
+    __builtin_amdgcn_sched_barrier(0);
     // ---- 9 taps x (TC x TP) MFMAs from LDS
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap) {
@@ -107,6 +123,7 @@ __global__ __launch_bounds__(256) void igemm_halo_kernel(IgemmArgs a) {
         for (int ip = 0; ip < TP; ++ip)
           acc[ic][ip] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ic], bfr[ip], acc[ic][ip], 0, 0, 0);
     }
+    __builtin_amdgcn_sched_barrier(0);
   }
 
   // ---- epilogue (mode 0): bias, ReLU, ReLU-backward mask, accumulate; 8-byte bf16 stores
