@@ -40,6 +40,7 @@ def parse():
     ap.add_argument("--bucket-mb", type=float, default=8.0)
     ap.add_argument("--pool", type=int, default=2, help="distinct synthetic batches cycled")
     ap.add_argument("--out", default=None, help="also append the JSON line to this file")
+    ap.add_argument("--graph", action="store_true", help="N=1: replay the step from a captured HIP graph")
     return ap.parse_args()
 
 
@@ -103,9 +104,14 @@ def main():
         img, mask = synthetic_batch(a.batch, a.img, a.img, 3, seed=1000 * rank + i, device=device)
         pool.append((img, mask.float().unsqueeze(1)))
 
+    graphed = None
+    if a.graph and world == 1:
+        from distributedpytorch_amd.trainer import GraphedStep
+        graphed = GraphedStep(strat, *pool[0])
+
     def step(i):
         x, t = pool[i % len(pool)]
-        return strat.train_step(x, t)
+        return graphed(x, t) if graphed is not None else strat.train_step(x, t)
 
     t_w0 = time.perf_counter()
     loss = None
@@ -147,7 +153,8 @@ def main():
         "config": {"model": f"{a.model} (reference 4-level UNet, base 32, {nparams} params)" if a.model == "unet"
                    else a.model, "global_batch": a.batch * world, "per_gpu_batch": a.batch,
                    "seq_len": a.img * a.img, "image_hw": [a.img, a.img],
-                   "parallelism": f"dp{world}", "backend": backend, "bucket_mb": a.bucket_mb},
+                   "parallelism": f"dp{world}", "backend": backend, "bucket_mb": a.bucket_mb,
+                   "hip_graph": graphed is not None},
         "final_loss": round(final_loss, 5), "warmup_s": round(warm_s, 2),
         "peak_mem_gb": round(torch.cuda.max_memory_allocated(device) / 2 ** 30, 2),
     }

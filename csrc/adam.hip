@@ -3,9 +3,18 @@
 // Memory-bound: 4 streams in (p, g, m, v) + 3 out -> float4 per lane, grid-stride, one launch per step.
 #include "common.h"
 
+// DEV: hyper-parameters read from a device state block (HIP-graph replay: the captured launch cannot
+// bake host scalars that change every step); state = {step, lr, 1/bc1, 1/sqrt(bc2)} in fp64.
+template <bool DEV>
 __global__ __launch_bounds__(256) void adam_flat_kernel(
     float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m, float* __restrict__ v,
-    long long n, float lr, float b1, float b2, float eps, float wd, float inv_bc1, float inv_sqrt_bc2) {
+    long long n, float lr, float b1, float b2, float eps, float wd, float inv_bc1, float inv_sqrt_bc2,
+    const double* __restrict__ state) {
+  if constexpr (DEV) {
+    lr = (float)state[1];
+    inv_bc1 = (float)state[2];
+    inv_sqrt_bc2 = (float)state[3];
+  }
   const long long n4 = n >> 2;
   const long long stride = (long long)gridDim.x * blockDim.x;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
@@ -40,8 +49,27 @@ DPA_API int dpa_adam_flat(float* p, const float* g, float* m, float* v, long lon
                           float b2, float eps, float wd, float bc1, float bc2, hipStream_t stream) {
   if (n <= 0) return 0;
   int grid = dpa_grid((n + 3) / 4, 256, 4096);
-  hipLaunchKernelGGL(adam_flat_kernel, dim3(grid), dim3(256), 0, stream, p, g, m, v, n, lr, b1, b2, eps, wd,
-                     1.f / bc1, 1.f / sqrtf(bc2));
+  hipLaunchKernelGGL(adam_flat_kernel<false>, dim3(grid), dim3(256), 0, stream, p, g, m, v, n, lr, b1, b2, eps,
+                     wd, 1.f / bc1, 1.f / sqrtf(bc2), nullptr);
+  return (int)hipGetLastError();
+}
+
+// state[0] += 1 and the bias corrections of the new step, in fp64 (same rounding as the host path)
+__global__ void adam_tick_kernel(double* state, double b1, double b2) {
+  const double t = state[0] + 1.0;
+  state[0] = t;
+  state[2] = 1.0 / (1.0 - pow(b1, t));
+  state[3] = 1.0 / sqrt(1.0 - pow(b2, t));
+}
+
+// graph-capturable step: tick + update, all hyper-parameters from `state` (lr = state[1], set by the host)
+DPA_API int dpa_adam_flat_dev(float* p, const float* g, float* m, float* v, long long n, double* state, double b1,
+                              double b2, float eps, float wd, hipStream_t stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(adam_tick_kernel, dim3(1), dim3(1), 0, stream, state, b1, b2);
+  int grid = dpa_grid((n + 3) / 4, 256, 4096);
+  hipLaunchKernelGGL(adam_flat_kernel<true>, dim3(grid), dim3(256), 0, stream, p, g, m, v, n, 0.f, (float)b1,
+                     (float)b2, eps, wd, 0.f, 0.f, (const double*)state);
   return (int)hipGetLastError();
 }
 

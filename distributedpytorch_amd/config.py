@@ -52,7 +52,11 @@ class TrainConfig:
     save_every_epoch: bool = True
     resume: bool = False
     profile: bool = False
-    cuda_graph: bool = False
+    cuda_graph: bool = False                         # singleGPU: replay the whole step from a HIP graph
+    debug_sync: bool = False                         # synchronise after every kernel / stage op
+    watchdog: float = 0.0                            # abort if no step completes for N seconds (0 = off)
+    comm_timeout: float = 1800.0                     # process-group (RCCL/gloo) collective timeout, seconds
+    nan_policy: str = "raise"                        # non-finite loss: raise | warn | ignore
 
     def to_dict(self):
         return asdict(self)
@@ -93,6 +97,12 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--resume", action="store_true", help="resume from checkpoints/<method>_last.pt")
     p.add_argument("--profile", action="store_true", help="torch.profiler trace of a few steps")
     p.add_argument("--cuda-graph", action="store_true", help="capture the training step in a HIP graph")
+    p.add_argument("--debug-sync", action="store_true",
+                   help="synchronise after every HIP kernel and pipeline stage op (race / fault triage)")
+    p.add_argument("--watchdog", type=float, default=0.0,
+                   help="abort (exit 124, for torchrun --max-restarts + --resume) after N s without a step")
+    p.add_argument("--comm-timeout", type=float, default=1800.0, help="collective timeout in seconds")
+    p.add_argument("--nan-policy", choices=["raise", "warn", "ignore"], default="raise")
     return p
 
 
@@ -109,7 +119,8 @@ def parse_args(argv=None) -> TrainConfig:
         synthetic_len=a.synthetic_len, data_dir=a.data_dir, out_dir=a.out_dir, device=a.device,
         stages=a.stages, microbatches=a.microbatches, bucket_mb=a.bucket_mb, global_dice=a.global_dice,
         loss_scale_by_batch=a.loss_scale_by_batch, max_steps=a.max_steps, num_workers=a.num_workers,
-        log_every=a.log_every, resume=a.resume, profile=a.profile, cuda_graph=a.cuda_graph)
+        log_every=a.log_every, resume=a.resume, profile=a.profile, cuda_graph=a.cuda_graph,
+        debug_sync=a.debug_sync, watchdog=a.watchdog, comm_timeout=a.comm_timeout, nan_policy=a.nan_policy)
     return cfg
 
 

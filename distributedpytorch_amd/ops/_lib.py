@@ -51,7 +51,7 @@ def lib():
 def _declare(L):
     for name in ("dpa_version", "dpa_igemm", "dpa_wgrad", "dpa_wgrad_reduce", "dpa_input_nhwc8", "dpa_maxpool2",
                  "dpa_pool_bwd", "dpa_pack_weights", "dpa_head_fwd", "dpa_head_bwd", "dpa_adam_flat",
-                 "dpa_igemm_halo", "dpa_wgrad_halo", "dpa_igemm_stream", "dpa_wgrad_stream"):
+                 "dpa_igemm_halo", "dpa_wgrad_halo", "dpa_igemm_stream", "dpa_wgrad_stream", "dpa_adam_flat_dev"):
         getattr(L, name).restype = ctypes.c_int
     L.dpa_head_slab_blocks.restype = ctypes.c_int
     L.dpa_head_slab_blocks.argtypes = [ctypes.c_longlong]
@@ -59,10 +59,32 @@ def _declare(L):
 
 
 def check(err: int, name: str):
+    """Raise on a launch error.  Under debug-sync (``--debug-sync`` / ``DPA_DEBUG_SYNC=1``) also wait
+    for the kernel and attribute any asynchronous fault to ``name`` (stream-ordering / race triage:
+    every launch becomes a synchronisation point)."""
     if err != 0:
         L = lib()
         msg = L.dpa_error_string(err).decode()
         raise RuntimeError(f"{name} failed: hip error {err} ({msg})")
+    if _DEBUG_SYNC[0]:
+        import torch
+        if torch.cuda.is_current_stream_capturing():
+            return
+        try:
+            torch.cuda.synchronize()
+        except RuntimeError as e:
+            raise RuntimeError(f"{name}: asynchronous fault detected right after launch: {e}") from e
+
+
+_DEBUG_SYNC = [os.environ.get("DPA_DEBUG_SYNC", "0") == "1"]
+
+
+def set_debug_sync(on: bool):
+    _DEBUG_SYNC[0] = bool(on)
+
+
+def debug_sync() -> bool:
+    return _DEBUG_SYNC[0]
 
 
 def stream_ptr(device=None) -> int:

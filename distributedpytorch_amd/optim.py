@@ -130,6 +130,25 @@ class FusedAdam(torch.optim.Optimizer):
         self.exp_avg_sq = [torch.zeros_like(s.data) for s in self.spaces]
         self.step_count = 0
         self.use_kernel = use_kernel
+        self.device_state = False
+        self._dev_state: List[torch.Tensor] = []
+        self._dev_lr = None
+
+    def enable_device_state(self):
+        """Keep (step, lr, bias corrections) in a per-space fp64 device block that the step kernel
+        updates itself: the launch sequence is then identical every step and can be captured once in
+        a HIP graph.  The host mirror ``step_count`` is kept by the caller of the replay."""
+        if not self.device_state:
+            self.device_state = True
+            self._dev_state = [torch.zeros(4, dtype=torch.float64, device=s.data.device) for s in self.spaces]
+        self.sync_device_state()
+
+    def sync_device_state(self):
+        """Upload the host step count and lr (after a restore, a resume or an LR plateau cut)."""
+        lr = float(self.param_groups[0]["lr"])
+        for st in self._dev_state:
+            st.copy_(torch.tensor([float(self.step_count), lr, 0.0, 0.0], dtype=torch.float64))
+        self._dev_lr = lr
 
     @property
     def space(self) -> FlatParameterSpace:
@@ -148,6 +167,16 @@ class FusedAdam(torch.optim.Optimizer):
         lr, eps, wd = g["lr"], g["eps"], g["weight_decay"]
         bc1 = 1 - b1 ** self.step_count
         bc2 = 1 - b2 ** self.step_count
+        if self.device_state:
+            from . import ops
+            if lr != self._dev_lr and not _capturing(self.spaces[0].data):
+                self.step_count -= 1
+                self.sync_device_state()
+                self.step_count += 1
+            for s, m, v, st in zip(self.spaces, self.exp_avg, self.exp_avg_sq, self._dev_state):
+                s.touch()
+                ops.adam_step_dev(s.data, s.grad, m, v, st, beta1=b1, beta2=b2, eps=eps, weight_decay=wd)
+            return loss
         for s, m, v in zip(self.spaces, self.exp_avg, self.exp_avg_sq):
             s.touch()
             use_k = s.data.is_cuda if self.use_kernel is None else self.use_kernel
@@ -174,6 +203,12 @@ class FusedAdam(torch.optim.Optimizer):
             v.copy_(src)
         for g, s in zip(self.param_groups, sd["param_groups"]):
             g.update(s)
+        if self.device_state:
+            self.sync_device_state()
+
+
+def _capturing(t: torch.Tensor) -> bool:
+    return t.is_cuda and torch.cuda.is_current_stream_capturing()
 
 
 @torch.no_grad()

@@ -35,6 +35,14 @@ from ..models.blocks import boundary_names, block_kind, n_blocks, partition, run
 from ..optim import FlatParameterSpace
 
 
+def _debug_point(device):
+    """Debug-sync mode (``--debug-sync``): drain the device after every stage op so a
+    stream-ordering race between compute and the send/recv streams shows up at its source."""
+    from ..ops._lib import debug_sync
+    if debug_sync() and device is not None and torch.device(device).type == "cuda":
+        torch.cuda.synchronize(device)
+
+
 def _block_param_prefixes(idx: int, depth: int) -> List[str]:
     kind, i = block_kind(idx, depth)
     if kind == "enc":
@@ -192,6 +200,7 @@ class GPipeDist:
                 leaves = {k: v.detach().requires_grad_(True) for k, v in bufs.items()}
                 env = dict(leaves)
             out = self.stage.forward(env, ts[m], "partials")
+            _debug_point(self.device)
             saved_in.append(leaves)
             if self.is_last:
                 partials.append(out["partials"])
@@ -227,6 +236,7 @@ class GPipeDist:
                 for wk in works:
                     wk.wait()
                 torch.autograd.backward(outs, [g.to(o.dtype) for o, g in zip(outs, grads)])
+            _debug_point(self.device)
             if not self.is_first:
                 for name, src in self.recv_spec[self.rank]:
                     gr = saved_in[m][name].grad
@@ -317,7 +327,9 @@ class GPipeLocal:
             target = target.to(dev, non_blocking=True)
         ctx = torch.cuda.device(dev) if dev.type == "cuda" else _Null()
         with ctx:
-            return run_segment(self.stage_blocks[s], self.cuts[s], self.cuts[s + 1], self.depth, env, target, want)
+            out = run_segment(self.stage_blocks[s], self.cuts[s], self.cuts[s + 1], self.depth, env, target, want)
+        _debug_point(dev)
+        return out
 
     def forward_partials(self, images, targets):
         M, S = self.M, self.S

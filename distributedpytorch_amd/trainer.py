@@ -11,6 +11,7 @@ the reference wrote them) and ``loss/<method>/{train,val}_loss.pkl``.
 """
 from __future__ import annotations
 
+import datetime
 import logging
 import os
 import time
@@ -32,6 +33,7 @@ from .parallel.dp import ReplicatedDataParallel
 from .parallel.pipeline import GPipeDist, GPipeLocal
 from .utils import LossCurves, MetricsLogger, load_model_state, save_model, set_seed
 from .utils.checkpoint import load_training_state, save_training_state
+from .utils.resilience import ShutdownGuard, StepWatchdog, check_finite, comm_env_defaults
 
 log = logging.getLogger("dpa")
 
@@ -272,7 +274,9 @@ def build_strategy(cfg: TrainConfig, model) -> Strategy:
             backend = os.environ.get("DPA_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
             if torch.cuda.is_available():
                 torch.cuda.set_device(local)   # A15: bind each rank to its own GPU
-            dist.init_process_group(backend=backend, init_method="env://")
+            comm_env_defaults()
+            dist.init_process_group(backend=backend, init_method="env://",
+                                    timeout=datetime.timedelta(seconds=cfg.comm_timeout))
         device = torch.device(f"cuda:{local}") if torch.cuda.is_available() else torch.device("cpu")
         return DDPStrategy(cfg, model, device) if m == "DDP" else PipelineDistStrategy(cfg, model, device)
     if m == "singleGPU":
@@ -315,6 +319,9 @@ def _setup_logging(cfg, rank):
 
 def train(cfg: TrainConfig):
     rank, local, world = dist_env()
+    if cfg.debug_sync:
+        from .ops._lib import set_debug_sync
+        set_debug_sync(True)
     set_seed(cfg.seed)
     _setup_logging(cfg, rank)
     log.info("UNet for Carvana Image Masking (Segmentation)")
@@ -346,6 +353,12 @@ def train(cfg: TrainConfig):
     t_start = time.time()
     pending = []
     prof = _Profiler(cfg, strat) if cfg.profile else None
+    guard = ShutdownGuard()
+    dog = StepWatchdog(cfg.watchdog) if cfg.watchdog > 0 else None
+    graphed = None
+    if cfg.cuda_graph and not GraphedStep.supported(strat):
+        log.warning(f"--cuda-graph: not supported for {strat.name} on {strat.device}; running eagerly")
+    stop_signal = None
     for epoch in range(start_epoch, cfg.epochs):
         if sampler is not None:
             sampler.set_epoch(epoch)  # A7
@@ -353,24 +366,45 @@ def train(cfg: TrainConfig):
         for images, targets in DeviceBatcher(train_loader, strat.device):
             if prof is not None:
                 prof.before(step)
-            loss = strat.train_step(images, targets)
+            if cfg.cuda_graph and graphed is None and GraphedStep.supported(strat):
+                graphed = GraphedStep(strat, images, targets)
+            if graphed is not None and graphed.matches(images, targets):
+                loss = graphed(images, targets)
+            else:
+                loss = strat.train_step(images, targets)
             step += 1
+            if dog is not None:
+                dog.kick(step)
             if prof is not None:
                 prof.after(step)
             n_img += images.shape[0]
             if loss is not None:
                 pending.append(loss)
-            if step % cfg.log_every == 0 and pending:
-                vals = torch.stack([p.float().to("cpu") for p in pending]).numpy()
-                mean_loss = float(np.mean(vals[-10:]))
-                pending = []
-                curves.add_train(step, time.time() - t_start, mean_loss)
-                metrics.log(kind="train", step=step, epoch=epoch, loss=mean_loss,
-                            lr=strat.optimizer.param_groups[0]["lr"])
-                if strat.is_main:
-                    log.info(f"step {step} loss {mean_loss:.5f}")
+            if step % cfg.log_every == 0:
+                if pending:
+                    vals = torch.stack([p.float().to("cpu") for p in pending]).numpy()
+                    if cfg.nan_policy != "ignore":
+                        check_finite(vals.tolist(), step, cfg.nan_policy)
+                    mean_loss = float(np.mean(vals[-10:]))
+                    pending = []
+                    curves.add_train(step, time.time() - t_start, mean_loss)
+                    metrics.log(kind="train", step=step, epoch=epoch, loss=mean_loss,
+                                lr=strat.optimizer.param_groups[0]["lr"])
+                    if strat.is_main:
+                        log.info(f"step {step} loss {mean_loss:.5f}")
+                stop_signal = _agree_stop(strat, guard.requested)
+                if stop_signal is not None:
+                    break
             if cfg.max_steps and step >= cfg.max_steps:
                 break
+        if stop_signal is not None:
+            # SIGTERM/SIGUSR1 (e.g. torchrun tearing the job down): save where we are and leave
+            sd_model = strat.state_dict()
+            if strat.rank == 0 and sd_model is not None:
+                save_training_state(last_path, model=_SD(sd_model), optimizer=strat.optimizer,
+                                    scheduler=scheduler, epoch=epoch, step=step)
+            log.warning(f"stopped by signal {stop_signal} at step {step}; state saved to {last_path}")
+            break
         ep_time = time.perf_counter() - t_ep
         val_loss, val_dice = evaluate(strat, val_loader)
         curves.add_val(step, time.time() - t_start, val_loss)
@@ -390,6 +424,13 @@ def train(cfg: TrainConfig):
                                     scheduler=scheduler, epoch=epoch + 1, step=step)
         if cfg.max_steps and step >= cfg.max_steps:
             break
+    guard.close()
+    if dog is not None:
+        dog.close()
+    if stop_signal is not None:
+        strat.barrier()
+        return {"step": step, "paths": {"last": last_path}, "curves": curves, "strategy": strat,
+                "stopped_by_signal": stop_signal}
 
     sd = strat.state_dict()
     paths = {}
@@ -401,6 +442,82 @@ def train(cfg: TrainConfig):
         paths["loss"] = curves.save(cfg.out_dir, cfg.train_method)
     strat.barrier()
     return {"step": step, "paths": paths, "curves": curves, "strategy": strat}
+
+
+def _agree_stop(strat, requested):
+    """All ranks stop at the same step boundary if any of them was signalled (a rank leaving alone
+    would strand its peers inside the next collective)."""
+    flag = 0 if requested is None else int(requested)
+    if strat.world > 1 and dist.is_initialized():
+        dev = strat.device if dist.get_backend() == "nccl" else torch.device("cpu")
+        t = torch.tensor([flag], dtype=torch.int64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        flag = int(t.item())
+    return flag or None
+
+
+class GraphedStep:
+    """``--cuda-graph``: the whole singleGPU training step — weight packing, forward, fused loss,
+    backward (explicit per-block HIP kernels), Adam — captured once in a HIP graph and replayed
+    (one ``hipGraphLaunch`` instead of ~130 kernel launches + the Python autograd walk per step).
+
+    Adam runs in device-state mode (step count / lr / bias corrections in a device block the
+    captured kernels update), new LR values are uploaded before a replay, and batches of another
+    shape (a short last batch) fall back to the eager step.  Capture needs one eager warm-up step
+    (lazy allocations); its effect on parameters and optimizer state is rolled back."""
+
+    @staticmethod
+    def supported(strat) -> bool:
+        return type(strat) is SingleDevice and strat.device.type == "cuda"
+
+    def __init__(self, strat, images, targets):
+        self.strat = strat
+        opt, space = strat.optimizer, strat.space
+        opt.enable_device_state()
+        self.x = images.detach().clone()
+        self.t = targets.detach().clone()
+        snap = (space.data.clone(), [m.clone() for m in opt.exp_avg], [v.clone() for v in opt.exp_avg_sq],
+                opt.step_count)
+        side = torch.cuda.Stream(strat.device)
+        side.wait_stream(torch.cuda.current_stream(strat.device))
+        with torch.cuda.stream(side):
+            strat.train_step(self.x, self.t)
+        torch.cuda.current_stream(strat.device).wait_stream(side)
+        torch.cuda.synchronize(strat.device)
+        self._restore(snap)
+        space.touch()                    # the captured forward must repack the weights
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.loss = strat.train_step(self.x, self.t)
+        opt.step_count = snap[3]         # capture recorded kernels but ran none
+        opt.sync_device_state()
+        log.info(f"captured the training step in a HIP graph (batch {tuple(images.shape)})")
+
+    def _restore(self, snap):
+        opt, space = self.strat.optimizer, self.strat.space
+        space.data.copy_(snap[0])
+        for m, s in zip(opt.exp_avg, snap[1]):
+            m.copy_(s)
+        for v, s in zip(opt.exp_avg_sq, snap[2]):
+            v.copy_(s)
+        opt.step_count = snap[3]
+        opt.sync_device_state()
+        space.touch()
+
+    def matches(self, images, targets) -> bool:
+        return images.shape == self.x.shape and targets.shape == self.t.shape
+
+    def __call__(self, images, targets):
+        opt = self.strat.optimizer
+        if float(opt.param_groups[0]["lr"]) != opt._dev_lr:
+            opt.sync_device_state()
+        if images.data_ptr() != self.x.data_ptr():
+            self.x.copy_(images, non_blocking=True)
+            self.t.copy_(targets, non_blocking=True)
+        self.graph.replay()
+        opt.step_count += 1
+        self.strat.space.touch()         # eager users (eval) must see the updated weights
+        return self.loss.clone()
 
 
 class _Profiler:

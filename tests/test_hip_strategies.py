@@ -83,3 +83,56 @@ def test_train_step_loss_decreases(hip_lib):
     st = SingleDevice(TrainConfig(backend="hip", lr=1e-3), build_model("unet"), "cuda:0")
     losses = [st.train_step(x, t).item() for _ in range(8)]
     assert losses[-1] < losses[0], losses
+
+
+def test_graphed_step_matches_eager(hip_lib):
+    """--cuda-graph: replaying the captured step (pack, fwd, loss, bwd, Adam) gives the eager
+    trajectory, including an LR change between replays and an eager fallback batch."""
+    from distributedpytorch_amd.config import TrainConfig
+    from distributedpytorch_amd.models.unet import build_model
+    from distributedpytorch_amd.trainer import GraphedStep, SingleDevice
+    torch.manual_seed(4)
+    a, b = build_model("unet"), build_model("unet")
+    b.load_state_dict(a.state_dict())
+    batches = [_batch(4, 64) for _ in range(3)]
+    ea = SingleDevice(TrainConfig(backend="hip", lr=1e-3), a, "cuda:0")
+    gb = SingleDevice(TrainConfig(backend="hip", lr=1e-3), b, "cuda:0")
+    ea.optimizer.enable_device_state()
+    g = GraphedStep(gb, *batches[0])
+    la, lb = [], []
+    for k in range(5):
+        if k == 3:
+            ea.optimizer.param_groups[0]["lr"] = gb.optimizer.param_groups[0]["lr"] = 3e-4
+        x, t = batches[k % 3]
+        la.append(ea.train_step(x, t))
+        lb.append(g(x, t))
+    xs, ts = _batch(2, 64)        # other shape -> eager step on the graphed strategy
+    la.append(ea.train_step(xs, ts))
+    assert not g.matches(xs, ts)
+    lb.append(gb.train_step(xs, ts))
+    torch.cuda.synchronize()
+    assert gb.optimizer.step_count == ea.optimizer.step_count == 6
+    for u, v in zip(la, lb):
+        assert abs(u.item() - v.item()) <= 1e-5 * abs(u.item()), (la, lb)
+    torch.testing.assert_close(gb.space.data, ea.space.data, rtol=1e-5, atol=1e-6)
+
+
+def test_step_is_deterministic_and_debug_sync_invariant(hip_lib):
+    """Race triage: the same step from the same state gives bitwise-identical gradients, with and
+    without per-launch synchronisation (a stream-ordering race or an LDS race shows up here)."""
+    from distributedpytorch_amd.ops._lib import set_debug_sync
+    from distributedpytorch_amd.models.unet import build_model
+    torch.manual_seed(5)
+    model = build_model("unet").cuda()
+    x, t = _batch(4, 64)
+    grads = []
+    for dbg in (False, False, True):
+        set_debug_sync(dbg)
+        try:
+            _, g = _single(model, x, t)
+        finally:
+            set_debug_sync(False)
+        grads.append(g)
+    for n in grads[0]:
+        assert torch.equal(grads[0][n], grads[1][n]), n
+        assert torch.equal(grads[0][n], grads[2][n]), n

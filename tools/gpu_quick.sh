@@ -5,8 +5,10 @@ cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 python -c "import __graft_entry__ as g; g.build()" > gpurun_out/build.log 2>&1 || { tail gpurun_out/build.log; exit 1; }
+if [ -n "$PYTEST" ]; then timeout -k 10 600 python -m pytest $PYTEST > gpurun_out/pytest_sel.log 2>&1; rc=$?; echo "pytest rc=$rc"; tail -15 gpurun_out/pytest_sel.log; [ $rc -ne 0 ] && exit $rc; fi
 if [ -n "$KBENCH" ]; then timeout -k 10 400 python tools/kbench.py $KBENCH > gpurun_out/kbench.log 2>&1; rc=$?; echo "kbench rc=$rc"; grep -v amdgpu gpurun_out/kbench.log; [ $rc -ne 0 ] && exit $rc; fi
 if [ -n "$BENCH" ]; then timeout -k 10 300 python bench.py $BENCH > gpurun_out/bench.log 2>&1; rc=$?; echo "bench rc=$rc"; tail -1 gpurun_out/bench.log; [ $rc -ne 0 ] && exit $rc; fi
+if [ -n "$BENCH2" ]; then timeout -k 10 300 python bench.py $BENCH2 > gpurun_out/bench2.log 2>&1; rc=$?; echo "bench2 rc=$rc"; tail -1 gpurun_out/bench2.log; [ $rc -ne 0 ] && exit $rc; fi
 if [ -n "$PROF" ]; then
   R=$PWD; rm -rf gpurun_out/prof
   (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof -o run -- python3 $R/bench.py $PROF > $R/gpurun_out/prof.log 2>&1); echo "prof rc=$?"
