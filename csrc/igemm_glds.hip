@@ -1,0 +1,225 @@
+// Implicit-GEMM convolution with LDS-DMA staging (gfx950), for the deep UNet layers
+// (64x64 / 32x32 grids, 256-1024 channels: enc.conv4, mid, dec.conv1 and the transposed convs;
+// SURVEY §2.5 K1/K2/K6, reference model/unet_parts.py:10-12,51-54).
+//
+// Why a second GEMM core: the register-staged kernel in igemm.hip spends more LDS cycles than
+// MFMA cycles per K-step -- ds_write_b128 moves only ~79 B/clk/CU (MI355X_MICROARCH §LDS) and a
+// 128x128x64 step writes 32 KB and reads 64 KB -- so it stalls near 800 TF.  Here both operands go
+// HBM/L2 -> LDS by `buffer_load_dwordx4 ... lds` (no VGPR round trip, no ds_write), three stages
+// deep, with counted `s_waitcnt vmcnt(N)` + raw `s_barrier` so two K-steps of loads stay in flight
+// across each barrier (cdna_hip_programming.md "Pipelining across barriers").
+//
+// Tile: BC (output channels = rows of the packed weights) x BP (pixels) x 64 (K), 8 waves.
+// LDS images are [rows][64] bf16 (128-B rows) with the 16-B chunk XOR swizzle swz_nk<64>; the DMA
+// writes lane-linearly, so the swizzle is applied on the SOURCE address (lane l of a wave fetches
+// chunk (l&7) ^ (row&7) of its row and lands in slot l&7).  Zero padding / M tail: the buffer
+// unit's range check (offset 0x80000000 -> zeros written to LDS), no branches in the loader.
+// Epilogue = igemm.hip's (bias, ReLU, ReLU-backward mask, accumulate, transposed-conv scatter).
+#include "common.h"
+
+#include "conv_args.h"
+
+namespace {
+
+constexpr int BK = 64;
+constexpr int RBY = BK * 2;   // bytes per LDS row
+
+// 16-B LDS-DMA: lane l's bytes land at lds + 16*l.  (Wrapped in a __device__ function: used
+// directly inside a kernel template the builtin makes the host pass drop the kernel's launch stub.)
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, char* lds, unsigned voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, voff, 0, 0, 0);
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+}  // namespace
+
+template <int BC, int BP, int WC, int WP, int ST>
+__global__ __launch_bounds__(512) void igemm_glds_kernel(IgemmArgs a) {
+  constexpr int NWC = BC / WC, NWP = BP / WP;
+  static_assert(NWC * NWP == 8, "8 waves");
+  constexpr int RA = BC / 64, RP = BP / 64;   // DMA rounds per stage per wave (64 rows per block round)
+  constexpr int LPS = RA + RP;                // DMA instructions per stage per wave
+  constexpr int TC = WC / 16, TP = WP / 16;
+  constexpr int STAGE = (BC + BP) * RBY;
+  __shared__ __attribute__((aligned(16))) char lds[ST * STAGE];
+
+  const int M = a.N * a.Ho * a.Wo;
+  const int nct = a.Ngemm / BC;
+  const int npt = (M + BP - 1) / BP;
+  const int bid = xcd_remap(blockIdx.x, npt * nct);
+  const int pt = bid / nct, ct = bid - pt * nct;
+  const int m0 = pt * BP, c0 = ct * BC;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wc = wid % NWC, wp = wid / NWC;
+
+  // loader geometry: in round j this wave fills rows j*64 + wid*8 + (lane>>3), slot lane&7
+  const int lrow = wid * 8 + (lane >> 3);
+  const int lchunk = (lane & 7) ^ (lane >> 3);   // swz_nk<64>: slot = chunk ^ (row & 7)
+
+  unsigned pbase[RP], tmask[RP];
+  const int taps = a.KH * a.KW;
+#pragma unroll
+  for (int j = 0; j < RP; ++j) {
+    const int m = m0 + j * 64 + lrow;
+    const bool pok = m < M;
+    const int mm = pok ? m : 0;
+    const int hw = a.Ho * a.Wo;
+    const int pn = mm / hw;
+    const int rem = mm - pn * hw;
+    const int ph = rem / a.Wo, pw = rem - (rem / a.Wo) * a.Wo;
+    const int h0 = ph * a.stride - a.pad, w0 = pw * a.stride - a.pad;
+    unsigned msk = 0;
+    for (int t = 0; t < taps; ++t) {
+      const int kh = t / a.KW, kw = t - (t / a.KW) * a.KW;
+      const int ih = h0 + kh, iw = w0 + kw;
+      if (pok && ih >= 0 && ih < a.Hs && iw >= 0 && iw < a.Ws) msk |= 1u << t;
+    }
+    tmask[j] = msk;
+    pbase[j] = (unsigned)((((pn * a.Hs + h0) * a.Ws + w0) * a.ldx) * 2 + lchunk * 16);
+  }
+  unsigned woff[RA];
+#pragma unroll
+  for (int j = 0; j < RA; ++j) woff[j] = (unsigned)(((c0 + j * 64 + lrow) * a.Kpad) * 2 + lchunk * 16);
+
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, 0, (int)a.xbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc((void*)a.w, 0, 0x7fffffff, 0x00020000);
+  const int S = a.Kpad / BK;
+
+  auto issue = [&](int s) {
+    char* base = lds + (s % ST) * STAGE;
+    const int tap = (s * BK) / a.Cs;                  // Cs % 64 == 0: one tap per K-step (scalar)
+    const int ci = s * BK - tap * a.Cs;
+    const int kh = tap / a.KW, kw = tap - (tap / a.KW) * a.KW;
+    const unsigned delta = (unsigned)(((kh * a.Ws + kw) * a.ldx + ci) * 2);
+#pragma unroll
+    for (int j = 0; j < RA; ++j)
+      dma16(wrs, base + (j * 64 + wid * 8) * RBY, woff[j] + s * RBY);
+#pragma unroll
+    for (int j = 0; j < RP; ++j) {
+      const bool ok = tap < taps && ((tmask[j] >> tap) & 1u);
+      dma16(xr, base + (BC + j * 64 + wid * 8) * RBY, ok ? pbase[j] + delta : 0x80000000u);
+    }
+  };
+
+  f32x4_t acc[TC][TP];
+#pragma unroll
+  for (int ic = 0; ic < TC; ++ic)
+#pragma unroll
+    for (int ip = 0; ip < TP; ++ip) acc[ic][ip] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int s = 0; s < ST - 1; ++s)
+    if (s < S) issue(s);
+
+  for (int s = 0; s < S; ++s) {
+    // own DMAs of step s done (the ST-2 newer steps may stay in flight), then everyone's
+    if (s + ST - 2 < S) wait_vm<(ST - 2) * LPS>();
+    else wait_vm<0>();
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (s + ST - 1 < S) issue(s + ST - 1);           // refills the buffer consumed at step s-1
+    __builtin_amdgcn_sched_barrier(0);
+    const char* Wt = lds + (s % ST) * STAGE;
+    const char* P = Wt + BC * RBY;
+#pragma unroll
+    for (int kk = 0; kk < BK / 32; ++kk) {
+      const int chunk = kk * 4 + (lane >> 4);
+      bf16x8_t af[TC], bfr[TP];
+#pragma unroll
+      for (int ic = 0; ic < TC; ++ic) {
+        const int row = wc * WC + ic * 16 + (lane & 15);
+        af[ic] = *reinterpret_cast<const bf16x8_t*>(Wt + row * RBY + ((chunk ^ (row & 7)) << 4));
+      }
+#pragma unroll
+      for (int ip = 0; ip < TP; ++ip) {
+        const int row = wp * WP + ip * 16 + (lane & 15);
+        bfr[ip] = *reinterpret_cast<const bf16x8_t*>(P + row * RBY + ((chunk ^ (row & 7)) << 4));
+      }
+#pragma unroll
+      for (int ic = 0; ic < TC; ++ic)
+#pragma unroll
+        for (int ip = 0; ip < TP; ++ip)
+          acc[ic][ip] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ic], bfr[ip], acc[ic][ip], 0, 0, 0);
+    }
+  }
+
+  // ------------------------------------------------------------------ epilogue (as igemm.hip)
+  const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc((void*)a.y, 0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t mr = __builtin_amdgcn_make_buffer_rsrc((void*)(a.mask ? a.mask : a.y), 0, 0x7fffffff, 0x00020000);
+#pragma unroll
+  for (int ip = 0; ip < TP; ++ip) {
+    const int m = m0 + wp * WP + ip * 16 + (lane & 15);
+    if (m >= M) continue;
+    unsigned ybase;
+    if (a.mode == 0) {
+      ybase = (unsigned)m * (unsigned)a.ldy;
+    } else {
+      const int hw = a.Ho * a.Wo;
+      const int n = m / hw, rem = m - n * hw, h = rem / a.Wo, w = rem - (rem / a.Wo) * a.Wo;
+      ybase = (unsigned)(((n * 2 * a.Ho + 2 * h) * (2 * a.Wo) + 2 * w) * a.ldy);
+    }
+#pragma unroll
+    for (int ic = 0; ic < TC; ++ic) {
+      const int nidx = c0 + wc * WC + ic * 16 + 4 * (lane >> 4);
+      int co = nidx;
+      unsigned off = ybase + nidx;
+      if (a.mode == 1) {
+        const int ij = nidx / a.Cout;
+        co = nidx - ij * a.Cout;
+        off = ybase + (unsigned)(((ij >> 1) * (2 * a.Wo) + (ij & 1)) * a.ldy + co);
+      }
+      float v0 = acc[ic][ip][0], v1 = acc[ic][ip][1], v2 = acc[ic][ip][2], v3 = acc[ic][ip][3];
+      if (a.bias) {
+        const float* b = a.bias + co;
+        v0 += b[0]; v1 += b[1]; v2 += b[2]; v3 += b[3];
+      }
+      if (a.relu) {
+        v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f);
+      }
+      if (a.mask && co < a.mask_ch) {
+        const u32x2_t mk = __builtin_amdgcn_raw_buffer_load_b64(mr, ((unsigned)m * (unsigned)a.ldm + co) * 2, 0, 0);
+        v0 = lo_bf(mk.x) > 0.f ? v0 : 0.f;
+        v1 = hi_bf(mk.x) > 0.f ? v1 : 0.f;
+        v2 = lo_bf(mk.y) > 0.f ? v2 : 0.f;
+        v3 = hi_bf(mk.y) > 0.f ? v3 : 0.f;
+      }
+      if (a.accumulate) {
+        const u32x2_t o = __builtin_amdgcn_raw_buffer_load_b64(yr, off * 2, 0, 0);
+        v0 += lo_bf(o.x); v1 += hi_bf(o.x); v2 += lo_bf(o.y); v3 += hi_bf(o.y);
+      }
+      __builtin_amdgcn_raw_buffer_store_b64(u32x2_t{pack_bf2(v0, v1), pack_bf2(v2, v3)}, yr, off * 2, 0, 0);
+    }
+  }
+}
+
+template <int BC, int BP, int WC, int WP, int ST>
+static int launch_glds(const IgemmArgs& a, hipStream_t st) {
+  const int M = a.N * a.Ho * a.Wo;
+  const int grid = ((M + BP - 1) / BP) * (a.Ngemm / BC);
+  hipLaunchKernelGGL((igemm_glds_kernel<BC, BP, WC, WP, ST>), dim3(grid), dim3(512), 0, st, a);
+  return (int)hipGetLastError();
+}
+
+// cfg 0 = auto.  1: 256(ch) x 128(px), 3 stages (144 KB)   2: 128 x 256, 3 stages
+//                3: 256 x 256, 2 stages (128 KB)            4: 128 x 128, 4 stages (128 KB)
+// Requires Cs % 64 == 0 (a K-step never straddles a tap), Kpad % 64 == 0, Ngemm % BC == 0.
+DPA_API int dpa_igemm_glds(const IgemmArgs* args, int cfg, hipStream_t st) {
+  const IgemmArgs& a = *args;
+  if ((a.Cs & 63) || (a.Kpad & 63) || (a.ldx & 7) || (a.ldy & 3) || a.KH * a.KW > 32) return (int)hipErrorInvalidValue;
+  if (a.mode == 1 && (a.Cout & 3)) return (int)hipErrorInvalidValue;
+  if (cfg == 0) cfg = (a.Ngemm % 256 == 0) ? 1 : 2;
+  switch (cfg) {
+    case 1: if (a.Ngemm % 256) break; return launch_glds<256, 128, 64, 64, 3>(a, st);
+    case 2: if (a.Ngemm % 128) break; return launch_glds<128, 256, 64, 64, 3>(a, st);
+    case 3: if (a.Ngemm % 256) break; return launch_glds<256, 256, 128, 64, 2>(a, st);
+    case 4: if (a.Ngemm % 128) break; return launch_glds<128, 128, 64, 32, 4>(a, st);
+    default: break;
+  }
+  return (int)hipErrorInvalidValue;
+}

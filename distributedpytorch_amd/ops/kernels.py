@@ -73,6 +73,7 @@ _MAX_BYTES = 2 ** 31 - 1024   # kernels address activations through 32-bit buffe
 USE_HALO = os.environ.get("DPA_NO_HALO", "0") != "1"
 # row-streaming conv3x3 (weights resident, 4-row LDS ring); DPA_NO_STREAM=1 disables
 USE_STREAM = os.environ.get("DPA_NO_STREAM", "0") != "1"
+USE_GLDS = os.environ.get("DPA_NO_GLDS", "0") != "1"
 
 
 def _extent_bytes(N, H, W, C, ld):
@@ -94,7 +95,8 @@ def igemm(x: torch.Tensor, wpacked: torch.Tensor, y: torch.Tensor, *, Ngemm: int
 
     ``path``: ``auto`` picks, for a conv3x3, the row-streaming kernel (Ngemm, Cs in {32, 64}), then the
     row-halo kernel (Cs % 32 == 0, Ngemm <= 128), then the generic gather kernel (csrc/igemm.hip);
-    ``stream`` / ``halo`` / ``generic`` force one (tests, A/B).  ``pool``: also produce the 2x2/s2
+    ``stream`` / ``halo`` / ``glds`` / ``generic`` force one (tests, A/B).  ``glds`` (csrc/igemm_glds.hip,
+    LDS-DMA staged, 8 waves, Cs % 64 == 0) serves the deep layers before the generic kernel.  ``pool``: also produce the 2x2/s2
     max-pool of ``y`` (fused into the streaming kernel's epilogue, else a separate pass)."""
     N, Hs, Ws, Cx, ldx = _nhwc(x, "igemm.x")
     _, _, _, Cy, ldy = _nhwc(y, "igemm.y")
@@ -147,6 +149,13 @@ def igemm(x: torch.Tensor, wpacked: torch.Tensor, y: torch.Tensor, *, Ngemm: int
                 continue
             if path == "halo":
                 _check(err, "igemm_halo")
+        if path == "glds" or (path == "auto" and USE_GLDS and cfg == 0 and Cs % 64 == 0 and Kpad % 64 == 0
+                              and Ngemm % 128 == 0):
+            err = L.dpa_igemm_glds(ctypes.byref(a), c_int(variant if path == "glds" else 0), st)
+            if err == 0:
+                continue
+            if path == "glds":
+                _check(err, "igemm_glds")
         _check(L.dpa_igemm(ctypes.byref(a), c_int(cfg), st), "igemm")
     if pool is not None and not pool_done:
         maxpool2(y, pool)

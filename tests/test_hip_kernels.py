@@ -115,6 +115,39 @@ def test_conv3x3_dgrad_masked(hip_lib, N, H, W, Cin, Cout, path):
     assert _rel(_nchw(out), ref) < 2e-2
 
 
+@pytest.mark.parametrize("N,H,W,Cin,Cout,var", [
+    (2, 9, 13, 128, 256, 1), (1, 16, 16, 256, 256, 1), (2, 9, 13, 64, 128, 2), (1, 16, 16, 256, 512, 3),
+    (2, 7, 11, 128, 128, 4), (1, 32, 32, 64, 256, 0)])
+def test_conv3x3_glds(hip_lib, N, H, W, Cin, Cout, var):
+    """LDS-DMA implicit GEMM (csrc/igemm_glds.hip): fwd with bias+ReLU and masked dgrad, every tile
+    config, pixel counts that are not tile multiples (zero-filled DMA rows)."""
+    from distributedpytorch_amd.ops import kernels as K
+    torch.manual_seed(7)
+    x = _bf(F.relu(torch.randn(N, Cin, H, W)))
+    w = _bf(torch.randn(Cout, Cin, 3, 3) * (2.0 / (9 * Cin)) ** 0.5)
+    b = torch.randn(Cout) * 0.1
+    ref = F.relu(F.conv2d(x, w, b, padding=1))
+    packed, ng, kp = _pack_one(0, w, Cin)
+    y = torch.empty(N, H, W, Cout, dtype=torch.bfloat16, device="cuda")
+    K.igemm(_nhwc(x), packed, y, Ngemm=ng, Kpad=kp, KH=3, KW=3, stride=1, pad=1, Cs=Cin, out_grid=(N, H, W),
+            bias=b.cuda(), relu=True, path="glds", variant=var)
+    torch.cuda.synchronize()
+    assert _rel(_nchw(y), ref) < 2e-2
+    if Cin % 128:          # dgrad has Ngemm = Cin: needs a 128-multiple
+        return
+    g = _bf(torch.randn(N, Cout, H, W))
+    xr = x.clone().requires_grad_(True)
+    F.conv2d(xr, w, padding=1).backward(g)
+    dref = xr.grad * (x > 0)
+    packed, ng, kp = _pack_one(1, w)
+    dx = torch.empty(N, H, W, Cin, dtype=torch.bfloat16, device="cuda")
+    v = var if (var not in (1, 3) or Cin % 256 == 0) else 2
+    K.igemm(_nhwc(g), packed, dx, Ngemm=ng, Kpad=kp, KH=3, KW=3, stride=1, pad=1, Cs=Cout, out_grid=(N, H, W),
+            mask=_nhwc(x), path="glds", variant=v)
+    torch.cuda.synchronize()
+    assert _rel(_nchw(dx), dref) < 2e-2
+
+
 @pytest.mark.parametrize("N,h,w,Cin,Cout", [(2, 5, 7, 64, 32), (1, 4, 4, 512, 256), (2, 8, 8, 128, 64)])
 def test_deconv_fwd_into_concat(hip_lib, N, h, w, Cin, Cout):
     from distributedpytorch_amd.ops import kernels as K

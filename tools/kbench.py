@@ -37,6 +37,8 @@ def main():
     ap.add_argument("--cfgs", type=int, nargs="*", default=[], help="extra generic tile configs to time")
     ap.add_argument("--no-wgrad", action="store_true")
     ap.add_argument("--svar", type=int, nargs="*", default=[], help="streaming-conv variants to time")
+    ap.add_argument("--gvar", type=int, nargs="*", default=[], help="LDS-DMA (glds) kernel configs to time")
+    ap.add_argument("--paths", default="stream,halo,generic", help="default paths to time")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     B, S = a.batch, a.img
@@ -57,12 +59,10 @@ def main():
         wd = (torch.randn(Cin * kd, device=dev) * 0.05).to(torch.bfloat16)
         bias = torch.zeros(Cout, device=dev)
         flops = 2.0 * B * H * H * Cin * Cout * 9
-        variants = [("stream", 0), ("halo", 0), ("generic", 0)] + [("generic", c) for c in a.cfgs] + \
-            [("stream", -v) for v in a.svar]
-        for path, cfg in variants:
-            label = path if cfg == 0 else (f"gen.c{cfg}" if cfg > 0 else f"strm.v{-cfg}")
-            var = -cfg if cfg < 0 else 0
-            cfg = max(cfg, 0)
+        variants = [(p, p, 0, 0) for p in a.paths.split(",") if p] + \
+            [(f"gen.c{c}", "generic", c, 0) for c in a.cfgs] + [(f"strm.v{v}", "stream", 0, v) for v in a.svar] + \
+            [(f"glds.c{v}", "glds", 0, v) for v in a.gvar]
+        for label, path, cfg, var in variants:
             try:
                 t = timeit(lambda: K.igemm(x, wf, y, Ngemm=Cout, Kpad=kf, KH=3, KW=3, stride=1, pad=1, Cs=Cin,
                                            out_grid=(B, H, H), bias=bias, relu=True, path=path, cfg=cfg, variant=var), a.reps)
