@@ -84,12 +84,12 @@ def _ddp_worker(rank, world, port, bucket_mb, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("bucket_mb", [0.001, 8.0])
-def test_ddp_gloo_two_ranks(bucket_mb):
+@pytest.mark.parametrize("world,bucket_mb", [(2, 0.001), (2, 8.0), (4, 0.004)])
+def test_ddp_gloo_ranks(world, bucket_mb):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_ddp_worker, args=(r, 2, port, bucket_mb, q)) for r in range(2)]
+    procs = [ctx.Process(target=_ddp_worker, args=(r, world, port, bucket_mb, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=240) for _ in procs]

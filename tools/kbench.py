@@ -85,6 +85,31 @@ def main():
             except Exception as e:
                 print(f"{name:14s} wgrad {path:8s}  n/a ({str(e)[:40]})", flush=True)
         del x, g, y, dx
+    # transposed convs (k2 s2): fwd = 1x1 GEMM scattered into the concat buffer, dgrad = stride-2 gather
+    for name, h, Cin, Cout in [("D1 512->256", S // 16, 512, 256), ("D2 256->128", S // 8, 256, 128),
+                               ("D3 128->64", S // 4, 128, 64), ("D4 64->32", S // 2, 64, 32)]:
+        if a.only and not any(o in name for o in a.only.split(",")):
+            continue
+        x = torch.randn(B, h, h, Cin, device=dev).to(torch.bfloat16)
+        cat = torch.empty(B, 2 * h, 2 * h, 2 * Cout, device=dev, dtype=torch.bfloat16)
+        wf = (torch.randn(4 * Cout * Cin, device=dev) * 0.05).to(torch.bfloat16)
+        wd = (torch.randn(Cin * 4 * Cout, device=dev) * 0.05).to(torch.bfloat16)
+        dx = torch.empty(B, h, h, Cin, device=dev, dtype=torch.bfloat16)
+        flops = 2.0 * B * h * h * Cin * Cout * 4
+        for label, path, var in [("generic", "generic", 0)] + [(f"glds.c{v}", "glds", v) for v in a.gvar]:
+            for kind in ("fwd", "dgrad"):
+                try:
+                    if kind == "fwd":
+                        fn = lambda: K.igemm(x, wf, cat[..., Cout:], Ngemm=4 * Cout, Kpad=Cin, KH=1, KW=1, stride=1,
+                                             pad=0, Cs=Cin, out_grid=(B, h, h), mode=1, Cout=Cout, path=path,
+                                             variant=var)
+                    else:
+                        fn = lambda: K.igemm(cat[..., Cout:], wd, dx, Ngemm=Cin, Kpad=4 * Cout, KH=2, KW=2, stride=2,
+                                             pad=0, Cs=Cout, out_grid=(B, h, h), mask=x, path=path, variant=var)
+                    t = timeit(fn, a.reps)
+                    print(f"{name:14s} {kind:5s} {label:8s} {t:9.1f} us {flops / t / 1e6:7.1f} TF", flush=True)
+                except Exception as e:
+                    print(f"{name:14s} {kind:5s} {label:8s}  n/a ({str(e)[:40]})", flush=True)
 
 
 if __name__ == "__main__":
