@@ -21,9 +21,6 @@
 
 namespace {
 
-constexpr int BK = 64;
-constexpr int RBY = BK * 2;   // bytes per LDS row
-
 // 16-B LDS-DMA: lane l's bytes land at lds + 16*l.  (Wrapped in a __device__ function: used
 // directly inside a kernel template the builtin makes the host pass drop the kernel's launch stub.)
 __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, char* lds, unsigned voff) {
@@ -38,11 +35,15 @@ __device__ __forceinline__ void wait_vm() {
 
 }  // namespace
 
-template <int BC, int BP, int WC, int WP, int ST>
+template <int BC, int BP, int WC, int WP, int ST, int BK>
 __global__ __launch_bounds__(512) void igemm_glds_kernel(IgemmArgs a) {
   constexpr int NWC = BC / WC, NWP = BP / WP;
   static_assert(NWC * NWP == 8, "8 waves");
-  constexpr int RA = BC / 64, RP = BP / 64;   // DMA rounds per stage per wave (64 rows per block round)
+  constexpr int RBY = BK * 2;                 // bytes per LDS row
+  constexpr int CPR = RBY / 16;               // 16-B chunks per row
+  constexpr int RPI = 64 / CPR;               // rows one wave-instruction (1 KB) fills
+  constexpr int RA = BC / (8 * RPI), RP = BP / (8 * RPI);   // DMA rounds per stage per wave
+  static_assert(RA * 8 * RPI == BC && RP * 8 * RPI == BP, "loader tiling");
   constexpr int LPS = RA + RP;                // DMA instructions per stage per wave
   constexpr int TC = WC / 16, TP = WP / 16;
   constexpr int STAGE = (BC + BP) * RBY;
@@ -57,15 +58,16 @@ __global__ __launch_bounds__(512) void igemm_glds_kernel(IgemmArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wc = wid % NWC, wp = wid / NWC;
 
-  // loader geometry: in round j this wave fills rows j*64 + wid*8 + (lane>>3), slot lane&7
-  const int lrow = wid * 8 + (lane >> 3);
-  const int lchunk = (lane & 7) ^ (lane >> 3);   // swz_nk<64>: slot = chunk ^ (row & 7)
+  // loader geometry: in round j this wave fills rows j*8*RPI + wid*RPI + lane/CPR, slot lane%CPR; the
+  // swizzle depends on row bits the round offset does not touch, and XOR is its own inverse
+  const int lrow = wid * RPI + lane / CPR;
+  const int lchunk = swz_nk<BK>(lrow, lane % CPR);
 
   unsigned pbase[RP], tmask[RP];
   const int taps = a.KH * a.KW;
 #pragma unroll
   for (int j = 0; j < RP; ++j) {
-    const int m = m0 + j * 64 + lrow;
+    const int m = m0 + j * 8 * RPI + lrow;
     const bool pok = m < M;
     const int mm = pok ? m : 0;
     const int hw = a.Ho * a.Wo;
@@ -84,7 +86,7 @@ __global__ __launch_bounds__(512) void igemm_glds_kernel(IgemmArgs a) {
   }
   unsigned woff[RA];
 #pragma unroll
-  for (int j = 0; j < RA; ++j) woff[j] = (unsigned)(((c0 + j * 64 + lrow) * a.Kpad) * 2 + lchunk * 16);
+  for (int j = 0; j < RA; ++j) woff[j] = (unsigned)(((c0 + j * 8 * RPI + lrow) * a.Kpad) * 2 + lchunk * 16);
 
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, 0, (int)a.xbytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc((void*)a.w, 0, 0x7fffffff, 0x00020000);
@@ -92,17 +94,17 @@ __global__ __launch_bounds__(512) void igemm_glds_kernel(IgemmArgs a) {
 
   auto issue = [&](int s) {
     char* base = lds + (s % ST) * STAGE;
-    const int tap = (s * BK) / a.Cs;                  // Cs % 64 == 0: one tap per K-step (scalar)
+    const int tap = (s * BK) / a.Cs;                  // Cs % BK == 0: one tap per K-step (scalar)
     const int ci = s * BK - tap * a.Cs;
     const int kh = tap / a.KW, kw = tap - (tap / a.KW) * a.KW;
     const unsigned delta = (unsigned)(((kh * a.Ws + kw) * a.ldx + ci) * 2);
 #pragma unroll
     for (int j = 0; j < RA; ++j)
-      dma16(wrs, base + (j * 64 + wid * 8) * RBY, woff[j] + s * RBY);
+      dma16(wrs, base + (j * 8 * RPI + wid * RPI) * RBY, woff[j] + s * RBY);
 #pragma unroll
     for (int j = 0; j < RP; ++j) {
       const bool ok = tap < taps && ((tmask[j] >> tap) & 1u);
-      dma16(xr, base + (BC + j * 64 + wid * 8) * RBY, ok ? pbase[j] + delta : 0x80000000u);
+      dma16(xr, base + (BC + j * 8 * RPI + wid * RPI) * RBY, ok ? pbase[j] + delta : 0x80000000u);
     }
   };
 
@@ -134,12 +136,12 @@ __global__ __launch_bounds__(512) void igemm_glds_kernel(IgemmArgs a) {
 #pragma unroll
       for (int ic = 0; ic < TC; ++ic) {
         const int row = wc * WC + ic * 16 + (lane & 15);
-        af[ic] = *reinterpret_cast<const bf16x8_t*>(Wt + row * RBY + ((chunk ^ (row & 7)) << 4));
+        af[ic] = *reinterpret_cast<const bf16x8_t*>(Wt + row * RBY + (swz_nk<BK>(row, chunk) << 4));
       }
 #pragma unroll
       for (int ip = 0; ip < TP; ++ip) {
         const int row = wp * WP + ip * 16 + (lane & 15);
-        bfr[ip] = *reinterpret_cast<const bf16x8_t*>(P + row * RBY + ((chunk ^ (row & 7)) << 4));
+        bfr[ip] = *reinterpret_cast<const bf16x8_t*>(P + row * RBY + (swz_nk<BK>(row, chunk) << 4));
       }
 #pragma unroll
       for (int ic = 0; ic < TC; ++ic)
@@ -198,27 +200,30 @@ __global__ __launch_bounds__(512) void igemm_glds_kernel(IgemmArgs a) {
   }
 }
 
-template <int BC, int BP, int WC, int WP, int ST>
+template <int BC, int BP, int WC, int WP, int ST, int BK = 64>
 static int launch_glds(const IgemmArgs& a, hipStream_t st) {
   const int M = a.N * a.Ho * a.Wo;
   const int grid = ((M + BP - 1) / BP) * (a.Ngemm / BC);
-  hipLaunchKernelGGL((igemm_glds_kernel<BC, BP, WC, WP, ST>), dim3(grid), dim3(512), 0, st, a);
+  hipLaunchKernelGGL((igemm_glds_kernel<BC, BP, WC, WP, ST, BK>), dim3(grid), dim3(512), 0, st, a);
   return (int)hipGetLastError();
 }
 
 // cfg 0 = auto.  1: 256(ch) x 128(px), 3 stages (144 KB)   2: 128 x 256, 3 stages
 //                3: 256 x 256, 2 stages (128 KB)            4: 128 x 128, 4 stages (128 KB)
+//                5: 256 x 256 x BK32, 4 stages (128 KB)     6: 128 x 256 x BK32, 5 stages (120 KB)
 // Requires Cs % 64 == 0 (a K-step never straddles a tap), Kpad % 64 == 0, Ngemm % BC == 0.
 DPA_API int dpa_igemm_glds(const IgemmArgs* args, int cfg, hipStream_t st) {
   const IgemmArgs& a = *args;
   if ((a.Cs & 63) || (a.Kpad & 63) || (a.ldx & 7) || (a.ldy & 3) || a.KH * a.KW > 32) return (int)hipErrorInvalidValue;
   if (a.mode == 1 && (a.Cout & 3)) return (int)hipErrorInvalidValue;
-  if (cfg == 0) cfg = (a.Ngemm % 256 == 0) ? 1 : 2;
+  if (cfg == 0) cfg = (a.Ngemm % 256 == 0) ? 3 : 2;
   switch (cfg) {
     case 1: if (a.Ngemm % 256) break; return launch_glds<256, 128, 64, 64, 3>(a, st);
     case 2: if (a.Ngemm % 128) break; return launch_glds<128, 256, 64, 64, 3>(a, st);
     case 3: if (a.Ngemm % 256) break; return launch_glds<256, 256, 128, 64, 2>(a, st);
     case 4: if (a.Ngemm % 128) break; return launch_glds<128, 128, 64, 32, 4>(a, st);
+    case 5: if (a.Ngemm % 256) break; return launch_glds<256, 256, 128, 64, 4, 32>(a, st);
+    case 6: if (a.Ngemm % 128) break; return launch_glds<128, 256, 64, 64, 5, 32>(a, st);
     default: break;
   }
   return (int)hipErrorInvalidValue;

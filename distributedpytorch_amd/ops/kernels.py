@@ -143,14 +143,20 @@ def igemm(x: torch.Tensor, wpacked: torch.Tensor, y: torch.Tensor, *, Ngemm: int
             if path == "stream":
                 _check(err, "igemm_stream")
         pool_done = False
+        glds_ok = USE_GLDS and cfg == 0 and Cs % 64 == 0 and Kpad % 64 == 0 and Ngemm % 128 == 0
+        # measured (tools/kbench.py, profiles/kbench_b32_512.txt): the LDS-DMA kernel beats the row-halo
+        # kernel on the 128-output-channel dgrads, the halo kernel wins the 128-channel forwards
+        glds_var = 0 if path == "glds" else (2 if Cs >= 128 else 6)
+        if path == "auto" and glds_ok and mask is not None and Ngemm == 128:
+            if L.dpa_igemm_glds(ctypes.byref(a), c_int(glds_var), st) == 0:
+                continue
         if path == "halo" or (path == "auto" and USE_HALO and conv3 and Cs % 32 == 0 and Ngemm <= 128):
             err = L.dpa_igemm_halo(ctypes.byref(a), c_int(0), st)
             if err == 0:
                 continue
             if path == "halo":
                 _check(err, "igemm_halo")
-        if path == "glds" or (path == "auto" and USE_GLDS and cfg == 0 and Cs % 64 == 0 and Kpad % 64 == 0
-                              and Ngemm % 128 == 0):
+        if path == "glds" or (path == "auto" and glds_ok):
             err = L.dpa_igemm_glds(ctypes.byref(a), c_int(variant if path == "glds" else 0), st)
             if err == 0:
                 continue
