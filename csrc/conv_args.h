@@ -18,7 +18,28 @@ struct IgemmArgs {
   unsigned xbytes;      // bytes addressable from x (< 2^31; the host splits larger batches by image)
   bf16_t* pool;         // optional fused 2x2/s2 max-pool output [N][Ho/2][Wo/2][ldp] (stream kernels)
   int ldp;
+  unsigned char* pcode; // optional with pool: per (window, channel) code = argmax(2b) | (4 pixels > 0) << 2,
+                        // dense [N][Ho/2][Wo/2][Ngemm] bytes: the max-pool backward needs nothing else
+  bf16_t* y2;           // optional split output (mode 0, no accumulate): channels >= split go to
+  int ldy2, split;      // y2[m][co - split] -- the two halves of a concat gradient as dense tensors
 };
+
+// 2x2 window code from the four (bf16-rounded) values in window order tl, tr, bl, br: first
+// occurrence of the maximum (torch max_pool2d / the old pool_bwd order) and the ReLU masks.
+__device__ __forceinline__ unsigned pool_code(float tl, float tr, float bl, float br) {
+  const unsigned it = tr > tl ? 1u : 0u, ib = br > bl ? 3u : 2u;
+  const float mt = fmaxf(tl, tr), mb = fmaxf(bl, br);
+  return (mb > mt ? ib : it) | (unsigned)(tl > 0.f) << 2 | (unsigned)(tr > 0.f) << 3 | (unsigned)(bl > 0.f) << 4 |
+         (unsigned)(br > 0.f) << 5;
+}
+
+// split-output store (see IgemmArgs::y2); returns false when the output is not split
+__device__ __forceinline__ bool split_store(const IgemmArgs& a, unsigned m, int co, u32x2_t v) {
+  if (a.y2 == nullptr) return false;
+  bf16_t* p = co >= a.split ? a.y2 + (size_t)m * a.ldy2 + (co - a.split) : a.y + (size_t)m * a.ldy + co;
+  *reinterpret_cast<u32x2_t*>(p) = v;
+  return true;
+}
 
 struct WgradArgs {
   const bf16_t* A; const bf16_t* B;

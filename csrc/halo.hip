@@ -153,7 +153,8 @@ __global__ __launch_bounds__(256) void igemm_halo_kernel(IgemmArgs a) {
         const uint2 o = *dst;
         v0 += lo_bf(o.x); v1 += hi_bf(o.x); v2 += lo_bf(o.y); v3 += hi_bf(o.y);
       }
-      *dst = make_uint2(pack_bf2(v0, v1), pack_bf2(v2, v3));
+      const u32x2_t packed = u32x2_t{pack_bf2(v0, v1), pack_bf2(v2, v3)};
+      if (!split_store(a, (unsigned)m, co, packed)) *reinterpret_cast<u32x2_t*>(dst) = packed;
     }
   }
 }
@@ -357,7 +358,9 @@ DPA_API int dpa_wgrad_halo(const WgradArgs* args, int cfg, hipStream_t st) {
 // once per block in 32 bits, rows only add a wave-uniform scalar, and all global traffic goes
 // through buffer instructions (32-bit offsets, range-checked zero padding, no 64-bit math).
 // LDS images are [.. ][rows][32 channels] 64-B-row nk images (swz_nk<32>, conflict-free).
-template <int BP, int NG, int CS, int RH, int WCS>
+// EPI: 0 plain epilogue, 1 + fused 2x2 max-pool (and window codes), 2 split output (a.y2); the
+// pool registers and branches exist only in the instantiations that use them.
+template <int BP, int NG, int CS, int RH, int WCS, int EPI>
 __global__ __launch_bounds__(256 * WCS) void igemm_stream_kernel(IgemmArgs a) {
   constexpr int NT = 256 * WCS;               // 4 waves along the pixels x WCS along the channels
   constexpr int HR = BP + 2;                  // pixels per staged input row
@@ -452,9 +455,10 @@ __global__ __launch_bounds__(256 * WCS) void igemm_stream_kernel(IgemmArgs a) {
   const bool has_mask = a.mask != nullptr;
   // fused 2x2 max-pool (encoder conv2 -> next level input): even rows keep their horizontally
   // max-reduced values in registers, odd rows finish the window and write the pooled pixel.
-  const bool do_pool = a.pool != nullptr;
+  constexpr bool do_pool = EPI == 1;
   const __amdgpu_buffer_rsrc_t pr = __builtin_amdgcn_make_buffer_rsrc((void*)(do_pool ? a.pool : a.y), 0, 0x7fffffff, 0x00020000);
-  float pkeep[TP][TC][4];
+  constexpr int PT = do_pool ? TP : 1, PC = do_pool ? TC : 1;
+  float ptop[PT][PC][4], ptop2[PT][PC][4];   // even row of the window: left / right pixel
 
   // prologue: input rows h0-1, h0, h0+1 -> slots 0, 1, 2
 #pragma unroll 1
@@ -532,24 +536,39 @@ __global__ __launch_bounds__(256 * WCS) void igemm_stream_kernel(IgemmArgs a) {
           v0 += lo_bf(o.x); v1 += hi_bf(o.x); v2 += lo_bf(o.y); v3 += hi_bf(o.y);
         }
         const u32x2_t packed = u32x2_t{pack_bf2(v0, v1), pack_bf2(v2, v3)};
-        __builtin_amdgcn_raw_buffer_store_b64(packed, yr, yo, 0, 0);
-        if (do_pool) {
-          // pool the STORED (bf16-rounded) values: identical to max-pooling the tensor afterwards
+        if constexpr (EPI == 2)
+          split_store(a, (unsigned)(orow * a.Wo + w0 + wp * WP + ip * 16 + (lane & 15)), wc * WCN + ic * 16 + 4 * chunk,
+                      packed);
+        else
+          __builtin_amdgcn_raw_buffer_store_b64(packed, yr, yo, 0, 0);
+        if constexpr (do_pool) {
+          // pool the STORED (bf16-rounded) values: identical to max-pooling the tensor afterwards.
+          // Even lanes hold pixel w (left), their xor-1 partner pixel w+1 (right).
           float q[4] = {lo_bf(packed.x), hi_bf(packed.x), lo_bf(packed.y), hi_bf(packed.y)};
+          float pq[4];
 #pragma unroll
-          for (int e = 0; e < 4; ++e) q[e] = fmaxf(q[e], __shfl_xor(q[e], 1, 64));   // pixel pair (w, w+1)
+          for (int e = 0; e < 4; ++e) pq[e] = __shfl_xor(q[e], 1, 64);
           const int hrow = h0 + r;
           if ((hrow & 1) == 0) {
 #pragma unroll
-            for (int e = 0; e < 4; ++e) pkeep[ip][ic][e] = q[e];
+            for (int e = 0; e < 4; ++e) {
+              ptop[ip][ic][e] = q[e];
+              ptop2[ip][ic][e] = pq[e];
+            }
           } else if (hrow < 2 * (a.Ho >> 1) && (lane & 1) == 0) {
             const int pw = (w0 + wp * WP + ip * 16 + (lane & 15)) >> 1;
-            const unsigned po = (unsigned)((((n * (a.Ho >> 1) + (hrow >> 1)) * (a.Wo >> 1) + pw) * a.ldp +
-                                            wc * WCN + ic * 16 + 4 * chunk) * 2);
-            __builtin_amdgcn_raw_buffer_store_b64(
-                u32x2_t{pack_bf2(fmaxf(q[0], pkeep[ip][ic][0]), fmaxf(q[1], pkeep[ip][ic][1])),
-                        pack_bf2(fmaxf(q[2], pkeep[ip][ic][2]), fmaxf(q[3], pkeep[ip][ic][3]))},
-                pr, po, 0, 0);
+            const unsigned pidx = (unsigned)((n * (a.Ho >> 1) + (hrow >> 1)) * (a.Wo >> 1) + pw);
+            const unsigned po = (pidx * a.ldp + wc * WCN + ic * 16 + 4 * chunk) * 2;
+            float mx[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) mx[e] = fmaxf(fmaxf(q[e], pq[e]), fmaxf(ptop[ip][ic][e], ptop2[ip][ic][e]));
+            __builtin_amdgcn_raw_buffer_store_b64(u32x2_t{pack_bf2(mx[0], mx[1]), pack_bf2(mx[2], mx[3])}, pr, po, 0, 0);
+            if (a.pcode) {
+              unsigned code = 0;
+#pragma unroll
+              for (int e = 0; e < 4; ++e) code |= pool_code(ptop[ip][ic][e], ptop2[ip][ic][e], q[e], pq[e]) << (8 * e);
+              *reinterpret_cast<unsigned*>(a.pcode + (size_t)pidx * a.Ngemm + wc * WCN + ic * 16 + 4 * chunk) = code;
+            }
           }
         }
       }
@@ -677,7 +696,21 @@ static int launch_igemm_stream8(const IgemmArgs& a, hipStream_t st) {
 template <int BP, int NG, int CS, int RH, int WCS>
 static int launch_igemm_stream(const IgemmArgs& a, hipStream_t st) {
   const int grid = a.N * ((a.Ho + RH - 1) / RH) * (a.Wo / BP);
-  hipLaunchKernelGGL((igemm_stream_kernel<BP, NG, CS, RH, WCS>), dim3(grid), dim3(256 * WCS), 0, st, a);
+  if (a.pool) {   // encoder conv2 (NG == CS): pool + window codes fused
+    if constexpr (NG == CS) {
+      hipLaunchKernelGGL((igemm_stream_kernel<BP, NG, CS, RH, WCS, 1>), dim3(grid), dim3(256 * WCS), 0, st, a);
+      return (int)hipGetLastError();
+    }
+    return (int)hipErrorInvalidValue;
+  }
+  if (a.y2) {     // decoder conv1 dgrad over the concat (NG = 2 CS): skip / up gradients as dense tensors
+    if constexpr (NG == 2 * CS) {
+      hipLaunchKernelGGL((igemm_stream_kernel<BP, NG, CS, RH, WCS, 2>), dim3(grid), dim3(256 * WCS), 0, st, a);
+      return (int)hipGetLastError();
+    }
+    return (int)hipErrorInvalidValue;
+  }
+  hipLaunchKernelGGL((igemm_stream_kernel<BP, NG, CS, RH, WCS, 0>), dim3(grid), dim3(256 * WCS), 0, st, a);
   return (int)hipGetLastError();
 }
 

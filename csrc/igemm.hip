@@ -212,7 +212,8 @@ __global__ __launch_bounds__(64 * (BP / WP) * (BC / WC)) void igemm_kernel(Igemm
         const u32x2_t o = __builtin_amdgcn_raw_buffer_load_b64(yr, off * 2, 0, 0);
         v0 += lo_bf(o.x); v1 += hi_bf(o.x); v2 += lo_bf(o.y); v3 += hi_bf(o.y);
       }
-      __builtin_amdgcn_raw_buffer_store_b64(u32x2_t{pack_bf2(v0, v1), pack_bf2(v2, v3)}, yr, off * 2, 0, 0);
+      const u32x2_t packed = u32x2_t{pack_bf2(v0, v1), pack_bf2(v2, v3)};
+      if (!split_store(a, (unsigned)m, co, packed)) __builtin_amdgcn_raw_buffer_store_b64(packed, yr, off * 2, 0, 0);
     }
   }
 }

@@ -8,6 +8,7 @@
 // Reference semantics: model/unet_parts.py:26-41 (MaxPool2d(2,2)), model/unet_model.py:10-11
 // (segmap, Sigmoid), utils/utils.py:9-25 (BCE - log Dice, global over the batch).
 #include "common.h"
+#include "conv_args.h"
 
 // ------------------------------------------------------------------------------ input conversion
 __global__ __launch_bounds__(256) void nchw3_to_nhwc8_kernel(const float* __restrict__ x, bf16_t* __restrict__ y, int B,
@@ -30,7 +31,7 @@ DPA_API int dpa_input_nhwc8(const float* x, bf16_t* y, int B, int C, int H, int 
 // ------------------------------------------------------------------------------ max-pool 2x2 / s2
 // Floor semantics (nn.MaxPool2d(2,2)); first maximum in scan order wins (matches PyTorch).
 __global__ __launch_bounds__(256) void maxpool2_kernel(const bf16_t* __restrict__ x, int ldx, bf16_t* __restrict__ y, int ldy,
-                                                       int N, int H, int W, int C) {
+                                                       int N, int H, int W, int C, unsigned char* __restrict__ code) {
   const int Ho = H / 2, Wo = W / 2, CC = C / 8;
   const long tot = (long)N * Ho * Wo * CC;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < tot; i += (long)gridDim.x * blockDim.x) {
@@ -46,20 +47,72 @@ __global__ __launch_bounds__(256) void maxpool2_kernel(const bf16_t* __restrict_
     const uint4 c = *reinterpret_cast<const uint4*>(x + (p00 + W) * ldx + cc * 8);
     const uint4 d = *reinterpret_cast<const uint4*>(x + (p00 + W + 1) * ldx + cc * 8);
     const unsigned int* pa = &a.x; const unsigned int* pb = &b.x; const unsigned int* pc = &c.x; const unsigned int* pd = &d.x;
-    unsigned int o[4];
+    unsigned int o[4], cd[2] = {0u, 0u};
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       float l = fmaxf(fmaxf(lo_bf(pa[k]), lo_bf(pb[k])), fmaxf(lo_bf(pc[k]), lo_bf(pd[k])));
       float h = fmaxf(fmaxf(hi_bf(pa[k]), hi_bf(pb[k])), fmaxf(hi_bf(pc[k]), hi_bf(pd[k])));
       o[k] = pack_bf2(l, h);
+      if (code) {
+        const unsigned cl = pool_code(lo_bf(pa[k]), lo_bf(pb[k]), lo_bf(pc[k]), lo_bf(pd[k]));
+        const unsigned ch = pool_code(hi_bf(pa[k]), hi_bf(pb[k]), hi_bf(pc[k]), hi_bf(pd[k]));
+        cd[k >> 1] |= (cl | ch << 8) << (16 * (k & 1));
+      }
     }
     *reinterpret_cast<uint4*>(y + op * ldy + cc * 8) = make_uint4(o[0], o[1], o[2], o[3]);
+    if (code) *reinterpret_cast<uint2*>(code + op * C + cc * 8) = make_uint2(cd[0], cd[1]);
   }
 }
-DPA_API int dpa_maxpool2(const bf16_t* x, int ldx, bf16_t* y, int ldy, int N, int H, int W, int C, hipStream_t st) {
+DPA_API int dpa_maxpool2(const bf16_t* x, int ldx, bf16_t* y, int ldy, int N, int H, int W, int C, unsigned char* code,
+                         hipStream_t st) {
   if ((C & 7) || (ldx & 7) || (ldy & 7)) return (int)hipErrorInvalidValue;
   const long tot = (long)N * (H / 2) * (W / 2) * (C / 8);
-  hipLaunchKernelGGL(maxpool2_kernel, dim3(dpa_grid(tot, 256, 8192)), dim3(256), 0, st, x, ldx, y, ldy, N, H, W, C);
+  hipLaunchKernelGGL(maxpool2_kernel, dim3(dpa_grid(tot, 256, 8192)), dim3(256), 0, st, x, ldx, y, ldy, N, H, W, C, code);
+  return (int)hipGetLastError();
+}
+
+// Max-pool backward from window codes (even H, W): one thread per (pixel, 8 channels), so the
+// full-resolution streams (dskip in, g out) are read/written as contiguous 16-B pieces; the
+// window code and dpool (a quarter of the pixels) come through the cache.
+//   g[p][c] = (dskip[p][c] + (argmax(window)[c] == q(p) ? dpool[window][c] : 0)) * mask_q(p)[c]
+__global__ __launch_bounds__(256) void pool_bwd_code_kernel(const unsigned char* __restrict__ code,
+                                                            const bf16_t* __restrict__ dskip, int ldd,
+                                                            const bf16_t* __restrict__ dpool, int ldp,
+                                                            bf16_t* __restrict__ g, int ldg, int N, int H, int W, int C) {
+  const int CC = C >> 3, Ho = H >> 1, Wo = W >> 1;
+  const unsigned tot = (unsigned)N * H * W * CC;
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < tot; i += gridDim.x * blockDim.x) {
+    const unsigned cc = i % CC, p = i / CC;
+    const unsigned w = p % W, nh = p / W, h = nh % H, n = nh / H;
+    const unsigned win = (n * Ho + (h >> 1)) * Wo + (w >> 1);
+    const unsigned q = (h & 1) * 2 + (w & 1);
+    const uint2 cw = *reinterpret_cast<const uint2*>(code + (size_t)win * C + cc * 8);
+    const uint4 dp = *reinterpret_cast<const uint4*>(dpool + (size_t)win * ldp + cc * 8);
+    uint4 ds = make_uint4(0u, 0u, 0u, 0u);
+    if (dskip) ds = *reinterpret_cast<const uint4*>(dskip + (size_t)p * ldd + cc * 8);
+    const unsigned* pd = &dp.x;
+    const unsigned* ps = &ds.x;
+    unsigned o[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const unsigned c2 = (k < 2 ? cw.x : cw.y) >> (16 * (k & 1));   // codes of channels 2k, 2k+1
+      const unsigned cl = c2 & 0xffu, ch = (c2 >> 8) & 0xffu;
+      float lo = lo_bf(ps[k]) + ((cl & 3u) == q ? lo_bf(pd[k]) : 0.f);
+      float hi = hi_bf(ps[k]) + ((ch & 3u) == q ? hi_bf(pd[k]) : 0.f);
+      lo = (cl >> (2 + q)) & 1u ? lo : 0.f;
+      hi = (ch >> (2 + q)) & 1u ? hi : 0.f;
+      o[k] = pack_bf2(lo, hi);
+    }
+    *reinterpret_cast<uint4*>(g + (size_t)p * ldg + cc * 8) = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+}
+DPA_API int dpa_pool_bwd_code(const unsigned char* code, const bf16_t* dskip, int ldd, const bf16_t* dpool, int ldp,
+                              bf16_t* g, int ldg, int N, int H, int W, int C, hipStream_t st) {
+  if ((C & 7) || (ldd & 7) || (ldp & 7) || (ldg & 7) || (H & 1) || (W & 1)) return (int)hipErrorInvalidValue;
+  const long tot = (long)N * H * W * (C / 8);
+  if (tot >= (1l << 31)) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(pool_bwd_code_kernel, dim3(dpa_grid(tot, 256, 16384)), dim3(256), 0, st, code, dskip, ldd, dpool, ldp, g,
+                     ldg, N, H, W, C);
   return (int)hipGetLastError();
 }
 
@@ -351,3 +404,38 @@ DPA_API int dpa_head_bwd(const bf16_t* y, int ldy, int C, const float* w, const 
 }
 
 DPA_API int dpa_head_slab_blocks(long long P) { return head_grid(P); }
+
+// ------------------------------------------------------------------------------ loss from partials
+// loss = S0/n - dice * log(2 S1 / (S2 + S3 + 1e-15))   (reference utils/utils.py:14-25)
+// One thread: the scalar tail of the loss that eager torch spends ~8 launches on (and ~8 more in
+// backward).  out = [loss, dL/dS0..3]; the backward scales the stored derivative by the incoming
+// gradient.  fp32 throughout, same operation order as the torch formula.
+__global__ void loss_finish_kernel(const float* __restrict__ S, float inv_n, int dice, float* __restrict__ out) {
+  const float s0 = S[0], s1 = S[1], s2 = S[2], s3 = S[3];
+  float loss = s0 * inv_n;
+  float d1 = 0.f, d2 = 0.f;
+  if (dice) {
+    const float u = s2 + s3 + 1e-15f;
+    loss = loss - logf(2.f * s1 / u);
+    d1 = -1.f / s1;
+    d2 = 1.f / u;
+  }
+  out[0] = loss;
+  out[1] = inv_n;
+  out[2] = d1;
+  out[3] = d2;
+  out[4] = d2;
+}
+__global__ void loss_grad_kernel(const float* __restrict__ g, const float* __restrict__ coef, float scale,
+                                 float* __restrict__ dS) {
+  const int i = threadIdx.x;
+  if (i < 4) dS[i] = g[0] * scale * coef[i];
+}
+DPA_API int dpa_loss_finish(const float* S, float inv_n, int dice, float* out, hipStream_t st) {
+  hipLaunchKernelGGL(loss_finish_kernel, dim3(1), dim3(1), 0, st, S, inv_n, dice, out);
+  return (int)hipGetLastError();
+}
+DPA_API int dpa_loss_grad(const float* g, const float* coef, float scale, float* dS, hipStream_t st) {
+  hipLaunchKernelGGL(loss_grad_kernel, dim3(1), dim3(64), 0, st, g, coef, scale, dS);
+  return (int)hipGetLastError();
+}

@@ -32,6 +32,9 @@ def loss_partials_from_probs(p: torch.Tensor, t: torch.Tensor) -> torch.Tensor:
 
 
 def loss_from_partials(S: torch.Tensor, n: int, dice: bool = True) -> torch.Tensor:
+    if S.is_cuda and S.dtype == torch.float32:
+        from .ops import kernels as K
+        return K.loss_from_partials(S, n, dice)      # one HIP launch each way (csrc/unet_aux.hip)
     loss = S[0] / n
     if dice:
         loss = loss - torch.log(2 * S[1] / (S[2] + S[3] + EPS))

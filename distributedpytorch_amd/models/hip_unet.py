@@ -144,12 +144,13 @@ class HipBlocks:
         return self.packed[c.off_d:c.off_d + c.Cin * c.Kd]
 
     # ------------------------------------------------------------------ primitive launches
-    def conv_fwd(self, c: _Conv, x: torch.Tensor, y: torch.Tensor = None, pool: torch.Tensor = None):
+    def conv_fwd(self, c: _Conv, x: torch.Tensor, y: torch.Tensor = None, pool: torch.Tensor = None,
+                 pcode: torch.Tensor = None):
         N, H, W = x.shape[:3]
         if y is None:
             y = torch.empty(N, H, W, c.Cout, dtype=torch.bfloat16, device=x.device)
         K.igemm(x, self.wf(c), y, Ngemm=c.Cout, Kpad=c.Kf, KH=3, KW=3, stride=1, pad=1, Cs=c.Cs, out_grid=(N, H, W),
-                bias=c.mod.bias, relu=True, pool=pool)
+                bias=c.mod.bias, relu=True, pool=pool, pcode=pcode)
         return y
 
     def conv_dgrad(self, c: _Conv, g: torch.Tensor, mask: torch.Tensor = None, out: torch.Tensor = None):
@@ -159,6 +160,17 @@ class HipBlocks:
         K.igemm(g, self.wd(c), out, Ngemm=c.Cin, Kpad=c.Kd, KH=3, KW=3, stride=1, pad=1, Cs=c.Cout,
                 out_grid=(N, H, W), mask=mask)
         return out
+
+    def conv_dgrad_split(self, c: _Conv, g: torch.Tensor, split: int):
+        """dgrad of a conv over a concat input, written as two dense tensors (channels < split, >= split):
+        the skip gradient and the up-path gradient are then read at full cache-line efficiency by the
+        max-pool backward and the transposed-conv backward (interleaved halves cost ~1.6x there)."""
+        N, H, W = g.shape[:3]
+        lo = torch.empty(N, H, W, split, dtype=torch.bfloat16, device=g.device)
+        hi = torch.empty(N, H, W, c.Cin - split, dtype=torch.bfloat16, device=g.device)
+        K.igemm(g, self.wd(c), lo, Ngemm=c.Cin, Kpad=c.Kd, KH=3, KW=3, stride=1, pad=1, Cs=c.Cout,
+                out_grid=(N, H, W), y2=hi, split=split)
+        return lo, hi
 
     def conv_wgrad(self, c: _Conv, g: torch.Tensor, x: torch.Tensor):
         N, H, W = g.shape[:3]
@@ -269,16 +281,20 @@ class _EncFn(torch.autograd.Function):
         cat = B.new_cat(N, H, W, c2.Cout)
         skip = cat[..., :c2.Cout]
         pooled = torch.empty(N, H // 2, W // 2, c2.Cout, dtype=torch.bfloat16, device=x.device)
-        B.conv_fwd(c2, a, skip, pool=pooled)          # max-pool fused into the conv epilogue when streaming
+        # window codes (argmax + ReLU masks) for the backward: it then never re-reads the skip
+        code = (torch.empty(N, H // 2, W // 2, c2.Cout, dtype=torch.uint8, device=x.device)
+                if H % 2 == 0 and W % 2 == 0 else None)
+        B.conv_fwd(c2, a, skip, pool=pooled, pcode=code)   # pool fused into the conv epilogue when streaming
         ctx.B, ctx.l = B, l
         ctx.x_needs_grad = l > 0
-        ctx.save_for_backward(x, a, cat)
+        ctx.has_code = code is not None
+        ctx.save_for_backward(x, a, cat, code if code is not None else cat)
         return _o(skip), _o(pooled)
 
     @staticmethod
     def backward(ctx, dskip, dpooled):
         B, l = ctx.B, ctx.l
-        x, a, cat = ctx.saved_tensors
+        x, a, cat, code = ctx.saved_tensors
         c1, c2 = B.enc_convs[l]
         C = c2.Cout
         skip = cat[..., :C]
@@ -287,8 +303,11 @@ class _EncFn(torch.autograd.Function):
         else:
             dpooled = _v(dpooled)
         dskip = None if dskip is None else _v(dskip)
-        g2 = torch.empty_like(a)
-        K.pool_bwd(skip, dskip, dpooled, g2)
+        g2 = torch.empty(a.shape[:3] + (C,), dtype=torch.bfloat16, device=a.device)
+        if ctx.has_code:
+            K.pool_bwd_code(code, dskip, dpooled, g2)
+        else:
+            K.pool_bwd(skip, dskip, dpooled, g2)
         g1 = B.conv_dgrad(c2, g2, mask=a)
         B.conv_wgrad(c2, g2, a)
         B.ready([c2.mod])
@@ -350,14 +369,13 @@ class _DecFn(torch.autograd.Function):
         g1 = B.conv_dgrad(c2, g2, mask=a)
         B.conv_wgrad(c2, g2, a)
         B.ready([c2.mod])
-        dcat = B.conv_dgrad(c1, g1)
+        dskip, gup = B.conv_dgrad_split(c1, g1, C)
         B.conv_wgrad(c1, g1, cat)
         B.ready([c1.mod])
-        gup = dcat[..., C:]
         dx = B.deconv_dgrad(d, gup, x)
         B.deconv_wgrad(d, gup, x)
         B.ready([d.mod])
-        return None, _o(dx), _o(dcat[..., :C]), None, None
+        return None, _o(dx), _o(dskip), None, None
 
 
 class _HeadFn(torch.autograd.Function):

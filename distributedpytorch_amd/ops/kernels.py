@@ -26,7 +26,8 @@ class IgemmArgs(ctypes.Structure):
     _fields_ = [("x", c_void_p), ("w", c_void_p), ("bias", c_void_p), ("y", c_void_p), ("mask", c_void_p)] + \
                [(n, c_int) for n in ("ldx", "ldy", "ldm", "mask_ch", "N", "Ho", "Wo", "Hs", "Ws", "Cs", "KH", "KW",
                                      "stride", "pad", "Ngemm", "Kpad", "mode", "relu", "accumulate", "Cout")] + \
-               [("xbytes", ctypes.c_uint), ("pool", c_void_p), ("ldp", c_int)]
+               [("xbytes", ctypes.c_uint), ("pool", c_void_p), ("ldp", c_int), ("pcode", c_void_p), ("y2", c_void_p),
+                ("ldy2", c_int), ("split", c_int)]
 
 
 class WgradArgs(ctypes.Structure):
@@ -90,14 +91,18 @@ def _image_chunks(N: int, per_image_bytes: int):
 def igemm(x: torch.Tensor, wpacked: torch.Tensor, y: torch.Tensor, *, Ngemm: int, Kpad: int, KH: int, KW: int,
           stride: int, pad: int, Cs: int, out_grid, bias: Optional[torch.Tensor] = None, relu: bool = False,
           mask: Optional[torch.Tensor] = None, mode: int = 0, Cout: int = 0, accumulate: bool = False, cfg: int = 0,
-          path: str = "auto", pool: Optional[torch.Tensor] = None, variant: int = 0):
+          path: str = "auto", pool: Optional[torch.Tensor] = None, variant: int = 0,
+          pcode: Optional[torch.Tensor] = None, y2: Optional[torch.Tensor] = None, split: int = 0):
     """Implicit-GEMM conv.  ``out_grid`` = (N, Ho, Wo) pixel grid of GEMM-M.
 
     ``path``: ``auto`` picks, for a conv3x3, the row-streaming kernel (Ngemm, Cs in {32, 64}), then the
     row-halo kernel (Cs % 32 == 0, Ngemm <= 128), then the generic gather kernel (csrc/igemm.hip);
     ``stream`` / ``halo`` / ``glds`` / ``generic`` force one (tests, A/B).  ``glds`` (csrc/igemm_glds.hip,
     LDS-DMA staged, 8 waves, Cs % 64 == 0) serves the deep layers before the generic kernel.  ``pool``: also produce the 2x2/s2
-    max-pool of ``y`` (fused into the streaming kernel's epilogue, else a separate pass)."""
+    max-pool of ``y`` (fused into the streaming kernel's epilogue, else a separate pass); ``pcode``: with
+    ``pool``, the per-window codes (argmax + ReLU masks, uint8 [N, Ho/2, Wo/2, Ngemm]) that
+    :func:`pool_bwd_code` consumes.  ``y2``/``split``: output channels >= ``split`` go to the dense
+    tensor ``y2`` (channel ``co - split``) -- the two halves of a concat gradient."""
     N, Hs, Ws, Cx, ldx = _nhwc(x, "igemm.x")
     _, _, _, Cy, ldy = _nhwc(y, "igemm.y")
     No, Ho, Wo = out_grid
@@ -105,7 +110,7 @@ def igemm(x: torch.Tensor, wpacked: torch.Tensor, y: torch.Tensor, *, Ngemm: int
     assert wpacked.dtype == torch.bfloat16 and wpacked.numel() >= Ngemm * Kpad
     assert Kpad >= KH * KW * Cs
     if mode == 0:
-        assert tuple(y.shape[:3]) == (N, Ho, Wo) and Cy >= Ngemm, (tuple(y.shape), out_grid, Ngemm)
+        assert tuple(y.shape[:3]) == (N, Ho, Wo) and (Cy >= Ngemm or y2 is not None), (tuple(y.shape), out_grid, Ngemm)
     else:
         assert tuple(y.shape[:3]) == (N, 2 * Ho, 2 * Wo) and Cy >= Cout and Ngemm == 4 * Cout
     # gathered source extent must stay inside x
@@ -121,6 +126,14 @@ def igemm(x: torch.Tensor, wpacked: torch.Tensor, y: torch.Tensor, *, Ngemm: int
     if pool is not None:
         Np, Hp, Wp, Cp, ldp = _nhwc(pool, "igemm.pool")
         assert (Np, Hp, Wp) == (N, Ho // 2, Wo // 2) and Cp >= Ngemm and mode == 0
+    if pcode is not None:
+        assert pool is not None and y2 is None and pcode.dtype == torch.uint8 and pcode.is_contiguous()
+        assert tuple(pcode.shape) == (N, Ho // 2, Wo // 2, Ngemm)
+    ldy2 = 0
+    if y2 is not None:
+        N2, H2, W2, C2, ldy2 = _nhwc(y2, "igemm.y2")
+        assert mode == 0 and not accumulate and (N2, H2, W2) == (N, Ho, Wo) and split % 16 == 0
+        assert 0 < split < Ngemm and C2 >= Ngemm - split and Cy >= split
     L = _lib.lib()
     st = _stream(y)
     pool_done = True
@@ -130,16 +143,18 @@ def igemm(x: torch.Tensor, wpacked: torch.Tensor, y: torch.Tensor, *, Ngemm: int
         a = IgemmArgs(xs.data_ptr(), _p(wpacked).value, None if bias is None else bias.data_ptr(), ys.data_ptr(),
                       None if mask is None else mask[n0:n1].data_ptr(), ldx, ldy, ldm, mch, nb, Ho, Wo, Hs, Ws, Cs,
                       KH, KW, stride, pad, Ngemm, Kpad, mode, int(relu), int(accumulate), Cout,
-                      _extent_bytes(nb, Hs, Ws, Cx, ldx), None, 0)
+                      _extent_bytes(nb, Hs, Ws, Cx, ldx), None, 0, None,
+                      None if y2 is None else y2[n0:n1].data_ptr(), ldy2, split)
         conv3 = mode == 0 and KH == 3 and stride == 1 and cfg == 0
         stream_ok = (Ngemm in (32, 64) and Cs in (32, 64)) or (Ngemm == 32 and Cs == 8 and pool is None)
         if path == "stream" or (path == "auto" and USE_STREAM and conv3 and stream_ok):
             if pool is not None:
                 a.pool, a.ldp = pool[n0:n1].data_ptr(), ldp
+                a.pcode = None if pcode is None else pcode[n0:n1].data_ptr()
             err = L.dpa_igemm_stream(ctypes.byref(a), c_int(variant), st)
             if err == 0:
                 continue
-            a.pool, a.ldp = None, 0
+            a.pool, a.ldp, a.pcode = None, 0, None
             if path == "stream":
                 _check(err, "igemm_stream")
         pool_done = False
@@ -164,7 +179,7 @@ def igemm(x: torch.Tensor, wpacked: torch.Tensor, y: torch.Tensor, *, Ngemm: int
                 _check(err, "igemm_glds")
         _check(L.dpa_igemm(ctypes.byref(a), c_int(cfg), st), "igemm")
     if pool is not None and not pool_done:
-        maxpool2(y, pool)
+        maxpool2(y, pool, pcode)
 
 
 # ------------------------------------------------------------------------------------------ wgrad
@@ -264,12 +279,28 @@ def input_nhwc8(x: torch.Tensor) -> torch.Tensor:
     return y
 
 
-def maxpool2(x: torch.Tensor, y: torch.Tensor):
+def maxpool2(x: torch.Tensor, y: torch.Tensor, code: Optional[torch.Tensor] = None):
     N, H, W, C, ldx = _nhwc(x, "maxpool.x")
     _, Ho, Wo, Cy, ldy = _nhwc(y, "maxpool.y")
     assert (Ho, Wo) == (H // 2, W // 2) and Cy == C and C % 8 == 0
+    if code is not None:
+        assert code.dtype == torch.uint8 and code.is_contiguous() and tuple(code.shape) == (N, Ho, Wo, C)
     _check(_lib.lib().dpa_maxpool2(_p(x), c_int(ldx), _p(y), c_int(ldy), c_int(N), c_int(H), c_int(W), c_int(C),
-                                   _stream(x)), "maxpool2")
+                                   _p(code), _stream(x)), "maxpool2")
+
+
+def pool_bwd_code(code: torch.Tensor, dskip: Optional[torch.Tensor], dpool: torch.Tensor, g: torch.Tensor):
+    """Max-pool backward + skip-gradient add + ReLU mask from the forward's window codes."""
+    N, H, W, C, ldg = _nhwc(g, "pool_bwd_code.g")
+    assert code.dtype == torch.uint8 and tuple(code.shape) == (N, H // 2, W // 2, C) and code.is_contiguous()
+    ldd = 8
+    if dskip is not None:
+        Nd, Hd, Wd, Cd, ldd = _nhwc(dskip, "pool_bwd_code.dskip")
+        assert (Nd, Hd, Wd, Cd) == (N, H, W, C)
+    Np, Hp, Wp, Cp, ldp = _nhwc(dpool, "pool_bwd_code.dpool")
+    assert (Np, Hp, Wp, Cp) == (N, H // 2, W // 2, C)
+    _check(_lib.lib().dpa_pool_bwd_code(_p(code), _p(dskip), c_int(ldd), _p(dpool), c_int(ldp), _p(g), c_int(ldg),
+                                        c_int(N), c_int(H), c_int(W), c_int(C), _stream(g)), "pool_bwd_code")
 
 
 def pool_bwd(skip: torch.Tensor, dskip: Optional[torch.Tensor], dpool: torch.Tensor, g: torch.Tensor):
@@ -325,3 +356,30 @@ def head_bwd(y: torch.Tensor, w: torch.Tensor, b: torch.Tensor, t: torch.Tensor,
     _check(L.dpa_head_bwd(_p(y), c_int(ldy), c_int(C), _p(w.reshape(-1).contiguous()), _p(b), _p(t), _p(dS), _p(gy),
                           c_int(C), _p(slab), _p(tmp), _p(gw), _p(gb), c_ll(P), _stream(y)), "head_bwd")
     return gy
+
+
+# ------------------------------------------------------------------------------------- loss tail
+class _LossFromPartials(torch.autograd.Function):
+    """loss = S0/n - log(2 S1 / (S2 + S3 + eps)) in one launch forward and one backward."""
+
+    @staticmethod
+    def forward(ctx, S, n: int, dice: bool):
+        assert S.dtype == torch.float32 and S.is_contiguous() and S.numel() == 4
+        out = torch.empty(5, dtype=torch.float32, device=S.device)
+        L = _lib.lib()
+        _check(L.dpa_loss_finish(_p(S), ctypes.c_float(1.0 / n), c_int(int(dice)), _p(out), _stream(S)), "loss_finish")
+        ctx.save_for_backward(out)
+        return out[0]
+
+    @staticmethod
+    def backward(ctx, g):
+        (out,) = ctx.saved_tensors
+        g = g.float().contiguous()
+        dS = torch.empty(4, dtype=torch.float32, device=out.device)
+        L = _lib.lib()
+        _check(L.dpa_loss_grad(_p(g), _p(out[1:]), ctypes.c_float(1.0), _p(dS), _stream(out)), "loss_grad")
+        return dS, None, None
+
+
+def loss_from_partials(S: torch.Tensor, n: int, dice: bool = True) -> torch.Tensor:
+    return _LossFromPartials.apply(S.contiguous(), n, dice)

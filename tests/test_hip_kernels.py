@@ -315,3 +315,91 @@ def test_conv_fused_maxpool(hip_lib, N, H, W, Cin, Cout):
     y = _nchw(cat[..., :Cout])
     assert _rel(y, F.relu(F.conv2d(x, w, b, padding=1))) < 2e-2
     assert torch.equal(_nchw(pooled), F.max_pool2d(y, 2, 2))      # pool of the stored values, exactly
+
+
+@pytest.mark.parametrize("dice", [True, False])
+def test_loss_from_partials_kernel(hip_lib, dice):
+    """Fused loss tail (csrc/unet_aux.hip loss_finish/loss_grad) == the torch formula, value and grad."""
+    from distributedpytorch_amd.ops import kernels as K
+    from distributedpytorch_amd.loss import EPS
+    S0 = torch.tensor([1234.5, 321.25, 800.0, 600.0], dtype=torch.float32)
+    n = 4096
+    a = S0.clone().cuda().requires_grad_(True)
+    la = K.loss_from_partials(a, n, dice)
+    (la * 3.0).backward()
+    b = S0.clone().requires_grad_(True)
+    lb = b[0] / n
+    if dice:
+        lb = lb - torch.log(2 * b[1] / (b[2] + b[3] + EPS))
+    (lb * 3.0).backward()
+    torch.testing.assert_close(la.cpu(), lb, rtol=1e-6, atol=1e-6)
+    torch.testing.assert_close(a.grad.cpu(), b.grad, rtol=1e-6, atol=1e-7)
+
+
+@pytest.mark.parametrize("N,H,W,C,fused", [(2, 6, 128, 32, True), (1, 8, 256, 64, True), (2, 10, 14, 32, False),
+                                           (1, 16, 16, 128, False)])
+def test_pool_codes_backward(hip_lib, N, H, W, C, fused):
+    """Window codes (argmax + ReLU masks) written by the fused streaming-conv pool epilogue or by
+    maxpool2 drive pool_bwd_code to the same gradient as the value-based pool_bwd (incl. ties)."""
+    from distributedpytorch_amd.ops import kernels as K
+    torch.manual_seed(9)
+    x = _bf(F.relu(torch.randn(N, C, H, W)))
+    w = _bf(torch.randn(C, C, 3, 3) * (2.0 / (9 * C)) ** 0.5)
+    b = torch.randn(C) * 0.1
+    packed, ng, kp = _pack_one(0, w, C)
+    cat = torch.zeros(N, H, W, 2 * C, dtype=torch.bfloat16, device="cuda")
+    pooled = torch.empty(N, H // 2, W // 2, C, dtype=torch.bfloat16, device="cuda")
+    code = torch.empty(N, H // 2, W // 2, C, dtype=torch.uint8, device="cuda")
+    K.igemm(_nhwc(x), packed, cat[..., :C], Ngemm=ng, Kpad=kp, KH=3, KW=3, stride=1, pad=1, Cs=C,
+            out_grid=(N, H, W), bias=b.cuda(), relu=True, pool=pooled, pcode=code, path="stream" if fused else "auto")
+    skip = cat[..., :C]
+    skip[:, 0, 0, :4] = skip[:, 0, 1, :4]          # force ties inside a window
+    skip[:, 1, 0, 4:8] = 0
+    K.maxpool2(skip, pooled, code)                 # codes of the edited values
+    dpool = torch.randn(N, H // 2, W // 2, C, device="cuda").to(torch.bfloat16)
+    dskip = torch.randn(N, H, W, C, device="cuda").to(torch.bfloat16)
+    g_ref = torch.empty(N, H, W, C, dtype=torch.bfloat16, device="cuda")
+    K.pool_bwd(skip, dskip, dpool, g_ref)
+    g = torch.empty_like(g_ref)
+    K.pool_bwd_code(code, dskip, dpool, g)
+    torch.cuda.synchronize()
+    assert torch.equal(g, g_ref)
+
+
+def test_stream_pool_codes_match_maxpool(hip_lib):
+    """Codes from the fused streaming epilogue == codes from maxpool2 on the stored conv output."""
+    from distributedpytorch_amd.ops import kernels as K
+    torch.manual_seed(10)
+    N, H, W, C = 2, 6, 128, 32
+    x = _bf(F.relu(torch.randn(N, C, H, W)))
+    w = _bf(torch.randn(C, C, 3, 3) * (2.0 / (9 * C)) ** 0.5)
+    packed, ng, kp = _pack_one(0, w, C)
+    y = torch.empty(N, H, W, C, dtype=torch.bfloat16, device="cuda")
+    pooled = torch.empty(N, H // 2, W // 2, C, dtype=torch.bfloat16, device="cuda")
+    code = torch.empty(N, H // 2, W // 2, C, dtype=torch.uint8, device="cuda")
+    K.igemm(_nhwc(x), packed, y, Ngemm=ng, Kpad=kp, KH=3, KW=3, stride=1, pad=1, Cs=C, out_grid=(N, H, W),
+            bias=(torch.randn(C) * 0.1).cuda(), relu=True, pool=pooled, pcode=code, path="stream")
+    p2, c2 = torch.empty_like(pooled), torch.empty_like(code)
+    K.maxpool2(y, p2, c2)
+    torch.cuda.synchronize()
+    assert torch.equal(pooled, p2) and torch.equal(code, c2)
+
+
+@pytest.mark.parametrize("N,H,W,Cin,Cout,path", [(2, 3, 256, 64, 32, "stream"), (1, 4, 128, 128, 64, "halo"),
+                                                 (2, 9, 13, 256, 128, "glds"), (2, 9, 13, 128, 64, "generic")])
+def test_dgrad_split_output(hip_lib, N, H, W, Cin, Cout, path):
+    """Split output (concat gradient as two dense tensors) == the interleaved output's halves."""
+    from distributedpytorch_amd.ops import kernels as K
+    torch.manual_seed(11)
+    w = _bf(torch.randn(Cout, Cin, 3, 3) * 0.05)
+    g = torch.randn(N, H, W, Cout, device="cuda").to(torch.bfloat16)
+    packed, ng, kp = _pack_one(1, w)
+    full = torch.empty(N, H, W, Cin, dtype=torch.bfloat16, device="cuda")
+    kw = dict(Ngemm=ng, Kpad=kp, KH=3, KW=3, stride=1, pad=1, Cs=Cout, out_grid=(N, H, W), path=path)
+    K.igemm(g, packed, full, **kw)
+    s = Cin // 2
+    lo = torch.empty(N, H, W, s, dtype=torch.bfloat16, device="cuda")
+    hi = torch.empty(N, H, W, Cin - s, dtype=torch.bfloat16, device="cuda")
+    K.igemm(g, packed, lo, y2=hi, split=s, **kw)
+    torch.cuda.synchronize()
+    assert torch.equal(lo, full[..., :s]) and torch.equal(hi, full[..., s:])

@@ -14,6 +14,12 @@ if [ -n "$PROF" ]; then
   (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof -o run -- python3 $R/bench.py $PROF > $R/gpurun_out/prof.log 2>&1); echo "prof rc=$?"
   python tools/prof_summary.py gpurun_out/prof > gpurun_out/prof_summary.txt 2>&1; head -40 gpurun_out/prof_summary.txt
 fi
+if [ -n "$PMC" ]; then
+  # hardware counters (own pass, kernel-trace only): PMC="<counters>" PMC_ARGS="<kbench args>"
+  R=$PWD; rm -rf gpurun_out/pmc
+  (cd /tmp && timeout -k 10 300 rocprofv3 --pmc $PMC --kernel-trace --output-format csv -d $R/gpurun_out/pmc -o run -- python3 $R/tools/kbench.py $PMC_ARGS > $R/gpurun_out/pmc.log 2>&1); echo "pmc rc=$?"
+  python tools/pmc_summary.py gpurun_out/pmc > gpurun_out/pmc_summary.txt 2>&1; cat gpurun_out/pmc_summary.txt | head -40
+fi
 if [ -n "$DDP_REHEARSAL" ]; then
   DPA_SAME_DEVICE=1 DPA_DIST_BACKEND=gloo timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 3 --warmup 2 --batch 4 > gpurun_out/ddp_rehearsal.log 2>&1; echo "ddp rehearsal rc=$?"; grep -v amdgpu.ids gpurun_out/ddp_rehearsal.log | tail -4
   DPA_SAME_DEVICE=1 DPA_DIST_BACKEND=gloo timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29518 train.py -t DDP --synthetic --synthetic-len 16 --img-size 128 -e 1 -b 2 --out-dir /tmp/ddp_train > gpurun_out/ddp_train.log 2>&1; echo "ddp train rc=$?"; grep -v amdgpu.ids gpurun_out/ddp_train.log | tail -4

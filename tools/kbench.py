@@ -39,6 +39,8 @@ def main():
     ap.add_argument("--svar", type=int, nargs="*", default=[], help="streaming-conv variants to time")
     ap.add_argument("--gvar", type=int, nargs="*", default=[], help="LDS-DMA (glds) kernel configs to time")
     ap.add_argument("--paths", default="stream,halo,generic", help="default paths to time")
+    ap.add_argument("--layout-probe", action="store_true",
+                    help="full-res memory-bound ops on concat halves (ld=2C) vs dense tensors (ld=C)")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     B, S = a.batch, a.img
@@ -85,6 +87,26 @@ def main():
             except Exception as e:
                 print(f"{name:14s} wgrad {path:8s}  n/a ({str(e)[:40]})", flush=True)
         del x, g, y, dx
+    if a.layout_probe:
+        C, H = 32, S
+        for ld in (2 * C, C):
+            big = torch.randn(B, H, H, ld, device=dev).to(torch.bfloat16)
+            big2 = torch.randn(B, H, H, ld, device=dev).to(torch.bfloat16)
+            skip, dskip = big[..., :C], big2[..., :C]
+            dpool = torch.randn(B, H // 2, H // 2, C, device=dev).to(torch.bfloat16)
+            g = torch.empty(B, H, H, C, device=dev, dtype=torch.bfloat16)
+            t = timeit(lambda: K.pool_bwd(skip, dskip, dpool, g), a.reps)
+            gb = (3 * B * H * H * C * 2 + B * H * H * C // 2) / 1e9
+            print(f"pool_bwd ld={ld:3d}      {t:9.1f} us {gb / t * 1e3:7.2f} TB/s(useful)", flush=True)
+            x = torch.randn(B, H // 2, H // 2, 2 * C, device=dev).to(torch.bfloat16)
+            wf = (torch.randn(4 * C * 2 * C, device=dev) * 0.05).to(torch.bfloat16)
+            for path, var in (("generic", 0), ("glds", 2)):
+                t = timeit(lambda: K.igemm(x, wf, big[..., ld - C:], Ngemm=4 * C, Kpad=2 * C, KH=1, KW=1, stride=1,
+                                           pad=0, Cs=2 * C, out_grid=(B, H // 2, H // 2), mode=1, Cout=C, path=path,
+                                           variant=var), a.reps)
+                gb = (B * H * H * C * 2 + B * H * H * C // 2) / 1e9
+                print(f"deconv4 fwd ld={ld:3d} {path:7s} {t:9.1f} us {gb / t * 1e3:7.2f} TB/s(useful)", flush=True)
+            del big, big2
     # transposed convs (k2 s2): fwd = 1x1 GEMM scattered into the concat buffer, dgrad = stride-2 gather
     for name, h, Cin, Cout in [("D1 512->256", S // 16, 512, 256), ("D2 256->128", S // 8, 256, 128),
                                ("D3 128->64", S // 4, 128, 64), ("D4 64->32", S // 2, 64, 32)]:
