@@ -1,0 +1,359 @@
+// BatchNorm(+ReLU) and bilinear x2 up-sampling for the UNet variant blocks on gfx950: NHWC bf16
+// activations, fp32 statistics and math, 16-byte accesses (8 channels per lane).
+//
+// The reference UNet has neither op (model/unet_parts.py:6-17 is Conv+ReLU, :51-54 ConvTranspose2d);
+// the north-star DoubleConv = Conv2d+BN+ReLU and the bilinear Up path are the variants listed next
+// to it (model/modelsummary.txt:153-247).  Semantics follow torch.nn.BatchNorm2d (training: biased
+// batch variance for normalisation, unbiased for running_var, running stats updated with
+// `momentum`; eval: running stats) and F.interpolate(scale_factor=2, mode="bilinear",
+// align_corners=False).
+//
+// Batch statistics are a deterministic two-level reduction (no float atomics): bn_partial_kernel
+// gives every block one row of per-channel partial sums in a slab [nblk][2][C] (256 threads = R
+// pixel rows x G groups of 8 channels, consecutive rows = consecutive pixels, so a block streams a
+// contiguous R*C*2-byte span when G*8 == C); bn_*_finalize_kernel sums the rows in a fixed order,
+// one block per channel.  The same pair computes the backward sums (sum g, sum g*(z-mean)).
+#include "common.h"
+
+// ------------------------------------------------------------------------------ batch statistics
+// MODE 0: s = sum z, q = sum z^2          (a = z)
+// MODE 1: s = sum g, q = sum g*(z - mean)  (a = g, z = conv output, mean = saved[c])
+template <int MODE>
+__global__ __launch_bounds__(256) void bn_partial_kernel(const bf16_t* __restrict__ a, int lda, const bf16_t* __restrict__ z,
+                                                         int ldz, const float* __restrict__ saved, long P, int C, int G,
+                                                         float* __restrict__ slab) {
+  __shared__ float red[256 * 16];
+  const int tid = threadIdx.x;
+  const int R = 256 / G;
+  const int g = tid % G, r = tid / G;
+  const int c0 = (blockIdx.y * G + g) * 8;
+  float s[8], q[8], mu[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    s[k] = 0.f;
+    q[k] = 0.f;
+    mu[k] = MODE ? saved[c0 + k] : 0.f;
+  }
+  for (long p = (long)blockIdx.x * R + r; p < P; p += (long)gridDim.x * R) {
+    const uint4 u = *reinterpret_cast<const uint4*>(a + p * lda + c0);
+    const unsigned* pu = &u.x;
+    if (MODE == 0) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float v0 = lo_bf(pu[e]), v1 = hi_bf(pu[e]);
+        s[2 * e] += v0; q[2 * e] = fmaf(v0, v0, q[2 * e]);
+        s[2 * e + 1] += v1; q[2 * e + 1] = fmaf(v1, v1, q[2 * e + 1]);
+      }
+    } else {
+      const uint4 w = *reinterpret_cast<const uint4*>(z + p * ldz + c0);
+      const unsigned* pw = &w.x;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float g0 = lo_bf(pu[e]), g1 = hi_bf(pu[e]);
+        s[2 * e] += g0; q[2 * e] = fmaf(g0, lo_bf(pw[e]) - mu[2 * e], q[2 * e]);
+        s[2 * e + 1] += g1; q[2 * e + 1] = fmaf(g1, hi_bf(pw[e]) - mu[2 * e + 1], q[2 * e + 1]);
+      }
+    }
+  }
+  float* row = red + r * (G * 16) + g * 16;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    row[k] = s[k];
+    row[8 + k] = q[k];
+  }
+  __syncthreads();
+  for (int j = tid; j < G * 16; j += 256) {
+    float acc = 0.f;
+    for (int rr = 0; rr < R; ++rr) acc += red[rr * G * 16 + j];
+    const int gg = j >> 4, k = j & 15;
+    const int c = (blockIdx.y * G + gg) * 8 + (k & 7);
+    slab[(long)blockIdx.x * 2 * C + (k >> 3) * C + c] = acc;
+  }
+}
+
+// one block per channel: fixed-order sums of the slab rows
+__device__ __forceinline__ void slab_pair(const float* slab, int nblk, int C, int c, float* red, float& s, float& q) {
+  float a = 0.f, b = 0.f;
+  for (int i = threadIdx.x; i < nblk; i += blockDim.x) {
+    a += slab[(long)i * 2 * C + c];
+    b += slab[(long)i * 2 * C + C + c];
+  }
+  s = block_sum_256(a, red);
+  q = block_sum_256(b, red);
+}
+
+// Forward coefficients y = z*coef[c] + coef[C+c].  train: batch statistics (saved = mean, invstd
+// for the backward; running stats updated in place); eval (slab == null): running statistics.
+__global__ __launch_bounds__(256) void bn_finalize_kernel(const float* __restrict__ slab, int nblk, int C, long P,
+                                                          const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                          float eps, float momentum, float* __restrict__ rmean,
+                                                          float* __restrict__ rvar, float* __restrict__ coef,
+                                                          float* __restrict__ saved) {
+  __shared__ float red[4];
+  const int c = blockIdx.x;
+  float mean, var;
+  if (slab) {
+    float s, q;
+    slab_pair(slab, nblk, C, c, red, s, q);
+    const double m = (double)s / (double)P;
+    double v = (double)q / (double)P - m * m;
+    if (v < 0.0) v = 0.0;
+    mean = (float)m;
+    var = (float)v;
+  } else {
+    mean = rmean[c];
+    var = rvar[c];
+  }
+  if (threadIdx.x != 0) return;
+  const float invstd = 1.f / sqrtf(var + eps);
+  const float sc = gamma[c] * invstd;
+  coef[c] = sc;
+  coef[C + c] = beta[c] - mean * sc;
+  if (slab) {
+    saved[c] = mean;
+    saved[C + c] = invstd;
+    if (rmean) {
+      const float unbiased = P > 1 ? var * (float)((double)P / (double)(P - 1)) : var;
+      rmean[c] = (1.f - momentum) * rmean[c] + momentum * mean;
+      rvar[c] = (1.f - momentum) * rvar[c] + momentum * unbiased;
+    }
+  }
+}
+
+// Backward coefficients dz = a*g + b*z + c (torch batch_norm_backward, training mode):
+//   xhat = (z-mean)*invstd,  dz = gamma*invstd*(g - mean(g) - xhat*mean(g*xhat))
+// and dgamma += sum g*xhat, dbeta += sum g (accumulated into the flat fp32 gradient buffer).
+__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __restrict__ slab, int nblk, int C, long P,
+                                                              const float* __restrict__ gamma, const float* __restrict__ saved,
+                                                              float* __restrict__ coef3, float* __restrict__ dgamma,
+                                                              float* __restrict__ dbeta) {
+  __shared__ float red[4];
+  const int c = blockIdx.x;
+  float sg, sgz;
+  slab_pair(slab, nblk, C, c, red, sg, sgz);
+  if (threadIdx.x != 0) return;
+  const float mean = saved[c], invstd = saved[C + c];
+  const float sgx = sgz * invstd;
+  if (dgamma) dgamma[c] += sgx;
+  if (dbeta) dbeta[c] += sg;
+  const float sc = gamma[c] * invstd;
+  const float inv_p = (float)(1.0 / (double)P);
+  const float b = -sc * invstd * sgx * inv_p;
+  coef3[c] = sc;
+  coef3[C + c] = b;
+  coef3[2 * C + c] = -sc * sg * inv_p - b * mean;
+}
+
+// ------------------------------------------------------------------------------ elementwise passes
+// y = relu?(z*coef[c] + coef[C+c]); y may be a channel slice of a wider tensor (concat half)
+__global__ __launch_bounds__(256) void bn_apply_kernel(const bf16_t* __restrict__ z, int ldz, bf16_t* __restrict__ y, int ldy,
+                                                       const float* __restrict__ coef, long P, int C, int relu) {
+  const int CC = C >> 3;
+  const long tot = P * CC;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < tot; i += (long)gridDim.x * blockDim.x) {
+    const int cc = (int)(i % CC);
+    const long p = i / CC;
+    const int c0 = cc * 8;
+    const uint4 u = *reinterpret_cast<const uint4*>(z + p * ldz + c0);
+    const unsigned* pu = &u.x;
+    unsigned o[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float v0 = fmaf(lo_bf(pu[e]), coef[c0 + 2 * e], coef[C + c0 + 2 * e]);
+      float v1 = fmaf(hi_bf(pu[e]), coef[c0 + 2 * e + 1], coef[C + c0 + 2 * e + 1]);
+      if (relu) {
+        v0 = fmaxf(v0, 0.f);
+        v1 = fmaxf(v1, 0.f);
+      }
+      o[e] = pack_bf2(v0, v1);
+    }
+    *reinterpret_cast<uint4*>(y + p * ldy + c0) = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+}
+
+// dz = coef3[c]*g + coef3[C+c]*z + coef3[2C+c]
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16_t* __restrict__ g, int ldg, const bf16_t* __restrict__ z,
+                                                           int ldz, const float* __restrict__ coef3, bf16_t* __restrict__ dz,
+                                                           int lddz, long P, int C) {
+  const int CC = C >> 3;
+  const long tot = P * CC;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < tot; i += (long)gridDim.x * blockDim.x) {
+    const int cc = (int)(i % CC);
+    const long p = i / CC;
+    const int c0 = cc * 8;
+    const uint4 ug = *reinterpret_cast<const uint4*>(g + p * ldg + c0);
+    const uint4 uz = *reinterpret_cast<const uint4*>(z + p * ldz + c0);
+    const unsigned* pg = &ug.x;
+    const unsigned* pz = &uz.x;
+    unsigned o[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int c = c0 + 2 * e;
+      const float v0 = fmaf(coef3[c], lo_bf(pg[e]), fmaf(coef3[C + c], lo_bf(pz[e]), coef3[2 * C + c]));
+      const float v1 = fmaf(coef3[c + 1], hi_bf(pg[e]), fmaf(coef3[C + c + 1], hi_bf(pz[e]), coef3[2 * C + c + 1]));
+      o[e] = pack_bf2(v0, v1);
+    }
+    *reinterpret_cast<uint4*>(dz + p * lddz + c0) = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+}
+
+// G = channel groups of 8 per block (power of two dividing C/8, <= 32) and the block grid
+static bool bn_shape(long P, int C, int& G, dim3& grid) {
+  if (C <= 0 || (C & 7) || P <= 0) return false;
+  const int CG = C / 8;
+  G = 1;
+  while (G * 2 <= 32 && CG % (G * 2) == 0) G *= 2;
+  const int R = 256 / G;
+  long nbx = (P + R - 1) / R;
+  if (nbx > 512) nbx = 512;
+  grid = dim3((unsigned)nbx, (unsigned)(CG / G));
+  return true;
+}
+
+DPA_API int dpa_bn_slab_rows(long long P, int C) {
+  int G;
+  dim3 grid;
+  return bn_shape(P, C, G, grid) ? (int)grid.x : 0;
+}
+
+// training forward: statistics of z -> coef (scale, shift), saved (mean, invstd), running stats;
+// eval forward (train == 0): coef from the running statistics.  Then y = relu?(bn(z)).
+DPA_API int dpa_bn_fwd(const bf16_t* z, int ldz, bf16_t* y, int ldy, long long P, int C, const float* gamma, const float* beta,
+                       float eps, float momentum, float* rmean, float* rvar, float* slab, float* coef, float* saved, int train,
+                       int relu, hipStream_t st) {
+  int G;
+  dim3 grid;
+  if (!bn_shape(P, C, G, grid) || (ldz & 7) || (ldy & 7)) return (int)hipErrorInvalidValue;
+  if (train) {
+    hipLaunchKernelGGL(bn_partial_kernel<0>, grid, dim3(256), 0, st, z, ldz, (const bf16_t*)nullptr, 0, (const float*)nullptr,
+                       (long)P, C, G, slab);
+    hipLaunchKernelGGL(bn_finalize_kernel, dim3(C), dim3(256), 0, st, slab, (int)grid.x, C, (long)P, gamma, beta, eps, momentum,
+                       rmean, rvar, coef, saved);
+  } else {
+    hipLaunchKernelGGL(bn_finalize_kernel, dim3(C), dim3(256), 0, st, (const float*)nullptr, 0, C, (long)P, gamma, beta, eps,
+                       momentum, rmean, rvar, coef, saved);
+  }
+  const long tot = (long)P * (C / 8);
+  hipLaunchKernelGGL(bn_apply_kernel, dim3(dpa_grid(tot, 256, 16384)), dim3(256), 0, st, z, ldz, y, ldy, coef, (long)P, C, relu);
+  return (int)hipGetLastError();
+}
+
+// training backward: g = dL/d(bn output) (ReLU mask already applied by the consumer) -> dz,
+// dgamma/dbeta accumulated.  coef3: scratch [3C].
+DPA_API int dpa_bn_bwd(const bf16_t* g, int ldg, const bf16_t* z, int ldz, bf16_t* dz, int lddz, long long P, int C,
+                       const float* gamma, const float* saved, float* slab, float* coef3, float* dgamma, float* dbeta,
+                       hipStream_t st) {
+  int G;
+  dim3 grid;
+  if (!bn_shape(P, C, G, grid) || (ldg & 7) || (ldz & 7) || (lddz & 7)) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(bn_partial_kernel<1>, grid, dim3(256), 0, st, g, ldg, z, ldz, saved, (long)P, C, G, slab);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(256), 0, st, slab, (int)grid.x, C, (long)P, gamma, saved, coef3,
+                     dgamma, dbeta);
+  const long tot = (long)P * (C / 8);
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(dpa_grid(tot, 256, 16384)), dim3(256), 0, st, g, ldg, z, ldz, coef3, dz, lddz,
+                     (long)P, C);
+  return (int)hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------ bilinear x2
+// torch upsample_bilinear2d, align_corners=False, scale 2: src = max((o + 0.5)/2 - 0.5, 0)
+__device__ __forceinline__ void up_src(int o, int I, int& i0, int& i1, float& l1) {
+  const float src = fmaxf((o + 0.5f) * 0.5f - 0.5f, 0.f);
+  i0 = min((int)src, I - 1);
+  i1 = min(i0 + 1, I - 1);
+  l1 = src - (float)i0;
+}
+
+// y[n][oh][ow][c] (2h x 2w, y may be the second half of a concat buffer) from x[n][h][w][c]
+__global__ __launch_bounds__(256) void up2_fwd_kernel(const bf16_t* __restrict__ x, int ldx, bf16_t* __restrict__ y, int ldy,
+                                                      int N, int h, int w, int C) {
+  const int CC = C >> 3, Ho = 2 * h, Wo = 2 * w;
+  const long tot = (long)N * Ho * Wo * CC;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < tot; i += (long)gridDim.x * blockDim.x) {
+    const int cc = (int)(i % CC);
+    const long op = i / CC;
+    const int ow = (int)(op % Wo);
+    const long t = op / Wo;
+    const int oh = (int)(t % Ho);
+    const int n = (int)(t / Ho);
+    int h0, h1, w0, w1;
+    float lh, lw;
+    up_src(oh, h, h0, h1, lh);
+    up_src(ow, w, w0, w1, lw);
+    const long base = (long)n * h * w;
+    const bf16_t* xc = x + cc * 8;
+    const uint4 a = *reinterpret_cast<const uint4*>(xc + (base + (long)h0 * w + w0) * ldx);
+    const uint4 b = *reinterpret_cast<const uint4*>(xc + (base + (long)h0 * w + w1) * ldx);
+    const uint4 c = *reinterpret_cast<const uint4*>(xc + (base + (long)h1 * w + w0) * ldx);
+    const uint4 d = *reinterpret_cast<const uint4*>(xc + (base + (long)h1 * w + w1) * ldx);
+    const unsigned *pa = &a.x, *pb = &b.x, *pc = &c.x, *pd = &d.x;
+    const float h0l = 1.f - lh, w0l = 1.f - lw;
+    unsigned o[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float v0 = h0l * (w0l * lo_bf(pa[e]) + lw * lo_bf(pb[e])) + lh * (w0l * lo_bf(pc[e]) + lw * lo_bf(pd[e]));
+      const float v1 = h0l * (w0l * hi_bf(pa[e]) + lw * hi_bf(pb[e])) + lh * (w0l * hi_bf(pc[e]) + lw * hi_bf(pd[e]));
+      o[e] = pack_bf2(v0, v1);
+    }
+    *reinterpret_cast<uint4*>(y + op * ldy + cc * 8) = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+}
+
+// weight of input index i in output o's interpolation (0 if o does not touch i)
+__device__ __forceinline__ float up_weight(int o, int I, int i) {
+  int i0, i1;
+  float l1;
+  up_src(o, I, i0, i1, l1);
+  return (i0 == i ? 1.f - l1 : 0.f) + (i1 == i ? l1 : 0.f);
+}
+
+// Backward as a gather (deterministic, no atomics): dx[i][j] = sum over the <= 5x5 output
+// neighbourhood o in [2i-2, 2i+2] of w_h(o, i) w_w(o', j) g[o][o'].
+__global__ __launch_bounds__(256) void up2_bwd_kernel(const bf16_t* __restrict__ g, int ldg, bf16_t* __restrict__ dx, int lddx,
+                                                      int N, int h, int w, int C) {
+  const int CC = C >> 3, Ho = 2 * h, Wo = 2 * w;
+  const long tot = (long)N * h * w * CC;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < tot; i += (long)gridDim.x * blockDim.x) {
+    const int cc = (int)(i % CC);
+    const long ip = i / CC;
+    const int iw = (int)(ip % w);
+    const long t = ip / w;
+    const int ih = (int)(t % h);
+    const int n = (int)(t / h);
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    const int oh0 = max(2 * ih - 2, 0), oh1 = min(2 * ih + 2, Ho - 1);
+    const int ow0 = max(2 * iw - 2, 0), ow1 = min(2 * iw + 2, Wo - 1);
+    for (int oh = oh0; oh <= oh1; ++oh) {
+      const float wh = up_weight(oh, h, ih);
+      if (wh == 0.f) continue;
+      for (int ow = ow0; ow <= ow1; ++ow) {
+        const float ww = up_weight(ow, w, iw);
+        if (ww == 0.f) continue;
+        const float wt = wh * ww;
+        const uint4 u = *reinterpret_cast<const uint4*>(g + (((long)n * Ho + oh) * Wo + ow) * ldg + cc * 8);
+        const unsigned* pu = &u.x;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          acc[2 * e] = fmaf(wt, lo_bf(pu[e]), acc[2 * e]);
+          acc[2 * e + 1] = fmaf(wt, hi_bf(pu[e]), acc[2 * e + 1]);
+        }
+      }
+    }
+    *reinterpret_cast<uint4*>(dx + ip * lddx + cc * 8) =
+        make_uint4(pack_bf2(acc[0], acc[1]), pack_bf2(acc[2], acc[3]), pack_bf2(acc[4], acc[5]), pack_bf2(acc[6], acc[7]));
+  }
+}
+
+DPA_API int dpa_up2_fwd(const bf16_t* x, int ldx, bf16_t* y, int ldy, int N, int h, int w, int C, hipStream_t st) {
+  if ((C & 7) || (ldx & 7) || (ldy & 7) || h < 1 || w < 1) return (int)hipErrorInvalidValue;
+  const long tot = (long)N * 4 * h * w * (C / 8);
+  hipLaunchKernelGGL(up2_fwd_kernel, dim3(dpa_grid(tot, 256, 16384)), dim3(256), 0, st, x, ldx, y, ldy, N, h, w, C);
+  return (int)hipGetLastError();
+}
+
+DPA_API int dpa_up2_bwd(const bf16_t* g, int ldg, bf16_t* dx, int lddx, int N, int h, int w, int C, hipStream_t st) {
+  if ((C & 7) || (ldg & 7) || (lddx & 7) || h < 1 || w < 1) return (int)hipErrorInvalidValue;
+  const long tot = (long)N * h * w * (C / 8);
+  hipLaunchKernelGGL(up2_bwd_kernel, dim3(dpa_grid(tot, 256, 16384)), dim3(256), 0, st, g, ldg, dx, lddx, N, h, w, C);
+  return (int)hipGetLastError();
+}

@@ -205,6 +205,8 @@ DPA_API int dpa_pool_bwd(const bf16_t* skip, int lds, const bf16_t* dskip, int l
 //   mode 1: Conv2d dgrad   dst[ci][tap*Cout + co]    = W[co][ci][8-tap]        (Ngemm=Cin,  K=9*Cout)
 //   mode 2: ConvT fwd      dst[(2i+j)*Cout+co][ci]   = W[ci][co][i][j]         (Ngemm=4*Cout, K=Cin)
 //   mode 3: ConvT dgrad    dst[ci][(2i+j)*Cout+co]   = W[ci][co][i][j]         (Ngemm=Cin, K=4*Cout)
+//   mode 4: Conv1x1 fwd    dst[co][ci]               = W[co][ci]               (Ngemm=Cout, K=Cin)
+//   mode 5: Conv1x1 dgrad  dst[ci][co]               = W[co][ci]               (Ngemm=Cin,  K=Cout)
 // k >= K (padding to Kpad) and ci >= Cin (first-layer channel padding) are zero.
 struct PackDesc {
   long long src;   // device address of the fp32 weight (PyTorch layout)
@@ -228,9 +230,13 @@ __global__ __launch_bounds__(256) void pack_kernel(bf16_t* __restrict__ packed,
     } else if (d.mode == 2) {
       const int ij = n / d.Cout, co = n - ij * d.Cout;
       if (k < d.Cin) v = W[((long)k * d.Cout + co) * 4 + ij];
-    } else {
+    } else if (d.mode == 3) {
       const int ij = k / d.Cout, co = k - ij * d.Cout;
       if (ij < 4) v = W[((long)n * d.Cout + co) * 4 + ij];
+    } else if (d.mode == 4) {
+      if (k < d.Cin) v = W[(long)n * d.Cin + k];
+    } else {
+      if (k < d.Cout) v = W[(long)k * d.Cin + n];
     }
     packed[d.dst + i] = f2bf(v);
   }

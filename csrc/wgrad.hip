@@ -195,14 +195,16 @@ static int launch_wgrad(const WgradArgs& a, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
-// kind: 0 = conv3x3 (T=9, B tap-dependent), 1 = transposed conv 2x2/s2 (T=4, A tap-dependent).
+// kind: 0 = conv3x3 (T=9, B tap-dependent), 1 = transposed conv 2x2/s2 (T=4, A tap-dependent),
+//       2 = conv1x1 (T=1; the bilinear Up path's projection).
 // cfg: 0 = auto; otherwise a tile id (see switch).  M % BM == 0 is required.
 DPA_API int dpa_wgrad(const WgradArgs* args, int kind, int cfg, hipStream_t st) {
   const WgradArgs& a = *args;
   if ((a.M & 31) || (a.lda & 7) || (a.ldb & 7) || (a.pix_per_split & 31) || a.splits < 1) return (int)hipErrorInvalidValue;
   if (cfg == 0) {
     if (kind == 0) cfg = (a.Nc <= 16) ? 1 : (a.M >= 64 && a.Nc >= 32) ? 3 : 2;
-    else cfg = (a.M >= 64 && a.Nc >= 64) ? 12 : 11;
+    else if (kind == 1) cfg = (a.M >= 64 && a.Nc >= 64) ? 12 : 11;
+    else cfg = (a.M % 64 == 0 && a.Nc >= 64) ? 22 : 21;
   }
   if (kind == 0) {
     switch (cfg) {
@@ -210,6 +212,12 @@ DPA_API int dpa_wgrad(const WgradArgs* args, int kind, int cfg, hipStream_t st) 
       case 2: if (a.M % 32) break; return launch_wgrad<32, 32, 16, 16, 9, false>(a, st);
       case 3: if (a.M % 64) break; return launch_wgrad<64, 32, 32, 16, 9, false>(a, st);
       case 4: if (a.M % 64) break; return launch_wgrad<64, 64, 32, 32, 9, false>(a, st);
+      default: break;
+    }
+  } else if (kind == 2) {
+    switch (cfg) {
+      case 21: if (a.M % 32) break; return launch_wgrad<32, 32, 16, 16, 1, false>(a, st);
+      case 22: if (a.M % 64) break; return launch_wgrad<64, 64, 32, 32, 1, false>(a, st);
       default: break;
     }
   } else {

@@ -80,7 +80,7 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--dtype", choices=["bf16", "fp32"], default="bf16")
     p.add_argument("--backend", choices=["auto", "hip", "torch"], default="auto",
                    help="hip = hand-written MI355X kernels; torch = stock PyTorch ops")
-    p.add_argument("--model", type=str, default="unet", help="model preset: unet | unet-xl | unet-bn64 | unet-tiny")
+    p.add_argument("--model", type=str, default="unet", help="model preset: unet | unet-xl | unet-bn64 | unet-bn | unet-bilinear | unet-bn-bilinear | unet-tiny | unet-tiny-bn")
     p.add_argument("--synthetic", action="store_true", help="use synthetic images/masks instead of data/")
     p.add_argument("--synthetic-len", type=int, default=64)
     p.add_argument("--data-dir", type=str, default="./data")

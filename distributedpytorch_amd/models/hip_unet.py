@@ -33,14 +33,16 @@ import torch
 
 from ..ops import kernels as K
 from ..optim import FlatParameterSpace
-from .unet import UNet
+from .unet import UNet, Up
 
 
 class _Conv:
-    """Packing bookkeeping for one Conv2d(3x3, pad 1) layer."""
+    """Packing bookkeeping for one Conv2d(3x3, pad 1) layer (+ the BatchNorm2d that follows it in
+    the BN variant: then the conv writes its raw output z and BN+ReLU is a separate fused pass)."""
 
-    def __init__(self, mod: torch.nn.Conv2d, cin_pad: int, need_dgrad: bool):
+    def __init__(self, mod: torch.nn.Conv2d, cin_pad: int, need_dgrad: bool, bn=None):
         self.mod = mod
+        self.bn = bn
         self.Cout, self.Cin = mod.out_channels, mod.in_channels
         self.Cs = cin_pad
         self.Kf = K.round_up(9 * self.Cs, 32)        # fwd: K = 9*Cs
@@ -58,13 +60,24 @@ class _Deconv:
         self.off_f = self.off_d = 0
 
 
+class _Up:
+    """Bilinear x2 + 1x1 projection (``models.unet.Up``).  Both are linear and the interpolation
+    weights sum to 1, so proj(up(x)) == up(proj(x)) including the bias: the 1x1 conv runs at the LOW
+    resolution (4x fewer MACs and bytes) and the up-sampling writes straight into the concat half."""
+
+    def __init__(self, mod):
+        self.mod = mod.proj
+        self.Cin, self.Cout = self.mod.in_channels, self.mod.out_channels
+        self.Kf = K.round_up(self.Cin, 32)
+        self.Kd = K.round_up(self.Cout, 32)
+        self.off_f = self.off_d = 0
+
+
 class HipBlocks:
     name = "hip"
 
     def __init__(self, model: UNet, dtype: str = "bf16", device=None):
         cfg = model.cfg
-        if cfg.batchnorm or cfg.bilinear:
-            raise NotImplementedError("hip backend: BatchNorm / bilinear UNet variants run on --backend torch")
         if dtype != "bf16":
             raise NotImplementedError("hip backend computes in bf16 (fp32 accumulate); use --backend torch for fp32")
         self.model = model
@@ -75,12 +88,17 @@ class HipBlocks:
         if not any(hasattr(p, "_dpa_space") for p in model.parameters()):
             FlatParameterSpace(model, device=self.device)     # standalone use: flatten here
         self.anchor = torch.zeros(1, device=self.device, requires_grad=True)
+        def bns(b):
+            return b.bns() if cfg.batchnorm else [None] * len(b.convs())
+
         self.enc_convs = [[_Conv(c, K.round_up(c.in_channels, 8) if (l == 0 and j == 0) else c.in_channels,
-                                 need_dgrad=not (l == 0 and j == 0))
-                           for j, c in enumerate(b.convs())] for l, b in enumerate(model.encoder.blocks())]
-        self.mid_convs = [_Conv(c, c.in_channels, True) for c in model.mid.convs()]
-        self.dec_convs = [[_Conv(c, c.in_channels, True) for c in b.convs()] for b in model.decoder.blocks()]
-        self.deconvs = [_Deconv(m) for m in model.decoder.ups()]
+                                 need_dgrad=not (l == 0 and j == 0), bn=bn)
+                           for j, (c, bn) in enumerate(zip(b.convs(), bns(b)))]
+                          for l, b in enumerate(model.encoder.blocks())]
+        self.mid_convs = [_Conv(c, c.in_channels, True, bn) for c, bn in zip(model.mid.convs(), bns(model.mid))]
+        self.dec_convs = [[_Conv(c, c.in_channels, True, bn) for c, bn in zip(b.convs(), bns(b))]
+                          for b in model.decoder.blocks()]
+        self.deconvs = [_Up(m) if isinstance(m, Up) else _Deconv(m) for m in model.decoder.ups()]
         for convs in self.enc_convs + [self.mid_convs] + self.dec_convs:
             for c in convs:
                 assert c.Cout % 32 == 0 and c.Cs % 8 == 0, "hip backend needs channel widths divisible by 32"
@@ -119,8 +137,12 @@ class HipBlocks:
         for d in self.deconvs:
             if not here(d.mod):
                 continue
-            d.off_f = add(2, d.mod.weight, d.Cout, d.Cin, d.Cin, 4 * d.Cout, d.Kf)
-            d.off_d = add(3, d.mod.weight, d.Cout, d.Cin, d.Cout, d.Cin, d.Kd)
+            if isinstance(d, _Up):
+                d.off_f = add(4, d.mod.weight, d.Cout, d.Cin, d.Cin, d.Cout, d.Kf)
+                d.off_d = add(5, d.mod.weight, d.Cout, d.Cin, d.Cout, d.Cin, d.Kd)
+            else:
+                d.off_f = add(2, d.mod.weight, d.Cout, d.Cin, d.Cin, 4 * d.Cout, d.Kf)
+                d.off_d = add(3, d.mod.weight, d.Cout, d.Cin, d.Cout, d.Cin, d.Kd)
         self.packed = torch.zeros(max(off, 64), dtype=torch.bfloat16, device=self.device)
         raw = (K.PackDesc * len(descs))(*descs)
         host = torch.frombuffer(bytearray(bytes(raw)), dtype=torch.uint8)
@@ -138,20 +160,39 @@ class HipBlocks:
             self._packed_version = v
 
     def wf(self, c):
-        return self.packed[c.off_f:c.off_f + (c.Cout if isinstance(c, _Conv) else 4 * c.Cout) * c.Kf]
+        return self.packed[c.off_f:c.off_f + (4 * c.Cout if isinstance(c, _Deconv) else c.Cout) * c.Kf]
 
     def wd(self, c):
         return self.packed[c.off_d:c.off_d + c.Cin * c.Kd]
 
     # ------------------------------------------------------------------ primitive launches
     def conv_fwd(self, c: _Conv, x: torch.Tensor, y: torch.Tensor = None, pool: torch.Tensor = None,
-                 pcode: torch.Tensor = None):
+                 pcode: torch.Tensor = None, st: list = None):
+        """relu(conv(x)) -> y (and its 2x2 max-pool + window codes).  BN variant: the conv writes z,
+        then one statistics pass + one normalise/ReLU pass; ``st`` receives (z, saved) for the backward."""
         N, H, W = x.shape[:3]
         if y is None:
             y = torch.empty(N, H, W, c.Cout, dtype=torch.bfloat16, device=x.device)
-        K.igemm(x, self.wf(c), y, Ngemm=c.Cout, Kpad=c.Kf, KH=3, KW=3, stride=1, pad=1, Cs=c.Cs, out_grid=(N, H, W),
-                bias=c.mod.bias, relu=True, pool=pool, pcode=pcode)
+        if c.bn is None:
+            K.igemm(x, self.wf(c), y, Ngemm=c.Cout, Kpad=c.Kf, KH=3, KW=3, stride=1, pad=1, Cs=c.Cs,
+                    out_grid=(N, H, W), bias=c.mod.bias, relu=True, pool=pool, pcode=pcode)
+            return y
+        z = torch.empty(N, H, W, c.Cout, dtype=torch.bfloat16, device=x.device)
+        K.igemm(x, self.wf(c), z, Ngemm=c.Cout, Kpad=c.Kf, KH=3, KW=3, stride=1, pad=1, Cs=c.Cs, out_grid=(N, H, W),
+                bias=c.mod.bias, relu=False)
+        saved = K.bn_fwd(z, y, c.bn, train=self.model.training)
+        if pool is not None:
+            K.maxpool2(y, pool, pcode)
+        if st is not None:
+            st.append((z, saved))
         return y
+
+    def bn_bwd(self, c: _Conv, g: torch.Tensor, st):
+        """gradient w.r.t. the conv output: identity without BN, BatchNorm backward with it."""
+        if c.bn is None:
+            return g
+        z, saved = st
+        return K.bn_bwd(g, z, saved, c.bn, _grad(c.bn.weight), _grad(c.bn.bias))
 
     def conv_dgrad(self, c: _Conv, g: torch.Tensor, mask: torch.Tensor = None, out: torch.Tensor = None):
         N, H, W = g.shape[:3]
@@ -180,24 +221,40 @@ class HipBlocks:
 
     def deconv_fwd(self, d: _Deconv, x: torch.Tensor, out: torch.Tensor):
         N, h, w = x.shape[:3]
+        if isinstance(d, _Up):
+            low = torch.empty(N, h, w, d.Cout, dtype=torch.bfloat16, device=x.device)
+            K.igemm(x, self.wf(d), low, Ngemm=d.Cout, Kpad=d.Kf, KH=1, KW=1, stride=1, pad=0, Cs=d.Cin,
+                    out_grid=(N, h, w), bias=d.mod.bias)
+            K.up2_fwd(low, out)
+            return
         K.igemm(x, self.wf(d), out, Ngemm=4 * d.Cout, Kpad=d.Kf, KH=1, KW=1, stride=1, pad=0, Cs=d.Cin,
                 out_grid=(N, h, w), bias=d.mod.bias, mode=1, Cout=d.Cout)
 
     def deconv_dgrad(self, d: _Deconv, gup: torch.Tensor, x: torch.Tensor):
         N, h, w = x.shape[:3]
         dx = torch.empty(N, h, w, d.Cin, dtype=torch.bfloat16, device=x.device)
+        if isinstance(d, _Up):   # gup is the low-resolution gradient here (see _DecFn.backward)
+            K.igemm(gup, self.wd(d), dx, Ngemm=d.Cin, Kpad=d.Kd, KH=1, KW=1, stride=1, pad=0, Cs=d.Cout,
+                    out_grid=(N, h, w), mask=x)
+            return dx
         K.igemm(gup, self.wd(d), dx, Ngemm=d.Cin, Kpad=d.Kd, KH=2, KW=2, stride=2, pad=0, Cs=d.Cout,
                 out_grid=(N, h, w), mask=x)
         return dx
 
     def deconv_wgrad(self, d: _Deconv, gup: torch.Tensor, x: torch.Tensor):
         N, h, w = x.shape[:3]
+        if isinstance(d, _Up):
+            K.wgrad(gup, x, kind=2, grid=(N, h, w), M=d.Cout, Nc=d.Cin, s=1, pad=0, KW=1,
+                    gw=_grad(d.mod.weight).view(-1), gb=_grad(d.mod.bias), Nreal=d.Cin)
+            return
         K.wgrad(gup, x, kind=1, grid=(N, h, w), M=d.Cout, Nc=d.Cin, s=2, pad=0, KW=2, gw=_grad(d.mod.weight).view(-1),
                 gb=_grad(d.mod.bias), Nreal=d.Cin)
 
     def ready(self, mods):
         by_space = {}
         for m in mods:
+            if m is None:
+                continue
             for p in (m.weight, m.bias):
                 sp = getattr(p, "_dpa_space", None)
                 if sp is not None:
@@ -277,17 +334,19 @@ class _EncFn(torch.autograd.Function):
         c1, c2 = B.enc_convs[l]
         x = _v(x)
         N, H, W = x.shape[:3]
-        a = B.conv_fwd(c1, x)
+        st1, st2 = [], []
+        a = B.conv_fwd(c1, x, st=st1)
         cat = B.new_cat(N, H, W, c2.Cout)
         skip = cat[..., :c2.Cout]
         pooled = torch.empty(N, H // 2, W // 2, c2.Cout, dtype=torch.bfloat16, device=x.device)
         # window codes (argmax + ReLU masks) for the backward: it then never re-reads the skip
         code = (torch.empty(N, H // 2, W // 2, c2.Cout, dtype=torch.uint8, device=x.device)
                 if H % 2 == 0 and W % 2 == 0 else None)
-        B.conv_fwd(c2, a, skip, pool=pooled, pcode=code)   # pool fused into the conv epilogue when streaming
+        B.conv_fwd(c2, a, skip, pool=pooled, pcode=code, st=st2)   # pool fused into the conv epilogue when streaming
         ctx.B, ctx.l = B, l
         ctx.x_needs_grad = l > 0
         ctx.has_code = code is not None
+        ctx.st = (st1[0] if st1 else None, st2[0] if st2 else None)
         ctx.save_for_backward(x, a, cat, code if code is not None else cat)
         return _o(skip), _o(pooled)
 
@@ -295,6 +354,7 @@ class _EncFn(torch.autograd.Function):
     def backward(ctx, dskip, dpooled):
         B, l = ctx.B, ctx.l
         x, a, cat, code = ctx.saved_tensors
+        st1, st2 = ctx.st
         c1, c2 = B.enc_convs[l]
         C = c2.Cout
         skip = cat[..., :C]
@@ -308,12 +368,15 @@ class _EncFn(torch.autograd.Function):
             K.pool_bwd_code(code, dskip, dpooled, g2)
         else:
             K.pool_bwd(skip, dskip, dpooled, g2)
+        g2 = B.bn_bwd(c2, g2, st2)
         g1 = B.conv_dgrad(c2, g2, mask=a)
         B.conv_wgrad(c2, g2, a)
-        B.ready([c2.mod])
+        B.ready([c2.mod, c2.bn])
+        g1 = B.bn_bwd(c1, g1, st1)
         gx = B.conv_dgrad(c1, g1) if ctx.x_needs_grad else None
         B.conv_wgrad(c1, g1, x)
-        B.ready([c1.mod])
+        B.ready([c1.mod, c1.bn])
+        ctx.st = None
         return None, (None if gx is None else _o(gx)), None, None
 
 
@@ -322,9 +385,11 @@ class _MidFn(torch.autograd.Function):
     def forward(ctx, anchor, x, B: HipBlocks):
         c1, c2 = B.mid_convs
         x = _v(x)
-        a = B.conv_fwd(c1, x)
-        y = B.conv_fwd(c2, a)
+        st1, st2 = [], []
+        a = B.conv_fwd(c1, x, st=st1)
+        y = B.conv_fwd(c2, a, st=st2)
         ctx.B = B
+        ctx.st = (st1[0] if st1 else None, st2[0] if st2 else None)
         ctx.save_for_backward(x, a)
         return _o(y)
 
@@ -332,14 +397,17 @@ class _MidFn(torch.autograd.Function):
     def backward(ctx, g2):
         B = ctx.B
         x, a = ctx.saved_tensors
+        st1, st2 = ctx.st
         c1, c2 = B.mid_convs
-        g2 = _v(g2)
+        g2 = B.bn_bwd(c2, _v(g2), st2)
         g1 = B.conv_dgrad(c2, g2, mask=a)
         B.conv_wgrad(c2, g2, a)
-        B.ready([c2.mod])
+        B.ready([c2.mod, c2.bn])
+        g1 = B.bn_bwd(c1, g1, st1)
         gx = B.conv_dgrad(c1, g1)
         B.conv_wgrad(c1, g1, x)
-        B.ready([c1.mod])
+        B.ready([c1.mod, c1.bn])
+        ctx.st = None
         return None, _o(gx), None
 
 
@@ -352,9 +420,11 @@ class _DecFn(torch.autograd.Function):
         x = _v(x)
         cat = B.cat_for(_v(skip))
         B.deconv_fwd(d, x, cat[..., C:])
-        a = B.conv_fwd(c1, cat)
-        y = B.conv_fwd(c2, a)
+        st1, st2 = [], []
+        a = B.conv_fwd(c1, cat, st=st1)
+        y = B.conv_fwd(c2, a, st=st2)
         ctx.B, ctx.i = B, i
+        ctx.st = (st1[0] if st1 else None, st2[0] if st2 else None)
         ctx.save_for_backward(x, cat, a)
         return _o(y)
 
@@ -362,19 +432,24 @@ class _DecFn(torch.autograd.Function):
     def backward(ctx, g2):
         B, i = ctx.B, ctx.i
         x, cat, a = ctx.saved_tensors
+        st1, st2 = ctx.st
         d = B.deconvs[i]
         c1, c2 = B.dec_convs[i]
         C = d.Cout
-        g2 = _v(g2)
+        g2 = B.bn_bwd(c2, _v(g2), st2)
         g1 = B.conv_dgrad(c2, g2, mask=a)
         B.conv_wgrad(c2, g2, a)
-        B.ready([c2.mod])
+        B.ready([c2.mod, c2.bn])
+        g1 = B.bn_bwd(c1, g1, st1)
         dskip, gup = B.conv_dgrad_split(c1, g1, C)
         B.conv_wgrad(c1, g1, cat)
-        B.ready([c1.mod])
+        B.ready([c1.mod, c1.bn])
+        if isinstance(d, _Up):
+            gup = K.up2_bwd(gup)          # to the projection's (low) resolution
         dx = B.deconv_dgrad(d, gup, x)
         B.deconv_wgrad(d, gup, x)
         B.ready([d.mod])
+        ctx.st = None
         return None, _o(dx), _o(dskip), None, None
 
 

@@ -57,8 +57,13 @@ PRESETS = {
     "unet-xl": UNetConfig(base=64, depth=5),
     # milesial-style variant listed in model/modelsummary.txt:153-247 (BN, base 64)
     "unet-bn64": UNetConfig(base=64, batchnorm=True),
-    # tiny config for fast CPU tests
+    # north-star block variants at the reference width: DoubleConv = Conv2d+BN+ReLU, bilinear Up
+    "unet-bn": UNetConfig(batchnorm=True),
+    "unet-bilinear": UNetConfig(bilinear=True),
+    "unet-bn-bilinear": UNetConfig(batchnorm=True, bilinear=True),
+    # tiny configs for fast CPU tests
     "unet-tiny": UNetConfig(base=8, depth=2),
+    "unet-tiny-bn": UNetConfig(base=8, depth=2, batchnorm=True, bilinear=True),
 }
 
 

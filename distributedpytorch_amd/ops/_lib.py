@@ -52,10 +52,13 @@ def _declare(L):
     for name in ("dpa_version", "dpa_igemm", "dpa_wgrad", "dpa_wgrad_reduce", "dpa_input_nhwc8", "dpa_maxpool2",
                  "dpa_pool_bwd", "dpa_pack_weights", "dpa_head_fwd", "dpa_head_bwd", "dpa_adam_flat",
                  "dpa_igemm_halo", "dpa_wgrad_halo", "dpa_igemm_stream", "dpa_wgrad_stream", "dpa_adam_flat_dev", "dpa_igemm_glds",
-                 "dpa_loss_finish", "dpa_loss_grad", "dpa_pool_bwd_code"):
+                 "dpa_loss_finish", "dpa_loss_grad", "dpa_pool_bwd_code", "dpa_bn_fwd", "dpa_bn_bwd",
+                 "dpa_up2_fwd", "dpa_up2_bwd"):
         getattr(L, name).restype = ctypes.c_int
     L.dpa_head_slab_blocks.restype = ctypes.c_int
     L.dpa_head_slab_blocks.argtypes = [ctypes.c_longlong]
+    L.dpa_bn_slab_rows.restype = ctypes.c_int
+    L.dpa_bn_slab_rows.argtypes = [ctypes.c_longlong, ctypes.c_int]
     L.dpa_error_string.restype = ctypes.c_char_p
 
 

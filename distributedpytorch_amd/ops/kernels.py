@@ -8,6 +8,8 @@ fallback: on a GPU the library must be present (``_lib.lib()`` raises otherwise)
 Kernel map:  conv3x3 fwd / dgrad, convT fwd / dgrad -> ``igemm``;  conv / convT
 weight gradients -> ``wgrad`` + ``wgrad_reduce``;  max-pool (K5) -> ``maxpool2`` / ``pool_bwd``;
 segmap + sigmoid + BCE + Dice (K8-K11) -> ``head_fwd`` / ``head_bwd``;  Adam (K13) -> ``adam_step``.
+Variant blocks (north-star DoubleConv with BatchNorm, bilinear Up): ``bn_fwd`` / ``bn_bwd``,
+``up2_fwd`` / ``up2_bwd`` (csrc/norm_up.hip) and the 1x1 projection through ``igemm`` / ``wgrad(kind=2)``.
 """
 from __future__ import annotations
 
@@ -193,7 +195,8 @@ def wgrad_splits(P: int, tiles: int, target_blocks: int = 1024, min_pix: int = 5
 def wgrad(A: torch.Tensor, B: torch.Tensor, *, kind: int, grid, M: int, Nc: int, s: int, pad: int, KW: int,
           gw: torch.Tensor, gb: Optional[torch.Tensor], Nreal: int, cfg: int = 0, target_blocks: int = 1024,
           path: str = "auto"):
-    """Weight (+bias) gradient of a conv3x3 (kind 0) or transposed conv 2x2/s2 (kind 1); accumulates into gw/gb.
+    """Weight (+bias) gradient of a conv3x3 (kind 0), transposed conv 2x2/s2 (kind 1) or conv1x1
+    (kind 2); accumulates into gw/gb.
 
     ``path``: ``auto`` = row-streaming kernel when W % 64 == 0, else row-halo (W % 32 == 0), else the
     generic per-tap gather kernel; ``stream`` / ``halo`` / ``generic`` force one."""
@@ -206,8 +209,8 @@ def wgrad(A: torch.Tensor, B: torch.Tensor, *, kind: int, grid, M: int, Nc: int,
     NB, HB, WB, CB, ldb = _nhwc(B, "wgrad.B")
     N, Hg, Wg = grid
     assert NA == NB == N and CA >= M and CB >= Nc and M % 32 == 0
-    T = 9 if kind == 0 else 4
-    if kind == 0:
+    T = {0: 9, 1: 4, 2: 1}[kind]
+    if kind in (0, 2):
         assert (HA, WA) == (Hg, Wg) and (HB, WB) == (Hg, Wg)
     else:
         assert (HA, WA) == (2 * Hg, 2 * Wg) and (HB, WB) == (Hg, Wg)
@@ -220,9 +223,12 @@ def wgrad(A: torch.Tensor, B: torch.Tensor, *, kind: int, grid, M: int, Nc: int,
         if cfg == 0:
             if kind == 0:
                 cfg = 1 if Nc <= 16 else (3 if M % 64 == 0 else 2)
-            else:
+            elif kind == 1:
                 cfg = 12 if (M % 64 == 0 and Nc >= 64) else 11
-        bm, bn = {1: (32, 16), 2: (32, 32), 3: (64, 32), 4: (64, 64), 11: (32, 32), 12: (64, 64)}[cfg]
+            else:
+                cfg = 22 if (M % 64 == 0 and Nc >= 64) else 21
+        bm, bn = {1: (32, 16), 2: (32, 32), 3: (64, 32), 4: (64, 64), 11: (32, 32), 12: (64, 64), 21: (32, 32),
+                  22: (64, 64)}[cfg]
     tiles = (M // bm) * (-(-Nc // bn))
     assert gw.dtype == torch.float32 and gw.is_contiguous() and gw.numel() == M * Nreal * T
     L = _lib.lib()
@@ -236,12 +242,14 @@ def wgrad(A: torch.Tensor, B: torch.Tensor, *, kind: int, grid, M: int, Nc: int,
         a = WgradArgs(A[n0:n1].data_ptr(), B[n0:n1].data_ptr(), slab.data_ptr(),
                       None if bslab is None else bslab.data_ptr(), lda, ldb, nb, Hg, Wg, HA, WA, HB, WB, M, Nc, s,
                       pad, KW, pps, splits, _extent_bytes(nb, HA, WA, CA, lda), _extent_bytes(nb, HB, WB, CB, ldb))
+        if kind == 2:
+            assert s == 1 and pad == 0 and KW == 1
         if halo:
             _check(L.dpa_wgrad_halo(ctypes.byref(a), c_int(hcfg), st), "wgrad_halo")
         else:
             _check(L.dpa_wgrad(ctypes.byref(a), c_int(kind), c_int(cfg), st), "wgrad")
         _check(L.dpa_wgrad_reduce(_p(slab), _p(bslab), _p(gw), _p(gb), c_int(splits), c_int(T), c_int(M), c_int(Nc),
-                                  c_int(Nreal), c_int(kind), st), "wgrad_reduce")
+                                  c_int(Nreal), c_int(1 if kind == 1 else 0), st), "wgrad_reduce")
 
 
 def _wgrad_stream(A, B, *, grid, M, Nc, gw, gb, Nreal):
@@ -356,6 +364,83 @@ def head_bwd(y: torch.Tensor, w: torch.Tensor, b: torch.Tensor, t: torch.Tensor,
     _check(L.dpa_head_bwd(_p(y), c_int(ldy), c_int(C), _p(w.reshape(-1).contiguous()), _p(b), _p(t), _p(dS), _p(gy),
                           c_int(C), _p(slab), _p(tmp), _p(gw), _p(gb), c_ll(P), _stream(y)), "head_bwd")
     return gy
+
+
+# ------------------------------------------------------------------------------------- BN / bilinear
+def _flat_f32(t: torch.Tensor, n: int, name: str):
+    assert t.dtype == torch.float32 and t.is_contiguous() and t.numel() == n and t.is_cuda, f"{name}: need fp32[{n}]"
+    return t
+
+
+def bn_fwd(z: torch.Tensor, y: torch.Tensor, bn: torch.nn.BatchNorm2d, train: bool, relu: bool = True):
+    """y = relu(BatchNorm2d(z)) (NHWC bf16; y may be a concat half).  Training: batch statistics,
+    running stats updated (torch momentum semantics); returns ``saved`` = [mean, invstd] (fp32 [2C])
+    for :func:`bn_bwd`.  Eval: running statistics, returns None."""
+    N, H, W, C, ldz = _nhwc(z, "bn.z")
+    Ny, Hy, Wy, Cy, ldy = _nhwc(y, "bn.y")
+    assert (Ny, Hy, Wy, Cy) == (N, H, W, C) and bn.num_features == C and bn.affine
+    P = N * H * W
+    L = _lib.lib()
+    rows = L.dpa_bn_slab_rows(c_ll(P), c_int(C))
+    assert rows > 0, f"bn: unsupported shape P={P} C={C}"
+    gamma, beta = _flat_f32(bn.weight, C, "bn.weight"), _flat_f32(bn.bias, C, "bn.bias")
+    track = bn.track_running_stats and bn.running_mean is not None
+    use_batch = train or not track
+    scratch = torch.empty(rows * 2 * C + 4 * C, dtype=torch.float32, device=z.device)
+    slab, coef, saved = scratch[:rows * 2 * C], scratch[rows * 2 * C:rows * 2 * C + 2 * C], scratch[rows * 2 * C + 2 * C:]
+    rm = rv = None
+    if track:
+        rm, rv = _flat_f32(bn.running_mean, C, "bn.running_mean"), _flat_f32(bn.running_var, C, "bn.running_var")
+        if train and bn.num_batches_tracked is not None:
+            bn.num_batches_tracked.add_(1)
+    if bn.momentum is not None:
+        mom = bn.momentum
+    else:   # cumulative moving average (torch: momentum = 1 / num_batches_tracked)
+        mom = 1.0 / max(1, int(bn.num_batches_tracked.item())) if track else 0.0
+    # running stats: updated when training, read in eval (use_batch False), untouched otherwise
+    _check(L.dpa_bn_fwd(_p(z), c_int(ldz), _p(y), c_int(ldy), c_ll(P), c_int(C), _p(gamma), _p(beta),
+                        ctypes.c_float(bn.eps), ctypes.c_float(mom), _p(rm), _p(rv), _p(slab) if use_batch else None,
+                        _p(coef), _p(saved), c_int(int(use_batch)), c_int(int(relu)), _stream(z)), "bn_fwd")
+    return saved if use_batch else None
+
+
+def bn_bwd(g: torch.Tensor, z: torch.Tensor, saved: torch.Tensor, bn: torch.nn.BatchNorm2d,
+           dgamma: Optional[torch.Tensor], dbeta: Optional[torch.Tensor]) -> torch.Tensor:
+    """dz from g = dL/d(BN output) (ReLU mask already applied); dgamma/dbeta += (fp32 [C])."""
+    N, H, W, C, ldg = _nhwc(g, "bn_bwd.g")
+    Nz, Hz, Wz, Cz, ldz = _nhwc(z, "bn_bwd.z")
+    assert (Nz, Hz, Wz, Cz) == (N, H, W, C) and saved.numel() == 2 * C
+    P = N * H * W
+    L = _lib.lib()
+    rows = L.dpa_bn_slab_rows(c_ll(P), c_int(C))
+    dz = torch.empty(N, H, W, C, dtype=torch.bfloat16, device=g.device)
+    scratch = torch.empty(rows * 2 * C + 3 * C, dtype=torch.float32, device=g.device)
+    if dgamma is not None:
+        _flat_f32(dgamma, C, "bn.dgamma")
+    if dbeta is not None:
+        _flat_f32(dbeta, C, "bn.dbeta")
+    _check(L.dpa_bn_bwd(_p(g), c_int(ldg), _p(z), c_int(ldz), _p(dz), c_int(C), c_ll(P), c_int(C),
+                        _p(_flat_f32(bn.weight, C, "bn.weight")), _p(saved), _p(scratch[:rows * 2 * C]),
+                        _p(scratch[rows * 2 * C:]), _p(dgamma), _p(dbeta), _stream(g)), "bn_bwd")
+    return dz
+
+
+def up2_fwd(x: torch.Tensor, y: torch.Tensor):
+    """Bilinear x2 up-sampling (align_corners=False) of NHWC x into y (may be a concat half)."""
+    N, h, w, C, ldx = _nhwc(x, "up2.x")
+    Ny, Hy, Wy, Cy, ldy = _nhwc(y, "up2.y")
+    assert (Ny, Hy, Wy, Cy) == (N, 2 * h, 2 * w, C)
+    _check(_lib.lib().dpa_up2_fwd(_p(x), c_int(ldx), _p(y), c_int(ldy), c_int(N), c_int(h), c_int(w), c_int(C),
+                                  _stream(x)), "up2_fwd")
+
+
+def up2_bwd(g: torch.Tensor) -> torch.Tensor:
+    N, H, W, C, ldg = _nhwc(g, "up2_bwd.g")
+    assert H % 2 == 0 and W % 2 == 0
+    dx = torch.empty(N, H // 2, W // 2, C, dtype=torch.bfloat16, device=g.device)
+    _check(_lib.lib().dpa_up2_bwd(_p(g), c_int(ldg), _p(dx), c_int(C), c_int(N), c_int(H // 2), c_int(W // 2), c_int(C),
+                                  _stream(g)), "up2_bwd")
+    return dx
 
 
 # ------------------------------------------------------------------------------------- loss tail

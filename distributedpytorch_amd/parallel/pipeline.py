@@ -60,6 +60,13 @@ def stage_param_names(model, start: int, end: int) -> List[str]:
     return [n for n, _ in model.named_parameters() if any(n.startswith(p) for p in prefixes)]
 
 
+def stage_buffer_names(model, start: int, end: int) -> List[str]:
+    """Buffers (BatchNorm running statistics) of the blocks in ``[start, end)``."""
+    depth = model.cfg.depth
+    prefixes = [p for idx in range(start, end) for p in _block_param_prefixes(idx, depth)]
+    return [n for n, _ in model.named_buffers() if any(n.startswith(p) for p in prefixes)]
+
+
 def _tensor_producer(name: str, cut_start: int, cuts: Sequence[int], depth: int) -> int:
     """Stage that produces boundary tensor ``name`` entering the stage starting at ``cut_start``."""
     if name == "x":
@@ -270,13 +277,13 @@ class GPipeDist:
         return out.get("probs")
 
     def gather_state_dict(self):
-        """Full model state dict on stage 0 (other stages send their parameters)."""
-        names = stage_param_names(self.model, self.start, self.end)
-        params = dict(self.model.named_parameters())
+        """Full model state dict on stage 0 (other stages send their parameters and buffers)."""
+        params = {**dict(self.model.named_parameters()), **dict(self.model.named_buffers())}
         all_cuts = self.cuts
         sd = {}
         for s in range(self.S):
-            snames = stage_param_names(self.model, all_cuts[s], all_cuts[s + 1])
+            snames = (stage_param_names(self.model, all_cuts[s], all_cuts[s + 1])
+                      + stage_buffer_names(self.model, all_cuts[s], all_cuts[s + 1]))
             for n in snames:
                 if s == 0:
                     if self.rank == 0:
@@ -287,7 +294,6 @@ class GPipeDist:
                     t = torch.empty_like(params[n])
                     dist.recv(t, src=self._glob(s), group=self.group)
                     sd[n] = t
-        del names
         if self.rank == 0:
             full = self.model.state_dict()
             return {k: sd.get(k, v) for k, v in full.items()}
@@ -311,6 +317,10 @@ class GPipeLocal:
                 mod_name, _, pname = n.rpartition(".")
                 mod = model.get_submodule(mod_name)
                 setattr(mod, pname, torch.nn.Parameter(getattr(mod, pname).detach().to(self.devices[s])))
+            for n in stage_buffer_names(model, self.cuts[s], self.cuts[s + 1]):
+                mod_name, _, bname = n.rpartition(".")
+                mod = model.get_submodule(mod_name)
+                setattr(mod, bname, getattr(mod, bname).to(self.devices[s]))
         self.spaces = []
         for s in range(self.S):
             names = set(stage_param_names(model, self.cuts[s], self.cuts[s + 1]))

@@ -28,7 +28,7 @@ from .data.loaders import DeviceBatcher
 from .loss import dice_score
 from .models.unet import build_model
 from .optim import FlatParameterSpace, FusedAdam, make_plateau, plateau_step
-from .parallel.ddp import BucketedAllReduce, broadcast_parameters
+from .parallel.ddp import BucketedAllReduce, broadcast_parameters, sync_buffers
 from .parallel.dp import ReplicatedDataParallel
 from .parallel.pipeline import GPipeDist, GPipeLocal
 from .utils import LossCurves, MetricsLogger, load_model_state, save_model, set_seed
@@ -68,6 +68,13 @@ class Strategy:
 
     def lr_scale(self) -> float:
         return 1.0
+
+    def set_train(self, mode: bool):
+        """train/eval mode (BatchNorm variants: batch vs running statistics)."""
+        self.model.train(mode)
+
+    def before_eval(self):
+        pass
 
 
 def _loss_scale(cfg, batch):
@@ -145,6 +152,11 @@ class DDPStrategy(SingleDevice):
         dist.all_reduce(vals, op=dist.ReduceOp.SUM)
         return vals
 
+    def before_eval(self):
+        # torch DDP's broadcast_buffers: every rank evaluates with rank 0's BN running statistics
+        if any(True for _ in self.model.buffers()):
+            sync_buffers(self.model, src=0)
+
     def barrier(self):
         dist.barrier()
 
@@ -176,6 +188,10 @@ class DPStrategy(Strategy):
         self.device = self.dp.devices[0]
         self.model = self.dp.module
         self.optimizer = FusedAdam(self.dp.spaces, lr=cfg.lr, weight_decay=cfg.weight_decay)
+
+    def set_train(self, mode: bool):
+        for r in self.dp.replicas:
+            r.train(mode)
 
     def train_step(self, images, targets):
         self.optimizer.zero_grad()
@@ -563,13 +579,19 @@ class _SD:
 
 @torch.no_grad()
 def evaluate(strat: Strategy, val_loader):
-    """Reference ``evaluate.py:6-25`` (mean per-batch loss) + Dice; sharded and all-reduced."""
+    """Reference ``evaluate.py:6-25`` (``model.eval()``, mean per-batch loss, ``model.train()``) + Dice;
+    sharded and all-reduced."""
     tot = torch.zeros(3, dtype=torch.float64)
-    for images, targets in DeviceBatcher(val_loader, strat.device):
-        r = strat.eval_batch(images, targets)
-        if r is not None:
-            loss, dice = r
-            tot += torch.tensor([float(loss), float(dice), 1.0], dtype=torch.float64)
+    strat.before_eval()
+    strat.set_train(False)
+    try:
+        for images, targets in DeviceBatcher(val_loader, strat.device):
+            r = strat.eval_batch(images, targets)
+            if r is not None:
+                loss, dice = r
+                tot += torch.tensor([float(loss), float(dice), 1.0], dtype=torch.float64)
+    finally:
+        strat.set_train(True)
     if strat.name == "DDP":
         t = tot.to(strat.device) if strat.device.type == "cuda" else tot
         tot = strat.reduce_eval(t).cpu()

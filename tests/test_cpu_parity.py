@@ -192,3 +192,52 @@ def test_trainer_end_to_end_outputs(tmp_path):
                        "--resume"])
     out2 = train(cfg2)
     assert out2["step"] > out["step"]
+
+
+def test_variant_presets_layout():
+    """BN / bilinear variants (north-star DoubleConv = Conv2d+BN+ReLU, bilinear Up): torch key layout
+    (``conv_block.{0,1,3,4}``, ``deconvN.proj``), running-stat buffers, shapes."""
+    m = build_model("unet-bn-bilinear")
+    sd = m.state_dict()
+    assert "encoder.conv1.conv_block.1.running_mean" in sd and "encoder.conv1.conv_block.3.weight" in sd
+    assert tuple(sd["decoder.deconv1.proj.weight"].shape) == (256, 512, 1, 1)
+    assert len(list(m.buffers())) == 3 * 18
+    with torch.no_grad():
+        assert tuple(m(torch.rand(2, 3, 32, 48)).shape) == (2, 1, 32, 48)
+
+
+def test_local_pipeline_bn_variant_one_microbatch():
+    """BN running statistics live on their stage's device; with one microbatch the pipelined step
+    equals the plain model exactly (batch statistics over the same images)."""
+    from distributedpytorch_amd.parallel.pipeline import GPipeLocal
+    torch.manual_seed(4)
+    a, b = build_model("unet-tiny-bn"), build_model("unet-tiny-bn")
+    b.load_state_dict(a.state_dict())
+    x = torch.rand(4, 3, 32, 32)
+    t = (torch.rand(4, 1, 32, 32) > 0.5).float()
+    pipe = GPipeLocal(a, ["cpu"] * 2, 1, backend="torch", dtype="fp32", img_hw=(32, 32), mode="reference")
+    loss = pipe.forward_loss(x, t)
+    loss.backward()
+    ref = bce_dice_from_probs(b(x), t)
+    ref.backward()
+    assert torch.allclose(loss, ref, atol=1e-6)
+    for (n, p), (_, q) in zip(a.named_parameters(), b.named_parameters()):
+        assert torch.allclose(p.grad, q.grad, atol=1e-5), n
+    for (n, p), (_, q) in zip(a.named_buffers(), b.named_buffers()):
+        assert torch.allclose(p.float(), q.float(), atol=1e-6), n
+    a.eval()
+    b.eval()
+    with torch.no_grad():
+        assert torch.allclose(pipe.probs(x), b(x), atol=1e-5)
+
+
+def test_trainer_bn_variant_eval_mode(tmp_path):
+    """Evaluation runs in eval mode (running statistics) and training resumes in train mode."""
+    from distributedpytorch_amd.trainer import train
+    cfg = parse_args(["-e", "1", "-b", "4", "--synthetic", "--synthetic-len", "16", "--img-size", "32",
+                      "--model", "unet-tiny-bn", "--backend", "torch", "--dtype", "fp32", "--out-dir", str(tmp_path)])
+    out = train(cfg)
+    m = out["strategy"].model
+    assert m.training
+    sd = torch.load(tmp_path / "checkpoints" / "singleGPU.pth", weights_only=True)
+    assert int(sd["encoder.conv1.conv_block.1.num_batches_tracked"]) == out["step"]

@@ -155,3 +155,35 @@ def test_gpipe_gloo_matches_single_process(world, mb, mode):
         if rank == world - 1:
             assert abs(loss - lref) < 1e-5
     assert total_own == len(build_model("unet-tiny").state_dict())   # each parameter owned by one stage
+
+
+def _ddp_bn_worker(rank, world, port, q):
+    _init(rank, world, port)
+    from distributedpytorch_amd.config import TrainConfig
+    from distributedpytorch_amd.trainer import DDPStrategy
+    model = build_model("unet-tiny-bn")
+    st = DDPStrategy(TrainConfig(train_method="DDP", backend="torch", dtype="fp32", lr=1e-3), model, "cpu")
+    st.train_step(*_data(4, seed=20 + rank))          # rank-local batch statistics
+    rm = st.model.encoder.conv1.conv_block[1].running_mean.clone()
+    before = [torch.zeros_like(rm) for _ in range(world)]
+    dist.all_gather(before, rm)
+    st.before_eval()                                  # torch DDP broadcast_buffers semantics
+    rm = st.model.encoder.conv1.conv_block[1].running_mean.clone()
+    after = [torch.zeros_like(rm) for _ in range(world)]
+    dist.all_gather(after, rm)
+    q.put((rank, not torch.equal(before[0], before[1]), all(torch.equal(after[0], a) for a in after)))
+    dist.destroy_process_group()
+
+
+def test_ddp_bn_running_stats_follow_rank0():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ddp_bn_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    for rank, differed, same in res:
+        assert differed and same, (rank, differed, same)
