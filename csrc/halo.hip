@@ -779,7 +779,7 @@ __global__ __launch_bounds__(192) void wgrad_stream_kernel(WgradArgs a) {
   char* const Aimg = lds;
   char* const Ring = lds + 2 * IMGA;
 
-  const int nmt = a.M / BM, nnt = a.Nc / BN, tiles = nmt * nnt;
+  const int nmt = a.M / BM, nnt = (a.Nc + BN - 1) / BN, tiles = nmt * nnt;
   const int stripsW = a.Wg / BP, segsH = (a.Hg + RH - 1) / RH;
   const int bid = xcd_remap(blockIdx.x, tiles * a.splits);
   const int split = bid / tiles, tile = bid - split * tiles;     // split = (n, hs, ws)
@@ -809,7 +809,7 @@ __global__ __launch_bounds__(192) void wgrad_stream_kernel(WgradArgs a) {
   for (int j = 0; j < LB; ++j) {
     const int c = tid + j * NT, px = c / CPRB, cc = c - px * CPRB;
     const int iw = w0 + px - 1;
-    bok[j] = c < CHB && iw >= 0 && iw < a.WB;
+    bok[j] = c < CHB && iw >= 0 && iw < a.WB && n0 + cc * 8 < a.Nc;   // channel tail (first layer: 8 of 16)
     boff[j] = (unsigned)((iw * a.ldb + n0 + cc * 8) * 2);
     bsto[j] = c < CHB ? px * RBB + ((cc ^ swz_kk<RBB>(px)) << 4) : -1;
   }
@@ -911,6 +911,7 @@ __global__ __launch_bounds__(192) void wgrad_stream_kernel(WgradArgs a) {
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int nn = n0 + j * 16 + (lane & 15);
+        if (nn >= a.Nc) continue;
         const int mb = m0 + i * 16 + 4 * (lane >> 4);
         float* dst = a.slab + (((long)split * 9 + kh * 3 + kw) * a.M + mb) * a.Nc + nn;
 #pragma unroll
@@ -931,12 +932,13 @@ __global__ __launch_bounds__(192) void wgrad_stream_kernel(WgradArgs a) {
 
 template <int BM, int BN, int BP, int RH>
 static int launch_wgrad_stream(const WgradArgs& a, hipStream_t st) {
-  const int tiles = (a.M / BM) * (a.Nc / BN);
+  const int tiles = (a.M / BM) * ((a.Nc + BN - 1) / BN);
   hipLaunchKernelGGL((wgrad_stream_kernel<BM, BN, BP, RH>), dim3(tiles * a.splits), dim3(192), 0, st, a);
   return (int)hipGetLastError();
 }
 
 // splits must equal N * ceil(Hg/RH) * (Wg/BP); cfg picks (BM, BN): 1: 32x32  2: 64x32  3: 32x64
+// 4: 32x16 with Nc == 8 (the first layer's 8-padded RGB input; channels 8..15 read as zeros)
 DPA_API int dpa_wgrad_stream(const WgradArgs* args, int cfg, int bp, int rh, hipStream_t st) {
   const WgradArgs& a = *args;
   if ((a.lda & 7) || (a.ldb & 7) || a.s != 1 || a.pad != 1 || a.KW != 3 || a.HA != a.Hg || a.WA != a.Wg ||
@@ -951,5 +953,9 @@ DPA_API int dpa_wgrad_stream(const WgradArgs* args, int cfg, int bp, int rh, hip
   DPA_WS(2, 64, 32, 64, 32)
   DPA_WS(3, 32, 64, 64, 32)
 #undef DPA_WS
+  if (cfg == 4 && a.Nc == 8 && a.M % 32 == 0 && bp == 64) {
+    if (rh == 64) return launch_wgrad_stream<32, 16, 64, 64>(a, st);
+    if (rh == 32) return launch_wgrad_stream<32, 16, 64, 32>(a, st);
+  }
   return (int)hipErrorInvalidValue;
 }

@@ -201,7 +201,7 @@ def wgrad(A: torch.Tensor, B: torch.Tensor, *, kind: int, grid, M: int, Nc: int,
     ``path``: ``auto`` = row-streaming kernel when W % 64 == 0, else row-halo (W % 32 == 0), else the
     generic per-tap gather kernel; ``stream`` / ``halo`` / ``generic`` force one."""
     if path in ("auto", "stream") and kind == 0 and cfg == 0 and (USE_STREAM or path == "stream") \
-            and grid[2] % 64 == 0 and M % 32 == 0 and Nc % 32 == 0:
+            and grid[2] % 64 == 0 and M % 32 == 0 and (Nc % 32 == 0 or Nc == 8):
         return _wgrad_stream(A, B, grid=grid, M=M, Nc=Nc, gw=gw, gb=gb, Nreal=Nreal)
     if path == "stream":
         raise RuntimeError("wgrad stream path not eligible for this shape")
@@ -258,9 +258,12 @@ def _wgrad_stream(A, B, *, grid, M, Nc, gw, gb, Nreal):
     N, Hg, Wg = grid
     assert (HA, WA) == (Hg, Wg) == (HB, WB) and NA == NB == N and CA >= M and CB >= Nc
     assert gw.dtype == torch.float32 and gw.is_contiguous() and gw.numel() == M * Nreal * 9
-    hcfg = 2 if M % 64 == 0 else (3 if Nc % 64 == 0 else 1)
-    bm, bn = {1: (32, 32), 2: (64, 32), 3: (32, 64)}[hcfg]
-    tiles = (M // bm) * (Nc // bn)
+    if Nc == 8:            # first layer (RGB padded to 8 channels): 32x16 tile, half the columns zero
+        hcfg = 4
+    else:
+        hcfg = 2 if M % 64 == 0 else (3 if Nc % 64 == 0 else 1)
+    bm, bn = {1: (32, 32), 2: (64, 32), 3: (32, 64), 4: (32, 16)}[hcfg]
+    tiles = (M // bm) * (-(-Nc // bn))
     L = _lib.lib()
     st = _stream(A)
     for n0, n1 in _image_chunks(N, max(HA * WA * lda, HB * WB * ldb) * 2):

@@ -194,7 +194,9 @@ def test_deconv_dgrad_from_concat(hip_lib, N, h, w, Cin, Cout):
     (1, 4, 32, 128, 64, None, "halo"), (2, 4, 32, 3, 32, 8, "auto"),
     # row-streaming wgrad (W % 64 == 0), odd row counts -> partial row segments
     (2, 5, 64, 32, 32, None, "stream"), (1, 37, 64, 64, 32, None, "stream"), (2, 3, 128, 32, 64, None, "stream"),
-    (1, 70, 64, 128, 64, None, "stream"), (1, 4, 64, 64, 128, None, "generic")])
+    (1, 70, 64, 128, 64, None, "stream"), (1, 4, 64, 64, 128, None, "generic"),
+    # first layer through the streaming wgrad (8 padded input channels in a 16-wide tile)
+    (2, 5, 128, 3, 32, 8, "stream"), (1, 66, 64, 3, 32, 8, "stream")])
 def test_conv3x3_wgrad(hip_lib, N, H, W, Cin, Cout, cin_pad, path):
     from distributedpytorch_amd.ops import kernels as K
     torch.manual_seed(4)
