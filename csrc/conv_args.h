@@ -67,7 +67,7 @@ template <int RB>
 __device__ __forceinline__ int swz_kk(int r) {
   if constexpr (RB == 64) return ((r >> 3) & 1) * 2;
   else if constexpr (RB == 128) return (((r >> 1) & 1) * 2) ^ (((r >> 3) & 1) * 4);
-  else if constexpr (RB == 256) return ((r & 1) * 2) ^ (((r >> 1) & 1) * 4) ^ (((r >> 3) & 1) * 8);
+  else if constexpr (RB == 256 || RB == 512) return ((r & 1) * 2) ^ (((r >> 1) & 1) * 4) ^ (((r >> 3) & 1) * 8);
   else return 0;
 }
 

@@ -1,0 +1,230 @@
+// Fused backward of the full-resolution transposed convolutions (ConvTranspose2d k2 s2, reference
+// model/unet_parts.py:51-54; SURVEY §2.5 K6 dgrad + wgrad) for the 64->32 and 128->64 layers.
+//
+// Both halves of the backward read the same two tensors:
+//   dgrad  dx[p][ci] = (x[p][ci] > 0) * sum_{ij,co} g[2p+ij][co] * W[ci][co][ij]      (GEMM K = 4*Cout)
+//   wgrad  dW[ci][co][ij] += sum_p x[p][ci] * g[2p+ij][co],   db[co] += sum_{p,ij} g  (GEMM K = pixels)
+// so one pass streams each tile of 64 low-resolution pixels -- its 4*Cout up-sampled gradient values
+// per pixel and its Cin input channels -- into LDS once and runs both products from there: the
+// separate kernels read g twice and x twice (plus the ReLU mask re-read), 1.5-2.2x the bytes of this
+// memory-bound pair.  The dgrad weights (Cin x 4*Cout bf16) live in VGPRs for the whole kernel (each
+// wave owns 16 input channels), the weight-gradient tile (Cin x 4*Cout fp32) accumulates in
+// registers across all of a block's pixel tiles and is written once as this block's split slab,
+// reduced in a fixed order by wgrad_reduce (deterministic).  Next-tile global loads are issued
+// before the current tile's MFMAs (register prefetch).
+//
+// LDS images: [64 pixels][channels] bf16 with the kk swizzle, read as ds_read_b128 k-fragments
+// (dgrad B operand: pixel rows, k contiguous) and as ds_read_b64_tr_b16 pixel-fragments (wgrad).
+#include "conv_args.h"
+
+template <int CIN, int COUT>
+__global__ __launch_bounds__(512) void deconv_bwd_kernel(const bf16_t* __restrict__ g, int ldg, const bf16_t* __restrict__ x,
+                                                        int ldx, const bf16_t* __restrict__ wd, bf16_t* __restrict__ dx,
+                                                        int lddx, float* __restrict__ slab, float* __restrict__ bslab,
+                                                        int N, int h, int w, int tiles_per_block, unsigned gbytes,
+                                                        unsigned xbytes) {
+  constexpr int P = 64;                       // low-resolution pixels per tile
+  constexpr int K4 = 4 * COUT;                // dgrad K / wgrad N
+  constexpr int RBX = CIN * 2, RBG = K4 * 2;  // LDS row bytes
+  constexpr int CPX = CIN / 8, CPG = K4 / 8;  // 16-B chunks per pixel
+  constexpr int CG = P * CPG, CT = CG + P * CPX;
+  constexpr int L = (CT + 511) / 512;
+  // dgrad: 8 waves = NCG channel groups of 16 x NPG pixel groups
+  constexpr int NCG = CIN / 16, NPG = 8 / NCG, TPX = P / NPG / 16, KS = K4 / 32;
+  // wgrad: 2 x 4 waves over the CIN x K4 tile
+  constexpr int WM = CIN / 2, WN = K4 / 4, TM = WM / 16, TN = WN / 16;
+  constexpr int NRG = 512 / K4;               // bias-gradient row groups
+  static_assert(NCG * NPG == 8 && TPX >= 1 && NRG >= 1 && 512 % K4 == 0, "tiling");
+  __shared__ __attribute__((aligned(16))) char lds[P * (RBX + RBG)];
+  char* const ximg = lds;
+  char* const gimg = lds + P * RBX;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int M = N * h * w;
+  const int ntiles = (M + P - 1) / P;
+  const int split = blockIdx.x;
+  const int t0 = split * tiles_per_block;
+  const int t1 = min(ntiles, t0 + tiles_per_block);
+  const __amdgpu_buffer_rsrc_t gr = __builtin_amdgcn_make_buffer_rsrc((void*)g, 0, (int)gbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)x, 0, (int)xbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t dr = __builtin_amdgcn_make_buffer_rsrc((void*)dx, 0, 0x7fffffff, 0x00020000);
+
+  // ---- per-thread staging plan (fixed across tiles)
+  int cpix[L], cofs[L], lsto[L];
+  bool isg[L];
+#pragma unroll
+  for (int j = 0; j < L; ++j) {
+    const int c = tid + j * 512;
+    isg[j] = c < CG;
+    if (c < CG) {
+      const int p = c / CPG, kc = c - p * CPG;
+      const int ij = kc / (COUT / 8), cw = kc - ij * (COUT / 8);
+      cpix[j] = p;
+      cofs[j] = ij * 16 + cw;                 // (i, j, channel chunk) packed: ij = cofs >> 4
+      lsto[j] = p * RBG + ((kc ^ swz_kk<RBG>(p)) << 4);
+    } else if (c < CT) {
+      const int c2 = c - CG, p = c2 / CPX, xc = c2 - p * CPX;
+      cpix[j] = p;
+      cofs[j] = xc;
+      lsto[j] = P * RBG + p * RBX + ((xc ^ swz_kk<RBX>(p)) << 4);   // relative to gimg: fixed below
+    } else {
+      cpix[j] = 0;
+      cofs[j] = 0;
+      lsto[j] = -1;
+    }
+  }
+  u32x4_t reg[L];
+  auto gload = [&](int t) {
+    const int m0 = t * P;
+#pragma unroll
+    for (int j = 0; j < L; ++j) {
+      const int m = m0 + cpix[j];
+      const bool ok = lsto[j] >= 0 && m < M;
+      const int mm = ok ? m : 0;
+      if (isg[j]) {
+        const int nh = mm / w, ww = mm - nh * w;
+        const int ij = cofs[j] >> 4, cw = cofs[j] & 15;
+        const unsigned off = (unsigned)((((2 * nh + (ij >> 1)) * (2 * w) + 2 * ww + (ij & 1)) * ldg + cw * 8) * 2);
+        reg[j] = __builtin_amdgcn_raw_buffer_load_b128(gr, ok ? off : 0x80000000u, 0, 0);
+      } else {
+        const unsigned off = (unsigned)((mm * ldx + cofs[j] * 8) * 2);
+        reg[j] = __builtin_amdgcn_raw_buffer_load_b128(xr, ok ? off : 0x80000000u, 0, 0);
+      }
+    }
+  };
+  auto lstore = [&]() {
+#pragma unroll
+    for (int j = 0; j < L; ++j) {
+      if (lsto[j] < 0) continue;
+      char* dst = isg[j] ? gimg + lsto[j] : ximg + (lsto[j] - P * RBG);
+      *reinterpret_cast<u32x4_t*>(dst) = reg[j];
+    }
+  };
+
+  // ---- dgrad weights -> VGPRs: wave owns channels ci0..ci0+15, all K4
+  const int cg = wid % NCG, pg = wid / NCG;
+  const int ci0 = cg * 16;
+  bf16x8_t wf[KS];
+  {
+    const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)wd, 0, 0x7fffffff, 0x00020000);
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const unsigned off = (unsigned)(((ci0 + (lane & 15)) * K4 + ks * 32 + (lane >> 4) * 8) * 2);
+      wf[ks] = __builtin_bit_cast(bf16x8_t, __builtin_amdgcn_raw_buffer_load_b128(wr, off, 0, 0));
+    }
+  }
+
+  const int wm = wid >> 2, wn = wid & 3;
+  f32x4_t accw[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) accw[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  const int bcol = tid % K4, brg = tid / K4;
+  float bsum = 0.f;
+
+  if (t0 < t1) {
+    gload(t0);
+    lstore();
+  }
+  __syncthreads();
+#pragma unroll 1
+  for (int t = t0; t < t1; ++t) {
+    const bool more = t + 1 < t1;
+    if (more) gload(t + 1);
+    __builtin_amdgcn_sched_barrier(0);
+    const int m0 = t * P;
+    // ---- dgrad: dx[px][ci0..+15] for this wave's pixel group
+#pragma unroll
+    for (int tp = 0; tp < TPX; ++tp) {
+      const int prow = pg * (P / NPG) + tp * 16 + (lane & 15);
+      f32x4_t acc = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const int chunk = ks * 4 + (lane >> 4);
+        const bf16x8_t bfr = *reinterpret_cast<const bf16x8_t*>(gimg + prow * RBG + ((chunk ^ swz_kk<RBG>(prow)) << 4));
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[ks], bfr, acc, 0, 0, 0);
+      }
+      const int ci = ci0 + 4 * (lane >> 4);
+      const u32x2_t mk = *reinterpret_cast<const u32x2_t*>(ximg + prow * RBX + (((ci >> 3) ^ swz_kk<RBX>(prow)) << 4) +
+                                                          (ci & 7) * 2);
+      const float v0 = lo_bf(mk.x) > 0.f ? acc[0] : 0.f;
+      const float v1 = hi_bf(mk.x) > 0.f ? acc[1] : 0.f;
+      const float v2 = lo_bf(mk.y) > 0.f ? acc[2] : 0.f;
+      const float v3 = hi_bf(mk.y) > 0.f ? acc[3] : 0.f;
+      const int m = m0 + prow;
+      if (m < M)
+        __builtin_amdgcn_raw_buffer_store_b64(u32x2_t{pack_bf2(v0, v1), pack_bf2(v2, v3)}, dr,
+                                              (unsigned)((m * lddx + ci) * 2), 0, 0);
+    }
+    // ---- wgrad: accw[ci][k] += sum_px x[px][ci] * g[px][k]
+#pragma unroll
+    for (int ks2 = 0; ks2 < P / 32; ++ks2) {
+      bf16x8_t af[TM];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[i] = tr_frag<RBX>(ximg, wm * WM + i * 16, lane, ks2 * 32);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const bf16x8_t bfr = tr_frag<RBG>(gimg, wn * WN + j * 16, lane, ks2 * 32);
+#pragma unroll
+        for (int i = 0; i < TM; ++i) accw[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr, accw[i][j], 0, 0, 0);
+      }
+    }
+    // ---- bias gradient partials (column sums of the staged gradient)
+#pragma unroll 4
+    for (int r = brg; r < P; r += NRG) {
+      const bf16_t v = *reinterpret_cast<const bf16_t*>(gimg + r * RBG + (((bcol >> 3) ^ swz_kk<RBG>(r)) << 4) + (bcol & 7) * 2);
+      bsum += bf2f(v);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    __syncthreads();
+    if (more) {
+      lstore();
+      __syncthreads();
+    }
+  }
+
+  // ---- epilogue: this split's slab [4][COUT][CIN] (wgrad_reduce mode 1 layout) + bias partial
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int k = wn * WN + j * 16 + (lane & 15);
+      const int ij = k / COUT, co = k - ij * COUT;
+      const int ci = wm * WM + i * 16 + 4 * (lane >> 4);
+      float* dst = slab + (((long)split * 4 + ij) * COUT + co) * CIN + ci;
+      *reinterpret_cast<f32x4_t*>(dst) = accw[i][j];
+    }
+  if (bslab) {
+    float* red = reinterpret_cast<float*>(lds);   // all LDS reads of the last tile are behind the barrier
+    red[brg * K4 + bcol] = bsum;
+    __syncthreads();
+    if (tid < COUT) {
+      float s = 0.f;
+#pragma unroll
+      for (int q = 0; q < NRG; ++q)
+#pragma unroll
+        for (int ij = 0; ij < 4; ++ij) s += red[q * K4 + ij * COUT + tid];
+      bslab[(long)split * COUT + tid] = s;
+    }
+  }
+}
+
+DPA_API int dpa_deconv_bwd(const bf16_t* g, int ldg, const bf16_t* x, int ldx, const bf16_t* wd, bf16_t* dx, int lddx,
+                           float* slab, float* bslab, int N, int h, int w, int Cin, int Cout, int splits,
+                           unsigned gbytes, unsigned xbytes, hipStream_t st) {
+  if ((ldg & 7) || (ldx & 7) || (lddx & 3) || splits < 1) return (int)hipErrorInvalidValue;
+  const long M = (long)N * h * w;
+  const int ntiles = (int)((M + 63) / 64);
+  const int tpb = (ntiles + splits - 1) / splits;
+  if ((long)(splits - 1) * tpb >= ntiles) return (int)hipErrorInvalidValue;   // every split owns >= 1 tile
+  if (Cin == 64 && Cout == 32)
+    hipLaunchKernelGGL((deconv_bwd_kernel<64, 32>), dim3(splits), dim3(512), 0, st, g, ldg, x, ldx, wd, dx, lddx, slab, bslab,
+                       N, h, w, tpb, gbytes, xbytes);
+  else if (Cin == 128 && Cout == 64)
+    hipLaunchKernelGGL((deconv_bwd_kernel<128, 64>), dim3(splits), dim3(512), 0, st, g, ldg, x, ldx, wd, dx, lddx, slab,
+                       bslab, N, h, w, tpb, gbytes, xbytes);
+  else
+    return (int)hipErrorInvalidValue;
+  return (int)hipGetLastError();
+}

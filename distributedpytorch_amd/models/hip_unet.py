@@ -250,6 +250,15 @@ class HipBlocks:
         K.wgrad(gup, x, kind=1, grid=(N, h, w), M=d.Cout, Nc=d.Cin, s=2, pad=0, KW=2, gw=_grad(d.mod.weight).view(-1),
                 gb=_grad(d.mod.bias), Nreal=d.Cin)
 
+    def deconv_bwd(self, d, gup: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
+        """dgrad + weight gradient of the up-path layer; the full-resolution transposed convs run
+        both in one pass over (gup, x) (csrc/deconv.hip)."""
+        if isinstance(d, _Deconv) and K.USE_FUSED_DECONV and (d.Cin, d.Cout) in K.DECONV_BWD_SHAPES:
+            return K.deconv_bwd_fused(gup, x, self.wd(d), _grad(d.mod.weight).view(-1), _grad(d.mod.bias))
+        dx = self.deconv_dgrad(d, gup, x)
+        self.deconv_wgrad(d, gup, x)
+        return dx
+
     def ready(self, mods):
         by_space = {}
         for m in mods:
@@ -446,8 +455,7 @@ class _DecFn(torch.autograd.Function):
         B.ready([c1.mod, c1.bn])
         if isinstance(d, _Up):
             gup = K.up2_bwd(gup)          # to the projection's (low) resolution
-        dx = B.deconv_dgrad(d, gup, x)
-        B.deconv_wgrad(d, gup, x)
+        dx = B.deconv_bwd(d, gup, x)
         B.ready([d.mod])
         ctx.st = None
         return None, _o(dx), _o(dskip), None, None

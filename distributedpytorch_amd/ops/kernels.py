@@ -369,6 +369,40 @@ def head_bwd(y: torch.Tensor, w: torch.Tensor, b: torch.Tensor, t: torch.Tensor,
     return gy
 
 
+# ------------------------------------------------------------------------------------- fused deconv bwd
+USE_FUSED_DECONV = os.environ.get("DPA_NO_FUSED_DECONV", "0") != "1"
+DECONV_BWD_SHAPES = ((64, 32), (128, 64))
+
+
+def deconv_bwd_fused(gup: torch.Tensor, x: torch.Tensor, wd: torch.Tensor, gw: torch.Tensor,
+                     gb: Optional[torch.Tensor]) -> torch.Tensor:
+    """ConvTranspose2d(k2, s2) dgrad (ReLU-masked by x) AND weight/bias gradient in one pass over
+    (gup, x) (csrc/deconv.hip); gw [Cin*Cout*4] / gb [Cout] accumulate.  Returns dx [N,h,w,Cin]."""
+    N, H2, W2, Cout, ldg = _nhwc(gup, "deconv_bwd.g")
+    Nx, h, w, Cin, ldx = _nhwc(x, "deconv_bwd.x")
+    assert Nx == N and (H2, W2) == (2 * h, 2 * w) and (Cin, Cout) in DECONV_BWD_SHAPES
+    assert wd.dtype == torch.bfloat16 and wd.numel() >= Cin * 4 * Cout
+    assert gw.dtype == torch.float32 and gw.is_contiguous() and gw.numel() == Cin * Cout * 4
+    dx = torch.empty(N, h, w, Cin, dtype=torch.bfloat16, device=x.device)
+    L = _lib.lib()
+    st = _stream(x)
+    for n0, n1 in _image_chunks(N, max(H2 * W2 * ldg, h * w * ldx) * 2):
+        nb = n1 - n0
+        ntiles = -(-nb * h * w // 64)
+        splits = min(ntiles, 512 if Cin == 64 else 256)
+        tpb = -(-ntiles // splits)
+        splits = -(-ntiles // tpb)
+        slab = torch.empty(splits * 4 * Cout * Cin + splits * Cout, dtype=torch.float32, device=x.device)
+        bslab = slab[splits * 4 * Cout * Cin:] if gb is not None else None
+        _check(L.dpa_deconv_bwd(_p(gup[n0:n1]), c_int(ldg), _p(x[n0:n1]), c_int(ldx), _p(wd), _p(dx[n0:n1]), c_int(Cin),
+                                _p(slab), _p(bslab), c_int(nb), c_int(h), c_int(w), c_int(Cin), c_int(Cout),
+                                c_int(splits), ctypes.c_uint(_extent_bytes(nb, H2, W2, Cout, ldg)),
+                                ctypes.c_uint(_extent_bytes(nb, h, w, Cin, ldx)), st), "deconv_bwd")
+        _check(L.dpa_wgrad_reduce(_p(slab), _p(bslab), _p(gw), _p(gb), c_int(splits), c_int(4), c_int(Cout), c_int(Cin),
+                                  c_int(Cin), c_int(1), st), "wgrad_reduce")
+    return dx
+
+
 # ------------------------------------------------------------------------------------- BN / bilinear
 def _flat_f32(t: torch.Tensor, n: int, name: str):
     assert t.dtype == torch.float32 and t.is_contiguous() and t.numel() == n and t.is_cuda, f"{name}: need fp32[{n}]"

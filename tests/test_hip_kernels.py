@@ -237,6 +237,35 @@ def test_deconv_wgrad(hip_lib, N, h, w, Cin, Cout):
     assert _rel(gb.cpu(), br.grad) < 1e-2
 
 
+@pytest.mark.parametrize("N,h,w,Cin,Cout,strided", [(2, 5, 7, 64, 32, False), (1, 8, 8, 128, 64, False),
+                                                     (3, 16, 20, 64, 32, True), (2, 33, 31, 128, 64, False)])
+def test_deconv_bwd_fused(hip_lib, N, h, w, Cin, Cout, strided):
+    """One-pass transposed-conv backward (csrc/deconv.hip): ReLU-masked dgrad + weight/bias grads."""
+    from distributedpytorch_amd.ops import kernels as K
+    torch.manual_seed(6)
+    x = _bf(torch.randn(N, Cin, h, w)).relu()
+    gup = _bf(torch.randn(N, Cout, 2 * h, 2 * w))
+    wt = torch.randn(Cin, Cout, 2, 2) / Cin ** 0.5
+    xr = x.clone().requires_grad_(True)
+    wr = _bf(wt).clone().requires_grad_(True)
+    br = torch.zeros(Cout, requires_grad=True)
+    F.conv_transpose2d(xr, wr, br, stride=2).backward(gup)
+    wd, _, _ = _pack_one(3, wt)
+    if strided:   # gradient read from a concat half
+        buf = torch.zeros(N, 2 * h, 2 * w, 2 * Cout, dtype=torch.bfloat16, device="cuda")
+        buf[..., Cout:] = _nhwc(gup)
+        g_in = buf[..., Cout:]
+    else:
+        g_in = _nhwc(gup)
+    gw = torch.full((Cin, Cout, 2, 2), 0.5, device="cuda")
+    gb = torch.full((Cout,), 0.5, device="cuda")
+    dx = K.deconv_bwd_fused(g_in, _nhwc(x), wd, gw.view(-1), gb)
+    torch.cuda.synchronize()
+    assert _rel(_nchw(dx), xr.grad * (x > 0)) < 1e-2
+    assert _rel(gw.cpu() - 0.5, wr.grad) < 1e-2
+    assert _rel(gb.cpu() - 0.5, br.grad) < 1e-2
+
+
 @pytest.mark.parametrize("N,H,W,C", [(2, 16, 16, 32), (1, 9, 11, 64)])
 def test_maxpool_and_backward(hip_lib, N, H, W, C):
     from distributedpytorch_amd.ops import kernels as K
