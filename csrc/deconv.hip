@@ -228,3 +228,144 @@ DPA_API int dpa_deconv_bwd(const bf16_t* g, int ldg, const bf16_t* x, int ldx, c
     return (int)hipErrorInvalidValue;
   return (int)hipGetLastError();
 }
+
+// ------------------------------------------------------------------------------------ forward
+// y[2p+ij][co] = b[co] + sum_ci x[p][ci] * W[ci][co][ij], written into the decoder's concat buffer
+// (second half, row pitch ldy = 2*Cout).  Same tiling as the backward: 64 low-resolution pixels per
+// tile through LDS (register prefetch of the next tile), the packed forward weights
+// ([(2i+j)*Cout + co][ci], 4*Cout x Cin) in VGPRs (wave w owns rows w*4*Cout/8 ..), and the output
+// tile staged in LDS so the global stores are whole 16-B chunks ordered along each output row
+// (the MFMA layout alone would give 8-B pieces scattered over four sub-pixel rows).
+template <int CIN, int COUT>
+__global__ __launch_bounds__(512) void deconv_fwd_kernel(const bf16_t* __restrict__ x, int ldx, const bf16_t* __restrict__ wf,
+                                                        const float* __restrict__ bias, bf16_t* __restrict__ y, int ldy,
+                                                        int N, int h, int w, int tiles_per_block, unsigned xbytes) {
+  constexpr int P = 64;
+  constexpr int K4 = 4 * COUT;                 // GEMM N (output sub-pixel x channel)
+  constexpr int RBX = CIN * 2, RBO = K4 * 2;
+  constexpr int CPX = CIN / 8;
+  constexpr int CX = P * CPX;
+  constexpr int LX = (CX + 511) / 512;
+  constexpr int NT_W = K4 / 8 / 16;            // 16-row n-tiles per wave
+  constexpr int KS = CIN / 32;
+  constexpr int OCH = COUT / 8;                // 16-B chunks per output pixel
+  constexpr int CO = P * 4 * OCH;              // output chunks per tile
+  constexpr int LO = (CO + 511) / 512;
+  static_assert(NT_W >= 1 && CX % 512 == 0 && CO % 512 == 0, "tiling");
+  __shared__ __attribute__((aligned(16))) char lds[P * (RBX + RBO)];
+  char* const ximg = lds;
+  char* const oimg = lds + P * RBX;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int M = N * h * w;
+  const int ntiles = (M + P - 1) / P;
+  const int t0 = blockIdx.x * tiles_per_block;
+  const int t1 = min(ntiles, t0 + tiles_per_block);
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)x, 0, (int)xbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc((void*)y, 0, 0x7fffffff, 0x00020000);
+
+  // weights of this wave's n rows, bias of its output channels
+  bf16x8_t wfr[NT_W][KS];
+  float bv[NT_W][4];
+  {
+    const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)wf, 0, 0x7fffffff, 0x00020000);
+#pragma unroll
+    for (int nt = 0; nt < NT_W; ++nt) {
+      const int nrow = (wid * NT_W + nt) * 16 + (lane & 15);
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks)
+        wfr[nt][ks] = __builtin_bit_cast(
+            bf16x8_t, __builtin_amdgcn_raw_buffer_load_b128(wr, (unsigned)((nrow * CIN + ks * 32 + (lane >> 4) * 8) * 2), 0, 0));
+      const int nb = (wid * NT_W + nt) * 16 + 4 * (lane >> 4);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bv[nt][r] = bias ? bias[(nb + r) % COUT] : 0.f;
+    }
+  }
+  u32x4_t reg[LX];
+  auto gload = [&](int t) {
+#pragma unroll
+    for (int j = 0; j < LX; ++j) {
+      const int c = tid + j * 512, p = c / CPX, xc = c - p * CPX;
+      const int m = t * P + p;
+      reg[j] = __builtin_amdgcn_raw_buffer_load_b128(xr, m < M ? (unsigned)((m * ldx + xc * 8) * 2) : 0x80000000u, 0, 0);
+    }
+  };
+  auto lstore = [&]() {
+#pragma unroll
+    for (int j = 0; j < LX; ++j) {
+      const int c = tid + j * 512, p = c / CPX, xc = c - p * CPX;
+      *reinterpret_cast<u32x4_t*>(ximg + p * RBX + ((xc ^ swz_kk<RBX>(p)) << 4)) = reg[j];
+    }
+  };
+
+  if (t0 < t1) {
+    gload(t0);
+    lstore();
+  }
+  __syncthreads();
+#pragma unroll 1
+  for (int t = t0; t < t1; ++t) {
+    const bool more = t + 1 < t1;
+    if (more) gload(t + 1);
+    __builtin_amdgcn_sched_barrier(0);
+    // ---- GEMM: out[px][n] for this wave's n-tiles, all 64 pixels
+#pragma unroll
+    for (int tp = 0; tp < P / 16; ++tp) {
+      const int prow = tp * 16 + (lane & 15);
+      bf16x8_t bfr[KS];
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const int chunk = ks * 4 + (lane >> 4);
+        bfr[ks] = *reinterpret_cast<const bf16x8_t*>(ximg + prow * RBX + ((chunk ^ swz_kk<RBX>(prow)) << 4));
+      }
+#pragma unroll
+      for (int nt = 0; nt < NT_W; ++nt) {
+        f32x4_t acc = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfr[nt][ks], bfr[ks], acc, 0, 0, 0);
+        const int n = (wid * NT_W + nt) * 16 + 4 * (lane >> 4);
+        const u32x2_t v = u32x2_t{pack_bf2(acc[0] + bv[nt][0], acc[1] + bv[nt][1]), pack_bf2(acc[2] + bv[nt][2], acc[3] + bv[nt][3])};
+        *reinterpret_cast<u32x2_t*>(oimg + prow * RBO + (((n >> 3) ^ swz_kk<RBO>(prow)) << 4) + (n & 7) * 2) = v;
+      }
+    }
+    __syncthreads();
+    // ---- whole-chunk stores, ordered (sub-row i, pixel, j, chunk) so consecutive threads walk an output row
+    const int m0 = t * P;
+#pragma unroll
+    for (int j = 0; j < LO; ++j) {
+      const int c = tid + j * 512;
+      const int i = c / (P * 2 * OCH);
+      const int rem = c - i * (P * 2 * OCH);
+      const int p = rem / (2 * OCH), rem2 = rem - p * (2 * OCH);
+      const int jj = rem2 / OCH, cw = rem2 - jj * OCH;
+      const int m = m0 + p;
+      if (m < M) {
+        const int ij = 2 * i + jj;
+        const int kc = ij * OCH + cw;
+        const u32x4_t v = *reinterpret_cast<const u32x4_t*>(oimg + p * RBO + ((kc ^ swz_kk<RBO>(p)) << 4));
+        const int nh = m / w, ww = m - nh * w;
+        const unsigned off = (unsigned)((((2 * nh + i) * (2 * w) + 2 * ww + jj) * ldy + cw * 8) * 2);
+        __builtin_amdgcn_raw_buffer_store_b128(v, yr, off, 0, 0);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if (more) lstore();
+    __syncthreads();
+  }
+}
+
+DPA_API int dpa_deconv_fwd(const bf16_t* x, int ldx, const bf16_t* wf, const float* bias, bf16_t* y, int ldy, int N, int h,
+                           int w, int Cin, int Cout, int blocks, unsigned xbytes, hipStream_t st) {
+  if ((ldx & 7) || (ldy & 7) || blocks < 1) return (int)hipErrorInvalidValue;
+  const long M = (long)N * h * w;
+  const int ntiles = (int)((M + 63) / 64);
+  const int tpb = (ntiles + blocks - 1) / blocks;
+  const int grid = (ntiles + tpb - 1) / tpb;
+  if (Cin == 64 && Cout == 32)
+    hipLaunchKernelGGL((deconv_fwd_kernel<64, 32>), dim3(grid), dim3(512), 0, st, x, ldx, wf, bias, y, ldy, N, h, w, tpb, xbytes);
+  else if (Cin == 128 && Cout == 64)
+    hipLaunchKernelGGL((deconv_fwd_kernel<128, 64>), dim3(grid), dim3(512), 0, st, x, ldx, wf, bias, y, ldy, N, h, w, tpb, xbytes);
+  else
+    return (int)hipErrorInvalidValue;
+  return (int)hipGetLastError();
+}

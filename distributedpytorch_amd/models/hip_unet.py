@@ -227,6 +227,9 @@ class HipBlocks:
                     out_grid=(N, h, w), bias=d.mod.bias)
             K.up2_fwd(low, out)
             return
+        if K.USE_FUSED_DECONV and (d.Cin, d.Cout) in K.DECONV_BWD_SHAPES:
+            K.deconv_fwd_fused(x, self.wf(d), d.mod.bias, out)
+            return
         K.igemm(x, self.wf(d), out, Ngemm=4 * d.Cout, Kpad=d.Kf, KH=1, KW=1, stride=1, pad=0, Cs=d.Cin,
                 out_grid=(N, h, w), bias=d.mod.bias, mode=1, Cout=d.Cout)
 

@@ -403,6 +403,25 @@ def deconv_bwd_fused(gup: torch.Tensor, x: torch.Tensor, wd: torch.Tensor, gw: t
     return dx
 
 
+def deconv_fwd_fused(x: torch.Tensor, wf: torch.Tensor, bias: Optional[torch.Tensor], y: torch.Tensor):
+    """ConvTranspose2d(k2, s2) forward of the full-resolution up-convs (csrc/deconv.hip) into ``y``
+    (the decoder concat buffer's second half), whole-chunk stores along each output row."""
+    N, h, w, Cin, ldx = _nhwc(x, "deconv_fwd.x")
+    Ny, H2, W2, Cy, ldy = _nhwc(y, "deconv_fwd.y")
+    Cout = Cy
+    assert Ny == N and (H2, W2) == (2 * h, 2 * w) and (Cin, Cout) in DECONV_BWD_SHAPES
+    assert wf.dtype == torch.bfloat16 and wf.numel() >= 4 * Cout * Cin
+    if bias is not None:
+        assert bias.dtype == torch.float32 and bias.numel() == Cout
+    L = _lib.lib()
+    st = _stream(x)
+    for n0, n1 in _image_chunks(N, max(H2 * W2 * ldy, h * w * ldx) * 2):
+        nb = n1 - n0
+        _check(L.dpa_deconv_fwd(_p(x[n0:n1]), c_int(ldx), _p(wf), _p(bias), _p(y[n0:n1]), c_int(ldy), c_int(nb), c_int(h),
+                                c_int(w), c_int(Cin), c_int(Cout), c_int(1024 if Cin == 64 else 512),
+                                ctypes.c_uint(_extent_bytes(nb, h, w, Cin, ldx)), st), "deconv_fwd")
+
+
 # ------------------------------------------------------------------------------------- BN / bilinear
 def _flat_f32(t: torch.Tensor, n: int, name: str):
     assert t.dtype == torch.float32 and t.is_contiguous() and t.numel() == n and t.is_cuda, f"{name}: need fp32[{n}]"

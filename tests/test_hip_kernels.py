@@ -237,6 +237,23 @@ def test_deconv_wgrad(hip_lib, N, h, w, Cin, Cout):
     assert _rel(gb.cpu(), br.grad) < 1e-2
 
 
+@pytest.mark.parametrize("N,h,w,Cin,Cout", [(2, 5, 7, 64, 32), (1, 8, 8, 128, 64), (2, 33, 31, 128, 64)])
+def test_deconv_fwd_fused(hip_lib, N, h, w, Cin, Cout):
+    """Full-resolution transposed-conv forward (csrc/deconv.hip) into the concat buffer's second half."""
+    from distributedpytorch_amd.ops import kernels as K
+    torch.manual_seed(7)
+    x = _bf(torch.randn(N, Cin, h, w))
+    wt = torch.randn(Cin, Cout, 2, 2) / Cin ** 0.5
+    b = torch.randn(Cout)
+    ref = F.conv_transpose2d(x, _bf(wt), b, stride=2)
+    wf, _, _ = _pack_one(2, wt)
+    cat = torch.zeros(N, 2 * h, 2 * w, 2 * Cout, dtype=torch.bfloat16, device="cuda")
+    K.deconv_fwd_fused(_nhwc(x), wf, b.cuda(), cat[..., Cout:])
+    torch.cuda.synchronize()
+    assert _rel(_nchw(cat[..., Cout:]), ref) < 1e-2
+    assert cat[..., :Cout].abs().max().item() == 0
+
+
 @pytest.mark.parametrize("N,h,w,Cin,Cout,strided", [(2, 5, 7, 64, 32, False), (1, 8, 8, 128, 64, False),
                                                      (3, 16, 20, 64, 32, True), (2, 33, 31, 128, 64, False)])
 def test_deconv_bwd_fused(hip_lib, N, h, w, Cin, Cout, strided):
