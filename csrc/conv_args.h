@@ -22,6 +22,9 @@ struct IgemmArgs {
                         // dense [N][Ho/2][Wo/2][Ngemm] bytes: the max-pool backward needs nothing else
   bf16_t* y2;           // optional split output (mode 0, no accumulate): channels >= split go to
   int ldy2, split;      // y2[m][co - split] -- the two halves of a concat gradient as dense tensors
+  // optional fused segmentation head (streaming kernel, last decoder conv, Ngemm == 32): per pixel
+  // z = hb + sum_c y[c] hw[c], p = sigmoid(z), BCE/Dice partial sums vs tgt -> hslab[block][4]
+  const float* hw; const float* hb; const float* tgt; float* hslab;
 };
 
 // 2x2 window code from the four (bf16-rounded) values in window order tl, tr, bl, br: first

@@ -460,6 +460,17 @@ __global__ __launch_bounds__(256 * WCS) void igemm_stream_kernel(IgemmArgs a) {
   constexpr int PT = do_pool ? TP : 1, PC = do_pool ? TC : 1;
   float ptop[PT][PC][4], ptop2[PT][PC][4];   // even row of the window: left / right pixel
 
+  // fused segmentation head (EPI 3): segmap weights of this lane's channels, BCE/Dice partials
+  constexpr bool do_head = EPI == 3;
+  float hwv[do_head ? TC : 1][4];
+  float hsum[4] = {0.f, 0.f, 0.f, 0.f};
+  if constexpr (do_head) {
+#pragma unroll
+    for (int ic = 0; ic < TC; ++ic)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) hwv[ic][e] = a.hw[wc * WCN + ic * 16 + 4 * chunk + e];
+  }
+
   // prologue: input rows h0-1, h0, h0+1 -> slots 0, 1, 2
 #pragma unroll 1
   for (int j = 0; j < 3; ++j) {
@@ -517,6 +528,7 @@ __global__ __launch_bounds__(256 * WCS) void igemm_stream_kernel(IgemmArgs a) {
     // epilogue for output row h0 + r: 32-bit buffer offsets = per-lane constant + uniform row base
 #pragma unroll
     for (int ip = 0; ip < TP; ++ip) {
+      float hdot = 0.f;
 #pragma unroll
       for (int ic = 0; ic < TC; ++ic) {
         float v0 = acc[ic][ip][0] + bias[ic][0], v1 = acc[ic][ip][1] + bias[ic][1];
@@ -541,6 +553,12 @@ __global__ __launch_bounds__(256 * WCS) void igemm_stream_kernel(IgemmArgs a) {
                       packed);
         else
           __builtin_amdgcn_raw_buffer_store_b64(packed, yr, yo, 0, 0);
+        if constexpr (do_head) {   // the head sees the STORED bf16 values, like a separate pass would
+          hdot = fmaf(lo_bf(packed.x), hwv[ic][0], hdot);
+          hdot = fmaf(hi_bf(packed.x), hwv[ic][1], hdot);
+          hdot = fmaf(lo_bf(packed.y), hwv[ic][2], hdot);
+          hdot = fmaf(hi_bf(packed.y), hwv[ic][3], hdot);
+        }
         if constexpr (do_pool) {
           // pool the STORED (bf16-rounded) values: identical to max-pooling the tensor afterwards.
           // Even lanes hold pixel w (left), their xor-1 partner pixel w+1 (right).
@@ -572,10 +590,36 @@ __global__ __launch_bounds__(256 * WCS) void igemm_stream_kernel(IgemmArgs a) {
           }
         }
       }
+      if constexpr (do_head) {
+        // the pixel's 32 channels live in lanes l, l^16, l^32, l^48 of this wave
+        hdot += __shfl_xor(hdot, 16, 64);
+        hdot += __shfl_xor(hdot, 32, 64);
+        if (chunk == 0) {
+          const unsigned pix = (unsigned)(orow * a.Wo + w0 + wp * WP + ip * 16 + (lane & 15));
+          const float z = hdot + a.hb[0];
+          const float p = 1.f / (1.f + __expf(-z));
+          const float tt = a.tgt[pix];
+          const float lp = fmaxf(__logf(p), -100.f), l1p = fmaxf(__logf(1.f - p), -100.f);
+          const float one = tt == 1.f ? 1.f : 0.f;
+          hsum[0] -= tt * lp + (1.f - tt) * l1p;
+          hsum[1] += p * one;
+          hsum[2] += p;
+          hsum[3] += one;
+        }
+      }
     }
     __builtin_amdgcn_sched_barrier(0);
     if (r + 1 < nrows) rstore((r + 3) & 3);
     __syncthreads();
+  }
+  if constexpr (do_head) {
+    static_assert(!do_head || NT == 256, "head epilogue reduces over 256 threads");
+    __shared__ float hred[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float v = block_sum_256(hsum[k], hred);
+      if (tid == 0) a.hslab[(long)blockIdx.x * 4 + k] = v;
+    }
   }
 }
 
@@ -703,6 +747,13 @@ static int launch_igemm_stream(const IgemmArgs& a, hipStream_t st) {
     }
     return (int)hipErrorInvalidValue;
   }
+  if (a.hslab) {  // last decoder conv + fused segmentation head / loss partials
+    if constexpr (NG == 32 && WCS == 1) {
+      hipLaunchKernelGGL((igemm_stream_kernel<BP, NG, CS, RH, WCS, 3>), dim3(grid), dim3(256 * WCS), 0, st, a);
+      return (int)hipGetLastError();
+    }
+    return (int)hipErrorInvalidValue;
+  }
   if (a.y2) {     // decoder conv1 dgrad over the concat (NG = 2 CS): skip / up gradients as dense tensors
     if constexpr (NG == 2 * CS) {
       hipLaunchKernelGGL((igemm_stream_kernel<BP, NG, CS, RH, WCS, 2>), dim3(grid), dim3(256 * WCS), 0, st, a);
@@ -712,6 +763,21 @@ static int launch_igemm_stream(const IgemmArgs& a, hipStream_t st) {
   }
   hipLaunchKernelGGL((igemm_stream_kernel<BP, NG, CS, RH, WCS, 0>), dim3(grid), dim3(256 * WCS), 0, st, a);
   return (int)hipGetLastError();
+}
+
+// blocks the streaming launch of `a` (variant 0) uses -- rows of the fused head's slab
+DPA_API int dpa_igemm_stream_blocks(const IgemmArgs* args) {
+  const IgemmArgs& a = *args;
+  int variant;
+  if (a.Cs == 32 && a.Ngemm == 32) variant = 1;
+  else if (a.Cs == 64 && a.Ngemm == 32) variant = 2;
+  else if (a.Cs == 32 && a.Ngemm == 64) variant = 3;
+  else variant = 4;
+  const int bp = (variant == 1 || variant == 3) ? 128 : 64;
+  if (a.Wo % bp) return 0;
+  const long blocks32 = (long)a.N * ((a.Ho + 31) / 32) * (a.Wo / bp);
+  const int rh = blocks32 >= 1024 ? 32 : 16;
+  return a.N * ((a.Ho + rh - 1) / rh) * (a.Wo / bp);
 }
 
 // Eligible: conv3x3 s1 p1 mode 0, Ngemm and Cs in {32, 64}, Wo % 64 == 0, Ho >= 1.

@@ -305,16 +305,15 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(const bf16_t* __restrict_
   }
 }
 
-// deterministic sum of the [nblk][K] slab into out[K] (one block)
+// deterministic sum of the [nblk][K] slab into out[K]: one block per column, fixed order
 __global__ __launch_bounds__(256) void slab_sum_kernel(const float* __restrict__ slab, int nblk, int K, float* __restrict__ out,
                                                        int accumulate) {
   __shared__ float red[4];
-  for (int k = 0; k < K; ++k) {
-    float s = 0.f;
-    for (int i = threadIdx.x; i < nblk; i += blockDim.x) s += slab[(long)i * K + k];
-    s = block_sum_256(s, red);
-    if (threadIdx.x == 0) out[k] = accumulate ? out[k] + s : s;
-  }
+  const int k = blockIdx.x;
+  float s = 0.f;
+  for (int i = threadIdx.x; i < nblk; i += blockDim.x) s += slab[(long)i * K + k];
+  s = block_sum_256(s, red);
+  if (threadIdx.x == 0) out[k] = accumulate ? out[k] + s : s;
 }
 
 static int head_grid(long P) { return dpa_grid(P, 256, 2048); }
@@ -330,7 +329,7 @@ DPA_API int dpa_head_fwd(const bf16_t* y, int ldy, int C, const float* w, const 
     case 64: hipLaunchKernelGGL(head_fwd_kernel<64>, dim3(grid), dim3(256), 0, st, y, ldy, w, b, t, slab, probs, (long)P); break;
     default: return (int)hipErrorInvalidValue;
   }
-  if (slab && S) hipLaunchKernelGGL(slab_sum_kernel, dim3(1), dim3(256), 0, st, slab, grid, 4, S, 0);
+  if (slab && S) hipLaunchKernelGGL(slab_sum_kernel, dim3(4), dim3(256), 0, st, slab, grid, 4, S, 0);
   return (int)hipGetLastError();
 }
 
@@ -404,12 +403,17 @@ DPA_API int dpa_head_bwd(const bf16_t* y, int ldy, int C, const float* w, const 
     case 64: hipLaunchKernelGGL(head_bwd_kernel<64>, dim3(grid), dim3(256), 0, st, y, ldy, w, b, t, dS, gy, ldg, slab, (long)P); break;
     default: return (int)hipErrorInvalidValue;
   }
-  hipLaunchKernelGGL(slab_sum_kernel, dim3(1), dim3(256), 0, st, slab, grid, C + 1, tmp, 0);
+  hipLaunchKernelGGL(slab_sum_kernel, dim3(C + 1), dim3(256), 0, st, slab, grid, C + 1, tmp, 0);
   hipLaunchKernelGGL(head_grad_finish, dim3(1), dim3(128), 0, st, tmp, gw, gb, C);
   return (int)hipGetLastError();
 }
 
 DPA_API int dpa_head_slab_blocks(long long P) { return head_grid(P); }
+
+DPA_API int dpa_slab_sum(const float* slab, int nblk, int K, float* out, hipStream_t st) {
+  hipLaunchKernelGGL(slab_sum_kernel, dim3(K), dim3(256), 0, st, slab, nblk, K, out, 0);
+  return (int)hipGetLastError();
+}
 
 // ------------------------------------------------------------------------------ loss from partials
 // loss = S0/n - dice * log(2 S1 / (S2 + S3 + 1e-15))   (reference utils/utils.py:14-25)

@@ -113,6 +113,8 @@ def run_segment(blocks, start: int, end: int, depth: int, env: Dict[str, torch.T
     ``probs`` (inference) instead of ``x``.
     """
     env = dict(env)
+    if want == "partials" and end == n_blocks(depth) and hasattr(blocks, "expect_target"):
+        blocks.expect_target(target)      # lets a backend fuse the head into the last decoder conv
     if start == 0:
         env["x"] = blocks.prep(env["x"])
     for idx in range(start, end):

@@ -105,6 +105,8 @@ class HipBlocks:
         self._build_packing()
         self._packed_version = None
         self._cats: Dict[int, torch.Tensor] = {}
+        self._target = None        # (target as given, fp32 flat copy) announced by run_segment
+        self._head_cache = None    # (y ptr, target ptr, S) from the fused head epilogue
 
     # ------------------------------------------------------------------ weight packing
     def _build_packing(self):
@@ -292,9 +294,18 @@ class HipBlocks:
         self.ensure_packed()
         return _DecFn.apply(self.anchor, x, skip, self, i)
 
+    def expect_target(self, t):
+        """The segment being run ends in the head: the last decoder conv may compute the head and the
+        loss partial sums in its epilogue (one pass less over the full-resolution activation)."""
+        self._target = None if t is None else (t, t.float().reshape(-1).contiguous())
+
     def head_partials(self, x, t):
-        t = t.float().contiguous()
-        return _HeadFn.apply(self.anchor, x, t, self)
+        if self._target is not None and self._target[0] is t:
+            tf = self._target[1].view(t.shape)
+        else:
+            tf = t.float().contiguous()
+        self._target = None
+        return _HeadFn.apply(self.anchor, x, tf, self)
 
     @torch.no_grad()
     def head_probs(self, x):
@@ -434,7 +445,19 @@ class _DecFn(torch.autograd.Function):
         B.deconv_fwd(d, x, cat[..., C:])
         st1, st2 = [], []
         a = B.conv_fwd(c1, cat, st=st1)
-        y = B.conv_fwd(c2, a, st=st2)
+        N, H, W = a.shape[:3]
+        tgt = B._target[1] if (B._target is not None and i == len(B.deconvs) - 1) else None
+        seg = B.model.segmap
+        if (tgt is not None and c2.bn is None and seg.out_channels == 1 and tgt.numel() == N * H * W
+                and K.head_fusable(N, H, W, c2.Cin, c2.Cout)):
+            # last decoder conv + segmap + sigmoid + BCE/Dice partial sums in one kernel
+            y = torch.empty(N, H, W, c2.Cout, dtype=torch.bfloat16, device=a.device)
+            S = K.igemm(a, B.wf(c2), y, Ngemm=c2.Cout, Kpad=c2.Kf, KH=3, KW=3, stride=1, pad=1, Cs=c2.Cs,
+                        out_grid=(N, H, W), bias=c2.mod.bias, relu=True,
+                        head=(seg.weight.view(-1), seg.bias, tgt))
+            B._head_cache = (y.data_ptr(), tgt.data_ptr(), S)
+        else:
+            y = B.conv_fwd(c2, a, st=st2)
         ctx.B, ctx.i = B, i
         ctx.st = (st1[0] if st1 else None, st2[0] if st2 else None)
         ctx.save_for_backward(x, cat, a)
@@ -469,7 +492,11 @@ class _HeadFn(torch.autograd.Function):
     def forward(ctx, anchor, y, t, B: HipBlocks):
         seg = B.model.segmap
         y = _v(y)
-        S, _ = K.head_fwd(y, seg.weight, seg.bias, t)
+        cache, B._head_cache = B._head_cache, None
+        if cache is not None and cache[0] == y.data_ptr() and cache[1] == t.data_ptr():
+            S = cache[2]                     # computed by the last decoder conv's epilogue
+        else:
+            S, _ = K.head_fwd(y, seg.weight, seg.bias, t)
         ctx.B = B
         ctx.save_for_backward(y, t)
         return S.clone()

@@ -29,7 +29,8 @@ class IgemmArgs(ctypes.Structure):
                [(n, c_int) for n in ("ldx", "ldy", "ldm", "mask_ch", "N", "Ho", "Wo", "Hs", "Ws", "Cs", "KH", "KW",
                                      "stride", "pad", "Ngemm", "Kpad", "mode", "relu", "accumulate", "Cout")] + \
                [("xbytes", ctypes.c_uint), ("pool", c_void_p), ("ldp", c_int), ("pcode", c_void_p), ("y2", c_void_p),
-                ("ldy2", c_int), ("split", c_int)]
+                ("ldy2", c_int), ("split", c_int), ("hw", c_void_p), ("hb", c_void_p), ("tgt", c_void_p),
+                ("hslab", c_void_p)]
 
 
 class WgradArgs(ctypes.Structure):
@@ -77,6 +78,8 @@ USE_HALO = os.environ.get("DPA_NO_HALO", "0") != "1"
 # row-streaming conv3x3 (weights resident, 4-row LDS ring); DPA_NO_STREAM=1 disables
 USE_STREAM = os.environ.get("DPA_NO_STREAM", "0") != "1"
 USE_GLDS = os.environ.get("DPA_NO_GLDS", "0") != "1"
+# segmentation head + loss partials fused into the last decoder conv; DPA_NO_FUSED_HEAD=1 disables
+USE_FUSED_HEAD = os.environ.get("DPA_NO_FUSED_HEAD", "0") != "1"
 
 
 def _extent_bytes(N, H, W, C, ld):
@@ -94,7 +97,7 @@ def igemm(x: torch.Tensor, wpacked: torch.Tensor, y: torch.Tensor, *, Ngemm: int
           stride: int, pad: int, Cs: int, out_grid, bias: Optional[torch.Tensor] = None, relu: bool = False,
           mask: Optional[torch.Tensor] = None, mode: int = 0, Cout: int = 0, accumulate: bool = False, cfg: int = 0,
           path: str = "auto", pool: Optional[torch.Tensor] = None, variant: int = 0,
-          pcode: Optional[torch.Tensor] = None, y2: Optional[torch.Tensor] = None, split: int = 0):
+          pcode: Optional[torch.Tensor] = None, y2: Optional[torch.Tensor] = None, split: int = 0, head=None):
     """Implicit-GEMM conv.  ``out_grid`` = (N, Ho, Wo) pixel grid of GEMM-M.
 
     ``path``: ``auto`` picks, for a conv3x3, the row-streaming kernel (Ngemm, Cs in {32, 64}), then the
@@ -104,7 +107,9 @@ def igemm(x: torch.Tensor, wpacked: torch.Tensor, y: torch.Tensor, *, Ngemm: int
     max-pool of ``y`` (fused into the streaming kernel's epilogue, else a separate pass); ``pcode``: with
     ``pool``, the per-window codes (argmax + ReLU masks, uint8 [N, Ho/2, Wo/2, Ngemm]) that
     :func:`pool_bwd_code` consumes.  ``y2``/``split``: output channels >= ``split`` go to the dense
-    tensor ``y2`` (channel ``co - split``) -- the two halves of a concat gradient."""
+    tensor ``y2`` (channel ``co - split``) -- the two halves of a concat gradient.  ``head`` =
+    (segmap weight, segmap bias, target [N*Ho*Wo] fp32): the streaming kernel also computes the fused
+    segmap + sigmoid + BCE/Dice partial sums of its (bf16) output; returns them as S[4]."""
     N, Hs, Ws, Cx, ldx = _nhwc(x, "igemm.x")
     _, _, _, Cy, ldy = _nhwc(y, "igemm.y")
     No, Ho, Wo = out_grid
@@ -139,6 +144,13 @@ def igemm(x: torch.Tensor, wpacked: torch.Tensor, y: torch.Tensor, *, Ngemm: int
     L = _lib.lib()
     st = _stream(y)
     pool_done = True
+    hslab, hrows = None, 0
+    if head is not None:
+        hw, hb, tgt = head
+        assert mode == 0 and Ngemm == 32 and Cs == 32 and pool is None and y2 is None and mask is None
+        assert hw.dtype == torch.float32 and hw.is_contiguous() and hw.numel() == 32 and hb.numel() == 1
+        assert tgt.dtype == torch.float32 and tgt.is_contiguous() and tgt.numel() == N * Ho * Wo
+        hslab = torch.empty((N * -(-Ho // 16) * max(1, Wo // 64) + 1) * 4, dtype=torch.float32, device=y.device)
     for n0, n1 in _image_chunks(N, max(Hs * Ws * ldx, (4 if mode else 1) * Ho * Wo * ldy) * 2):
         xs, ys = x[n0:n1], y[n0:n1]
         nb = n1 - n0
@@ -149,6 +161,15 @@ def igemm(x: torch.Tensor, wpacked: torch.Tensor, y: torch.Tensor, *, Ngemm: int
                       None if y2 is None else y2[n0:n1].data_ptr(), ldy2, split)
         conv3 = mode == 0 and KH == 3 and stride == 1 and cfg == 0
         stream_ok = (Ngemm in (32, 64) and Cs in (32, 64)) or (Ngemm == 32 and Cs == 8 and pool is None)
+        if head is not None:
+            rows = L.dpa_igemm_stream_blocks(ctypes.byref(a))
+            assert conv3 and stream_ok and rows > 0 and path in ("auto", "stream"), "fused head needs the stream kernel"
+            a.hw, a.hb = hw.data_ptr(), hb.data_ptr()
+            a.tgt = tgt[n0 * Ho * Wo:].data_ptr()
+            a.hslab = hslab[hrows * 4:].data_ptr()
+            _check(L.dpa_igemm_stream(ctypes.byref(a), c_int(0), st), "igemm_stream+head")
+            hrows += rows
+            continue
         if path == "stream" or (path == "auto" and USE_STREAM and conv3 and stream_ok):
             if pool is not None:
                 a.pool, a.ldp = pool[n0:n1].data_ptr(), ldp
@@ -182,6 +203,15 @@ def igemm(x: torch.Tensor, wpacked: torch.Tensor, y: torch.Tensor, *, Ngemm: int
         _check(L.dpa_igemm(ctypes.byref(a), c_int(cfg), st), "igemm")
     if pool is not None and not pool_done:
         maxpool2(y, pool, pcode)
+    if head is not None:
+        S = hslab[hslab.numel() - 4:]
+        _check(L.dpa_slab_sum(_p(hslab), c_int(hrows), c_int(4), _p(S), st), "slab_sum")
+        return S
+
+
+def head_fusable(N: int, H: int, W: int, Cin: int, Cout: int) -> bool:
+    """Can the last decoder conv (Cin -> Cout = 32) carry the segmentation head in its epilogue?"""
+    return USE_STREAM and USE_FUSED_HEAD and Cin == 32 and Cout == 32 and W % 128 == 0
 
 
 # ------------------------------------------------------------------------------------------ wgrad

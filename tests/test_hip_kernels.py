@@ -451,3 +451,28 @@ def test_dgrad_split_output(hip_lib, N, H, W, Cin, Cout, path):
     K.igemm(g, packed, lo, y2=hi, split=s, **kw)
     torch.cuda.synchronize()
     assert torch.equal(lo, full[..., :s]) and torch.equal(hi, full[..., s:])
+
+
+@pytest.mark.parametrize("N,H,W", [(2, 7, 128), (1, 33, 256)])
+def test_stream_conv_fused_head(hip_lib, N, H, W):
+    """Last decoder conv with the segmentation head + loss partial sums in its epilogue == conv, then
+    the separate head kernel on the stored output (same bf16 values)."""
+    from distributedpytorch_amd.ops import kernels as K
+    torch.manual_seed(8)
+    x = _nhwc(_bf(torch.randn(N, 32, H, W)).relu())
+    w = torch.randn(32, 32, 3, 3) / 17
+    wf, _, _ = _pack_one(0, w)
+    b = (torch.randn(32) * 0.1).cuda()
+    hw = (torch.randn(32) * 0.3).cuda()
+    hb = torch.tensor([0.1], device="cuda")
+    t = (torch.rand(N * H * W, device="cuda") > 0.5).float()
+    y = torch.empty(N, H, W, 32, dtype=torch.bfloat16, device="cuda")
+    S = K.igemm(x, wf, y, Ngemm=32, Kpad=K.round_up(9 * 32, 32), KH=3, KW=3, stride=1, pad=1, Cs=32,
+                out_grid=(N, H, W), bias=b, relu=True, head=(hw, hb, t))
+    y2 = torch.empty_like(y)
+    K.igemm(x, wf, y2, Ngemm=32, Kpad=K.round_up(9 * 32, 32), KH=3, KW=3, stride=1, pad=1, Cs=32,
+            out_grid=(N, H, W), bias=b, relu=True, path="stream")
+    S_ref, _ = K.head_fwd(y2, hw, hb, t)
+    torch.cuda.synchronize()
+    assert torch.equal(y, y2)
+    assert torch.allclose(S, S_ref, rtol=1e-4, atol=1e-2), (S, S_ref)
