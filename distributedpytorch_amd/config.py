@@ -52,6 +52,7 @@ class TrainConfig:
     save_every_epoch: bool = True
     resume: bool = False
     profile: bool = False
+    trace_ranges: bool = False                      # roctx ranges per block / bucket / stage op
     cuda_graph: bool = False                         # singleGPU: replay the whole step from a HIP graph
     debug_sync: bool = False                         # synchronise after every kernel / stage op
     watchdog: float = 0.0                            # abort if no step completes for N seconds (0 = off)
@@ -96,6 +97,8 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--log-every", type=int, default=10)
     p.add_argument("--resume", action="store_true", help="resume from checkpoints/<method>_last.pt")
     p.add_argument("--profile", action="store_true", help="torch.profiler trace of a few steps")
+    p.add_argument("--trace-ranges", action="store_true",
+                   help="roctx ranges around blocks, pipeline transfers and all-reduce buckets (rocprofv3 --marker-trace)")
     p.add_argument("--cuda-graph", action="store_true", help="capture the training step in a HIP graph")
     p.add_argument("--debug-sync", action="store_true",
                    help="synchronise after every HIP kernel and pipeline stage op (race / fault triage)")
@@ -119,7 +122,7 @@ def parse_args(argv=None) -> TrainConfig:
         synthetic_len=a.synthetic_len, data_dir=a.data_dir, out_dir=a.out_dir, device=a.device,
         stages=a.stages, microbatches=a.microbatches, bucket_mb=a.bucket_mb, global_dice=a.global_dice,
         loss_scale_by_batch=a.loss_scale_by_batch, max_steps=a.max_steps, num_workers=a.num_workers,
-        log_every=a.log_every, resume=a.resume, profile=a.profile, cuda_graph=a.cuda_graph,
+        log_every=a.log_every, resume=a.resume, profile=a.profile, trace_ranges=a.trace_ranges, cuda_graph=a.cuda_graph,
         debug_sync=a.debug_sync, watchdog=a.watchdog, comm_timeout=a.comm_timeout, nan_policy=a.nan_policy)
     return cfg
 

@@ -20,6 +20,7 @@ from typing import Dict, List, Sequence, Tuple
 import torch
 import torch.nn.functional as F
 
+from ..utils.tracing import trace_range
 from .unet import UNet, UNetConfig
 
 
@@ -119,20 +120,21 @@ def run_segment(blocks, start: int, end: int, depth: int, env: Dict[str, torch.T
         env["x"] = blocks.prep(env["x"])
     for idx in range(start, end):
         kind, i = block_kind(idx, depth)
-        if kind == "enc":
-            s, env["x"] = blocks.enc(i, env["x"])
-            env[skip_name(i)] = s
-        elif kind == "mid":
-            env["x"] = blocks.mid(env["x"])
-        elif kind == "dec":
-            name = skip_name(depth - 1 - i)
-            env["x"] = blocks.dec(i, env["x"], env.pop(name))
-        else:
-            x = env.pop("x")
-            if want == "partials":
-                env["partials"] = blocks.head_partials(x, target)
+        with trace_range(f"{kind}{i}" if kind in ("enc", "dec") else kind):
+            if kind == "enc":
+                s, env["x"] = blocks.enc(i, env["x"])
+                env[skip_name(i)] = s
+            elif kind == "mid":
+                env["x"] = blocks.mid(env["x"])
+            elif kind == "dec":
+                name = skip_name(depth - 1 - i)
+                env["x"] = blocks.dec(i, env["x"], env.pop(name))
             else:
-                env["probs"] = blocks.head_probs(x)
+                x = env.pop("x")
+                if want == "partials":
+                    env["partials"] = blocks.head_partials(x, target)
+                else:
+                    env["probs"] = blocks.head_probs(x)
     return env
 
 

@@ -23,6 +23,15 @@ output is already multiplied by the ReLU mask (the consumer applies it in its ow
 for the encoder skip, whose two consumers (pool, decoder concat) add up, the mask is applied once in
 the fused pool-backward kernel.  Parameters stay fp32 (master weights); a single batched kernel
 repacks them to bf16 GEMM layouts whenever they changed (``space.version``).
+
+Fusions across block boundaries: the last decoder conv computes the segmentation head and the loss
+partial sums in its epilogue when the segment ends in the head (``expect_target``); the
+full-resolution transposed convs run their dgrad and weight gradient in one pass.
+
+Variants (north-star DoubleConv / Up): a conv followed by BatchNorm writes its raw output z, then
+``bn_fwd`` (statistics + normalise + ReLU) produces the activation; the backward runs ``bn_bwd``
+on the masked gradient before the conv's dgrad/wgrad.  The bilinear Up path runs its 1x1
+projection at the low resolution and up-samples into the concat half (``_Up``).
 """
 from __future__ import annotations
 

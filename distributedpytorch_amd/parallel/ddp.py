@@ -26,6 +26,7 @@ import torch
 import torch.distributed as dist
 
 from ..optim import FlatParameterSpace
+from ..utils.tracing import trace_range
 
 
 class BucketedAllReduce:
@@ -83,6 +84,10 @@ class BucketedAllReduce:
             self.next_launch += 1
 
     def _launch(self, b: int):
+        with trace_range(f"allreduce_bucket{b}"):
+            self._launch_bucket(b)
+
+    def _launch_bucket(self, b: int):
         s, e, _, _ = self.buckets[b]
         t = self.space.grad[s:e]
         if self.nccl and self.average and self.scale == 1.0:

@@ -33,6 +33,7 @@ import torch.distributed as dist
 from ..compute import loss_from_partials, make_blocks
 from ..models.blocks import boundary_names, block_kind, n_blocks, partition, run_segment, skip_name
 from ..optim import FlatParameterSpace
+from ..utils.tracing import trace_range
 
 
 def _debug_point(device):
@@ -206,7 +207,8 @@ class GPipeDist:
                     nxt = self._irecv(mb, h, w)
                 leaves = {k: v.detach().requires_grad_(True) for k, v in bufs.items()}
                 env = dict(leaves)
-            out = self.stage.forward(env, ts[m], "partials")
+            with trace_range(f"stage{self.rank}_fwd_mb{m}"):
+                out = self.stage.forward(env, ts[m], "partials")
             _debug_point(self.device)
             saved_in.append(leaves)
             if self.is_last:
@@ -229,6 +231,8 @@ class GPipeDist:
             (loss * loss_scale).backward()
             dP = P.grad
         for m in reversed(range(M)):
+            rng = trace_range(f"stage{self.rank}_bwd_mb{m}")
+            rng.__enter__()
             if self.is_last:
                 torch.autograd.backward(partials[m], dP[m])
             else:
@@ -243,6 +247,7 @@ class GPipeDist:
                 for wk in works:
                     wk.wait()
                 torch.autograd.backward(outs, [g.to(o.dtype) for o, g in zip(outs, grads)])
+            rng.__exit__(None, None, None)
             _debug_point(self.device)
             if not self.is_first:
                 for name, src in self.recv_spec[self.rank]:

@@ -338,6 +338,9 @@ def train(cfg: TrainConfig):
     if cfg.debug_sync:
         from .ops._lib import set_debug_sync
         set_debug_sync(True)
+    if cfg.trace_ranges or cfg.profile:
+        from .utils.tracing import enable_ranges
+        enable_ranges(True)
     set_seed(cfg.seed)
     _setup_logging(cfg, rank)
     log.info("UNet for Carvana Image Masking (Segmentation)")

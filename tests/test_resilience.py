@@ -68,3 +68,27 @@ def test_cli_resilience_flags():
                       "--cuda-graph"])
     assert cfg.watchdog == 60 and cfg.comm_timeout == 120 and cfg.nan_policy == "warn"
     assert cfg.debug_sync and cfg.cuda_graph
+
+
+def test_trace_ranges_wrap_blocks_without_changing_results():
+    """roctx/record_function ranges (utils.tracing) around blocks: results identical, ranges visible
+    in a torch.profiler trace."""
+    import torch
+    from distributedpytorch_amd.compute import make_compute
+    from distributedpytorch_amd.models.unet import build_model
+    from distributedpytorch_amd.utils import tracing
+    torch.manual_seed(0)
+    m = build_model("unet-tiny")
+    comp = make_compute(m, backend="torch", dtype="fp32")
+    x = torch.rand(2, 3, 32, 32)
+    t = (torch.rand(2, 1, 32, 32) > 0.5).float()
+    s0 = comp.forward_partials(x, t)
+    tracing.enable_ranges(True)
+    try:
+        with torch.profiler.profile() as prof:
+            s1 = comp.forward_partials(x, t)
+    finally:
+        tracing.enable_ranges(False)
+    assert torch.equal(s0, s1)
+    names = {e.name for e in prof.events()}
+    assert {"enc0", "enc1", "mid", "dec0", "dec1", "head"} <= names
