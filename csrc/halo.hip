@@ -832,7 +832,7 @@ DPA_API int dpa_igemm_stream(const IgemmArgs* args, int variant, hipStream_t st)
 // [pixel][channel] LDS images through ds_read_b64_tr_b16 (conflict-free swizzles, any row shift).
 // Bias gradient: the loader threads sum the gradient chunks they stage, reduced once per block.
 template <int BM, int BN, int BP, int RH>
-__global__ __launch_bounds__(192) void wgrad_stream_kernel(WgradArgs a) {
+__global__ __launch_bounds__(192) void wgrad_stream_kernel(WgradArgs a, int ipb) {
   constexpr int NT = 192;
   constexpr int HR = BP + 2;
   constexpr int CPRA = BM / 8, CPRB = BN / 8, RBA = BM * 2, RBB = BN * 2;
@@ -848,14 +848,15 @@ __global__ __launch_bounds__(192) void wgrad_stream_kernel(WgradArgs a) {
   const int nmt = a.M / BM, nnt = (a.Nc + BN - 1) / BN, tiles = nmt * nnt;
   const int stripsW = a.Wg / BP, segsH = (a.Hg + RH - 1) / RH;
   const int bid = xcd_remap(blockIdx.x, tiles * a.splits);
-  const int split = bid / tiles, tile = bid - split * tiles;     // split = (n, hs, ws)
+  const int split = bid / tiles, tile = bid - split * tiles;     // split = (image group, hs, ws)
   const int mt = tile / nnt, nt = tile - mt * nnt;
   const int m0 = mt * BM, n0 = nt * BN;
-  const int n = split / (segsH * stripsW);
-  const int rem = split - n * segsH * stripsW;
+  const int ig = split / (segsH * stripsW);                      // images [ig*ipb, ig*ipb + ipb)
+  const int rem = split - ig * segsH * stripsW;
   const int hs = rem / stripsW;
   const int w0 = (rem - hs * stripsW) * BP, h0 = hs * RH;
   const int nrows = min(RH, a.Hg - h0);
+  const int nimg = min(ipb, a.N - ig * ipb);
   const int tid = threadIdx.x, lane = tid & 63, kh = tid >> 6;
   const bool do_bias = a.bslab != nullptr && nt == 0;
   const __amdgpu_buffer_rsrc_t ar = __builtin_amdgcn_make_buffer_rsrc((void*)a.A, 0, (int)a.abytes, 0x00020000);
@@ -881,6 +882,7 @@ __global__ __launch_bounds__(192) void wgrad_stream_kernel(WgradArgs a) {
   }
   const unsigned arow = (unsigned)(a.WA * a.lda * 2), brow = (unsigned)(a.WB * a.ldb * 2);
   u32x4_t ra[LA], rb[LB];
+  int n = ig * ipb;
   auto load_a = [&](int h) {
     const unsigned base = (unsigned)(n * a.HA + h) * arow;
 #pragma unroll
@@ -914,6 +916,8 @@ __global__ __launch_bounds__(192) void wgrad_stream_kernel(WgradArgs a) {
 #pragma unroll
       for (int j = 0; j < TN; ++j) acc[kw][i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
+#pragma unroll 1
+  for (int im = 0; im < nimg; ++im, ++n) {
   // prologue: input rows h0-1, h0, h0+1 -> ring slots 0..2; gradient row h0 -> A buffer 0
   if (nrows > 0) {
 #pragma unroll 1
@@ -969,6 +973,7 @@ __global__ __launch_bounds__(192) void wgrad_stream_kernel(WgradArgs a) {
     }
     __syncthreads();
   }
+  }   // images of this split
   // epilogue: this split's partial dW for taps (kh, 0..2)
 #pragma unroll
   for (int kw = 0; kw < 3; ++kw)
@@ -997,21 +1002,24 @@ __global__ __launch_bounds__(192) void wgrad_stream_kernel(WgradArgs a) {
 }
 
 template <int BM, int BN, int BP, int RH>
-static int launch_wgrad_stream(const WgradArgs& a, hipStream_t st) {
+static int launch_wgrad_stream(const WgradArgs& a, int ipb, hipStream_t st) {
   const int tiles = (a.M / BM) * ((a.Nc + BN - 1) / BN);
-  hipLaunchKernelGGL((wgrad_stream_kernel<BM, BN, BP, RH>), dim3(tiles * a.splits), dim3(192), 0, st, a);
+  hipLaunchKernelGGL((wgrad_stream_kernel<BM, BN, BP, RH>), dim3(tiles * a.splits), dim3(192), 0, st, a, ipb);
   return (int)hipGetLastError();
 }
 
-// splits must equal N * ceil(Hg/RH) * (Wg/BP); cfg picks (BM, BN): 1: 32x32  2: 64x32  3: 32x64
+// A split = ipb consecutive images x one (row segment, column strip): splits must equal
+// ceil(N/ipb) * ceil(Hg/RH) * (Wg/BP).  More images per split = fewer fp32 slabs to reduce (the
+// reduction's bytes otherwise grow with the batch).  cfg picks (BM, BN): 1: 32x32  2: 64x32  3: 32x64
 // 4: 32x16 with Nc == 8 (the first layer's 8-padded RGB input; channels 8..15 read as zeros)
-DPA_API int dpa_wgrad_stream(const WgradArgs* args, int cfg, int bp, int rh, hipStream_t st) {
+DPA_API int dpa_wgrad_stream(const WgradArgs* args, int cfg, int bp, int rh, int ipb, hipStream_t st) {
   const WgradArgs& a = *args;
-  if ((a.lda & 7) || (a.ldb & 7) || a.s != 1 || a.pad != 1 || a.KW != 3 || a.HA != a.Hg || a.WA != a.Wg ||
-      a.HB != a.Hg || a.WB != a.Wg || a.Wg % bp || a.splits != a.N * ((a.Hg + rh - 1) / rh) * (a.Wg / bp))
+  if (ipb < 1 || (a.lda & 7) || (a.ldb & 7) || a.s != 1 || a.pad != 1 || a.KW != 3 || a.HA != a.Hg || a.WA != a.Wg ||
+      a.HB != a.Hg || a.WB != a.Wg || a.Wg % bp ||
+      a.splits != ((a.N + ipb - 1) / ipb) * ((a.Hg + rh - 1) / rh) * (a.Wg / bp))
     return (int)hipErrorInvalidValue;
 #define DPA_WS(C, BMv, BNv, BPv, RHv)                                                              \
-  if (cfg == C && bp == BPv && rh == RHv && a.M % BMv == 0 && a.Nc % BNv == 0) return launch_wgrad_stream<BMv, BNv, BPv, RHv>(a, st);
+  if (cfg == C && bp == BPv && rh == RHv && a.M % BMv == 0 && a.Nc % BNv == 0) return launch_wgrad_stream<BMv, BNv, BPv, RHv>(a, ipb, st);
   DPA_WS(1, 32, 32, 64, 64)
   DPA_WS(2, 64, 32, 64, 64)
   DPA_WS(3, 32, 64, 64, 64)
@@ -1020,8 +1028,8 @@ DPA_API int dpa_wgrad_stream(const WgradArgs* args, int cfg, int bp, int rh, hip
   DPA_WS(3, 32, 64, 64, 32)
 #undef DPA_WS
   if (cfg == 4 && a.Nc == 8 && a.M % 32 == 0 && bp == 64) {
-    if (rh == 64) return launch_wgrad_stream<32, 16, 64, 64>(a, st);
-    if (rh == 32) return launch_wgrad_stream<32, 16, 64, 32>(a, st);
+    if (rh == 64) return launch_wgrad_stream<32, 16, 64, 64>(a, ipb, st);
+    if (rh == 32) return launch_wgrad_stream<32, 16, 64, 32>(a, ipb, st);
   }
   return (int)hipErrorInvalidValue;
 }

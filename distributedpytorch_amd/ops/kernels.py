@@ -282,6 +282,9 @@ def wgrad(A: torch.Tensor, B: torch.Tensor, *, kind: int, grid, M: int, Nc: int,
                                   c_int(Nreal), c_int(1 if kind == 1 else 0), st), "wgrad_reduce")
 
 
+WGRAD_STREAM_BLOCKS = int(os.environ.get("DPA_WGRAD_STREAM_BLOCKS", "2048"))
+
+
 def _wgrad_stream(A, B, *, grid, M, Nc, gw, gb, Nreal):
     NA, HA, WA, CA, lda = _nhwc(A, "wgrad.A")
     NB, HB, WB, CB, ldb = _nhwc(B, "wgrad.B")
@@ -299,13 +302,17 @@ def _wgrad_stream(A, B, *, grid, M, Nc, gw, gb, Nreal):
     for n0, n1 in _image_chunks(N, max(HA * WA * lda, HB * WB * ldb) * 2):
         nb = n1 - n0
         rh = 64 if nb * -(-Hg // 64) * (Wg // 64) * tiles >= 1024 else 32
-        splits = nb * -(-Hg // rh) * (Wg // 64)
+        per_img = -(-Hg // rh) * (Wg // 64)
+        # images per split: keep >= ~2048 blocks (8 per CU) but no more slabs than that -- the fp32
+        # slab reduction otherwise grows linearly with the batch
+        ipb = max(1, (nb * per_img * tiles) // WGRAD_STREAM_BLOCKS)
+        splits = -(-nb // ipb) * per_img
         slab = torch.empty(splits * 9 * M * Nc + splits * M, dtype=torch.float32, device=A.device)
         bslab = slab[splits * 9 * M * Nc:] if gb is not None else None
         a = WgradArgs(A[n0:n1].data_ptr(), B[n0:n1].data_ptr(), slab.data_ptr(),
                       None if bslab is None else bslab.data_ptr(), lda, ldb, nb, Hg, Wg, HA, WA, HB, WB, M, Nc, 1,
                       1, 3, 0, splits, _extent_bytes(nb, HA, WA, CA, lda), _extent_bytes(nb, HB, WB, CB, ldb))
-        _check(L.dpa_wgrad_stream(ctypes.byref(a), c_int(hcfg), c_int(64), c_int(rh), st), "wgrad_stream")
+        _check(L.dpa_wgrad_stream(ctypes.byref(a), c_int(hcfg), c_int(64), c_int(rh), c_int(ipb), st), "wgrad_stream")
         _check(L.dpa_wgrad_reduce(_p(slab), _p(bslab), _p(gw), _p(gb), c_int(splits), c_int(9), c_int(M), c_int(Nc),
                                   c_int(Nreal), c_int(0), st), "wgrad_reduce")
 
