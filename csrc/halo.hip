@@ -16,10 +16,13 @@
 #include "conv_args.h"
 
 // ------------------------------------------------------------------------------------ igemm_halo
-template <int BP, int BC, int WP, int WC>
+// ROWS output rows per block share one staging of each weight slice (the weights are ~60% of a
+// slice's LDS writes at 64-128 output channels, and ds_write bandwidth, not the MFMAs, bounds this
+// kernel): ROWS = 2 stages 4 input rows + the weights for twice the MFMAs of ROWS = 1.
+template <int BP, int BC, int WP, int WC, int ROWS = 1>
 __global__ __launch_bounds__(256) void igemm_halo_kernel(IgemmArgs a) {
   constexpr int HR = BP + 2;              // pixels per halo row
-  constexpr int PROWS = 3 * HR;           // staged pixel rows (64 B = 32 channels each)
+  constexpr int PROWS = (ROWS + 2) * HR;  // staged pixel rows (64 B = 32 channels each)
   constexpr int PBYTES = PROWS * 64;
   constexpr int WRB = 9 * 64;             // weight row bytes: 9 taps x 32 channels (576 = 64 mod 256)
   constexpr int NWC = BC / WC, NWP = BP / WP;
@@ -32,24 +35,27 @@ __global__ __launch_bounds__(256) void igemm_halo_kernel(IgemmArgs a) {
   char* const Wimg = lds + PBYTES;
 
   const int tilesPerRow = a.Wo / BP;
-  const int npt = a.N * a.Ho * tilesPerRow;
+  const int rowGroups = (a.Ho + ROWS - 1) / ROWS;
+  const int npt = a.N * rowGroups * tilesPerRow;
   const int nct = a.Ngemm / BC;
   const int bid = xcd_remap(blockIdx.x, npt * nct);
   const int pt = bid / nct, ct = bid - pt * nct;
   const int c0 = ct * BC;
-  const int rowid = pt / tilesPerRow;               // n * Ho + h (uniform)
+  const int rowid = pt / tilesPerRow;               // n * rowGroups + row group (uniform)
   const int w0 = (pt - rowid * tilesPerRow) * BP;
-  const int n = rowid / a.Ho, h = rowid - n * a.Ho;
-  const long m0 = (long)rowid * a.Wo + w0;
+  const int n = rowid / rowGroups, h = (rowid - n * rowGroups) * ROWS;
+  const long m0 = ((long)n * a.Ho + h) * a.Wo + w0;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wp = wid / NWC, wc = wid - wp * NWC;
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, 0, (int)a.xbytes, 0x00020000);
 
-  f32x4_t acc[TC][TP];
+  f32x4_t acc[ROWS][TC][TP];
 #pragma unroll
-  for (int ic = 0; ic < TC; ++ic)
+  for (int rr = 0; rr < ROWS; ++rr)
 #pragma unroll
-    for (int ip = 0; ip < TP; ++ip) acc[ic][ip] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    for (int ic = 0; ic < TC; ++ic)
+#pragma unroll
+      for (int ip = 0; ip < TP; ++ip) acc[rr][ic][ip] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
   // per-thread staging plan, computed once: global byte offsets (slice 0) + LDS offsets
   const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)a.w, 0, 0x7fffffff, 0x00020000);
@@ -113,27 +119,33 @@ __global__ __launch_bounds__(256) void igemm_halo_kernel(IgemmArgs a) {
         af[ic] = *reinterpret_cast<const bf16x8_t*>(Wimg + r * WRB + tap * 64 + (swz_nk<32>(r, chunk) << 4));
       }
 #pragma unroll
-      for (int ip = 0; ip < TP; ++ip) {
-        const int r = kh * HR + wp * WP + ip * 16 + (lane & 15) + kw;
-        bfr[ip] = *reinterpret_cast<const bf16x8_t*>(Pimg + r * 64 + (swz_nk<32>(r, chunk) << 4));
+      for (int rr = 0; rr < ROWS; ++rr) {
+#pragma unroll
+        for (int ip = 0; ip < TP; ++ip) {
+          const int r = (kh + rr) * HR + wp * WP + ip * 16 + (lane & 15) + kw;
+          bfr[ip] = *reinterpret_cast<const bf16x8_t*>(Pimg + r * 64 + (swz_nk<32>(r, chunk) << 4));
+        }
+#pragma unroll
+        for (int ic = 0; ic < TC; ++ic)
+#pragma unroll
+          for (int ip = 0; ip < TP; ++ip)
+            acc[rr][ic][ip] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ic], bfr[ip], acc[rr][ic][ip], 0, 0, 0);
       }
-#pragma unroll
-      for (int ic = 0; ic < TC; ++ic)
-#pragma unroll
-        for (int ip = 0; ip < TP; ++ip)
-          acc[ic][ip] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ic], bfr[ip], acc[ic][ip], 0, 0, 0);
     }
     __builtin_amdgcn_sched_barrier(0);
   }
 
   // ---- epilogue (mode 0): bias, ReLU, ReLU-backward mask, accumulate; 8-byte bf16 stores
 #pragma unroll
+  for (int rr = 0; rr < ROWS; ++rr) {
+  if (h + rr >= a.Ho) break;
+#pragma unroll
   for (int ip = 0; ip < TP; ++ip) {
-    const long m = m0 + wp * WP + ip * 16 + (lane & 15);
+    const long m = m0 + (long)rr * a.Wo + wp * WP + ip * 16 + (lane & 15);
 #pragma unroll
     for (int ic = 0; ic < TC; ++ic) {
       const int co = c0 + wc * WC + ic * 16 + 4 * (lane >> 4);
-      float v0 = acc[ic][ip][0], v1 = acc[ic][ip][1], v2 = acc[ic][ip][2], v3 = acc[ic][ip][3];
+      float v0 = acc[rr][ic][ip][0], v1 = acc[rr][ic][ip][1], v2 = acc[rr][ic][ip][2], v3 = acc[rr][ic][ip][3];
       if (a.bias) {
         const float* b = a.bias + co;
         v0 += b[0]; v1 += b[1]; v2 += b[2]; v3 += b[3];
@@ -157,17 +169,18 @@ __global__ __launch_bounds__(256) void igemm_halo_kernel(IgemmArgs a) {
       if (!split_store(a, (unsigned)m, co, packed)) *reinterpret_cast<u32x2_t*>(dst) = packed;
     }
   }
+  }
 }
 
-template <int BP, int BC, int WP, int WC>
+template <int BP, int BC, int WP, int WC, int ROWS = 1>
 static int launch_igemm_halo(const IgemmArgs& a, hipStream_t st) {
-  const int grid = a.N * a.Ho * (a.Wo / BP) * (a.Ngemm / BC);
-  hipLaunchKernelGGL((igemm_halo_kernel<BP, BC, WP, WC>), dim3(grid), dim3(256), 0, st, a);
+  const int grid = a.N * ((a.Ho + ROWS - 1) / ROWS) * (a.Wo / BP) * (a.Ngemm / BC);
+  hipLaunchKernelGGL((igemm_halo_kernel<BP, BC, WP, WC, ROWS>), dim3(grid), dim3(256), 0, st, a);
   return (int)hipGetLastError();
 }
 
 // Returns hipErrorInvalidValue (nothing launched) when the shape is not eligible; the caller then
-// uses dpa_igemm.  cfg: 0 auto, 1: 256x32, 2: 128x64, 3: 128x32
+// uses dpa_igemm.  cfg: 0 auto, 1: 256x32, 2: 128x64, 3: 128x32, 4: 128x64 two rows, 5: 128x32 two rows
 DPA_API int dpa_igemm_halo(const IgemmArgs* args, int cfg, hipStream_t st) {
   const IgemmArgs& a = *args;
   if (a.mode != 0 || a.KH != 3 || a.KW != 3 || a.stride != 1 || a.pad != 1 || (a.Cs % 32) || (a.ldx & 7) ||
@@ -175,14 +188,18 @@ DPA_API int dpa_igemm_halo(const IgemmArgs* args, int cfg, hipStream_t st) {
     return (int)hipErrorInvalidValue;
   if (cfg == 0) {
     if (a.Ngemm == 32 && a.Wo % 256 == 0) cfg = 1;
-    else if (a.Ngemm % 64 == 0 && a.Ngemm <= 128 && a.Wo % 128 == 0) cfg = 2;
-    else if (a.Ngemm % 32 == 0 && a.Ngemm <= 64 && a.Wo % 128 == 0) cfg = 3;
+    // two output rows per block: 20-25% faster than one row on every 512^2 UNet shape
+    // (profiles/kbench_b32_512.txt halo.c4/c5 vs c2/c3)
+    else if (a.Ngemm % 64 == 0 && a.Ngemm <= 128 && a.Wo % 128 == 0) cfg = 4;
+    else if (a.Ngemm % 32 == 0 && a.Ngemm <= 64 && a.Wo % 128 == 0) cfg = 5;
     else return (int)hipErrorInvalidValue;
   }
   switch (cfg) {
     case 1: if (a.Wo % 256 || a.Ngemm % 32) break; return launch_igemm_halo<256, 32, 64, 32>(a, st);
     case 2: if (a.Wo % 128 || a.Ngemm % 64) break; return launch_igemm_halo<128, 64, 64, 32>(a, st);
     case 3: if (a.Wo % 128 || a.Ngemm % 32) break; return launch_igemm_halo<128, 32, 32, 32>(a, st);
+    case 4: if (a.Wo % 128 || a.Ngemm % 64) break; return launch_igemm_halo<128, 64, 64, 32, 2>(a, st);
+    case 5: if (a.Wo % 128 || a.Ngemm % 32) break; return launch_igemm_halo<128, 32, 32, 32, 2>(a, st);
     default: break;
   }
   return (int)hipErrorInvalidValue;

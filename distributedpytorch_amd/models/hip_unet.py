@@ -450,7 +450,19 @@ class _DecFn(torch.autograd.Function):
         c1, c2 = B.dec_convs[i]
         C = d.Cout
         x = _v(x)
-        cat = B.cat_for(_v(skip))
+        skip = _v(skip)
+        Ns, Hs, Ws, _ = skip.shape
+        h2, w2 = 2 * x.shape[1], 2 * x.shape[2]
+        ctx.crop = None
+        if (Hs, Ws) != (h2, w2):
+            # reference CenterCrop of the skip to the up-sampled size (model/unet_parts.py:58-74):
+            # H, W not divisible by 2**depth -- the cropped skip is copied into a fresh concat buffer
+            top, left = int(round((Hs - h2) / 2.0)), int(round((Ws - w2) / 2.0))
+            cat = torch.empty(Ns, h2, w2, 2 * C, dtype=torch.bfloat16, device=x.device)
+            cat[..., :C].copy_(skip[:, top:top + h2, left:left + w2])
+            ctx.crop = (Hs, Ws, top, left)
+        else:
+            cat = B.cat_for(skip)
         B.deconv_fwd(d, x, cat[..., C:])
         st1, st2 = [], []
         a = B.conv_fwd(c1, cat, st=st1)
@@ -493,6 +505,11 @@ class _DecFn(torch.autograd.Function):
         dx = B.deconv_bwd(d, gup, x)
         B.ready([d.mod])
         ctx.st = None
+        if ctx.crop is not None:     # gradient of the crop: zero outside the kept window
+            Hs, Ws, top, left = ctx.crop
+            full = torch.zeros(dskip.shape[0], Hs, Ws, C, dtype=dskip.dtype, device=dskip.device)
+            full[:, top:top + dskip.shape[1], left:left + dskip.shape[2]] = dskip
+            dskip = full
         return None, _o(dx), _o(dskip), None, None
 
 

@@ -78,6 +78,7 @@ USE_HALO = os.environ.get("DPA_NO_HALO", "0") != "1"
 # row-streaming conv3x3 (weights resident, 4-row LDS ring); DPA_NO_STREAM=1 disables
 USE_STREAM = os.environ.get("DPA_NO_STREAM", "0") != "1"
 USE_GLDS = os.environ.get("DPA_NO_GLDS", "0") != "1"
+HALO_CFG = int(os.environ.get("DPA_HALO_CFG", "0"))    # 0 = auto (csrc/halo.hip dpa_igemm_halo)
 # segmentation head + loss partials fused into the last decoder conv; DPA_NO_FUSED_HEAD=1 disables
 USE_FUSED_HEAD = os.environ.get("DPA_NO_FUSED_HEAD", "0") != "1"
 
@@ -189,7 +190,7 @@ def igemm(x: torch.Tensor, wpacked: torch.Tensor, y: torch.Tensor, *, Ngemm: int
             if L.dpa_igemm_glds(ctypes.byref(a), c_int(glds_var), st) == 0:
                 continue
         if path == "halo" or (path == "auto" and USE_HALO and conv3 and Cs % 32 == 0 and Ngemm <= 128):
-            err = L.dpa_igemm_halo(ctypes.byref(a), c_int(0), st)
+            err = L.dpa_igemm_halo(ctypes.byref(a), c_int(variant if path == "halo" else HALO_CFG), st)
             if err == 0:
                 continue
             if path == "halo":

@@ -476,3 +476,33 @@ def test_stream_conv_fused_head(hip_lib, N, H, W):
     torch.cuda.synchronize()
     assert torch.equal(y, y2)
     assert torch.allclose(S, S_ref, rtol=1e-4, atol=1e-2), (S, S_ref)
+
+
+@pytest.mark.parametrize("N,H,W,Cin,Cout,hcfg", [
+    (2, 5, 128, 64, 128, 4), (1, 4, 128, 128, 64, 4), (2, 3, 128, 32, 64, 5), (1, 7, 256, 256, 128, 4),
+    (2, 5, 128, 64, 128, 2)])
+def test_conv3x3_halo_two_rows(hip_lib, N, H, W, Cin, Cout, hcfg):
+    """Row-halo conv with two output rows per block (one weight staging per slice for both; odd
+    heights -> the last block's second row is masked): forward with bias+ReLU and masked dgrad."""
+    from distributedpytorch_amd.ops import kernels as K
+    torch.manual_seed(9)
+    x = _bf(F.relu(torch.randn(N, Cin, H, W)))
+    w = _bf(torch.randn(Cout, Cin, 3, 3) * (2.0 / (9 * Cin)) ** 0.5)
+    b = torch.randn(Cout) * 0.1
+    ref = F.relu(F.conv2d(x, w, b, padding=1))
+    packed, ng, kp = _pack_one(0, w)
+    y = torch.empty(N, H, W, Cout, dtype=torch.bfloat16, device="cuda")
+    K.igemm(_nhwc(x), packed, y, Ngemm=ng, Kpad=kp, KH=3, KW=3, stride=1, pad=1, Cs=Cin, out_grid=(N, H, W),
+            bias=b.cuda(), relu=True, path="halo", variant=hcfg)
+    g = _bf(torch.randn(N, Cout, H, W))
+    xr = x.clone().requires_grad_(True)
+    F.conv2d(xr, w, padding=1).backward(g)
+    packed_d, ngd, kpd = _pack_one(1, w)
+    dx = torch.empty(N, H, W, Cin, dtype=torch.bfloat16, device="cuda")
+    if Cin % 64 == 0 or hcfg == 5:
+        K.igemm(_nhwc(g), packed_d, dx, Ngemm=ngd, Kpad=kpd, KH=3, KW=3, stride=1, pad=1, Cs=Cout,
+                out_grid=(N, H, W), mask=_nhwc(x), path="halo", variant=hcfg)
+    torch.cuda.synchronize()
+    assert _rel(_nchw(y), ref) < 2e-2
+    if Cin % 64 == 0 or hcfg == 5:
+        assert _rel(_nchw(dx), xr.grad * (x > 0)) < 2e-2

@@ -84,3 +84,36 @@ def test_engine_image_chunking_invariant(hip_lib, monkeypatch):
     l1, g1 = run()
     assert abs(l0 - l1) < 1e-5 * abs(l0)
     assert torch.allclose(g0, g1, rtol=1e-3, atol=1e-6 * g0.abs().max().item())
+
+
+def test_hip_odd_size_center_crop_matches_reference(hip_lib):
+    """H, W not divisible by 16: the reference center-crops each skip (model/unet_parts.py:58-74) and
+    the output shrinks.  Probabilities, loss and every parameter gradient of the HIP
+    engine (cropped skips copied into fresh concat buffers, zero-padded crop gradient) match."""
+    from distributedpytorch_amd.compute import loss_from_partials, make_compute
+    from distributedpytorch_amd.loss import bce_dice_from_probs
+    from distributedpytorch_amd.models.unet import build_model
+    from distributedpytorch_amd.optim import FlatParameterSpace
+    torch.manual_seed(1)
+    ref = build_model("unet")
+    hip = build_model("unet")
+    hip.load_state_dict(ref.state_dict())
+    hip = hip.cuda()
+    FlatParameterSpace(hip)
+    comp = make_compute(hip, backend="hip", dtype="bf16")
+    x = torch.rand(2, 3, 50, 70)
+    t = (torch.rand(2, 1, 48, 64) > 0.6).float()
+    with torch.no_grad():
+        p = comp.probs(x.cuda()).cpu()
+    p_ref = ref(x)
+    assert p.shape == p_ref.shape == (2, 1, 48, 64)
+    assert (p - p_ref.detach()).abs().max().item() < 3e-2
+    loss_ref = bce_dice_from_probs(p_ref, t)
+    (2 * loss_ref).backward()
+    loss = loss_from_partials(comp.forward_partials(x.cuda(), t.cuda()), t.numel())
+    (2 * loss).backward()
+    torch.cuda.synchronize()
+    assert abs(loss.item() - loss_ref.item()) < 2e-2 * abs(loss_ref.item())
+    for (n, pr), (_, ph) in zip(ref.named_parameters(), hip.named_parameters()):
+        c = _cos(ph.grad.cpu(), pr.grad)
+        assert c > 0.98, f"{n}: cosine {c:.4f}"

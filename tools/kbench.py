@@ -38,6 +38,7 @@ def main():
     ap.add_argument("--no-wgrad", action="store_true")
     ap.add_argument("--svar", type=int, nargs="*", default=[], help="streaming-conv variants to time")
     ap.add_argument("--gvar", type=int, nargs="*", default=[], help="LDS-DMA (glds) kernel configs to time")
+    ap.add_argument("--hvar", type=int, nargs="*", default=[], help="row-halo kernel configs to time")
     ap.add_argument("--paths", default="stream,halo,generic", help="default paths to time")
     ap.add_argument("--layout-probe", action="store_true",
                     help="full-res memory-bound ops on concat halves (ld=2C) vs dense tensors (ld=C)")
@@ -63,7 +64,7 @@ def main():
         flops = 2.0 * B * H * H * Cin * Cout * 9
         variants = [(p, p, 0, 0) for p in a.paths.split(",") if p] + \
             [(f"gen.c{c}", "generic", c, 0) for c in a.cfgs] + [(f"strm.v{v}", "stream", 0, v) for v in a.svar] + \
-            [(f"glds.c{v}", "glds", 0, v) for v in a.gvar]
+            [(f"glds.c{v}", "glds", 0, v) for v in a.gvar] + [(f"halo.c{v}", "halo", 0, v) for v in a.hvar]
         for label, path, cfg, var in variants:
             try:
                 t = timeit(lambda: K.igemm(x, wf, y, Ngemm=Cout, Kpad=kf, KH=3, KW=3, stride=1, pad=1, Cs=Cin,
