@@ -41,6 +41,12 @@ def parse():
     ap.add_argument("--pool", type=int, default=2, help="distinct synthetic batches cycled")
     ap.add_argument("--out", default=None, help="also append the JSON line to this file")
     ap.add_argument("--graph", action="store_true", help="N=1: replay the step from a captured HIP graph")
+    ap.add_argument("--parallelism", choices=["dp", "mp"], default="dp",
+                    help="dp: one replica per GPU, RCCL all-reduce (weak scaling); mp: GPipe over the N ranks "
+                         "(one batch of --batch images split into --microbatches, strong scaling); with one "
+                         "process, mp runs --stages stages on cuda:0 (pipeline rehearsal)")
+    ap.add_argument("--microbatches", type=int, default=8)
+    ap.add_argument("--stages", type=int, default=2, help="mp with one process: stages on the local device")
     return ap.parse_args()
 
 
@@ -86,17 +92,24 @@ def main():
     from distributedpytorch_amd.config import TrainConfig
     from distributedpytorch_amd.data.synthetic import synthetic_batch
     from distributedpytorch_amd.models.unet import build_model, count_params
-    from distributedpytorch_amd.trainer import DDPStrategy, SingleDevice
+    from distributedpytorch_amd.trainer import DDPStrategy, PipelineDistStrategy, PipelineLocalStrategy, SingleDevice
     from distributedpytorch_amd.compute import resolve_backend
     from distributedpytorch_amd.utils import set_seed
 
     set_seed(1234)
-    cfg = TrainConfig(train_method="DDP" if world > 1 else "singleGPU", batch_size=a.batch,
-                      img_size=(a.img, a.img), dtype="bf16", backend=a.backend, model=a.model,
-                      bucket_mb=a.bucket_mb, lr=1e-4)
+    mp = a.parallelism == "mp"
+    method = "MP" if mp else ("DDP" if world > 1 else "singleGPU")
+    cfg = TrainConfig(train_method=method, batch_size=a.batch, img_size=(a.img, a.img), dtype="bf16",
+                      backend=a.backend, model=a.model, bucket_mb=a.bucket_mb, lr=1e-4,
+                      microbatches=a.microbatches, stages=a.stages)
     model = build_model(a.model)
     nparams = count_params(model)
-    strat = DDPStrategy(cfg, model, device) if world > 1 else SingleDevice(cfg, model, device)
+    if mp and world > 1:
+        strat = PipelineDistStrategy(cfg, model, device)
+    elif mp:
+        strat = PipelineLocalStrategy(cfg, model.to(device), [device] * a.stages)
+    else:
+        strat = DDPStrategy(cfg, model, device) if world > 1 else SingleDevice(cfg, model, device)
     backend = resolve_backend(a.backend, device)
 
     pool = []
@@ -105,7 +118,7 @@ def main():
         pool.append((img, mask.float().unsqueeze(1)))
 
     graphed = None
-    if a.graph and world == 1:
+    if a.graph and world == 1 and not mp:
         from distributedpytorch_amd.trainer import GraphedStep
         graphed = GraphedStep(strat, *pool[0])
 
@@ -139,23 +152,29 @@ def main():
     elapsed = float(el.item())
     final_loss = float(loss.item()) if loss is not None else float("nan")
 
-    imgs = a.batch * world * a.steps
+    # dp: every rank trains its own --batch images (weak scaling); mp: the N ranks share one batch
+    imgs = a.batch * (1 if mp else world) * a.steps
     value = imgs / elapsed
     ms = 1000.0 * elapsed / a.steps
     vs = None
     if STOCK_BASELINE_PER_GPU:
         vs = round(value / (STOCK_BASELINE_PER_GPU * world), 4)
+    if mp:
+        par = f"mp{world if world > 1 else a.stages}x{a.microbatches}mb" + ("" if world > 1 else "-1gpu")
+    else:
+        par = f"dp{world}"
     out = {
         "metric": BASELINE_METRIC, "value": round(value, 2), "unit": "images/s", "n_gpus": world,
         "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": vs, "dtype": "bf16",
+        "scaling": "strong" if mp else "weak", "vs_baseline": vs, "dtype": "bf16",
         "data": "synthetic (GPU-generated images + ellipse masks), random-init weights",
         "config": {"model": f"{a.model} (reference 4-level UNet, base 32, {nparams} params)" if a.model == "unet"
-                   else a.model, "global_batch": a.batch * world, "per_gpu_batch": a.batch,
+                   else a.model, "global_batch": a.batch * (1 if mp else world),
+                   "per_gpu_batch": a.batch if not mp else a.batch // max(1, world),
                    "seq_len": a.img * a.img, "image_hw": [a.img, a.img],
-                   "parallelism": f"dp{world}", "backend": backend, "bucket_mb": a.bucket_mb,
+                   "parallelism": par, "backend": backend, "bucket_mb": a.bucket_mb,
                    "hip_graph": graphed is not None},
-        "final_loss": round(final_loss, 5), "warmup_s": round(warm_s, 2),
+        "final_loss": round(final_loss, 5) if final_loss == final_loss else None, "warmup_s": round(warm_s, 2),
         "peak_mem_gb": round(torch.cuda.max_memory_allocated(device) / 2 ** 30, 2),
     }
     if rank == 0:

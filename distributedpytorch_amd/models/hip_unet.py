@@ -36,7 +36,8 @@ projection at the low resolution and up-samples into the concat half (``_Up``).
 from __future__ import annotations
 
 import ctypes
-from typing import Dict, List
+import weakref
+from typing import List
 
 import torch
 
@@ -113,7 +114,9 @@ class HipBlocks:
                 assert c.Cout % 32 == 0 and c.Cs % 8 == 0, "hip backend needs channel widths divisible by 32"
         self._build_packing()
         self._packed_version = None
-        self._cats: Dict[int, torch.Tensor] = {}
+        # concat buffers by the address of their first half; weak, so a buffer whose skip is consumed
+        # by another engine (pipeline stage boundary) is not kept alive by this map
+        self._cats: "weakref.WeakValueDictionary[int, torch.Tensor]" = weakref.WeakValueDictionary()
         self._target = None        # (target as given, fp32 flat copy) announced by run_segment
         self._head_cache = None    # (y ptr, target ptr, S) from the fused head epilogue
 

@@ -4,6 +4,8 @@ The pipeline splits the batch into microbatches and sums their loss partials on 
 (reference MP semantics, unet_model.py:24-53) and DP sums replica gradients (reference
 DataParallel); both must match a single-device step of the same batch with the same kernels.
 """
+import gc
+
 import pytest
 import torch
 
@@ -48,6 +50,20 @@ def test_pipeline_local_hip_matches_single(hip_lib):
     assert abs(loss.item() - l_ref.item()) < 1e-3 * abs(l_ref.item())
     for n, p in a.named_parameters():
         assert _cos(p.grad, g_ref[n]) > 0.999, n
+    # the encoder stage's concat buffers (consumed as copies by the decoder stage's engine) must not
+    # outlive the step: repeated steps keep allocated memory flat
+    del loss
+    gc.collect()
+    torch.cuda.synchronize()
+    base = torch.cuda.memory_allocated()
+    for _ in range(3):
+        for s in pipe.spaces:
+            s.zero_grad()
+        (pipe.forward_loss(x, t) * x.shape[0]).backward()
+    gc.collect()
+    torch.cuda.synchronize()
+    assert torch.cuda.memory_allocated() <= base + (1 << 20)
+    assert len(pipe.stage_blocks[0]._cats) == 0
 
 
 def test_dp_hip_matches_single(hip_lib):
