@@ -13,8 +13,10 @@ MI355X design (same semantics, less traffic):
   device produces the 4 partial loss sums of its shard, they are added on device 0 and the scalar
   loss is back-propagated through those tiny copies into every replica.
 * gradients are summed across devices with one single-process RCCL all-reduce over the flat
-  buffers (``torch.cuda.nccl.all_reduce``, i.e. ncclCommInitAll + grouped ncclAllReduce), each
-  device's slice riding its own xGMI links; fallback: ``torch.cuda.comm`` reduce+broadcast.
+  buffers: the native clique of :mod:`.dp_comm` (csrc/dp_comm.cpp: ncclCommInitAll once, then one
+  grouped ncclAllReduce per step on each device's compute stream), each device riding its own
+  xGMI links; fallbacks: ``torch.cuda.nccl.all_reduce``, then ``torch.cuda.comm`` reduce+broadcast.
+  The initial replicas are made identical with one grouped ncclBroadcast of the flat parameters.
 * per-device forward runs on one host thread per device (kernel launch cost overlaps).
 
 On CPU (tests) "devices" may repeat ``cpu``; the all-reduce is then a plain sum.
@@ -22,6 +24,7 @@ On CPU (tests) "devices" may repeat ``cpu``; the all-reduce is then a plain sum.
 from __future__ import annotations
 
 import copy
+import os
 import threading
 from typing import List, Sequence
 
@@ -44,6 +47,14 @@ class ReplicatedDataParallel:
         self.module = self.replicas[0]
         self._nccl = all(d.type == "cuda" for d in self.devices) and len(self.devices) > 1 and \
             len({d.index for d in self.devices}) == len(self.devices)
+        self.comm = None
+        if self._nccl and os.environ.get("DPA_DP_NATIVE_COMM", "1") == "1":
+            from . import dp_comm
+            if dp_comm.available():
+                self.comm = dp_comm.DPComm(self.devices)
+                self.comm.broadcast([s.data for s in self.spaces], root=0)
+                for s in self.spaces:
+                    s.version += 1
 
     # ------------------------------------------------------------------ forward
     def _parallel(self, fn, args_per_dev):
@@ -95,6 +106,9 @@ class ReplicatedDataParallel:
     def all_reduce_grads(self):
         grads = [s.grad for s in self.spaces]
         if len(grads) == 1:
+            return
+        if self.comm is not None:
+            self.comm.all_reduce(grads, "sum")
             return
         if self._nccl:
             try:

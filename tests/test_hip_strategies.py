@@ -152,3 +152,24 @@ def test_step_is_deterministic_and_debug_sync_invariant(hip_lib):
     for n in grads[0]:
         assert torch.equal(grads[0][n], grads[1][n]), n
         assert torch.equal(grads[0][n], grads[2][n]), n
+
+
+def test_native_dp_comm_single_device(hip_lib):
+    """csrc/dp_comm.cpp on the one device a test box has: a one-member clique (ncclCommInitAll) whose
+    grouped all-reduce (sum/avg) and broadcast are the identity, ordered on the current stream."""
+    from distributedpytorch_amd.parallel import dp_comm
+    assert dp_comm.available(), dp_comm.LIB_PATH
+    assert dp_comm.lib().dpa_dp_version() > 0
+    c = dp_comm.DPComm(["cuda:0"])
+    x = torch.randn(1 << 20, device="cuda")
+    ref = x.clone()
+    c.all_reduce([x], "sum")
+    c.all_reduce([x], "avg")
+    b = torch.randn(4096, device="cuda").to(torch.bfloat16)
+    bref = b.clone()
+    c.broadcast([b], root=0)
+    torch.cuda.synchronize()
+    assert torch.equal(x, ref) and torch.equal(b, bref)
+    with pytest.raises(AssertionError):
+        c.all_reduce([x.cpu()])
+    c.close()

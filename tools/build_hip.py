@@ -65,6 +65,7 @@ def build(force=False, verbose=False, jobs=None, flags=()):
     so = OUT / "libdpa_hip.so"
     newest = max(o.stat().st_mtime for o in objs)
     if so.exists() and so.stat().st_mtime >= newest and not force:
+        build_comm(force, verbose)
         return so
     tl = torch_lib_dir()
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(so), *map(str, objs),
@@ -74,6 +75,25 @@ def build(force=False, verbose=False, jobs=None, flags=()):
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed:\n{r.stderr[-4000:]}")
+    build_comm(force, verbose)
+    return so
+
+
+def build_comm(force=False, verbose=False) -> Path:
+    """Host-only RCCL communicator library (csrc/dp_comm.cpp -> _C/libdpa_comm.so) for ``-t DP``.
+    Linked against torch's bundled librccl.so (SONAME librccl.so.1), the copy torch itself loads."""
+    src = CSRC / "dp_comm.cpp"
+    so = OUT / "libdpa_comm.so"
+    if so.exists() and so.stat().st_mtime >= src.stat().st_mtime and not force:
+        return so
+    tl = torch_lib_dir()
+    cmd = [hipcc(), "-O2", "-fPIC", "-std=c++17", "-shared", str(src), "-o", str(so), "-I/opt/rocm/include",
+           f"-L{tl}", "-l:librccl.so", "-lamdhip64", f"-Wl,-rpath,{tl}", "-Wl,--enable-new-dtags"]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed for dp_comm.cpp:\n{r.stderr[-4000:]}")
     return so
 
 
