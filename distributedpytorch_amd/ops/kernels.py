@@ -183,12 +183,10 @@ def igemm(x: torch.Tensor, wpacked: torch.Tensor, y: torch.Tensor, *, Ngemm: int
                 _check(err, "igemm_stream")
         pool_done = False
         glds_ok = USE_GLDS and cfg == 0 and Cs % 64 == 0 and Kpad % 64 == 0 and Ngemm % 128 == 0
-        # measured (tools/kbench.py, profiles/kbench_b32_512.txt): the LDS-DMA kernel beats the row-halo
-        # kernel on the 128-output-channel dgrads, the halo kernel wins the 128-channel forwards
-        glds_var = 0 if path == "glds" else (2 if Cs >= 128 else 6)
-        if path == "auto" and glds_ok and mask is not None and Ngemm == 128:
-            if L.dpa_igemm_glds(ctypes.byref(a), c_int(glds_var), st) == 0:
-                continue
+        # measured at batch 128 (tools/kbench.py, profiles/kbench_b128_512.txt): the two-row halo kernel
+        # beats the LDS-DMA kernel on every shape both accept (128-channel dgrads: 837 vs 1042 us at
+        # 128^2, 2542 vs 2948 us at 256^2); the LDS-DMA kernel takes what the halo kernel cannot
+        # (64^2 and smaller grids, > 128 output channels)
         if path == "halo" or (path == "auto" and USE_HALO and conv3 and Cs % 32 == 0 and Ngemm <= 128):
             err = L.dpa_igemm_halo(ctypes.byref(a), c_int(variant if path == "halo" else HALO_CFG), st)
             if err == 0:
