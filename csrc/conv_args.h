@@ -25,6 +25,9 @@ struct IgemmArgs {
   // optional fused segmentation head (streaming kernel, last decoder conv, Ngemm == 32): per pixel
   // z = hb + sum_c y[c] hw[c], p = sigmoid(z), BCE/Dice partial sums vs tgt -> hslab[block][4]
   const float* hw; const float* hb; const float* tgt; float* hslab;
+  // optional BatchNorm batch statistics of the stored (bf16) output (streaming kernel, conv followed
+  // by BN): per block, per channel sum and sum of squares -> bnslab[block][2][Ngemm] (bn_finalize)
+  float* bnslab;
 };
 
 // 2x2 window code from the four (bf16-rounded) values in window order tl, tr, bl, br: first

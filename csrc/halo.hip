@@ -488,6 +488,16 @@ __global__ __launch_bounds__(256 * WCS) void igemm_stream_kernel(IgemmArgs a) {
       for (int e = 0; e < 4; ++e) hwv[ic][e] = a.hw[wc * WCN + ic * 16 + 4 * chunk + e];
   }
 
+  // fused BatchNorm statistics (EPI 4): per-lane running sums of this lane's 4*TC channels
+  constexpr bool do_bn = EPI == 4;
+  float bsum[do_bn ? TC : 1][4], bsq[do_bn ? TC : 1][4];
+  if constexpr (do_bn) {
+#pragma unroll
+    for (int ic = 0; ic < TC; ++ic)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) bsum[ic][e] = bsq[ic][e] = 0.f;
+  }
+
   // prologue: input rows h0-1, h0, h0+1 -> slots 0, 1, 2
 #pragma unroll 1
   for (int j = 0; j < 3; ++j) {
@@ -570,6 +580,14 @@ __global__ __launch_bounds__(256 * WCS) void igemm_stream_kernel(IgemmArgs a) {
                       packed);
         else
           __builtin_amdgcn_raw_buffer_store_b64(packed, yr, yo, 0, 0);
+        if constexpr (do_bn) {     // statistics of the STORED bf16 values, like a separate pass
+          const float q[4] = {lo_bf(packed.x), hi_bf(packed.x), lo_bf(packed.y), hi_bf(packed.y)};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            bsum[ic][e] += q[e];
+            bsq[ic][e] = fmaf(q[e], q[e], bsq[ic][e]);
+          }
+        }
         if constexpr (do_head) {   // the head sees the STORED bf16 values, like a separate pass would
           hdot = fmaf(lo_bf(packed.x), hwv[ic][0], hdot);
           hdot = fmaf(hi_bf(packed.x), hwv[ic][1], hdot);
@@ -628,6 +646,30 @@ __global__ __launch_bounds__(256 * WCS) void igemm_stream_kernel(IgemmArgs a) {
     __builtin_amdgcn_sched_barrier(0);
     if (r + 1 < nrows) rstore((r + 3) & 3);
     __syncthreads();
+  }
+  if constexpr (do_bn) {
+    // lanes l and l^1..l^15 hold the same channels (different pixels): butterfly over the 16, then
+    // the 4 pixel waves in a fixed order -> one deterministic slab row per block
+    __shared__ float bred[4][2 * NG];
+#pragma unroll
+    for (int ic = 0; ic < TC; ++ic)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float s = bsum[ic][e], q = bsq[ic][e];
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          s += __shfl_xor(s, o, 64);
+          q += __shfl_xor(q, o, 64);
+        }
+        if ((lane & 15) == 0) {
+          const int c = wc * WCN + ic * 16 + 4 * chunk + e;
+          bred[wp][c] = s;
+          bred[wp][NG + c] = q;
+        }
+      }
+    __syncthreads();
+    for (int k = tid; k < 2 * NG; k += NT)
+      a.bnslab[(long)blockIdx.x * 2 * NG + k] = (bred[0][k] + bred[1][k]) + (bred[2][k] + bred[3][k]);
   }
   if constexpr (do_head) {
     static_assert(!do_head || NT == 256, "head epilogue reduces over 256 threads");
@@ -770,6 +812,11 @@ static int launch_igemm_stream(const IgemmArgs& a, hipStream_t st) {
       return (int)hipGetLastError();
     }
     return (int)hipErrorInvalidValue;
+  }
+  if (a.bnslab) { // conv followed by BatchNorm: batch-statistics partials in the epilogue
+    if (a.y2 || a.mask || a.accumulate) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL((igemm_stream_kernel<BP, NG, CS, RH, WCS, 4>), dim3(grid), dim3(256 * WCS), 0, st, a);
+    return (int)hipGetLastError();
   }
   if (a.y2) {     // decoder conv1 dgrad over the concat (NG = 2 CS): skip / up gradients as dense tensors
     if constexpr (NG == 2 * CS) {

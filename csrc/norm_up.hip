@@ -220,15 +220,17 @@ DPA_API int dpa_bn_slab_rows(long long P, int C) {
 // eval forward (train == 0): coef from the running statistics.  Then y = relu?(bn(z)).
 DPA_API int dpa_bn_fwd(const bf16_t* z, int ldz, bf16_t* y, int ldy, long long P, int C, const float* gamma, const float* beta,
                        float eps, float momentum, float* rmean, float* rvar, float* slab, float* coef, float* saved, int train,
-                       int relu, hipStream_t st) {
+                       int relu, int slab_rows, hipStream_t st) {
   int G;
   dim3 grid;
   if (!bn_shape(P, C, G, grid) || (ldz & 7) || (ldy & 7)) return (int)hipErrorInvalidValue;
   if (train) {
-    hipLaunchKernelGGL(bn_partial_kernel<0>, grid, dim3(256), 0, st, z, ldz, (const bf16_t*)nullptr, 0, (const float*)nullptr,
-                       (long)P, C, G, slab);
-    hipLaunchKernelGGL(bn_finalize_kernel, dim3(C), dim3(256), 0, st, slab, (int)grid.x, C, (long)P, gamma, beta, eps, momentum,
-                       rmean, rvar, coef, saved);
+    // slab_rows > 0: the producing conv already wrote the partial sums (igemm_stream EPI 4)
+    if (slab_rows <= 0)
+      hipLaunchKernelGGL(bn_partial_kernel<0>, grid, dim3(256), 0, st, z, ldz, (const bf16_t*)nullptr, 0,
+                         (const float*)nullptr, (long)P, C, G, slab);
+    hipLaunchKernelGGL(bn_finalize_kernel, dim3(C), dim3(256), 0, st, slab, slab_rows > 0 ? slab_rows : (int)grid.x, C,
+                       (long)P, gamma, beta, eps, momentum, rmean, rvar, coef, saved);
   } else {
     hipLaunchKernelGGL(bn_finalize_kernel, dim3(C), dim3(256), 0, st, (const float*)nullptr, 0, C, (long)P, gamma, beta, eps,
                        momentum, rmean, rvar, coef, saved);

@@ -192,9 +192,10 @@ class HipBlocks:
                     out_grid=(N, H, W), bias=c.mod.bias, relu=True, pool=pool, pcode=pcode)
             return y
         z = torch.empty(N, H, W, c.Cout, dtype=torch.bfloat16, device=x.device)
+        stats = [] if self.model.training else None    # batch statistics from the conv epilogue
         K.igemm(x, self.wf(c), z, Ngemm=c.Cout, Kpad=c.Kf, KH=3, KW=3, stride=1, pad=1, Cs=c.Cs, out_grid=(N, H, W),
-                bias=c.mod.bias, relu=False)
-        saved = K.bn_fwd(z, y, c.bn, train=self.model.training)
+                bias=c.mod.bias, relu=False, bn_stats=stats)
+        saved = K.bn_fwd(z, y, c.bn, train=self.model.training, stats=stats)
         if pool is not None:
             K.maxpool2(y, pool, pcode)
         if st is not None:

@@ -30,7 +30,7 @@ class IgemmArgs(ctypes.Structure):
                                      "stride", "pad", "Ngemm", "Kpad", "mode", "relu", "accumulate", "Cout")] + \
                [("xbytes", ctypes.c_uint), ("pool", c_void_p), ("ldp", c_int), ("pcode", c_void_p), ("y2", c_void_p),
                 ("ldy2", c_int), ("split", c_int), ("hw", c_void_p), ("hb", c_void_p), ("tgt", c_void_p),
-                ("hslab", c_void_p)]
+                ("hslab", c_void_p), ("bnslab", c_void_p)]
 
 
 class WgradArgs(ctypes.Structure):
@@ -81,6 +81,8 @@ USE_GLDS = os.environ.get("DPA_NO_GLDS", "0") != "1"
 HALO_CFG = int(os.environ.get("DPA_HALO_CFG", "0"))    # 0 = auto (csrc/halo.hip dpa_igemm_halo)
 # segmentation head + loss partials fused into the last decoder conv; DPA_NO_FUSED_HEAD=1 disables
 USE_FUSED_HEAD = os.environ.get("DPA_NO_FUSED_HEAD", "0") != "1"
+# BatchNorm batch statistics in the producing streaming conv's epilogue; DPA_NO_FUSED_BN=1 disables
+USE_FUSED_BN = os.environ.get("DPA_NO_FUSED_BN", "0") != "1"
 
 
 def _extent_bytes(N, H, W, C, ld):
@@ -98,7 +100,8 @@ def igemm(x: torch.Tensor, wpacked: torch.Tensor, y: torch.Tensor, *, Ngemm: int
           stride: int, pad: int, Cs: int, out_grid, bias: Optional[torch.Tensor] = None, relu: bool = False,
           mask: Optional[torch.Tensor] = None, mode: int = 0, Cout: int = 0, accumulate: bool = False, cfg: int = 0,
           path: str = "auto", pool: Optional[torch.Tensor] = None, variant: int = 0,
-          pcode: Optional[torch.Tensor] = None, y2: Optional[torch.Tensor] = None, split: int = 0, head=None):
+          pcode: Optional[torch.Tensor] = None, y2: Optional[torch.Tensor] = None, split: int = 0, head=None,
+          bn_stats: Optional[list] = None):
     """Implicit-GEMM conv.  ``out_grid`` = (N, Ho, Wo) pixel grid of GEMM-M.
 
     ``path``: ``auto`` picks, for a conv3x3, the row-streaming kernel (Ngemm, Cs in {32, 64}), then the
@@ -110,7 +113,10 @@ def igemm(x: torch.Tensor, wpacked: torch.Tensor, y: torch.Tensor, *, Ngemm: int
     :func:`pool_bwd_code` consumes.  ``y2``/``split``: output channels >= ``split`` go to the dense
     tensor ``y2`` (channel ``co - split``) -- the two halves of a concat gradient.  ``head`` =
     (segmap weight, segmap bias, target [N*Ho*Wo] fp32): the streaming kernel also computes the fused
-    segmap + sigmoid + BCE/Dice partial sums of its (bf16) output; returns them as S[4]."""
+    segmap + sigmoid + BCE/Dice partial sums of its (bf16) output; returns them as S[4].
+    ``bn_stats`` (an empty list; conv followed by BatchNorm): when the streaming kernel runs, its
+    epilogue also writes the per-block channel sums / sums of squares of the stored output and the
+    list receives (slab [rows][2][Ngemm] fp32, rows) for :func:`bn_fwd`; left empty otherwise."""
     N, Hs, Ws, Cx, ldx = _nhwc(x, "igemm.x")
     _, _, _, Cy, ldy = _nhwc(y, "igemm.y")
     No, Ho, Wo = out_grid
@@ -146,6 +152,10 @@ def igemm(x: torch.Tensor, wpacked: torch.Tensor, y: torch.Tensor, *, Ngemm: int
     st = _stream(y)
     pool_done = True
     hslab, hrows = None, 0
+    bslab, brows = None, 0
+    if bn_stats is not None and USE_FUSED_BN and mode == 0 and pool is None and y2 is None and mask is None \
+            and head is None and not accumulate and path == "auto":
+        bslab = torch.empty(N * -(-Ho // 16) * max(1, Wo // 64) * 2 * Ngemm, dtype=torch.float32, device=y.device)
     if head is not None:
         hw, hb, tgt = head
         assert mode == 0 and Ngemm == 32 and Cs == 32 and pool is None and y2 is None and mask is None
@@ -171,6 +181,15 @@ def igemm(x: torch.Tensor, wpacked: torch.Tensor, y: torch.Tensor, *, Ngemm: int
             _check(L.dpa_igemm_stream(ctypes.byref(a), c_int(0), st), "igemm_stream+head")
             hrows += rows
             continue
+        if bslab is not None and conv3 and stream_ok and USE_STREAM and Cs != 8:
+            rows = L.dpa_igemm_stream_blocks(ctypes.byref(a))
+            if rows > 0:
+                a.bnslab = bslab[brows * 2 * Ngemm:].data_ptr()
+                if L.dpa_igemm_stream(ctypes.byref(a), c_int(0), st) == 0:
+                    brows += rows
+                    continue
+                a.bnslab = None
+            bslab = None   # not fusable for this chunk: the BN pass computes the statistics
         if path == "stream" or (path == "auto" and USE_STREAM and conv3 and stream_ok):
             if pool is not None:
                 a.pool, a.ldp = pool[n0:n1].data_ptr(), ldp
@@ -202,6 +221,8 @@ def igemm(x: torch.Tensor, wpacked: torch.Tensor, y: torch.Tensor, *, Ngemm: int
         _check(L.dpa_igemm(ctypes.byref(a), c_int(cfg), st), "igemm")
     if pool is not None and not pool_done:
         maxpool2(y, pool, pcode)
+    if bslab is not None and brows > 0:
+        bn_stats.extend([bslab, brows])
     if head is not None:
         S = hslab[hslab.numel() - 4:]
         _check(L.dpa_slab_sum(_p(hslab), c_int(hrows), c_int(4), _p(S), st), "slab_sum")
@@ -464,10 +485,12 @@ def _flat_f32(t: torch.Tensor, n: int, name: str):
     return t
 
 
-def bn_fwd(z: torch.Tensor, y: torch.Tensor, bn: torch.nn.BatchNorm2d, train: bool, relu: bool = True):
+def bn_fwd(z: torch.Tensor, y: torch.Tensor, bn: torch.nn.BatchNorm2d, train: bool, relu: bool = True,
+           stats: Optional[list] = None):
     """y = relu(BatchNorm2d(z)) (NHWC bf16; y may be a concat half).  Training: batch statistics,
     running stats updated (torch momentum semantics); returns ``saved`` = [mean, invstd] (fp32 [2C])
-    for :func:`bn_bwd`.  Eval: running statistics, returns None."""
+    for :func:`bn_bwd`.  Eval: running statistics, returns None.  ``stats`` = (slab, rows) partial
+    sums the producing conv already computed (:func:`igemm` ``bn_stats``): no statistics pass."""
     N, H, W, C, ldz = _nhwc(z, "bn.z")
     Ny, Hy, Wy, Cy, ldy = _nhwc(y, "bn.y")
     assert (Ny, Hy, Wy, Cy) == (N, H, W, C) and bn.num_features == C and bn.affine
@@ -490,9 +513,14 @@ def bn_fwd(z: torch.Tensor, y: torch.Tensor, bn: torch.nn.BatchNorm2d, train: bo
     else:   # cumulative moving average (torch: momentum = 1 / num_batches_tracked)
         mom = 1.0 / max(1, int(bn.num_batches_tracked.item())) if track else 0.0
     # running stats: updated when training, read in eval (use_batch False), untouched otherwise
+    pre_rows = 0
+    if stats and use_batch:
+        slab, pre_rows = stats
+        assert slab.numel() >= pre_rows * 2 * C
     _check(L.dpa_bn_fwd(_p(z), c_int(ldz), _p(y), c_int(ldy), c_ll(P), c_int(C), _p(gamma), _p(beta),
                         ctypes.c_float(bn.eps), ctypes.c_float(mom), _p(rm), _p(rv), _p(slab) if use_batch else None,
-                        _p(coef), _p(saved), c_int(int(use_batch)), c_int(int(relu)), _stream(z)), "bn_fwd")
+                        _p(coef), _p(saved), c_int(int(use_batch)), c_int(int(relu)), c_int(pre_rows), _stream(z)),
+           "bn_fwd")
     return saved if use_batch else None
 
 

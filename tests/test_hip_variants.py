@@ -204,3 +204,46 @@ def test_hip_unet_variants_match_torch_fp32(hip_lib, variant):
         p_ref = ref(img)
         p = comp.probs(img.cuda()).cpu()
     assert (p - p_ref).abs().max().item() < 5e-2
+
+
+@pytest.mark.parametrize("N,H,W,Cin,Cout", [(2, 5, 128, 32, 32), (1, 7, 64, 64, 32), (2, 6, 128, 32, 64),
+                                            (1, 33, 64, 64, 64)])
+def test_conv_bn_stats_fused_in_stream_epilogue(hip_lib, N, H, W, Cin, Cout):
+    """Conv followed by BatchNorm on the streaming kernel: the batch statistics come from the conv's
+    epilogue (per-block channel sums of the stored bf16 output) instead of a separate pass.  Output,
+    saved mean/invstd and running statistics equal the unfused path and match torch fp32."""
+    from distributedpytorch_amd.ops import kernels as K
+    torch.manual_seed(3)
+    x = _bf(torch.randn(N, Cin, H, W))
+    w = _bf(torch.randn(Cout, Cin, 3, 3) * (2.0 / (9 * Cin)) ** 0.5)
+    b = torch.randn(Cout) * 0.1
+    bn_ref = torch.nn.BatchNorm2d(Cout)
+    with torch.no_grad():
+        bn_ref.weight.uniform_(0.5, 1.5)
+        bn_ref.bias.uniform_(-0.5, 0.5)
+    kf = K.round_up(9 * Cin, 32)
+    packed = torch.zeros(Cout, kf)
+    packed[:, :9 * Cin] = w.permute(0, 2, 3, 1).reshape(Cout, 9 * Cin)
+    packed = packed.to(torch.bfloat16).cuda().reshape(-1)
+    xh = x.permute(0, 2, 3, 1).contiguous().to(torch.bfloat16).cuda()
+    outs = []
+    for fused in (True, False):
+        bn = torch.nn.BatchNorm2d(Cout).cuda()
+        bn.load_state_dict(bn_ref.state_dict())
+        z = torch.empty(N, H, W, Cout, dtype=torch.bfloat16, device="cuda")
+        stats = [] if fused else None
+        K.igemm(xh, packed, z, Ngemm=Cout, Kpad=kf, KH=3, KW=3, stride=1, pad=1, Cs=Cin, out_grid=(N, H, W),
+                bias=b.cuda(), relu=False, bn_stats=stats)
+        if fused:
+            assert len(stats) == 2 and stats[1] > 0, "streaming epilogue did not produce the statistics"
+        y = torch.empty_like(z)
+        saved = K.bn_fwd(z, y, bn, train=True, stats=stats)
+        torch.cuda.synchronize()
+        outs.append((y.float().cpu(), saved.cpu(), bn.running_mean.cpu(), bn.running_var.cpu()))
+    (y1, s1, m1, v1), (y0, s0, m0, v0) = outs
+    # the sums are taken in a different order: at most a bf16 rounding flip apart
+    assert _rel(y1, y0) < 1e-2
+    assert torch.allclose(s1, s0, rtol=1e-5, atol=1e-6) and torch.allclose(m1, m0, rtol=1e-5, atol=1e-6)
+    assert torch.allclose(v1, v0, rtol=1e-5, atol=1e-6)
+    y_ref = F.relu(bn_ref(F.conv2d(x, w, b, padding=1))).permute(0, 2, 3, 1)
+    assert _rel(y1, y_ref) < 3e-2
