@@ -15,6 +15,8 @@
 // one block per channel.  The same pair computes the backward sums (sum g, sum g*(z-mean)).
 #include "common.h"
 
+#include "conv_args.h"   // pool_code
+
 // ------------------------------------------------------------------------------ batch statistics
 // MODE 0: s = sum z, q = sum z^2          (a = z)
 // MODE 1: s = sum g, q = sum g*(z - mean)  (a = g, z = conv output, mean = saved[c])
@@ -171,6 +173,62 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const bf16_t* __restrict_
   }
 }
 
+// Encoder DoubleConv output: y = relu(bn(z)) AND its 2x2/s2 max-pool + window codes in one pass
+// (even H, W).  One thread per (window, 8 channels): reads the 4 z pixels once, writes the 4 y
+// pixels, the pooled pixel and the codes the pool backward consumes -- the separate max-pool pass
+// would re-read all of y.  Pools the STORED (bf16-rounded) y, like maxpool2_kernel.
+__global__ __launch_bounds__(256) void bn_apply_pool_kernel(const bf16_t* __restrict__ z, int ldz, bf16_t* __restrict__ y,
+                                                            int ldy, bf16_t* __restrict__ pool, int ldp,
+                                                            unsigned char* __restrict__ code, const float* __restrict__ coef,
+                                                            int N, int H, int W, int C, int relu) {
+  const int Ho = H >> 1, Wo = W >> 1, CC = C >> 3;
+  const long tot = (long)N * Ho * Wo * CC;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < tot; i += (long)gridDim.x * blockDim.x) {
+    const int cc = (int)(i % CC);
+    const long op = i / CC;
+    const int ow = (int)(op % Wo);
+    const long t = op / Wo;
+    const int oh = (int)(t % Ho);
+    const int n = (int)(t / Ho);
+    const int c0 = cc * 8;
+    const long p00 = ((long)(n * H + 2 * oh) * W + 2 * ow);
+    const long pix[4] = {p00, p00 + 1, p00 + W, p00 + W + 1};
+    float v[4][8];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint4 u = *reinterpret_cast<const uint4*>(z + pix[q] * ldz + c0);
+      const unsigned* pu = &u.x;
+      unsigned o[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float v0 = fmaf(lo_bf(pu[e]), coef[c0 + 2 * e], coef[C + c0 + 2 * e]);
+        float v1 = fmaf(hi_bf(pu[e]), coef[c0 + 2 * e + 1], coef[C + c0 + 2 * e + 1]);
+        if (relu) {
+          v0 = fmaxf(v0, 0.f);
+          v1 = fmaxf(v1, 0.f);
+        }
+        o[e] = pack_bf2(v0, v1);
+        v[q][2 * e] = lo_bf(o[e]);
+        v[q][2 * e + 1] = hi_bf(o[e]);
+      }
+      *reinterpret_cast<uint4*>(y + pix[q] * ldy + c0) = make_uint4(o[0], o[1], o[2], o[3]);
+    }
+    unsigned o[4], cd[2] = {0u, 0u};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int a = 2 * k, b = 2 * k + 1;
+      const float l = fmaxf(fmaxf(v[0][a], v[1][a]), fmaxf(v[2][a], v[3][a]));
+      const float h = fmaxf(fmaxf(v[0][b], v[1][b]), fmaxf(v[2][b], v[3][b]));
+      o[k] = pack_bf2(l, h);
+      const unsigned cl = pool_code(v[0][a], v[1][a], v[2][a], v[3][a]);
+      const unsigned ch = pool_code(v[0][b], v[1][b], v[2][b], v[3][b]);
+      cd[k >> 1] |= (cl | ch << 8) << (16 * (k & 1));
+    }
+    *reinterpret_cast<uint4*>(pool + op * ldp + c0) = make_uint4(o[0], o[1], o[2], o[3]);
+    if (code) *reinterpret_cast<uint2*>(code + op * C + c0) = make_uint2(cd[0], cd[1]);
+  }
+}
+
 // dz = coef3[c]*g + coef3[C+c]*z + coef3[2C+c]
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const bf16_t* __restrict__ g, int ldg, const bf16_t* __restrict__ z,
                                                            int ldz, const float* __restrict__ coef3, bf16_t* __restrict__ dz,
@@ -220,10 +278,12 @@ DPA_API int dpa_bn_slab_rows(long long P, int C) {
 // eval forward (train == 0): coef from the running statistics.  Then y = relu?(bn(z)).
 DPA_API int dpa_bn_fwd(const bf16_t* z, int ldz, bf16_t* y, int ldy, long long P, int C, const float* gamma, const float* beta,
                        float eps, float momentum, float* rmean, float* rvar, float* slab, float* coef, float* saved, int train,
-                       int relu, int slab_rows, hipStream_t st) {
+                       int relu, int slab_rows, bf16_t* pool, int ldp, unsigned char* code, int N, int H, int W,
+                       hipStream_t st) {
   int G;
   dim3 grid;
   if (!bn_shape(P, C, G, grid) || (ldz & 7) || (ldy & 7)) return (int)hipErrorInvalidValue;
+  if (pool && ((ldp & 7) || (H & 1) || (W & 1) || (long)N * H * W != (long)P)) return (int)hipErrorInvalidValue;
   if (train) {
     // slab_rows > 0: the producing conv already wrote the partial sums (igemm_stream EPI 4)
     if (slab_rows <= 0)
@@ -234,6 +294,12 @@ DPA_API int dpa_bn_fwd(const bf16_t* z, int ldz, bf16_t* y, int ldy, long long P
   } else {
     hipLaunchKernelGGL(bn_finalize_kernel, dim3(C), dim3(256), 0, st, (const float*)nullptr, 0, C, (long)P, gamma, beta, eps,
                        momentum, rmean, rvar, coef, saved);
+  }
+  if (pool) {
+    const long tot = (long)P / 4 * (C / 8);
+    hipLaunchKernelGGL(bn_apply_pool_kernel, dim3(dpa_grid(tot, 256, 16384)), dim3(256), 0, st, z, ldz, y, ldy, pool, ldp,
+                       code, coef, N, H, W, C, relu);
+    return (int)hipGetLastError();
   }
   const long tot = (long)P * (C / 8);
   hipLaunchKernelGGL(bn_apply_kernel, dim3(dpa_grid(tot, 256, 16384)), dim3(256), 0, st, z, ldz, y, ldy, coef, (long)P, C, relu);

@@ -195,9 +195,7 @@ class HipBlocks:
         stats = [] if self.model.training else None    # batch statistics from the conv epilogue
         K.igemm(x, self.wf(c), z, Ngemm=c.Cout, Kpad=c.Kf, KH=3, KW=3, stride=1, pad=1, Cs=c.Cs, out_grid=(N, H, W),
                 bias=c.mod.bias, relu=False, bn_stats=stats)
-        saved = K.bn_fwd(z, y, c.bn, train=self.model.training, stats=stats)
-        if pool is not None:
-            K.maxpool2(y, pool, pcode)
+        saved = K.bn_fwd(z, y, c.bn, train=self.model.training, stats=stats, pool=pool, pcode=pcode)
         if st is not None:
             st.append((z, saved))
         return y

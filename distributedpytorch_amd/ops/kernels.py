@@ -486,11 +486,13 @@ def _flat_f32(t: torch.Tensor, n: int, name: str):
 
 
 def bn_fwd(z: torch.Tensor, y: torch.Tensor, bn: torch.nn.BatchNorm2d, train: bool, relu: bool = True,
-           stats: Optional[list] = None):
+           stats: Optional[list] = None, pool: Optional[torch.Tensor] = None, pcode: Optional[torch.Tensor] = None):
     """y = relu(BatchNorm2d(z)) (NHWC bf16; y may be a concat half).  Training: batch statistics,
     running stats updated (torch momentum semantics); returns ``saved`` = [mean, invstd] (fp32 [2C])
     for :func:`bn_bwd`.  Eval: running statistics, returns None.  ``stats`` = (slab, rows) partial
-    sums the producing conv already computed (:func:`igemm` ``bn_stats``): no statistics pass."""
+    sums the producing conv already computed (:func:`igemm` ``bn_stats``): no statistics pass.
+    ``pool``/``pcode``: also the 2x2 max-pool of y and its window codes, in the same pass (even H, W;
+    otherwise a separate :func:`maxpool2`)."""
     N, H, W, C, ldz = _nhwc(z, "bn.z")
     Ny, Hy, Wy, Cy, ldy = _nhwc(y, "bn.y")
     assert (Ny, Hy, Wy, Cy) == (N, H, W, C) and bn.num_features == C and bn.affine
@@ -517,10 +519,20 @@ def bn_fwd(z: torch.Tensor, y: torch.Tensor, bn: torch.nn.BatchNorm2d, train: bo
     if stats and use_batch:
         slab, pre_rows = stats
         assert slab.numel() >= pre_rows * 2 * C
+    fuse_pool = pool is not None and H % 2 == 0 and W % 2 == 0
+    ldp = 0
+    if fuse_pool:
+        Np, Hp, Wp, Cp, ldp = _nhwc(pool, "bn.pool")
+        assert (Np, Hp, Wp, Cp) == (N, H // 2, W // 2, C)
+        if pcode is not None:
+            assert pcode.dtype == torch.uint8 and pcode.is_contiguous() and tuple(pcode.shape) == (N, H // 2, W // 2, C)
     _check(L.dpa_bn_fwd(_p(z), c_int(ldz), _p(y), c_int(ldy), c_ll(P), c_int(C), _p(gamma), _p(beta),
                         ctypes.c_float(bn.eps), ctypes.c_float(mom), _p(rm), _p(rv), _p(slab) if use_batch else None,
-                        _p(coef), _p(saved), c_int(int(use_batch)), c_int(int(relu)), c_int(pre_rows), _stream(z)),
-           "bn_fwd")
+                        _p(coef), _p(saved), c_int(int(use_batch)), c_int(int(relu)), c_int(pre_rows),
+                        _p(pool) if fuse_pool else None, c_int(ldp), _p(pcode) if fuse_pool else None,
+                        c_int(N), c_int(H), c_int(W), _stream(z)), "bn_fwd")
+    if pool is not None and not fuse_pool:
+        maxpool2(y, pool, pcode)
     return saved if use_batch else None
 
 

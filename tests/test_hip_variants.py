@@ -247,3 +247,32 @@ def test_conv_bn_stats_fused_in_stream_epilogue(hip_lib, N, H, W, Cin, Cout):
     assert torch.allclose(v1, v0, rtol=1e-5, atol=1e-6)
     y_ref = F.relu(bn_ref(F.conv2d(x, w, b, padding=1))).permute(0, 2, 3, 1)
     assert _rel(y1, y_ref) < 3e-2
+
+
+@pytest.mark.parametrize("N,H,W,C", [(2, 6, 10, 32), (1, 16, 16, 64), (2, 5, 8, 32)])
+def test_bn_apply_fused_maxpool(hip_lib, N, H, W, C):
+    """BN+ReLU and the encoder's 2x2 max-pool (+ window codes) in one pass == BN pass then max-pool
+    pass, bitwise (odd H falls back to the separate pool)."""
+    from distributedpytorch_amd.ops import kernels as K
+    torch.manual_seed(4)
+    z = (torch.randn(N, H, W, C) * 2).to(torch.bfloat16).cuda()
+    res = []
+    for fused in (True, False):
+        bn = torch.nn.BatchNorm2d(C).cuda()
+        with torch.no_grad():
+            bn.weight.copy_(torch.linspace(0.5, 1.5, C))
+            bn.bias.copy_(torch.linspace(-0.5, 0.5, C))
+        y = torch.empty_like(z)
+        pool = torch.empty(N, H // 2, W // 2, C, dtype=torch.bfloat16, device="cuda")
+        code = torch.empty(N, H // 2, W // 2, C, dtype=torch.uint8, device="cuda")
+        if fused:
+            K.bn_fwd(z, y, bn, train=True, pool=pool, pcode=code)
+        else:
+            K.bn_fwd(z, y, bn, train=True)
+            K.maxpool2(y, pool, code)
+        torch.cuda.synchronize()
+        res.append((y.cpu(), pool.cpu(), code.cpu()))
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
+    ref = F.max_pool2d(res[0][0].float().permute(0, 3, 1, 2), 2).permute(0, 2, 3, 1)
+    assert torch.equal(res[0][1].float(), ref)
