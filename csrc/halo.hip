@@ -488,8 +488,11 @@ __global__ __launch_bounds__(256 * WCS) void igemm_stream_kernel(IgemmArgs a) {
       for (int e = 0; e < 4; ++e) hwv[ic][e] = a.hw[wc * WCN + ic * 16 + 4 * chunk + e];
   }
 
-  // fused BatchNorm statistics (EPI 4): per-lane running sums of this lane's 4*TC channels
-  constexpr bool do_bn = EPI == 4;
+  // fused BatchNorm statistics: EPI 4 (forward, conv -> BN) sum z, sum z^2 of the stored output;
+  // EPI 5 (backward, dgrad with the ReLU mask y = relu(bn(z)) of the BN layer below) sum g, sum g*y
+  // of the stored masked gradient -- with sum g*(z - mean) = (sum g*y - beta sum g) / (gamma invstd)
+  // on the mask's support, the BN backward needs no statistics pass over (g, z)
+  constexpr bool do_bn = EPI == 4 || EPI == 5;
   float bsum[do_bn ? TC : 1][4], bsq[do_bn ? TC : 1][4];
   if constexpr (do_bn) {
 #pragma unroll
@@ -582,10 +585,14 @@ __global__ __launch_bounds__(256 * WCS) void igemm_stream_kernel(IgemmArgs a) {
           __builtin_amdgcn_raw_buffer_store_b64(packed, yr, yo, 0, 0);
         if constexpr (do_bn) {     // statistics of the STORED bf16 values, like a separate pass
           const float q[4] = {lo_bf(packed.x), hi_bf(packed.x), lo_bf(packed.y), hi_bf(packed.y)};
+          float f[4] = {q[0], q[1], q[2], q[3]};
+          if constexpr (EPI == 5) {
+            f[0] = lo_bf(mk[ip][ic].x); f[1] = hi_bf(mk[ip][ic].x); f[2] = lo_bf(mk[ip][ic].y); f[3] = hi_bf(mk[ip][ic].y);
+          }
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             bsum[ic][e] += q[e];
-            bsq[ic][e] = fmaf(q[e], q[e], bsq[ic][e]);
+            bsq[ic][e] = fmaf(q[e], f[e], bsq[ic][e]);
           }
         }
         if constexpr (do_head) {   // the head sees the STORED bf16 values, like a separate pass would
@@ -813,9 +820,12 @@ static int launch_igemm_stream(const IgemmArgs& a, hipStream_t st) {
     }
     return (int)hipErrorInvalidValue;
   }
-  if (a.bnslab) { // conv followed by BatchNorm: batch-statistics partials in the epilogue
-    if (a.y2 || a.mask || a.accumulate) return (int)hipErrorInvalidValue;
-    hipLaunchKernelGGL((igemm_stream_kernel<BP, NG, CS, RH, WCS, 4>), dim3(grid), dim3(256 * WCS), 0, st, a);
+  if (a.bnslab) { // BatchNorm partial sums in the epilogue: forward statistics (no mask) or backward (mask)
+    if (a.y2 || a.accumulate || a.relu || (a.mask && a.mask_ch < a.Ngemm)) return (int)hipErrorInvalidValue;
+    if (a.mask)
+      hipLaunchKernelGGL((igemm_stream_kernel<BP, NG, CS, RH, WCS, 5>), dim3(grid), dim3(256 * WCS), 0, st, a);
+    else
+      hipLaunchKernelGGL((igemm_stream_kernel<BP, NG, CS, RH, WCS, 4>), dim3(grid), dim3(256 * WCS), 0, st, a);
     return (int)hipGetLastError();
   }
   if (a.y2) {     // decoder conv1 dgrad over the concat (NG = 2 CS): skip / up gradients as dense tensors

@@ -125,17 +125,21 @@ __global__ __launch_bounds__(256) void bn_finalize_kernel(const float* __restric
 // Backward coefficients dz = a*g + b*z + c (torch batch_norm_backward, training mode):
 //   xhat = (z-mean)*invstd,  dz = gamma*invstd*(g - mean(g) - xhat*mean(g*xhat))
 // and dgamma += sum g*xhat, dbeta += sum g (accumulated into the flat fp32 gradient buffer).
+// gy_mode (slab from the dgrad epilogue, csrc/halo.hip EPI 5): the second column is sum g*y with
+// y = relu(gamma xhat + beta) the BN output; g vanishes where y == 0, elsewhere xhat = (y - beta)/gamma,
+// so sum g*xhat = (sum g*y - beta sum g) / gamma.
 __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __restrict__ slab, int nblk, int C, long P,
                                                               const float* __restrict__ gamma, const float* __restrict__ saved,
                                                               float* __restrict__ coef3, float* __restrict__ dgamma,
-                                                              float* __restrict__ dbeta) {
+                                                              float* __restrict__ dbeta, const float* __restrict__ beta,
+                                                              int gy_mode) {
   __shared__ float red[4];
   const int c = blockIdx.x;
   float sg, sgz;
   slab_pair(slab, nblk, C, c, red, sg, sgz);
   if (threadIdx.x != 0) return;
   const float mean = saved[c], invstd = saved[C + c];
-  const float sgx = sgz * invstd;
+  const float sgx = gy_mode ? (sgz - beta[c] * sg) / gamma[c] : sgz * invstd;
   if (dgamma) dgamma[c] += sgx;
   if (dbeta) dbeta[c] += sg;
   const float sc = gamma[c] * invstd;
@@ -310,13 +314,16 @@ DPA_API int dpa_bn_fwd(const bf16_t* z, int ldz, bf16_t* y, int ldy, long long P
 // dgamma/dbeta accumulated.  coef3: scratch [3C].
 DPA_API int dpa_bn_bwd(const bf16_t* g, int ldg, const bf16_t* z, int ldz, bf16_t* dz, int lddz, long long P, int C,
                        const float* gamma, const float* saved, float* slab, float* coef3, float* dgamma, float* dbeta,
-                       hipStream_t st) {
+                       const float* beta, int slab_rows, hipStream_t st) {
   int G;
   dim3 grid;
   if (!bn_shape(P, C, G, grid) || (ldg & 7) || (ldz & 7) || (lddz & 7)) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(bn_partial_kernel<1>, grid, dim3(256), 0, st, g, ldg, z, ldz, saved, (long)P, C, G, slab);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(256), 0, st, slab, (int)grid.x, C, (long)P, gamma, saved, coef3,
-                     dgamma, dbeta);
+  // slab_rows > 0: (sum g, sum g*y) partials already written by the producing dgrad (needs beta)
+  if (slab_rows > 0 && beta == nullptr) return (int)hipErrorInvalidValue;
+  if (slab_rows <= 0)
+    hipLaunchKernelGGL(bn_partial_kernel<1>, grid, dim3(256), 0, st, g, ldg, z, ldz, saved, (long)P, C, G, slab);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(256), 0, st, slab, slab_rows > 0 ? slab_rows : (int)grid.x, C,
+                     (long)P, gamma, saved, coef3, dgamma, dbeta, beta, slab_rows > 0 ? 1 : 0);
   const long tot = (long)P * (C / 8);
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(dpa_grid(tot, 256, 16384)), dim3(256), 0, st, g, ldg, z, ldz, coef3, dz, lddz,
                      (long)P, C);

@@ -200,20 +200,25 @@ class HipBlocks:
             st.append((z, saved))
         return y
 
-    def bn_bwd(self, c: _Conv, g: torch.Tensor, st):
-        """gradient w.r.t. the conv output: identity without BN, BatchNorm backward with it."""
+    def bn_bwd(self, c: _Conv, g: torch.Tensor, st, stats: list = None):
+        """gradient w.r.t. the conv output: identity without BN, BatchNorm backward with it (``stats``:
+        the (sum g, sum g*y) partials the dgrad producing g computed in its epilogue, if any)."""
         if c.bn is None:
             return g
         z, saved = st
-        return K.bn_bwd(g, z, saved, c.bn, _grad(c.bn.weight), _grad(c.bn.bias))
+        return K.bn_bwd(g, z, saved, c.bn, _grad(c.bn.weight), _grad(c.bn.bias), stats=stats)
 
-    def conv_dgrad(self, c: _Conv, g: torch.Tensor, mask: torch.Tensor = None, out: torch.Tensor = None):
+    def conv_dgrad(self, c: _Conv, g: torch.Tensor, mask: torch.Tensor = None, out: torch.Tensor = None,
+                   below: _Conv = None):
+        """dgrad of ``c`` (ReLU-masked by ``mask``).  ``below``: the conv whose output ``mask`` is; if it
+        has a BatchNorm, returns (dx, stats) with that BN's backward partial sums from the epilogue."""
         N, H, W = g.shape[:3]
         if out is None:
             out = torch.empty(N, H, W, c.Cin, dtype=torch.bfloat16, device=g.device)
+        stats = [] if (below is not None and below.bn is not None) else None
         K.igemm(g, self.wd(c), out, Ngemm=c.Cin, Kpad=c.Kd, KH=3, KW=3, stride=1, pad=1, Cs=c.Cout,
-                out_grid=(N, H, W), mask=mask)
-        return out
+                out_grid=(N, H, W), mask=mask, bn_stats=stats)
+        return out if below is None else (out, stats)
 
     def conv_dgrad_split(self, c: _Conv, g: torch.Tensor, split: int):
         """dgrad of a conv over a concat input, written as two dense tensors (channels < split, >= split):
@@ -403,10 +408,10 @@ class _EncFn(torch.autograd.Function):
         else:
             K.pool_bwd(skip, dskip, dpooled, g2)
         g2 = B.bn_bwd(c2, g2, st2)
-        g1 = B.conv_dgrad(c2, g2, mask=a)
+        g1, st_g = B.conv_dgrad(c2, g2, mask=a, below=c1)
         B.conv_wgrad(c2, g2, a)
         B.ready([c2.mod, c2.bn])
-        g1 = B.bn_bwd(c1, g1, st1)
+        g1 = B.bn_bwd(c1, g1, st1, stats=st_g)
         gx = B.conv_dgrad(c1, g1) if ctx.x_needs_grad else None
         B.conv_wgrad(c1, g1, x)
         B.ready([c1.mod, c1.bn])
@@ -434,10 +439,10 @@ class _MidFn(torch.autograd.Function):
         st1, st2 = ctx.st
         c1, c2 = B.mid_convs
         g2 = B.bn_bwd(c2, _v(g2), st2)
-        g1 = B.conv_dgrad(c2, g2, mask=a)
+        g1, st_g = B.conv_dgrad(c2, g2, mask=a, below=c1)
         B.conv_wgrad(c2, g2, a)
         B.ready([c2.mod, c2.bn])
-        g1 = B.bn_bwd(c1, g1, st1)
+        g1 = B.bn_bwd(c1, g1, st1, stats=st_g)
         gx = B.conv_dgrad(c1, g1)
         B.conv_wgrad(c1, g1, x)
         B.ready([c1.mod, c1.bn])
@@ -495,10 +500,10 @@ class _DecFn(torch.autograd.Function):
         c1, c2 = B.dec_convs[i]
         C = d.Cout
         g2 = B.bn_bwd(c2, _v(g2), st2)
-        g1 = B.conv_dgrad(c2, g2, mask=a)
+        g1, st_g = B.conv_dgrad(c2, g2, mask=a, below=c1)
         B.conv_wgrad(c2, g2, a)
         B.ready([c2.mod, c2.bn])
-        g1 = B.bn_bwd(c1, g1, st1)
+        g1 = B.bn_bwd(c1, g1, st1, stats=st_g)
         dskip, gup = B.conv_dgrad_split(c1, g1, C)
         B.conv_wgrad(c1, g1, cat)
         B.ready([c1.mod, c1.bn])

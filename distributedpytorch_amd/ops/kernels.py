@@ -114,9 +114,10 @@ def igemm(x: torch.Tensor, wpacked: torch.Tensor, y: torch.Tensor, *, Ngemm: int
     tensor ``y2`` (channel ``co - split``) -- the two halves of a concat gradient.  ``head`` =
     (segmap weight, segmap bias, target [N*Ho*Wo] fp32): the streaming kernel also computes the fused
     segmap + sigmoid + BCE/Dice partial sums of its (bf16) output; returns them as S[4].
-    ``bn_stats`` (an empty list; conv followed by BatchNorm): when the streaming kernel runs, its
-    epilogue also writes the per-block channel sums / sums of squares of the stored output and the
-    list receives (slab [rows][2][Ngemm] fp32, rows) for :func:`bn_fwd`; left empty otherwise."""
+    ``bn_stats`` (an empty list): when the streaming kernel runs, its epilogue also writes per-block
+    channel partial sums and the list receives (slab [rows][2][Ngemm] fp32, rows); left empty
+    otherwise.  Without ``mask`` (conv followed by BatchNorm): sum y, sum y^2 for :func:`bn_fwd`;
+    with ``mask`` = the BN layer's output (dgrad into it): sum g, sum g*mask for :func:`bn_bwd`."""
     N, Hs, Ws, Cx, ldx = _nhwc(x, "igemm.x")
     _, _, _, Cy, ldy = _nhwc(y, "igemm.y")
     No, Ho, Wo = out_grid
@@ -153,8 +154,8 @@ def igemm(x: torch.Tensor, wpacked: torch.Tensor, y: torch.Tensor, *, Ngemm: int
     pool_done = True
     hslab, hrows = None, 0
     bslab, brows = None, 0
-    if bn_stats is not None and USE_FUSED_BN and mode == 0 and pool is None and y2 is None and mask is None \
-            and head is None and not accumulate and path == "auto":
+    if bn_stats is not None and USE_FUSED_BN and mode == 0 and pool is None and y2 is None and head is None \
+            and not accumulate and not relu and path == "auto" and (mask is None or mch == Ngemm):
         bslab = torch.empty(N * -(-Ho // 16) * max(1, Wo // 64) * 2 * Ngemm, dtype=torch.float32, device=y.device)
     if head is not None:
         hw, hb, tgt = head
@@ -537,8 +538,10 @@ def bn_fwd(z: torch.Tensor, y: torch.Tensor, bn: torch.nn.BatchNorm2d, train: bo
 
 
 def bn_bwd(g: torch.Tensor, z: torch.Tensor, saved: torch.Tensor, bn: torch.nn.BatchNorm2d,
-           dgamma: Optional[torch.Tensor], dbeta: Optional[torch.Tensor]) -> torch.Tensor:
-    """dz from g = dL/d(BN output) (ReLU mask already applied); dgamma/dbeta += (fp32 [C])."""
+           dgamma: Optional[torch.Tensor], dbeta: Optional[torch.Tensor], stats: Optional[list] = None) -> torch.Tensor:
+    """dz from g = dL/d(BN output) (ReLU mask already applied); dgamma/dbeta += (fp32 [C]).
+    ``stats`` = (slab, rows) of (sum g, sum g*y) from the dgrad that produced g (:func:`igemm`
+    ``bn_stats`` with the BN output as mask): no reduction pass over (g, z)."""
     N, H, W, C, ldg = _nhwc(g, "bn_bwd.g")
     Nz, Hz, Wz, Cz, ldz = _nhwc(z, "bn_bwd.z")
     assert (Nz, Hz, Wz, Cz) == (N, H, W, C) and saved.numel() == 2 * C
@@ -551,9 +554,14 @@ def bn_bwd(g: torch.Tensor, z: torch.Tensor, saved: torch.Tensor, bn: torch.nn.B
         _flat_f32(dgamma, C, "bn.dgamma")
     if dbeta is not None:
         _flat_f32(dbeta, C, "bn.dbeta")
+    slab, pre_rows = scratch[:rows * 2 * C], 0
+    if stats:
+        slab, pre_rows = stats
+        assert slab.numel() >= pre_rows * 2 * C
     _check(L.dpa_bn_bwd(_p(g), c_int(ldg), _p(z), c_int(ldz), _p(dz), c_int(C), c_ll(P), c_int(C),
-                        _p(_flat_f32(bn.weight, C, "bn.weight")), _p(saved), _p(scratch[:rows * 2 * C]),
-                        _p(scratch[rows * 2 * C:]), _p(dgamma), _p(dbeta), _stream(g)), "bn_bwd")
+                        _p(_flat_f32(bn.weight, C, "bn.weight")), _p(saved), _p(slab),
+                        _p(scratch[rows * 2 * C:]), _p(dgamma), _p(dbeta), _p(_flat_f32(bn.bias, C, "bn.bias")),
+                        c_int(pre_rows), _stream(g)), "bn_bwd")
     return dz
 
 

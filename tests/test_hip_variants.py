@@ -276,3 +276,41 @@ def test_bn_apply_fused_maxpool(hip_lib, N, H, W, C):
         assert torch.equal(a, b)
     ref = F.max_pool2d(res[0][0].float().permute(0, 3, 1, 2), 2).permute(0, 2, 3, 1)
     assert torch.equal(res[0][1].float(), ref)
+
+
+@pytest.mark.parametrize("N,H,W,C1,C2", [(2, 5, 128, 32, 32), (1, 6, 64, 64, 64), (2, 3, 128, 32, 64),
+                                         (1, 4, 128, 64, 32)])
+def test_bn_backward_partials_fused_in_stream_dgrad(hip_lib, N, H, W, C1, C2):
+    """The dgrad into a BN layer's output y = relu(bn(z)) (ReLU mask y) also writes sum g, sum g*y per
+    channel from its epilogue; bn_bwd then skips its reduction pass (sum g*xhat = (sum g*y - beta
+    sum g) / gamma on the mask's support).  dz, dgamma, dbeta match the unfused path."""
+    from distributedpytorch_amd.ops import kernels as K
+    from test_hip_kernels import _pack_one
+    torch.manual_seed(6)
+    z = (torch.randn(N, H, W, C1) * 1.5 + 0.2).to(torch.bfloat16).cuda()
+    w2 = torch.randn(C2, C1, 3, 3) * (2.0 / (9 * C1)) ** 0.5
+    g2 = torch.randn(N, H, W, C2).to(torch.bfloat16).cuda()
+    packed, ng, kp = _pack_one(1, w2)
+    res = []
+    for fused in (True, False):
+        bn = torch.nn.BatchNorm2d(C1).cuda()
+        with torch.no_grad():
+            bn.weight.copy_(torch.linspace(0.6, 1.4, C1))
+            bn.bias.copy_(torch.linspace(-0.3, 0.3, C1))
+        y = torch.empty_like(z)
+        saved = K.bn_fwd(z, y, bn, train=True)
+        g1 = torch.empty(N, H, W, C1, dtype=torch.bfloat16, device="cuda")
+        stats = [] if fused else None
+        K.igemm(g2, packed, g1, Ngemm=ng, Kpad=kp, KH=3, KW=3, stride=1, pad=1, Cs=C2, out_grid=(N, H, W),
+                mask=y, bn_stats=stats)
+        if fused:
+            assert len(stats) == 2 and stats[1] > 0, "dgrad epilogue did not produce the BN partials"
+        dgam, dbet = torch.zeros(C1, device="cuda"), torch.zeros(C1, device="cuda")
+        dz = K.bn_bwd(g1, z, saved, bn, dgam, dbet, stats=stats)
+        torch.cuda.synchronize()
+        res.append((g1.float().cpu(), dz.float().cpu(), dgam.cpu(), dbet.cpu()))
+    (g1a, dza, dga, dba), (g1b, dzb, dgb, dbb) = res
+    assert torch.equal(g1a, g1b)
+    assert torch.allclose(dba, dbb, rtol=1e-5, atol=1e-4)
+    assert torch.allclose(dga, dgb, rtol=2e-2, atol=2e-2 * dgb.abs().max().item())
+    assert _rel(dza, dzb) < 2e-2
