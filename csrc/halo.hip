@@ -19,17 +19,19 @@
 // ROWS output rows per block share one staging of each weight slice (the weights are ~60% of a
 // slice's LDS writes at 64-128 output channels, and ds_write bandwidth, not the MFMAs, bounds this
 // kernel): ROWS = 2 stages 4 input rows + the weights for twice the MFMAs of ROWS = 1.
+// (BC/WC) x (BP/WP) waves: 4, or 8 for the 128-channel tile (one staging of the input rows serves
+// all 128 output channels -- the dgrads into 128 channels from 64 have only 2 K-slices to amortise it).
 template <int BP, int BC, int WP, int WC, int ROWS = 1>
-__global__ __launch_bounds__(256) void igemm_halo_kernel(IgemmArgs a) {
+__global__ __launch_bounds__(64 * (BC / WC) * (BP / WP)) void igemm_halo_kernel(IgemmArgs a) {
   constexpr int HR = BP + 2;              // pixels per halo row
   constexpr int PROWS = (ROWS + 2) * HR;  // staged pixel rows (64 B = 32 channels each)
   constexpr int PBYTES = PROWS * 64;
   constexpr int WRB = 9 * 64;             // weight row bytes: 9 taps x 32 channels (576 = 64 mod 256)
-  constexpr int NWC = BC / WC, NWP = BP / WP;
-  static_assert(NWC * NWP == 4, "4 waves");
+  constexpr int NWC = BC / WC, NWP = BP / WP, NT = 64 * NWC * NWP;
+  static_assert(NT == 256 || NT == 512, "4 or 8 waves");
   constexpr int TP = WP / 16, TC = WC / 16;
   constexpr int PCH = PROWS * 4, WCH = BC * 36, CH = PCH + WCH;   // 16-B chunks per slice
-  constexpr int L = (CH + 255) / 256;
+  constexpr int L = (CH + NT - 1) / NT;
   __shared__ __attribute__((aligned(16))) char lds[PBYTES + BC * WRB];
   char* const Pimg = lds;
   char* const Wimg = lds + PBYTES;
@@ -64,7 +66,7 @@ __global__ __launch_bounds__(256) void igemm_halo_kernel(IgemmArgs a) {
   bool isw[L], gok[L];
 #pragma unroll
   for (int j = 0; j < L; ++j) {
-    const int c = tid + j * 256;
+    const int c = tid + j * NT;
     isw[j] = c >= PCH;
     if (c < PCH) {
       const int row = c >> 2, cc = c & 3;
@@ -175,12 +177,13 @@ __global__ __launch_bounds__(256) void igemm_halo_kernel(IgemmArgs a) {
 template <int BP, int BC, int WP, int WC, int ROWS = 1>
 static int launch_igemm_halo(const IgemmArgs& a, hipStream_t st) {
   const int grid = a.N * ((a.Ho + ROWS - 1) / ROWS) * (a.Wo / BP) * (a.Ngemm / BC);
-  hipLaunchKernelGGL((igemm_halo_kernel<BP, BC, WP, WC, ROWS>), dim3(grid), dim3(256), 0, st, a);
+  hipLaunchKernelGGL((igemm_halo_kernel<BP, BC, WP, WC, ROWS>), dim3(grid), dim3(64 * (BC / WC) * (BP / WP)), 0, st, a);
   return (int)hipGetLastError();
 }
 
 // Returns hipErrorInvalidValue (nothing launched) when the shape is not eligible; the caller then
-// uses dpa_igemm.  cfg: 0 auto, 1: 256x32, 2: 128x64, 3: 128x32, 4: 128x64 two rows, 5: 128x32 two rows
+// uses dpa_igemm.  cfg: 0 auto, 1: 256x32, 2: 128x64, 3: 128x32, 4: 128x64 two rows, 5: 128x32 two rows,
+// 6: 128x128 two rows 8 waves (4 ch x 2 px), 7: 128x128 two rows 8 waves (2 ch x 4 px)
 DPA_API int dpa_igemm_halo(const IgemmArgs* args, int cfg, hipStream_t st) {
   const IgemmArgs& a = *args;
   if (a.mode != 0 || a.KH != 3 || a.KW != 3 || a.stride != 1 || a.pad != 1 || (a.Cs % 32) || (a.ldx & 7) ||
@@ -200,6 +203,8 @@ DPA_API int dpa_igemm_halo(const IgemmArgs* args, int cfg, hipStream_t st) {
     case 3: if (a.Wo % 128 || a.Ngemm % 32) break; return launch_igemm_halo<128, 32, 32, 32>(a, st);
     case 4: if (a.Wo % 128 || a.Ngemm % 64) break; return launch_igemm_halo<128, 64, 64, 32, 2>(a, st);
     case 5: if (a.Wo % 128 || a.Ngemm % 32) break; return launch_igemm_halo<128, 32, 32, 32, 2>(a, st);
+    case 6: if (a.Wo % 128 || a.Ngemm % 128) break; return launch_igemm_halo<128, 128, 64, 32, 2>(a, st);
+    case 7: if (a.Wo % 128 || a.Ngemm % 128) break; return launch_igemm_halo<128, 128, 32, 64, 2>(a, st);
     default: break;
   }
   return (int)hipErrorInvalidValue;
