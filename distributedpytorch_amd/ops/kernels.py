@@ -78,6 +78,8 @@ USE_HALO = os.environ.get("DPA_NO_HALO", "0") != "1"
 # row-streaming conv3x3 (weights resident, 4-row LDS ring); DPA_NO_STREAM=1 disables
 USE_STREAM = os.environ.get("DPA_NO_STREAM", "0") != "1"
 USE_GLDS = os.environ.get("DPA_NO_GLDS", "0") != "1"
+# row-streaming weight-gradient tile override (csrc/halo.hip dpa_wgrad_stream cfg; 0 = auto)
+WGRAD_STREAM_CFG = int(os.environ.get("DPA_WGRAD_STREAM_CFG", "0"))
 HALO_CFG = int(os.environ.get("DPA_HALO_CFG", "0"))    # 0 = auto (csrc/halo.hip dpa_igemm_halo)
 # segmentation head + loss partials fused into the last decoder conv; DPA_NO_FUSED_HEAD=1 disables
 USE_FUSED_HEAD = os.environ.get("DPA_NO_FUSED_HEAD", "0") != "1"
@@ -314,6 +316,8 @@ def _wgrad_stream(A, B, *, grid, M, Nc, gw, gb, Nreal):
     assert gw.dtype == torch.float32 and gw.is_contiguous() and gw.numel() == M * Nreal * 9
     if Nc == 8:            # first layer (RGB padded to 8 channels): 32x16 tile, half the columns zero
         hcfg = 4
+    elif WGRAD_STREAM_CFG in (1, 2, 3) and not (WGRAD_STREAM_CFG == 2 and M % 64) and not (WGRAD_STREAM_CFG == 3 and Nc % 64):
+        hcfg = WGRAD_STREAM_CFG
     else:
         hcfg = 2 if M % 64 == 0 else (3 if Nc % 64 == 0 else 1)
     bm, bn = {1: (32, 32), 2: (64, 32), 3: (32, 64), 4: (32, 16)}[hcfg]

@@ -39,6 +39,7 @@ def main():
     ap.add_argument("--svar", type=int, nargs="*", default=[], help="streaming-conv variants to time")
     ap.add_argument("--gvar", type=int, nargs="*", default=[], help="LDS-DMA (glds) kernel configs to time")
     ap.add_argument("--hvar", type=int, nargs="*", default=[], help="row-halo kernel configs to time")
+    ap.add_argument("--wsvar", type=int, nargs="*", default=[], help="row-streaming wgrad tile configs to time")
     ap.add_argument("--paths", default="stream,halo,generic", help="default paths to time")
     ap.add_argument("--layout-probe", action="store_true",
                     help="full-res memory-bound ops on concat halves (ld=2C) vs dense tensors (ld=C)")
@@ -80,13 +81,17 @@ def main():
                 print(f"{name:14s} dgrad {label:8s}  n/a ({str(e)[:40]})", flush=True)
         gw = torch.zeros(Cout * Cin * 9, device=dev)
         gb = torch.zeros(Cout, device=dev)
-        for path in (() if a.no_wgrad else ("stream", "halo", "generic")):
+        wvars = [(p, p, 0) for p in (() if a.no_wgrad else ("stream", "halo", "generic"))] + \
+            [(f"strm.w{v}", "stream", v) for v in a.wsvar]
+        for label, path, wv in wvars:
+            K.WGRAD_STREAM_CFG = wv
             try:
                 t = timeit(lambda: K.wgrad(g, x, kind=0, grid=(B, H, H), M=Cout, Nc=Cin, s=1, pad=1, KW=3, gw=gw,
                                            gb=gb, Nreal=Cin, path=path), a.reps)
-                print(f"{name:14s} wgrad {path:8s} {t:9.1f} us {flops / t / 1e6:7.1f} TF", flush=True)
+                print(f"{name:14s} wgrad {label:8s} {t:9.1f} us {flops / t / 1e6:7.1f} TF", flush=True)
             except Exception as e:
-                print(f"{name:14s} wgrad {path:8s}  n/a ({str(e)[:40]})", flush=True)
+                print(f"{name:14s} wgrad {label:8s}  n/a ({str(e)[:40]})", flush=True)
+        K.WGRAD_STREAM_CFG = 0
         del x, g, y, dx
     if a.layout_probe:
         C, H = 32, S
