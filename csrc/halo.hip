@@ -1106,6 +1106,12 @@ DPA_API int dpa_wgrad_stream(const WgradArgs* args, int cfg, int bp, int rh, int
   DPA_WS(1, 32, 32, 64, 32)
   DPA_WS(2, 64, 32, 64, 32)
   DPA_WS(3, 32, 64, 64, 32)
+  DPA_WS(1, 32, 32, 32, 64)
+  DPA_WS(2, 64, 32, 32, 64)
+  DPA_WS(3, 32, 64, 32, 64)
+  DPA_WS(1, 32, 32, 32, 32)
+  DPA_WS(2, 64, 32, 32, 32)
+  DPA_WS(3, 32, 64, 32, 32)
 #undef DPA_WS
   if (cfg == 4 && a.Nc == 8 && a.M % 32 == 0 && bp == 64) {
     if (rh == 64) return launch_wgrad_stream<32, 16, 64, 64>(a, ipb, st);

@@ -254,7 +254,7 @@ def wgrad(A: torch.Tensor, B: torch.Tensor, *, kind: int, grid, M: int, Nc: int,
     ``path``: ``auto`` = row-streaming kernel when W % 64 == 0, else row-halo (W % 32 == 0), else the
     generic per-tap gather kernel; ``stream`` / ``halo`` / ``generic`` force one."""
     if path in ("auto", "stream") and kind == 0 and cfg == 0 and (USE_STREAM or path == "stream") \
-            and grid[2] % 64 == 0 and M % 32 == 0 and (Nc % 32 == 0 or Nc == 8):
+            and (grid[2] % 64 == 0 or (grid[2] % 32 == 0 and Nc % 32 == 0)) and M % 32 == 0 and (Nc % 32 == 0 or Nc == 8):
         return _wgrad_stream(A, B, grid=grid, M=M, Nc=Nc, gw=gw, gb=gb, Nreal=Nreal)
     if path == "stream":
         raise RuntimeError("wgrad stream path not eligible for this shape")
@@ -326,8 +326,9 @@ def _wgrad_stream(A, B, *, grid, M, Nc, gw, gb, Nreal):
     st = _stream(A)
     for n0, n1 in _image_chunks(N, max(HA * WA * lda, HB * WB * ldb) * 2):
         nb = n1 - n0
-        rh = 64 if nb * -(-Hg // 64) * (Wg // 64) * tiles >= 1024 else 32
-        per_img = -(-Hg // rh) * (Wg // 64)
+        bp = 64 if Wg % 64 == 0 else 32   # 32-pixel strips for the 32x32 bottleneck (mid block)
+        rh = 64 if nb * -(-Hg // 64) * (Wg // bp) * tiles >= 1024 else 32
+        per_img = -(-Hg // rh) * (Wg // bp)
         # images per split: keep >= ~2048 blocks (8 per CU) but no more slabs than that -- the fp32
         # slab reduction otherwise grows linearly with the batch
         ipb = max(1, (nb * per_img * tiles) // WGRAD_STREAM_BLOCKS)
@@ -337,7 +338,7 @@ def _wgrad_stream(A, B, *, grid, M, Nc, gw, gb, Nreal):
         a = WgradArgs(A[n0:n1].data_ptr(), B[n0:n1].data_ptr(), slab.data_ptr(),
                       None if bslab is None else bslab.data_ptr(), lda, ldb, nb, Hg, Wg, HA, WA, HB, WB, M, Nc, 1,
                       1, 3, 0, splits, _extent_bytes(nb, HA, WA, CA, lda), _extent_bytes(nb, HB, WB, CB, ldb))
-        _check(L.dpa_wgrad_stream(ctypes.byref(a), c_int(hcfg), c_int(64), c_int(rh), c_int(ipb), st), "wgrad_stream")
+        _check(L.dpa_wgrad_stream(ctypes.byref(a), c_int(hcfg), c_int(bp), c_int(rh), c_int(ipb), st), "wgrad_stream")
         _check(L.dpa_wgrad_reduce(_p(slab), _p(bslab), _p(gw), _p(gb), c_int(splits), c_int(9), c_int(M), c_int(Nc),
                                   c_int(Nreal), c_int(0), st), "wgrad_reduce")
 

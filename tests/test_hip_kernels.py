@@ -195,6 +195,8 @@ def test_deconv_dgrad_from_concat(hip_lib, N, h, w, Cin, Cout):
     # row-streaming wgrad (W % 64 == 0), odd row counts -> partial row segments
     (2, 5, 64, 32, 32, None, "stream"), (1, 37, 64, 64, 32, None, "stream"), (2, 3, 128, 32, 64, None, "stream"),
     (1, 70, 64, 128, 64, None, "stream"), (1, 4, 64, 64, 128, None, "generic"),
+    # 32-pixel strips (the 32x32 bottleneck): W % 64 != 0
+    (2, 5, 32, 32, 32, None, "stream"), (1, 33, 32, 64, 128, None, "stream"), (2, 3, 96, 128, 64, None, "stream"),
     # first layer through the streaming wgrad (8 padded input channels in a 16-wide tile)
     (2, 5, 128, 3, 32, 8, "stream"), (1, 66, 64, 3, 32, 8, "stream")])
 def test_conv3x3_wgrad(hip_lib, N, H, W, Cin, Cout, cin_pad, path):
