@@ -84,6 +84,27 @@ __device__ __forceinline__ void slab_pair(const float* slab, int nblk, int C, in
   q = block_sum_256(b, red);
 }
 
+// Fold a tall slab [rows][K] into [ceil(rows/R)][K] (block b sums rows bR..bR+R-1, threads across
+// the K columns: coalesced rows, fixed order).  The conv epilogues write one slab row per block --
+// tens of thousands at full resolution -- and the one-block-per-channel finalize would otherwise walk
+// all of them serially.
+__global__ __launch_bounds__(256) void slab_fold_kernel(const float* __restrict__ in, int rows, int K, int R,
+                                                        float* __restrict__ out) {
+  const int r0 = blockIdx.x * R, r1 = min(rows, r0 + R);
+  for (int k = threadIdx.x; k < K; k += blockDim.x) {
+    float acc = 0.f;
+    for (int r = r0; r < r1; ++r) acc += in[(long)r * K + k];
+    out[(long)blockIdx.x * K + k] = acc;
+  }
+}
+
+DPA_API int dpa_slab_fold(const float* in, int rows, int K, int nout, float* out, hipStream_t st) {
+  if (rows <= 0 || K <= 0 || nout <= 0) return (int)hipErrorInvalidValue;
+  const int R = (rows + nout - 1) / nout;
+  hipLaunchKernelGGL(slab_fold_kernel, dim3((rows + R - 1) / R), dim3(256), 0, st, in, rows, K, R, out);
+  return (int)hipGetLastError();
+}
+
 // Forward coefficients y = z*coef[c] + coef[C+c].  train: batch statistics (saved = mean, invstd
 // for the backward; running stats updated in place); eval (slab == null): running statistics.
 __global__ __launch_bounds__(256) void bn_finalize_kernel(const float* __restrict__ slab, int nblk, int C, long P,
