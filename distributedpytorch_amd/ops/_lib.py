@@ -16,7 +16,8 @@ import os
 from pathlib import Path
 
 _HERE = Path(__file__).resolve().parent.parent
-LIB_PATH = _HERE / "_C" / "libdpa_hip.so"
+# DPA_LIB_PATH: load another build of the same library (tools/asan_host.sh: host code under ASan)
+LIB_PATH = Path(os.environ["DPA_LIB_PATH"]) if os.environ.get("DPA_LIB_PATH") else _HERE / "_C" / "libdpa_hip.so"
 _lib = None
 _err = None
 

@@ -1,0 +1,156 @@
+"""Host-side contracts of the HIP kernel library, checked on the CPU (no GPU, no kernel launch).
+
+Every ``dpa_*`` launcher validates its shapes, alignments and tiling before it touches the device
+and returns ``hipErrorInvalidValue`` (1) instead of launching a kernel whose grid or addressing
+would not match -- the guard against out-of-bounds waves that the GPU tests cannot exercise
+safely.  The Python wrappers (ops/kernels.py) assert the tensor-level contracts before building
+the argument blocks.  The same checks run under AddressSanitizer (host code) via
+``tools/asan_host.sh``.
+"""
+import ctypes
+import os
+
+import pytest
+import torch
+
+from distributedpytorch_amd.ops import _lib
+
+INVALID = 1   # hipErrorInvalidValue
+
+pytestmark = pytest.mark.skipif(not _lib.LIB_PATH.exists(), reason="HIP library not built")
+
+
+@pytest.fixture(scope="module")
+def L():
+    return _lib.lib()
+
+
+def _igemm_args(**kw):
+    from distributedpytorch_amd.ops import kernels as K
+    a = K.IgemmArgs()
+    base = dict(ldx=32, ldy=32, N=1, Ho=64, Wo=64, Hs=64, Ws=64, Cs=32, KH=3, KW=3, stride=1, pad=1, Ngemm=32,
+                Kpad=288, mode=0)
+    base.update(kw)
+    for k, v in base.items():
+        setattr(a, k, v)
+    return a
+
+
+def _wgrad_args(**kw):
+    from distributedpytorch_amd.ops import kernels as K
+    a = K.WgradArgs()
+    base = dict(lda=32, ldb=32, N=1, Hg=64, Wg=64, HA=64, WA=64, HB=64, WB=64, M=32, Nc=32, s=1, pad=1, KW=3,
+                pix_per_split=4096, splits=1)
+    base.update(kw)
+    for k, v in base.items():
+        setattr(a, k, v)
+    return a
+
+
+def test_library_exports_and_version(L):
+    assert L.dpa_version() > 0
+    for name in ("dpa_igemm", "dpa_igemm_glds", "dpa_igemm_halo", "dpa_igemm_stream", "dpa_wgrad", "dpa_wgrad_halo",
+                 "dpa_wgrad_stream", "dpa_wgrad_reduce", "dpa_deconv_fwd", "dpa_deconv_bwd", "dpa_maxpool2",
+                 "dpa_pool_bwd", "dpa_pool_bwd_code", "dpa_head_fwd", "dpa_head_bwd", "dpa_bn_fwd", "dpa_bn_bwd",
+                 "dpa_up2_fwd", "dpa_up2_bwd", "dpa_adam_flat", "dpa_adam_flat_dev", "dpa_pack_weights",
+                 "dpa_slab_fold", "dpa_loss_finish", "dpa_loss_grad"):
+        assert hasattr(L, name), name
+    assert L.dpa_error_string(INVALID).decode() == "invalid argument"
+
+
+@pytest.mark.parametrize("kw", [dict(Cs=12), dict(ldx=30), dict(Kpad=300), dict(Ngemm=48), dict(mode=1, Cout=6)])
+def test_generic_igemm_rejects(L, kw):
+    assert L.dpa_igemm(ctypes.byref(_igemm_args(**kw)), 0, None) == INVALID
+
+
+@pytest.mark.parametrize("kw", [dict(Cs=32), dict(Kpad=288), dict(KH=7, KW=7, Cs=64, Kpad=64 * 49)])
+def test_glds_igemm_rejects(L, kw):
+    a = _igemm_args(Cs=64, Kpad=576, Ngemm=256, ldx=64)
+    for k, v in kw.items():
+        setattr(a, k, v)
+    assert L.dpa_igemm_glds(ctypes.byref(a), 0, None) == INVALID
+
+
+@pytest.mark.parametrize("kw", [dict(mode=1), dict(KH=1, KW=1), dict(stride=2), dict(Cs=48, Kpad=448),
+                                dict(Hs=66), dict(Kpad=256), dict(Wo=96, Ws=96)])
+def test_halo_igemm_rejects(L, kw):
+    assert L.dpa_igemm_halo(ctypes.byref(_igemm_args(**kw)), 0, None) == INVALID
+
+
+@pytest.mark.parametrize("kw", [dict(Wo=96, Ws=96), dict(mode=1), dict(pad=0), dict(Kpad=256), dict(Ngemm=128, Kpad=288)])
+def test_stream_igemm_rejects(L, kw):
+    assert L.dpa_igemm_stream(ctypes.byref(_igemm_args(**kw)), 0, None) == INVALID
+
+
+def test_stream_block_count_matches_launch_geometry(L):
+    # variant 1 (Cs = Ngemm = 32): 128-pixel strips, 32-row segments when there are >= 1024 of them
+    a = _igemm_args(N=128, Ho=512, Wo=512, Hs=512, Ws=512)
+    assert L.dpa_igemm_stream_blocks(ctypes.byref(a)) == 128 * (512 // 32) * (512 // 128)
+    a = _igemm_args(N=2, Ho=40, Wo=128, Hs=40, Ws=128)
+    assert L.dpa_igemm_stream_blocks(ctypes.byref(a)) == 2 * 3 * 1       # 16-row segments: ceil(40/16)
+
+
+@pytest.mark.parametrize("kw", [dict(M=48), dict(lda=30), dict(pix_per_split=100), dict(splits=0)])
+def test_wgrad_rejects(L, kw):
+    assert L.dpa_wgrad(ctypes.byref(_wgrad_args(**kw)), 0, 0, None) == INVALID
+
+
+@pytest.mark.parametrize("kw", [dict(Wg=48, WA=48, WB=48), dict(Nc=48), dict(KW=2), dict(HB=32)])
+def test_wgrad_halo_rejects(L, kw):
+    assert L.dpa_wgrad_halo(ctypes.byref(_wgrad_args(**kw)), 0, None) == INVALID
+
+
+def test_wgrad_stream_checks_split_count(L):
+    # splits must equal ceil(N/ipb) * ceil(Hg/rh) * (Wg/bp): 1 image, rh 64, bp 64 -> 1 split
+    assert L.dpa_wgrad_stream(ctypes.byref(_wgrad_args(splits=2)), 1, 64, 64, 1, None) == INVALID
+    assert L.dpa_wgrad_stream(ctypes.byref(_wgrad_args(Wg=96, WA=96, WB=96)), 1, 64, 64, 1, None) == INVALID
+    assert L.dpa_wgrad_stream(ctypes.byref(_wgrad_args()), 1, 64, 64, 0, None) == INVALID   # ipb < 1
+
+
+def test_elementwise_launchers_reject(L):
+    n = None
+    i = ctypes.c_int
+    assert L.dpa_maxpool2(n, i(12), n, i(12), i(1), i(8), i(8), i(12), n, n) == INVALID            # C % 8
+    assert L.dpa_pool_bwd_code(n, n, i(8), n, i(8), n, i(8), i(1), i(7), i(8), i(8), n) == INVALID  # odd H
+    assert L.dpa_up2_fwd(n, i(8), n, i(8), i(1), i(0), i(4), i(8), n) == INVALID                   # h < 1
+    assert L.dpa_up2_bwd(n, i(8), n, i(8), i(1), i(4), i(4), i(12), n) == INVALID                  # C % 8
+    assert L.dpa_slab_fold(n, i(0), i(64), i(8), n, n) == INVALID
+    assert L.dpa_deconv_bwd(n, i(64), n, i(64), n, n, i(64), n, n, i(1), i(8), i(8), i(64), i(32), i(0),
+                            ctypes.c_uint(0), ctypes.c_uint(0), n) == INVALID                       # splits < 1
+    assert L.dpa_deconv_fwd(n, i(60), n, n, n, i(64), i(1), i(8), i(8), i(64), i(32), i(1), ctypes.c_uint(0),
+                            n) == INVALID                                                           # ldx % 8
+
+
+def test_bn_shapes(L):
+    assert L.dpa_bn_slab_rows(ctypes.c_longlong(1000), ctypes.c_int(12)) == 0     # C % 8
+    rows = L.dpa_bn_slab_rows(ctypes.c_longlong(128 * 512 * 512), ctypes.c_int(32))
+    assert 0 < rows <= 512
+    assert L.dpa_head_slab_blocks(ctypes.c_longlong(1 << 20)) > 0
+
+
+def test_python_wrappers_assert_before_launch():
+    """Tensor-level checks in ops/kernels.py fire before any argument block is built."""
+    from distributedpytorch_amd.ops import kernels as K
+    x = torch.zeros(1, 8, 8, 32, dtype=torch.bfloat16)
+    w = torch.zeros(32 * 288, dtype=torch.bfloat16)
+    y = torch.zeros(1, 8, 8, 16, dtype=torch.bfloat16)            # fewer channels than Ngemm
+    with pytest.raises(AssertionError):
+        K.igemm(x, w, y, Ngemm=32, Kpad=288, KH=3, KW=3, stride=1, pad=1, Cs=32, out_grid=(1, 8, 8))
+    with pytest.raises(AssertionError):                          # packed weights too short
+        K.igemm(x, w[:100], torch.zeros(1, 8, 8, 32, dtype=torch.bfloat16), Ngemm=32, Kpad=288, KH=3, KW=3,
+                stride=1, pad=1, Cs=32, out_grid=(1, 8, 8))
+    with pytest.raises(AssertionError):                          # fp32 activations
+        K.igemm(x.float(), w, y, Ngemm=32, Kpad=288, KH=3, KW=3, stride=1, pad=1, Cs=32, out_grid=(1, 8, 8))
+
+
+def test_native_dp_comm_rejects_bad_args():
+    from distributedpytorch_amd.parallel import dp_comm
+    if not dp_comm.LIB_PATH.exists():
+        pytest.skip("comm library not built")
+    L = dp_comm.lib()
+    h = ctypes.c_void_p()
+    assert L.dpa_dp_comm_init(ctypes.c_int(0), None, ctypes.byref(h)) != 0
+    assert L.dpa_dp_all_reduce(None, None, ctypes.c_longlong(4), ctypes.c_int(0), ctypes.c_int(0), None) != 0
+    assert L.dpa_dp_broadcast(None, None, ctypes.c_longlong(4), ctypes.c_int(0), ctypes.c_int(0), None) != 0
+    assert L.dpa_dp_comm_size(None) == 0
+    assert L.dpa_dp_version() > 0
