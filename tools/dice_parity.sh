@@ -7,7 +7,7 @@
 set -euo pipefail
 cd "$(dirname "$0")/.."
 E=${1:-6}; S=${2:-256}; NI=${3:-1024}
-OUT=${DICE_OUT:-gpurun_out/dice}
+OUT=${DICE_OUT:-/tmp/dice_parity}   # checkpoints stay out of gpurun_out/ (64 MiB merge cap)
 rm -rf "$OUT"; mkdir -p "$OUT"
 common="--synthetic --synthetic-len $NI --img-size $S -b 16 -e $E --lr 3e-4 -s 42"
 timeout -k 10 900 python train.py $common --backend hip --dtype bf16 --out-dir "$OUT/hip" > "$OUT/hip.log" 2>&1
