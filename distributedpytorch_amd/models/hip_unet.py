@@ -119,6 +119,13 @@ class HipBlocks:
         self._cats: "weakref.WeakValueDictionary[int, torch.Tensor]" = weakref.WeakValueDictionary()
         self._target = None        # (target as given, fp32 flat copy) announced by run_segment
         self._head_cache = None    # (y ptr, target ptr, S) from the fused head epilogue
+        # conv weight gradients on a second HIP stream: nothing in the backward consumes them, so a
+        # block's wgrads overlap its dgrad chain (filling each kernel's tail); the block's end joins
+        # the streams and only then announces its gradients (DDP buckets see finished values)
+        self.side = torch.cuda.Stream(device=self.device) if K.SIDE_WGRAD else None
+        self._side_pending = False
+        self._ready_pending = []
+        self._keep = []
 
     # ------------------------------------------------------------------ weight packing
     def _build_packing(self):
@@ -234,8 +241,30 @@ class HipBlocks:
     def conv_wgrad(self, c: _Conv, g: torch.Tensor, x: torch.Tensor):
         N, H, W = g.shape[:3]
         gw, gb = _grad(c.mod.weight), _grad(c.mod.bias)
-        K.wgrad(g, x, kind=0, grid=(N, H, W), M=c.Cout, Nc=c.Cs, s=1, pad=1, KW=3, gw=gw.view(-1), gb=gb,
-                Nreal=c.Cin)
+        if self.side is None:
+            K.wgrad(g, x, kind=0, grid=(N, H, W), M=c.Cout, Nc=c.Cs, s=1, pad=1, KW=3, gw=gw.view(-1), gb=gb,
+                    Nreal=c.Cin)
+            return
+        self.side.wait_stream(torch.cuda.current_stream(self.device))    # g and x are ready
+        with torch.cuda.stream(self.side):
+            K.wgrad(g, x, kind=0, grid=(N, H, W), M=c.Cout, Nc=c.Cs, s=1, pad=1, KW=3, gw=gw.view(-1), gb=gb,
+                    Nreal=c.Cin)
+        # keep g and x alive until join(): once the compute stream has waited for the side stream their
+        # memory is reused in order (record_stream would instead hold the blocks out of the caching
+        # allocator until an event query, forcing fresh allocations every step: measured 8x slower)
+        self._keep.extend((g, x))
+        self._side_pending = True
+
+    def join(self):
+        """End of a block's backward: the compute stream waits for the side-stream weight gradients,
+        then the block's parameters are announced ready."""
+        if self._side_pending:
+            torch.cuda.current_stream(self.device).wait_stream(self.side)
+            self._side_pending = False
+            self._keep = []
+        pending, self._ready_pending = self._ready_pending, []
+        if pending:
+            self._notify(pending)
 
     def deconv_fwd(self, d: _Deconv, x: torch.Tensor, out: torch.Tensor):
         N, h, w = x.shape[:3]
@@ -281,6 +310,12 @@ class HipBlocks:
         return dx
 
     def ready(self, mods):
+        if self._side_pending:          # some of these gradients may still be in flight on the side stream
+            self._ready_pending.extend(mods)
+            return
+        self._notify(mods)
+
+    def _notify(self, mods):
         by_space = {}
         for m in mods:
             if m is None:
@@ -408,13 +443,14 @@ class _EncFn(torch.autograd.Function):
         else:
             K.pool_bwd(skip, dskip, dpooled, g2)
         g2 = B.bn_bwd(c2, g2, st2)
+        B.conv_wgrad(c2, g2, a)                  # side stream: overlaps the dgrad chain
         g1, st_g = B.conv_dgrad(c2, g2, mask=a, below=c1)
-        B.conv_wgrad(c2, g2, a)
         B.ready([c2.mod, c2.bn])
         g1 = B.bn_bwd(c1, g1, st1, stats=st_g)
-        gx = B.conv_dgrad(c1, g1) if ctx.x_needs_grad else None
         B.conv_wgrad(c1, g1, x)
+        gx = B.conv_dgrad(c1, g1) if ctx.x_needs_grad else None
         B.ready([c1.mod, c1.bn])
+        B.join()
         ctx.st = None
         return None, (None if gx is None else _o(gx)), None, None
 
@@ -439,13 +475,14 @@ class _MidFn(torch.autograd.Function):
         st1, st2 = ctx.st
         c1, c2 = B.mid_convs
         g2 = B.bn_bwd(c2, _v(g2), st2)
-        g1, st_g = B.conv_dgrad(c2, g2, mask=a, below=c1)
         B.conv_wgrad(c2, g2, a)
+        g1, st_g = B.conv_dgrad(c2, g2, mask=a, below=c1)
         B.ready([c2.mod, c2.bn])
         g1 = B.bn_bwd(c1, g1, st1, stats=st_g)
-        gx = B.conv_dgrad(c1, g1)
         B.conv_wgrad(c1, g1, x)
+        gx = B.conv_dgrad(c1, g1)
         B.ready([c1.mod, c1.bn])
+        B.join()
         ctx.st = None
         return None, _o(gx), None
 
@@ -500,17 +537,18 @@ class _DecFn(torch.autograd.Function):
         c1, c2 = B.dec_convs[i]
         C = d.Cout
         g2 = B.bn_bwd(c2, _v(g2), st2)
-        g1, st_g = B.conv_dgrad(c2, g2, mask=a, below=c1)
         B.conv_wgrad(c2, g2, a)
+        g1, st_g = B.conv_dgrad(c2, g2, mask=a, below=c1)
         B.ready([c2.mod, c2.bn])
         g1 = B.bn_bwd(c1, g1, st1, stats=st_g)
-        dskip, gup = B.conv_dgrad_split(c1, g1, C)
         B.conv_wgrad(c1, g1, cat)
+        dskip, gup = B.conv_dgrad_split(c1, g1, C)
         B.ready([c1.mod, c1.bn])
         if isinstance(d, _Up):
             gup = K.up2_bwd(gup)          # to the projection's (low) resolution
         dx = B.deconv_bwd(d, gup, x)
         B.ready([d.mod])
+        B.join()
         ctx.st = None
         if ctx.crop is not None:     # gradient of the crop: zero outside the kept window
             Hs, Ws, top, left = ctx.crop

@@ -78,6 +78,8 @@ USE_HALO = os.environ.get("DPA_NO_HALO", "0") != "1"
 # row-streaming conv3x3 (weights resident, 4-row LDS ring); DPA_NO_STREAM=1 disables
 USE_STREAM = os.environ.get("DPA_NO_STREAM", "0") != "1"
 USE_GLDS = os.environ.get("DPA_NO_GLDS", "0") != "1"
+# conv weight gradients on a side HIP stream, overlapping each block's dgrad chain (models/hip_unet.py)
+SIDE_WGRAD = os.environ.get("DPA_NO_SIDE_WGRAD", "0") != "1"
 # row-streaming weight-gradient tile override (csrc/halo.hip dpa_wgrad_stream cfg; 0 = auto)
 WGRAD_STREAM_CFG = int(os.environ.get("DPA_WGRAD_STREAM_CFG", "0"))
 HALO_CFG = int(os.environ.get("DPA_HALO_CFG", "0"))    # 0 = auto (csrc/halo.hip dpa_igemm_halo)
