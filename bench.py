@@ -47,6 +47,9 @@ def parse():
                          "process, mp runs --stages stages on cuda:0 (pipeline rehearsal)")
     ap.add_argument("--microbatches", type=int, default=8)
     ap.add_argument("--stages", type=int, default=2, help="mp with one process: stages on the local device")
+    ap.add_argument("--infer", action="store_true",
+                    help="inference throughput instead of training: eval-mode forward to the probability map "
+                         "(BatchNorm folded into the convs), no loss/backward/optimizer")
     return ap.parse_args()
 
 
@@ -122,8 +125,15 @@ def main():
         from distributedpytorch_amd.trainer import GraphedStep
         graphed = GraphedStep(strat, *pool[0])
 
+    if a.infer:
+        assert not mp and world == 1, "--infer: single device"
+        strat.model.eval()
+
     def step(i):
         x, t = pool[i % len(pool)]
+        if a.infer:
+            with torch.no_grad():
+                return strat.compute.probs(x).mean()
         return graphed(x, t) if graphed is not None else strat.train_step(x, t)
 
     t_w0 = time.perf_counter()
@@ -157,14 +167,14 @@ def main():
     value = imgs / elapsed
     ms = 1000.0 * elapsed / a.steps
     vs = None
-    if STOCK_BASELINE_PER_GPU:
+    if STOCK_BASELINE_PER_GPU and not a.infer:
         vs = round(value / (STOCK_BASELINE_PER_GPU * world), 4)
     if mp:
         par = f"mp{world if world > 1 else a.stages}x{a.microbatches}mb" + ("" if world > 1 else "-1gpu")
     else:
         par = f"dp{world}"
     out = {
-        "metric": BASELINE_METRIC, "value": round(value, 2), "unit": "images/s", "n_gpus": world,
+        "metric": BASELINE_METRIC if not a.infer else "images/sec inference UNet 512x512 bf16 (eval forward)", "value": round(value, 2), "unit": "images/s", "n_gpus": world,
         "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
         "scaling": "strong" if mp else "weak", "vs_baseline": vs, "dtype": "bf16",
         "data": "synthetic (GPU-generated images + ellipse masks), random-init weights",

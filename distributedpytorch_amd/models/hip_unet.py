@@ -126,6 +126,8 @@ class HipBlocks:
         self._side_pending = False
         self._ready_pending = []
         self._keep = []
+        self._fold_cache = {}      # eval-mode BN folds: id(conv) -> (key, packed weights, bias)
+        self._bn_stats_version = 0
 
     # ------------------------------------------------------------------ weight packing
     def _build_packing(self):
@@ -198,7 +200,16 @@ class HipBlocks:
             K.igemm(x, self.wf(c), y, Ngemm=c.Cout, Kpad=c.Kf, KH=3, KW=3, stride=1, pad=1, Cs=c.Cs,
                     out_grid=(N, H, W), bias=c.mod.bias, relu=True, pool=pool, pcode=pcode)
             return y
+        if not self.model.training and K.FOLD_BN_EVAL and c.bn.track_running_stats and c.bn.running_mean is not None:
+            # inference: BatchNorm with running statistics is a per-channel affine map -> folded into
+            # the conv's weights and bias, so Conv2d+BN+ReLU(+pool) is ONE fused kernel, as without BN
+            wpk, bias = self._folded(c)
+            K.igemm(x, wpk, y, Ngemm=c.Cout, Kpad=c.Kf, KH=3, KW=3, stride=1, pad=1, Cs=c.Cs,
+                    out_grid=(N, H, W), bias=bias, relu=True, pool=pool, pcode=pcode)
+            return y
         z = torch.empty(N, H, W, c.Cout, dtype=torch.bfloat16, device=x.device)
+        if self.model.training:
+            self._bn_stats_version += 1                 # running statistics move (eval fold cache)
         stats = [] if self.model.training else None    # batch statistics from the conv epilogue
         K.igemm(x, self.wf(c), z, Ngemm=c.Cout, Kpad=c.Kf, KH=3, KW=3, stride=1, pad=1, Cs=c.Cs, out_grid=(N, H, W),
                 bias=c.mod.bias, relu=False, bn_stats=stats)
@@ -206,6 +217,29 @@ class HipBlocks:
         if st is not None:
             st.append((z, saved))
         return y
+
+    @torch.no_grad()
+    def _folded(self, c: _Conv):
+        """(packed bf16 weights, fp32 bias) of conv ``c`` with its eval-mode BatchNorm folded in:
+        W' = W * s, b' = (b - running_mean) * s + beta, s = gamma / sqrt(running_var + eps).  Recomputed
+        Cached until the weights (flat-space version), the running statistics (a training-mode forward
+        of this engine, or an in-place write such as load_state_dict) or the affine parameters change."""
+        bn = c.bn
+        key = (self._packed_version, self._bn_stats_version, bn.running_mean._version, bn.running_var._version,
+               bn.weight._version, bn.bias._version)
+        hit = self._fold_cache.get(id(c))
+        if hit is not None and hit[0] == key:
+            return hit[1], hit[2]
+        scale = bn.weight.float() / torch.sqrt(bn.running_var.float() + bn.eps)
+        w = (c.mod.weight.float() * scale.view(-1, 1, 1, 1)).contiguous()
+        b0 = c.mod.bias.float() if c.mod.bias is not None else torch.zeros_like(scale)
+        bias = ((b0 - bn.running_mean.float()) * scale + bn.bias.float()).contiguous()
+        packed = torch.zeros(c.Cout * c.Kf, dtype=torch.bfloat16, device=w.device)
+        d = K.PackDesc(w.data_ptr(), 0, 0, c.Cout, c.Cin, c.Cs, c.Cout, c.Kf)
+        descs = torch.frombuffer(bytearray(bytes(d)), dtype=torch.uint8).to(w.device)
+        K.pack_weights(packed, descs, 1, c.Cout * c.Kf)
+        self._fold_cache[id(c)] = (key, packed, bias)
+        return packed, bias
 
     def bn_bwd(self, c: _Conv, g: torch.Tensor, st, stats: list = None):
         """gradient w.r.t. the conv output: identity without BN, BatchNorm backward with it (``stats``:

@@ -87,6 +87,8 @@ HALO_CFG = int(os.environ.get("DPA_HALO_CFG", "0"))    # 0 = auto (csrc/halo.hip
 USE_FUSED_HEAD = os.environ.get("DPA_NO_FUSED_HEAD", "0") != "1"
 # BatchNorm batch statistics in the producing streaming conv's epilogue; DPA_NO_FUSED_BN=1 disables
 USE_FUSED_BN = os.environ.get("DPA_NO_FUSED_BN", "0") != "1"
+# eval-mode BatchNorm folded into the preceding conv's weights/bias (models/hip_unet.py); DPA_NO_FOLD_BN=1 disables
+FOLD_BN_EVAL = os.environ.get("DPA_NO_FOLD_BN", "0") != "1"
 
 
 def _extent_bytes(N, H, W, C, ld):

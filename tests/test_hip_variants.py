@@ -314,3 +314,66 @@ def test_bn_backward_partials_fused_in_stream_dgrad(hip_lib, N, H, W, C1, C2):
     assert torch.allclose(dba, dbb, rtol=1e-5, atol=1e-4)
     assert torch.allclose(dga, dgb, rtol=2e-2, atol=2e-2 * dgb.abs().max().item())
     assert _rel(dza, dzb) < 2e-2
+
+
+def test_eval_bn_folded_into_conv(hip_lib, monkeypatch):
+    """Inference of the BN DoubleConv model: with running statistics, BatchNorm folds into the conv
+    (one fused conv+bias+ReLU(+pool) kernel per layer).  Probabilities match the unfolded HIP path and
+    the torch fp32 model in eval mode."""
+    from distributedpytorch_amd.compute import make_compute
+    from distributedpytorch_amd.models.unet import build_model
+    from distributedpytorch_amd.ops import kernels as K
+    torch.manual_seed(2)
+    ref = build_model("unet-bn")
+    with torch.no_grad():
+        for m in ref.modules():
+            if isinstance(m, torch.nn.BatchNorm2d):
+                m.running_mean.uniform_(-0.2, 0.2)
+                m.running_var.uniform_(0.5, 2.0)
+                m.weight.uniform_(0.5, 1.5)
+                m.bias.uniform_(-0.3, 0.3)
+    ref.eval()
+    hip = build_model("unet-bn")
+    hip.load_state_dict(ref.state_dict())
+    hip = hip.cuda().eval()
+    comp = make_compute(hip, backend="hip", dtype="bf16")
+    x = torch.rand(2, 3, 64, 128)
+    with torch.no_grad():
+        p_ref = ref(x)
+        p_fold = comp.probs(x.cuda()).cpu()
+        monkeypatch.setattr(K, "FOLD_BN_EVAL", False)
+        p_unfold = comp.probs(x.cuda()).cpu()
+    assert (p_fold - p_ref).abs().max().item() < 3e-2
+    assert (p_fold - p_unfold).abs().max().item() < 2e-2
+
+
+def test_eval_bn_fold_cache_follows_running_stats(hip_lib, monkeypatch):
+    """The folded eval weights are cached; a training-mode forward (running statistics move) and a
+    load_state_dict (in-place writes) must both invalidate them."""
+    from distributedpytorch_amd.compute import make_compute
+    from distributedpytorch_amd.models.unet import build_model
+    from distributedpytorch_amd.ops import kernels as K
+    torch.manual_seed(3)
+    model = build_model("unet-bn").cuda()
+    comp = make_compute(model, backend="hip", dtype="bf16")
+    x = torch.rand(2, 3, 64, 128, device="cuda")
+    t = (torch.rand(2, 1, 64, 128, device="cuda") > 0.5).float()
+
+    def both():
+        with torch.no_grad():
+            monkeypatch.setattr(K, "FOLD_BN_EVAL", True)
+            a = comp.probs(x).cpu()
+            monkeypatch.setattr(K, "FOLD_BN_EVAL", False)
+            b = comp.probs(x).cpu()
+        return (a - b).abs().max().item()
+
+    model.eval()
+    assert both() < 2e-2                       # fills the cache
+    model.train()
+    with torch.no_grad():
+        comp.forward_partials(x * 3.0 + 1.0, t)   # shifts every BN layer's running statistics
+    model.eval()
+    assert both() < 2e-2
+    sd = {k: (v * 1.5 if k.endswith("running_var") else v) for k, v in model.state_dict().items()}
+    model.load_state_dict(sd)
+    assert both() < 2e-2
