@@ -33,7 +33,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=128, help="images per GPU per step (HBM: ~30 GB of 288 at 128)")
+    ap.add_argument("--batch", type=int, default=256,
+                    help="images per GPU per step (HBM: ~58 GB of 288 at 256; 128 -> ~29 GB, ~1%% lower img/s)")
     ap.add_argument("--img", type=int, default=512)
     ap.add_argument("--backend", choices=["hip", "torch", "auto"], default="auto")
     ap.add_argument("--model", default="unet")
