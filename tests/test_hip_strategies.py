@@ -173,3 +173,28 @@ def test_native_dp_comm_single_device(hip_lib):
     with pytest.raises(AssertionError):
         c.all_reduce([x.cpu()])
     c.close()
+
+
+@pytest.mark.parametrize("extra", [[], ["--infer"], ["--parallelism", "mp", "--stages", "2", "--microbatches", "2"]])
+def test_bench_json_contract(hip_lib, extra):
+    """bench.py prints ONE JSON line with the fields the round driver reads (metric, value, unit,
+    n_gpus, steps, warmup, ms_per_step, higher_is_better, scaling, vs_baseline, dtype, data, config)."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--steps", "2", "--warmup", "1", "--batch", "4",
+                        "--img", "128"] + extra, capture_output=True, text=True, timeout=300, cwd=root)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config"):
+        assert k in out, k
+    assert out["n_gpus"] == 1 and out["steps"] == 2 and out["warmup"] == 1 and out["dtype"] == "bf16"
+    assert out["value"] > 0 and out["higher_is_better"] is True
+    assert abs(out["value"] - 4 * 1000.0 / out["ms_per_step"]) < 0.02 * out["value"]
+    assert out["config"]["global_batch"] == 4
+    assert out["scaling"] == ("strong" if "mp" in extra else "weak")
