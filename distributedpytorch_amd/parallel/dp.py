@@ -54,7 +54,7 @@ class ReplicatedDataParallel:
                 self.comm = dp_comm.DPComm(self.devices)
                 self.comm.broadcast([s.data for s in self.spaces], root=0)
                 for s in self.spaces:
-                    s.version += 1
+                    s.touch()
 
     # ------------------------------------------------------------------ forward
     def _parallel(self, fn, args_per_dev):
