@@ -1,0 +1,44 @@
+"""torch.library ops (ops/library.py): CPU reference path, fake (meta) shapes, and on a GPU the HIP
+kernels against the plain-torch fp32 op."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+import distributedpytorch_amd.ops.library  # noqa: F401  (registers torch.ops.dpa.*)
+
+
+def test_cpu_reference_and_fake_shapes():
+    torch.manual_seed(0)
+    x = torch.randn(2, 5, 9, 12)
+    w = torch.randn(32, 5, 3, 3) * 0.1
+    b = torch.randn(32)
+    y = torch.ops.dpa.conv3x3(x, w, b, True)
+    assert torch.allclose(y, F.relu(F.conv2d(x, w, b, padding=1)), atol=1e-5)
+    assert torch.allclose(torch.ops.dpa.max_pool2x2(y), F.max_pool2d(y, 2, 2))
+    p = torch.rand(2, 1, 8, 8).clamp(0.01, 0.99)
+    t = (torch.rand(2, 1, 8, 8) > 0.5).float()
+    ref = F.binary_cross_entropy(p, t) - torch.log(2 * (p * t).sum() / (p.sum() + t.sum() + 1e-15))
+    assert torch.allclose(torch.ops.dpa.bce_dice_loss(p, t), ref, atol=1e-5)
+    from torch._subclasses.fake_tensor import FakeTensorMode
+    with FakeTensorMode():
+        fx = torch.empty(2, 5, 9, 12)
+        assert torch.ops.dpa.conv3x3(fx, torch.empty(32, 5, 3, 3), None, False).shape == (2, 32, 9, 12)
+        assert torch.ops.dpa.max_pool2x2(torch.empty(2, 32, 9, 12)).shape == (2, 32, 4, 6)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("N,Cin,Cout,H,W", [(2, 3, 32, 64, 128), (1, 32, 64, 64, 64), (2, 64, 64, 33, 40),
+                                            (1, 256, 256, 16, 16)])
+def test_hip_ops_match_torch(hip_lib, N, Cin, Cout, H, W):
+    torch.manual_seed(1)
+    x = torch.rand(N, Cin, H, W)
+    w = torch.randn(Cout, Cin, 3, 3) * (2.0 / (9 * Cin)) ** 0.5
+    b = torch.randn(Cout) * 0.1
+    ref = F.relu(F.conv2d(x.bfloat16().float(), w.bfloat16().float(), b, padding=1))
+    y = torch.ops.dpa.conv3x3(x.cuda(), w.cuda(), b.cuda(), True)
+    torch.cuda.synchronize()
+    assert y.dtype == torch.bfloat16 and y.shape == ref.shape
+    err = (y.float().cpu() - ref).abs().max() / ref.abs().max()
+    assert err < 2e-2, err
+    p = torch.ops.dpa.max_pool2x2(y)
+    assert torch.equal(p.float().cpu(), F.max_pool2d(y.float().cpu(), 2, 2))
