@@ -285,11 +285,11 @@ def wgrad(A: torch.Tensor, B: torch.Tensor, *, kind: int, grid, M: int, Nc: int,
             if kind == 0:
                 cfg = 1 if Nc <= 16 else (3 if M % 64 == 0 else 2)
             elif kind == 1:
-                cfg = 12 if (M % 64 == 0 and Nc >= 64) else 11
+                cfg = 14 if (M % 64 == 0 and Nc % 128 == 0) else (12 if (M % 64 == 0 and Nc >= 64) else 11)
             else:
                 cfg = 22 if (M % 64 == 0 and Nc >= 64) else 21
-        bm, bn = {1: (32, 16), 2: (32, 32), 3: (64, 32), 4: (64, 64), 11: (32, 32), 12: (64, 64), 21: (32, 32),
-                  22: (64, 64)}[cfg]
+        bm, bn = {1: (32, 16), 2: (32, 32), 3: (64, 32), 4: (64, 64), 11: (32, 32), 12: (64, 64), 13: (128, 64),
+                  14: (64, 128), 21: (32, 32), 22: (64, 64)}[cfg]
     tiles = (M // bm) * (-(-Nc // bn))
     assert gw.dtype == torch.float32 and gw.is_contiguous() and gw.numel() == M * Nreal * T
     L = _lib.lib()

@@ -149,7 +149,8 @@ def test_conv3x3_glds(hip_lib, N, H, W, Cin, Cout, var):
     assert _rel(_nchw(dx), dref) < 2e-2
 
 
-@pytest.mark.parametrize("N,h,w,Cin,Cout", [(2, 5, 7, 64, 32), (1, 4, 4, 512, 256), (2, 8, 8, 128, 64)])
+@pytest.mark.parametrize("N,h,w,Cin,Cout", [(2, 5, 7, 64, 32), (1, 4, 4, 512, 256), (2, 8, 8, 128, 64),
+                                          (2, 7, 9, 256, 128), (1, 33, 17, 512, 256)])
 def test_deconv_fwd_into_concat(hip_lib, N, h, w, Cin, Cout):
     from distributedpytorch_amd.ops import kernels as K
     torch.manual_seed(2)
@@ -219,7 +220,8 @@ def test_conv3x3_wgrad(hip_lib, N, H, W, Cin, Cout, cin_pad, path):
     assert _rel(gb.cpu() - 0.5, br.grad) < 1e-2
 
 
-@pytest.mark.parametrize("N,h,w,Cin,Cout", [(2, 5, 7, 64, 32), (1, 4, 4, 512, 256), (2, 8, 8, 128, 64)])
+@pytest.mark.parametrize("N,h,w,Cin,Cout", [(2, 5, 7, 64, 32), (1, 4, 4, 512, 256), (2, 8, 8, 128, 64),
+                                          (2, 7, 9, 256, 128), (1, 33, 17, 512, 256)])
 def test_deconv_wgrad(hip_lib, N, h, w, Cin, Cout):
     from distributedpytorch_amd.ops import kernels as K
     torch.manual_seed(5)

@@ -40,6 +40,7 @@ def main():
     ap.add_argument("--gvar", type=int, nargs="*", default=[], help="LDS-DMA (glds) kernel configs to time")
     ap.add_argument("--hvar", type=int, nargs="*", default=[], help="row-halo kernel configs to time")
     ap.add_argument("--wsvar", type=int, nargs="*", default=[], help="row-streaming wgrad tile configs to time")
+    ap.add_argument("--dwcfg", type=int, nargs="*", default=[], help="transposed-conv wgrad tile configs to time")
     ap.add_argument("--paths", default="stream,halo,generic", help="default paths to time")
     ap.add_argument("--layout-probe", action="store_true",
                     help="full-res memory-bound ops on concat halves (ld=2C) vs dense tensors (ld=C)")
@@ -138,6 +139,15 @@ def main():
                     print(f"{name:14s} {kind:5s} {label:8s} {t:9.1f} us {flops / t / 1e6:7.1f} TF", flush=True)
                 except Exception as e:
                     print(f"{name:14s} {kind:5s} {label:8s}  n/a ({str(e)[:40]})", flush=True)
+        gw = torch.zeros(Cin * Cout * 4, device=dev)
+        gb = torch.zeros(Cout, device=dev)
+        for c in [0] + a.dwcfg:
+            try:
+                t = timeit(lambda: K.wgrad(cat[..., Cout:], x, kind=1, grid=(B, h, h), M=Cout, Nc=Cin, s=2, pad=0, KW=2,
+                                           gw=gw, gb=gb, Nreal=Cin, cfg=c), a.reps)
+                print(f"{name:14s} wgrad cfg{c:<5d} {t:9.1f} us {flops / t / 1e6:7.1f} TF", flush=True)
+            except Exception as e:
+                print(f"{name:14s} wgrad cfg{c:<5d}  n/a ({str(e)[:40]})", flush=True)
 
 
 if __name__ == "__main__":
