@@ -844,14 +844,22 @@ static int launch_igemm_stream(const IgemmArgs& a, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
+// auto variant (measured at batch 128, tools/kbench.py --svar): 128-pixel strips where the LDS fits
+// them (Cs = Ngemm = 64 included: 8 waves, 140 KB, 10-20% over 64-pixel strips), 64-pixel strips
+// when the row width does not divide by 128
+static int stream_auto_variant(const IgemmArgs& a) {
+  int v;
+  if (a.Cs == 32 && a.Ngemm == 32) v = 1;
+  else if (a.Cs == 64 && a.Ngemm == 32) v = 2;
+  else v = 3;                                  // Ngemm = 64 with Cs = 32 or 64
+  if ((v == 1 || v == 3) && a.Wo % 128) v += 1;
+  return v;
+}
+
 // blocks the streaming launch of `a` (variant 0) uses -- rows of the fused head's slab
 DPA_API int dpa_igemm_stream_blocks(const IgemmArgs* args) {
   const IgemmArgs& a = *args;
-  int variant;
-  if (a.Cs == 32 && a.Ngemm == 32) variant = 1;
-  else if (a.Cs == 64 && a.Ngemm == 32) variant = 2;
-  else if (a.Cs == 32 && a.Ngemm == 64) variant = 3;
-  else variant = 4;
+  const int variant = stream_auto_variant(a);
   const int bp = (variant == 1 || variant == 3) ? 128 : 64;
   if (a.Wo % bp) return 0;
   const long blocks32 = (long)a.N * ((a.Ho + 31) / 32) * (a.Wo / bp);
@@ -868,13 +876,7 @@ DPA_API int dpa_igemm_stream(const IgemmArgs* args, int variant, hipStream_t st)
       a.Hs != a.Ho || a.Ws != a.Wo || a.Wo % 64 || a.Kpad < 9 * a.Cs || (a.pool && (a.ldp & 3)))
     return (int)hipErrorInvalidValue;
   if (a.Cs == 8 && a.Ngemm == 32 && !a.pool && a.Wo % 128 == 0) return launch_igemm_stream8<128, 32>(a, st);
-  if (variant == 0) {
-    // LDS decides the occupancy: CS=64 rings are twice as large -> narrower strips / more waves
-    if (a.Cs == 32 && a.Ngemm == 32) variant = 1;
-    else if (a.Cs == 64 && a.Ngemm == 32) variant = 2;
-    else if (a.Cs == 32 && a.Ngemm == 64) variant = 3;
-    else variant = 4;
-  }
+  if (variant == 0) variant = stream_auto_variant(a);
   const int bp = (variant == 1 || variant == 3) ? 128 : 64;
   if (a.Wo % bp) return (int)hipErrorInvalidValue;
   const long blocks32 = (long)a.N * ((a.Ho + 31) / 32) * (a.Wo / bp);
