@@ -71,46 +71,53 @@ DPA_API int dpa_maxpool2(const bf16_t* x, int ldx, bf16_t* y, int ldy, int N, in
   return (int)hipGetLastError();
 }
 
-// Max-pool backward from window codes (even H, W): one thread per (pixel, 8 channels), so the
-// full-resolution streams (dskip in, g out) are read/written as contiguous 16-B pieces; the
-// window code and dpool (a quarter of the pixels) come through the cache.
+// Max-pool backward from window codes (even H, W): one thread per (2x2 window, 8 channels).  The
+// window's code and dpool are loaded once for its 4 pixels, all 4 dskip loads are issued before
+// any math (4 independent 16-B loads in flight per lane), and the index math is one div chain per
+// window.  A wave covers 64/CC consecutive windows of one pooled row: each of its loads/stores
+// touches full 64-B runs of the two full-resolution rows.
 //   g[p][c] = (dskip[p][c] + (argmax(window)[c] == q(p) ? dpool[window][c] : 0)) * mask_q(p)[c]
 __global__ __launch_bounds__(256) void pool_bwd_code_kernel(const unsigned char* __restrict__ code,
                                                             const bf16_t* __restrict__ dskip, int ldd,
                                                             const bf16_t* __restrict__ dpool, int ldp,
                                                             bf16_t* __restrict__ g, int ldg, int N, int H, int W, int C) {
   const int CC = C >> 3, Ho = H >> 1, Wo = W >> 1;
-  const unsigned tot = (unsigned)N * H * W * CC;
+  const unsigned tot = (unsigned)N * Ho * Wo * CC;
   for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < tot; i += gridDim.x * blockDim.x) {
-    const unsigned cc = i % CC, p = i / CC;
-    const unsigned w = p % W, nh = p / W, h = nh % H, n = nh / H;
-    const unsigned win = (n * Ho + (h >> 1)) * Wo + (w >> 1);
-    const unsigned q = (h & 1) * 2 + (w & 1);
+    const unsigned cc = i % CC, win = i / CC;
+    const unsigned ow = win % Wo, noh = win / Wo;          // noh = n * Ho + oh
+    const size_t p00 = (size_t)noh * 2 * W + 2 * ow;        // (n*H + 2*oh) * W + 2*ow
+    const size_t pix[4] = {p00, p00 + 1, p00 + W, p00 + W + 1};
     const uint2 cw = *reinterpret_cast<const uint2*>(code + (size_t)win * C + cc * 8);
     const uint4 dp = *reinterpret_cast<const uint4*>(dpool + (size_t)win * ldp + cc * 8);
-    uint4 ds = make_uint4(0u, 0u, 0u, 0u);
-    if (dskip) ds = *reinterpret_cast<const uint4*>(dskip + (size_t)p * ldd + cc * 8);
-    const unsigned* pd = &dp.x;
-    const unsigned* ps = &ds.x;
-    unsigned o[4];
+    uint4 ds[4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const unsigned c2 = (k < 2 ? cw.x : cw.y) >> (16 * (k & 1));   // codes of channels 2k, 2k+1
-      const unsigned cl = c2 & 0xffu, ch = (c2 >> 8) & 0xffu;
-      float lo = lo_bf(ps[k]) + ((cl & 3u) == q ? lo_bf(pd[k]) : 0.f);
-      float hi = hi_bf(ps[k]) + ((ch & 3u) == q ? hi_bf(pd[k]) : 0.f);
-      lo = (cl >> (2 + q)) & 1u ? lo : 0.f;
-      hi = (ch >> (2 + q)) & 1u ? hi : 0.f;
-      o[k] = pack_bf2(lo, hi);
+    for (int q = 0; q < 4; ++q)
+      ds[q] = dskip ? *reinterpret_cast<const uint4*>(dskip + pix[q] * ldd + cc * 8) : make_uint4(0u, 0u, 0u, 0u);
+    const unsigned* pd = &dp.x;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const unsigned* ps = &ds[q].x;
+      unsigned o[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const unsigned c2 = (k < 2 ? cw.x : cw.y) >> (16 * (k & 1));   // codes of channels 2k, 2k+1
+        const unsigned cl = c2 & 0xffu, ch = (c2 >> 8) & 0xffu;
+        float lo = lo_bf(ps[k]) + ((cl & 3u) == (unsigned)q ? lo_bf(pd[k]) : 0.f);
+        float hi = hi_bf(ps[k]) + ((ch & 3u) == (unsigned)q ? hi_bf(pd[k]) : 0.f);
+        lo = (cl >> (2 + q)) & 1u ? lo : 0.f;
+        hi = (ch >> (2 + q)) & 1u ? hi : 0.f;
+        o[k] = pack_bf2(lo, hi);
+      }
+      *reinterpret_cast<uint4*>(g + pix[q] * ldg + cc * 8) = make_uint4(o[0], o[1], o[2], o[3]);
     }
-    *reinterpret_cast<uint4*>(g + (size_t)p * ldg + cc * 8) = make_uint4(o[0], o[1], o[2], o[3]);
   }
 }
 DPA_API int dpa_pool_bwd_code(const unsigned char* code, const bf16_t* dskip, int ldd, const bf16_t* dpool, int ldp,
                               bf16_t* g, int ldg, int N, int H, int W, int C, hipStream_t st) {
   if ((C & 7) || (ldd & 7) || (ldp & 7) || (ldg & 7) || (H & 1) || (W & 1)) return (int)hipErrorInvalidValue;
-  const long tot = (long)N * H * W * (C / 8);
-  if (tot >= (1l << 31)) return (int)hipErrorInvalidValue;
+  const long tot = (long)N * (H / 2) * (W / 2) * (C / 8);
+  if ((long)N * H * W * (C / 8) >= (1l << 31)) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(pool_bwd_code_kernel, dim3(dpa_grid(tot, 256, 16384)), dim3(256), 0, st, code, dskip, ldd, dpool, ldp, g,
                      ldg, N, H, W, C);
   return (int)hipGetLastError();
