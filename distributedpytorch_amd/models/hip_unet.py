@@ -272,22 +272,27 @@ class HipBlocks:
                 out_grid=(N, H, W), y2=hi, split=split)
         return lo, hi
 
+    def _side_launch(self, fn, *keep: torch.Tensor):
+        """Run ``fn`` (a weight-gradient launch reading ``keep``) on the side stream when there is one:
+        weight gradients are off the critical path (nothing in the backward reads them before the
+        optimizer), so they overlap the dgrad chain of the compute stream."""
+        if self.side is None:
+            fn()
+            return
+        self.side.wait_stream(torch.cuda.current_stream(self.device))    # the operands are ready
+        with torch.cuda.stream(self.side):
+            fn()
+        # keep the operands alive until join(): once the compute stream has waited for the side stream
+        # their memory is reused in order (record_stream would instead hold the blocks out of the
+        # caching allocator until an event query, forcing fresh allocations every step: measured 8x slower)
+        self._keep.extend(keep)
+        self._side_pending = True
+
     def conv_wgrad(self, c: _Conv, g: torch.Tensor, x: torch.Tensor):
         N, H, W = g.shape[:3]
         gw, gb = _grad(c.mod.weight), _grad(c.mod.bias)
-        if self.side is None:
-            K.wgrad(g, x, kind=0, grid=(N, H, W), M=c.Cout, Nc=c.Cs, s=1, pad=1, KW=3, gw=gw.view(-1), gb=gb,
-                    Nreal=c.Cin)
-            return
-        self.side.wait_stream(torch.cuda.current_stream(self.device))    # g and x are ready
-        with torch.cuda.stream(self.side):
-            K.wgrad(g, x, kind=0, grid=(N, H, W), M=c.Cout, Nc=c.Cs, s=1, pad=1, KW=3, gw=gw.view(-1), gb=gb,
-                    Nreal=c.Cin)
-        # keep g and x alive until join(): once the compute stream has waited for the side stream their
-        # memory is reused in order (record_stream would instead hold the blocks out of the caching
-        # allocator until an event query, forcing fresh allocations every step: measured 8x slower)
-        self._keep.extend((g, x))
-        self._side_pending = True
+        self._side_launch(lambda: K.wgrad(g, x, kind=0, grid=(N, H, W), M=c.Cout, Nc=c.Cs, s=1, pad=1, KW=3,
+                                          gw=gw.view(-1), gb=gb, Nreal=c.Cin), g, x)
 
     def join(self):
         """End of a block's backward: the compute stream waits for the side-stream weight gradients,
@@ -327,21 +332,22 @@ class HipBlocks:
 
     def deconv_wgrad(self, d: _Deconv, gup: torch.Tensor, x: torch.Tensor):
         N, h, w = x.shape[:3]
+        gw, gb = _grad(d.mod.weight).view(-1), _grad(d.mod.bias)
         if isinstance(d, _Up):
-            K.wgrad(gup, x, kind=2, grid=(N, h, w), M=d.Cout, Nc=d.Cin, s=1, pad=0, KW=1,
-                    gw=_grad(d.mod.weight).view(-1), gb=_grad(d.mod.bias), Nreal=d.Cin)
+            self._side_launch(lambda: K.wgrad(gup, x, kind=2, grid=(N, h, w), M=d.Cout, Nc=d.Cin, s=1, pad=0, KW=1,
+                                              gw=gw, gb=gb, Nreal=d.Cin), gup, x)
             return
-        K.wgrad(gup, x, kind=1, grid=(N, h, w), M=d.Cout, Nc=d.Cin, s=2, pad=0, KW=2, gw=_grad(d.mod.weight).view(-1),
-                gb=_grad(d.mod.bias), Nreal=d.Cin)
+        self._side_launch(lambda: K.wgrad(gup, x, kind=1, grid=(N, h, w), M=d.Cout, Nc=d.Cin, s=2, pad=0, KW=2,
+                                          gw=gw, gb=gb, Nreal=d.Cin), gup, x)
 
     def deconv_bwd(self, d, gup: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
         """dgrad + weight gradient of the up-path layer; the full-resolution transposed convs run
-        both in one pass over (gup, x) (csrc/deconv.hip)."""
+        both in one pass over (gup, x) (csrc/deconv.hip).  Elsewhere the weight gradient goes to the
+        side stream first, then the dgrad runs on the compute stream."""
         if isinstance(d, _Deconv) and K.USE_FUSED_DECONV and (d.Cin, d.Cout) in K.DECONV_BWD_SHAPES:
             return K.deconv_bwd_fused(gup, x, self.wd(d), _grad(d.mod.weight).view(-1), _grad(d.mod.bias))
-        dx = self.deconv_dgrad(d, gup, x)
         self.deconv_wgrad(d, gup, x)
-        return dx
+        return self.deconv_dgrad(d, gup, x)
 
     def ready(self, mods):
         if self._side_pending:          # some of these gradients may still be in flight on the side stream
