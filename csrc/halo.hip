@@ -21,7 +21,30 @@
 // kernel): ROWS = 2 stages 4 input rows + the weights for twice the MFMAs of ROWS = 1.
 // (BC/WC) x (BP/WP) waves: 4, or 8 for the 128-channel tile (one staging of the input rows serves
 // all 128 output channels -- the dgrads into 128 channels from 64 have only 2 K-slices to amortise it).
-template <int BP, int BC, int WP, int WC, int ROWS = 1>
+//
+// DPP = true: the kernel is LDS-read bound (each pixel fragment feeds only TC MFMAs), so the three
+// kw taps of a kernel row share ONE read of the pixel fragments: kw = 1, 2 are the kw = 0 fragments
+// shifted by 1, 2 pixels inside each 16-lane row (the MFMA B layout puts pixels along lane & 15),
+// built with row_shl DPP moves whose vacated lanes take the head of the next fragment (row_ror):
+// TP + 1 ds_read_b128 per (kh, row) instead of 3 * TP.  Measured (kbench --hvar 4 8 5 9 7 10, batch
+// 128): within -5..+1% of the LDS-read versions on every UNet shape, so the fragment reads are not
+// what bounds this kernel (the per-slice staging barrier is); kept as cfg 8-10, not auto.
+// B-fragment lanes l: pixel (l & 15), channel chunk (l >> 4).  Result lane i = cur[i + KW] for
+// i + KW < 16, else nxt[i + KW - 16].
+template <int KW>
+__device__ __forceinline__ bf16x8_t shift_px(const bf16x8_t cur, const bf16x8_t nxt) {
+  const u32x4_t c = __builtin_bit_cast(u32x4_t, cur), n = __builtin_bit_cast(u32x4_t, nxt);
+  u32x4_t o;
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    // row_ror:(16-KW): lane i <- n[(i + KW) & 15]; row_shl:KW: lane i <- c[i + KW], invalid lanes keep old
+    const int nr = __builtin_amdgcn_mov_dpp((int)n[d], 0x120 + (16 - KW), 0xf, 0xf, false);
+    o[d] = (unsigned)__builtin_amdgcn_update_dpp(nr, (int)c[d], 0x100 + KW, 0xf, 0xf, false);
+  }
+  return __builtin_bit_cast(bf16x8_t, o);
+}
+
+template <int BP, int BC, int WP, int WC, int ROWS = 1, bool DPP = false>
 __global__ __launch_bounds__(64 * (BC / WC) * (BP / WP)) void igemm_halo_kernel(IgemmArgs a) {
   constexpr int HR = BP + 2;              // pixels per halo row
   constexpr int PROWS = (ROWS + 2) * HR;  // staged pixel rows (64 B = 32 channels each)
@@ -109,6 +132,52 @@ __global__ __launch_bounds__(64 * (BC / WC) * (BP / WP)) void igemm_halo_kernel(
     __syncthreads();
     if (s + 1 < S) sload(s + 1);
     __builtin_amdgcn_sched_barrier(0);
+    if constexpr (DPP) {
+      const int chunk = lane >> 4;
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh) {
+        bf16x8_t af[3][TC];
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw)
+#pragma unroll
+          for (int ic = 0; ic < TC; ++ic) {
+            const int r = wc * WC + ic * 16 + (lane & 15);
+            af[kw][ic] = *reinterpret_cast<const bf16x8_t*>(Wimg + r * WRB + (kh * 3 + kw) * 64 +
+                                                             (swz_nk<32>(r, chunk) << 4));
+          }
+#pragma unroll
+        for (int rr = 0; rr < ROWS; ++rr) {
+          bf16x8_t fr[TP + 1];   // fr[TP]: only its lanes 0-1 of each row (the right halo) are used
+#pragma unroll
+          for (int ip = 0; ip <= TP; ++ip) {
+            const int r = (kh + rr) * HR + wp * WP + ip * 16 + (lane & 15);
+            fr[ip] = *reinterpret_cast<const bf16x8_t*>(Pimg + r * 64 + (swz_nk<32>(r, chunk) << 4));
+          }
+          bf16x8_t b1[TP], b2[TP];
+#pragma unroll
+          for (int ip = 0; ip < TP; ++ip) {
+            b1[ip] = shift_px<1>(fr[ip], fr[ip + 1]);
+            b2[ip] = shift_px<2>(fr[ip], fr[ip + 1]);
+          }
+          // kw outer: consecutive MFMAs hit different accumulators
+#pragma unroll
+          for (int ic = 0; ic < TC; ++ic)
+#pragma unroll
+            for (int ip = 0; ip < TP; ++ip)
+              acc[rr][ic][ip] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0][ic], fr[ip], acc[rr][ic][ip], 0, 0, 0);
+#pragma unroll
+          for (int ic = 0; ic < TC; ++ic)
+#pragma unroll
+            for (int ip = 0; ip < TP; ++ip)
+              acc[rr][ic][ip] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1][ic], b1[ip], acc[rr][ic][ip], 0, 0, 0);
+#pragma unroll
+          for (int ic = 0; ic < TC; ++ic)
+#pragma unroll
+            for (int ip = 0; ip < TP; ++ip)
+              acc[rr][ic][ip] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[2][ic], b2[ip], acc[rr][ic][ip], 0, 0, 0);
+        }
+      }
+    } else
     // ---- 9 taps x (TC x TP) MFMAs from LDS
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap) {
@@ -174,16 +243,17 @@ __global__ __launch_bounds__(64 * (BC / WC) * (BP / WP)) void igemm_halo_kernel(
   }
 }
 
-template <int BP, int BC, int WP, int WC, int ROWS = 1>
+template <int BP, int BC, int WP, int WC, int ROWS = 1, bool DPP = false>
 static int launch_igemm_halo(const IgemmArgs& a, hipStream_t st) {
   const int grid = a.N * ((a.Ho + ROWS - 1) / ROWS) * (a.Wo / BP) * (a.Ngemm / BC);
-  hipLaunchKernelGGL((igemm_halo_kernel<BP, BC, WP, WC, ROWS>), dim3(grid), dim3(64 * (BC / WC) * (BP / WP)), 0, st, a);
+  hipLaunchKernelGGL((igemm_halo_kernel<BP, BC, WP, WC, ROWS, DPP>), dim3(grid), dim3(64 * (BC / WC) * (BP / WP)), 0, st, a);
   return (int)hipGetLastError();
 }
 
 // Returns hipErrorInvalidValue (nothing launched) when the shape is not eligible; the caller then
 // uses dpa_igemm.  cfg: 0 auto, 1: 256x32, 2: 128x64, 3: 128x32, 4: 128x64 two rows, 5: 128x32 two rows,
-// 6: 128x128 two rows 8 waves (4 ch x 2 px), 7: 128x128 two rows 8 waves (2 ch x 4 px)
+// 6: 128x128 two rows 8 waves (4 ch x 2 px), 7: 128x128 two rows 8 waves (2 ch x 4 px),
+// 8 / 9 / 10: cfg 4 / 5 / 7 with DPP-shifted pixel fragments (one LDS read per kernel row)
 DPA_API int dpa_igemm_halo(const IgemmArgs* args, int cfg, hipStream_t st) {
   const IgemmArgs& a = *args;
   if (a.mode != 0 || a.KH != 3 || a.KW != 3 || a.stride != 1 || a.pad != 1 || (a.Cs % 32) || (a.ldx & 7) ||
@@ -205,6 +275,9 @@ DPA_API int dpa_igemm_halo(const IgemmArgs* args, int cfg, hipStream_t st) {
     case 5: if (a.Wo % 128 || a.Ngemm % 32) break; return launch_igemm_halo<128, 32, 32, 32, 2>(a, st);
     case 6: if (a.Wo % 128 || a.Ngemm % 128) break; return launch_igemm_halo<128, 128, 64, 32, 2>(a, st);
     case 7: if (a.Wo % 128 || a.Ngemm % 128) break; return launch_igemm_halo<128, 128, 32, 64, 2>(a, st);
+    case 8: if (a.Wo % 128 || a.Ngemm % 64) break; return launch_igemm_halo<128, 64, 64, 32, 2, true>(a, st);
+    case 9: if (a.Wo % 128 || a.Ngemm % 32) break; return launch_igemm_halo<128, 32, 32, 32, 2, true>(a, st);
+    case 10: if (a.Wo % 128 || a.Ngemm % 128) break; return launch_igemm_halo<128, 128, 32, 64, 2, true>(a, st);
     default: break;
   }
   return (int)hipErrorInvalidValue;

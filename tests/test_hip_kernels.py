@@ -484,7 +484,9 @@ def test_stream_conv_fused_head(hip_lib, N, H, W):
 
 @pytest.mark.parametrize("N,H,W,Cin,Cout,hcfg", [
     (2, 5, 128, 64, 128, 4), (1, 4, 128, 128, 64, 4), (2, 3, 128, 32, 64, 5), (1, 7, 256, 256, 128, 4),
-    (2, 5, 128, 64, 128, 2), (2, 5, 128, 64, 128, 6), (1, 3, 128, 128, 128, 7), (2, 4, 256, 128, 256, 6)])
+    (2, 5, 128, 64, 128, 2), (2, 5, 128, 64, 128, 6), (1, 3, 128, 128, 128, 7), (2, 4, 256, 128, 256, 6),
+    (2, 5, 128, 64, 128, 8), (1, 4, 128, 128, 64, 8), (2, 3, 128, 32, 64, 9), (1, 7, 256, 256, 128, 8),
+    (1, 3, 128, 128, 128, 10), (2, 5, 256, 32, 32, 9)])
 def test_conv3x3_halo_two_rows(hip_lib, N, H, W, Cin, Cout, hcfg):
     """Row-halo conv with two output rows per block (one weight staging per slice for both; odd
     heights -> the last block's second row is masked): forward with bias+ReLU and masked dgrad."""
@@ -503,10 +505,11 @@ def test_conv3x3_halo_two_rows(hip_lib, N, H, W, Cin, Cout, hcfg):
     F.conv2d(xr, w, padding=1).backward(g)
     packed_d, ngd, kpd = _pack_one(1, w)
     dx = torch.empty(N, H, W, Cin, dtype=torch.bfloat16, device="cuda")
-    if (Cin % 64 == 0 or hcfg == 5) and (hcfg < 6 or Cin % 128 == 0):
+    bc = {2: 64, 4: 64, 5: 32, 6: 128, 7: 128, 8: 64, 9: 32, 10: 128}[hcfg]   # output-channel tile
+    if Cin % bc == 0:
         K.igemm(_nhwc(g), packed_d, dx, Ngemm=ngd, Kpad=kpd, KH=3, KW=3, stride=1, pad=1, Cs=Cout,
                 out_grid=(N, H, W), mask=_nhwc(x), path="halo", variant=hcfg)
     torch.cuda.synchronize()
     assert _rel(_nchw(y), ref) < 2e-2
-    if (Cin % 64 == 0 or hcfg == 5) and (hcfg < 6 or Cin % 128 == 0):
+    if Cin % bc == 0:
         assert _rel(_nchw(dx), xr.grad * (x > 0)) < 2e-2
