@@ -70,6 +70,8 @@ def _pack_one(mode, w, cin_pad=None):
     (1, 37, 128, 64, 32, "stream"), (1, 4, 256, 64, 32, "halo"),
     (1, 3, 128, 32, 64, "stream"), (1, 3, 128, 32, 64, "halo"),
     (2, 20, 128, 64, 64, "stream"),
+    # rows narrower than the 128-pixel strip: the 64-pixel variant of the same channel pair
+    (2, 5, 64, 32, 32, "stream"), (1, 3, 64, 32, 64, "stream"), (1, 6, 192, 64, 64, "stream"),
     (2, 2, 128, 64, 128, "auto"),
     (2, 5, 128, 3, 32, "stream"),          # first layer (8 padded channels) streaming kernel
     (1, 34, 256, 3, 32, "auto"),
@@ -97,7 +99,8 @@ def test_conv3x3_fwd(hip_lib, N, H, W, Cin, Cout, cfg):
 @pytest.mark.parametrize("N,H,W,Cin,Cout,path", [
     (2, 13, 18, 32, 64, "auto"), (1, 8, 8, 256, 128, "auto"), (2, 16, 16, 64, 32, "auto"),
     (2, 3, 256, 32, 32, "stream"), (1, 3, 256, 64, 32, "halo"), (1, 2, 128, 32, 64, "stream"),
-    (1, 35, 128, 64, 64, "stream"), (2, 3, 256, 32, 32, "generic")])
+    (1, 35, 128, 64, 64, "stream"), (2, 3, 256, 32, 32, "generic"), (2, 5, 64, 32, 32, "stream"),
+    (1, 4, 192, 64, 64, "stream")])
 def test_conv3x3_dgrad_masked(hip_lib, N, H, W, Cin, Cout, path):
     from distributedpytorch_amd.ops import kernels as K
     torch.manual_seed(1)
