@@ -161,6 +161,11 @@ def main():
     if world > 1:
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
     elapsed = float(el.item())
+    if mp and world > 1:  # the loss lives on the last pipeline stage; rank 0 prints it
+        lt = (loss.detach().float().reshape(1) if loss is not None
+              else torch.zeros(1, device=device))
+        dist.broadcast(lt, src=world - 1)
+        loss = lt
     final_loss = float(loss.item()) if loss is not None else float("nan")
 
     # dp: every rank trains its own --batch images (weak scaling); mp: the N ranks share one batch

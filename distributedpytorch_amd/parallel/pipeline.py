@@ -174,12 +174,28 @@ class GPipeDist:
         """channels_last on GPU (matches what the backends produce)."""
         return torch.channels_last if self.device.type == "cuda" else torch.contiguous_format
 
+    def _empty_wire(self, shape):
+        """(tensor, flat): a logical-NCHW receive buffer in the stage layout and the 1-D contiguous
+        view of its storage that goes on the wire (gloo and RCCL both take a dense 1-D buffer; a
+        channels_last 4-D tensor is rejected by gloo as non-contiguous)."""
+        n, c, hh, ww = shape
+        flat = torch.empty(n * c * hh * ww, dtype=self.comm_dtype, device=self.device)
+        if self._recv_layout() == torch.channels_last:
+            return flat.view(n, hh, ww, c).permute(0, 3, 1, 2), flat
+        return flat.view(n, c, hh, ww), flat
+
+    def _wire(self, t):
+        """Send side: ``t`` in the stage layout, flattened in storage order (a view when dense)."""
+        t = t.detach().to(self.comm_dtype).contiguous(memory_format=self._recv_layout())
+        if self._recv_layout() == torch.channels_last:
+            return t.permute(0, 2, 3, 1).reshape(-1)
+        return t.reshape(-1)
+
     def _irecv(self, mb, h, w):
         bufs, works = {}, []
         for name, src in self.recv_spec[self.rank]:
-            shp = self._shape(name, mb, h, w)
-            t = torch.empty(shp, dtype=self.comm_dtype, device=self.device, memory_format=self._recv_layout())
-            works.append(dist.irecv(t, src=self._glob(src), group=self.group))
+            t, flat = self._empty_wire(self._shape(name, mb, h, w))
+            works.append(dist.irecv(flat, src=self._glob(src), group=self.group))
             bufs[name] = t
         return bufs, works
 
@@ -219,7 +235,7 @@ class GPipeDist:
                 for name, dst in self.send_spec[self.rank]:
                     t = out[name]
                     sends[name] = t
-                    buf = t.detach().to(self.comm_dtype)
+                    buf = self._wire(t)
                     pending_sends.append((dist.isend(buf, dst=self._glob(dst), group=self.group), buf))
                 saved_out.append(sends)
 
@@ -239,9 +255,8 @@ class GPipeDist:
                 outs, grads, works = [], [], []
                 for name, dst in self.send_spec[self.rank]:
                     t = saved_out[m][name]
-                    g = torch.empty(t.shape, dtype=self.comm_dtype, device=self.device,
-                                    memory_format=self._recv_layout())
-                    works.append(dist.irecv(g, src=self._glob(dst), group=self.group))
+                    g, flat = self._empty_wire(t.shape)
+                    works.append(dist.irecv(flat, src=self._glob(dst), group=self.group))
                     outs.append(t)
                     grads.append(g)
                 for wk in works:
@@ -254,7 +269,7 @@ class GPipeDist:
                     gr = saved_in[m][name].grad
                     if gr is None:
                         gr = torch.zeros_like(saved_in[m][name])
-                    buf = gr.to(self.comm_dtype).contiguous(memory_format=self._recv_layout())
+                    buf = self._wire(gr)
                     pending_sends.append((dist.isend(buf, dst=self._glob(src), group=self.group), buf))
         for wk, _ in pending_sends:
             wk.wait()
@@ -275,9 +290,9 @@ class GPipeDist:
         sends = []
         if not self.is_last:
             for name, dst in self.send_spec[self.rank]:
-                buf = out[name].to(self.comm_dtype).contiguous(memory_format=self._recv_layout())
-                sends.append(dist.isend(buf, dst=self._glob(dst), group=self.group))
-        for wk in sends:
+                buf = self._wire(out[name])
+                sends.append((dist.isend(buf, dst=self._glob(dst), group=self.group), buf))
+        for wk, _ in sends:
             wk.wait()
         return out.get("probs")
 
@@ -296,7 +311,7 @@ class GPipeDist:
                 elif self.rank == s:
                     dist.send(params[n].detach().contiguous(), dst=self._glob(0), group=self.group)
                 elif self.rank == 0:
-                    t = torch.empty_like(params[n])
+                    t = torch.empty(params[n].shape, dtype=params[n].dtype, device=params[n].device)
                     dist.recv(t, src=self._glob(s), group=self.group)
                     sd[n] = t
         if self.rank == 0:

@@ -198,3 +198,31 @@ def test_bench_json_contract(hip_lib, extra):
     assert abs(out["value"] - 4 * 1000.0 / out["ms_per_step"]) < 0.02 * out["value"]
     assert out["config"]["global_batch"] == 4
     assert out["scaling"] == ("strong" if "mp" in extra else "weak")
+
+
+@pytest.mark.parametrize("extra", [[], ["--parallelism", "mp", "--microbatches", "2"]])
+def test_bench_two_ranks_same_device(hip_lib, extra):
+    """Rehearsal of the multi-rank bench path on one GPU: torchrun with 2 ranks sharing cuda:0 over
+    gloo (DPA_SAME_DEVICE=1) - DDP bucketed all-reduce of HIP-engine gradients, and GPipe send/recv of
+    channels_last activations/skips (flattened in storage order on the wire)."""
+    import json
+    import os
+    import socket
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, DPA_SAME_DEVICE="1", DPA_DIST_BACKEND="gloo")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(root, "bench.py"),
+                        "--gpus", "2", "--steps", "2", "--warmup", "1", "--batch", "4", "--img", "128"] + extra,
+                       capture_output=True, text=True, timeout=300, cwd=root, env=env)
+    assert r.returncode == 0, (r.stdout[-1500:], r.stderr[-3000:])
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["value"] > 0
+    assert out["config"]["global_batch"] == (4 if extra else 8)
+    assert out["final_loss"] is not None and out["final_loss"] == out["final_loss"]
