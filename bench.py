@@ -193,6 +193,10 @@ def main():
         "final_loss": round(final_loss, 5) if final_loss == final_loss else None, "warmup_s": round(warm_s, 2),
         "peak_mem_gb": round(torch.cuda.max_memory_allocated(device) / 2 ** 30, 2),
     }
+    red = getattr(strat, "reducer", None)
+    if red is not None and world > 1:  # rank 0's last step: all-reduce time not hidden behind backward
+        c = red.exposed_comm_ms()
+        out["exposed_comm_ms_last_step"] = round(c, 3) if c is not None else None
     if rank == 0:
         line = json.dumps(out)
         print(line, flush=True)

@@ -103,9 +103,27 @@ class BucketedAllReduce:
         while self.next_launch < len(self.buckets):
             self._launch(self.next_launch)
             self.next_launch += 1
+        timed = self.space.grad.is_cuda and bool(self.works)
+        if timed:
+            ev0 = torch.cuda.Event(enable_timing=True)
+            ev0.record()
         for w in self.works:
             w.wait()
+        if timed:
+            ev1 = torch.cuda.Event(enable_timing=True)
+            ev1.record()
+            self._exposed = (ev0, ev1)
         self.reset()
+
+    def exposed_comm_ms(self) -> Optional[float]:
+        """Exposed (non-overlapped) all-reduce time of the last step: how long the compute stream
+        stalled after the backward waiting for the outstanding buckets (HIP events around the
+        stream-level waits; synchronises on the second event, so call it at logging points only)."""
+        ev = getattr(self, "_exposed", None)
+        if ev is None:
+            return None
+        ev[1].synchronize()
+        return float(ev[0].elapsed_time(ev[1]))
 
     def all_reduce_now(self):
         """No-hook path: reduce the whole flat buffer bucket by bucket (used after a fused backward)."""

@@ -407,8 +407,10 @@ def train(cfg: TrainConfig):
                     mean_loss = float(np.mean(vals[-10:]))
                     pending = []
                     curves.add_train(step, time.time() - t_start, mean_loss)
+                    red = getattr(strat, "reducer", None)
+                    comm_ms = red.exposed_comm_ms() if red is not None else None
                     metrics.log(kind="train", step=step, epoch=epoch, loss=mean_loss,
-                                lr=strat.optimizer.param_groups[0]["lr"])
+                                lr=strat.optimizer.param_groups[0]["lr"], exposed_comm_ms=comm_ms)
                     if strat.is_main:
                         log.info(f"step {step} loss {mean_loss:.5f}")
                 stop_signal = _agree_stop(strat, guard.requested)

@@ -226,3 +226,5 @@ def test_bench_two_ranks_same_device(hip_lib, extra):
     assert out["n_gpus"] == 2 and out["value"] > 0
     assert out["config"]["global_batch"] == (4 if extra else 8)
     assert out["final_loss"] is not None and out["final_loss"] == out["final_loss"]
+    if not extra:  # DDP: the reducer timed the stall on outstanding all-reduce buckets
+        assert out["exposed_comm_ms_last_step"] is not None and out["exposed_comm_ms_last_step"] >= 0
