@@ -122,7 +122,8 @@ class HipBlocks:
         # conv weight gradients on a second HIP stream: nothing in the backward consumes them, so a
         # block's wgrads overlap its dgrad chain (filling each kernel's tail); the block's end joins
         # the streams and only then announces its gradients (DDP buckets see finished values)
-        self.side = torch.cuda.Stream(device=self.device) if K.SIDE_WGRAD else None
+        self.side = (torch.cuda.Stream(device=self.device, priority=K.SIDE_PRIORITY)
+                     if K.SIDE_WGRAD else None)
         self._side_pending = False
         self._ready_pending = []
         self._keep = []

@@ -80,6 +80,9 @@ USE_STREAM = os.environ.get("DPA_NO_STREAM", "0") != "1"
 USE_GLDS = os.environ.get("DPA_NO_GLDS", "0") != "1"
 # conv weight gradients on a side HIP stream, overlapping each block's dgrad chain (models/hip_unet.py)
 SIDE_WGRAD = os.environ.get("DPA_NO_SIDE_WGRAD", "0") != "1"
+# HIP stream priority of the weight-gradient side stream (torch convention: lower = higher priority,
+# 0 = the default stream's priority)
+SIDE_PRIORITY = int(os.environ.get("DPA_SIDE_PRIORITY", "0"))
 # row-streaming weight-gradient tile override (csrc/halo.hip dpa_wgrad_stream cfg; 0 = auto)
 WGRAD_STREAM_CFG = int(os.environ.get("DPA_WGRAD_STREAM_CFG", "0"))
 HALO_CFG = int(os.environ.get("DPA_HALO_CFG", "0"))    # 0 = auto (csrc/halo.hip dpa_igemm_halo)
