@@ -39,6 +39,8 @@ def parse():
     ap.add_argument("--backend", choices=["hip", "torch", "auto"], default="auto")
     ap.add_argument("--model", default="unet")
     ap.add_argument("--bucket-mb", type=float, default=8.0)
+    ap.add_argument("--grad-comm-dtype", choices=["fp32", "bf16"], default="fp32",
+                    help="N>1: gradient all-reduce wire dtype")
     ap.add_argument("--pool", type=int, default=2, help="distinct synthetic batches cycled")
     ap.add_argument("--out", default=None, help="also append the JSON line to this file")
     ap.add_argument("--graph", action="store_true", help="N=1: replay the step from a captured HIP graph")
@@ -105,6 +107,7 @@ def main():
     method = "MP" if mp else ("DDP" if world > 1 else "singleGPU")
     cfg = TrainConfig(train_method=method, batch_size=a.batch, img_size=(a.img, a.img), dtype="bf16",
                       backend=a.backend, model=a.model, bucket_mb=a.bucket_mb, lr=1e-4,
+                      grad_comm_dtype=a.grad_comm_dtype,
                       microbatches=a.microbatches, stages=a.stages)
     model = build_model(a.model)
     nparams = count_params(model)
@@ -189,6 +192,7 @@ def main():
                    "per_gpu_batch": a.batch if not mp else a.batch // max(1, world),
                    "seq_len": a.img * a.img, "image_hw": [a.img, a.img],
                    "parallelism": par, "backend": backend, "bucket_mb": a.bucket_mb,
+                   "grad_comm_dtype": a.grad_comm_dtype,
                    "hip_graph": graphed is not None},
         "final_loss": round(final_loss, 5) if final_loss == final_loss else None, "warmup_s": round(warm_s, 2),
         "peak_mem_gb": round(torch.cuda.max_memory_allocated(device) / 2 ** 30, 2),

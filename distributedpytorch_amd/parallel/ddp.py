@@ -31,8 +31,12 @@ from ..utils.tracing import trace_range
 
 class BucketedAllReduce:
     def __init__(self, space: FlatParameterSpace, bucket_mb: float = 8.0, first_bucket_mb: float = 1.0,
-                 group=None, average: bool = True, scale: float = 1.0):
+                 group=None, average: bool = True, scale: float = 1.0, comm_dtype: str = "fp32"):
         self.space = space
+        # "bf16": each bucket travels as bf16 (half the xGMI bytes; torch's bf16_compress_hook
+        # semantics: pre-scaled, reduced in bf16, written back into the fp32 flat buffer)
+        assert comm_dtype in ("fp32", "bf16"), comm_dtype
+        self.comm_dtype = torch.bfloat16 if comm_dtype == "bf16" else None
         self.group = group
         self.world = dist.get_world_size(group)
         self.average = average
@@ -75,6 +79,7 @@ class BucketedAllReduce:
         self.pending = list(self.expected)
         self.next_launch = 0
         self.works = []
+        self._writeback = []
 
     def mark_ready(self, param_index: int):
         b = self.bucket_of[param_index]
@@ -90,6 +95,13 @@ class BucketedAllReduce:
     def _launch_bucket(self, b: int):
         s, e, _, _ = self.buckets[b]
         t = self.space.grad[s:e]
+        if self.comm_dtype is not None:
+            f = (1.0 / self.world if self.average else 1.0) * self.scale
+            c = (t * f).to(self.comm_dtype)
+            w = dist.all_reduce(c, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+            self.works.append(w)
+            self._writeback.append((t, c))
+            return
         if self.nccl and self.average and self.scale == 1.0:
             w = dist.all_reduce(t, op=dist.ReduceOp.AVG, group=self.group, async_op=True)
         else:
@@ -109,6 +121,8 @@ class BucketedAllReduce:
             ev0.record()
         for w in self.works:
             w.wait()
+        for t, c in self._writeback:
+            t.copy_(c)
         if timed:
             ev1 = torch.cuda.Event(enable_timing=True)
             ev1.record()

@@ -126,7 +126,8 @@ class DDPStrategy(SingleDevice):
         self.is_main = self.rank == 0
         broadcast_parameters(self.space, src=0)
         scale = float(self.world) if cfg.global_dice else 1.0
-        self.reducer = BucketedAllReduce(self.space, bucket_mb=cfg.bucket_mb, scale=scale).register_hooks()
+        self.reducer = BucketedAllReduce(self.space, bucket_mb=cfg.bucket_mb, scale=scale,
+                                         comm_dtype=cfg.grad_comm_dtype).register_hooks()
 
     def lr_scale(self):
         # reference: Adam(lr * world_size) (utils/train_utils.py:199) - with the real world size (A6)

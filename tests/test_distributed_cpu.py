@@ -40,7 +40,7 @@ def _data(n, seed, hw=32):
     return x, t
 
 
-def _ddp_worker(rank, world, port, bucket_mb, q):
+def _ddp_worker(rank, world, port, bucket_mb, q, comm="fp32"):
     _init(rank, world, port)
     from distributedpytorch_amd.config import TrainConfig
     from distributedpytorch_amd.trainer import DDPStrategy
@@ -48,7 +48,8 @@ def _ddp_worker(rank, world, port, bucket_mb, q):
     if rank == 1:   # different init on purpose: DDP must broadcast rank 0's parameters
         for p in model.parameters():
             p.data.add_(1.0)
-    cfg = TrainConfig(train_method="DDP", backend="torch", dtype="fp32", lr=1e-3, bucket_mb=bucket_mb)
+    cfg = TrainConfig(train_method="DDP", backend="torch", dtype="fp32", lr=1e-3, bucket_mb=bucket_mb,
+                      grad_comm_dtype=comm)
     st = DDPStrategy(cfg, model, "cpu")
     x, t = _data(4, seed=10 + rank)
     # expected: per-rank plain-autograd grads of the (broadcast) rank-0 weights, averaged
@@ -64,7 +65,10 @@ def _ddp_worker(rank, world, port, bucket_mb, q):
     loss = st.forward_loss(x, t)
     (loss * x.shape[0]).backward()      # buckets are all-reduced in place, overlapped with backward
     st.reducer.finish()
-    ok_reduce = torch.allclose(st.space.grad, expect, atol=1e-6)
+    if comm == "bf16":   # bf16 wire: relative error of a few bf16 ulps
+        ok_reduce = torch.allclose(st.space.grad, expect, rtol=2e-2, atol=1e-4 * float(expect.abs().max()))
+    else:
+        ok_reduce = torch.allclose(st.space.grad, expect, atol=1e-6)
     st.optimizer.step()
     for i in range(2):
         st.train_step(*_data(4, seed=100 + 10 * i + rank))
@@ -84,12 +88,13 @@ def _ddp_worker(rank, world, port, bucket_mb, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,bucket_mb", [(2, 0.001), (2, 8.0), (4, 0.004)])
-def test_ddp_gloo_ranks(world, bucket_mb):
+@pytest.mark.parametrize("world,bucket_mb,comm", [(2, 0.001, "fp32"), (2, 8.0, "fp32"), (4, 0.004, "fp32"),
+                                                  (2, 0.004, "bf16")])
+def test_ddp_gloo_ranks(world, bucket_mb, comm):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_ddp_worker, args=(r, world, port, bucket_mb, q)) for r in range(world)]
+    procs = [ctx.Process(target=_ddp_worker, args=(r, world, port, bucket_mb, q, comm)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=240) for _ in procs]

@@ -200,7 +200,7 @@ def test_bench_json_contract(hip_lib, extra):
     assert out["scaling"] == ("strong" if "mp" in extra else "weak")
 
 
-@pytest.mark.parametrize("extra", [[], ["--parallelism", "mp", "--microbatches", "2"]])
+@pytest.mark.parametrize("extra", [[], ["--grad-comm-dtype", "bf16"], ["--parallelism", "mp", "--microbatches", "2"]])
 def test_bench_two_ranks_same_device(hip_lib, extra):
     """Rehearsal of the multi-rank bench path on one GPU: torchrun with 2 ranks sharing cuda:0 over
     gloo (DPA_SAME_DEVICE=1) - DDP bucketed all-reduce of HIP-engine gradients, and GPipe send/recv of
@@ -224,7 +224,8 @@ def test_bench_two_ranks_same_device(hip_lib, extra):
     assert len(lines) == 1, r.stdout
     out = json.loads(lines[0])
     assert out["n_gpus"] == 2 and out["value"] > 0
-    assert out["config"]["global_batch"] == (4 if extra else 8)
+    mp_run = "mp" in extra
+    assert out["config"]["global_batch"] == (4 if mp_run else 8)
     assert out["final_loss"] is not None and out["final_loss"] == out["final_loss"]
-    if not extra:  # DDP: the reducer timed the stall on outstanding all-reduce buckets
+    if not mp_run:  # DDP: the reducer timed the stall on outstanding all-reduce buckets
         assert out["exposed_comm_ms_last_step"] is not None and out["exposed_comm_ms_last_step"] >= 0
