@@ -192,3 +192,19 @@ def test_ddp_bn_running_stats_follow_rank0():
         p.join(timeout=60)
     for rank, differed, same in res:
         assert differed and same, (rank, differed, same)
+
+
+@pytest.mark.parametrize("layout", [torch.channels_last, torch.contiguous_format])
+def test_pipeline_wire_roundtrip(layout):
+    """GPipe wire format: a stage-layout tensor flattened in storage order on the send side and the
+    receive buffer's 1-D storage view reassemble the same logical NCHW tensor in the stage layout."""
+    import types
+    from distributedpytorch_amd.parallel.pipeline import GPipeDist
+    f = types.SimpleNamespace(comm_dtype=torch.float32, device=torch.device("cpu"), _recv_layout=lambda: layout)
+    t = torch.randn(2, 5, 3, 4).contiguous(memory_format=layout)
+    wire = GPipeDist._wire(f, t)
+    assert wire.dim() == 1 and wire.is_contiguous() and wire.numel() == t.numel()
+    r, flat = GPipeDist._empty_wire(f, tuple(t.shape))
+    assert flat.dim() == 1 and flat.is_contiguous()
+    flat.copy_(wire)
+    assert torch.equal(r, t) and r.is_contiguous(memory_format=layout)
