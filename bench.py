@@ -50,6 +50,8 @@ def parse():
                          "process, mp runs --stages stages on cuda:0 (pipeline rehearsal)")
     ap.add_argument("--microbatches", type=int, default=8)
     ap.add_argument("--stages", type=int, default=2, help="mp with one process: stages on the local device")
+    ap.add_argument("--mp-cut", choices=["auto", "reference", "balanced"], default="auto",
+                    help="mp stage boundaries (auto: reference encoder|decoder cut for 2 stages, else balanced)")
     ap.add_argument("--infer", action="store_true",
                     help="inference throughput instead of training: eval-mode forward to the probability map "
                          "(BatchNorm folded into the convs), no loss/backward/optimizer")
@@ -108,7 +110,7 @@ def main():
     cfg = TrainConfig(train_method=method, batch_size=a.batch, img_size=(a.img, a.img), dtype="bf16",
                       backend=a.backend, model=a.model, bucket_mb=a.bucket_mb, lr=1e-4,
                       grad_comm_dtype=a.grad_comm_dtype,
-                      microbatches=a.microbatches, stages=a.stages)
+                      microbatches=a.microbatches, stages=a.stages, mp_cut=a.mp_cut)
     model = build_model(a.model)
     nparams = count_params(model)
     if mp and world > 1:
@@ -191,7 +193,8 @@ def main():
                    else a.model, "global_batch": a.batch * (1 if mp else world),
                    "per_gpu_batch": a.batch if not mp else a.batch // max(1, world),
                    "seq_len": a.img * a.img, "image_hw": [a.img, a.img],
-                   "parallelism": par, "backend": backend, "bucket_mb": a.bucket_mb,
+                   "parallelism": par, "backend": backend,
+                   "mp_cut": (strat.pipe.cuts if mp else None), "bucket_mb": a.bucket_mb,
                    "grad_comm_dtype": a.grad_comm_dtype,
                    "hip_graph": graphed is not None},
         "final_loss": round(final_loss, 5) if final_loss == final_loss else None, "warmup_s": round(warm_s, 2),

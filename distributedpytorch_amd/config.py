@@ -41,6 +41,7 @@ class TrainConfig:
     device: Optional[str] = None
     stages: int = 2                                  # pipeline stages for -t MP
     microbatches: int = 2                            # reference MP: split_size=B/2 -> 2 microbatches
+    mp_cut: str = "auto"                             # MP stage cut: reference | balanced | auto (reference iff 2 stages)
     bucket_mb: float = 8.0                           # DDP/DP all-reduce bucket size (MiB of fp32 grads)
     grad_comm_dtype: str = "fp32"                    # DDP gradient all-reduce wire dtype: fp32 | bf16
     global_dice: bool = False                        # DDP: Dice over the global batch (all-reduced sums)
@@ -90,6 +91,10 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--device", type=str, default=None)
     p.add_argument("--stages", type=int, default=2)
     p.add_argument("--microbatches", type=int, default=2)
+    p.add_argument("--mp-cut", choices=["auto", "reference", "balanced"], default="auto",
+                   help="MP stage boundaries: reference = encoder+mid | decoder+head (2 stages, ~34|62 GFLOP "
+                        "per image at 512^2); balanced = FLOP-balanced contiguous blocks; auto = reference for 2 "
+                        "stages, balanced otherwise")
     p.add_argument("--bucket-mb", type=float, default=8.0)
     p.add_argument("--grad-comm-dtype", choices=["fp32", "bf16"], default="fp32",
                    help="DDP: all-reduce gradient buckets in bf16 (half the bytes) instead of fp32")
@@ -123,11 +128,17 @@ def parse_args(argv=None) -> TrainConfig:
         batch_size=a.batch_size, checkpoint=a.checkpoint, seed=a.seed, img_size=img_size,
         dtype=a.dtype, backend=a.backend, model=a.model, synthetic=a.synthetic,
         synthetic_len=a.synthetic_len, data_dir=a.data_dir, out_dir=a.out_dir, device=a.device,
-        stages=a.stages, microbatches=a.microbatches, bucket_mb=a.bucket_mb, grad_comm_dtype=a.grad_comm_dtype, global_dice=a.global_dice,
+        stages=a.stages, microbatches=a.microbatches, mp_cut=a.mp_cut, bucket_mb=a.bucket_mb, grad_comm_dtype=a.grad_comm_dtype, global_dice=a.global_dice,
         loss_scale_by_batch=a.loss_scale_by_batch, max_steps=a.max_steps, num_workers=a.num_workers,
         log_every=a.log_every, resume=a.resume, profile=a.profile, trace_ranges=a.trace_ranges, cuda_graph=a.cuda_graph,
         debug_sync=a.debug_sync, watchdog=a.watchdog, comm_timeout=a.comm_timeout, nan_policy=a.nan_policy)
     return cfg
+
+
+def mp_cut_mode(cfg: "TrainConfig", stages: int) -> str:
+    if cfg.mp_cut != "auto":
+        return cfg.mp_cut
+    return "reference" if stages == 2 else "balanced"
 
 
 def dist_env():

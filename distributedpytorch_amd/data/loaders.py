@@ -13,7 +13,7 @@ from __future__ import annotations
 from typing import Iterator, Optional
 
 import torch
-from torch.utils.data import DataLoader, Dataset, random_split
+from torch.utils.data import DataLoader, Dataset, Sampler, random_split
 from torch.utils.data.distributed import DistributedSampler
 
 
@@ -23,9 +23,31 @@ def split_dataset(dataset: Dataset, val_percent: float, seed: int = 0):
     return random_split(dataset, [n_train, n_val], generator=torch.Generator().manual_seed(seed))
 
 
+class EpochShuffleSampler(Sampler):
+    """Shuffled order that is a pure function of ``(seed, epoch)``.
+
+    Used instead of ``shuffle=True`` (which draws from the process-global torch RNG): every rank
+    of a multi-process pipeline iterates its own loader - stage 0 takes the images, the last stage
+    the masks - and they pair up only if both see the same order; resuming at epoch ``e``
+    replays exactly the order an uninterrupted run would have used (reference shuffled with the
+    global RNG, ``utils/train_utils.py:41``)."""
+
+    def __init__(self, n: int, seed: int = 0):
+        self.n, self.seed, self.epoch = int(n), int(seed), 0
+
+    def set_epoch(self, epoch: int):
+        self.epoch = int(epoch)
+
+    def __len__(self):
+        return self.n
+
+    def __iter__(self):
+        g = torch.Generator().manual_seed(self.seed * 1_000_003 + self.epoch)
+        return iter(torch.randperm(self.n, generator=g).tolist())
+
+
 def build_loaders(train_set, val_set, batch_size: int, *, rank: int = 0, world_size: int = 1,
                   num_workers: int = 0, pin_memory: bool = False, seed: int = 0, drop_last: bool = False):
-    train_sampler = None
     val_sampler = None
     if world_size > 1:
         train_sampler = DistributedSampler(train_set, num_replicas=world_size, rank=rank, shuffle=True,
@@ -33,7 +55,9 @@ def build_loaders(train_set, val_set, batch_size: int, *, rank: int = 0, world_s
         if len(val_set) >= world_size:
             val_sampler = DistributedSampler(val_set, num_replicas=world_size, rank=rank, shuffle=False,
                                              drop_last=True)
-    train_loader = DataLoader(train_set, batch_size=batch_size, shuffle=train_sampler is None,
+    else:
+        train_sampler = EpochShuffleSampler(len(train_set), seed)
+    train_loader = DataLoader(train_set, batch_size=batch_size, shuffle=False,
                               sampler=train_sampler, num_workers=num_workers, pin_memory=pin_memory,
                               drop_last=drop_last, persistent_workers=num_workers > 0)
     val_loader = DataLoader(val_set, batch_size=batch_size, shuffle=False, sampler=val_sampler,

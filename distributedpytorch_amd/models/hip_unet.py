@@ -129,6 +129,9 @@ class HipBlocks:
         self._keep = []
         self._fold_cache = {}      # eval-mode BN folds: id(conv) -> (key, packed weights, bias)
         self._bn_stats_version = 0
+        # encoder levels whose skip leaves this engine (pipeline stage boundary): the second conv writes
+        # that skip into a dense tensor, which then goes on the wire as is (no concat-half copy)
+        self.dense_skips = set()
 
     # ------------------------------------------------------------------ weight packing
     def _build_packing(self):
@@ -451,8 +454,12 @@ class _EncFn(torch.autograd.Function):
         N, H, W = x.shape[:3]
         st1, st2 = [], []
         a = B.conv_fwd(c1, x, st=st1)
-        cat = B.new_cat(N, H, W, c2.Cout)
-        skip = cat[..., :c2.Cout]
+        if l in B.dense_skips:
+            cat = None
+            skip = torch.empty(N, H, W, c2.Cout, dtype=torch.bfloat16, device=x.device)
+        else:
+            cat = B.new_cat(N, H, W, c2.Cout)
+            skip = cat[..., :c2.Cout]
         pooled = torch.empty(N, H // 2, W // 2, c2.Cout, dtype=torch.bfloat16, device=x.device)
         # window codes (argmax + ReLU masks) for the backward: it then never re-reads the skip
         code = (torch.empty(N, H // 2, W // 2, c2.Cout, dtype=torch.uint8, device=x.device)
@@ -462,17 +469,20 @@ class _EncFn(torch.autograd.Function):
         ctx.x_needs_grad = l > 0
         ctx.has_code = code is not None
         ctx.st = (st1[0] if st1 else None, st2[0] if st2 else None)
-        ctx.save_for_backward(x, a, cat, code if code is not None else cat)
+        ctx.dense = cat is None
+        # the concat buffer itself is saved (not its half): it keeps the engine's weak cat map entry alive
+        own = skip if cat is None else cat
+        ctx.save_for_backward(x, a, own, code if code is not None else own)
         return _o(skip), _o(pooled)
 
     @staticmethod
     def backward(ctx, dskip, dpooled):
         B, l = ctx.B, ctx.l
-        x, a, cat, code = ctx.saved_tensors
+        x, a, own, code = ctx.saved_tensors
         st1, st2 = ctx.st
         c1, c2 = B.enc_convs[l]
         C = c2.Cout
-        skip = cat[..., :C]
+        skip = own if ctx.dense else own[..., :C]
         if dpooled is None:
             dpooled = torch.zeros(x.shape[0], x.shape[1] // 2, x.shape[2] // 2, C, dtype=torch.bfloat16, device=x.device)
         else:

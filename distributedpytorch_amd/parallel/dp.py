@@ -129,5 +129,25 @@ class ReplicatedDataParallel:
         for g in grads:
             g.copy_(total.to(g.device))
 
+    @torch.no_grad()
+    def sync_buffers(self):
+        """Replica 0's floating-point buffers (BatchNorm running statistics) to every replica."""
+        src = [b for b in self.replicas[0].buffers()]
+        for r in self.replicas[1:]:
+            for b, s in zip(r.buffers(), src):
+                b.copy_(s.to(b.device))
+
+    @torch.no_grad()
+    def sync_from_replica0(self):
+        """After replica 0's parameters were overwritten (resume): replicate them and its buffers."""
+        if self.comm is not None:
+            self.comm.broadcast([s.data for s in self.spaces], root=0)
+        else:
+            for s in self.spaces[1:]:
+                s.data.copy_(self.spaces[0].data.to(s.data.device))
+        for s in self.spaces:
+            s.touch()
+        self.sync_buffers()
+
     def state_dict(self):
         return self.module.state_dict()

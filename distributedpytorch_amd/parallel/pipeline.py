@@ -123,10 +123,23 @@ class _Stage:
 
 
 class GPipeDist:
-    """Multi-process GPipe over a process group whose size == number of stages."""
+    """Multi-process GPipe over a process group whose size == number of stages.
+
+    Communication (RCCL over xGMI, or gloo on CPU):
+    * every tensor of one microbatch that goes to / comes from the same step is posted as ONE
+      ``batch_isend_irecv`` group (RCCL group call: the x and skip transfers to different peers
+      start together instead of one ``isend`` at a time);
+    * forward receives for microbatch m+1 and backward gradient receives for microbatch m-1 are
+      posted before microbatch m computes, so transfer latency hides behind compute;
+    * every peer communicator is created at construction (a 1-element exchange with each peer),
+      so the lazy RCCL pair-communicator setup never lands inside a training step;
+    * a skip that leaves this stage is written by the encoder conv into a dense tensor (HIP engine
+      ``dense_skips``) and sent as is; activations travel in the compute dtype (bf16).
+    """
 
     def __init__(self, model, microbatches: int, backend: str = "auto", dtype: str = "bf16",
-                 group=None, cuts: Optional[List[int]] = None, img_hw=(512, 512), mode: str = "balanced"):
+                 group=None, cuts: Optional[List[int]] = None, img_hw=(512, 512), mode: str = "balanced",
+                 warm: bool = True):
         self.group = group
         self.rank = dist.get_rank(group)
         self.S = dist.get_world_size(group)
@@ -145,30 +158,52 @@ class GPipeDist:
                 p.requires_grad_(False)
         self.space = FlatParameterSpace(own, device=self.device)
         self.blocks = make_blocks(model, backend, dtype)
+        if hasattr(self.blocks, "dense_skips"):
+            self.blocks.dense_skips = {int(n[len("skip"):]) for n, _ in self.send_spec[self.rank]
+                                       if n.startswith("skip")}
         self.stage = _Stage(model, self.blocks, self.start, self.end, self.depth)
         self.comm_dtype = torch.bfloat16 if (dtype == "bf16" and self.device.type == "cuda") else torch.float32
         self.is_first = self.rank == 0
         self.is_last = self.rank == self.S - 1
         self._glob = lambda s: dist.get_global_rank(group, s) if group is not None else s
+        self._host_staged = self.device.type == "cuda" and dist.get_backend(group) != "nccl"
+        self.peers = sorted({p for _, p in self.recv_spec[self.rank]} | {p for _, p in self.send_spec[self.rank]})
+        if warm:
+            self.warm_up()
+
+    def warm_up(self):
+        """One tiny exchange with every peer stage (both directions): creates the RCCL pair
+        communicators now instead of inside the first timed step."""
+        ops, keep = [], []
+        dev = "cpu" if self._host_staged else self.device
+        for p in self.peers:
+            out = torch.full((1,), float(self.rank), dtype=self.comm_dtype, device=dev)
+            inp = torch.empty(1, dtype=self.comm_dtype, device=dev)
+            ops.append(dist.P2POp(dist.isend, out, self._glob(p), self.group))
+            ops.append(dist.P2POp(dist.irecv, inp, self._glob(p), self.group))
+            keep.append((p, inp, out))
+        for w in (dist.batch_isend_irecv(ops) if ops else []):
+            w.wait()
+        for p, inp, _ in keep:
+            assert int(inp.float().item()) == p, f"stage {self.rank}: peer {p} answered {inp.item()}"
 
     # shapes of the boundary tensors for this microbatch size
     def _shape(self, name, mb, h, w):
         cfg = self.model.cfg
         if name.startswith("skip"):
             return infer_shapes(cfg, mb, h, w)[name]
-        # "x" entering block `cut`
+        # "x" entering block `cut`: encoder levels floor-halve, the decoder doubles from the bottom
         cut = self.start
         kind, i = block_kind(cut, self.depth)
-        H, W = h, w
+        hb, wb = h >> self.depth, w >> self.depth
         if kind == "enc":
-            c = cfg.widths[i - 1]
-            return (mb, c, H >> i, W >> i)
+            return (mb, cfg.widths[i - 1], h >> i, w >> i)
         if kind == "mid":
-            return (mb, cfg.widths[-1], H >> self.depth, W >> self.depth)
+            return (mb, cfg.widths[-1], hb, wb)
         if kind == "dec":
             c = cfg.mid_width if i == 0 else cfg.widths[self.depth - i]
-            return (mb, c, H >> (self.depth - i), W >> (self.depth - i))
-        return (mb, cfg.base, H, W)
+            return (mb, c, hb << i, wb << i)
+        return (mb, cfg.base, hb << self.depth, wb << self.depth)
 
     def _recv_layout(self):
         """channels_last on GPU (matches what the backends produce)."""
@@ -191,13 +226,44 @@ class GPipeDist:
             return t.permute(0, 2, 3, 1).reshape(-1)
         return t.reshape(-1)
 
+    def _post(self, sends=(), recvs=()):
+        """One grouped P2P launch: ``sends`` = [(tensor, dst)], ``recvs`` = [(flat buffer, src)].
+        Returns a :class:`_Transfer` whose ``wait()`` completes it (and keeps the send buffers alive).
+
+        RCCL moves device memory directly (ordered after the producing kernels on the current
+        stream).  gloo (CPU tests; the one-GPU rehearsal of this path, ranks sharing cuda:0) is
+        host-staged explicitly: a device buffer is copied to host memory before the send and from
+        it after the receive completes."""
+        ops, keep, copies = [], [], []
+        for t, dst in sends:
+            buf = self._wire(t)
+            if self._host_staged:
+                buf = buf.to("cpu")                   # synchronous: the producing kernels have finished
+            keep.append(buf)
+            ops.append(dist.P2POp(dist.isend, buf, self._glob(dst), self.group))
+        for flat, src in recvs:
+            if self._host_staged:
+                host = torch.empty(flat.shape, dtype=flat.dtype)
+                copies.append((host, flat))
+                flat = host
+            ops.append(dist.P2POp(dist.irecv, flat, self._glob(src), self.group))
+        return _Transfer(dist.batch_isend_irecv(ops) if ops else [], keep, copies)
+
     def _irecv(self, mb, h, w):
-        bufs, works = {}, []
+        bufs, recvs = {}, []
         for name, src in self.recv_spec[self.rank]:
             t, flat = self._empty_wire(self._shape(name, mb, h, w))
-            works.append(dist.irecv(flat, src=self._glob(src), group=self.group))
+            recvs.append((flat, src))
             bufs[name] = t
-        return bufs, works
+        return bufs, self._post(recvs=recvs)
+
+    def _irecv_grads(self, outs: Dict[str, torch.Tensor]):
+        grads, recvs = [], []
+        for name, dst in self.send_spec[self.rank]:
+            g, flat = self._empty_wire(tuple(outs[name].shape))
+            recvs.append((flat, dst))
+            grads.append(g)
+        return grads, self._post(recvs=recvs)
 
     def train_step(self, images: Optional[torch.Tensor], targets: Optional[torch.Tensor], batch: int,
                    hw, dice: bool = True, loss_scale: float = 1.0):
@@ -208,7 +274,7 @@ class GPipeDist:
         mb = batch // M
         xs = images.chunk(M) if self.is_first else [None] * M
         ts = targets.chunk(M) if self.is_last else [None] * M
-        saved_in, saved_out, pending_sends = [], [], []
+        saved_in, saved_out, pending = [], [], []
         partials = []
         nxt = self._irecv(mb, h, w) if not self.is_first else None
         for m in range(M):
@@ -216,11 +282,10 @@ class GPipeDist:
                 env = {"x": xs[m]}
                 leaves = {}
             else:
-                bufs, works = nxt
-                for wk in works:
-                    wk.wait()
+                bufs, xfer = nxt
+                xfer.wait()
                 if m + 1 < M:
-                    nxt = self._irecv(mb, h, w)
+                    nxt = self._irecv(mb, h, w)        # microbatch m+1 lands while m computes
                 leaves = {k: v.detach().requires_grad_(True) for k, v in bufs.items()}
                 env = dict(leaves)
             with trace_range(f"stage{self.rank}_fwd_mb{m}"):
@@ -231,12 +296,8 @@ class GPipeDist:
                 partials.append(out["partials"])
                 saved_out.append({})
             else:
-                sends = {}
-                for name, dst in self.send_spec[self.rank]:
-                    t = out[name]
-                    sends[name] = t
-                    buf = self._wire(t)
-                    pending_sends.append((dist.isend(buf, dst=self._glob(dst), group=self.group), buf))
+                sends = {name: out[name] for name, _ in self.send_spec[self.rank]}
+                pending.append(self._post(sends=[(sends[n], d) for n, d in self.send_spec[self.rank]]))
                 saved_out.append(sends)
 
         # ---------------- backward (microbatches in reverse order) ----------------
@@ -246,33 +307,32 @@ class GPipeDist:
             loss = loss_from_partials(P.sum(0), targets.numel(), dice)
             (loss * loss_scale).backward()
             dP = P.grad
+        gnxt = self._irecv_grads(saved_out[M - 1]) if not self.is_last else None
         for m in reversed(range(M)):
             rng = trace_range(f"stage{self.rank}_bwd_mb{m}")
             rng.__enter__()
             if self.is_last:
                 torch.autograd.backward(partials[m], dP[m])
             else:
-                outs, grads, works = [], [], []
-                for name, dst in self.send_spec[self.rank]:
-                    t = saved_out[m][name]
-                    g, flat = self._empty_wire(t.shape)
-                    works.append(dist.irecv(flat, src=self._glob(dst), group=self.group))
-                    outs.append(t)
-                    grads.append(g)
-                for wk in works:
-                    wk.wait()
+                grads, xfer = gnxt
+                xfer.wait()
+                if m > 0:
+                    gnxt = self._irecv_grads(saved_out[m - 1])   # gradients of m-1 land while m runs
+                outs = [saved_out[m][name] for name, _ in self.send_spec[self.rank]]
                 torch.autograd.backward(outs, [g.to(o.dtype) for o, g in zip(outs, grads)])
             rng.__exit__(None, None, None)
             _debug_point(self.device)
             if not self.is_first:
+                gsends = []
                 for name, src in self.recv_spec[self.rank]:
                     gr = saved_in[m][name].grad
                     if gr is None:
                         gr = torch.zeros_like(saved_in[m][name])
-                    buf = self._wire(gr)
-                    pending_sends.append((dist.isend(buf, dst=self._glob(src), group=self.group), buf))
-        for wk, _ in pending_sends:
-            wk.wait()
+                    gsends.append((gr, src))
+                pending.append(self._post(sends=gsends))
+            saved_in[m] = saved_out[m] = None
+        for xfer in pending:
+            xfer.wait()
         return loss
 
     @torch.no_grad()
@@ -282,18 +342,12 @@ class GPipeDist:
         if self.is_first:
             env = {"x": images}
         else:
-            bufs, works = self._irecv(batch, h, w)
-            for wk in works:
-                wk.wait()
+            bufs, xfer = self._irecv(batch, h, w)
+            xfer.wait()
             env = dict(bufs)
         out = self.stage.forward(env, None, "probs")
-        sends = []
         if not self.is_last:
-            for name, dst in self.send_spec[self.rank]:
-                buf = self._wire(out[name])
-                sends.append((dist.isend(buf, dst=self._glob(dst), group=self.group), buf))
-        for wk, _ in sends:
-            wk.wait()
+            self._post(sends=[(out[n], d) for n, d in self.send_spec[self.rank]]).wait()
         return out.get("probs")
 
     def gather_state_dict(self):
@@ -309,15 +363,31 @@ class GPipeDist:
                     if self.rank == 0:
                         sd[n] = params[n].detach().clone()
                 elif self.rank == s:
-                    dist.send(params[n].detach().contiguous(), dst=self._glob(0), group=self.group)
+                    t = params[n].detach().contiguous()
+                    dist.send(t.cpu() if self._host_staged else t, dst=self._glob(0), group=self.group)
                 elif self.rank == 0:
-                    t = torch.empty(params[n].shape, dtype=params[n].dtype, device=params[n].device)
+                    dev = "cpu" if self._host_staged else params[n].device
+                    t = torch.empty(params[n].shape, dtype=params[n].dtype, device=dev)
                     dist.recv(t, src=self._glob(s), group=self.group)
-                    sd[n] = t
+                    sd[n] = t.to(params[n].device)
         if self.rank == 0:
             full = self.model.state_dict()
             return {k: sd.get(k, v) for k, v in full.items()}
         return None
+
+
+class _Transfer:
+    """Outstanding grouped P2P operations of one pipeline step phase."""
+
+    def __init__(self, works, keep, copies):
+        self.works, self.keep, self.copies = works, keep, copies
+
+    def wait(self):
+        for w in self.works:
+            w.wait()
+        for host, dev in self.copies:
+            dev.copy_(host)
+        self.works, self.keep, self.copies = [], [], []
 
 
 class GPipeLocal:

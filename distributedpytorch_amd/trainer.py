@@ -22,7 +22,7 @@ import torch
 import torch.distributed as dist
 
 from .compute import loss_from_partials, make_compute, resolve_backend
-from .config import TrainConfig, dist_env
+from .config import TrainConfig, dist_env, mp_cut_mode
 from .data import CarvanaDataset, SyntheticSegmentation, build_loaders, split_dataset
 from .data.loaders import DeviceBatcher
 from .loss import dice_score
@@ -75,6 +75,23 @@ class Strategy:
 
     def before_eval(self):
         pass
+
+    # ---- checkpoint / resume hooks
+    def spaces(self):
+        opt = getattr(self, "optimizer", None)
+        return list(getattr(opt, "spaces", []))
+
+    def after_load(self):
+        """Parameters were overwritten in place (resume / load): kernels re-pack their weights."""
+        for sp in self.spaces():
+            sp.touch()
+
+    def optimizer_state_dict(self):
+        """Optimizer state to checkpoint (collective for strategies whose state is sharded)."""
+        return self.optimizer.state_dict()
+
+    def load_optimizer_state_dict(self, sd):
+        self.optimizer.load_state_dict(sd)
 
 
 def _loss_scale(cfg, batch):
@@ -194,6 +211,19 @@ class DPStrategy(Strategy):
         for r in self.dp.replicas:
             r.train(mode)
 
+    def before_eval(self):
+        # torch.nn.DataParallel re-broadcasts device 0's buffers every forward: every replica
+        # evaluates with replica 0's BatchNorm running statistics
+        self.dp.sync_buffers()
+
+    def after_load(self):
+        # a resume loads replica 0 only; replicate its parameters and buffers to the others
+        self.dp.sync_from_replica0()
+
+    def state_dict(self):
+        self.dp.sync_buffers()
+        return self.model.state_dict()
+
     def train_step(self, images, targets):
         self.optimizer.zero_grad()
         loss = self.dp.forward_loss(images, targets)
@@ -216,7 +246,7 @@ class PipelineLocalStrategy(Strategy):
         super().__init__(cfg)
         H, W = cfg.img_size
         self.pipe = GPipeLocal(model, devices, cfg.microbatches, cfg.backend, cfg.dtype, img_hw=(H, W),
-                               mode="reference" if len(devices) == 2 else "balanced")
+                               mode=mp_cut_mode(cfg, len(devices)))
         self.model = model
         self.device = self.pipe.devices[0]
         self.optimizer = FusedAdam(self.pipe.spaces, lr=cfg.lr, weight_decay=cfg.weight_decay)
@@ -245,7 +275,7 @@ class PipelineDistStrategy(Strategy):
         self.model = model.to(self.device)
         H, W = cfg.img_size
         self.pipe = GPipeDist(self.model, cfg.microbatches, cfg.backend, cfg.dtype, img_hw=(H, W),
-                              mode="reference" if self.world == 2 else "balanced")
+                              mode=mp_cut_mode(cfg, self.world))
         self.is_main = self.pipe.is_last  # the last stage owns the loss; rank 0 saves
         self.optimizer = FusedAdam(self.pipe.space, lr=cfg.lr, weight_decay=cfg.weight_decay)
 
@@ -255,7 +285,7 @@ class PipelineDistStrategy(Strategy):
         loss = self.pipe.train_step(images, targets, B, self.cfg.img_size,
                                     loss_scale=_loss_scale(self.cfg, B))
         self.optimizer.step()
-        return loss
+        return None if loss is None else loss.detach()
 
     @torch.no_grad()
     def eval_batch(self, images, targets):
@@ -266,6 +296,17 @@ class PipelineDistStrategy(Strategy):
 
     def state_dict(self):
         return self.pipe.gather_state_dict()
+
+    def optimizer_state_dict(self):
+        """Each stage owns the Adam state of its own parameters: gather all of them to rank 0 as
+        ``{"stages": [state of stage 0, ..., state of stage S-1]}``."""
+        mine = self.optimizer.state_dict()
+        out = [None] * self.world if self.rank == 0 else None
+        dist.gather_object(mine, out, dst=0)
+        return {"stages": out} if self.rank == 0 else None
+
+    def load_optimizer_state_dict(self, sd):
+        self.optimizer.load_state_dict(sd["stages"][self.rank] if "stages" in sd else sd)
 
     def barrier(self):
         dist.barrier()
@@ -366,8 +407,9 @@ def train(cfg: TrainConfig):
     last_path = os.path.join(cfg.out_dir, "checkpoints", f"{cfg.train_method}_last.pt")
     start_epoch, step = 0, 0
     if cfg.resume and os.path.exists(last_path):
-        start_epoch, step = load_training_state(last_path, model=strat.model, optimizer=strat.optimizer,
+        start_epoch, step = load_training_state(last_path, model=strat.model, optimizer=_OptIO(strat),
                                                 scheduler=scheduler)
+        strat.after_load()
         log.info(f"resumed from {last_path} at epoch {start_epoch} step {step}")
 
     t_start = time.time()
@@ -421,9 +463,9 @@ def train(cfg: TrainConfig):
                 break
         if stop_signal is not None:
             # SIGTERM/SIGUSR1 (e.g. torchrun tearing the job down): save where we are and leave
-            sd_model = strat.state_dict()
+            sd_model, sd_opt = strat.state_dict(), strat.optimizer_state_dict()
             if strat.rank == 0 and sd_model is not None:
-                save_training_state(last_path, model=_SD(sd_model), optimizer=strat.optimizer,
+                save_training_state(last_path, model=_SD(sd_model), optimizer=_SD(sd_opt),
                                     scheduler=scheduler, epoch=epoch, step=step)
             log.warning(f"stopped by signal {stop_signal} at step {step}; state saved to {last_path}")
             break
@@ -440,9 +482,9 @@ def train(cfg: TrainConfig):
             print(f"epoch {epoch + 1}/{cfg.epochs} step {step} val_loss {val_loss:.5f} dice {val_dice:.4f} "
                   f"({n_img / max(ep_time, 1e-9):.1f} img/s/rank)", flush=True)
         if cfg.save_every_epoch:
-            sd_model = strat.state_dict()
+            sd_model, sd_opt = strat.state_dict(), strat.optimizer_state_dict()
             if strat.rank == 0 and sd_model is not None:
-                save_training_state(last_path, model=_SD(sd_model), optimizer=strat.optimizer,
+                save_training_state(last_path, model=_SD(sd_model), optimizer=_SD(sd_opt),
                                     scheduler=scheduler, epoch=epoch + 1, step=step)
         if cfg.max_steps and step >= cfg.max_steps:
             break
@@ -581,6 +623,16 @@ class _SD:
 
     def state_dict(self):
         return self._sd
+
+
+class _OptIO:
+    """Adapter: ``load_training_state`` hands the saved optimizer state to the strategy."""
+
+    def __init__(self, strat):
+        self.strat = strat
+
+    def load_state_dict(self, sd):
+        self.strat.load_optimizer_state_dict(sd)
 
 
 @torch.no_grad()
