@@ -35,7 +35,8 @@ class TrainConfig:
     backend: str = "auto"                            # hip | torch | auto
     model: str = "unet"                              # preset name (models.unet.PRESETS)
     synthetic: bool = False
-    synthetic_len: int = 64
+    synthetic_len: int = 5088                        # Carvana's size (train_hq: 5,088 images)
+    device_data: bool = True                         # synthetic data rendered once into HBM (no DataLoader/H2D)
     data_dir: str = "./data"
     out_dir: str = "."
     device: Optional[str] = None
@@ -60,6 +61,7 @@ class TrainConfig:
     watchdog: float = 0.0                            # abort if no step completes for N seconds (0 = off)
     comm_timeout: float = 1800.0                     # process-group (RCCL/gloo) collective timeout, seconds
     nan_policy: str = "raise"                        # non-finite loss: raise | warn | ignore
+    progress: Optional[bool] = None                  # tqdm bars (reference); None = only on a terminal
 
     def to_dict(self):
         return asdict(self)
@@ -85,7 +87,10 @@ def build_parser() -> argparse.ArgumentParser:
                    help="hip = hand-written MI355X kernels; torch = stock PyTorch ops")
     p.add_argument("--model", type=str, default="unet", help="model preset: unet | unet-xl | unet-bn64 | unet-bn | unet-bilinear | unet-bn-bilinear | unet-tiny | unet-tiny-bn")
     p.add_argument("--synthetic", action="store_true", help="use synthetic images/masks instead of data/")
-    p.add_argument("--synthetic-len", type=int, default=64)
+    p.add_argument("--synthetic-len", type=int, default=5088,
+                   help="synthetic dataset size (default: Carvana's 5,088 images)")
+    p.add_argument("--host-data", dest="device_data", action="store_false",
+                   help="synthetic data through the CPU Dataset/DataLoader + H2D path instead of HBM-resident")
     p.add_argument("--data-dir", type=str, default="./data")
     p.add_argument("--out-dir", type=str, default=".")
     p.add_argument("--device", type=str, default=None)
@@ -114,6 +119,9 @@ def build_parser() -> argparse.ArgumentParser:
                    help="abort (exit 124, for torchrun --max-restarts + --resume) after N s without a step")
     p.add_argument("--comm-timeout", type=float, default=1800.0, help="collective timeout in seconds")
     p.add_argument("--nan-policy", choices=["raise", "warn", "ignore"], default="raise")
+    p.add_argument("--progress", dest="progress", action="store_true", default=None,
+                   help="tqdm progress bars for training images and validation batches (default: on a terminal)")
+    p.add_argument("--no-progress", dest="progress", action="store_false")
     return p
 
 
@@ -127,11 +135,11 @@ def parse_args(argv=None) -> TrainConfig:
         train_method=a.train_method, val=a.val, load=a.load, epochs=a.epochs, lr=a.lr,
         batch_size=a.batch_size, checkpoint=a.checkpoint, seed=a.seed, img_size=img_size,
         dtype=a.dtype, backend=a.backend, model=a.model, synthetic=a.synthetic,
-        synthetic_len=a.synthetic_len, data_dir=a.data_dir, out_dir=a.out_dir, device=a.device,
+        synthetic_len=a.synthetic_len, device_data=a.device_data, data_dir=a.data_dir, out_dir=a.out_dir, device=a.device,
         stages=a.stages, microbatches=a.microbatches, mp_cut=a.mp_cut, bucket_mb=a.bucket_mb, grad_comm_dtype=a.grad_comm_dtype, global_dice=a.global_dice,
         loss_scale_by_batch=a.loss_scale_by_batch, max_steps=a.max_steps, num_workers=a.num_workers,
         log_every=a.log_every, resume=a.resume, profile=a.profile, trace_ranges=a.trace_ranges, cuda_graph=a.cuda_graph,
-        debug_sync=a.debug_sync, watchdog=a.watchdog, comm_timeout=a.comm_timeout, nan_policy=a.nan_policy)
+        debug_sync=a.debug_sync, watchdog=a.watchdog, comm_timeout=a.comm_timeout, nan_policy=a.nan_policy, progress=a.progress)
     return cfg
 
 

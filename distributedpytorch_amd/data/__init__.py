@@ -6,8 +6,10 @@ Parity target: reference ``utils/dataloading.py:12-78`` for the fol
 from .synthetic import SyntheticSegmentation, synthetic_batch
 from .folder import BasicDataset, CarvanaDataset
 from .loaders import split_dataset, build_loaders, DeviceBatcher
+from .device import DeviceSyntheticSegmentation, DeviceLoader, device_loaders
 
 __all__ = [
     "SyntheticSegmentation", "synthetic_batch", "BasicDataset", "CarvanaDataset",
     "split_dataset", "build_loaders", "DeviceBatcher",
+    "DeviceSyntheticSegmentation", "DeviceLoader", "device_loaders",
 ]

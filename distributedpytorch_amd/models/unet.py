@@ -167,13 +167,19 @@ class Decoder(nn.Module):
 class UNet(nn.Module):
     """Reference-parity UNet (unet_model.py:4-62).  ``forward(x[B,C,H,W]) -> probs[B,1,H,W]``.
 
-    The reference's ``pipe=True`` (2-GPU placement + microbatch loop inside ``forward``,
-    unet_model.py:14-53) is provided by :class:`distributedpytorch_amd.parallel.pipeline.GPipe`
-    instead of being baked into the model.
+    ``UNet(pipe=True)`` keeps the reference constructor (unet_model.py:5,14-21): encoder + mid on
+    the first device, decoder + head on the second (``cuda:0``/``cuda:1``; both stages on one device
+    when the box has a single GPU, CPU without one), and ``forward`` runs the 2-microbatch
+    pipelined schedule (unet_model.py:24-53) through
+    :class:`distributedpytorch_amd.parallel.pipeline.GPipeLocal`, returning the probabilities on
+    the first device like the reference.  ``train.py -t MP`` uses the pipeline strategies directly.
     """
 
-    def __init__(self, cfg: UNetConfig | None = None, **kw):
+    def __init__(self, cfg: UNetConfig | None = None, pipe: bool = False, devices=None, microbatches: int = 2,
+                 **kw):
         super().__init__()
+        if isinstance(cfg, bool):          # UNet(True): the reference's positional ``pipe``
+            cfg, pipe = None, cfg
         cfg = cfg or UNetConfig(**kw)
         self.cfg = cfg
         self.encoder = Encoder(cfg)
@@ -181,6 +187,16 @@ class UNet(nn.Module):
         self.decoder = Decoder(cfg)
         self.segmap = nn.Conv2d(cfg.base, cfg.out_channels, 1)
         self.sigmoid = nn.Sigmoid()
+        self.pipe = bool(pipe)
+        self._pipe = None
+        if self.pipe:
+            from ..parallel.pipeline import GPipeLocal
+            if devices is None:
+                n = torch.cuda.device_count() if torch.cuda.is_available() else 0
+                devices = ["cuda:0", "cuda:1"] if n >= 2 else (["cuda:0", "cuda:0"] if n == 1 else ["cpu", "cpu"])
+            # the pipeline is not a submodule: state_dict keys stay the reference's
+            object.__setattr__(self, "_pipe", GPipeLocal(self, devices, microbatches, backend="torch",
+                                                         dtype="fp32", mode="reference"))
 
     def logits(self, x):
         x, *skips = self.encoder(x)
@@ -189,6 +205,8 @@ class UNet(nn.Module):
         return self.segmap(x)
 
     def forward(self, x):
+        if self._pipe is not None:
+            return self._pipe.forward_probs(x)
         return self.sigmoid(self.logits(x))
 
     # ---- introspection used by the engine / pipeline partitioner ----

@@ -29,6 +29,26 @@ from ..optim import FlatParameterSpace
 from ..utils.tracing import trace_range
 
 
+def bucket_plan(space: FlatParameterSpace, bucket_mb: float = 8.0, first_bucket_mb: float = 1.0):
+    """Cut the flat gradient buffer (backward order) into contiguous buckets: a small first bucket
+    (its all-reduce starts after the first blocks' backward) then ``bucket_mb`` MiB ones.
+    Returns (buckets [(start, end, first_param, last_param_exclusive)], bucket index per param)."""
+    cap = int(bucket_mb * 2 ** 20 / 4)
+    first = int(min(first_bucket_mb, bucket_mb) * 2 ** 20 / 4)
+    buckets: List[tuple] = []
+    bucket_of: List[int] = []
+    start_p = 0
+    start = 0
+    limit = first if first > 0 else cap
+    for i, n in enumerate(space.numels):
+        end = space.offsets[i + 1]
+        bucket_of.append(len(buckets))
+        if end - start >= limit or i == len(space.numels) - 1:
+            buckets.append((start, end, start_p, i + 1))
+            start, start_p, limit = end, i + 1, cap
+    return buckets, bucket_of
+
+
 class BucketedAllReduce:
     def __init__(self, space: FlatParameterSpace, bucket_mb: float = 8.0, first_bucket_mb: float = 1.0,
                  group=None, average: bool = True, scale: float = 1.0, comm_dtype: str = "fp32"):
@@ -42,19 +62,7 @@ class BucketedAllReduce:
         self.average = average
         self.scale = scale
         self.nccl = dist.get_backend(group) == "nccl"
-        cap = int(bucket_mb * 2 ** 20 / 4)
-        first = int(min(first_bucket_mb, bucket_mb) * 2 ** 20 / 4)
-        self.buckets: List[tuple] = []   # (start, end, first_param, last_param_exclusive)
-        self.bucket_of: List[int] = []
-        start_p = 0
-        start = 0
-        limit = first if first > 0 else cap
-        for i, n in enumerate(space.numels):
-            end = space.offsets[i + 1]
-            self.bucket_of.append(len(self.buckets))
-            if end - start >= limit or i == len(space.numels) - 1:
-                self.buckets.append((start, end, start_p, i + 1))
-                start, start_p, limit = end, i + 1, cap
+        self.buckets, self.bucket_of = bucket_plan(space, bucket_mb, first_bucket_mb)
         self.expected = [b[3] - b[2] for b in self.buckets]
         self._hooks = []
         self.reset()

@@ -12,11 +12,16 @@ MI355X design (same semantics, less traffic):
 * the loss keeps the reference's *global-batch* semantics without gathering outputs (N8): each
   device produces the 4 partial loss sums of its shard, they are added on device 0 and the scalar
   loss is back-propagated through those tiny copies into every replica.
-* gradients are summed across devices with one single-process RCCL all-reduce over the flat
-  buffers: the native clique of :mod:`.dp_comm` (csrc/dp_comm.cpp: ncclCommInitAll once, then one
-  grouped ncclAllReduce per step on each device's compute stream), each device riding its own
-  xGMI links; fallbacks: ``torch.cuda.nccl.all_reduce``, then ``torch.cuda.comm`` reduce+broadcast.
-  The initial replicas are made identical with one grouped ncclBroadcast of the flat parameters.
+* gradients are summed across devices by bucketed single-process RCCL all-reduces overlapped with
+  the backward (:class:`DPBucketReducer`): the flat gradient buffers are cut into the same
+  contiguous buckets as DDP's (``ddp.bucket_plan``); the HIP backward announces finished
+  gradients block by block on every replica (``space.notify_ready``, autograd hooks for the torch
+  backend) and as soon as a bucket is final on ALL replicas one grouped ncclAllReduce over that
+  slice runs on per-device comm streams (the native clique of :mod:`.dp_comm`, csrc/dp_comm.cpp:
+  ncclCommInitAll once), each device riding its own xGMI links while the earlier (full-resolution)
+  layers' backward still computes.  The initial replicas are made identical with one grouped
+  ncclBroadcast of the flat parameters.  Without the native clique (CPU tests, same-device
+  rehearsal) the same bucket schedule sums the slices directly.
 * per-device forward runs on one host thread per device (kernel launch cost overlaps).
 
 On CPU (tests) "devices" may repeat ``cpu``; the all-reduce is then a plain sum.
@@ -32,10 +37,13 @@ import torch
 
 from ..compute import loss_from_partials, make_compute
 from ..optim import FlatParameterSpace
+from ..utils.tracing import trace_range
+from .ddp import bucket_plan
 
 
 class ReplicatedDataParallel:
-    def __init__(self, model: torch.nn.Module, devices: Sequence, backend: str = "auto", dtype: str = "bf16"):
+    def __init__(self, model: torch.nn.Module, devices: Sequence, backend: str = "auto", dtype: str = "bf16",
+                 bucket_mb: float = 8.0):
         self.devices = [torch.device(d) for d in devices]
         assert len(self.devices) >= 1
         self.replicas: List[torch.nn.Module] = []
@@ -55,6 +63,8 @@ class ReplicatedDataParallel:
                 self.comm.broadcast([s.data for s in self.spaces], root=0)
                 for s in self.spaces:
                     s.touch()
+        self.reducer = DPBucketReducer(self.spaces, self.devices, self.comm, bucket_mb) \
+            if len(self.devices) > 1 else None
 
     # ------------------------------------------------------------------ forward
     def _parallel(self, fn, args_per_dev):
@@ -104,30 +114,10 @@ class ReplicatedDataParallel:
             s.zero_grad()
 
     def all_reduce_grads(self):
-        grads = [s.grad for s in self.spaces]
-        if len(grads) == 1:
-            return
-        if self.comm is not None:
-            self.comm.all_reduce(grads, "sum")
-            return
-        if self._nccl:
-            try:
-                import torch.cuda.nccl as nccl
-                if nccl.is_available(grads):
-                    nccl.all_reduce(grads)
-                    return
-            except (RuntimeError, ImportError):
-                pass
-            total = torch.cuda.comm.reduce_add(grads, destination=self.devices[0].index)
-            outs = torch.cuda.comm.broadcast(total, devices=[d.index for d in self.devices])
-            for g, o in zip(grads, outs):
-                g.copy_(o)
-            return
-        total = grads[0].clone()
-        for g in grads[1:]:
-            total += g.to(total.device)
-        for g in grads:
-            g.copy_(total.to(g.device))
+        """End of the backward: launch the buckets not started yet, then every compute stream
+        waits for its comm stream (the optimizer reads summed gradients)."""
+        if self.reducer is not None:
+            self.reducer.finish()
 
     @torch.no_grad()
     def sync_buffers(self):
@@ -151,3 +141,79 @@ class ReplicatedDataParallel:
 
     def state_dict(self):
         return self.module.state_dict()
+
+
+class DPBucketReducer:
+    """Bucketed, backward-overlapped gradient sum across the replicas of one process.
+
+    Readiness arrives from several threads (the autograd engine runs one worker thread per device;
+    each replica's backward calls its flat space's ``notify_ready``), so the per-bucket counters
+    are guarded by a lock; the thread that completes a bucket on the last replica launches it.
+    Buckets launch strictly in index order.  On GPUs with the native clique each bucket is one
+    grouped ncclAllReduce (sum) over the slices, issued on per-device comm streams that first wait
+    for their device's compute stream; :meth:`finish` makes every compute stream wait for its comm
+    stream and records the exposed (un-overlapped) wait on device 0."""
+
+    def __init__(self, spaces, devices, comm=None, bucket_mb: float = 8.0, first_bucket_mb: float = 1.0):
+        self.spaces, self.devices, self.comm = list(spaces), list(devices), comm
+        self.buckets, self.bucket_of = bucket_plan(self.spaces[0], bucket_mb, first_bucket_mb)
+        for sp in self.spaces[1:]:
+            assert sp.offsets == self.spaces[0].offsets, "replicas must share one flat layout"
+        self.expected = [(b[3] - b[2]) * len(self.spaces) for b in self.buckets]
+        self.lock = threading.Lock()
+        self.streams = ([torch.cuda.Stream(device=d) for d in self.devices] if comm is not None else None)
+        self._exposed = None
+        self._hooks = []
+        for k, sp in enumerate(self.spaces):
+            sp.add_ready_listener(lambda i, k=k: self.mark_ready(i))
+            for i, p in enumerate(sp.params):       # torch-op backend: autograd accumulation hooks
+                self._hooks.append(p.register_post_accumulate_grad_hook(lambda _p, i=i: self.mark_ready(i)))
+        self.reset()
+
+    def reset(self):
+        self.pending = list(self.expected)
+        self.next_launch = 0
+
+    def mark_ready(self, param_index: int):
+        with self.lock:
+            self.pending[self.bucket_of[param_index]] -= 1
+            while self.next_launch < len(self.buckets) and self.pending[self.next_launch] <= 0:
+                self._launch(self.next_launch)
+                self.next_launch += 1
+
+    def _launch(self, b: int):
+        s, e = self.buckets[b][:2]
+        grads = [sp.grad[s:e] for sp in self.spaces]
+        with trace_range(f"dp_allreduce_bucket{b}"):
+            if self.comm is not None:
+                for d, st in zip(self.devices, self.streams):
+                    st.wait_stream(torch.cuda.current_stream(d))   # the slice's gradients are enqueued
+                self.comm.all_reduce(grads, "sum", streams=self.streams)
+                return
+            total = grads[0].clone()
+            for g in grads[1:]:
+                total += g.to(total.device)
+            for g in grads:
+                g.copy_(total.to(g.device))
+
+    def finish(self):
+        with self.lock:
+            while self.next_launch < len(self.buckets):
+                self._launch(self.next_launch)
+                self.next_launch += 1
+            if self.streams is not None:
+                cur0 = torch.cuda.current_stream(self.devices[0])
+                ev0 = torch.cuda.Event(enable_timing=True)
+                ev0.record(cur0)
+                for d, st in zip(self.devices, self.streams):
+                    torch.cuda.current_stream(d).wait_stream(st)
+                ev1 = torch.cuda.Event(enable_timing=True)
+                ev1.record(cur0)
+                self._exposed = (ev0, ev1)
+            self.reset()
+
+    def exposed_comm_ms(self):
+        if self._exposed is None:
+            return None
+        self._exposed[1].synchronize()
+        return float(self._exposed[0].elapsed_time(self._exposed[1]))

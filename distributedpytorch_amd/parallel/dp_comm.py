@@ -59,18 +59,23 @@ class DPComm:
         if r != 0:
             raise RuntimeError(f"{what} failed: rccl error {r} ({lib().dpa_dp_error(r).decode()})")
 
-    def _args(self, tensors: List[torch.Tensor]):
+    def _args(self, tensors: List[torch.Tensor], streams=None):
         assert len(tensors) == len(self.devices)
         n = tensors[0].numel()
         dt = tensors[0].dtype
         for t, d in zip(tensors, self.devices):
             assert t.device == d and t.is_contiguous() and t.numel() == n and t.dtype == dt, (t.device, d)
         bufs = (ctypes.c_void_p * len(tensors))(*[t.data_ptr() for t in tensors])
-        sts = (ctypes.c_void_p * len(tensors))(*[torch.cuda.current_stream(d).cuda_stream for d in self.devices])
+        if streams is None:
+            streams = [torch.cuda.current_stream(d) for d in self.devices]
+        assert len(streams) == len(self.devices)
+        sts = (ctypes.c_void_p * len(tensors))(*[s.cuda_stream for s in streams])
         return bufs, sts, n, _DT[dt]
 
-    def all_reduce(self, tensors: List[torch.Tensor], op: str = "sum"):
-        bufs, sts, n, dt = self._args(tensors)
+    def all_reduce(self, tensors: List[torch.Tensor], op: str = "sum", streams=None):
+        """In-place all-reduce, one tensor per device, on ``streams`` (default: each device's
+        current stream)."""
+        bufs, sts, n, dt = self._args(tensors, streams)
         self._check(lib().dpa_dp_all_reduce(self._h, bufs, ctypes.c_longlong(n), ctypes.c_int(dt),
                                             ctypes.c_int(_OP[op]), sts), "ncclAllReduce")
 

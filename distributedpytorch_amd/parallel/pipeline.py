@@ -459,6 +459,22 @@ class GPipeLocal:
             env = self._run(s, env, None, "probs" if s == self.S - 1 else "partials")
         return env["probs"].to(self.devices[0])
 
+    def forward_probs(self, images):
+        """Differentiable pipelined forward to the probability map (``UNet(pipe=True).forward``):
+        microbatches in wavefront order, outputs concatenated on the first device (reference
+        ``torch.cat(ret).to('cuda:0')``, unet_model.py:53)."""
+        M, S = self.M, self.S
+        envs = [{"x": x} for x in images.chunk(M)]
+        outs = [None] * len(envs)
+        for k in range(len(envs) + S - 1):
+            for s in reversed(range(S)):
+                m = k - s
+                if 0 <= m < len(envs):
+                    envs[m] = self._run(s, envs[m], None, "probs" if s == S - 1 else "partials")
+                    if s == S - 1:
+                        outs[m] = envs[m]["probs"].to(self.devices[0])
+        return torch.cat(outs)
+
 
 class _Null:
     def __enter__(self):

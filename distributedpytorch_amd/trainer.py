@@ -24,6 +24,7 @@ import torch.distributed as dist
 from .compute import loss_from_partials, make_compute, resolve_backend
 from .config import TrainConfig, dist_env, mp_cut_mode
 from .data import CarvanaDataset, SyntheticSegmentation, build_loaders, split_dataset
+from .data.device import DeviceLoader, DeviceSyntheticSegmentation, device_loaders
 from .data.loaders import DeviceBatcher
 from .loss import dice_score
 from .models.unet import build_model
@@ -202,7 +203,8 @@ class DPStrategy(Strategy):
 
     def __init__(self, cfg, model, devices):
         super().__init__(cfg)
-        self.dp = ReplicatedDataParallel(model, devices, cfg.backend, cfg.dtype)
+        self.dp = ReplicatedDataParallel(model, devices, cfg.backend, cfg.dtype, bucket_mb=cfg.bucket_mb)
+        self.reducer = self.dp.reducer
         self.device = self.dp.devices[0]
         self.model = self.dp.module
         self.optimizer = FusedAdam(self.dp.spaces, lr=cfg.lr, weight_decay=cfg.weight_decay)
@@ -353,14 +355,29 @@ def build_strategy(cfg: TrainConfig, model) -> Strategy:
     raise ValueError(m)
 
 
-def build_datasets(cfg: TrainConfig):
+def build_datasets(cfg: TrainConfig, device=None):
     H, W = cfg.img_size
-    if cfg.synthetic:
+    if cfg.synthetic and device is not None and cfg.device_data and torch.device(device).type == "cuda":
+        ds = DeviceSyntheticSegmentation(cfg.synthetic_len, (H, W), 3, seed=cfg.seed, device=device)
+        log.info(f"synthetic dataset resident on {device}: {len(ds)} images, {ds.nbytes / 2 ** 30:.2f} GiB")
+    elif cfg.synthetic:
         ds = SyntheticSegmentation(cfg.synthetic_len, (H, W), 3, seed=cfg.seed)
     else:
         root = cfg.data_dir
         ds = CarvanaDataset(os.path.join(root, "train_hq"), os.path.join(root, "train_masks"), newsize=(W, H))
     return split_dataset(ds, cfg.val, seed=0)
+
+
+def _base_dataset(ds):
+    while isinstance(ds, torch.utils.data.Subset):
+        ds = ds.dataset
+    return ds
+
+
+def _batches(loader, device):
+    """(images, targets) on the device: HBM-resident loaders yield them directly; host loaders go
+    through the prefetching H2D batcher."""
+    return loader if isinstance(loader, DeviceLoader) else DeviceBatcher(loader, device)
 
 
 def _setup_logging(cfg, rank):
@@ -395,12 +412,17 @@ def train(cfg: TrainConfig):
     strat = build_strategy(cfg, model)
     log.info(f"strategy={strat.name} backend={resolve_backend(cfg.backend, strat.device)} device={strat.device}")
 
-    train_set, val_set = build_datasets(cfg)
+    train_set, val_set = build_datasets(cfg, strat.device)
     dp_ranks = world if strat.name == "DDP" else 1
     dp_rank = strat.rank if strat.name == "DDP" else 0
-    train_loader, val_loader, sampler = build_loaders(
-        train_set, val_set, cfg.batch_size, rank=dp_rank, world_size=dp_ranks, num_workers=cfg.num_workers,
-        pin_memory=strat.device.type == "cuda", seed=cfg.seed, drop_last=strat.name in ("MP",))
+    if isinstance(_base_dataset(train_set), DeviceSyntheticSegmentation):
+        train_loader, val_loader, sampler = device_loaders(
+            train_set, val_set, cfg.batch_size, rank=dp_rank, world_size=dp_ranks, seed=cfg.seed,
+            drop_last=strat.name in ("MP",))
+    else:
+        train_loader, val_loader, sampler = build_loaders(
+            train_set, val_set, cfg.batch_size, rank=dp_rank, world_size=dp_ranks, num_workers=cfg.num_workers,
+            pin_memory=strat.device.type == "cuda", seed=cfg.seed, drop_last=strat.name in ("MP",))
     scheduler = make_plateau(strat.optimizer, cfg.patience)
     metrics = MetricsLogger(os.path.join(cfg.out_dir, "logs", f"{cfg.train_method}.jsonl"), strat.is_main)
     curves = LossCurves()
@@ -425,7 +447,10 @@ def train(cfg: TrainConfig):
         if sampler is not None:
             sampler.set_epoch(epoch)  # A7
         n_img, t_ep = 0, time.perf_counter()
-        for images, targets in DeviceBatcher(train_loader, strat.device):
+        steady = _SteadyMeter(strat.device)
+        bar = _progress(cfg, strat, f"Epoch {epoch + 1}/{cfg.epochs}", len(train_loader) * cfg.batch_size, "img")
+        for images, targets in _batches(train_loader, strat.device):
+            steady.tick(images.shape[0])
             if prof is not None:
                 prof.before(step)
             if cfg.cuda_graph and graphed is None and GraphedStep.supported(strat):
@@ -440,6 +465,7 @@ def train(cfg: TrainConfig):
             if prof is not None:
                 prof.after(step)
             n_img += images.shape[0]
+            bar.update(images.shape[0])
             if loss is not None:
                 pending.append(loss)
             if step % cfg.log_every == 0:
@@ -456,6 +482,7 @@ def train(cfg: TrainConfig):
                                 lr=strat.optimizer.param_groups[0]["lr"], exposed_comm_ms=comm_ms)
                     if strat.is_main:
                         log.info(f"step {step} loss {mean_loss:.5f}")
+                    bar.set_postfix(loss=f"{mean_loss:.4f}")
                 stop_signal = _agree_stop(strat, guard.requested)
                 if stop_signal is not None:
                     break
@@ -470,17 +497,22 @@ def train(cfg: TrainConfig):
             log.warning(f"stopped by signal {stop_signal} at step {step}; state saved to {last_path}")
             break
         ep_time = time.perf_counter() - t_ep
-        val_loss, val_dice = evaluate(strat, val_loader)
+        steady_ips = steady.finish()
+        bar.close()
+        val_loss, val_dice = evaluate(strat, val_loader, cfg)
         curves.add_val(step, time.time() - t_start, val_loss)
         plateau_step(scheduler, val_loss)
         metrics.log(kind="epoch", epoch=epoch, step=step, val_loss=val_loss, val_dice=val_dice,
                     img_per_s=n_img * max(1, strat.world if strat.name == "DDP" else 1) / max(ep_time, 1e-9),
+                    img_per_s_steady=(None if steady_ips is None
+                                      else steady_ips * max(1, strat.world if strat.name == "DDP" else 1)),
                     peak_mem_gb=(torch.cuda.max_memory_allocated(strat.device) / 2 ** 30
                                  if strat.device.type == "cuda" else 0.0))
         if strat.is_main:
             log.info(f"epoch {epoch}: val_loss {val_loss:.5f} val_dice {val_dice:.4f}")
+            sps = "" if steady_ips is None else f", {steady_ips:.1f} img/s/rank after {steady.skip} warm-up steps"
             print(f"epoch {epoch + 1}/{cfg.epochs} step {step} val_loss {val_loss:.5f} dice {val_dice:.4f} "
-                  f"({n_img / max(ep_time, 1e-9):.1f} img/s/rank)", flush=True)
+                  f"({n_img / max(ep_time, 1e-9):.1f} img/s/rank{sps})", flush=True)
         if cfg.save_every_epoch:
             sd_model, sd_opt = strat.state_dict(), strat.optimizer_state_dict()
             if strat.rank == 0 and sd_model is not None:
@@ -635,21 +667,74 @@ class _OptIO:
         self.strat.load_optimizer_state_dict(sd)
 
 
+class _SteadyMeter:
+    """Training throughput without the first ``skip`` steps of an epoch (weight packing, allocator
+    warm-up, lazy communicator setup): device-synchronised at the start mark and at the end."""
+
+    def __init__(self, device, skip: int = 3):
+        self.device, self.skip = torch.device(device), skip
+        self.k, self.n, self.t0 = 0, 0, None
+
+    def _sync(self):
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+
+    def tick(self, batch: int):
+        """Called before each step with its batch size."""
+        if self.k == self.skip:
+            self._sync()
+            self.t0 = time.perf_counter()
+        if self.k >= self.skip:
+            self.n += batch
+        self.k += 1
+
+    def finish(self) -> Optional[float]:
+        if self.t0 is None or self.n == 0:
+            return None
+        self._sync()
+        return self.n / max(time.perf_counter() - self.t0, 1e-9)
+
+
+class _NoBar:
+    def update(self, n=1):
+        pass
+
+    def set_postfix(self, **kw):
+        pass
+
+    def close(self):
+        pass
+
+
+def _progress(cfg, strat, desc, total, unit):
+    """tqdm bar on the main rank (reference: images per epoch, ``utils/train_utils.py:57,132``, and
+    validation batches, ``evaluate.py:12``); ``--progress`` auto = only on a terminal."""
+    import sys
+    on = cfg.progress if cfg.progress is not None else sys.stderr.isatty()
+    if not (on and strat.is_main):
+        return _NoBar()
+    from tqdm import tqdm
+    return tqdm(total=total, desc=desc, unit=unit, leave=False)
+
+
 @torch.no_grad()
-def evaluate(strat: Strategy, val_loader):
+def evaluate(strat: Strategy, val_loader, cfg: Optional[TrainConfig] = None):
     """Reference ``evaluate.py:6-25`` (``model.eval()``, mean per-batch loss, ``model.train()``) + Dice;
     sharded and all-reduced."""
     tot = torch.zeros(3, dtype=torch.float64)
     strat.before_eval()
     strat.set_train(False)
+    bar = _progress(cfg, strat, "Validation round", len(val_loader), "batch") if cfg is not None else _NoBar()
     try:
-        for images, targets in DeviceBatcher(val_loader, strat.device):
+        for images, targets in _batches(val_loader, strat.device):
+            bar.update(1)
             r = strat.eval_batch(images, targets)
             if r is not None:
                 loss, dice = r
                 tot += torch.tensor([float(loss), float(dice), 1.0], dtype=torch.float64)
     finally:
         strat.set_train(True)
+        bar.close()
     if strat.name == "DDP":
         t = tot.to(strat.device) if strat.device.type == "cuda" else tot
         tot = strat.reduce_eval(t).cpu()

@@ -229,3 +229,32 @@ def test_bench_two_ranks_same_device(hip_lib, extra):
     assert out["final_loss"] is not None and out["final_loss"] == out["final_loss"]
     if not mp_run:  # DDP: the reducer timed the stall on outstanding all-reduce buckets
         assert out["exposed_comm_ms_last_step"] is not None and out["exposed_comm_ms_last_step"] >= 0
+
+
+def test_dp_bucket_reducer_native_clique(hip_lib):
+    """-t DP's bucketed reducer on the native RCCL clique (one member here): buckets are launched
+    on the comm stream while the HIP backward runs (readiness from notify_ready), the compute
+    stream waits for them at the end, and a one-member sum leaves the gradients bitwise unchanged."""
+    from distributedpytorch_amd.compute import make_compute
+    from distributedpytorch_amd.models.unet import build_model
+    from distributedpytorch_amd.optim import FlatParameterSpace
+    from distributedpytorch_amd.parallel import dp_comm
+    from distributedpytorch_amd.parallel.dp import DPBucketReducer
+    torch.manual_seed(6)
+    m = build_model("unet").cuda()
+    sp = FlatParameterSpace(m)
+    comp = make_compute(m, "hip", "bf16")
+    x, t = _batch(4, 64)
+    sp.zero_grad()
+    from distributedpytorch_amd.compute import loss_from_partials
+    (loss_from_partials(comp.forward_partials(x, t), t.numel()) * 4).backward()
+    torch.cuda.synchronize()
+    ref = sp.grad.clone()
+    red = DPBucketReducer([sp], [torch.device("cuda:0")], dp_comm.DPComm(["cuda:0"]), bucket_mb=1.0)
+    sp.zero_grad()
+    (loss_from_partials(comp.forward_partials(x, t), t.numel()) * 4).backward()
+    assert red.next_launch >= len(red.buckets) - 1     # launched during the backward
+    red.finish()
+    torch.cuda.synchronize()
+    assert torch.equal(sp.grad, ref)
+    assert red.exposed_comm_ms() >= 0
