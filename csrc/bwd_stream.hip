@@ -1,0 +1,425 @@
+// Fused backward of a full-resolution conv3x3 (s1 p1) for 32/64-channel layers: input gradient AND
+// weight + bias gradient in ONE pass over the row stream (reference layers: the 512^2 / 256^2
+// conv_blocks of model/unet_parts.py:9-14; SURVEY K2 + K3 + K4-bwd).
+//
+// Why: at these widths both backward GEMMs are bound by HBM traffic, not MFMAs.  Run separately,
+// the dgrad reads g (the ReLU-masked output gradient) and the layer input x (for ReLU mask of the
+// input gradient) and writes dx, and the weight gradient reads g and x AGAIN: 5 activation-sized
+// passes per conv (21.5 GB per 32->32 conv at 512^2, batch 256).  Here one block streams the rows
+// of an image column strip once: g rows go through one 4-slot LDS ring, x rows through another,
+// and for every output row the block
+//   * computes the dx row from the three g rows in the ring with the dgrad weights resident in LDS
+//     (the igemm_stream schedule: 9 taps x 32-channel slices of 16x16x32 bf16 MFMAs),
+//   * masks it with x > 0 read from the x ring (EPI 0: the input is a ReLU output), or splits it
+//     into the two halves of a concat gradient (EPI 1), or stores it as is (EPI 2),
+//   * accumulates dW[tap][co][ci] += sum_px g[h][px][co] * x[h+kh-1][px+kw-1][ci] from the same ring
+//     slots (transposed LDS reads, ds_read_b64_tr_b16; fp32 accumulators live in registers for the
+//     whole block), and db[co] += sum_px g[h][px][co],
+// so every byte of g and x is read from HBM ~once ((BP+2)/BP) and dx written once: 3 passes.
+// Each block writes its partial dW / db as fp32 slab rows; dpa_wgrad_reduce sums them in a fixed
+// order (bitwise reproducible) into the flat gradient buffer.
+//
+// Wave roles: dx row = WPX waves along the pixels x WCS along the channels (as igemm_stream);
+// weight gradient = wave w owns input-channel tile (w % NTI), output-channel tiles
+// [msp*MTW, msp*MTW + MTW) (msp = w / NTI % MSPL) for all 9 taps, over the pixel k-steps
+// pg + j*PG of the row (pg = w / (NTI*MSPL)); the PG pixel groups write separate slab rows.
+#include "conv_args.h"
+
+struct BwdArgs {
+  const bf16_t* g;      // gradient w.r.t. the conv output [N][H][W][ldg], CO channels (ReLU mask applied)
+  const bf16_t* x;      // conv input [N][H][W][ldx], CI channels
+  const bf16_t* wd;     // dgrad-packed weights [CI][Kd]: k = tap*CO + co (pack mode 1, taps flipped)
+  bf16_t* y;            // dx [N][H][W][ldy] (EPI 1: channels < split)
+  bf16_t* y2;           // EPI 1: channels >= split -> y2[..][c - split]
+  float* slab;          // [nblocks*PG][9][CO][CI] partial weight gradients
+  float* bslab;         // [nblocks*PG][CO] partial bias gradients (rows of pixel group > 0 zero) or null
+  int ldg, ldx, ldy, ldy2, split, Kd;
+  int N, H, W;
+  int rh, ipb;          // rows per block, images per block
+  unsigned gbytes, xbytes;  // addressable bytes of ONE image of g / x (buffer offsets are per image)
+};
+
+// 8 consecutive k (pixel rows roff+8g .. +7) of 16 channels starting at col0, from an nk image
+// ([rows][32 channels], 64-B rows, swz_nk<32> chunk swizzle): the tr_frag of conv_args.h for the
+// dgrad-friendly layout of the g ring.
+__device__ __forceinline__ bf16x8_t tr_frag_nk32(const char* img, int col0, int lane, int roff) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int col = col0 + 4 * p;
+  const int ch = col >> 3, hb = (col & 7) * 2;
+  const int r0 = roff + 8 * g + q, r1 = r0 + 4;
+  const char* a0 = img + r0 * 64 + (swz_nk<32>(r0, ch) << 4) + hb;
+  const char* a1 = img + r1 * 64 + (swz_nk<32>(r1, ch) << 4) + hb;
+  s16x4_t v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4_t, a0));
+  s16x4_t v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4_t, a1));
+  typedef __attribute__((ext_vector_type(8))) short s16x8_t;
+  s16x8_t v = __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8_t, v);
+}
+
+// the two ds_read_b64_tr_b16 of a transposed fragment at precomputed byte offsets (see tr_frag)
+__device__ __forceinline__ bf16x8_t tr_pair(const char* base, int off0, int off1) {
+  s16x4_t v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4_t, base + off0));
+  s16x4_t v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4_t, base + off1));
+  typedef __attribute__((ext_vector_type(8))) short s16x8_t;
+  s16x8_t v = __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8_t, v);
+}
+
+template <int BP, int CI, int CO, int NW, int PG, int EPI>
+__global__ __launch_bounds__(64 * NW) void bwd_stream_kernel(BwdArgs a) {
+  constexpr int NT = 64 * NW;
+  constexpr int HR = BP + 2;                   // ring row: BP pixels + 1 halo pixel each side
+  constexpr int KSO = CO / 32;                 // 32-channel slices of g
+  constexpr int WBYTES = 9 * KSO * CI * 64;    // dgrad weights [tap][ks][CI][32] (nk)
+  constexpr int GSLOT = KSO * HR * 64;         // g row [ks][HR][32] (nk)
+  constexpr int RBX = CI * 2;                  // x row image [HR][CI] (kk)
+  constexpr int XSLOT = HR * RBX;
+  constexpr int WCS = NW == 8 ? 2 : 1, WPX = NW / WCS;
+  constexpr int WP = BP / WPX, TP = WP / 16;
+  constexpr int WCN = CI / WCS, TC = WCN / 16;
+  constexpr int NTI = CI / 16, MTI = CO / 16;
+  constexpr int MSPL = NW / (NTI * PG), MTW = MTI / MSPL;
+  constexpr int KST = BP / 32 / PG;            // pixel k-steps per wave per row
+  static_assert(TP >= 1 && TC >= 1 && MSPL >= 1 && NTI * MSPL * PG == NW && MTW * MSPL == MTI && (BP / 32) % PG == 0,
+                "tile");
+  constexpr int GCH = KSO * HR * 4, XCH = HR * (CI / 8);         // 16-B chunks per ring row
+  constexpr int LG = (GCH + NT - 1) / NT, LX = (XCH + NT - 1) / NT;
+  constexpr int BCH = BP * 4 * KSO, LBI = (BCH + NT - 1) / NT;   // bias: chunks of the g row's BP pixels
+  __shared__ __attribute__((aligned(16))) char lds[WBYTES + 4 * GSLOT + 4 * XSLOT];
+  char* const Wimg = lds;
+  char* const Gring = lds + WBYTES;
+  char* const Xring = Gring + 4 * GSLOT;
+
+  const int stripsW = a.W / BP, segsH = (a.H + a.rh - 1) / a.rh;
+  const int split_id = blockIdx.x;
+  const int ig = split_id / (segsH * stripsW);
+  const int rem = split_id - ig * segsH * stripsW;
+  const int hs = rem / stripsW;
+  const int w0 = (rem - hs * stripsW) * BP, h0 = hs * a.rh;
+  const int nrows = min(a.rh, a.H - h0);
+  const int nimg = min(a.ipb, a.N - ig * a.ipb);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wp = wid % WPX, wc = wid / WPX;                      // dx role
+  const int nt = wid % NTI, msp = (wid / NTI) % MSPL, pg = wid / (NTI * MSPL);   // dW role
+  // buffer resources are rebuilt per image (32-bit offsets stay inside one image at any batch size)
+  __amdgpu_buffer_rsrc_t gr, xr, yr, y2r;
+  auto bind = [&](int img) {
+    const long pix = (long)img * a.H * a.W;
+    gr = __builtin_amdgcn_make_buffer_rsrc((void*)(a.g + pix * a.ldg), 0, (int)a.gbytes, 0x00020000);
+    xr = __builtin_amdgcn_make_buffer_rsrc((void*)(a.x + pix * a.ldx), 0, (int)a.xbytes, 0x00020000);
+    yr = __builtin_amdgcn_make_buffer_rsrc((void*)(a.y + pix * a.ldy), 0, 0x7fffffff, 0x00020000);
+    y2r = __builtin_amdgcn_make_buffer_rsrc((void*)(EPI == 1 ? a.y2 + pix * a.ldy2 : a.y), 0, 0x7fffffff, 0x00020000);
+  };
+
+  // resident dgrad weights: packed [CI][Kd], k = tap*CO + ks*32 + c
+  for (int c = tid; c < 9 * KSO * CI * 4; c += NT) {
+    const int cc = c & 3, row = (c >> 2) % CI, tk = (c >> 2) / CI;   // tk = tap*KSO + ks
+    const int tap = tk / KSO, ks = tk - tap * KSO;
+    const u32x4_t v = *reinterpret_cast<const u32x4_t*>(a.wd + (long)row * a.Kd + tap * CO + ks * 32 + cc * 8);
+    *reinterpret_cast<u32x4_t*>(Wimg + (tk * CI + row) * 64 + (swz_nk<32>(row, cc) << 4)) = v;
+  }
+  // ---- loader constants
+  unsigned goff[LG], xoff[LX];
+  int gsto[LG], xsto[LX];
+  bool gok[LG], xok[LX];
+#pragma unroll
+  for (int j = 0; j < LG; ++j) {
+    const int c = tid + j * NT;
+    const int cc = c & 3, px = (c >> 2) % HR, ks = (c >> 2) / HR;
+    const int iw = w0 + px - 1;
+    gok[j] = c < GCH && iw >= 0 && iw < a.W;
+    goff[j] = (unsigned)((iw * a.ldg + ks * 32 + cc * 8) * 2);
+    gsto[j] = c < GCH ? (ks * HR + px) * 64 + (swz_nk<32>(px, cc) << 4) : -1;
+  }
+#pragma unroll
+  for (int j = 0; j < LX; ++j) {
+    const int c = tid + j * NT;
+    const int px = c / (CI / 8), cc = c - px * (CI / 8);
+    const int iw = w0 + px - 1;
+    xok[j] = c < XCH && iw >= 0 && iw < a.W;
+    xoff[j] = (unsigned)((iw * a.ldx + cc * 8) * 2);
+    xsto[j] = c < XCH ? px * RBX + ((cc ^ swz_kk<RBX>(px)) << 4) : -1;
+  }
+  const unsigned growb = (unsigned)(a.W * a.ldg * 2), xrowb = (unsigned)(a.W * a.ldx * 2);
+  // two register sets: the loads of a row are issued two rows before it is stored into the ring
+  // (one row of compute was too short to cover the load latency at 1-2 blocks per CU)
+  struct RowRegs {
+    u32x4_t g[LG], x[LX];
+  };
+  RowRegs setA, setB;
+  int n = ig * a.ipb;
+  auto rload = [&](int ih, RowRegs& R) {
+    const bool rok = ih >= 0 && ih < a.H;                     // wave-uniform
+    const unsigned gb = (unsigned)ih * growb, xb = (unsigned)ih * xrowb;
+#pragma unroll
+    for (int j = 0; j < LG; ++j) R.g[j] = __builtin_amdgcn_raw_buffer_load_b128(gr, (rok && gok[j]) ? gb + goff[j] : 0x80000000u, 0, 0);
+#pragma unroll
+    for (int j = 0; j < LX; ++j) R.x[j] = __builtin_amdgcn_raw_buffer_load_b128(xr, (rok && xok[j]) ? xb + xoff[j] : 0x80000000u, 0, 0);
+  };
+  auto rstore = [&](int slot, const RowRegs& R) {
+#pragma unroll
+    for (int j = 0; j < LG; ++j)
+      if (gsto[j] >= 0) *reinterpret_cast<u32x4_t*>(Gring + slot * GSLOT + gsto[j]) = R.g[j];
+#pragma unroll
+    for (int j = 0; j < LX; ++j)
+      if (xsto[j] >= 0) *reinterpret_cast<u32x4_t*>(Xring + slot * XSLOT + xsto[j]) = R.x[j];
+  };
+  // ---- dx role: LDS fragment offsets, mask offsets, output offsets
+  const int chunk = lane >> 4;
+  int aoff[TC];
+#pragma unroll
+  for (int ic = 0; ic < TC; ++ic) {
+    const int row = wc * WCN + ic * 16 + (lane & 15);
+    aoff[ic] = row * 64 + (swz_nk<32>(row, chunk) << 4);
+  }
+  int boff[TP][3];
+#pragma unroll
+  for (int ip = 0; ip < TP; ++ip)
+#pragma unroll
+    for (int kw = 0; kw < 3; ++kw) {
+      const int px = wp * WP + ip * 16 + (lane & 15) + kw;
+      boff[ip][kw] = px * 64 + (swz_nk<32>(px, chunk) << 4);
+    }
+  int moff[TP][TC];
+  unsigned yoff[TP][TC];
+  bool hi[TP][TC];
+#pragma unroll
+  for (int ip = 0; ip < TP; ++ip)
+#pragma unroll
+    for (int ic = 0; ic < TC; ++ic) {
+      const int px = wp * WP + ip * 16 + (lane & 15);
+      const int c0 = wc * WCN + ic * 16 + 4 * chunk;
+      moff[ip][ic] = (px + 1) * RBX + (((c0 >> 3) ^ swz_kk<RBX>(px + 1)) << 4) + ((c0 >> 2) & 1) * 8;
+      hi[ip][ic] = EPI == 1 && c0 >= a.split;
+      yoff[ip][ic] = hi[ip][ic] ? (unsigned)(((w0 + px) * a.ldy2 + c0 - a.split) * 2)
+                                : (unsigned)(((w0 + px) * a.ldy + c0) * 2);
+    }
+  const unsigned yrowb = (unsigned)(a.W * a.ldy * 2), y2rowb = (unsigned)(a.W * (EPI == 1 ? a.ldy2 : a.ldy) * 2);
+
+  // ---- dW role: per-lane byte offsets of the transposed fragments inside a ring slot (row-invariant;
+  // computing the swizzled addresses per row cost more VALU issue than the MFMAs they feed)
+  int gta[KST][MTW][2], xta[KST][3][2];
+  {
+    const int g8 = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+#pragma unroll
+    for (int j = 0; j < KST; ++j) {
+      const int k0 = (pg + j * PG) * 32;
+#pragma unroll
+      for (int mm = 0; mm < MTW; ++mm) {
+        const int m = msp * MTW + mm, col = (m & 1) * 16 + 4 * p, ch = col >> 3, hb = (col & 7) * 2;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int rr = 1 + k0 + 8 * g8 + q + 4 * h;
+          gta[j][mm][h] = (m >> 1) * HR * 64 + rr * 64 + (swz_nk<32>(rr, ch) << 4) + hb;
+        }
+      }
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        const int col = nt * 16 + 4 * p, ch = col >> 3, hb = (col & 7) * 2;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int rr = k0 + kw + 8 * g8 + q + 4 * h;
+          xta[j][kw][h] = rr * RBX + ((ch ^ swz_kk<RBX>(rr)) << 4) + hb;
+        }
+      }
+    }
+  }
+  // ---- dW role accumulators: [tap][co tile] for input-channel tile nt
+  f32x4_t accw[9][MTW];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int m = 0; m < MTW; ++m) accw[t][m] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  float bsum[LBI][8];
+#pragma unroll
+  for (int i = 0; i < LBI; ++i)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) bsum[i][e] = 0.f;
+  const bool do_bias = a.bslab != nullptr;
+
+#pragma unroll 1
+  for (int im = 0; im < nimg; ++im, ++n) {
+    bind(n);
+    if (nrows > 0) {
+#pragma unroll 1
+      for (int j = 0; j < 3; ++j) {           // rows h0-1, h0, h0+1 -> slots 0..2
+        rload(h0 - 1 + j, setA);
+        rstore(j, setA);
+      }
+      if (nrows > 1) rload(h0 + 2, setA);      // in flight during row 0
+    }
+    __syncthreads();
+    // row r: `cur` holds row h0+r+2 (issued during row r-1); row h0+r+3 is issued into `nxt`
+    auto row = [&](int r, RowRegs& cur, RowRegs& nxt) {
+      if (r + 2 < nrows) rload(h0 + r + 3, nxt);
+      __builtin_amdgcn_sched_barrier(0);
+      const char* Gm = Gring + ((r + 1) & 3) * GSLOT;             // g row h
+      const char* Xm = Xring + ((r + 1) & 3) * XSLOT;             // x row h (mask)
+      // ---------------- dx row h
+      f32x4_t acc[TC][TP];
+#pragma unroll
+      for (int ic = 0; ic < TC; ++ic)
+#pragma unroll
+        for (int ip = 0; ip < TP; ++ip) acc[ic][ip] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh) {
+        const char* S = Gring + ((r + kh) & 3) * GSLOT;
+#pragma unroll
+        for (int kw = 0; kw < 3; ++kw)
+#pragma unroll
+          for (int ks = 0; ks < KSO; ++ks) {
+            const int tk = (kh * 3 + kw) * KSO + ks;
+            bf16x8_t af[TC], bfr[TP];
+#pragma unroll
+            for (int ic = 0; ic < TC; ++ic) af[ic] = *reinterpret_cast<const bf16x8_t*>(Wimg + tk * CI * 64 + aoff[ic]);
+#pragma unroll
+            for (int ip = 0; ip < TP; ++ip) bfr[ip] = *reinterpret_cast<const bf16x8_t*>(S + ks * HR * 64 + boff[ip][kw]);
+#pragma unroll
+            for (int ic = 0; ic < TC; ++ic)
+#pragma unroll
+              for (int ip = 0; ip < TP; ++ip)
+                acc[ic][ip] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ic], bfr[ip], acc[ic][ip], 0, 0, 0);
+          }
+      }
+      // ---------------- dW += g[h]^T x[h+kh-1] (this wave: input-channel tile nt, pixel group pg)
+#pragma unroll
+      for (int j = 0; j < KST; ++j) {
+        bf16x8_t ga[MTW];
+#pragma unroll
+        for (int mm = 0; mm < MTW; ++mm) ga[mm] = tr_pair(Gm, gta[j][mm][0], gta[j][mm][1]);
+#pragma unroll
+        for (int kh = 0; kh < 3; ++kh) {
+          const char* XS = Xring + ((r + kh) & 3) * XSLOT;
+#pragma unroll
+          for (int kw = 0; kw < 3; ++kw) {
+            const bf16x8_t xb = tr_pair(XS, xta[j][kw][0], xta[j][kw][1]);
+#pragma unroll
+            for (int m = 0; m < MTW; ++m)
+              accw[kh * 3 + kw][m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ga[m], xb, accw[kh * 3 + kw][m], 0, 0, 0);
+          }
+        }
+      }
+      // ---------------- db: sum of the g row's BP pixels (chunk c = (ks*BP + px)*4 + cc; cc = tid & 3)
+      if (do_bias) {
+#pragma unroll
+        for (int i = 0; i < LBI; ++i) {
+          const int c = tid + i * NT;
+          if (c < BCH) {
+            const int cc = c & 3, px = ((c >> 2) % BP) + 1, ks = (c >> 2) / BP;
+            const u32x4_t v = *reinterpret_cast<const u32x4_t*>(Gm + ks * HR * 64 + px * 64 + (swz_nk<32>(px, cc) << 4));
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              bsum[i][2 * e] += lo_bf(v[e]);
+              bsum[i][2 * e + 1] += hi_bf(v[e]);
+            }
+          }
+        }
+      }
+      // ---------------- dx epilogue (mask from the x ring, split store)
+      const unsigned orow = (unsigned)(h0 + r);
+#pragma unroll
+      for (int ip = 0; ip < TP; ++ip)
+#pragma unroll
+        for (int ic = 0; ic < TC; ++ic) {
+          float v0 = acc[ic][ip][0], v1 = acc[ic][ip][1], v2 = acc[ic][ip][2], v3 = acc[ic][ip][3];
+          if constexpr (EPI == 0) {
+            const u32x2_t mk = *reinterpret_cast<const u32x2_t*>(Xm + moff[ip][ic]);
+            v0 = lo_bf(mk.x) > 0.f ? v0 : 0.f;
+            v1 = hi_bf(mk.x) > 0.f ? v1 : 0.f;
+            v2 = lo_bf(mk.y) > 0.f ? v2 : 0.f;
+            v3 = hi_bf(mk.y) > 0.f ? v3 : 0.f;
+          }
+          const u32x2_t packed = u32x2_t{pack_bf2(v0, v1), pack_bf2(v2, v3)};
+          if (EPI == 1 && hi[ip][ic])
+            __builtin_amdgcn_raw_buffer_store_b64(packed, y2r, orow * y2rowb + yoff[ip][ic], 0, 0);
+          else
+            __builtin_amdgcn_raw_buffer_store_b64(packed, yr, orow * yrowb + yoff[ip][ic], 0, 0);
+        }
+      __builtin_amdgcn_sched_barrier(0);
+      if (r + 1 < nrows) rstore((r + 3) & 3, cur);
+      __syncthreads();
+    };
+#pragma unroll 1
+    for (int r = 0; r < nrows; r += 2) {
+      row(r, setA, setB);
+      if (r + 1 < nrows) row(r + 1, setB, setA);
+    }
+  }
+  // ---------------- partial weight gradient of this (block, pixel group): slab row blockIdx*PG + pg
+  const long srow = (long)split_id * PG + pg;
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int m = 0; m < MTW; ++m) {
+      const int ci = nt * 16 + (lane & 15);
+      const int co = (msp * MTW + m) * 16 + 4 * (lane >> 4);
+      float* dst = a.slab + ((srow * 9 + t) * CO + co) * CI + ci;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) dst[(long)e * CI] = accw[t][m][e];
+    }
+  if (do_bias) {
+    // deterministic: partials by chunk index in LDS, then per channel a fixed-order sum
+    float* part = reinterpret_cast<float*>(lds);               // BCH*8 floats (rings are free now)
+    static_assert(BCH * 8 * 4 <= WBYTES + 4 * GSLOT + 4 * XSLOT, "bias scratch");
+#pragma unroll
+    for (int i = 0; i < LBI; ++i) {
+      const int c = tid + i * NT;
+      if (c < BCH)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) part[c * 8 + e] = bsum[i][e];
+    }
+    __syncthreads();
+    for (int co = tid; co < CO * PG; co += NT) {
+      const int q = co / CO, cch = co - q * CO;                  // q > 0: zero rows of the other groups
+      float s = 0.f;
+      if (q == 0) {
+        const int ks = cch >> 5, cc = (cch & 31) >> 3, e = cch & 7;
+        for (int px = 0; px < BP; ++px) s += part[((ks * BP + px) * 4 + cc) * 8 + e];
+      }
+      a.bslab[((long)split_id * PG + q) * CO + cch] = s;
+    }
+  }
+}
+
+template <int BP, int CI, int CO, int NW, int PG, int EPI>
+static int launch_bwd_stream(const BwdArgs& a, hipStream_t st) {
+  const int blocks = ((a.N + a.ipb - 1) / a.ipb) * ((a.H + a.rh - 1) / a.rh) * (a.W / BP);
+  hipLaunchKernelGGL((bwd_stream_kernel<BP, CI, CO, NW, PG, EPI>), dim3(blocks), dim3(64 * NW), 0, st, a);
+  return (int)hipGetLastError();
+}
+
+// Tile (BP pixels x NW waves) per channel pair; pixel groups per block (slab rows per block).
+static int bwd_cfg(int ci, int co, int* bp, int* nw) {
+  if (ci == 32 && co == 32) { *bp = 64; *nw = 4; return 2; }
+  if (ci == 64 && co == 32) { *bp = 64; *nw = 8; return 2; }
+  if (ci == 32 && co == 64) { *bp = 64; *nw = 8; return 2; }
+  if (ci == 64 && co == 64) { *bp = 64; *nw = 8; return 1; }
+  return 0;
+}
+
+// Slab rows per block for (ci, co) (0: not supported) and the pixel strip width.
+DPA_API int dpa_bwd_stream_geom(int ci, int co, int* bp) {
+  int nw = 0;
+  return bwd_cfg(ci, co, bp, &nw);
+}
+
+// epi: 0 dx masked by x > 0, 1 dx split at `split` into y / y2, 2 dx plain.
+DPA_API int dpa_bwd_stream(const BwdArgs* args, int ci, int co, int epi, hipStream_t st) {
+  const BwdArgs& a = *args;
+  int bp = 0, nw = 0;
+  if (!bwd_cfg(ci, co, &bp, &nw) || a.W % bp || (a.ldg & 7) || (a.ldx & 7) || (a.ldy & 3) || a.rh < 1 || a.ipb < 1 ||
+      a.Kd < 9 * co || (epi == 1 && (a.y2 == nullptr || (a.ldy2 & 3) || a.split % 16 || a.split <= 0 || a.split >= ci)))
+    return (int)hipErrorInvalidValue;
+#define DPA_BWD(CIv, COv, BPv, NWv, PGv)                                          \
+  if (ci == CIv && co == COv) {                                                    \
+    if (epi == 0) return launch_bwd_stream<BPv, CIv, COv, NWv, PGv, 0>(a, st);     \
+    if (epi == 1) return launch_bwd_stream<BPv, CIv, COv, NWv, PGv, 1>(a, st);     \
+    if (epi == 2) return launch_bwd_stream<BPv, CIv, COv, NWv, PGv, 2>(a, st);     \
+  }
+  DPA_BWD(32, 32, 64, 4, 2)
+  DPA_BWD(64, 32, 64, 8, 2)
+  DPA_BWD(32, 64, 64, 8, 2)
+  DPA_BWD(64, 64, 64, 8, 1)
+#undef DPA_BWD
+  return (int)hipErrorInvalidValue;
+}

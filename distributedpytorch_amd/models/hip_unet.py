@@ -132,6 +132,7 @@ class HipBlocks:
         # encoder levels whose skip leaves this engine (pipeline stage boundary): the second conv writes
         # that skip into a dense tensor, which then goes on the wire as is (no concat-half copy)
         self.dense_skips = set()
+        self._fusable = {}
 
     # ------------------------------------------------------------------ weight packing
     def _build_packing(self):
@@ -291,6 +292,28 @@ class HipBlocks:
         # caching allocator until an event query, forcing fresh allocations every step: measured 8x slower)
         self._keep.extend(keep)
         self._side_pending = True
+
+    def fusable(self, c: _Conv, below, W: int) -> bool:
+        """The fused backward (dgrad + weight/bias gradient in one pass, csrc/bwd_stream.hip) serves
+        this conv: 32/64 channels in and out, no BatchNorm around it (its backward needs the dgrad
+        epilogue's statistics), image rows a multiple of the kernel's pixel strip."""
+        if not (K.USE_FUSED_BWD and c.bn is None and (below is None or below.bn is None) and c.Cs == c.Cin):
+            return False
+        key = (c.Cin, c.Cout, W)
+        ok = self._fusable.get(key)
+        if ok is None:
+            ok = self._fusable[key] = K.bwd_fused_eligible(c.Cin, c.Cout, W)
+        return ok
+
+    def conv_bwd(self, c: _Conv, g: torch.Tensor, x: torch.Tensor, mask: bool, split: int = 0):
+        """Fused backward of ``c``: returns dx (ReLU-masked by ``x`` when ``mask``; with ``split`` the
+        two dense halves of a concat gradient) and accumulates the weight and bias gradients."""
+        gw, gb = _grad(c.mod.weight).view(-1), _grad(c.mod.bias)
+        if split:
+            N, H, W = g.shape[:3]
+            hi = torch.empty(N, H, W, c.Cin - split, dtype=torch.bfloat16, device=g.device)
+            return K.conv_bwd_fused(g, x, self.wd(c), c.Kd, gw, gb, mask=False, dx2=hi, split=split)
+        return K.conv_bwd_fused(g, x, self.wd(c), c.Kd, gw, gb, mask=mask)
 
     def conv_wgrad(self, c: _Conv, g: torch.Tensor, x: torch.Tensor):
         N, H, W = g.shape[:3]
@@ -494,12 +517,19 @@ class _EncFn(torch.autograd.Function):
         else:
             K.pool_bwd(skip, dskip, dpooled, g2)
         g2 = B.bn_bwd(c2, g2, st2)
-        B.conv_wgrad(c2, g2, a)                  # side stream: overlaps the dgrad chain
-        g1, st_g = B.conv_dgrad(c2, g2, mask=a, below=c1)
+        W = g2.shape[2]
+        if B.fusable(c2, c1, W):
+            g1, st_g = B.conv_bwd(c2, g2, a, mask=True), None
+        else:
+            B.conv_wgrad(c2, g2, a)              # side stream: overlaps the dgrad chain
+            g1, st_g = B.conv_dgrad(c2, g2, mask=a, below=c1)
         B.ready([c2.mod, c2.bn])
         g1 = B.bn_bwd(c1, g1, st1, stats=st_g)
-        B.conv_wgrad(c1, g1, x)
-        gx = B.conv_dgrad(c1, g1) if ctx.x_needs_grad else None
+        if ctx.x_needs_grad and B.fusable(c1, None, W):
+            gx = B.conv_bwd(c1, g1, x, mask=False)   # the pool backward below applies the ReLU mask
+        else:
+            B.conv_wgrad(c1, g1, x)
+            gx = B.conv_dgrad(c1, g1) if ctx.x_needs_grad else None
         B.ready([c1.mod, c1.bn])
         B.join()
         ctx.st = None
@@ -588,12 +618,19 @@ class _DecFn(torch.autograd.Function):
         c1, c2 = B.dec_convs[i]
         C = d.Cout
         g2 = B.bn_bwd(c2, _v(g2), st2)
-        B.conv_wgrad(c2, g2, a)
-        g1, st_g = B.conv_dgrad(c2, g2, mask=a, below=c1)
+        W = g2.shape[2]
+        if B.fusable(c2, c1, W):
+            g1, st_g = B.conv_bwd(c2, g2, a, mask=True), None
+        else:
+            B.conv_wgrad(c2, g2, a)
+            g1, st_g = B.conv_dgrad(c2, g2, mask=a, below=c1)
         B.ready([c2.mod, c2.bn])
         g1 = B.bn_bwd(c1, g1, st1, stats=st_g)
-        B.conv_wgrad(c1, g1, cat)
-        dskip, gup = B.conv_dgrad_split(c1, g1, C)
+        if B.fusable(c1, None, W):
+            dskip, gup = B.conv_bwd(c1, g1, cat, mask=False, split=C)
+        else:
+            B.conv_wgrad(c1, g1, cat)
+            dskip, gup = B.conv_dgrad_split(c1, g1, C)
         B.ready([c1.mod, c1.bn])
         if isinstance(d, _Up):
             gup = K.up2_bwd(gup)          # to the projection's (low) resolution

@@ -55,12 +55,14 @@ def _declare(L):
                  "dpa_igemm_halo", "dpa_wgrad_halo", "dpa_igemm_stream", "dpa_wgrad_stream", "dpa_adam_flat_dev", "dpa_igemm_glds",
                  "dpa_loss_finish", "dpa_loss_grad", "dpa_pool_bwd_code", "dpa_bn_fwd", "dpa_bn_bwd",
                  "dpa_up2_fwd", "dpa_up2_bwd", "dpa_deconv_bwd", "dpa_deconv_fwd", "dpa_slab_sum",
-                 "dpa_igemm_stream_blocks", "dpa_slab_fold"):
+                 "dpa_igemm_stream_blocks", "dpa_slab_fold", "dpa_bwd_stream"):
         getattr(L, name).restype = ctypes.c_int
     L.dpa_head_slab_blocks.restype = ctypes.c_int
     L.dpa_head_slab_blocks.argtypes = [ctypes.c_longlong]
     L.dpa_bn_slab_rows.restype = ctypes.c_int
     L.dpa_bn_slab_rows.argtypes = [ctypes.c_longlong, ctypes.c_int]
+    L.dpa_bwd_stream_geom.restype = ctypes.c_int
+    L.dpa_bwd_stream_geom.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
     L.dpa_error_string.restype = ctypes.c_char_p
 
 

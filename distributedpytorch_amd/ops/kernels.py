@@ -40,6 +40,13 @@ class WgradArgs(ctypes.Structure):
                [("abytes", ctypes.c_uint), ("bbytes", ctypes.c_uint)]
 
 
+class BwdArgs(ctypes.Structure):
+    _fields_ = [("g", c_void_p), ("x", c_void_p), ("wd", c_void_p), ("y", c_void_p), ("y2", c_void_p),
+                ("slab", c_void_p), ("bslab", c_void_p)] + \
+               [(n, c_int) for n in ("ldg", "ldx", "ldy", "ldy2", "split", "Kd", "N", "H", "W", "rh", "ipb")] + \
+               [("gbytes", ctypes.c_uint), ("xbytes", ctypes.c_uint)]
+
+
 class PackDesc(ctypes.Structure):
     _fields_ = [("src", c_ll), ("dst", c_ll), ("mode", c_int), ("Cout", c_int), ("Cin", c_int), ("Cs", c_int),
                 ("Ngemm", c_int), ("Kpad", c_int)]
@@ -92,6 +99,9 @@ USE_FUSED_HEAD = os.environ.get("DPA_NO_FUSED_HEAD", "0") != "1"
 USE_FUSED_BN = os.environ.get("DPA_NO_FUSED_BN", "0") != "1"
 # eval-mode BatchNorm folded into the preceding conv's weights/bias (models/hip_unet.py); DPA_NO_FOLD_BN=1 disables
 FOLD_BN_EVAL = os.environ.get("DPA_NO_FOLD_BN", "0") != "1"
+# fused conv backward (dgrad + weight/bias gradient in one row-streaming pass, csrc/bwd_stream.hip)
+# for the full-resolution 32/64-channel convs; DPA_NO_FUSED_BWD=1 -> separate dgrad / wgrad kernels
+USE_FUSED_BWD = os.environ.get("DPA_NO_FUSED_BWD", "0") != "1"
 
 
 def _extent_bytes(N, H, W, C, ld):
@@ -352,6 +362,65 @@ def _wgrad_stream(A, B, *, grid, M, Nc, gw, gb, Nreal):
         _check(L.dpa_wgrad_stream(ctypes.byref(a), c_int(hcfg), c_int(bp), c_int(rh), c_int(ipb), st), "wgrad_stream")
         _check(L.dpa_wgrad_reduce(_p(slab), _p(bslab), _p(gw), _p(gb), c_int(splits), c_int(9), c_int(M), c_int(Nc),
                                   c_int(Nreal), c_int(0), st), "wgrad_reduce")
+
+
+# ------------------------------------------------------------------------------- fused conv backward
+def bwd_fused_eligible(ci: int, co: int, W: int) -> bool:
+    """csrc/bwd_stream.hip serves conv3x3 s1 p1 with (Cin, Cout) in {32, 64}^2 and W % strip == 0."""
+    bp = ctypes.c_int(0)
+    pg = _lib.lib().dpa_bwd_stream_geom(c_int(ci), c_int(co), ctypes.byref(bp))
+    return pg > 0 and W % bp.value == 0
+
+
+def conv_bwd_fused(g: torch.Tensor, x: torch.Tensor, wd: torch.Tensor, Kd: int, gw: torch.Tensor,
+                   gb: Optional[torch.Tensor], *, mask: bool, dx: Optional[torch.Tensor] = None,
+                   dx2: Optional[torch.Tensor] = None, split: int = 0, target_blocks: int = 1024):
+    """Backward of ``y = conv3x3(x) (+bias)`` in one pass (csrc/bwd_stream.hip): returns
+    ``dx = conv3x3^T(g)`` (times ``x > 0`` when ``mask``; with ``dx2``/``split`` the channels
+    ``>= split`` go to ``dx2``) and ACCUMULATES the weight gradient into ``gw`` (PyTorch OIHW
+    layout, fp32) and the bias gradient into ``gb``.  ``g`` is the gradient w.r.t. the conv output
+    (ReLU mask already applied), ``wd`` the dgrad-packed weights ``[Cin][Kd]``."""
+    N, H, W, CO, ldg = _nhwc(g, "bwd.g")
+    Nx, Hx, Wx, CI, ldx = _nhwc(x, "bwd.x")
+    assert (Nx, Hx, Wx) == (N, H, W), (tuple(g.shape), tuple(x.shape))
+    assert wd.dtype == torch.bfloat16 and wd.numel() >= CI * Kd and Kd >= 9 * CO and Kd % 32 == 0
+    assert gw.dtype == torch.float32 and gw.is_contiguous() and gw.numel() == CO * CI * 9
+    assert gb is None or (gb.dtype == torch.float32 and gb.numel() == CO)
+    bp = ctypes.c_int(0)
+    L = _lib.lib()
+    pg = L.dpa_bwd_stream_geom(c_int(CI), c_int(CO), ctypes.byref(bp))
+    assert pg > 0 and W % bp.value == 0, f"fused backward not available for {CI}->{CO} at W={W}"
+    if dx2 is not None:
+        assert 0 < split < CI and split % 16 == 0 and not mask
+        if dx is None:
+            dx = torch.empty(N, H, W, split, dtype=torch.bfloat16, device=g.device)
+        _, _, _, C1, ldy = _nhwc(dx, "bwd.dx")
+        _, _, _, C2, ldy2 = _nhwc(dx2, "bwd.dx2")
+        assert C1 >= split and C2 >= CI - split and tuple(dx2.shape[:3]) == (N, H, W)
+        epi = 1
+    else:
+        if dx is None:
+            dx = torch.empty(N, H, W, CI, dtype=torch.bfloat16, device=g.device)
+        _, _, _, C1, ldy = _nhwc(dx, "bwd.dx")
+        assert C1 >= CI
+        ldy2, epi = 0, (0 if mask else 2)
+    assert tuple(dx.shape[:3]) == (N, H, W)
+    strips = W // bp.value
+    # whole image columns per block; split the rows only when the batch gives too few blocks
+    segs = max(1, min(H, -(-target_blocks // max(1, N * strips))))
+    rh = -(-H // segs)
+    nblk = N * strips * (-(-H // rh))
+    slab = torch.empty(nblk * pg * 9 * CO * CI + (nblk * pg * CO if gb is not None else 0), dtype=torch.float32,
+                       device=g.device)
+    bslab = slab[nblk * pg * 9 * CO * CI:] if gb is not None else None
+    a = BwdArgs(g.data_ptr(), x.data_ptr(), wd.data_ptr(), dx.data_ptr(), None if dx2 is None else dx2.data_ptr(),
+                slab.data_ptr(), None if bslab is None else bslab.data_ptr(), ldg, ldx, ldy, ldy2, split, Kd,
+                N, H, W, rh, 1, _extent_bytes(1, H, W, CO, ldg), _extent_bytes(1, H, W, CI, ldx))
+    st = _stream(g)
+    _check(L.dpa_bwd_stream(ctypes.byref(a), c_int(CI), c_int(CO), c_int(epi), st), "bwd_stream")
+    _check(L.dpa_wgrad_reduce(_p(slab), _p(bslab), _p(gw), _p(gb), c_int(nblk * pg), c_int(9), c_int(CO), c_int(CI),
+                              c_int(CI), c_int(0), st), "wgrad_reduce(bwd_stream)")
+    return (dx, dx2) if dx2 is not None else dx
 
 
 # ------------------------------------------------------------------------------------------ aux

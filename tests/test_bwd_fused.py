@@ -1,0 +1,75 @@
+"""Fused conv3x3 backward (csrc/bwd_stream.hip): input gradient + weight gradient + bias gradient of
+one conv in a single row-streaming pass, against the fp32 PyTorch reference of the same op
+(autograd of ``F.conv2d``), for every (Cin, Cout) pair it serves and each epilogue: dx masked by the
+input's ReLU support, dx split into the two halves of a concat gradient, dx plain.  The weight /
+bias gradients accumulate into the flat fp32 buffer (existing content is kept)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from test_hip_kernels import _bf, _nchw, _nhwc, _pack_one, _rel
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("N,H,W,Cin,Cout,epi", [
+    (2, 5, 64, 32, 32, "mask"), (1, 37, 128, 32, 32, "mask"), (2, 3, 64, 32, 32, "plain"),
+    (2, 6, 64, 64, 32, "split"), (1, 9, 128, 64, 32, "mask"),
+    (2, 4, 64, 32, 64, "plain"), (1, 7, 192, 32, 64, "mask"),
+    (2, 5, 64, 64, 64, "mask"), (1, 3, 128, 64, 64, "split"),
+])
+def test_conv_bwd_fused_matches_torch(hip_lib, N, H, W, Cin, Cout, epi):
+    from distributedpytorch_amd.ops import kernels as K
+    torch.manual_seed(7)
+    x = _bf(F.relu(torch.randn(N, Cin, H, W)))          # a ReLU output (mask source)
+    w = _bf(torch.randn(Cout, Cin, 3, 3) * 0.05)
+    g = _bf(torch.randn(N, Cout, H, W))
+    xr = x.clone().requires_grad_(True)
+    wr = w.clone().requires_grad_(True)
+    br = torch.zeros(Cout, requires_grad=True)
+    F.conv2d(xr, wr, br, padding=1).backward(g)
+    dx_ref = xr.grad * (x > 0) if epi == "mask" else xr.grad
+    packed, ng, kd = _pack_one(1, w)
+    gw0 = torch.randn(Cout * Cin * 9, device="cuda")   # accumulate semantics
+    gb0 = torch.randn(Cout, device="cuda")
+    gw, gb = gw0.clone(), gb0.clone()
+    if epi == "split":
+        s = Cin // 2
+        dx, dx2 = K.conv_bwd_fused(_nhwc(g), _nhwc(x), packed, kd, gw, gb, mask=False,
+                                   dx2=torch.empty(N, H, W, Cin - s, dtype=torch.bfloat16, device="cuda"), split=s)
+        full = torch.cat([_nchw(dx), _nchw(dx2)], dim=1)
+    else:
+        full = _nchw(K.conv_bwd_fused(_nhwc(g), _nhwc(x), packed, kd, gw, gb, mask=epi == "mask"))
+    torch.cuda.synchronize()
+    assert _rel(full, dx_ref) < 2e-2
+    # weight / bias gradients: bf16 inputs, fp32 accumulation -> only summation order differs
+    assert _rel((gw - gw0).cpu(), wr.grad.reshape(-1)) < 1e-4
+    assert _rel((gb - gb0).cpu(), br.grad) < 1e-4
+
+
+def test_conv_bwd_fused_deterministic_and_matches_unfused(hip_lib):
+    """Bitwise run-to-run reproducible (fixed-order slab reduction); agrees with the separate
+    dgrad + weight-gradient kernels it replaces."""
+    from distributedpytorch_amd.ops import kernels as K
+    torch.manual_seed(8)
+    N, H, W, C = 3, 16, 128, 32
+    x = _nhwc(_bf(F.relu(torch.randn(N, C, H, W))))
+    g = _nhwc(_bf(torch.randn(N, C, H, W)))
+    w = _bf(torch.randn(C, C, 3, 3) * 0.05)
+    packed, ng, kd = _pack_one(1, w)
+    outs = []
+    for _ in range(2):
+        gw = torch.zeros(C * C * 9, device="cuda")
+        gb = torch.zeros(C, device="cuda")
+        dx = K.conv_bwd_fused(g, x, packed, kd, gw, gb, mask=True)
+        outs.append((dx.clone(), gw, gb))
+    torch.cuda.synchronize()
+    assert all(torch.equal(a, b) for a, b in zip(outs[0], outs[1]))
+    dx_u = torch.empty_like(outs[0][0])
+    K.igemm(g, packed, dx_u, Ngemm=ng, Kpad=kd, KH=3, KW=3, stride=1, pad=1, Cs=C, out_grid=(N, H, W), mask=x)
+    gw_u = torch.zeros(C * C * 9, device="cuda")
+    gb_u = torch.zeros(C, device="cuda")
+    K.wgrad(g, x, kind=0, grid=(N, H, W), M=C, Nc=C, s=1, pad=1, KW=3, gw=gw_u, gb=gb_u, Nreal=C)
+    torch.cuda.synchronize()
+    assert torch.equal(dx_u, outs[0][0])           # same MFMA sequence per output element
+    assert _rel(outs[0][1].cpu(), gw_u.cpu()) < 1e-5 and _rel(outs[0][2].cpu(), gb_u.cpu()) < 1e-5
