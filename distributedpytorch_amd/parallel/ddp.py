@@ -6,11 +6,15 @@ Design (MI355X-first, not a translation of torch's C++ Reducer):
 * Gradients live in ONE flat fp32 buffer in backward order (:class:`..optim.FlatParameterSpace`).
   A bucket is a contiguous slice of it -> the all-reduce runs in place on the slice, no
   flatten/unflatten copies.
-* Buckets are cut at ``bucket_mb`` (default 8 MiB): 29.6 MiB of UNet grads -> 4 buckets plus a small
-  first one, so the collective for the deepest (largest) layers starts while the full-resolution
-  backward layers (the long tail of the step) are still running.  On 8 GPUs with 7 xGMI links
-  each, RCCL's ring/tree channels spread an 8 MiB message over all links; smaller buckets only
-  add per-collective latency (measured sweep in BASELINE.md).
+* Buckets are cut at ``bucket_mb`` (default 8 MiB) after a 1 MiB first bucket: 29.6 MiB of UNet
+  grads -> 5 buckets.  ``tools/bucket_plan.py`` derives the choice from the measured per-block
+  backward timeline (batch 256, 512^2) and an all-reduce cost model: the decoder's full-resolution
+  levels take the first ~40 ms of the ~63 ms backward, so every bucket but the last hides behind
+  compute; what can be exposed is the all-reduce of the LAST bucket (the encoder levels, whose
+  gradients finish last), which the backward-ordered layout keeps at 0.5 MiB.  Model estimate at
+  8 GPUs: 30-80 us exposed for 1-8 MiB buckets, more for 16-25 MiB (the last bucket then holds
+  the bottleneck too); 8 MiB keeps the collective count at 5.  The bench JSON reports the measured
+  ``exposed_comm_ms_last_step``.
 * Buckets are launched strictly in index order, as soon as every gradient in it and in all
   earlier buckets has been produced -> identical collective order on every rank (no deadlock even
   if autograd finishes parameters in a different order) and overlap with the rest of backward.
