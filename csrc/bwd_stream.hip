@@ -37,6 +37,11 @@ struct BwdArgs {
   int N, H, W;
   int rh, ipb;          // rows per block, images per block
   unsigned gbytes, xbytes;  // addressable bytes of ONE image of g / x (buffer offsets are per image)
+  // HEAD mode (last decoder conv feeding the fused segmentation head): `g` is the conv's OUTPUT y and
+  // the gradient is formed on load, g = dz * hw[c] * (y > 0) with z = hb + sum_c hw[c] y[c],
+  // p = sigmoid(z), dz from the BCE/Dice partial-sum gradient dS (head_bwd_kernel's formula);
+  // the segmap gradients sum_p dz*y[c], sum_p dz go to hslab[block][C+1].
+  const float* tgt; const float* hw; const float* hb; const float* dS; float* hslab;
 };
 
 // 8 consecutive k (pixel rows roff+8g .. +7) of 16 channels starting at col0, from an nk image
@@ -65,7 +70,7 @@ __device__ __forceinline__ bf16x8_t tr_pair(const char* base, int off0, int off1
   return __builtin_bit_cast(bf16x8_t, v);
 }
 
-template <int BP, int CI, int CO, int NW, int PG, int EPI>
+template <int BP, int CI, int CO, int NW, int PG, int EPI, bool HEAD>
 __global__ __launch_bounds__(64 * NW) void bwd_stream_kernel(BwdArgs a) {
   constexpr int NT = 64 * NW;
   constexpr int HR = BP + 2;                   // ring row: BP pixels + 1 halo pixel each side
@@ -82,6 +87,7 @@ __global__ __launch_bounds__(64 * NW) void bwd_stream_kernel(BwdArgs a) {
   constexpr int KST = BP / 32 / PG;            // pixel k-steps per wave per row
   static_assert(TP >= 1 && TC >= 1 && MSPL >= 1 && NTI * MSPL * PG == NW && MTW * MSPL == MTI && (BP / 32) % PG == 0,
                 "tile");
+  static_assert(!HEAD || (CO == 32 && EPI == 0), "head mode: 32-channel last decoder conv");
   constexpr int GCH = KSO * HR * 4, XCH = HR * (CI / 8);         // 16-B chunks per ring row
   constexpr int LG = (GCH + NT - 1) / NT, LX = (XCH + NT - 1) / NT;
   constexpr int BCH = BP * 4 * KSO, LBI = (BCH + NT - 1) / NT;   // bias: chunks of the g row's BP pixels
@@ -102,9 +108,10 @@ __global__ __launch_bounds__(64 * NW) void bwd_stream_kernel(BwdArgs a) {
   const int wp = wid % WPX, wc = wid / WPX;                      // dx role
   const int nt = wid % NTI, msp = (wid / NTI) % MSPL, pg = wid / (NTI * MSPL);   // dW role
   // buffer resources are rebuilt per image (32-bit offsets stay inside one image at any batch size)
-  __amdgpu_buffer_rsrc_t gr, xr, yr, y2r;
+  __amdgpu_buffer_rsrc_t gr, xr, yr, y2r, tr;
   auto bind = [&](int img) {
     const long pix = (long)img * a.H * a.W;
+    if constexpr (HEAD) tr = __builtin_amdgcn_make_buffer_rsrc((void*)(a.tgt + pix), 0, a.H * a.W * 4, 0x00020000);
     gr = __builtin_amdgcn_make_buffer_rsrc((void*)(a.g + pix * a.ldg), 0, (int)a.gbytes, 0x00020000);
     xr = __builtin_amdgcn_make_buffer_rsrc((void*)(a.x + pix * a.ldx), 0, (int)a.xbytes, 0x00020000);
     yr = __builtin_amdgcn_make_buffer_rsrc((void*)(a.y + pix * a.ldy), 0, 0x7fffffff, 0x00020000);
@@ -141,10 +148,31 @@ __global__ __launch_bounds__(64 * NW) void bwd_stream_kernel(BwdArgs a) {
     xsto[j] = c < XCH ? px * RBX + ((cc ^ swz_kk<RBX>(px)) << 4) : -1;
   }
   const unsigned growb = (unsigned)(a.W * a.ldg * 2), xrowb = (unsigned)(a.W * a.ldx * 2);
+  // HEAD: segmap weights of this thread's 8 channels (cc = tid & 3 for every chunk it loads), the
+  // target offset of each chunk's pixel, and whether the pixel is this block's own (not halo)
+  float hwv[8], hdw[8], hbias = 0.f, hd0 = 0.f, hd1 = 0.f, hd2 = 0.f, hdb = 0.f;
+  unsigned tpo[HEAD ? LG : 1];
+  bool hval[HEAD ? LG : 1];
+  if constexpr (HEAD) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      hwv[e] = a.hw[(tid & 3) * 8 + e];
+      hdw[e] = 0.f;
+    }
+    hbias = a.hb[0];
+    hd0 = a.dS[0]; hd1 = a.dS[1]; hd2 = a.dS[2];
+#pragma unroll
+    for (int j = 0; j < LG; ++j) {
+      const int c = tid + j * NT, px = (c >> 2) % HR;
+      tpo[j] = (unsigned)(w0 + px - 1) * 4u;
+      hval[j] = c < GCH && px >= 1 && px <= BP;
+    }
+  }
   // two register sets: the loads of a row are issued two rows before it is stored into the ring
   // (one row of compute was too short to cover the load latency at 1-2 blocks per CU)
   struct RowRegs {
     u32x4_t g[LG], x[LX];
+    unsigned t[HEAD ? LG : 1];            // HEAD: target bits of each chunk's pixel
   };
   RowRegs setA, setB;
   int n = ig * a.ipb;
@@ -155,8 +183,46 @@ __global__ __launch_bounds__(64 * NW) void bwd_stream_kernel(BwdArgs a) {
     for (int j = 0; j < LG; ++j) R.g[j] = __builtin_amdgcn_raw_buffer_load_b128(gr, (rok && gok[j]) ? gb + goff[j] : 0x80000000u, 0, 0);
 #pragma unroll
     for (int j = 0; j < LX; ++j) R.x[j] = __builtin_amdgcn_raw_buffer_load_b128(xr, (rok && xok[j]) ? xb + xoff[j] : 0x80000000u, 0, 0);
+    if constexpr (HEAD) {
+#pragma unroll
+      for (int j = 0; j < LG; ++j)
+        R.t[j] = __builtin_amdgcn_raw_buffer_load_b32(tr, (rok && gok[j]) ? (unsigned)(ih * a.W) * 4u + tpo[j] : 0x80000000u, 0, 0);
+    }
   };
-  auto rstore = [&](int slot, const RowRegs& R) {
+  auto rstore = [&](int slot, RowRegs& R, int ih) {
+    if constexpr (HEAD) {                       // y chunk -> gradient chunk (+ segmap gradient partials)
+      const bool rowv = ih >= h0 && ih < h0 + nrows;
+#pragma unroll
+      for (int j = 0; j < LG; ++j) {
+        float yv[8];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          yv[2 * e] = lo_bf(R.g[j][e]);
+          yv[2 * e + 1] = hi_bf(R.g[j][e]);
+        }
+        float zp = 0.f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) zp = fmaf(yv[e], hwv[e], zp);
+        zp += __shfl_xor(zp, 1, 64);             // the pixel's 4 chunks sit in lanes 4k..4k+3
+        zp += __shfl_xor(zp, 2, 64);
+        const float z = zp + hbias;
+        const float p = 1.f / (1.f + __expf(-z));
+        const float tt = __uint_as_float(R.t[j]);
+        const float one = tt == 1.f ? 1.f : 0.f;
+        const float dp = hd0 * (p - tt) / fmaxf((1.f - p) * p, 1e-12f) + hd1 * one + hd2;
+        const float dz = dp * (1.f - p) * p;
+        unsigned o[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          o[e] = pack_bf2(yv[2 * e] > 0.f ? dz * hwv[2 * e] : 0.f, yv[2 * e + 1] > 0.f ? dz * hwv[2 * e + 1] : 0.f);
+        R.g[j] = u32x4_t{o[0], o[1], o[2], o[3]};
+        if (rowv && hval[j]) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) hdw[e] = fmaf(dz, yv[e], hdw[e]);
+          if ((tid & 3) == 0) hdb += dz;
+        }
+      }
+    }
 #pragma unroll
     for (int j = 0; j < LG; ++j)
       if (gsto[j] >= 0) *reinterpret_cast<u32x4_t*>(Gring + slot * GSLOT + gsto[j]) = R.g[j];
@@ -244,7 +310,7 @@ __global__ __launch_bounds__(64 * NW) void bwd_stream_kernel(BwdArgs a) {
 #pragma unroll 1
       for (int j = 0; j < 3; ++j) {           // rows h0-1, h0, h0+1 -> slots 0..2
         rload(h0 - 1 + j, setA);
-        rstore(j, setA);
+        rstore(j, setA, h0 - 1 + j);
       }
       if (nrows > 1) rload(h0 + 2, setA);      // in flight during row 0
     }
@@ -336,7 +402,7 @@ __global__ __launch_bounds__(64 * NW) void bwd_stream_kernel(BwdArgs a) {
             __builtin_amdgcn_raw_buffer_store_b64(packed, yr, orow * yrowb + yoff[ip][ic], 0, 0);
         }
       __builtin_amdgcn_sched_barrier(0);
-      if (r + 1 < nrows) rstore((r + 3) & 3, cur);
+      if (r + 1 < nrows) rstore((r + 3) & 3, cur, h0 + r + 2);
       __syncthreads();
     };
 #pragma unroll 1
@@ -379,12 +445,31 @@ __global__ __launch_bounds__(64 * NW) void bwd_stream_kernel(BwdArgs a) {
       a.bslab[((long)split_id * PG + q) * CO + cch] = s;
     }
   }
+  if constexpr (HEAD) {
+    // segmap gradient partials: per thread 8 channels (cc = tid & 3) + dz sum; fixed-order reduction
+    __syncthreads();
+    float* hp = reinterpret_cast<float*>(lds);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) hp[tid * 9 + e] = hdw[e];
+    hp[tid * 9 + 8] = hdb;
+    __syncthreads();
+    if (tid < 33) {
+      float sacc = 0.f;
+      if (tid < 32) {
+        const int cc = tid >> 3, e = tid & 7;
+        for (int t2 = cc; t2 < NT; t2 += 4) sacc += hp[t2 * 9 + e];
+      } else {
+        for (int t2 = 0; t2 < NT; t2 += 4) sacc += hp[t2 * 9 + 8];
+      }
+      a.hslab[(long)split_id * 33 + tid] = sacc;
+    }
+  }
 }
 
-template <int BP, int CI, int CO, int NW, int PG, int EPI>
+template <int BP, int CI, int CO, int NW, int PG, int EPI, bool HEAD = false>
 static int launch_bwd_stream(const BwdArgs& a, hipStream_t st) {
   const int blocks = ((a.N + a.ipb - 1) / a.ipb) * ((a.H + a.rh - 1) / a.rh) * (a.W / BP);
-  hipLaunchKernelGGL((bwd_stream_kernel<BP, CI, CO, NW, PG, EPI>), dim3(blocks), dim3(64 * NW), 0, st, a);
+  hipLaunchKernelGGL((bwd_stream_kernel<BP, CI, CO, NW, PG, EPI, HEAD>), dim3(blocks), dim3(64 * NW), 0, st, a);
   return (int)hipGetLastError();
 }
 
@@ -415,6 +500,11 @@ DPA_API int dpa_bwd_stream(const BwdArgs* args, int ci, int co, int epi, hipStre
     if (epi == 0) return launch_bwd_stream<BPv, CIv, COv, NWv, PGv, 0>(a, st);     \
     if (epi == 1) return launch_bwd_stream<BPv, CIv, COv, NWv, PGv, 1>(a, st);     \
     if (epi == 2) return launch_bwd_stream<BPv, CIv, COv, NWv, PGv, 2>(a, st);     \
+  }
+  if (a.hslab != nullptr) {                        // fused head backward: last decoder conv 32 -> 32
+    if (ci == 32 && co == 32 && epi == 0 && a.tgt && a.hw && a.hb && a.dS)
+      return launch_bwd_stream<64, 32, 32, 4, 2, 0, true>(a, st);
+    return (int)hipErrorInvalidValue;
   }
   DPA_BWD(32, 32, 64, 4, 2)
   DPA_BWD(64, 32, 64, 8, 2)

@@ -417,6 +417,13 @@ DPA_API int dpa_head_bwd(const bf16_t* y, int ldy, int C, const float* w, const 
 
 DPA_API int dpa_head_slab_blocks(long long P) { return head_grid(P); }
 
+// segmap gradients from a [nblk][C+1] slab written elsewhere (the fused conv backward's head mode)
+DPA_API int dpa_head_grad_from_slab(const float* slab, int nblk, int C, float* tmp, float* gw, float* gb, hipStream_t st) {
+  hipLaunchKernelGGL(slab_sum_kernel, dim3(C + 1), dim3(256), 0, st, slab, nblk, C + 1, tmp, 0);
+  hipLaunchKernelGGL(head_grad_finish, dim3(1), dim3(128), 0, st, tmp, gw, gb, C);
+  return (int)hipGetLastError();
+}
+
 DPA_API int dpa_slab_sum(const float* slab, int nblk, int K, float* out, hipStream_t st) {
   hipLaunchKernelGGL(slab_sum_kernel, dim3(K), dim3(256), 0, st, slab, nblk, K, out, 0);
   return (int)hipGetLastError();

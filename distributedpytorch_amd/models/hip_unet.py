@@ -133,6 +133,7 @@ class HipBlocks:
         # that skip into a dense tensor, which then goes on the wire as is (no concat-half copy)
         self.dense_skips = set()
         self._fusable = {}
+        self._head_pending = None   # (placeholder grad, y, target, dS): head backward deferred to the decoder
 
     # ------------------------------------------------------------------ weight packing
     def _build_packing(self):
@@ -305,15 +306,22 @@ class HipBlocks:
             ok = self._fusable[key] = K.bwd_fused_eligible(c.Cin, c.Cout, W)
         return ok
 
-    def conv_bwd(self, c: _Conv, g: torch.Tensor, x: torch.Tensor, mask: bool, split: int = 0):
+    def conv_bwd(self, c: _Conv, g: torch.Tensor, x: torch.Tensor, mask: bool, split: int = 0, head=None):
         """Fused backward of ``c``: returns dx (ReLU-masked by ``x`` when ``mask``; with ``split`` the
-        two dense halves of a concat gradient) and accumulates the weight and bias gradients."""
+        two dense halves of a concat gradient) and accumulates the weight and bias gradients.
+        ``head``: ``g`` is the conv output and the segmentation-head backward is folded in."""
         gw, gb = _grad(c.mod.weight).view(-1), _grad(c.mod.bias)
         if split:
             N, H, W = g.shape[:3]
             hi = torch.empty(N, H, W, c.Cin - split, dtype=torch.bfloat16, device=g.device)
             return K.conv_bwd_fused(g, x, self.wd(c), c.Kd, gw, gb, mask=False, dx2=hi, split=split)
-        return K.conv_bwd_fused(g, x, self.wd(c), c.Kd, gw, gb, mask=mask)
+        return K.conv_bwd_fused(g, x, self.wd(c), c.Kd, gw, gb, mask=mask, head=head)
+
+    def head_bwd_foldable(self, W: int) -> bool:
+        """The head backward can be folded into the last decoder conv's fused backward."""
+        c1, c2 = self.dec_convs[-1]
+        return (K.USE_FUSED_HEAD_BWD and c2.Cin == 32 and c2.Cout == 32 and self.model.segmap.out_channels == 1
+                and self.fusable(c2, c1, W))
 
     def conv_wgrad(self, c: _Conv, g: torch.Tensor, x: torch.Tensor):
         N, H, W = g.shape[:3]
@@ -617,13 +625,25 @@ class _DecFn(torch.autograd.Function):
         d = B.deconvs[i]
         c1, c2 = B.dec_convs[i]
         C = d.Cout
-        g2 = B.bn_bwd(c2, _v(g2), st2)
-        W = g2.shape[2]
-        if B.fusable(c2, c1, W):
-            g1, st_g = B.conv_bwd(c2, g2, a, mask=True), None
+        pend = B._head_pending
+        if pend is not None and g2.data_ptr() == pend[0].data_ptr() and g2.stride() == pend[0].stride():
+            # the head's gradient was deferred (_HeadFn.backward): it is formed from y inside this
+            # conv's fused backward instead of being materialised (saves a write + read of it)
+            B._head_pending = None
+            _, y, t, dS = pend
+            seg = B.model.segmap
+            W = y.shape[2]
+            g1, st_g = B.conv_bwd(c2, y, a, mask=True, head=(t, seg.weight, seg.bias, dS,
+                                                             _grad(seg.weight).view(-1), _grad(seg.bias))), None
+            B.ready([seg])
         else:
-            B.conv_wgrad(c2, g2, a)
-            g1, st_g = B.conv_dgrad(c2, g2, mask=a, below=c1)
+            g2 = B.bn_bwd(c2, _v(g2), st2)
+            W = g2.shape[2]
+            if B.fusable(c2, c1, W):
+                g1, st_g = B.conv_bwd(c2, g2, a, mask=True), None
+            else:
+                B.conv_wgrad(c2, g2, a)
+                g1, st_g = B.conv_dgrad(c2, g2, mask=a, below=c1)
         B.ready([c2.mod, c2.bn])
         g1 = B.bn_bwd(c1, g1, st1, stats=st_g)
         if B.fusable(c1, None, W):
@@ -657,6 +677,8 @@ class _HeadFn(torch.autograd.Function):
         else:
             S, _ = K.head_fwd(y, seg.weight, seg.bias, t)
         ctx.B = B
+        # fused forward => y is this engine's last decoder conv output and its backward runs next
+        ctx.fold = cache is not None and cache[0] == y.data_ptr() and B.head_bwd_foldable(y.shape[2])
         ctx.save_for_backward(y, t)
         return S.clone()
 
@@ -665,6 +687,12 @@ class _HeadFn(torch.autograd.Function):
         B = ctx.B
         y, t = ctx.saved_tensors
         seg = B.model.segmap
+        if ctx.fold and t.is_contiguous():
+            # defer: hand the decoder a zero-stride placeholder of y's gradient; _DecFn.backward
+            # recognises it and folds the head backward into the last conv's fused backward
+            ph = torch.zeros((), dtype=y.dtype, device=y.device).expand(y.shape[0], y.shape[3], y.shape[1], y.shape[2])
+            B._head_pending = (ph, y, t.reshape(-1), dS)
+            return None, ph, None, None
         gy = K.head_bwd(y, seg.weight, seg.bias, t, dS, _grad(seg.weight).view(-1), _grad(seg.bias))
         B.ready([seg])
         return None, _o(gy), None, None

@@ -44,7 +44,8 @@ class BwdArgs(ctypes.Structure):
     _fields_ = [("g", c_void_p), ("x", c_void_p), ("wd", c_void_p), ("y", c_void_p), ("y2", c_void_p),
                 ("slab", c_void_p), ("bslab", c_void_p)] + \
                [(n, c_int) for n in ("ldg", "ldx", "ldy", "ldy2", "split", "Kd", "N", "H", "W", "rh", "ipb")] + \
-               [("gbytes", ctypes.c_uint), ("xbytes", ctypes.c_uint)]
+               [("gbytes", ctypes.c_uint), ("xbytes", ctypes.c_uint)] + \
+               [("tgt", c_void_p), ("hw", c_void_p), ("hb", c_void_p), ("dS", c_void_p), ("hslab", c_void_p)]
 
 
 class PackDesc(ctypes.Structure):
@@ -102,6 +103,9 @@ FOLD_BN_EVAL = os.environ.get("DPA_NO_FOLD_BN", "0") != "1"
 # fused conv backward (dgrad + weight/bias gradient in one row-streaming pass, csrc/bwd_stream.hip)
 # for the full-resolution 32/64-channel convs; DPA_NO_FUSED_BWD=1 -> separate dgrad / wgrad kernels
 USE_FUSED_BWD = os.environ.get("DPA_NO_FUSED_BWD", "0") != "1"
+# the segmentation head's backward folded into the last decoder conv's fused backward (the head
+# gradient is formed from y on load, never stored); DPA_NO_FUSED_HEAD_BWD=1 -> separate head_bwd
+USE_FUSED_HEAD_BWD = USE_FUSED_BWD and os.environ.get("DPA_NO_FUSED_HEAD_BWD", "0") != "1"
 
 
 def _extent_bytes(N, H, W, C, ld):
@@ -374,12 +378,18 @@ def bwd_fused_eligible(ci: int, co: int, W: int) -> bool:
 
 def conv_bwd_fused(g: torch.Tensor, x: torch.Tensor, wd: torch.Tensor, Kd: int, gw: torch.Tensor,
                    gb: Optional[torch.Tensor], *, mask: bool, dx: Optional[torch.Tensor] = None,
-                   dx2: Optional[torch.Tensor] = None, split: int = 0, target_blocks: int = 1024):
+                   dx2: Optional[torch.Tensor] = None, split: int = 0, target_blocks: int = 1024, head=None):
     """Backward of ``y = conv3x3(x) (+bias)`` in one pass (csrc/bwd_stream.hip): returns
     ``dx = conv3x3^T(g)`` (times ``x > 0`` when ``mask``; with ``dx2``/``split`` the channels
     ``>= split`` go to ``dx2``) and ACCUMULATES the weight gradient into ``gw`` (PyTorch OIHW
     layout, fp32) and the bias gradient into ``gb``.  ``g`` is the gradient w.r.t. the conv output
-    (ReLU mask already applied), ``wd`` the dgrad-packed weights ``[Cin][Kd]``."""
+    (ReLU mask already applied), ``wd`` the dgrad-packed weights ``[Cin][Kd]``.
+
+    ``head`` = (target fp32 [N*H*W], segmap weight [C], segmap bias [1], dS [4], segmap weight grad,
+    segmap bias grad): ``g`` is then the conv's OUTPUT y (the last decoder conv, whose epilogue
+    computed the fused head + loss partials in the forward) and the head backward (``head_bwd``) is
+    folded into the loader: the gradient is formed from y on the fly and never stored; the segmap
+    gradients accumulate into the last two tensors."""
     N, H, W, CO, ldg = _nhwc(g, "bwd.g")
     Nx, Hx, Wx, CI, ldx = _nhwc(x, "bwd.x")
     assert (Nx, Hx, Wx) == (N, H, W), (tuple(g.shape), tuple(x.shape))
@@ -417,7 +427,21 @@ def conv_bwd_fused(g: torch.Tensor, x: torch.Tensor, wd: torch.Tensor, Kd: int, 
                 slab.data_ptr(), None if bslab is None else bslab.data_ptr(), ldg, ldx, ldy, ldy2, split, Kd,
                 N, H, W, rh, 1, _extent_bytes(1, H, W, CO, ldg), _extent_bytes(1, H, W, CI, ldx))
     st = _stream(g)
+    hslab = None
+    if head is not None:
+        tgt, hw, hb, dS, hgw, hgb = head
+        assert epi == 0 and CI == CO == 32, "head mode: the 32->32 last decoder conv"
+        assert tgt.dtype == torch.float32 and tgt.is_contiguous() and tgt.numel() == N * H * W
+        assert hw.dtype == torch.float32 and hw.numel() == CO and hb.numel() == 1
+        assert hgw.is_contiguous() and hgw.numel() == CO and hgb.numel() == 1
+        dS = dS.float().contiguous()
+        hslab = torch.empty(nblk * (CO + 1) + CO + 1, dtype=torch.float32, device=g.device)
+        hw = hw.reshape(-1).contiguous()
+        a.tgt, a.hw, a.hb, a.dS, a.hslab = tgt.data_ptr(), hw.data_ptr(), hb.data_ptr(), dS.data_ptr(), hslab.data_ptr()
     _check(L.dpa_bwd_stream(ctypes.byref(a), c_int(CI), c_int(CO), c_int(epi), st), "bwd_stream")
+    if hslab is not None:
+        _check(L.dpa_head_grad_from_slab(_p(hslab), c_int(nblk), c_int(CO), _p(hslab[nblk * (CO + 1):]), _p(hgw),
+                                         _p(hgb), st), "head_grad_from_slab")
     _check(L.dpa_wgrad_reduce(_p(slab), _p(bslab), _p(gw), _p(gb), c_int(nblk * pg), c_int(9), c_int(CO), c_int(CI),
                               c_int(CI), c_int(0), st), "wgrad_reduce(bwd_stream)")
     return (dx, dx2) if dx2 is not None else dx

@@ -73,3 +73,33 @@ def test_conv_bwd_fused_deterministic_and_matches_unfused(hip_lib):
     torch.cuda.synchronize()
     assert torch.equal(dx_u, outs[0][0])           # same MFMA sequence per output element
     assert _rel(outs[0][1].cpu(), gw_u.cpu()) < 1e-5 and _rel(outs[0][2].cpu(), gb_u.cpu()) < 1e-5
+
+
+@pytest.mark.parametrize("N,H,W", [(2, 5, 64), (1, 33, 128)])
+def test_conv_bwd_fused_head_mode_matches_separate_head_bwd(hip_lib, N, H, W):
+    """Head mode: the segmentation-head backward folded into the last decoder conv's fused backward
+    (gradient formed from the conv output y on load) equals head_bwd followed by the plain fused
+    backward: dx, conv weight/bias gradients and segmap weight/bias gradients."""
+    from distributedpytorch_amd.ops import kernels as K
+    torch.manual_seed(9)
+    C = 32
+    a = _nhwc(_bf(F.relu(torch.randn(N, C, H, W))))              # conv input (ReLU output)
+    y = _nhwc(_bf(F.relu(torch.randn(N, C, H, W))))              # conv output (ReLU output)
+    t = (torch.rand(N * H * W, device="cuda") > 0.5).float()
+    hw = (torch.randn(C) * 0.2).cuda()
+    hb = torch.randn(1).cuda()
+    dS = torch.tensor([1.0 / (N * H * W), -0.01, 0.002, 0.002], device="cuda")
+    w = _bf(torch.randn(C, C, 3, 3) * 0.05)
+    packed, ng, kd = _pack_one(1, w)
+    # reference: separate head backward, then the fused conv backward on the stored gradient
+    hgw_r, hgb_r = torch.zeros(C, device="cuda"), torch.zeros(1, device="cuda")
+    gy = K.head_bwd(y, hw, hb, t, dS, hgw_r, hgb_r)
+    gw_r, gb_r = torch.zeros(C * C * 9, device="cuda"), torch.zeros(C, device="cuda")
+    dx_r = K.conv_bwd_fused(gy, a, packed, kd, gw_r, gb_r, mask=True)
+    hgw, hgb = torch.zeros(C, device="cuda"), torch.zeros(1, device="cuda")
+    gw, gb = torch.zeros(C * C * 9, device="cuda"), torch.zeros(C, device="cuda")
+    dx = K.conv_bwd_fused(y, a, packed, kd, gw, gb, mask=True, head=(t, hw, hb, dS, hgw, hgb))
+    torch.cuda.synchronize()
+    assert _rel(dx.float().cpu(), dx_r.float().cpu()) < 1e-2
+    assert _rel(gw.cpu(), gw_r.cpu()) < 1e-2 and _rel(gb.cpu(), gb_r.cpu()) < 1e-2
+    assert _rel(hgw.cpu(), hgw_r.cpu()) < 1e-4 and _rel(hgb.cpu(), hgb_r.cpu()) < 1e-4
