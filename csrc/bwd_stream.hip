@@ -42,6 +42,10 @@ struct BwdArgs {
   // p = sigmoid(z), dz from the BCE/Dice partial-sum gradient dS (head_bwd_kernel's formula);
   // the segmap gradients sum_p dz*y[c], sum_p dz go to hslab[block][C+1].
   const float* tgt; const float* hw; const float* hb; const float* dS; float* hslab;
+  // POOL mode (encoder conv2 whose output was max-pooled with window codes): `g` is the skip gradient
+  // dskip (or null) and the gradient is formed on load as in pool_bwd_code_kernel,
+  //   g[p][c] = (dskip[p][c] + (argmax(window)[c] == q(p) ? dpool[window][c] : 0)) * mask_q(p)[c]
+  const unsigned char* pcode; const bf16_t* dpool; int ldp;
 };
 
 // 8 consecutive k (pixel rows roff+8g .. +7) of 16 channels starting at col0, from an nk image
@@ -70,8 +74,8 @@ __device__ __forceinline__ bf16x8_t tr_pair(const char* base, int off0, int off1
   return __builtin_bit_cast(bf16x8_t, v);
 }
 
-template <int BP, int CI, int CO, int NW, int PG, int EPI, bool HEAD>
-__global__ __launch_bounds__(64 * NW) void bwd_stream_kernel(BwdArgs a) {
+template <int BP, int CI, int CO, int NW, int PG, int EPI, bool HEAD, bool POOL>
+__global__ __launch_bounds__(64 * NW, 2) void bwd_stream_kernel(BwdArgs a) {
   constexpr int NT = 64 * NW;
   constexpr int HR = BP + 2;                   // ring row: BP pixels + 1 halo pixel each side
   constexpr int KSO = CO / 32;                 // 32-channel slices of g
@@ -88,6 +92,7 @@ __global__ __launch_bounds__(64 * NW) void bwd_stream_kernel(BwdArgs a) {
   static_assert(TP >= 1 && TC >= 1 && MSPL >= 1 && NTI * MSPL * PG == NW && MTW * MSPL == MTI && (BP / 32) % PG == 0,
                 "tile");
   static_assert(!HEAD || (CO == 32 && EPI == 0), "head mode: 32-channel last decoder conv");
+  static_assert(!(HEAD && POOL), "one gradient source");
   constexpr int GCH = KSO * HR * 4, XCH = HR * (CI / 8);         // 16-B chunks per ring row
   constexpr int LG = (GCH + NT - 1) / NT, LX = (XCH + NT - 1) / NT;
   constexpr int BCH = BP * 4 * KSO, LBI = (BCH + NT - 1) / NT;   // bias: chunks of the g row's BP pixels
@@ -108,11 +113,17 @@ __global__ __launch_bounds__(64 * NW) void bwd_stream_kernel(BwdArgs a) {
   const int wp = wid % WPX, wc = wid / WPX;                      // dx role
   const int nt = wid % NTI, msp = (wid / NTI) % MSPL, pg = wid / (NTI * MSPL);   // dW role
   // buffer resources are rebuilt per image (32-bit offsets stay inside one image at any batch size)
-  __amdgpu_buffer_rsrc_t gr, xr, yr, y2r, tr;
+  __amdgpu_buffer_rsrc_t gr, xr, yr, y2r, tr, pr, cr;
+  const bool has_g = !POOL || a.g != nullptr;
   auto bind = [&](int img) {
     const long pix = (long)img * a.H * a.W;
+    if constexpr (POOL) {
+      const long win = (long)img * (a.H >> 1) * (a.W >> 1);
+      pr = __builtin_amdgcn_make_buffer_rsrc((void*)(a.dpool + win * a.ldp), 0, 0x7fffffff, 0x00020000);
+      cr = __builtin_amdgcn_make_buffer_rsrc((void*)(a.pcode + win * CO), 0, 0x7fffffff, 0x00020000);
+    }
     if constexpr (HEAD) tr = __builtin_amdgcn_make_buffer_rsrc((void*)(a.tgt + pix), 0, a.H * a.W * 4, 0x00020000);
-    gr = __builtin_amdgcn_make_buffer_rsrc((void*)(a.g + pix * a.ldg), 0, (int)a.gbytes, 0x00020000);
+    gr = __builtin_amdgcn_make_buffer_rsrc((void*)(has_g ? a.g + pix * a.ldg : a.x), 0, has_g ? (int)a.gbytes : 0, 0x00020000);
     xr = __builtin_amdgcn_make_buffer_rsrc((void*)(a.x + pix * a.ldx), 0, (int)a.xbytes, 0x00020000);
     yr = __builtin_amdgcn_make_buffer_rsrc((void*)(a.y + pix * a.ldy), 0, 0x7fffffff, 0x00020000);
     y2r = __builtin_amdgcn_make_buffer_rsrc((void*)(EPI == 1 ? a.y2 + pix * a.ldy2 : a.y), 0, 0x7fffffff, 0x00020000);
@@ -151,6 +162,19 @@ __global__ __launch_bounds__(64 * NW) void bwd_stream_kernel(BwdArgs a) {
   // HEAD: segmap weights of this thread's 8 channels (cc = tid & 3 for every chunk it loads), the
   // target offset of each chunk's pixel, and whether the pixel is this block's own (not halo)
   float hwv[8], hdw[8], hbias = 0.f, hd0 = 0.f, hd1 = 0.f, hd2 = 0.f, hdb = 0.f;
+  // POOL: per chunk the window column's byte offsets into dpool / codes and the pixel's column parity
+  unsigned ppo[POOL ? LG : 1], pco[POOL ? LG : 1], pq[POOL ? LG : 1];
+  if constexpr (POOL) {
+#pragma unroll
+    for (int j = 0; j < LG; ++j) {
+      const int c = tid + j * NT;
+      const int cc = c & 3, px = (c >> 2) % HR, ks = (c >> 2) / HR;
+      const int iw = max(w0 + px - 1, 0);
+      ppo[j] = (unsigned)(((iw >> 1) * a.ldp + ks * 32 + cc * 8) * 2);
+      pco[j] = (unsigned)((iw >> 1) * CO + ks * 32 + cc * 8);
+      pq[j] = (unsigned)(iw & 1);
+    }
+  }
   unsigned tpo[HEAD ? LG : 1];
   bool hval[HEAD ? LG : 1];
   if constexpr (HEAD) {
@@ -173,6 +197,8 @@ __global__ __launch_bounds__(64 * NW) void bwd_stream_kernel(BwdArgs a) {
   struct RowRegs {
     u32x4_t g[LG], x[LX];
     unsigned t[HEAD ? LG : 1];            // HEAD: target bits of each chunk's pixel
+    u32x4_t pd[POOL ? LG : 1];            // POOL: the pooled gradient of each chunk's window
+    u32x2_t pc[POOL ? LG : 1];            // POOL: the window codes of the chunk's 8 channels
   };
   RowRegs setA, setB;
   int n = ig * a.ipb;
@@ -188,8 +214,36 @@ __global__ __launch_bounds__(64 * NW) void bwd_stream_kernel(BwdArgs a) {
       for (int j = 0; j < LG; ++j)
         R.t[j] = __builtin_amdgcn_raw_buffer_load_b32(tr, (rok && gok[j]) ? (unsigned)(ih * a.W) * 4u + tpo[j] : 0x80000000u, 0, 0);
     }
+    if constexpr (POOL) {
+      const unsigned wrow = (unsigned)(ih >> 1) * (unsigned)(a.W >> 1);
+#pragma unroll
+      for (int j = 0; j < LG; ++j) {
+        const bool ok = rok && gok[j];
+        R.pd[j] = __builtin_amdgcn_raw_buffer_load_b128(pr, ok ? (wrow * a.ldp) * 2u + ppo[j] : 0x80000000u, 0, 0);
+        R.pc[j] = __builtin_amdgcn_raw_buffer_load_b64(cr, ok ? wrow * CO + pco[j] : 0x80000000u, 0, 0);
+      }
+    }
   };
   auto rstore = [&](int slot, RowRegs& R, int ih) {
+    if constexpr (POOL) {                       // (dskip, dpool, code) chunk -> gradient chunk
+#pragma unroll
+      for (int j = 0; j < LG; ++j) {
+        const unsigned q = (unsigned)((ih & 1) * 2) + pq[j];
+        const u32x4_t ps = R.g[j], pd = R.pd[j];
+        unsigned o[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const unsigned c2 = (k < 2 ? R.pc[j].x : R.pc[j].y) >> (16 * (k & 1));   // codes of channels 2k, 2k+1
+          const unsigned cl = c2 & 0xffu, ch = (c2 >> 8) & 0xffu;
+          float lo = lo_bf(ps[k]) + ((cl & 3u) == q ? lo_bf(pd[k]) : 0.f);
+          float hi = hi_bf(ps[k]) + ((ch & 3u) == q ? hi_bf(pd[k]) : 0.f);
+          lo = (cl >> (2 + q)) & 1u ? lo : 0.f;
+          hi = (ch >> (2 + q)) & 1u ? hi : 0.f;
+          o[k] = pack_bf2(lo, hi);
+        }
+        R.g[j] = u32x4_t{o[0], o[1], o[2], o[3]};
+      }
+    }
     if constexpr (HEAD) {                       // y chunk -> gradient chunk (+ segmap gradient partials)
       const bool rowv = ih >= h0 && ih < h0 + nrows;
 #pragma unroll
@@ -466,10 +520,10 @@ __global__ __launch_bounds__(64 * NW) void bwd_stream_kernel(BwdArgs a) {
   }
 }
 
-template <int BP, int CI, int CO, int NW, int PG, int EPI, bool HEAD = false>
+template <int BP, int CI, int CO, int NW, int PG, int EPI, bool HEAD = false, bool POOL = false>
 static int launch_bwd_stream(const BwdArgs& a, hipStream_t st) {
   const int blocks = ((a.N + a.ipb - 1) / a.ipb) * ((a.H + a.rh - 1) / a.rh) * (a.W / BP);
-  hipLaunchKernelGGL((bwd_stream_kernel<BP, CI, CO, NW, PG, EPI, HEAD>), dim3(blocks), dim3(64 * NW), 0, st, a);
+  hipLaunchKernelGGL((bwd_stream_kernel<BP, CI, CO, NW, PG, EPI, HEAD, POOL>), dim3(blocks), dim3(64 * NW), 0, st, a);
   return (int)hipGetLastError();
 }
 
@@ -483,6 +537,8 @@ static int bwd_cfg(int ci, int co, int* bp, int* nw) {
 }
 
 // Slab rows per block for (ci, co) (0: not supported) and the pixel strip width.
+DPA_API int dpa_bwd_stream_pool_ok(int ci, int co) { return ci == 32 && co == 32; }
+
 DPA_API int dpa_bwd_stream_geom(int ci, int co, int* bp) {
   int nw = 0;
   return bwd_cfg(ci, co, bp, &nw);
@@ -500,6 +556,12 @@ DPA_API int dpa_bwd_stream(const BwdArgs* args, int ci, int co, int epi, hipStre
     if (epi == 0) return launch_bwd_stream<BPv, CIv, COv, NWv, PGv, 0>(a, st);     \
     if (epi == 1) return launch_bwd_stream<BPv, CIv, COv, NWv, PGv, 1>(a, st);     \
     if (epi == 2) return launch_bwd_stream<BPv, CIv, COv, NWv, PGv, 2>(a, st);     \
+  }
+  if (a.pcode != nullptr) {    // fused max-pool backward: the full-resolution encoder conv2 (32 -> 32)
+    // (the 64 -> 64 instantiation spilled 104 B/lane at two waves per SIMD: kept on pool_bwd_code)
+    if (a.dpool == nullptr || (a.H & 1) || (a.ldp & 7) || epi != 0 || a.hslab != nullptr) return (int)hipErrorInvalidValue;
+    if (ci == 32 && co == 32) return launch_bwd_stream<64, 32, 32, 4, 2, 0, false, true>(a, st);
+    return (int)hipErrorInvalidValue;
   }
   if (a.hslab != nullptr) {                        // fused head backward: last decoder conv 32 -> 32
     if (ci == 32 && co == 32 && epi == 0 && a.tgt && a.hw && a.hb && a.dS)

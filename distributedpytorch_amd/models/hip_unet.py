@@ -306,16 +306,17 @@ class HipBlocks:
             ok = self._fusable[key] = K.bwd_fused_eligible(c.Cin, c.Cout, W)
         return ok
 
-    def conv_bwd(self, c: _Conv, g: torch.Tensor, x: torch.Tensor, mask: bool, split: int = 0, head=None):
+    def conv_bwd(self, c: _Conv, g, x: torch.Tensor, mask: bool, split: int = 0, head=None, pool=None):
         """Fused backward of ``c``: returns dx (ReLU-masked by ``x`` when ``mask``; with ``split`` the
         two dense halves of a concat gradient) and accumulates the weight and bias gradients.
-        ``head``: ``g`` is the conv output and the segmentation-head backward is folded in."""
+        ``head``: ``g`` is the conv output and the segmentation-head backward is folded in; ``pool``:
+        ``g`` is the skip gradient and the max-pool backward is folded in."""
         gw, gb = _grad(c.mod.weight).view(-1), _grad(c.mod.bias)
         if split:
-            N, H, W = g.shape[:3]
-            hi = torch.empty(N, H, W, c.Cin - split, dtype=torch.bfloat16, device=g.device)
+            N, H, W = x.shape[:3]
+            hi = torch.empty(N, H, W, c.Cin - split, dtype=torch.bfloat16, device=x.device)
             return K.conv_bwd_fused(g, x, self.wd(c), c.Kd, gw, gb, mask=False, dx2=hi, split=split)
-        return K.conv_bwd_fused(g, x, self.wd(c), c.Kd, gw, gb, mask=mask, head=head)
+        return K.conv_bwd_fused(g, x, self.wd(c), c.Kd, gw, gb, mask=mask, head=head, pool=pool)
 
     def head_bwd_foldable(self, W: int) -> bool:
         """The head backward can be folded into the last decoder conv's fused backward."""
@@ -519,18 +520,23 @@ class _EncFn(torch.autograd.Function):
         else:
             dpooled = _v(dpooled)
         dskip = None if dskip is None else _v(dskip)
-        g2 = torch.empty(a.shape[:3] + (C,), dtype=torch.bfloat16, device=a.device)
-        if ctx.has_code:
-            K.pool_bwd_code(code, dskip, dpooled, g2)
+        W = a.shape[2]
+        if ctx.has_code and K.USE_FUSED_POOL_BWD and B.fusable(c2, c1, W) and K.bwd_pool_foldable(c2.Cin, c2.Cout):
+            # max-pool backward folded into the conv's fused backward: the gradient is formed from
+            # (skip gradient, pooled gradient, window codes) on load and never stored
+            g1, st_g = B.conv_bwd(c2, dskip, a, mask=True, pool=(code, dpooled)), None
         else:
-            K.pool_bwd(skip, dskip, dpooled, g2)
-        g2 = B.bn_bwd(c2, g2, st2)
-        W = g2.shape[2]
-        if B.fusable(c2, c1, W):
-            g1, st_g = B.conv_bwd(c2, g2, a, mask=True), None
-        else:
-            B.conv_wgrad(c2, g2, a)              # side stream: overlaps the dgrad chain
-            g1, st_g = B.conv_dgrad(c2, g2, mask=a, below=c1)
+            g2 = torch.empty(a.shape[:3] + (C,), dtype=torch.bfloat16, device=a.device)
+            if ctx.has_code:
+                K.pool_bwd_code(code, dskip, dpooled, g2)
+            else:
+                K.pool_bwd(skip, dskip, dpooled, g2)
+            g2 = B.bn_bwd(c2, g2, st2)
+            if B.fusable(c2, c1, W):
+                g1, st_g = B.conv_bwd(c2, g2, a, mask=True), None
+            else:
+                B.conv_wgrad(c2, g2, a)              # side stream: overlaps the dgrad chain
+                g1, st_g = B.conv_dgrad(c2, g2, mask=a, below=c1)
         B.ready([c2.mod, c2.bn])
         g1 = B.bn_bwd(c1, g1, st1, stats=st_g)
         if ctx.x_needs_grad and B.fusable(c1, None, W):

@@ -45,7 +45,8 @@ class BwdArgs(ctypes.Structure):
                 ("slab", c_void_p), ("bslab", c_void_p)] + \
                [(n, c_int) for n in ("ldg", "ldx", "ldy", "ldy2", "split", "Kd", "N", "H", "W", "rh", "ipb")] + \
                [("gbytes", ctypes.c_uint), ("xbytes", ctypes.c_uint)] + \
-               [("tgt", c_void_p), ("hw", c_void_p), ("hb", c_void_p), ("dS", c_void_p), ("hslab", c_void_p)]
+               [("tgt", c_void_p), ("hw", c_void_p), ("hb", c_void_p), ("dS", c_void_p), ("hslab", c_void_p)] + \
+               [("pcode", c_void_p), ("dpool", c_void_p), ("ldp", c_int)]
 
 
 class PackDesc(ctypes.Structure):
@@ -106,6 +107,8 @@ USE_FUSED_BWD = os.environ.get("DPA_NO_FUSED_BWD", "0") != "1"
 # the segmentation head's backward folded into the last decoder conv's fused backward (the head
 # gradient is formed from y on load, never stored); DPA_NO_FUSED_HEAD_BWD=1 -> separate head_bwd
 USE_FUSED_HEAD_BWD = USE_FUSED_BWD and os.environ.get("DPA_NO_FUSED_HEAD_BWD", "0") != "1"
+# the max-pool backward folded into the full-resolution encoder conv2's fused backward; DPA_NO_FUSED_POOL_BWD=1 disables
+USE_FUSED_POOL_BWD = USE_FUSED_BWD and os.environ.get("DPA_NO_FUSED_POOL_BWD", "0") != "1"
 
 
 def _extent_bytes(N, H, W, C, ld):
@@ -376,9 +379,14 @@ def bwd_fused_eligible(ci: int, co: int, W: int) -> bool:
     return pg > 0 and W % bp.value == 0
 
 
-def conv_bwd_fused(g: torch.Tensor, x: torch.Tensor, wd: torch.Tensor, Kd: int, gw: torch.Tensor,
+def bwd_pool_foldable(ci: int, co: int) -> bool:
+    return bool(_lib.lib().dpa_bwd_stream_pool_ok(c_int(ci), c_int(co)))
+
+
+def conv_bwd_fused(g: Optional[torch.Tensor], x: torch.Tensor, wd: torch.Tensor, Kd: int, gw: torch.Tensor,
                    gb: Optional[torch.Tensor], *, mask: bool, dx: Optional[torch.Tensor] = None,
-                   dx2: Optional[torch.Tensor] = None, split: int = 0, target_blocks: int = 1024, head=None):
+                   dx2: Optional[torch.Tensor] = None, split: int = 0, target_blocks: int = 1024, head=None,
+                   pool=None):
     """Backward of ``y = conv3x3(x) (+bias)`` in one pass (csrc/bwd_stream.hip): returns
     ``dx = conv3x3^T(g)`` (times ``x > 0`` when ``mask``; with ``dx2``/``split`` the channels
     ``>= split`` go to ``dx2``) and ACCUMULATES the weight gradient into ``gw`` (PyTorch OIHW
@@ -389,10 +397,18 @@ def conv_bwd_fused(g: torch.Tensor, x: torch.Tensor, wd: torch.Tensor, Kd: int, 
     segmap bias grad): ``g`` is then the conv's OUTPUT y (the last decoder conv, whose epilogue
     computed the fused head + loss partials in the forward) and the head backward (``head_bwd``) is
     folded into the loader: the gradient is formed from y on the fly and never stored; the segmap
-    gradients accumulate into the last two tensors."""
-    N, H, W, CO, ldg = _nhwc(g, "bwd.g")
+    gradients accumulate into the last two tensors.
+
+    ``pool`` = (window codes uint8 [N, H/2, W/2, Cout], pooled gradient [N, H/2, W/2, Cout]): the conv
+    is an encoder conv2 whose output was max-pooled in its forward epilogue; ``g`` is then the skip
+    gradient (or None) and the max-pool backward (``pool_bwd_code``) is folded into the loader."""
     Nx, Hx, Wx, CI, ldx = _nhwc(x, "bwd.x")
-    assert (Nx, Hx, Wx) == (N, H, W), (tuple(g.shape), tuple(x.shape))
+    if g is None:                       # pool mode without a skip gradient
+        assert pool is not None
+        N, H, W, CO, ldg = Nx, Hx, Wx, pool[0].shape[3], 0
+    else:
+        N, H, W, CO, ldg = _nhwc(g, "bwd.g")
+    assert (Nx, Hx, Wx) == (N, H, W), ((N, H, W), tuple(x.shape))
     assert wd.dtype == torch.bfloat16 and wd.numel() >= CI * Kd and Kd >= 9 * CO and Kd % 32 == 0
     assert gw.dtype == torch.float32 and gw.is_contiguous() and gw.numel() == CO * CI * 9
     assert gb is None or (gb.dtype == torch.float32 and gb.numel() == CO)
@@ -403,14 +419,14 @@ def conv_bwd_fused(g: torch.Tensor, x: torch.Tensor, wd: torch.Tensor, Kd: int, 
     if dx2 is not None:
         assert 0 < split < CI and split % 16 == 0 and not mask
         if dx is None:
-            dx = torch.empty(N, H, W, split, dtype=torch.bfloat16, device=g.device)
+            dx = torch.empty(N, H, W, split, dtype=torch.bfloat16, device=x.device)
         _, _, _, C1, ldy = _nhwc(dx, "bwd.dx")
         _, _, _, C2, ldy2 = _nhwc(dx2, "bwd.dx2")
         assert C1 >= split and C2 >= CI - split and tuple(dx2.shape[:3]) == (N, H, W)
         epi = 1
     else:
         if dx is None:
-            dx = torch.empty(N, H, W, CI, dtype=torch.bfloat16, device=g.device)
+            dx = torch.empty(N, H, W, CI, dtype=torch.bfloat16, device=x.device)
         _, _, _, C1, ldy = _nhwc(dx, "bwd.dx")
         assert C1 >= CI
         ldy2, epi = 0, (0 if mask else 2)
@@ -421,12 +437,19 @@ def conv_bwd_fused(g: torch.Tensor, x: torch.Tensor, wd: torch.Tensor, Kd: int, 
     rh = -(-H // segs)
     nblk = N * strips * (-(-H // rh))
     slab = torch.empty(nblk * pg * 9 * CO * CI + (nblk * pg * CO if gb is not None else 0), dtype=torch.float32,
-                       device=g.device)
+                       device=x.device)
     bslab = slab[nblk * pg * 9 * CO * CI:] if gb is not None else None
-    a = BwdArgs(g.data_ptr(), x.data_ptr(), wd.data_ptr(), dx.data_ptr(), None if dx2 is None else dx2.data_ptr(),
+    a = BwdArgs(None if g is None else g.data_ptr(), x.data_ptr(), wd.data_ptr(), dx.data_ptr(), None if dx2 is None else dx2.data_ptr(),
                 slab.data_ptr(), None if bslab is None else bslab.data_ptr(), ldg, ldx, ldy, ldy2, split, Kd,
-                N, H, W, rh, 1, _extent_bytes(1, H, W, CO, ldg), _extent_bytes(1, H, W, CI, ldx))
-    st = _stream(g)
+                N, H, W, rh, 1, _extent_bytes(1, H, W, CO, ldg) if g is not None else 0, _extent_bytes(1, H, W, CI, ldx))
+    st = _stream(x)
+    if pool is not None:
+        code, dpool = pool
+        assert L.dpa_bwd_stream_pool_ok(c_int(CI), c_int(CO)) and epi == 0 and H % 2 == 0 and head is None
+        assert code.dtype == torch.uint8 and code.is_contiguous() and tuple(code.shape) == (N, H // 2, W // 2, CO)
+        Np, Hp, Wp, Cp, ldp = _nhwc(dpool, "bwd.dpool")
+        assert (Np, Hp, Wp) == (N, H // 2, W // 2) and Cp >= CO
+        a.pcode, a.dpool, a.ldp = code.data_ptr(), dpool.data_ptr(), ldp
     hslab = None
     if head is not None:
         tgt, hw, hb, dS, hgw, hgb = head
@@ -435,7 +458,7 @@ def conv_bwd_fused(g: torch.Tensor, x: torch.Tensor, wd: torch.Tensor, Kd: int, 
         assert hw.dtype == torch.float32 and hw.numel() == CO and hb.numel() == 1
         assert hgw.is_contiguous() and hgw.numel() == CO and hgb.numel() == 1
         dS = dS.float().contiguous()
-        hslab = torch.empty(nblk * (CO + 1) + CO + 1, dtype=torch.float32, device=g.device)
+        hslab = torch.empty(nblk * (CO + 1) + CO + 1, dtype=torch.float32, device=x.device)
         hw = hw.reshape(-1).contiguous()
         a.tgt, a.hw, a.hb, a.dS, a.hslab = tgt.data_ptr(), hw.data_ptr(), hb.data_ptr(), dS.data_ptr(), hslab.data_ptr()
     _check(L.dpa_bwd_stream(ctypes.byref(a), c_int(CI), c_int(CO), c_int(epi), st), "bwd_stream")

@@ -103,3 +103,33 @@ def test_conv_bwd_fused_head_mode_matches_separate_head_bwd(hip_lib, N, H, W):
     assert _rel(dx.float().cpu(), dx_r.float().cpu()) < 1e-2
     assert _rel(gw.cpu(), gw_r.cpu()) < 1e-2 and _rel(gb.cpu(), gb_r.cpu()) < 1e-2
     assert _rel(hgw.cpu(), hgw_r.cpu()) < 1e-4 and _rel(hgb.cpu(), hgb_r.cpu()) < 1e-4
+
+
+@pytest.mark.parametrize("N,H,W,with_skip", [(2, 6, 64, True), (1, 34, 128, True), (2, 4, 64, False)])
+def test_conv_bwd_fused_pool_mode_matches_pool_bwd(hip_lib, N, H, W, with_skip):
+    """Pool mode: the max-pool backward (window codes from the forward epilogue) folded into the
+    encoder conv2's fused backward equals pool_bwd_code followed by the plain fused backward."""
+    from distributedpytorch_amd.ops import kernels as K
+    torch.manual_seed(10)
+    C = 32
+    a = _nhwc(_bf(F.relu(torch.randn(N, C, H, W))))              # conv input (ReLU output)
+    w = _bf(torch.randn(C, C, 3, 3) * 0.05)
+    packed_f, _, kf = _pack_one(0, w)
+    packed, ng, kd = _pack_one(1, w)
+    # forward with the fused pool: the skip (conv output), pooled output and window codes
+    y = torch.empty(N, H, W, C, dtype=torch.bfloat16, device="cuda")
+    pooled = torch.empty(N, H // 2, W // 2, C, dtype=torch.bfloat16, device="cuda")
+    code = torch.empty(N, H // 2, W // 2, C, dtype=torch.uint8, device="cuda")
+    K.igemm(a, packed_f, y, Ngemm=C, Kpad=kf, KH=3, KW=3, stride=1, pad=1, Cs=C, out_grid=(N, H, W),
+            bias=torch.randn(C).cuda() * 0.1, relu=True, pool=pooled, pcode=code)
+    dskip = _nhwc(_bf(torch.randn(N, C, H, W))) if with_skip else None
+    dpool = _nhwc(_bf(torch.randn(N, C, H // 2, W // 2)))
+    g2 = torch.empty(N, H, W, C, dtype=torch.bfloat16, device="cuda")
+    K.pool_bwd_code(code, dskip, dpool, g2)
+    gw_r, gb_r = torch.zeros(C * C * 9, device="cuda"), torch.zeros(C, device="cuda")
+    dx_r = K.conv_bwd_fused(g2, a, packed, kd, gw_r, gb_r, mask=True)
+    gw, gb = torch.zeros(C * C * 9, device="cuda"), torch.zeros(C, device="cuda")
+    dx = K.conv_bwd_fused(dskip, a, packed, kd, gw, gb, mask=True, pool=(code, dpool))
+    torch.cuda.synchronize()
+    assert torch.equal(dx, dx_r)                 # identical gradient bits -> identical MFMA inputs
+    assert torch.equal(gw, gw_r) and torch.equal(gb, gb_r)
