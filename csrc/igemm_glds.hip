@@ -217,7 +217,17 @@ DPA_API int dpa_igemm_glds(const IgemmArgs* args, int cfg, hipStream_t st) {
   const IgemmArgs& a = *args;
   if ((a.Cs & 63) || (a.Kpad & 63) || (a.ldx & 7) || (a.ldy & 3) || a.KH * a.KW > 32) return (int)hipErrorInvalidValue;
   if (a.mode == 1 && (a.Cout & 3)) return (int)hipErrorInvalidValue;
-  if (cfg == 0) cfg = (a.Ngemm % 256 == 0) ? 3 : 2;
+  if (cfg == 0) {
+    // largest tile that still gives >= 512 workgroups (2 per CU; one 131-147 KB workgroup fits a CU):
+    // a microbatched pipeline stage or a small batch has few output pixels at the deep levels
+    // (XL bottleneck, 2 images: 2048 pixels x 2048 channels = 64 tiles of 256x256 for 256 CUs)
+    const long M = (long)a.N * a.Ho * a.Wo;
+    auto grid_of = [&](long bc, long bp) { return ((M + bp - 1) / bp) * (a.Ngemm / bc); };
+    if (a.Ngemm % 256 == 0 && grid_of(256, 256) >= 512) cfg = 3;
+    else if (a.Ngemm % 128 == 0 && grid_of(128, 256) >= 512) cfg = 2;
+    else if (a.Ngemm % 256 == 0 && grid_of(256, 128) >= 512) cfg = 1;
+    else cfg = 4;
+  }
   switch (cfg) {
     case 1: if (a.Ngemm % 256) break; return launch_glds<256, 128, 64, 64, 3>(a, st);
     case 2: if (a.Ngemm % 128) break; return launch_glds<128, 256, 64, 64, 3>(a, st);

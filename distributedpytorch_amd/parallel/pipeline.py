@@ -419,6 +419,22 @@ class GPipeLocal:
         self.stage_blocks = [make_blocks(model, backend, dtype, device=self.devices[s]) for s in range(self.S)]
         for s, b in enumerate(self.stage_blocks):
             b.device = self.devices[s]
+        # skips between stages: engines on the SAME device share one concat-buffer registry (the decoder
+        # stage finds the encoder's concat buffer: zero-copy, as in a single-stage run); a skip that
+        # changes device is written dense by its producer (one peer copy into the consumer's buffer)
+        _, send = stage_io(self.cuts, self.depth)
+        first = {}
+        for s, b in enumerate(self.stage_blocks):
+            if hasattr(b, "_cats"):
+                d = self.devices[s]
+                if d in first:
+                    b._cats = first[d]._cats
+                else:
+                    first[d] = b
+        for s, b in enumerate(self.stage_blocks):
+            if hasattr(b, "dense_skips"):
+                b.dense_skips = {int(n[len("skip"):]) for n, dst in send[s]
+                                 if n.startswith("skip") and self.devices[dst] != self.devices[s]}
 
     def _run(self, s, env, target, want):
         dev = self.devices[s]
