@@ -66,11 +66,18 @@ def conv3x3(x: torch.Tensor, weight: torch.Tensor, bias: Optional[torch.Tensor],
     return y.permute(0, 3, 1, 2)
 
 
+def _fake_out(x, shape):
+    """Fake output with the REAL op's strides: on the GPU the kernels return a channels_last bf16
+    view (NHWC memory), on the CPU a contiguous tensor of the input dtype."""
+    if x.is_cuda:
+        return x.new_empty(shape, dtype=torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    return x.new_empty(shape, dtype=x.dtype)
+
+
 @conv3x3.register_fake
 def _(x, weight, bias, relu):
     N, _, H, W = x.shape
-    dtype = torch.bfloat16 if x.is_cuda else x.dtype
-    return x.new_empty((N, weight.shape[0], H, W), dtype=dtype)
+    return _fake_out(x, (N, weight.shape[0], H, W))
 
 
 @torch.library.custom_op("dpa::max_pool2x2", mutates_args=())
@@ -91,7 +98,7 @@ def max_pool2x2(x: torch.Tensor) -> torch.Tensor:
 @max_pool2x2.register_fake
 def _(x):
     N, C, H, W = x.shape
-    return x.new_empty((N, C, H // 2, W // 2), dtype=torch.bfloat16 if x.is_cuda else x.dtype)
+    return _fake_out(x, (N, C, H // 2, W // 2))
 
 
 @torch.library.custom_op("dpa::bce_dice_loss", mutates_args=())
