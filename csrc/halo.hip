@@ -504,20 +504,24 @@ __global__ __launch_bounds__(256 * WCS) void igemm_stream_kernel(IgemmArgs a) {
     lsto[j] = c < RCH ? (ks * HR + px) * 64 + (swz_nk<32>(px, cc) << 4) : -1;
   }
   const unsigned rowbytes_x = (unsigned)(a.Ws * a.ldx * 2);
-  u32x4_t reg[LR];
-  auto rload = [&](int ih) {
+  // two register sets: a row's loads are issued two rows before it is stored into the ring
+  struct RowRegs {
+    u32x4_t v[LR];
+  };
+  RowRegs setA, setB;
+  auto rload = [&](int ih, RowRegs& R) {
     const bool rok = ih >= 0 && ih < a.Hs;                     // wave-uniform
     const unsigned rbase = (unsigned)(n * a.Hs + ih) * rowbytes_x;
 #pragma unroll
     for (int j = 0; j < LR; ++j) {
       const unsigned off = (rok && lok[j]) ? rbase + loff[j] : 0x80000000u;
-      reg[j] = __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0);
+      R.v[j] = __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0);
     }
   };
-  auto rstore = [&](int slot) {
+  auto rstore = [&](int slot, const RowRegs& R) {
 #pragma unroll
     for (int j = 0; j < LR; ++j)
-      if (lsto[j] >= 0) *reinterpret_cast<u32x4_t*>(Ring + slot * SLOT + lsto[j]) = reg[j];
+      if (lsto[j] >= 0) *reinterpret_cast<u32x4_t*>(Ring + slot * SLOT + lsto[j]) = R.v[j];
   };
   // ---- per-lane LDS fragment offsets and epilogue constants
   const int chunk = lane >> 4;
@@ -579,18 +583,19 @@ __global__ __launch_bounds__(256 * WCS) void igemm_stream_kernel(IgemmArgs a) {
       for (int e = 0; e < 4; ++e) bsum[ic][e] = bsq[ic][e] = 0.f;
   }
 
-  // prologue: input rows h0-1, h0, h0+1 -> slots 0, 1, 2
-#pragma unroll 1
-  for (int j = 0; j < 3; ++j) {
-    rload(h0 - 1 + j);
-    rstore(j);
-  }
-  __syncthreads();
-
+  // prologue: input rows h0-1, h0, h0+1 -> slots 0, 1, 2; row h0+2 in flight
   const int nrows = min(RH, a.Ho - h0);
 #pragma unroll 1
-  for (int r = 0; r < nrows; ++r) {
-    if (r + 1 < nrows) rload(h0 + r + 2);                  // prefetch into registers
+  for (int j = 0; j < 3; ++j) {
+    rload(h0 - 1 + j, setA);
+    rstore(j, setA);
+  }
+  if (nrows > 1) rload(h0 + 2, setA);
+  __syncthreads();
+
+  // row r: `cur` holds row h0+r+2 (issued during row r-1); row h0+r+3 is issued into `nxt`
+  auto row = [&](int r, RowRegs& cur, RowRegs& nxt) {
+    if (r + 2 < nrows) rload(h0 + r + 3, nxt);
     const int orow = n * a.Ho + h0 + r;
     const unsigned ybase = (unsigned)orow * (unsigned)(a.Wo * a.ldy * 2);
     const unsigned mbase = (unsigned)orow * (unsigned)(a.Wo * a.ldm * 2);
@@ -729,8 +734,13 @@ __global__ __launch_bounds__(256 * WCS) void igemm_stream_kernel(IgemmArgs a) {
       }
     }
     __builtin_amdgcn_sched_barrier(0);
-    if (r + 1 < nrows) rstore((r + 3) & 3);
+    if (r + 1 < nrows) rstore((r + 3) & 3, cur);
     __syncthreads();
+  };
+#pragma unroll 1
+  for (int r = 0; r < nrows; r += 2) {
+    row(r, setA, setB);
+    if (r + 1 < nrows) row(r + 1, setB, setA);
   }
   if constexpr (do_bn) {
     // lanes l and l^1..l^15 hold the same channels (different pixels): butterfly over the 16, then
