@@ -44,9 +44,11 @@ def test_hip_ops_match_torch(hip_lib, N, Cin, Cout, H, W):
     assert torch.equal(p.float().cpu(), F.max_pool2d(y.float().cpu(), 2, 2))
     # the fake (tracing) kernels report the real output layout: channels_last bf16 on the GPU
     from torch._subclasses.fake_tensor import FakeTensorMode
-    with FakeTensorMode() as mode:
-        fx = mode.from_tensor(x.cuda())
-        fy = torch.ops.dpa.conv3x3(fx, mode.from_tensor(w.cuda()), mode.from_tensor(b.cuda()), True)
+    xc, wc, bc = x.cuda(), w.cuda(), b.cuda()
+    mode = FakeTensorMode()
+    fx, fw, fb = mode.from_tensor(xc), mode.from_tensor(wc), mode.from_tensor(bc)
+    with mode:
+        fy = torch.ops.dpa.conv3x3(fx, fw, fb, True)
         fp = torch.ops.dpa.max_pool2x2(fy)
     assert fy.stride() == y.stride() and fy.dtype == y.dtype
     assert fp.stride() == p.stride() and fp.dtype == p.dtype
