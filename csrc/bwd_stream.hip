@@ -46,6 +46,13 @@ struct BwdArgs {
   // dskip (or null) and the gradient is formed on load as in pool_bwd_code_kernel,
   //   g[p][c] = (dskip[p][c] + (argmax(window)[c] == q(p) ? dpool[window][c] : 0)) * mask_q(p)[c]
   const unsigned char* pcode; const bf16_t* dpool; int ldp;
+  // W1 mode (POOL, 32 -> 32, the first encoder level): the input gradient of this conv is the output
+  // gradient of the level's FIRST conv (input x1: the 8-channel padded image [N][H][W][8]), whose only
+  // remaining use is that conv's weight + bias gradient.  It is not stored: each dx row goes (ReLU-
+  // masked, bf16) into an LDS buffer and the next row step accumulates dW1[tap][co][ci] +=
+  // sum_px dx[h][px][co] * x1[h+kh-1][px+kw-1][ci] from it and an x1 row ring; partials go to
+  // slab1 [nblocks][9][32][8] / bslab1 [nblocks][32].
+  const bf16_t* x1; float* slab1; float* bslab1; unsigned x1bytes;
 };
 
 // 8 consecutive k (pixel rows roff+8g .. +7) of 16 channels starting at col0, from an nk image
@@ -74,7 +81,7 @@ __device__ __forceinline__ bf16x8_t tr_pair(const char* base, int off0, int off1
   return __builtin_bit_cast(bf16x8_t, v);
 }
 
-template <int BP, int CI, int CO, int NW, int PG, int EPI, bool HEAD, bool POOL>
+template <int BP, int CI, int CO, int NW, int PG, int EPI, bool HEAD, bool POOL, bool W1>
 __global__ __launch_bounds__(64 * NW, 2) void bwd_stream_kernel(BwdArgs a) {
   constexpr int NT = 64 * NW;
   constexpr int HR = BP + 2;                   // ring row: BP pixels + 1 halo pixel each side
@@ -93,13 +100,20 @@ __global__ __launch_bounds__(64 * NW, 2) void bwd_stream_kernel(BwdArgs a) {
                 "tile");
   static_assert(!HEAD || (CO == 32 && EPI == 0), "head mode: 32-channel last decoder conv");
   static_assert(!(HEAD && POOL), "one gradient source");
+  static_assert(!W1 || (POOL && CI == 32 && CO == 32 && EPI == 0 && BP % 32 == 0), "W1 mode");
+  // W1: x1 row ring (5 slots: the delayed dW1 step still reads row h-2 while row h+2 is stored),
+  // dx row double buffer [BP][32] (nk, swz_nk<32>), per-wave tiles of the 32 x (9 taps x 8) dW1
+  constexpr int X1SLOT = HR * 16, G1SLOT = BP * 64;
+  constexpr int W1BYTES = W1 ? 5 * X1SLOT + 2 * G1SLOT : 0;
   constexpr int GCH = KSO * HR * 4, XCH = HR * (CI / 8);         // 16-B chunks per ring row
   constexpr int LG = (GCH + NT - 1) / NT, LX = (XCH + NT - 1) / NT;
   constexpr int BCH = BP * 4 * KSO, LBI = (BCH + NT - 1) / NT;   // bias: chunks of the g row's BP pixels
-  __shared__ __attribute__((aligned(16))) char lds[WBYTES + 4 * GSLOT + 4 * XSLOT];
+  __shared__ __attribute__((aligned(16))) char lds[WBYTES + 4 * GSLOT + 4 * XSLOT + W1BYTES];
   char* const Wimg = lds;
   char* const Gring = lds + WBYTES;
   char* const Xring = Gring + 4 * GSLOT;
+  char* const X1ring = Xring + 4 * XSLOT;
+  char* const G1buf = X1ring + 5 * X1SLOT;
 
   const int stripsW = a.W / BP, segsH = (a.H + a.rh - 1) / a.rh;
   const int split_id = blockIdx.x;
@@ -113,7 +127,7 @@ __global__ __launch_bounds__(64 * NW, 2) void bwd_stream_kernel(BwdArgs a) {
   const int wp = wid % WPX, wc = wid / WPX;                      // dx role
   const int nt = wid % NTI, msp = (wid / NTI) % MSPL, pg = wid / (NTI * MSPL);   // dW role
   // buffer resources are rebuilt per image (32-bit offsets stay inside one image at any batch size)
-  __amdgpu_buffer_rsrc_t gr, xr, yr, y2r, tr, pr, cr;
+  __amdgpu_buffer_rsrc_t gr, xr, yr, y2r, tr, pr, cr, x1r;
   const bool has_g = !POOL || a.g != nullptr;
   auto bind = [&](int img) {
     const long pix = (long)img * a.H * a.W;
@@ -123,6 +137,7 @@ __global__ __launch_bounds__(64 * NW, 2) void bwd_stream_kernel(BwdArgs a) {
       cr = __builtin_amdgcn_make_buffer_rsrc((void*)(a.pcode + win * CO), 0, 0x7fffffff, 0x00020000);
     }
     if constexpr (HEAD) tr = __builtin_amdgcn_make_buffer_rsrc((void*)(a.tgt + pix), 0, a.H * a.W * 4, 0x00020000);
+    if constexpr (W1) x1r = __builtin_amdgcn_make_buffer_rsrc((void*)(a.x1 + pix * 8), 0, (int)a.x1bytes, 0x00020000);
     gr = __builtin_amdgcn_make_buffer_rsrc((void*)(has_g ? a.g + pix * a.ldg : a.x), 0, has_g ? (int)a.gbytes : 0, 0x00020000);
     xr = __builtin_amdgcn_make_buffer_rsrc((void*)(a.x + pix * a.ldx), 0, (int)a.xbytes, 0x00020000);
     yr = __builtin_amdgcn_make_buffer_rsrc((void*)(a.y + pix * a.ldy), 0, 0x7fffffff, 0x00020000);
@@ -159,6 +174,9 @@ __global__ __launch_bounds__(64 * NW, 2) void bwd_stream_kernel(BwdArgs a) {
     xsto[j] = c < XCH ? px * RBX + ((cc ^ swz_kk<RBX>(px)) << 4) : -1;
   }
   const unsigned growb = (unsigned)(a.W * a.ldg * 2), xrowb = (unsigned)(a.W * a.ldx * 2);
+  // W1: one 16-B chunk (8 channels) per ring pixel
+  const bool x1ok = W1 && tid < HR && w0 + tid - 1 >= 0 && w0 + tid - 1 < a.W;
+  const unsigned x1off = (unsigned)((w0 + tid - 1) * 16), x1rowb = (unsigned)(a.W * 16);
   // HEAD: segmap weights of this thread's 8 channels (cc = tid & 3 for every chunk it loads), the
   // target offset of each chunk's pixel, and whether the pixel is this block's own (not halo)
   float hwv[8], hdw[8], hbias = 0.f, hd0 = 0.f, hd1 = 0.f, hd2 = 0.f, hdb = 0.f;
@@ -199,6 +217,7 @@ __global__ __launch_bounds__(64 * NW, 2) void bwd_stream_kernel(BwdArgs a) {
     unsigned t[HEAD ? LG : 1];            // HEAD: target bits of each chunk's pixel
     u32x4_t pd[POOL ? LG : 1];            // POOL: the pooled gradient of each chunk's window
     u32x2_t pc[POOL ? LG : 1];            // POOL: the window codes of the chunk's 8 channels
+    u32x4_t x1[1];                        // W1: the x1 chunk of this thread's pixel
   };
   RowRegs setA, setB;
   int n = ig * a.ipb;
@@ -209,6 +228,7 @@ __global__ __launch_bounds__(64 * NW, 2) void bwd_stream_kernel(BwdArgs a) {
     for (int j = 0; j < LG; ++j) R.g[j] = __builtin_amdgcn_raw_buffer_load_b128(gr, (rok && gok[j]) ? gb + goff[j] : 0x80000000u, 0, 0);
 #pragma unroll
     for (int j = 0; j < LX; ++j) R.x[j] = __builtin_amdgcn_raw_buffer_load_b128(xr, (rok && xok[j]) ? xb + xoff[j] : 0x80000000u, 0, 0);
+    if constexpr (W1) R.x1[0] = __builtin_amdgcn_raw_buffer_load_b128(x1r, (rok && x1ok) ? (unsigned)ih * x1rowb + x1off : 0x80000000u, 0, 0);
     if constexpr (HEAD) {
 #pragma unroll
       for (int j = 0; j < LG; ++j)
@@ -283,6 +303,8 @@ __global__ __launch_bounds__(64 * NW, 2) void bwd_stream_kernel(BwdArgs a) {
 #pragma unroll
     for (int j = 0; j < LX; ++j)
       if (xsto[j] >= 0) *reinterpret_cast<u32x4_t*>(Xring + slot * XSLOT + xsto[j]) = R.x[j];
+    if constexpr (W1)
+      if (tid < HR) *reinterpret_cast<u32x4_t*>(X1ring + ((ih - h0 + 1) % 5) * X1SLOT + tid * 16) = R.x1[0];
   };
   // ---- dx role: LDS fragment offsets, mask offsets, output offsets
   const int chunk = lane >> 4;
@@ -356,6 +378,57 @@ __global__ __launch_bounds__(64 * NW, 2) void bwd_stream_kernel(BwdArgs a) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) bsum[i][e] = 0.f;
   const bool do_bias = a.bslab != nullptr;
+  // ---- W1 role: the 10 tiles u = mt1*5 + t1 (co tile mt1, n-tile t1 = taps 2*t1, 2*t1+1) go round-robin
+  // over the waves, each over all BP/32 pixel k-steps.  Columns 8..15 of n-tile 4 (a tap 9 that does
+  // not exist) are fed ones instead: D[co][8] = sum_px dx[px][co] is conv1's bias gradient.
+  constexpr int NTL1 = (10 + NW - 1) / NW, KS1 = BP / 32;
+  int g1a[NTL1][2], x1a[NTL1][2], x1kh[NTL1];
+  f32x4_t acc1[NTL1];
+  if constexpr (W1) {
+    const int g8 = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+#pragma unroll
+    for (int i = 0; i < NTL1; ++i) {
+      const int u = wid + i * NW, mt1 = u / 5, t1 = u - mt1 * 5;
+      const int col = mt1 * 16 + 4 * p, ch = col >> 3, hb = (col & 7) * 2;
+      const int tap = 2 * t1 + (p >> 1);
+      const bool ok = u < 10 && tap < 9;
+      const int kh = ok ? tap / 3 : 0, kw = ok ? tap % 3 : 0;
+      x1kh[i] = kh;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int rr = 8 * g8 + q + 4 * h;          // + 32 per k-step: same swizzle, +32 rows
+        g1a[i][h] = rr * 64 + (swz_nk<32>(rr, ch) << 4) + hb;
+        x1a[i][h] = (kw + rr) * 16 + (p & 1) * 8;
+      }
+      acc1[i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+  // dW1 += dx[h0+r-1]^T x1[h0+r-2+kh] for the dx row stored into G1buf during row step r-1
+  auto w1_row = [&](int r) {
+    const char* G1 = G1buf + ((r - 1) & 1) * G1SLOT;
+#pragma unroll
+    for (int i = 0; i < NTL1; ++i) {
+      const int u = wid + i * NW;
+      if (u >= 10) continue;                                     // wave-uniform
+      const char* XS = X1ring + ((r - 1 + x1kh[i]) % 5) * X1SLOT;
+      const bool ones = u % 5 == 4 && (lane & 15) >= 8;
+#pragma unroll
+      for (int k = 0; k < KS1; ++k) {
+        const bf16x8_t ga = tr_pair(G1 + k * 32 * 64, g1a[i][0], g1a[i][1]);
+        bf16x8_t xb = tr_pair(XS + k * 32 * 16, x1a[i][0], x1a[i][1]);
+        if (ones) xb = __builtin_bit_cast(bf16x8_t, u32x4_t{0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u});
+        acc1[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ga, xb, acc1[i], 0, 0, 0);
+      }
+    }
+  };
+  int g1o[TP][TC];
+#pragma unroll
+  for (int ip = 0; ip < TP; ++ip)
+#pragma unroll
+    for (int ic = 0; ic < TC; ++ic) {
+      const int px = wp * WP + ip * 16 + (lane & 15), c0 = wc * WCN + ic * 16 + 4 * chunk;
+      g1o[ip][ic] = px * 64 + (swz_nk<32>(px, c0 >> 3) << 4) + ((c0 >> 2) & 1) * 8;
+    }
 
 #pragma unroll 1
   for (int im = 0; im < nimg; ++im, ++n) {
@@ -419,6 +492,8 @@ __global__ __launch_bounds__(64 * NW, 2) void bwd_stream_kernel(BwdArgs a) {
           }
         }
       }
+      if constexpr (W1)
+        if (r > 0) w1_row(r);
       // ---------------- db: sum of the g row's BP pixels (chunk c = (ks*BP + px)*4 + cc; cc = tid & 3)
       if (do_bias) {
 #pragma unroll
@@ -450,7 +525,9 @@ __global__ __launch_bounds__(64 * NW, 2) void bwd_stream_kernel(BwdArgs a) {
             v3 = hi_bf(mk.y) > 0.f ? v3 : 0.f;
           }
           const u32x2_t packed = u32x2_t{pack_bf2(v0, v1), pack_bf2(v2, v3)};
-          if (EPI == 1 && hi[ip][ic])
+          if constexpr (W1)                      // dx row -> LDS only (bf16, as it would be stored)
+            *reinterpret_cast<u32x2_t*>(G1buf + (r & 1) * G1SLOT + g1o[ip][ic]) = packed;
+          else if (EPI == 1 && hi[ip][ic])
             __builtin_amdgcn_raw_buffer_store_b64(packed, y2r, orow * y2rowb + yoff[ip][ic], 0, 0);
           else
             __builtin_amdgcn_raw_buffer_store_b64(packed, yr, orow * yrowb + yoff[ip][ic], 0, 0);
@@ -463,6 +540,10 @@ __global__ __launch_bounds__(64 * NW, 2) void bwd_stream_kernel(BwdArgs a) {
     for (int r = 0; r < nrows; r += 2) {
       row(r, setA, setB);
       if (r + 1 < nrows) row(r + 1, setB, setA);
+    }
+    if constexpr (W1) {                          // the last dx row of this image
+      if (nrows > 0) w1_row(nrows);
+      __syncthreads();
     }
   }
   // ---------------- partial weight gradient of this (block, pixel group): slab row blockIdx*PG + pg
@@ -518,12 +599,30 @@ __global__ __launch_bounds__(64 * NW, 2) void bwd_stream_kernel(BwdArgs a) {
       a.hslab[(long)split_id * 33 + tid] = sacc;
     }
   }
+  if constexpr (W1) {
+    // dW1 partials -> slab1 row split_id: D element (co = mt1*16 + 4*(lane>>4) + e, n = lane&15) of
+    // n-tile t1 is (tap 2*t1 + n/8, ci n%8); n-tile 4, n == 8 is the bias partial
+    const int n1 = lane & 15;
+#pragma unroll
+    for (int i = 0; i < NTL1; ++i) {
+      const int u = wid + i * NW, mt1 = u / 5, t1 = u - mt1 * 5, tap = 2 * t1 + (n1 >> 3);
+      const int co = mt1 * 16 + 4 * (lane >> 4);
+      if (u < 10 && tap < 9) {
+        float* dst = a.slab1 + (((long)split_id * 9 + tap) * 32 + co) * 8 + (n1 & 7);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) dst[e * 8] = acc1[i][e];
+      } else if (u < 10 && n1 == 8) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) a.bslab1[(long)split_id * 32 + co + e] = acc1[i][e];
+      }
+    }
+  }
 }
 
-template <int BP, int CI, int CO, int NW, int PG, int EPI, bool HEAD = false, bool POOL = false>
+template <int BP, int CI, int CO, int NW, int PG, int EPI, bool HEAD = false, bool POOL = false, bool W1 = false>
 static int launch_bwd_stream(const BwdArgs& a, hipStream_t st) {
   const int blocks = ((a.N + a.ipb - 1) / a.ipb) * ((a.H + a.rh - 1) / a.rh) * (a.W / BP);
-  hipLaunchKernelGGL((bwd_stream_kernel<BP, CI, CO, NW, PG, EPI, HEAD, POOL>), dim3(blocks), dim3(64 * NW), 0, st, a);
+  hipLaunchKernelGGL((bwd_stream_kernel<BP, CI, CO, NW, PG, EPI, HEAD, POOL, W1>), dim3(blocks), dim3(64 * NW), 0, st, a);
   return (int)hipGetLastError();
 }
 
@@ -544,6 +643,13 @@ DPA_API int dpa_bwd_stream_geom(int ci, int co, int* bp) {
   return bwd_cfg(ci, co, bp, &nw);
 }
 
+// W1 runs 8 waves (one block per CU, 198 VGPRs): at 4 waves the extra accumulators spill 208 B/lane.
+// Measured at batch 256, 512^2: 6.05 ms vs 4.08 ms (pool-mode kernel) + 1.2 ms (separate conv1
+// weight gradient) -- the 8-wave row step reads ~60% more LDS per pixel row -- so the engine keeps
+// the separate path unless DPA_FUSED_W1=1.
+#ifndef W1_NW
+#define W1_NW 8
+#endif
 // epi: 0 dx masked by x > 0, 1 dx split at `split` into y / y2, 2 dx plain.
 DPA_API int dpa_bwd_stream(const BwdArgs* args, int ci, int co, int epi, hipStream_t st) {
   const BwdArgs& a = *args;
@@ -560,8 +666,12 @@ DPA_API int dpa_bwd_stream(const BwdArgs* args, int ci, int co, int epi, hipStre
   if (a.pcode != nullptr) {    // fused max-pool backward: the full-resolution encoder conv2 (32 -> 32)
     // (the 64 -> 64 instantiation spilled 104 B/lane at two waves per SIMD: kept on pool_bwd_code)
     if (a.dpool == nullptr || (a.H & 1) || (a.ldp & 7) || epi != 0 || a.hslab != nullptr) return (int)hipErrorInvalidValue;
-    if (ci == 32 && co == 32) return launch_bwd_stream<64, 32, 32, 4, 2, 0, false, true>(a, st);
-    return (int)hipErrorInvalidValue;
+    if (ci != 32 || co != 32) return (int)hipErrorInvalidValue;
+    if (a.x1 != nullptr) {     // + the first conv's weight gradient from the unstored input gradient
+      if (a.slab1 == nullptr || a.bslab1 == nullptr) return (int)hipErrorInvalidValue;
+      return launch_bwd_stream<64, 32, 32, W1_NW, 2, 0, false, true, true>(a, st);
+    }
+    return launch_bwd_stream<64, 32, 32, 4, 2, 0, false, true>(a, st);
   }
   if (a.hslab != nullptr) {                        // fused head backward: last decoder conv 32 -> 32
     if (ci == 32 && co == 32 && epi == 0 && a.tgt && a.hw && a.hb && a.dS)

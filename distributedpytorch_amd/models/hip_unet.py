@@ -306,11 +306,18 @@ class HipBlocks:
             ok = self._fusable[key] = K.bwd_fused_eligible(c.Cin, c.Cout, W)
         return ok
 
-    def conv_bwd(self, c: _Conv, g, x: torch.Tensor, mask: bool, split: int = 0, head=None, pool=None):
+    def conv_bwd(self, c: _Conv, g, x: torch.Tensor, mask: bool, split: int = 0, head=None, pool=None, first=None):
         """Fused backward of ``c``: returns dx (ReLU-masked by ``x`` when ``mask``; with ``split`` the
         two dense halves of a concat gradient) and accumulates the weight and bias gradients.
         ``head``: ``g`` is the conv output and the segmentation-head backward is folded in; ``pool``:
-        ``g`` is the skip gradient and the max-pool backward is folded in."""
+        ``g`` is the skip gradient and the max-pool backward is folded in; ``first`` = (conv c1, its
+        input x1): ``x = relu(c1(x1))`` and x1 needs no gradient, so dx is consumed in-kernel by
+        c1's weight/bias gradient and never stored (returns None)."""
+        if first is not None:
+            c1, x1 = first
+            w1 = (x1, _grad(c1.mod.weight).view(-1), _grad(c1.mod.bias))
+            return K.conv_bwd_fused(g, x, self.wd(c), c.Kd, _grad(c.mod.weight).view(-1), _grad(c.mod.bias),
+                                    mask=True, pool=pool, w1=w1)
         gw, gb = _grad(c.mod.weight).view(-1), _grad(c.mod.bias)
         if split:
             N, H, W = x.shape[:3]
@@ -521,7 +528,19 @@ class _EncFn(torch.autograd.Function):
             dpooled = _v(dpooled)
         dskip = None if dskip is None else _v(dskip)
         W = a.shape[2]
-        if ctx.has_code and K.USE_FUSED_POOL_BWD and B.fusable(c2, c1, W) and K.bwd_pool_foldable(c2.Cin, c2.Cout):
+        pool_fold = (ctx.has_code and K.USE_FUSED_POOL_BWD and B.fusable(c2, c1, W)
+                     and K.bwd_pool_foldable(c2.Cin, c2.Cout))
+        if pool_fold and not ctx.x_needs_grad and K.USE_FUSED_W1 and c1.bn is None and c1.Cs == 8 \
+                and c1.Cout == 32 and x.is_contiguous():
+            # first level: conv2's fused backward also forms conv1's weight/bias gradient from its
+            # (never stored) input gradient -- the level's whole backward in one pass
+            B.conv_bwd(c2, dskip, a, mask=True, pool=(code, dpooled), first=(c1, x))
+            B.ready([c2.mod, c2.bn])
+            B.ready([c1.mod, c1.bn])
+            B.join()
+            ctx.st = None
+            return None, None, None, None
+        if pool_fold:
             # max-pool backward folded into the conv's fused backward: the gradient is formed from
             # (skip gradient, pooled gradient, window codes) on load and never stored
             g1, st_g = B.conv_bwd(c2, dskip, a, mask=True, pool=(code, dpooled)), None

@@ -46,7 +46,8 @@ class BwdArgs(ctypes.Structure):
                [(n, c_int) for n in ("ldg", "ldx", "ldy", "ldy2", "split", "Kd", "N", "H", "W", "rh", "ipb")] + \
                [("gbytes", ctypes.c_uint), ("xbytes", ctypes.c_uint)] + \
                [("tgt", c_void_p), ("hw", c_void_p), ("hb", c_void_p), ("dS", c_void_p), ("hslab", c_void_p)] + \
-               [("pcode", c_void_p), ("dpool", c_void_p), ("ldp", c_int)]
+               [("pcode", c_void_p), ("dpool", c_void_p), ("ldp", c_int)] + \
+               [("x1", c_void_p), ("slab1", c_void_p), ("bslab1", c_void_p), ("x1bytes", ctypes.c_uint)]
 
 
 class PackDesc(ctypes.Structure):
@@ -109,6 +110,9 @@ USE_FUSED_BWD = os.environ.get("DPA_NO_FUSED_BWD", "0") != "1"
 USE_FUSED_HEAD_BWD = USE_FUSED_BWD and os.environ.get("DPA_NO_FUSED_HEAD_BWD", "0") != "1"
 # the max-pool backward folded into the full-resolution encoder conv2's fused backward; DPA_NO_FUSED_POOL_BWD=1 disables
 USE_FUSED_POOL_BWD = USE_FUSED_BWD and os.environ.get("DPA_NO_FUSED_POOL_BWD", "0") != "1"
+# the first encoder conv's weight gradient folded into the pool-mode backward of the second: opt-in,
+# slower at batch 256 (6.05 ms vs 5.3 ms for the two kernels it replaces; see csrc/bwd_stream.hip)
+USE_FUSED_W1 = USE_FUSED_POOL_BWD and os.environ.get("DPA_FUSED_W1", "0") == "1"
 
 
 def _extent_bytes(N, H, W, C, ld):
@@ -386,7 +390,7 @@ def bwd_pool_foldable(ci: int, co: int) -> bool:
 def conv_bwd_fused(g: Optional[torch.Tensor], x: torch.Tensor, wd: torch.Tensor, Kd: int, gw: torch.Tensor,
                    gb: Optional[torch.Tensor], *, mask: bool, dx: Optional[torch.Tensor] = None,
                    dx2: Optional[torch.Tensor] = None, split: int = 0, target_blocks: int = 1024, head=None,
-                   pool=None):
+                   pool=None, w1=None):
     """Backward of ``y = conv3x3(x) (+bias)`` in one pass (csrc/bwd_stream.hip): returns
     ``dx = conv3x3^T(g)`` (times ``x > 0`` when ``mask``; with ``dx2``/``split`` the channels
     ``>= split`` go to ``dx2``) and ACCUMULATES the weight gradient into ``gw`` (PyTorch OIHW
@@ -401,7 +405,13 @@ def conv_bwd_fused(g: Optional[torch.Tensor], x: torch.Tensor, wd: torch.Tensor,
 
     ``pool`` = (window codes uint8 [N, H/2, W/2, Cout], pooled gradient [N, H/2, W/2, Cout]): the conv
     is an encoder conv2 whose output was max-pooled in its forward epilogue; ``g`` is then the skip
-    gradient (or None) and the max-pool backward (``pool_bwd_code``) is folded into the loader."""
+    gradient (or None) and the max-pool backward (``pool_bwd_code``) is folded into the loader.
+
+    ``w1`` = (x1 [N, H, W, 8] bf16, weight grad [32*Creal*9], bias grad [32]) with ``pool``: ``x`` is
+    the output of a first conv ``x = relu(conv3x3(x1))`` (32 channels, 8-channel padded input of
+    which ``Creal`` are real) whose input needs no gradient.  dx -- that conv's output gradient -- is
+    then never stored: the kernel accumulates the first conv's weight and bias gradients from it row
+    by row, and the function returns None."""
     Nx, Hx, Wx, CI, ldx = _nhwc(x, "bwd.x")
     if g is None:                       # pool mode without a skip gradient
         assert pool is not None
@@ -424,13 +434,16 @@ def conv_bwd_fused(g: Optional[torch.Tensor], x: torch.Tensor, wd: torch.Tensor,
         _, _, _, C2, ldy2 = _nhwc(dx2, "bwd.dx2")
         assert C1 >= split and C2 >= CI - split and tuple(dx2.shape[:3]) == (N, H, W)
         epi = 1
+    elif w1 is not None:
+        assert pool is not None and mask and dx is None and CI == CO == 32
+        ldy, ldy2, epi = 0, 0, 0
     else:
         if dx is None:
             dx = torch.empty(N, H, W, CI, dtype=torch.bfloat16, device=x.device)
         _, _, _, C1, ldy = _nhwc(dx, "bwd.dx")
         assert C1 >= CI
         ldy2, epi = 0, (0 if mask else 2)
-    assert tuple(dx.shape[:3]) == (N, H, W)
+    assert dx is None or tuple(dx.shape[:3]) == (N, H, W)
     strips = W // bp.value
     # whole image columns per block; split the rows only when the batch gives too few blocks
     segs = max(1, min(H, -(-target_blocks // max(1, N * strips))))
@@ -439,7 +452,8 @@ def conv_bwd_fused(g: Optional[torch.Tensor], x: torch.Tensor, wd: torch.Tensor,
     slab = torch.empty(nblk * pg * 9 * CO * CI + (nblk * pg * CO if gb is not None else 0), dtype=torch.float32,
                        device=x.device)
     bslab = slab[nblk * pg * 9 * CO * CI:] if gb is not None else None
-    a = BwdArgs(None if g is None else g.data_ptr(), x.data_ptr(), wd.data_ptr(), dx.data_ptr(), None if dx2 is None else dx2.data_ptr(),
+    a = BwdArgs(None if g is None else g.data_ptr(), x.data_ptr(), wd.data_ptr(), None if dx is None else dx.data_ptr(),
+                None if dx2 is None else dx2.data_ptr(),
                 slab.data_ptr(), None if bslab is None else bslab.data_ptr(), ldg, ldx, ldy, ldy2, split, Kd,
                 N, H, W, rh, 1, _extent_bytes(1, H, W, CO, ldg) if g is not None else 0, _extent_bytes(1, H, W, CI, ldx))
     st = _stream(x)
@@ -450,6 +464,16 @@ def conv_bwd_fused(g: Optional[torch.Tensor], x: torch.Tensor, wd: torch.Tensor,
         Np, Hp, Wp, Cp, ldp = _nhwc(dpool, "bwd.dpool")
         assert (Np, Hp, Wp) == (N, H // 2, W // 2) and Cp >= CO
         a.pcode, a.dpool, a.ldp = code.data_ptr(), dpool.data_ptr(), ldp
+    slab1 = None
+    if w1 is not None:
+        x1, gw1, gb1 = w1
+        assert x1.dtype == torch.bfloat16 and x1.is_contiguous() and tuple(x1.shape) == (N, H, W, 8)
+        creal = gw1.numel() // (CI * 9)
+        assert gw1.dtype == torch.float32 and gw1.is_contiguous() and gw1.numel() == CI * creal * 9 and 0 < creal <= 8
+        assert gb1.dtype == torch.float32 and gb1.numel() == CI
+        slab1 = torch.empty(nblk * (9 * CI * 8 + CI), dtype=torch.float32, device=x.device)   # one row per block
+        a.x1, a.slab1, a.bslab1 = x1.data_ptr(), slab1.data_ptr(), slab1[nblk * 9 * CI * 8:].data_ptr()
+        a.x1bytes = _extent_bytes(1, H, W, 8, 8)
     hslab = None
     if head is not None:
         tgt, hw, hb, dS, hgw, hgb = head
@@ -467,6 +491,9 @@ def conv_bwd_fused(g: Optional[torch.Tensor], x: torch.Tensor, wd: torch.Tensor,
                                          _p(hgb), st), "head_grad_from_slab")
     _check(L.dpa_wgrad_reduce(_p(slab), _p(bslab), _p(gw), _p(gb), c_int(nblk * pg), c_int(9), c_int(CO), c_int(CI),
                               c_int(CI), c_int(0), st), "wgrad_reduce(bwd_stream)")
+    if slab1 is not None:
+        _check(L.dpa_wgrad_reduce(_p(slab1), _p(slab1[nblk * 9 * CI * 8:]), _p(gw1), _p(gb1), c_int(nblk),
+                                  c_int(9), c_int(CI), c_int(8), c_int(creal), c_int(0), st), "wgrad_reduce(bwd_stream.w1)")
     return (dx, dx2) if dx2 is not None else dx
 
 

@@ -133,3 +133,45 @@ def test_conv_bwd_fused_pool_mode_matches_pool_bwd(hip_lib, N, H, W, with_skip):
     torch.cuda.synchronize()
     assert torch.equal(dx, dx_r)                 # identical gradient bits -> identical MFMA inputs
     assert torch.equal(gw, gw_r) and torch.equal(gb, gb_r)
+
+
+@pytest.mark.parametrize("N,H,W", [(2, 6, 64), (1, 34, 128), (2, 4, 192)])
+def test_conv_bwd_fused_first_level_matches_separate(hip_lib, N, H, W):
+    """W1 mode (first encoder level): the pool-mode fused backward of conv2 also accumulates conv1's
+    weight and bias gradients from its never-stored input gradient; equals the pool-mode backward
+    returning that gradient followed by conv1's separate weight-gradient kernel."""
+    from distributedpytorch_amd.ops import kernels as K
+    torch.manual_seed(11)
+    C, CR = 32, 3
+    x1 = torch.zeros(N, H, W, 8, dtype=torch.bfloat16, device="cuda")
+    x1[..., :CR] = torch.rand(N, H, W, CR, device="cuda").to(torch.bfloat16)   # padded 3-channel image
+    a = _nhwc(_bf(F.relu(torch.randn(N, C, H, W))))              # conv1 output = conv2 input
+    w = _bf(torch.randn(C, C, 3, 3) * 0.05)
+    packed_f, _, kf = _pack_one(0, w)
+    packed, ng, kd = _pack_one(1, w)
+    y = torch.empty(N, H, W, C, dtype=torch.bfloat16, device="cuda")
+    pooled = torch.empty(N, H // 2, W // 2, C, dtype=torch.bfloat16, device="cuda")
+    code = torch.empty(N, H // 2, W // 2, C, dtype=torch.uint8, device="cuda")
+    K.igemm(a, packed_f, y, Ngemm=C, Kpad=kf, KH=3, KW=3, stride=1, pad=1, Cs=C, out_grid=(N, H, W),
+            bias=torch.randn(C).cuda() * 0.1, relu=True, pool=pooled, pcode=code)
+    dskip = _nhwc(_bf(torch.randn(N, C, H, W)))
+    dpool = _nhwc(_bf(torch.randn(N, C, H // 2, W // 2)))
+    # reference: pool-mode fused backward returning g1, then conv1's weight gradient
+    gw_r, gb_r = torch.zeros(C * C * 9, device="cuda"), torch.zeros(C, device="cuda")
+    g1 = K.conv_bwd_fused(dskip, a, packed, kd, gw_r, gb_r, mask=True, pool=(code, dpool))
+    gw1_r, gb1_r = torch.zeros(C * CR * 9, device="cuda"), torch.zeros(C, device="cuda")
+    K.wgrad(g1, x1, kind=0, grid=(N, H, W), M=C, Nc=8, s=1, pad=1, KW=3, gw=gw1_r, gb=gb1_r, Nreal=CR)
+    gw, gb = torch.zeros(C * C * 9, device="cuda"), torch.zeros(C, device="cuda")
+    gw1, gb1 = torch.randn(C * CR * 9, device="cuda"), torch.randn(C, device="cuda")   # accumulate semantics
+    gw10, gb10 = gw1.clone(), gb1.clone()
+    out = K.conv_bwd_fused(dskip, a, packed, kd, gw, gb, mask=True, pool=(code, dpool), w1=(x1, gw1, gb1))
+    torch.cuda.synchronize()
+    assert out is None
+    assert _rel(gw.cpu(), gw_r.cpu()) < 1e-5 and _rel(gb.cpu(), gb_r.cpu()) < 1e-5
+    assert _rel((gw1 - gw10).cpu(), gw1_r.cpu()) < 1e-4, _rel((gw1 - gw10).cpu(), gw1_r.cpu())
+    assert _rel((gb1 - gb10).cpu(), gb1_r.cpu()) < 1e-4
+    # and against the fp32 autograd reference of conv1's weight gradient from the same g1
+    x1n = x1[..., :CR].permute(0, 3, 1, 2).float().cpu().requires_grad_(False)
+    w1r = torch.zeros(C, CR, 3, 3, requires_grad=True)
+    F.conv2d(x1n, w1r, padding=1).backward(g1.permute(0, 3, 1, 2).float().cpu())
+    assert _rel((gw1 - gw10).cpu(), w1r.grad.reshape(-1)) < 1e-4
