@@ -325,6 +325,34 @@ class HipBlocks:
             return K.conv_bwd_fused(g, x, self.wd(c), c.Kd, gw, gb, mask=False, dx2=hi, split=split)
         return K.conv_bwd_fused(g, x, self.wd(c), c.Kd, gw, gb, mask=mask, head=head, pool=pool)
 
+    def halves_fusable(self, c: _Conv, C: int, W: int) -> bool:
+        """A conv over a concat of two C-channel halves whose fused backward does not exist at 2C input
+        channels but does at C (the 256^2 decoder conv 128 -> 64): conv(cat) = conv_lo(skip) +
+        conv_hi(up), so its backward is two fused passes, one per half."""
+        if not (K.USE_FUSED_HALVES and c.bn is None and c.Cs == c.Cin == 2 * C):
+            return False
+        key = ("halves", C, c.Cout, W)
+        ok = self._fusable.get(key)
+        if ok is None:
+            ok = self._fusable[key] = K.bwd_fused_eligible(C, c.Cout, W)
+        return ok
+
+    def conv_bwd_halves(self, c: _Conv, g: torch.Tensor, cat: torch.Tensor, C: int):
+        """Backward of a conv over ``cat = [lo | hi]`` (C channels each) as two fused passes: each
+        writes its half's dense input gradient and its half of the weight gradient (the dgrad rows of
+        the packed weights and the input-channel columns of dW belonging to that half); the bias
+        gradient comes with the first.  Replaces one 2C-channel dgrad + a side-stream weight gradient
+        that together did ~1.7x the work at a third of the MFMA rate (profiles/kbench_halo_b256_r02.txt)."""
+        gw, gb = _grad(c.mod.weight).view(c.Cout, c.Cin, 9), _grad(c.mod.bias)
+        wd = self.wd(c)
+        outs = []
+        for h in range(2):
+            part = torch.zeros(c.Cout * C * 9, dtype=torch.float32, device=g.device)
+            outs.append(K.conv_bwd_fused(g, cat[..., h * C:(h + 1) * C], wd[h * C * c.Kd:(h + 1) * C * c.Kd], c.Kd,
+                                         part, gb if h == 0 else None, mask=False))
+            gw[:, h * C:(h + 1) * C].add_(part.view(c.Cout, C, 9))
+        return outs[0], outs[1]
+
     def head_bwd_foldable(self, W: int) -> bool:
         """The head backward can be folded into the last decoder conv's fused backward."""
         c1, c2 = self.dec_convs[-1]
@@ -673,6 +701,8 @@ class _DecFn(torch.autograd.Function):
         g1 = B.bn_bwd(c1, g1, st1, stats=st_g)
         if B.fusable(c1, None, W):
             dskip, gup = B.conv_bwd(c1, g1, cat, mask=False, split=C)
+        elif B.halves_fusable(c1, C, W):
+            dskip, gup = B.conv_bwd_halves(c1, g1, cat, C)
         else:
             B.conv_wgrad(c1, g1, cat)
             dskip, gup = B.conv_dgrad_split(c1, g1, C)

@@ -109,6 +109,8 @@ USE_FUSED_BWD = os.environ.get("DPA_NO_FUSED_BWD", "0") != "1"
 # gradient is formed from y on load, never stored); DPA_NO_FUSED_HEAD_BWD=1 -> separate head_bwd
 USE_FUSED_HEAD_BWD = USE_FUSED_BWD and os.environ.get("DPA_NO_FUSED_HEAD_BWD", "0") != "1"
 # the max-pool backward folded into the full-resolution encoder conv2's fused backward; DPA_NO_FUSED_POOL_BWD=1 disables
+# concat convs whose 2C-input fused backward does not exist: two fused passes, one per half
+USE_FUSED_HALVES = USE_FUSED_BWD and os.environ.get("DPA_NO_FUSED_HALVES", "0") != "1"
 USE_FUSED_POOL_BWD = USE_FUSED_BWD and os.environ.get("DPA_NO_FUSED_POOL_BWD", "0") != "1"
 # the first encoder conv's weight gradient folded into the pool-mode backward of the second: opt-in,
 # slower at batch 256 (6.05 ms vs 5.3 ms for the two kernels it replaces; see csrc/bwd_stream.hip)
