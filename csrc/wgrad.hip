@@ -278,11 +278,145 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
   }
 }
 
-DPA_API int dpa_wgrad_reduce(const float* slab, const float* bslab, float* gw, float* gb, int splits, int T, int M, int Nc,
-                             int Nreal, int mode, hipStream_t st) {
+// Quad version (T*M*Nc and M multiples of 4): a thread sums 4 consecutive slab elements (16-B loads)
+// over the splits k = g, g + G, ...; the G split groups of a quad are combined through LDS in a fixed
+// order.  G is chosen from the shape alone (enough threads to cover the chip, no more groups than
+// splits), so the summation order -- and the result bits -- do not change from run to run.  Compared
+// with wgrad_reduce_kernel: 4x fewer load instructions, no idle split rows when splits < 8, and
+// every thread of a block busy in the grid-stride loop.
+template <int G>
+__global__ __launch_bounds__(256) void wgrad_reduce4_kernel(const float* __restrict__ slab, const float* __restrict__ bslab,
+                                                            float* __restrict__ gw, float* __restrict__ gb, int splits,
+                                                            int T, int M, int Nc, int Nreal, int mode) {
+  constexpr int Q = 256 / G;                   // quads per block
+  __shared__ f32x4_t part[G][Q];
+  const long totq = (long)T * M * Nc / 4, mq = bslab ? M / 4 : 0;
+  const int tq = threadIdx.x % Q, tg = threadIdx.x / Q;
+  const long nblk = (totq + mq + Q - 1) / Q;
+  for (long b = blockIdx.x; b < nblk; b += gridDim.x) {
+    const long q = b * Q + tq;
+    const bool isb = q >= totq;
+    const long qi = isb ? q - totq : q;
+    const bool ok = isb ? qi < mq : true;
+    const float* src = isb ? bslab : slab;
+    const long stride = isb ? M : totq * 4;
+    f32x4_t s = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    if (ok) {
+#pragma unroll 4
+      for (int k = tg; k < splits; k += G) s += *reinterpret_cast<const f32x4_t*>(src + (long)k * stride + qi * 4);
+    }
+    part[tg][tq] = s;
+    __syncthreads();
+    if (tg == 0 && ok) {
+      f32x4_t r = part[0][tq];
+#pragma unroll
+      for (int g = 1; g < G; ++g) r += part[g][tq];
+      if (isb) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) gb[qi * 4 + e] += r[e];
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const long idx = qi * 4 + e;
+          const int n = (int)(idx % Nc);
+          const int m = (int)((idx / Nc) % M);
+          const int t = (int)(idx / ((long)Nc * M));
+          if (n < Nreal) gw[mode == 0 ? ((long)m * Nreal + n) * T + t : ((long)n * M + m) * T + t] += r[e];
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// Tiled version for the Conv2d layout with few splits (mode 0, Nreal == Nc, Nc % 64 == 0, T <= 9).
+// The two kernels above read the slab coalesced but scatter their read-modify-write of gw at a stride
+// of T floats, so every T-slice of a weight-sized slab sweeps all of gw's cache lines again: with one
+// to four splits (the deep layers of a small (micro)batch) that transpose, not the summation, is the
+// cost (a 2048x2048 conv: 0.9 ms).  Here a block owns (m, 64 consecutive n) for all T taps: it sums the
+// splits into LDS (4 split groups, fixed combine order), then adds the [64 n][T] tile to gw as ONE
+// contiguous run of 64*T floats.  Blocks past the weight tiles sum the bias slab, 64 channels each.
+__global__ __launch_bounds__(256) void wgrad_reduce_tile_kernel(const float* __restrict__ slab,
+                                                                const float* __restrict__ bslab, float* __restrict__ gw,
+                                                                float* __restrict__ gb, int splits, int T, int M, int Nc) {
+  __shared__ float part[4][9][64];
+  __shared__ float out[64 * 9];
   const long tot = (long)T * M * Nc;
+  const int ntn = Nc / 64;
+  const long ntile = (long)M * ntn, nbias = bslab ? (M + 63) / 64 : 0;
+  const int n = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  for (long b = blockIdx.x; b < ntile + nbias; b += gridDim.x) {
+    if (b < ntile) {
+      const int m = (int)(b / ntn), n0 = (int)(b - (long)m * ntn) * 64;
+      for (int t = 0; t < T; ++t) {
+        const float* src = slab + ((long)t * M + m) * Nc + n0 + n;
+        float acc = 0.f;
+#pragma unroll 4
+        for (int k = grp; k < splits; k += 4) acc += src[(long)k * tot];
+        part[grp][t][n] = acc;
+      }
+      __syncthreads();
+      for (int o = threadIdx.x; o < 64 * T; o += 256) {
+        const int t = o >> 6, nn = o & 63;
+        out[nn * T + t] = ((part[0][t][nn] + part[1][t][nn]) + part[2][t][nn]) + part[3][t][nn];
+      }
+      __syncthreads();
+      float* dst = gw + ((long)m * Nc + n0) * T;
+      for (int o = threadIdx.x; o < 64 * T; o += 256) dst[o] += out[o];
+      __syncthreads();
+    } else {
+      const int m0 = (int)(b - ntile) * 64;
+      float acc = 0.f;
+      if (m0 + n < M)
+        for (int k = grp; k < splits; k += 4) acc += bslab[(long)k * M + m0 + n];
+      part[grp][0][n] = acc;
+      __syncthreads();
+      if (grp == 0 && m0 + n < M) gb[m0 + n] += ((part[0][0][n] + part[1][0][n]) + part[2][0][n]) + part[3][0][n];
+      __syncthreads();
+    }
+  }
+}
+
+// g: -1 auto, 0 the 32-element kernel, > 0 the quad kernel with g split groups, -2 the tiled kernel
+// (tools/kbench_reduce.py)
+DPA_API int dpa_wgrad_reduce_cfg(const float* slab, const float* bslab, float* gw, float* gb, int splits, int T, int M,
+                                 int Nc, int Nreal, int mode, int g, hipStream_t st) {
+  const long tot = (long)T * M * Nc;
+  const bool tile_ok = mode == 0 && Nreal == Nc && Nc % 64 == 0 && T <= 9;
+  if (g == -1) {
+    // measured on the UNet / UNet-XL slab shapes (profiles/kbench_reduce_r02.txt): tiled for few
+    // splits, quad kernel with 4-8 groups for a moderate count, the 32-element kernel for thousands
+    if (tile_ok && splits <= 16) g = -2;
+    else if (splits >= 1024 || tot < 65536 || (mode == 1 && splits > 32)) g = 0;
+    else if (mode == 1) g = splits <= 8 ? 4 : 8;
+    else g = splits <= 32 ? 4 : 8;
+  }
+  if (g == -2) {
+    if (!tile_ok) return (int)hipErrorInvalidValue;
+    const long nb = (long)M * (Nc / 64) + (bslab ? (M + 63) / 64 : 0);
+    hipLaunchKernelGGL(wgrad_reduce_tile_kernel, dim3((unsigned)(nb < 16384 ? nb : 16384)), dim3(256), 0, st, slab, bslab,
+                       gw, gb, splits, T, M, Nc);
+    return (int)hipGetLastError();
+  }
+  if (g != 0 && tot % 4 == 0 && M % 4 == 0 && ((size_t)slab & 15) == 0 && (!bslab || ((size_t)bslab & 15) == 0)) {
+    // G split groups per quad (chosen above or by the caller)
+    const long quads = tot / 4 + (bslab ? M / 4 : 0);
+    const int G = g;
+    const long nb = (quads + (256 / G) - 1) / (256 / G);
+    const dim3 grid((unsigned)(nb < 8192 ? nb : 8192));
+#define DPA_RED4(Gv) \
+    if (G == Gv) { hipLaunchKernelGGL(wgrad_reduce4_kernel<Gv>, grid, dim3(256), 0, st, slab, bslab, gw, gb, splits, T, M, Nc, Nreal, mode); return (int)hipGetLastError(); }
+    DPA_RED4(1) DPA_RED4(2) DPA_RED4(4) DPA_RED4(8) DPA_RED4(16) DPA_RED4(32) DPA_RED4(64)
+#undef DPA_RED4
+    return (int)hipErrorInvalidValue;
+  }
   const long nb = (tot + 31) / 32 + (bslab ? (M + 31) / 32 : 0);
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)(nb < 8192 ? nb : 8192)), dim3(256), 0, st, slab, bslab, gw, gb,
                      splits, T, M, Nc, Nreal, mode);
   return (int)hipGetLastError();
+}
+
+DPA_API int dpa_wgrad_reduce(const float* slab, const float* bslab, float* gw, float* gb, int splits, int T, int M, int Nc,
+                             int Nreal, int mode, hipStream_t st) {
+  return dpa_wgrad_reduce_cfg(slab, bslab, gw, gb, splits, T, M, Nc, Nreal, mode, -1, st);
 }

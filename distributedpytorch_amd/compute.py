@@ -66,12 +66,12 @@ def resolve_backend(backend: str, device) -> str:
     return backend
 
 
-def make_blocks(model, backend: str = "auto", dtype: str = "bf16", device=None):
+def make_blocks(model, backend: str = "auto", dtype: str = "bf16", device=None, owned=None):
     dev = torch.device(device) if device is not None else next(model.parameters()).device
     backend = resolve_backend(backend, dev)
     if backend == "hip":
         from .models.hip_unet import HipBlocks
-        return HipBlocks(model, dtype=dtype, device=dev)
+        return HipBlocks(model, dtype=dtype, device=dev, owned=owned)
     from .models.blocks import TorchBlocks
     return TorchBlocks(model, dtype=dtype)
 

@@ -86,8 +86,11 @@ class _Up:
 class HipBlocks:
     name = "hip"
 
-    def __init__(self, model: UNet, dtype: str = "bf16", device=None):
+    def __init__(self, model: UNet, dtype: str = "bf16", device=None, owned=None):
+        """``owned``: ids of the parameters this engine computes with (a pipeline stage's share when
+        several stages live on one device); None = every parameter on ``device``."""
         cfg = model.cfg
+        self._owned = owned
         if dtype != "bf16":
             raise NotImplementedError("hip backend computes in bf16 (fp32 accumulate); use --backend torch for fp32")
         self.model = model
@@ -156,7 +159,8 @@ class HipBlocks:
             max_elems = max(max_elems, ngemm * kpad)
             return start
 
-        here = lambda m: m.weight.device == self.device   # noqa: E731
+        here = lambda m: (m.weight.device == self.device   # noqa: E731
+                          and (self._owned is None or id(m.weight) in self._owned))
         for c in [c for cs in self.enc_convs for c in cs] + self.mid_convs + [c for cs in self.dec_convs for c in cs]:
             if not here(c.mod):
                 continue

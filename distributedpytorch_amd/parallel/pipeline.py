@@ -416,7 +416,11 @@ class GPipeLocal:
             names = set(stage_param_names(model, self.cuts[s], self.cuts[s + 1]))
             own = [(n, p) for n, p in model.named_parameters() if n in names]
             self.spaces.append(FlatParameterSpace(own, device=self.devices[s]))
-        self.stage_blocks = [make_blocks(model, backend, dtype, device=self.devices[s]) for s in range(self.S)]
+        # each stage's engine packs only its own layers' weights (stages sharing a device would
+        # otherwise each re-pack the whole model every step)
+        self.stage_blocks = [make_blocks(model, backend, dtype, device=self.devices[s],
+                                         owned={id(p) for p in self.spaces[s].params})
+                             for s in range(self.S)]
         for s, b in enumerate(self.stage_blocks):
             b.device = self.devices[s]
         # skips between stages: engines on the SAME device share one concat-buffer registry (the decoder
