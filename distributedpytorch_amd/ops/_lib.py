@@ -56,7 +56,7 @@ def _declare(L):
                  "dpa_loss_finish", "dpa_loss_grad", "dpa_pool_bwd_code", "dpa_bn_fwd", "dpa_bn_bwd",
                  "dpa_up2_fwd", "dpa_up2_bwd", "dpa_deconv_bwd", "dpa_deconv_fwd", "dpa_slab_sum",
                  "dpa_igemm_stream_blocks", "dpa_slab_fold", "dpa_bwd_stream", "dpa_head_grad_from_slab", "dpa_bwd_stream_pool_ok",
-                 "dpa_wgrad_reduce_cfg"):
+                 "dpa_wgrad_reduce_cfg", "dpa_dconv1_fwd"):
         getattr(L, name).restype = ctypes.c_int
     L.dpa_head_slab_blocks.restype = ctypes.c_int
     L.dpa_head_slab_blocks.argtypes = [ctypes.c_longlong]

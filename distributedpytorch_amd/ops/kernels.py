@@ -50,6 +50,11 @@ class BwdArgs(ctypes.Structure):
                [("x1", c_void_p), ("slab1", c_void_p), ("bslab1", c_void_p), ("x1bytes", ctypes.c_uint)]
 
 
+class DconvArgs(ctypes.Structure):
+    _fields_ = [(n, c_void_p) for n in ("x", "w1", "b1", "w2", "b2", "a1", "y", "pool", "pcode")] + \
+               [(n, c_int) for n in ("N", "H", "W", "ldy", "ldp", "kp1", "kp2", "rh")]
+
+
 class PackDesc(ctypes.Structure):
     _fields_ = [("src", c_ll), ("dst", c_ll), ("mode", c_int), ("Cout", c_int), ("Cin", c_int), ("Cs", c_int),
                 ("Ngemm", c_int), ("Kpad", c_int)]
@@ -497,6 +502,46 @@ def conv_bwd_fused(g: Optional[torch.Tensor], x: torch.Tensor, wd: torch.Tensor,
         _check(L.dpa_wgrad_reduce(_p(slab1), _p(slab1[nblk * 9 * CI * 8:]), _p(gw1), _p(gb1), c_int(nblk),
                                   c_int(9), c_int(CI), c_int(8), c_int(creal), c_int(0), st), "wgrad_reduce(bwd_stream.w1)")
     return (dx, dx2) if dx2 is not None else dx
+
+
+# ------------------------------------------------------------------------- fused first-level forward
+# opt-in: measured equal to the two streaming kernels it replaces (tools/ab_dconv.sh: 2623-2649 img/s
+# either way; 4.18 ms vs 1.40 + 2.73 ms) -- those kernels are bound by per-row latency, not by the
+# a1 re-read the fusion removes
+USE_FUSED_DCONV1 = os.environ.get("DPA_FUSED_DCONV1", "0") == "1"
+DCONV1_BP = int(os.environ.get("DPA_DCONV1_BP", "0"))      # pixel strip of the fused kernel (0 = auto)
+
+
+def dconv1_fusable(H: int, W: int, c1_out: int, c2_in: int, c2_out: int) -> bool:
+    return USE_FUSED_DCONV1 and W % 64 == 0 and H % 2 == 0 and c1_out == c2_in == c2_out == 32 and H * W * 64 < 2 ** 31
+
+
+def dconv1_fwd(x8: torch.Tensor, w1: torch.Tensor, kp1: int, b1: torch.Tensor, w2: torch.Tensor, kp2: int,
+               b2: torch.Tensor, a1: torch.Tensor, y: torch.Tensor, pool: torch.Tensor,
+               pcode: Optional[torch.Tensor] = None, target_blocks: int = 1024):
+    """The first encoder level's forward in one kernel (csrc/dconv_fwd.hip): a1 = relu(conv3x3(x8)),
+    y = relu(conv3x3(a1)) into ``y`` (the concat-buffer half), its 2x2 max-pool into ``pool`` and the
+    window codes into ``pcode``; a1 is kept in an LDS row ring between the convs and written once
+    (the backward needs it).  Bitwise equal to igemm_stream8 followed by igemm_stream + pool."""
+    assert x8.dtype == torch.bfloat16 and x8.is_contiguous() and x8.dim() == 4 and x8.shape[3] == 8
+    N, H, W, _ = x8.shape
+    assert a1.is_contiguous() and tuple(a1.shape) == (N, H, W, 32) and a1.dtype == torch.bfloat16
+    Ny, Hy, Wy, Cy, ldy = _nhwc(y, "dconv1.y")
+    Np, Hp, Wp, Cp, ldp = _nhwc(pool, "dconv1.pool")
+    assert (Ny, Hy, Wy) == (N, H, W) and Cy >= 32 and (Np, Hp, Wp) == (N, H // 2, W // 2) and Cp >= 32
+    if pcode is not None:
+        assert pcode.dtype == torch.uint8 and pcode.is_contiguous() and tuple(pcode.shape) == (N, H // 2, W // 2, 32)
+    assert w1.dtype == w2.dtype == torch.bfloat16 and w1.numel() >= 32 * kp1 and w2.numel() >= 32 * kp2
+    assert b1.dtype == b2.dtype == torch.float32 and b1.numel() >= 32 and b2.numel() >= 32
+    bp = DCONV1_BP if DCONV1_BP in (64, 128) else 64
+    strips = W // bp
+    segs = max(1, min(H // 2, -(-target_blocks // max(1, N * strips))))
+    rh = -(-H // segs)
+    rh += rh & 1
+    a = DconvArgs(x8.data_ptr(), w1.data_ptr(), b1.data_ptr(), w2.data_ptr(), b2.data_ptr(), a1.data_ptr(),
+                  y.data_ptr(), pool.data_ptr(), None if pcode is None else pcode.data_ptr(),
+                  N, H, W, ldy, ldp, kp1, kp2, rh)
+    _check(_lib.lib().dpa_dconv1_fwd(ctypes.byref(a), c_int(bp), _stream(x8)), "dconv1_fwd")
 
 
 # ------------------------------------------------------------------------------------------ aux
