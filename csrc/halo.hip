@@ -453,7 +453,8 @@ DPA_API int dpa_wgrad_halo(const WgradArgs* args, int cfg, hipStream_t st) {
 // once per block in 32 bits, rows only add a wave-uniform scalar, and all global traffic goes
 // through buffer instructions (32-bit offsets, range-checked zero padding, no 64-bit math).
 // LDS images are [.. ][rows][32 channels] 64-B-row nk images (swz_nk<32>, conflict-free).
-// EPI: 0 plain epilogue, 1 + fused 2x2 max-pool (and window codes), 2 split output (a.y2); the
+// EPI: 0 plain epilogue, 1 + fused 2x2 max-pool (and window codes), 2 split output (a.y2), 3 fused
+// head, 4/5 BatchNorm partials (forward / backward), 6 plain forward (no mask / accumulate); the
 // pool registers and branches exist only in the instantiations that use them.
 template <int BP, int NG, int CS, int RH, int WCS, int EPI>
 __global__ __launch_bounds__(256 * WCS) void igemm_stream_kernel(IgemmArgs a) {
@@ -551,7 +552,11 @@ __global__ __launch_bounds__(256 * WCS) void igemm_stream_kernel(IgemmArgs a) {
     yl[ip] = (unsigned)((pl * a.ldy + wc * WCN + 4 * chunk) * 2);
     ml[ip] = (unsigned)((pl * a.ldm + wc * WCN + 4 * chunk) * 2);
   }
-  const bool has_mask = a.mask != nullptr;
+  // forward epilogues (pool, head, BN statistics, plain forward EPI 6) never mask or accumulate: with
+  // those paths compiled out, no epilogue load shares the in-order vmcnt queue with the two-rows-ahead
+  // prefetch, which a runtime-dead mask load otherwise forced to drain every row (s_waitcnt vmcnt(0))
+  constexpr bool MAYMASK = EPI == 0 || EPI == 2 || EPI == 5;
+  const bool has_mask = MAYMASK && a.mask != nullptr;
   // fused 2x2 max-pool (encoder conv2 -> next level input): even rows keep their horizontally
   // max-reduced values in registers, odd rows finish the window and write the pooled pixel.
   constexpr bool do_pool = EPI == 1;
@@ -595,11 +600,11 @@ __global__ __launch_bounds__(256 * WCS) void igemm_stream_kernel(IgemmArgs a) {
 
   // row r: `cur` holds row h0+r+2 (issued during row r-1); row h0+r+3 is issued into `nxt`
   auto row = [&](int r, RowRegs& cur, RowRegs& nxt) {
-    if (r + 2 < nrows) rload(h0 + r + 3, nxt);
     const int orow = n * a.Ho + h0 + r;
     const unsigned ybase = (unsigned)orow * (unsigned)(a.Wo * a.ldy * 2);
     const unsigned mbase = (unsigned)orow * (unsigned)(a.Wo * a.ldm * 2);
-    // ReLU-mask of this output row: issued before the MFMAs so its latency hides under them
+    // ReLU-mask of this output row: issued before the MFMAs so its latency hides under them, and
+    // before the row prefetch, so waiting for it does not wait for the prefetch (in-order vmcnt)
     u32x2_t mk[TP][TC];
     if (has_mask) {
 #pragma unroll
@@ -609,6 +614,8 @@ __global__ __launch_bounds__(256 * WCS) void igemm_stream_kernel(IgemmArgs a) {
           mk[ip][ic] = (wc * WCN + ic * 16 < a.mask_ch) ? __builtin_amdgcn_raw_buffer_load_b64(mr, mbase + ml[ip] + ic * 32, 0, 0)
                                              : u32x2_t{0x3f803f80u, 0x3f803f80u};
     }
+    __builtin_amdgcn_sched_barrier(0);
+    if (r + 2 < nrows) rload(h0 + r + 3, nxt);
     __builtin_amdgcn_sched_barrier(0);
     f32x4_t acc[TC][TP];
 #pragma unroll
@@ -656,7 +663,7 @@ __global__ __launch_bounds__(256 * WCS) void igemm_stream_kernel(IgemmArgs a) {
           v3 = hi_bf(mk[ip][ic].y) > 0.f ? v3 : 0.f;
         }
         const unsigned yo = ybase + yl[ip] + ic * 32;
-        if (a.accumulate) {
+        if (MAYMASK && a.accumulate) {
           const u32x2_t o = __builtin_amdgcn_raw_buffer_load_b64(yr, yo, 0, 0);
           v0 += lo_bf(o.x); v1 += hi_bf(o.x); v2 += lo_bf(o.y); v3 += hi_bf(o.y);
         }
@@ -923,7 +930,10 @@ static int launch_igemm_stream(const IgemmArgs& a, hipStream_t st) {
     }
     return (int)hipErrorInvalidValue;
   }
-  hipLaunchKernelGGL((igemm_stream_kernel<BP, NG, CS, RH, WCS, 0>), dim3(grid), dim3(256 * WCS), 0, st, a);
+  if (a.mask == nullptr && !a.accumulate)    // plain forward conv: the epilogue without mask / accumulate
+    hipLaunchKernelGGL((igemm_stream_kernel<BP, NG, CS, RH, WCS, 6>), dim3(grid), dim3(256 * WCS), 0, st, a);
+  else
+    hipLaunchKernelGGL((igemm_stream_kernel<BP, NG, CS, RH, WCS, 0>), dim3(grid), dim3(256 * WCS), 0, st, a);
   return (int)hipGetLastError();
 }
 
