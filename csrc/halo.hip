@@ -1005,6 +1005,15 @@ DPA_API int dpa_igemm_stream(const IgemmArgs* args, int variant, hipStream_t st)
 // dW[co][kh][kw][ci] += sum_px g[h][px][co] * x[h+kh-1][px+kw-1][ci].  Fragments come from the
 // [pixel][channel] LDS images through ds_read_b64_tr_b16 (conflict-free swizzles, any row shift).
 // Bias gradient: the loader threads sum the gradient chunks they stage, reduced once per block.
+// the two ds_read_b64_tr_b16 of a transposed fragment (tr_frag) at precomputed byte offsets
+__device__ __forceinline__ bf16x8_t tr_pair_off(const char* base, int off0, int off1) {
+  s16x4_t v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4_t, base + off0));
+  s16x4_t v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(LDS_PTR(s16x4_t, base + off1));
+  typedef __attribute__((ext_vector_type(8))) short s16x8_t;
+  s16x8_t v = __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8_t, v);
+}
+
 template <int BM, int BN, int BP, int RH>
 __global__ __launch_bounds__(192) void wgrad_stream_kernel(WgradArgs a, int ipb) {
   constexpr int NT = 192;
@@ -1089,6 +1098,20 @@ __global__ __launch_bounds__(192) void wgrad_stream_kernel(WgradArgs a, int ipb)
     for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int j = 0; j < TN; ++j) acc[kw][i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  // transposed-fragment addressing (tr_frag) with the per-lane parts precomputed: fragment (column
+  // tile c, k-step ks, half h) sits at base + ((2c << 4) ^ sw4[h]) + const -- the swizzle only sees row
+  // bits that ks*32 and the column tile do not touch, so per fragment one XOR + one add remain (the
+  // per-fragment swizzle arithmetic was more VALU issue than the MFMAs it fed)
+  const int fg = lane >> 4, fq = (lane >> 2) & 3, fp = lane & 3;
+  const int fcol = (fp & 1) * 8 + (fp >> 1) * 16;            // byte offset of this lane's 4 columns
+  int swA[2], swB[3][2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    swA[h] = swz_kk<RBA>(8 * fg + fq + 4 * h) << 4;
+#pragma unroll
+    for (int kw = 0; kw < 3; ++kw) swB[kw][h] = swz_kk<RBB>(kw + 8 * fg + fq + 4 * h) << 4;
+  }
+  const int baseA = (8 * fg + fq) * RBA + fcol, baseB = (8 * fg + fq) * RBB + fcol;
 
 #pragma unroll 1
   for (int im = 0; im < nimg; ++im, ++n) {
@@ -1117,12 +1140,14 @@ __global__ __launch_bounds__(192) void wgrad_stream_kernel(WgradArgs a, int ipb)
     for (int ks = 0; ks < BP / 32; ++ks) {
       bf16x8_t af[TM];
 #pragma unroll
-      for (int i = 0; i < TM; ++i) af[i] = tr_frag<RBA>(Ai, i * 16, lane, ks * 32);
+      for (int i = 0; i < TM; ++i)
+        af[i] = tr_pair_off(Ai + ks * 32 * RBA, baseA + (((2 * i) << 4) ^ swA[0]), baseA + 4 * RBA + (((2 * i) << 4) ^ swA[1]));
 #pragma unroll
       for (int kw = 0; kw < 3; ++kw)
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
-          const bf16x8_t bf = tr_frag<RBB>(Bi, j * 16, lane, ks * 32 + kw);
+          const char* Bk = Bi + (ks * 32 + kw) * RBB;
+          const bf16x8_t bf = tr_pair_off(Bk, baseB + (((2 * j) << 4) ^ swB[kw][0]), baseB + 4 * RBB + (((2 * j) << 4) ^ swB[kw][1]));
 #pragma unroll
           for (int i = 0; i < TM; ++i)
             acc[kw][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf, acc[kw][i][j], 0, 0, 0);
