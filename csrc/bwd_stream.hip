@@ -53,7 +53,6 @@ struct BwdArgs {
   // sum_px dx[h][px][co] * x1[h+kh-1][px+kw-1][ci] from it and an x1 row ring; partials go to
   // slab1 [nblocks][9][32][8] / bslab1 [nblocks][32].
   const bf16_t* x1; float* slab1; float* bslab1; unsigned x1bytes;
-  int dma;              // plain modes: 0 register-staged rows, 4 / 5 LDS-DMA row ring of that many slots
 };
 
 // 8 consecutive k (pixel rows roff+8g .. +7) of 16 channels starting at col0, from an nk image
@@ -620,348 +619,6 @@ __global__ __launch_bounds__(64 * NW, 2) void bwd_stream_kernel(BwdArgs a) {
   }
 }
 
-
-// ------------------------------------------------------------------------------ LDS-DMA variant
-// The plain modes (EPI 0/1/2, no head / pool transform on load) with the g and x rows brought into
-// the rings by `buffer_load_dwordx4 ... lds` instead of through registers.  Register staging waits
-// for its prefetch with in-order vmcnt counts the compiler derives conservatively across the
-// unrolled row loop (the dx stores of a row count too), so in practice a row's loads had to land
-// within that same row; here the waits are explicit counts and, with NS = 5 slots, the DMA for input
-// row h+3 is issued at the start of row h and only waited for at the end of row h+1.
-// DMA writes 64 lanes x 16 B lane-linearly: each slot image ([ks][HR][32] nk for g, [HR][CI] kk for
-// x) is padded to whole KB and every lane fetches the chunk that its destination slot must hold
-// (the XOR swizzle applied on the source side, as igemm_glds does); padding lanes read zeros.
-namespace {
-__device__ __forceinline__ void bdma16(__amdgpu_buffer_rsrc_t r, char* lds, unsigned voff) {
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, voff, 0, 0, 0);
-}
-template <int N>
-__device__ __forceinline__ void bwait_vm() {
-  static_assert(N >= 0 && N < 64, "vmcnt range");
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-}  // namespace
-
-template <int BP, int CI, int CO, int NW, int PG, int EPI, int NS>
-__global__ __launch_bounds__(64 * NW, 1) void bwd_dma_kernel(BwdArgs a) {
-  constexpr int NT = 64 * NW;
-  constexpr int HR = BP + 2;
-  constexpr int KSO = CO / 32;
-  constexpr int WBYTES = 9 * KSO * CI * 64;
-  constexpr int GIMG = KSO * HR * 64, RBX = CI * 2, XIMG = HR * RBX;
-  constexpr int GSLOT = (GIMG + 1023) / 1024 * 1024, XSLOT = (XIMG + 1023) / 1024 * 1024;
-  constexpr int GI = GSLOT / 1024, TI = GI + XSLOT / 1024;      // DMA instructions per row
-  constexpr int IPW = (TI + NW - 1) / NW;                        // per wave (at most)
-  constexpr int WCS = NW == 8 ? 2 : 1, WPX = NW / WCS;
-  constexpr int WP = BP / WPX, TP = WP / 16;
-  constexpr int WCN = CI / WCS, TC = WCN / 16;
-  constexpr int NTI = CI / 16, MTI = CO / 16;
-  constexpr int MSPL = NW / (NTI * PG), MTW = MTI / MSPL;
-  constexpr int KST = BP / 32 / PG;
-  constexpr int BCH = BP * 4 * KSO, LBI = (BCH + NT - 1) / NT;
-  constexpr int ST = TP * TC;                                   // dx stores per lane per row
-  static_assert(TP >= 1 && TC >= 1 && MSPL >= 1 && NTI * MSPL * PG == NW && MTW * MSPL == MTI, "tile");
-  static_assert(NS == 4 || NS == 5, "ring slots");
-  __shared__ __attribute__((aligned(1024))) char lds[WBYTES + NS * GSLOT + NS * XSLOT];
-  char* const Wimg = lds;
-  char* const Gring = lds + WBYTES;
-  char* const Xring = Gring + NS * GSLOT;
-  auto sl = [](int v) { if constexpr (NS == 4) return v & 3; else return v % NS; };
-
-  const int stripsW = a.W / BP, segsH = (a.H + a.rh - 1) / a.rh;
-  const int split_id = blockIdx.x;
-  const int ig = split_id / (segsH * stripsW);
-  const int rem = split_id - ig * segsH * stripsW;
-  const int hs = rem / stripsW;
-  const int w0 = (rem - hs * stripsW) * BP, h0 = hs * a.rh;
-  const int nrows = min(a.rh, a.H - h0);
-  const int nimg = min(a.ipb, a.N - ig * a.ipb);
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wp = wid % WPX, wc = wid / WPX;
-  const int nt = wid % NTI, msp = (wid / NTI) % MSPL, pg = wid / (NTI * MSPL);
-  __amdgpu_buffer_rsrc_t gr, xr, yr, y2r;
-  auto bind = [&](int img) {
-    const long pix = (long)img * a.H * a.W;
-    gr = __builtin_amdgcn_make_buffer_rsrc((void*)(a.g + pix * a.ldg), 0, (int)a.gbytes, 0x00020000);
-    xr = __builtin_amdgcn_make_buffer_rsrc((void*)(a.x + pix * a.ldx), 0, (int)a.xbytes, 0x00020000);
-    yr = __builtin_amdgcn_make_buffer_rsrc((void*)(a.y + pix * a.ldy), 0, 0x7fffffff, 0x00020000);
-    y2r = __builtin_amdgcn_make_buffer_rsrc((void*)(EPI == 1 ? a.y2 + pix * a.ldy2 : a.y), 0, 0x7fffffff, 0x00020000);
-  };
-  for (int c = tid; c < 9 * KSO * CI * 4; c += NT) {
-    const int cc = c & 3, row = (c >> 2) % CI, tk = (c >> 2) / CI;
-    const int tap = tk / KSO, ks = tk - tap * KSO;
-    const u32x4_t v = *reinterpret_cast<const u32x4_t*>(a.wd + (long)row * a.Kd + tap * CO + ks * 32 + cc * 8);
-    *reinterpret_cast<u32x4_t*>(Wimg + (tk * CI + row) * 64 + (swz_nk<32>(row, cc) << 4)) = v;
-  }
-  // ---- DMA plan: instruction k = wid + j*NW (k < GI: g image KB k, else x image KB k-GI); this lane's
-  // 16 B land at byte o = KB*1024 + 16*lane of the image, holding the chunk the swizzle puts there
-  unsigned doff[IPW];
-  bool dok[IPW], dg[IPW];
-  int dkb[IPW];
-#pragma unroll
-  for (int j = 0; j < IPW; ++j) {
-    const int k = wid + j * NW;
-    dg[j] = k < GI;
-    dkb[j] = dg[j] ? k : k - GI;
-    const int o = dkb[j] * 1024 + 16 * lane;
-    if (dg[j]) {
-      const int ks = o / (HR * 64), r2 = o - ks * HR * 64, px = r2 >> 6, s = (r2 >> 4) & 3;
-      const int cc = s ^ ((px >> 1) & 3), iw = w0 + px - 1;     // swz_nk<32> inverse (an involution)
-      dok[j] = k < TI && o < GIMG && iw >= 0 && iw < a.W;
-      doff[j] = (unsigned)((iw * a.ldg + ks * 32 + cc * 8) * 2);
-    } else {
-      const int px = o / RBX, s = (o % RBX) >> 4;
-      const int cc = s ^ swz_kk<RBX>(px), iw = w0 + px - 1;
-      dok[j] = k < TI && o < XIMG && iw >= 0 && iw < a.W;
-      doff[j] = (unsigned)((iw * a.ldx + cc * 8) * 2);
-    }
-  }
-  const int nd = wid < TI ? (TI - 1 - wid) / NW + 1 : 0;        // DMA instructions of this wave per row
-  const unsigned growb = (unsigned)(a.W * a.ldg * 2), xrowb = (unsigned)(a.W * a.ldx * 2);
-  auto dma_row = [&](int ih, int slot) {
-    const bool rok = ih >= 0 && ih < a.H;
-#pragma unroll
-    for (int j = 0; j < IPW; ++j) {
-      if (wid + j * NW >= TI) continue;                          // wave-uniform
-      if (dg[j])
-        bdma16(gr, Gring + slot * GSLOT + dkb[j] * 1024, (rok && dok[j]) ? (unsigned)ih * growb + doff[j] : 0x80000000u);
-      else
-        bdma16(xr, Xring + slot * XSLOT + dkb[j] * 1024, (rok && dok[j]) ? (unsigned)ih * xrowb + doff[j] : 0x80000000u);
-    }
-  };
-  // wait until at most `younger` vector-memory ops of this wave are outstanding (immediate counts)
-  auto wait_younger = [&](int younger) {
-    switch (younger) {
-      case 0: bwait_vm<0>(); break;
-      case 1: bwait_vm<1>(); break;
-      case 2: bwait_vm<2>(); break;
-      case 3: bwait_vm<3>(); break;
-      case 4: bwait_vm<4>(); break;
-      case 5: bwait_vm<5>(); break;
-      case 6: bwait_vm<6>(); break;
-      case 7: bwait_vm<7>(); break;
-      case 8: bwait_vm<8>(); break;
-      case 9: bwait_vm<9>(); break;
-      case 10: bwait_vm<10>(); break;
-      case 11: bwait_vm<11>(); break;
-      default: bwait_vm<12>(); break;
-    }
-  };
-  static_assert(2 * ST + IPW <= 12, "wait table");
-  // ---- dx / dW role offsets (as bwd_stream_kernel)
-  const int chunk = lane >> 4;
-  int aoff[TC];
-#pragma unroll
-  for (int ic = 0; ic < TC; ++ic) {
-    const int row = wc * WCN + ic * 16 + (lane & 15);
-    aoff[ic] = row * 64 + (swz_nk<32>(row, chunk) << 4);
-  }
-  int boff[TP][3];
-#pragma unroll
-  for (int ip = 0; ip < TP; ++ip)
-#pragma unroll
-    for (int kw = 0; kw < 3; ++kw) {
-      const int px = wp * WP + ip * 16 + (lane & 15) + kw;
-      boff[ip][kw] = px * 64 + (swz_nk<32>(px, chunk) << 4);
-    }
-  int moff[TP][TC];
-  unsigned yoff[TP][TC];
-  bool hi[TP][TC];
-#pragma unroll
-  for (int ip = 0; ip < TP; ++ip)
-#pragma unroll
-    for (int ic = 0; ic < TC; ++ic) {
-      const int px = wp * WP + ip * 16 + (lane & 15);
-      const int c0 = wc * WCN + ic * 16 + 4 * chunk;
-      moff[ip][ic] = (px + 1) * RBX + (((c0 >> 3) ^ swz_kk<RBX>(px + 1)) << 4) + ((c0 >> 2) & 1) * 8;
-      hi[ip][ic] = EPI == 1 && c0 >= a.split;
-      yoff[ip][ic] = hi[ip][ic] ? (unsigned)(((w0 + px) * a.ldy2 + c0 - a.split) * 2)
-                                : (unsigned)(((w0 + px) * a.ldy + c0) * 2);
-    }
-  const unsigned yrowb = (unsigned)(a.W * a.ldy * 2), y2rowb = (unsigned)(a.W * (EPI == 1 ? a.ldy2 : a.ldy) * 2);
-  int gta[KST][MTW][2], xta[KST][3][2];
-  {
-    const int g8 = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
-#pragma unroll
-    for (int j = 0; j < KST; ++j) {
-      const int k0 = (pg + j * PG) * 32;
-#pragma unroll
-      for (int mm = 0; mm < MTW; ++mm) {
-        const int m = msp * MTW + mm, col = (m & 1) * 16 + 4 * p, ch = col >> 3, hb = (col & 7) * 2;
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int rr = 1 + k0 + 8 * g8 + q + 4 * h;
-          gta[j][mm][h] = (m >> 1) * HR * 64 + rr * 64 + (swz_nk<32>(rr, ch) << 4) + hb;
-        }
-      }
-#pragma unroll
-      for (int kw = 0; kw < 3; ++kw) {
-        const int col = nt * 16 + 4 * p, ch = col >> 3, hb = (col & 7) * 2;
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int rr = k0 + kw + 8 * g8 + q + 4 * h;
-          xta[j][kw][h] = rr * RBX + ((ch ^ swz_kk<RBX>(rr)) << 4) + hb;
-        }
-      }
-    }
-  }
-  f32x4_t accw[9][MTW];
-#pragma unroll
-  for (int t = 0; t < 9; ++t)
-#pragma unroll
-    for (int m = 0; m < MTW; ++m) accw[t][m] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  float bsum[LBI][8];
-#pragma unroll
-  for (int i = 0; i < LBI; ++i)
-#pragma unroll
-    for (int e = 0; e < 8; ++e) bsum[i][e] = 0.f;
-  const bool do_bias = a.bslab != nullptr;
-
-  int n = ig * a.ipb;
-#pragma unroll 1
-  for (int im = 0; im < nimg; ++im, ++n) {
-    bind(n);
-    // prologue: rows h0-1 .. h0+1 (+ h0+2 with 5 slots, left in flight) -> slots 0..
-    if (nrows > 0) {
-      for (int j = 0; j < 3; ++j) dma_row(h0 - 1 + j, j);
-      if (NS == 5 && nrows > 1) {
-        dma_row(h0 + 2, 3);
-        wait_younger(nd);
-      } else {
-        bwait_vm<0>();
-      }
-    }
-    __syncthreads();
-#pragma unroll 1
-    for (int r = 0; r < nrows; ++r) {
-      // issue the next row: NS 5 -> input row h0+r+3 (needed from row r+2), NS 4 -> h0+r+2 (row r+1)
-      const bool issue = NS == 5 ? r + 2 < nrows : r + 1 < nrows;
-      if (issue) dma_row(NS == 5 ? h0 + r + 3 : h0 + r + 2, sl(r + NS - 1));
-      __builtin_amdgcn_sched_barrier(0);
-      const char* Gm = Gring + sl(r + 1) * GSLOT;
-      const char* Xm = Xring + sl(r + 1) * XSLOT;
-      f32x4_t acc[TC][TP];
-#pragma unroll
-      for (int ic = 0; ic < TC; ++ic)
-#pragma unroll
-        for (int ip = 0; ip < TP; ++ip) acc[ic][ip] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int kh = 0; kh < 3; ++kh) {
-        const char* S = Gring + sl(r + kh) * GSLOT;
-#pragma unroll
-        for (int kw = 0; kw < 3; ++kw)
-#pragma unroll
-          for (int ks = 0; ks < KSO; ++ks) {
-            const int tk = (kh * 3 + kw) * KSO + ks;
-            bf16x8_t af[TC], bfr[TP];
-#pragma unroll
-            for (int ic = 0; ic < TC; ++ic) af[ic] = *reinterpret_cast<const bf16x8_t*>(Wimg + tk * CI * 64 + aoff[ic]);
-#pragma unroll
-            for (int ip = 0; ip < TP; ++ip) bfr[ip] = *reinterpret_cast<const bf16x8_t*>(S + ks * HR * 64 + boff[ip][kw]);
-#pragma unroll
-            for (int ic = 0; ic < TC; ++ic)
-#pragma unroll
-              for (int ip = 0; ip < TP; ++ip)
-                acc[ic][ip] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ic], bfr[ip], acc[ic][ip], 0, 0, 0);
-          }
-      }
-#pragma unroll
-      for (int j = 0; j < KST; ++j) {
-        bf16x8_t ga[MTW];
-#pragma unroll
-        for (int mm = 0; mm < MTW; ++mm) ga[mm] = tr_pair(Gm, gta[j][mm][0], gta[j][mm][1]);
-#pragma unroll
-        for (int kh = 0; kh < 3; ++kh) {
-          const char* XS = Xring + sl(r + kh) * XSLOT;
-#pragma unroll
-          for (int kw = 0; kw < 3; ++kw) {
-            const bf16x8_t xb = tr_pair(XS, xta[j][kw][0], xta[j][kw][1]);
-#pragma unroll
-            for (int m = 0; m < MTW; ++m)
-              accw[kh * 3 + kw][m] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ga[m], xb, accw[kh * 3 + kw][m], 0, 0, 0);
-          }
-        }
-      }
-      if (do_bias) {
-#pragma unroll
-        for (int i = 0; i < LBI; ++i) {
-          const int c = tid + i * NT;
-          if (c < BCH) {
-            const int cc = c & 3, px = ((c >> 2) % BP) + 1, ks = (c >> 2) / BP;
-            const u32x4_t v = *reinterpret_cast<const u32x4_t*>(Gm + ks * HR * 64 + px * 64 + (swz_nk<32>(px, cc) << 4));
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              bsum[i][2 * e] += lo_bf(v[e]);
-              bsum[i][2 * e + 1] += hi_bf(v[e]);
-            }
-          }
-        }
-      }
-      const unsigned orow = (unsigned)(h0 + r);
-#pragma unroll
-      for (int ip = 0; ip < TP; ++ip)
-#pragma unroll
-        for (int ic = 0; ic < TC; ++ic) {
-          float v0 = acc[ic][ip][0], v1 = acc[ic][ip][1], v2 = acc[ic][ip][2], v3 = acc[ic][ip][3];
-          if constexpr (EPI == 0) {
-            const u32x2_t mk = *reinterpret_cast<const u32x2_t*>(Xm + moff[ip][ic]);
-            v0 = lo_bf(mk.x) > 0.f ? v0 : 0.f;
-            v1 = hi_bf(mk.x) > 0.f ? v1 : 0.f;
-            v2 = lo_bf(mk.y) > 0.f ? v2 : 0.f;
-            v3 = hi_bf(mk.y) > 0.f ? v3 : 0.f;
-          }
-          const u32x2_t packed = u32x2_t{pack_bf2(v0, v1), pack_bf2(v2, v3)};
-          if (EPI == 1 && hi[ip][ic])
-            __builtin_amdgcn_raw_buffer_store_b64(packed, y2r, orow * y2rowb + yoff[ip][ic], 0, 0);
-          else
-            __builtin_amdgcn_raw_buffer_store_b64(packed, yr, orow * yrowb + yoff[ip][ic], 0, 0);
-        }
-      __builtin_amdgcn_sched_barrier(0);
-      // the row read next (slot of input row h0+r+2) must have landed: younger ops of this wave are
-      // this row's stores, plus (NS 5) this row's DMA and the previous row's stores
-      if (r + 1 < nrows) {
-        if constexpr (NS == 5) wait_younger(ST + (issue ? nd : 0) + (r > 0 ? ST : 0));
-        else wait_younger(ST);
-      }
-      __syncthreads();
-    }
-  }
-  const long srow = (long)split_id * PG + pg;
-#pragma unroll
-  for (int t = 0; t < 9; ++t)
-#pragma unroll
-    for (int m = 0; m < MTW; ++m) {
-      const int ci = nt * 16 + (lane & 15);
-      const int co = (msp * MTW + m) * 16 + 4 * (lane >> 4);
-      float* dst = a.slab + ((srow * 9 + t) * CO + co) * CI + ci;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) dst[(long)e * CI] = accw[t][m][e];
-    }
-  if (do_bias) {
-    bwait_vm<0>();
-    __syncthreads();
-    float* part = reinterpret_cast<float*>(lds);
-    static_assert(BCH * 8 * 4 <= WBYTES + NS * GSLOT + NS * XSLOT, "bias scratch");
-#pragma unroll
-    for (int i = 0; i < LBI; ++i) {
-      const int c = tid + i * NT;
-      if (c < BCH)
-#pragma unroll
-        for (int e = 0; e < 8; ++e) part[c * 8 + e] = bsum[i][e];
-    }
-    __syncthreads();
-    for (int co = tid; co < CO * PG; co += NT) {
-      const int q = co / CO, cch = co - q * CO;
-      float sacc = 0.f;
-      if (q == 0) {
-        const int ks = cch >> 5, cc = (cch & 31) >> 3, e = cch & 7;
-        for (int px = 0; px < BP; ++px) sacc += part[((ks * BP + px) * 4 + cc) * 8 + e];
-      }
-      a.bslab[((long)split_id * PG + q) * CO + cch] = sacc;
-    }
-  }
-}
-
 template <int BP, int CI, int CO, int NW, int PG, int EPI, bool HEAD = false, bool POOL = false, bool W1 = false>
 static int launch_bwd_stream(const BwdArgs& a, hipStream_t st) {
   const int blocks = ((a.N + a.ipb - 1) / a.ipb) * ((a.H + a.rh - 1) / a.rh) * (a.W / BP);
@@ -1020,22 +677,6 @@ DPA_API int dpa_bwd_stream(const BwdArgs* args, int ci, int co, int epi, hipStre
     if (ci == 32 && co == 32 && epi == 0 && a.tgt && a.hw && a.hb && a.dS)
       return launch_bwd_stream<64, 32, 32, 4, 2, 0, true>(a, st);
     return (int)hipErrorInvalidValue;
-  }
-  if (a.dma == 4 || a.dma == 5) {   // LDS-DMA row ring (plain modes)
-#define DPA_BWDD(CIv, COv, BPv, NWv, PGv, NSv)                                                              \
-    if (ci == CIv && co == COv && a.dma == NSv) {                                                            \
-      const int blocks = ((a.N + a.ipb - 1) / a.ipb) * ((a.H + a.rh - 1) / a.rh) * (a.W / BPv);              \
-      if (epi == 0) hipLaunchKernelGGL((bwd_dma_kernel<BPv, CIv, COv, NWv, PGv, 0, NSv>), dim3(blocks), dim3(64 * NWv), 0, st, a); \
-      else if (epi == 1) hipLaunchKernelGGL((bwd_dma_kernel<BPv, CIv, COv, NWv, PGv, 1, NSv>), dim3(blocks), dim3(64 * NWv), 0, st, a); \
-      else hipLaunchKernelGGL((bwd_dma_kernel<BPv, CIv, COv, NWv, PGv, 2, NSv>), dim3(blocks), dim3(64 * NWv), 0, st, a); \
-      return (int)hipGetLastError();                                                                        \
-    }
-    DPA_BWDD(64, 32, 64, 8, 2, 5)
-    DPA_BWDD(64, 32, 64, 8, 2, 4)
-    DPA_BWDD(32, 64, 64, 8, 2, 5)
-    DPA_BWDD(32, 64, 64, 8, 2, 4)
-    DPA_BWDD(64, 64, 64, 8, 1, 4)
-#undef DPA_BWDD
   }
   DPA_BWD(32, 32, 64, 4, 2)
   DPA_BWD(64, 32, 64, 8, 2)

@@ -47,7 +47,7 @@ class BwdArgs(ctypes.Structure):
                [("gbytes", ctypes.c_uint), ("xbytes", ctypes.c_uint)] + \
                [("tgt", c_void_p), ("hw", c_void_p), ("hb", c_void_p), ("dS", c_void_p), ("hslab", c_void_p)] + \
                [("pcode", c_void_p), ("dpool", c_void_p), ("ldp", c_int)] + \
-               [("x1", c_void_p), ("slab1", c_void_p), ("bslab1", c_void_p), ("x1bytes", ctypes.c_uint), ("dma", c_int)]
+               [("x1", c_void_p), ("slab1", c_void_p), ("bslab1", c_void_p), ("x1bytes", ctypes.c_uint)]
 
 
 class DconvArgs(ctypes.Structure):
@@ -115,8 +115,6 @@ USE_FUSED_BWD = os.environ.get("DPA_NO_FUSED_BWD", "0") != "1"
 USE_FUSED_HEAD_BWD = USE_FUSED_BWD and os.environ.get("DPA_NO_FUSED_HEAD_BWD", "0") != "1"
 # the max-pool backward folded into the full-resolution encoder conv2's fused backward; DPA_NO_FUSED_POOL_BWD=1 disables
 # concat convs whose 2C-input fused backward does not exist: two fused passes, one per half
-# fused backward plain modes: 0 register-staged row prefetch, 4 / 5 LDS-DMA row ring with that many slots
-BWD_DMA = int(os.environ.get("DPA_BWD_DMA", "0"))
 USE_FUSED_HALVES = USE_FUSED_BWD and os.environ.get("DPA_NO_FUSED_HALVES", "0") != "1"
 USE_FUSED_POOL_BWD = USE_FUSED_BWD and os.environ.get("DPA_NO_FUSED_POOL_BWD", "0") != "1"
 # the first encoder conv's weight gradient folded into the pool-mode backward of the second: opt-in,
@@ -466,8 +464,6 @@ def conv_bwd_fused(g: Optional[torch.Tensor], x: torch.Tensor, wd: torch.Tensor,
                 slab.data_ptr(), None if bslab is None else bslab.data_ptr(), ldg, ldx, ldy, ldy2, split, Kd,
                 N, H, W, rh, 1, _extent_bytes(1, H, W, CO, ldg) if g is not None else 0, _extent_bytes(1, H, W, CI, ldx))
     st = _stream(x)
-    if BWD_DMA in (4, 5) and pool is None and head is None and w1 is None:
-        a.dma = 4 if (CI == 64 and CO == 64) else BWD_DMA       # 64->64: 5 slots exceed the 160 KB LDS
     if pool is not None:
         code, dpool = pool
         assert L.dpa_bwd_stream_pool_ok(c_int(CI), c_int(CO)) and epi == 0 and H % 2 == 0 and head is None
