@@ -21,21 +21,23 @@ def main():
         cat = torch.empty(a.batch, 2 * h, 2 * h, 2 * cout, device="cuda", dtype=torch.bfloat16)
         wf = (torch.randn(4 * cout * cin, device="cuda") * 0.05).to(torch.bfloat16)
         b = torch.zeros(cout, device="cuda")
-        fn = lambda: K.deconv_fwd_fused(x, wf, b, cat[..., cout:])
-        fn()
-        torch.cuda.synchronize()
-        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        ts = []
-        for _ in range(a.reps):
-            s.record()
+        dense = torch.empty(a.batch, 2 * h, 2 * h, cout, device="cuda", dtype=torch.bfloat16)
+        for label, out in (("concat half", cat[..., cout:]), ("dense", dense)):
+            fn = lambda: K.deconv_fwd_fused(x, wf, b, out)
             fn()
-            e.record()
             torch.cuda.synchronize()
-            ts.append(s.elapsed_time(e) * 1e3)
-        t = sorted(ts)[len(ts) // 2]
-        gb = (x.numel() + a.batch * 4 * h * h * cout) * 2 / 1e9
-        print(f"{name:24s} {t:9.1f} us  {gb / t * 1e3:6.2f} TB/s", flush=True)
-        del x, cat
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            ts = []
+            for _ in range(a.reps):
+                s.record()
+                fn()
+                e.record()
+                torch.cuda.synchronize()
+                ts.append(s.elapsed_time(e) * 1e3)
+            t = sorted(ts)[len(ts) // 2]
+            gb = (x.numel() + a.batch * 4 * h * h * cout) * 2 / 1e9
+            print(f"{name:24s} {label:12s} {t:9.1f} us  {gb / t * 1e3:6.2f} TB/s", flush=True)
+        del x, cat, dense
 
 
 if __name__ == "__main__":
