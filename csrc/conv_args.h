@@ -28,6 +28,7 @@ struct IgemmArgs {
   // optional BatchNorm batch statistics of the stored (bf16) output (streaming kernel, conv followed
   // by BN): per block, per channel sum and sum of squares -> bnslab[block][2][Ngemm] (bn_finalize)
   float* bnslab;
+  int korder;           // LDS-DMA kernels: 0 = slice-major K-tile order when K is unpadded, 1 = tap-major
 };
 
 // 2x2 window code from the four (bf16-rounded) values in window order tl, tr, bl, br: first
@@ -59,6 +60,18 @@ struct WgradArgs {
   int pix_per_split, splits;
   unsigned abytes, bbytes;  // addressable bytes of A / B (< 2^31; the host splits larger batches)
 };
+
+// 16-B LDS-DMA: lane l's bytes land at lds + 16*l.  (Wrapped in a __device__ function: used
+// directly inside a kernel template the builtin makes the host pass drop the kernel's launch stub.)
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, char* lds, unsigned voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, voff, 0, 0, 0);
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
 
 // nk images ([rows][BK] bf16, 16-B chunks): conflict-free ds_read_b128 fragment reads for any
 // 16 consecutive rows (tools/lds_banks.py)

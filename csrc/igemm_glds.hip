@@ -19,21 +19,76 @@
 
 #include "conv_args.h"
 
-namespace {
 
-// 16-B LDS-DMA: lane l's bytes land at lds + 16*l.  (Wrapped in a __device__ function: used
-// directly inside a kernel template the builtin makes the host pass drop the kernel's launch stub.)
-__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, char* lds, unsigned voff) {
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, voff, 0, 0, 0);
+// K-tile s -> (tap, first channel).  Slice-major order (all taps of one 64-channel slice, then the next
+// slice) when the packed K has no padding: consecutive K-tiles then gather the SAME channel slice at
+// 9 neighbouring pixel offsets, so the pixel lines a K-tile fetches were mostly fetched by the previous
+// one and are still in the XCD's L2 (tap-major order re-reads a line only Cs/64 K-tiles later, after
+// ~8 MB of other traffic went through the 4 MB L2).  The weight block of (tap, ci) is the 128-B
+// column block tap*Cs + ci of the packed [Ngemm][Kpad] matrix in either order.
+__device__ __forceinline__ void ktile_coords(const IgemmArgs& a, int s, int BK, int taps, bool slm, int& tap, int& ci) {
+  if (slm) {
+    const int sl = s / taps;
+    tap = s - sl * taps;
+    ci = sl * BK;
+  } else {
+    tap = (s * BK) / a.Cs;                           // Cs % BK == 0: one tap per K-step (scalar)
+    ci = s * BK - tap * a.Cs;
+  }
 }
 
-template <int N>
-__device__ __forceinline__ void wait_vm() {
-  static_assert(N >= 0 && N < 64, "vmcnt range");
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+// epilogue (as igemm.hip): bias, ReLU, ReLU-backward mask, accumulate, transposed-conv scatter
+template <int TC, int TP, int WC, int WP>
+__device__ __forceinline__ void glds_epilogue(const IgemmArgs& a, f32x4_t (&acc)[TC][TP], int M, int m0, int c0,
+                                              int wc, int wp, int lane) {
+  const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc((void*)a.y, 0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t mr = __builtin_amdgcn_make_buffer_rsrc((void*)(a.mask ? a.mask : a.y), 0, 0x7fffffff, 0x00020000);
+#pragma unroll
+  for (int ip = 0; ip < TP; ++ip) {
+    const int m = m0 + wp * WP + ip * 16 + (lane & 15);
+    if (m >= M) continue;
+    unsigned ybase;
+    if (a.mode == 0) {
+      ybase = (unsigned)m * (unsigned)a.ldy;
+    } else {
+      const int hw = a.Ho * a.Wo;
+      const int n = m / hw, rem = m - n * hw, h = rem / a.Wo, w = rem - (rem / a.Wo) * a.Wo;
+      ybase = (unsigned)(((n * 2 * a.Ho + 2 * h) * (2 * a.Wo) + 2 * w) * a.ldy);
+    }
+#pragma unroll
+    for (int ic = 0; ic < TC; ++ic) {
+      const int nidx = c0 + wc * WC + ic * 16 + 4 * (lane >> 4);
+      int co = nidx;
+      unsigned off = ybase + nidx;
+      if (a.mode == 1) {
+        const int ij = nidx / a.Cout;
+        co = nidx - ij * a.Cout;
+        off = ybase + (unsigned)(((ij >> 1) * (2 * a.Wo) + (ij & 1)) * a.ldy + co);
+      }
+      float v0 = acc[ic][ip][0], v1 = acc[ic][ip][1], v2 = acc[ic][ip][2], v3 = acc[ic][ip][3];
+      if (a.bias) {
+        const float* b = a.bias + co;
+        v0 += b[0]; v1 += b[1]; v2 += b[2]; v3 += b[3];
+      }
+      if (a.relu) {
+        v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f);
+      }
+      if (a.mask && co < a.mask_ch) {
+        const u32x2_t mk = __builtin_amdgcn_raw_buffer_load_b64(mr, ((unsigned)m * (unsigned)a.ldm + co) * 2, 0, 0);
+        v0 = lo_bf(mk.x) > 0.f ? v0 : 0.f;
+        v1 = hi_bf(mk.x) > 0.f ? v1 : 0.f;
+        v2 = lo_bf(mk.y) > 0.f ? v2 : 0.f;
+        v3 = hi_bf(mk.y) > 0.f ? v3 : 0.f;
+      }
+      if (a.accumulate) {
+        const u32x2_t o = __builtin_amdgcn_raw_buffer_load_b64(yr, off * 2, 0, 0);
+        v0 += lo_bf(o.x); v1 += hi_bf(o.x); v2 += lo_bf(o.y); v3 += hi_bf(o.y);
+      }
+      const u32x2_t packed = u32x2_t{pack_bf2(v0, v1), pack_bf2(v2, v3)};
+      if (!split_store(a, (unsigned)m, co, packed)) __builtin_amdgcn_raw_buffer_store_b64(packed, yr, off * 2, 0, 0);
+    }
+  }
 }
-
-}  // namespace
 
 template <int BC, int BP, int WC, int WP, int ST, int BK>
 __global__ __launch_bounds__(512) void igemm_glds_kernel(IgemmArgs a) {
@@ -92,15 +147,17 @@ __global__ __launch_bounds__(512) void igemm_glds_kernel(IgemmArgs a) {
   const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc((void*)a.w, 0, 0x7fffffff, 0x00020000);
   const int S = a.Kpad / BK;
 
+  const bool slm = a.korder == 0 && a.Kpad == taps * a.Cs;
   auto issue = [&](int s) {
     char* base = lds + (s % ST) * STAGE;
-    const int tap = (s * BK) / a.Cs;                  // Cs % BK == 0: one tap per K-step (scalar)
-    const int ci = s * BK - tap * a.Cs;
+    int tap, ci;
+    ktile_coords(a, s, BK, taps, slm, tap, ci);
     const int kh = tap / a.KW, kw = tap - (tap / a.KW) * a.KW;
     const unsigned delta = (unsigned)(((kh * a.Ws + kw) * a.ldx + ci) * 2);
+    const unsigned wk = (unsigned)((tap * a.Cs + ci) * 2);
 #pragma unroll
     for (int j = 0; j < RA; ++j)
-      dma16(wrs, base + (j * 8 * RPI + wid * RPI) * RBY, woff[j] + s * RBY);
+      dma16(wrs, base + (j * 8 * RPI + wid * RPI) * RBY, woff[j] + wk);
 #pragma unroll
     for (int j = 0; j < RP; ++j) {
       const bool ok = tap < taps && ((tmask[j] >> tap) & 1u);
@@ -151,54 +208,7 @@ __global__ __launch_bounds__(512) void igemm_glds_kernel(IgemmArgs a) {
     }
   }
 
-  // ------------------------------------------------------------------ epilogue (as igemm.hip)
-  const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc((void*)a.y, 0, 0x7fffffff, 0x00020000);
-  const __amdgpu_buffer_rsrc_t mr = __builtin_amdgcn_make_buffer_rsrc((void*)(a.mask ? a.mask : a.y), 0, 0x7fffffff, 0x00020000);
-#pragma unroll
-  for (int ip = 0; ip < TP; ++ip) {
-    const int m = m0 + wp * WP + ip * 16 + (lane & 15);
-    if (m >= M) continue;
-    unsigned ybase;
-    if (a.mode == 0) {
-      ybase = (unsigned)m * (unsigned)a.ldy;
-    } else {
-      const int hw = a.Ho * a.Wo;
-      const int n = m / hw, rem = m - n * hw, h = rem / a.Wo, w = rem - (rem / a.Wo) * a.Wo;
-      ybase = (unsigned)(((n * 2 * a.Ho + 2 * h) * (2 * a.Wo) + 2 * w) * a.ldy);
-    }
-#pragma unroll
-    for (int ic = 0; ic < TC; ++ic) {
-      const int nidx = c0 + wc * WC + ic * 16 + 4 * (lane >> 4);
-      int co = nidx;
-      unsigned off = ybase + nidx;
-      if (a.mode == 1) {
-        const int ij = nidx / a.Cout;
-        co = nidx - ij * a.Cout;
-        off = ybase + (unsigned)(((ij >> 1) * (2 * a.Wo) + (ij & 1)) * a.ldy + co);
-      }
-      float v0 = acc[ic][ip][0], v1 = acc[ic][ip][1], v2 = acc[ic][ip][2], v3 = acc[ic][ip][3];
-      if (a.bias) {
-        const float* b = a.bias + co;
-        v0 += b[0]; v1 += b[1]; v2 += b[2]; v3 += b[3];
-      }
-      if (a.relu) {
-        v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f);
-      }
-      if (a.mask && co < a.mask_ch) {
-        const u32x2_t mk = __builtin_amdgcn_raw_buffer_load_b64(mr, ((unsigned)m * (unsigned)a.ldm + co) * 2, 0, 0);
-        v0 = lo_bf(mk.x) > 0.f ? v0 : 0.f;
-        v1 = hi_bf(mk.x) > 0.f ? v1 : 0.f;
-        v2 = lo_bf(mk.y) > 0.f ? v2 : 0.f;
-        v3 = hi_bf(mk.y) > 0.f ? v3 : 0.f;
-      }
-      if (a.accumulate) {
-        const u32x2_t o = __builtin_amdgcn_raw_buffer_load_b64(yr, off * 2, 0, 0);
-        v0 += lo_bf(o.x); v1 += hi_bf(o.x); v2 += lo_bf(o.y); v3 += hi_bf(o.y);
-      }
-      const u32x2_t packed = u32x2_t{pack_bf2(v0, v1), pack_bf2(v2, v3)};
-      if (!split_store(a, (unsigned)m, co, packed)) __builtin_amdgcn_raw_buffer_store_b64(packed, yr, off * 2, 0, 0);
-    }
-  }
+  glds_epilogue<TC, TP, WC, WP>(a, acc, M, m0, c0, wc, wp, lane);
 }
 
 template <int BC, int BP, int WC, int WP, int ST, int BK = 64>
@@ -209,12 +219,16 @@ static int launch_glds(const IgemmArgs& a, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
-// cfg 0 = auto.  1: 256(ch) x 128(px), 3 stages (144 KB)   2: 128 x 256, 3 stages
+// cfg 0 = auto (+16: tap-major K order, for A/B).  1: 256(ch) x 128(px), 3 stages (144 KB)   2: 128 x 256, 3 stages
 //                3: 256 x 256, 2 stages (128 KB)            4: 128 x 128, 4 stages (128 KB)
 //                5: 256 x 256 x BK32, 4 stages (128 KB)     6: 128 x 256 x BK32, 5 stages (120 KB)
 // Requires Cs % 64 == 0 (a K-step never straddles a tap), Kpad % 64 == 0, Ngemm % BC == 0.
 DPA_API int dpa_igemm_glds(const IgemmArgs* args, int cfg, hipStream_t st) {
-  const IgemmArgs& a = *args;
+  IgemmArgs a = *args;
+  if (cfg & 16) {            // A/B: tap-major K-tile order
+    a.korder = 1;
+    cfg &= 15;
+  }
   if ((a.Cs & 63) || (a.Kpad & 63) || (a.ldx & 7) || (a.ldy & 3) || a.KH * a.KW > 32) return (int)hipErrorInvalidValue;
   if (a.mode == 1 && (a.Cout & 3)) return (int)hipErrorInvalidValue;
   if (cfg == 0) {

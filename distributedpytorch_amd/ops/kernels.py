@@ -30,7 +30,7 @@ class IgemmArgs(ctypes.Structure):
                                      "stride", "pad", "Ngemm", "Kpad", "mode", "relu", "accumulate", "Cout")] + \
                [("xbytes", ctypes.c_uint), ("pool", c_void_p), ("ldp", c_int), ("pcode", c_void_p), ("y2", c_void_p),
                 ("ldy2", c_int), ("split", c_int), ("hw", c_void_p), ("hb", c_void_p), ("tgt", c_void_p),
-                ("hslab", c_void_p), ("bnslab", c_void_p)]
+                ("hslab", c_void_p), ("bnslab", c_void_p), ("korder", c_int)]
 
 
 class WgradArgs(ctypes.Structure):
@@ -93,6 +93,8 @@ USE_HALO = os.environ.get("DPA_NO_HALO", "0") != "1"
 # row-streaming conv3x3 (weights resident, 4-row LDS ring); DPA_NO_STREAM=1 disables
 USE_STREAM = os.environ.get("DPA_NO_STREAM", "0") != "1"
 USE_GLDS = os.environ.get("DPA_NO_GLDS", "0") != "1"
+# A/B: tap-major K-tile order in the LDS-DMA kernels (default slice-major, csrc/igemm_glds.hip ktile_coords)
+GLDS_TAP_MAJOR = os.environ.get("DPA_GLDS_TAP_MAJOR", "0") == "1"
 # conv weight gradients on a side HIP stream, overlapping each block's dgrad chain (models/hip_unet.py)
 SIDE_WGRAD = os.environ.get("DPA_NO_SIDE_WGRAD", "0") != "1"
 # HIP stream priority of the weight-gradient side stream (torch convention: lower = higher priority,
@@ -255,7 +257,7 @@ def igemm(x: torch.Tensor, wpacked: torch.Tensor, y: torch.Tensor, *, Ngemm: int
             if path == "halo":
                 _check(err, "igemm_halo")
         if path == "glds" or (path == "auto" and glds_ok):
-            err = L.dpa_igemm_glds(ctypes.byref(a), c_int(variant if path == "glds" else 0), st)
+            err = L.dpa_igemm_glds(ctypes.byref(a), c_int(variant if path == "glds" else 16 * GLDS_TAP_MAJOR), st)
             if err == 0:
                 continue
             if path == "glds":
