@@ -28,7 +28,8 @@ struct IgemmArgs {
   // optional BatchNorm batch statistics of the stored (bf16) output (streaming kernel, conv followed
   // by BN): per block, per channel sum and sum of squares -> bnslab[block][2][Ngemm] (bn_finalize)
   float* bnslab;
-  int korder;           // LDS-DMA kernels: 0 = slice-major K-tile order when K is unpadded, 1 = tap-major
+  int korder;           // LDS-DMA kernels: bit 0 = tap-major K-tile order (default slice-major when K is
+                        // unpadded), bit 1 = no persistent kernel in the auto choice (A/B switches)
 };
 
 // 2x2 window code from the four (bf16-rounded) values in window order tl, tr, bl, br: first

@@ -147,7 +147,7 @@ __global__ __launch_bounds__(512) void igemm_glds_kernel(IgemmArgs a) {
   const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc((void*)a.w, 0, 0x7fffffff, 0x00020000);
   const int S = a.Kpad / BK;
 
-  const bool slm = a.korder == 0 && a.Kpad == taps * a.Cs;
+  const bool slm = !(a.korder & 1) && a.Kpad == taps * a.Cs;
   auto issue = [&](int s) {
     char* base = lds + (s % ST) * STAGE;
     int tap, ci;
@@ -211,6 +211,181 @@ __global__ __launch_bounds__(512) void igemm_glds_kernel(IgemmArgs a) {
   glds_epilogue<TC, TP, WC, WP>(a, acc, M, m0, c0, wc, wp, lane);
 }
 
+// ------------------------------------------------------------------------------------------------
+// Persistent variant (cfg 8-10): one workgroup per CU walks a list of output tiles and keeps the
+// LDS-DMA pipeline running ACROSS tile boundaries -- the first K-steps of tile j+1 are issued during
+// the last K-steps of tile j and land while tile j's epilogue stores its outputs -- instead of one
+// workgroup per tile, where every tile pays the first loads' HBM latency and its epilogue on an
+// otherwise idle CU (one 128-144 KB workgroup fits a CU, so nothing else overlaps them).  That
+// ramp is ~5-15 % of a tile at K = 2304-4608 and far more at the short K of the transposed convs
+// and the K = 1152 layers.  Tiles are dealt in XCD-contiguous chunks (workgroup b runs on XCD b & 7,
+// its slot b >> 3 takes every (grid/8)-th tile of that XCD's chunk), so the ~32 tiles an XCD works on
+// at a time are neighbours sharing halo rows and weights in its L2.
+template <int BC, int BP, int WC, int WP, int ST, int BK>
+__global__ __launch_bounds__(512) void igemm_glds_pers_kernel(IgemmArgs a) {
+  constexpr int NWC = BC / WC, NWP = BP / WP;
+  static_assert(NWC * NWP == 8, "8 waves");
+  constexpr int RBY = BK * 2, CPR = RBY / 16, RPI = 64 / CPR;
+  constexpr int RA = BC / (8 * RPI), RP = BP / (8 * RPI);
+  static_assert(RA * 8 * RPI == BC && RP * 8 * RPI == BP, "loader tiling");
+  constexpr int LPS = RA + RP;
+  constexpr int TC = WC / 16, TP = WP / 16;
+  constexpr int STAGE = (BC + BP) * RBY;
+  __shared__ __attribute__((aligned(16))) char lds[ST * STAGE];
+
+  const int M = a.N * a.Ho * a.Wo;
+  const int nct = a.Ngemm / BC;
+  const int T = ((M + BP - 1) / BP) * nct;
+  const int G8 = gridDim.x >> 3, xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
+  const int q = T >> 3, r = T & 7;
+  const int cstart = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  const int clen = q + (xcd < r ? 1 : 0);
+  const int J = slot < clen ? (clen - slot + G8 - 1) / G8 : 0;
+  if (J == 0) return;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wc = wid % NWC, wp = wid / NWC;
+  const int lrow = wid * RPI + lane / CPR;
+  const int lchunk = swz_nk<BK>(lrow, lane % CPR);
+  const int taps = a.KH * a.KW;
+  const int hw = a.Ho * a.Wo;
+
+  // loader geometry of tile j of this workgroup's list
+  auto geo = [&](int j, unsigned (&pb)[RP], unsigned (&tm)[RP], unsigned (&wo)[RA], int& m0, int& c0) {
+    const int t = cstart + slot + j * G8;
+    const int pt = t / nct, ct = t - pt * nct;
+    m0 = pt * BP;
+    c0 = ct * BC;
+#pragma unroll
+    for (int i = 0; i < RP; ++i) {
+      const int m = m0 + i * 8 * RPI + lrow;
+      const bool pok = m < M;
+      const int mm = pok ? m : 0;
+      const int pn = mm / hw;
+      const int rem = mm - pn * hw;
+      const int ph = rem / a.Wo, pw = rem - ph * a.Wo;
+      const int h0 = ph * a.stride - a.pad, w0 = pw * a.stride - a.pad;
+      unsigned msk = 0;
+      for (int k = 0; k < taps; ++k) {
+        const int kh = k / a.KW, kw = k - kh * a.KW;
+        const int ih = h0 + kh, iw = w0 + kw;
+        if (pok && ih >= 0 && ih < a.Hs && iw >= 0 && iw < a.Ws) msk |= 1u << k;
+      }
+      tm[i] = msk;
+      pb[i] = (unsigned)((((pn * a.Hs + h0) * a.Ws + w0) * a.ldx) * 2 + lchunk * 16);
+    }
+#pragma unroll
+    for (int i = 0; i < RA; ++i) wo[i] = (unsigned)(((c0 + i * 8 * RPI + lrow) * a.Kpad) * 2 + lchunk * 16);
+  };
+
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, 0, (int)a.xbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc((void*)a.w, 0, 0x7fffffff, 0x00020000);
+  const int S = a.Kpad / BK;
+  const int GT = J * S;
+  const bool slm = !(a.korder & 1) && a.Kpad == taps * a.Cs;
+
+  // one geometry set: the next tile's overwrites the current one at K-step S-ST+1, after the current
+  // tile's last DMA was issued (the epilogue keeps only the tile origin)
+  unsigned pb[RP], tm[RP], wo[RA];
+  int m0, c0, m0g, c0g;
+  geo(0, pb, tm, wo, m0g, c0g);
+
+  // K-step sk of the tile whose geometry is loaded into stage buffer b
+  auto issue = [&](int b, int sk) {
+    char* base = lds + b * STAGE;
+    int tap, ci;
+    ktile_coords(a, sk, BK, taps, slm, tap, ci);
+    const int kh = tap / a.KW, kw = tap - kh * a.KW;
+    const unsigned delta = (unsigned)(((kh * a.Ws + kw) * a.ldx + ci) * 2);
+    const unsigned wk = (unsigned)((tap * a.Cs + ci) * 2);
+#pragma unroll
+    for (int i = 0; i < RA; ++i) dma16(wrs, base + (i * 8 * RPI + wid * RPI) * RBY, wo[i] + wk);
+#pragma unroll
+    for (int i = 0; i < RP; ++i) {
+      const bool ok = tap < taps && ((tm[i] >> tap) & 1u);
+      dma16(xr, base + (BC + i * 8 * RPI + wid * RPI) * RBY, ok ? pb[i] + delta : 0x80000000u);
+    }
+  };
+
+  f32x4_t acc[TC][TP];
+#pragma unroll
+  for (int ic = 0; ic < TC; ++ic)
+#pragma unroll
+    for (int ip = 0; ip < TP; ++ip) acc[ic][ip] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int s = 0; s < ST - 1; ++s) issue(s, s);      // host guarantees S >= ST - 1
+
+  int g = 0;
+  for (int j = 0; j < J; ++j) {
+    m0 = m0g;
+    c0 = c0g;
+    for (int s = 0; s < S; ++s, ++g) {
+      // after an epilogue (its loads/stores share the counter) drain; else keep ST-2 steps in flight
+      if ((s == 0 && j > 0) || g + ST - 2 >= GT) wait_vm<0>();
+      else wait_vm<(ST - 2) * LPS>();
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      if (g + ST - 1 < GT) {
+        const int sk = s + ST - 1;
+        if (sk == S) geo(j + 1, pb, tm, wo, m0g, c0g);
+        issue((g + ST - 1) % ST, sk >= S ? sk - S : sk);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      const char* Wt = lds + (g % ST) * STAGE;
+      const char* P = Wt + BC * RBY;
+#pragma unroll
+      for (int kk = 0; kk < BK / 32; ++kk) {
+        const int chunk = kk * 4 + (lane >> 4);
+        bf16x8_t af[TC], bfr[TP];
+#pragma unroll
+        for (int ic = 0; ic < TC; ++ic) {
+          const int row = wc * WC + ic * 16 + (lane & 15);
+          af[ic] = *reinterpret_cast<const bf16x8_t*>(Wt + row * RBY + (swz_nk<BK>(row, chunk) << 4));
+        }
+#pragma unroll
+        for (int ip = 0; ip < TP; ++ip) {
+          const int row = wp * WP + ip * 16 + (lane & 15);
+          bfr[ip] = *reinterpret_cast<const bf16x8_t*>(P + row * RBY + (swz_nk<BK>(row, chunk) << 4));
+        }
+#pragma unroll
+        for (int ic = 0; ic < TC; ++ic)
+#pragma unroll
+          for (int ip = 0; ip < TP; ++ip)
+            acc[ic][ip] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ic], bfr[ip], acc[ic][ip], 0, 0, 0);
+      }
+    }
+    glds_epilogue<TC, TP, WC, WP>(a, acc, M, m0, c0, wc, wp, lane);
+#pragma unroll
+    for (int ic = 0; ic < TC; ++ic)
+#pragma unroll
+      for (int ip = 0; ip < TP; ++ip) acc[ic][ip] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  }
+}
+
+static int cu_count() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+  }
+  return n;
+}
+
+template <int BC, int BP, int WC, int WP, int ST, int BK = 64>
+static int launch_glds_pers(const IgemmArgs& a, hipStream_t st) {
+  if (a.Kpad / BK < ST - 1) return (int)hipErrorInvalidValue;
+  const int M = a.N * a.Ho * a.Wo;
+  const int tiles = ((M + BP - 1) / BP) * (a.Ngemm / BC);
+  int grid = cu_count();
+  if (grid > tiles) grid = tiles;
+  grid = (grid + 7) & ~7;                     // XCD chunks: a multiple of 8 workgroups
+  hipLaunchKernelGGL((igemm_glds_pers_kernel<BC, BP, WC, WP, ST, BK>), dim3(grid), dim3(512), 0, st, a);
+  return (int)hipGetLastError();
+}
+
 template <int BC, int BP, int WC, int WP, int ST, int BK = 64>
 static int launch_glds(const IgemmArgs& a, hipStream_t st) {
   const int M = a.N * a.Ho * a.Wo;
@@ -219,16 +394,16 @@ static int launch_glds(const IgemmArgs& a, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
-// cfg 0 = auto (+16: tap-major K order, for A/B).  1: 256(ch) x 128(px), 3 stages (144 KB)   2: 128 x 256, 3 stages
+// cfg 0 = auto (+16: tap-major K order, +32: auto without the persistent kernel; for A/B).  1: 256(ch) x 128(px), 3 stages (144 KB)   2: 128 x 256, 3 stages
 //                3: 256 x 256, 2 stages (128 KB)            4: 128 x 128, 4 stages (128 KB)
 //                5: 256 x 256 x BK32, 4 stages (128 KB)     6: 128 x 256 x BK32, 5 stages (120 KB)
+//                8 / 9 / 10: cfg 3 / 2 / 1 as a persistent kernel (one workgroup per CU, pipelined across tiles)
 // Requires Cs % 64 == 0 (a K-step never straddles a tap), Kpad % 64 == 0, Ngemm % BC == 0.
 DPA_API int dpa_igemm_glds(const IgemmArgs* args, int cfg, hipStream_t st) {
   IgemmArgs a = *args;
-  if (cfg & 16) {            // A/B: tap-major K-tile order
-    a.korder = 1;
-    cfg &= 15;
-  }
+  if (cfg & 16) a.korder |= 1;   // A/B: tap-major K-tile order
+  if (cfg & 32) a.korder |= 2;   // A/B: no persistent kernel in the auto choice
+  cfg &= 15;
   if ((a.Cs & 63) || (a.Kpad & 63) || (a.ldx & 7) || (a.ldy & 3) || a.KH * a.KW > 32) return (int)hipErrorInvalidValue;
   if (a.mode == 1 && (a.Cout & 3)) return (int)hipErrorInvalidValue;
   if (cfg == 0) {
@@ -237,7 +412,10 @@ DPA_API int dpa_igemm_glds(const IgemmArgs* args, int cfg, hipStream_t st) {
     // (XL bottleneck, 2 images: 2048 pixels x 2048 channels = 64 tiles of 256x256 for 256 CUs)
     const long M = (long)a.N * a.Ho * a.Wo;
     auto grid_of = [&](long bc, long bp) { return ((M + bp - 1) / bp) * (a.Ngemm / bc); };
-    if (a.Ngemm % 256 == 0 && grid_of(256, 256) >= 512) cfg = 3;
+    // short K (<= 18 K-steps: the K = 1152 convs, the transposed convs): the persistent kernel, which
+    // hides each tile's first-load latency and epilogue behind the neighbouring tile, is 3-11 % faster
+    // there; at longer K it is 4-7 % slower (profiles/kbench_glds_pers_b256_r02.txt)
+    if (a.Ngemm % 256 == 0 && grid_of(256, 256) >= 512) cfg = (a.Kpad <= 18 * 64 && !(a.korder & 2)) ? 8 : 3;
     else if (a.Ngemm % 128 == 0 && grid_of(128, 256) >= 512) cfg = 2;
     else if (a.Ngemm % 256 == 0 && grid_of(256, 128) >= 512) cfg = 1;
     else cfg = 4;
@@ -249,6 +427,9 @@ DPA_API int dpa_igemm_glds(const IgemmArgs* args, int cfg, hipStream_t st) {
     case 4: if (a.Ngemm % 128) break; return launch_glds<128, 128, 64, 32, 4>(a, st);
     case 5: if (a.Ngemm % 256) break; return launch_glds<256, 256, 128, 64, 4, 32>(a, st);
     case 6: if (a.Ngemm % 128) break; return launch_glds<128, 256, 64, 64, 5, 32>(a, st);
+    case 8: if (a.Ngemm % 256) break; return launch_glds_pers<256, 256, 128, 64, 2>(a, st);
+    case 9: if (a.Ngemm % 128) break; return launch_glds_pers<128, 256, 64, 64, 3>(a, st);
+    case 10: if (a.Ngemm % 256) break; return launch_glds_pers<256, 128, 64, 64, 3>(a, st);
     default: break;
   }
   return (int)hipErrorInvalidValue;
