@@ -126,9 +126,9 @@ def _run(worker, world, *args, timeout=240):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("comm", ["fp32", "bf16"])
-def test_ddp_hip_allreduce_equals_mean_of_rank_grads(hip_lib, comm):
-    res = _run(_ddp_worker, 2, comm)
+@pytest.mark.parametrize("world,comm", [(2, "fp32"), (2, "bf16"), (4, "fp32")])
+def test_ddp_hip_allreduce_equals_mean_of_rank_grads(hip_lib, world, comm):
+    res = _run(_ddp_worker, world, comm)
     for rank, ok, err, same, nb, _ in res:
         assert nb >= 4, f"expected several buckets at 1 MiB, got {nb}"
         assert ok, f"rank {rank}: reduced grads != mean of per-rank grads (max rel err {err:.2e})"
