@@ -37,7 +37,48 @@ __device__ __forceinline__ void ktile_coords(const IgemmArgs& a, int s, int BK, 
   }
 }
 
-// epilogue (as igemm.hip): bias, ReLU, ReLU-backward mask, accumulate, transposed-conv scatter
+// epilogue (as igemm.hip): bias, ReLU, ReLU-backward mask, accumulate, transposed-conv scatter.
+// Output base of GEMM row (pixel) m: NHWC row, or the (2h, 2w) corner of its 2x2 block (mode 1).
+__device__ __forceinline__ unsigned glds_ybase(const IgemmArgs& a, int m) {
+  if (a.mode == 0) return (unsigned)m * (unsigned)a.ldy;
+  const int hw = a.Ho * a.Wo;
+  const int n = m / hw, rem = m - n * hw, h = rem / a.Wo, w = rem - (rem / a.Wo) * a.Wo;
+  return (unsigned)(((n * 2 * a.Ho + 2 * h) * (2 * a.Wo) + 2 * w) * a.ldy);
+}
+
+// four consecutive GEMM columns nidx..nidx+3 of pixel m
+__device__ __forceinline__ void glds_store4(const IgemmArgs& a, __amdgpu_buffer_rsrc_t yr, __amdgpu_buffer_rsrc_t mr,
+                                            int m, unsigned ybase, int nidx, float v0, float v1, float v2, float v3) {
+  int co = nidx;
+  unsigned off = ybase + nidx;
+  if (a.mode == 1) {
+    const int ij = nidx / a.Cout;
+    co = nidx - ij * a.Cout;
+    off = ybase + (unsigned)(((ij >> 1) * (2 * a.Wo) + (ij & 1)) * a.ldy + co);
+  }
+  if (a.bias) {
+    const float* b = a.bias + co;
+    v0 += b[0]; v1 += b[1]; v2 += b[2]; v3 += b[3];
+  }
+  if (a.relu) {
+    v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f);
+  }
+  if (a.mask && co < a.mask_ch) {
+    const u32x2_t mk = __builtin_amdgcn_raw_buffer_load_b64(mr, ((unsigned)m * (unsigned)a.ldm + co) * 2, 0, 0);
+    v0 = lo_bf(mk.x) > 0.f ? v0 : 0.f;
+    v1 = hi_bf(mk.x) > 0.f ? v1 : 0.f;
+    v2 = lo_bf(mk.y) > 0.f ? v2 : 0.f;
+    v3 = hi_bf(mk.y) > 0.f ? v3 : 0.f;
+  }
+  if (a.accumulate) {
+    const u32x2_t o = __builtin_amdgcn_raw_buffer_load_b64(yr, off * 2, 0, 0);
+    v0 += lo_bf(o.x); v1 += hi_bf(o.x); v2 += lo_bf(o.y); v3 += hi_bf(o.y);
+  }
+  const u32x2_t packed = u32x2_t{pack_bf2(v0, v1), pack_bf2(v2, v3)};
+  if (!split_store(a, (unsigned)m, co, packed)) __builtin_amdgcn_raw_buffer_store_b64(packed, yr, off * 2, 0, 0);
+}
+
+// 16x16 accumulator tiles: pixel = lane & 15, channels 4*(lane >> 4) + 0..3
 template <int TC, int TP, int WC, int WP>
 __device__ __forceinline__ void glds_epilogue(const IgemmArgs& a, f32x4_t (&acc)[TC][TP], int M, int m0, int c0,
                                               int wc, int wp, int lane) {
@@ -47,46 +88,11 @@ __device__ __forceinline__ void glds_epilogue(const IgemmArgs& a, f32x4_t (&acc)
   for (int ip = 0; ip < TP; ++ip) {
     const int m = m0 + wp * WP + ip * 16 + (lane & 15);
     if (m >= M) continue;
-    unsigned ybase;
-    if (a.mode == 0) {
-      ybase = (unsigned)m * (unsigned)a.ldy;
-    } else {
-      const int hw = a.Ho * a.Wo;
-      const int n = m / hw, rem = m - n * hw, h = rem / a.Wo, w = rem - (rem / a.Wo) * a.Wo;
-      ybase = (unsigned)(((n * 2 * a.Ho + 2 * h) * (2 * a.Wo) + 2 * w) * a.ldy);
-    }
+    const unsigned ybase = glds_ybase(a, m);
 #pragma unroll
-    for (int ic = 0; ic < TC; ++ic) {
-      const int nidx = c0 + wc * WC + ic * 16 + 4 * (lane >> 4);
-      int co = nidx;
-      unsigned off = ybase + nidx;
-      if (a.mode == 1) {
-        const int ij = nidx / a.Cout;
-        co = nidx - ij * a.Cout;
-        off = ybase + (unsigned)(((ij >> 1) * (2 * a.Wo) + (ij & 1)) * a.ldy + co);
-      }
-      float v0 = acc[ic][ip][0], v1 = acc[ic][ip][1], v2 = acc[ic][ip][2], v3 = acc[ic][ip][3];
-      if (a.bias) {
-        const float* b = a.bias + co;
-        v0 += b[0]; v1 += b[1]; v2 += b[2]; v3 += b[3];
-      }
-      if (a.relu) {
-        v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f);
-      }
-      if (a.mask && co < a.mask_ch) {
-        const u32x2_t mk = __builtin_amdgcn_raw_buffer_load_b64(mr, ((unsigned)m * (unsigned)a.ldm + co) * 2, 0, 0);
-        v0 = lo_bf(mk.x) > 0.f ? v0 : 0.f;
-        v1 = hi_bf(mk.x) > 0.f ? v1 : 0.f;
-        v2 = lo_bf(mk.y) > 0.f ? v2 : 0.f;
-        v3 = hi_bf(mk.y) > 0.f ? v3 : 0.f;
-      }
-      if (a.accumulate) {
-        const u32x2_t o = __builtin_amdgcn_raw_buffer_load_b64(yr, off * 2, 0, 0);
-        v0 += lo_bf(o.x); v1 += hi_bf(o.x); v2 += lo_bf(o.y); v3 += hi_bf(o.y);
-      }
-      const u32x2_t packed = u32x2_t{pack_bf2(v0, v1), pack_bf2(v2, v3)};
-      if (!split_store(a, (unsigned)m, co, packed)) __builtin_amdgcn_raw_buffer_store_b64(packed, yr, off * 2, 0, 0);
-    }
+    for (int ic = 0; ic < TC; ++ic)
+      glds_store4(a, yr, mr, m, ybase, c0 + wc * WC + ic * 16 + 4 * (lane >> 4), acc[ic][ip][0], acc[ic][ip][1],
+                  acc[ic][ip][2], acc[ic][ip][3]);
   }
 }
 
@@ -386,6 +392,135 @@ static int launch_glds_pers(const IgemmArgs& a, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
+// ------------------------------------------------------------------------------------------------
+// 32x32x16 variant (cfg 11): cfg 3's tile and pipeline with v_mfma_f32_32x32x16_bf16 -- half the MFMA
+// instructions for the same LDS fragment traffic (per wave and K=64: 4 x (4 A + 2 B) ds_read_b128,
+// 32 MFMAs of 32 cycles instead of 64 of 16).  A 32x32x16 fragment read covers 32 rows with one
+// chunk per 32-lane half, so the image swizzle is chunk ^ ((row >> 1) & 7) (conflict-free for the
+// ds_read_b128 lane groups over 32 consecutive rows; the DMA applies it on the source side).
+__device__ __forceinline__ int swz32(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
+
+__global__ __launch_bounds__(512) void igemm_glds32_kernel(IgemmArgs a) {
+  constexpr int BC = 256, BP = 256, WC = 128, WP = 64, ST = 2, BK = 64;
+  constexpr int NWC = BC / WC, RBY = 128, RPI = 8;
+  constexpr int RA = BC / 64, RP = BP / 64, LPS = RA + RP;
+  constexpr int TC = WC / 32, TP = WP / 32;
+  constexpr int STAGE = (BC + BP) * RBY;
+  __shared__ __attribute__((aligned(16))) char lds[ST * STAGE];
+
+  const int M = a.N * a.Ho * a.Wo;
+  const int nct = a.Ngemm / BC;
+  const int npt = (M + BP - 1) / BP;
+  const int bid = xcd_remap(blockIdx.x, npt * nct);
+  const int pt = bid / nct, ct = bid - pt * nct;
+  const int m0 = pt * BP, c0 = ct * BC;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wc = wid % NWC, wp = wid / NWC;
+  const int lrow = wid * RPI + (lane >> 3);          // + j*64 per round: bits 1-3 unchanged
+  const int lchunk = swz32(lrow, lane & 7);
+
+  unsigned pbase[RP], tmask[RP];
+  const int taps = a.KH * a.KW;
+  const int hw = a.Ho * a.Wo;
+#pragma unroll
+  for (int j = 0; j < RP; ++j) {
+    const int m = m0 + j * 64 + lrow;
+    const bool pok = m < M;
+    const int mm = pok ? m : 0;
+    const int pn = mm / hw;
+    const int rem = mm - pn * hw;
+    const int ph = rem / a.Wo, pw = rem - ph * a.Wo;
+    const int h0 = ph * a.stride - a.pad, w0 = pw * a.stride - a.pad;
+    unsigned msk = 0;
+    for (int t = 0; t < taps; ++t) {
+      const int kh = t / a.KW, kw = t - kh * a.KW;
+      const int ih = h0 + kh, iw = w0 + kw;
+      if (pok && ih >= 0 && ih < a.Hs && iw >= 0 && iw < a.Ws) msk |= 1u << t;
+    }
+    tmask[j] = msk;
+    pbase[j] = (unsigned)((((pn * a.Hs + h0) * a.Ws + w0) * a.ldx) * 2 + lchunk * 16);
+  }
+  unsigned woff[RA];
+#pragma unroll
+  for (int j = 0; j < RA; ++j) woff[j] = (unsigned)(((c0 + j * 64 + lrow) * a.Kpad) * 2 + lchunk * 16);
+
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, 0, (int)a.xbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc((void*)a.w, 0, 0x7fffffff, 0x00020000);
+  const int S = a.Kpad / BK;
+  const bool slm = !(a.korder & 1) && a.Kpad == taps * a.Cs;
+  auto issue = [&](int s) {
+    char* base = lds + (s % ST) * STAGE;
+    int tap, ci;
+    ktile_coords(a, s, BK, taps, slm, tap, ci);
+    const int kh = tap / a.KW, kw = tap - kh * a.KW;
+    const unsigned delta = (unsigned)(((kh * a.Ws + kw) * a.ldx + ci) * 2);
+    const unsigned wk = (unsigned)((tap * a.Cs + ci) * 2);
+#pragma unroll
+    for (int j = 0; j < RA; ++j) dma16(wrs, base + (j * 64 + wid * RPI) * RBY, woff[j] + wk);
+#pragma unroll
+    for (int j = 0; j < RP; ++j) {
+      const bool ok = tap < taps && ((tmask[j] >> tap) & 1u);
+      dma16(xr, base + (BC + j * 64 + wid * RPI) * RBY, ok ? pbase[j] + delta : 0x80000000u);
+    }
+  };
+
+  f32x16_t acc[TC][TP];
+#pragma unroll
+  for (int ic = 0; ic < TC; ++ic)
+#pragma unroll
+    for (int ip = 0; ip < TP; ++ip)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[ic][ip][e] = 0.f;
+
+  issue(0);
+  for (int s = 0; s < S; ++s) {
+    wait_vm<0>();
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (s + 1 < S) issue(s + 1);
+    __builtin_amdgcn_sched_barrier(0);
+    const char* Wt = lds + (s % ST) * STAGE;
+    const char* P = Wt + BC * RBY;
+#pragma unroll
+    for (int kk = 0; kk < BK / 16; ++kk) {
+      const int chunk = kk * 2 + (lane >> 5);
+      bf16x8_t af[TC], bfr[TP];
+#pragma unroll
+      for (int ic = 0; ic < TC; ++ic) {
+        const int row = wc * WC + ic * 32 + (lane & 31);
+        af[ic] = *reinterpret_cast<const bf16x8_t*>(Wt + row * RBY + (swz32(row, chunk) << 4));
+      }
+#pragma unroll
+      for (int ip = 0; ip < TP; ++ip) {
+        const int row = wp * WP + ip * 32 + (lane & 31);
+        bfr[ip] = *reinterpret_cast<const bf16x8_t*>(P + row * RBY + (swz32(row, chunk) << 4));
+      }
+#pragma unroll
+      for (int ic = 0; ic < TC; ++ic)
+#pragma unroll
+        for (int ip = 0; ip < TP; ++ip)
+          acc[ic][ip] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[ic], bfr[ip], acc[ic][ip], 0, 0, 0);
+    }
+  }
+
+  // 32x32 tiles: pixel = lane & 31; register r holds channel (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
+  const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc((void*)a.y, 0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t mr = __builtin_amdgcn_make_buffer_rsrc((void*)(a.mask ? a.mask : a.y), 0, 0x7fffffff, 0x00020000);
+#pragma unroll
+  for (int ip = 0; ip < TP; ++ip) {
+    const int m = m0 + wp * WP + ip * 32 + (lane & 31);
+    if (m >= M) continue;
+    const unsigned ybase = glds_ybase(a, m);
+#pragma unroll
+    for (int ic = 0; ic < TC; ++ic)
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        glds_store4(a, yr, mr, m, ybase, c0 + wc * WC + ic * 32 + 8 * q + 4 * (lane >> 5), acc[ic][ip][4 * q],
+                    acc[ic][ip][4 * q + 1], acc[ic][ip][4 * q + 2], acc[ic][ip][4 * q + 3]);
+  }
+}
+
 template <int BC, int BP, int WC, int WP, int ST, int BK = 64>
 static int launch_glds(const IgemmArgs& a, hipStream_t st) {
   const int M = a.N * a.Ho * a.Wo;
@@ -398,6 +533,7 @@ static int launch_glds(const IgemmArgs& a, hipStream_t st) {
 //                3: 256 x 256, 2 stages (128 KB)            4: 128 x 128, 4 stages (128 KB)
 //                5: 256 x 256 x BK32, 4 stages (128 KB)     6: 128 x 256 x BK32, 5 stages (120 KB)
 //                8 / 9 / 10: cfg 3 / 2 / 1 as a persistent kernel (one workgroup per CU, pipelined across tiles)
+//                11: cfg 3 with 32x32x16 MFMAs (igemm_glds32_kernel)
 // Requires Cs % 64 == 0 (a K-step never straddles a tap), Kpad % 64 == 0, Ngemm % BC == 0.
 DPA_API int dpa_igemm_glds(const IgemmArgs* args, int cfg, hipStream_t st) {
   IgemmArgs a = *args;
@@ -430,6 +566,12 @@ DPA_API int dpa_igemm_glds(const IgemmArgs* args, int cfg, hipStream_t st) {
     case 8: if (a.Ngemm % 256) break; return launch_glds_pers<256, 256, 128, 64, 2>(a, st);
     case 9: if (a.Ngemm % 128) break; return launch_glds_pers<128, 256, 64, 64, 3>(a, st);
     case 10: if (a.Ngemm % 256) break; return launch_glds_pers<256, 128, 64, 64, 3>(a, st);
+    case 11: {
+      if (a.Ngemm % 256) break;
+      const int grid = ((a.N * a.Ho * a.Wo + 255) / 256) * (a.Ngemm / 256);
+      hipLaunchKernelGGL(igemm_glds32_kernel, dim3(grid), dim3(512), 0, st, a);
+      return (int)hipGetLastError();
+    }
     default: break;
   }
   return (int)hipErrorInvalidValue;
