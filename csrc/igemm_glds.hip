@@ -521,6 +521,199 @@ __global__ __launch_bounds__(512) void igemm_glds32_kernel(IgemmArgs a) {
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Ping-pong variant (cfg 7, opt-in): the same 256(ch) x 256(px) x 64 tile and 128 KB of LDS (two K-tile
+// buffers), but each K-tile is consumed in four phases, one 64x32 accumulator quadrant per wave per
+// phase (16 MFMAs), and the two halves of the workgroup (waves 0-3 / 4-7: one wave of each per SIMD)
+// run one barrier apart -- while one wave of a SIMD issues its quadrant's MFMAs the other reads the
+// next quadrant's fragments and issues its share of the LDS-DMA prefetch
+// (cdna_hip_programming.md "The 256^2 8-phase template", "Pipelining across barriers").
+// Half-tiles: A0/A1 = weight rows of quadrant qa of both channel-waves, B0/B1 = pixel rows of quadrant
+// qb of all four pixel-waves: 128 rows x 128 B each, two 1-KB DMA instructions per wave.
+// Phase p of K-tile s reads: p0 A0+B0 (12 ds_read_b128), p1 B1 (4), p2 A1 (8), p3 nothing, and issues
+// one half-tile: p0 -> B1(s+1), p1 -> A1(s+1), p2 -> A0(s+2), p3 -> B0(s+2).  WAR: every half-tile is
+// restaged >= 2 phases after its last read.  RAW: a half-tile read at phase q was issued at slot q-5
+// or earlier and each wave waits for it in phase q-1 before that phase's first barrier with
+// vmcnt(#DMAs issued in the 4 newest slots) = 8 in steady state.
+__device__ __forceinline__ void wait_vm_n(int n) {
+  if (n >= 8) wait_vm<8>();
+  else if (n >= 6) wait_vm<6>();
+  else if (n >= 4) wait_vm<4>();
+  else if (n >= 2) wait_vm<2>();
+  else wait_vm<0>();
+}
+
+__global__ __launch_bounds__(512) void igemm_pp_kernel(IgemmArgs a) {
+  constexpr int BC = 256, BP = 256, WC = 128, WP = 64, TC = 8, TP = 4, RBY = 128;
+  constexpr int STAGE = (BC + BP) * RBY;
+  __shared__ __attribute__((aligned(16))) char lds[2 * STAGE];
+
+  const int M = a.N * a.Ho * a.Wo;
+  const int nct = a.Ngemm / BC;
+  const int npt = (M + BP - 1) / BP;
+  const int bid = xcd_remap(blockIdx.x, npt * nct);
+  const int pt = bid / nct, ct = bid - pt * nct;
+  const int m0 = pt * BP, c0 = ct * BC;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wc = wid & 1, wp = wid >> 1, grp = wid >> 2;
+  const int lr = lane >> 3;
+  const int lchunk = (lane & 7) ^ lr;
+  unsigned woff[2][2], pbase[2][2], tmask[2][2];
+  const int taps = a.KH * a.KW;
+  const int hw = a.Ho * a.Wo;
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      woff[h][j] = (unsigned)(((c0 + j * 128 + h * 64 + wid * 8 + lr) * a.Kpad) * 2 + lchunk * 16);
+      const int m = m0 + (2 * j + grp) * 64 + h * 32 + (wid & 3) * 8 + lr;
+      const bool pok = m < M;
+      const int mm = pok ? m : 0;
+      const int pn = mm / hw;
+      const int rem = mm - pn * hw;
+      const int ph = rem / a.Wo, pw = rem - ph * a.Wo;
+      const int h0 = ph * a.stride - a.pad, w0 = pw * a.stride - a.pad;
+      unsigned msk = 0;
+      for (int t = 0; t < taps; ++t) {
+        const int kh = t / a.KW, kw = t - kh * a.KW;
+        const int ih = h0 + kh, iw = w0 + kw;
+        if (pok && ih >= 0 && ih < a.Hs && iw >= 0 && iw < a.Ws) msk |= 1u << t;
+      }
+      tmask[h][j] = msk;
+      pbase[h][j] = (unsigned)((((pn * a.Hs + h0) * a.Ws + w0) * a.ldx) * 2 + lchunk * 16);
+    }
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, 0, (int)a.xbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc((void*)a.w, 0, 0x7fffffff, 0x00020000);
+  const int S = a.Kpad / 64;
+  const bool slm = !(a.korder & 1) && a.Kpad == taps * a.Cs;
+  auto issueA = [&](int h, int t) {
+    char* base = lds + (t & 1) * STAGE;
+    int tap, ci;
+    ktile_coords(a, t, 64, taps, slm, tap, ci);
+    const unsigned wk = (unsigned)((tap * a.Cs + ci) * 2);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) dma16(wrs, base + (j * 128 + h * 64 + wid * 8) * RBY, woff[h][j] + wk);
+  };
+  auto issueB = [&](int h, int t) {
+    char* base = lds + (t & 1) * STAGE + BC * RBY;
+    int tap, ci;
+    ktile_coords(a, t, 64, taps, slm, tap, ci);
+    const int kh = tap / a.KW, kw = tap - kh * a.KW;
+    const unsigned delta = (unsigned)(((kh * a.Ws + kw) * a.ldx + ci) * 2);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const bool ok = tap < taps && ((tmask[h][j] >> tap) & 1u);
+      dma16(xr, base + ((2 * j + grp) * 64 + h * 32 + (wid & 3) * 8) * RBY, ok ? pbase[h][j] + delta : 0x80000000u);
+    }
+  };
+  const int X = 4 * S - 6;   // slot q issues iff q < X (its K-tile (q+2)/4 + 1 < S)
+
+  f32x4_t acc[TC][TP];
+#pragma unroll
+  for (int ic = 0; ic < TC; ++ic)
+#pragma unroll
+    for (int ip = 0; ip < TP; ++ip) acc[ic][ip] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  issueA(0, 0);
+  issueB(0, 0);
+  issueB(1, 0);
+  issueA(1, 0);
+  if (S > 1) {
+    issueA(0, 1);
+    issueB(0, 1);
+    wait_vm<8>();
+  } else {
+    wait_vm<4>();
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  if (grp) __builtin_amdgcn_s_barrier();       // the second half runs one barrier behind
+  __builtin_amdgcn_sched_barrier(0);
+
+  bf16x8_t af[4][2], bfr[2][2][2];
+  auto readA = [&](const char* Wt, int h) {
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int ic = 0; ic < 4; ++ic) {
+        const int row = wc * WC + h * 64 + ic * 16 + (lane & 15);
+        const int chunk = kk * 4 + (lane >> 4);
+        af[ic][kk] = *reinterpret_cast<const bf16x8_t*>(Wt + row * RBY + ((chunk ^ (row & 7)) << 4));
+      }
+  };
+  auto readB = [&](const char* P, int h) {
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int ip = 0; ip < 2; ++ip) {
+        const int row = wp * WP + h * 32 + ip * 16 + (lane & 15);
+        const int chunk = kk * 4 + (lane >> 4);
+        bfr[h][ip][kk] = *reinterpret_cast<const bf16x8_t*>(P + row * RBY + ((chunk ^ (row & 7)) << 4));
+      }
+  };
+  auto mfma_quad = [&](int qa, int qb) {
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int ic = 0; ic < 4; ++ic)
+#pragma unroll
+        for (int ip = 0; ip < 2; ++ip)
+          acc[qa * 4 + ic][qb * 2 + ip] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ic][kk], bfr[qb][ip][kk], acc[qa * 4 + ic][qb * 2 + ip], 0, 0, 0);
+  };
+  auto sync_in = [&]() {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+  };
+  auto sync_out = [&]() {
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  for (int s = 0; s < S; ++s) {
+    const char* Wt = lds + (s & 1) * STAGE;
+    const char* P = Wt + BC * RBY;
+    const int q0 = 4 * s;
+    const bool steady = s + 2 < S;
+    readB(P, 0);
+    readA(Wt, 0);
+    if (s + 1 < S) issueB(1, s + 1);
+    if (steady) wait_vm<8>();
+    else wait_vm_n(2 * min(max(X - (q0 - 3), 0), 4));
+    sync_in();
+    mfma_quad(0, 0);
+    sync_out();
+    readB(P, 1);
+    if (s + 1 < S) issueA(1, s + 1);
+    if (steady) wait_vm<8>();
+    else wait_vm_n(2 * min(max(X - (q0 - 2), 0), 4));
+    sync_in();
+    mfma_quad(0, 1);
+    sync_out();
+    readA(Wt, 1);
+    if (s + 2 < S) issueA(0, s + 2);
+    sync_in();
+    mfma_quad(1, 1);
+    sync_out();
+    if (s + 2 < S) issueB(0, s + 2);
+    if (s + 1 < S) {
+      if (steady) wait_vm<8>();
+      else wait_vm_n(2 * min(max(X - q0, 0), 4));
+    }
+    sync_in();
+    mfma_quad(1, 0);
+    sync_out();
+  }
+  if (!grp) __builtin_amdgcn_s_barrier();      // balance the second half's extra barrier
+
+  glds_epilogue<TC, TP, WC, WP>(a, acc, M, m0, c0, wc, wp, lane);
+}
+
 template <int BC, int BP, int WC, int WP, int ST, int BK = 64>
 static int launch_glds(const IgemmArgs& a, hipStream_t st) {
   const int M = a.N * a.Ho * a.Wo;
@@ -533,6 +726,7 @@ static int launch_glds(const IgemmArgs& a, hipStream_t st) {
 //                3: 256 x 256, 2 stages (128 KB)            4: 128 x 128, 4 stages (128 KB)
 //                5: 256 x 256 x BK32, 4 stages (128 KB)     6: 128 x 256 x BK32, 5 stages (120 KB)
 //                8 / 9 / 10: cfg 3 / 2 / 1 as a persistent kernel (one workgroup per CU, pipelined across tiles)
+//                7: cfg 3's tile in four MFMA phases per K-tile with the wave halves ping-ponged (igemm_pp_kernel)
 //                11: cfg 3 with 32x32x16 MFMAs (igemm_glds32_kernel)
 // Requires Cs % 64 == 0 (a K-step never straddles a tap), Kpad % 64 == 0, Ngemm % BC == 0.
 DPA_API int dpa_igemm_glds(const IgemmArgs* args, int cfg, hipStream_t st) {
@@ -566,6 +760,12 @@ DPA_API int dpa_igemm_glds(const IgemmArgs* args, int cfg, hipStream_t st) {
     case 8: if (a.Ngemm % 256) break; return launch_glds_pers<256, 256, 128, 64, 2>(a, st);
     case 9: if (a.Ngemm % 128) break; return launch_glds_pers<128, 256, 64, 64, 3>(a, st);
     case 10: if (a.Ngemm % 256) break; return launch_glds_pers<256, 128, 64, 64, 3>(a, st);
+    case 7: {
+      if (a.Ngemm % 256) break;
+      const int grid = ((a.N * a.Ho * a.Wo + 255) / 256) * (a.Ngemm / 256);
+      hipLaunchKernelGGL(igemm_pp_kernel, dim3(grid), dim3(512), 0, st, a);
+      return (int)hipGetLastError();
+    }
     case 11: {
       if (a.Ngemm % 256) break;
       const int grid = ((a.N * a.Ho * a.Wo + 255) / 256) * (a.Ngemm / 256);
