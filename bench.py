@@ -102,7 +102,8 @@ def main():
 
     from distributedpytorch_amd.config import TrainConfig
     from distributedpytorch_amd.data.synthetic import synthetic_batch
-    from distributedpytorch_amd.models.unet import build_model, count_params
+    from distributedpytorch_amd.models.summary import layer_table
+    from distributedpytorch_amd.models.unet import PRESETS, build_model, count_params
     from distributedpytorch_amd.trainer import DDPStrategy, PipelineDistStrategy, PipelineLocalStrategy, SingleDevice
     from distributedpytorch_amd.compute import resolve_backend
     from distributedpytorch_amd.utils import set_seed
@@ -203,6 +204,11 @@ def main():
         "final_loss": round(final_loss, 5) if final_loss == final_loss else None, "warmup_s": round(warm_s, 2),
         "peak_mem_gb": round(torch.cuda.max_memory_allocated(device) / 2 ** 30, 2),
     }
+    if not a.infer and a.model in PRESETS:
+        # achieved model FLOP rate: forward FLOPs (analytic layer table) x 3 for forward + dgrad + wgrad
+        fwd_gflop = sum(r[3] for r in layer_table(PRESETS[a.model], a.img, a.img))
+        out["model_gflop_per_image"] = round(3 * fwd_gflop, 2)
+        out["achieved_tflops"] = round(value * 3 * fwd_gflop / 1e3, 1)
     red = getattr(strat, "reducer", None)
     if red is not None and world > 1:  # rank 0's last step: all-reduce time not hidden behind backward
         c = red.exposed_comm_ms()

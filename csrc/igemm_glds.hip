@@ -20,6 +20,24 @@
 #include "conv_args.h"
 
 
+// Logical tile id -> (pixel tile, channel tile).  Consecutive ids run on one XCD (xcd_remap), so
+// ~32 consecutive ids share an L2: with many channel tiles, group them as 8 pixel tiles x (ids / 8)
+// channel tiles instead of one pixel tile x 32 channel tiles (the whole weight panel per K-step):
+// 12 distinct operand tiles per K-step instead of 33.  With 1-2 channel tiles (the UNet) the order is
+// the plain row-major one.
+__device__ __forceinline__ void glds_tile(int L, int npt, int nct, int& pt, int& ct) {
+  if (nct < 4) {
+    pt = L / nct;
+    ct = L - pt * nct;
+    return;
+  }
+  constexpr int GM = 8;
+  const int g = L / (GM * nct), r = L - g * GM * nct;
+  const int gm = min(GM, npt - g * GM);
+  pt = g * GM + r % gm;
+  ct = r / gm;
+}
+
 // K-tile s -> (tap, first channel).  Slice-major order (all taps of one 64-channel slice, then the next
 // slice) when the packed K has no padding: consecutive K-tiles then gather the SAME channel slice at
 // 9 neighbouring pixel offsets, so the pixel lines a K-tile fetches were mostly fetched by the previous
@@ -96,7 +114,7 @@ __device__ __forceinline__ void glds_epilogue(const IgemmArgs& a, f32x4_t (&acc)
   }
 }
 
-template <int BC, int BP, int WC, int WP, int ST, int BK>
+template <int BC, int BP, int WC, int WP, int ST, int BK, bool PRE = false>
 __global__ __launch_bounds__(512) void igemm_glds_kernel(IgemmArgs a) {
   constexpr int NWC = BC / WC, NWP = BP / WP;
   static_assert(NWC * NWP == 8, "8 waves");
@@ -114,7 +132,8 @@ __global__ __launch_bounds__(512) void igemm_glds_kernel(IgemmArgs a) {
   const int nct = a.Ngemm / BC;
   const int npt = (M + BP - 1) / BP;
   const int bid = xcd_remap(blockIdx.x, npt * nct);
-  const int pt = bid / nct, ct = bid - pt * nct;
+  int pt, ct;
+  glds_tile(bid, npt, nct, pt, ct);
   const int m0 = pt * BP, c0 = ct * BC;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wc = wid % NWC, wp = wid / NWC;
@@ -192,6 +211,33 @@ __global__ __launch_bounds__(512) void igemm_glds_kernel(IgemmArgs a) {
     __builtin_amdgcn_sched_barrier(0);
     const char* Wt = lds + (s % ST) * STAGE;
     const char* P = Wt + BC * RBY;
+    if constexpr (PRE) {
+      // every fragment of the K-step into registers first (96 VGPRs), then the MFMAs back to back:
+      // the compiler's default interleave issues two reads per eight MFMAs and waits lgkmcnt(0) on them
+      bf16x8_t af[BK / 32][TC], bfr[BK / 32][TP];
+#pragma unroll
+      for (int kk = 0; kk < BK / 32; ++kk) {
+        const int chunk = kk * 4 + (lane >> 4);
+#pragma unroll
+        for (int ip = 0; ip < TP; ++ip) {
+          const int row = wp * WP + ip * 16 + (lane & 15);
+          bfr[kk][ip] = *reinterpret_cast<const bf16x8_t*>(P + row * RBY + (swz_nk<BK>(row, chunk) << 4));
+        }
+#pragma unroll
+        for (int ic = 0; ic < TC; ++ic) {
+          const int row = wc * WC + ic * 16 + (lane & 15);
+          af[kk][ic] = *reinterpret_cast<const bf16x8_t*>(Wt + row * RBY + (swz_nk<BK>(row, chunk) << 4));
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int kk = 0; kk < BK / 32; ++kk)
+#pragma unroll
+        for (int ic = 0; ic < TC; ++ic)
+#pragma unroll
+          for (int ip = 0; ip < TP; ++ip)
+            acc[ic][ip] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kk][ic], bfr[kk][ip], acc[ic][ip], 0, 0, 0);
+    } else {
 #pragma unroll
     for (int kk = 0; kk < BK / 32; ++kk) {
       const int chunk = kk * 4 + (lane >> 4);
@@ -211,6 +257,7 @@ __global__ __launch_bounds__(512) void igemm_glds_kernel(IgemmArgs a) {
 #pragma unroll
         for (int ip = 0; ip < TP; ++ip)
           acc[ic][ip] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ic], bfr[ip], acc[ic][ip], 0, 0, 0);
+    }
     }
   }
 
@@ -259,7 +306,8 @@ __global__ __launch_bounds__(512) void igemm_glds_pers_kernel(IgemmArgs a) {
   // loader geometry of tile j of this workgroup's list
   auto geo = [&](int j, unsigned (&pb)[RP], unsigned (&tm)[RP], unsigned (&wo)[RA], int& m0, int& c0) {
     const int t = cstart + slot + j * G8;
-    const int pt = t / nct, ct = t - pt * nct;
+    int pt, ct;
+    glds_tile(t, (M + BP - 1) / BP, nct, pt, ct);
     m0 = pt * BP;
     c0 = ct * BC;
 #pragma unroll
@@ -341,6 +389,10 @@ __global__ __launch_bounds__(512) void igemm_glds_pers_kernel(IgemmArgs a) {
       __builtin_amdgcn_sched_barrier(0);
       const char* Wt = lds + (g % ST) * STAGE;
       const char* P = Wt + BC * RBY;
+      // all fragments first (see igemm_glds_kernel PRE) where the registers allow it: the 256x256 tile's
+      // 128 accumulators + 96 fragment registers + the persistent loop's state would spill
+      constexpr bool PRE = TC * TP * 4 + (TC + TP) * (BK / 32) * 4 <= 192;
+      if constexpr (!PRE) {
 #pragma unroll
       for (int kk = 0; kk < BK / 32; ++kk) {
         const int chunk = kk * 4 + (lane >> 4);
@@ -360,6 +412,31 @@ __global__ __launch_bounds__(512) void igemm_glds_pers_kernel(IgemmArgs a) {
 #pragma unroll
           for (int ip = 0; ip < TP; ++ip)
             acc[ic][ip] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ic], bfr[ip], acc[ic][ip], 0, 0, 0);
+      }
+      } else {
+      bf16x8_t af[BK / 32][TC], bfr[BK / 32][TP];
+#pragma unroll
+      for (int kk = 0; kk < BK / 32; ++kk) {
+        const int chunk = kk * 4 + (lane >> 4);
+#pragma unroll
+        for (int ip = 0; ip < TP; ++ip) {
+          const int row = wp * WP + ip * 16 + (lane & 15);
+          bfr[kk][ip] = *reinterpret_cast<const bf16x8_t*>(P + row * RBY + (swz_nk<BK>(row, chunk) << 4));
+        }
+#pragma unroll
+        for (int ic = 0; ic < TC; ++ic) {
+          const int row = wc * WC + ic * 16 + (lane & 15);
+          af[kk][ic] = *reinterpret_cast<const bf16x8_t*>(Wt + row * RBY + (swz_nk<BK>(row, chunk) << 4));
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int kk = 0; kk < BK / 32; ++kk)
+#pragma unroll
+        for (int ic = 0; ic < TC; ++ic)
+#pragma unroll
+          for (int ip = 0; ip < TP; ++ip)
+            acc[ic][ip] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kk][ic], bfr[kk][ip], acc[ic][ip], 0, 0, 0);
       }
     }
     glds_epilogue<TC, TP, WC, WP>(a, acc, M, m0, c0, wc, wp, lane);
@@ -412,7 +489,8 @@ __global__ __launch_bounds__(512) void igemm_glds32_kernel(IgemmArgs a) {
   const int nct = a.Ngemm / BC;
   const int npt = (M + BP - 1) / BP;
   const int bid = xcd_remap(blockIdx.x, npt * nct);
-  const int pt = bid / nct, ct = bid - pt * nct;
+  int pt, ct;
+  glds_tile(bid, npt, nct, pt, ct);
   const int m0 = pt * BP, c0 = ct * BC;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wc = wid % NWC, wp = wid / NWC;
@@ -552,7 +630,8 @@ __global__ __launch_bounds__(512) void igemm_pp_kernel(IgemmArgs a) {
   const int nct = a.Ngemm / BC;
   const int npt = (M + BP - 1) / BP;
   const int bid = xcd_remap(blockIdx.x, npt * nct);
-  const int pt = bid / nct, ct = bid - pt * nct;
+  int pt, ct;
+  glds_tile(bid, npt, nct, pt, ct);
   const int m0 = pt * BP, c0 = ct * BC;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -714,25 +793,28 @@ __global__ __launch_bounds__(512) void igemm_pp_kernel(IgemmArgs a) {
   glds_epilogue<TC, TP, WC, WP>(a, acc, M, m0, c0, wc, wp, lane);
 }
 
-template <int BC, int BP, int WC, int WP, int ST, int BK = 64>
+template <int BC, int BP, int WC, int WP, int ST, int BK = 64, bool PRE = false>
 static int launch_glds(const IgemmArgs& a, hipStream_t st) {
   const int M = a.N * a.Ho * a.Wo;
   const int grid = ((M + BP - 1) / BP) * (a.Ngemm / BC);
-  hipLaunchKernelGGL((igemm_glds_kernel<BC, BP, WC, WP, ST, BK>), dim3(grid), dim3(512), 0, st, a);
+  hipLaunchKernelGGL((igemm_glds_kernel<BC, BP, WC, WP, ST, BK, PRE>), dim3(grid), dim3(512), 0, st, a);
   return (int)hipGetLastError();
 }
 
-// cfg 0 = auto (+16: tap-major K order, +32: auto without the persistent kernel; for A/B).  1: 256(ch) x 128(px), 3 stages (144 KB)   2: 128 x 256, 3 stages
+// cfg 0 = auto (+16: tap-major K order, +32: auto without the persistent kernel, +64: cfg 3 / 2 without
+// the fragment preload; for A/B).  1: 256(ch) x 128(px), 3 stages (144 KB)   2: 128 x 256, 3 stages
 //                3: 256 x 256, 2 stages (128 KB)            4: 128 x 128, 4 stages (128 KB)
 //                5: 256 x 256 x BK32, 4 stages (128 KB)     6: 128 x 256 x BK32, 5 stages (120 KB)
 //                8 / 9 / 10: cfg 3 / 2 / 1 as a persistent kernel (one workgroup per CU, pipelined across tiles)
 //                7: cfg 3's tile in four MFMA phases per K-tile with the wave halves ping-ponged (igemm_pp_kernel)
 //                11: cfg 3 with 32x32x16 MFMAs (igemm_glds32_kernel)
+//                12 / 13: cfg 3 / 2 with the compiler's read/MFMA interleave instead of all fragments first (A/B)
 // Requires Cs % 64 == 0 (a K-step never straddles a tap), Kpad % 64 == 0, Ngemm % BC == 0.
 DPA_API int dpa_igemm_glds(const IgemmArgs* args, int cfg, hipStream_t st) {
   IgemmArgs a = *args;
   if (cfg & 16) a.korder |= 1;   // A/B: tap-major K-tile order
   if (cfg & 32) a.korder |= 2;   // A/B: no persistent kernel in the auto choice
+  const bool no_pre = cfg & 64;  // A/B: the compiler's read/MFMA interleave (cfg 12 / 13) for cfg 3 / 2
   cfg &= 15;
   if ((a.Cs & 63) || (a.Kpad & 63) || (a.ldx & 7) || (a.ldy & 3) || a.KH * a.KW > 32) return (int)hipErrorInvalidValue;
   if (a.mode == 1 && (a.Cout & 3)) return (int)hipErrorInvalidValue;
@@ -750,16 +832,19 @@ DPA_API int dpa_igemm_glds(const IgemmArgs* args, int cfg, hipStream_t st) {
     else if (a.Ngemm % 256 == 0 && grid_of(256, 128) >= 512) cfg = 1;
     else cfg = 4;
   }
+  if (no_pre && (cfg == 3 || cfg == 2)) cfg += 9 + (cfg == 2 ? 2 : 0);   // 3 -> 12, 2 -> 13
   switch (cfg) {
-    case 1: if (a.Ngemm % 256) break; return launch_glds<256, 128, 64, 64, 3>(a, st);
-    case 2: if (a.Ngemm % 128) break; return launch_glds<128, 256, 64, 64, 3>(a, st);
-    case 3: if (a.Ngemm % 256) break; return launch_glds<256, 256, 128, 64, 2>(a, st);
-    case 4: if (a.Ngemm % 128) break; return launch_glds<128, 128, 64, 32, 4>(a, st);
+    case 1: if (a.Ngemm % 256) break; return launch_glds<256, 128, 64, 64, 3, 64, true>(a, st);
+    case 2: if (a.Ngemm % 128) break; return launch_glds<128, 256, 64, 64, 3, 64, true>(a, st);
+    case 3: if (a.Ngemm % 256) break; return launch_glds<256, 256, 128, 64, 2, 64, true>(a, st);
+    case 4: if (a.Ngemm % 128) break; return launch_glds<128, 128, 64, 32, 4, 64, true>(a, st);
     case 5: if (a.Ngemm % 256) break; return launch_glds<256, 256, 128, 64, 4, 32>(a, st);
     case 6: if (a.Ngemm % 128) break; return launch_glds<128, 256, 64, 64, 5, 32>(a, st);
     case 8: if (a.Ngemm % 256) break; return launch_glds_pers<256, 256, 128, 64, 2>(a, st);
     case 9: if (a.Ngemm % 128) break; return launch_glds_pers<128, 256, 64, 64, 3>(a, st);
     case 10: if (a.Ngemm % 256) break; return launch_glds_pers<256, 128, 64, 64, 3>(a, st);
+    case 12: if (a.Ngemm % 256) break; return launch_glds<256, 256, 128, 64, 2>(a, st);
+    case 13: if (a.Ngemm % 128) break; return launch_glds<128, 256, 64, 64, 3>(a, st);
     case 7: {
       if (a.Ngemm % 256) break;
       const int grid = ((a.N * a.Ho * a.Wo + 255) / 256) * (a.Ngemm / 256);

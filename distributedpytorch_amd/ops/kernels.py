@@ -97,6 +97,8 @@ USE_GLDS = os.environ.get("DPA_NO_GLDS", "0") != "1"
 GLDS_TAP_MAJOR = os.environ.get("DPA_GLDS_TAP_MAJOR", "0") == "1"
 # A/B: no persistent LDS-DMA kernel for the short-K deep layers (csrc/igemm_glds.hip cfg 8)
 GLDS_NO_PERS = os.environ.get("DPA_GLDS_NO_PERS", "0") == "1"
+# A/B: LDS-DMA GEMM without the all-fragments-first K-step schedule
+GLDS_NO_PRELOAD = os.environ.get("DPA_GLDS_NO_PRELOAD", "0") == "1"
 # conv weight gradients on a side HIP stream, overlapping each block's dgrad chain (models/hip_unet.py)
 SIDE_WGRAD = os.environ.get("DPA_NO_SIDE_WGRAD", "0") != "1"
 # HIP stream priority of the weight-gradient side stream (torch convention: lower = higher priority,
@@ -259,7 +261,7 @@ def igemm(x: torch.Tensor, wpacked: torch.Tensor, y: torch.Tensor, *, Ngemm: int
             if path == "halo":
                 _check(err, "igemm_halo")
         if path == "glds" or (path == "auto" and glds_ok):
-            err = L.dpa_igemm_glds(ctypes.byref(a), c_int(variant if path == "glds" else 16 * GLDS_TAP_MAJOR + 32 * GLDS_NO_PERS), st)
+            err = L.dpa_igemm_glds(ctypes.byref(a), c_int(variant if path == "glds" else 16 * GLDS_TAP_MAJOR + 32 * GLDS_NO_PERS + 64 * GLDS_NO_PRELOAD), st)
             if err == 0:
                 continue
             if path == "glds":

@@ -128,7 +128,10 @@ def test_conv3x3_dgrad_masked(hip_lib, N, H, W, Cin, Cout, path):
     # 32x32x16 MFMA variant
     (2, 9, 13, 128, 256, 11), (1, 16, 16, 256, 512, 11), (3, 11, 7, 512, 256, 11),
     # ping-pong variant
-    (2, 9, 13, 128, 256, 7), (1, 16, 16, 256, 256, 7), (3, 11, 7, 512, 256, 7), (2, 5, 6, 256, 512, 7)])
+    (2, 9, 13, 128, 256, 7), (1, 16, 16, 256, 256, 7), (3, 11, 7, 512, 256, 7), (2, 5, 6, 256, 512, 7),
+    # >= 4 channel tiles: grouped tile order, full and partial groups of 8 pixel tiles
+    (1, 16, 16, 64, 1024, 3), (2, 40, 40, 64, 1024, 3), (2, 40, 40, 64, 1024, 8), (2, 40, 40, 256, 1024, 7),
+    (2, 9, 13, 128, 256, 12), (3, 11, 7, 512, 256, 12), (2, 9, 13, 64, 128, 13)])
 def test_conv3x3_glds(hip_lib, N, H, W, Cin, Cout, var):
     """LDS-DMA implicit GEMM (csrc/igemm_glds.hip): fwd with bias+ReLU and masked dgrad, every tile
     config, pixel counts that are not tile multiples (zero-filled DMA rows)."""
@@ -152,7 +155,7 @@ def test_conv3x3_glds(hip_lib, N, H, W, Cin, Cout, var):
     dref = xr.grad * (x > 0)
     packed, ng, kp = _pack_one(1, w)
     dx = torch.empty(N, H, W, Cin, dtype=torch.bfloat16, device="cuda")
-    v = var if (var % 16 not in (1, 3, 5, 7, 8, 10, 11) or Cin % 256 == 0) else (9 if var in (8, 10) else 2)
+    v = var if (var % 16 not in (1, 3, 5, 7, 8, 10, 11, 12) or Cin % 256 == 0) else (9 if var in (8, 10) else 2)
     K.igemm(_nhwc(g), packed, dx, Ngemm=ng, Kpad=kp, KH=3, KW=3, stride=1, pad=1, Cs=Cout, out_grid=(N, H, W),
             mask=_nhwc(x), path="glds", variant=v)
     torch.cuda.synchronize()
