@@ -824,10 +824,11 @@ DPA_API int dpa_igemm_glds(const IgemmArgs* args, int cfg, hipStream_t st) {
     // (XL bottleneck, 2 images: 2048 pixels x 2048 channels = 64 tiles of 256x256 for 256 CUs)
     const long M = (long)a.N * a.Ho * a.Wo;
     auto grid_of = [&](long bc, long bp) { return ((M + bp - 1) / bp) * (a.Ngemm / bc); };
-    // short K (<= 18 K-steps: the K = 1152 convs, the transposed convs): the persistent kernel, which
-    // hides each tile's first-load latency and epilogue behind the neighbouring tile, is 3-11 % faster
-    // there; at longer K it is 4-7 % slower (profiles/kbench_glds_pers_b256_r02.txt)
-    if (a.Ngemm % 256 == 0 && grid_of(256, 256) >= 512) cfg = (a.Kpad <= 18 * 64 && !(a.korder & 2)) ? 8 : 3;
+    // short K (<= 8 K-steps: the transposed convs' forward and up-path dgrads): the persistent kernel,
+    // which hides each tile's first-load latency and epilogue behind the neighbouring tile, is 3-9 %
+    // faster there; from K = 1024 on the fragment-preloaded cfg 3 wins by 3-6 %
+    // (profiles/kbench_glds_shortk_b256_r02.txt, interleaved)
+    if (a.Ngemm % 256 == 0 && grid_of(256, 256) >= 512) cfg = (a.Kpad <= 8 * 64 && !(a.korder & 2)) ? 8 : 3;
     else if (a.Ngemm % 128 == 0 && grid_of(128, 256) >= 512) cfg = 2;
     else if (a.Ngemm % 256 == 0 && grid_of(256, 128) >= 512) cfg = 1;
     else cfg = 4;
