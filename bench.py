@@ -29,6 +29,15 @@ BASELINE_METRIC = "images/sec (whole node) UNet 512x512 bf16 at 1/2/4/8 MI355X; 
 # (MIOpen kernel compilation + find) did not finish within 1080 s (profiles/stock_torch_b256_attempt_r02.log),
 # so vs_baseline compares against the batch-32 rate; the reference publishes no number.
 STOCK_BASELINE_PER_GPU = 909.62
+STOCK_BASELINE_BATCH = 32
+# this framework at the SAME per-GPU batch 32, same box and session as the stock run
+# (profiles/batch_sweep_r02.txt: 2383 img/s) -> the equal-batch ratio
+EQUAL_BATCH_RATIO_B32 = round(2383.24 / 909.62, 3)
+
+
+def _hw(s: str):
+    p = [int(v) for v in str(s).lower().split("x")]
+    return (p[0], p[0]) if len(p) == 1 else (p[0], p[1])
 
 
 def parse():
@@ -38,7 +47,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=256,
                     help="images per GPU per step (HBM: ~58 GB of 288 at 256; 128 -> ~29 GB, ~1%% lower img/s)")
-    ap.add_argument("--img", type=int, default=512)
+    ap.add_argument("--img", type=_hw, default=(512, 512),
+                    help="image size: S (square) or HxW, e.g. 640x960 (the reference's default, utils/train_utils.py:26)")
     ap.add_argument("--backend", choices=["hip", "torch", "auto"], default="auto")
     ap.add_argument("--model", default="unet")
     ap.add_argument("--bucket-mb", type=float, default=8.0)
@@ -111,7 +121,7 @@ def main():
     set_seed(1234)
     mp = a.parallelism == "mp"
     method = "MP" if mp else ("DDP" if world > 1 else "singleGPU")
-    cfg = TrainConfig(train_method=method, batch_size=a.batch, img_size=(a.img, a.img), dtype="bf16",
+    cfg = TrainConfig(train_method=method, batch_size=a.batch, img_size=a.img, dtype="bf16",
                       backend=a.backend, model=a.model, bucket_mb=a.bucket_mb, lr=1e-4,
                       grad_comm_dtype=a.grad_comm_dtype,
                       microbatches=a.microbatches, stages=a.stages, mp_cut=a.mp_cut)
@@ -127,7 +137,7 @@ def main():
 
     pool = []
     for i in range(a.pool):
-        img, mask = synthetic_batch(a.batch, a.img, a.img, 3, seed=1000 * rank + i, device=device)
+        img, mask = synthetic_batch(a.batch, a.img[0], a.img[1], 3, seed=1000 * rank + i, device=device)
         pool.append((img, mask.float().unsqueeze(1)))
 
     graphed = None
@@ -191,12 +201,19 @@ def main():
     out = {
         "metric": BASELINE_METRIC if not a.infer else "images/sec inference UNet 512x512 bf16 (eval forward)", "value": round(value, 2), "unit": "images/s", "n_gpus": world,
         "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
-        "scaling": "strong" if mp else "weak", "vs_baseline": vs, "dtype": "bf16",
+        "scaling": "strong" if mp else "weak", "vs_baseline": vs,
+        # vs_baseline divides by stock PyTorch-ROCm at per-GPU batch 32 (its best measured rate; at
+        # batch 256 its MIOpen tuning does not finish in 1080 s); equal batch only when --batch 32
+        "vs_baseline_basis": {"stock_per_gpu_img_s": STOCK_BASELINE_PER_GPU, "stock_per_gpu_batch": STOCK_BASELINE_BATCH,
+                              "this_per_gpu_batch": a.batch if not mp else a.batch // max(1, world),
+                              "equal_batch": (a.batch == STOCK_BASELINE_BATCH and not mp),
+                              "equal_batch_ratio_b32": EQUAL_BATCH_RATIO_B32},
+        "dtype": "bf16",
         "data": "synthetic (GPU-generated images + ellipse masks), random-init weights",
         "config": {"model": f"{a.model} (reference 4-level UNet, base 32, {nparams} params)" if a.model == "unet"
                    else a.model, "global_batch": a.batch * (1 if mp else world),
                    "per_gpu_batch": a.batch if not mp else a.batch // max(1, world),
-                   "seq_len": a.img * a.img, "image_hw": [a.img, a.img],
+                   "seq_len": a.img[0] * a.img[1], "image_hw": list(a.img),
                    "parallelism": par, "backend": backend,
                    "mp_cut": (strat.pipe.cuts if mp else None), "bucket_mb": a.bucket_mb,
                    "grad_comm_dtype": a.grad_comm_dtype,
@@ -206,7 +223,7 @@ def main():
     }
     if not a.infer and a.model in PRESETS:
         # achieved model FLOP rate: forward FLOPs (analytic layer table) x 3 for forward + dgrad + wgrad
-        fwd_gflop = sum(r[3] for r in layer_table(PRESETS[a.model], a.img, a.img))
+        fwd_gflop = sum(r[3] for r in layer_table(PRESETS[a.model], a.img[0], a.img[1]))
         out["model_gflop_per_image"] = round(3 * fwd_gflop, 2)
         out["achieved_tflops"] = round(value * 3 * fwd_gflop / 1e3, 1)
     red = getattr(strat, "reducer", None)

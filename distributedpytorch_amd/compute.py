@@ -59,16 +59,28 @@ class Compute:
         return run_segment(self.blocks, 0, n_blocks(self.depth), self.depth, {"x": x}, want="probs")["probs"]
 
 
-def resolve_backend(backend: str, device) -> str:
+def resolve_backend(backend: str, device, dtype: str = "bf16") -> str:
+    """``auto`` -> the HIP engine on a GPU for bf16 compute; stock ops on CPU and for fp32 (the
+    reference's precision, utils/train_utils.py:60-61: the HIP kernels store bf16 activations, so an
+    fp32 run -- e.g. a parity run -- goes to the torch backend, which computes in fp32 on the GPU)."""
     device = torch.device(device)
     if backend == "auto":
-        return "hip" if device.type == "cuda" else "torch"
+        if device.type != "cuda":
+            return "torch"
+        if dtype != "bf16":
+            import logging
+            logging.getLogger(__name__).info(
+                "dtype=%s: the HIP engine computes in bf16; using the torch backend (fp32 on %s)", dtype, device)
+            return "torch"
+        return "hip"
+    if backend == "hip" and dtype != "bf16":
+        raise ValueError(f"--backend hip computes in bf16 (fp32 accumulate); --dtype {dtype} needs --backend torch/auto")
     return backend
 
 
 def make_blocks(model, backend: str = "auto", dtype: str = "bf16", device=None, owned=None):
     dev = torch.device(device) if device is not None else next(model.parameters()).device
-    backend = resolve_backend(backend, dev)
+    backend = resolve_backend(backend, dev, dtype)
     if backend == "hip":
         from .models.hip_unet import HipBlocks
         return HipBlocks(model, dtype=dtype, device=dev, owned=owned)

@@ -9,8 +9,10 @@ rendered ONCE on the device and every step only gathers its batch there:
   ellipse masks, colours and shading as :class:`.synthetic.SyntheticSegmentation` item ``i`` (their
   parameters come from the same per-item CPU generator, drawn in the same order); only the +/-0.05
   pixel noise differs (a counter-based integer hash of (seed, i, c, y, x) evaluated on the device
-  instead of the CPU generator's stream).  Images stay float32 ``[3,H,W]`` in [0,1] (reference item
-  format, ``dataloading.py:70-73``), masks ``uint8``.
+  instead of the CPU generator's stream).  Images are STORED as uint8 (k/255: what a decoded JPEG
+  divided by 255 is, reference ``dataloading.py:40``) -- 4x less HBM than float32, so the 5,088-image
+  set is 4 GB at 512x512 and ranks sharing a device in a rehearsal stay small -- and served as float32
+  ``[3,H,W]`` in [0,1] (reference item format, ``dataloading.py:70-73``); masks ``uint8``.
 * :class:`DeviceLoader` - batches of indices from any sampler (the epoch-seeded shuffle or
   ``DistributedSampler``; ``random_split`` subsets are resolved to base indices), gathered with one
   ``index_select`` each into ``(images float32[B,3,H,W], targets float32[B,1,H,W])``.
@@ -83,22 +85,30 @@ class DeviceSyntheticSegmentation(Dataset):
         self.h, self.w = int(size[0]), int(size[1])
         self.channels, self.seed = channels, seed
         self.device = torch.device(device)
-        self.images = torch.empty(self.length, channels, self.h, self.w, dtype=torch.float32, device=self.device)
+        import logging
+        logging.getLogger(__name__).info(
+            "rendering %d synthetic %dx%d images into %s: %.2f GiB (uint8 images + masks)", self.length, self.h,
+            self.w, self.device, self.length * (channels + 1) * self.h * self.w / 2 ** 30)
+        self.images = torch.empty(self.length, channels, self.h, self.w, dtype=torch.uint8, device=self.device)
         self.masks = torch.empty(self.length, self.h, self.w, dtype=torch.uint8, device=self.device)
         for s in range(0, self.length, chunk):
             e = min(self.length, s + chunk)
-            self.images[s:e], self.masks[s:e] = render_items(seed, range(s, e), self.h, self.w, channels,
-                                                             self.device)
+            img, self.masks[s:e] = render_items(seed, range(s, e), self.h, self.w, channels, self.device)
+            self.images[s:e] = img.mul_(255.0).round_().to(torch.uint8)
 
     @property
     def nbytes(self) -> int:
-        return self.images.numel() * 4 + self.masks.numel()
+        return self.images.numel() + self.masks.numel()
 
     def __len__(self):
         return self.length
 
+    @staticmethod
+    def to_float(img_u8: torch.Tensor) -> torch.Tensor:
+        return img_u8.to(torch.float32).mul_(1.0 / 255.0)
+
     def __getitem__(self, idx):
-        return {"image": self.images[idx], "mask": self.masks[idx].long()}
+        return {"image": self.to_float(self.images[idx]), "mask": self.masks[idx].long()}
 
 
 def _base(ds):
@@ -131,7 +141,7 @@ class DeviceLoader:
             i = torch.as_tensor(b, dtype=torch.int64).to(dev, non_blocking=True)
             if self.index_map is not None:
                 i = self.index_map.index_select(0, i)
-            img = self.base.images.index_select(0, i)
+            img = self.base.to_float(self.base.images.index_select(0, i))
             tgt = self.base.masks.index_select(0, i).to(torch.float32).unsqueeze(1)
             yield img, tgt
 

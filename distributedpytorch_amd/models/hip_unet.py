@@ -702,7 +702,17 @@ class _DecFn(torch.autograd.Function):
                                                              _grad(seg.weight).view(-1), _grad(seg.bias))), None
             B.ready([seg])
         else:
-            g2 = B.bn_bwd(c2, _v(g2), st2)
+            g2 = _v(g2)
+            if pend is not None:
+                # the head's deferred gradient reached us in another form (summed with another
+                # gradient, or materialised by a hook): form it now and add it, never drop it
+                B._head_pending = None
+                ph, y, t, dS = pend
+                seg = B.model.segmap
+                gy = K.head_bwd(y, seg.weight, seg.bias, t, dS, _grad(seg.weight).view(-1), _grad(seg.bias))
+                B.ready([seg])
+                g2 = (gy.float() + g2.float()).to(torch.bfloat16).contiguous()
+            g2 = B.bn_bwd(c2, g2, st2)
             W = g2.shape[2]
             if B.fusable(c2, c1, W):
                 g1, st_g = B.conv_bwd(c2, g2, a, mask=True), None

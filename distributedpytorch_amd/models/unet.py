@@ -64,6 +64,8 @@ PRESETS = {
     # tiny configs for fast CPU tests
     "unet-tiny": UNetConfig(base=8, depth=2),
     "unet-tiny-bn": UNetConfig(base=8, depth=2, batchnorm=True, bilinear=True),
+    # reference depth at a tiny width: up to 10 pipeline stages in CPU tests
+    "unet-tiny4": UNetConfig(base=8, depth=4),
 }
 
 

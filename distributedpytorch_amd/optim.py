@@ -196,6 +196,18 @@ class FusedAdam(torch.optim.Optimizer):
                 "param_groups": [{k: v for k, v in g.items() if k != "params"} for g in self.param_groups]}
 
     def load_state_dict(self, sd):
+        # the moments are flat buffers matched by position: refuse a state whose parameter layout
+        # differs (another --mp-cut / --stages, another model) instead of loading foreign moments
+        mine = [list(s.names) for s in self.spaces]
+        saved = sd.get("names")
+        if saved is not None and [list(n) for n in saved] != mine:
+            def brief(nn):
+                return [f"{len(n)} params ({n[0]} .. {n[-1]})" if n else "0 params" for n in nn]
+            raise ValueError(f"optimizer state was saved for a different parameter layout: saved {brief(saved)}, "
+                             f"this run {brief(mine)} (same --mp-cut/--stages/model needed to resume)")
+        if len(sd["exp_avg"]) != len(self.exp_avg) or any(
+                tuple(a.shape) != tuple(b.shape) for a, b in zip(self.exp_avg, sd["exp_avg"])):
+            raise ValueError("optimizer state buffers do not match this run's flat parameter spaces")
         self.step_count = int(sd["step"])
         for m, src in zip(self.exp_avg, sd["exp_avg"]):
             m.copy_(src)

@@ -88,19 +88,33 @@ class BucketedAllReduce:
         self._hooks = []
 
     def reset(self):
+        if getattr(self, "launch_log", None):
+            self.last_launch_log = self.launch_log
         self.pending = list(self.expected)
+        self.seen = [False] * len(self.bucket_of)
+        self.n_ready = 0
         self.next_launch = 0
         self.works = []
         self._writeback = []
+        # per launched bucket: (bucket, readiness announcements received so far, launched by finish())
+        # -- the overlap evidence the tests check: every bucket but the last launches during backward
+        self.launch_log = []
 
     def mark_ready(self, param_index: int):
+        # a parameter announced twice in one step (an autograd hook AND notify_ready, or a double
+        # notify) would otherwise drive its bucket's count below zero and stall it until finish()
+        assert not self.seen[param_index], \
+            f"gradient of parameter {param_index} ({self.space.names[param_index]}) announced twice in one step"
+        self.seen[param_index] = True
+        self.n_ready += 1
         b = self.bucket_of[param_index]
         self.pending[b] -= 1
         while self.next_launch < len(self.buckets) and self.pending[self.next_launch] == 0:
             self._launch(self.next_launch)
             self.next_launch += 1
 
-    def _launch(self, b: int):
+    def _launch(self, b: int, in_finish: bool = False):
+        self.launch_log.append((b, self.n_ready, in_finish))
         with trace_range(f"allreduce_bucket{b}"):
             self._launch_bucket(b)
 
@@ -125,7 +139,7 @@ class BucketedAllReduce:
     def finish(self):
         """Launch any bucket whose grads never arrived (unused params) and wait for all collectives."""
         while self.next_launch < len(self.buckets):
-            self._launch(self.next_launch)
+            self._launch(self.next_launch, in_finish=True)
             self.next_launch += 1
         timed = self.space.grad.is_cuda and bool(self.works)
         if timed:
@@ -154,7 +168,7 @@ class BucketedAllReduce:
     def all_reduce_now(self):
         """No-hook path: reduce the whole flat buffer bucket by bucket (used after a fused backward)."""
         for b in range(len(self.buckets)):
-            self._launch(b)
+            self._launch(b, in_finish=True)
         self.next_launch = len(self.buckets)
         self.finish()
 

@@ -154,9 +154,17 @@ class DPBucketReducer:
     for their device's compute stream; :meth:`finish` makes every compute stream wait for its comm
     stream and records the exposed (un-overlapped) wait on device 0."""
 
-    def __init__(self, spaces, devices, comm=None, bucket_mb: float = 8.0, first_bucket_mb: float = 1.0):
+    def __init__(self, spaces, devices, comm=None, bucket_mb: float = 8.0, first_bucket_mb: float = 1.0,
+                 overlap: bool = None):
         self.spaces, self.devices, self.comm = list(spaces), list(devices), comm
-        self.buckets, self.bucket_of = bucket_plan(self.spaces[0], bucket_mb, first_bucket_mb)
+        # DPA_DP_OVERLAP=0: opt-out to ONE reduction of the whole gradient buffer after the backward
+        # (no bucket launches from the autograd device threads)
+        self.overlap = os.environ.get("DPA_DP_OVERLAP", "1") == "1" if overlap is None else overlap
+        if self.overlap:
+            self.buckets, self.bucket_of = bucket_plan(self.spaces[0], bucket_mb, first_bucket_mb)
+        else:
+            n = len(self.spaces[0].numels)
+            self.buckets, self.bucket_of = [(0, self.spaces[0].offsets[-1], 0, n)], [0] * n
         for sp in self.spaces[1:]:
             assert sp.offsets == self.spaces[0].offsets, "replicas must share one flat layout"
         self.expected = [(b[3] - b[2]) * len(self.spaces) for b in self.buckets]
@@ -165,23 +173,34 @@ class DPBucketReducer:
         self._exposed = None
         self._hooks = []
         for k, sp in enumerate(self.spaces):
-            sp.add_ready_listener(lambda i, k=k: self.mark_ready(i))
+            sp.add_ready_listener(lambda i, k=k: self.mark_ready(i, k))
             for i, p in enumerate(sp.params):       # torch-op backend: autograd accumulation hooks
-                self._hooks.append(p.register_post_accumulate_grad_hook(lambda _p, i=i: self.mark_ready(i)))
+                self._hooks.append(p.register_post_accumulate_grad_hook(lambda _p, i=i, k=k: self.mark_ready(i, k)))
         self.reset()
 
     def reset(self):
+        if getattr(self, "launch_log", None):
+            self.last_launch_log = self.launch_log
         self.pending = list(self.expected)
+        self.seen = [[False] * len(self.bucket_of) for _ in self.spaces]
+        self.n_ready = 0
         self.next_launch = 0
+        self.launch_log = []     # (bucket, announcements so far, launched by finish())
 
-    def mark_ready(self, param_index: int):
+    def mark_ready(self, param_index: int, replica: int = 0):
         with self.lock:
+            assert not self.seen[replica][param_index], \
+                f"replica {replica}: gradient of parameter {param_index} announced twice in one step"
+            self.seen[replica][param_index] = True
+            self.n_ready += 1
             self.pending[self.bucket_of[param_index]] -= 1
-            while self.next_launch < len(self.buckets) and self.pending[self.next_launch] <= 0:
+            while (self.overlap and self.next_launch < len(self.buckets)
+                   and self.pending[self.next_launch] == 0):
                 self._launch(self.next_launch)
                 self.next_launch += 1
 
-    def _launch(self, b: int):
+    def _launch(self, b: int, in_finish: bool = False):
+        self.launch_log.append((b, self.n_ready, in_finish))
         s, e = self.buckets[b][:2]
         grads = [sp.grad[s:e] for sp in self.spaces]
         with trace_range(f"dp_allreduce_bucket{b}"):
@@ -199,7 +218,7 @@ class DPBucketReducer:
     def finish(self):
         with self.lock:
             while self.next_launch < len(self.buckets):
-                self._launch(self.next_launch)
+                self._launch(self.next_launch, in_finish=True)
                 self.next_launch += 1
             if self.streams is not None:
                 cur0 = torch.cuda.current_stream(self.devices[0])

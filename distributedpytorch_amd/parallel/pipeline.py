@@ -104,6 +104,13 @@ def stage_io(cuts: Sequence[int], depth: int):
     return recv, send
 
 
+def sender_groups(recv_spec, send_spec) -> List[List[int]]:
+    """Members of each stage's sender communicator: the stage, the stages it sends activations to
+    (forward) and the stages it sends gradients to (backward: its producers), sorted."""
+    S = len(send_spec)
+    return [sorted({s} | {d for _, d in send_spec[s]} | {p for _, p in recv_spec[s]}) for s in range(S)]
+
+
 def infer_shapes(cfg, microbatch: int, h: int, w: int) -> Dict[str, tuple]:
     """Shapes (NCHW) of every boundary tensor for one microbatch, by arithmetic (no tracing)."""
     shapes = {}
@@ -126,13 +133,19 @@ class GPipeDist:
     """Multi-process GPipe over a process group whose size == number of stages.
 
     Communication (RCCL over xGMI, or gloo on CPU):
-    * every tensor of one microbatch that goes to / comes from the same step is posted as ONE
-      ``batch_isend_irecv`` group (RCCL group call: the x and skip transfers to different peers
-      start together instead of one ``isend`` at a time);
+    * one communicator PER SENDING STAGE (:func:`sender_groups`): stage s sends only on its own
+      group G[s] = {s} + its consumers + its producers, and receives from p only on G[p].  torch
+      puts every coalesced P2P op of a group on that group's single RCCL stream in issue order, so
+      with one shared group a pre-posted receive would hold back the same rank's later send (a
+      middle stage could not hand microbatch m downstream before m+1 arrived from upstream); with
+      sender groups no rank ever both sends and receives on one group, so sends never queue behind
+      its own receives (checked op by op in ``tests/test_pipeline_p2p_order.py``);
+    * the tensors of one microbatch that go to the same group are posted as ONE
+      ``batch_isend_irecv`` group (RCCL group call: the x and skip transfers start together);
     * forward receives for microbatch m+1 and backward gradient receives for microbatch m-1 are
       posted before microbatch m computes, so transfer latency hides behind compute;
-    * every peer communicator is created at construction (a 1-element exchange with each peer),
-      so the lazy RCCL pair-communicator setup never lands inside a training step;
+    * every group's communicator is created at construction (a 1-element exchange from its sender
+      to every member), so the lazy RCCL communicator setup never lands inside a training step;
     * a skip that leaves this stage is written by the encoder conv into a dense tensor (HIP engine
       ``dense_skips``) and sent as is; activations travel in the compute dtype (bf16).
     """
@@ -168,24 +181,47 @@ class GPipeDist:
         self._glob = lambda s: dist.get_global_rank(group, s) if group is not None else s
         self._host_staged = self.device.type == "cuda" and dist.get_backend(group) != "nccl"
         self.peers = sorted({p for _, p in self.recv_spec[self.rank]} | {p for _, p in self.send_spec[self.rank]})
+        # per-sender communicators: stage s sends only on groups[s], receives from p only on groups[p]
+        self.members = sender_groups(self.recv_spec, self.send_spec)
+        self.groups: Dict[int, object] = {}
+        world_pipeline = group is None or dist.get_world_size(group) == dist.get_world_size()
+        for s in range(self.S):
+            ranks = [self._glob(r) for r in self.members[s]]
+            if len(ranks) < 2:
+                continue
+            if world_pipeline:      # every rank of the job calls new_group, members or not
+                g = dist.new_group(ranks)
+            elif self.rank in self.members[s]:   # pipeline inside a bigger job: members only, in order
+                g = dist.new_group(ranks, use_local_synchronization=True)
+            else:
+                continue
+            if self.rank in self.members[s]:
+                self.groups[s] = g
+        self.op_log: Optional[list] = None   # tests: [(sender group, "send"/"recv", peer stage)] per posted op
         if warm:
             self.warm_up()
 
     def warm_up(self):
-        """One tiny exchange with every peer stage (both directions): creates the RCCL pair
-        communicators now instead of inside the first timed step."""
-        ops, keep = [], []
+        """One tiny exchange on every group this stage belongs to (its sender to each member), in
+        stage order on every rank: creates the RCCL communicators now instead of inside the first
+        timed step, and every group's first operation involves all of its members."""
         dev = "cpu" if self._host_staged else self.device
-        for p in self.peers:
-            out = torch.full((1,), float(self.rank), dtype=self.comm_dtype, device=dev)
-            inp = torch.empty(1, dtype=self.comm_dtype, device=dev)
-            ops.append(dist.P2POp(dist.isend, out, self._glob(p), self.group))
-            ops.append(dist.P2POp(dist.irecv, inp, self._glob(p), self.group))
-            keep.append((p, inp, out))
-        for w in (dist.batch_isend_irecv(ops) if ops else []):
-            w.wait()
-        for p, inp, _ in keep:
-            assert int(inp.float().item()) == p, f"stage {self.rank}: peer {p} answered {inp.item()}"
+        for s in sorted(self.groups):
+            g = self.groups[s]
+            others = [r for r in self.members[s] if r != s]
+            ops, keep = [], []
+            if s == self.rank:
+                out = torch.full((1,), float(self.rank), dtype=self.comm_dtype, device=dev)
+                keep.append(out)
+                ops = [dist.P2POp(dist.isend, out, self._glob(r), g) for r in others]
+            else:
+                inp = torch.empty(1, dtype=self.comm_dtype, device=dev)
+                keep.append(inp)
+                ops = [dist.P2POp(dist.irecv, inp, self._glob(s), g)]
+            for w in dist.batch_isend_irecv(ops):
+                w.wait()
+            if s != self.rank:
+                assert int(keep[0].float().item()) == s, f"stage {self.rank}: sender {s} answered {keep[0].item()}"
 
     # shapes of the boundary tensors for this microbatch size
     def _shape(self, name, mb, h, w):
@@ -234,20 +270,30 @@ class GPipeDist:
         stream).  gloo (CPU tests; the one-GPU rehearsal of this path, ranks sharing cuda:0) is
         host-staged explicitly: a device buffer is copied to host memory before the send and from
         it after the receive completes."""
-        ops, keep, copies = [], [], []
-        for t, dst in sends:
+        by_group: Dict[int, list] = {}
+        keep, copies = [], []
+        for t, dst in sends:                      # all on this stage's own sender group
             buf = self._wire(t)
             if self._host_staged:
                 buf = buf.to("cpu")                   # synchronous: the producing kernels have finished
             keep.append(buf)
-            ops.append(dist.P2POp(dist.isend, buf, self._glob(dst), self.group))
-        for flat, src in recvs:
+            by_group.setdefault(self.rank, []).append(dist.P2POp(dist.isend, buf, self._glob(dst), self.groups[self.rank]))
+            self._log(self.rank, "send", dst)
+        for flat, src in recvs:                   # on the SENDER's group
             if self._host_staged:
                 host = torch.empty(flat.shape, dtype=flat.dtype)
                 copies.append((host, flat))
                 flat = host
-            ops.append(dist.P2POp(dist.irecv, flat, self._glob(src), self.group))
-        return _Transfer(dist.batch_isend_irecv(ops) if ops else [], keep, copies)
+            by_group.setdefault(src, []).append(dist.P2POp(dist.irecv, flat, self._glob(src), self.groups[src]))
+            self._log(src, "recv", src)
+        works = []
+        for g in sorted(by_group):
+            works.extend(dist.batch_isend_irecv(by_group[g]))
+        return _Transfer(works, keep, copies)
+
+    def _log(self, group_sender: int, kind: str, peer: int):
+        if self.op_log is not None:
+            self.op_log.append((group_sender, kind, peer))
 
     def _irecv(self, mb, h, w):
         bufs, recvs = {}, []

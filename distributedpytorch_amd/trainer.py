@@ -308,6 +308,9 @@ class PipelineDistStrategy(Strategy):
         return {"stages": out} if self.rank == 0 else None
 
     def load_optimizer_state_dict(self, sd):
+        if "stages" in sd and len(sd["stages"]) != self.world:
+            raise ValueError(f"checkpoint holds optimizer state for {len(sd['stages'])} pipeline stages, "
+                             f"this run has {self.world}")
         self.optimizer.load_state_dict(sd["stages"][self.rank] if "stages" in sd else sd)
 
     def barrier(self):
@@ -410,7 +413,7 @@ def train(cfg: TrainConfig):
     if cfg.load:
         load_model_state(model, cfg.load)
     strat = build_strategy(cfg, model)
-    log.info(f"strategy={strat.name} backend={resolve_backend(cfg.backend, strat.device)} device={strat.device}")
+    log.info(f"strategy={strat.name} backend={resolve_backend(cfg.backend, strat.device, cfg.dtype)} device={strat.device}")
 
     train_set, val_set = build_datasets(cfg, strat.device)
     dp_ranks = world if strat.name == "DDP" else 1

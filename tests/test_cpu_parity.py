@@ -265,6 +265,7 @@ def test_dp_buckets_launch_during_backward():
     (st.dp.forward_loss(x, t) * 4).backward()
     launched = red.next_launch
     assert launched >= len(red.buckets) - 1, (launched, len(red.buckets))
+    assert not any(fin for _, _, fin in red.launch_log), red.launch_log
     st.dp.all_reduce_grads()
     assert red.next_launch == 0          # reset for the next step
     ref = _ref_grads(b, x, t)
@@ -290,3 +291,40 @@ def test_unet_pipe_constructor_matches_plain():
     pb.sum().backward()
     for (n, p), q in zip(a.named_parameters(), b.parameters()):
         torch.testing.assert_close(p.grad, q.grad, rtol=1e-4, atol=1e-5, msg=n)
+
+
+def test_reducers_reject_double_announcement():
+    """A gradient announced twice in one step (autograd hook AND notify_ready) is an error, not a
+    silently stalled bucket (both reducers)."""
+    import pytest
+    from distributedpytorch_amd.optim import FlatParameterSpace
+    from distributedpytorch_amd.parallel.dp import DPBucketReducer
+    m = build_model("unet-tiny")
+    sp = FlatParameterSpace(m)
+    red = DPBucketReducer([sp], ["cpu"], None, bucket_mb=0.002)
+    red.mark_ready(0)
+    with pytest.raises(AssertionError, match="announced twice"):
+        red.mark_ready(0)
+
+
+def test_dp_single_reduction_opt_out(monkeypatch):
+    """DPA_DP_OVERLAP=0: one reduction of the whole buffer at the end of the backward, same result."""
+    from distributedpytorch_amd.config import TrainConfig
+    from distributedpytorch_amd.trainer import DPStrategy
+    monkeypatch.setenv("DPA_DP_OVERLAP", "0")
+    torch.manual_seed(3)
+    a, b = build_model("unet-tiny"), build_model("unet-tiny")
+    b.load_state_dict(a.state_dict())
+    x = torch.rand(4, 3, 32, 32)
+    t = (torch.rand(4, 1, 32, 32) > 0.5).float()
+    st = DPStrategy(TrainConfig(backend="torch", lr=1e-3, dtype="fp32", bucket_mb=0.002), a, ["cpu", "cpu"])
+    red = st.dp.reducer
+    assert len(red.buckets) == 1
+    st.optimizer.zero_grad()
+    (st.dp.forward_loss(x, t) * 4).backward()
+    assert red.next_launch == 0 and red.launch_log == []
+    st.dp.all_reduce_grads()
+    assert red.last_launch_log == [(0, 2 * len(st.dp.spaces[0].names), True)]
+    ref = _ref_grads(b, x, t)
+    for n, p in st.model.named_parameters():
+        assert torch.allclose(p.grad, ref[n], atol=1e-6), n

@@ -83,9 +83,17 @@ def _ddp_worker(rank, world, port, comm, q):
         expect = torch.stack(_gather_cpu(sd.space.grad, world)).mean(0)
         st.optimizer.zero_grad()
         (st.forward_loss(x, t) * 4).backward()
+        # overlap, not just numerics: every bucket but the last was launched by a readiness
+        # announcement DURING the backward, in index order, before finish() (torch DDP's overlapped
+        # bucket all-reduce, reference utils/train_utils.py:196,224)
+        log = list(st.reducer.launch_log)
         st.reducer.finish()
-        got = st.space.grad.detach().cpu()
         nb = len(st.reducer.buckets)
+        assert nb >= 3, nb
+        assert [b for b, _, _ in log] == list(range(len(log))), log
+        assert len(log) >= nb - 1 and not any(fin for _, _, fin in log), log
+        assert log[0][1] < len(st.space.names), log          # the first bucket left long before the last gradient
+        got = st.space.grad.detach().cpu()
         if comm == "fp32":
             ok = torch.allclose(got, expect, rtol=1e-6, atol=1e-9 * float(expect.abs().max()))
         else:

@@ -75,10 +75,17 @@ def test_dp_hip_matches_single(hip_lib):
     b.load_state_dict(a.state_dict())
     x, t = _batch()
     l_ref, g_ref = _single(b.cuda(), x, t)
-    st = DPStrategy(TrainConfig(backend="hip", lr=1e-3), a, ["cuda:0", "cuda:0"])
+    st = DPStrategy(TrainConfig(backend="hip", lr=1e-3, bucket_mb=1.0), a, ["cuda:0", "cuda:0"])
     st.optimizer.zero_grad()
     loss = st.dp.forward_loss(x, t)
     (loss * x.shape[0]).backward()
+    # overlap: the HIP backward announced gradients block by block on both replicas, and every
+    # bucket but the last was launched during the backward (in index order), not by finish()
+    red = st.dp.reducer
+    log = list(red.launch_log)
+    assert len(red.buckets) >= 3
+    assert [b for b, _, _ in log] == list(range(len(log))) and len(log) >= len(red.buckets) - 1, log
+    assert not any(fin for _, _, fin in log) and log[0][1] < 2 * len(st.dp.spaces[0].names), log
     st.dp.all_reduce_grads()
     torch.cuda.synchronize()
     assert abs(loss.item() - l_ref.item()) < 1e-3 * abs(l_ref.item())
