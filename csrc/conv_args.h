@@ -30,6 +30,9 @@ struct IgemmArgs {
   float* bnslab;
   int korder;           // LDS-DMA kernels: bit 0 = tap-major K-tile order (default slice-major when K is
                         // unpadded), bit 1 = no persistent kernel in the auto choice (A/B switches)
+  unsigned ximg;        // bytes addressable from ONE image of x: the row-streaming / row-halo kernels
+                        // bind one image per block (64-bit base, 32-bit offsets inside it), so they take
+                        // the whole batch in one launch whatever its size (no 2 GiB chunking)
 };
 
 // 2x2 window code from the four (bf16-rounded) values in window order tl, tr, bl, br: first

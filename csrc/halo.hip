@@ -59,7 +59,7 @@ __global__ __launch_bounds__(64 * (BC / WC) * (BP / WP)) void igemm_halo_kernel(
   char* const Pimg = lds;
   char* const Wimg = lds + PBYTES;
 
-  const int tilesPerRow = a.Wo / BP;
+  const int tilesPerRow = (a.Wo + BP - 1) / BP;     // the last tile of a row may be partial (ragged W)
   const int rowGroups = (a.Ho + ROWS - 1) / ROWS;
   const int npt = a.N * rowGroups * tilesPerRow;
   const int nct = a.Ngemm / BC;
@@ -72,7 +72,8 @@ __global__ __launch_bounds__(64 * (BC / WC) * (BP / WP)) void igemm_halo_kernel(
   const long m0 = ((long)n * a.Ho + h) * a.Wo + w0;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wp = wid / NWC, wc = wid - wp * NWC;
-  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, 0, (int)a.xbytes, 0x00020000);
+  // one image per block: 64-bit image base, 32-bit offsets inside it (whole batch in one launch)
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)(a.x + (long)n * a.Hs * a.Ws * a.ldx), 0, (int)a.ximg, 0x00020000);
 
   f32x4_t acc[ROWS][TC][TP];
 #pragma unroll
@@ -96,7 +97,7 @@ __global__ __launch_bounds__(64 * (BC / WC) * (BP / WP)) void igemm_halo_kernel(
       const int kh = row / HR, col = row - kh * HR;
       const int ih = h + kh - 1, iw = w0 + col - 1;
       gok[j] = ih >= 0 && ih < a.Hs && iw >= 0 && iw < a.Ws;
-      goff[j] = (unsigned)((((n * a.Hs + ih) * a.Ws + iw) * a.ldx + cc * 8) * 2);
+      goff[j] = (unsigned)(((ih * a.Ws + iw) * a.ldx + cc * 8) * 2);
       lsto[j] = row * 64 + (swz_nk<32>(row, cc) << 4);
     } else {
       const int cw = c - PCH, r = cw / 36, k = cw - r * 36;     // k = tap*4 + chunk
@@ -212,6 +213,7 @@ __global__ __launch_bounds__(64 * (BC / WC) * (BP / WP)) void igemm_halo_kernel(
   if (h + rr >= a.Ho) break;
 #pragma unroll
   for (int ip = 0; ip < TP; ++ip) {
+    if (w0 + wp * WP + ip * 16 + (lane & 15) >= a.Wo) continue;     // ragged last tile
     const long m = m0 + (long)rr * a.Wo + wp * WP + ip * 16 + (lane & 15);
 #pragma unroll
     for (int ic = 0; ic < TC; ++ic) {
@@ -245,7 +247,7 @@ __global__ __launch_bounds__(64 * (BC / WC) * (BP / WP)) void igemm_halo_kernel(
 
 template <int BP, int BC, int WP, int WC, int ROWS = 1, bool DPP = false>
 static int launch_igemm_halo(const IgemmArgs& a, hipStream_t st) {
-  const int grid = a.N * ((a.Ho + ROWS - 1) / ROWS) * (a.Wo / BP) * (a.Ngemm / BC);
+  const int grid = a.N * ((a.Ho + ROWS - 1) / ROWS) * ((a.Wo + BP - 1) / BP) * (a.Ngemm / BC);
   hipLaunchKernelGGL((igemm_halo_kernel<BP, BC, WP, WC, ROWS, DPP>), dim3(grid), dim3(64 * (BC / WC) * (BP / WP)), 0, st, a);
   return (int)hipGetLastError();
 }
@@ -254,30 +256,37 @@ static int launch_igemm_halo(const IgemmArgs& a, hipStream_t st) {
 // uses dpa_igemm.  cfg: 0 auto, 1: 256x32, 2: 128x64, 3: 128x32, 4: 128x64 two rows, 5: 128x32 two rows,
 // 6: 128x128 two rows 8 waves (4 ch x 2 px), 7: 128x128 two rows 8 waves (2 ch x 4 px),
 // 8 / 9 / 10: cfg 4 / 5 / 7 with DPP-shifted pixel fragments (one LDS read per kernel row)
+// a row of W pixels in tiles of bp: whole tiles, or a partial last tile that keeps >= 85 % of the
+// tile pixels useful (640x960: widths 960 / 480 / 240 / 120 in 128-pixel tiles are 94 % useful)
+static bool tiles_ok(int W, int bp) {
+  const int t = (W + bp - 1) / bp;
+  return W >= 16 && (W % bp == 0 || W * 100 >= 85 * t * bp);
+}
+
 DPA_API int dpa_igemm_halo(const IgemmArgs* args, int cfg, hipStream_t st) {
   const IgemmArgs& a = *args;
   if (a.mode != 0 || a.KH != 3 || a.KW != 3 || a.stride != 1 || a.pad != 1 || (a.Cs % 32) || (a.ldx & 7) ||
       (a.ldy & 3) || a.Hs != a.Ho || a.Ws != a.Wo || a.Kpad < 9 * a.Cs)
     return (int)hipErrorInvalidValue;
   if (cfg == 0) {
-    if (a.Ngemm == 32 && a.Wo % 256 == 0) cfg = 1;
+    if (a.Ngemm == 32 && tiles_ok(a.Wo, 256)) cfg = 1;
     // two output rows per block: 20-25% faster than one row on every 512^2 UNet shape
     // (profiles/kbench_b32_512.txt halo.c4/c5 vs c2/c3)
-    else if (a.Ngemm % 64 == 0 && a.Ngemm <= 128 && a.Wo % 128 == 0) cfg = 4;
-    else if (a.Ngemm % 32 == 0 && a.Ngemm <= 64 && a.Wo % 128 == 0) cfg = 5;
+    else if (a.Ngemm % 64 == 0 && a.Ngemm <= 128 && tiles_ok(a.Wo, 128)) cfg = 4;
+    else if (a.Ngemm % 32 == 0 && a.Ngemm <= 64 && tiles_ok(a.Wo, 128)) cfg = 5;
     else return (int)hipErrorInvalidValue;
   }
   switch (cfg) {
-    case 1: if (a.Wo % 256 || a.Ngemm % 32) break; return launch_igemm_halo<256, 32, 64, 32>(a, st);
-    case 2: if (a.Wo % 128 || a.Ngemm % 64) break; return launch_igemm_halo<128, 64, 64, 32>(a, st);
-    case 3: if (a.Wo % 128 || a.Ngemm % 32) break; return launch_igemm_halo<128, 32, 32, 32>(a, st);
-    case 4: if (a.Wo % 128 || a.Ngemm % 64) break; return launch_igemm_halo<128, 64, 64, 32, 2>(a, st);
-    case 5: if (a.Wo % 128 || a.Ngemm % 32) break; return launch_igemm_halo<128, 32, 32, 32, 2>(a, st);
-    case 6: if (a.Wo % 128 || a.Ngemm % 128) break; return launch_igemm_halo<128, 128, 64, 32, 2>(a, st);
-    case 7: if (a.Wo % 128 || a.Ngemm % 128) break; return launch_igemm_halo<128, 128, 32, 64, 2>(a, st);
-    case 8: if (a.Wo % 128 || a.Ngemm % 64) break; return launch_igemm_halo<128, 64, 64, 32, 2, true>(a, st);
-    case 9: if (a.Wo % 128 || a.Ngemm % 32) break; return launch_igemm_halo<128, 32, 32, 32, 2, true>(a, st);
-    case 10: if (a.Wo % 128 || a.Ngemm % 128) break; return launch_igemm_halo<128, 128, 32, 64, 2, true>(a, st);
+    case 1: if (!tiles_ok(a.Wo, 256) || a.Ngemm % 32) break; return launch_igemm_halo<256, 32, 64, 32>(a, st);
+    case 2: if (!tiles_ok(a.Wo, 128) || a.Ngemm % 64) break; return launch_igemm_halo<128, 64, 64, 32>(a, st);
+    case 3: if (!tiles_ok(a.Wo, 128) || a.Ngemm % 32) break; return launch_igemm_halo<128, 32, 32, 32>(a, st);
+    case 4: if (!tiles_ok(a.Wo, 128) || a.Ngemm % 64) break; return launch_igemm_halo<128, 64, 64, 32, 2>(a, st);
+    case 5: if (!tiles_ok(a.Wo, 128) || a.Ngemm % 32) break; return launch_igemm_halo<128, 32, 32, 32, 2>(a, st);
+    case 6: if (!tiles_ok(a.Wo, 128) || a.Ngemm % 128) break; return launch_igemm_halo<128, 128, 64, 32, 2>(a, st);
+    case 7: if (!tiles_ok(a.Wo, 128) || a.Ngemm % 128) break; return launch_igemm_halo<128, 128, 32, 64, 2>(a, st);
+    case 8: if (!tiles_ok(a.Wo, 128) || a.Ngemm % 64) break; return launch_igemm_halo<128, 64, 64, 32, 2, true>(a, st);
+    case 9: if (!tiles_ok(a.Wo, 128) || a.Ngemm % 32) break; return launch_igemm_halo<128, 32, 32, 32, 2, true>(a, st);
+    case 10: if (!tiles_ok(a.Wo, 128) || a.Ngemm % 128) break; return launch_igemm_halo<128, 128, 32, 64, 2, true>(a, st);
     default: break;
   }
   return (int)hipErrorInvalidValue;
@@ -471,7 +480,7 @@ __global__ __launch_bounds__(256 * WCS) void igemm_stream_kernel(IgemmArgs a) {
   char* const Wimg = lds;
   char* const Ring = lds + WBYTES;
 
-  const int stripsW = a.Wo / BP;
+  const int stripsW = (a.Wo + BP - 1) / BP;                // the last strip may be partial (ragged W)
   const int segsH = (a.Ho + RH - 1) / RH;
   const int bid = blockIdx.x;                               // streaming: no L2 reuse to chase
   const int n = bid / (segsH * stripsW);
@@ -480,9 +489,11 @@ __global__ __launch_bounds__(256 * WCS) void igemm_stream_kernel(IgemmArgs a) {
   const int w0 = (rem - hs * stripsW) * BP;
   const int h0 = hs * RH;
   const int tid = threadIdx.x, lane = tid & 63, wp = (tid >> 6) & 3, wc = tid >> 8;
-  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, 0, (int)a.xbytes, 0x00020000);
-  const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc((void*)a.y, 0, 0x7fffffff, 0x00020000);
-  const __amdgpu_buffer_rsrc_t mr = __builtin_amdgcn_make_buffer_rsrc((void*)(a.mask ? a.mask : a.y), 0, 0x7fffffff, 0x00020000);
+  // one image per block: 64-bit image bases, 32-bit offsets inside the image (any batch size)
+  const long opix = (long)n * a.Ho * a.Wo;
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)(a.x + (long)n * a.Hs * a.Ws * a.ldx), 0, (int)a.ximg, 0x00020000);
+  const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc((void*)(a.y + opix * a.ldy), 0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t mr = __builtin_amdgcn_make_buffer_rsrc((void*)(a.mask ? a.mask + opix * a.ldm : a.y), 0, 0x7fffffff, 0x00020000);
 
   // resident weights: packed [NG][Kpad] with k = tap*CS + ci
   for (int c = tid; c < 9 * KS * NG * 4; c += NT) {
@@ -512,7 +523,7 @@ __global__ __launch_bounds__(256 * WCS) void igemm_stream_kernel(IgemmArgs a) {
   RowRegs setA, setB;
   auto rload = [&](int ih, RowRegs& R) {
     const bool rok = ih >= 0 && ih < a.Hs;                     // wave-uniform
-    const unsigned rbase = (unsigned)(n * a.Hs + ih) * rowbytes_x;
+    const unsigned rbase = (unsigned)ih * rowbytes_x;
 #pragma unroll
     for (int j = 0; j < LR; ++j) {
       const unsigned off = (rok && lok[j]) ? rbase + loff[j] : 0x80000000u;
@@ -546,11 +557,14 @@ __global__ __launch_bounds__(256 * WCS) void igemm_stream_kernel(IgemmArgs a) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) bias[ic][e] = a.bias ? a.bias[wc * WCN + ic * 16 + 4 * chunk + e] : 0.f;
   unsigned yl[TP], ml[TP];
+  bool pv[TP];                  // pixel inside the row (false only in a ragged last strip)
 #pragma unroll
   for (int ip = 0; ip < TP; ++ip) {
     const int pl = w0 + wp * WP + ip * 16 + (lane & 15);
-    yl[ip] = (unsigned)((pl * a.ldy + wc * WCN + 4 * chunk) * 2);
-    ml[ip] = (unsigned)((pl * a.ldm + wc * WCN + 4 * chunk) * 2);
+    pv[ip] = pl < a.Wo;
+    // out-of-row pixels: an offset past the range check -> their stores are dropped, mask loads read 0
+    yl[ip] = pv[ip] ? (unsigned)((pl * a.ldy + wc * WCN + 4 * chunk) * 2) : 0x80000000u;
+    ml[ip] = pv[ip] ? (unsigned)((pl * a.ldm + wc * WCN + 4 * chunk) * 2) : 0x80000000u;
   }
   // forward epilogues (pool, head, BN statistics, plain forward EPI 6) never mask or accumulate: with
   // those paths compiled out, no epilogue load shares the in-order vmcnt queue with the two-rows-ahead
@@ -560,7 +574,8 @@ __global__ __launch_bounds__(256 * WCS) void igemm_stream_kernel(IgemmArgs a) {
   // fused 2x2 max-pool (encoder conv2 -> next level input): even rows keep their horizontally
   // max-reduced values in registers, odd rows finish the window and write the pooled pixel.
   constexpr bool do_pool = EPI == 1;
-  const __amdgpu_buffer_rsrc_t pr = __builtin_amdgcn_make_buffer_rsrc((void*)(do_pool ? a.pool : a.y), 0, 0x7fffffff, 0x00020000);
+  const long ppix = (long)n * (a.Ho >> 1) * (a.Wo >> 1);
+  const __amdgpu_buffer_rsrc_t pr = __builtin_amdgcn_make_buffer_rsrc((void*)(do_pool ? a.pool + ppix * a.ldp : a.y), 0, 0x7fffffff, 0x00020000);
   constexpr int PT = do_pool ? TP : 1, PC = do_pool ? TC : 1;
   float ptop[PT][PC][4], ptop2[PT][PC][4];   // even row of the window: left / right pixel
 
@@ -600,9 +615,9 @@ __global__ __launch_bounds__(256 * WCS) void igemm_stream_kernel(IgemmArgs a) {
 
   // row r: `cur` holds row h0+r+2 (issued during row r-1); row h0+r+3 is issued into `nxt`
   auto row = [&](int r, RowRegs& cur, RowRegs& nxt) {
-    const int orow = n * a.Ho + h0 + r;
-    const unsigned ybase = (unsigned)orow * (unsigned)(a.Wo * a.ldy * 2);
-    const unsigned mbase = (unsigned)orow * (unsigned)(a.Wo * a.ldm * 2);
+    const int orow = n * a.Ho + h0 + r;                        // global output row (pointer-math epilogues)
+    const unsigned ybase = (unsigned)(h0 + r) * (unsigned)(a.Wo * a.ldy * 2);   // inside this image
+    const unsigned mbase = (unsigned)(h0 + r) * (unsigned)(a.Wo * a.ldm * 2);
     // ReLU-mask of this output row: issued before the MFMAs so its latency hides under them, and
     // before the row prefetch, so waiting for it does not wait for the prefetch (in-order vmcnt)
     u32x2_t mk[TP][TC];
@@ -668,13 +683,15 @@ __global__ __launch_bounds__(256 * WCS) void igemm_stream_kernel(IgemmArgs a) {
           v0 += lo_bf(o.x); v1 += hi_bf(o.x); v2 += lo_bf(o.y); v3 += hi_bf(o.y);
         }
         const u32x2_t packed = u32x2_t{pack_bf2(v0, v1), pack_bf2(v2, v3)};
-        if constexpr (EPI == 2)
-          split_store(a, (unsigned)(orow * a.Wo + w0 + wp * WP + ip * 16 + (lane & 15)), wc * WCN + ic * 16 + 4 * chunk,
-                      packed);
-        else
+        if constexpr (EPI == 2) {
+          if (pv[ip])
+            split_store(a, (unsigned)(orow * a.Wo + w0 + wp * WP + ip * 16 + (lane & 15)), wc * WCN + ic * 16 + 4 * chunk,
+                        packed);
+        } else
           __builtin_amdgcn_raw_buffer_store_b64(packed, yr, yo, 0, 0);
         if constexpr (do_bn) {     // statistics of the STORED bf16 values, like a separate pass
-          const float q[4] = {lo_bf(packed.x), hi_bf(packed.x), lo_bf(packed.y), hi_bf(packed.y)};
+          const float pz = pv[ip] ? 1.f : 0.f;                  // out-of-row pixels add nothing
+          const float q[4] = {pz * lo_bf(packed.x), pz * hi_bf(packed.x), pz * lo_bf(packed.y), pz * hi_bf(packed.y)};
           float f[4] = {q[0], q[1], q[2], q[3]};
           if constexpr (EPI == 5) {
             f[0] = lo_bf(mk[ip][ic].x); f[1] = hi_bf(mk[ip][ic].x); f[2] = lo_bf(mk[ip][ic].y); f[3] = hi_bf(mk[ip][ic].y);
@@ -705,10 +722,11 @@ __global__ __launch_bounds__(256 * WCS) void igemm_stream_kernel(IgemmArgs a) {
               ptop[ip][ic][e] = q[e];
               ptop2[ip][ic][e] = pq[e];
             }
-          } else if (hrow < 2 * (a.Ho >> 1) && (lane & 1) == 0) {
+          } else if (hrow < 2 * (a.Ho >> 1) && (lane & 1) == 0 && pv[ip]) {
             const int pw = (w0 + wp * WP + ip * 16 + (lane & 15)) >> 1;
-            const unsigned pidx = (unsigned)((n * (a.Ho >> 1) + (hrow >> 1)) * (a.Wo >> 1) + pw);
-            const unsigned po = (pidx * a.ldp + wc * WCN + ic * 16 + 4 * chunk) * 2;
+            const unsigned lidx = (unsigned)((hrow >> 1) * (a.Wo >> 1) + pw);       // inside this image
+            const size_t pidx = (size_t)ppix + lidx;
+            const unsigned po = (lidx * a.ldp + wc * WCN + ic * 16 + 4 * chunk) * 2;
             float mx[4];
 #pragma unroll
             for (int e = 0; e < 4; ++e) mx[e] = fmaxf(fmaxf(q[e], pq[e]), fmaxf(ptop[ip][ic][e], ptop2[ip][ic][e]));
@@ -726,7 +744,7 @@ __global__ __launch_bounds__(256 * WCS) void igemm_stream_kernel(IgemmArgs a) {
         // the pixel's 32 channels live in lanes l, l^16, l^32, l^48 of this wave
         hdot += __shfl_xor(hdot, 16, 64);
         hdot += __shfl_xor(hdot, 32, 64);
-        if (chunk == 0) {
+        if (chunk == 0 && pv[ip]) {
           const unsigned pix = (unsigned)(orow * a.Wo + w0 + wp * WP + ip * 16 + (lane & 15));
           const float z = hdot + a.hb[0];
           const float p = 1.f / (1.f + __expf(-z));
@@ -794,15 +812,15 @@ __global__ __launch_bounds__(256) void igemm_stream8_kernel(IgemmArgs a) {
   __shared__ __attribute__((aligned(16))) char lds[3 * NG * 64 + 4 * SLOT];
   char* const Wimg = lds;
   char* const Ring = lds + 3 * NG * 64;
-  const int stripsW = a.Wo / BP, segsH = (a.Ho + RH - 1) / RH;
+  const int stripsW = (a.Wo + BP - 1) / BP, segsH = (a.Ho + RH - 1) / RH;
   const int bid = blockIdx.x;
   const int n = bid / (segsH * stripsW);
   const int rem = bid - n * segsH * stripsW;
   const int hs = rem / stripsW;
   const int w0 = (rem - hs * stripsW) * BP, h0 = hs * RH;
   const int tid = threadIdx.x, lane = tid & 63, wp = tid >> 6;
-  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, 0, (int)a.xbytes, 0x00020000);
-  const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc((void*)a.y, 0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)(a.x + (long)n * a.Hs * a.Ws * a.ldx), 0, (int)a.ximg, 0x00020000);
+  const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc((void*)(a.y + (long)n * a.Ho * a.Wo * a.ldy), 0, 0x7fffffff, 0x00020000);
   // weights [co][96] -> [kstep][co][64 B] (swz_nk<32>)
   for (int c = tid; c < 3 * NG * 4; c += 256) {
     const int cc = c & 3, row = (c >> 2) % NG, s = (c >> 2) / NG;
@@ -816,7 +834,7 @@ __global__ __launch_bounds__(256) void igemm_stream8_kernel(IgemmArgs a) {
   u32x4_t reg;
   auto rload = [&](int ih) {
     const bool ok = lcol && ih >= 0 && ih < a.Hs;
-    reg = __builtin_amdgcn_raw_buffer_load_b128(xr, ok ? (unsigned)(n * a.Hs + ih) * rowbytes + (unsigned)(iw_l * a.ldx * 2)
+    reg = __builtin_amdgcn_raw_buffer_load_b128(xr, ok ? (unsigned)ih * rowbytes + (unsigned)(iw_l * a.ldx * 2)
                                                        : 0x80000000u, 0, 0);
   };
   auto rstore = [&](int slot) {
@@ -836,7 +854,10 @@ __global__ __launch_bounds__(256) void igemm_stream8_kernel(IgemmArgs a) {
     for (int e = 0; e < 4; ++e) bias[ic][e] = a.bias ? a.bias[ic * 16 + 4 * chunk + e] : 0.f;
   unsigned yl[TP];
 #pragma unroll
-  for (int ip = 0; ip < TP; ++ip) yl[ip] = (unsigned)(((w0 + wp * WP + ip * 16 + (lane & 15)) * a.ldy + 4 * chunk) * 2);
+  for (int ip = 0; ip < TP; ++ip) {
+    const int pl = w0 + wp * WP + ip * 16 + (lane & 15);
+    yl[ip] = pl < a.Wo ? (unsigned)((pl * a.ldy + 4 * chunk) * 2) : 0x80000000u;   // ragged strip: dropped
+  }
 #pragma unroll 1
   for (int j = 0; j < 3; ++j) {
     rload(h0 - 1 + j);
@@ -873,7 +894,7 @@ __global__ __launch_bounds__(256) void igemm_stream8_kernel(IgemmArgs a) {
         for (int ip = 0; ip < TP; ++ip)
           acc[ic][ip] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ic], bfr[ip], acc[ic][ip], 0, 0, 0);
     }
-    const unsigned ybase = (unsigned)(n * a.Ho + h0 + r) * (unsigned)(a.Wo * a.ldy * 2);
+    const unsigned ybase = (unsigned)(h0 + r) * (unsigned)(a.Wo * a.ldy * 2);
 #pragma unroll
     for (int ip = 0; ip < TP; ++ip)
 #pragma unroll
@@ -893,14 +914,14 @@ __global__ __launch_bounds__(256) void igemm_stream8_kernel(IgemmArgs a) {
 
 template <int BP, int RH>
 static int launch_igemm_stream8(const IgemmArgs& a, hipStream_t st) {
-  const int grid = a.N * ((a.Ho + RH - 1) / RH) * (a.Wo / BP);
+  const int grid = a.N * ((a.Ho + RH - 1) / RH) * ((a.Wo + BP - 1) / BP);
   hipLaunchKernelGGL((igemm_stream8_kernel<BP, RH>), dim3(grid), dim3(256), 0, st, a);
   return (int)hipGetLastError();
 }
 
 template <int BP, int NG, int CS, int RH, int WCS>
 static int launch_igemm_stream(const IgemmArgs& a, hipStream_t st) {
-  const int grid = a.N * ((a.Ho + RH - 1) / RH) * (a.Wo / BP);
+  const int grid = a.N * ((a.Ho + RH - 1) / RH) * ((a.Wo + BP - 1) / BP);
   if (a.pool) {   // encoder conv2 (NG == CS): pool + window codes fused
     if constexpr (NG == CS) {
       hipLaunchKernelGGL((igemm_stream_kernel<BP, NG, CS, RH, WCS, 1>), dim3(grid), dim3(256 * WCS), 0, st, a);
@@ -954,25 +975,26 @@ DPA_API int dpa_igemm_stream_blocks(const IgemmArgs* args) {
   const IgemmArgs& a = *args;
   const int variant = stream_auto_variant(a);
   const int bp = (variant == 1 || variant == 3) ? 128 : 64;
-  if (a.Wo % bp) return 0;
-  const long blocks32 = (long)a.N * ((a.Ho + 31) / 32) * (a.Wo / bp);
+  const int strips = (a.Wo + bp - 1) / bp;
+  const long blocks32 = (long)a.N * ((a.Ho + 31) / 32) * strips;
   const int rh = blocks32 >= 1024 ? 32 : 16;
-  return a.N * ((a.Ho + rh - 1) / rh) * (a.Wo / bp);
+  return a.N * ((a.Ho + rh - 1) / rh) * strips;
 }
 
-// Eligible: conv3x3 s1 p1 mode 0, Ngemm and Cs in {32, 64}, Wo % 64 == 0, Ho >= 1.
+// Eligible: conv3x3 s1 p1 mode 0, Ngemm and Cs in {32, 64}, Wo >= 16 (a ragged last strip is masked), Ho >= 1.
 // With a.pool set the kernel also writes the 2x2/s2 max-pool of y (floor semantics).
 // variant: 0 auto, 1: BP128 x 4 waves, 2: BP64 x 4 waves, 3: BP128 x 8 waves, 4: BP64 x 8 waves
 DPA_API int dpa_igemm_stream(const IgemmArgs* args, int variant, hipStream_t st) {
   const IgemmArgs& a = *args;
+  // any row width: a partial last strip masks its out-of-row pixels (loads read zeros, stores are
+  // dropped); the fused pool needs whole 2x2 windows along the row (even width)
   if (a.mode != 0 || a.KH != 3 || a.KW != 3 || a.stride != 1 || a.pad != 1 || (a.ldx & 7) || (a.ldy & 3) ||
-      a.Hs != a.Ho || a.Ws != a.Wo || a.Wo % 64 || a.Kpad < 9 * a.Cs || (a.pool && (a.ldp & 3)))
+      a.Hs != a.Ho || a.Ws != a.Wo || a.Wo < 16 || a.Kpad < 9 * a.Cs || (a.pool && ((a.ldp & 3) || (a.Wo & 1))))
     return (int)hipErrorInvalidValue;
-  if (a.Cs == 8 && a.Ngemm == 32 && !a.pool && a.Wo % 128 == 0) return launch_igemm_stream8<128, 32>(a, st);
+  if (a.Cs == 8 && a.Ngemm == 32 && !a.pool) return launch_igemm_stream8<128, 32>(a, st);
   if (variant == 0) variant = stream_auto_variant(a);
   const int bp = (variant == 1 || variant == 3) ? 128 : 64;
-  if (a.Wo % bp) return (int)hipErrorInvalidValue;
-  const long blocks32 = (long)a.N * ((a.Ho + 31) / 32) * (a.Wo / bp);
+  const long blocks32 = (long)a.N * ((a.Ho + 31) / 32) * ((a.Wo + bp - 1) / bp);
   const int rh = blocks32 >= 1024 ? 32 : 16;
 #define DPA_STREAM(NGv, CSv)                                                                               \
   if (a.Ngemm == NGv && a.Cs == CSv) {                                                                    \
@@ -1029,7 +1051,7 @@ __global__ __launch_bounds__(192) void wgrad_stream_kernel(WgradArgs a, int ipb)
   char* const Ring = lds + 2 * IMGA;
 
   const int nmt = a.M / BM, nnt = (a.Nc + BN - 1) / BN, tiles = nmt * nnt;
-  const int stripsW = a.Wg / BP, segsH = (a.Hg + RH - 1) / RH;
+  const int stripsW = (a.Wg + BP - 1) / BP, segsH = (a.Hg + RH - 1) / RH;   // ragged last strip allowed
   const int bid = xcd_remap(blockIdx.x, tiles * a.splits);
   const int split = bid / tiles, tile = bid - split * tiles;     // split = (image group, hs, ws)
   const int mt = tile / nnt, nt = tile - mt * nnt;
@@ -1042,8 +1064,9 @@ __global__ __launch_bounds__(192) void wgrad_stream_kernel(WgradArgs a, int ipb)
   const int nimg = min(ipb, a.N - ig * ipb);
   const int tid = threadIdx.x, lane = tid & 63, kh = tid >> 6;
   const bool do_bias = a.bslab != nullptr && nt == 0;
-  const __amdgpu_buffer_rsrc_t ar = __builtin_amdgcn_make_buffer_rsrc((void*)a.A, 0, (int)a.abytes, 0x00020000);
-  const __amdgpu_buffer_rsrc_t br = __builtin_amdgcn_make_buffer_rsrc((void*)a.B, 0, (int)a.bbytes, 0x00020000);
+  // one image at a time: 64-bit image bases (rebound per image below), 32-bit offsets inside it;
+  // a.abytes / a.bbytes are the extents of ONE image here, so one launch covers any batch
+  __amdgpu_buffer_rsrc_t ar, br;
 
   // per-thread loader constants
   unsigned aoff[LA], boff[LB];
@@ -1052,7 +1075,8 @@ __global__ __launch_bounds__(192) void wgrad_stream_kernel(WgradArgs a, int ipb)
 #pragma unroll
   for (int j = 0; j < LA; ++j) {
     const int c = tid + j * NT, px = c / CPRA, cc = c - px * CPRA;
-    aoff[j] = (unsigned)(((w0 + px) * a.lda + m0 + cc * 8) * 2);
+    // gradient pixels past the row (ragged last strip) read as zeros: they add nothing to dW / db
+    aoff[j] = w0 + px < a.Wg ? (unsigned)(((w0 + px) * a.lda + m0 + cc * 8) * 2) : 0x80000000u;
     asto[j] = c < CHA ? px * RBA + ((cc ^ swz_kk<RBA>(px)) << 4) : -1;
   }
 #pragma unroll
@@ -1067,13 +1091,13 @@ __global__ __launch_bounds__(192) void wgrad_stream_kernel(WgradArgs a, int ipb)
   u32x4_t ra[LA], rb[LB];
   int n = ig * ipb;
   auto load_a = [&](int h) {
-    const unsigned base = (unsigned)(n * a.HA + h) * arow;
+    const unsigned base = (unsigned)h * arow;
 #pragma unroll
     for (int j = 0; j < LA; ++j) ra[j] = __builtin_amdgcn_raw_buffer_load_b128(ar, asto[j] >= 0 ? base + aoff[j] : 0x80000000u, 0, 0);
   };
   auto load_b = [&](int ih) {
     const bool rok = ih >= 0 && ih < a.HB;
-    const unsigned base = (unsigned)(n * a.HB + ih) * brow;
+    const unsigned base = (unsigned)ih * brow;
 #pragma unroll
     for (int j = 0; j < LB; ++j)
       rb[j] = __builtin_amdgcn_raw_buffer_load_b128(br, (rok && bok[j]) ? base + boff[j] : 0x80000000u, 0, 0);
@@ -1115,6 +1139,8 @@ __global__ __launch_bounds__(192) void wgrad_stream_kernel(WgradArgs a, int ipb)
 
 #pragma unroll 1
   for (int im = 0; im < nimg; ++im, ++n) {
+  ar = __builtin_amdgcn_make_buffer_rsrc((void*)(a.A + (long)n * a.HA * a.WA * a.lda), 0, (int)a.abytes, 0x00020000);
+  br = __builtin_amdgcn_make_buffer_rsrc((void*)(a.B + (long)n * a.HB * a.WB * a.ldb), 0, (int)a.bbytes, 0x00020000);
   // prologue: input rows h0-1, h0, h0+1 -> ring slots 0..2; gradient row h0 -> A buffer 0
   if (nrows > 0) {
 #pragma unroll 1
@@ -1215,8 +1241,8 @@ static int launch_wgrad_stream(const WgradArgs& a, int ipb, hipStream_t st) {
 DPA_API int dpa_wgrad_stream(const WgradArgs* args, int cfg, int bp, int rh, int ipb, hipStream_t st) {
   const WgradArgs& a = *args;
   if (ipb < 1 || (a.lda & 7) || (a.ldb & 7) || a.s != 1 || a.pad != 1 || a.KW != 3 || a.HA != a.Hg || a.WA != a.Wg ||
-      a.HB != a.Hg || a.WB != a.Wg || a.Wg % bp ||
-      a.splits != ((a.N + ipb - 1) / ipb) * ((a.Hg + rh - 1) / rh) * (a.Wg / bp))
+      a.HB != a.Hg || a.WB != a.Wg || a.Wg < 8 ||
+      a.splits != ((a.N + ipb - 1) / ipb) * ((a.Hg + rh - 1) / rh) * ((a.Wg + bp - 1) / bp))
     return (int)hipErrorInvalidValue;
 #define DPA_WS(C, BMv, BNv, BPv, RHv)                                                              \
   if (cfg == C && bp == BPv && rh == RHv && a.M % BMv == 0 && a.Nc % BNv == 0) return launch_wgrad_stream<BMv, BNv, BPv, RHv>(a, ipb, st);

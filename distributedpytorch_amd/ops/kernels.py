@@ -30,7 +30,7 @@ class IgemmArgs(ctypes.Structure):
                                      "stride", "pad", "Ngemm", "Kpad", "mode", "relu", "accumulate", "Cout")] + \
                [("xbytes", ctypes.c_uint), ("pool", c_void_p), ("ldp", c_int), ("pcode", c_void_p), ("y2", c_void_p),
                 ("ldy2", c_int), ("split", c_int), ("hw", c_void_p), ("hb", c_void_p), ("tgt", c_void_p),
-                ("hslab", c_void_p), ("bnslab", c_void_p), ("korder", c_int)]
+                ("hslab", c_void_p), ("bnslab", c_void_p), ("korder", c_int), ("ximg", ctypes.c_uint)]
 
 
 class WgradArgs(ctypes.Structure):
@@ -194,72 +194,80 @@ def igemm(x: torch.Tensor, wpacked: torch.Tensor, y: torch.Tensor, *, Ngemm: int
         assert 0 < split < Ngemm and C2 >= Ngemm - split and Cy >= split
     L = _lib.lib()
     st = _stream(y)
-    pool_done = True
-    hslab, hrows = None, 0
-    bslab, brows = None, 0
+    hslab = None
+    bslab = None
     if bn_stats is not None and USE_FUSED_BN and mode == 0 and pool is None and y2 is None and head is None \
             and not accumulate and not relu and path == "auto" and (mask is None or mch == Ngemm):
-        bslab = torch.empty(N * -(-Ho // 16) * max(1, Wo // 64) * 2 * Ngemm, dtype=torch.float32, device=y.device)
+        bslab = torch.empty(N * -(-Ho // 16) * -(-Wo // 64) * 2 * Ngemm, dtype=torch.float32, device=y.device)
     if head is not None:
         hw, hb, tgt = head
         assert mode == 0 and Ngemm == 32 and Cs == 32 and pool is None and y2 is None and mask is None
         assert hw.dtype == torch.float32 and hw.is_contiguous() and hw.numel() == 32 and hb.numel() == 1
         assert tgt.dtype == torch.float32 and tgt.is_contiguous() and tgt.numel() == N * Ho * Wo
-        hslab = torch.empty((N * -(-Ho // 16) * max(1, Wo // 64) + 1) * 4, dtype=torch.float32, device=y.device)
-    for n0, n1 in _image_chunks(N, max(Hs * Ws * ldx, (4 if mode else 1) * Ho * Wo * ldy) * 2):
+        hslab = torch.empty((N * -(-Ho // 16) * -(-Wo // 64) + 1) * 4, dtype=torch.float32, device=y.device)
+    def args(n0, n1, per_image):
         xs, ys = x[n0:n1], y[n0:n1]
         nb = n1 - n0
         a = IgemmArgs(xs.data_ptr(), _p(wpacked).value, None if bias is None else bias.data_ptr(), ys.data_ptr(),
                       None if mask is None else mask[n0:n1].data_ptr(), ldx, ldy, ldm, mch, nb, Ho, Wo, Hs, Ws, Cs,
                       KH, KW, stride, pad, Ngemm, Kpad, mode, int(relu), int(accumulate), Cout,
-                      _extent_bytes(nb, Hs, Ws, Cx, ldx), None, 0, None,
+                      0 if per_image else _extent_bytes(nb, Hs, Ws, Cx, ldx), None, 0, None,
                       None if y2 is None else y2[n0:n1].data_ptr(), ldy2, split)
-        conv3 = mode == 0 and KH == 3 and stride == 1 and cfg == 0
-        stream_ok = (Ngemm in (32, 64) and Cs in (32, 64)) or (Ngemm == 32 and Cs == 8 and pool is None)
-        if head is not None:
+        a.ximg = _extent_bytes(1, Hs, Ws, Cx, ldx)
+        return a
+
+    conv3 = mode == 0 and KH == 3 and stride == 1 and cfg == 0
+    stream_ok = (Ngemm in (32, 64) and Cs in (32, 64)) or (Ngemm == 32 and Cs == 8 and pool is None)
+    # ---- per-image kernels (row-streaming, row-halo): each block binds one image, so ONE launch
+    # covers the whole batch (no 2 GiB chunks, no chunk tails)
+    per_image_ok = Hs * Ws * ldx * 2 < _MAX_BYTES
+    a = args(0, N, True) if per_image_ok else None
+    if head is not None:
+        rows = L.dpa_igemm_stream_blocks(ctypes.byref(a)) if a is not None else 0
+        assert conv3 and stream_ok and 0 < rows and (rows + 1) * 4 <= hslab.numel() and path in ("auto", "stream"), \
+            "fused head needs the stream kernel"
+        a.hw, a.hb, a.tgt, a.hslab = hw.data_ptr(), hb.data_ptr(), tgt.data_ptr(), hslab.data_ptr()
+        _check(L.dpa_igemm_stream(ctypes.byref(a), c_int(0), st), "igemm_stream+head")
+        S = hslab[hslab.numel() - 4:]
+        _check(L.dpa_slab_sum(_p(hslab), c_int(rows), c_int(4), _p(S), st), "slab_sum")
+        return S
+    done = False
+    if bslab is not None:
+        if a is not None and conv3 and stream_ok and USE_STREAM and Cs != 8:
             rows = L.dpa_igemm_stream_blocks(ctypes.byref(a))
-            assert conv3 and stream_ok and rows > 0 and path in ("auto", "stream"), "fused head needs the stream kernel"
-            a.hw, a.hb = hw.data_ptr(), hb.data_ptr()
-            a.tgt = tgt[n0 * Ho * Wo:].data_ptr()
-            a.hslab = hslab[hrows * 4:].data_ptr()
-            _check(L.dpa_igemm_stream(ctypes.byref(a), c_int(0), st), "igemm_stream+head")
-            hrows += rows
-            continue
-        if bslab is not None and conv3 and stream_ok and USE_STREAM and Cs != 8:
-            rows = L.dpa_igemm_stream_blocks(ctypes.byref(a))
-            if rows > 0:
-                a.bnslab = bslab[brows * 2 * Ngemm:].data_ptr()
+            if rows > 0 and rows * 2 * Ngemm <= bslab.numel():
+                a.bnslab = bslab.data_ptr()
                 if L.dpa_igemm_stream(ctypes.byref(a), c_int(0), st) == 0:
-                    brows += rows
-                    continue
+                    bn_stats.extend([bslab, rows])
+                    return
                 a.bnslab = None
-            bslab = None   # not fusable for this chunk: the BN pass computes the statistics
-        elif bslab is not None:
-            # (the same epilogue in the row-halo kernel measured 4% slower end to end: its extra
-            # registers cost more than the statistics pass it saves)
-            bslab = None
-        if path == "stream" or (path == "auto" and USE_STREAM and conv3 and stream_ok):
-            if pool is not None:
-                a.pool, a.ldp = pool[n0:n1].data_ptr(), ldp
-                a.pcode = None if pcode is None else pcode[n0:n1].data_ptr()
-            err = L.dpa_igemm_stream(ctypes.byref(a), c_int(variant), st)
-            if err == 0:
-                continue
-            a.pool, a.ldp, a.pcode = None, 0, None
-            if path == "stream":
-                _check(err, "igemm_stream")
-        pool_done = False
-        glds_ok = USE_GLDS and cfg == 0 and Cs % 64 == 0 and Kpad % 64 == 0 and Ngemm % 128 == 0
-        # measured at batch 128 (tools/kbench.py, profiles/kbench_b128_512.txt): the two-row halo kernel
-        # beats the LDS-DMA kernel on every shape both accept (128-channel dgrads: 837 vs 1042 us at
-        # 128^2, 2542 vs 2948 us at 256^2); the LDS-DMA kernel takes what the halo kernel cannot
-        # (64^2 and smaller grids, > 128 output channels)
-        if path == "halo" or (path == "auto" and USE_HALO and conv3 and Cs % 32 == 0 and Ngemm <= 128):
-            err = L.dpa_igemm_halo(ctypes.byref(a), c_int(variant if path == "halo" else HALO_CFG), st)
-            if err == 0:
-                continue
-            if path == "halo":
-                _check(err, "igemm_halo")
+        # not fusable here: the BN pass computes the statistics (the same epilogue in the row-halo
+        # kernel measured 4% slower end to end: its extra registers cost more than the pass it saves)
+        bslab = None
+    if a is not None and (path == "stream" or (path == "auto" and USE_STREAM and conv3 and stream_ok)):
+        if pool is not None:
+            a.pool, a.ldp = pool.data_ptr(), ldp
+            a.pcode = None if pcode is None else pcode.data_ptr()
+        err = L.dpa_igemm_stream(ctypes.byref(a), c_int(variant), st)
+        if err == 0:
+            return
+        a.pool, a.ldp, a.pcode = None, 0, None
+        if path == "stream":
+            _check(err, "igemm_stream")
+    # measured at batch 128 (tools/kbench.py, profiles/kbench_b128_512.txt): the two-row halo kernel
+    # beats the LDS-DMA kernel on every shape both accept (128-channel dgrads: 837 vs 1042 us at
+    # 128^2, 2542 vs 2948 us at 256^2); the LDS-DMA kernel takes what the halo kernel cannot
+    # (64^2 and smaller grids, > 128 output channels)
+    if a is not None and (path == "halo" or (path == "auto" and USE_HALO and conv3 and Cs % 32 == 0 and Ngemm <= 128)):
+        err = L.dpa_igemm_halo(ctypes.byref(a), c_int(variant if path == "halo" else HALO_CFG), st)
+        if err == 0:
+            done = True
+        elif path == "halo":
+            _check(err, "igemm_halo")
+    # ---- chunked kernels (LDS-DMA GEMM, generic gather): 32-bit offsets over the whole chunk
+    glds_ok = USE_GLDS and cfg == 0 and Cs % 64 == 0 and Kpad % 64 == 0 and Ngemm % 128 == 0
+    for n0, n1 in ([] if done else _image_chunks(N, max(Hs * Ws * ldx, (4 if mode else 1) * Ho * Wo * ldy) * 2)):
+        a = args(n0, n1, False)
         if path == "glds" or (path == "auto" and glds_ok):
             err = L.dpa_igemm_glds(ctypes.byref(a), c_int(variant if path == "glds" else 16 * GLDS_TAP_MAJOR + 32 * GLDS_NO_PERS + 64 * GLDS_NO_PRELOAD), st)
             if err == 0:
@@ -267,19 +275,13 @@ def igemm(x: torch.Tensor, wpacked: torch.Tensor, y: torch.Tensor, *, Ngemm: int
             if path == "glds":
                 _check(err, "igemm_glds")
         _check(L.dpa_igemm(ctypes.byref(a), c_int(cfg), st), "igemm")
-    if pool is not None and not pool_done:
+    if pool is not None:
         maxpool2(y, pool, pcode)
-    if bslab is not None and brows > 0:
-        bn_stats.extend([bslab, brows])
-    if head is not None:
-        S = hslab[hslab.numel() - 4:]
-        _check(L.dpa_slab_sum(_p(hslab), c_int(hrows), c_int(4), _p(S), st), "slab_sum")
-        return S
 
 
 def head_fusable(N: int, H: int, W: int, Cin: int, Cout: int) -> bool:
     """Can the last decoder conv (Cin -> Cout = 32) carry the segmentation head in its epilogue?"""
-    return USE_STREAM and USE_FUSED_HEAD and Cin == 32 and Cout == 32 and W % 128 == 0
+    return USE_STREAM and USE_FUSED_HEAD and Cin == 32 and Cout == 32 and W >= 16 and H * W * Cin * 2 < _MAX_BYTES
 
 
 # ------------------------------------------------------------------------------------------ wgrad
@@ -299,7 +301,7 @@ def wgrad(A: torch.Tensor, B: torch.Tensor, *, kind: int, grid, M: int, Nc: int,
     ``path``: ``auto`` = row-streaming kernel when W % 64 == 0, else row-halo (W % 32 == 0), else the
     generic per-tap gather kernel; ``stream`` / ``halo`` / ``generic`` force one."""
     if path in ("auto", "stream") and kind == 0 and cfg == 0 and (USE_STREAM or path == "stream") \
-            and (grid[2] % 64 == 0 or (grid[2] % 32 == 0 and Nc % 32 == 0)) and M % 32 == 0 and (Nc % 32 == 0 or Nc == 8):
+            and grid[2] >= 8 and M % 32 == 0 and (Nc % 32 == 0 or Nc == 8):
         return _wgrad_stream(A, B, grid=grid, M=M, Nc=Nc, gw=gw, gb=gb, Nreal=Nreal)
     if path == "stream":
         raise RuntimeError("wgrad stream path not eligible for this shape")
@@ -369,23 +371,27 @@ def _wgrad_stream(A, B, *, grid, M, Nc, gw, gb, Nreal):
     tiles = (M // bm) * (-(-Nc // bn))
     L = _lib.lib()
     st = _stream(A)
-    for n0, n1 in _image_chunks(N, max(HA * WA * lda, HB * WB * ldb) * 2):
-        nb = n1 - n0
-        bp = 64 if Wg % 64 == 0 else 32   # 32-pixel strips for the 32x32 bottleneck (mid block)
-        rh = 64 if nb * -(-Hg // 64) * (Wg // bp) * tiles >= 1024 else 32
-        per_img = -(-Hg // rh) * (Wg // bp)
-        # images per split: keep >= ~2048 blocks (8 per CU) but no more slabs than that -- the fp32
-        # slab reduction otherwise grows linearly with the batch
-        ipb = max(1, (nb * per_img * tiles) // WGRAD_STREAM_BLOCKS)
-        splits = -(-nb // ipb) * per_img
-        slab = torch.empty(splits * 9 * M * Nc + splits * M, dtype=torch.float32, device=A.device)
-        bslab = slab[splits * 9 * M * Nc:] if gb is not None else None
-        a = WgradArgs(A[n0:n1].data_ptr(), B[n0:n1].data_ptr(), slab.data_ptr(),
-                      None if bslab is None else bslab.data_ptr(), lda, ldb, nb, Hg, Wg, HA, WA, HB, WB, M, Nc, 1,
-                      1, 3, 0, splits, _extent_bytes(nb, HA, WA, CA, lda), _extent_bytes(nb, HB, WB, CB, ldb))
-        _check(L.dpa_wgrad_stream(ctypes.byref(a), c_int(hcfg), c_int(bp), c_int(rh), c_int(ipb), st), "wgrad_stream")
-        _check(L.dpa_wgrad_reduce(_p(slab), _p(bslab), _p(gw), _p(gb), c_int(splits), c_int(9), c_int(M), c_int(Nc),
-                                  c_int(Nreal), c_int(0), st), "wgrad_reduce")
+    nb = N
+    # one launch for the whole batch: the kernel binds one image at a time (per-image extents below).
+    # Strip width: 64 pixels unless 32-pixel strips waste less of a ragged row (the first layer's
+    # 8-channel tile exists only with 64-pixel strips)
+    waste = lambda b: -(-Wg // b) * b - Wg     # noqa: E731
+    bp = 64 if (Nc == 8 or waste(64) <= waste(32)) else 32
+    strips = -(-Wg // bp)
+    rh = 64 if nb * -(-Hg // 64) * strips * tiles >= 1024 else 32
+    per_img = -(-Hg // rh) * strips
+    # images per split: keep >= ~2048 blocks (8 per CU) but no more slabs than that -- the fp32
+    # slab reduction otherwise grows linearly with the batch
+    ipb = max(1, (nb * per_img * tiles) // WGRAD_STREAM_BLOCKS)
+    splits = -(-nb // ipb) * per_img
+    slab = torch.empty(splits * 9 * M * Nc + splits * M, dtype=torch.float32, device=A.device)
+    bslab = slab[splits * 9 * M * Nc:] if gb is not None else None
+    a = WgradArgs(A.data_ptr(), B.data_ptr(), slab.data_ptr(), None if bslab is None else bslab.data_ptr(), lda, ldb,
+                  nb, Hg, Wg, HA, WA, HB, WB, M, Nc, 1, 1, 3, 0, splits, _extent_bytes(1, HA, WA, CA, lda),
+                  _extent_bytes(1, HB, WB, CB, ldb))
+    _check(L.dpa_wgrad_stream(ctypes.byref(a), c_int(hcfg), c_int(bp), c_int(rh), c_int(ipb), st), "wgrad_stream")
+    _check(L.dpa_wgrad_reduce(_p(slab), _p(bslab), _p(gw), _p(gb), c_int(splits), c_int(9), c_int(M), c_int(Nc),
+                              c_int(Nreal), c_int(0), st), "wgrad_reduce")
 
 
 # ------------------------------------------------------------------------------- fused conv backward

@@ -75,6 +75,10 @@ def _pack_one(mode, w, cin_pad=None):
     (2, 2, 128, 64, 128, "auto"),
     (2, 5, 128, 3, 32, "stream"),          # first layer (8 padded channels) streaming kernel
     (1, 34, 256, 3, 32, "auto"),
+    # ragged rows (640x960 widths 480 / 240 / 120 and others): a partial last strip / tile
+    (2, 5, 96, 32, 32, "stream"), (1, 6, 240, 64, 64, "stream"), (1, 4, 480, 32, 64, "auto"),
+    (1, 4, 240, 64, 128, "halo"), (2, 3, 120, 128, 128, "halo"), (1, 3, 480, 64, 32, "halo"),
+    (1, 5, 200, 3, 32, "stream"), (2, 4, 240, 128, 128, "auto"),
 ])
 def test_conv3x3_fwd(hip_lib, N, H, W, Cin, Cout, cfg):
     from distributedpytorch_amd.ops import kernels as K
@@ -100,7 +104,9 @@ def test_conv3x3_fwd(hip_lib, N, H, W, Cin, Cout, cfg):
     (2, 13, 18, 32, 64, "auto"), (1, 8, 8, 256, 128, "auto"), (2, 16, 16, 64, 32, "auto"),
     (2, 3, 256, 32, 32, "stream"), (1, 3, 256, 64, 32, "halo"), (1, 2, 128, 32, 64, "stream"),
     (1, 35, 128, 64, 64, "stream"), (2, 3, 256, 32, 32, "generic"), (2, 5, 64, 32, 32, "stream"),
-    (1, 4, 192, 64, 64, "stream")])
+    (1, 4, 192, 64, 64, "stream"),
+    # ragged rows
+    (1, 4, 240, 128, 64, "halo"), (2, 3, 96, 64, 32, "stream"), (1, 3, 120, 128, 128, "auto")])
 def test_conv3x3_dgrad_masked(hip_lib, N, H, W, Cin, Cout, path):
     from distributedpytorch_amd.ops import kernels as K
     torch.manual_seed(1)
@@ -212,7 +218,10 @@ def test_deconv_dgrad_from_concat(hip_lib, N, h, w, Cin, Cout):
     # 32-pixel strips (the 32x32 bottleneck): W % 64 != 0
     (2, 5, 32, 32, 32, None, "stream"), (1, 33, 32, 64, 128, None, "stream"), (2, 3, 96, 128, 64, None, "stream"),
     # first layer through the streaming wgrad (8 padded input channels in a 16-wide tile)
-    (2, 5, 128, 3, 32, 8, "stream"), (1, 66, 64, 3, 32, 8, "stream")])
+    (2, 5, 128, 3, 32, 8, "stream"), (1, 66, 64, 3, 32, 8, "stream"),
+    # ragged rows (partial last strip: out-of-row gradient pixels read as zeros)
+    (1, 5, 240, 128, 64, None, "stream"), (2, 3, 120, 64, 128, None, "stream"), (1, 4, 60, 128, 128, None, "stream"),
+    (2, 5, 200, 3, 32, 8, "stream"), (1, 3, 480, 64, 64, None, "stream")])
 def test_conv3x3_wgrad(hip_lib, N, H, W, Cin, Cout, cin_pad, path):
     from distributedpytorch_amd.ops import kernels as K
     torch.manual_seed(4)
@@ -363,7 +372,8 @@ def test_input_conversion(hip_lib):
     assert _rel(_nchw(y[..., :3].contiguous()), _bf(x)) == 0.0
 
 
-@pytest.mark.parametrize("N,H,W,Cin,Cout", [(2, 34, 128, 32, 32), (1, 9, 128, 64, 64), (1, 6, 256, 32, 64)])
+@pytest.mark.parametrize("N,H,W,Cin,Cout", [(2, 34, 128, 32, 32), (1, 9, 128, 64, 64), (1, 6, 256, 32, 64),
+                                          (1, 6, 96, 32, 32), (2, 5, 240, 64, 64)])     # ragged rows
 def test_conv_fused_maxpool(hip_lib, N, H, W, Cin, Cout):
     """Encoder conv2 writes its output into the concat buffer AND its 2x2 max-pool in one pass."""
     from distributedpytorch_amd.ops import kernels as K
@@ -451,7 +461,8 @@ def test_stream_pool_codes_match_maxpool(hip_lib):
 
 
 @pytest.mark.parametrize("N,H,W,Cin,Cout,path", [(2, 3, 256, 64, 32, "stream"), (1, 4, 128, 128, 64, "halo"),
-                                                 (2, 9, 13, 256, 128, "glds"), (2, 9, 13, 128, 64, "generic")])
+                                                 (2, 9, 13, 256, 128, "glds"), (2, 9, 13, 128, 64, "generic"),
+                                                 (2, 3, 96, 64, 32, "stream"), (1, 4, 240, 128, 64, "halo")])
 def test_dgrad_split_output(hip_lib, N, H, W, Cin, Cout, path):
     """Split output (concat gradient as two dense tensors) == the interleaved output's halves."""
     from distributedpytorch_amd.ops import kernels as K
@@ -470,7 +481,7 @@ def test_dgrad_split_output(hip_lib, N, H, W, Cin, Cout, path):
     assert torch.equal(lo, full[..., :s]) and torch.equal(hi, full[..., s:])
 
 
-@pytest.mark.parametrize("N,H,W", [(2, 7, 128), (1, 33, 256)])
+@pytest.mark.parametrize("N,H,W", [(2, 7, 128), (1, 33, 256), (2, 5, 96), (1, 3, 960)])
 def test_stream_conv_fused_head(hip_lib, N, H, W):
     """Last decoder conv with the segmentation head + loss partial sums in its epilogue == conv, then
     the separate head kernel on the stored output (same bf16 values)."""
@@ -526,3 +537,42 @@ def test_conv3x3_halo_two_rows(hip_lib, N, H, W, Cin, Cout, hcfg):
     assert _rel(_nchw(y), ref) < 2e-2
     if Cin % bc == 0:
         assert _rel(_nchw(dx), xr.grad * (x > 0)) < 2e-2
+
+
+@pytest.mark.parametrize("path", ["stream", "halo", "wgrad"])
+def test_per_image_launch_beyond_2gib(hip_lib, path):
+    """The row-streaming / row-halo kernels bind one image per block (64-bit image base, 32-bit
+    offsets inside it), so a batch whose activations exceed the 2 GiB buffer range runs as ONE
+    launch: the images past 2 GiB must equal the same images run as a small batch."""
+    from distributedpytorch_amd.ops import kernels as K
+    torch.manual_seed(12)
+    if path == "halo":
+        N, H, W, Cin, Cout = 132, 128, 512, 128, 64       # x: 2.2 GB
+    else:
+        N, H, W, Cin, Cout = 132, 256, 512, 64, 32        # x: 2.2 GB (concat-sized input)
+    x = torch.randn(N, H, W, Cin, device="cuda").to(torch.bfloat16)
+    assert x.numel() * 2 > 2 ** 31
+    w = torch.randn(Cout, Cin, 3, 3) * (2.0 / (9 * Cin)) ** 0.5
+    if path == "wgrad":
+        g = torch.randn(N, H, W, Cout, device="cuda").to(torch.bfloat16)
+        gw = torch.zeros(Cout * Cin * 9, device="cuda")
+        K.wgrad(g, x, kind=0, grid=(N, H, W), M=Cout, Nc=Cin, s=1, pad=1, KW=3, gw=gw, gb=None, Nreal=Cin, path="stream")
+        tail = slice(N - 3, N)
+        gw2 = torch.zeros_like(gw)
+        K.wgrad(g[tail].contiguous(), x[tail].contiguous(), kind=0, grid=(3, H, W), M=Cout, Nc=Cin, s=1, pad=1, KW=3,
+                gw=gw2, gb=None, Nreal=Cin, path="stream")
+        gw3 = torch.zeros_like(gw)
+        K.wgrad(g[:N - 3].contiguous(), x[:N - 3].contiguous(), kind=0, grid=(N - 3, H, W), M=Cout, Nc=Cin, s=1,
+                pad=1, KW=3, gw=gw3, gb=None, Nreal=Cin, path="stream")
+        torch.cuda.synchronize()
+        assert _rel(gw, gw2 + gw3) < 1e-3
+        return
+    packed, ng, kp = _pack_one(0, w)
+    y = torch.empty(N, H, W, Cout, dtype=torch.bfloat16, device="cuda")
+    kw = dict(Ngemm=ng, Kpad=kp, KH=3, KW=3, stride=1, pad=1, Cs=Cin, relu=True, path=path)
+    K.igemm(x, packed, y, out_grid=(N, H, W), **kw)
+    tail = x[N - 2:].contiguous()
+    y2 = torch.empty(2, H, W, Cout, dtype=torch.bfloat16, device="cuda")
+    K.igemm(tail, packed, y2, out_grid=(2, H, W), **kw)
+    torch.cuda.synchronize()
+    assert torch.equal(y[N - 2:], y2)

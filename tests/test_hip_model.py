@@ -12,7 +12,10 @@ def _cos(a, b):
     return (a @ b / (a.norm() * b.norm()).clamp_min(1e-30)).item()
 
 
-@pytest.mark.parametrize("name,hw", [("unet", (64, 64)), ("unet", (48, 80)), ("unet-xl", (64, 64)), ("unet", (64, 256))])
+@pytest.mark.parametrize("name,hw", [("unet", (64, 64)), ("unet", (48, 80)), ("unet-xl", (64, 64)), ("unet", (64, 256)),
+                                     # the reference's 640x960 aspect (utils/train_utils.py:26): deep levels
+                                     # not multiples of 32 (15 / 7.5 / ... strips), ragged row tiles
+                                     ("unet", (160, 240)), ("unet", (320, 480))])
 def test_hip_unet_matches_torch_fp32(hip_lib, name, hw):
     from distributedpytorch_amd.compute import loss_from_partials, make_compute
     from distributedpytorch_amd.loss import bce_dice_from_probs
