@@ -267,8 +267,10 @@ class HipBlocks:
         if out is None:
             out = torch.empty(N, H, W, c.Cin, dtype=torch.bfloat16, device=g.device)
         stats = [] if (below is not None and below.bn is not None) else None
+        # a persistent GEMM grid assumes it owns every CU; with side-stream weight gradients in flight
+        # it would wait for them (profiles/hip_b256_512_timeline_r02_end.txt: 3.0-3.3 ms vs 0.4-0.8 alone)
         K.igemm(g, self.wd(c), out, Ngemm=c.Cin, Kpad=c.Kd, KH=3, KW=3, stride=1, pad=1, Cs=c.Cout,
-                out_grid=(N, H, W), mask=mask, bn_stats=stats)
+                out_grid=(N, H, W), mask=mask, bn_stats=stats, persistent=not self._side_pending)
         return out if below is None else (out, stats)
 
     def conv_dgrad_split(self, c: _Conv, g: torch.Tensor, split: int):
@@ -279,7 +281,7 @@ class HipBlocks:
         lo = torch.empty(N, H, W, split, dtype=torch.bfloat16, device=g.device)
         hi = torch.empty(N, H, W, c.Cin - split, dtype=torch.bfloat16, device=g.device)
         K.igemm(g, self.wd(c), lo, Ngemm=c.Cin, Kpad=c.Kd, KH=3, KW=3, stride=1, pad=1, Cs=c.Cout,
-                out_grid=(N, H, W), y2=hi, split=split)
+                out_grid=(N, H, W), y2=hi, split=split, persistent=not self._side_pending)
         return lo, hi
 
     def _side_launch(self, fn, *keep: torch.Tensor):
@@ -402,7 +404,7 @@ class HipBlocks:
                     out_grid=(N, h, w), mask=x)
             return dx
         K.igemm(gup, self.wd(d), dx, Ngemm=d.Cin, Kpad=d.Kd, KH=2, KW=2, stride=2, pad=0, Cs=d.Cout,
-                out_grid=(N, h, w), mask=x)
+                out_grid=(N, h, w), mask=x, persistent=not self._side_pending)
         return dx
 
     def deconv_wgrad(self, d: _Deconv, gup: torch.Tensor, x: torch.Tensor):

@@ -128,6 +128,12 @@ USE_FUSED_POOL_BWD = USE_FUSED_BWD and os.environ.get("DPA_NO_FUSED_POOL_BWD", "
 USE_FUSED_W1 = USE_FUSED_POOL_BWD and os.environ.get("DPA_FUSED_W1", "0") == "1"
 
 
+# TIMING ABLATION ONLY (numerically wrong results): DPA_ABLATE=halo,glds,... skips the launches of the
+# listed kernel families so a bench run measures how much of the step they cost end to end
+# (tools/gpu_ablate.sh); categories: stream, halo, glds, wgrad, wgrad_deep, bwd, deconv
+_ABLATE = frozenset(v for v in os.environ.get("DPA_ABLATE", "").split(",") if v)
+
+
 def _extent_bytes(N, H, W, C, ld):
     return ((N * H * W - 1) * ld + C) * 2
 
@@ -144,7 +150,7 @@ def igemm(x: torch.Tensor, wpacked: torch.Tensor, y: torch.Tensor, *, Ngemm: int
           mask: Optional[torch.Tensor] = None, mode: int = 0, Cout: int = 0, accumulate: bool = False, cfg: int = 0,
           path: str = "auto", pool: Optional[torch.Tensor] = None, variant: int = 0,
           pcode: Optional[torch.Tensor] = None, y2: Optional[torch.Tensor] = None, split: int = 0, head=None,
-          bn_stats: Optional[list] = None):
+          bn_stats: Optional[list] = None, persistent: bool = True):
     """Implicit-GEMM conv.  ``out_grid`` = (N, Ho, Wo) pixel grid of GEMM-M.
 
     ``path``: ``auto`` picks, for a conv3x3, the row-streaming kernel (Ngemm, Cs in {32, 64}), then the
@@ -160,7 +166,10 @@ def igemm(x: torch.Tensor, wpacked: torch.Tensor, y: torch.Tensor, *, Ngemm: int
     ``bn_stats`` (an empty list): when the streaming kernel runs, its epilogue also writes per-block
     channel partial sums and the list receives (slab [rows][2][Ngemm] fp32, rows); left empty
     otherwise.  Without ``mask`` (conv followed by BatchNorm): sum y, sum y^2 for :func:`bn_fwd`;
-    with ``mask`` = the BN layer's output (dgrad into it): sum g, sum g*mask for :func:`bn_bwd`."""
+    with ``mask`` = the BN layer's output (dgrad into it): sum g, sum g*mask for :func:`bn_bwd`.
+    ``persistent=False``: the LDS-DMA path never picks its persistent (one workgroup per CU) kernel --
+    the backward passes it while side-stream weight gradients hold CUs, which a persistent grid
+    sized for the whole chip would otherwise wait for."""
     N, Hs, Ws, Cx, ldx = _nhwc(x, "igemm.x")
     _, _, _, Cy, ldy = _nhwc(y, "igemm.y")
     No, Ho, Wo = out_grid
@@ -244,6 +253,12 @@ def igemm(x: torch.Tensor, wpacked: torch.Tensor, y: torch.Tensor, *, Ngemm: int
         # not fusable here: the BN pass computes the statistics (the same epilogue in the row-halo
         # kernel measured 4% slower end to end: its extra registers cost more than the pass it saves)
         bslab = None
+    if _ABLATE and path == "auto":
+        fam = ("stream" if (a is not None and USE_STREAM and conv3 and stream_ok) else
+               "halo" if (a is not None and USE_HALO and conv3 and Cs % 32 == 0 and Ngemm <= 128) else
+               "glds" if (USE_GLDS and cfg == 0 and Cs % 64 == 0 and Kpad % 64 == 0 and Ngemm % 128 == 0) else "generic")
+        if fam in _ABLATE:
+            return
     if a is not None and (path == "stream" or (path == "auto" and USE_STREAM and conv3 and stream_ok)):
         if pool is not None:
             a.pool, a.ldp = pool.data_ptr(), ldp
@@ -269,7 +284,8 @@ def igemm(x: torch.Tensor, wpacked: torch.Tensor, y: torch.Tensor, *, Ngemm: int
     for n0, n1 in ([] if done else _image_chunks(N, max(Hs * Ws * ldx, (4 if mode else 1) * Ho * Wo * ldy) * 2)):
         a = args(n0, n1, False)
         if path == "glds" or (path == "auto" and glds_ok):
-            err = L.dpa_igemm_glds(ctypes.byref(a), c_int(variant if path == "glds" else 16 * GLDS_TAP_MAJOR + 32 * GLDS_NO_PERS + 64 * GLDS_NO_PRELOAD), st)
+            no_pers = GLDS_NO_PERS or not persistent
+            err = L.dpa_igemm_glds(ctypes.byref(a), c_int(variant if path == "glds" else 16 * GLDS_TAP_MAJOR + 32 * no_pers + 64 * GLDS_NO_PRELOAD), st)
             if err == 0:
                 continue
             if path == "glds":
@@ -300,6 +316,10 @@ def wgrad(A: torch.Tensor, B: torch.Tensor, *, kind: int, grid, M: int, Nc: int,
 
     ``path``: ``auto`` = row-streaming kernel when W % 64 == 0, else row-halo (W % 32 == 0), else the
     generic per-tap gather kernel; ``stream`` / ``halo`` / ``generic`` force one."""
+    if _ABLATE and ("wgrad" in _ABLATE or ("wgrad_deep" in _ABLATE and (M >= 128 or Nc >= 128))):
+        return
+    if (path == "rows" or (path == "auto" and wgrad_rows_eligible(M, Nc, grid[2]))) and kind == 0 and cfg == 0:
+        return _wgrad_rows(A, B, grid=grid, M=M, Nc=Nc, gw=gw, gb=gb, Nreal=Nreal)
     if path in ("auto", "stream") and kind == 0 and cfg == 0 and (USE_STREAM or path == "stream") \
             and grid[2] >= 8 and M % 32 == 0 and (Nc % 32 == 0 or Nc == 8):
         return _wgrad_stream(A, B, grid=grid, M=M, Nc=Nc, gw=gw, gb=gb, Nreal=Nreal)
@@ -353,6 +373,42 @@ def wgrad(A: torch.Tensor, B: torch.Tensor, *, kind: int, grid, M: int, Nc: int,
 
 
 WGRAD_STREAM_BLOCKS = int(os.environ.get("DPA_WGRAD_STREAM_BLOCKS", "2048"))
+# deep-layer weight gradients on the LDS-DMA row pipeline (csrc/wgrad_rows.hip): 128 x 64 x 9-tap
+# tiles.  Opt-in (DPA_WGRAD_ROWS=1): end to end equal to the row-streaming kernel at batch 256
+# (profiles/ab_wgrad_rows_b256_r03.txt); DPA_WGRAD_ROWS_DEPTH = row bundles in flight
+USE_WGRAD_ROWS = os.environ.get("DPA_WGRAD_ROWS", "0") == "1"
+WGRAD_ROWS_DEPTH = int(os.environ.get("DPA_WGRAD_ROWS_DEPTH", "2"))
+
+
+def wgrad_rows_eligible(M: int, Nc: int, W: int) -> bool:
+    return USE_WGRAD_ROWS and M % 128 == 0 and Nc % 64 == 0 and W >= 48
+
+
+def _wgrad_rows(A, B, *, grid, M, Nc, gw, gb, Nreal, rh: int = 0, depth: int = 0):
+    """conv3x3 weight (+bias) gradient of the deep layers (M = Cout % 128 == 0, Nc = Cin % 64 == 0):
+    one workgroup per (image, row segment, 64-pixel strip) x (128 x 64 channel tile), LDS-DMA rows."""
+    NA, HA, WA, CA, lda = _nhwc(A, "wgrad_rows.A")
+    NB, HB, WB, CB, ldb = _nhwc(B, "wgrad_rows.B")
+    N, Hg, Wg = grid
+    assert (HA, WA) == (Hg, Wg) == (HB, WB) and NA == NB == N and CA >= M and CB >= Nc
+    assert gw.dtype == torch.float32 and gw.is_contiguous() and gw.numel() == M * Nreal * 9
+    tiles = (M // 128) * (Nc // 64)
+    strips = -(-Wg // 64)
+    if rh <= 0:
+        # whole images per workgroup unless that leaves fewer than ~2 workgroups per CU
+        segs = max(1, min(Hg, -(-512 // max(1, N * strips * tiles))))
+        rh = -(-Hg // segs)
+    splits = N * -(-Hg // rh) * strips
+    slab = torch.empty(splits * 9 * M * Nc + splits * M, dtype=torch.float32, device=A.device)
+    bslab = slab[splits * 9 * M * Nc:] if gb is not None else None
+    a = WgradArgs(A.data_ptr(), B.data_ptr(), slab.data_ptr(), None if bslab is None else bslab.data_ptr(), lda, ldb,
+                  N, Hg, Wg, HA, WA, HB, WB, M, Nc, 1, 1, 3, 0, splits, _extent_bytes(1, HA, WA, CA, lda),
+                  _extent_bytes(1, HB, WB, CB, ldb))
+    L = _lib.lib()
+    st = _stream(A)
+    _check(L.dpa_wgrad_rows(ctypes.byref(a), c_int(rh), c_int(depth or WGRAD_ROWS_DEPTH), st), "wgrad_rows")
+    _check(L.dpa_wgrad_reduce(_p(slab), _p(bslab), _p(gw), _p(gb), c_int(splits), c_int(9), c_int(M), c_int(Nc),
+                              c_int(Nreal), c_int(0), st), "wgrad_reduce(rows)")
 
 
 def _wgrad_stream(A, B, *, grid, M, Nc, gw, gb, Nreal):
@@ -432,6 +488,13 @@ def conv_bwd_fused(g: Optional[torch.Tensor], x: torch.Tensor, wd: torch.Tensor,
     then never stored: the kernel accumulates the first conv's weight and bias gradients from it row
     by row, and the function returns None."""
     Nx, Hx, Wx, CI, ldx = _nhwc(x, "bwd.x")
+    if "bwd" in _ABLATE:
+        N_, H_, W_ = Nx, Hx, Wx
+        if w1 is not None:
+            return None
+        d1 = dx if dx is not None else torch.empty(N_, H_, W_, split if dx2 is not None else CI, dtype=torch.bfloat16,
+                                                   device=x.device)
+        return (d1, dx2) if dx2 is not None else d1
     if g is None:                       # pool mode without a skip gradient
         assert pool is not None
         N, H, W, CO, ldg = Nx, Hx, Wx, pool[0].shape[3], 0
@@ -660,6 +723,8 @@ def deconv_bwd_fused(gup: torch.Tensor, x: torch.Tensor, wd: torch.Tensor, gw: t
     assert wd.dtype == torch.bfloat16 and wd.numel() >= Cin * 4 * Cout
     assert gw.dtype == torch.float32 and gw.is_contiguous() and gw.numel() == Cin * Cout * 4
     dx = torch.empty(N, h, w, Cin, dtype=torch.bfloat16, device=x.device)
+    if "deconv" in _ABLATE:
+        return dx
     L = _lib.lib()
     st = _stream(x)
     for n0, n1 in _image_chunks(N, max(H2 * W2 * ldg, h * w * ldx) * 2):
@@ -689,6 +754,8 @@ def deconv_fwd_fused(x: torch.Tensor, wf: torch.Tensor, bias: Optional[torch.Ten
     assert wf.dtype == torch.bfloat16 and wf.numel() >= 4 * Cout * Cin
     if bias is not None:
         assert bias.dtype == torch.float32 and bias.numel() == Cout
+    if "deconv" in _ABLATE:
+        return
     L = _lib.lib()
     st = _stream(x)
     for n0, n1 in _image_chunks(N, max(H2 * W2 * ldy, h * w * ldx) * 2):

@@ -54,6 +54,8 @@ def main(argv=None):
     ap.add_argument("--out-dir", default=".")
     ap.add_argument("--model", default="unet")
     ap.add_argument("--backend", default="auto", choices=["auto", "hip", "torch"])
+    ap.add_argument("--dtype", default=None, choices=["bf16", "fp32"],
+                    help="compute dtype (default bf16 on a GPU, fp32 on CPU; fp32 selects the torch backend)")
     ap.add_argument("--seed", "-s", type=int, default=42)
     a = ap.parse_args(argv)
     H, W = (a.img_size[0], a.img_size[-1])
@@ -61,14 +63,24 @@ def main(argv=None):
     path = a.load or (os.path.join(a.out_dir, "checkpoints", f"{a.checkpoint}.pth") if a.checkpoint else None)
     if path:
         load_model_state(model, path)
-    ds = SyntheticSegmentation(a.synthetic_len, (H, W), 3, seed=a.seed) if a.synthetic else \
-        CarvanaDataset(os.path.join(a.data_dir, "train_hq"), os.path.join(a.data_dir, "train_masks"), newsize=(W, H))
-    _, val_set = split_dataset(ds, a.validation, seed=0)
     dev = "cuda:0" if torch.cuda.is_available() else "cpu"
-    cfg = TrainConfig(backend=a.backend, img_size=(H, W), dtype="bf16" if dev != "cpu" else "fp32")
+    dtype = a.dtype or ("bf16" if dev != "cpu" else "fp32")
+    cfg = TrainConfig(backend=a.backend, img_size=(H, W), dtype=dtype, synthetic=a.synthetic,
+                      synthetic_len=a.synthetic_len, seed=a.seed, val=a.validation, data_dir=a.data_dir)
     strat = SingleDevice(cfg, model, dev)
-    _, val_loader, _ = build_loaders(val_set, val_set, a.batch_size)
+    if a.synthetic and dev != "cpu":
+        # the SAME validation images train.py --synthetic held out (GPU-resident set, seed, split)
+        from distributedpytorch_amd.trainer import build_datasets
+        from distributedpytorch_amd.data.device import device_loaders
+        train_set, val_set = build_datasets(cfg, dev)
+        _, val_loader, _ = device_loaders(train_set, val_set, a.batch_size)
+    else:
+        ds = SyntheticSegmentation(a.synthetic_len, (H, W), 3, seed=a.seed) if a.synthetic else \
+            CarvanaDataset(os.path.join(a.data_dir, "train_hq"), os.path.join(a.data_dir, "train_masks"), newsize=(W, H))
+        _, val_set = split_dataset(ds, a.validation, seed=0)
+        _, val_loader, _ = build_loaders(val_set, val_set, a.batch_size)
     loss, dice = evaluate_strategy(strat, val_loader)
+    print(f"backend {strat.compute.name} dtype {dtype}")
     print(f"val_loss {loss:.5f} dice {dice:.4f} ({len(val_set)} images, checkpoint {path})")
     return loss, dice
 

@@ -221,7 +221,10 @@ def test_deconv_dgrad_from_concat(hip_lib, N, h, w, Cin, Cout):
     (2, 5, 128, 3, 32, 8, "stream"), (1, 66, 64, 3, 32, 8, "stream"),
     # ragged rows (partial last strip: out-of-row gradient pixels read as zeros)
     (1, 5, 240, 128, 64, None, "stream"), (2, 3, 120, 64, 128, None, "stream"), (1, 4, 60, 128, 128, None, "stream"),
-    (2, 5, 200, 3, 32, 8, "stream"), (1, 3, 480, 64, 64, None, "stream")])
+    (2, 5, 200, 3, 32, 8, "stream"), (1, 3, 480, 64, 64, None, "stream"),
+    # deep layers on the LDS-DMA row pipeline (128 x 64 x 9-tap tiles; ragged strips, row segments)
+    (2, 5, 64, 128, 128, None, "rows"), (1, 7, 120, 64, 128, None, "rows"), (2, 4, 128, 256, 256, None, "rows"),
+    (1, 3, 48, 64, 256, None, "rows"), (1, 66, 64, 128, 128, None, "rows"), (2, 9, 100, 192, 128, None, "rows")])
 def test_conv3x3_wgrad(hip_lib, N, H, W, Cin, Cout, cin_pad, path):
     from distributedpytorch_amd.ops import kernels as K
     torch.manual_seed(4)
@@ -576,3 +579,24 @@ def test_per_image_launch_beyond_2gib(hip_lib, path):
     K.igemm(tail, packed, y2, out_grid=(2, H, W), **kw)
     torch.cuda.synchronize()
     assert torch.equal(y[N - 2:], y2)
+
+
+@pytest.mark.parametrize("depth", [1, 2, 3])
+def test_wgrad_rows_pipeline_depths(hip_lib, depth):
+    """csrc/wgrad_rows.hip at every pipeline depth (row bundles in flight) and forced row segments:
+    the counted vmcnt waits and ring-buffer reuse must give the fp32 reference for each."""
+    from distributedpytorch_amd.ops import kernels as K
+    torch.manual_seed(13)
+    N, H, W, Cin, Cout = 2, 11, 96, 64, 128
+    x = _bf(torch.randn(N, Cin, H, W))
+    g = _bf(torch.randn(N, Cout, H, W))
+    wr = torch.zeros(Cout, Cin, 3, 3, requires_grad=True)
+    br = torch.zeros(Cout, requires_grad=True)
+    F.conv2d(x, wr, br, padding=1).backward(g)
+    for rh in (0, 1, 4):
+        gw = torch.zeros(Cout * Cin * 9, device="cuda")
+        gb = torch.zeros(Cout, device="cuda")
+        K._wgrad_rows(_nhwc(g), _nhwc(x), grid=(N, H, W), M=Cout, Nc=Cin, gw=gw, gb=gb, Nreal=Cin, rh=rh, depth=depth)
+        torch.cuda.synchronize()
+        assert _rel(gw.cpu().view(Cout, Cin, 3, 3), wr.grad) < 1e-2, (depth, rh)
+        assert _rel(gb.cpu(), br.grad) < 1e-2, (depth, rh)
