@@ -63,6 +63,10 @@ struct WgradArgs {
   int s, pad, KW;       // tap-dependent operand is read at (h*s + kh - pad, w*s + kw - pad)
   int pix_per_split, splits;
   unsigned abytes, bbytes;  // addressable bytes of A / B (< 2^31; the host splits larger batches)
+  // optional per-image base pointers (device arrays of N entries): image n of A / B starts at
+  // atab[n] / btab[n] instead of A / B + n * image size -- one weight-gradient launch over the images
+  // of several tensors of the same per-image layout (the microbatches of a pipeline stage)
+  const bf16_t* const* atab; const bf16_t* const* btab;
 };
 
 // 16-B LDS-DMA: lane l's bytes land at lds + 16*l.  (Wrapped in a __device__ function: used

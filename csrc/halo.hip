@@ -1139,8 +1139,8 @@ __global__ __launch_bounds__(192) void wgrad_stream_kernel(WgradArgs a, int ipb)
 
 #pragma unroll 1
   for (int im = 0; im < nimg; ++im, ++n) {
-  ar = __builtin_amdgcn_make_buffer_rsrc((void*)(a.A + (long)n * a.HA * a.WA * a.lda), 0, (int)a.abytes, 0x00020000);
-  br = __builtin_amdgcn_make_buffer_rsrc((void*)(a.B + (long)n * a.HB * a.WB * a.ldb), 0, (int)a.bbytes, 0x00020000);
+  ar = __builtin_amdgcn_make_buffer_rsrc((void*)(a.atab ? a.atab[n] : a.A + (long)n * a.HA * a.WA * a.lda), 0, (int)a.abytes, 0x00020000);
+  br = __builtin_amdgcn_make_buffer_rsrc((void*)(a.btab ? a.btab[n] : a.B + (long)n * a.HB * a.WB * a.ldb), 0, (int)a.bbytes, 0x00020000);
   // prologue: input rows h0-1, h0, h0+1 -> ring slots 0..2; gradient row h0 -> A buffer 0
   if (nrows > 0) {
 #pragma unroll 1

@@ -76,10 +76,10 @@ __global__ __launch_bounds__(768) void wgrad_rows_kernel(WgradArgs a, int rh) {
   const bool do_bias = a.bslab != nullptr && nt == 0;
 
   // one image per workgroup: 64-bit image bases, 32-bit offsets inside the image
-  const __amdgpu_buffer_rsrc_t ar =
-      __builtin_amdgcn_make_buffer_rsrc((void*)(a.A + (long)n * a.HA * a.WA * a.lda), 0, (int)a.abytes, 0x00020000);
-  const __amdgpu_buffer_rsrc_t br =
-      __builtin_amdgcn_make_buffer_rsrc((void*)(a.B + (long)n * a.HB * a.WB * a.ldb), 0, (int)a.bbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t ar = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(a.atab ? a.atab[n] : a.A + (long)n * a.HA * a.WA * a.lda), 0, (int)a.abytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t br = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(a.btab ? a.btab[n] : a.B + (long)n * a.HB * a.WB * a.ldb), 0, (int)a.bbytes, 0x00020000);
 
   // ---- DMA plan per row bundle: 16 gradient-row instructions (4 pixel rows x 16 chunks of 1 KB
   // each) and 9 input-row instructions (8 pixel rows x 8 chunks).  Wave w issues gradient

@@ -137,6 +137,16 @@ class HipBlocks:
         self.dense_skips = set()
         self._fusable = {}
         self._head_pending = None   # (placeholder grad, y, target, dS): head backward deferred to the decoder
+        # pipeline microbatches: the side-stream conv weight gradients of every microbatch are deferred
+        # and run as ONE launch per layer over all microbatches' images (K.wgrad_multi) -- one split-K
+        # slab set and reduction per step instead of one per microbatch.  Flushed at the end of the
+        # autograd backward (queue_callback), or by the pipeline when it opened a window (GPipeDist
+        # back-propagates microbatch by microbatch); readiness announcements wait for the flush.
+        self.defer_wgrad = False
+        self._defer_window = False
+        self._deferred = {}
+        self._deferred_ready = []
+        self._flush_queued = False
 
     # ------------------------------------------------------------------ weight packing
     def _build_packing(self):
@@ -367,6 +377,14 @@ class HipBlocks:
 
     def conv_wgrad(self, c: _Conv, g: torch.Tensor, x: torch.Tensor):
         N, H, W = g.shape[:3]
+        if self.defer_wgrad and K.wgrad_multi_eligible(c.Cout, c.Cs, W):
+            ent = self._deferred.setdefault(id(c), (c, [], []))
+            ent[1].append(g)
+            ent[2].append(x)
+            if not self._defer_window and not self._flush_queued:
+                torch.autograd.Variable._execution_engine.queue_callback(self.flush_wgrad)
+                self._flush_queued = True
+            return
         gw, gb = _grad(c.mod.weight), _grad(c.mod.bias)
         self._side_launch(lambda: K.wgrad(g, x, kind=0, grid=(N, H, W), M=c.Cout, Nc=c.Cs, s=1, pad=1, KW=3,
                                           gw=gw.view(-1), gb=gb, Nreal=c.Cin), g, x)
@@ -427,10 +445,34 @@ class HipBlocks:
         return self.deconv_dgrad(d, gup, x)
 
     def ready(self, mods):
+        if self.defer_wgrad and (self._deferred or self._defer_window):
+            self._deferred_ready.extend(mods)   # final only after flush_wgrad
+            return
         if self._side_pending:          # some of these gradients may still be in flight on the side stream
             self._ready_pending.extend(mods)
             return
         self._notify(mods)
+
+    def open_defer_window(self):
+        """Pipeline stage backward over several microbatches begins: defer until close_defer_window()."""
+        self._defer_window = self.defer_wgrad
+
+    def close_defer_window(self):
+        self._defer_window = False
+        self.flush_wgrad()
+
+    def flush_wgrad(self):
+        """Run the deferred weight gradients: one launch per layer over all deferred microbatches."""
+        self._flush_queued = False
+        deferred, self._deferred = self._deferred, {}
+        for c, gs, xs in deferred.values():
+            gw, gb = _grad(c.mod.weight), _grad(c.mod.bias)
+            self._side_launch(lambda c=c, gs=gs, xs=xs, gw=gw, gb=gb: K.wgrad_multi(
+                gs, xs, M=c.Cout, Nc=c.Cs, gw=gw.view(-1), gb=gb, Nreal=c.Cin), *gs, *xs)
+        self.join()
+        mods, self._deferred_ready = self._deferred_ready, []
+        if mods:
+            self._notify(mods)
 
     def _notify(self, mods):
         by_space = {}

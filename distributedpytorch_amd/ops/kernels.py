@@ -37,7 +37,7 @@ class WgradArgs(ctypes.Structure):
     _fields_ = [("A", c_void_p), ("B", c_void_p), ("slab", c_void_p), ("bslab", c_void_p)] + \
                [(n, c_int) for n in ("lda", "ldb", "N", "Hg", "Wg", "HA", "WA", "HB", "WB", "M", "Nc", "s", "pad",
                                      "KW", "pix_per_split", "splits")] + \
-               [("abytes", ctypes.c_uint), ("bbytes", ctypes.c_uint)]
+               [("abytes", ctypes.c_uint), ("bbytes", ctypes.c_uint), ("atab", c_void_p), ("btab", c_void_p)]
 
 
 class BwdArgs(ctypes.Structure):
@@ -380,17 +380,24 @@ USE_WGRAD_ROWS = os.environ.get("DPA_WGRAD_ROWS", "0") == "1"
 WGRAD_ROWS_DEPTH = int(os.environ.get("DPA_WGRAD_ROWS_DEPTH", "2"))
 
 
+def wgrad_multi_eligible(M: int, Nc: int, W: int) -> bool:
+    """Can :func:`wgrad_multi` take this conv3x3 weight gradient (row-streaming or row kernels)?"""
+    return (wgrad_rows_eligible(M, Nc, W) or (USE_STREAM and W >= 8 and M % 32 == 0 and (Nc % 32 == 0 or Nc == 8))) \
+        and "wgrad" not in _ABLATE
+
+
 def wgrad_rows_eligible(M: int, Nc: int, W: int) -> bool:
     return USE_WGRAD_ROWS and M % 128 == 0 and Nc % 64 == 0 and W >= 48
 
 
-def _wgrad_rows(A, B, *, grid, M, Nc, gw, gb, Nreal, rh: int = 0, depth: int = 0):
+def _wgrad_rows(A, B, *, grid, M, Nc, gw, gb, Nreal, rh: int = 0, depth: int = 0, tabs=None):
     """conv3x3 weight (+bias) gradient of the deep layers (M = Cout % 128 == 0, Nc = Cin % 64 == 0):
     one workgroup per (image, row segment, 64-pixel strip) x (128 x 64 channel tile), LDS-DMA rows."""
     NA, HA, WA, CA, lda = _nhwc(A, "wgrad_rows.A")
     NB, HB, WB, CB, ldb = _nhwc(B, "wgrad_rows.B")
     N, Hg, Wg = grid
-    assert (HA, WA) == (Hg, Wg) == (HB, WB) and NA == NB == N and CA >= M and CB >= Nc
+    assert (HA, WA) == (Hg, Wg) == (HB, WB) and CA >= M and CB >= Nc
+    assert (NA == NB == N) or (tabs is not None and tabs[0].numel() == tabs[1].numel() == N)
     assert gw.dtype == torch.float32 and gw.is_contiguous() and gw.numel() == M * Nreal * 9
     tiles = (M // 128) * (Nc // 64)
     strips = -(-Wg // 64)
@@ -404,6 +411,8 @@ def _wgrad_rows(A, B, *, grid, M, Nc, gw, gb, Nreal, rh: int = 0, depth: int = 0
     a = WgradArgs(A.data_ptr(), B.data_ptr(), slab.data_ptr(), None if bslab is None else bslab.data_ptr(), lda, ldb,
                   N, Hg, Wg, HA, WA, HB, WB, M, Nc, 1, 1, 3, 0, splits, _extent_bytes(1, HA, WA, CA, lda),
                   _extent_bytes(1, HB, WB, CB, ldb))
+    if tabs is not None:
+        a.atab, a.btab = tabs[0].data_ptr(), tabs[1].data_ptr()
     L = _lib.lib()
     st = _stream(A)
     _check(L.dpa_wgrad_rows(ctypes.byref(a), c_int(rh), c_int(depth or WGRAD_ROWS_DEPTH), st), "wgrad_rows")
@@ -411,11 +420,39 @@ def _wgrad_rows(A, B, *, grid, M, Nc, gw, gb, Nreal, rh: int = 0, depth: int = 0
                               c_int(Nreal), c_int(0), st), "wgrad_reduce(rows)")
 
 
-def _wgrad_stream(A, B, *, grid, M, Nc, gw, gb, Nreal):
+def _image_table(ts, C_min: int, name: str):
+    """Device array of per-image base pointers over the images of tensors ``ts`` (same H, W, ld)."""
+    ptrs, geo = [], None
+    for t in ts:
+        n, h, w, c, ld = _nhwc(t, name)
+        assert c >= C_min and (geo is None or geo == (h, w, ld)), f"{name}: images of different layouts"
+        geo = (h, w, ld)
+        ptrs.extend(t.data_ptr() + i * h * w * ld * 2 for i in range(n))
+    return torch.tensor(ptrs, dtype=torch.int64, device=ts[0].device), len(ptrs)
+
+
+def wgrad_multi(As, Bs, *, M: int, Nc: int, gw: torch.Tensor, gb: Optional[torch.Tensor], Nreal: int):
+    """conv3x3 weight (+bias) gradient over the images of several (gradient, input) tensor pairs in
+    ONE launch -- the microbatches of a pipeline stage: one split-K slab set and one reduction for
+    the whole batch instead of one per microbatch.  Accumulates into gw / gb."""
+    assert len(As) == len(Bs) and As
+    N = sum(a.shape[0] for a in As)
+    _, H, W, _, _ = _nhwc(As[0], "wgrad_multi.A")
+    atab, na = _image_table(As, M, "wgrad_multi.A")
+    btab, nb = _image_table(Bs, Nc, "wgrad_multi.B")
+    assert na == nb == N
+    tabs = (atab, btab)
+    if wgrad_rows_eligible(M, Nc, W):
+        return _wgrad_rows(As[0], Bs[0], grid=(N, H, W), M=M, Nc=Nc, gw=gw, gb=gb, Nreal=Nreal, tabs=tabs)
+    return _wgrad_stream(As[0], Bs[0], grid=(N, H, W), M=M, Nc=Nc, gw=gw, gb=gb, Nreal=Nreal, tabs=tabs)
+
+
+def _wgrad_stream(A, B, *, grid, M, Nc, gw, gb, Nreal, tabs=None):
     NA, HA, WA, CA, lda = _nhwc(A, "wgrad.A")
     NB, HB, WB, CB, ldb = _nhwc(B, "wgrad.B")
     N, Hg, Wg = grid
-    assert (HA, WA) == (Hg, Wg) == (HB, WB) and NA == NB == N and CA >= M and CB >= Nc
+    assert (HA, WA) == (Hg, Wg) == (HB, WB) and CA >= M and CB >= Nc
+    assert (NA == NB == N) or (tabs is not None and tabs[0].numel() == tabs[1].numel() == N)
     assert gw.dtype == torch.float32 and gw.is_contiguous() and gw.numel() == M * Nreal * 9
     if Nc == 8:            # first layer (RGB padded to 8 channels): 32x16 tile, half the columns zero
         hcfg = 4
@@ -445,12 +482,17 @@ def _wgrad_stream(A, B, *, grid, M, Nc, gw, gb, Nreal):
     a = WgradArgs(A.data_ptr(), B.data_ptr(), slab.data_ptr(), None if bslab is None else bslab.data_ptr(), lda, ldb,
                   nb, Hg, Wg, HA, WA, HB, WB, M, Nc, 1, 1, 3, 0, splits, _extent_bytes(1, HA, WA, CA, lda),
                   _extent_bytes(1, HB, WB, CB, ldb))
+    if tabs is not None:
+        a.atab, a.btab = tabs[0].data_ptr(), tabs[1].data_ptr()
     _check(L.dpa_wgrad_stream(ctypes.byref(a), c_int(hcfg), c_int(bp), c_int(rh), c_int(ipb), st), "wgrad_stream")
     _check(L.dpa_wgrad_reduce(_p(slab), _p(bslab), _p(gw), _p(gb), c_int(splits), c_int(9), c_int(M), c_int(Nc),
                               c_int(Nreal), c_int(0), st), "wgrad_reduce")
 
 
 # ------------------------------------------------------------------------------- fused conv backward
+# minimum workgroups of a fused backward launch (image column strips are split into row segments
+# below it); more segments = more fp32 weight-gradient slab rows to reduce
+BWD_BLOCKS = int(os.environ.get("DPA_BWD_BLOCKS", "1024"))
 def bwd_fused_eligible(ci: int, co: int, W: int) -> bool:
     """csrc/bwd_stream.hip serves conv3x3 s1 p1 with (Cin, Cout) in {32, 64}^2 and W % strip == 0."""
     bp = ctypes.c_int(0)
@@ -464,7 +506,7 @@ def bwd_pool_foldable(ci: int, co: int) -> bool:
 
 def conv_bwd_fused(g: Optional[torch.Tensor], x: torch.Tensor, wd: torch.Tensor, Kd: int, gw: torch.Tensor,
                    gb: Optional[torch.Tensor], *, mask: bool, dx: Optional[torch.Tensor] = None,
-                   dx2: Optional[torch.Tensor] = None, split: int = 0, target_blocks: int = 1024, head=None,
+                   dx2: Optional[torch.Tensor] = None, split: int = 0, target_blocks: int = 0, head=None,
                    pool=None, w1=None):
     """Backward of ``y = conv3x3(x) (+bias)`` in one pass (csrc/bwd_stream.hip): returns
     ``dx = conv3x3^T(g)`` (times ``x > 0`` when ``mask``; with ``dx2``/``split`` the channels
@@ -528,7 +570,7 @@ def conv_bwd_fused(g: Optional[torch.Tensor], x: torch.Tensor, wd: torch.Tensor,
     assert dx is None or tuple(dx.shape[:3]) == (N, H, W)
     strips = W // bp.value
     # whole image columns per block; split the rows only when the batch gives too few blocks
-    segs = max(1, min(H, -(-target_blocks // max(1, N * strips))))
+    segs = max(1, min(H, -(-(target_blocks or BWD_BLOCKS) // max(1, N * strips))))
     rh = -(-H // segs)
     nblk = N * strips * (-(-H // rh))
     slab = torch.empty(nblk * pg * 9 * CO * CI + (nblk * pg * CO if gb is not None else 0), dtype=torch.float32,

@@ -171,6 +171,9 @@ class GPipeDist:
                 p.requires_grad_(False)
         self.space = FlatParameterSpace(own, device=self.device)
         self.blocks = make_blocks(model, backend, dtype)
+        # microbatches: one weight-gradient launch per layer per step (HIP engine, see HipBlocks)
+        if hasattr(self.blocks, "defer_wgrad"):
+            self.blocks.defer_wgrad = microbatches > 1
         if hasattr(self.blocks, "dense_skips"):
             self.blocks.dense_skips = {int(n[len("skip"):]) for n, _ in self.send_spec[self.rank]
                                        if n.startswith("skip")}
@@ -354,6 +357,8 @@ class GPipeDist:
             (loss * loss_scale).backward()
             dP = P.grad
         gnxt = self._irecv_grads(saved_out[M - 1]) if not self.is_last else None
+        if hasattr(self.blocks, "open_defer_window"):
+            self.blocks.open_defer_window()     # the microbatches' weight gradients: one launch per layer
         for m in reversed(range(M)):
             rng = trace_range(f"stage{self.rank}_bwd_mb{m}")
             rng.__enter__()
@@ -377,6 +382,8 @@ class GPipeDist:
                     gsends.append((gr, src))
                 pending.append(self._post(sends=gsends))
             saved_in[m] = saved_out[m] = None
+        if hasattr(self.blocks, "close_defer_window"):
+            self.blocks.close_defer_window()
         for xfer in pending:
             xfer.wait()
         return loss
@@ -469,6 +476,8 @@ class GPipeLocal:
                              for s in range(self.S)]
         for s, b in enumerate(self.stage_blocks):
             b.device = self.devices[s]
+            if hasattr(b, "defer_wgrad"):      # one weight-gradient launch per layer per step (HipBlocks)
+                b.defer_wgrad = microbatches > 1
         # skips between stages: engines on the SAME device share one concat-buffer registry (the decoder
         # stage finds the encoder's concat buffer: zero-copy, as in a single-stage run); a skip that
         # changes device is written dense by its producer (one peer copy into the consumer's buffer)

@@ -77,7 +77,10 @@ def test_halo_igemm_rejects(L, kw):
     assert L.dpa_igemm_halo(ctypes.byref(_igemm_args(**kw)), 0, None) == INVALID
 
 
-@pytest.mark.parametrize("kw", [dict(Wo=96, Ws=96), dict(mode=1), dict(pad=0), dict(Kpad=256), dict(Ngemm=128, Kpad=288)])
+# any row width >= 16 streams (a ragged last strip is masked); narrower rows and a fused pool over an
+# odd width (half a 2x2 window) are rejected
+@pytest.mark.parametrize("kw", [dict(Wo=8, Ws=8), dict(mode=1), dict(pad=0), dict(Kpad=256), dict(Ngemm=128, Kpad=288),
+                                dict(Wo=97, Ws=97, pool=16, ldp=32)])
 def test_stream_igemm_rejects(L, kw):
     assert L.dpa_igemm_stream(ctypes.byref(_igemm_args(**kw)), 0, None) == INVALID
 
