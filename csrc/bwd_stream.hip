@@ -115,7 +115,7 @@ __global__ __launch_bounds__(64 * NW, 2) void bwd_stream_kernel(BwdArgs a) {
   char* const X1ring = Xring + 4 * XSLOT;
   char* const G1buf = X1ring + 5 * X1SLOT;
 
-  const int stripsW = a.W / BP, segsH = (a.H + a.rh - 1) / a.rh;
+  const int stripsW = (a.W + BP - 1) / BP, segsH = (a.H + a.rh - 1) / a.rh;   // ragged last strip allowed
   const int split_id = blockIdx.x;
   const int ig = split_id / (segsH * stripsW);
   const int rem = split_id - ig * segsH * stripsW;
@@ -333,7 +333,9 @@ __global__ __launch_bounds__(64 * NW, 2) void bwd_stream_kernel(BwdArgs a) {
       const int c0 = wc * WCN + ic * 16 + 4 * chunk;
       moff[ip][ic] = (px + 1) * RBX + (((c0 >> 3) ^ swz_kk<RBX>(px + 1)) << 4) + ((c0 >> 2) & 1) * 8;
       hi[ip][ic] = EPI == 1 && c0 >= a.split;
-      yoff[ip][ic] = hi[ip][ic] ? (unsigned)(((w0 + px) * a.ldy2 + c0 - a.split) * 2)
+      // pixels past the row (ragged last strip): offset past the range check, the store is dropped
+      yoff[ip][ic] = w0 + px >= a.W ? 0x80000000u
+                   : hi[ip][ic] ? (unsigned)(((w0 + px) * a.ldy2 + c0 - a.split) * 2)
                                 : (unsigned)(((w0 + px) * a.ldy + c0) * 2);
     }
   const unsigned yrowb = (unsigned)(a.W * a.ldy * 2), y2rowb = (unsigned)(a.W * (EPI == 1 ? a.ldy2 : a.ldy) * 2);
@@ -621,7 +623,7 @@ __global__ __launch_bounds__(64 * NW, 2) void bwd_stream_kernel(BwdArgs a) {
 
 template <int BP, int CI, int CO, int NW, int PG, int EPI, bool HEAD = false, bool POOL = false, bool W1 = false>
 static int launch_bwd_stream(const BwdArgs& a, hipStream_t st) {
-  const int blocks = ((a.N + a.ipb - 1) / a.ipb) * ((a.H + a.rh - 1) / a.rh) * (a.W / BP);
+  const int blocks = ((a.N + a.ipb - 1) / a.ipb) * ((a.H + a.rh - 1) / a.rh) * ((a.W + BP - 1) / BP);
   hipLaunchKernelGGL((bwd_stream_kernel<BP, CI, CO, NW, PG, EPI, HEAD, POOL, W1>), dim3(blocks), dim3(64 * NW), 0, st, a);
   return (int)hipGetLastError();
 }
@@ -654,7 +656,11 @@ DPA_API int dpa_bwd_stream_geom(int ci, int co, int* bp) {
 DPA_API int dpa_bwd_stream(const BwdArgs* args, int ci, int co, int epi, hipStream_t st) {
   const BwdArgs& a = *args;
   int bp = 0, nw = 0;
-  if (!bwd_cfg(ci, co, &bp, &nw) || a.W % bp || (a.ldg & 7) || (a.ldx & 7) || (a.ldy & 3) || a.rh < 1 || a.ipb < 1 ||
+  // a ragged last strip (W % bp != 0) is masked in the plain / split / masked modes; the fused pool,
+  // head and first-conv modes need whole strips
+  const bool fused_mode = a.pcode != nullptr || a.hslab != nullptr || a.x1 != nullptr;
+  if (!bwd_cfg(ci, co, &bp, &nw) || (fused_mode && a.W % bp) || a.W < 16 || (a.ldg & 7) || (a.ldx & 7) || (a.ldy & 3) ||
+      a.rh < 1 || a.ipb < 1 ||
       a.Kd < 9 * co || (epi == 1 && (a.y2 == nullptr || (a.ldy2 & 3) || a.split % 16 || a.split <= 0 || a.split >= ci)))
     return (int)hipErrorInvalidValue;
 #define DPA_BWD(CIv, COv, BPv, NWv, PGv)                                          \

@@ -310,16 +310,16 @@ class HipBlocks:
         self._keep.extend(keep)
         self._side_pending = True
 
-    def fusable(self, c: _Conv, below, W: int) -> bool:
+    def fusable(self, c: _Conv, below, W: int, whole: bool = False) -> bool:
         """The fused backward (dgrad + weight/bias gradient in one pass, csrc/bwd_stream.hip) serves
         this conv: 32/64 channels in and out, no BatchNorm around it (its backward needs the dgrad
         epilogue's statistics), image rows a multiple of the kernel's pixel strip."""
         if not (K.USE_FUSED_BWD and c.bn is None and (below is None or below.bn is None) and c.Cs == c.Cin):
             return False
-        key = (c.Cin, c.Cout, W)
+        key = (c.Cin, c.Cout, W, whole)
         ok = self._fusable.get(key)
         if ok is None:
-            ok = self._fusable[key] = K.bwd_fused_eligible(c.Cin, c.Cout, W)
+            ok = self._fusable[key] = K.bwd_fused_eligible(c.Cin, c.Cout, W, whole=whole)
         return ok
 
     def conv_bwd(self, c: _Conv, g, x: torch.Tensor, mask: bool, split: int = 0, head=None, pool=None, first=None):
@@ -373,7 +373,7 @@ class HipBlocks:
         """The head backward can be folded into the last decoder conv's fused backward."""
         c1, c2 = self.dec_convs[-1]
         return (K.USE_FUSED_HEAD_BWD and c2.Cin == 32 and c2.Cout == 32 and self.model.segmap.out_channels == 1
-                and self.fusable(c2, c1, W))
+                and self.fusable(c2, c1, W, whole=True))
 
     def conv_wgrad(self, c: _Conv, g: torch.Tensor, x: torch.Tensor):
         N, H, W = g.shape[:3]
@@ -612,7 +612,7 @@ class _EncFn(torch.autograd.Function):
             dpooled = _v(dpooled)
         dskip = None if dskip is None else _v(dskip)
         W = a.shape[2]
-        pool_fold = (ctx.has_code and K.USE_FUSED_POOL_BWD and B.fusable(c2, c1, W)
+        pool_fold = (ctx.has_code and K.USE_FUSED_POOL_BWD and B.fusable(c2, c1, W, whole=True)
                      and K.bwd_pool_foldable(c2.Cin, c2.Cout))
         if pool_fold and not ctx.x_needs_grad and K.USE_FUSED_W1 and c1.bn is None and c1.Cs == 8 \
                 and c1.Cout == 32 and x.is_contiguous():

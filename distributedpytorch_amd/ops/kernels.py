@@ -493,11 +493,18 @@ def _wgrad_stream(A, B, *, grid, M, Nc, gw, gb, Nreal, tabs=None):
 # minimum workgroups of a fused backward launch (image column strips are split into row segments
 # below it); more segments = more fp32 weight-gradient slab rows to reduce
 BWD_BLOCKS = int(os.environ.get("DPA_BWD_BLOCKS", "1024"))
-def bwd_fused_eligible(ci: int, co: int, W: int) -> bool:
-    """csrc/bwd_stream.hip serves conv3x3 s1 p1 with (Cin, Cout) in {32, 64}^2 and W % strip == 0."""
+def _strips_ok(W: int, bp: int) -> bool:
+    """Whole strips, or a ragged last one that keeps >= 85 % of the strip pixels useful."""
+    t = -(-W // bp)
+    return W >= 16 and (W % bp == 0 or W * 100 >= 85 * t * bp)
+
+
+def bwd_fused_eligible(ci: int, co: int, W: int, whole: bool = False) -> bool:
+    """csrc/bwd_stream.hip serves conv3x3 s1 p1 with (Cin, Cout) in {32, 64}^2; ``whole``: the fused
+    pool / head modes, which need W % strip == 0 (the plain modes mask a ragged last strip)."""
     bp = ctypes.c_int(0)
     pg = _lib.lib().dpa_bwd_stream_geom(c_int(ci), c_int(co), ctypes.byref(bp))
-    return pg > 0 and W % bp.value == 0
+    return pg > 0 and (W % bp.value == 0 if whole else _strips_ok(W, bp.value))
 
 
 def bwd_pool_foldable(ci: int, co: int) -> bool:
@@ -549,7 +556,8 @@ def conv_bwd_fused(g: Optional[torch.Tensor], x: torch.Tensor, wd: torch.Tensor,
     bp = ctypes.c_int(0)
     L = _lib.lib()
     pg = L.dpa_bwd_stream_geom(c_int(CI), c_int(CO), ctypes.byref(bp))
-    assert pg > 0 and W % bp.value == 0, f"fused backward not available for {CI}->{CO} at W={W}"
+    assert pg > 0 and (W % bp.value == 0 or (head is None and pool is None and w1 is None and _strips_ok(W, bp.value))), \
+        f"fused backward not available for {CI}->{CO} at W={W}"
     if dx2 is not None:
         assert 0 < split < CI and split % 16 == 0 and not mask
         if dx is None:
@@ -568,7 +576,7 @@ def conv_bwd_fused(g: Optional[torch.Tensor], x: torch.Tensor, wd: torch.Tensor,
         assert C1 >= CI
         ldy2, epi = 0, (0 if mask else 2)
     assert dx is None or tuple(dx.shape[:3]) == (N, H, W)
-    strips = W // bp.value
+    strips = -(-W // bp.value)
     # whole image columns per block; split the rows only when the batch gives too few blocks
     segs = max(1, min(H, -(-(target_blocks or BWD_BLOCKS) // max(1, N * strips))))
     rh = -(-H // segs)

@@ -17,6 +17,8 @@ pytestmark = pytest.mark.gpu
     (2, 6, 64, 64, 32, "split"), (1, 9, 128, 64, 32, "mask"),
     (2, 4, 64, 32, 64, "plain"), (1, 7, 192, 32, 64, "mask"),
     (2, 5, 64, 64, 64, "mask"), (1, 3, 128, 64, 64, "split"),
+    # ragged last strip (640x960 level widths 480 / 240): out-of-row pixels masked
+    (1, 5, 480, 64, 64, "mask"), (2, 4, 120, 32, 64, "plain"), (1, 3, 240, 64, 32, "split"), (2, 3, 60, 32, 32, "mask"),
 ])
 def test_conv_bwd_fused_matches_torch(hip_lib, N, H, W, Cin, Cout, epi):
     from distributedpytorch_amd.ops import kernels as K
