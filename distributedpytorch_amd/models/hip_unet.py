@@ -142,11 +142,13 @@ class HipBlocks:
         # slab set and reduction per step instead of one per microbatch.  Flushed at the end of the
         # autograd backward (queue_callback), or by the pipeline when it opened a window (GPipeDist
         # back-propagates microbatch by microbatch); readiness announcements wait for the flush.
-        self.defer_wgrad = False
+        self.defer_wgrad = 0          # microbatches per step whose weight gradients are merged (0/1: off)
         self._defer_window = False
         self._deferred = {}
         self._deferred_ready = []
         self._flush_queued = False
+        self.side2 = None             # stream of the merged (all-microbatch) weight-gradient launches
+        self._keep2 = []
 
     # ------------------------------------------------------------------ weight packing
     def _build_packing(self):
@@ -377,11 +379,16 @@ class HipBlocks:
 
     def conv_wgrad(self, c: _Conv, g: torch.Tensor, x: torch.Tensor):
         N, H, W = g.shape[:3]
-        if self.defer_wgrad and K.wgrad_multi_eligible(c.Cout, c.Cs, W):
+        if self.defer_wgrad > 1 and K.wgrad_multi_eligible(c.Cout, c.Cs, W):
             ent = self._deferred.setdefault(id(c), (c, [], []))
             ent[1].append(g)
             ent[2].append(x)
+            if len(ent[1]) >= self.defer_wgrad:
+                # every microbatch of this layer is in: launch now, so it overlaps the rest of the backward
+                del self._deferred[id(c)]
+                self._launch_multi(c, ent[1], ent[2])
             if not self._defer_window and not self._flush_queued:
+                # end of this backward: leftovers, the merged stream's join, the readiness announcements
                 torch.autograd.Variable._execution_engine.queue_callback(self.flush_wgrad)
                 self._flush_queued = True
             return
@@ -445,7 +452,7 @@ class HipBlocks:
         return self.deconv_dgrad(d, gup, x)
 
     def ready(self, mods):
-        if self.defer_wgrad and (self._deferred or self._defer_window):
+        if self.defer_wgrad > 1 and (self._deferred or self._defer_window or self._flush_queued):
             self._deferred_ready.extend(mods)   # final only after flush_wgrad
             return
         if self._side_pending:          # some of these gradients may still be in flight on the side stream
@@ -455,20 +462,34 @@ class HipBlocks:
 
     def open_defer_window(self):
         """Pipeline stage backward over several microbatches begins: defer until close_defer_window()."""
-        self._defer_window = self.defer_wgrad
+        self._defer_window = self.defer_wgrad > 1
 
     def close_defer_window(self):
         self._defer_window = False
         self.flush_wgrad()
 
+    def _launch_multi(self, c, gs, xs):
+        """One weight-gradient launch over the deferred microbatches of conv ``c``, on a stream of its
+        own: the per-block joins (side stream) must not wait for it, only flush_wgrad does."""
+        gw, gb = _grad(c.mod.weight), _grad(c.mod.bias)
+        if self.side2 is None:
+            self.side2 = torch.cuda.Stream(device=self.device, priority=K.SIDE_PRIORITY)
+        self.side2.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(self.side2):
+            K.wgrad_multi(gs, xs, M=c.Cout, Nc=c.Cs, gw=gw.view(-1), gb=gb, Nreal=c.Cin)
+        self._keep2.extend(gs)
+        self._keep2.extend(xs)
+
     def flush_wgrad(self):
-        """Run the deferred weight gradients: one launch per layer over all deferred microbatches."""
+        """Run the deferred weight gradients still waiting for microbatches (one launch per layer over
+        the ones that arrived), join the side stream, announce the gradients."""
         self._flush_queued = False
         deferred, self._deferred = self._deferred, {}
         for c, gs, xs in deferred.values():
-            gw, gb = _grad(c.mod.weight), _grad(c.mod.bias)
-            self._side_launch(lambda c=c, gs=gs, xs=xs, gw=gw, gb=gb: K.wgrad_multi(
-                gs, xs, M=c.Cout, Nc=c.Cs, gw=gw.view(-1), gb=gb, Nreal=c.Cin), *gs, *xs)
+            self._launch_multi(c, gs, xs)
+        if self._keep2:
+            torch.cuda.current_stream(self.device).wait_stream(self.side2)
+            self._keep2 = []
         self.join()
         mods, self._deferred_ready = self._deferred_ready, []
         if mods:

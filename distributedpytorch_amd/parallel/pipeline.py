@@ -173,7 +173,7 @@ class GPipeDist:
         self.blocks = make_blocks(model, backend, dtype)
         # microbatches: one weight-gradient launch per layer per step (HIP engine, see HipBlocks)
         if hasattr(self.blocks, "defer_wgrad"):
-            self.blocks.defer_wgrad = microbatches > 1
+            self.blocks.defer_wgrad = microbatches
         if hasattr(self.blocks, "dense_skips"):
             self.blocks.dense_skips = {int(n[len("skip"):]) for n, _ in self.send_spec[self.rank]
                                        if n.startswith("skip")}
@@ -477,7 +477,7 @@ class GPipeLocal:
         for s, b in enumerate(self.stage_blocks):
             b.device = self.devices[s]
             if hasattr(b, "defer_wgrad"):      # one weight-gradient launch per layer per step (HipBlocks)
-                b.defer_wgrad = microbatches > 1
+                b.defer_wgrad = microbatches
         # skips between stages: engines on the SAME device share one concat-buffer registry (the decoder
         # stage finds the encoder's concat buffer: zero-copy, as in a single-stage run); a skip that
         # changes device is written dense by its producer (one peer copy into the consumer's buffer)
