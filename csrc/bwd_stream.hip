@@ -174,6 +174,12 @@ __global__ __launch_bounds__(64 * NW, 2) void bwd_stream_kernel(BwdArgs a) {
     xsto[j] = c < XCH ? px * RBX + ((cc ^ swz_kk<RBX>(px)) << 4) : -1;
   }
   const unsigned growb = (unsigned)(a.W * a.ldg * 2), xrowb = (unsigned)(a.W * a.ldx * 2);
+  // ring rows are BP + 2 pixels, so the last register chunk of a row is live in one wave only: the
+  // other waves skip its (HEAD/POOL) gradient transform on a wave-uniform branch
+  const int wid_s = __builtin_amdgcn_readfirstlane(wid);
+  bool glive[LG];
+#pragma unroll
+  for (int j = 0; j < LG; ++j) glive[j] = wid_s * 64 + j * NT < GCH;
   // W1: one 16-B chunk (8 channels) per ring pixel
   const bool x1ok = W1 && tid < HR && w0 + tid - 1 >= 0 && w0 + tid - 1 < a.W;
   const unsigned x1off = (unsigned)((w0 + tid - 1) * 16), x1rowb = (unsigned)(a.W * 16);
@@ -225,9 +231,11 @@ __global__ __launch_bounds__(64 * NW, 2) void bwd_stream_kernel(BwdArgs a) {
     const bool rok = ih >= 0 && ih < a.H;                     // wave-uniform
     const unsigned gb = (unsigned)ih * growb, xb = (unsigned)ih * xrowb;
 #pragma unroll
-    for (int j = 0; j < LG; ++j) R.g[j] = __builtin_amdgcn_raw_buffer_load_b128(gr, (rok && gok[j]) ? gb + goff[j] : 0x80000000u, 0, 0);
+    for (int j = 0; j < LG; ++j)
+      R.g[j] = __builtin_amdgcn_raw_buffer_load_b128(gr, (rok && gok[j]) ? gb + goff[j] : 0x80000000u, 0, 0);
 #pragma unroll
-    for (int j = 0; j < LX; ++j) R.x[j] = __builtin_amdgcn_raw_buffer_load_b128(xr, (rok && xok[j]) ? xb + xoff[j] : 0x80000000u, 0, 0);
+    for (int j = 0; j < LX; ++j)
+      R.x[j] = __builtin_amdgcn_raw_buffer_load_b128(xr, (rok && xok[j]) ? xb + xoff[j] : 0x80000000u, 0, 0);
     if constexpr (W1) R.x1[0] = __builtin_amdgcn_raw_buffer_load_b128(x1r, (rok && x1ok) ? (unsigned)ih * x1rowb + x1off : 0x80000000u, 0, 0);
     if constexpr (HEAD) {
 #pragma unroll
@@ -248,6 +256,7 @@ __global__ __launch_bounds__(64 * NW, 2) void bwd_stream_kernel(BwdArgs a) {
     if constexpr (POOL) {                       // (dskip, dpool, code) chunk -> gradient chunk
 #pragma unroll
       for (int j = 0; j < LG; ++j) {
+        if (!glive[j]) continue;
         const unsigned q = (unsigned)((ih & 1) * 2) + pq[j];
         const u32x4_t ps = R.g[j], pd = R.pd[j];
         unsigned o[4];
@@ -268,6 +277,7 @@ __global__ __launch_bounds__(64 * NW, 2) void bwd_stream_kernel(BwdArgs a) {
       const bool rowv = ih >= h0 && ih < h0 + nrows;
 #pragma unroll
       for (int j = 0; j < LG; ++j) {
+        if (!glive[j]) continue;
         float yv[8];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -280,11 +290,10 @@ __global__ __launch_bounds__(64 * NW, 2) void bwd_stream_kernel(BwdArgs a) {
         zp += __shfl_xor(zp, 1, 64);             // the pixel's 4 chunks sit in lanes 4k..4k+3
         zp += __shfl_xor(zp, 2, 64);
         const float z = zp + hbias;
-        const float p = 1.f / (1.f + __expf(-z));
+        const float p = fast_sigmoid(z);
         const float tt = __uint_as_float(R.t[j]);
         const float one = tt == 1.f ? 1.f : 0.f;
-        const float dp = hd0 * (p - tt) / fmaxf((1.f - p) * p, 1e-12f) + hd1 * one + hd2;
-        const float dz = dp * (1.f - p) * p;
+        const float dz = head_dz(p, tt, one, hd0, hd1, hd2);
         unsigned o[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e)

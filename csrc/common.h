@@ -31,6 +31,18 @@ static __device__ __forceinline__ unsigned int pack_bf2(float lo, float hi) {
 static __device__ __forceinline__ float lo_bf(unsigned int u) { return __uint_as_float(u << 16); }
 static __device__ __forceinline__ float hi_bf(unsigned int u) { return __uint_as_float(u & 0xffff0000u); }
 
+// Segmentation-head backward per pixel (torch formulas: BCE backward (p - t) / max(p(1-p), 1e-12),
+// sigmoid backward g p (1-p)), from the loss's partial-sum gradient dS = (d0, d1, d2):
+//   dz = (d0 (p-t) / max(s, 1e-12) + d1 [t==1] + d2) s,   s = p (1-p)
+// written without the division: s / max(s, 1e-12) is 1 unless the sigmoid saturated.
+static __device__ __forceinline__ float head_dz(float p, float t, float one, float d0, float d1, float d2) {
+  const float s = (1.f - p) * p;
+  const float rs = s >= 1e-12f ? 1.f : s * 1e12f;
+  return d0 * (p - t) * rs + (d1 * one + d2) * s;
+}
+// sigmoid with the hardware reciprocal (1 ulp) instead of an IEEE division
+static __device__ __forceinline__ float fast_sigmoid(float z) { return __builtin_amdgcn_rcpf(1.f + __expf(-z)); }
+
 static __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

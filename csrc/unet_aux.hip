@@ -289,7 +289,7 @@ __global__ __launch_bounds__(256) void head_fwd_kernel(const bf16_t* __restrict_
     float z = bias;
 #pragma unroll
     for (int c = 0; c < C; ++c) z = fmaf(v[c], wv[c], z);
-    const float p = 1.f / (1.f + __expf(-z));
+    const float p = fast_sigmoid(z);
     if (probs) probs[i] = p;
     if (t) {
       const float tt = t[i];
@@ -363,11 +363,10 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const bf16_t* __restrict_
     float z = bias;
 #pragma unroll
     for (int c = 0; c < C; ++c) z = fmaf(v[c], wv[c], z);
-    const float p = 1.f / (1.f + __expf(-z));
+    const float p = fast_sigmoid(z);
     const float tt = t[i];
     const float one = tt == 1.f ? 1.f : 0.f;
-    const float dp = d0 * (p - tt) / fmaxf((1.f - p) * p, 1e-12f) + d1 * one + d2;
-    const float dz = dp * (1.f - p) * p;
+    const float dz = head_dz(p, tt, one, d0, d1, d2);
     db += dz;
     unsigned int o[C / 2];
 #pragma unroll
