@@ -52,7 +52,7 @@ def main():
     # (name, H, Cin, Cout)
     layers = [("L0 32->32", S, 32, 32), ("L0 64->32", S, 64, 32), ("L1 32->64", S // 2, 32, 64),
               ("L1 64->64", S // 2, 64, 64), ("L1 128->64", S // 2, 128, 64), ("L2 64->128", S // 4, 64, 128),
-              ("L2 128->128", S // 4, 128, 128), ("L3 128->256", S // 8, 128, 256), ("L3 256->256", S // 8, 256, 256), ("L3 512->256", S // 8, 512, 256),
+              ("L2 128->128", S // 4, 128, 128), ("L2 256->128", S // 4, 256, 128), ("L3 128->256", S // 8, 128, 256), ("L3 256->256", S // 8, 256, 256), ("L3 512->256", S // 8, 512, 256),
               ("mid 512->512", S // 16, 512, 512)]
     for name, H, Cin, Cout in layers:
         if a.only and not any(o in name for o in a.only.split(",")):
