@@ -40,6 +40,25 @@ static __device__ __forceinline__ float head_dz(float p, float t, float one, flo
   const float rs = s >= 1e-12f ? 1.f : s * 1e12f;
   return d0 * (p - t) * rs + (d1 * one + d2) * s;
 }
+// ReLU as one integer max on the f32 bits (negative floats are negative ints): no NaN-quieting
+// v_max_f32 in front of the v_max_f32 that fmaxf(v, 0) costs on MFMA results
+static __device__ __forceinline__ float relu_f(float v) { return __int_as_float(max(__float_as_int(v), 0)); }
+
+// Packed bf16 pairs of NON-NEGATIVE values (post-ReLU) order like unsigned 16-bit integers, so
+// 2x2 max-pool windows reduce two channels per instruction (v_pk_max_u16 / v_pk_sub_u16).
+typedef __attribute__((ext_vector_type(2))) unsigned short u16x2_t;
+static __device__ __forceinline__ unsigned pk_max16(unsigned a, unsigned b) {
+  return __builtin_bit_cast(unsigned, __builtin_elementwise_max(__builtin_bit_cast(u16x2_t, a), __builtin_bit_cast(u16x2_t, b)));
+}
+// bit 15 / 31 set where the half of b exceeds the half of a (halves in [0, 0x7fff])
+static __device__ __forceinline__ unsigned pk_gt16(unsigned b, unsigned a) {
+  return __builtin_bit_cast(unsigned, __builtin_bit_cast(u16x2_t, a) - __builtin_bit_cast(u16x2_t, b)) & 0x80008000u;
+}
+// bit 15 / 31 set where the half is non-zero
+static __device__ __forceinline__ unsigned pk_nz16(unsigned a) {
+  return __builtin_bit_cast(unsigned, __builtin_bit_cast(u16x2_t, a) + u16x2_t{0x7fff, 0x7fff}) & 0x80008000u;
+}
+
 // sigmoid with the hardware reciprocal (1 ulp) instead of an IEEE division
 static __device__ __forceinline__ float fast_sigmoid(float z) { return __builtin_amdgcn_rcpf(1.f + __expf(-z)); }
 

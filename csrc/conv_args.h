@@ -44,6 +44,22 @@ __device__ __forceinline__ unsigned pool_code(float tl, float tr, float bl, floa
          (unsigned)(br > 0.f) << 5;
 }
 
+// pool_code of two channels at once from packed non-negative bf16 pairs (window order tl, tr, bl, br):
+// the code of the low halves in bits 0-7, of the high halves in bits 8-15
+__device__ __forceinline__ unsigned pool_code2(unsigned tl, unsigned tr, unsigned bl, unsigned br) {
+  const unsigned mt = pk_max16(tl, tr), mb = pk_max16(bl, br);
+  const unsigned it = pk_gt16(tr, tl), ib = pk_gt16(br, bl), sel = pk_gt16(mb, mt);
+  const unsigned b0 = (sel & ib) | (~sel & it);                   // argmax bit 0, bit 1 = sel
+  // flag bits at 15 / 31 -> code bit k at k / 16 + k, then the high code to bits 8-13
+  unsigned x = b0 >> 15;
+  x |= sel >> 14;
+  x |= pk_nz16(tl) >> 13;
+  x |= pk_nz16(tr) >> 12;
+  x |= pk_nz16(bl) >> 11;
+  x |= pk_nz16(br) >> 10;
+  return (x & 0x3fu) | ((x >> 8) & 0x3f00u);
+}
+
 // split-output store (see IgemmArgs::y2); returns false when the output is not split
 __device__ __forceinline__ bool split_store(const IgemmArgs& a, unsigned m, int co, u32x2_t v) {
   if (a.y2 == nullptr) return false;

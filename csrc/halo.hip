@@ -224,7 +224,7 @@ __global__ __launch_bounds__(64 * (BC / WC) * (BP / WP)) void igemm_halo_kernel(
         v0 += b[0]; v1 += b[1]; v2 += b[2]; v3 += b[3];
       }
       if (a.relu) {
-        v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f);
+        v0 = relu_f(v0); v1 = relu_f(v1); v2 = relu_f(v2); v3 = relu_f(v3);
       }
       if (a.mask && co < a.mask_ch) {
         const uint2 mk = *reinterpret_cast<const uint2*>(a.mask + m * a.ldm + co);
@@ -577,7 +577,7 @@ __global__ __launch_bounds__(256 * WCS) void igemm_stream_kernel(IgemmArgs a) {
   const long ppix = (long)n * (a.Ho >> 1) * (a.Wo >> 1);
   const __amdgpu_buffer_rsrc_t pr = __builtin_amdgcn_make_buffer_rsrc((void*)(do_pool ? a.pool + ppix * a.ldp : a.y), 0, 0x7fffffff, 0x00020000);
   constexpr int PT = do_pool ? TP : 1, PC = do_pool ? TC : 1;
-  float ptop[PT][PC][4], ptop2[PT][PC][4];   // even row of the window: left / right pixel
+  u32x2_t ptop[PT][PC], ptop2[PT][PC];       // even row of the window (stored bf16): own / partner pixel
 
   // fused segmentation head (EPI 3): segmap weights of this lane's channels, BCE/Dice partials
   constexpr bool do_head = EPI == 3;
@@ -669,7 +669,7 @@ __global__ __launch_bounds__(256 * WCS) void igemm_stream_kernel(IgemmArgs a) {
         float v0 = acc[ic][ip][0] + bias[ic][0], v1 = acc[ic][ip][1] + bias[ic][1];
         float v2 = acc[ic][ip][2] + bias[ic][2], v3 = acc[ic][ip][3] + bias[ic][3];
         if (a.relu) {
-          v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f);
+          v0 = relu_f(v0); v1 = relu_f(v1); v2 = relu_f(v2); v3 = relu_f(v3);
         }
         if (has_mask) {
           v0 = lo_bf(mk[ip][ic].x) > 0.f ? v0 : 0.f;
@@ -709,32 +709,26 @@ __global__ __launch_bounds__(256 * WCS) void igemm_stream_kernel(IgemmArgs a) {
           hdot = fmaf(hi_bf(packed.y), hwv[ic][3], hdot);
         }
         if constexpr (do_pool) {
-          // pool the STORED (bf16-rounded) values: identical to max-pooling the tensor afterwards.
-          // Even lanes hold pixel w (left), their xor-1 partner pixel w+1 (right).
-          float q[4] = {lo_bf(packed.x), hi_bf(packed.x), lo_bf(packed.y), hi_bf(packed.y)};
-          float pq[4];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) pq[e] = __shfl_xor(q[e], 1, 64);
+          // pool the STORED bf16 values (identical to max-pooling the tensor afterwards).  They are
+          // post-ReLU (>= 0; the host requires relu with pool), so the window max and argmax run on
+          // the packed channel pairs as 16-bit integers.  Even lanes hold pixel w (left), their
+          // xor-1 partner pixel w+1 (right).
+          const u32x2_t pq = u32x2_t{(unsigned)__shfl_xor((int)packed.x, 1, 64), (unsigned)__shfl_xor((int)packed.y, 1, 64)};
           const int hrow = h0 + r;
           if ((hrow & 1) == 0) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              ptop[ip][ic][e] = q[e];
-              ptop2[ip][ic][e] = pq[e];
-            }
+            ptop[ip][ic] = packed;
+            ptop2[ip][ic] = pq;
           } else if (hrow < 2 * (a.Ho >> 1) && (lane & 1) == 0 && pv[ip]) {
             const int pw = (w0 + wp * WP + ip * 16 + (lane & 15)) >> 1;
             const unsigned lidx = (unsigned)((hrow >> 1) * (a.Wo >> 1) + pw);       // inside this image
             const size_t pidx = (size_t)ppix + lidx;
             const unsigned po = (lidx * a.ldp + wc * WCN + ic * 16 + 4 * chunk) * 2;
-            float mx[4];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) mx[e] = fmaxf(fmaxf(q[e], pq[e]), fmaxf(ptop[ip][ic][e], ptop2[ip][ic][e]));
-            __builtin_amdgcn_raw_buffer_store_b64(u32x2_t{pack_bf2(mx[0], mx[1]), pack_bf2(mx[2], mx[3])}, pr, po, 0, 0);
+            const u32x2_t tl = ptop[ip][ic], tr = ptop2[ip][ic];
+            const u32x2_t mx = u32x2_t{pk_max16(pk_max16(tl.x, tr.x), pk_max16(packed.x, pq.x)),
+                                       pk_max16(pk_max16(tl.y, tr.y), pk_max16(packed.y, pq.y))};
+            __builtin_amdgcn_raw_buffer_store_b64(mx, pr, po, 0, 0);
             if (a.pcode) {
-              unsigned code = 0;
-#pragma unroll
-              for (int e = 0; e < 4; ++e) code |= pool_code(ptop[ip][ic][e], ptop2[ip][ic][e], q[e], pq[e]) << (8 * e);
+              const unsigned code = pool_code2(tl.x, tr.x, packed.x, pq.x) | pool_code2(tl.y, tr.y, packed.y, pq.y) << 16;
               *reinterpret_cast<unsigned*>(a.pcode + (size_t)pidx * a.Ngemm + wc * WCN + ic * 16 + 4 * chunk) = code;
             }
           }
@@ -902,7 +896,7 @@ __global__ __launch_bounds__(256) void igemm_stream8_kernel(IgemmArgs a) {
         float v0 = acc[ic][ip][0] + bias[ic][0], v1 = acc[ic][ip][1] + bias[ic][1];
         float v2 = acc[ic][ip][2] + bias[ic][2], v3 = acc[ic][ip][3] + bias[ic][3];
         if (a.relu) {
-          v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f);
+          v0 = relu_f(v0); v1 = relu_f(v1); v2 = relu_f(v2); v3 = relu_f(v3);
         }
         __builtin_amdgcn_raw_buffer_store_b64(u32x2_t{pack_bf2(v0, v1), pack_bf2(v2, v3)}, yr, ybase + yl[ip] + ic * 32, 0, 0);
       }
@@ -989,7 +983,8 @@ DPA_API int dpa_igemm_stream(const IgemmArgs* args, int variant, hipStream_t st)
   // any row width: a partial last strip masks its out-of-row pixels (loads read zeros, stores are
   // dropped); the fused pool needs whole 2x2 windows along the row (even width)
   if (a.mode != 0 || a.KH != 3 || a.KW != 3 || a.stride != 1 || a.pad != 1 || (a.ldx & 7) || (a.ldy & 3) ||
-      a.Hs != a.Ho || a.Ws != a.Wo || a.Wo < 16 || a.Kpad < 9 * a.Cs || (a.pool && ((a.ldp & 3) || (a.Wo & 1))))
+      a.Hs != a.Ho || a.Ws != a.Wo || a.Wo < 16 || a.Kpad < 9 * a.Cs ||
+      (a.pool && ((a.ldp & 3) || (a.Wo & 1) || !a.relu)))
     return (int)hipErrorInvalidValue;
   if (a.Cs == 8 && a.Ngemm == 32 && !a.pool) return launch_igemm_stream8<128, 32>(a, st);
   if (variant == 0) variant = stream_auto_variant(a);

@@ -199,7 +199,7 @@ __global__ __launch_bounds__(64 * (BP / WP) * (BC / WC)) void igemm_kernel(Igemm
         v0 += b[0]; v1 += b[1]; v2 += b[2]; v3 += b[3];
       }
       if (a.relu) {
-        v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f);
+        v0 = relu_f(v0); v1 = relu_f(v1); v2 = relu_f(v2); v3 = relu_f(v3);
       }
       if (a.mask && co < a.mask_ch) {
         const u32x2_t mk = __builtin_amdgcn_raw_buffer_load_b64(mr, ((unsigned)m * (unsigned)a.ldm + co) * 2, 0, 0);

@@ -79,7 +79,7 @@ __device__ __forceinline__ void glds_store4(const IgemmArgs& a, __amdgpu_buffer_
     v0 += b[0]; v1 += b[1]; v2 += b[2]; v3 += b[3];
   }
   if (a.relu) {
-    v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f);
+    v0 = relu_f(v0); v1 = relu_f(v1); v2 = relu_f(v2); v3 = relu_f(v3);
   }
   if (a.mask && co < a.mask_ch) {
     const u32x2_t mk = __builtin_amdgcn_raw_buffer_load_b64(mr, ((unsigned)m * (unsigned)a.ldm + co) * 2, 0, 0);
