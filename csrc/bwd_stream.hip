@@ -53,6 +53,15 @@ struct BwdArgs {
   // sum_px dx[h][px][co] * x1[h+kh-1][px+kw-1][ci] from it and an x1 row ring; partials go to
   // slab1 [nblocks][9][32][8] / bslab1 [nblocks][32].
   const bf16_t* x1; float* slab1; float* bslab1; unsigned x1bytes;
+  // BN mode (the conv is followed by BatchNorm + ReLU): `g` is the ReLU-masked gradient of the BN
+  // output and the conv-output gradient is formed on load with bn_bwd_apply's formula,
+  //   dz = bncoef[c] g + bncoef[CO + c] z + bncoef[2 CO + c]     (z: the BN input, ldz == ldg),
+  // zero outside the image (the conv's zero padding), so the dz pass over HBM never happens.
+  const bf16_t* z; const float* bncoef;
+  // BN statistics of the layer BELOW (its ReLU output is this conv's input x, the dx mask): per block
+  // and channel, sum dx and sum dx*x of the stored masked dx -> bnslab[block][2][CI] (the partial
+  // sums igemm_stream's EPI 5 writes; bn_bwd_finalize_kernel's gy mode consumes them)
+  float* bnslab;
 };
 
 // 8 consecutive k (pixel rows roff+8g .. +7) of 16 channels starting at col0, from an nk image
@@ -81,7 +90,7 @@ __device__ __forceinline__ bf16x8_t tr_pair(const char* base, int off0, int off1
   return __builtin_bit_cast(bf16x8_t, v);
 }
 
-template <int BP, int CI, int CO, int NW, int PG, int EPI, bool HEAD, bool POOL, bool W1>
+template <int BP, int CI, int CO, int NW, int PG, int EPI, bool HEAD, bool POOL, bool W1, int BNM>
 __global__ __launch_bounds__(64 * NW, 2) void bwd_stream_kernel(BwdArgs a) {
   constexpr int NT = 64 * NW;
   constexpr int HR = BP + 2;                   // ring row: BP pixels + 1 halo pixel each side
@@ -101,6 +110,10 @@ __global__ __launch_bounds__(64 * NW, 2) void bwd_stream_kernel(BwdArgs a) {
   static_assert(!HEAD || (CO == 32 && EPI == 0), "head mode: 32-channel last decoder conv");
   static_assert(!(HEAD && POOL), "one gradient source");
   static_assert(!W1 || (POOL && CI == 32 && CO == 32 && EPI == 0 && BP % 32 == 0), "W1 mode");
+  // BNM: 0 none, 1 BatchNorm backward on load, 2 that + the layer below's BN statistics from dx
+  constexpr bool BNL = BNM >= 1, BNS = BNM == 2;
+  static_assert(!BNM || !(HEAD || POOL || W1), "BN mode: plain gradient source");
+  static_assert(!BNS || EPI == 0, "BN statistics of the layer below need the masked dx");
   // W1: x1 row ring (5 slots: the delayed dW1 step still reads row h-2 while row h+2 is stored),
   // dx row double buffer [BP][32] (nk, swz_nk<32>), per-wave tiles of the 32 x (9 taps x 8) dW1
   constexpr int X1SLOT = HR * 16, G1SLOT = BP * 64;
@@ -109,6 +122,7 @@ __global__ __launch_bounds__(64 * NW, 2) void bwd_stream_kernel(BwdArgs a) {
   constexpr int LG = (GCH + NT - 1) / NT, LX = (XCH + NT - 1) / NT;
   constexpr int BCH = BP * 4 * KSO, LBI = (BCH + NT - 1) / NT;   // bias: chunks of the g row's BP pixels
   __shared__ __attribute__((aligned(16))) char lds[WBYTES + 4 * GSLOT + 4 * XSLOT + W1BYTES];
+  __shared__ __attribute__((aligned(16))) float bnc[BNL ? 3 * CO : 4];   // BN mode: the dz coefficients
   char* const Wimg = lds;
   char* const Gring = lds + WBYTES;
   char* const Xring = Gring + 4 * GSLOT;
@@ -127,7 +141,7 @@ __global__ __launch_bounds__(64 * NW, 2) void bwd_stream_kernel(BwdArgs a) {
   const int wp = wid % WPX, wc = wid / WPX;                      // dx role
   const int nt = wid % NTI, msp = (wid / NTI) % MSPL, pg = wid / (NTI * MSPL);   // dW role
   // buffer resources are rebuilt per image (32-bit offsets stay inside one image at any batch size)
-  __amdgpu_buffer_rsrc_t gr, xr, yr, y2r, tr, pr, cr, x1r;
+  __amdgpu_buffer_rsrc_t gr, xr, yr, y2r, tr, pr, cr, x1r, zr;
   const bool has_g = !POOL || a.g != nullptr;
   auto bind = [&](int img) {
     const long pix = (long)img * a.H * a.W;
@@ -138,6 +152,7 @@ __global__ __launch_bounds__(64 * NW, 2) void bwd_stream_kernel(BwdArgs a) {
     }
     if constexpr (HEAD) tr = __builtin_amdgcn_make_buffer_rsrc((void*)(a.tgt + pix), 0, a.H * a.W * 4, 0x00020000);
     if constexpr (W1) x1r = __builtin_amdgcn_make_buffer_rsrc((void*)(a.x1 + pix * 8), 0, (int)a.x1bytes, 0x00020000);
+    if constexpr (BNL) zr = __builtin_amdgcn_make_buffer_rsrc((void*)(a.z + pix * a.ldg), 0, (int)a.gbytes, 0x00020000);
     gr = __builtin_amdgcn_make_buffer_rsrc((void*)(has_g ? a.g + pix * a.ldg : a.x), 0, has_g ? (int)a.gbytes : 0, 0x00020000);
     xr = __builtin_amdgcn_make_buffer_rsrc((void*)(a.x + pix * a.ldx), 0, (int)a.xbytes, 0x00020000);
     yr = __builtin_amdgcn_make_buffer_rsrc((void*)(a.y + pix * a.ldy), 0, 0x7fffffff, 0x00020000);
@@ -150,6 +165,10 @@ __global__ __launch_bounds__(64 * NW, 2) void bwd_stream_kernel(BwdArgs a) {
     const int tap = tk / KSO, ks = tk - tap * KSO;
     const u32x4_t v = *reinterpret_cast<const u32x4_t*>(a.wd + (long)row * a.Kd + tap * CO + ks * 32 + cc * 8);
     *reinterpret_cast<u32x4_t*>(Wimg + (tk * CI + row) * 64 + (swz_nk<32>(row, cc) << 4)) = v;
+  }
+  if constexpr (BNL) {
+    for (int i = tid; i < 3 * CO; i += NT) bnc[i] = a.bncoef[i];
+    __syncthreads();
   }
   // ---- loader constants
   unsigned goff[LG], xoff[LX];
@@ -224,6 +243,7 @@ __global__ __launch_bounds__(64 * NW, 2) void bwd_stream_kernel(BwdArgs a) {
     u32x4_t pd[POOL ? LG : 1];            // POOL: the pooled gradient of each chunk's window
     u32x2_t pc[POOL ? LG : 1];            // POOL: the window codes of the chunk's 8 channels
     u32x4_t x1[1];                        // W1: the x1 chunk of this thread's pixel
+    u32x4_t z[BNL ? LG : 1];              // BN: the BN input chunk at the gradient chunk's position
   };
   RowRegs setA, setB;
   int n = ig * a.ipb;
@@ -237,6 +257,10 @@ __global__ __launch_bounds__(64 * NW, 2) void bwd_stream_kernel(BwdArgs a) {
     for (int j = 0; j < LX; ++j)
       R.x[j] = __builtin_amdgcn_raw_buffer_load_b128(xr, (rok && xok[j]) ? xb + xoff[j] : 0x80000000u, 0, 0);
     if constexpr (W1) R.x1[0] = __builtin_amdgcn_raw_buffer_load_b128(x1r, (rok && x1ok) ? (unsigned)ih * x1rowb + x1off : 0x80000000u, 0, 0);
+    if constexpr (BNL) {
+#pragma unroll
+      for (int j = 0; j < LG; ++j) R.z[j] = __builtin_amdgcn_raw_buffer_load_b128(zr, (rok && gok[j]) ? gb + goff[j] : 0x80000000u, 0, 0);
+    }
     if constexpr (HEAD) {
 #pragma unroll
       for (int j = 0; j < LG; ++j)
@@ -269,6 +293,27 @@ __global__ __launch_bounds__(64 * NW, 2) void bwd_stream_kernel(BwdArgs a) {
           lo = (cl >> (2 + q)) & 1u ? lo : 0.f;
           hi = (ch >> (2 + q)) & 1u ? hi : 0.f;
           o[k] = pack_bf2(lo, hi);
+        }
+        R.g[j] = u32x4_t{o[0], o[1], o[2], o[3]};
+      }
+    }
+    if constexpr (BNL) {                        // (g, z) chunk -> conv-output gradient chunk
+      const bool rok = ih >= 0 && ih < a.H;
+#pragma unroll
+      for (int j = 0; j < LG; ++j) {
+        if (!glive[j]) continue;
+        const int c = tid + j * NT;
+        const int cb = ((c >> 2) / HR) * 32 + (c & 3) * 8;       // first channel of the chunk
+        const bool ok = rok && gok[j];                            // padding stays zero
+        unsigned o[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {     // two channels at a time: few coefficient registers live
+          const float2 ca = *reinterpret_cast<const float2*>(bnc + cb + 2 * k);
+          const float2 cz = *reinterpret_cast<const float2*>(bnc + CO + cb + 2 * k);
+          const float2 cc = *reinterpret_cast<const float2*>(bnc + 2 * CO + cb + 2 * k);
+          const float lo = fmaf(ca.x, lo_bf(R.g[j][k]), fmaf(cz.x, lo_bf(R.z[j][k]), cc.x));
+          const float hi = fmaf(ca.y, hi_bf(R.g[j][k]), fmaf(cz.y, hi_bf(R.z[j][k]), cc.y));
+          o[k] = ok ? pack_bf2(lo, hi) : 0u;
         }
         R.g[j] = u32x4_t{o[0], o[1], o[2], o[3]};
       }
@@ -348,6 +393,11 @@ __global__ __launch_bounds__(64 * NW, 2) void bwd_stream_kernel(BwdArgs a) {
                                 : (unsigned)(((w0 + px) * a.ldy + c0) * 2);
     }
   const unsigned yrowb = (unsigned)(a.W * a.ldy * 2), y2rowb = (unsigned)(a.W * (EPI == 1 ? a.ldy2 : a.ldy) * 2);
+  float bsm[BNS ? TC : 1][4], bsq[BNS ? TC : 1][4];      // BN statistics of the layer below (per lane)
+#pragma unroll
+  for (int ic = 0; ic < (BNS ? TC : 1); ++ic)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) bsm[ic][e] = bsq[ic][e] = 0.f;
 
   // ---- dW role: per-lane byte offsets of the transposed fragments inside a ring slot (row-invariant;
   // computing the swizzled addresses per row cost more VALU issue than the MFMAs they feed)
@@ -528,14 +578,24 @@ __global__ __launch_bounds__(64 * NW, 2) void bwd_stream_kernel(BwdArgs a) {
 #pragma unroll
         for (int ic = 0; ic < TC; ++ic) {
           float v0 = acc[ic][ip][0], v1 = acc[ic][ip][1], v2 = acc[ic][ip][2], v3 = acc[ic][ip][3];
+          u32x2_t mk = u32x2_t{0u, 0u};
           if constexpr (EPI == 0) {
-            const u32x2_t mk = *reinterpret_cast<const u32x2_t*>(Xm + moff[ip][ic]);
+            mk = *reinterpret_cast<const u32x2_t*>(Xm + moff[ip][ic]);
             v0 = lo_bf(mk.x) > 0.f ? v0 : 0.f;
             v1 = hi_bf(mk.x) > 0.f ? v1 : 0.f;
             v2 = lo_bf(mk.y) > 0.f ? v2 : 0.f;
             v3 = hi_bf(mk.y) > 0.f ? v3 : 0.f;
           }
           const u32x2_t packed = u32x2_t{pack_bf2(v0, v1), pack_bf2(v2, v3)};
+          if constexpr (BNS) {     // statistics of the STORED masked dx (out-of-row pixels have x = 0)
+            const float q[4] = {lo_bf(packed.x), hi_bf(packed.x), lo_bf(packed.y), hi_bf(packed.y)};
+            const float m[4] = {lo_bf(mk.x), hi_bf(mk.x), lo_bf(mk.y), hi_bf(mk.y)};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              bsm[ic][e] += q[e];
+              bsq[ic][e] = fmaf(q[e], m[e], bsq[ic][e]);
+            }
+          }
           if constexpr (W1)                      // dx row -> LDS only (bf16, as it would be stored)
             *reinterpret_cast<u32x2_t*>(G1buf + (r & 1) * G1SLOT + g1o[ip][ic]) = packed;
           else if (EPI == 1 && hi[ip][ic])
@@ -556,6 +616,35 @@ __global__ __launch_bounds__(64 * NW, 2) void bwd_stream_kernel(BwdArgs a) {
       if (nrows > 0) w1_row(nrows);
       __syncthreads();
     }
+  }
+  if constexpr (BNS) {
+    // lanes l, l^1 .. l^15 hold the same channels (different pixels): butterfly over the 16, then the
+    // WPX pixel waves in a fixed order -> one deterministic bnslab row per block
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(lds);                 // [WPX][2][CI] (the rings are free)
+#pragma unroll
+    for (int ic = 0; ic < TC; ++ic)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float sm = bsm[ic][e], sq = bsq[ic][e];
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          sm += __shfl_xor(sm, o, 64);
+          sq += __shfl_xor(sq, o, 64);
+        }
+        if ((lane & 15) == 0) {
+          const int c = wc * WCN + ic * 16 + 4 * chunk + e;
+          red[(wp * 2) * CI + c] = sm;
+          red[(wp * 2 + 1) * CI + c] = sq;
+        }
+      }
+    __syncthreads();
+    for (int k = tid; k < 2 * CI; k += NT) {
+      float t = 0.f;
+      for (int w = 0; w < WPX; ++w) t += red[w * 2 * CI + k];
+      a.bnslab[(long)split_id * 2 * CI + k] = t;
+    }
+    __syncthreads();
   }
   // ---------------- partial weight gradient of this (block, pixel group): slab row blockIdx*PG + pg
   const long srow = (long)split_id * PG + pg;
@@ -630,10 +719,10 @@ __global__ __launch_bounds__(64 * NW, 2) void bwd_stream_kernel(BwdArgs a) {
   }
 }
 
-template <int BP, int CI, int CO, int NW, int PG, int EPI, bool HEAD = false, bool POOL = false, bool W1 = false>
+template <int BP, int CI, int CO, int NW, int PG, int EPI, bool HEAD = false, bool POOL = false, bool W1 = false, int BNM = 0>
 static int launch_bwd_stream(const BwdArgs& a, hipStream_t st) {
   const int blocks = ((a.N + a.ipb - 1) / a.ipb) * ((a.H + a.rh - 1) / a.rh) * ((a.W + BP - 1) / BP);
-  hipLaunchKernelGGL((bwd_stream_kernel<BP, CI, CO, NW, PG, EPI, HEAD, POOL, W1>), dim3(blocks), dim3(64 * NW), 0, st, a);
+  hipLaunchKernelGGL((bwd_stream_kernel<BP, CI, CO, NW, PG, EPI, HEAD, POOL, W1, BNM>), dim3(blocks), dim3(64 * NW), 0, st, a);
   return (int)hipGetLastError();
 }
 
@@ -672,11 +761,20 @@ DPA_API int dpa_bwd_stream(const BwdArgs* args, int ci, int co, int epi, hipStre
       a.rh < 1 || a.ipb < 1 ||
       a.Kd < 9 * co || (epi == 1 && (a.y2 == nullptr || (a.ldy2 & 3) || a.split % 16 || a.split <= 0 || a.split >= ci)))
     return (int)hipErrorInvalidValue;
-#define DPA_BWD(CIv, COv, BPv, NWv, PGv)                                          \
-  if (ci == CIv && co == COv) {                                                    \
-    if (epi == 0) return launch_bwd_stream<BPv, CIv, COv, NWv, PGv, 0>(a, st);     \
-    if (epi == 1) return launch_bwd_stream<BPv, CIv, COv, NWv, PGv, 1>(a, st);     \
-    if (epi == 2) return launch_bwd_stream<BPv, CIv, COv, NWv, PGv, 2>(a, st);     \
+  // BN modes: the gradient source is plain (no pool / head / first-conv fold); statistics for the
+  // layer below only with the masked dx
+  const bool bn = a.z != nullptr;
+  if (bn && (a.bncoef == nullptr || fused_mode || (a.bnslab != nullptr && epi != 0))) return (int)hipErrorInvalidValue;
+  if (!bn && a.bnslab != nullptr) return (int)hipErrorInvalidValue;
+#define DPA_BWD(CIv, COv, BPv, NWv, PGv)                                                              \
+  if (ci == CIv && co == COv) {                                                                        \
+    if (bn && a.bnslab) return launch_bwd_stream<BPv, CIv, COv, NWv, PGv, 0, false, false, false, 2>(a, st); \
+    if (bn && epi == 1) return launch_bwd_stream<BPv, CIv, COv, NWv, PGv, 1, false, false, false, 1>(a, st); \
+    if (bn && epi == 2) return launch_bwd_stream<BPv, CIv, COv, NWv, PGv, 2, false, false, false, 1>(a, st); \
+    if (bn) return (int)hipErrorInvalidValue;                                                          \
+    if (epi == 0) return launch_bwd_stream<BPv, CIv, COv, NWv, PGv, 0>(a, st);                         \
+    if (epi == 1) return launch_bwd_stream<BPv, CIv, COv, NWv, PGv, 1>(a, st);                         \
+    if (epi == 2) return launch_bwd_stream<BPv, CIv, COv, NWv, PGv, 2>(a, st);                         \
   }
   if (a.pcode != nullptr) {    // fused max-pool backward: the full-resolution encoder conv2 (32 -> 32)
     // (the 64 -> 64 instantiation spilled 104 B/lane at two waves per SIMD: kept on pool_bwd_code)

@@ -331,6 +331,22 @@ DPA_API int dpa_bn_fwd(const bf16_t* z, int ldz, bf16_t* y, int ldy, long long P
   return (int)hipGetLastError();
 }
 
+// training backward coefficients only: dz = coef3[c] g + coef3[C+c] z + coef3[2C+c] (dgamma/dbeta
+// accumulated) -- for a consumer that forms dz itself on load (csrc/bwd_stream.hip BN mode)
+DPA_API int dpa_bn_bwd_coef(const bf16_t* g, int ldg, const bf16_t* z, int ldz, long long P, int C, const float* gamma,
+                            const float* saved, float* slab, float* coef3, float* dgamma, float* dbeta,
+                            const float* beta, int slab_rows, hipStream_t st) {
+  int G;
+  dim3 grid;
+  if (!bn_shape(P, C, G, grid) || (ldg & 7) || (ldz & 7)) return (int)hipErrorInvalidValue;
+  if (slab_rows > 0 && beta == nullptr) return (int)hipErrorInvalidValue;
+  if (slab_rows <= 0)
+    hipLaunchKernelGGL(bn_partial_kernel<1>, grid, dim3(256), 0, st, g, ldg, z, ldz, saved, (long)P, C, G, slab);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(256), 0, st, slab, slab_rows > 0 ? slab_rows : (int)grid.x, C,
+                     (long)P, gamma, saved, coef3, dgamma, dbeta, beta, slab_rows > 0 ? 1 : 0);
+  return (int)hipGetLastError();
+}
+
 // training backward: g = dL/d(bn output) (ReLU mask already applied by the consumer) -> dz,
 // dgamma/dbeta accumulated.  coef3: scratch [3C].
 DPA_API int dpa_bn_bwd(const bf16_t* g, int ldg, const bf16_t* z, int ldz, bf16_t* dz, int lddz, long long P, int C,

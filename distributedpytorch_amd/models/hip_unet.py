@@ -314,9 +314,13 @@ class HipBlocks:
 
     def fusable(self, c: _Conv, below, W: int, whole: bool = False) -> bool:
         """The fused backward (dgrad + weight/bias gradient in one pass, csrc/bwd_stream.hip) serves
-        this conv: 32/64 channels in and out, no BatchNorm around it (its backward needs the dgrad
-        epilogue's statistics), image rows a multiple of the kernel's pixel strip."""
-        if not (K.USE_FUSED_BWD and c.bn is None and (below is None or below.bn is None) and c.Cs == c.Cin):
+        this conv: 32/64 channels in and out, image rows a multiple of the kernel's pixel strip.  A
+        BatchNorm after the conv (its backward formed on load) or below it (its statistics from the dx
+        epilogue) needs the plain modes (:meth:`bwd_conv`); the pool / head folds (``whole``) do not
+        combine with BatchNorm."""
+        bn_ok = K.USE_FUSED_BN_BWD and not whole
+        if not (K.USE_FUSED_BWD and (c.bn is None or bn_ok) and (below is None or below.bn is None or bn_ok)
+                and c.Cs == c.Cin):
             return False
         key = (c.Cin, c.Cout, W, whole)
         ok = self._fusable.get(key)
@@ -342,6 +346,27 @@ class HipBlocks:
             hi = torch.empty(N, H, W, c.Cin - split, dtype=torch.bfloat16, device=x.device)
             return K.conv_bwd_fused(g, x, self.wd(c), c.Kd, gw, gb, mask=False, dx2=hi, split=split)
         return K.conv_bwd_fused(g, x, self.wd(c), c.Kd, gw, gb, mask=mask, head=head, pool=pool)
+
+    def bwd_conv(self, c: _Conv, g: torch.Tensor, x: torch.Tensor, st, *, mask: bool, below: _Conv = None,
+                 stats: list = None, split: int = 0):
+        """Fused backward of ``c`` (:meth:`fusable`) when ``g`` is the gradient of its output -- of its
+        BatchNorm+ReLU output if it has one (``st`` = that BN's saved (z, mean/invstd), ``stats`` = the
+        BN's backward partial sums from whoever produced ``g``, if any): the BN backward is formed in the
+        kernel's loader from per-channel coefficients, so neither dz nor a BN pass over HBM exists.
+        Returns (dx -- or the (lo, hi) halves with ``split`` --, st_g) with st_g the BatchNorm partial
+        sums of ``below`` (its ReLU output is ``x``, the dx mask) or None."""
+        gw, gb = _grad(c.mod.weight).view(-1), _grad(c.mod.bias)
+        bn = None
+        if c.bn is not None:
+            z, saved = st
+            bn = (z, K.bn_bwd_coef(g, z, saved, c.bn, _grad(c.bn.weight), _grad(c.bn.bias), stats=stats))
+        want = below is not None and below.bn is not None
+        dx2 = None
+        if split:
+            N, H, W = x.shape[:3]
+            dx2 = torch.empty(N, H, W, c.Cin - split, dtype=torch.bfloat16, device=x.device)
+        res = K.conv_bwd_fused(g, x, self.wd(c), c.Kd, gw, gb, mask=mask, dx2=dx2, split=split, bn=bn, bn_stats=want)
+        return res if want else (res, None)
 
     def halves_fusable(self, c: _Conv, C: int, W: int) -> bool:
         """A conv over a concat of two C-channel halves whose fused backward does not exist at 2C input
@@ -655,17 +680,18 @@ class _EncFn(torch.autograd.Function):
                 K.pool_bwd_code(code, dskip, dpooled, g2)
             else:
                 K.pool_bwd(skip, dskip, dpooled, g2)
-            g2 = B.bn_bwd(c2, g2, st2)
             if B.fusable(c2, c1, W):
-                g1, st_g = B.conv_bwd(c2, g2, a, mask=True), None
+                g1, st_g = B.bwd_conv(c2, g2, a, st2, mask=True, below=c1)
             else:
+                g2 = B.bn_bwd(c2, g2, st2)
                 B.conv_wgrad(c2, g2, a)              # side stream: overlaps the dgrad chain
                 g1, st_g = B.conv_dgrad(c2, g2, mask=a, below=c1)
         B.ready([c2.mod, c2.bn])
-        g1 = B.bn_bwd(c1, g1, st1, stats=st_g)
         if ctx.x_needs_grad and B.fusable(c1, None, W):
-            gx = B.conv_bwd(c1, g1, x, mask=False)   # the pool backward below applies the ReLU mask
+            # the pool backward below applies the ReLU mask
+            gx, _ = B.bwd_conv(c1, g1, x, st1, mask=False, stats=st_g)
         else:
+            g1 = B.bn_bwd(c1, g1, st1, stats=st_g)
             B.conv_wgrad(c1, g1, x)
             gx = B.conv_dgrad(c1, g1) if ctx.x_needs_grad else None
         B.ready([c1.mod, c1.bn])
@@ -777,22 +803,23 @@ class _DecFn(torch.autograd.Function):
                 gy = K.head_bwd(y, seg.weight, seg.bias, t, dS, _grad(seg.weight).view(-1), _grad(seg.bias))
                 B.ready([seg])
                 g2 = (gy.float() + g2.float()).to(torch.bfloat16).contiguous()
-            g2 = B.bn_bwd(c2, g2, st2)
             W = g2.shape[2]
             if B.fusable(c2, c1, W):
-                g1, st_g = B.conv_bwd(c2, g2, a, mask=True), None
+                g1, st_g = B.bwd_conv(c2, g2, a, st2, mask=True, below=c1)
             else:
+                g2 = B.bn_bwd(c2, g2, st2)
                 B.conv_wgrad(c2, g2, a)
                 g1, st_g = B.conv_dgrad(c2, g2, mask=a, below=c1)
         B.ready([c2.mod, c2.bn])
-        g1 = B.bn_bwd(c1, g1, st1, stats=st_g)
         if B.fusable(c1, None, W):
-            dskip, gup = B.conv_bwd(c1, g1, cat, mask=False, split=C)
-        elif B.halves_fusable(c1, C, W):
-            dskip, gup = B.conv_bwd_halves(c1, g1, cat, C)
+            (dskip, gup), _ = B.bwd_conv(c1, g1, cat, st1, mask=False, stats=st_g, split=C)
         else:
-            B.conv_wgrad(c1, g1, cat)
-            dskip, gup = B.conv_dgrad_split(c1, g1, C)
+            g1 = B.bn_bwd(c1, g1, st1, stats=st_g)
+            if B.halves_fusable(c1, C, W):
+                dskip, gup = B.conv_bwd_halves(c1, g1, cat, C)
+            else:
+                B.conv_wgrad(c1, g1, cat)
+                dskip, gup = B.conv_dgrad_split(c1, g1, C)
         B.ready([c1.mod, c1.bn])
         if isinstance(d, _Up):
             gup = K.up2_bwd(gup)          # to the projection's (low) resolution

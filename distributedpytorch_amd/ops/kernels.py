@@ -47,7 +47,8 @@ class BwdArgs(ctypes.Structure):
                [("gbytes", ctypes.c_uint), ("xbytes", ctypes.c_uint)] + \
                [("tgt", c_void_p), ("hw", c_void_p), ("hb", c_void_p), ("dS", c_void_p), ("hslab", c_void_p)] + \
                [("pcode", c_void_p), ("dpool", c_void_p), ("ldp", c_int)] + \
-               [("x1", c_void_p), ("slab1", c_void_p), ("bslab1", c_void_p), ("x1bytes", ctypes.c_uint)]
+               [("x1", c_void_p), ("slab1", c_void_p), ("bslab1", c_void_p), ("x1bytes", ctypes.c_uint)] + \
+               [("z", c_void_p), ("bncoef", c_void_p), ("bnslab", c_void_p)]
 
 
 class DconvArgs(ctypes.Structure):
@@ -126,6 +127,9 @@ USE_FUSED_POOL_BWD = USE_FUSED_BWD and os.environ.get("DPA_NO_FUSED_POOL_BWD", "
 # the first encoder conv's weight gradient folded into the pool-mode backward of the second: opt-in,
 # slower at batch 256 (6.05 ms vs 5.3 ms for the two kernels it replaces; see csrc/bwd_stream.hip)
 USE_FUSED_W1 = USE_FUSED_POOL_BWD and os.environ.get("DPA_FUSED_W1", "0") == "1"
+# BatchNorm backward formed in the fused backward's loader (csrc/bwd_stream.hip BN modes) instead of a
+# bn_bwd_apply pass + separate dgrad / weight-gradient passes over the dz it wrote; DPA_FUSED_BN_BWD=0 opts out
+USE_FUSED_BN_BWD = USE_FUSED_BWD and os.environ.get("DPA_FUSED_BN_BWD", "1") == "1"
 
 
 # TIMING ABLATION ONLY (numerically wrong results): DPA_ABLATE=halo,glds,... skips the launches of the
@@ -514,7 +518,7 @@ def bwd_pool_foldable(ci: int, co: int) -> bool:
 def conv_bwd_fused(g: Optional[torch.Tensor], x: torch.Tensor, wd: torch.Tensor, Kd: int, gw: torch.Tensor,
                    gb: Optional[torch.Tensor], *, mask: bool, dx: Optional[torch.Tensor] = None,
                    dx2: Optional[torch.Tensor] = None, split: int = 0, target_blocks: int = 0, head=None,
-                   pool=None, w1=None):
+                   pool=None, w1=None, bn=None, bn_stats: bool = False):
     """Backward of ``y = conv3x3(x) (+bias)`` in one pass (csrc/bwd_stream.hip): returns
     ``dx = conv3x3^T(g)`` (times ``x > 0`` when ``mask``; with ``dx2``/``split`` the channels
     ``>= split`` go to ``dx2``) and ACCUMULATES the weight gradient into ``gw`` (PyTorch OIHW
@@ -535,7 +539,14 @@ def conv_bwd_fused(g: Optional[torch.Tensor], x: torch.Tensor, wd: torch.Tensor,
     the output of a first conv ``x = relu(conv3x3(x1))`` (32 channels, 8-channel padded input of
     which ``Creal`` are real) whose input needs no gradient.  dx -- that conv's output gradient -- is
     then never stored: the kernel accumulates the first conv's weight and bias gradients from it row
-    by row, and the function returns None."""
+    by row, and the function returns None.
+
+    ``bn`` = (z, coef3 fp32 [3*Cout]) (:func:`bn_bwd_coef`): the conv is followed by BatchNorm + ReLU,
+    ``g`` is the ReLU-masked gradient of the BN output and the conv-output gradient
+    ``dz = coef3[c] g + coef3[C+c] z + coef3[2C+c]`` is formed on load (no dz pass over HBM).
+    ``bn_stats``: ``x`` is the ReLU output of a BatchNorm (the dx mask); the kernel also writes that
+    BN's backward partial sums (sum dx, sum dx*x per block, as :func:`igemm` ``bn_stats``) and the
+    function returns ``(dx, (slab, rows))``."""
     Nx, Hx, Wx, CI, ldx = _nhwc(x, "bwd.x")
     if "bwd" in _ABLATE:
         N_, H_, W_ = Nx, Hx, Wx
@@ -617,6 +628,18 @@ def conv_bwd_fused(g: Optional[torch.Tensor], x: torch.Tensor, wd: torch.Tensor,
         hslab = torch.empty(nblk * (CO + 1) + CO + 1, dtype=torch.float32, device=x.device)
         hw = hw.reshape(-1).contiguous()
         a.tgt, a.hw, a.hb, a.dS, a.hslab = tgt.data_ptr(), hw.data_ptr(), hb.data_ptr(), dS.data_ptr(), hslab.data_ptr()
+    bnslab = None
+    if bn is not None:
+        z, coef3 = bn
+        assert head is None and pool is None and w1 is None, "BN mode: plain gradient source"
+        Nz, Hz, Wz, Cz, ldz = _nhwc(z, "bwd.z")
+        assert (Nz, Hz, Wz, Cz) == (N, H, W, CO) and ldz == ldg, "BN mode: z laid out like g"
+        assert coef3.dtype == torch.float32 and coef3.is_contiguous() and coef3.numel() == 3 * CO
+        a.z, a.bncoef = z.data_ptr(), coef3.data_ptr()
+    if bn_stats:
+        assert bn is not None and epi == 0, "BN statistics of the layer below: BN mode with the masked dx"
+        bnslab = torch.empty(nblk * 2 * CI, dtype=torch.float32, device=x.device)
+        a.bnslab = bnslab.data_ptr()
     _check(L.dpa_bwd_stream(ctypes.byref(a), c_int(CI), c_int(CO), c_int(epi), st), "bwd_stream")
     if hslab is not None:
         _check(L.dpa_head_grad_from_slab(_p(hslab), c_int(nblk), c_int(CO), _p(hslab[nblk * (CO + 1):]), _p(hgw),
@@ -626,7 +649,8 @@ def conv_bwd_fused(g: Optional[torch.Tensor], x: torch.Tensor, wd: torch.Tensor,
     if slab1 is not None:
         _check(L.dpa_wgrad_reduce(_p(slab1), _p(slab1[nblk * 9 * CI * 8:]), _p(gw1), _p(gb1), c_int(nblk),
                                   c_int(9), c_int(CI), c_int(8), c_int(creal), c_int(0), st), "wgrad_reduce(bwd_stream.w1)")
-    return (dx, dx2) if dx2 is not None else dx
+    out = (dx, dx2) if dx2 is not None else dx
+    return (out, (bnslab, nblk)) if bnslab is not None else out
 
 
 # ------------------------------------------------------------------------- fused first-level forward
@@ -909,6 +933,32 @@ def bn_bwd(g: torch.Tensor, z: torch.Tensor, saved: torch.Tensor, bn: torch.nn.B
                         _p(scratch[rows * 2 * C:]), _p(dgamma), _p(dbeta), _p(_flat_f32(bn.bias, C, "bn.bias")),
                         c_int(pre_rows), _stream(g)), "bn_bwd")
     return dz
+
+
+def bn_bwd_coef(g: torch.Tensor, z: torch.Tensor, saved: torch.Tensor, bn: torch.nn.BatchNorm2d,
+                dgamma: Optional[torch.Tensor], dbeta: Optional[torch.Tensor], stats: Optional[list] = None) -> torch.Tensor:
+    """:func:`bn_bwd` without its elementwise pass: returns coef3 (fp32 [3C]) with
+    ``dz = coef3[c] g + coef3[C+c] z + coef3[2C+c]`` for a consumer that forms dz on load
+    (:func:`conv_bwd_fused` ``bn``); dgamma/dbeta accumulate as in :func:`bn_bwd`."""
+    N, H, W, C, ldg = _nhwc(g, "bn_coef.g")
+    Nz, Hz, Wz, Cz, ldz = _nhwc(z, "bn_coef.z")
+    assert (Nz, Hz, Wz, Cz) == (N, H, W, C) and saved.numel() == 2 * C
+    P = N * H * W
+    L = _lib.lib()
+    rows = L.dpa_bn_slab_rows(c_ll(P), c_int(C))
+    scratch = torch.empty(rows * 2 * C + 3 * C, dtype=torch.float32, device=g.device)
+    if dgamma is not None:
+        _flat_f32(dgamma, C, "bn.dgamma")
+    if dbeta is not None:
+        _flat_f32(dbeta, C, "bn.dbeta")
+    slab, pre_rows = scratch[:rows * 2 * C], 0
+    if stats:
+        slab, pre_rows = _fold_slab(*stats, 2 * C)
+    coef3 = scratch[rows * 2 * C:]
+    _check(L.dpa_bn_bwd_coef(_p(g), c_int(ldg), _p(z), c_int(ldz), c_ll(P), c_int(C),
+                             _p(_flat_f32(bn.weight, C, "bn.weight")), _p(saved), _p(slab), _p(coef3), _p(dgamma),
+                             _p(dbeta), _p(_flat_f32(bn.bias, C, "bn.bias")), c_int(pre_rows), _stream(g)), "bn_bwd_coef")
+    return coef3
 
 
 def up2_fwd(x: torch.Tensor, y: torch.Tensor):

@@ -177,3 +177,57 @@ def test_conv_bwd_fused_first_level_matches_separate(hip_lib, N, H, W):
     w1r = torch.zeros(C, CR, 3, 3, requires_grad=True)
     F.conv2d(x1n, w1r, padding=1).backward(g1.permute(0, 3, 1, 2).float().cpu())
     assert _rel((gw1 - gw10).cpu(), w1r.grad.reshape(-1)) < 1e-4
+
+
+@pytest.mark.parametrize("N,H,W,Cin,Cout,epi", [
+    (2, 5, 64, 32, 32, "stats"), (1, 6, 128, 64, 64, "stats"), (2, 4, 64, 32, 64, "stats"), (1, 5, 64, 64, 32, "stats"),
+    (2, 3, 64, 64, 32, "split"), (2, 4, 64, 32, 64, "plain"), (1, 5, 120, 64, 64, "stats"),
+])
+def test_conv_bwd_fused_batchnorm_modes(hip_lib, N, H, W, Cin, Cout, epi):
+    """BatchNorm backward formed in the fused backward's loader (dz from the masked BN-output gradient
+    and the BN input z) == bn_bwd's elementwise pass followed by the plain fused backward: the same
+    bf16 dz, so dx and the weight / bias gradients agree exactly; dgamma / dbeta equal; with ``stats``
+    the per-block (sum dx, sum dx*x) partials of the layer below's BatchNorm match torch sums of dx."""
+    from distributedpytorch_amd.ops import kernels as K
+    torch.manual_seed(11)
+    z = (torch.randn(N, H, W, Cout) * 1.5 + 0.2).to(torch.bfloat16).cuda()
+    x = _nhwc(_bf(F.relu(torch.randn(N, Cin, H, W))))
+    w = _bf(torch.randn(Cout, Cin, 3, 3) * 0.05)
+    packed, ng, kd = _pack_one(1, w)
+    res = []
+    for fused in (True, False):
+        bn = torch.nn.BatchNorm2d(Cout).cuda()
+        with torch.no_grad():
+            bn.weight.copy_(torch.linspace(0.6, 1.4, Cout))
+            bn.bias.copy_(torch.linspace(-0.3, 0.3, Cout))
+        y = torch.empty_like(z)
+        saved = K.bn_fwd(z, y, bn, train=True)
+        torch.manual_seed(12)
+        g = (torch.randn(N, H, W, Cout, device="cuda") * (y > 0)).to(torch.bfloat16)   # ReLU-masked
+        dgam, dbet = torch.zeros(Cout, device="cuda"), torch.zeros(Cout, device="cuda")
+        gw, gb = torch.zeros(Cout * Cin * 9, device="cuda"), torch.zeros(Cout, device="cuda")
+        kw = dict(mask=epi == "stats")
+        if epi == "split":
+            kw.update(dx2=torch.empty(N, H, W, Cin - Cin // 2, dtype=torch.bfloat16, device="cuda"), split=Cin // 2)
+        st = None
+        if fused:
+            coef = K.bn_bwd_coef(g, z, saved, bn, dgam, dbet)
+            out = K.conv_bwd_fused(g, x, packed, kd, gw, gb, bn=(z, coef), bn_stats=epi == "stats", **kw)
+            if epi == "stats":
+                out, st = out
+        else:
+            dz = K.bn_bwd(g, z, saved, bn, dgam, dbet)
+            out = K.conv_bwd_fused(dz, x, packed, kd, gw, gb, **kw)
+        dx = torch.cat([out[0], out[1]], dim=3) if epi == "split" else out
+        torch.cuda.synchronize()
+        res.append((dx.float().cpu(), gw.cpu(), gb.cpu(), dgam.cpu(), dbet.cpu(), st))
+    (dxa, gwa, gba, dga, dba, st), (dxb, gwb, gbb, dgb, dbb, _) = res
+    assert torch.equal(dxa, dxb)
+    assert torch.equal(gwa, gwb) and torch.equal(gba, gbb)
+    assert torch.equal(dga, dgb) and torch.equal(dba, dbb)
+    if epi == "stats":
+        slab, rows = st
+        sums = slab.view(rows, 2, Cin).sum(0).cpu()
+        xs = x.float().cpu()
+        assert _rel(sums[0], dxa.sum((0, 1, 2))) < 1e-3
+        assert _rel(sums[1], (dxa * xs).sum((0, 1, 2))) < 1e-3
