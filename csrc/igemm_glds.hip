@@ -793,6 +793,249 @@ __global__ __launch_bounds__(512) void igemm_pp_kernel(IgemmArgs a) {
   glds_epilogue<TC, TP, WC, WP>(a, acc, M, m0, c0, wc, wp, lane);
 }
 
+// ------------------------------------------------------------------------------------------------
+// Ping-pong, steady-state form (cfg 14): igemm_pp_kernel's tile, half-tile schedule and wave pairing,
+// restructured so the K loop body is straight-line code: the K-tile coordinates of the two tiles in
+// flight (s+1, s+2) advance incrementally (no per-issue integer division), every phase of the steady
+// loop issues its half-tile and waits a constant vmcnt(8), and the last two K-tiles are a peeled tail
+// with compile-time waits.  Per phase: B fragments first, then A (as the 8-phase template orders them).
+__global__ __launch_bounds__(512) void igemm_pp2_kernel(IgemmArgs a) {
+  constexpr int BC = 256, BP = 256, WC = 128, WP = 64, TC = 8, TP = 4, RBY = 128;
+  constexpr int STAGE = (BC + BP) * RBY;
+  __shared__ __attribute__((aligned(16))) char lds[2 * STAGE];
+
+  const int M = a.N * a.Ho * a.Wo;
+  const int nct = a.Ngemm / BC;
+  const int npt = (M + BP - 1) / BP;
+  const int bid = xcd_remap(blockIdx.x, npt * nct);
+  int pt, ct;
+  glds_tile(bid, npt, nct, pt, ct);
+  const int m0 = pt * BP, c0 = ct * BC;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wc = wid & 1, wp = wid >> 1, grp = wid >> 2;
+  const int lr = lane >> 3;
+  const int lchunk = (lane & 7) ^ lr;
+  unsigned woff[2][2], pbase[2][2], tmask[2][2];
+  const int taps = a.KH * a.KW;
+  const int hw = a.Ho * a.Wo;
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      woff[h][j] = (unsigned)(((c0 + j * 128 + h * 64 + wid * 8 + lr) * a.Kpad) * 2 + lchunk * 16);
+      const int m = m0 + (2 * j + grp) * 64 + h * 32 + (wid & 3) * 8 + lr;
+      const bool pok = m < M;
+      const int mm = pok ? m : 0;
+      const int pn = mm / hw;
+      const int rem = mm - pn * hw;
+      const int ph = rem / a.Wo, pw = rem - ph * a.Wo;
+      const int h0 = ph * a.stride - a.pad, w0 = pw * a.stride - a.pad;
+      unsigned msk = 0;
+      for (int t = 0; t < taps; ++t) {
+        const int kh = t / a.KW, kw = t - kh * a.KW;
+        const int ih = h0 + kh, iw = w0 + kw;
+        if (pok && ih >= 0 && ih < a.Hs && iw >= 0 && iw < a.Ws) msk |= 1u << t;
+      }
+      tmask[h][j] = msk;
+      pbase[h][j] = (unsigned)((((pn * a.Hs + h0) * a.Ws + w0) * a.ldx) * 2 + lchunk * 16);
+    }
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, 0, (int)a.xbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc((void*)a.w, 0, 0x7fffffff, 0x00020000);
+  const int S = a.Kpad / 64;                   // host guarantees S >= 2
+  const bool slm = !(a.korder & 1) && a.Kpad == taps * a.Cs;
+
+  // K-tile coordinates, advanced one K-tile at a time (wave-uniform scalars)
+  struct KC { int tap, ci, kh, kw; };
+  auto knext = [&](KC c) {
+    bool tapinc = true;
+    if (!slm) {
+      c.ci += 64;
+      tapinc = c.ci == a.Cs;
+      if (tapinc) c.ci = 0;
+    }
+    if (tapinc) {
+      if (++c.tap == taps) {
+        c.tap = c.kh = c.kw = 0;
+        if (slm) c.ci += 64;
+      } else if (++c.kw == a.KW) {
+        c.kw = 0;
+        ++c.kh;
+      }
+    }
+    return c;
+  };
+  auto issueA = [&](int h, int buf, KC c) {
+    char* base = lds + buf * STAGE;
+    const unsigned wk = (unsigned)((c.tap * a.Cs + c.ci) * 2);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) dma16(wrs, base + (j * 128 + h * 64 + wid * 8) * RBY, woff[h][j] + wk);
+  };
+  auto issueB = [&](int h, int buf, KC c) {
+    char* base = lds + buf * STAGE + BC * RBY;
+    const unsigned delta = (unsigned)(((c.kh * a.Ws + c.kw) * a.ldx + c.ci) * 2);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const bool ok = (tmask[h][j] >> c.tap) & 1u;
+      dma16(xr, base + ((2 * j + grp) * 64 + h * 32 + (wid & 3) * 8) * RBY, ok ? pbase[h][j] + delta : 0x80000000u);
+    }
+  };
+
+  f32x4_t acc[TC][TP];
+#pragma unroll
+  for (int ic = 0; ic < TC; ++ic)
+#pragma unroll
+    for (int ip = 0; ip < TP; ++ip) acc[ic][ip] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  KC k0{0, 0, 0, 0};
+  KC k1 = knext(k0);
+  issueA(0, 0, k0);
+  issueB(0, 0, k0);
+  issueB(1, 0, k0);
+  issueA(1, 0, k0);
+  issueA(0, 1, k1);
+  issueB(0, 1, k1);
+  wait_vm<8>();
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  if (grp) __builtin_amdgcn_s_barrier();       // the second half runs one barrier behind
+  __builtin_amdgcn_sched_barrier(0);
+
+  bf16x8_t af[4][2], bfr[2][2][2];
+  auto readA = [&](const char* Wt, int h) {
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int ic = 0; ic < 4; ++ic) {
+        const int row = wc * WC + h * 64 + ic * 16 + (lane & 15);
+        const int chunk = kk * 4 + (lane >> 4);
+        af[ic][kk] = *reinterpret_cast<const bf16x8_t*>(Wt + row * RBY + ((chunk ^ (row & 7)) << 4));
+      }
+  };
+  auto readB = [&](const char* P, int h) {
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int ip = 0; ip < 2; ++ip) {
+        const int row = wp * WP + h * 32 + ip * 16 + (lane & 15);
+        const int chunk = kk * 4 + (lane >> 4);
+        bfr[h][ip][kk] = *reinterpret_cast<const bf16x8_t*>(P + row * RBY + ((chunk ^ (row & 7)) << 4));
+      }
+  };
+  auto mfma_quad = [&](int qa, int qb) {
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int ic = 0; ic < 4; ++ic)
+#pragma unroll
+        for (int ip = 0; ip < 2; ++ip)
+          acc[qa * 4 + ic][qb * 2 + ip] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ic][kk], bfr[qb][ip][kk], acc[qa * 4 + ic][qb * 2 + ip], 0, 0, 0);
+  };
+  auto sync_in = [&]() {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+  };
+  auto sync_out = [&]() {
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  // steady state: K-tiles s < S-2 issue halves of s+1 (B1, A1) and s+2 (A0, B0)
+  KC kc1 = k1, kc2 = knext(k1);
+  int s = 0;
+  for (; s < S - 2; ++s) {
+    const int b = s & 1;
+    const char* Wt = lds + b * STAGE;
+    const char* P = Wt + BC * RBY;
+    readB(P, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    readA(Wt, 0);
+    issueB(1, b ^ 1, kc1);
+    wait_vm<8>();
+    sync_in();
+    mfma_quad(0, 0);
+    sync_out();
+    readB(P, 1);
+    issueA(1, b ^ 1, kc1);
+    wait_vm<8>();
+    sync_in();
+    mfma_quad(0, 1);
+    sync_out();
+    readA(Wt, 1);
+    issueA(0, b, kc2);
+    sync_in();
+    mfma_quad(1, 1);
+    sync_out();
+    issueB(0, b, kc2);
+    wait_vm<8>();
+    sync_in();
+    mfma_quad(1, 0);
+    sync_out();
+    kc1 = kc2;
+    kc2 = knext(kc2);
+  }
+  {  // K-tile S-2: halves of S-1 still to issue; nothing of S
+    const int b = s & 1;
+    const char* Wt = lds + b * STAGE;
+    const char* P = Wt + BC * RBY;
+    readB(P, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    readA(Wt, 0);
+    issueB(1, b ^ 1, kc1);
+    wait_vm<8>();
+    sync_in();
+    mfma_quad(0, 0);
+    sync_out();
+    readB(P, 1);
+    issueA(1, b ^ 1, kc1);
+    wait_vm<8>();
+    sync_in();
+    mfma_quad(0, 1);
+    sync_out();
+    readA(Wt, 1);
+    sync_in();
+    mfma_quad(1, 1);
+    sync_out();
+    wait_vm<4>();                              // A0/B0 of S-1 (B1, A1 of S-1 may stay in flight)
+    sync_in();
+    mfma_quad(1, 0);
+    sync_out();
+    ++s;
+  }
+  {  // K-tile S-1
+    const int b = s & 1;
+    const char* Wt = lds + b * STAGE;
+    const char* P = Wt + BC * RBY;
+    readB(P, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    readA(Wt, 0);
+    wait_vm<2>();                              // B1 of S-1
+    sync_in();
+    mfma_quad(0, 0);
+    sync_out();
+    readB(P, 1);
+    wait_vm<0>();                              // A1 of S-1
+    sync_in();
+    mfma_quad(0, 1);
+    sync_out();
+    readA(Wt, 1);
+    sync_in();
+    mfma_quad(1, 1);
+    sync_out();
+    sync_in();
+    mfma_quad(1, 0);
+    sync_out();
+  }
+  if (!grp) __builtin_amdgcn_s_barrier();      // balance the second half's extra barrier
+
+  glds_epilogue<TC, TP, WC, WP>(a, acc, M, m0, c0, wc, wp, lane);
+}
+
 template <int BC, int BP, int WC, int WP, int ST, int BK = 64, bool PRE = false>
 static int launch_glds(const IgemmArgs& a, hipStream_t st) {
   const int M = a.N * a.Ho * a.Wo;
@@ -815,6 +1058,7 @@ DPA_API int dpa_igemm_glds(const IgemmArgs* args, int cfg, hipStream_t st) {
   if (cfg & 16) a.korder |= 1;   // A/B: tap-major K-tile order
   if (cfg & 32) a.korder |= 2;   // A/B: no persistent kernel in the auto choice
   const bool no_pre = cfg & 64;  // A/B: the compiler's read/MFMA interleave (cfg 12 / 13) for cfg 3 / 2
+  const bool no_pp = cfg & 128;  // A/B: the 2-stage cfg 3 instead of the ping-pong cfg 14 in the auto choice
   cfg &= 15;
   if ((a.Cs & 63) || (a.Kpad & 63) || (a.ldx & 7) || (a.ldy & 3) || a.KH * a.KW > 32) return (int)hipErrorInvalidValue;
   if (a.mode == 1 && (a.Cout & 3)) return (int)hipErrorInvalidValue;
@@ -828,7 +1072,10 @@ DPA_API int dpa_igemm_glds(const IgemmArgs* args, int cfg, hipStream_t st) {
     // which hides each tile's first-load latency and epilogue behind the neighbouring tile, is 3-9 %
     // faster there; from K = 1024 on the fragment-preloaded cfg 3 wins by 3-6 %
     // (profiles/kbench_glds_shortk_b256_r02.txt, interleaved)
-    if (a.Ngemm % 256 == 0 && grid_of(256, 256) >= 512) cfg = (a.Kpad <= 8 * 64 && !(a.korder & 2)) ? 8 : 3;
+    // K >= 1024: the ping-pong steady-state kernel, 4-10 % faster than cfg 3 on every deep layer and
+    // 1.38 vs 1.18 PF on a plain 8192^3 GEMM (profiles/kbench_glds_pp2_b256_r03.txt)
+    if (a.Ngemm % 256 == 0 && grid_of(256, 256) >= 512)
+      cfg = (a.Kpad <= 8 * 64 && !(a.korder & 2)) ? 8 : (no_pp ? 3 : 14);
     else if (a.Ngemm % 128 == 0 && grid_of(128, 256) >= 512) cfg = 2;
     else if (a.Ngemm % 256 == 0 && grid_of(256, 128) >= 512) cfg = 1;
     else cfg = 4;
@@ -850,6 +1097,12 @@ DPA_API int dpa_igemm_glds(const IgemmArgs* args, int cfg, hipStream_t st) {
       if (a.Ngemm % 256) break;
       const int grid = ((a.N * a.Ho * a.Wo + 255) / 256) * (a.Ngemm / 256);
       hipLaunchKernelGGL(igemm_pp_kernel, dim3(grid), dim3(512), 0, st, a);
+      return (int)hipGetLastError();
+    }
+    case 14: {
+      if (a.Ngemm % 256 || a.Kpad < 128) break;     // the steady loop + peeled tail need S >= 2
+      const int grid = ((a.N * a.Ho * a.Wo + 255) / 256) * (a.Ngemm / 256);
+      hipLaunchKernelGGL(igemm_pp2_kernel, dim3(grid), dim3(512), 0, st, a);
       return (int)hipGetLastError();
     }
     case 11: {
