@@ -324,6 +324,9 @@ def wgrad(A: torch.Tensor, B: torch.Tensor, *, kind: int, grid, M: int, Nc: int,
     generic per-tap gather kernel; ``stream`` / ``halo`` / ``generic`` force one."""
     if _ABLATE and ("wgrad" in _ABLATE or ("wgrad_deep" in _ABLATE and (M >= 128 or Nc >= 128))):
         return
+    if (path == "gemm" or (path == "auto" and wgrad_gemm_eligible(M, Nc, grid))) and kind == 0 and cfg == 0 \
+            and A.shape[1:3] == B.shape[1:3] == tuple(grid[1:]):
+        return _wgrad_gemm(A, B, grid=grid, M=M, Nc=Nc, gw=gw, gb=gb, Nreal=Nreal)
     if (path == "rows" or (path == "auto" and wgrad_rows_eligible(M, Nc, grid[2]))) and kind == 0 and cfg == 0:
         return _wgrad_rows(A, B, grid=grid, M=M, Nc=Nc, gw=gw, gb=gb, Nreal=Nreal)
     if path in ("auto", "stream") and kind == 0 and cfg == 0 and (USE_STREAM or path == "stream") \
@@ -394,6 +397,44 @@ def wgrad_multi_eligible(M: int, Nc: int, W: int) -> bool:
 
 def wgrad_rows_eligible(M: int, Nc: int, W: int) -> bool:
     return USE_WGRAD_ROWS and M % 128 == 0 and Nc % 64 == 0 and W >= 48
+
+
+# deep-layer weight gradients as a dense 256x256 LDS-DMA GEMM on the ping-pong schedule
+# (csrc/wgrad_gemm.hip); DPA_NO_WGRAD_GEMM=1 falls back to the row-streaming kernel
+USE_WGRAD_GEMM = os.environ.get("DPA_NO_WGRAD_GEMM", "0") != "1"
+WGRAD_GEMM_BLOCKS = int(os.environ.get("DPA_WGRAD_GEMM_BLOCKS", "768"))
+
+
+def wgrad_gemm_eligible(M: int, Nc: int, grid) -> bool:
+    N, H, W = grid
+    return (USE_WGRAD_GEMM and M % 256 == 0 and Nc % 8 == 0 and Nc >= 64 and (W % 64 == 0 or W == 32)
+            and (H * W) % 64 == 0)
+
+
+def _wgrad_gemm(A, B, *, grid, M, Nc, gw, gb, Nreal, blocks: int = 0):
+    """conv3x3 weight (+bias) gradient of the deep layers (M = Cout % 256 == 0): one workgroup per
+    (group of images, 256 x 256 tile of dW[co][tap, ci]); split-K slabs over the image groups."""
+    NA, HA, WA, CA, lda = _nhwc(A, "wgrad_gemm.A")
+    NB, HB, WB, CB, ldb = _nhwc(B, "wgrad_gemm.B")
+    N, Hg, Wg = grid
+    assert (HA, WA) == (Hg, Wg) == (HB, WB) and CA >= M and CB >= Nc and NA == NB == N
+    assert gw.dtype == torch.float32 and gw.is_contiguous() and gw.numel() == M * Nreal * 9
+    tiles = (M // 256) * -(-9 * Nc // 256)
+    spi = Hg * Wg // 64
+    ips = max(1, -(-N * tiles // (blocks or WGRAD_GEMM_BLOCKS)), -(-2 // spi))
+    # 32-bit offsets inside one split's images
+    ips = max(1, min(ips, _MAX_BYTES // (Hg * Wg * max(lda, ldb) * 2)))
+    splits = -(-N // ips)
+    slab = torch.empty(splits * 9 * M * Nc + splits * M, dtype=torch.float32, device=A.device)
+    bslab = slab[splits * 9 * M * Nc:] if gb is not None else None
+    a = WgradArgs(A.data_ptr(), B.data_ptr(), slab.data_ptr(), None if bslab is None else bslab.data_ptr(), lda, ldb,
+                  N, Hg, Wg, HA, WA, HB, WB, M, Nc, 1, 1, 3, ips, splits, ips * Hg * Wg * lda * 2,
+                  ips * Hg * Wg * ldb * 2)
+    L = _lib.lib()
+    st = _stream(A)
+    _check(L.dpa_wgrad_gemm(ctypes.byref(a), st), "wgrad_gemm")
+    _check(L.dpa_wgrad_reduce(_p(slab), _p(bslab), _p(gw), _p(gb), c_int(splits), c_int(9), c_int(M), c_int(Nc),
+                              c_int(Nreal), c_int(0), st), "wgrad_reduce(gemm)")
 
 
 def _wgrad_rows(A, B, *, grid, M, Nc, gw, gb, Nreal, rh: int = 0, depth: int = 0, tabs=None):

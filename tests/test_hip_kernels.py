@@ -224,7 +224,11 @@ def test_deconv_dgrad_from_concat(hip_lib, N, h, w, Cin, Cout):
     (2, 5, 200, 3, 32, 8, "stream"), (1, 3, 480, 64, 64, None, "stream"),
     # deep layers on the LDS-DMA row pipeline (128 x 64 x 9-tap tiles; ragged strips, row segments)
     (2, 5, 64, 128, 128, None, "rows"), (1, 7, 120, 64, 128, None, "rows"), (2, 4, 128, 256, 256, None, "rows"),
-    (1, 3, 48, 64, 256, None, "rows"), (1, 66, 64, 128, 128, None, "rows"), (2, 9, 100, 192, 128, None, "rows")])
+    (1, 3, 48, 64, 256, None, "rows"), (1, 66, 64, 128, 128, None, "rows"), (2, 9, 100, 192, 128, None, "rows"),
+    # deep layers as a dense 256x256 LDS-DMA GEMM (csrc/wgrad_gemm.hip): partial last column tile
+    # (9 x 128 = 1152, 9 x 64 = 576 columns), 32-wide rows (two rows per K-step), several channel tiles
+    (2, 4, 64, 128, 256, None, "gemm"), (3, 6, 32, 256, 256, None, "gemm"), (1, 2, 128, 64, 512, None, "gemm"),
+    (2, 5, 64, 512, 256, None, "gemm")])
 def test_conv3x3_wgrad(hip_lib, N, H, W, Cin, Cout, cin_pad, path):
     from distributedpytorch_amd.ops import kernels as K
     torch.manual_seed(4)
@@ -600,3 +604,23 @@ def test_wgrad_rows_pipeline_depths(hip_lib, depth):
         torch.cuda.synchronize()
         assert _rel(gw.cpu().view(Cout, Cin, 3, 3), wr.grad) < 1e-2, (depth, rh)
         assert _rel(gb.cpu(), br.grad) < 1e-2, (depth, rh)
+
+
+@pytest.mark.parametrize("blocks", [1, 7, 100000])
+def test_wgrad_gemm_image_groups(hip_lib, blocks):
+    """csrc/wgrad_gemm.hip with 1 .. N images per split (the split-K slabs over image groups, K-steps
+    crossing image boundaries, a short last group) against the fp32 reference."""
+    from distributedpytorch_amd.ops import kernels as K
+    torch.manual_seed(17)
+    N, H, W, Cin, Cout = 5, 4, 64, 256, 256
+    x = _bf(torch.randn(N, Cin, H, W))
+    g = _bf(torch.randn(N, Cout, H, W))
+    wr = torch.zeros(Cout, Cin, 3, 3, requires_grad=True)
+    br = torch.zeros(Cout, requires_grad=True)
+    F.conv2d(x, wr, br, padding=1).backward(g)
+    gw = torch.zeros(Cout * Cin * 9, device="cuda")
+    gb = torch.zeros(Cout, device="cuda")
+    K._wgrad_gemm(_nhwc(g), _nhwc(x), grid=(N, H, W), M=Cout, Nc=Cin, gw=gw, gb=gb, Nreal=Cin, blocks=blocks)
+    torch.cuda.synchronize()
+    assert _rel(gw.cpu().view(Cout, Cin, 3, 3), wr.grad) < 1e-2, blocks
+    assert _rel(gb.cpu(), br.grad) < 1e-2, blocks
