@@ -48,6 +48,25 @@ __device__ __forceinline__ bf16x8_t wr_tr(const char* base, int off0, int off1) 
   return __builtin_bit_cast(bf16x8_t, v);
 }
 
+// the same two reads as inline asm: the builtin makes hipcc wait vmcnt(0) before every read while an
+// LDS-DMA is in flight (it cannot tell the read from the DMA's destination) -- that drained the row
+// pipeline before each row's first fragment read.  The asm reads are invisible to the wait-count pass:
+// the kernel waits lgkmcnt(0) itself before the MFMAs that consume them (wr_lgkm0).
+__device__ __forceinline__ s16x4_t wr_trld(unsigned addr) {
+  s16x4_t v;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"(addr) : "memory");
+  return v;
+}
+__device__ __forceinline__ bf16x8_t wr_join(s16x4_t v0, s16x4_t v1) {
+  typedef __attribute__((ext_vector_type(8))) short s16x8_t;
+  s16x8_t v = __builtin_shufflevector(v0, v1, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8_t, v);
+}
+__device__ __forceinline__ void wr_lgkm0() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
 }  // namespace
 
 // D: row bundles in flight beyond the one being consumed.  LDS: (D+1) gradient rows + (D+3) input
@@ -177,20 +196,41 @@ __global__ __launch_bounds__(768) void wgrad_rows_kernel(WgradArgs a, int rh) {
     __builtin_amdgcn_sched_barrier(0);
     const char* Ai = Abuf + (t % NA) * WR_AIMG;
     const char* Bi = Bbuf + ((t + kh) % NB) * WR_BIMG;   // input row h0 + t + kh - 1
+    const unsigned ua = (unsigned)(size_t)LDS_PTR(char, Ai), ub = (unsigned)(size_t)LDS_PTR(char, Bi);
 #pragma unroll
     for (int ks = 0; ks < WR_BP / 32; ++ks) {
+      // A fragments + the kw = 0 B pair, then per kw: the next pair's reads behind this pair's MFMAs
+      s16x4_t ra[4][2], rb[2][2][2];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) ra[i][h] = wr_trld(ua + ks * 32 * WR_RBA + offA[i][h]);
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) rb[0][j][h] = wr_trld(ub + ks * 32 * WR_RBB + offB[0][j][h]);
+      wr_lgkm0();
       bf16x8_t af[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) af[i] = wr_tr(Ai + ks * 32 * WR_RBA, offA[i][0], offA[i][1]);
+      for (int i = 0; i < 4; ++i) af[i] = wr_join(ra[i][0], ra[i][1]);
 #pragma unroll
-      for (int kw = 0; kw < 3; ++kw)
+      for (int kw = 0; kw < 3; ++kw) {
+        const int cur = kw & 1;
+        if (kw < 2) {
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) rb[cur ^ 1][j][h] = wr_trld(ub + ks * 32 * WR_RBB + offB[kw + 1][j][h]);
+        }
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
-          const bf16x8_t bf = wr_tr(Bi + ks * 32 * WR_RBB, offB[kw][j][0], offB[kw][j][1]);
+          const bf16x8_t bf = wr_join(rb[cur][j][0], rb[cur][j][1]);
 #pragma unroll
           for (int i = 0; i < 4; ++i)
             acc[kw][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf, acc[kw][i][j], 0, 0, 0);
         }
+        if (kw < 2) wr_lgkm0();
+      }
     }
     if (bias_lane) {
       const int ch = tid & 15;
