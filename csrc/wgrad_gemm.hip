@@ -82,10 +82,12 @@ __global__ __launch_bounds__(512) void wgrad_gemm_kernel(WgradArgs a) {
   const int wc = wid & 1, wp = wid >> 1, grp = wid >> 2;
 
   // split's image range: 64-bit bases, 32-bit offsets inside it (host: < 2^31 bytes)
+  // (per-image tables -- the microbatches of a pipeline stage: the host makes every split's images
+  // consecutive images of ONE tensor, so the split's first image pointer is its base)
   const __amdgpu_buffer_rsrc_t ar = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(a.A + (long)nimg0 * HW * a.lda), 0, (int)a.abytes, 0x00020000);
+      (void*)(a.atab ? a.atab[nimg0] : a.A + (long)nimg0 * HW * a.lda), 0, (int)a.abytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t br = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(a.B + (long)nimg0 * HW * a.ldb), 0, (int)a.bbytes, 0x00020000);
+      (void*)(a.btab ? a.btab[nimg0] : a.B + (long)nimg0 * HW * a.ldb), 0, (int)a.bbytes, 0x00020000);
 
   // ---- per-lane DMA constants.  Half-tile image = 16 instructions of 1 KB (4 pixel rows x 16
   // chunks); wave wid issues instructions wid and 8 + wid.  Lane l: pixel row r = 4 ins + (l >> 4),
@@ -392,15 +394,15 @@ __global__ __launch_bounds__(512) void wgrad_gemm_kernel(WgradArgs a) {
 }
 
 // Eligible: conv3x3 s1 p1 (A = the output gradient, B = the layer input, same pixel grid), M % 256 == 0,
-// Nc % 8 == 0, W % 64 == 0 or W == 32, H * W % 64 == 0, 16-B aligned channel strides, no
-// per-image tables; pix_per_split = images per split (splits = ceil(N / ips)), >= 2 K-steps per split,
+// Nc % 8 == 0, W % 64 == 0 or W == 32, H * W % 64 == 0, 16-B aligned channel strides; with per-image
+// tables every split's images must be consecutive images of one tensor (host); pix_per_split = images per split (splits = ceil(N / ips)), >= 2 K-steps per split,
 // each split's images addressable with 32-bit offsets (abytes / bbytes = ips images).
 DPA_API int dpa_wgrad_gemm(const WgradArgs* args, hipStream_t st) {
   const WgradArgs& a = *args;
   const int ips = a.pix_per_split;
   if ((a.M % 256) || (a.Nc % 8) || (a.lda & 7) || (a.ldb & 7) || a.s != 1 || a.pad != 1 || a.KW != 3 ||
       a.HA != a.Hg || a.WA != a.Wg || a.HB != a.Hg || a.WB != a.Wg || (a.Wg % 64 && a.Wg != 32) ||
-      ((a.Hg * a.Wg) % 64) || a.atab || a.btab || ips < 1 || a.splits != (a.N + ips - 1) / ips ||
+      ((a.Hg * a.Wg) % 64) || (!a.atab != !a.btab) || ips < 1 || a.splits != (a.N + ips - 1) / ips ||
       (long)ips * a.Hg * a.Wg / 64 < 2 || a.lda < a.M || a.ldb < a.Nc ||
       (long)ips * a.Hg * a.Wg * a.lda * 2 > (long)a.abytes || (long)ips * a.Hg * a.Wg * a.ldb * 2 > (long)a.bbytes)
     return (int)hipErrorInvalidValue;

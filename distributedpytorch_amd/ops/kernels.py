@@ -411,25 +411,35 @@ def wgrad_gemm_eligible(M: int, Nc: int, grid) -> bool:
             and (H * W) % 64 == 0)
 
 
-def _wgrad_gemm(A, B, *, grid, M, Nc, gw, gb, Nreal, blocks: int = 0):
+def _wgrad_gemm(A, B, *, grid, M, Nc, gw, gb, Nreal, blocks: int = 0, tabs=None, group: int = 0):
     """conv3x3 weight (+bias) gradient of the deep layers (M = Cout % 256 == 0): one workgroup per
-    (group of images, 256 x 256 tile of dW[co][tap, ci]); split-K slabs over the image groups."""
+    (group of images, 256 x 256 tile of dW[co][tap, ci]); split-K slabs over the image groups.
+    ``tabs`` = per-image pointer tables (the images of ``group``-image tensors: every split stays
+    inside one of them)."""
     NA, HA, WA, CA, lda = _nhwc(A, "wgrad_gemm.A")
     NB, HB, WB, CB, ldb = _nhwc(B, "wgrad_gemm.B")
     N, Hg, Wg = grid
-    assert (HA, WA) == (Hg, Wg) == (HB, WB) and CA >= M and CB >= Nc and NA == NB == N
+    assert (HA, WA) == (Hg, Wg) == (HB, WB) and CA >= M and CB >= Nc
+    assert (NA == NB == N) or (tabs is not None and tabs[0].numel() == tabs[1].numel() == N and group > 0
+                               and N % group == 0)
     assert gw.dtype == torch.float32 and gw.is_contiguous() and gw.numel() == M * Nreal * 9
     tiles = (M // 256) * -(-9 * Nc // 256)
     spi = Hg * Wg // 64
     ips = max(1, -(-N * tiles // (blocks or WGRAD_GEMM_BLOCKS)), -(-2 // spi))
     # 32-bit offsets inside one split's images
     ips = max(1, min(ips, _MAX_BYTES // (Hg * Wg * max(lda, ldb) * 2)))
+    if tabs is not None:
+        while group % ips:        # a split never straddles two tensors
+            ips -= 1
+        assert ips * spi >= 2
     splits = -(-N // ips)
     slab = torch.empty(splits * 9 * M * Nc + splits * M, dtype=torch.float32, device=A.device)
     bslab = slab[splits * 9 * M * Nc:] if gb is not None else None
     a = WgradArgs(A.data_ptr(), B.data_ptr(), slab.data_ptr(), None if bslab is None else bslab.data_ptr(), lda, ldb,
                   N, Hg, Wg, HA, WA, HB, WB, M, Nc, 1, 1, 3, ips, splits, ips * Hg * Wg * lda * 2,
                   ips * Hg * Wg * ldb * 2)
+    if tabs is not None:
+        a.atab, a.btab = tabs[0].data_ptr(), tabs[1].data_ptr()
     L = _lib.lib()
     st = _stream(A)
     _check(L.dpa_wgrad_gemm(ctypes.byref(a), st), "wgrad_gemm")
@@ -489,6 +499,13 @@ def wgrad_multi(As, Bs, *, M: int, Nc: int, gw: torch.Tensor, gb: Optional[torch
     btab, nb = _image_table(Bs, Nc, "wgrad_multi.B")
     assert na == nb == N
     tabs = (atab, btab)
+    sizes = {a.shape[0] for a in As} | {b.shape[0] for b in Bs}
+    # splits cannot straddle two microbatch tensors: with few-image microbatches at the deepest levels
+    # (UNet-XL, 2 images of 32x32) that means short splits and a slab set several times the batch's
+    # dW -- keep the gemm path for >= 64 K-steps per split (profiles/pipeline_rehearsal_r03.txt)
+    if wgrad_gemm_eligible(M, Nc, (N, H, W)) and len(sizes) == 1 and min(sizes) * (H * W // 64) >= 64:
+        return _wgrad_gemm(As[0], Bs[0], grid=(N, H, W), M=M, Nc=Nc, gw=gw, gb=gb, Nreal=Nreal, tabs=tabs,
+                           group=sizes.pop())
     if wgrad_rows_eligible(M, Nc, W):
         return _wgrad_rows(As[0], Bs[0], grid=(N, H, W), M=M, Nc=Nc, gw=gw, gb=gb, Nreal=Nreal, tabs=tabs)
     return _wgrad_stream(As[0], Bs[0], grid=(N, H, W), M=M, Nc=Nc, gw=gw, gb=gb, Nreal=Nreal, tabs=tabs)

@@ -624,3 +624,25 @@ def test_wgrad_gemm_image_groups(hip_lib, blocks):
     torch.cuda.synchronize()
     assert _rel(gw.cpu().view(Cout, Cin, 3, 3), wr.grad) < 1e-2, blocks
     assert _rel(gb.cpu(), br.grad) < 1e-2, blocks
+
+
+@pytest.mark.parametrize("M,Nc,H,W,mb,nmb", [(256, 256, 4, 64, 3, 3), (256, 128, 3, 32, 2, 4), (512, 64, 2, 64, 4, 2),
+                                             (128, 64, 3, 64, 2, 3)])
+def test_wgrad_multi_microbatches(hip_lib, M, Nc, H, W, mb, nmb):
+    """One weight-gradient launch over the images of several microbatch tensors (per-image pointer
+    tables; a pipeline stage's deferred weight gradients): dense-GEMM path for M % 256 == 0, row kernels
+    otherwise -- equal to the fp32 reference over the concatenated batch."""
+    from distributedpytorch_amd.ops import kernels as K
+    torch.manual_seed(19)
+    xs = [_bf(torch.randn(mb, Nc, H, W)) for _ in range(nmb)]
+    gs = [_bf(torch.randn(mb, M, H, W)) for _ in range(nmb)]
+    wr = torch.zeros(M, Nc, 3, 3, requires_grad=True)
+    br = torch.zeros(M, requires_grad=True)
+    F.conv2d(torch.cat(xs), wr, br, padding=1).backward(torch.cat(gs))
+    gw = torch.zeros(M * Nc * 9, device="cuda")
+    gb = torch.zeros(M, device="cuda")
+    # separate allocations (not views of one tensor): the tables must carry each tensor's own base
+    K.wgrad_multi([_nhwc(g).clone() for g in gs], [_nhwc(x).clone() for x in xs], M=M, Nc=Nc, gw=gw, gb=gb, Nreal=Nc)
+    torch.cuda.synchronize()
+    assert _rel(gw.cpu().view(M, Nc, 3, 3), wr.grad) < 1e-2
+    assert _rel(gb.cpu(), br.grad) < 1e-2
