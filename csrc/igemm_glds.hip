@@ -799,6 +799,7 @@ __global__ __launch_bounds__(512) void igemm_pp_kernel(IgemmArgs a) {
 // flight (s+1, s+2) advance incrementally (no per-issue integer division), every phase of the steady
 // loop issues its half-tile and waits a constant vmcnt(8), and the last two K-tiles are a peeled tail
 // with compile-time waits.  Per phase: B fragments first, then A (as the 8-phase template orders them).
+template <int PROBE = 0>   // timing probes (A/B only): 1 = no epilogue, 2 = no MFMAs in the K loop
 __global__ __launch_bounds__(512) void igemm_pp2_kernel(IgemmArgs a) {
   constexpr int BC = 256, BP = 256, WC = 128, WP = 64, TC = 8, TP = 4, RBY = 128;
   constexpr int STAGE = (BC + BP) * RBY;
@@ -923,6 +924,17 @@ __global__ __launch_bounds__(512) void igemm_pp2_kernel(IgemmArgs a) {
       }
   };
   auto mfma_quad = [&](int qa, int qb) {
+    if constexpr (PROBE == 2) {
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int ic = 0; ic < 4; ++ic) asm volatile("" ::"v"(af[ic][kk]));
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int ip = 0; ip < 2; ++ip) asm volatile("" ::"v"(bfr[qb][ip][kk]));
+      return;
+    }
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
@@ -1033,6 +1045,13 @@ __global__ __launch_bounds__(512) void igemm_pp2_kernel(IgemmArgs a) {
   }
   if (!grp) __builtin_amdgcn_s_barrier();      // balance the second half's extra barrier
 
+  if constexpr (PROBE == 1) {
+#pragma unroll
+    for (int ic = 0; ic < TC; ++ic)
+#pragma unroll
+      for (int ip = 0; ip < TP; ++ip) asm volatile("" ::"v"(acc[ic][ip]));
+    return;
+  }
   glds_epilogue<TC, TP, WC, WP>(a, acc, M, m0, c0, wc, wp, lane);
 }
 
@@ -1059,6 +1078,7 @@ DPA_API int dpa_igemm_glds(const IgemmArgs* args, int cfg, hipStream_t st) {
   if (cfg & 32) a.korder |= 2;   // A/B: no persistent kernel in the auto choice
   const bool no_pre = cfg & 64;  // A/B: the compiler's read/MFMA interleave (cfg 12 / 13) for cfg 3 / 2
   const bool no_pp = cfg & 128;  // A/B: the 2-stage cfg 3 instead of the ping-pong cfg 14 in the auto choice
+  const int probe = (cfg >> 8) & 3;   // timing probes of cfg 14 (numerically wrong): 1 no epilogue, 2 no MFMAs
   cfg &= 15;
   if ((a.Cs & 63) || (a.Kpad & 63) || (a.ldx & 7) || (a.ldy & 3) || a.KH * a.KW > 32) return (int)hipErrorInvalidValue;
   if (a.mode == 1 && (a.Cout & 3)) return (int)hipErrorInvalidValue;
@@ -1102,7 +1122,9 @@ DPA_API int dpa_igemm_glds(const IgemmArgs* args, int cfg, hipStream_t st) {
     case 14: {
       if (a.Ngemm % 256 || a.Kpad < 128) break;     // the steady loop + peeled tail need S >= 2
       const int grid = ((a.N * a.Ho * a.Wo + 255) / 256) * (a.Ngemm / 256);
-      hipLaunchKernelGGL(igemm_pp2_kernel, dim3(grid), dim3(512), 0, st, a);
+      if (probe == 1) hipLaunchKernelGGL(igemm_pp2_kernel<1>, dim3(grid), dim3(512), 0, st, a);
+      else if (probe == 2) hipLaunchKernelGGL(igemm_pp2_kernel<2>, dim3(grid), dim3(512), 0, st, a);
+      else hipLaunchKernelGGL(igemm_pp2_kernel<0>, dim3(grid), dim3(512), 0, st, a);
       return (int)hipGetLastError();
     }
     case 11: {
