@@ -114,6 +114,70 @@ __device__ __forceinline__ void glds_epilogue(const IgemmArgs& a, f32x4_t (&acc)
   }
 }
 
+// Specialised epilogues (EP 1: plain conv forward -- optional bias, optional ReLU; EP 2: dgrad with the
+// ReLU-backward mask only): straight-line code with the row offsets computed once per pixel fragment.
+// The generic epilogue carries every mode (scatter, split, accumulate, mask) behind runtime branches:
+// ~5000 instructions that cost 10-20 % of a deep layer's time (profiles/experiments_r03_late.txt).
+// Out-of-range pixels store to an offset past the buffer's range check (dropped) instead of branching.
+template <int TC, int TP, int WC, int WP, int EP>
+__device__ __forceinline__ void glds_epilogue_fast(const IgemmArgs& a, f32x4_t (&acc)[TC][TP], int M, int m0, int c0,
+                                                   int wc, int wp, int lane) {
+  static_assert(EP == 1 || EP == 2, "fast epilogue kinds");
+  const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc((void*)a.y, 0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t mr = __builtin_amdgcn_make_buffer_rsrc((void*)(EP == 2 ? a.mask : a.y), 0, 0x7fffffff, 0x00020000);
+  const int cb = c0 + wc * WC + 4 * (lane >> 4);
+  float bias[TC][4];
+  const bool relu = a.relu != 0;
+#pragma unroll
+  for (int ic = 0; ic < TC; ++ic)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) bias[ic][e] = 0.f;
+  if (EP == 1 && a.bias) {
+#pragma unroll
+    for (int ic = 0; ic < TC; ++ic) {
+      const float4 b = *reinterpret_cast<const float4*>(a.bias + cb + ic * 16);
+      bias[ic][0] = b.x; bias[ic][1] = b.y; bias[ic][2] = b.z; bias[ic][3] = b.w;
+    }
+  }
+#pragma unroll
+  for (int ip = 0; ip < TP; ++ip) {
+    const int m = m0 + wp * WP + ip * 16 + (lane & 15);
+    const bool ok = m < M;
+    const unsigned yo = ok ? (unsigned)m * (unsigned)a.ldy * 2u + (unsigned)cb * 2u : 0x80000000u;
+    u32x2_t mk[TC];
+    if constexpr (EP == 2) {
+      const unsigned mo = ok ? (unsigned)m * (unsigned)a.ldm * 2u + (unsigned)cb * 2u : 0x80000000u;
+#pragma unroll
+      for (int ic = 0; ic < TC; ++ic) mk[ic] = __builtin_amdgcn_raw_buffer_load_b64(mr, mo + ic * 32, 0, 0);
+    }
+#pragma unroll
+    for (int ic = 0; ic < TC; ++ic) {
+      float v0 = acc[ic][ip][0] + bias[ic][0], v1 = acc[ic][ip][1] + bias[ic][1];
+      float v2 = acc[ic][ip][2] + bias[ic][2], v3 = acc[ic][ip][3] + bias[ic][3];
+      if (EP == 1 && relu) {
+        v0 = relu_f(v0); v1 = relu_f(v1); v2 = relu_f(v2); v3 = relu_f(v3);
+      }
+      if constexpr (EP == 2) {
+        if (cb + ic * 16 < a.mask_ch) {
+          v0 = lo_bf(mk[ic].x) > 0.f ? v0 : 0.f;
+          v1 = hi_bf(mk[ic].x) > 0.f ? v1 : 0.f;
+          v2 = lo_bf(mk[ic].y) > 0.f ? v2 : 0.f;
+          v3 = hi_bf(mk[ic].y) > 0.f ? v3 : 0.f;
+        }
+      }
+      __builtin_amdgcn_raw_buffer_store_b64(u32x2_t{pack_bf2(v0, v1), pack_bf2(v2, v3)}, yr, yo + ic * 32, 0, 0);
+    }
+  }
+}
+
+// epilogue kind for a launch: 1 / 2 when the specialised code covers it, else 0 (generic)
+static inline int glds_ep_kind(const IgemmArgs& a) {
+  if (a.mode != 0 || a.accumulate || a.y2 != nullptr || (a.ldy & 3)) return 0;
+  if (a.mask == nullptr) return ((a.Ngemm % 16) == 0 && (a.bias == nullptr || (((size_t)a.bias) & 15) == 0)) ? 1 : 0;
+  if (a.bias == nullptr && !a.relu && (a.ldm & 3) == 0) return 2;
+  return 0;
+}
+
 template <int BC, int BP, int WC, int WP, int ST, int BK, bool PRE = false>
 __global__ __launch_bounds__(512) void igemm_glds_kernel(IgemmArgs a) {
   constexpr int NWC = BC / WC, NWP = BP / WP;
@@ -799,7 +863,9 @@ __global__ __launch_bounds__(512) void igemm_pp_kernel(IgemmArgs a) {
 // flight (s+1, s+2) advance incrementally (no per-issue integer division), every phase of the steady
 // loop issues its half-tile and waits a constant vmcnt(8), and the last two K-tiles are a peeled tail
 // with compile-time waits.  Per phase: B fragments first, then A (as the 8-phase template orders them).
-template <int PROBE = 0>   // timing probes (A/B only): 1 = no epilogue, 2 = no MFMAs in the K loop
+template <int PROBE = 0,   // timing probes (A/B only): 1 = no epilogue, 2 = no MFMAs in the K loop,
+                           // 3 = no MFMAs and no DMA, 4 = no DMA (LDS reads of whatever is there)
+          int EP = 0>      // epilogue kind (glds_ep_kind)
 __global__ __launch_bounds__(512) void igemm_pp2_kernel(IgemmArgs a) {
   constexpr int BC = 256, BP = 256, WC = 128, WP = 64, TC = 8, TP = 4, RBY = 128;
   constexpr int STAGE = (BC + BP) * RBY;
@@ -867,12 +933,14 @@ __global__ __launch_bounds__(512) void igemm_pp2_kernel(IgemmArgs a) {
     return c;
   };
   auto issueA = [&](int h, int buf, KC c) {
+    if constexpr (PROBE >= 3) return;
     char* base = lds + buf * STAGE;
     const unsigned wk = (unsigned)((c.tap * a.Cs + c.ci) * 2);
 #pragma unroll
     for (int j = 0; j < 2; ++j) dma16(wrs, base + (j * 128 + h * 64 + wid * 8) * RBY, woff[h][j] + wk);
   };
   auto issueB = [&](int h, int buf, KC c) {
+    if constexpr (PROBE >= 3) return;
     char* base = lds + buf * STAGE + BC * RBY;
     const unsigned delta = (unsigned)(((c.kh * a.Ws + c.kw) * a.ldx + c.ci) * 2);
 #pragma unroll
@@ -924,7 +992,7 @@ __global__ __launch_bounds__(512) void igemm_pp2_kernel(IgemmArgs a) {
       }
   };
   auto mfma_quad = [&](int qa, int qb) {
-    if constexpr (PROBE == 2) {
+    if constexpr (PROBE == 2 || PROBE == 3) {
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
@@ -1052,7 +1120,8 @@ __global__ __launch_bounds__(512) void igemm_pp2_kernel(IgemmArgs a) {
       for (int ip = 0; ip < TP; ++ip) asm volatile("" ::"v"(acc[ic][ip]));
     return;
   }
-  glds_epilogue<TC, TP, WC, WP>(a, acc, M, m0, c0, wc, wp, lane);
+  if constexpr (EP != 0) glds_epilogue_fast<TC, TP, WC, WP, EP>(a, acc, M, m0, c0, wc, wp, lane);
+  else glds_epilogue<TC, TP, WC, WP>(a, acc, M, m0, c0, wc, wp, lane);
 }
 
 template <int BC, int BP, int WC, int WP, int ST, int BK = 64, bool PRE = false>
@@ -1078,7 +1147,8 @@ DPA_API int dpa_igemm_glds(const IgemmArgs* args, int cfg, hipStream_t st) {
   if (cfg & 32) a.korder |= 2;   // A/B: no persistent kernel in the auto choice
   const bool no_pre = cfg & 64;  // A/B: the compiler's read/MFMA interleave (cfg 12 / 13) for cfg 3 / 2
   const bool no_pp = cfg & 128;  // A/B: the 2-stage cfg 3 instead of the ping-pong cfg 14 in the auto choice
-  const int probe = (cfg >> 8) & 3;   // timing probes of cfg 14 (numerically wrong): 1 no epilogue, 2 no MFMAs
+  const int probe = (cfg >> 8) & 7;   // timing probes of cfg 14 (numerically wrong): see igemm_pp2_kernel
+  const bool no_fast_ep = cfg & 2048; // A/B: the generic epilogue in cfg 14
   cfg &= 15;
   if ((a.Cs & 63) || (a.Kpad & 63) || (a.ldx & 7) || (a.ldy & 3) || a.KH * a.KW > 32) return (int)hipErrorInvalidValue;
   if (a.mode == 1 && (a.Cout & 3)) return (int)hipErrorInvalidValue;
@@ -1122,8 +1192,13 @@ DPA_API int dpa_igemm_glds(const IgemmArgs* args, int cfg, hipStream_t st) {
     case 14: {
       if (a.Ngemm % 256 || a.Kpad < 128) break;     // the steady loop + peeled tail need S >= 2
       const int grid = ((a.N * a.Ho * a.Wo + 255) / 256) * (a.Ngemm / 256);
-      if (probe == 1) hipLaunchKernelGGL(igemm_pp2_kernel<1>, dim3(grid), dim3(512), 0, st, a);
+      const int ep = no_fast_ep ? 0 : glds_ep_kind(a);
+      if (probe == 0 && ep == 1) hipLaunchKernelGGL((igemm_pp2_kernel<0, 1>), dim3(grid), dim3(512), 0, st, a);
+      else if (probe == 0 && ep == 2) hipLaunchKernelGGL((igemm_pp2_kernel<0, 2>), dim3(grid), dim3(512), 0, st, a);
+      else if (probe == 1) hipLaunchKernelGGL(igemm_pp2_kernel<1>, dim3(grid), dim3(512), 0, st, a);
       else if (probe == 2) hipLaunchKernelGGL(igemm_pp2_kernel<2>, dim3(grid), dim3(512), 0, st, a);
+      else if (probe == 3) hipLaunchKernelGGL(igemm_pp2_kernel<3>, dim3(grid), dim3(512), 0, st, a);
+      else if (probe == 4) hipLaunchKernelGGL(igemm_pp2_kernel<4>, dim3(grid), dim3(512), 0, st, a);
       else hipLaunchKernelGGL(igemm_pp2_kernel<0>, dim3(grid), dim3(512), 0, st, a);
       return (int)hipGetLastError();
     }

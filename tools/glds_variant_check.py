@@ -45,6 +45,9 @@ def main():
                 continue
             Kp = 9 * Cs
             w = (torch.randn(N, Kp, device=dev) * (1.0 / Kp ** 0.5)).to(torch.bfloat16)
+            # the production epilogues: bias + ReLU (forward), ReLU-backward mask (dgrad)
+            extra = (dict(bias=torch.randn(N, device=dev) * 0.1, relu=True) if kind == "fwd" else
+                     dict(mask=torch.randn(B, H, H, N, device=dev).to(torch.bfloat16)))
             outs = {}
             fns = {}
             for v in [a.base] + a.new:
@@ -52,7 +55,7 @@ def main():
                     continue
                 y = torch.empty(B, H, H, N, device=dev, dtype=torch.bfloat16)
                 fn = (lambda y=y, v=v: K.igemm(src, w, y, Ngemm=N, Kpad=Kp, KH=3, KW=3, stride=1, pad=1, Cs=Cs,
-                                             out_grid=(B, H, H), path="glds" if v else "auto", variant=v))
+                                             out_grid=(B, H, H), path="glds" if v else "auto", variant=v, **extra))
                 fn()
                 torch.cuda.synchronize()
                 outs[v], fns[v] = y, fn
