@@ -115,16 +115,17 @@ __device__ __forceinline__ void glds_epilogue(const IgemmArgs& a, f32x4_t (&acc)
 }
 
 // Specialised epilogues (EP 1: plain conv forward -- optional bias, optional ReLU; EP 2: dgrad with the
-// ReLU-backward mask only): straight-line code with the row offsets computed once per pixel fragment.
+// ReLU-backward mask only; EP 3: dgrad split into the two dense halves of a concat gradient): straight-line code with the row offsets computed once per pixel fragment.
 // The generic epilogue carries every mode (scatter, split, accumulate, mask) behind runtime branches:
 // ~5000 instructions that cost 10-20 % of a deep layer's time (profiles/experiments_r03_late.txt).
 // Out-of-range pixels store to an offset past the buffer's range check (dropped) instead of branching.
 template <int TC, int TP, int WC, int WP, int EP>
 __device__ __forceinline__ void glds_epilogue_fast(const IgemmArgs& a, f32x4_t (&acc)[TC][TP], int M, int m0, int c0,
                                                    int wc, int wp, int lane) {
-  static_assert(EP == 1 || EP == 2, "fast epilogue kinds");
+  static_assert(EP == 1 || EP == 2 || EP == 3, "fast epilogue kinds");
   const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc((void*)a.y, 0, 0x7fffffff, 0x00020000);
   const __amdgpu_buffer_rsrc_t mr = __builtin_amdgcn_make_buffer_rsrc((void*)(EP == 2 ? a.mask : a.y), 0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t y2r = __builtin_amdgcn_make_buffer_rsrc((void*)(EP == 3 ? a.y2 : a.y), 0, 0x7fffffff, 0x00020000);
   const int cb = c0 + wc * WC + 4 * (lane >> 4);
   float bias[TC][4];
   const bool relu = a.relu != 0;
@@ -134,16 +135,16 @@ __device__ __forceinline__ void glds_epilogue_fast(const IgemmArgs& a, f32x4_t (
     for (int e = 0; e < 4; ++e) bias[ic][e] = 0.f;
   if (EP == 1 && a.bias) {
 #pragma unroll
-    for (int ic = 0; ic < TC; ++ic) {
-      const float4 b = *reinterpret_cast<const float4*>(a.bias + cb + ic * 16);
-      bias[ic][0] = b.x; bias[ic][1] = b.y; bias[ic][2] = b.z; bias[ic][3] = b.w;
-    }
+    for (int ic = 0; ic < TC; ++ic)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) bias[ic][e] = a.bias[cb + ic * 16 + e];   // (flat parameter views: 4-B aligned)
   }
 #pragma unroll
   for (int ip = 0; ip < TP; ++ip) {
     const int m = m0 + wp * WP + ip * 16 + (lane & 15);
     const bool ok = m < M;
     const unsigned yo = ok ? (unsigned)m * (unsigned)a.ldy * 2u + (unsigned)cb * 2u : 0x80000000u;
+    const unsigned yo2 = EP == 3 ? (unsigned)m * (unsigned)a.ldy2 * 2u : 0u;
     u32x2_t mk[TC];
     if constexpr (EP == 2) {
       const unsigned mo = ok ? (unsigned)m * (unsigned)a.ldm * 2u + (unsigned)cb * 2u : 0x80000000u;
@@ -165,15 +166,27 @@ __device__ __forceinline__ void glds_epilogue_fast(const IgemmArgs& a, f32x4_t (
           v3 = hi_bf(mk[ic].y) > 0.f ? v3 : 0.f;
         }
       }
-      __builtin_amdgcn_raw_buffer_store_b64(u32x2_t{pack_bf2(v0, v1), pack_bf2(v2, v3)}, yr, yo + ic * 32, 0, 0);
+      const u32x2_t pk = u32x2_t{pack_bf2(v0, v1), pack_bf2(v2, v3)};
+      if constexpr (EP == 3) {
+        // split output: a 16-channel group lies wholly below or above `split` (split % 16 == 0), so the
+        // target tensor is wave-uniform per group
+        if (c0 + wc * WC + ic * 16 < a.split)
+          __builtin_amdgcn_raw_buffer_store_b64(pk, yr, yo + ic * 32, 0, 0);
+        else
+          __builtin_amdgcn_raw_buffer_store_b64(pk, y2r, ok ? yo2 + (unsigned)(cb + ic * 16 - a.split) * 2u : 0x80000000u, 0, 0);
+      } else {
+        __builtin_amdgcn_raw_buffer_store_b64(pk, yr, yo + ic * 32, 0, 0);
+      }
     }
   }
 }
 
 // epilogue kind for a launch: 1 / 2 when the specialised code covers it, else 0 (generic)
 static inline int glds_ep_kind(const IgemmArgs& a) {
-  if (a.mode != 0 || a.accumulate || a.y2 != nullptr || (a.ldy & 3)) return 0;
-  if (a.mask == nullptr) return ((a.Ngemm % 16) == 0 && (a.bias == nullptr || (((size_t)a.bias) & 15) == 0)) ? 1 : 0;
+  if (a.mode != 0 || a.accumulate || (a.ldy & 3)) return 0;
+  if (a.y2 != nullptr)     // split dgrad (the two halves of a concat gradient)
+    return (a.mask == nullptr && a.bias == nullptr && !a.relu && (a.split % 16) == 0 && (a.ldy2 & 3) == 0) ? 3 : 0;
+  if (a.mask == nullptr) return (a.Ngemm % 16) == 0 ? 1 : 0;
   if (a.bias == nullptr && !a.relu && (a.ldm & 3) == 0) return 2;
   return 0;
 }
@@ -1195,6 +1208,7 @@ DPA_API int dpa_igemm_glds(const IgemmArgs* args, int cfg, hipStream_t st) {
       const int ep = no_fast_ep ? 0 : glds_ep_kind(a);
       if (probe == 0 && ep == 1) hipLaunchKernelGGL((igemm_pp2_kernel<0, 1>), dim3(grid), dim3(512), 0, st, a);
       else if (probe == 0 && ep == 2) hipLaunchKernelGGL((igemm_pp2_kernel<0, 2>), dim3(grid), dim3(512), 0, st, a);
+      else if (probe == 0 && ep == 3) hipLaunchKernelGGL((igemm_pp2_kernel<0, 3>), dim3(grid), dim3(512), 0, st, a);
       else if (probe == 1) hipLaunchKernelGGL(igemm_pp2_kernel<1>, dim3(grid), dim3(512), 0, st, a);
       else if (probe == 2) hipLaunchKernelGGL(igemm_pp2_kernel<2>, dim3(grid), dim3(512), 0, st, a);
       else if (probe == 3) hipLaunchKernelGGL(igemm_pp2_kernel<3>, dim3(grid), dim3(512), 0, st, a);

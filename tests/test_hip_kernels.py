@@ -469,7 +469,10 @@ def test_stream_pool_codes_match_maxpool(hip_lib):
 
 @pytest.mark.parametrize("N,H,W,Cin,Cout,path", [(2, 3, 256, 64, 32, "stream"), (1, 4, 128, 128, 64, "halo"),
                                                  (2, 9, 13, 256, 128, "glds"), (2, 9, 13, 128, 64, "generic"),
-                                                 (2, 3, 96, 64, 32, "stream"), (1, 4, 240, 128, 64, "halo")])
+                                                 (2, 3, 96, 64, 32, "stream"), (1, 4, 240, 128, 64, "halo"),
+                                                 # >= 512 tiles of 256 x 256: the ping-pong kernel's split epilogue,
+                                                 # with a partial last pixel tile
+                                                 (10, 115, 117, 256, 128, "glds")])
 def test_dgrad_split_output(hip_lib, N, H, W, Cin, Cout, path):
     """Split output (concat gradient as two dense tensors) == the interleaved output's halves."""
     from distributedpytorch_amd.ops import kernels as K
@@ -646,3 +649,26 @@ def test_wgrad_multi_microbatches(hip_lib, M, Nc, H, W, mb, nmb):
     torch.cuda.synchronize()
     assert _rel(gw.cpu().view(M, Nc, 3, 3), wr.grad) < 1e-2
     assert _rel(gb.cpu(), br.grad) < 1e-2
+
+
+@pytest.mark.parametrize("N,H,W,Cs,Ng,kind", [(9, 64, 64, 256, 256, "fwd"), (5, 61, 67, 128, 512, "fwd"),
+                                               (9, 64, 64, 256, 256, "dgrad"), (5, 61, 67, 512, 256, "dgrad")])
+def test_glds_pingpong_epilogues(hip_lib, N, H, W, Cs, Ng, kind):
+    """The ping-pong deep GEMM (cfg 14) with its specialised epilogues (forward bias + ReLU, dgrad ReLU
+    mask; partial last pixel tile) == the 2-stage kernel (cfg 3) bitwise: both accumulate K in the
+    same order."""
+    from distributedpytorch_amd.ops import kernels as K
+    torch.manual_seed(23)
+    x = torch.randn(N, H, W, Cs, device="cuda").to(torch.bfloat16)
+    Kp = 9 * Cs
+    w = (torch.randn(Ng, Kp, device="cuda") / Kp ** 0.5).to(torch.bfloat16)
+    extra = (dict(bias=torch.randn(Ng, device="cuda") * 0.1, relu=True) if kind == "fwd" else
+             dict(mask=torch.randn(N, H, W, Ng, device="cuda").to(torch.bfloat16)))
+    outs = []
+    for v in (3, 14):
+        y = torch.empty(N, H, W, Ng, device="cuda", dtype=torch.bfloat16)
+        K.igemm(x, w, y, Ngemm=Ng, Kpad=Kp, KH=3, KW=3, stride=1, pad=1, Cs=Cs, out_grid=(N, H, W), path="glds",
+                variant=v, **extra)
+        outs.append(y)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
