@@ -2,7 +2,7 @@
 # Same-box interleaved A/B of launch-geometry knobs (env settings in KNOBS, ';'-separated).
 set -o pipefail
 cd "$(dirname "$0")/.." && export TMPDIR=/tmp && mkdir -p gpurun_out
-python -c "import __graft_entry__ as g; g.build()" > gpurun_out/build.log 2>&1 || exit 1
+[ -n "$KNOB_BUILD" ] && { python -c "import __graft_entry__ as g; g.build()" > gpurun_out/build.log 2>&1 || exit 1; }
 IFS=';' read -ra ARR <<< "${KNOBS:-X=0}"
 for i in 1 2; do for j in "${!ARR[@]}"; do
   E="${ARR[$j]}"
