@@ -19,6 +19,8 @@
 
 #include "conv_args.h"
 
+#include <type_traits>
+
 
 // Logical tile id -> (pixel tile, channel tile).  Consecutive ids run on one XCD (xcd_remap), so
 // ~32 consecutive ids share an L2: with many channel tiles, group them as 8 pixel tiles x (ids / 8)
@@ -1137,6 +1139,308 @@ __global__ __launch_bounds__(512) void igemm_pp2_kernel(IgemmArgs a) {
   else glds_epilogue<TC, TP, WC, WP>(a, acc, M, m0, c0, wc, wp, lane);
 }
 
+// ------------------------------------------------------------------------------------------------
+// Row-block ping-pong (cfg 14 with row-block pixel staging, 3x3 s1 p1 convs whose 256-pixel tiles are
+// whole image rows: W in {32, 64, 128, 256}).  cfg 14 stages the pixel operand per K-tile = per (tap,
+// 64-channel slice): the three kw taps of a kernel row fetch three 1-pixel-shifted copies of the same
+// rows (32 KB each).  Here the pixel half-tiles of a kernel row kh are fetched ONCE as blocks of four
+// 34-pixel row segments (the 32 pixels of a wave's quadrant + the kw halo; 17 KB) and the kw = 0,1,2
+// K-tiles read them at a 0/1/2-row offset: per kernel row 96 KB of weights + 34 KB of pixels instead
+// of 96 + 96 KB.  The K order (slice-major, taps kh-major) and hence every accumulation is the same as
+// cfg 14's: bitwise-equal output.  Weight half-tiles keep cfg 14's schedule (p1 -> A1(s+1), p2 ->
+// A0(s+2)); the pixel blocks of kernel-row group g+1 are issued during the first two K-tiles of group g
+// (p3 of t = 0 -> B0, p0 of t = 1 -> B1) into the other of two group buffers.  The K loop runs one
+// kernel-row group (three K-tiles) per iteration with every position's wait a constant: the number of
+// DMA instructions this wave issued after the unit it needs (wave 0 issues the 17th instruction of
+// each pixel block, so its counts are one higher per block).
+template <int EP>
+__global__ __launch_bounds__(512) void igemm_pp2h_kernel(IgemmArgs a) {
+  constexpr int BC = 256, BP = 256, WC = 128, WP = 64, TC = 8, TP = 4, RBY = 128;
+  constexpr int ASTAGE = BC * RBY;             // weight K-tile image (32 KB)
+  constexpr int SEG = 34;                      // pixel rows per quadrant segment (32 + kw halo)
+  constexpr int BHALF = 4 * SEG * RBY;         // one pixel half-block (17 KB, 17 DMA instructions)
+  __shared__ __attribute__((aligned(16))) char lds[2 * ASTAGE + 4 * BHALF];
+  char* const Bimg = lds + 2 * ASTAGE;
+
+  const int M = a.N * a.Ho * a.Wo;
+  const int W = a.Wo, H = a.Ho, HW = H * W;
+  const int nct = a.Ngemm / BC;
+  const int npt = M / BP;
+  const int bid = xcd_remap(blockIdx.x, npt * nct);
+  int pt, ct;
+  glds_tile(bid, npt, nct, pt, ct);
+  const int m0 = pt * BP, c0 = ct * BC;
+  const int img = m0 / HW, tr0 = (m0 - img * HW) / W;        // tile = image rows tr0 .. tr0 + 256/W - 1
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wc = wid & 1, wp = wid >> 1, grp = wid >> 2;
+  const int lr = lane >> 3;
+  const int lchunk = (lane & 7) ^ lr;
+  unsigned woff[2][2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      woff[h][j] = (unsigned)(((c0 + j * 128 + h * 64 + wid * 8 + lr) * a.Kpad) * 2 + lchunk * 16);
+  // pixel block DMA: instruction i of a half-block fills LDS rows 8i .. 8i+7; wave w issues i = w, 8 + w
+  // and wave 0 also i = 16.  LDS row q -> quadrant segment q / 34, pixel (q % 34) - 1 of the segment's
+  // 32 columns; for kernel row kh the image row is the segment's row + kh - 1.
+  const int NI = wid == 0 ? 3 : 2;
+  int bbase[2][3];                             // byte offset of the (kh = 0) source pixel, per half / instruction
+  unsigned bvalid[2][3];                       // bit kh: source row of kernel row kh inside the image
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const int i = j < 2 ? j * 8 + wid : 16;
+      const int q = 8 * i + lr;
+      const int sg = q / SEG, loc = q - sg * SEG;
+      const int pq = sg * 64 + h * 32;                        // first pixel of the quadrant segment
+      const int r = tr0 + pq / W, col = pq % W + loc - 1;
+      const bool cok = col >= 0 && col < W && (j < 2 || wid == 0);
+      unsigned vb = 0;
+#pragma unroll
+      for (int kh = 0; kh < 3; ++kh) {
+        const int ih = r + kh - 1;
+        if (cok && ih >= 0 && ih < H) vb |= 1u << kh;
+      }
+      bvalid[h][j] = vb;
+      bbase[h][j] = (((img * a.Hs + r - 1) * a.Ws + col) * a.ldx) * 2 + lchunk * 16;
+    }
+  const int rowB = W * a.ldx * 2;              // bytes per image row
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, 0, (int)a.xbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc((void*)a.w, 0, 0x7fffffff, 0x00020000);
+  const int S = a.Kpad / 64;                   // 9 K-tiles per 64-channel slice; host: S >= 9
+  const int G = S / 3;                         // kernel-row groups
+
+  // K-tile coordinates (tap, 64-channel slice), advanced one K-tile at a time (no division)
+  struct KC { int tap, ci; };
+  auto knext = [&](KC c) {
+    if (++c.tap == 9) { c.tap = 0; c.ci += 64; }
+    return c;
+  };
+  auto issueA = [&](int h, int buf, KC c) {
+    const unsigned wk = (unsigned)((c.tap * a.Cs + c.ci) * 2);
+    char* base = lds + buf * ASTAGE;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) dma16(wrs, base + (j * 128 + h * 64 + wid * 8) * RBY, woff[h][j] + wk);
+  };
+  // pixel half-block h of kernel row kh, slice ci, into group buffer gb (2 instructions; wave 0: 3)
+  auto issueB = [&](int h, int gb, int kh, int ci) {
+    char* base = Bimg + (gb * 2 + h) * BHALF;
+    const int add = kh * rowB + ci * 2;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const bool ok = (bvalid[h][j] >> kh) & 1u;
+      dma16(xr, base + (j * 8 + wid) * 1024, ok ? (unsigned)(bbase[h][j] + add) : 0x80000000u);
+    }
+    if (wid == 0) {
+      const bool ok = (bvalid[h][2] >> kh) & 1u;
+      dma16(xr, base + 16 * 1024, ok ? (unsigned)(bbase[h][2] + add) : 0x80000000u);
+    }
+  };
+  // the waits count the DMA instructions this wave issued after the staged unit it needs; a pixel
+  // block is 3 instructions in wave 0 and 2 in the others (static per position in the group)
+  const bool w0 = wid == 0;
+
+  f32x4_t acc[TC][TP];
+#pragma unroll
+  for (int ic = 0; ic < TC; ++ic)
+#pragma unroll
+    for (int ip = 0; ip < TP; ++ip) acc[ic][ip] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  // prologue: weights of K-tiles 0 (both halves) and 1 (half 0), pixel blocks of group 0
+  const KC k0{0, 0};
+  KC kA1 = knext(k0);                          // K-tile s+1 (A1 issue at p1 of s)
+  issueA(0, 0, k0);
+  issueB(0, 0, 0, 0);
+  issueB(1, 0, 0, 0);
+  issueA(1, 0, k0);
+  issueA(0, 1, kA1);
+  KC kA0 = knext(kA1);                         // K-tile s+2 (A0 issue at p2 of s)
+  if (w0) wait_vm<7>(); else wait_vm<6>();     // A0(0), B0(0): newer are B1(0), A1(0), A0(1)
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  if (grp) __builtin_amdgcn_s_barrier();       // the second half runs one barrier behind
+  __builtin_amdgcn_sched_barrier(0);
+
+  bf16x8_t af[4][2], bfr[2][2][2];
+  auto readA = [&](const char* Wt, int h) {
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int ic = 0; ic < 4; ++ic) {
+        const int row = wc * WC + h * 64 + ic * 16 + (lane & 15);
+        const int chunk = kk * 4 + (lane >> 4);
+        af[ic][kk] = *reinterpret_cast<const bf16x8_t*>(Wt + row * RBY + ((chunk ^ (row & 7)) << 4));
+      }
+  };
+  // B quadrant h of group buffer gb at kw: segment rows wp*34 + ip*16 + (lane & 15) + kw
+  auto readB = [&](int gb, int h, int kw) {
+    const char* P = Bimg + (gb * 2 + h) * BHALF;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int ip = 0; ip < 2; ++ip) {
+        const int row = wp * SEG + ip * 16 + (lane & 15) + kw;
+        const int chunk = kk * 4 + (lane >> 4);
+        bfr[h][ip][kk] = *reinterpret_cast<const bf16x8_t*>(P + row * RBY + ((chunk ^ (row & 7)) << 4));
+      }
+  };
+  auto mfma_quad = [&](int qa, int qb) {
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int ic = 0; ic < 4; ++ic)
+#pragma unroll
+        for (int ip = 0; ip < 2; ++ip)
+          acc[qa * 4 + ic][qb * 2 + ip] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ic][kk], bfr[qb][ip][kk], acc[qa * 4 + ic][qb * 2 + ip], 0, 0, 0);
+  };
+  auto sync_in = [&]() {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+  };
+  auto sync_out = [&]() {
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  // one kernel-row group (3 K-tiles, kw = 0, 1, 2) of group buffer gb; LAST: no next group, and the
+  // K-tiles beyond S are not issued.  kh2/ci2 = kernel row / slice of the next group.
+  auto group = [&](auto LASTc, int gb, int bA, int kh2, int ci2) {
+    constexpr bool LAST = decltype(LASTc)::value;
+    // ---- t = 0 (weights buffer bA)
+    {
+      const char* Wt = lds + bA * ASTAGE;
+      readB(gb, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      readA(Wt, 0);
+      wait_vm<4>();                            // B1 of this group (conservative: newer >= 4)
+      sync_in();
+      mfma_quad(0, 0);
+      sync_out();
+      readB(gb, 1, 0);
+      issueA(1, bA ^ 1, kA1);
+      wait_vm<4>();                            // A1 of this K-tile
+      sync_in();
+      mfma_quad(0, 1);
+      sync_out();
+      readA(Wt, 1);
+      issueA(0, bA, kA0);
+      sync_in();
+      mfma_quad(1, 1);
+      sync_out();
+      if constexpr (!LAST) {
+        issueB(0, gb ^ 1, kh2, ci2);
+        if (w0) wait_vm<7>(); else wait_vm<6>();   // A0 of K-tile t = 1
+      } else {
+        wait_vm<4>();
+      }
+      sync_in();
+      mfma_quad(1, 0);
+      sync_out();
+      kA1 = kA0;
+      kA0 = knext(kA0);
+    }
+    // ---- t = 1 (weights buffer bA ^ 1)
+    {
+      const char* Wt = lds + (bA ^ 1) * ASTAGE;
+      readB(gb, 0, 1);
+      __builtin_amdgcn_sched_barrier(0);
+      readA(Wt, 0);
+      if constexpr (!LAST) issueB(1, gb ^ 1, kh2, ci2);
+      sync_in();
+      mfma_quad(0, 0);
+      sync_out();
+      readB(gb, 1, 1);
+      issueA(1, bA, kA1);
+      if constexpr (!LAST) {
+        if (w0) wait_vm<10>(); else wait_vm<8>();  // A1 of this K-tile
+      } else {
+        wait_vm<4>();
+      }
+      sync_in();
+      mfma_quad(0, 1);
+      sync_out();
+      readA(Wt, 1);
+      if constexpr (!LAST) issueA(0, bA ^ 1, kA0);
+      sync_in();
+      mfma_quad(1, 1);
+      sync_out();
+      if constexpr (!LAST) {
+        if (w0) wait_vm<10>(); else wait_vm<8>();  // A0 of K-tile t = 2
+      } else {
+        wait_vm<2>();
+      }
+      sync_in();
+      mfma_quad(1, 0);
+      sync_out();
+      kA1 = kA0;
+      kA0 = knext(kA0);
+    }
+    // ---- t = 2 (weights buffer bA)
+    {
+      const char* Wt = lds + bA * ASTAGE;
+      readB(gb, 0, 2);
+      __builtin_amdgcn_sched_barrier(0);
+      readA(Wt, 0);
+      sync_in();
+      mfma_quad(0, 0);
+      sync_out();
+      readB(gb, 1, 2);
+      if constexpr (!LAST) {
+        issueA(1, bA ^ 1, kA1);
+        wait_vm<4>();                          // A1 of this K-tile
+      } else {
+        wait_vm<0>();
+      }
+      sync_in();
+      mfma_quad(0, 1);
+      sync_out();
+      readA(Wt, 1);
+      if constexpr (!LAST) issueA(0, bA, kA0);
+      sync_in();
+      mfma_quad(1, 1);
+      sync_out();
+      if constexpr (!LAST) wait_vm<4>();       // A0 of the next group's first K-tile (+ its B0, older)
+      sync_in();
+      mfma_quad(1, 0);
+      sync_out();
+      kA1 = kA0;
+      kA0 = knext(kA0);
+    }
+  };
+
+  // K-tile s = 3 g + t uses weights buffer s & 1: (g & 1, !(g & 1), g & 1) within group g
+  int kh = 0, ci = 0;
+#pragma unroll 1
+  for (int g = 0; g < G - 1; ++g) {
+    int kh2 = kh + 1, ci2 = ci;
+    if (kh2 == 3) { kh2 = 0; ci2 += 64; }
+    group(std::integral_constant<bool, false>{}, g & 1, g & 1, kh2, ci2);
+    kh = kh2;
+    ci = ci2;
+  }
+  group(std::integral_constant<bool, true>{}, (G - 1) & 1, (G - 1) & 1, 0, 0);
+  if (!grp) __builtin_amdgcn_s_barrier();      // balance the second half's extra barrier
+
+  if constexpr (EP != 0) glds_epilogue_fast<TC, TP, WC, WP, EP>(a, acc, M, m0, c0, wc, wp, lane);
+  else glds_epilogue<TC, TP, WC, WP>(a, acc, M, m0, c0, wc, wp, lane);
+}
+
+// row-block staging eligible: conv3x3 s1 p1, slice-major K (Kpad == 9 Cs, Cs % 64 == 0), tiles = whole rows
+static inline bool pp2h_ok(const IgemmArgs& a) {
+  const int W = a.Wo;
+  return a.mode == 0 && a.KH == 3 && a.KW == 3 && a.stride == 1 && a.pad == 1 && a.Hs == a.Ho && a.Ws == a.Wo &&
+         !(a.korder & 1) && a.Kpad == 9 * a.Cs && (a.Cs % 64) == 0 && (W == 32 || W == 64 || W == 128 || W == 256) &&
+         ((long)a.Ho * W) % 256 == 0 && a.Ngemm % 256 == 0;
+}
+
 template <int BC, int BP, int WC, int WP, int ST, int BK = 64, bool PRE = false>
 static int launch_glds(const IgemmArgs& a, hipStream_t st) {
   const int M = a.N * a.Ho * a.Wo;
@@ -1162,6 +1466,7 @@ DPA_API int dpa_igemm_glds(const IgemmArgs* args, int cfg, hipStream_t st) {
   const bool no_pp = cfg & 128;  // A/B: the 2-stage cfg 3 instead of the ping-pong cfg 14 in the auto choice
   const int probe = (cfg >> 8) & 7;   // timing probes of cfg 14 (numerically wrong): see igemm_pp2_kernel
   const bool no_fast_ep = cfg & 2048; // A/B: the generic epilogue in cfg 14
+  const bool no_rowblock = cfg & 8192;  // A/B: cfg 14 with per-K-tile pixel staging (no row blocks)
   cfg &= 15;
   if ((a.Cs & 63) || (a.Kpad & 63) || (a.ldx & 7) || (a.ldy & 3) || a.KH * a.KW > 32) return (int)hipErrorInvalidValue;
   if (a.mode == 1 && (a.Cout & 3)) return (int)hipErrorInvalidValue;
@@ -1206,6 +1511,13 @@ DPA_API int dpa_igemm_glds(const IgemmArgs* args, int cfg, hipStream_t st) {
       if (a.Ngemm % 256 || a.Kpad < 128) break;     // the steady loop + peeled tail need S >= 2
       const int grid = ((a.N * a.Ho * a.Wo + 255) / 256) * (a.Ngemm / 256);
       const int ep = no_fast_ep ? 0 : glds_ep_kind(a);
+      if (probe == 0 && !no_rowblock && pp2h_ok(a)) {
+        if (ep == 1) hipLaunchKernelGGL((igemm_pp2h_kernel<1>), dim3(grid), dim3(512), 0, st, a);
+        else if (ep == 2) hipLaunchKernelGGL((igemm_pp2h_kernel<2>), dim3(grid), dim3(512), 0, st, a);
+        else if (ep == 3) hipLaunchKernelGGL((igemm_pp2h_kernel<3>), dim3(grid), dim3(512), 0, st, a);
+        else hipLaunchKernelGGL((igemm_pp2h_kernel<0>), dim3(grid), dim3(512), 0, st, a);
+        return (int)hipGetLastError();
+      }
       if (probe == 0 && ep == 1) hipLaunchKernelGGL((igemm_pp2_kernel<0, 1>), dim3(grid), dim3(512), 0, st, a);
       else if (probe == 0 && ep == 2) hipLaunchKernelGGL((igemm_pp2_kernel<0, 2>), dim3(grid), dim3(512), 0, st, a);
       else if (probe == 0 && ep == 3) hipLaunchKernelGGL((igemm_pp2_kernel<0, 3>), dim3(grid), dim3(512), 0, st, a);

@@ -102,6 +102,8 @@ GLDS_NO_PERS = os.environ.get("DPA_GLDS_NO_PERS", "0") == "1"
 GLDS_NO_PRELOAD = os.environ.get("DPA_GLDS_NO_PRELOAD", "0") == "1"
 # A/B: the 2-stage 256x256 LDS-DMA kernel instead of the ping-pong steady-state one (csrc/igemm_glds.hip cfg 14)
 GLDS_NO_PP = os.environ.get("DPA_GLDS_NO_PP", "0") == "1"
+# A/B: the ping-pong kernel without row-block pixel staging (csrc/igemm_glds.hip igemm_pp2h_kernel)
+GLDS_NO_ROWBLOCK = os.environ.get("DPA_GLDS_NO_ROWBLOCK", "0") == "1"
 # conv weight gradients on a side HIP stream, overlapping each block's dgrad chain (models/hip_unet.py)
 SIDE_WGRAD = os.environ.get("DPA_NO_SIDE_WGRAD", "0") != "1"
 # HIP stream priority of the weight-gradient side stream (torch convention: lower = higher priority,
@@ -291,7 +293,7 @@ def igemm(x: torch.Tensor, wpacked: torch.Tensor, y: torch.Tensor, *, Ngemm: int
         a = args(n0, n1, False)
         if path == "glds" or (path == "auto" and glds_ok):
             no_pers = GLDS_NO_PERS or not persistent
-            err = L.dpa_igemm_glds(ctypes.byref(a), c_int(variant if path == "glds" else 16 * GLDS_TAP_MAJOR + 32 * no_pers + 64 * GLDS_NO_PRELOAD + 128 * GLDS_NO_PP), st)
+            err = L.dpa_igemm_glds(ctypes.byref(a), c_int(variant if path == "glds" else 16 * GLDS_TAP_MAJOR + 32 * no_pers + 64 * GLDS_NO_PRELOAD + 128 * GLDS_NO_PP + 8192 * GLDS_NO_ROWBLOCK), st)
             if err == 0:
                 continue
             if path == "glds":

@@ -652,11 +652,14 @@ def test_wgrad_multi_microbatches(hip_lib, M, Nc, H, W, mb, nmb):
 
 
 @pytest.mark.parametrize("N,H,W,Cs,Ng,kind", [(9, 64, 64, 256, 256, "fwd"), (5, 61, 67, 128, 512, "fwd"),
-                                               (9, 64, 64, 256, 256, "dgrad"), (5, 61, 67, 512, 256, "dgrad")])
+                                               (9, 64, 64, 256, 256, "dgrad"), (5, 61, 67, 512, 256, "dgrad"),
+                                               # row-block tiles of 8 / 2 / 1 image rows (W = 32 / 128 / 256)
+                                               (16, 32, 32, 128, 256, "fwd"), (3, 30, 128, 64, 256, "dgrad"),
+                                               (2, 70, 256, 64, 256, "fwd")])
 def test_glds_pingpong_epilogues(hip_lib, N, H, W, Cs, Ng, kind):
-    """The ping-pong deep GEMM (cfg 14) with its specialised epilogues (forward bias + ReLU, dgrad ReLU
-    mask; partial last pixel tile) == the 2-stage kernel (cfg 3) bitwise: both accumulate K in the
-    same order."""
+    """The ping-pong deep GEMM (cfg 14; on whole-row tiles its row-block pixel staging form, 8206 = cfg 14
+    without row blocks) with its specialised epilogues (forward bias + ReLU, dgrad ReLU mask; partial
+    last pixel tile) == the 2-stage kernel (cfg 3) bitwise: all accumulate K in the same order."""
     from distributedpytorch_amd.ops import kernels as K
     torch.manual_seed(23)
     x = torch.randn(N, H, W, Cs, device="cuda").to(torch.bfloat16)
@@ -665,10 +668,10 @@ def test_glds_pingpong_epilogues(hip_lib, N, H, W, Cs, Ng, kind):
     extra = (dict(bias=torch.randn(Ng, device="cuda") * 0.1, relu=True) if kind == "fwd" else
              dict(mask=torch.randn(N, H, W, Ng, device="cuda").to(torch.bfloat16)))
     outs = []
-    for v in (3, 14):
+    for v in (3, 14, 8206):
         y = torch.empty(N, H, W, Ng, device="cuda", dtype=torch.bfloat16)
         K.igemm(x, w, y, Ngemm=Ng, Kpad=Kp, KH=3, KW=3, stride=1, pad=1, Cs=Cs, out_grid=(N, H, W), path="glds",
                 variant=v, **extra)
         outs.append(y)
     torch.cuda.synchronize()
-    assert torch.equal(outs[0], outs[1])
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
