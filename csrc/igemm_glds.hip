@@ -1153,10 +1153,17 @@ __global__ __launch_bounds__(512) void igemm_pp2_kernel(IgemmArgs a) {
 // kernel-row group (three K-tiles) per iteration with every position's wait a constant: the number of
 // DMA instructions this wave issued after the unit it needs (wave 0 issues the 17th instruction of
 // each pixel block, so its counts are one higher per block).
-template <int EP>
+// BC = 128 (the 128-output-channel convs / dgrads of the 128^2 level): the same schedule with 64 channels
+// per wave (2 x 32-row quadrant halves, 8 MFMAs per quadrant, one weight DMA instruction per half-tile);
+// 100 KB of LDS instead of 132.
+template <int EP, int BC = 256>
 __global__ __launch_bounds__(512) void igemm_pp2h_kernel(IgemmArgs a) {
-  constexpr int BC = 256, BP = 256, WC = 128, WP = 64, TC = 8, TP = 4, RBY = 128;
-  constexpr int ASTAGE = BC * RBY;             // weight K-tile image (32 KB)
+  static_assert(BC == 256 || BC == 128, "channel tile");
+  constexpr int BP = 256, WC = BC / 2, WP = 64, TC = WC / 16, TP = 4, RBY = 128;
+  constexpr int QA = WC / 2;                   // weight rows per wave and quadrant half
+  constexpr int NIC = QA / 16;                 // weight fragments per quadrant half
+  constexpr int AI = BC / 128;                 // weight DMA instructions per half-tile per wave
+  constexpr int ASTAGE = BC * RBY;             // weight K-tile image (32 / 16 KB)
   constexpr int SEG = 34;                      // pixel rows per quadrant segment (32 + kw halo)
   constexpr int BHALF = 4 * SEG * RBY;         // one pixel half-block (17 KB, 17 DMA instructions)
   __shared__ __attribute__((aligned(16))) char lds[2 * ASTAGE + 4 * BHALF];
@@ -1176,12 +1183,19 @@ __global__ __launch_bounds__(512) void igemm_pp2h_kernel(IgemmArgs a) {
   const int wc = wid & 1, wp = wid >> 1, grp = wid >> 2;
   const int lr = lane >> 3;
   const int lchunk = (lane & 7) ^ lr;
-  unsigned woff[2][2];
+  // weight half-tile h = rows {w*WC + h*QA + [0, QA) : w = 0, 1}; instruction i = j*8 + wid of it covers
+  // its rows 8i .. 8i+7 (channel wave (8i) / QA, row (8i) % QA of that wave's half)
+  unsigned woff[2][AI];
+  int wdst[2][AI];
 #pragma unroll
   for (int h = 0; h < 2; ++h)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
-      woff[h][j] = (unsigned)(((c0 + j * 128 + h * 64 + wid * 8 + lr) * a.Kpad) * 2 + lchunk * 16);
+    for (int j = 0; j < AI; ++j) {
+      const int i8 = 8 * (j * 8 + wid);
+      const int row = (i8 / QA) * WC + h * QA + i8 % QA;
+      wdst[h][j] = row * RBY;
+      woff[h][j] = (unsigned)(((c0 + row + lr) * a.Kpad) * 2 + lchunk * 16);
+    }
   // pixel block DMA: instruction i of a half-block fills LDS rows 8i .. 8i+7; wave w issues i = w, 8 + w
   // and wave 0 also i = 16.  LDS row q -> quadrant segment q / 34, pixel (q % 34) - 1 of the segment's
   // 32 columns; for kernel row kh the image row is the segment's row + kh - 1.
@@ -1223,7 +1237,7 @@ __global__ __launch_bounds__(512) void igemm_pp2h_kernel(IgemmArgs a) {
     const unsigned wk = (unsigned)((c.tap * a.Cs + c.ci) * 2);
     char* base = lds + buf * ASTAGE;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) dma16(wrs, base + (j * 128 + h * 64 + wid * 8) * RBY, woff[h][j] + wk);
+    for (int j = 0; j < AI; ++j) dma16(wrs, base + wdst[h][j], woff[h][j] + wk);
   };
   // pixel half-block h of kernel row kh, slice ci, into group buffer gb (2 instructions; wave 0: 3)
   auto issueB = [&](int h, int gb, int kh, int ci) {
@@ -1258,19 +1272,20 @@ __global__ __launch_bounds__(512) void igemm_pp2h_kernel(IgemmArgs a) {
   issueA(1, 0, k0);
   issueA(0, 1, kA1);
   KC kA0 = knext(kA1);                         // K-tile s+2 (A0 issue at p2 of s)
-  if (w0) wait_vm<7>(); else wait_vm<6>();     // A0(0), B0(0): newer are B1(0), A1(0), A0(1)
+  // waits below: "2 * AI" = two weight half-tiles, "+ 3 / + 2" = one pixel half-block (wave 0 / others)
+  if (w0) wait_vm<2 * AI + 3>(); else wait_vm<2 * AI + 2>();   // A0(0), B0(0): newer are B1(0), A1(0), A0(1)
   __builtin_amdgcn_sched_barrier(0);
   __builtin_amdgcn_s_barrier();
   if (grp) __builtin_amdgcn_s_barrier();       // the second half runs one barrier behind
   __builtin_amdgcn_sched_barrier(0);
 
-  bf16x8_t af[4][2], bfr[2][2][2];
+  bf16x8_t af[NIC][2], bfr[2][2][2];
   auto readA = [&](const char* Wt, int h) {
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-      for (int ic = 0; ic < 4; ++ic) {
-        const int row = wc * WC + h * 64 + ic * 16 + (lane & 15);
+      for (int ic = 0; ic < NIC; ++ic) {
+        const int row = wc * WC + h * QA + ic * 16 + (lane & 15);
         const int chunk = kk * 4 + (lane >> 4);
         af[ic][kk] = *reinterpret_cast<const bf16x8_t*>(Wt + row * RBY + ((chunk ^ (row & 7)) << 4));
       }
@@ -1291,11 +1306,11 @@ __global__ __launch_bounds__(512) void igemm_pp2h_kernel(IgemmArgs a) {
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-      for (int ic = 0; ic < 4; ++ic)
+      for (int ic = 0; ic < NIC; ++ic)
 #pragma unroll
         for (int ip = 0; ip < 2; ++ip)
-          acc[qa * 4 + ic][qb * 2 + ip] =
-              __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ic][kk], bfr[qb][ip][kk], acc[qa * 4 + ic][qb * 2 + ip], 0, 0, 0);
+          acc[qa * NIC + ic][qb * 2 + ip] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ic][kk], bfr[qb][ip][kk], acc[qa * NIC + ic][qb * 2 + ip], 0, 0, 0);
   };
   auto sync_in = [&]() {
     __builtin_amdgcn_sched_barrier(0);
@@ -1320,13 +1335,13 @@ __global__ __launch_bounds__(512) void igemm_pp2h_kernel(IgemmArgs a) {
       readB(gb, 0, 0);
       __builtin_amdgcn_sched_barrier(0);
       readA(Wt, 0);
-      wait_vm<4>();                            // B1 of this group (conservative: newer >= 4)
+      wait_vm<2 * AI>();                       // B1 of this group (conservative: newer >= 2 half-tiles)
       sync_in();
       mfma_quad(0, 0);
       sync_out();
       readB(gb, 1, 0);
       issueA(1, bA ^ 1, kA1);
-      wait_vm<4>();                            // A1 of this K-tile
+      wait_vm<2 * AI>();                       // A1 of this K-tile
       sync_in();
       mfma_quad(0, 1);
       sync_out();
@@ -1337,9 +1352,9 @@ __global__ __launch_bounds__(512) void igemm_pp2h_kernel(IgemmArgs a) {
       sync_out();
       if constexpr (!LAST) {
         issueB(0, gb ^ 1, kh2, ci2);
-        if (w0) wait_vm<7>(); else wait_vm<6>();   // A0 of K-tile t = 1
+        if (w0) wait_vm<2 * AI + 3>(); else wait_vm<2 * AI + 2>();   // A0 of K-tile t = 1
       } else {
-        wait_vm<4>();
+        wait_vm<2 * AI>();
       }
       sync_in();
       mfma_quad(1, 0);
@@ -1360,9 +1375,9 @@ __global__ __launch_bounds__(512) void igemm_pp2h_kernel(IgemmArgs a) {
       readB(gb, 1, 1);
       issueA(1, bA, kA1);
       if constexpr (!LAST) {
-        if (w0) wait_vm<10>(); else wait_vm<8>();  // A1 of this K-tile
+        if (w0) wait_vm<2 * AI + 6>(); else wait_vm<2 * AI + 4>();   // A1 of this K-tile
       } else {
-        wait_vm<4>();
+        wait_vm<2 * AI>();
       }
       sync_in();
       mfma_quad(0, 1);
@@ -1373,9 +1388,9 @@ __global__ __launch_bounds__(512) void igemm_pp2h_kernel(IgemmArgs a) {
       mfma_quad(1, 1);
       sync_out();
       if constexpr (!LAST) {
-        if (w0) wait_vm<10>(); else wait_vm<8>();  // A0 of K-tile t = 2
+        if (w0) wait_vm<2 * AI + 6>(); else wait_vm<2 * AI + 4>();   // A0 of K-tile t = 2
       } else {
-        wait_vm<2>();
+        wait_vm<AI>();
       }
       sync_in();
       mfma_quad(1, 0);
@@ -1395,7 +1410,7 @@ __global__ __launch_bounds__(512) void igemm_pp2h_kernel(IgemmArgs a) {
       readB(gb, 1, 2);
       if constexpr (!LAST) {
         issueA(1, bA ^ 1, kA1);
-        wait_vm<4>();                          // A1 of this K-tile
+        wait_vm<2 * AI>();                     // A1 of this K-tile
       } else {
         wait_vm<0>();
       }
@@ -1407,7 +1422,7 @@ __global__ __launch_bounds__(512) void igemm_pp2h_kernel(IgemmArgs a) {
       sync_in();
       mfma_quad(1, 1);
       sync_out();
-      if constexpr (!LAST) wait_vm<4>();       // A0 of the next group's first K-tile (+ its B0, older)
+      if constexpr (!LAST) wait_vm<2 * AI>();  // A0 of the next group's first K-tile (+ its B0, older)
       sync_in();
       mfma_quad(1, 0);
       sync_out();
@@ -1439,6 +1454,13 @@ static inline bool pp2h_ok(const IgemmArgs& a) {
   return a.mode == 0 && a.KH == 3 && a.KW == 3 && a.stride == 1 && a.pad == 1 && a.Hs == a.Ho && a.Ws == a.Wo &&
          !(a.korder & 1) && a.Kpad == 9 * a.Cs && (a.Cs % 64) == 0 && (W == 32 || W == 64 || W == 128 || W == 256) &&
          ((long)a.Ho * W) % 256 == 0 && a.Ngemm % 256 == 0;
+}
+
+// the 128-channel form (cfg 15): same conditions with Ngemm % 128
+static inline bool pp2h128_ok(const IgemmArgs& a) {
+  IgemmArgs b = a;
+  b.Ngemm = 256;
+  return pp2h_ok(b) && a.Ngemm % 128 == 0;
 }
 
 template <int BC, int BP, int WC, int WP, int ST, int BK = 64, bool PRE = false>
@@ -1526,6 +1548,16 @@ DPA_API int dpa_igemm_glds(const IgemmArgs* args, int cfg, hipStream_t st) {
       else if (probe == 3) hipLaunchKernelGGL(igemm_pp2_kernel<3>, dim3(grid), dim3(512), 0, st, a);
       else if (probe == 4) hipLaunchKernelGGL(igemm_pp2_kernel<4>, dim3(grid), dim3(512), 0, st, a);
       else hipLaunchKernelGGL(igemm_pp2_kernel<0>, dim3(grid), dim3(512), 0, st, a);
+      return (int)hipGetLastError();
+    }
+    case 15: {
+      if (!pp2h128_ok(a)) break;
+      const int grid = (a.N * a.Ho * a.Wo / 256) * (a.Ngemm / 128);
+      const int ep = no_fast_ep ? 0 : glds_ep_kind(a);
+      if (ep == 1) hipLaunchKernelGGL((igemm_pp2h_kernel<1, 128>), dim3(grid), dim3(512), 0, st, a);
+      else if (ep == 2) hipLaunchKernelGGL((igemm_pp2h_kernel<2, 128>), dim3(grid), dim3(512), 0, st, a);
+      else if (ep == 3) hipLaunchKernelGGL((igemm_pp2h_kernel<3, 128>), dim3(grid), dim3(512), 0, st, a);
+      else hipLaunchKernelGGL((igemm_pp2h_kernel<0, 128>), dim3(grid), dim3(512), 0, st, a);
       return (int)hipGetLastError();
     }
     case 11: {

@@ -104,6 +104,10 @@ GLDS_NO_PRELOAD = os.environ.get("DPA_GLDS_NO_PRELOAD", "0") == "1"
 GLDS_NO_PP = os.environ.get("DPA_GLDS_NO_PP", "0") == "1"
 # A/B: the ping-pong kernel without row-block pixel staging (csrc/igemm_glds.hip igemm_pp2h_kernel)
 GLDS_NO_ROWBLOCK = os.environ.get("DPA_GLDS_NO_ROWBLOCK", "0") == "1"
+# 128-channel convs on the row-block ping-pong GEMM (csrc/igemm_glds.hip cfg 15, igemm_pp2h_kernel<EP, 128>)
+# instead of the row-halo kernel: 10-15 % faster on every 128-output-channel 3x3 conv / dgrad of the 512^2
+# UNet (profiles/kbench_glds_rowblock128_b256_r03.txt); DPA_NO_GLDS128=1 disables (A/B)
+USE_GLDS128 = os.environ.get("DPA_NO_GLDS128", "0") != "1"
 # conv weight gradients on a side HIP stream, overlapping each block's dgrad chain (models/hip_unet.py)
 SIDE_WGRAD = os.environ.get("DPA_NO_SIDE_WGRAD", "0") != "1"
 # HIP stream priority of the weight-gradient side stream (torch convention: lower = higher priority,
@@ -281,7 +285,11 @@ def igemm(x: torch.Tensor, wpacked: torch.Tensor, y: torch.Tensor, *, Ngemm: int
     # beats the LDS-DMA kernel on every shape both accept (128-channel dgrads: 837 vs 1042 us at
     # 128^2, 2542 vs 2948 us at 256^2); the LDS-DMA kernel takes what the halo kernel cannot
     # (64^2 and smaller grids, > 128 output channels)
-    if a is not None and (path == "halo" or (path == "auto" and USE_HALO and conv3 and Cs % 32 == 0 and Ngemm <= 128)):
+    # whole-row 256-pixel tiles, slice-major K, N % 256 != 0 (N % 256 == 0 takes cfg 14's 256-channel form)
+    rb128 = (path == "auto" and USE_GLDS128 and USE_GLDS and not GLDS_TAP_MAJOR and conv3 and pad == 1 and
+             (Hs, Ws) == (Ho, Wo) and Kpad == 9 * Cs and Cs % 64 == 0 and Wo in (32, 64, 128, 256) and
+             (Ho * Wo) % 256 == 0 and Ngemm % 128 == 0 and Ngemm % 256 != 0)
+    if a is not None and not rb128 and (path == "halo" or (path == "auto" and USE_HALO and conv3 and Cs % 32 == 0 and Ngemm <= 128)):
         err = L.dpa_igemm_halo(ctypes.byref(a), c_int(variant if path == "halo" else HALO_CFG), st)
         if err == 0:
             done = True
@@ -293,7 +301,7 @@ def igemm(x: torch.Tensor, wpacked: torch.Tensor, y: torch.Tensor, *, Ngemm: int
         a = args(n0, n1, False)
         if path == "glds" or (path == "auto" and glds_ok):
             no_pers = GLDS_NO_PERS or not persistent
-            err = L.dpa_igemm_glds(ctypes.byref(a), c_int(variant if path == "glds" else 16 * GLDS_TAP_MAJOR + 32 * no_pers + 64 * GLDS_NO_PRELOAD + 128 * GLDS_NO_PP + 8192 * GLDS_NO_ROWBLOCK), st)
+            err = L.dpa_igemm_glds(ctypes.byref(a), c_int(variant if path == "glds" else 15 if rb128 else 16 * GLDS_TAP_MAJOR + 32 * no_pers + 64 * GLDS_NO_PRELOAD + 128 * GLDS_NO_PP + 8192 * GLDS_NO_ROWBLOCK), st)
             if err == 0:
                 continue
             if path == "glds":

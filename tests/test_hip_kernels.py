@@ -675,3 +675,26 @@ def test_glds_pingpong_epilogues(hip_lib, N, H, W, Cs, Ng, kind):
         outs.append(y)
     torch.cuda.synchronize()
     assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+
+
+@pytest.mark.parametrize("N,H,W,Cs,Ng,kind", [(4, 128, 128, 128, 128, "fwd"), (3, 30, 256, 64, 128, "dgrad"),
+                                               (2, 64, 64, 256, 384, "fwd"), (8, 32, 32, 64, 128, "dgrad")])
+def test_glds_rowblock_128(hip_lib, N, H, W, Cs, Ng, kind):
+    """The 128-channel row-block kernel (cfg 15) == the 128x256 3-stage kernel (cfg 2) bitwise (same K
+    order), with the specialised and the generic (cfg 15 + 2048) epilogues."""
+    from distributedpytorch_amd.ops import kernels as K
+    torch.manual_seed(29)
+    x = torch.randn(N, H, W, Cs, device="cuda").to(torch.bfloat16)
+    Kp = 9 * Cs
+    w = (torch.randn(Ng, Kp, device="cuda") / Kp ** 0.5).to(torch.bfloat16)
+    extra = (dict(bias=torch.randn(Ng, device="cuda") * 0.1, relu=True) if kind == "fwd" else
+             dict(mask=torch.randn(N, H, W, Ng, device="cuda").to(torch.bfloat16)))
+    outs = []
+    for v in (2, 15, 2048 + 15):
+        y = torch.empty(N, H, W, Ng, device="cuda", dtype=torch.bfloat16)
+        K.igemm(x, w, y, Ngemm=Ng, Kpad=Kp, KH=3, KW=3, stride=1, pad=1, Cs=Cs, out_grid=(N, H, W), path="glds",
+                variant=v, **extra)
+        outs.append(y)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[1], outs[2])
+    assert torch.equal(outs[0], outs[1]) or _rel(outs[1].float().cpu(), outs[0].float().cpu()) < 1e-2

@@ -26,7 +26,7 @@ def main():
     B, S = a.batch, a.img
     torch.manual_seed(0)
     # (name, H, Cin, Cout): fwd GEMM N = Cout, dgrad GEMM N = Cin
-    layers = [("L2 64->128", S // 4, 64, 128), ("L2 128->128", S // 4, 128, 128),
+    layers = [("L1 128->64", S // 2, 128, 64), ("L2 64->128", S // 4, 64, 128), ("L2 128->128", S // 4, 128, 128),
               ("L2 256->128", S // 4, 256, 128), ("L3 128->256", S // 8, 128, 256), ("L3 256->256", S // 8, 256, 256),
               ("L3 512->256", S // 8, 512, 256), ("mid 256->512", S // 16, 256, 512), ("mid 512->512", S // 16, 512, 512)]
     bad = 0
