@@ -1141,7 +1141,7 @@ __global__ __launch_bounds__(512) void igemm_pp2_kernel(IgemmArgs a) {
 
 // ------------------------------------------------------------------------------------------------
 // Row-block ping-pong (cfg 14 with row-block pixel staging, 3x3 s1 p1 convs whose 256-pixel tiles are
-// whole image rows: W in {32, 64, 128, 256}).  cfg 14 stages the pixel operand per K-tile = per (tap,
+// whole image rows, W in {32, 64, 128, 256}, or 256-pixel parts of rows, W % 256 == 0).  cfg 14 stages the pixel operand per K-tile = per (tap,
 // 64-channel slice): the three kw taps of a kernel row fetch three 1-pixel-shifted copies of the same
 // rows (32 KB each).  Here the pixel half-tiles of a kernel row kh are fetched ONCE as blocks of four
 // 34-pixel row segments (the 32 pixels of a wave's quadrant + the kw halo; 17 KB) and the kw = 0,1,2
@@ -1177,7 +1177,8 @@ __global__ __launch_bounds__(512) void igemm_pp2h_kernel(IgemmArgs a) {
   int pt, ct;
   glds_tile(bid, npt, nct, pt, ct);
   const int m0 = pt * BP, c0 = ct * BC;
-  const int img = m0 / HW, tr0 = (m0 - img * HW) / W;        // tile = image rows tr0 .. tr0 + 256/W - 1
+  const int img = m0 / HW, p0 = m0 - img * HW;               // tile = pixels p0 .. p0 + 255 of image img
+                                                             // (whole rows, or a part of one row for W >= 512)
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wc = wid & 1, wp = wid >> 1, grp = wid >> 2;
@@ -1210,7 +1211,7 @@ __global__ __launch_bounds__(512) void igemm_pp2h_kernel(IgemmArgs a) {
       const int q = 8 * i + lr;
       const int sg = q / SEG, loc = q - sg * SEG;
       const int pq = sg * 64 + h * 32;                        // first pixel of the quadrant segment
-      const int r = tr0 + pq / W, col = pq % W + loc - 1;
+      const int r = (p0 + pq) / W, col = (p0 + pq) % W + loc - 1;
       const bool cok = col >= 0 && col < W && (j < 2 || wid == 0);
       unsigned vb = 0;
 #pragma unroll
@@ -1452,7 +1453,7 @@ __global__ __launch_bounds__(512) void igemm_pp2h_kernel(IgemmArgs a) {
 static inline bool pp2h_ok(const IgemmArgs& a) {
   const int W = a.Wo;
   return a.mode == 0 && a.KH == 3 && a.KW == 3 && a.stride == 1 && a.pad == 1 && a.Hs == a.Ho && a.Ws == a.Wo &&
-         !(a.korder & 1) && a.Kpad == 9 * a.Cs && (a.Cs % 64) == 0 && (W == 32 || W == 64 || W == 128 || W == 256) &&
+         !(a.korder & 1) && a.Kpad == 9 * a.Cs && (a.Cs % 64) == 0 && (W == 32 || W == 64 || W == 128 || W % 256 == 0) &&
          ((long)a.Ho * W) % 256 == 0 && a.Ngemm % 256 == 0;
 }
 

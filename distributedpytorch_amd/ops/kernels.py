@@ -287,7 +287,7 @@ def igemm(x: torch.Tensor, wpacked: torch.Tensor, y: torch.Tensor, *, Ngemm: int
     # (64^2 and smaller grids, > 128 output channels)
     # whole-row 256-pixel tiles, slice-major K, N % 256 != 0 (N % 256 == 0 takes cfg 14's 256-channel form)
     rb128 = (path == "auto" and USE_GLDS128 and USE_GLDS and not GLDS_TAP_MAJOR and conv3 and pad == 1 and
-             (Hs, Ws) == (Ho, Wo) and Kpad == 9 * Cs and Cs % 64 == 0 and Wo in (32, 64, 128, 256) and
+             (Hs, Ws) == (Ho, Wo) and Kpad == 9 * Cs and Cs % 64 == 0 and (Wo in (32, 64, 128) or Wo % 256 == 0) and
              (Ho * Wo) % 256 == 0 and Ngemm % 128 == 0 and Ngemm % 256 != 0)
     if a is not None and not rb128 and (path == "halo" or (path == "auto" and USE_HALO and conv3 and Cs % 32 == 0 and Ngemm <= 128)):
         err = L.dpa_igemm_halo(ctypes.byref(a), c_int(variant if path == "halo" else HALO_CFG), st)

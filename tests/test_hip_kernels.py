@@ -655,7 +655,9 @@ def test_wgrad_multi_microbatches(hip_lib, M, Nc, H, W, mb, nmb):
                                                (9, 64, 64, 256, 256, "dgrad"), (5, 61, 67, 512, 256, "dgrad"),
                                                # row-block tiles of 8 / 2 / 1 image rows (W = 32 / 128 / 256)
                                                (16, 32, 32, 128, 256, "fwd"), (3, 30, 128, 64, 256, "dgrad"),
-                                               (2, 70, 256, 64, 256, "fwd")])
+                                               (2, 70, 256, 64, 256, "fwd"),
+                                               # tiles = half / third of a row (W = 512 / 768)
+                                               (2, 9, 512, 64, 256, "dgrad"), (1, 5, 768, 128, 256, "fwd")])
 def test_glds_pingpong_epilogues(hip_lib, N, H, W, Cs, Ng, kind):
     """The ping-pong deep GEMM (cfg 14; on whole-row tiles its row-block pixel staging form, 8206 = cfg 14
     without row blocks) with its specialised epilogues (forward bias + ReLU, dgrad ReLU mask; partial
@@ -678,7 +680,8 @@ def test_glds_pingpong_epilogues(hip_lib, N, H, W, Cs, Ng, kind):
 
 
 @pytest.mark.parametrize("N,H,W,Cs,Ng,kind", [(4, 128, 128, 128, 128, "fwd"), (3, 30, 256, 64, 128, "dgrad"),
-                                               (2, 64, 64, 256, 384, "fwd"), (8, 32, 32, 64, 128, "dgrad")])
+                                               (2, 64, 64, 256, 384, "fwd"), (8, 32, 32, 64, 128, "dgrad"),
+                                               (2, 9, 512, 128, 128, "fwd"), (1, 5, 768, 64, 128, "dgrad")])
 def test_glds_rowblock_128(hip_lib, N, H, W, Cs, Ng, kind):
     """The 128-channel row-block kernel (cfg 15) == the 128x256 3-stage kernel (cfg 2) bitwise (same K
     order), with the specialised and the generic (cfg 15 + 2048) epilogues."""
