@@ -183,6 +183,99 @@ __device__ __forceinline__ void glds_epilogue_fast(const IgemmArgs& a, f32x4_t (
   }
 }
 
+// sum over the 16 lanes of a DPP row (every lane gets it; lane order of the adds is fixed per lane):
+// row rotations by 8, 4, 2, 1 on the VALU (ds_bpermute / __shfl_xor goes through the LDS unit and
+// serialises: 128 of them cost ~4 us per workgroup in this epilogue)
+__device__ __forceinline__ float row16_sum(float v) {
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x128, 0xf, 0xf, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x124, 0xf, 0xf, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x122, 0xf, 0xf, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x121, 0xf, 0xf, false));
+  return v;
+}
+
+// EP 1 / 2 plus the BatchNorm partial sums of the STORED bf16 values for the producing conv's BN (row-block
+// kernels, 4 pixel waves x 2 channel waves): forward (EP 1: bias, no ReLU): sum y, sum y^2; backward (EP 2,
+// mask = the BN output): sum g, sum g * mask.  One slab row per 256-pixel tile, bnslab[m0 / 256][2][Ngemm],
+// reduced in a fixed order (16-lane DPP row sum, then the 4 pixel waves in order).
+// Channel fragments outermost so only one fragment's sums are live (acc already holds 128 VGPRs).
+// bred: 4 x 2BC floats of the kernel's own LDS that no wave reads any more (a separate __shared__
+// array makes hipcc wait vmcnt(0) before every fragment read of the K loop: it cannot tell the second
+// LDS object from the LDS-DMA destination -- +15 % on the 128-channel layers).
+template <int TC, int TP, int WC, int WP, int EP>
+__device__ __forceinline__ void glds_epilogue_bns(const IgemmArgs& a, f32x4_t (&acc)[TC][TP], int M, int m0, int c0,
+                                                  int wc, int wp, int lane, float* bred_) {
+  static_assert(EP == 1 || EP == 2, "BN partial sums: EP 1 / 2");
+  constexpr int BC = 2 * WC;
+  float (*bred)[2 * BC] = reinterpret_cast<float (*)[2 * BC]>(bred_);
+  const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc((void*)a.y, 0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t mr = __builtin_amdgcn_make_buffer_rsrc((void*)(EP == 2 ? a.mask : a.y), 0, 0x7fffffff, 0x00020000);
+  const int cb = c0 + wc * WC + 4 * (lane >> 4);
+  unsigned yo[TP], mo[TP];
+  float okf[TP];
+#pragma unroll
+  for (int ip = 0; ip < TP; ++ip) {
+    const int m = m0 + wp * WP + ip * 16 + (lane & 15);
+    const bool ok = m < M;
+    okf[ip] = ok ? 1.f : 0.f;
+    yo[ip] = ok ? (unsigned)m * (unsigned)a.ldy * 2u + (unsigned)cb * 2u : 0x80000000u;
+    mo[ip] = EP == 2 && ok ? (unsigned)m * (unsigned)a.ldm * 2u + (unsigned)cb * 2u : 0x80000000u;
+  }
+#pragma unroll
+  for (int ic = 0; ic < TC; ++ic) {
+    float bias[4] = {0.f, 0.f, 0.f, 0.f};
+    if (EP == 1 && a.bias) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) bias[e] = a.bias[cb + ic * 16 + e];
+    }
+    u32x2_t mk[TP];
+    if constexpr (EP == 2) {
+#pragma unroll
+      for (int ip = 0; ip < TP; ++ip) mk[ip] = __builtin_amdgcn_raw_buffer_load_b64(mr, mo[ip] + ic * 32, 0, 0);
+    }
+    float s[4] = {0.f, 0.f, 0.f, 0.f}, q[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ip = 0; ip < TP; ++ip) {
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = acc[ic][ip][e] + bias[e];
+      float f[4];
+      if constexpr (EP == 2) {
+        f[0] = lo_bf(mk[ip].x); f[1] = hi_bf(mk[ip].x); f[2] = lo_bf(mk[ip].y); f[3] = hi_bf(mk[ip].y);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = f[e] > 0.f ? v[e] : 0.f;      // host: mask_ch == Ngemm
+      }
+      const u32x2_t pk = u32x2_t{pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3])};
+      __builtin_amdgcn_raw_buffer_store_b64(pk, yr, yo[ip] + ic * 32, 0, 0);
+      const float st[4] = {okf[ip] * lo_bf(pk.x), okf[ip] * hi_bf(pk.x), okf[ip] * lo_bf(pk.y), okf[ip] * hi_bf(pk.y)};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        s[e] += st[e];
+        q[e] = fmaf(st[e], EP == 2 ? f[e] : st[e], q[e]);
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      s[e] = row16_sum(s[e]);
+      q[e] = row16_sum(q[e]);
+      if ((lane & 15) == 0) {
+        const int c = wc * WC + ic * 16 + 4 * (lane >> 4) + e;
+        bred[wp][c] = s[e];
+        bred[wp][BC + c] = q[e];
+      }
+    }
+  }
+  // LDS-only barrier: __syncthreads' release fence would first wait for every output store of the
+  // block to be acknowledged (vmcnt(0)), several us per block with one 132-KB block per CU
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  float* row = a.bnslab + (long)(m0 / 256) * 2 * a.Ngemm;
+  for (int k = threadIdx.x; k < 2 * BC; k += blockDim.x) {
+    const float t = (bred[0][k] + bred[1][k]) + (bred[2][k] + bred[3][k]);
+    row[k < BC ? c0 + k : a.Ngemm + c0 + (k - BC)] = t;
+  }
+}
+
 // epilogue kind for a launch: 1 / 2 when the specialised code covers it, else 0 (generic)
 static inline int glds_ep_kind(const IgemmArgs& a) {
   if (a.mode != 0 || a.accumulate || (a.ldy & 3)) return 0;
@@ -1156,7 +1249,7 @@ __global__ __launch_bounds__(512) void igemm_pp2_kernel(IgemmArgs a) {
 // BC = 128 (the 128-output-channel convs / dgrads of the 128^2 level): the same schedule with 64 channels
 // per wave (2 x 32-row quadrant halves, 8 MFMAs per quadrant, one weight DMA instruction per half-tile);
 // 100 KB of LDS instead of 132.
-template <int EP, int BC = 256>
+template <int EP, int BC = 256, bool BNS = false>
 __global__ __launch_bounds__(512) void igemm_pp2h_kernel(IgemmArgs a) {
   static_assert(BC == 256 || BC == 128, "channel tile");
   constexpr int BP = 256, WC = BC / 2, WP = 64, TC = WC / 16, TP = 4, RBY = 128;
@@ -1166,6 +1259,7 @@ __global__ __launch_bounds__(512) void igemm_pp2h_kernel(IgemmArgs a) {
   constexpr int ASTAGE = BC * RBY;             // weight K-tile image (32 / 16 KB)
   constexpr int SEG = 34;                      // pixel rows per quadrant segment (32 + kw halo)
   constexpr int BHALF = 4 * SEG * RBY;         // one pixel half-block (17 KB, 17 DMA instructions)
+  static_assert(2 * BHALF >= 4 * 2 * BC * 4, "BN sums staging fits one pixel group buffer");
   __shared__ __attribute__((aligned(16))) char lds[2 * ASTAGE + 4 * BHALF];
   char* const Bimg = lds + 2 * ASTAGE;
 
@@ -1445,7 +1539,12 @@ __global__ __launch_bounds__(512) void igemm_pp2h_kernel(IgemmArgs a) {
   group(std::integral_constant<bool, true>{}, (G - 1) & 1, (G - 1) & 1, 0, 0);
   if (!grp) __builtin_amdgcn_s_barrier();      // balance the second half's extra barrier
 
-  if constexpr (EP != 0) glds_epilogue_fast<TC, TP, WC, WP, EP>(a, acc, M, m0, c0, wc, wp, lane);
+  // BN sums: staged in the pixel group buffer the last kernel-row group does not use (last read in
+  // group G-2, before barriers every wave has passed; no DMA targets it any more)
+  if constexpr (BNS)
+    glds_epilogue_bns<TC, TP, WC, WP, EP>(a, acc, M, m0, c0, wc, wp, lane,
+                                          reinterpret_cast<float*>(Bimg + ((((G - 1) & 1) ^ 1) * 2) * BHALF));
+  else if constexpr (EP != 0) glds_epilogue_fast<TC, TP, WC, WP, EP>(a, acc, M, m0, c0, wc, wp, lane);
   else glds_epilogue<TC, TP, WC, WP>(a, acc, M, m0, c0, wc, wp, lane);
 }
 
@@ -1492,6 +1591,28 @@ DPA_API int dpa_igemm_glds(const IgemmArgs* args, int cfg, hipStream_t st) {
   const bool no_rowblock = cfg & 8192;  // A/B: cfg 14 with per-K-tile pixel staging (no row blocks)
   cfg &= 15;
   if ((a.Cs & 63) || (a.Kpad & 63) || (a.ldx & 7) || (a.ldy & 3) || a.KH * a.KW > 32) return (int)hipErrorInvalidValue;
+  if (a.bnslab) {
+    // BatchNorm partial sums (bnslab[M / 256][2][Ngemm]): only the row-block kernels' EP 1 / 2 epilogues
+    // carry them (cfg 0 -> 14 / 15 by the channel count); anything else is refused, never silently skipped
+    const long M = (long)a.N * a.Ho * a.Wo;
+    const int ep = glds_ep_kind(a);
+    if (probe || no_fast_ep || no_rowblock || (a.korder & 1) || (ep != 1 && ep != 2) ||
+        (ep == 2 && a.mask_ch != a.Ngemm) || M % 256)
+      return (int)hipErrorInvalidValue;
+    if (cfg == 0) cfg = a.Ngemm % 256 == 0 ? 14 : 15;
+    const bool ok = cfg == 14 ? (pp2h_ok(a) && a.Kpad >= 128) : cfg == 15 ? pp2h128_ok(a) : false;
+    if (!ok) return (int)hipErrorInvalidValue;
+    const int BCt = cfg == 14 ? 256 : 128;
+    const int grid = (int)(M / 256) * (a.Ngemm / BCt);
+    if (cfg == 14) {
+      if (ep == 1) hipLaunchKernelGGL((igemm_pp2h_kernel<1, 256, true>), dim3(grid), dim3(512), 0, st, a);
+      else hipLaunchKernelGGL((igemm_pp2h_kernel<2, 256, true>), dim3(grid), dim3(512), 0, st, a);
+    } else {
+      if (ep == 1) hipLaunchKernelGGL((igemm_pp2h_kernel<1, 128, true>), dim3(grid), dim3(512), 0, st, a);
+      else hipLaunchKernelGGL((igemm_pp2h_kernel<2, 128, true>), dim3(grid), dim3(512), 0, st, a);
+    }
+    return (int)hipGetLastError();
+  }
   if (a.mode == 1 && (a.Cout & 3)) return (int)hipErrorInvalidValue;
   if (cfg == 0) {
     // largest tile that still gives >= 512 workgroups (2 per CU; one 131-147 KB workgroup fits a CU):

@@ -108,6 +108,8 @@ GLDS_NO_ROWBLOCK = os.environ.get("DPA_GLDS_NO_ROWBLOCK", "0") == "1"
 # instead of the row-halo kernel: 10-15 % faster on every 128-output-channel 3x3 conv / dgrad of the 512^2
 # UNet (profiles/kbench_glds_rowblock128_b256_r03.txt); DPA_NO_GLDS128=1 disables (A/B)
 USE_GLDS128 = os.environ.get("DPA_NO_GLDS128", "0") != "1"
+# BatchNorm partial sums in the row-block GEMM epilogue (deep BN layers); DPA_NO_GLDS_BN=1 disables (A/B)
+USE_GLDS_BN = os.environ.get("DPA_NO_GLDS_BN", "0") != "1"
 # conv weight gradients on a side HIP stream, overlapping each block's dgrad chain (models/hip_unet.py)
 SIDE_WGRAD = os.environ.get("DPA_NO_SIDE_WGRAD", "0") != "1"
 # HIP stream priority of the weight-gradient side stream (torch convention: lower = higher priority,
@@ -217,6 +219,7 @@ def igemm(x: torch.Tensor, wpacked: torch.Tensor, y: torch.Tensor, *, Ngemm: int
     st = _stream(y)
     hslab = None
     bslab = None
+    want_bn = False
     if bn_stats is not None and USE_FUSED_BN and mode == 0 and pool is None and y2 is None and head is None \
             and not accumulate and not relu and path == "auto" and (mask is None or mch == Ngemm):
         bslab = torch.empty(N * -(-Ho // 16) * -(-Wo // 64) * 2 * Ngemm, dtype=torch.float32, device=y.device)
@@ -263,8 +266,10 @@ def igemm(x: torch.Tensor, wpacked: torch.Tensor, y: torch.Tensor, *, Ngemm: int
                     return
                 a.bnslab = None
         # not fusable here: the BN pass computes the statistics (the same epilogue in the row-halo
-        # kernel measured 4% slower end to end: its extra registers cost more than the pass it saves)
+        # kernel measured 4% slower end to end: its extra registers cost more than the pass it saves),
+        # unless the row-block GEMM (below) takes the conv: its epilogue writes one slab row per tile
         bslab = None
+        want_bn = True
     if _ABLATE and path == "auto":
         fam = ("stream" if (a is not None and USE_STREAM and conv3 and stream_ok) else
                "halo" if (a is not None and USE_HALO and conv3 and Cs % 32 == 0 and Ngemm <= 128) else
@@ -297,8 +302,19 @@ def igemm(x: torch.Tensor, wpacked: torch.Tensor, y: torch.Tensor, *, Ngemm: int
             _check(err, "igemm_halo")
     # ---- chunked kernels (LDS-DMA GEMM, generic gather): 32-bit offsets over the whole chunk
     glds_ok = USE_GLDS and cfg == 0 and Cs % 64 == 0 and Kpad % 64 == 0 and Ngemm % 128 == 0
+    # BatchNorm partial sums from the row-block GEMM's epilogue (csrc/igemm_glds.hip glds_epilogue_bns):
+    # bnslab[M / 256][2][Ngemm]; the kernel refuses shapes it cannot take (then the BN pass computes them)
+    gslab = None
+    if want_bn and not done and path == "auto" and glds_ok and (Ho * Wo) % 256 == 0 and USE_GLDS_BN:
+        gslab = torch.empty(N * Ho * Wo // 256 * 2 * Ngemm, dtype=torch.float32, device=y.device)
     for n0, n1 in ([] if done else _image_chunks(N, max(Hs * Ws * ldx, (4 if mode else 1) * Ho * Wo * ldy) * 2)):
         a = args(n0, n1, False)
+        if gslab is not None:
+            a.bnslab = gslab[n0 * Ho * Wo // 256 * 2 * Ngemm:].data_ptr()
+            if L.dpa_igemm_glds(ctypes.byref(a), c_int(0), st) == 0:
+                continue
+            assert n0 == 0, "row-block BN statistics refused after the first chunk"
+            a.bnslab, gslab = None, None
         if path == "glds" or (path == "auto" and glds_ok):
             no_pers = GLDS_NO_PERS or not persistent
             err = L.dpa_igemm_glds(ctypes.byref(a), c_int(variant if path == "glds" else 15 if rb128 else 16 * GLDS_TAP_MAJOR + 32 * no_pers + 64 * GLDS_NO_PRELOAD + 128 * GLDS_NO_PP + 8192 * GLDS_NO_ROWBLOCK), st)
@@ -307,6 +323,8 @@ def igemm(x: torch.Tensor, wpacked: torch.Tensor, y: torch.Tensor, *, Ngemm: int
             if path == "glds":
                 _check(err, "igemm_glds")
         _check(L.dpa_igemm(ctypes.byref(a), c_int(cfg), st), "igemm")
+    if gslab is not None:
+        bn_stats.extend([gslab, N * Ho * Wo // 256])
     if pool is not None:
         maxpool2(y, pool, pcode)
 

@@ -207,7 +207,9 @@ def test_hip_unet_variants_match_torch_fp32(hip_lib, variant):
 
 
 @pytest.mark.parametrize("N,H,W,Cin,Cout", [(2, 5, 128, 32, 32), (1, 7, 64, 64, 32), (2, 6, 128, 32, 64),
-                                            (1, 33, 64, 64, 64)])
+                                            (1, 33, 64, 64, 64),
+                                            # deep layers: the row-block GEMM's epilogue (256 / 128 channels)
+                                            (2, 16, 64, 128, 256), (1, 8, 128, 64, 128), (1, 2, 512, 128, 128)])
 def test_conv_bn_stats_fused_in_stream_epilogue(hip_lib, N, H, W, Cin, Cout):
     """Conv followed by BatchNorm on the streaming kernel: the batch statistics come from the conv's
     epilogue (per-block channel sums of the stored bf16 output) instead of a separate pass.  Output,
@@ -279,7 +281,9 @@ def test_bn_apply_fused_maxpool(hip_lib, N, H, W, C):
 
 
 @pytest.mark.parametrize("N,H,W,C1,C2", [(2, 5, 128, 32, 32), (1, 6, 64, 64, 64), (2, 3, 128, 32, 64),
-                                         (1, 4, 128, 64, 32)])
+                                         (1, 4, 128, 64, 32),
+                                         # deep layers: the row-block GEMM's epilogue (256 / 128 channels)
+                                         (1, 8, 64, 256, 128), (2, 4, 64, 128, 256)])
 def test_bn_backward_partials_fused_in_stream_dgrad(hip_lib, N, H, W, C1, C2):
     """The dgrad into a BN layer's output y = relu(bn(z)) (ReLU mask y) also writes sum g, sum g*y per
     channel from its epilogue; bn_bwd then skips its reduction pass (sum g*xhat = (sum g*y - beta
