@@ -1596,7 +1596,7 @@ DPA_API int dpa_igemm_glds(const IgemmArgs* args, int cfg, hipStream_t st) {
     // carry them (cfg 0 -> 14 / 15 by the channel count); anything else is refused, never silently skipped
     const long M = (long)a.N * a.Ho * a.Wo;
     const int ep = glds_ep_kind(a);
-    if (probe || no_fast_ep || no_rowblock || (a.korder & 1) || (ep != 1 && ep != 2) ||
+    if (probe || no_fast_ep || no_rowblock || (a.korder & 1) || (ep != 1 && ep != 2) || (ep == 1 && a.relu) ||
         (ep == 2 && a.mask_ch != a.Ngemm) || M % 256)
       return (int)hipErrorInvalidValue;
     if (cfg == 0) cfg = a.Ngemm % 256 == 0 ? 14 : 15;

@@ -71,6 +71,19 @@ def test_glds_igemm_rejects(L, kw):
     assert L.dpa_igemm_glds(ctypes.byref(a), 0, None) == INVALID
 
 
+@pytest.mark.parametrize("kw", [dict(Wo=96, Ws=96), dict(relu=1), dict(Kpad=640), dict(Ngemm=192),
+                                dict(mask=1, mask_ch=128, ldm=256)])
+def test_glds_bn_sums_refuse_other_shapes(L, kw):
+    """BatchNorm partial sums (bnslab) exist only in the row-block kernels' forward (bias, no ReLU) and
+    full-mask dgrad epilogues: every other launch is refused before anything runs (the caller then
+    computes the statistics with the BN pass), never silently run without them."""
+    a = _igemm_args(Cs=64, Kpad=576, Ngemm=256, ldx=64, ldy=256, N=2, Ho=32, Wo=64, Hs=32, Ws=64)
+    a.bnslab = 0x1000     # never dereferenced: the host checks return first
+    for k, v in kw.items():
+        setattr(a, k, v)
+    assert L.dpa_igemm_glds(ctypes.byref(a), 0, None) == INVALID
+
+
 @pytest.mark.parametrize("kw", [dict(mode=1), dict(KH=1, KW=1), dict(stride=2), dict(Cs=48, Kpad=448),
                                 dict(Hs=66), dict(Kpad=256), dict(Wo=96, Ws=96)])
 def test_halo_igemm_rejects(L, kw):
