@@ -121,10 +121,15 @@ __device__ __forceinline__ void glds_epilogue(const IgemmArgs& a, f32x4_t (&acc)
 // The generic epilogue carries every mode (scatter, split, accumulate, mask) behind runtime branches:
 // ~5000 instructions that cost 10-20 % of a deep layer's time (profiles/experiments_r03_late.txt).
 // Out-of-range pixels store to an offset past the buffer's range check (dropped) instead of branching.
-template <int TC, int TP, int WC, int WP, int EP>
+// PM: the EP 2 mask fragments were loaded by the caller up front (pmk[ip * TC + ic]), so their latency
+// overlaps the K loop instead of opening the epilogue.
+// PB: likewise the EP 1 bias values (pbias[ic * 4 + e]).
+template <int TC, int TP, int WC, int WP, int EP, bool PM = false, bool PB = false>
 __device__ __forceinline__ void glds_epilogue_fast(const IgemmArgs& a, f32x4_t (&acc)[TC][TP], int M, int m0, int c0,
-                                                   int wc, int wp, int lane) {
+                                                   int wc, int wp, int lane, const u32x2_t* pmk = nullptr,
+                                                   const float* pbias = nullptr) {
   static_assert(EP == 1 || EP == 2 || EP == 3, "fast epilogue kinds");
+  static_assert(!PM || EP == 2, "preloaded masks: EP 2");
   const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc((void*)a.y, 0, 0x7fffffff, 0x00020000);
   const __amdgpu_buffer_rsrc_t mr = __builtin_amdgcn_make_buffer_rsrc((void*)(EP == 2 ? a.mask : a.y), 0, 0x7fffffff, 0x00020000);
   const __amdgpu_buffer_rsrc_t y2r = __builtin_amdgcn_make_buffer_rsrc((void*)(EP == 3 ? a.y2 : a.y), 0, 0x7fffffff, 0x00020000);
@@ -135,7 +140,12 @@ __device__ __forceinline__ void glds_epilogue_fast(const IgemmArgs& a, f32x4_t (
   for (int ic = 0; ic < TC; ++ic)
 #pragma unroll
     for (int e = 0; e < 4; ++e) bias[ic][e] = 0.f;
-  if (EP == 1 && a.bias) {
+  if constexpr (PB) {
+#pragma unroll
+    for (int ic = 0; ic < TC; ++ic)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) bias[ic][e] = pbias[ic * 4 + e];
+  } else if (EP == 1 && a.bias) {
 #pragma unroll
     for (int ic = 0; ic < TC; ++ic)
 #pragma unroll
@@ -148,7 +158,10 @@ __device__ __forceinline__ void glds_epilogue_fast(const IgemmArgs& a, f32x4_t (
     const unsigned yo = ok ? (unsigned)m * (unsigned)a.ldy * 2u + (unsigned)cb * 2u : 0x80000000u;
     const unsigned yo2 = EP == 3 ? (unsigned)m * (unsigned)a.ldy2 * 2u : 0u;
     u32x2_t mk[TC];
-    if constexpr (EP == 2) {
+    if constexpr (PM) {
+#pragma unroll
+      for (int ic = 0; ic < TC; ++ic) mk[ic] = pmk[ip * TC + ic];
+    } else if constexpr (EP == 2) {
       const unsigned mo = ok ? (unsigned)m * (unsigned)a.ldm * 2u + (unsigned)cb * 2u : 0x80000000u;
 #pragma unroll
       for (int ic = 0; ic < TC; ++ic) mk[ic] = __builtin_amdgcn_raw_buffer_load_b64(mr, mo + ic * 32, 0, 0);
@@ -1358,6 +1371,29 @@ __global__ __launch_bounds__(512) void igemm_pp2h_kernel(IgemmArgs a) {
 #pragma unroll
     for (int ip = 0; ip < TP; ++ip) acc[ic][ip] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
+  // 128-channel dgrad: the ReLU-mask fragments of the epilogue (32 VGPRs) are loaded before the first
+  // DMA; they are older than every staged unit, so the constant waits below are unchanged
+  constexpr bool PM = EP == 2 && BC == 128 && !BNS;
+  constexpr bool PB = EP == 1 && BC == 128 && !BNS;   // likewise the forward bias (16 VGPRs)
+  float pbias[PB ? TC * 4 : 1];
+  if constexpr (PB) {
+    const int cb = c0 + wc * WC + 4 * (lane >> 4);
+#pragma unroll
+    for (int k = 0; k < TC * 4; ++k) pbias[k] = a.bias ? a.bias[cb + (k >> 2) * 16 + (k & 3)] : 0.f;
+  }
+  u32x2_t pmk[PM ? TP * TC : 1];
+  if constexpr (PM) {
+    const __amdgpu_buffer_rsrc_t mr = __builtin_amdgcn_make_buffer_rsrc((void*)a.mask, 0, 0x7fffffff, 0x00020000);
+    const int cb = c0 + wc * WC + 4 * (lane >> 4);
+#pragma unroll
+    for (int ip = 0; ip < TP; ++ip) {
+      const int m = m0 + wp * WP + ip * 16 + (lane & 15);
+      const unsigned mo = m < M ? (unsigned)m * (unsigned)a.ldm * 2u + (unsigned)cb * 2u : 0x80000000u;
+#pragma unroll
+      for (int ic = 0; ic < TC; ++ic) pmk[ip * TC + ic] = __builtin_amdgcn_raw_buffer_load_b64(mr, mo + ic * 32, 0, 0);
+    }
+  }
+
   // prologue: weights of K-tiles 0 (both halves) and 1 (half 0), pixel blocks of group 0
   const KC k0{0, 0};
   KC kA1 = knext(k0);                          // K-tile s+1 (A1 issue at p1 of s)
@@ -1544,6 +1580,8 @@ __global__ __launch_bounds__(512) void igemm_pp2h_kernel(IgemmArgs a) {
   if constexpr (BNS)
     glds_epilogue_bns<TC, TP, WC, WP, EP>(a, acc, M, m0, c0, wc, wp, lane,
                                           reinterpret_cast<float*>(Bimg + ((((G - 1) & 1) ^ 1) * 2) * BHALF));
+  else if constexpr (PM) glds_epilogue_fast<TC, TP, WC, WP, EP, true>(a, acc, M, m0, c0, wc, wp, lane, pmk);
+  else if constexpr (PB) glds_epilogue_fast<TC, TP, WC, WP, EP, false, true>(a, acc, M, m0, c0, wc, wp, lane, nullptr, pbias);
   else if constexpr (EP != 0) glds_epilogue_fast<TC, TP, WC, WP, EP>(a, acc, M, m0, c0, wc, wp, lane);
   else glds_epilogue<TC, TP, WC, WP>(a, acc, M, m0, c0, wc, wp, lane);
 }
