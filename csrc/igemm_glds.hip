@@ -1666,6 +1666,12 @@ DPA_API int dpa_igemm_glds(const IgemmArgs* args, int cfg, hipStream_t st) {
     // 1.38 vs 1.18 PF on a plain 8192^3 GEMM (profiles/kbench_glds_pp2_b256_r03.txt)
     if (a.Ngemm % 256 == 0 && grid_of(256, 256) >= 512)
       cfg = (a.Kpad <= 8 * 64 && !(a.korder & 2)) ? 8 : (no_pp ? 3 : 14);
+    // small grids (pipeline microbatches, small batches): the 128-channel row-block kernel when its
+    // 128 x 256 tiles still fill every CU once -- it replaces the 3-stage 128 x 256 kernel (cfg 2) and,
+    // at 256..511 of its tiles, the 128 x 128 one (cfg 4: twice the tiles at lower efficiency)
+    else if (a.Ngemm % 128 == 0 && grid_of(128, 256) >= 256 && !no_pp && !no_rowblock && !(a.korder & 1) &&
+             pp2h128_ok(a))
+      cfg = 15;
     else if (a.Ngemm % 128 == 0 && grid_of(128, 256) >= 512) cfg = 2;
     else if (a.Ngemm % 256 == 0 && grid_of(256, 128) >= 512) cfg = 1;
     else cfg = 4;
