@@ -10,6 +10,6 @@ run single --batch $B --steps 10 --warmup 3 &&
 run mp2ref --batch $B --steps 10 --warmup 3 --parallelism mp --stages 2 --microbatches ${MB:-8} &&
 run mp2bal --batch $B --steps 10 --warmup 3 --parallelism mp --stages 2 --microbatches ${MB:-8} --mp-cut balanced &&
 run mp2mb4 --batch $B --steps 10 --warmup 3 --parallelism mp --stages 2 --microbatches 4 &&
-run xl1 --model unet-xl --img 1024 --batch 16 --steps 5 --warmup 2 &&
-run xl8 --model unet-xl --img 1024 --batch 16 --steps 5 --warmup 2 --parallelism mp --stages 8 --microbatches 8 &&
-run xl8mb4 --model unet-xl --img 1024 --batch 16 --steps 5 --warmup 2 --parallelism mp --stages 8 --microbatches 4
+run xl1 --model unet-xl --img 1024 --batch 16 --steps 10 --warmup 4 &&
+run xl8 --model unet-xl --img 1024 --batch 16 --steps 10 --warmup 4 --parallelism mp --stages 8 --microbatches 8 &&
+run xl8mb4 --model unet-xl --img 1024 --batch 16 --steps 10 --warmup 4 --parallelism mp --stages 8 --microbatches 4
