@@ -585,6 +585,13 @@ def _wgrad_stream(A, B, *, grid, M, Nc, gw, gb, Nreal, tabs=None):
 # minimum workgroups of a fused backward launch (image column strips are split into row segments
 # below it); more segments = more fp32 weight-gradient slab rows to reduce
 BWD_BLOCKS = int(os.environ.get("DPA_BWD_BLOCKS", "1024"))
+# launches over fewer than BWD_SMALL_PIXELS output pixels (pipeline microbatches, small batches) aim at
+# BWD_BLOCKS_SMALL: each launch's slab rows are reduced separately, and at 1024 blocks per microbatch the
+# reductions read 8x the single-batch bytes (2 stages x 8 microbatches: 2690 -> 2760 img/s at 512,
+# 256 worse; profiles/knobs_r03_end.txt).  DPA_BWD_BLOCKS set explicitly applies to every launch.
+BWD_BLOCKS_SMALL = int(os.environ.get("DPA_BWD_BLOCKS_SMALL", "512"))
+BWD_SMALL_PIXELS = 1 << 25
+_BWD_BLOCKS_SET = "DPA_BWD_BLOCKS" in os.environ
 def _strips_ok(W: int, bp: int) -> bool:
     """Whole strips, or a ragged last one that keeps >= 85 % of the strip pixels useful."""
     t = -(-W // bp)
@@ -677,7 +684,9 @@ def conv_bwd_fused(g: Optional[torch.Tensor], x: torch.Tensor, wd: torch.Tensor,
     assert dx is None or tuple(dx.shape[:3]) == (N, H, W)
     strips = -(-W // bp.value)
     # whole image columns per block; split the rows only when the batch gives too few blocks
-    segs = max(1, min(H, -(-(target_blocks or BWD_BLOCKS) // max(1, N * strips))))
+    if not target_blocks:
+        target_blocks = BWD_BLOCKS if (_BWD_BLOCKS_SET or N * H * W >= BWD_SMALL_PIXELS) else BWD_BLOCKS_SMALL
+    segs = max(1, min(H, -(-target_blocks // max(1, N * strips))))
     rh = -(-H // segs)
     nblk = N * strips * (-(-H // rh))
     slab = torch.empty(nblk * pg * 9 * CO * CI + (nblk * pg * CO if gb is not None else 0), dtype=torch.float32,
