@@ -31,8 +31,8 @@ BASELINE_METRIC = "images/sec (whole node) UNet 512x512 bf16 at 1/2/4/8 MI355X; 
 STOCK_BASELINE_PER_GPU = 909.62
 STOCK_BASELINE_BATCH = 32
 # this framework at the SAME per-GPU batch 32, same box and session as the stock run
-# (profiles/batch_sweep_r02.txt: 2383 img/s) -> the equal-batch ratio
-EQUAL_BATCH_RATIO_B32 = round(2383.24 / 909.62, 3)
+# (profiles/bench_b32_640x960_r03_end.txt: 2680 img/s; round 2: 2383) -> the equal-batch ratio
+EQUAL_BATCH_RATIO_B32 = round(2679.87 / 909.62, 3)
 
 
 def _hw(s: str):
