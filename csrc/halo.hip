@@ -258,6 +258,12 @@ static int launch_igemm_halo(const IgemmArgs& a, hipStream_t st) {
 // 8 / 9 / 10: cfg 4 / 5 / 7 with DPP-shifted pixel fragments (one LDS read per kernel row)
 // a row of W pixels in tiles of bp: whole tiles, or a partial last tile that keeps >= 85 % of the
 // tile pixels useful (640x960: widths 960 / 480 / 240 / 120 in 128-pixel tiles are 94 % useful)
+// the per-image buffer binding (IgemmArgs::ximg) must cover one whole image of x: a short extent would
+// read zeros past it instead of failing
+static bool ximg_ok(const IgemmArgs& a) {
+  return (long)a.ximg >= ((long)a.Hs * a.Ws - 1) * a.ldx * 2 + (long)a.Cs * 2;
+}
+
 static bool tiles_ok(int W, int bp) {
   const int t = (W + bp - 1) / bp;
   return W >= 16 && (W % bp == 0 || W * 100 >= 85 * t * bp);
@@ -266,7 +272,7 @@ static bool tiles_ok(int W, int bp) {
 DPA_API int dpa_igemm_halo(const IgemmArgs* args, int cfg, hipStream_t st) {
   const IgemmArgs& a = *args;
   if (a.mode != 0 || a.KH != 3 || a.KW != 3 || a.stride != 1 || a.pad != 1 || (a.Cs % 32) || (a.ldx & 7) ||
-      (a.ldy & 3) || a.Hs != a.Ho || a.Ws != a.Wo || a.Kpad < 9 * a.Cs)
+      (a.ldy & 3) || a.Hs != a.Ho || a.Ws != a.Wo || a.Kpad < 9 * a.Cs || !ximg_ok(a))
     return (int)hipErrorInvalidValue;
   if (cfg == 0) {
     if (a.Ngemm == 32 && tiles_ok(a.Wo, 256)) cfg = 1;
@@ -983,7 +989,7 @@ DPA_API int dpa_igemm_stream(const IgemmArgs* args, int variant, hipStream_t st)
   // any row width: a partial last strip masks its out-of-row pixels (loads read zeros, stores are
   // dropped); the fused pool needs whole 2x2 windows along the row (even width)
   if (a.mode != 0 || a.KH != 3 || a.KW != 3 || a.stride != 1 || a.pad != 1 || (a.ldx & 7) || (a.ldy & 3) ||
-      a.Hs != a.Ho || a.Ws != a.Wo || a.Wo < 16 || a.Kpad < 9 * a.Cs ||
+      a.Hs != a.Ho || a.Ws != a.Wo || a.Wo < 16 || a.Kpad < 9 * a.Cs || !ximg_ok(a) ||
       (a.pool && ((a.ldp & 3) || (a.Wo & 1) || !a.relu)))
     return (int)hipErrorInvalidValue;
   if (a.Cs == 8 && a.Ngemm == 32 && !a.pool) return launch_igemm_stream8<128, 32>(a, st);

@@ -395,7 +395,8 @@ __global__ __launch_bounds__(512) void wgrad_gemm_kernel(WgradArgs a) {
 
 // Eligible: conv3x3 s1 p1 (A = the output gradient, B = the layer input, same pixel grid), M % 256 == 0,
 // Nc % 8 == 0, W % 64 == 0 or W == 32, H * W % 64 == 0, 16-B aligned channel strides; with per-image
-// tables every split's images must be consecutive images of one tensor (host); pix_per_split = images per split (splits = ceil(N / ips)), >= 2 K-steps per split,
+// tables every split's images must be consecutive images of one tensor (host); pix_per_split = images per split (splits = ceil(N / ips)), >= 2 K-steps per split
+// (the ragged last split included: the steady loop and its peeled tail need S >= 2),
 // each split's images addressable with 32-bit offsets (abytes / bbytes = ips images).
 DPA_API int dpa_wgrad_gemm(const WgradArgs* args, hipStream_t st) {
   const WgradArgs& a = *args;
@@ -403,7 +404,8 @@ DPA_API int dpa_wgrad_gemm(const WgradArgs* args, hipStream_t st) {
   if ((a.M % 256) || (a.Nc % 8) || (a.lda & 7) || (a.ldb & 7) || a.s != 1 || a.pad != 1 || a.KW != 3 ||
       a.HA != a.Hg || a.WA != a.Wg || a.HB != a.Hg || a.WB != a.Wg || (a.Wg % 64 && a.Wg != 32) ||
       ((a.Hg * a.Wg) % 64) || (!a.atab != !a.btab) || ips < 1 || a.splits != (a.N + ips - 1) / ips ||
-      (long)ips * a.Hg * a.Wg / 64 < 2 || a.lda < a.M || a.ldb < a.Nc ||
+      (long)ips * a.Hg * a.Wg / 64 < 2 || (long)((a.N - 1) % ips + 1) * a.Hg * a.Wg / 64 < 2 ||
+      a.lda < a.M || a.ldb < a.Nc ||
       (long)ips * a.Hg * a.Wg * a.lda * 2 > (long)a.abytes || (long)ips * a.Hg * a.Wg * a.ldb * 2 > (long)a.bbytes)
     return (int)hipErrorInvalidValue;
   const int tiles = (a.M / 256) * ((9 * a.Nc + 255) / 256);

@@ -45,6 +45,8 @@ class TrainConfig:
     mp_cut: str = "auto"                             # MP stage cut: reference | balanced | auto (reference iff 2 stages)
     bucket_mb: float = 8.0                           # DDP/DP all-reduce bucket size (MiB of fp32 grads)
     grad_comm_dtype: str = "fp32"                    # DDP gradient all-reduce wire dtype: fp32 | bf16
+    comm_overlap: bool = True                        # DDP/DP: launch gradient buckets during the backward
+                                                     # (False: all buckets after it, no CU sharing with RCCL)
     global_dice: bool = False                        # DDP: Dice over the global batch (all-reduced sums)
     loss_scale_by_batch: bool = True                 # reference multiplies loss by batch size (A11)
     max_steps: int = 0                               # stop after N optimizer steps (0 = full epochs)
@@ -103,6 +105,9 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--bucket-mb", type=float, default=8.0)
     p.add_argument("--grad-comm-dtype", choices=["fp32", "bf16"], default="fp32",
                    help="DDP: all-reduce gradient buckets in bf16 (half the bytes) instead of fp32")
+    p.add_argument("--no-comm-overlap", dest="comm_overlap", action="store_false",
+                   help="DDP/DP: all-reduce the gradient buckets after the backward instead of during it "
+                        "(RCCL kernels then never share CUs with the backward's kernels)")
     p.add_argument("--global-dice", action="store_true")
     p.add_argument("--no-batch-loss-scale", dest="loss_scale_by_batch", action="store_false")
     p.add_argument("--max-steps", type=int, default=0)
@@ -136,7 +141,8 @@ def parse_args(argv=None) -> TrainConfig:
         batch_size=a.batch_size, checkpoint=a.checkpoint, seed=a.seed, img_size=img_size,
         dtype=a.dtype, backend=a.backend, model=a.model, synthetic=a.synthetic,
         synthetic_len=a.synthetic_len, device_data=a.device_data, data_dir=a.data_dir, out_dir=a.out_dir, device=a.device,
-        stages=a.stages, microbatches=a.microbatches, mp_cut=a.mp_cut, bucket_mb=a.bucket_mb, grad_comm_dtype=a.grad_comm_dtype, global_dice=a.global_dice,
+        stages=a.stages, microbatches=a.microbatches, mp_cut=a.mp_cut, bucket_mb=a.bucket_mb, grad_comm_dtype=a.grad_comm_dtype,
+        comm_overlap=a.comm_overlap, global_dice=a.global_dice,
         loss_scale_by_batch=a.loss_scale_by_batch, max_steps=a.max_steps, num_workers=a.num_workers,
         log_every=a.log_every, resume=a.resume, profile=a.profile, trace_ranges=a.trace_ranges, cuda_graph=a.cuda_graph,
         debug_sync=a.debug_sync, watchdog=a.watchdog, comm_timeout=a.comm_timeout, nan_policy=a.nan_policy, progress=a.progress)

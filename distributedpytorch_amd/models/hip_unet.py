@@ -148,7 +148,12 @@ class HipBlocks:
         self._deferred_ready = []
         self._flush_queued = False
         self.side2 = None             # stream of the merged (all-microbatch) weight-gradient launches
-        self._keep2 = []
+        self._keep2 = []              # (event after the launch, its operands): released once the event is done
+        # memory bound of the deferral: a layer's deferred gradients and inputs stay alive
+        # until its merged launch, so when the not-yet-launched operands of all layers exceed this many
+        # bytes, the layer that crossed it launches over the microbatches it has (a partial merge)
+        self.defer_cap_bytes = 8 << 30
+        self._deferred_bytes = 0
 
     # ------------------------------------------------------------------ weight packing
     def _build_packing(self):
@@ -282,7 +287,7 @@ class HipBlocks:
         # a persistent GEMM grid assumes it owns every CU; with side-stream weight gradients in flight
         # it would wait for them (profiles/hip_b256_512_timeline_r02_end.txt: 3.0-3.3 ms vs 0.4-0.8 alone)
         K.igemm(g, self.wd(c), out, Ngemm=c.Cin, Kpad=c.Kd, KH=3, KW=3, stride=1, pad=1, Cs=c.Cout,
-                out_grid=(N, H, W), mask=mask, bn_stats=stats, persistent=not self._side_pending)
+                out_grid=(N, H, W), mask=mask, bn_stats=stats, persistent=not self._side_busy())
         return out if below is None else (out, stats)
 
     def conv_dgrad_split(self, c: _Conv, g: torch.Tensor, split: int):
@@ -293,8 +298,13 @@ class HipBlocks:
         lo = torch.empty(N, H, W, split, dtype=torch.bfloat16, device=g.device)
         hi = torch.empty(N, H, W, c.Cin - split, dtype=torch.bfloat16, device=g.device)
         K.igemm(g, self.wd(c), lo, Ngemm=c.Cin, Kpad=c.Kd, KH=3, KW=3, stride=1, pad=1, Cs=c.Cout,
-                out_grid=(N, H, W), y2=hi, split=split, persistent=not self._side_pending)
+                out_grid=(N, H, W), y2=hi, split=split, persistent=not self._side_busy())
         return lo, hi
+
+    def _side_busy(self) -> bool:
+        """Weight gradients may be in flight on a side stream: the per-block one, or the merged
+        (all-microbatch) launches of a pipeline stage on ``side2`` (held in ``_keep2`` until flushed)."""
+        return self._side_pending or bool(self._keep2)
 
     def _side_launch(self, fn, *keep: torch.Tensor):
         """Run ``fn`` (a weight-gradient launch reading ``keep``) on the side stream when there is one:
@@ -318,9 +328,8 @@ class HipBlocks:
         BatchNorm after the conv (its backward formed on load) or below it (its statistics from the dx
         epilogue) needs the plain modes (:meth:`bwd_conv`); the pool / head folds (``whole``) do not
         combine with BatchNorm."""
-        bn_ok = K.USE_FUSED_BN_BWD and not whole
-        if not (K.USE_FUSED_BWD and (c.bn is None or bn_ok) and (below is None or below.bn is None or bn_ok)
-                and c.Cs == c.Cin):
+        if not (K.USE_FUSED_BWD and bn_combo_ok(c.bn is not None, None if below is None else below.bn is not None,
+                                                K.USE_FUSED_BN_BWD and not whole) and c.Cs == c.Cin):
             return False
         key = (c.Cin, c.Cout, W, whole)
         ok = self._fusable.get(key)
@@ -405,12 +414,16 @@ class HipBlocks:
     def conv_wgrad(self, c: _Conv, g: torch.Tensor, x: torch.Tensor):
         N, H, W = g.shape[:3]
         if self.defer_wgrad > 1 and K.wgrad_multi_eligible(c.Cout, c.Cs, W):
+            self._release_done()
             ent = self._deferred.setdefault(id(c), (c, [], []))
             ent[1].append(g)
             ent[2].append(x)
-            if len(ent[1]) >= self.defer_wgrad:
-                # every microbatch of this layer is in: launch now, so it overlaps the rest of the backward
+            self._deferred_bytes += _nbytes(g) + _nbytes(x)
+            if len(ent[1]) >= self.defer_wgrad or self._deferred_bytes > self.defer_cap_bytes:
+                # every microbatch of this layer is in (or the deferral hit its memory cap): launch now,
+                # so it overlaps the rest of the backward
                 del self._deferred[id(c)]
+                self._deferred_bytes -= sum(_nbytes(t) for t in ent[1] + ent[2])
                 self._launch_multi(c, ent[1], ent[2])
             if not self._defer_window and not self._flush_queued:
                 # end of this backward: leftovers, the merged stream's join, the readiness announcements
@@ -454,7 +467,7 @@ class HipBlocks:
                     out_grid=(N, h, w), mask=x)
             return dx
         K.igemm(gup, self.wd(d), dx, Ngemm=d.Cin, Kpad=d.Kd, KH=2, KW=2, stride=2, pad=0, Cs=d.Cout,
-                out_grid=(N, h, w), mask=x, persistent=not self._side_pending)
+                out_grid=(N, h, w), mask=x, persistent=not self._side_busy())
         return dx
 
     def deconv_wgrad(self, d: _Deconv, gup: torch.Tensor, x: torch.Tensor):
@@ -502,14 +515,23 @@ class HipBlocks:
         self.side2.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(self.side2):
             K.wgrad_multi(gs, xs, M=c.Cout, Nc=c.Cs, gw=gw.view(-1), gb=gb, Nreal=c.Cin)
-        self._keep2.extend(gs)
-        self._keep2.extend(xs)
+            ev = torch.cuda.Event()
+            ev.record(self.side2)
+        self._keep2.append((ev, list(gs) + list(xs)))
+
+    def _release_done(self):
+        """Drop the operands of merged weight-gradient launches that have finished (an event query, no
+        sync): their memory returns to the caching allocator during the backward instead of at
+        flush_wgrad.  Safe without record_stream: the kernel reading them is complete."""
+        while self._keep2 and self._keep2[0][0].query():
+            self._keep2.pop(0)
 
     def flush_wgrad(self):
         """Run the deferred weight gradients still waiting for microbatches (one launch per layer over
         the ones that arrived), join the side stream, announce the gradients."""
         self._flush_queued = False
         deferred, self._deferred = self._deferred, {}
+        self._deferred_bytes = 0
         for c, gs, xs in deferred.values():
             self._launch_multi(c, gs, xs)
         if self._keep2:
@@ -587,6 +609,20 @@ class HipBlocks:
         return cat
 
 
+def bn_combo_ok(conv_bn: bool, below_bn, bn_fusable: bool) -> bool:
+    """BatchNorm combinations the fused backward kernel (csrc/bwd_stream.hip) implements.  ``below_bn``
+    is None when the dx is not ReLU-masked by a layer below (no ``below``), else whether that layer has a
+    BatchNorm.  Without BN anywhere: always.  With BN: only when fusing it is allowed and, for a masked dx,
+    the conv and the layer below agree -- the kernel's BN modes pair the loader's BN backward (this conv)
+    with the dx epilogue's BN partial sums (the layer below); a BN on one side only has no instantiation
+    (mixed models must take the unfused path, not fail an assert / InvalidValue)."""
+    if not conv_bn and not below_bn:
+        return True
+    if not bn_fusable:
+        return False
+    return below_bn is None or below_bn == conv_bn
+
+
 def _v(t: torch.Tensor) -> torch.Tensor:
     """logical-NCHW channels_last -> NHWC view (copies only if the layout is something else)."""
     if t.dim() == 4 and t.stride(1) != 1:
@@ -597,6 +633,10 @@ def _v(t: torch.Tensor) -> torch.Tensor:
 def _o(t: torch.Tensor) -> torch.Tensor:
     """NHWC -> logical-NCHW view (channels_last strides)."""
     return t.permute(0, 3, 1, 2)
+
+
+def _nbytes(t: torch.Tensor) -> int:
+    return t.numel() * t.element_size()
 
 
 def _grad(p: torch.nn.Parameter) -> torch.Tensor:

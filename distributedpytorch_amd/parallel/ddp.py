@@ -19,6 +19,9 @@ Design (MI355X-first, not a translation of torch's C++ Reducer):
   earlier buckets has been produced -> identical collective order on every rank (no deadlock even
   if autograd finishes parameters in a different order) and overlap with the rest of backward.
 * ``op=AVG`` on RCCL (ncclAvg) so no separate divide kernel; gloo (CPU tests) uses SUM + scale.
+* ``overlap=False`` (CLI ``--no-comm-overlap``): no launches during the backward; :meth:`finish`
+  all-reduces the whole flat buffer as ONE collective after it.  The fallback for when RCCL's
+  kernels sharing CUs with the one-workgroup-per-CU backward GEMMs costs more than the overlap gains.
 * Initial parameters are broadcast from rank 0 in one collective over the flat buffer
   (torch DDP's ``_sync_module_states``, N3).
 """
@@ -55,8 +58,10 @@ def bucket_plan(space: FlatParameterSpace, bucket_mb: float = 8.0, first_bucket_
 
 class BucketedAllReduce:
     def __init__(self, space: FlatParameterSpace, bucket_mb: float = 8.0, first_bucket_mb: float = 1.0,
-                 group=None, average: bool = True, scale: float = 1.0, comm_dtype: str = "fp32"):
+                 group=None, average: bool = True, scale: float = 1.0, comm_dtype: str = "fp32",
+                 overlap: bool = True):
         self.space = space
+        self.overlap = bool(overlap)
         # "bf16": each bucket travels as bf16 (half the xGMI bytes; torch's bf16_compress_hook
         # semantics: pre-scaled, reduced in bf16, written back into the fp32 flat buffer)
         assert comm_dtype in ("fp32", "bf16"), comm_dtype
@@ -66,7 +71,11 @@ class BucketedAllReduce:
         self.average = average
         self.scale = scale
         self.nccl = dist.get_backend(group) == "nccl"
-        self.buckets, self.bucket_of = bucket_plan(space, bucket_mb, first_bucket_mb)
+        if self.overlap:
+            self.buckets, self.bucket_of = bucket_plan(space, bucket_mb, first_bucket_mb)
+        else:   # one collective over the whole buffer, after the backward
+            n = len(space.numels)
+            self.buckets, self.bucket_of = [(0, space.offsets[-1], 0, n)], [0] * n
         self.expected = [b[3] - b[2] for b in self.buckets]
         self._hooks = []
         self.reset()
@@ -109,7 +118,7 @@ class BucketedAllReduce:
         self.n_ready += 1
         b = self.bucket_of[param_index]
         self.pending[b] -= 1
-        while self.next_launch < len(self.buckets) and self.pending[self.next_launch] == 0:
+        while self.overlap and self.next_launch < len(self.buckets) and self.pending[self.next_launch] == 0:
             self._launch(self.next_launch)
             self.next_launch += 1
 

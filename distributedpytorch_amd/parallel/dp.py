@@ -43,7 +43,7 @@ from .ddp import bucket_plan
 
 class ReplicatedDataParallel:
     def __init__(self, model: torch.nn.Module, devices: Sequence, backend: str = "auto", dtype: str = "bf16",
-                 bucket_mb: float = 8.0):
+                 bucket_mb: float = 8.0, overlap: bool = True):
         self.devices = [torch.device(d) for d in devices]
         assert len(self.devices) >= 1
         self.replicas: List[torch.nn.Module] = []
@@ -63,7 +63,7 @@ class ReplicatedDataParallel:
                 self.comm.broadcast([s.data for s in self.spaces], root=0)
                 for s in self.spaces:
                     s.touch()
-        self.reducer = DPBucketReducer(self.spaces, self.devices, self.comm, bucket_mb) \
+        self.reducer = DPBucketReducer(self.spaces, self.devices, self.comm, bucket_mb, overlap=overlap) \
             if len(self.devices) > 1 else None
 
     # ------------------------------------------------------------------ forward
@@ -155,11 +155,11 @@ class DPBucketReducer:
     stream and records the exposed (un-overlapped) wait on device 0."""
 
     def __init__(self, spaces, devices, comm=None, bucket_mb: float = 8.0, first_bucket_mb: float = 1.0,
-                 overlap: bool = None):
+                 overlap: bool = True):
         self.spaces, self.devices, self.comm = list(spaces), list(devices), comm
-        # DPA_DP_OVERLAP=0: opt-out to ONE reduction of the whole gradient buffer after the backward
-        # (no bucket launches from the autograd device threads)
-        self.overlap = os.environ.get("DPA_DP_OVERLAP", "1") == "1" if overlap is None else overlap
+        # overlap=False (``--no-comm-overlap``): ONE reduction of the whole gradient buffer after the
+        # backward (no bucket launches from the autograd device threads)
+        self.overlap = bool(overlap)
         if self.overlap:
             self.buckets, self.bucket_of = bucket_plan(self.spaces[0], bucket_mb, first_bucket_mb)
         else:

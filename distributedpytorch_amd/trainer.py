@@ -145,7 +145,8 @@ class DDPStrategy(SingleDevice):
         broadcast_parameters(self.space, src=0)
         scale = float(self.world) if cfg.global_dice else 1.0
         self.reducer = BucketedAllReduce(self.space, bucket_mb=cfg.bucket_mb, scale=scale,
-                                         comm_dtype=cfg.grad_comm_dtype).register_hooks()
+                                         comm_dtype=cfg.grad_comm_dtype,
+                                         overlap=cfg.comm_overlap).register_hooks()
 
     def lr_scale(self):
         # reference: Adam(lr * world_size) (utils/train_utils.py:199) - with the real world size (A6)
@@ -203,7 +204,8 @@ class DPStrategy(Strategy):
 
     def __init__(self, cfg, model, devices):
         super().__init__(cfg)
-        self.dp = ReplicatedDataParallel(model, devices, cfg.backend, cfg.dtype, bucket_mb=cfg.bucket_mb)
+        self.dp = ReplicatedDataParallel(model, devices, cfg.backend, cfg.dtype, bucket_mb=cfg.bucket_mb,
+                                         overlap=cfg.comm_overlap)
         self.reducer = self.dp.reducer
         self.device = self.dp.devices[0]
         self.model = self.dp.module

@@ -307,17 +307,17 @@ def test_reducers_reject_double_announcement():
         red.mark_ready(0)
 
 
-def test_dp_single_reduction_opt_out(monkeypatch):
-    """DPA_DP_OVERLAP=0: one reduction of the whole buffer at the end of the backward, same result."""
+def test_dp_single_reduction_opt_out():
+    """--no-comm-overlap: one reduction of the whole buffer at the end of the backward, same result."""
     from distributedpytorch_amd.config import TrainConfig
     from distributedpytorch_amd.trainer import DPStrategy
-    monkeypatch.setenv("DPA_DP_OVERLAP", "0")
     torch.manual_seed(3)
     a, b = build_model("unet-tiny"), build_model("unet-tiny")
     b.load_state_dict(a.state_dict())
     x = torch.rand(4, 3, 32, 32)
     t = (torch.rand(4, 1, 32, 32) > 0.5).float()
-    st = DPStrategy(TrainConfig(backend="torch", lr=1e-3, dtype="fp32", bucket_mb=0.002), a, ["cpu", "cpu"])
+    st = DPStrategy(TrainConfig(backend="torch", lr=1e-3, dtype="fp32", bucket_mb=0.002, comm_overlap=False),
+                    a, ["cpu", "cpu"])
     red = st.dp.reducer
     assert len(red.buckets) == 1
     st.optimizer.zero_grad()

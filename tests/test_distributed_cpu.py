@@ -40,7 +40,7 @@ def _data(n, seed, hw=32):
     return x, t
 
 
-def _ddp_worker(rank, world, port, bucket_mb, q, comm="fp32"):
+def _ddp_worker(rank, world, port, bucket_mb, q, comm="fp32", overlap=True):
     _init(rank, world, port)
     from distributedpytorch_amd.config import TrainConfig
     from distributedpytorch_amd.trainer import DDPStrategy
@@ -49,7 +49,7 @@ def _ddp_worker(rank, world, port, bucket_mb, q, comm="fp32"):
         for p in model.parameters():
             p.data.add_(1.0)
     cfg = TrainConfig(train_method="DDP", backend="torch", dtype="fp32", lr=1e-3, bucket_mb=bucket_mb,
-                      grad_comm_dtype=comm)
+                      grad_comm_dtype=comm, comm_overlap=overlap)
     st = DDPStrategy(cfg, model, "cpu")
     x, t = _data(4, seed=10 + rank)
     # expected: per-rank plain-autograd grads of the (broadcast) rank-0 weights, averaged
@@ -64,6 +64,7 @@ def _ddp_worker(rank, world, port, bucket_mb, q, comm="fp32"):
     st.optimizer.zero_grad()
     loss = st.forward_loss(x, t)
     (loss * x.shape[0]).backward()      # buckets are all-reduced in place, overlapped with backward
+    launched_in_backward = len(st.reducer.launch_log)
     st.reducer.finish()
     if comm == "bf16":   # bf16 wire: relative error of a few bf16 ulps
         ok_reduce = torch.allclose(st.space.grad, expect, rtol=2e-2, atol=1e-4 * float(expect.abs().max()))
@@ -84,28 +85,32 @@ def _ddp_worker(rank, world, port, bucket_mb, q, comm="fp32"):
     lr = torch.tensor([st.optimizer.param_groups[0]["lr"]])
     alllr = [torch.zeros_like(lr) for _ in range(world)]
     dist.all_gather(alllr, lr)
-    q.put((rank, ok_reduce, same, [float(v) for v in alllr], len(st.reducer.buckets)))
+    q.put((rank, ok_reduce, same, [float(v) for v in alllr], len(st.reducer.buckets), launched_in_backward))
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,bucket_mb,comm", [(2, 0.001, "fp32"), (2, 8.0, "fp32"), (4, 0.004, "fp32"),
-                                                  (2, 0.004, "bf16")])
-def test_ddp_gloo_ranks(world, bucket_mb, comm):
+@pytest.mark.parametrize("world,bucket_mb,comm,overlap", [(2, 0.001, "fp32", True), (2, 8.0, "fp32", True),
+                                                          (4, 0.004, "fp32", True), (2, 0.004, "bf16", True),
+                                                          (2, 0.001, "fp32", False)])
+def test_ddp_gloo_ranks(world, bucket_mb, comm, overlap):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_ddp_worker, args=(r, world, port, bucket_mb, q, comm)) for r in range(world)]
+    procs = [ctx.Process(target=_ddp_worker, args=(r, world, port, bucket_mb, q, comm, overlap))
+             for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=240) for _ in procs]
     for p in procs:
         p.join(timeout=60)
-    for rank, ok_reduce, same, lrs, nb in res:
+    for rank, ok_reduce, same, lrs, nb, in_bwd in res:
         assert ok_reduce, f"rank {rank}: bucketed all-reduce != mean of grads"
         assert same, "replicas diverged"
         assert len(set(lrs)) == 1, f"scheduler diverged across ranks: {lrs}"
-        if bucket_mb < 0.01:
-            assert nb > 3
+        if not overlap:   # --no-comm-overlap: one collective, launched after the backward
+            assert nb == 1 and in_bwd == 0
+        elif bucket_mb < 0.01:
+            assert nb > 3 and in_bwd >= nb - 1
 
 
 def _pipe_worker(rank, world, port, microbatches, mode, q):

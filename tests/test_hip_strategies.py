@@ -207,7 +207,8 @@ def test_bench_json_contract(hip_lib, extra):
     assert out["scaling"] == ("strong" if "mp" in extra else "weak")
 
 
-@pytest.mark.parametrize("extra", [[], ["--grad-comm-dtype", "bf16"], ["--parallelism", "mp", "--microbatches", "2"]])
+@pytest.mark.parametrize("extra", [[], ["--grad-comm-dtype", "bf16"], ["--no-comm-overlap"],
+                                   ["--parallelism", "mp", "--microbatches", "2"]])
 def test_bench_two_ranks_same_device(hip_lib, extra):
     """Rehearsal of the multi-rank bench path on one GPU: torchrun with 2 ranks sharing cuda:0 over
     gloo (DPA_SAME_DEVICE=1) - DDP bucketed all-reduce of HIP-engine gradients, and GPipe send/recv of
@@ -234,8 +235,13 @@ def test_bench_two_ranks_same_device(hip_lib, extra):
     mp_run = "mp" in extra
     assert out["config"]["global_batch"] == (4 if mp_run else 8)
     assert out["final_loss"] is not None and out["final_loss"] == out["final_loss"]
-    if not mp_run:  # DDP: the reducer timed the stall on outstanding all-reduce buckets
+    assert out["rccl_world"]["world_size"] == 2 and out["rccl_world"]["backend"] == "gloo"
+    rm = out["rank_ms_per_step"]
+    assert len(rm["per_rank"]) == 2 and 0 < rm["min"] <= rm["max"]
+    assert out["config"]["comm_overlap"] == ("--no-comm-overlap" not in extra)
+    if not mp_run:  # DDP: the reducer timed the stall on outstanding all-reduce buckets, on every rank
         assert out["exposed_comm_ms_last_step"] is not None and out["exposed_comm_ms_last_step"] >= 0
+        assert 0 <= out["exposed_comm_ms"]["min"] <= out["exposed_comm_ms"]["max"]
 
 
 def test_dp_bucket_reducer_native_clique(hip_lib):

@@ -29,7 +29,7 @@ def _igemm_args(**kw):
     from distributedpytorch_amd.ops import kernels as K
     a = K.IgemmArgs()
     base = dict(ldx=32, ldy=32, N=1, Ho=64, Wo=64, Hs=64, Ws=64, Cs=32, KH=3, KW=3, stride=1, pad=1, Ngemm=32,
-                Kpad=288, mode=0)
+                Kpad=288, mode=0, ximg=64 * 64 * 32 * 2)
     base.update(kw)
     for k, v in base.items():
         setattr(a, k, v)
@@ -85,7 +85,8 @@ def test_glds_bn_sums_refuse_other_shapes(L, kw):
 
 
 @pytest.mark.parametrize("kw", [dict(mode=1), dict(KH=1, KW=1), dict(stride=2), dict(Cs=48, Kpad=448),
-                                dict(Hs=66), dict(Kpad=256), dict(Wo=96, Ws=96)])
+                                dict(Hs=66), dict(Kpad=256), dict(Wo=96, Ws=96), dict(ximg=0),
+                                dict(ximg=64 * 64 * 32 * 2 - 66)])
 def test_halo_igemm_rejects(L, kw):
     assert L.dpa_igemm_halo(ctypes.byref(_igemm_args(**kw)), 0, None) == INVALID
 
@@ -93,7 +94,7 @@ def test_halo_igemm_rejects(L, kw):
 # any row width >= 16 streams (a ragged last strip is masked); narrower rows and a fused pool over an
 # odd width (half a 2x2 window) are rejected
 @pytest.mark.parametrize("kw", [dict(Wo=8, Ws=8), dict(mode=1), dict(pad=0), dict(Kpad=256), dict(Ngemm=128, Kpad=288),
-                                dict(Wo=97, Ws=97, pool=16, ldp=32)])
+                                dict(Wo=97, Ws=97, pool=16, ldp=32), dict(ximg=0), dict(ximg=64 * 64 * 32 * 2 - 66)])
 def test_stream_igemm_rejects(L, kw):
     assert L.dpa_igemm_stream(ctypes.byref(_igemm_args(**kw)), 0, None) == INVALID
 
@@ -125,10 +126,13 @@ def test_wgrad_stream_checks_split_count(L):
 
 @pytest.mark.parametrize("kw", [dict(M=128), dict(Nc=36), dict(Wg=96, WA=96, WB=96), dict(Hg=3, HA=3, HB=3, Wg=32, WA=32, WB=32),
                                 dict(KW=2), dict(HB=32), dict(splits=2), dict(pix_per_split=0), dict(lda=36),
-                                dict(abytes=1024), dict(N=1, Hg=1, HA=1, HB=1)])
+                                dict(abytes=1024), dict(N=1, Hg=1, HA=1, HB=1),
+                                dict(N=3, pix_per_split=2, splits=2, Hg=1, HA=1, HB=1, abytes=2 * 64 * 256 * 2,
+                                     bbytes=2 * 64 * 64 * 2)])
 def test_wgrad_gemm_rejects(L, kw):
     """csrc/wgrad_gemm.hip: M % 256, Nc % 8, W % 64 or 32, H*W % 64, 3x3 s1 p1 on one grid, split count =
-    ceil(N / images per split), 16-B strides, >= 2 K-steps per split, 32-bit split extents."""
+    ceil(N / images per split), 16-B strides, >= 2 K-steps per split (the ragged last one too: 3 one-row
+    images of 64 pixels in splits of 2 leave the last split ONE K-step), 32-bit split extents."""
     base = dict(M=256, Nc=64, lda=256, ldb=64, pix_per_split=1, splits=1,
                 abytes=64 * 64 * 256 * 2, bbytes=64 * 64 * 64 * 2)
     assert L.dpa_wgrad_gemm(ctypes.byref(_wgrad_args(**base)), None) != INVALID     # the valid case passes
@@ -183,3 +187,15 @@ def test_native_dp_comm_rejects_bad_args():
     assert L.dpa_dp_broadcast(None, None, ctypes.c_longlong(4), ctypes.c_int(0), ctypes.c_int(0), None) != 0
     assert L.dpa_dp_comm_size(None) == 0
     assert L.dpa_dp_version() > 0
+
+
+def test_fused_bwd_bn_combinations():
+    """HipBlocks.fusable's BatchNorm rule: the fused backward pairs the conv's BN backward
+    (loader) with the BN partial sums of the layer below (dx epilogue); a masked dx with BN on one side
+    only must take the unfused path instead of failing in the kernel host code."""
+    from distributedpytorch_amd.models.hip_unet import bn_combo_ok
+    assert bn_combo_ok(False, None, False) and bn_combo_ok(False, False, False)   # no BN anywhere
+    assert bn_combo_ok(True, True, True) and bn_combo_ok(True, None, True)        # BN both sides / unmasked dx
+    assert not bn_combo_ok(True, True, False) and not bn_combo_ok(True, None, False)   # BN fusion off
+    assert not bn_combo_ok(False, True, True)     # no BN here, BN below: no epilogue-only instantiation
+    assert not bn_combo_ok(True, False, True)     # BN here, plain layer below: no loader-only masked mode
