@@ -104,6 +104,9 @@ GLDS_NO_PRELOAD = os.environ.get("DPA_GLDS_NO_PRELOAD", "0") == "1"
 GLDS_NO_PP = os.environ.get("DPA_GLDS_NO_PP", "0") == "1"
 # A/B: the ping-pong kernel without row-block pixel staging (csrc/igemm_glds.hip igemm_pp2h_kernel)
 GLDS_NO_ROWBLOCK = os.environ.get("DPA_GLDS_NO_ROWBLOCK", "0") == "1"
+# row-block GEMMs with two MFMA phases per K-tile (csrc/igemm_glds.hip igemm_rb2_kernel, cfg 16 / 17)
+# instead of pp2h's four quadrant phases
+GLDS_RB2 = os.environ.get("DPA_GLDS_RB2", "0") == "1"
 # 128-channel convs on the row-block ping-pong GEMM (csrc/igemm_glds.hip cfg 15, igemm_pp2h_kernel<EP, 128>)
 # instead of the row-halo kernel: 10-15 % faster on every 128-output-channel 3x3 conv / dgrad of the 512^2
 # UNet (profiles/kbench_glds_rowblock128_b256_r03.txt); DPA_NO_GLDS128=1 disables (A/B)
@@ -311,13 +314,16 @@ def igemm(x: torch.Tensor, wpacked: torch.Tensor, y: torch.Tensor, *, Ngemm: int
         a = args(n0, n1, False)
         if gslab is not None:
             a.bnslab = gslab[n0 * Ho * Wo // 256 * 2 * Ngemm:].data_ptr()
-            if L.dpa_igemm_glds(ctypes.byref(a), c_int(0), st) == 0:
+            if L.dpa_igemm_glds(ctypes.byref(a), c_int(16384 * GLDS_RB2 if variant == 0 else variant), st) == 0:
                 continue
             assert n0 == 0, "row-block BN statistics refused after the first chunk"
             a.bnslab, gslab = None, None
         if path == "glds" or (path == "auto" and glds_ok):
             no_pers = GLDS_NO_PERS or not persistent
-            err = L.dpa_igemm_glds(ctypes.byref(a), c_int(variant if path == "glds" else 15 if rb128 else 16 * GLDS_TAP_MAJOR + 32 * no_pers + 64 * GLDS_NO_PRELOAD + 128 * GLDS_NO_PP + 8192 * GLDS_NO_ROWBLOCK), st)
+            auto_cfg = ((131072 if GLDS_RB2 else 15) if rb128 else
+                        16 * GLDS_TAP_MAJOR + 32 * no_pers + 64 * GLDS_NO_PRELOAD + 128 * GLDS_NO_PP +
+                        8192 * GLDS_NO_ROWBLOCK + 16384 * GLDS_RB2)
+            err = L.dpa_igemm_glds(ctypes.byref(a), c_int(variant if path == "glds" else auto_cfg), st)
             if err == 0:
                 continue
             if path == "glds":

@@ -1,0 +1,208 @@
+"""GPipe schedule model and time-balanced stage partitioner.
+
+The pipeline engine (:class:`.pipeline.GPipeDist`, reference ``model/unet_model.py:24-53`` generalised
+to S stages x M microbatches) runs ALL forwards, then ALL backwards: the loss is the reference's
+global Dice over the whole batch, so no microbatch's backward can start before every microbatch's
+forward has reached the head.  Its step time is therefore not the ideal ``M (F + B)`` of the slowest
+stage but a fill / drain schedule, and the stage boundaries that minimise it depend on measured
+per-block TIME, not FLOPs (the full-resolution levels run at ~0.6 PF on MI355X, the deep GEMMs at
+1.3-1.5 PF).  This module
+
+* simulates that schedule (:func:`simulate`) from per-stage costs: forward / backward per microbatch,
+  the deferred weight gradients (:class:`..models.hip_unet.HipBlocks` merges every microbatch's
+  weight gradient of a layer into one launch after the layer's last microbatch -- work that runs in
+  the drain, after the stage's last backward), and point-to-point transfer times of the boundary
+  tensors (x and the UNet skips go straight from producer to consumer stage over xGMI);
+* builds stage costs from a measured per-block time table (``tools/block_times.py`` on one GPU,
+  JSON in ``profiles/``) and a transfer model (:func:`stage_costs`);
+* searches every contiguous partition for the one with the smallest simulated step
+  (:func:`best_partition`) and the microbatch count that maximises throughput (:func:`plan`).
+
+Dependencies modelled (they are exactly GPipeDist.train_step's):
+  forward  (s, m): after (s, m-1) and after every producer stage p of s has finished (p, m) and its
+                   tensors arrived (x from s-1, each skip from the stage that ran its encoder level);
+  backward (s, m), m = M-1 .. 0: after (s, m+1) [for m = M-1: after the stage's last forward; the
+                   last stage also after the loss], and after every consumer stage c has finished
+                   backward (c, m) and its gradient arrived;
+  the stage ends after its last backward plus its deferred weight gradients (work-conserving: they
+  share the CUs with the last microbatch's dgrads, so they extend the stage by their own time);
+  the step ends when every stage has run its optimizer step.
+Communication is asynchronous (RCCL on its own streams) and does not delay the sender's compute.
+"""
+from __future__ import annotations
+
+import itertools
+import json
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence, Tuple
+
+
+@dataclass
+class StageCost:
+    fwd: float                  # ms per microbatch forward
+    bwd: float                  # ms per microbatch backward (dgrads + weight gradients not deferred)
+    wgrad: float = 0.0          # ms of the deferred (merged over all microbatches) weight gradients
+    opt: float = 0.0            # ms of the stage's optimizer step
+    # transfer ms per microbatch: forward activations / skips to consumer stage c, gradients to producer p
+    xfer_fwd: Dict[int, float] = field(default_factory=dict)
+    xfer_bwd: Dict[int, float] = field(default_factory=dict)
+
+
+@dataclass
+class Timeline:
+    step_ms: float
+    fwd: List[List[Tuple[float, float]]]     # [stage][microbatch] -> (start, end)
+    bwd: List[List[Tuple[float, float]]]
+    stage_end: List[float]
+    busy_ms: List[float]                     # compute time per stage
+
+    def efficiency(self) -> float:
+        """Mean stage utilisation: sum of stage busy time / (stages x step)."""
+        return sum(self.busy_ms) / (len(self.busy_ms) * self.step_ms)
+
+
+def simulate(costs: Sequence[StageCost], M: int, loss_ms: float = 0.0) -> Timeline:
+    """Simulate one all-forward / all-backward GPipe step (see the module docstring)."""
+    S = len(costs)
+    producers = [sorted(p for p in range(S) if s in costs[p].xfer_fwd) for s in range(S)]
+    consumers = [sorted(costs[s].xfer_fwd) for s in range(S)]
+    fwd = [[(0.0, 0.0)] * M for _ in range(S)]
+    bwd = [[(0.0, 0.0)] * M for _ in range(S)]
+    # forward: producers always have lower stage indices, so stage order is a topological order
+    for s in range(S):
+        t = 0.0
+        for m in range(M):
+            start = t
+            for p in producers[s]:
+                start = max(start, fwd[p][m][1] + costs[p].xfer_fwd[s])
+            end = start + costs[s].fwd
+            fwd[s][m] = (start, end)
+            t = end
+    # backward: consumers have higher indices -> reverse stage order
+    for s in reversed(range(S)):
+        t = fwd[s][M - 1][1] + (loss_ms if s == S - 1 else 0.0)
+        for m in reversed(range(M)):
+            start = t
+            for c in consumers[s]:
+                start = max(start, bwd[c][m][1] + costs[c].xfer_bwd[s])
+            end = start + costs[s].bwd
+            bwd[s][m] = (start, end)
+            t = end
+    stage_end = [bwd[s][0][1] + costs[s].wgrad + costs[s].opt for s in range(S)]
+    busy = [M * (c.fwd + c.bwd) + c.wgrad + c.opt for c in costs]
+    return Timeline(max(stage_end), fwd, bwd, stage_end, busy)
+
+
+# ------------------------------------------------------------------------------------ cost model
+def _stage_of(idx: int, cuts: Sequence[int]) -> int:
+    for s in range(len(cuts) - 1):
+        if cuts[s] <= idx < cuts[s + 1]:
+            return s
+    raise ValueError(idx)
+
+
+def boundary_bytes(depth: int, widths: Sequence[int], mid_width: int, mb: int, h: int, w: int,
+                   dtype_bytes: int = 2) -> Dict[str, Tuple[int, int, int]]:
+    """(producer block, consumer block, bytes per microbatch) of every tensor that can cross a cut:
+    the x between consecutive blocks and the skip of each encoder level."""
+    out = {}
+    H, W = h, w
+    for lvl, wd in enumerate(widths):
+        out[f"skip{lvl}"] = (lvl, depth + 1 + (depth - 1 - lvl), mb * wd * H * W * dtype_bytes)
+        H, W = H // 2, W // 2
+        out[f"x{lvl}"] = (lvl, lvl + 1, mb * wd * H * W * dtype_bytes)      # pooled -> next block
+    out[f"x{depth}"] = (depth, depth + 1, mb * mid_width * H * W * dtype_bytes)   # mid -> dec0
+    for i, wd in enumerate(reversed(widths)):
+        H, W = H * 2, W * 2
+        out[f"x{depth + 1 + i}"] = (depth + 1 + i, depth + 2 + i, mb * wd * H * W * dtype_bytes)
+    return out
+
+
+def stage_costs(table: dict, mb: int, M: int, cuts: Sequence[int], link_gbs: float = 100.0,
+                link_latency_ms: float = 0.015, defer: bool = True) -> List[StageCost]:
+    """Stage costs of partition ``cuts`` at microbatch ``mb`` (M microbatches) from a block time table.
+
+    ``table``: {"depth", "widths", "mid_width", "img": [h, w], "per_mb": {str(mb): {"fwd": [...],
+    "bwd": [...], "bwd_nowgrad": [...]}}, "opt_ms": [...]} (ms per block, tools/block_times.py).
+    With ``defer`` the stage's weight gradients are merged over the M microbatches (one launch per
+    layer, measured at the full step's image count M*mb when the table has it, else scaled)."""
+    depth, widths, mid_width = table["depth"], table["widths"], table["mid_width"]
+    h, w = table["img"]
+    row = table["per_mb"][str(mb)]
+    big = table["per_mb"].get(str(mb * M))
+    S = len(cuts) - 1
+    costs = []
+    for s in range(S):
+        blocks = range(cuts[s], cuts[s + 1])
+        f = sum(row["fwd"][b] for b in blocks)
+        if defer:
+            b = sum(row["bwd_nowgrad"][i] for i in blocks)
+            if big is not None:
+                wg = sum(big["bwd"][i] - big["bwd_nowgrad"][i] for i in blocks)
+            else:
+                wg = M * sum(row["bwd"][i] - row["bwd_nowgrad"][i] for i in blocks)
+        else:
+            b = sum(row["bwd"][i] for i in blocks)
+            wg = 0.0
+        opt = sum(table.get("opt_ms", [0.0] * len(row["fwd"]))[i] for i in blocks)
+        costs.append(StageCost(f, b, max(wg, 0.0), opt))
+    for name, (pb, cb, nbytes) in boundary_bytes(depth, widths, mid_width, mb, h, w).items():
+        if pb >= len(table["per_mb"][str(mb)]["fwd"]) or cb >= len(table["per_mb"][str(mb)]["fwd"]):
+            continue
+        ps, cs = _stage_of(pb, cuts), _stage_of(cb, cuts)
+        if ps == cs:
+            continue
+        ms = link_latency_ms + nbytes / (link_gbs * 1e6)
+        # several tensors to the same peer travel in one grouped launch: bytes add, latency once
+        costs[ps].xfer_fwd[cs] = costs[ps].xfer_fwd.get(cs, link_latency_ms) + ms - link_latency_ms
+        costs[cs].xfer_bwd[ps] = costs[cs].xfer_bwd.get(ps, link_latency_ms) + ms - link_latency_ms
+    return costs
+
+
+def single_device_ms(table: dict, batch: int) -> Optional[float]:
+    """Measured single-stage step of the whole batch (sum of blocks + optimizer), if the table has it."""
+    row = table["per_mb"].get(str(batch))
+    if row is None:
+        return None
+    return sum(row["fwd"]) + sum(row["bwd"]) + sum(table.get("opt_ms", []))
+
+
+def partitions(nblocks: int, S: int):
+    """Every contiguous split of ``nblocks`` blocks into S non-empty stages (cut lists)."""
+    for inner in itertools.combinations(range(1, nblocks), S - 1):
+        yield [0, *inner, nblocks]
+
+
+def best_partition(table: dict, S: int, mb: int, M: int, **kw) -> Tuple[List[int], Timeline]:
+    nb = len(table["per_mb"][str(mb)]["fwd"])
+    best = None
+    for cuts in partitions(nb, S):
+        tl = simulate(stage_costs(table, mb, M, cuts, **kw), M)
+        if best is None or tl.step_ms < best[1].step_ms:
+            best = (cuts, tl)
+    return best
+
+
+def plan(table: dict, S: int, batch: int, cuts: Optional[Sequence[int]] = None, **kw) -> List[dict]:
+    """For every microbatch count M whose microbatch size the table has: the best (or the given)
+    partition, its simulated step, img/s and efficiency against the measured single-stage step."""
+    out = []
+    t1 = single_device_ms(table, batch)
+    for M in sorted({batch // int(k) for k in table["per_mb"] if batch % int(k) == 0 and batch // int(k) >= 1}):
+        mb = batch // M
+        if cuts is None:
+            c, tl = best_partition(table, S, mb, M, **kw)
+        else:
+            c, tl = list(cuts), simulate(stage_costs(table, mb, M, cuts, **kw), M)
+        r = {"stages": S, "microbatches": M, "mb": mb, "cuts": c, "step_ms": round(tl.step_ms, 3),
+             "img_s": round(batch * 1000.0 / tl.step_ms, 1), "utilisation": round(tl.efficiency(), 3)}
+        if t1 is not None:
+            r["speedup_vs_1gpu"] = round(t1 / tl.step_ms, 3)
+            r["scaling_efficiency"] = round(t1 / tl.step_ms / S, 3)
+        out.append(r)
+    return out
+
+
+def load_table(path: str) -> dict:
+    with open(path) as f:
+        return json.load(f)

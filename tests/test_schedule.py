@@ -1,0 +1,79 @@
+"""GPipe schedule model (parallel/schedule.py) against hand-computed timelines, and the
+time-balanced partitioner on a synthetic block-time table (CPU only)."""
+import pytest
+
+from distributedpytorch_amd.parallel.schedule import (StageCost, best_partition, boundary_bytes, partitions,
+                                                      plan, simulate, stage_costs)
+
+
+def test_two_stage_hand_computed():
+    # F = (1, 2), B = (2, 3), M = 2, no transfers:
+    #   s0 fwd m0 [0,1] m1 [1,2]; s1 fwd m0 [1,3] m1 [3,5]
+    #   s1 bwd m1 [5,8] m0 [8,11]; s0 bwd m1 [max(2,8)=8,10] m0 [max(10,11)=11,13]
+    c = [StageCost(1, 2, xfer_fwd={1: 0.0}), StageCost(2, 3, xfer_bwd={0: 0.0})]
+    tl = simulate(c, 2)
+    assert tl.fwd == [[(0, 1), (1, 2)], [(1, 3), (3, 5)]]
+    assert tl.bwd == [[(11, 13), (8, 10)], [(8, 11), (5, 8)]]
+    assert tl.step_ms == 13
+    # the first stage's deferred weight gradients run in its drain: 13 + 1
+    c[0].wgrad = 1.0
+    assert simulate(c, 2).step_ms == 14
+    # transfers delay the consumer: x arrives 0.5 after the producer's forward ends
+    c = [StageCost(1, 2, xfer_fwd={1: 0.5}), StageCost(2, 3, xfer_bwd={0: 0.5})]
+    tl = simulate(c, 2)
+    assert tl.fwd[1] == [(1.5, 3.5), (3.5, 5.5)]
+    assert tl.bwd[0] == [(12.0, 14.0), (9.0, 11.0)]      # s1 bwd m1 [5.5,8.5] m0 [8.5,11.5]
+
+
+def test_four_stage_uniform_matches_gpipe_formula():
+    # F = 1, B = 2 everywhere, M = 2: (M + S - 1)(F + B) = 15; stage 0 also feeds stage 3 (a skip)
+    c = [StageCost(1, 2, xfer_fwd={1: 0.0, 3: 0.0}), StageCost(1, 2, xfer_fwd={2: 0.0}, xfer_bwd={0: 0.0}),
+         StageCost(1, 2, xfer_fwd={3: 0.0}, xfer_bwd={1: 0.0}), StageCost(1, 2, xfer_bwd={2: 0.0, 0: 0.0})]
+    tl = simulate(c, 2)
+    assert tl.step_ms == 15
+    assert tl.bwd[0] == [(13, 15), (11, 13)]
+    assert abs(tl.efficiency() - 2 / 5) < 1e-12
+    for M in (1, 4, 8, 32):
+        assert abs(simulate(c, M).efficiency() - M / (M + 3)) < 1e-12
+
+
+def _table():
+    # depth 2 UNet (6 blocks); uneven block times; per_mb 1, 2, 4
+    depth, widths, mid = 2, [8, 16], 32
+    base_f = [4.0, 2.0, 1.0, 2.0, 4.0, 0.5]
+    per = {}
+    for mb in (1, 2, 4):
+        f = [v * mb for v in base_f]
+        per[str(mb)] = {"fwd": f, "bwd": [2 * v for v in f], "bwd_nowgrad": [1.5 * v for v in f]}
+    return {"depth": depth, "widths": widths, "mid_width": mid, "img": [32, 32], "per_mb": per,
+            "opt_ms": [0.0] * 6}
+
+
+def test_boundary_bytes_shapes():
+    b = boundary_bytes(2, [8, 16], 32, 1, 32, 32)
+    assert b["skip0"] == (0, 4, 8 * 32 * 32 * 2) and b["skip1"] == (1, 3, 16 * 16 * 16 * 2)
+    assert b["x0"] == (0, 1, 8 * 16 * 16 * 2) and b["x2"] == (2, 3, 32 * 8 * 8 * 2)
+    assert b["x4"] == (4, 5, 8 * 32 * 32 * 2)
+
+
+def test_time_partition_beats_flop_like_cut():
+    t = _table()
+    assert sum(1 for _ in partitions(6, 3)) == 10
+    cuts, tl = best_partition(t, 2, 1, 4, link_gbs=1e9)
+    # brute force over the simulator: no other 2-stage cut is faster
+    for c in partitions(6, 2):
+        assert simulate(stage_costs(t, 1, 4, c, link_gbs=1e9), 4).step_ms >= tl.step_ms - 1e-9
+    assert cuts == [0, 3, 6]            # 7 | 6.5 forward ms: the balanced-by-time cut
+    rows = plan(t, 2, 4, link_gbs=1e9)
+    assert [r["microbatches"] for r in rows] == [1, 2, 4]
+    assert rows[-1]["step_ms"] < rows[0]["step_ms"]   # more microbatches: smaller bubble
+    assert all(0 < r["scaling_efficiency"] <= 1 for r in rows)
+
+
+def test_deferred_wgrad_accounting():
+    t = _table()
+    a = stage_costs(t, 1, 4, [0, 3, 6], defer=True)
+    b = stage_costs(t, 1, 4, [0, 3, 6], defer=False)
+    # same total backward work, split into per-microbatch dgrads + one merged weight-gradient tail
+    for x, y in zip(a, b):
+        assert x.bwd * 4 + x.wgrad == pytest.approx(y.bwd * 4)

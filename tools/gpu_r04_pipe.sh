@@ -1,0 +1,12 @@
+#!/bin/bash
+# Slice-staged GEMM tests + per-layer timing, then the per-block time tables of the pipeline model.
+set -o pipefail
+cd "$(dirname "$0")/.." && export TMPDIR=/tmp && mkdir -p gpurun_out/sl gpurun_out/pipe
+timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_rowblock.py > gpurun_out/sl/pytest.log 2>&1
+rc=$?; tail -3 gpurun_out/sl/pytest.log; [ $rc -ne 0 ] && exit $rc
+timeout -k 10 300 python tools/kbench.py --batch 256 --paths "" --no-wgrad --gvar 14 15 262144 524288 --reps 7 --only "L2,L3,mid" > gpurun_out/sl/kbench.log 2>&1 || { echo kbench failed; tail gpurun_out/sl/kbench.log; exit 1; }
+grep -v "n/a" gpurun_out/sl/kbench.log
+timeout -k 10 400 python -u tools/block_times.py --model unet --img 512 --mbs 8 16 32 64 128 256 --out gpurun_out/pipe/block_times_unet_512.json > gpurun_out/pipe/bt_unet.log 2>&1 || { echo bt unet failed; tail gpurun_out/pipe/bt_unet.log; exit 1; }
+tail -3 gpurun_out/pipe/bt_unet.log
+timeout -k 10 400 python -u tools/block_times.py --model unet-xl --img 1024 --mbs 1 2 4 8 16 --out gpurun_out/pipe/block_times_unetxl_1024.json > gpurun_out/pipe/bt_xl.log 2>&1 || { echo bt xl failed; tail gpurun_out/pipe/bt_xl.log; exit 1; }
+tail -3 gpurun_out/pipe/bt_xl.log
