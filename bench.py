@@ -68,6 +68,10 @@ def parse():
     ap.add_argument("--stages", type=int, default=2, help="mp with one process: stages on the local device")
     ap.add_argument("--mp-cut", choices=["auto", "reference", "balanced"], default="auto",
                     help="mp stage boundaries (auto: reference encoder|decoder cut for 2 stages, else balanced)")
+    ap.add_argument("--timing-ablation", default="",
+                    help="MEASUREMENT ONLY, numerically wrong: skip these kernel families (comma list of "
+                         "stream,halo,glds,wgrad,wgrad_deep,bwd,deconv) to see what they cost; the JSON line is "
+                         "marked invalid")
     ap.add_argument("--infer", action="store_true",
                     help="inference throughput instead of training: eval-mode forward to the probability map "
                          "(BatchNorm folded into the convs), no loss/backward/optimizer")
@@ -122,6 +126,11 @@ def main():
     from distributedpytorch_amd.utils import set_seed
 
     set_seed(1234)
+    from distributedpytorch_amd.ops import kernels as K
+    ablate = [v for v in a.timing_ablation.split(",") if v]
+    if ablate:
+        K.set_timing_ablation(ablate)
+        print(f"[bench] TIMING ABLATION {ablate}: results are numerically wrong", file=sys.stderr, flush=True)
     mp = a.parallelism == "mp"
     method = "MP" if mp else ("DDP" if world > 1 else "singleGPU")
     cfg = TrainConfig(train_method=method, batch_size=a.batch, img_size=a.img, dtype="bf16",
@@ -242,7 +251,11 @@ def main():
                    "hip_graph": graphed is not None},
         "final_loss": round(final_loss, 5) if final_loss == final_loss else None, "warmup_s": round(warm_s, 2),
         "peak_mem_gb": round(torch.cuda.max_memory_allocated(device) / 2 ** 30, 2),
+        # the run's non-default kernel switches (ops/config.py; empty = the shipped dispatch)
+        "kernel_config": {k: v for k, v in K.CFG.non_default().items()},
     }
+    if ablate:
+        out["INVALID_timing_ablation"] = ablate
     if not a.infer and a.model in PRESETS:
         # achieved model FLOP rate: forward FLOPs (analytic layer table) x 3 for forward + dgrad + wgrad
         fwd_gflop = sum(r[3] for r in layer_table(PRESETS[a.model], a.img[0], a.img[1]))

@@ -655,338 +655,13 @@ static int launch_glds_pers(const IgemmArgs& a, hipStream_t st) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// 32x32x16 variant (cfg 11): cfg 3's tile and pipeline with v_mfma_f32_32x32x16_bf16 -- half the MFMA
-// instructions for the same LDS fragment traffic (per wave and K=64: 4 x (4 A + 2 B) ds_read_b128,
-// 32 MFMAs of 32 cycles instead of 64 of 16).  A 32x32x16 fragment read covers 32 rows with one
-// chunk per 32-lane half, so the image swizzle is chunk ^ ((row >> 1) & 7) (conflict-free for the
-// ds_read_b128 lane groups over 32 consecutive rows; the DMA applies it on the source side).
-__device__ __forceinline__ int swz32(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
-
-__global__ __launch_bounds__(512) void igemm_glds32_kernel(IgemmArgs a) {
-  constexpr int BC = 256, BP = 256, WC = 128, WP = 64, ST = 2, BK = 64;
-  constexpr int NWC = BC / WC, RBY = 128, RPI = 8;
-  constexpr int RA = BC / 64, RP = BP / 64, LPS = RA + RP;
-  constexpr int TC = WC / 32, TP = WP / 32;
-  constexpr int STAGE = (BC + BP) * RBY;
-  __shared__ __attribute__((aligned(16))) char lds[ST * STAGE];
-
-  const int M = a.N * a.Ho * a.Wo;
-  const int nct = a.Ngemm / BC;
-  const int npt = (M + BP - 1) / BP;
-  const int bid = xcd_remap(blockIdx.x, npt * nct);
-  int pt, ct;
-  glds_tile(bid, npt, nct, pt, ct);
-  const int m0 = pt * BP, c0 = ct * BC;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wc = wid % NWC, wp = wid / NWC;
-  const int lrow = wid * RPI + (lane >> 3);          // + j*64 per round: bits 1-3 unchanged
-  const int lchunk = swz32(lrow, lane & 7);
-
-  unsigned pbase[RP], tmask[RP];
-  const int taps = a.KH * a.KW;
-  const int hw = a.Ho * a.Wo;
-#pragma unroll
-  for (int j = 0; j < RP; ++j) {
-    const int m = m0 + j * 64 + lrow;
-    const bool pok = m < M;
-    const int mm = pok ? m : 0;
-    const int pn = mm / hw;
-    const int rem = mm - pn * hw;
-    const int ph = rem / a.Wo, pw = rem - ph * a.Wo;
-    const int h0 = ph * a.stride - a.pad, w0 = pw * a.stride - a.pad;
-    unsigned msk = 0;
-    for (int t = 0; t < taps; ++t) {
-      const int kh = t / a.KW, kw = t - kh * a.KW;
-      const int ih = h0 + kh, iw = w0 + kw;
-      if (pok && ih >= 0 && ih < a.Hs && iw >= 0 && iw < a.Ws) msk |= 1u << t;
-    }
-    tmask[j] = msk;
-    pbase[j] = (unsigned)((((pn * a.Hs + h0) * a.Ws + w0) * a.ldx) * 2 + lchunk * 16);
-  }
-  unsigned woff[RA];
-#pragma unroll
-  for (int j = 0; j < RA; ++j) woff[j] = (unsigned)(((c0 + j * 64 + lrow) * a.Kpad) * 2 + lchunk * 16);
-
-  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, 0, (int)a.xbytes, 0x00020000);
-  const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc((void*)a.w, 0, 0x7fffffff, 0x00020000);
-  const int S = a.Kpad / BK;
-  const bool slm = !(a.korder & 1) && a.Kpad == taps * a.Cs;
-  auto issue = [&](int s) {
-    char* base = lds + (s % ST) * STAGE;
-    int tap, ci;
-    ktile_coords(a, s, BK, taps, slm, tap, ci);
-    const int kh = tap / a.KW, kw = tap - kh * a.KW;
-    const unsigned delta = (unsigned)(((kh * a.Ws + kw) * a.ldx + ci) * 2);
-    const unsigned wk = (unsigned)((tap * a.Cs + ci) * 2);
-#pragma unroll
-    for (int j = 0; j < RA; ++j) dma16(wrs, base + (j * 64 + wid * RPI) * RBY, woff[j] + wk);
-#pragma unroll
-    for (int j = 0; j < RP; ++j) {
-      const bool ok = tap < taps && ((tmask[j] >> tap) & 1u);
-      dma16(xr, base + (BC + j * 64 + wid * RPI) * RBY, ok ? pbase[j] + delta : 0x80000000u);
-    }
-  };
-
-  f32x16_t acc[TC][TP];
-#pragma unroll
-  for (int ic = 0; ic < TC; ++ic)
-#pragma unroll
-    for (int ip = 0; ip < TP; ++ip)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[ic][ip][e] = 0.f;
-
-  issue(0);
-  for (int s = 0; s < S; ++s) {
-    wait_vm<0>();
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    if (s + 1 < S) issue(s + 1);
-    __builtin_amdgcn_sched_barrier(0);
-    const char* Wt = lds + (s % ST) * STAGE;
-    const char* P = Wt + BC * RBY;
-#pragma unroll
-    for (int kk = 0; kk < BK / 16; ++kk) {
-      const int chunk = kk * 2 + (lane >> 5);
-      bf16x8_t af[TC], bfr[TP];
-#pragma unroll
-      for (int ic = 0; ic < TC; ++ic) {
-        const int row = wc * WC + ic * 32 + (lane & 31);
-        af[ic] = *reinterpret_cast<const bf16x8_t*>(Wt + row * RBY + (swz32(row, chunk) << 4));
-      }
-#pragma unroll
-      for (int ip = 0; ip < TP; ++ip) {
-        const int row = wp * WP + ip * 32 + (lane & 31);
-        bfr[ip] = *reinterpret_cast<const bf16x8_t*>(P + row * RBY + (swz32(row, chunk) << 4));
-      }
-#pragma unroll
-      for (int ic = 0; ic < TC; ++ic)
-#pragma unroll
-        for (int ip = 0; ip < TP; ++ip)
-          acc[ic][ip] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[ic], bfr[ip], acc[ic][ip], 0, 0, 0);
-    }
-  }
-
-  // 32x32 tiles: pixel = lane & 31; register r holds channel (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
-  const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc((void*)a.y, 0, 0x7fffffff, 0x00020000);
-  const __amdgpu_buffer_rsrc_t mr = __builtin_amdgcn_make_buffer_rsrc((void*)(a.mask ? a.mask : a.y), 0, 0x7fffffff, 0x00020000);
-#pragma unroll
-  for (int ip = 0; ip < TP; ++ip) {
-    const int m = m0 + wp * WP + ip * 32 + (lane & 31);
-    if (m >= M) continue;
-    const unsigned ybase = glds_ybase(a, m);
-#pragma unroll
-    for (int ic = 0; ic < TC; ++ic)
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        glds_store4(a, yr, mr, m, ybase, c0 + wc * WC + ic * 32 + 8 * q + 4 * (lane >> 5), acc[ic][ip][4 * q],
-                    acc[ic][ip][4 * q + 1], acc[ic][ip][4 * q + 2], acc[ic][ip][4 * q + 3]);
-  }
-}
-
-// ------------------------------------------------------------------------------------------------
-// Ping-pong variant (cfg 7, opt-in): the same 256(ch) x 256(px) x 64 tile and 128 KB of LDS (two K-tile
-// buffers), but each K-tile is consumed in four phases, one 64x32 accumulator quadrant per wave per
-// phase (16 MFMAs), and the two halves of the workgroup (waves 0-3 / 4-7: one wave of each per SIMD)
-// run one barrier apart -- while one wave of a SIMD issues its quadrant's MFMAs the other reads the
-// next quadrant's fragments and issues its share of the LDS-DMA prefetch
-// (cdna_hip_programming.md "The 256^2 8-phase template", "Pipelining across barriers").
-// Half-tiles: A0/A1 = weight rows of quadrant qa of both channel-waves, B0/B1 = pixel rows of quadrant
-// qb of all four pixel-waves: 128 rows x 128 B each, two 1-KB DMA instructions per wave.
-// Phase p of K-tile s reads: p0 A0+B0 (12 ds_read_b128), p1 B1 (4), p2 A1 (8), p3 nothing, and issues
-// one half-tile: p0 -> B1(s+1), p1 -> A1(s+1), p2 -> A0(s+2), p3 -> B0(s+2).  WAR: every half-tile is
-// restaged >= 2 phases after its last read.  RAW: a half-tile read at phase q was issued at slot q-5
-// or earlier and each wave waits for it in phase q-1 before that phase's first barrier with
-// vmcnt(#DMAs issued in the 4 newest slots) = 8 in steady state.
-__device__ __forceinline__ void wait_vm_n(int n) {
-  if (n >= 8) wait_vm<8>();
-  else if (n >= 6) wait_vm<6>();
-  else if (n >= 4) wait_vm<4>();
-  else if (n >= 2) wait_vm<2>();
-  else wait_vm<0>();
-}
-
-__global__ __launch_bounds__(512) void igemm_pp_kernel(IgemmArgs a) {
-  constexpr int BC = 256, BP = 256, WC = 128, WP = 64, TC = 8, TP = 4, RBY = 128;
-  constexpr int STAGE = (BC + BP) * RBY;
-  __shared__ __attribute__((aligned(16))) char lds[2 * STAGE];
-
-  const int M = a.N * a.Ho * a.Wo;
-  const int nct = a.Ngemm / BC;
-  const int npt = (M + BP - 1) / BP;
-  const int bid = xcd_remap(blockIdx.x, npt * nct);
-  int pt, ct;
-  glds_tile(bid, npt, nct, pt, ct);
-  const int m0 = pt * BP, c0 = ct * BC;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wc = wid & 1, wp = wid >> 1, grp = wid >> 2;
-  const int lr = lane >> 3;
-  const int lchunk = (lane & 7) ^ lr;
-  unsigned woff[2][2], pbase[2][2], tmask[2][2];
-  const int taps = a.KH * a.KW;
-  const int hw = a.Ho * a.Wo;
-#pragma unroll
-  for (int h = 0; h < 2; ++h)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      woff[h][j] = (unsigned)(((c0 + j * 128 + h * 64 + wid * 8 + lr) * a.Kpad) * 2 + lchunk * 16);
-      const int m = m0 + (2 * j + grp) * 64 + h * 32 + (wid & 3) * 8 + lr;
-      const bool pok = m < M;
-      const int mm = pok ? m : 0;
-      const int pn = mm / hw;
-      const int rem = mm - pn * hw;
-      const int ph = rem / a.Wo, pw = rem - ph * a.Wo;
-      const int h0 = ph * a.stride - a.pad, w0 = pw * a.stride - a.pad;
-      unsigned msk = 0;
-      for (int t = 0; t < taps; ++t) {
-        const int kh = t / a.KW, kw = t - kh * a.KW;
-        const int ih = h0 + kh, iw = w0 + kw;
-        if (pok && ih >= 0 && ih < a.Hs && iw >= 0 && iw < a.Ws) msk |= 1u << t;
-      }
-      tmask[h][j] = msk;
-      pbase[h][j] = (unsigned)((((pn * a.Hs + h0) * a.Ws + w0) * a.ldx) * 2 + lchunk * 16);
-    }
-  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, 0, (int)a.xbytes, 0x00020000);
-  const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc((void*)a.w, 0, 0x7fffffff, 0x00020000);
-  const int S = a.Kpad / 64;
-  const bool slm = !(a.korder & 1) && a.Kpad == taps * a.Cs;
-  auto issueA = [&](int h, int t) {
-    char* base = lds + (t & 1) * STAGE;
-    int tap, ci;
-    ktile_coords(a, t, 64, taps, slm, tap, ci);
-    const unsigned wk = (unsigned)((tap * a.Cs + ci) * 2);
-#pragma unroll
-    for (int j = 0; j < 2; ++j) dma16(wrs, base + (j * 128 + h * 64 + wid * 8) * RBY, woff[h][j] + wk);
-  };
-  auto issueB = [&](int h, int t) {
-    char* base = lds + (t & 1) * STAGE + BC * RBY;
-    int tap, ci;
-    ktile_coords(a, t, 64, taps, slm, tap, ci);
-    const int kh = tap / a.KW, kw = tap - kh * a.KW;
-    const unsigned delta = (unsigned)(((kh * a.Ws + kw) * a.ldx + ci) * 2);
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const bool ok = tap < taps && ((tmask[h][j] >> tap) & 1u);
-      dma16(xr, base + ((2 * j + grp) * 64 + h * 32 + (wid & 3) * 8) * RBY, ok ? pbase[h][j] + delta : 0x80000000u);
-    }
-  };
-  const int X = 4 * S - 6;   // slot q issues iff q < X (its K-tile (q+2)/4 + 1 < S)
-
-  f32x4_t acc[TC][TP];
-#pragma unroll
-  for (int ic = 0; ic < TC; ++ic)
-#pragma unroll
-    for (int ip = 0; ip < TP; ++ip) acc[ic][ip] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-
-  issueA(0, 0);
-  issueB(0, 0);
-  issueB(1, 0);
-  issueA(1, 0);
-  if (S > 1) {
-    issueA(0, 1);
-    issueB(0, 1);
-    wait_vm<8>();
-  } else {
-    wait_vm<4>();
-  }
-  __builtin_amdgcn_sched_barrier(0);
-  __builtin_amdgcn_s_barrier();
-  if (grp) __builtin_amdgcn_s_barrier();       // the second half runs one barrier behind
-  __builtin_amdgcn_sched_barrier(0);
-
-  bf16x8_t af[4][2], bfr[2][2][2];
-  auto readA = [&](const char* Wt, int h) {
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int ic = 0; ic < 4; ++ic) {
-        const int row = wc * WC + h * 64 + ic * 16 + (lane & 15);
-        const int chunk = kk * 4 + (lane >> 4);
-        af[ic][kk] = *reinterpret_cast<const bf16x8_t*>(Wt + row * RBY + ((chunk ^ (row & 7)) << 4));
-      }
-  };
-  auto readB = [&](const char* P, int h) {
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int ip = 0; ip < 2; ++ip) {
-        const int row = wp * WP + h * 32 + ip * 16 + (lane & 15);
-        const int chunk = kk * 4 + (lane >> 4);
-        bfr[h][ip][kk] = *reinterpret_cast<const bf16x8_t*>(P + row * RBY + ((chunk ^ (row & 7)) << 4));
-      }
-  };
-  auto mfma_quad = [&](int qa, int qb) {
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int ic = 0; ic < 4; ++ic)
-#pragma unroll
-        for (int ip = 0; ip < 2; ++ip)
-          acc[qa * 4 + ic][qb * 2 + ip] =
-              __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ic][kk], bfr[qb][ip][kk], acc[qa * 4 + ic][qb * 2 + ip], 0, 0, 0);
-  };
-  auto sync_in = [&]() {
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_setprio(1);
-  };
-  auto sync_out = [&]() {
-    __builtin_amdgcn_s_setprio(0);
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-  };
-
-  for (int s = 0; s < S; ++s) {
-    const char* Wt = lds + (s & 1) * STAGE;
-    const char* P = Wt + BC * RBY;
-    const int q0 = 4 * s;
-    const bool steady = s + 2 < S;
-    readB(P, 0);
-    readA(Wt, 0);
-    if (s + 1 < S) issueB(1, s + 1);
-    if (steady) wait_vm<8>();
-    else wait_vm_n(2 * min(max(X - (q0 - 3), 0), 4));
-    sync_in();
-    mfma_quad(0, 0);
-    sync_out();
-    readB(P, 1);
-    if (s + 1 < S) issueA(1, s + 1);
-    if (steady) wait_vm<8>();
-    else wait_vm_n(2 * min(max(X - (q0 - 2), 0), 4));
-    sync_in();
-    mfma_quad(0, 1);
-    sync_out();
-    readA(Wt, 1);
-    if (s + 2 < S) issueA(0, s + 2);
-    sync_in();
-    mfma_quad(1, 1);
-    sync_out();
-    if (s + 2 < S) issueB(0, s + 2);
-    if (s + 1 < S) {
-      if (steady) wait_vm<8>();
-      else wait_vm_n(2 * min(max(X - q0, 0), 4));
-    }
-    sync_in();
-    mfma_quad(1, 0);
-    sync_out();
-  }
-  if (!grp) __builtin_amdgcn_s_barrier();      // balance the second half's extra barrier
-
-  glds_epilogue<TC, TP, WC, WP>(a, acc, M, m0, c0, wc, wp, lane);
-}
-
-// ------------------------------------------------------------------------------------------------
-// Ping-pong, steady-state form (cfg 14): igemm_pp_kernel's tile, half-tile schedule and wave pairing,
-// restructured so the K loop body is straight-line code: the K-tile coordinates of the two tiles in
+// Ping-pong, steady-state form (cfg 14): a 256 x 256 tile in four MFMA phases per K-tile (one 64 x 32
+// accumulator quadrant each) with the two wave halves one barrier apart, and a half-tile LDS-DMA
+// schedule; the K loop body is straight-line code: the K-tile coordinates of the two tiles in
 // flight (s+1, s+2) advance incrementally (no per-issue integer division), every phase of the steady
 // loop issues its half-tile and waits a constant vmcnt(8), and the last two K-tiles are a peeled tail
 // with compile-time waits.  Per phase: B fragments first, then A (as the 8-phase template orders them).
-template <int PROBE = 0,   // timing probes (A/B only): 1 = no epilogue, 2 = no MFMAs in the K loop,
-                           // 3 = no MFMAs and no DMA, 4 = no DMA (LDS reads of whatever is there)
-          int EP = 0>      // epilogue kind (glds_ep_kind)
+template <int EP = 0>       // epilogue kind (glds_ep_kind)
 __global__ __launch_bounds__(512) void igemm_pp2_kernel(IgemmArgs a) {
   constexpr int BC = 256, BP = 256, WC = 128, WP = 64, TC = 8, TP = 4, RBY = 128;
   constexpr int STAGE = (BC + BP) * RBY;
@@ -1054,14 +729,12 @@ __global__ __launch_bounds__(512) void igemm_pp2_kernel(IgemmArgs a) {
     return c;
   };
   auto issueA = [&](int h, int buf, KC c) {
-    if constexpr (PROBE >= 3) return;
     char* base = lds + buf * STAGE;
     const unsigned wk = (unsigned)((c.tap * a.Cs + c.ci) * 2);
 #pragma unroll
     for (int j = 0; j < 2; ++j) dma16(wrs, base + (j * 128 + h * 64 + wid * 8) * RBY, woff[h][j] + wk);
   };
   auto issueB = [&](int h, int buf, KC c) {
-    if constexpr (PROBE >= 3) return;
     char* base = lds + buf * STAGE + BC * RBY;
     const unsigned delta = (unsigned)(((c.kh * a.Ws + c.kw) * a.ldx + c.ci) * 2);
 #pragma unroll
@@ -1113,17 +786,6 @@ __global__ __launch_bounds__(512) void igemm_pp2_kernel(IgemmArgs a) {
       }
   };
   auto mfma_quad = [&](int qa, int qb) {
-    if constexpr (PROBE == 2 || PROBE == 3) {
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-        for (int ic = 0; ic < 4; ++ic) asm volatile("" ::"v"(af[ic][kk]));
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-        for (int ip = 0; ip < 2; ++ip) asm volatile("" ::"v"(bfr[qb][ip][kk]));
-      return;
-    }
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
@@ -1234,13 +896,6 @@ __global__ __launch_bounds__(512) void igemm_pp2_kernel(IgemmArgs a) {
   }
   if (!grp) __builtin_amdgcn_s_barrier();      // balance the second half's extra barrier
 
-  if constexpr (PROBE == 1) {
-#pragma unroll
-    for (int ic = 0; ic < TC; ++ic)
-#pragma unroll
-      for (int ip = 0; ip < TP; ++ip) asm volatile("" ::"v"(acc[ic][ip]));
-    return;
-  }
   if constexpr (EP != 0) glds_epilogue_fast<TC, TP, WC, WP, EP>(a, acc, M, m0, c0, wc, wp, lane);
   else glds_epilogue<TC, TP, WC, WP>(a, acc, M, m0, c0, wc, wp, lane);
 }
@@ -2051,34 +1706,34 @@ static int launch_glds(const IgemmArgs& a, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
-// cfg 0 = auto (+16: tap-major K order, +32: auto without the persistent kernel, +64: cfg 3 / 2 without
-// the fragment preload; for A/B).  1: 256(ch) x 128(px), 3 stages (144 KB)   2: 128 x 256, 3 stages
-//                3: 256 x 256, 2 stages (128 KB)            4: 128 x 128, 4 stages (128 KB)
-//                5: 256 x 256 x BK32, 4 stages (128 KB)     6: 128 x 256 x BK32, 5 stages (120 KB)
-//                8 / 9 / 10: cfg 3 / 2 / 1 as a persistent kernel (one workgroup per CU, pipelined across tiles)
-//                7: cfg 3's tile in four MFMA phases per K-tile with the wave halves ping-ponged (igemm_pp_kernel)
-//                11: cfg 3 with 32x32x16 MFMAs (igemm_glds32_kernel)
-//                12 / 13: cfg 3 / 2 with the compiler's read/MFMA interleave instead of all fragments first (A/B)
-// Requires Cs % 64 == 0 (a K-step never straddles a tap), Kpad % 64 == 0, Ngemm % BC == 0.
+// cfg 0 = auto.  Tile families (all LDS-DMA, MFMA 16x16x32 bf16):
+//   1: 256 (ch) x 128 (px), 3 stages      2: 128 x 256, 3 stages      4: 128 x 128, 4 stages
+//   8: 256 x 256 persistent (one workgroup per CU walking XCD-contiguous tiles; short K)
+//   14: 256 x 256 ping-pong: row-block pixel staging (igemm_pp2h_kernel) on whole-row tiles of 3x3 s1 p1
+//       convs, per-K-tile staging (igemm_pp2_kernel) otherwise
+//   15: 128 x 256 row-block ping-pong (igemm_pp2h_kernel<EP, 128>)
+//   16 / 17 (variant 65536 / 131072): the row-block GEMMs with two MFMA phases per K-tile (igemm_rb2_kernel)
+//   18 / 19 (variant 262144 / 524288): slice-staged 128 x 512 / 256 x 256 (igemm_sl_kernel)
+// Flags: +32 no persistent kernel in the auto choice (a side stream owns CUs), +2048 generic epilogue
+// (tests), +8192 cfg 14 without row blocks (tests), +16384 auto prefers the two-phase row-block kernels.
+// Requires Cs % 64 == 0 (a K-step never straddles a tap; slice-staged: Cs % 32), Kpad % 64 == 0,
+// Ngemm % BC == 0.
 DPA_API int dpa_igemm_glds(const IgemmArgs* args, int cfg, hipStream_t st) {
   IgemmArgs a = *args;
-  if (cfg & 16) a.korder |= 1;   // A/B: tap-major K-tile order
-  if (cfg & 32) a.korder |= 2;   // A/B: no persistent kernel in the auto choice
-  const bool no_pre = cfg & 64;  // A/B: the compiler's read/MFMA interleave (cfg 12 / 13) for cfg 3 / 2
-  const bool no_pp = cfg & 128;  // A/B: the 2-stage cfg 3 instead of the ping-pong cfg 14 in the auto choice
-  const int probe = (cfg >> 8) & 7;   // timing probes of cfg 14 (numerically wrong): see igemm_pp2_kernel
-  const bool no_fast_ep = cfg & 2048; // A/B: the generic epilogue in cfg 14
-  const bool no_rowblock = cfg & 8192;  // A/B: cfg 14 with per-K-tile pixel staging (no row blocks)
-  const bool rb2 = cfg & 16384;         // A/B: the two-phase row-block kernels (cfg 16 / 17) in place of 14 / 15
-  // the explicit two-phase row-block kernels: variant 65536 = cfg 16 (256 channels), 131072 = cfg 17 (128)
+  if (cfg & 32) a.korder |= 2;          // no persistent kernel in the auto choice
+  const bool no_fast_ep = cfg & 2048;   // the generic epilogue (tests)
+  const bool no_rowblock = cfg & 8192;  // cfg 14 with per-K-tile pixel staging (tests)
+  const bool rb2 = cfg & 16384;         // auto: the two-phase row-block kernels (cfg 16 / 17) in place of 14 / 15
   cfg = (cfg & 65536) ? 16 : (cfg & 131072) ? 17 : (cfg & 262144) ? 18 : (cfg & 524288) ? 19 : (cfg & 15);
-  if ((a.Cs & 63) || (a.Kpad & 63) || (a.ldx & 7) || (a.ldy & 3) || a.KH * a.KW > 32) return (int)hipErrorInvalidValue;
+  const bool sl = cfg == 18 || cfg == 19;
+  if ((a.Cs & (sl ? 31 : 63)) || (a.Kpad & 63) || (a.ldx & 7) || (a.ldy & 3) || a.KH * a.KW > 32 || (a.korder & 1))
+    return (int)hipErrorInvalidValue;
   if (a.bnslab) {
     // BatchNorm partial sums (bnslab[M / 256][2][Ngemm]): only the row-block kernels' EP 1 / 2 epilogues
     // carry them (cfg 0 -> 14 / 15 by the channel count); anything else is refused, never silently skipped
     const long M = (long)a.N * a.Ho * a.Wo;
     const int ep = glds_ep_kind(a);
-    if (probe || no_fast_ep || no_rowblock || (a.korder & 1) || (ep != 1 && ep != 2) || (ep == 1 && a.relu) ||
+    if (no_fast_ep || no_rowblock || (ep != 1 && ep != 2) || (ep == 1 && a.relu) ||
         (ep == 2 && a.mask_ch != a.Ngemm) || M % 256)
       return (int)hipErrorInvalidValue;
     if (cfg == 0) cfg = a.Ngemm % 256 == 0 ? (rb2 ? 16 : 14) : (rb2 ? 17 : 15);
@@ -2110,66 +1765,45 @@ DPA_API int dpa_igemm_glds(const IgemmArgs* args, int cfg, hipStream_t st) {
     auto grid_of = [&](long bc, long bp) { return ((M + bp - 1) / bp) * (a.Ngemm / bc); };
     // short K (<= 8 K-steps: the transposed convs' forward and up-path dgrads): the persistent kernel,
     // which hides each tile's first-load latency and epilogue behind the neighbouring tile, is 3-9 %
-    // faster there; from K = 1024 on the fragment-preloaded cfg 3 wins by 3-6 %
-    // (profiles/kbench_glds_shortk_b256_r02.txt, interleaved)
-    // K >= 1024: the ping-pong steady-state kernel, 4-10 % faster than cfg 3 on every deep layer and
-    // 1.38 vs 1.18 PF on a plain 8192^3 GEMM (profiles/kbench_glds_pp2_b256_r03.txt)
+    // faster there (profiles/kbench_glds_shortk_b256_r02.txt, interleaved); otherwise the ping-pong
+    // steady-state kernel, 4-10 % faster than the 2-stage 256 x 256 tile on every deep layer and 1.38 vs
+    // 1.18 PF on a plain 8192^3 GEMM (profiles/kbench_glds_pp2_b256_r03.txt)
     if (a.Ngemm % 256 == 0 && grid_of(256, 256) >= 512)
-      cfg = (a.Kpad <= 8 * 64 && !(a.korder & 2)) ? 8 : (no_pp ? 3 : (rb2 && pp2h_ok(a)) ? 16 : 14);
+      cfg = (a.Kpad <= 8 * 64 && !(a.korder & 2)) ? 8 : (rb2 && pp2h_ok(a)) ? 16 : 14;
     // small grids (pipeline microbatches, small batches): the 128-channel row-block kernel when its
     // 128 x 256 tiles still fill every CU once -- it replaces the 3-stage 128 x 256 kernel (cfg 2) and,
     // at 256..511 of its tiles, the 128 x 128 one (cfg 4: twice the tiles at lower efficiency)
-    else if (a.Ngemm % 128 == 0 && grid_of(128, 256) >= 256 && !no_pp && !no_rowblock && !(a.korder & 1) &&
-             pp2h128_ok(a))
+    else if (a.Ngemm % 128 == 0 && grid_of(128, 256) >= 256 && !no_rowblock && pp2h128_ok(a))
       cfg = rb2 ? 17 : 15;
     else if (a.Ngemm % 128 == 0 && grid_of(128, 256) >= 512) cfg = 2;
     else if (a.Ngemm % 256 == 0 && grid_of(256, 128) >= 512) cfg = 1;
     else cfg = 4;
   }
-  if (no_pre && (cfg == 3 || cfg == 2)) cfg += 9 + (cfg == 2 ? 2 : 0);   // 3 -> 12, 2 -> 13
+  const int ep = no_fast_ep ? 0 : glds_ep_kind(a);
+  // launch kernel template K<EP> with the specialised epilogue of this launch
+#define DPA_EP_LAUNCH(K, grid)                                                                     \
+  do {                                                                                             \
+    if (ep == 1) hipLaunchKernelGGL((K<1>), dim3(grid), dim3(512), 0, st, a);                      \
+    else if (ep == 2) hipLaunchKernelGGL((K<2>), dim3(grid), dim3(512), 0, st, a);                 \
+    else if (ep == 3) hipLaunchKernelGGL((K<3>), dim3(grid), dim3(512), 0, st, a);                 \
+    else hipLaunchKernelGGL((K<0>), dim3(grid), dim3(512), 0, st, a);                              \
+    return (int)hipGetLastError();                                                                 \
+  } while (0)
+  const int M = a.N * a.Ho * a.Wo;
   switch (cfg) {
     case 1: if (a.Ngemm % 256) break; return launch_glds<256, 128, 64, 64, 3, 64, true>(a, st);
     case 2: if (a.Ngemm % 128) break; return launch_glds<128, 256, 64, 64, 3, 64, true>(a, st);
-    case 3: if (a.Ngemm % 256) break; return launch_glds<256, 256, 128, 64, 2, 64, true>(a, st);
     case 4: if (a.Ngemm % 128) break; return launch_glds<128, 128, 64, 32, 4, 64, true>(a, st);
-    case 5: if (a.Ngemm % 256) break; return launch_glds<256, 256, 128, 64, 4, 32>(a, st);
-    case 6: if (a.Ngemm % 128) break; return launch_glds<128, 256, 64, 64, 5, 32>(a, st);
     case 8: if (a.Ngemm % 256) break; return launch_glds_pers<256, 256, 128, 64, 2>(a, st);
-    case 9: if (a.Ngemm % 128) break; return launch_glds_pers<128, 256, 64, 64, 3>(a, st);
-    case 10: if (a.Ngemm % 256) break; return launch_glds_pers<256, 128, 64, 64, 3>(a, st);
-    case 12: if (a.Ngemm % 256) break; return launch_glds<256, 256, 128, 64, 2>(a, st);
-    case 13: if (a.Ngemm % 128) break; return launch_glds<128, 256, 64, 64, 3>(a, st);
-    case 7: {
-      if (a.Ngemm % 256) break;
-      const int grid = ((a.N * a.Ho * a.Wo + 255) / 256) * (a.Ngemm / 256);
-      hipLaunchKernelGGL(igemm_pp_kernel, dim3(grid), dim3(512), 0, st, a);
-      return (int)hipGetLastError();
-    }
     case 14: {
       if (a.Ngemm % 256 || a.Kpad < 128) break;     // the steady loop + peeled tail need S >= 2
-      const int grid = ((a.N * a.Ho * a.Wo + 255) / 256) * (a.Ngemm / 256);
-      const int ep = no_fast_ep ? 0 : glds_ep_kind(a);
-      if (probe == 0 && !no_rowblock && pp2h_ok(a)) {
-        if (ep == 1) hipLaunchKernelGGL((igemm_pp2h_kernel<1>), dim3(grid), dim3(512), 0, st, a);
-        else if (ep == 2) hipLaunchKernelGGL((igemm_pp2h_kernel<2>), dim3(grid), dim3(512), 0, st, a);
-        else if (ep == 3) hipLaunchKernelGGL((igemm_pp2h_kernel<3>), dim3(grid), dim3(512), 0, st, a);
-        else hipLaunchKernelGGL((igemm_pp2h_kernel<0>), dim3(grid), dim3(512), 0, st, a);
-        return (int)hipGetLastError();
-      }
-      if (probe == 0 && ep == 1) hipLaunchKernelGGL((igemm_pp2_kernel<0, 1>), dim3(grid), dim3(512), 0, st, a);
-      else if (probe == 0 && ep == 2) hipLaunchKernelGGL((igemm_pp2_kernel<0, 2>), dim3(grid), dim3(512), 0, st, a);
-      else if (probe == 0 && ep == 3) hipLaunchKernelGGL((igemm_pp2_kernel<0, 3>), dim3(grid), dim3(512), 0, st, a);
-      else if (probe == 1) hipLaunchKernelGGL(igemm_pp2_kernel<1>, dim3(grid), dim3(512), 0, st, a);
-      else if (probe == 2) hipLaunchKernelGGL(igemm_pp2_kernel<2>, dim3(grid), dim3(512), 0, st, a);
-      else if (probe == 3) hipLaunchKernelGGL(igemm_pp2_kernel<3>, dim3(grid), dim3(512), 0, st, a);
-      else if (probe == 4) hipLaunchKernelGGL(igemm_pp2_kernel<4>, dim3(grid), dim3(512), 0, st, a);
-      else hipLaunchKernelGGL(igemm_pp2_kernel<0>, dim3(grid), dim3(512), 0, st, a);
-      return (int)hipGetLastError();
+      const int grid = ((M + 255) / 256) * (a.Ngemm / 256);
+      if (!no_rowblock && pp2h_ok(a)) DPA_EP_LAUNCH(igemm_pp2h_kernel, grid);
+      DPA_EP_LAUNCH(igemm_pp2_kernel, grid);
     }
     case 15: {
       if (!pp2h128_ok(a)) break;
-      const int grid = (a.N * a.Ho * a.Wo / 256) * (a.Ngemm / 128);
-      const int ep = no_fast_ep ? 0 : glds_ep_kind(a);
+      const int grid = (M / 256) * (a.Ngemm / 128);
       if (ep == 1) hipLaunchKernelGGL((igemm_pp2h_kernel<1, 128>), dim3(grid), dim3(512), 0, st, a);
       else if (ep == 2) hipLaunchKernelGGL((igemm_pp2h_kernel<2, 128>), dim3(grid), dim3(512), 0, st, a);
       else if (ep == 3) hipLaunchKernelGGL((igemm_pp2h_kernel<3, 128>), dim3(grid), dim3(512), 0, st, a);
@@ -2178,8 +1812,7 @@ DPA_API int dpa_igemm_glds(const IgemmArgs* args, int cfg, hipStream_t st) {
     }
     case 16: {
       if (!pp2h_ok(a) || a.Kpad < 9 * 64) break;
-      const int grid = (a.N * a.Ho * a.Wo / 256) * (a.Ngemm / 256);
-      const int ep = no_fast_ep ? 0 : glds_ep_kind(a);
+      const int grid = (M / 256) * (a.Ngemm / 256);
       if (ep == 1) hipLaunchKernelGGL((igemm_rb2_kernel<1, 256>), dim3(grid), dim3(512), 0, st, a);
       else if (ep == 2) hipLaunchKernelGGL((igemm_rb2_kernel<2, 256>), dim3(grid), dim3(512), 0, st, a);
       else if (ep == 3) hipLaunchKernelGGL((igemm_rb2_kernel<3, 256>), dim3(grid), dim3(512), 0, st, a);
@@ -2188,8 +1821,7 @@ DPA_API int dpa_igemm_glds(const IgemmArgs* args, int cfg, hipStream_t st) {
     }
     case 17: {
       if (!pp2h128_ok(a)) break;
-      const int grid = (a.N * a.Ho * a.Wo / 256) * (a.Ngemm / 128);
-      const int ep = no_fast_ep ? 0 : glds_ep_kind(a);
+      const int grid = (M / 256) * (a.Ngemm / 128);
       if (ep == 1) hipLaunchKernelGGL((igemm_rb2_kernel<1, 128>), dim3(grid), dim3(512), 0, st, a);
       else if (ep == 2) hipLaunchKernelGGL((igemm_rb2_kernel<2, 128>), dim3(grid), dim3(512), 0, st, a);
       else if (ep == 3) hipLaunchKernelGGL((igemm_rb2_kernel<3, 128>), dim3(grid), dim3(512), 0, st, a);
@@ -2200,24 +1832,22 @@ DPA_API int dpa_igemm_glds(const IgemmArgs* args, int cfg, hipStream_t st) {
     case 19: {
       const int BCt = cfg == 18 ? 128 : 256;
       if (!sl_ok(a, BCt)) break;
-      const int grid = (a.N * a.Ho * a.Wo / (cfg == 18 ? 512 : 256)) * (a.Ngemm / BCt);
-      const int ep = no_fast_ep ? 0 : glds_ep_kind(a);
-#define DPA_SL(BCv)                                                                                 \
-      if (ep == 1) hipLaunchKernelGGL((igemm_sl_kernel<1, BCv>), dim3(grid), dim3(512), 0, st, a); \
-      else if (ep == 2) hipLaunchKernelGGL((igemm_sl_kernel<2, BCv>), dim3(grid), dim3(512), 0, st, a); \
-      else if (ep == 3) hipLaunchKernelGGL((igemm_sl_kernel<3, BCv>), dim3(grid), dim3(512), 0, st, a); \
-      else hipLaunchKernelGGL((igemm_sl_kernel<0, BCv>), dim3(grid), dim3(512), 0, st, a);
-      if (cfg == 18) { DPA_SL(128) } else { DPA_SL(256) }
-#undef DPA_SL
-      return (int)hipGetLastError();
-    }
-    case 11: {
-      if (a.Ngemm % 256) break;
-      const int grid = ((a.N * a.Ho * a.Wo + 255) / 256) * (a.Ngemm / 256);
-      hipLaunchKernelGGL(igemm_glds32_kernel, dim3(grid), dim3(512), 0, st, a);
+      const int grid = (M / (cfg == 18 ? 512 : 256)) * (a.Ngemm / BCt);
+      if (cfg == 18) {
+        if (ep == 1) hipLaunchKernelGGL((igemm_sl_kernel<1, 128>), dim3(grid), dim3(512), 0, st, a);
+        else if (ep == 2) hipLaunchKernelGGL((igemm_sl_kernel<2, 128>), dim3(grid), dim3(512), 0, st, a);
+        else if (ep == 3) hipLaunchKernelGGL((igemm_sl_kernel<3, 128>), dim3(grid), dim3(512), 0, st, a);
+        else hipLaunchKernelGGL((igemm_sl_kernel<0, 128>), dim3(grid), dim3(512), 0, st, a);
+      } else {
+        if (ep == 1) hipLaunchKernelGGL((igemm_sl_kernel<1, 256>), dim3(grid), dim3(512), 0, st, a);
+        else if (ep == 2) hipLaunchKernelGGL((igemm_sl_kernel<2, 256>), dim3(grid), dim3(512), 0, st, a);
+        else if (ep == 3) hipLaunchKernelGGL((igemm_sl_kernel<3, 256>), dim3(grid), dim3(512), 0, st, a);
+        else hipLaunchKernelGGL((igemm_sl_kernel<0, 256>), dim3(grid), dim3(512), 0, st, a);
+      }
       return (int)hipGetLastError();
     }
     default: break;
   }
+#undef DPA_EP_LAUNCH
   return (int)hipErrorInvalidValue;
 }

@@ -654,9 +654,7 @@ class _EncFn(torch.autograd.Function):
         x = _v(x)
         N, H, W = x.shape[:3]
         st1, st2 = [], []
-        fuse1 = (l == 0 and c1.bn is None and c2.bn is None and c1.Cs == 8 and H % 2 == 0 and W % 2 == 0
-                 and x.is_contiguous() and K.dconv1_fusable(H, W, c1.Cout, c2.Cin, c2.Cout))
-        a = None if fuse1 else B.conv_fwd(c1, x, st=st1)
+        a = B.conv_fwd(c1, x, st=st1)
         if l in B.dense_skips:
             cat = None
             skip = torch.empty(N, H, W, c2.Cout, dtype=torch.bfloat16, device=x.device)
@@ -667,13 +665,7 @@ class _EncFn(torch.autograd.Function):
         # window codes (argmax + ReLU masks) for the backward: it then never re-reads the skip
         code = (torch.empty(N, H // 2, W // 2, c2.Cout, dtype=torch.uint8, device=x.device)
                 if H % 2 == 0 and W % 2 == 0 else None)
-        if fuse1:
-            # the level's whole forward in one kernel: conv1's output stays in an LDS row ring for
-            # conv2 (written once for the backward, never read back)
-            a = torch.empty(N, H, W, c1.Cout, dtype=torch.bfloat16, device=x.device)
-            K.dconv1_fwd(x, B.wf(c1), c1.Kf, c1.mod.bias, B.wf(c2), c2.Kf, c2.mod.bias, a, skip, pooled, code)
-        else:
-            B.conv_fwd(c2, a, skip, pool=pooled, pcode=code, st=st2)   # pool fused into the conv epilogue when streaming
+        B.conv_fwd(c2, a, skip, pool=pooled, pcode=code, st=st2)   # pool fused into the conv epilogue when streaming
         ctx.B, ctx.l = B, l
         ctx.x_needs_grad = l > 0
         ctx.has_code = code is not None

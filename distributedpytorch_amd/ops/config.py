@@ -1,0 +1,151 @@
+"""Kernel-dispatch configuration of the HIP engine: every environment switch, in ONE documented table.
+
+The engine picks a kernel family per layer automatically (``ops/kernels.py``); the switches below
+exist to fall back to a simpler path when triaging a problem on a GPU box, or to A/B launch geometry.
+They are read once, at import, from the variables named here and NOWHERE else: an environment
+variable outside :data:`KNOBS` / :data:`RUNTIME_ENV` cannot change which kernels run
+(``tests/test_kernel_config.py`` checks the package source and a fresh interpreter).  The run's
+non-default switches are logged once (:func:`log_once`; bench.py also puts them in its JSON line).
+
+Timing ablation (skipping kernel families to see what they cost; numerically WRONG) is not an
+environment switch: only :func:`..ops.kernels.set_timing_ablation` enables it, called explicitly by
+the measurement tools (``bench.py --timing-ablation``, ``tools/block_times.py``), and bench marks
+such a run invalid in its output.
+"""
+from __future__ import annotations
+
+import logging
+import os
+from dataclasses import dataclass, fields
+from typing import Dict, Mapping
+
+log = logging.getLogger("dpa.kernels")
+
+
+@dataclass(frozen=True)
+class Knob:
+    attr: str
+    env: str
+    default: object
+    doc: str
+
+
+def _flag_off(env):      # DPA_NO_X=1 turns feature X off
+    return lambda e: e.get(env, "0") != "1"
+
+
+KNOBS = (
+    # kernel families (a switch falls back to the next family / the generic register-staged GEMM)
+    Knob("halo", "DPA_NO_HALO", True, "row-halo conv3x3 (csrc/halo.hip) for <= 128-output-channel layers"),
+    Knob("stream", "DPA_NO_STREAM", True, "row-streaming conv3x3 / weight gradients (csrc/halo.hip) at 32/64 channels"),
+    Knob("glds", "DPA_NO_GLDS", True, "LDS-DMA implicit GEMMs (csrc/igemm_glds.hip) for the deep layers"),
+    Knob("glds128", "DPA_NO_GLDS128", True, "128-output-channel convs on the row-block GEMM instead of the row-halo conv"),
+    Knob("glds_bn", "DPA_NO_GLDS_BN", True, "BatchNorm partial sums in the row-block GEMM epilogue"),
+    Knob("glds_rb2", "DPA_GLDS_RB2", False, "row-block GEMMs with two MFMA phases per K-tile (cfg 16/17)"),
+    Knob("wgrad_gemm", "DPA_NO_WGRAD_GEMM", True, "deep weight gradients as a dense LDS-DMA GEMM (csrc/wgrad_gemm.hip)"),
+    Knob("side_wgrad", "DPA_NO_SIDE_WGRAD", True, "weight gradients on a side HIP stream, overlapping the dgrad chain"),
+    # fusions
+    Knob("fused_head", "DPA_NO_FUSED_HEAD", True, "segmentation head + loss partials in the last decoder conv's epilogue"),
+    Knob("fused_bn", "DPA_NO_FUSED_BN", True, "BatchNorm statistics in the producing streaming conv's epilogue"),
+    Knob("fold_bn_eval", "DPA_NO_FOLD_BN", True, "eval-mode BatchNorm folded into the conv weights"),
+    Knob("fused_bwd", "DPA_NO_FUSED_BWD", True, "fused conv backward (dgrad + weight gradient, csrc/bwd_stream.hip)"),
+    Knob("fused_head_bwd", "DPA_NO_FUSED_HEAD_BWD", True, "head backward folded into the last conv's fused backward"),
+    Knob("fused_halves", "DPA_NO_FUSED_HALVES", True, "concat-input convs: one fused backward per half"),
+    Knob("fused_pool_bwd", "DPA_NO_FUSED_POOL_BWD", True, "max-pool backward folded into the fused backward"),
+    Knob("fused_bn_bwd", "DPA_FUSED_BN_BWD", True, "BatchNorm backward formed in the fused backward's loader (=0 opts out)"),
+    Knob("fused_w1", "DPA_FUSED_W1", False, "first conv's weight gradient in the pool-mode fused backward (slower at b256)"),
+    Knob("fused_deconv", "DPA_NO_FUSED_DECONV", True, "full-resolution transposed conv: fused forward / backward"),
+    # launch geometry / streams
+    Knob("side_priority", "DPA_SIDE_PRIORITY", 0, "HIP priority of the weight-gradient side stream (torch convention)"),
+    Knob("wgrad_stream_blocks", "DPA_WGRAD_STREAM_BLOCKS", 2048, "target workgroups of a row-streaming weight gradient"),
+    Knob("wgrad_gemm_blocks", "DPA_WGRAD_GEMM_BLOCKS", 768, "target workgroups of a dense-GEMM weight gradient"),
+    Knob("bwd_blocks", "DPA_BWD_BLOCKS", 1024, "minimum workgroups of a fused backward launch"),
+    Knob("bwd_blocks_small", "DPA_BWD_BLOCKS_SMALL", 512, "the same for launches over < 2^25 pixels"),
+)
+
+# process / launcher environment (not kernel dispatch): documented here so the allow-list is complete
+RUNTIME_ENV = {
+    "DPA_LIB_PATH": "load the HIP kernel library from this path instead of distributedpytorch_amd/_C",
+    "DPA_DEBUG_SYNC": "synchronise after every kernel launch (fault triage; same as --debug-sync)",
+    "DPA_ROCTX": "emit roctx ranges (same as --trace-ranges)",
+    "DPA_SAME_DEVICE": "multi-rank rehearsal: every rank on cuda:0 (tests, one-GPU boxes)",
+    "DPA_DIST_BACKEND": "process-group backend override (gloo for the one-GPU rehearsal)",
+    "DPA_DP_NATIVE_COMM": "-t DP: the native single-process RCCL clique (=0: torch collectives)",
+    "DPA_ARCH": "tools/build_hip.py: --offload-arch (default gfx950)",
+}
+
+# the DPA_NO_* switches turn a default-on feature off; the others carry their value
+_NEGATED = {k.env for k in KNOBS if k.env.startswith("DPA_NO_")}
+
+
+def _read(k: Knob, env: Mapping[str, str]):
+    raw = env.get(k.env)
+    if raw is None:
+        return k.default
+    if isinstance(k.default, bool):
+        on = raw == "1"
+        return (not on) if k.env in _NEGATED else on
+    return int(raw)
+
+
+@dataclass(frozen=True)
+class KernelConfig:
+    halo: bool = True
+    stream: bool = True
+    glds: bool = True
+    glds128: bool = True
+    glds_bn: bool = True
+    glds_rb2: bool = False
+    wgrad_gemm: bool = True
+    side_wgrad: bool = True
+    fused_head: bool = True
+    fused_bn: bool = True
+    fold_bn_eval: bool = True
+    fused_bwd: bool = True
+    fused_head_bwd: bool = True
+    fused_halves: bool = True
+    fused_pool_bwd: bool = True
+    fused_bn_bwd: bool = True
+    fused_w1: bool = False
+    fused_deconv: bool = True
+    side_priority: int = 0
+    wgrad_stream_blocks: int = 2048
+    wgrad_gemm_blocks: int = 768
+    bwd_blocks: int = 1024
+    bwd_blocks_small: int = 512
+    bwd_blocks_set: bool = False          # DPA_BWD_BLOCKS given explicitly: applies to every launch
+
+    @classmethod
+    def from_env(cls, env: Mapping[str, str] = None) -> "KernelConfig":
+        env = os.environ if env is None else env
+        vals = {k.attr: _read(k, env) for k in KNOBS}
+        # dependent switches: the fused-backward modes need the fused backward
+        for dep in ("fused_head_bwd", "fused_halves", "fused_pool_bwd", "fused_bn_bwd"):
+            vals[dep] = vals[dep] and vals["fused_bwd"]
+        vals["fused_w1"] = vals["fused_w1"] and vals["fused_pool_bwd"]
+        vals["bwd_blocks_set"] = "DPA_BWD_BLOCKS" in env
+        return cls(**vals)
+
+    def non_default(self) -> Dict[str, object]:
+        ref = KernelConfig()
+        return {f.name: getattr(self, f.name) for f in fields(self) if getattr(self, f.name) != getattr(ref, f.name)}
+
+    def describe(self) -> str:
+        nd = self.non_default()
+        return "kernel config: defaults" if not nd else "kernel config: " + ", ".join(f"{k}={v}" for k, v in nd.items())
+
+
+def allowed_env() -> Dict[str, str]:
+    """Every DPA_* variable the package reads, with its meaning."""
+    out = {k.env: k.doc for k in KNOBS}
+    out.update(RUNTIME_ENV)
+    return out
+
+
+_logged = [False]
+
+
+def log_once(cfg: KernelConfig) -> None:
+    if not _logged[0]:
+        _logged[0] = True
+        log.info(cfg.describe())

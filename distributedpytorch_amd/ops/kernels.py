@@ -14,12 +14,12 @@ Variant blocks (north-star DoubleConv with BatchNorm, bilinear Up): ``bn_fwd`` /
 from __future__ import annotations
 
 import ctypes
-import os
 from typing import Optional
 
 import torch
 
 from . import _lib
+from . import config as _config
 
 c_int, c_ll, c_void_p = ctypes.c_int, ctypes.c_longlong, ctypes.c_void_p
 
@@ -49,11 +49,6 @@ class BwdArgs(ctypes.Structure):
                [("pcode", c_void_p), ("dpool", c_void_p), ("ldp", c_int)] + \
                [("x1", c_void_p), ("slab1", c_void_p), ("bslab1", c_void_p), ("x1bytes", ctypes.c_uint)] + \
                [("z", c_void_p), ("bncoef", c_void_p), ("bnslab", c_void_p)]
-
-
-class DconvArgs(ctypes.Structure):
-    _fields_ = [(n, c_void_p) for n in ("x", "w1", "b1", "w2", "b2", "a1", "y", "pool", "pcode")] + \
-               [(n, c_int) for n in ("N", "H", "W", "ldy", "ldp", "kp1", "kp2", "rh")]
 
 
 class PackDesc(ctypes.Structure):
@@ -89,66 +84,50 @@ def round_up(x: int, m: int) -> int:
 
 
 _MAX_BYTES = 2 ** 31 - 1024   # kernels address activations through 32-bit buffer offsets
-# row-halo kernels (csrc/halo.hip) for full-resolution low-channel convs; DPA_NO_HALO=1 disables
-USE_HALO = os.environ.get("DPA_NO_HALO", "0") != "1"
-# row-streaming conv3x3 (weights resident, 4-row LDS ring); DPA_NO_STREAM=1 disables
-USE_STREAM = os.environ.get("DPA_NO_STREAM", "0") != "1"
-USE_GLDS = os.environ.get("DPA_NO_GLDS", "0") != "1"
-# A/B: tap-major K-tile order in the LDS-DMA kernels (default slice-major, csrc/igemm_glds.hip ktile_coords)
-GLDS_TAP_MAJOR = os.environ.get("DPA_GLDS_TAP_MAJOR", "0") == "1"
-# A/B: no persistent LDS-DMA kernel for the short-K deep layers (csrc/igemm_glds.hip cfg 8)
-GLDS_NO_PERS = os.environ.get("DPA_GLDS_NO_PERS", "0") == "1"
-# A/B: LDS-DMA GEMM without the all-fragments-first K-step schedule
-GLDS_NO_PRELOAD = os.environ.get("DPA_GLDS_NO_PRELOAD", "0") == "1"
-# A/B: the 2-stage 256x256 LDS-DMA kernel instead of the ping-pong steady-state one (csrc/igemm_glds.hip cfg 14)
-GLDS_NO_PP = os.environ.get("DPA_GLDS_NO_PP", "0") == "1"
-# A/B: the ping-pong kernel without row-block pixel staging (csrc/igemm_glds.hip igemm_pp2h_kernel)
-GLDS_NO_ROWBLOCK = os.environ.get("DPA_GLDS_NO_ROWBLOCK", "0") == "1"
-# row-block GEMMs with two MFMA phases per K-tile (csrc/igemm_glds.hip igemm_rb2_kernel, cfg 16 / 17)
-# instead of pp2h's four quadrant phases
-GLDS_RB2 = os.environ.get("DPA_GLDS_RB2", "0") == "1"
-# 128-channel convs on the row-block ping-pong GEMM (csrc/igemm_glds.hip cfg 15, igemm_pp2h_kernel<EP, 128>)
-# instead of the row-halo kernel: 10-15 % faster on every 128-output-channel 3x3 conv / dgrad of the 512^2
-# UNet (profiles/kbench_glds_rowblock128_b256_r03.txt); DPA_NO_GLDS128=1 disables (A/B)
-USE_GLDS128 = os.environ.get("DPA_NO_GLDS128", "0") != "1"
-# BatchNorm partial sums in the row-block GEMM epilogue (deep BN layers); DPA_NO_GLDS_BN=1 disables (A/B)
-USE_GLDS_BN = os.environ.get("DPA_NO_GLDS_BN", "0") != "1"
-# conv weight gradients on a side HIP stream, overlapping each block's dgrad chain (models/hip_unet.py)
-SIDE_WGRAD = os.environ.get("DPA_NO_SIDE_WGRAD", "0") != "1"
-# HIP stream priority of the weight-gradient side stream (torch convention: lower = higher priority,
-# 0 = the default stream's priority)
-SIDE_PRIORITY = int(os.environ.get("DPA_SIDE_PRIORITY", "0"))
-# row-streaming weight-gradient tile override (csrc/halo.hip dpa_wgrad_stream cfg; 0 = auto)
-WGRAD_STREAM_CFG = int(os.environ.get("DPA_WGRAD_STREAM_CFG", "0"))
-HALO_CFG = int(os.environ.get("DPA_HALO_CFG", "0"))    # 0 = auto (csrc/halo.hip dpa_igemm_halo)
-# segmentation head + loss partials fused into the last decoder conv; DPA_NO_FUSED_HEAD=1 disables
-USE_FUSED_HEAD = os.environ.get("DPA_NO_FUSED_HEAD", "0") != "1"
-# BatchNorm batch statistics in the producing streaming conv's epilogue; DPA_NO_FUSED_BN=1 disables
-USE_FUSED_BN = os.environ.get("DPA_NO_FUSED_BN", "0") != "1"
-# eval-mode BatchNorm folded into the preceding conv's weights/bias (models/hip_unet.py); DPA_NO_FOLD_BN=1 disables
-FOLD_BN_EVAL = os.environ.get("DPA_NO_FOLD_BN", "0") != "1"
-# fused conv backward (dgrad + weight/bias gradient in one row-streaming pass, csrc/bwd_stream.hip)
-# for the full-resolution 32/64-channel convs; DPA_NO_FUSED_BWD=1 -> separate dgrad / wgrad kernels
-USE_FUSED_BWD = os.environ.get("DPA_NO_FUSED_BWD", "0") != "1"
-# the segmentation head's backward folded into the last decoder conv's fused backward (the head
-# gradient is formed from y on load, never stored); DPA_NO_FUSED_HEAD_BWD=1 -> separate head_bwd
-USE_FUSED_HEAD_BWD = USE_FUSED_BWD and os.environ.get("DPA_NO_FUSED_HEAD_BWD", "0") != "1"
-# the max-pool backward folded into the full-resolution encoder conv2's fused backward; DPA_NO_FUSED_POOL_BWD=1 disables
-# concat convs whose 2C-input fused backward does not exist: two fused passes, one per half
-USE_FUSED_HALVES = USE_FUSED_BWD and os.environ.get("DPA_NO_FUSED_HALVES", "0") != "1"
-USE_FUSED_POOL_BWD = USE_FUSED_BWD and os.environ.get("DPA_NO_FUSED_POOL_BWD", "0") != "1"
+# dispatch switches: ONE table, read once from the documented DPA_* variables (ops/config.py)
+CFG = _config.KernelConfig.from_env()
+USE_HALO = CFG.halo                    # row-halo kernels (csrc/halo.hip)
+USE_STREAM = CFG.stream                # row-streaming conv3x3 (weights resident, row ring)
+USE_GLDS = CFG.glds                    # LDS-DMA GEMMs (csrc/igemm_glds.hip)
+# row-block GEMMs with two MFMA phases per K-tile (igemm_rb2_kernel, cfg 16 / 17) instead of pp2h's four
+GLDS_RB2 = CFG.glds_rb2
+# 128-channel convs on the row-block ping-pong GEMM (cfg 15) instead of the row-halo conv: 10-15 % faster
+# on every 128-output-channel 3x3 conv / dgrad of the 512^2 UNet (profiles/kbench_glds_rowblock128_b256_r03.txt)
+USE_GLDS128 = CFG.glds128
+USE_GLDS_BN = CFG.glds_bn              # BatchNorm partial sums in the row-block GEMM epilogue
+SIDE_WGRAD = CFG.side_wgrad            # weight gradients on a side stream (models/hip_unet.py)
+SIDE_PRIORITY = CFG.side_priority      # its HIP priority (torch convention: lower = higher, 0 = default)
+WGRAD_STREAM_CFG = 0                   # row-streaming weight-gradient tile override (kbench A/B; 0 = auto)
+HALO_CFG = 0                           # row-halo conv tile override (kbench A/B; 0 = auto)
+USE_FUSED_HEAD = CFG.fused_head        # segmentation head + loss partials in the last decoder conv
+USE_FUSED_BN = CFG.fused_bn            # BatchNorm statistics in the producing streaming conv
+FOLD_BN_EVAL = CFG.fold_bn_eval        # eval-mode BatchNorm folded into the conv weights
+# fused conv backward (dgrad + weight/bias gradient in one row-streaming pass, csrc/bwd_stream.hip) for
+# the full-resolution 32/64-channel convs, and its modes: the head backward folded in, concat convs as
+# one fused pass per half, the max-pool backward folded in, BatchNorm backward formed in the loader
+USE_FUSED_BWD = CFG.fused_bwd
+USE_FUSED_HEAD_BWD = CFG.fused_head_bwd
+USE_FUSED_HALVES = CFG.fused_halves
+USE_FUSED_POOL_BWD = CFG.fused_pool_bwd
+USE_FUSED_BN_BWD = CFG.fused_bn_bwd
 # the first encoder conv's weight gradient folded into the pool-mode backward of the second: opt-in,
 # slower at batch 256 (6.05 ms vs 5.3 ms for the two kernels it replaces; see csrc/bwd_stream.hip)
-USE_FUSED_W1 = USE_FUSED_POOL_BWD and os.environ.get("DPA_FUSED_W1", "0") == "1"
-# BatchNorm backward formed in the fused backward's loader (csrc/bwd_stream.hip BN modes) instead of a
-# bn_bwd_apply pass + separate dgrad / weight-gradient passes over the dz it wrote; DPA_FUSED_BN_BWD=0 opts out
-USE_FUSED_BN_BWD = USE_FUSED_BWD and os.environ.get("DPA_FUSED_BN_BWD", "1") == "1"
+USE_FUSED_W1 = CFG.fused_w1
+
+# TIMING ABLATION ONLY (numerically wrong results): the listed kernel families are skipped so a bench
+# run measures what they cost end to end.  Never read from the environment: set_timing_ablation() is
+# called explicitly by bench.py --timing-ablation and tools/block_times.py.  Categories: stream, halo,
+# glds, wgrad, wgrad_deep, bwd, deconv
+_ABLATE = frozenset()
+ABLATE_CATEGORIES = frozenset({"stream", "halo", "glds", "wgrad", "wgrad_deep", "bwd", "deconv"})
 
 
-# TIMING ABLATION ONLY (numerically wrong results): DPA_ABLATE=halo,glds,... skips the launches of the
-# listed kernel families so a bench run measures how much of the step they cost end to end
-# (tools/gpu_ablate.sh); categories: stream, halo, glds, wgrad, wgrad_deep, bwd, deconv
-_ABLATE = frozenset(v for v in os.environ.get("DPA_ABLATE", "").split(",") if v)
+def set_timing_ablation(categories) -> None:
+    global _ABLATE
+    cats = frozenset(categories or ())
+    unknown = cats - ABLATE_CATEGORIES
+    assert not unknown, f"unknown ablation categories {sorted(unknown)}"
+    _ABLATE = cats
 
 
 def _extent_bytes(N, H, W, C, ld):
@@ -294,7 +273,7 @@ def igemm(x: torch.Tensor, wpacked: torch.Tensor, y: torch.Tensor, *, Ngemm: int
     # 128^2, 2542 vs 2948 us at 256^2); the LDS-DMA kernel takes what the halo kernel cannot
     # (64^2 and smaller grids, > 128 output channels)
     # whole-row 256-pixel tiles, slice-major K, N % 256 != 0 (N % 256 == 0 takes cfg 14's 256-channel form)
-    rb128 = (path == "auto" and USE_GLDS128 and USE_GLDS and not GLDS_TAP_MAJOR and conv3 and pad == 1 and
+    rb128 = (path == "auto" and USE_GLDS128 and USE_GLDS and conv3 and pad == 1 and
              (Hs, Ws) == (Ho, Wo) and Kpad == 9 * Cs and Cs % 64 == 0 and (Wo in (32, 64, 128) or Wo % 256 == 0) and
              (Ho * Wo) % 256 == 0 and Ngemm % 128 == 0 and Ngemm % 256 != 0)
     if a is not None and not rb128 and (path == "halo" or (path == "auto" and USE_HALO and conv3 and Cs % 32 == 0 and Ngemm <= 128)):
@@ -319,10 +298,9 @@ def igemm(x: torch.Tensor, wpacked: torch.Tensor, y: torch.Tensor, *, Ngemm: int
             assert n0 == 0, "row-block BN statistics refused after the first chunk"
             a.bnslab, gslab = None, None
         if path == "glds" or (path == "auto" and glds_ok):
-            no_pers = GLDS_NO_PERS or not persistent
+            no_pers = not persistent
             auto_cfg = ((131072 if GLDS_RB2 else 15) if rb128 else
-                        16 * GLDS_TAP_MAJOR + 32 * no_pers + 64 * GLDS_NO_PRELOAD + 128 * GLDS_NO_PP +
-                        8192 * GLDS_NO_ROWBLOCK + 16384 * GLDS_RB2)
+                        32 * no_pers + 16384 * GLDS_RB2)
             err = L.dpa_igemm_glds(ctypes.byref(a), c_int(variant if path == "glds" else auto_cfg), st)
             if err == 0:
                 continue
@@ -361,8 +339,6 @@ def wgrad(A: torch.Tensor, B: torch.Tensor, *, kind: int, grid, M: int, Nc: int,
     if (path == "gemm" or (path == "auto" and wgrad_gemm_eligible(M, Nc, grid))) and kind == 0 and cfg == 0 \
             and A.shape[1:3] == B.shape[1:3] == tuple(grid[1:]):
         return _wgrad_gemm(A, B, grid=grid, M=M, Nc=Nc, gw=gw, gb=gb, Nreal=Nreal)
-    if (path == "rows" or (path == "auto" and wgrad_rows_eligible(M, Nc, grid[2]))) and kind == 0 and cfg == 0:
-        return _wgrad_rows(A, B, grid=grid, M=M, Nc=Nc, gw=gw, gb=gb, Nreal=Nreal)
     if path in ("auto", "stream") and kind == 0 and cfg == 0 and (USE_STREAM or path == "stream") \
             and grid[2] >= 8 and M % 32 == 0 and (Nc % 32 == 0 or Nc == 8):
         return _wgrad_stream(A, B, grid=grid, M=M, Nc=Nc, gw=gw, gb=gb, Nreal=Nreal)
@@ -415,28 +391,18 @@ def wgrad(A: torch.Tensor, B: torch.Tensor, *, kind: int, grid, M: int, Nc: int,
                                   c_int(Nreal), c_int(1 if kind == 1 else 0), st), "wgrad_reduce")
 
 
-WGRAD_STREAM_BLOCKS = int(os.environ.get("DPA_WGRAD_STREAM_BLOCKS", "2048"))
-# deep-layer weight gradients on the LDS-DMA row pipeline (csrc/wgrad_rows.hip): 128 x 64 x 9-tap
-# tiles.  Opt-in (DPA_WGRAD_ROWS=1): end to end equal to the row-streaming kernel at batch 256
-# (profiles/ab_wgrad_rows_b256_r03.txt); DPA_WGRAD_ROWS_DEPTH = row bundles in flight
-USE_WGRAD_ROWS = os.environ.get("DPA_WGRAD_ROWS", "0") == "1"
-WGRAD_ROWS_DEPTH = int(os.environ.get("DPA_WGRAD_ROWS_DEPTH", "2"))
+WGRAD_STREAM_BLOCKS = CFG.wgrad_stream_blocks
 
 
 def wgrad_multi_eligible(M: int, Nc: int, W: int) -> bool:
     """Can :func:`wgrad_multi` take this conv3x3 weight gradient (row-streaming or row kernels)?"""
-    return (wgrad_rows_eligible(M, Nc, W) or (USE_STREAM and W >= 8 and M % 32 == 0 and (Nc % 32 == 0 or Nc == 8))) \
-        and "wgrad" not in _ABLATE
-
-
-def wgrad_rows_eligible(M: int, Nc: int, W: int) -> bool:
-    return USE_WGRAD_ROWS and M % 128 == 0 and Nc % 64 == 0 and W >= 48
+    return USE_STREAM and W >= 8 and M % 32 == 0 and (Nc % 32 == 0 or Nc == 8) and "wgrad" not in _ABLATE
 
 
 # deep-layer weight gradients as a dense 256x256 LDS-DMA GEMM on the ping-pong schedule
 # (csrc/wgrad_gemm.hip); DPA_NO_WGRAD_GEMM=1 falls back to the row-streaming kernel
-USE_WGRAD_GEMM = os.environ.get("DPA_NO_WGRAD_GEMM", "0") != "1"
-WGRAD_GEMM_BLOCKS = int(os.environ.get("DPA_WGRAD_GEMM_BLOCKS", "768"))
+USE_WGRAD_GEMM = CFG.wgrad_gemm
+WGRAD_GEMM_BLOCKS = CFG.wgrad_gemm_blocks
 
 
 def wgrad_gemm_eligible(M: int, Nc: int, grid) -> bool:
@@ -481,36 +447,6 @@ def _wgrad_gemm(A, B, *, grid, M, Nc, gw, gb, Nreal, blocks: int = 0, tabs=None,
                               c_int(Nreal), c_int(0), st), "wgrad_reduce(gemm)")
 
 
-def _wgrad_rows(A, B, *, grid, M, Nc, gw, gb, Nreal, rh: int = 0, depth: int = 0, tabs=None):
-    """conv3x3 weight (+bias) gradient of the deep layers (M = Cout % 128 == 0, Nc = Cin % 64 == 0):
-    one workgroup per (image, row segment, 64-pixel strip) x (128 x 64 channel tile), LDS-DMA rows."""
-    NA, HA, WA, CA, lda = _nhwc(A, "wgrad_rows.A")
-    NB, HB, WB, CB, ldb = _nhwc(B, "wgrad_rows.B")
-    N, Hg, Wg = grid
-    assert (HA, WA) == (Hg, Wg) == (HB, WB) and CA >= M and CB >= Nc
-    assert (NA == NB == N) or (tabs is not None and tabs[0].numel() == tabs[1].numel() == N)
-    assert gw.dtype == torch.float32 and gw.is_contiguous() and gw.numel() == M * Nreal * 9
-    tiles = (M // 128) * (Nc // 64)
-    strips = -(-Wg // 64)
-    if rh <= 0:
-        # whole images per workgroup unless that leaves fewer than ~2 workgroups per CU
-        segs = max(1, min(Hg, -(-512 // max(1, N * strips * tiles))))
-        rh = -(-Hg // segs)
-    splits = N * -(-Hg // rh) * strips
-    slab = torch.empty(splits * 9 * M * Nc + splits * M, dtype=torch.float32, device=A.device)
-    bslab = slab[splits * 9 * M * Nc:] if gb is not None else None
-    a = WgradArgs(A.data_ptr(), B.data_ptr(), slab.data_ptr(), None if bslab is None else bslab.data_ptr(), lda, ldb,
-                  N, Hg, Wg, HA, WA, HB, WB, M, Nc, 1, 1, 3, 0, splits, _extent_bytes(1, HA, WA, CA, lda),
-                  _extent_bytes(1, HB, WB, CB, ldb))
-    if tabs is not None:
-        a.atab, a.btab = tabs[0].data_ptr(), tabs[1].data_ptr()
-    L = _lib.lib()
-    st = _stream(A)
-    _check(L.dpa_wgrad_rows(ctypes.byref(a), c_int(rh), c_int(depth or WGRAD_ROWS_DEPTH), st), "wgrad_rows")
-    _check(L.dpa_wgrad_reduce(_p(slab), _p(bslab), _p(gw), _p(gb), c_int(splits), c_int(9), c_int(M), c_int(Nc),
-                              c_int(Nreal), c_int(0), st), "wgrad_reduce(rows)")
-
-
 def _image_table(ts, C_min: int, name: str):
     """Device array of per-image base pointers over the images of tensors ``ts`` (same H, W, ld)."""
     ptrs, geo = [], None
@@ -540,8 +476,6 @@ def wgrad_multi(As, Bs, *, M: int, Nc: int, gw: torch.Tensor, gb: Optional[torch
     if wgrad_gemm_eligible(M, Nc, (N, H, W)) and len(sizes) == 1 and min(sizes) * (H * W // 64) >= 64:
         return _wgrad_gemm(As[0], Bs[0], grid=(N, H, W), M=M, Nc=Nc, gw=gw, gb=gb, Nreal=Nreal, tabs=tabs,
                            group=sizes.pop())
-    if wgrad_rows_eligible(M, Nc, W):
-        return _wgrad_rows(As[0], Bs[0], grid=(N, H, W), M=M, Nc=Nc, gw=gw, gb=gb, Nreal=Nreal, tabs=tabs)
     return _wgrad_stream(As[0], Bs[0], grid=(N, H, W), M=M, Nc=Nc, gw=gw, gb=gb, Nreal=Nreal, tabs=tabs)
 
 
@@ -590,14 +524,14 @@ def _wgrad_stream(A, B, *, grid, M, Nc, gw, gb, Nreal, tabs=None):
 # ------------------------------------------------------------------------------- fused conv backward
 # minimum workgroups of a fused backward launch (image column strips are split into row segments
 # below it); more segments = more fp32 weight-gradient slab rows to reduce
-BWD_BLOCKS = int(os.environ.get("DPA_BWD_BLOCKS", "1024"))
+BWD_BLOCKS = CFG.bwd_blocks
 # launches over fewer than BWD_SMALL_PIXELS output pixels (pipeline microbatches, small batches) aim at
 # BWD_BLOCKS_SMALL: each launch's slab rows are reduced separately, and at 1024 blocks per microbatch the
 # reductions read 8x the single-batch bytes (2 stages x 8 microbatches: 2690 -> 2760 img/s at 512,
 # 256 worse; profiles/knobs_r03_end.txt).  DPA_BWD_BLOCKS set explicitly applies to every launch.
-BWD_BLOCKS_SMALL = int(os.environ.get("DPA_BWD_BLOCKS_SMALL", "512"))
+BWD_BLOCKS_SMALL = CFG.bwd_blocks_small
 BWD_SMALL_PIXELS = 1 << 25
-_BWD_BLOCKS_SET = "DPA_BWD_BLOCKS" in os.environ
+_BWD_BLOCKS_SET = CFG.bwd_blocks_set
 def _strips_ok(W: int, bp: int) -> bool:
     """Whole strips, or a ragged last one that keeps >= 85 % of the strip pixels useful."""
     t = -(-W // bp)
@@ -756,46 +690,6 @@ def conv_bwd_fused(g: Optional[torch.Tensor], x: torch.Tensor, wd: torch.Tensor,
     return (out, (bnslab, nblk)) if bnslab is not None else out
 
 
-# ------------------------------------------------------------------------- fused first-level forward
-# opt-in: measured equal to the two streaming kernels it replaces (tools/ab_dconv.sh: 2623-2649 img/s
-# either way; 4.18 ms vs 1.40 + 2.73 ms) -- those kernels are bound by per-row latency, not by the
-# a1 re-read the fusion removes
-USE_FUSED_DCONV1 = os.environ.get("DPA_FUSED_DCONV1", "0") == "1"
-DCONV1_BP = int(os.environ.get("DPA_DCONV1_BP", "0"))      # pixel strip of the fused kernel (0 = auto)
-
-
-def dconv1_fusable(H: int, W: int, c1_out: int, c2_in: int, c2_out: int) -> bool:
-    return USE_FUSED_DCONV1 and W % 64 == 0 and H % 2 == 0 and c1_out == c2_in == c2_out == 32 and H * W * 64 < 2 ** 31
-
-
-def dconv1_fwd(x8: torch.Tensor, w1: torch.Tensor, kp1: int, b1: torch.Tensor, w2: torch.Tensor, kp2: int,
-               b2: torch.Tensor, a1: torch.Tensor, y: torch.Tensor, pool: torch.Tensor,
-               pcode: Optional[torch.Tensor] = None, target_blocks: int = 1024):
-    """The first encoder level's forward in one kernel (csrc/dconv_fwd.hip): a1 = relu(conv3x3(x8)),
-    y = relu(conv3x3(a1)) into ``y`` (the concat-buffer half), its 2x2 max-pool into ``pool`` and the
-    window codes into ``pcode``; a1 is kept in an LDS row ring between the convs and written once
-    (the backward needs it).  Bitwise equal to igemm_stream8 followed by igemm_stream + pool."""
-    assert x8.dtype == torch.bfloat16 and x8.is_contiguous() and x8.dim() == 4 and x8.shape[3] == 8
-    N, H, W, _ = x8.shape
-    assert a1.is_contiguous() and tuple(a1.shape) == (N, H, W, 32) and a1.dtype == torch.bfloat16
-    Ny, Hy, Wy, Cy, ldy = _nhwc(y, "dconv1.y")
-    Np, Hp, Wp, Cp, ldp = _nhwc(pool, "dconv1.pool")
-    assert (Ny, Hy, Wy) == (N, H, W) and Cy >= 32 and (Np, Hp, Wp) == (N, H // 2, W // 2) and Cp >= 32
-    if pcode is not None:
-        assert pcode.dtype == torch.uint8 and pcode.is_contiguous() and tuple(pcode.shape) == (N, H // 2, W // 2, 32)
-    assert w1.dtype == w2.dtype == torch.bfloat16 and w1.numel() >= 32 * kp1 and w2.numel() >= 32 * kp2
-    assert b1.dtype == b2.dtype == torch.float32 and b1.numel() >= 32 and b2.numel() >= 32
-    bp = DCONV1_BP if DCONV1_BP in (64, 128) else 64
-    strips = W // bp
-    segs = max(1, min(H // 2, -(-target_blocks // max(1, N * strips))))
-    rh = -(-H // segs)
-    rh += rh & 1
-    a = DconvArgs(x8.data_ptr(), w1.data_ptr(), b1.data_ptr(), w2.data_ptr(), b2.data_ptr(), a1.data_ptr(),
-                  y.data_ptr(), pool.data_ptr(), None if pcode is None else pcode.data_ptr(),
-                  N, H, W, ldy, ldp, kp1, kp2, rh)
-    _check(_lib.lib().dpa_dconv1_fwd(ctypes.byref(a), c_int(bp), _stream(x8)), "dconv1_fwd")
-
-
 # ------------------------------------------------------------------------------------------ aux
 def input_nhwc8(x: torch.Tensor) -> torch.Tensor:
     assert x.dtype == torch.float32 and x.dim() == 4 and x.shape[1] <= 8
@@ -886,7 +780,7 @@ def head_bwd(y: torch.Tensor, w: torch.Tensor, b: torch.Tensor, t: torch.Tensor,
 
 
 # ------------------------------------------------------------------------------------- fused deconv bwd
-USE_FUSED_DECONV = os.environ.get("DPA_NO_FUSED_DECONV", "0") != "1"
+USE_FUSED_DECONV = CFG.fused_deconv
 DECONV_BWD_SHAPES = ((64, 32), (128, 64))
 
 

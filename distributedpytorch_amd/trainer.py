@@ -416,6 +416,9 @@ def train(cfg: TrainConfig):
         load_model_state(model, cfg.load)
     strat = build_strategy(cfg, model)
     log.info(f"strategy={strat.name} backend={resolve_backend(cfg.backend, strat.device, cfg.dtype)} device={strat.device}")
+    if resolve_backend(cfg.backend, strat.device, cfg.dtype) == "hip":
+        from .ops import kernels as _K
+        log.info(_K.CFG.describe())        # the run's kernel switches, once (ops/config.py)
 
     train_set, val_set = build_datasets(cfg, strat.device)
     dp_ranks = world if strat.name == "DDP" else 1

@@ -125,19 +125,14 @@ def test_conv3x3_dgrad_masked(hip_lib, N, H, W, Cin, Cout, path):
 
 
 @pytest.mark.parametrize("N,H,W,Cin,Cout,var", [
-    (2, 9, 13, 128, 256, 1), (1, 16, 16, 256, 256, 1), (2, 9, 13, 64, 128, 2), (1, 16, 16, 256, 512, 3),
-    (2, 7, 11, 128, 128, 4), (1, 32, 32, 64, 256, 0), (2, 9, 13, 128, 256, 5), (1, 16, 16, 64, 128, 6),
-    (2, 9, 13, 256, 128, 6), (3, 11, 7, 512, 256, 3), (3, 11, 7, 512, 256, 19),
-    # persistent kernels (one workgroup per CU, several tiles each when tiles > CUs)
-    (2, 9, 13, 128, 256, 8), (1, 16, 16, 256, 512, 8), (2, 9, 13, 64, 128, 9), (2, 7, 11, 256, 256, 10),
-    (2, 128, 160, 128, 512, 8), (2, 128, 160, 256, 256, 9),
-    # 32x32x16 MFMA variant
-    (2, 9, 13, 128, 256, 11), (1, 16, 16, 256, 512, 11), (3, 11, 7, 512, 256, 11),
-    # ping-pong variant
-    (2, 9, 13, 128, 256, 7), (1, 16, 16, 256, 256, 7), (3, 11, 7, 512, 256, 7), (2, 5, 6, 256, 512, 7),
+    (2, 9, 13, 128, 256, 1), (1, 16, 16, 256, 256, 1), (2, 9, 13, 64, 128, 2), (2, 7, 11, 128, 128, 4),
+    (1, 32, 32, 64, 256, 0), (3, 11, 7, 512, 256, 0),
+    # persistent kernel (one workgroup per CU, several tiles each when tiles > CUs)
+    (2, 9, 13, 128, 256, 8), (1, 16, 16, 256, 512, 8), (2, 128, 160, 128, 512, 8),
+    # ping-pong kernel with per-K-tile staging (shapes the row-block form does not take)
+    (2, 9, 13, 128, 256, 14), (1, 16, 16, 256, 256, 14), (3, 11, 7, 512, 256, 14), (2, 5, 6, 256, 512, 14),
     # >= 4 channel tiles: grouped tile order, full and partial groups of 8 pixel tiles
-    (1, 16, 16, 64, 1024, 3), (2, 40, 40, 64, 1024, 3), (2, 40, 40, 64, 1024, 8), (2, 40, 40, 256, 1024, 7),
-    (2, 9, 13, 128, 256, 12), (3, 11, 7, 512, 256, 12), (2, 9, 13, 64, 128, 13)])
+    (2, 40, 40, 64, 1024, 8), (2, 40, 40, 256, 1024, 14)])
 def test_conv3x3_glds(hip_lib, N, H, W, Cin, Cout, var):
     """LDS-DMA implicit GEMM (csrc/igemm_glds.hip): fwd with bias+ReLU and masked dgrad, every tile
     config, pixel counts that are not tile multiples (zero-filled DMA rows)."""
@@ -161,7 +156,7 @@ def test_conv3x3_glds(hip_lib, N, H, W, Cin, Cout, var):
     dref = xr.grad * (x > 0)
     packed, ng, kp = _pack_one(1, w)
     dx = torch.empty(N, H, W, Cin, dtype=torch.bfloat16, device="cuda")
-    v = var if (var % 16 not in (1, 3, 5, 7, 8, 10, 11, 12) or Cin % 256 == 0) else (9 if var in (8, 10) else 2)
+    v = var if (var not in (1, 8, 14) or Cin % 256 == 0) else 2      # 256-channel tiles need Ngemm % 256
     K.igemm(_nhwc(g), packed, dx, Ngemm=ng, Kpad=kp, KH=3, KW=3, stride=1, pad=1, Cs=Cout, out_grid=(N, H, W),
             mask=_nhwc(x), path="glds", variant=v)
     torch.cuda.synchronize()
@@ -588,27 +583,6 @@ def test_per_image_launch_beyond_2gib(hip_lib, path):
     assert torch.equal(y[N - 2:], y2)
 
 
-@pytest.mark.parametrize("depth", [1, 2, 3])
-def test_wgrad_rows_pipeline_depths(hip_lib, depth):
-    """csrc/wgrad_rows.hip at every pipeline depth (row bundles in flight) and forced row segments:
-    the counted vmcnt waits and ring-buffer reuse must give the fp32 reference for each."""
-    from distributedpytorch_amd.ops import kernels as K
-    torch.manual_seed(13)
-    N, H, W, Cin, Cout = 2, 11, 96, 64, 128
-    x = _bf(torch.randn(N, Cin, H, W))
-    g = _bf(torch.randn(N, Cout, H, W))
-    wr = torch.zeros(Cout, Cin, 3, 3, requires_grad=True)
-    br = torch.zeros(Cout, requires_grad=True)
-    F.conv2d(x, wr, br, padding=1).backward(g)
-    for rh in (0, 1, 4):
-        gw = torch.zeros(Cout * Cin * 9, device="cuda")
-        gb = torch.zeros(Cout, device="cuda")
-        K._wgrad_rows(_nhwc(g), _nhwc(x), grid=(N, H, W), M=Cout, Nc=Cin, gw=gw, gb=gb, Nreal=Cin, rh=rh, depth=depth)
-        torch.cuda.synchronize()
-        assert _rel(gw.cpu().view(Cout, Cin, 3, 3), wr.grad) < 1e-2, (depth, rh)
-        assert _rel(gb.cpu(), br.grad) < 1e-2, (depth, rh)
-
-
 @pytest.mark.parametrize("blocks", [1, 7, 100000])
 def test_wgrad_gemm_image_groups(hip_lib, blocks):
     """csrc/wgrad_gemm.hip with 1 .. N images per split (the split-K slabs over image groups, K-steps
@@ -661,7 +635,8 @@ def test_wgrad_multi_microbatches(hip_lib, M, Nc, H, W, mb, nmb):
 def test_glds_pingpong_epilogues(hip_lib, N, H, W, Cs, Ng, kind):
     """The ping-pong deep GEMM (cfg 14; on whole-row tiles its row-block pixel staging form, 8206 = cfg 14
     without row blocks) with its specialised epilogues (forward bias + ReLU, dgrad ReLU mask; partial
-    last pixel tile) == the 2-stage kernel (cfg 3) bitwise: all accumulate K in the same order."""
+    last pixel tile): both forms accumulate K in the same order -> bitwise equal (fp32 anchors of the
+    same kernels: tests/test_rowblock.py)."""
     from distributedpytorch_amd.ops import kernels as K
     torch.manual_seed(23)
     x = torch.randn(N, H, W, Cs, device="cuda").to(torch.bfloat16)
@@ -670,13 +645,13 @@ def test_glds_pingpong_epilogues(hip_lib, N, H, W, Cs, Ng, kind):
     extra = (dict(bias=torch.randn(Ng, device="cuda") * 0.1, relu=True) if kind == "fwd" else
              dict(mask=torch.randn(N, H, W, Ng, device="cuda").to(torch.bfloat16)))
     outs = []
-    for v in (3, 14, 8206):
+    for v in (14, 8206):
         y = torch.empty(N, H, W, Ng, device="cuda", dtype=torch.bfloat16)
         K.igemm(x, w, y, Ngemm=Ng, Kpad=Kp, KH=3, KW=3, stride=1, pad=1, Cs=Cs, out_grid=(N, H, W), path="glds",
                 variant=v, **extra)
         outs.append(y)
     torch.cuda.synchronize()
-    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+    assert torch.equal(outs[0], outs[1])
 
 
 @pytest.mark.parametrize("N,H,W,Cs,Ng,kind", [(4, 128, 128, 128, 128, "fwd"), (3, 30, 256, 64, 128, "dgrad"),

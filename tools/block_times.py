@@ -134,12 +134,11 @@ def main():
                 return ts[len(ts) // 2]
 
             bwd.append(tback(a.reps))
-            saved = K._ABLATE
-            K._ABLATE = frozenset({"wgrad"})       # timing ablation: skip the deferrable weight gradients
+            K.set_timing_ablation({"wgrad"})      # timing ablation: skip the deferrable weight gradients
             try:
                 bwd_nw.append(tback(a.reps))
             finally:
-                K._ABLATE = saved
+                K.set_timing_ablation(())
             print(f"mb {mb:4d} {table['blocks'][idx]:6s} fwd {fwd[-1]:8.3f} bwd {bwd[-1]:8.3f} "
                   f"bwd-wgrad {bwd_nw[-1]:8.3f} ms", flush=True)
         table["per_mb"][str(mb)] = {"fwd": fwd, "bwd": bwd, "bwd_nowgrad": bwd_nw}

@@ -41,7 +41,6 @@ def main():
     ap.add_argument("--hvar", type=int, nargs="*", default=[], help="row-halo kernel configs to time")
     ap.add_argument("--wsvar", type=int, nargs="*", default=[], help="row-streaming wgrad tile configs to time")
     ap.add_argument("--wpaths", default="stream,halo,generic", help="weight-gradient paths to time (also: rows)")
-    ap.add_argument("--rowdepth", type=int, nargs="*", default=[], help="wgrad_rows pipeline depths to time")
     ap.add_argument("--dwcfg", type=int, nargs="*", default=[], help="transposed-conv wgrad tile configs to time")
     ap.add_argument("--paths", default="stream,halo,generic", help="default paths to time")
     ap.add_argument("--layout-probe", action="store_true",
@@ -85,10 +84,9 @@ def main():
         gw = torch.zeros(Cout * Cin * 9, device=dev)
         gb = torch.zeros(Cout, device=dev)
         wvars = [(p, p, 0) for p in (() if a.no_wgrad else a.wpaths.split(","))] + \
-            [(f"strm.w{v}", "stream", v) for v in a.wsvar] + [(f"rows.d{d}", "rows", d) for d in a.rowdepth]
+            [(f"strm.w{v}", "stream", v) for v in a.wsvar]
         for label, path, wv in wvars:
             K.WGRAD_STREAM_CFG = wv if path == "stream" else 0
-            K.WGRAD_ROWS_DEPTH = wv if path == "rows" and wv else 3
             try:
                 t = timeit(lambda: K.wgrad(g, x, kind=0, grid=(B, H, H), M=Cout, Nc=Cin, s=1, pad=1, KW=3, gw=gw,
                                            gb=gb, Nreal=Cin, path=path), a.reps)
