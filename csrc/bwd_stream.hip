@@ -62,6 +62,9 @@ struct BwdArgs {
   // and channel, sum dx and sum dx*x of the stored masked dx -> bnslab[block][2][CI] (the partial
   // sums igemm_stream's EPI 5 writes; bn_bwd_finalize_kernel's gy mode consumes them)
   float* bnslab;
+  // HEAD mode: the forward's per-pixel probability p = sigmoid(z) [N*H*W] (igemm_stream's fused head
+  // epilogue writes it), read per pixel instead of the 32-channel dot + sigmoid
+  const float* hprob;
 };
 
 // 8 consecutive k (pixel rows roff+8g .. +7) of 16 channels starting at col0, from an nk image
@@ -141,7 +144,7 @@ __global__ __launch_bounds__(64 * NW, 2) void bwd_stream_kernel(BwdArgs a) {
   const int wp = wid % WPX, wc = wid / WPX;                      // dx role
   const int nt = wid % NTI, msp = (wid / NTI) % MSPL, pg = wid / (NTI * MSPL);   // dW role
   // buffer resources are rebuilt per image (32-bit offsets stay inside one image at any batch size)
-  __amdgpu_buffer_rsrc_t gr, xr, yr, y2r, tr, pr, cr, x1r, zr;
+  __amdgpu_buffer_rsrc_t gr, xr, yr, y2r, tr, hpr, pr, cr, x1r, zr;
   const bool has_g = !POOL || a.g != nullptr;
   auto bind = [&](int img) {
     const long pix = (long)img * a.H * a.W;
@@ -150,7 +153,10 @@ __global__ __launch_bounds__(64 * NW, 2) void bwd_stream_kernel(BwdArgs a) {
       pr = __builtin_amdgcn_make_buffer_rsrc((void*)(a.dpool + win * a.ldp), 0, 0x7fffffff, 0x00020000);
       cr = __builtin_amdgcn_make_buffer_rsrc((void*)(a.pcode + win * CO), 0, 0x7fffffff, 0x00020000);
     }
-    if constexpr (HEAD) tr = __builtin_amdgcn_make_buffer_rsrc((void*)(a.tgt + pix), 0, a.H * a.W * 4, 0x00020000);
+    if constexpr (HEAD) {
+      tr = __builtin_amdgcn_make_buffer_rsrc((void*)(a.tgt + pix), 0, a.H * a.W * 4, 0x00020000);
+      hpr = __builtin_amdgcn_make_buffer_rsrc((void*)(a.hprob + pix), 0, a.H * a.W * 4, 0x00020000);
+    }
     if constexpr (W1) x1r = __builtin_amdgcn_make_buffer_rsrc((void*)(a.x1 + pix * 8), 0, (int)a.x1bytes, 0x00020000);
     if constexpr (BNL) zr = __builtin_amdgcn_make_buffer_rsrc((void*)(a.z + pix * a.ldg), 0, (int)a.gbytes, 0x00020000);
     gr = __builtin_amdgcn_make_buffer_rsrc((void*)(has_g ? a.g + pix * a.ldg : a.x), 0, has_g ? (int)a.gbytes : 0, 0x00020000);
@@ -204,7 +210,7 @@ __global__ __launch_bounds__(64 * NW, 2) void bwd_stream_kernel(BwdArgs a) {
   const unsigned x1off = (unsigned)((w0 + tid - 1) * 16), x1rowb = (unsigned)(a.W * 16);
   // HEAD: segmap weights of this thread's 8 channels (cc = tid & 3 for every chunk it loads), the
   // target offset of each chunk's pixel, and whether the pixel is this block's own (not halo)
-  float hwv[8], hdw[8], hbias = 0.f, hd0 = 0.f, hd1 = 0.f, hd2 = 0.f, hdb = 0.f;
+  float hwv[8], hdw[8], hd0 = 0.f, hd1 = 0.f, hd2 = 0.f, hdb = 0.f;
   // POOL: per chunk the window column's byte offsets into dpool / codes and the pixel's column parity
   unsigned ppo[POOL ? LG : 1], pco[POOL ? LG : 1], pq[POOL ? LG : 1];
   if constexpr (POOL) {
@@ -226,7 +232,6 @@ __global__ __launch_bounds__(64 * NW, 2) void bwd_stream_kernel(BwdArgs a) {
       hwv[e] = a.hw[(tid & 3) * 8 + e];
       hdw[e] = 0.f;
     }
-    hbias = a.hb[0];
     hd0 = a.dS[0]; hd1 = a.dS[1]; hd2 = a.dS[2];
 #pragma unroll
     for (int j = 0; j < LG; ++j) {
@@ -240,6 +245,7 @@ __global__ __launch_bounds__(64 * NW, 2) void bwd_stream_kernel(BwdArgs a) {
   struct RowRegs {
     u32x4_t g[LG], x[LX];
     unsigned t[HEAD ? LG : 1];            // HEAD: target bits of each chunk's pixel
+    unsigned p[HEAD ? LG : 1];            // HEAD: the forward's probability of each chunk's pixel
     u32x4_t pd[POOL ? LG : 1];            // POOL: the pooled gradient of each chunk's window
     u32x2_t pc[POOL ? LG : 1];            // POOL: the window codes of the chunk's 8 channels
     u32x4_t x1[1];                        // W1: the x1 chunk of this thread's pixel
@@ -263,8 +269,11 @@ __global__ __launch_bounds__(64 * NW, 2) void bwd_stream_kernel(BwdArgs a) {
     }
     if constexpr (HEAD) {
 #pragma unroll
-      for (int j = 0; j < LG; ++j)
-        R.t[j] = __builtin_amdgcn_raw_buffer_load_b32(tr, (rok && gok[j]) ? (unsigned)(ih * a.W) * 4u + tpo[j] : 0x80000000u, 0, 0);
+      for (int j = 0; j < LG; ++j) {
+        const unsigned o = (rok && gok[j]) ? (unsigned)(ih * a.W) * 4u + tpo[j] : 0x80000000u;
+        R.t[j] = __builtin_amdgcn_raw_buffer_load_b32(tr, o, 0, 0);
+        R.p[j] = __builtin_amdgcn_raw_buffer_load_b32(hpr, o, 0, 0);
+      }
     }
     if constexpr (POOL) {
       const unsigned wrow = (unsigned)(ih >> 1) * (unsigned)(a.W >> 1);
@@ -329,13 +338,7 @@ __global__ __launch_bounds__(64 * NW, 2) void bwd_stream_kernel(BwdArgs a) {
           yv[2 * e] = lo_bf(R.g[j][e]);
           yv[2 * e + 1] = hi_bf(R.g[j][e]);
         }
-        float zp = 0.f;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) zp = fmaf(yv[e], hwv[e], zp);
-        zp += __shfl_xor(zp, 1, 64);             // the pixel's 4 chunks sit in lanes 4k..4k+3
-        zp += __shfl_xor(zp, 2, 64);
-        const float z = zp + hbias;
-        const float p = fast_sigmoid(z);
+        const float p = __uint_as_float(R.p[j]);  // the forward's sigmoid(z) (no 32-channel dot here)
         const float tt = __uint_as_float(R.t[j]);
         const float one = tt == 1.f ? 1.f : 0.f;
         const float dz = head_dz(p, tt, one, hd0, hd1, hd2);
@@ -787,7 +790,7 @@ DPA_API int dpa_bwd_stream(const BwdArgs* args, int ci, int co, int epi, hipStre
     return launch_bwd_stream<64, 32, 32, 4, 2, 0, false, true>(a, st);
   }
   if (a.hslab != nullptr) {                        // fused head backward: last decoder conv 32 -> 32
-    if (ci == 32 && co == 32 && epi == 0 && a.tgt && a.hw && a.hb && a.dS)
+    if (ci == 32 && co == 32 && epi == 0 && a.tgt && a.hw && a.hb && a.dS && a.hprob)
       return launch_bwd_stream<64, 32, 32, 4, 2, 0, true>(a, st);
     return (int)hipErrorInvalidValue;
   }

@@ -33,6 +33,9 @@ struct IgemmArgs {
   unsigned ximg;        // bytes addressable from ONE image of x: the row-streaming / row-halo kernels
                         // bind one image per block (64-bit base, 32-bit offsets inside it), so they take
                         // the whole batch in one launch whatever its size (no 2 GiB chunking)
+  float* hprob;         // fused head (optional): the per-pixel probability p = sigmoid(z) [N*Ho*Wo] fp32,
+                        // kept for the head backward (bwd_stream HEAD mode reads it instead of re-deriving
+                        // it from the 32-channel output)
 };
 
 // 2x2 window code from the four (bf16-rounded) values in window order tl, tr, bl, br: first

@@ -748,6 +748,7 @@ __global__ __launch_bounds__(256 * WCS) void igemm_stream_kernel(IgemmArgs a) {
           const unsigned pix = (unsigned)(orow * a.Wo + w0 + wp * WP + ip * 16 + (lane & 15));
           const float z = hdot + a.hb[0];
           const float p = fast_sigmoid(z);
+          if (a.hprob) a.hprob[pix] = p;
           const float tt = a.tgt[pix];
           const float lp = fmaxf(__logf(p), -100.f), l1p = fmaxf(__logf(1.f - p), -100.f);
           const float one = tt == 1.f ? 1.f : 0.f;

@@ -794,10 +794,12 @@ class _DecFn(torch.autograd.Function):
                 and K.head_fusable(N, H, W, c2.Cin, c2.Cout)):
             # last decoder conv + segmap + sigmoid + BCE/Dice partial sums in one kernel
             y = torch.empty(N, H, W, c2.Cout, dtype=torch.bfloat16, device=a.device)
+            # the per-pixel probability is kept for the head backward folded into this conv's backward
+            hprob = torch.empty(N * H * W, dtype=torch.float32, device=a.device)
             S = K.igemm(a, B.wf(c2), y, Ngemm=c2.Cout, Kpad=c2.Kf, KH=3, KW=3, stride=1, pad=1, Cs=c2.Cs,
                         out_grid=(N, H, W), bias=c2.mod.bias, relu=True,
-                        head=(seg.weight.view(-1), seg.bias, tgt))
-            B._head_cache = (y.data_ptr(), tgt.data_ptr(), S)
+                        head=(seg.weight.view(-1), seg.bias, tgt, hprob))
+            B._head_cache = (y.data_ptr(), tgt.data_ptr(), S, hprob)
         else:
             y = B.conv_fwd(c2, a, st=st2)
         ctx.B, ctx.i = B, i
@@ -818,11 +820,11 @@ class _DecFn(torch.autograd.Function):
             # the head's gradient was deferred (_HeadFn.backward): it is formed from y inside this
             # conv's fused backward instead of being materialised (saves a write + read of it)
             B._head_pending = None
-            _, y, t, dS = pend
+            _, y, t, dS, hprob = pend
             seg = B.model.segmap
             W = y.shape[2]
             g1, st_g = B.conv_bwd(c2, y, a, mask=True, head=(t, seg.weight, seg.bias, dS,
-                                                             _grad(seg.weight).view(-1), _grad(seg.bias))), None
+                                                             _grad(seg.weight).view(-1), _grad(seg.bias), hprob)), None
             B.ready([seg])
         else:
             g2 = _v(g2)
@@ -830,7 +832,7 @@ class _DecFn(torch.autograd.Function):
                 # the head's deferred gradient reached us in another form (summed with another
                 # gradient, or materialised by a hook): form it now and add it, never drop it
                 B._head_pending = None
-                ph, y, t, dS = pend
+                ph, y, t, dS, _ = pend
                 seg = B.model.segmap
                 gy = K.head_bwd(y, seg.weight, seg.bias, t, dS, _grad(seg.weight).view(-1), _grad(seg.bias))
                 B.ready([seg])
@@ -880,6 +882,7 @@ class _HeadFn(torch.autograd.Function):
         ctx.B = B
         # fused forward => y is this engine's last decoder conv output and its backward runs next
         ctx.fold = cache is not None and cache[0] == y.data_ptr() and B.head_bwd_foldable(y.shape[2])
+        ctx.hprob = cache[3] if ctx.fold else None      # the forward's probabilities, for the folded backward
         ctx.save_for_backward(y, t)
         return S.clone()
 
@@ -892,7 +895,8 @@ class _HeadFn(torch.autograd.Function):
             # defer: hand the decoder a zero-stride placeholder of y's gradient; _DecFn.backward
             # recognises it and folds the head backward into the last conv's fused backward
             ph = torch.zeros((), dtype=y.dtype, device=y.device).expand(y.shape[0], y.shape[3], y.shape[1], y.shape[2])
-            B._head_pending = (ph, y, t.reshape(-1), dS)
+            B._head_pending = (ph, y, t.reshape(-1), dS, ctx.hprob)
+            ctx.hprob = None
             return None, ph, None, None
         gy = K.head_bwd(y, seg.weight, seg.bias, t, dS, _grad(seg.weight).view(-1), _grad(seg.bias))
         B.ready([seg])

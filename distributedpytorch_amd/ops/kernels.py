@@ -30,7 +30,8 @@ class IgemmArgs(ctypes.Structure):
                                      "stride", "pad", "Ngemm", "Kpad", "mode", "relu", "accumulate", "Cout")] + \
                [("xbytes", ctypes.c_uint), ("pool", c_void_p), ("ldp", c_int), ("pcode", c_void_p), ("y2", c_void_p),
                 ("ldy2", c_int), ("split", c_int), ("hw", c_void_p), ("hb", c_void_p), ("tgt", c_void_p),
-                ("hslab", c_void_p), ("bnslab", c_void_p), ("korder", c_int), ("ximg", ctypes.c_uint)]
+                ("hslab", c_void_p), ("bnslab", c_void_p), ("korder", c_int), ("ximg", ctypes.c_uint),
+                ("hprob", c_void_p)]
 
 
 class WgradArgs(ctypes.Structure):
@@ -48,7 +49,7 @@ class BwdArgs(ctypes.Structure):
                [("tgt", c_void_p), ("hw", c_void_p), ("hb", c_void_p), ("dS", c_void_p), ("hslab", c_void_p)] + \
                [("pcode", c_void_p), ("dpool", c_void_p), ("ldp", c_int)] + \
                [("x1", c_void_p), ("slab1", c_void_p), ("bslab1", c_void_p), ("x1bytes", ctypes.c_uint)] + \
-               [("z", c_void_p), ("bncoef", c_void_p), ("bnslab", c_void_p)]
+               [("z", c_void_p), ("bncoef", c_void_p), ("bnslab", c_void_p), ("hprob", c_void_p)]
 
 
 class PackDesc(ctypes.Structure):
@@ -205,8 +206,11 @@ def igemm(x: torch.Tensor, wpacked: torch.Tensor, y: torch.Tensor, *, Ngemm: int
     if bn_stats is not None and USE_FUSED_BN and mode == 0 and pool is None and y2 is None and head is None \
             and not accumulate and not relu and path == "auto" and (mask is None or mch == Ngemm):
         bslab = torch.empty(N * -(-Ho // 16) * -(-Wo // 64) * 2 * Ngemm, dtype=torch.float32, device=y.device)
+    hprob = None
     if head is not None:
-        hw, hb, tgt = head
+        hw, hb, tgt = head[:3]
+        hprob = head[3] if len(head) > 3 else None
+        assert hprob is None or (hprob.dtype == torch.float32 and hprob.is_contiguous() and hprob.numel() == N * Ho * Wo)
         assert mode == 0 and Ngemm == 32 and Cs == 32 and pool is None and y2 is None and mask is None
         assert hw.dtype == torch.float32 and hw.is_contiguous() and hw.numel() == 32 and hb.numel() == 1
         assert tgt.dtype == torch.float32 and tgt.is_contiguous() and tgt.numel() == N * Ho * Wo
@@ -233,6 +237,7 @@ def igemm(x: torch.Tensor, wpacked: torch.Tensor, y: torch.Tensor, *, Ngemm: int
         assert conv3 and stream_ok and 0 < rows and (rows + 1) * 4 <= hslab.numel() and path in ("auto", "stream"), \
             "fused head needs the stream kernel"
         a.hw, a.hb, a.tgt, a.hslab = hw.data_ptr(), hb.data_ptr(), tgt.data_ptr(), hslab.data_ptr()
+        a.hprob = None if hprob is None else hprob.data_ptr()
         _check(L.dpa_igemm_stream(ctypes.byref(a), c_int(0), st), "igemm_stream+head")
         S = hslab[hslab.numel() - 4:]
         _check(L.dpa_slab_sum(_p(hslab), c_int(rows), c_int(4), _p(S), st), "slab_sum")
@@ -561,10 +566,10 @@ def conv_bwd_fused(g: Optional[torch.Tensor], x: torch.Tensor, wd: torch.Tensor,
     (ReLU mask already applied), ``wd`` the dgrad-packed weights ``[Cin][Kd]``.
 
     ``head`` = (target fp32 [N*H*W], segmap weight [C], segmap bias [1], dS [4], segmap weight grad,
-    segmap bias grad): ``g`` is then the conv's OUTPUT y (the last decoder conv, whose epilogue
-    computed the fused head + loss partials in the forward) and the head backward (``head_bwd``) is
-    folded into the loader: the gradient is formed from y on the fly and never stored; the segmap
-    gradients accumulate into the last two tensors.
+    segmap bias grad, the forward's probabilities fp32 [N*H*W]): ``g`` is then the conv's OUTPUT y (the
+    last decoder conv, whose epilogue computed the fused head + loss partials -- and stored p -- in the
+    forward) and the head backward (``head_bwd``) is folded into the loader: the gradient is formed
+    from (y, p) on the fly and never stored; the segmap gradients accumulate into the weight / bias grads.
 
     ``pool`` = (window codes uint8 [N, H/2, W/2, Cout], pooled gradient [N, H/2, W/2, Cout]): the conv
     is an encoder conv2 whose output was max-pooled in its forward epilogue; ``g`` is then the skip
@@ -656,15 +661,17 @@ def conv_bwd_fused(g: Optional[torch.Tensor], x: torch.Tensor, wd: torch.Tensor,
         a.x1bytes = _extent_bytes(1, H, W, 8, 8)
     hslab = None
     if head is not None:
-        tgt, hw, hb, dS, hgw, hgb = head
+        tgt, hw, hb, dS, hgw, hgb, hprob = head
         assert epi == 0 and CI == CO == 32, "head mode: the 32->32 last decoder conv"
         assert tgt.dtype == torch.float32 and tgt.is_contiguous() and tgt.numel() == N * H * W
+        assert hprob.dtype == torch.float32 and hprob.is_contiguous() and hprob.numel() == N * H * W
         assert hw.dtype == torch.float32 and hw.numel() == CO and hb.numel() == 1
         assert hgw.is_contiguous() and hgw.numel() == CO and hgb.numel() == 1
         dS = dS.float().contiguous()
         hslab = torch.empty(nblk * (CO + 1) + CO + 1, dtype=torch.float32, device=x.device)
         hw = hw.reshape(-1).contiguous()
         a.tgt, a.hw, a.hb, a.dS, a.hslab = tgt.data_ptr(), hw.data_ptr(), hb.data_ptr(), dS.data_ptr(), hslab.data_ptr()
+        a.hprob = hprob.data_ptr()
     bnslab = None
     if bn is not None:
         z, coef3 = bn

@@ -80,8 +80,9 @@ def test_conv_bwd_fused_deterministic_and_matches_unfused(hip_lib):
 @pytest.mark.parametrize("N,H,W", [(2, 5, 64), (1, 33, 128)])
 def test_conv_bwd_fused_head_mode_matches_separate_head_bwd(hip_lib, N, H, W):
     """Head mode: the segmentation-head backward folded into the last decoder conv's fused backward
-    (gradient formed from the conv output y on load) equals head_bwd followed by the plain fused
-    backward: dx, conv weight/bias gradients and segmap weight/bias gradients."""
+    (gradient formed from the conv output y and the forward's stored probabilities on load) equals
+    head_bwd followed by the plain fused backward: dx, conv weight/bias gradients and segmap weight/bias
+    gradients."""
     from distributedpytorch_amd.ops import kernels as K
     torch.manual_seed(9)
     C = 32
@@ -100,7 +101,9 @@ def test_conv_bwd_fused_head_mode_matches_separate_head_bwd(hip_lib, N, H, W):
     dx_r = K.conv_bwd_fused(gy, a, packed, kd, gw_r, gb_r, mask=True)
     hgw, hgb = torch.zeros(C, device="cuda"), torch.zeros(1, device="cuda")
     gw, gb = torch.zeros(C * C * 9, device="cuda"), torch.zeros(C, device="cuda")
-    dx = K.conv_bwd_fused(y, a, packed, kd, gw, gb, mask=True, head=(t, hw, hb, dS, hgw, hgb))
+    # the probabilities the forward's fused head epilogue stores (sigmoid of the head logit of y)
+    hprob = torch.sigmoid(y.float().reshape(-1, C) @ hw + hb).contiguous()
+    dx = K.conv_bwd_fused(y, a, packed, kd, gw, gb, mask=True, head=(t, hw, hb, dS, hgw, hgb, hprob))
     torch.cuda.synchronize()
     assert _rel(dx.float().cpu(), dx_r.float().cpu()) < 1e-2
     assert _rel(gw.cpu(), gw_r.cpu()) < 1e-2 and _rel(gb.cpu(), gb_r.cpu()) < 1e-2

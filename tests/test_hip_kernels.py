@@ -500,8 +500,9 @@ def test_stream_conv_fused_head(hip_lib, N, H, W):
     hb = torch.tensor([0.1], device="cuda")
     t = (torch.rand(N * H * W, device="cuda") > 0.5).float()
     y = torch.empty(N, H, W, 32, dtype=torch.bfloat16, device="cuda")
+    hprob = torch.full((N * H * W,), -1.0, device="cuda")
     S = K.igemm(x, wf, y, Ngemm=32, Kpad=K.round_up(9 * 32, 32), KH=3, KW=3, stride=1, pad=1, Cs=32,
-                out_grid=(N, H, W), bias=b, relu=True, head=(hw, hb, t))
+                out_grid=(N, H, W), bias=b, relu=True, head=(hw, hb, t, hprob))
     y2 = torch.empty_like(y)
     K.igemm(x, wf, y2, Ngemm=32, Kpad=K.round_up(9 * 32, 32), KH=3, KW=3, stride=1, pad=1, Cs=32,
             out_grid=(N, H, W), bias=b, relu=True, path="stream")
@@ -509,6 +510,9 @@ def test_stream_conv_fused_head(hip_lib, N, H, W):
     torch.cuda.synchronize()
     assert torch.equal(y, y2)
     assert torch.allclose(S, S_ref, rtol=1e-4, atol=1e-2), (S, S_ref)
+    # the stored probabilities (read by the fused head backward) = sigmoid of the head logit of y
+    p_ref = torch.sigmoid(y.float().reshape(-1, 32) @ hw + hb)
+    assert (hprob - p_ref).abs().max().item() < 1e-5
 
 
 @pytest.mark.parametrize("N,H,W,Cin,Cout,hcfg", [
