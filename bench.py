@@ -64,10 +64,14 @@ def parse():
                     help="dp: one replica per GPU, RCCL all-reduce (weak scaling); mp: GPipe over the N ranks "
                          "(one batch of --batch images split into --microbatches, strong scaling); with one "
                          "process, mp runs --stages stages on cuda:0 (pipeline rehearsal)")
-    ap.add_argument("--microbatches", type=int, default=8)
+    ap.add_argument("--microbatches", type=int, default=0,
+                    help="mp microbatches (0: the measured pipeline plan's count for this model / image / stages "
+                         "/ batch, parallel/plans.json; 8 without one)")
     ap.add_argument("--stages", type=int, default=2, help="mp with one process: stages on the local device")
-    ap.add_argument("--mp-cut", choices=["auto", "reference", "balanced"], default="auto",
-                    help="mp stage boundaries (auto: reference encoder|decoder cut for 2 stages, else balanced)")
+    ap.add_argument("--mp-cut", choices=["auto", "reference", "balanced", "time"], default="auto",
+                    help="mp stage boundaries (auto: the time-balanced plan from measured block times when "
+                         "parallel/plans.json has one for this configuration, else the reference "
+                         "encoder|decoder cut for 2 stages and the FLOP-balanced cut otherwise)")
     ap.add_argument("--timing-ablation", default="",
                     help="MEASUREMENT ONLY, numerically wrong: skip these kernel families (comma list of "
                          "stream,halo,glds,wgrad,wgrad_deep,bwd,deconv) to see what they cost; the JSON line is "
@@ -137,6 +141,16 @@ def main():
                       backend=a.backend, model=a.model, bucket_mb=a.bucket_mb, lr=1e-4,
                       grad_comm_dtype=a.grad_comm_dtype, comm_overlap=a.comm_overlap,
                       microbatches=a.microbatches, stages=a.stages, mp_cut=a.mp_cut)
+    mp_info = None
+    if mp:
+        from distributedpytorch_amd.config import mp_plan
+        mode, cuts, M = mp_plan(cfg, world if world > 1 else a.stages, default_microbatches=8)
+        cfg.microbatches = M
+        mp_info = {"cut_mode": mode, "microbatches": M}
+        if mode == "time":
+            from distributedpytorch_amd.parallel.schedule import load_plan
+            pl = load_plan(a.model, a.img[0], a.img[1], world if world > 1 else a.stages, a.batch)
+            mp_info.update(predicted_img_s=pl.get("predicted_img_s"), predicted_efficiency=pl.get("predicted_efficiency"))
     model = build_model(a.model)
     nparams = count_params(model)
     if mp and world > 1:
@@ -224,7 +238,7 @@ def main():
         cross = round(value / (STOCK_BASELINE_PER_GPU * world), 4)
         vs = cross if (per_gpu_batch == STOCK_BASELINE_BATCH and not mp) else EQUAL_BATCH_RATIO_B32
     if mp:
-        par = f"mp{world if world > 1 else a.stages}x{a.microbatches}mb" + ("" if world > 1 else "-1gpu")
+        par = f"mp{world if world > 1 else a.stages}x{strat.pipe.M}mb" + ("" if world > 1 else "-1gpu")
     else:
         par = f"dp{world}"
     out = {
@@ -246,7 +260,7 @@ def main():
                    "per_gpu_batch": a.batch if not mp else a.batch // max(1, world),
                    "seq_len": a.img[0] * a.img[1], "image_hw": list(a.img),
                    "parallelism": par, "backend": backend,
-                   "mp_cut": (strat.pipe.cuts if mp else None), "bucket_mb": a.bucket_mb,
+                   "mp_cut": (strat.pipe.cuts if mp else None), "mp_plan": mp_info, "bucket_mb": a.bucket_mb,
                    "grad_comm_dtype": a.grad_comm_dtype, "comm_overlap": a.comm_overlap,
                    "hip_graph": graphed is not None},
         "final_loss": round(final_loss, 5) if final_loss == final_loss else None, "warmup_s": round(warm_s, 2),

@@ -65,6 +65,9 @@ struct BwdArgs {
   // HEAD mode: the forward's per-pixel probability p = sigmoid(z) [N*H*W] (igemm_stream's fused head
   // epilogue writes it), read per pixel instead of the 32-channel dot + sigmoid
   const float* hprob;
+  // dual input (CI == 64): channels 32-63 of x come from this second tensor, laid out like x (same
+  // ldx, xbytes) -- the decoder conv over [skip | up] without a concat buffer
+  const bf16_t* x2;
 };
 
 // 8 consecutive k (pixel rows roff+8g .. +7) of 16 channels starting at col0, from an nk image
@@ -122,7 +125,11 @@ __global__ __launch_bounds__(64 * NW, 2) void bwd_stream_kernel(BwdArgs a) {
   constexpr int X1SLOT = HR * 16, G1SLOT = BP * 64;
   constexpr int W1BYTES = W1 ? 5 * X1SLOT + 2 * G1SLOT : 0;
   constexpr int GCH = KSO * HR * 4, XCH = HR * (CI / 8);         // 16-B chunks per ring row
-  constexpr int LG = (GCH + NT - 1) / NT, LX = (XCH + NT - 1) / NT;
+  // dual input (CI == 64, a.x2): plane-major x chunks, each 32-channel plane padded to whole waves
+  // so every wave's loads use one buffer resource (no more load slots than the interleaved mapping)
+  constexpr int PLX = (HR * 4 + 63) / 64 * 64;
+  constexpr int LX0 = (XCH + NT - 1) / NT, LX1 = CI == 64 ? (2 * PLX + NT - 1) / NT : 0;
+  constexpr int LG = (GCH + NT - 1) / NT, LX = LX0 > LX1 ? LX0 : LX1;
   constexpr int BCH = BP * 4 * KSO, LBI = (BCH + NT - 1) / NT;   // bias: chunks of the g row's BP pixels
   __shared__ __attribute__((aligned(16))) char lds[WBYTES + 4 * GSLOT + 4 * XSLOT + W1BYTES];
   __shared__ __attribute__((aligned(16))) float bnc[BNL ? 3 * CO : 4];   // BN mode: the dz coefficients
@@ -144,8 +151,9 @@ __global__ __launch_bounds__(64 * NW, 2) void bwd_stream_kernel(BwdArgs a) {
   const int wp = wid % WPX, wc = wid / WPX;                      // dx role
   const int nt = wid % NTI, msp = (wid / NTI) % MSPL, pg = wid / (NTI * MSPL);   // dW role
   // buffer resources are rebuilt per image (32-bit offsets stay inside one image at any batch size)
-  __amdgpu_buffer_rsrc_t gr, xr, yr, y2r, tr, hpr, pr, cr, x1r, zr;
+  __amdgpu_buffer_rsrc_t gr, xr, x2r, yr, y2r, tr, hpr, pr, cr, x1r, zr;
   const bool has_g = !POOL || a.g != nullptr;
+  const bool dual = CI == 64 && a.x2 != nullptr;
   auto bind = [&](int img) {
     const long pix = (long)img * a.H * a.W;
     if constexpr (POOL) {
@@ -161,6 +169,7 @@ __global__ __launch_bounds__(64 * NW, 2) void bwd_stream_kernel(BwdArgs a) {
     if constexpr (BNL) zr = __builtin_amdgcn_make_buffer_rsrc((void*)(a.z + pix * a.ldg), 0, (int)a.gbytes, 0x00020000);
     gr = __builtin_amdgcn_make_buffer_rsrc((void*)(has_g ? a.g + pix * a.ldg : a.x), 0, has_g ? (int)a.gbytes : 0, 0x00020000);
     xr = __builtin_amdgcn_make_buffer_rsrc((void*)(a.x + pix * a.ldx), 0, (int)a.xbytes, 0x00020000);
+    x2r = dual ? __builtin_amdgcn_make_buffer_rsrc((void*)(a.x2 + pix * a.ldx), 0, (int)a.xbytes, 0x00020000) : xr;
     yr = __builtin_amdgcn_make_buffer_rsrc((void*)(a.y + pix * a.ldy), 0, 0x7fffffff, 0x00020000);
     y2r = __builtin_amdgcn_make_buffer_rsrc((void*)(EPI == 1 ? a.y2 + pix * a.ldy2 : a.y), 0, 0x7fffffff, 0x00020000);
   };
@@ -179,7 +188,8 @@ __global__ __launch_bounds__(64 * NW, 2) void bwd_stream_kernel(BwdArgs a) {
   // ---- loader constants
   unsigned goff[LG], xoff[LX];
   int gsto[LG], xsto[LX];
-  bool gok[LG], xok[LX];
+  bool gok[LG], xok[LX], xpl[LX];     // xpl: this wave's x chunk j comes from x2 (wave-uniform)
+  const int wid_s = __builtin_amdgcn_readfirstlane(wid);
 #pragma unroll
   for (int j = 0; j < LG; ++j) {
     const int c = tid + j * NT;
@@ -192,16 +202,23 @@ __global__ __launch_bounds__(64 * NW, 2) void bwd_stream_kernel(BwdArgs a) {
 #pragma unroll
   for (int j = 0; j < LX; ++j) {
     const int c = tid + j * NT;
-    const int px = c / (CI / 8), cc = c - px * (CI / 8);
+    int px = c / (CI / 8), cc = c - px * (CI / 8), xc = cc * 8;
+    bool live = c < XCH;
+    xpl[j] = false;
+    if (dual) {
+      const int pl = (wid_s * 64 + j * NT) / PLX, cl = c - pl * PLX;
+      live = pl < 2 && cl < HR * 4;
+      px = cl >> 2, xc = (cl & 3) * 8, cc = pl * 4 + (cl & 3);
+      xpl[j] = pl == 1;
+    }
     const int iw = w0 + px - 1;
-    xok[j] = c < XCH && iw >= 0 && iw < a.W;
-    xoff[j] = (unsigned)((iw * a.ldx + cc * 8) * 2);
-    xsto[j] = c < XCH ? px * RBX + ((cc ^ swz_kk<RBX>(px)) << 4) : -1;
+    xok[j] = live && iw >= 0 && iw < a.W;
+    xoff[j] = (unsigned)((iw * a.ldx + xc) * 2);
+    xsto[j] = live ? px * RBX + ((cc ^ swz_kk<RBX>(px)) << 4) : -1;
   }
   const unsigned growb = (unsigned)(a.W * a.ldg * 2), xrowb = (unsigned)(a.W * a.ldx * 2);
   // ring rows are BP + 2 pixels, so the last register chunk of a row is live in one wave only: the
   // other waves skip its (HEAD/POOL) gradient transform on a wave-uniform branch
-  const int wid_s = __builtin_amdgcn_readfirstlane(wid);
   bool glive[LG];
 #pragma unroll
   for (int j = 0; j < LG; ++j) glive[j] = wid_s * 64 + j * NT < GCH;
@@ -261,7 +278,7 @@ __global__ __launch_bounds__(64 * NW, 2) void bwd_stream_kernel(BwdArgs a) {
       R.g[j] = __builtin_amdgcn_raw_buffer_load_b128(gr, (rok && gok[j]) ? gb + goff[j] : 0x80000000u, 0, 0);
 #pragma unroll
     for (int j = 0; j < LX; ++j)
-      R.x[j] = __builtin_amdgcn_raw_buffer_load_b128(xr, (rok && xok[j]) ? xb + xoff[j] : 0x80000000u, 0, 0);
+      R.x[j] = __builtin_amdgcn_raw_buffer_load_b128(xpl[j] ? x2r : xr, (rok && xok[j]) ? xb + xoff[j] : 0x80000000u, 0, 0);
     if constexpr (W1) R.x1[0] = __builtin_amdgcn_raw_buffer_load_b128(x1r, (rok && x1ok) ? (unsigned)ih * x1rowb + x1off : 0x80000000u, 0, 0);
     if constexpr (BNL) {
 #pragma unroll
@@ -762,7 +779,8 @@ DPA_API int dpa_bwd_stream(const BwdArgs* args, int ci, int co, int epi, hipStre
   const bool fused_mode = a.pcode != nullptr || a.hslab != nullptr || a.x1 != nullptr;
   if (!bwd_cfg(ci, co, &bp, &nw) || (fused_mode && a.W % bp) || a.W < 16 || (a.ldg & 7) || (a.ldx & 7) || (a.ldy & 3) ||
       a.rh < 1 || a.ipb < 1 ||
-      a.Kd < 9 * co || (epi == 1 && (a.y2 == nullptr || (a.ldy2 & 3) || a.split % 16 || a.split <= 0 || a.split >= ci)))
+      a.Kd < 9 * co || (epi == 1 && (a.y2 == nullptr || (a.ldy2 & 3) || a.split % 16 || a.split <= 0 || a.split >= ci)) ||
+      (a.x2 && (ci != 64 || a.ldx < 32 || fused_mode)))
     return (int)hipErrorInvalidValue;
   // BN modes: the gradient source is plain (no pool / head / first-conv fold); statistics for the
   // layer below only with the masked dx

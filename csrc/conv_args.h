@@ -36,6 +36,9 @@ struct IgemmArgs {
   float* hprob;         // fused head (optional): the per-pixel probability p = sigmoid(z) [N*Ho*Wo] fp32,
                         // kept for the head backward (bwd_stream HEAD mode reads it instead of re-deriving
                         // it from the 32-channel output)
+  const bf16_t* x2;     // dual input (row-streaming kernel, Cs == 64 only): channels 32-63 of the conv input
+                        // come from this second tensor, laid out like x ([N][Hs][Ws][ldx], same ximg) --
+                        // a decoder conv over [skip | up] reads the two dense halves, no concat buffer
 };
 
 // 2x2 window code from the four (bf16-rounded) values in window order tl, tr, bl, br: first

@@ -261,7 +261,8 @@ static int launch_igemm_halo(const IgemmArgs& a, hipStream_t st) {
 // the per-image buffer binding (IgemmArgs::ximg) must cover one whole image of x: a short extent would
 // read zeros past it instead of failing
 static bool ximg_ok(const IgemmArgs& a) {
-  return (long)a.ximg >= ((long)a.Hs * a.Ws - 1) * a.ldx * 2 + (long)a.Cs * 2;
+  // a dual input (a.x2) holds Cs / 2 channels per tensor, each tensor with this extent
+  return (long)a.ximg >= ((long)a.Hs * a.Ws - 1) * a.ldx * 2 + (long)(a.x2 ? a.Cs / 2 : a.Cs) * 2;
 }
 
 static bool tiles_ok(int W, int bp) {
@@ -272,7 +273,7 @@ static bool tiles_ok(int W, int bp) {
 DPA_API int dpa_igemm_halo(const IgemmArgs* args, int cfg, hipStream_t st) {
   const IgemmArgs& a = *args;
   if (a.mode != 0 || a.KH != 3 || a.KW != 3 || a.stride != 1 || a.pad != 1 || (a.Cs % 32) || (a.ldx & 7) ||
-      (a.ldy & 3) || a.Hs != a.Ho || a.Ws != a.Wo || a.Kpad < 9 * a.Cs || !ximg_ok(a))
+      (a.ldy & 3) || a.Hs != a.Ho || a.Ws != a.Wo || a.Kpad < 9 * a.Cs || !ximg_ok(a) || a.x2)
     return (int)hipErrorInvalidValue;
   if (cfg == 0) {
     if (a.Ngemm == 32 && tiles_ok(a.Wo, 256)) cfg = 1;
@@ -481,7 +482,12 @@ __global__ __launch_bounds__(256 * WCS) void igemm_stream_kernel(IgemmArgs a) {
   constexpr int WP = BP / 4, TP = WP / 16, WCN = NG / WCS, TC = WCN / 16;
   static_assert(TP >= 1 && TC >= 1, "tile");
   constexpr int RCH = KS * HR * 4;            // 16-B chunks per input row
-  constexpr int LR = (RCH + NT - 1) / NT;
+  // dual input (KS == 2, a.x2): channels 32-63 come from a second dense tensor.  Its chunks are laid
+  // out plane-major with each plane padded to whole waves, so every wave's loads use ONE buffer
+  // resource; for every strip width this needs no more load slots than the interleaved mapping
+  constexpr int PL = (HR * 4 + 63) / 64 * 64;
+  constexpr int LR0 = (RCH + NT - 1) / NT, LR1 = KS == 2 ? (2 * PL + NT - 1) / NT : 0;
+  constexpr int LR = LR0 > LR1 ? LR0 : LR1;
   __shared__ __attribute__((aligned(16))) char lds[WBYTES + 4 * SLOT];
   char* const Wimg = lds;
   char* const Ring = lds + WBYTES;
@@ -500,6 +506,8 @@ __global__ __launch_bounds__(256 * WCS) void igemm_stream_kernel(IgemmArgs a) {
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)(a.x + (long)n * a.Hs * a.Ws * a.ldx), 0, (int)a.ximg, 0x00020000);
   const __amdgpu_buffer_rsrc_t yr = __builtin_amdgcn_make_buffer_rsrc((void*)(a.y + opix * a.ldy), 0, 0x7fffffff, 0x00020000);
   const __amdgpu_buffer_rsrc_t mr = __builtin_amdgcn_make_buffer_rsrc((void*)(a.mask ? a.mask + opix * a.ldm : a.y), 0, 0x7fffffff, 0x00020000);
+  const bool dual = KS == 2 && a.x2 != nullptr;
+  const __amdgpu_buffer_rsrc_t x2r = dual ? __builtin_amdgcn_make_buffer_rsrc((void*)(a.x2 + (long)n * a.Hs * a.Ws * a.ldx), 0, (int)a.ximg, 0x00020000) : xr;
 
   // resident weights: packed [NG][Kpad] with k = tap*CS + ci
   for (int c = tid; c < 9 * KS * NG * 4; c += NT) {
@@ -511,15 +519,25 @@ __global__ __launch_bounds__(256 * WCS) void igemm_stream_kernel(IgemmArgs a) {
   // ---- per-thread loader constants (row-invariant)
   unsigned loff[LR];
   int lsto[LR];
-  bool lok[LR];
+  bool lok[LR], lpl[LR];      // lpl: this wave's chunk j comes from x2 (wave-uniform)
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
 #pragma unroll
   for (int j = 0; j < LR; ++j) {
     const int c = tid + j * NT;
-    const int cc = c & 3, px = (c >> 2) % HR, ks = (c >> 2) / HR;
+    int cc = c & 3, px = (c >> 2) % HR, ks = (c >> 2) / HR, xch = ks * 32;
+    bool live = c < RCH;
+    lpl[j] = false;
+    if (dual) {
+      ks = (wv * 64 + j * NT) / PL;
+      const int cl = c - ks * PL;
+      live = ks < 2 && cl < HR * 4;
+      cc = cl & 3, px = cl >> 2, xch = 0;
+      lpl[j] = ks == 1;
+    }
     const int iw = w0 + px - 1;
-    lok[j] = c < RCH && iw >= 0 && iw < a.Ws;
-    loff[j] = (unsigned)((iw * a.ldx + ks * 32 + cc * 8) * 2);
-    lsto[j] = c < RCH ? (ks * HR + px) * 64 + (swz_nk<32>(px, cc) << 4) : -1;
+    lok[j] = live && iw >= 0 && iw < a.Ws;
+    loff[j] = (unsigned)((iw * a.ldx + xch + cc * 8) * 2);
+    lsto[j] = live ? (ks * HR + px) * 64 + (swz_nk<32>(px, cc) << 4) : -1;
   }
   const unsigned rowbytes_x = (unsigned)(a.Ws * a.ldx * 2);
   // two register sets: a row's loads are issued two rows before it is stored into the ring
@@ -533,7 +551,7 @@ __global__ __launch_bounds__(256 * WCS) void igemm_stream_kernel(IgemmArgs a) {
 #pragma unroll
     for (int j = 0; j < LR; ++j) {
       const unsigned off = (rok && lok[j]) ? rbase + loff[j] : 0x80000000u;
-      R.v[j] = __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 0);
+      R.v[j] = __builtin_amdgcn_raw_buffer_load_b128(lpl[j] ? x2r : xr, off, 0, 0);
     }
   };
   auto rstore = [&](int slot, const RowRegs& R) {
@@ -991,7 +1009,7 @@ DPA_API int dpa_igemm_stream(const IgemmArgs* args, int variant, hipStream_t st)
   // dropped); the fused pool needs whole 2x2 windows along the row (even width)
   if (a.mode != 0 || a.KH != 3 || a.KW != 3 || a.stride != 1 || a.pad != 1 || (a.ldx & 7) || (a.ldy & 3) ||
       a.Hs != a.Ho || a.Ws != a.Wo || a.Wo < 16 || a.Kpad < 9 * a.Cs || !ximg_ok(a) ||
-      (a.pool && ((a.ldp & 3) || (a.Wo & 1) || !a.relu)))
+      (a.pool && ((a.ldp & 3) || (a.Wo & 1) || !a.relu)) || (a.x2 && (a.Cs != 64 || a.ldx < 32)))
     return (int)hipErrorInvalidValue;
   if (a.Cs == 8 && a.Ngemm == 32 && !a.pool) return launch_igemm_stream8<128, 32>(a, st);
   if (variant == 0) variant = stream_auto_variant(a);

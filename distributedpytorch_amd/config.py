@@ -41,8 +41,8 @@ class TrainConfig:
     out_dir: str = "."
     device: Optional[str] = None
     stages: int = 2                                  # pipeline stages for -t MP
-    microbatches: int = 2                            # reference MP: split_size=B/2 -> 2 microbatches
-    mp_cut: str = "auto"                             # MP stage cut: reference | balanced | auto (reference iff 2 stages)
+    microbatches: int = 0                            # 0: the measured plan's count, else 2 (reference split_size=B/2)
+    mp_cut: str = "auto"                             # MP stage cut: reference | balanced | time | auto (see mp_plan)
     bucket_mb: float = 8.0                           # DDP/DP all-reduce bucket size (MiB of fp32 grads)
     grad_comm_dtype: str = "fp32"                    # DDP gradient all-reduce wire dtype: fp32 | bf16
     comm_overlap: bool = True                        # DDP/DP: launch gradient buckets during the backward
@@ -97,8 +97,9 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--out-dir", type=str, default=".")
     p.add_argument("--device", type=str, default=None)
     p.add_argument("--stages", type=int, default=2)
-    p.add_argument("--microbatches", type=int, default=2)
-    p.add_argument("--mp-cut", choices=["auto", "reference", "balanced"], default="auto",
+    p.add_argument("--microbatches", type=int, default=0,
+                   help="MP microbatches (0: the measured pipeline plan's count, else 2 as the reference)")
+    p.add_argument("--mp-cut", choices=["auto", "reference", "balanced", "time"], default="auto",
                    help="MP stage boundaries: reference = encoder+mid | decoder+head (2 stages, ~34|62 GFLOP "
                         "per image at 512^2); balanced = FLOP-balanced contiguous blocks; auto = reference for 2 "
                         "stages, balanced otherwise")
@@ -150,9 +151,30 @@ def parse_args(argv=None) -> TrainConfig:
 
 
 def mp_cut_mode(cfg: "TrainConfig", stages: int) -> str:
-    if cfg.mp_cut != "auto":
-        return cfg.mp_cut
-    return "reference" if stages == 2 else "balanced"
+    return mp_plan(cfg, stages)[0]
+
+
+def mp_plan(cfg: "TrainConfig", stages: int, default_microbatches: int = 2):
+    """(cut mode, cuts or None, microbatches) of an MP run.
+
+    ``time`` / ``auto``: the time-balanced cut and microbatch count that tools/pipeline_plan.py chose
+    from MEASURED per-block times with the GPipe schedule simulator (parallel/schedule.py; plans in
+    parallel/plans.json, keyed by model, image, stages and global batch).  Without a plan for the
+    configuration, ``auto`` falls back to the reference encoder|decoder cut for 2 stages
+    (unet_model.py:14-20) and the FLOP-balanced cut otherwise, ``time`` to the FLOP-balanced cut.
+    An explicit ``--microbatches`` always wins."""
+    from .parallel.schedule import load_plan
+    mode = cfg.mp_cut
+    plan = None
+    if mode in ("auto", "time"):
+        h, w = cfg.img_size
+        plan = load_plan(cfg.model, h, w, stages, cfg.batch_size)
+        if plan is None:
+            mode = "reference" if (mode == "auto" and stages == 2) else "balanced"
+        else:
+            mode = "time"
+    M = cfg.microbatches or (plan["microbatches"] if plan else default_microbatches)
+    return mode, (plan["cuts"] if plan else None), M
 
 
 def dist_env():

@@ -217,16 +217,18 @@ class HipBlocks:
 
     # ------------------------------------------------------------------ primitive launches
     def conv_fwd(self, c: _Conv, x: torch.Tensor, y: torch.Tensor = None, pool: torch.Tensor = None,
-                 pcode: torch.Tensor = None, st: list = None):
+                 pcode: torch.Tensor = None, st: list = None, x2: torch.Tensor = None):
         """relu(conv(x)) -> y (and its 2x2 max-pool + window codes).  BN variant: the conv writes z,
-        then one statistics pass + one normalise/ReLU pass; ``st`` receives (z, saved) for the backward."""
+        then one statistics pass + one normalise/ReLU pass; ``st`` receives (z, saved) for the backward.
+        ``x2``: dual input, the conv reads [x | x2] (:meth:`dual_level`)."""
         N, H, W = x.shape[:3]
         if y is None:
             y = torch.empty(N, H, W, c.Cout, dtype=torch.bfloat16, device=x.device)
         if c.bn is None:
             K.igemm(x, self.wf(c), y, Ngemm=c.Cout, Kpad=c.Kf, KH=3, KW=3, stride=1, pad=1, Cs=c.Cs,
-                    out_grid=(N, H, W), bias=c.mod.bias, relu=True, pool=pool, pcode=pcode)
+                    out_grid=(N, H, W), bias=c.mod.bias, relu=True, pool=pool, pcode=pcode, x2=x2)
             return y
+        assert x2 is None, "dual input: convs without BatchNorm"
         if not self.model.training and K.FOLD_BN_EVAL and c.bn.track_running_stats and c.bn.running_mean is not None:
             # inference: BatchNorm with running statistics is a per-channel affine map -> folded into
             # the conv's weights and bias, so Conv2d+BN+ReLU(+pool) is ONE fused kernel, as without BN
@@ -357,7 +359,7 @@ class HipBlocks:
         return K.conv_bwd_fused(g, x, self.wd(c), c.Kd, gw, gb, mask=mask, head=head, pool=pool)
 
     def bwd_conv(self, c: _Conv, g: torch.Tensor, x: torch.Tensor, st, *, mask: bool, below: _Conv = None,
-                 stats: list = None, split: int = 0):
+                 stats: list = None, split: int = 0, x2: torch.Tensor = None):
         """Fused backward of ``c`` (:meth:`fusable`) when ``g`` is the gradient of its output -- of its
         BatchNorm+ReLU output if it has one (``st`` = that BN's saved (z, mean/invstd), ``stats`` = the
         BN's backward partial sums from whoever produced ``g``, if any): the BN backward is formed in the
@@ -374,7 +376,8 @@ class HipBlocks:
         if split:
             N, H, W = x.shape[:3]
             dx2 = torch.empty(N, H, W, c.Cin - split, dtype=torch.bfloat16, device=x.device)
-        res = K.conv_bwd_fused(g, x, self.wd(c), c.Kd, gw, gb, mask=mask, dx2=dx2, split=split, bn=bn, bn_stats=want)
+        res = K.conv_bwd_fused(g, x, self.wd(c), c.Kd, gw, gb, mask=mask, dx2=dx2, split=split, bn=bn, bn_stats=want,
+                               x2=x2)
         return res if want else (res, None)
 
     def halves_fusable(self, c: _Conv, C: int, W: int) -> bool:
@@ -388,6 +391,23 @@ class HipBlocks:
         if ok is None:
             ok = self._fusable[key] = K.bwd_fused_eligible(C, c.Cout, W)
         return ok
+
+    def dual_level(self, l: int, H: int, W: int) -> bool:
+        """Encoder level ``l`` and its decoder conv run WITHOUT a concat buffer: the skip and the
+        up-sampled half are two dense [N,H,W,32] tensors and the decoder's first conv (forward: the
+        row-streaming kernel; backward: the fused one) reads its 64 input channels from both (their
+        ``x2`` dual input).  Every write of either half is then a whole-cache-line store -- the skip
+        from the encoder conv's epilogue, the up half from the transposed conv -- instead of a 64-B half
+        of each 128-B concat pixel (the full-resolution level's stores ran at ~2/3 of the HBM rate)."""
+        if not (K.USE_STREAM and K.USE_DUAL_INPUT):
+            return False
+        d = len(self.dec_convs)
+        if not 0 <= l < d:
+            return False
+        c1 = self.dec_convs[d - 1 - l][0]
+        if not (c1.bn is None and c1.Cs == c1.Cin == 64 and self.enc_convs[l][1].Cout == 32):
+            return False
+        return W >= 16 and H * W * 64 < 2 ** 31 - 1024 and self.fusable(c1, None, W)
 
     def conv_bwd_halves(self, c: _Conv, g: torch.Tensor, cat: torch.Tensor, C: int):
         """Backward of a conv over ``cat = [lo | hi]`` (C channels each) as two fused passes: each
@@ -655,7 +675,7 @@ class _EncFn(torch.autograd.Function):
         N, H, W = x.shape[:3]
         st1, st2 = [], []
         a = B.conv_fwd(c1, x, st=st1)
-        if l in B.dense_skips:
+        if l in B.dense_skips or B.dual_level(l, H, W):
             cat = None
             skip = torch.empty(N, H, W, c2.Cout, dtype=torch.bfloat16, device=x.device)
         else:
@@ -782,11 +802,17 @@ class _DecFn(torch.autograd.Function):
             cat = torch.empty(Ns, h2, w2, 2 * C, dtype=torch.bfloat16, device=x.device)
             cat[..., :C].copy_(skip[:, top:top + h2, left:left + w2])
             ctx.crop = (Hs, Ws, top, left)
+            up = None
+        elif (skip.is_contiguous() and B.dual_level(len(B.deconvs) - 1 - i, h2, w2)):
+            # dual input: skip and up stay two dense tensors, the conv reads both (no concat buffer)
+            cat = skip
+            up = torch.empty(Ns, h2, w2, C, dtype=torch.bfloat16, device=x.device)
         else:
             cat = B.cat_for(skip)
-        B.deconv_fwd(d, x, cat[..., C:])
+            up = None
+        B.deconv_fwd(d, x, cat[..., C:] if up is None else up)
         st1, st2 = [], []
-        a = B.conv_fwd(c1, cat, st=st1)
+        a = B.conv_fwd(c1, cat, st=st1, x2=up)
         N, H, W = a.shape[:3]
         tgt = B._target[1] if (B._target is not None and i == len(B.deconvs) - 1) else None
         seg = B.model.segmap
@@ -804,13 +830,14 @@ class _DecFn(torch.autograd.Function):
             y = B.conv_fwd(c2, a, st=st2)
         ctx.B, ctx.i = B, i
         ctx.st = (st1[0] if st1 else None, st2[0] if st2 else None)
-        ctx.save_for_backward(x, cat, a)
+        ctx.dual = up is not None
+        ctx.save_for_backward(x, cat, a, up if up is not None else cat)
         return _o(y)
 
     @staticmethod
     def backward(ctx, g2):
         B, i = ctx.B, ctx.i
-        x, cat, a = ctx.saved_tensors
+        x, cat, a, up = ctx.saved_tensors
         st1, st2 = ctx.st
         d = B.deconvs[i]
         c1, c2 = B.dec_convs[i]
@@ -845,7 +872,10 @@ class _DecFn(torch.autograd.Function):
                 B.conv_wgrad(c2, g2, a)
                 g1, st_g = B.conv_dgrad(c2, g2, mask=a, below=c1)
         B.ready([c2.mod, c2.bn])
-        if B.fusable(c1, None, W):
+        if ctx.dual:
+            # the forward checked fusable() (dual_level): the fused backward reads [skip | up] too
+            (dskip, gup), _ = B.bwd_conv(c1, g1, cat, st1, mask=False, stats=st_g, split=C, x2=up)
+        elif B.fusable(c1, None, W):
             (dskip, gup), _ = B.bwd_conv(c1, g1, cat, st1, mask=False, stats=st_g, split=C)
         else:
             g1 = B.bn_bwd(c1, g1, st1, stats=st_g)

@@ -31,7 +31,7 @@ class IgemmArgs(ctypes.Structure):
                [("xbytes", ctypes.c_uint), ("pool", c_void_p), ("ldp", c_int), ("pcode", c_void_p), ("y2", c_void_p),
                 ("ldy2", c_int), ("split", c_int), ("hw", c_void_p), ("hb", c_void_p), ("tgt", c_void_p),
                 ("hslab", c_void_p), ("bnslab", c_void_p), ("korder", c_int), ("ximg", ctypes.c_uint),
-                ("hprob", c_void_p)]
+                ("hprob", c_void_p), ("x2", c_void_p)]
 
 
 class WgradArgs(ctypes.Structure):
@@ -49,7 +49,7 @@ class BwdArgs(ctypes.Structure):
                [("tgt", c_void_p), ("hw", c_void_p), ("hb", c_void_p), ("dS", c_void_p), ("hslab", c_void_p)] + \
                [("pcode", c_void_p), ("dpool", c_void_p), ("ldp", c_int)] + \
                [("x1", c_void_p), ("slab1", c_void_p), ("bslab1", c_void_p), ("x1bytes", ctypes.c_uint)] + \
-               [("z", c_void_p), ("bncoef", c_void_p), ("bnslab", c_void_p), ("hprob", c_void_p)]
+               [("z", c_void_p), ("bncoef", c_void_p), ("bnslab", c_void_p), ("hprob", c_void_p), ("x2", c_void_p)]
 
 
 class PackDesc(ctypes.Structure):
@@ -114,6 +114,9 @@ USE_FUSED_BN_BWD = CFG.fused_bn_bwd
 # the first encoder conv's weight gradient folded into the pool-mode backward of the second: opt-in,
 # slower at batch 256 (6.05 ms vs 5.3 ms for the two kernels it replaces; see csrc/bwd_stream.hip)
 USE_FUSED_W1 = CFG.fused_w1
+# the 32-channel level without a concat buffer: dense skip + dense up half, read by the decoder conv's
+# row-streaming forward and fused backward through their dual input (x2)
+USE_DUAL_INPUT = CFG.dual_input
 
 # TIMING ABLATION ONLY (numerically wrong results): the listed kernel families are skipped so a bench
 # run measures what they cost end to end.  Never read from the environment: set_timing_ablation() is
@@ -147,7 +150,7 @@ def igemm(x: torch.Tensor, wpacked: torch.Tensor, y: torch.Tensor, *, Ngemm: int
           mask: Optional[torch.Tensor] = None, mode: int = 0, Cout: int = 0, accumulate: bool = False, cfg: int = 0,
           path: str = "auto", pool: Optional[torch.Tensor] = None, variant: int = 0,
           pcode: Optional[torch.Tensor] = None, y2: Optional[torch.Tensor] = None, split: int = 0, head=None,
-          bn_stats: Optional[list] = None, persistent: bool = True):
+          bn_stats: Optional[list] = None, persistent: bool = True, x2: Optional[torch.Tensor] = None):
     """Implicit-GEMM conv.  ``out_grid`` = (N, Ho, Wo) pixel grid of GEMM-M.
 
     ``path``: ``auto`` picks, for a conv3x3, the row-streaming kernel (Ngemm, Cs in {32, 64}), then the
@@ -166,8 +169,14 @@ def igemm(x: torch.Tensor, wpacked: torch.Tensor, y: torch.Tensor, *, Ngemm: int
     with ``mask`` = the BN layer's output (dgrad into it): sum g, sum g*mask for :func:`bn_bwd`.
     ``persistent=False``: the LDS-DMA path never picks its persistent (one workgroup per CU) kernel --
     the backward passes it while side-stream weight gradients hold CUs, which a persistent grid
-    sized for the whole chip would otherwise wait for."""
+    sized for the whole chip would otherwise wait for.  ``x2``: dual input -- the conv input is the
+    channel concat [x | x2] of two tensors of identical layout (32 channels each, ``Cs`` = 64), read
+    by the row-streaming kernel from both (a decoder conv over [skip | up] without a concat buffer)."""
     N, Hs, Ws, Cx, ldx = _nhwc(x, "igemm.x")
+    if x2 is not None:
+        assert _nhwc(x2, "igemm.x2") == (N, Hs, Ws, Cx, ldx) and Cx == 32 and Cs == 64, "dual input: two [N,H,W,32]"
+        assert mode == 0 and pool is None and head is None and path in ("auto", "stream"), "dual input: plain stream conv"
+        Cx = Cs
     _, _, _, Cy, ldy = _nhwc(y, "igemm.y")
     No, Ho, Wo = out_grid
     assert No == N and Cs <= Cx and Cs % 8 == 0 and Kpad % 32 == 0 and Ngemm % 32 == 0
@@ -223,7 +232,11 @@ def igemm(x: torch.Tensor, wpacked: torch.Tensor, y: torch.Tensor, *, Ngemm: int
                       KH, KW, stride, pad, Ngemm, Kpad, mode, int(relu), int(accumulate), Cout,
                       0 if per_image else _extent_bytes(nb, Hs, Ws, Cx, ldx), None, 0, None,
                       None if y2 is None else y2[n0:n1].data_ptr(), ldy2, split)
-        a.ximg = _extent_bytes(1, Hs, Ws, Cx, ldx)
+        if x2 is not None:
+            a.x2 = x2[n0:n1].data_ptr()
+            a.ximg = _extent_bytes(1, Hs, Ws, 32, ldx)
+        else:
+            a.ximg = _extent_bytes(1, Hs, Ws, Cx, ldx)
         return a
 
     conv3 = mode == 0 and KH == 3 and stride == 1 and cfg == 0
@@ -271,8 +284,9 @@ def igemm(x: torch.Tensor, wpacked: torch.Tensor, y: torch.Tensor, *, Ngemm: int
         if err == 0:
             return
         a.pool, a.ldp, a.pcode = None, 0, None
-        if path == "stream":
+        if path == "stream" or x2 is not None:
             _check(err, "igemm_stream")
+    assert x2 is None, "dual input: only the row-streaming kernel reads it"
     # measured at batch 128 (tools/kbench.py, profiles/kbench_b128_512.txt): the two-row halo kernel
     # beats the LDS-DMA kernel on every shape both accept (128-channel dgrads: 837 vs 1042 us at
     # 128^2, 2542 vs 2948 us at 256^2); the LDS-DMA kernel takes what the halo kernel cannot
@@ -558,7 +572,7 @@ def bwd_pool_foldable(ci: int, co: int) -> bool:
 def conv_bwd_fused(g: Optional[torch.Tensor], x: torch.Tensor, wd: torch.Tensor, Kd: int, gw: torch.Tensor,
                    gb: Optional[torch.Tensor], *, mask: bool, dx: Optional[torch.Tensor] = None,
                    dx2: Optional[torch.Tensor] = None, split: int = 0, target_blocks: int = 0, head=None,
-                   pool=None, w1=None, bn=None, bn_stats: bool = False):
+                   pool=None, w1=None, bn=None, bn_stats: bool = False, x2: Optional[torch.Tensor] = None):
     """Backward of ``y = conv3x3(x) (+bias)`` in one pass (csrc/bwd_stream.hip): returns
     ``dx = conv3x3^T(g)`` (times ``x > 0`` when ``mask``; with ``dx2``/``split`` the channels
     ``>= split`` go to ``dx2``) and ACCUMULATES the weight gradient into ``gw`` (PyTorch OIHW
@@ -586,8 +600,15 @@ def conv_bwd_fused(g: Optional[torch.Tensor], x: torch.Tensor, wd: torch.Tensor,
     ``dz = coef3[c] g + coef3[C+c] z + coef3[2C+c]`` is formed on load (no dz pass over HBM).
     ``bn_stats``: ``x`` is the ReLU output of a BatchNorm (the dx mask); the kernel also writes that
     BN's backward partial sums (sum dx, sum dx*x per block, as :func:`igemm` ``bn_stats``) and the
-    function returns ``(dx, (slab, rows))``."""
+    function returns ``(dx, (slab, rows))``.
+
+    ``x2``: dual input -- the conv input is [x | x2] (two [N,H,W,32] tensors of identical layout), as
+    :func:`igemm` ``x2``; the kernel's x loader reads both."""
     Nx, Hx, Wx, CI, ldx = _nhwc(x, "bwd.x")
+    if x2 is not None:
+        assert _nhwc(x2, "bwd.x2") == (Nx, Hx, Wx, CI, ldx) and CI == 32, "dual input: two [N,H,W,32]"
+        assert head is None and pool is None and w1 is None, "dual input: plain / split / BN modes"
+        CI = 64
     if "bwd" in _ABLATE:
         N_, H_, W_ = Nx, Hx, Wx
         if w1 is not None:
@@ -640,7 +661,10 @@ def conv_bwd_fused(g: Optional[torch.Tensor], x: torch.Tensor, wd: torch.Tensor,
     a = BwdArgs(None if g is None else g.data_ptr(), x.data_ptr(), wd.data_ptr(), None if dx is None else dx.data_ptr(),
                 None if dx2 is None else dx2.data_ptr(),
                 slab.data_ptr(), None if bslab is None else bslab.data_ptr(), ldg, ldx, ldy, ldy2, split, Kd,
-                N, H, W, rh, 1, _extent_bytes(1, H, W, CO, ldg) if g is not None else 0, _extent_bytes(1, H, W, CI, ldx))
+                N, H, W, rh, 1, _extent_bytes(1, H, W, CO, ldg) if g is not None else 0,
+                _extent_bytes(1, H, W, 32 if x2 is not None else CI, ldx))
+    if x2 is not None:
+        a.x2 = x2.data_ptr()
     st = _stream(x)
     if pool is not None:
         code, dpool = pool

@@ -33,6 +33,7 @@ from __future__ import annotations
 
 import itertools
 import json
+import os
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -206,3 +207,29 @@ def plan(table: dict, S: int, batch: int, cuts: Optional[Sequence[int]] = None, 
 def load_table(path: str) -> dict:
     with open(path) as f:
         return json.load(f)
+
+
+# ------------------------------------------------------------------------------------ chosen plans
+PLANS_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "plans.json")
+
+
+def plan_key(model: str, h: int, w: int, stages: int, batch: int) -> str:
+    return f"{model}:{h}x{w}:{stages}:{batch}"
+
+
+def load_plan(model: str, h: int, w: int, stages: int, batch: int, path: str = None) -> Optional[dict]:
+    """The time-balanced plan tools/pipeline_plan.py chose from measured block times for this
+    (model, image, stages, global batch): {"cuts", "microbatches", "predicted_img_s", ...}, or None."""
+    path = path or PLANS_PATH
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        plans = json.load(f)
+    p = plans.get(plan_key(model, h, w, stages, batch))
+    if p is None:
+        return None
+    cuts = [int(c) for c in p["cuts"]]
+    M = int(p["microbatches"])
+    if len(cuts) != stages + 1 or cuts[0] != 0 or any(b <= a for a, b in zip(cuts, cuts[1:])) or batch % M:
+        raise ValueError(f"malformed pipeline plan {plan_key(model, h, w, stages, batch)}: {p}")
+    return dict(p, cuts=cuts, microbatches=M)

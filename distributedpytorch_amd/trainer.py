@@ -22,7 +22,7 @@ import torch
 import torch.distributed as dist
 
 from .compute import loss_from_partials, make_compute, resolve_backend
-from .config import TrainConfig, dist_env, mp_cut_mode
+from .config import TrainConfig, dist_env, mp_plan
 from .data import CarvanaDataset, SyntheticSegmentation, build_loaders, split_dataset
 from .data.device import DeviceLoader, DeviceSyntheticSegmentation, device_loaders
 from .data.loaders import DeviceBatcher
@@ -249,8 +249,9 @@ class PipelineLocalStrategy(Strategy):
     def __init__(self, cfg, model, devices):
         super().__init__(cfg)
         H, W = cfg.img_size
-        self.pipe = GPipeLocal(model, devices, cfg.microbatches, cfg.backend, cfg.dtype, img_hw=(H, W),
-                               mode=mp_cut_mode(cfg, len(devices)))
+        mode, cuts, M = mp_plan(cfg, len(devices))
+        self.pipe = GPipeLocal(model, devices, M, cfg.backend, cfg.dtype, img_hw=(H, W),
+                               mode="balanced" if mode == "time" else mode, cuts=cuts)
         self.model = model
         self.device = self.pipe.devices[0]
         self.optimizer = FusedAdam(self.pipe.spaces, lr=cfg.lr, weight_decay=cfg.weight_decay)
@@ -278,8 +279,9 @@ class PipelineDistStrategy(Strategy):
         self.device = torch.device(device)
         self.model = model.to(self.device)
         H, W = cfg.img_size
-        self.pipe = GPipeDist(self.model, cfg.microbatches, cfg.backend, cfg.dtype, img_hw=(H, W),
-                              mode=mp_cut_mode(cfg, self.world))
+        mode, cuts, M = mp_plan(cfg, self.world)
+        self.pipe = GPipeDist(self.model, M, cfg.backend, cfg.dtype, img_hw=(H, W),
+                              mode="balanced" if mode == "time" else mode, cuts=cuts)
         self.is_main = self.pipe.is_last  # the last stage owns the loss; rank 0 saves
         self.optimizer = FusedAdam(self.pipe.space, lr=cfg.lr, weight_decay=cfg.weight_decay)
 

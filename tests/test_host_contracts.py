@@ -99,6 +99,28 @@ def test_stream_igemm_rejects(L, kw):
     assert L.dpa_igemm_stream(ctypes.byref(_igemm_args(**kw)), 0, None) == INVALID
 
 
+def test_dual_input_only_on_the_stream_kernels(L):
+    """A dual conv input (IgemmArgs.x2 / BwdArgs.x2: channels 32-63 from a second tensor) is read only
+    by the row-streaming forward at Cs = 64 and the fused backward at 64 input channels; every other
+    launcher refuses it instead of silently reading [x | garbage]."""
+    dual = dict(Cs=64, Kpad=576, ldx=32, ximg=64 * 64 * 32 * 2)
+    for launch in (lambda a: L.dpa_igemm(ctypes.byref(a), 0, None), lambda a: L.dpa_igemm_halo(ctypes.byref(a), 0, None),
+                   lambda a: L.dpa_igemm_glds(ctypes.byref(a), 0, None)):
+        a = _igemm_args(**dual)
+        a.x2 = 0x1000
+        assert launch(a) == INVALID
+    for kw in (dict(Cs=32, Kpad=288), dict(ldx=16), dict(ximg=64 * 64 * 32 * 2 - 66)):
+        a = _igemm_args(**{**dual, **kw})
+        a.x2 = 0x1000
+        assert L.dpa_igemm_stream(ctypes.byref(a), 0, None) == INVALID, kw
+    from distributedpytorch_amd.ops import kernels as K
+    b = K.BwdArgs(ldg=32, ldx=32, ldy=32, Kd=288, N=1, H=64, W=64, rh=64, ipb=1)
+    b.x2 = 0x1000
+    assert L.dpa_bwd_stream(ctypes.byref(b), 32, 32, 0, None) == INVALID            # 32 input channels
+    b.ldx = 16
+    assert L.dpa_bwd_stream(ctypes.byref(b), 64, 32, 0, None) == INVALID            # a plane is 32 channels
+
+
 def test_stream_block_count_matches_launch_geometry(L):
     # variant 1 (Cs = Ngemm = 32): 128-pixel strips, 32-row segments when there are >= 1024 of them
     a = _igemm_args(N=128, Ho=512, Wo=512, Hs=512, Ws=512)

@@ -1,5 +1,7 @@
 """GPipe schedule model (parallel/schedule.py) against hand-computed timelines, and the
 time-balanced partitioner on a synthetic block-time table (CPU only)."""
+import os
+
 import pytest
 
 from distributedpytorch_amd.parallel.schedule import (StageCost, best_partition, boundary_bytes, partitions,
@@ -77,3 +79,46 @@ def test_deferred_wgrad_accounting():
     # same total backward work, split into per-microbatch dgrads + one merged weight-gradient tail
     for x, y in zip(a, b):
         assert x.bwd * 4 + x.wgrad == pytest.approx(y.bwd * 4)
+
+
+def test_plan_lookup_drives_mp_defaults(tmp_path, monkeypatch):
+    """parallel/plans.json (tools/pipeline_plan.py output) sets the MP cut and microbatch count for the
+    configurations it covers; others fall back to the reference / FLOP-balanced cut; an explicit
+    --microbatches wins; a malformed plan is an error, not a silent default."""
+    import json
+    from distributedpytorch_amd.config import TrainConfig, mp_plan
+    from distributedpytorch_amd.parallel import schedule as sch
+    path = tmp_path / "plans.json"
+    path.write_text(json.dumps({"unet:512x512:2:256": {"cuts": [0, 4, 10], "microbatches": 8,
+                                                       "predicted_img_s": 5000.0}}))
+    monkeypatch.setattr(sch, "PLANS_PATH", str(path))
+    cfg = TrainConfig(model="unet", img_size=(512, 512), batch_size=256)
+    assert mp_plan(cfg, 2) == ("time", [0, 4, 10], 8)
+    cfg.microbatches = 4
+    assert mp_plan(cfg, 2) == ("time", [0, 4, 10], 4)
+    cfg.mp_cut = "reference"
+    assert mp_plan(cfg, 2) == ("reference", None, 4)
+    cfg = TrainConfig(model="unet", img_size=(512, 512), batch_size=128)        # no plan for this batch
+    assert mp_plan(cfg, 2) == ("reference", None, 2)
+    assert mp_plan(cfg, 4, default_microbatches=8) == ("balanced", None, 8)
+    cfg.mp_cut = "time"
+    assert mp_plan(cfg, 2)[0] == "balanced"
+    path.write_text(json.dumps({"unet:512x512:2:256": {"cuts": [0, 10, 4], "microbatches": 8}}))
+    with pytest.raises(ValueError):
+        sch.load_plan("unet", 512, 512, 2, 256)
+
+
+def test_shipped_plans_are_well_formed():
+    import json
+    from distributedpytorch_amd.models.blocks import n_blocks
+    from distributedpytorch_amd.models.unet import PRESETS
+    from distributedpytorch_amd.parallel import schedule as sch
+    if not os.path.exists(sch.PLANS_PATH):
+        pytest.skip("no plans shipped")
+    with open(sch.PLANS_PATH) as f:
+        plans = json.load(f)
+    for key in plans:
+        model, hw, S, batch = key.split(":")
+        h, w = map(int, hw.split("x"))
+        p = sch.load_plan(model, h, w, int(S), int(batch))
+        assert p["cuts"][-1] == n_blocks(PRESETS[model].depth)

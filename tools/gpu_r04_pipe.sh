@@ -2,7 +2,7 @@
 # Round-4 iteration: tests of the changed kernels, slice-staged GEMM timing, bench, per-block time tables.
 set -o pipefail
 cd "$(dirname "$0")/.." && export TMPDIR=/tmp && mkdir -p gpurun_out/sl gpurun_out/pipe
-timeout -k 10 900 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_rowblock.py tests/test_bwd_fused.py tests/test_hip_kernels.py tests/test_hip_model.py > gpurun_out/sl/pytest.log 2>&1
+timeout -k 10 900 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_dual_input.py tests/test_rowblock.py tests/test_bwd_fused.py tests/test_hip_kernels.py tests/test_hip_model.py > gpurun_out/sl/pytest.log 2>&1
 rc=$?; tail -3 gpurun_out/sl/pytest.log; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 300 python bench.py > gpurun_out/sl/bench.log 2>&1 || { echo bench failed; tail -3 gpurun_out/sl/bench.log; exit 1; }
 tail -1 gpurun_out/sl/bench.log | cut -c1-200
