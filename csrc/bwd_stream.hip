@@ -68,6 +68,10 @@ struct BwdArgs {
   // dual input (CI == 64): channels 32-63 of x come from this second tensor, laid out like x (same
   // ldx, xbytes) -- the decoder conv over [skip | up] without a concat buffer
   const bf16_t* x2;
+  // BN-on-load of x (BN mode 2: x is the ReLU output of a BatchNorm layer below): x holds that layer's
+  // pre-BN output z and the loader forms relu(z * xbn[c] + xbn[CI + c]) (the forward's bn_apply
+  // arithmetic) -- the BN output is never stored in the forward
+  const float* xbn;
 };
 
 // 8 consecutive k (pixel rows roff+8g .. +7) of 16 channels starting at col0, from an nk image
@@ -133,6 +137,8 @@ __global__ __launch_bounds__(64 * NW, 2) void bwd_stream_kernel(BwdArgs a) {
   constexpr int BCH = BP * 4 * KSO, LBI = (BCH + NT - 1) / NT;   // bias: chunks of the g row's BP pixels
   __shared__ __attribute__((aligned(16))) char lds[WBYTES + 4 * GSLOT + 4 * XSLOT + W1BYTES];
   __shared__ __attribute__((aligned(16))) float bnc[BNL ? 3 * CO : 4];   // BN mode: the dz coefficients
+  constexpr bool XBN = BNS;                     // x = relu(bn(z)) formed on load (a.xbn)
+  __shared__ __attribute__((aligned(16))) float xbc[XBN ? 2 * CI : 4];
   char* const Wimg = lds;
   char* const Gring = lds + WBYTES;
   char* const Xring = Gring + 4 * GSLOT;
@@ -181,8 +187,11 @@ __global__ __launch_bounds__(64 * NW, 2) void bwd_stream_kernel(BwdArgs a) {
     const u32x4_t v = *reinterpret_cast<const u32x4_t*>(a.wd + (long)row * a.Kd + tap * CO + ks * 32 + cc * 8);
     *reinterpret_cast<u32x4_t*>(Wimg + (tk * CI + row) * 64 + (swz_nk<32>(row, cc) << 4)) = v;
   }
+  const bool xbn = XBN && a.xbn != nullptr;
   if constexpr (BNL) {
     for (int i = tid; i < 3 * CO; i += NT) bnc[i] = a.bncoef[i];
+    if (xbn)
+      for (int i = tid; i < 2 * CI; i += NT) xbc[i] = a.xbn[i];
     __syncthreads();
   }
   // ---- loader constants
@@ -374,6 +383,23 @@ __global__ __launch_bounds__(64 * NW, 2) void bwd_stream_kernel(BwdArgs a) {
 #pragma unroll
     for (int j = 0; j < LG; ++j)
       if (gsto[j] >= 0) *reinterpret_cast<u32x4_t*>(Gring + slot * GSLOT + gsto[j]) = R.g[j];
+    if constexpr (XBN) {                        // z chunk -> relu(bn(z)) chunk (padding stays zero)
+      const bool rok = ih >= 0 && ih < a.H;
+      if (xbn && rok) {
+#pragma unroll
+        for (int j = 0; j < LX; ++j) {
+          if (!xok[j]) continue;
+          const int cb = dual ? (xpl[j] ? 32 : 0) + (tid & 3) * 8 : (tid % (CI / 8)) * 8;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const float2 sc = *reinterpret_cast<const float2*>(xbc + cb + 2 * k);
+            const float2 sh = *reinterpret_cast<const float2*>(xbc + CI + cb + 2 * k);
+            R.x[j][k] = pack_bf2(fmaxf(fmaf(lo_bf(R.x[j][k]), sc.x, sh.x), 0.f),
+                                 fmaxf(fmaf(hi_bf(R.x[j][k]), sc.y, sh.y), 0.f));
+          }
+        }
+      }
+    }
 #pragma unroll
     for (int j = 0; j < LX; ++j)
       if (xsto[j] >= 0) *reinterpret_cast<u32x4_t*>(Xring + slot * XSLOT + xsto[j]) = R.x[j];
@@ -780,7 +806,7 @@ DPA_API int dpa_bwd_stream(const BwdArgs* args, int ci, int co, int epi, hipStre
   if (!bwd_cfg(ci, co, &bp, &nw) || (fused_mode && a.W % bp) || a.W < 16 || (a.ldg & 7) || (a.ldx & 7) || (a.ldy & 3) ||
       a.rh < 1 || a.ipb < 1 ||
       a.Kd < 9 * co || (epi == 1 && (a.y2 == nullptr || (a.ldy2 & 3) || a.split % 16 || a.split <= 0 || a.split >= ci)) ||
-      (a.x2 && (ci != 64 || a.ldx < 32 || fused_mode)))
+      (a.x2 && (ci != 64 || a.ldx < 32 || fused_mode)) || (a.xbn && (a.z == nullptr || a.bnslab == nullptr)))
     return (int)hipErrorInvalidValue;
   // BN modes: the gradient source is plain (no pool / head / first-conv fold); statistics for the
   // layer below only with the masked dx

@@ -39,6 +39,8 @@ struct IgemmArgs {
   const bf16_t* x2;     // dual input (row-streaming kernel, Cs == 64 only): channels 32-63 of the conv input
                         // come from this second tensor, laid out like x ([N][Hs][Ws][ldx], same ximg) --
                         // a decoder conv over [skip | up] reads the two dense halves, no concat buffer
+  const float* xbn;     // BN-on-load (row-streaming kernel with BN statistics, EPI 4): x holds the layer
+                        // below's pre-BatchNorm output z; the loader forms relu(z * xbn[c] + xbn[Cs + c])
 };
 
 // 2x2 window code from the four (bf16-rounded) values in window order tl, tr, bl, br: first

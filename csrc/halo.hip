@@ -273,7 +273,7 @@ static bool tiles_ok(int W, int bp) {
 DPA_API int dpa_igemm_halo(const IgemmArgs* args, int cfg, hipStream_t st) {
   const IgemmArgs& a = *args;
   if (a.mode != 0 || a.KH != 3 || a.KW != 3 || a.stride != 1 || a.pad != 1 || (a.Cs % 32) || (a.ldx & 7) ||
-      (a.ldy & 3) || a.Hs != a.Ho || a.Ws != a.Wo || a.Kpad < 9 * a.Cs || !ximg_ok(a) || a.x2)
+      (a.ldy & 3) || a.Hs != a.Ho || a.Ws != a.Wo || a.Kpad < 9 * a.Cs || !ximg_ok(a) || a.x2 || a.xbn)
     return (int)hipErrorInvalidValue;
   if (cfg == 0) {
     if (a.Ngemm == 32 && tiles_ok(a.Wo, 256)) cfg = 1;
@@ -540,13 +540,27 @@ __global__ __launch_bounds__(256 * WCS) void igemm_stream_kernel(IgemmArgs a) {
     lsto[j] = live ? (ks * HR + px) * 64 + (swz_nk<32>(px, cc) << 4) : -1;
   }
   const unsigned rowbytes_x = (unsigned)(a.Ws * a.ldx * 2);
+  // BN-on-load (EPI 4, a.xbn): the input is the PRE-BatchNorm output z of the layer below and the
+  // loader stores y = relu(z * xbn[c] + xbn[CS + c]) into the ring -- bn_apply's exact arithmetic,
+  // so the layer below never writes y (its BN+ReLU pass over HBM disappears); padding stays zero
+  constexpr bool XBN = EPI == 4;
+  __shared__ float xbc[XBN ? 2 * CS : 1];
+  const bool xbn = XBN && a.xbn != nullptr;
+  if constexpr (XBN) {
+    if (xbn) {
+      for (int i = tid; i < 2 * CS; i += NT) xbc[i] = a.xbn[i];
+      __syncthreads();
+    }
+  }
   // two register sets: a row's loads are issued two rows before it is stored into the ring
   struct RowRegs {
     u32x4_t v[LR];
+    bool rok;
   };
   RowRegs setA, setB;
   auto rload = [&](int ih, RowRegs& R) {
     const bool rok = ih >= 0 && ih < a.Hs;                     // wave-uniform
+    R.rok = rok;
     const unsigned rbase = (unsigned)ih * rowbytes_x;
 #pragma unroll
     for (int j = 0; j < LR; ++j) {
@@ -556,8 +570,23 @@ __global__ __launch_bounds__(256 * WCS) void igemm_stream_kernel(IgemmArgs a) {
   };
   auto rstore = [&](int slot, const RowRegs& R) {
 #pragma unroll
-    for (int j = 0; j < LR; ++j)
-      if (lsto[j] >= 0) *reinterpret_cast<u32x4_t*>(Ring + slot * SLOT + lsto[j]) = R.v[j];
+    for (int j = 0; j < LR; ++j) {
+      u32x4_t v = R.v[j];
+      if constexpr (XBN) {
+        if (xbn && R.rok && lok[j]) {
+          // chunk j's first channel: slice ks (plane for a dual input) * 32 + (c & 3) * 8
+          const int c = tid + j * NT;
+          const int cb = (dual ? (lpl[j] ? 32 : 0) : ((c >> 2) / HR) * 32) + (c & 3) * 8;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const float2 sc = *reinterpret_cast<const float2*>(xbc + cb + 2 * k);
+            const float2 sh = *reinterpret_cast<const float2*>(xbc + CS + cb + 2 * k);
+            v[k] = pack_bf2(fmaxf(fmaf(lo_bf(v[k]), sc.x, sh.x), 0.f), fmaxf(fmaf(hi_bf(v[k]), sc.y, sh.y), 0.f));
+          }
+        }
+      }
+      if (lsto[j] >= 0) *reinterpret_cast<u32x4_t*>(Ring + slot * SLOT + lsto[j]) = v;
+    }
   };
   // ---- per-lane LDS fragment offsets and epilogue constants
   const int chunk = lane >> 4;
@@ -1009,7 +1038,8 @@ DPA_API int dpa_igemm_stream(const IgemmArgs* args, int variant, hipStream_t st)
   // dropped); the fused pool needs whole 2x2 windows along the row (even width)
   if (a.mode != 0 || a.KH != 3 || a.KW != 3 || a.stride != 1 || a.pad != 1 || (a.ldx & 7) || (a.ldy & 3) ||
       a.Hs != a.Ho || a.Ws != a.Wo || a.Wo < 16 || a.Kpad < 9 * a.Cs || !ximg_ok(a) ||
-      (a.pool && ((a.ldp & 3) || (a.Wo & 1) || !a.relu)) || (a.x2 && (a.Cs != 64 || a.ldx < 32)))
+      (a.pool && ((a.ldp & 3) || (a.Wo & 1) || !a.relu)) || (a.x2 && (a.Cs != 64 || a.ldx < 32)) ||
+      (a.xbn && (a.bnslab == nullptr || a.mask || a.pool || a.hslab || a.Cs == 8)))     // BN-on-load: the EPI 4 kernels only
     return (int)hipErrorInvalidValue;
   if (a.Cs == 8 && a.Ngemm == 32 && !a.pool) return launch_igemm_stream8<128, 32>(a, st);
   if (variant == 0) variant = stream_auto_variant(a);

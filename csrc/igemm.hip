@@ -231,7 +231,7 @@ static int launch_igemm(const IgemmArgs& a, hipStream_t st) {
 //      8: 256x128x64 (8 waves)  9: 128x256x64 (8 waves)
 DPA_API int dpa_igemm(const IgemmArgs* args, int cfg, hipStream_t st) {
   IgemmArgs a = *args;
-  if ((a.Cs & 7) || (a.ldx & 7) || (a.ldy & 3) || (a.Kpad & 31) || (a.Ngemm & 31) || a.x2) return (int)hipErrorInvalidValue;
+  if ((a.Cs & 7) || (a.ldx & 7) || (a.ldy & 3) || (a.Kpad & 31) || (a.Ngemm & 31) || a.x2 || a.xbn) return (int)hipErrorInvalidValue;
   if (a.mode == 1 && (a.Cout & 3)) return (int)hipErrorInvalidValue;
   if (cfg == 0) {
     const long M = (long)a.N * a.Ho * a.Wo;

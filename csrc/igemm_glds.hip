@@ -1726,7 +1726,7 @@ DPA_API int dpa_igemm_glds(const IgemmArgs* args, int cfg, hipStream_t st) {
   const bool rb2 = cfg & 16384;         // auto: the two-phase row-block kernels (cfg 16 / 17) in place of 14 / 15
   cfg = (cfg & 65536) ? 16 : (cfg & 131072) ? 17 : (cfg & 262144) ? 18 : (cfg & 524288) ? 19 : (cfg & 15);
   const bool sl = cfg == 18 || cfg == 19;
-  if ((a.Cs & (sl ? 31 : 63)) || (a.Kpad & 63) || (a.ldx & 7) || (a.ldy & 3) || a.KH * a.KW > 32 || (a.korder & 1) || a.x2)
+  if ((a.Cs & (sl ? 31 : 63)) || (a.Kpad & 63) || (a.ldx & 7) || (a.ldy & 3) || a.KH * a.KW > 32 || (a.korder & 1) || a.x2 || a.xbn)
     return (int)hipErrorInvalidValue;
   if (a.bnslab) {
     // BatchNorm partial sums (bnslab[M / 256][2][Ngemm]): only the row-block kernels' EP 1 / 2 epilogues

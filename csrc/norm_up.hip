@@ -320,6 +320,8 @@ DPA_API int dpa_bn_fwd(const bf16_t* z, int ldz, bf16_t* y, int ldy, long long P
     hipLaunchKernelGGL(bn_finalize_kernel, dim3(C), dim3(256), 0, st, (const float*)nullptr, 0, C, (long)P, gamma, beta, eps,
                        momentum, rmean, rvar, coef, saved);
   }
+  // coefficients only (y == pool == null): the consumer applies the BN + ReLU on load (IgemmArgs::xbn)
+  if (y == nullptr && pool == nullptr) return (int)hipGetLastError();
   if (pool) {
     const long tot = (long)P / 4 * (C / 8);
     hipLaunchKernelGGL(bn_apply_pool_kernel, dim3(dpa_grid(tot, 256, 16384)), dim3(256), 0, st, z, ldz, y, ldy, pool, ldp,

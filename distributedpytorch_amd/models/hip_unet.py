@@ -216,11 +216,38 @@ class HipBlocks:
         return self.packed[c.off_d:c.off_d + c.Cin * c.Kd]
 
     # ------------------------------------------------------------------ primitive launches
+    def bn_on_load(self, c1: _Conv, c2: _Conv, W: int) -> bool:
+        """DoubleConv conv1 -> BN -> ReLU -> conv2 -> BN at the 32/64-channel levels (training): conv1
+        stops at its pre-BN output z (statistics from its epilogue, :meth:`conv_bn_z`) and conv2 forms
+        relu(bn(z)) in its row-streaming loader, forward and fused backward (``xbn``).  The BN output
+        of conv1 -- a full-resolution tensor per DoubleConv -- is never written, read or kept."""
+        if not (K.USE_BN_ON_LOAD and K.USE_STREAM and K.USE_FUSED_BN and self.model.training):
+            return False
+        if c1.bn is None or c2.bn is None or not (c2.Cs == c2.Cin == c1.Cout and c2.Cin in (32, 64)
+                                                  and c2.Cout in (32, 64)):
+            return False
+        return self.fusable(c2, c1, W)
+
+    def conv_bn_z(self, c: _Conv, x: torch.Tensor, st: list):
+        """Training conv + BatchNorm statistics without the normalise pass: returns (z, coef) with the
+        consumer's on-load transform relu(z * coef[c] + coef[C + c]); ``st`` receives (z, saved)."""
+        N, H, W = x.shape[:3]
+        z = torch.empty(N, H, W, c.Cout, dtype=torch.bfloat16, device=x.device)
+        self._bn_stats_version += 1
+        stats = []
+        K.igemm(x, self.wf(c), z, Ngemm=c.Cout, Kpad=c.Kf, KH=3, KW=3, stride=1, pad=1, Cs=c.Cs, out_grid=(N, H, W),
+                bias=c.mod.bias, relu=False, bn_stats=stats)
+        coef = []
+        saved = K.bn_fwd(z, None, c.bn, train=True, stats=stats, coef_out=coef)
+        st.append((z, saved))
+        return z, coef[0]
+
     def conv_fwd(self, c: _Conv, x: torch.Tensor, y: torch.Tensor = None, pool: torch.Tensor = None,
-                 pcode: torch.Tensor = None, st: list = None, x2: torch.Tensor = None):
+                 pcode: torch.Tensor = None, st: list = None, x2: torch.Tensor = None, xbn: torch.Tensor = None):
         """relu(conv(x)) -> y (and its 2x2 max-pool + window codes).  BN variant: the conv writes z,
         then one statistics pass + one normalise/ReLU pass; ``st`` receives (z, saved) for the backward.
-        ``x2``: dual input, the conv reads [x | x2] (:meth:`dual_level`)."""
+        ``x2``: dual input, the conv reads [x | x2] (:meth:`dual_level`).  ``xbn``: ``x`` is the layer
+        below's pre-BN output and the conv reads relu(bn(x)) (:meth:`bn_on_load`)."""
         N, H, W = x.shape[:3]
         if y is None:
             y = torch.empty(N, H, W, c.Cout, dtype=torch.bfloat16, device=x.device)
@@ -229,6 +256,7 @@ class HipBlocks:
                     out_grid=(N, H, W), bias=c.mod.bias, relu=True, pool=pool, pcode=pcode, x2=x2)
             return y
         assert x2 is None, "dual input: convs without BatchNorm"
+        assert xbn is None or self.model.training, "BN-on-load: training forward"
         if not self.model.training and K.FOLD_BN_EVAL and c.bn.track_running_stats and c.bn.running_mean is not None:
             # inference: BatchNorm with running statistics is a per-channel affine map -> folded into
             # the conv's weights and bias, so Conv2d+BN+ReLU(+pool) is ONE fused kernel, as without BN
@@ -241,7 +269,7 @@ class HipBlocks:
             self._bn_stats_version += 1                 # running statistics move (eval fold cache)
         stats = [] if self.model.training else None    # batch statistics from the conv epilogue
         K.igemm(x, self.wf(c), z, Ngemm=c.Cout, Kpad=c.Kf, KH=3, KW=3, stride=1, pad=1, Cs=c.Cs, out_grid=(N, H, W),
-                bias=c.mod.bias, relu=False, bn_stats=stats)
+                bias=c.mod.bias, relu=False, bn_stats=stats, xbn=xbn)
         saved = K.bn_fwd(z, y, c.bn, train=self.model.training, stats=stats, pool=pool, pcode=pcode)
         if st is not None:
             st.append((z, saved))
@@ -359,7 +387,7 @@ class HipBlocks:
         return K.conv_bwd_fused(g, x, self.wd(c), c.Kd, gw, gb, mask=mask, head=head, pool=pool)
 
     def bwd_conv(self, c: _Conv, g: torch.Tensor, x: torch.Tensor, st, *, mask: bool, below: _Conv = None,
-                 stats: list = None, split: int = 0, x2: torch.Tensor = None):
+                 stats: list = None, split: int = 0, x2: torch.Tensor = None, xbn: torch.Tensor = None):
         """Fused backward of ``c`` (:meth:`fusable`) when ``g`` is the gradient of its output -- of its
         BatchNorm+ReLU output if it has one (``st`` = that BN's saved (z, mean/invstd), ``stats`` = the
         BN's backward partial sums from whoever produced ``g``, if any): the BN backward is formed in the
@@ -377,7 +405,7 @@ class HipBlocks:
             N, H, W = x.shape[:3]
             dx2 = torch.empty(N, H, W, c.Cin - split, dtype=torch.bfloat16, device=x.device)
         res = K.conv_bwd_fused(g, x, self.wd(c), c.Kd, gw, gb, mask=mask, dx2=dx2, split=split, bn=bn, bn_stats=want,
-                               x2=x2)
+                               x2=x2, xbn=xbn)
         return res if want else (res, None)
 
     def halves_fusable(self, c: _Conv, C: int, W: int) -> bool:
@@ -674,7 +702,11 @@ class _EncFn(torch.autograd.Function):
         x = _v(x)
         N, H, W = x.shape[:3]
         st1, st2 = [], []
-        a = B.conv_fwd(c1, x, st=st1)
+        xbn1 = None
+        if B.bn_on_load(c1, c2, W):
+            a, xbn1 = B.conv_bn_z(c1, x, st1)         # a = conv1's pre-BN output; conv2 applies BN + ReLU
+        else:
+            a = B.conv_fwd(c1, x, st=st1)
         if l in B.dense_skips or B.dual_level(l, H, W):
             cat = None
             skip = torch.empty(N, H, W, c2.Cout, dtype=torch.bfloat16, device=x.device)
@@ -685,8 +717,9 @@ class _EncFn(torch.autograd.Function):
         # window codes (argmax + ReLU masks) for the backward: it then never re-reads the skip
         code = (torch.empty(N, H // 2, W // 2, c2.Cout, dtype=torch.uint8, device=x.device)
                 if H % 2 == 0 and W % 2 == 0 else None)
-        B.conv_fwd(c2, a, skip, pool=pooled, pcode=code, st=st2)   # pool fused into the conv epilogue when streaming
+        B.conv_fwd(c2, a, skip, pool=pooled, pcode=code, st=st2, xbn=xbn1)   # pool fused into the conv epilogue when streaming
         ctx.B, ctx.l = B, l
+        ctx.xbn1 = xbn1
         ctx.x_needs_grad = l > 0
         ctx.has_code = code is not None
         ctx.st = (st1[0] if st1 else None, st2[0] if st2 else None)
@@ -733,11 +766,13 @@ class _EncFn(torch.autograd.Function):
             else:
                 K.pool_bwd(skip, dskip, dpooled, g2)
             if B.fusable(c2, c1, W):
-                g1, st_g = B.bwd_conv(c2, g2, a, st2, mask=True, below=c1)
+                g1, st_g = B.bwd_conv(c2, g2, a, st2, mask=True, below=c1, xbn=ctx.xbn1)
             else:
+                assert ctx.xbn1 is None, "BN-on-load forward needs the fused backward"
                 g2 = B.bn_bwd(c2, g2, st2)
                 B.conv_wgrad(c2, g2, a)              # side stream: overlaps the dgrad chain
                 g1, st_g = B.conv_dgrad(c2, g2, mask=a, below=c1)
+        ctx.xbn1 = None
         B.ready([c2.mod, c2.bn])
         if ctx.x_needs_grad and B.fusable(c1, None, W):
             # the pool backward below applies the ReLU mask
@@ -812,7 +847,11 @@ class _DecFn(torch.autograd.Function):
             up = None
         B.deconv_fwd(d, x, cat[..., C:] if up is None else up)
         st1, st2 = [], []
-        a = B.conv_fwd(c1, cat, st=st1, x2=up)
+        xbn1 = None
+        if up is None and B.bn_on_load(c1, c2, w2):
+            a, xbn1 = B.conv_bn_z(c1, cat, st1)       # a = conv1's pre-BN output; conv2 applies BN + ReLU
+        else:
+            a = B.conv_fwd(c1, cat, st=st1, x2=up)
         N, H, W = a.shape[:3]
         tgt = B._target[1] if (B._target is not None and i == len(B.deconvs) - 1) else None
         seg = B.model.segmap
@@ -827,7 +866,8 @@ class _DecFn(torch.autograd.Function):
                         head=(seg.weight.view(-1), seg.bias, tgt, hprob))
             B._head_cache = (y.data_ptr(), tgt.data_ptr(), S, hprob)
         else:
-            y = B.conv_fwd(c2, a, st=st2)
+            y = B.conv_fwd(c2, a, st=st2, xbn=xbn1)
+        ctx.xbn1 = xbn1
         ctx.B, ctx.i = B, i
         ctx.st = (st1[0] if st1 else None, st2[0] if st2 else None)
         ctx.dual = up is not None
@@ -866,8 +906,9 @@ class _DecFn(torch.autograd.Function):
                 g2 = (gy.float() + g2.float()).to(torch.bfloat16).contiguous()
             W = g2.shape[2]
             if B.fusable(c2, c1, W):
-                g1, st_g = B.bwd_conv(c2, g2, a, st2, mask=True, below=c1)
+                g1, st_g = B.bwd_conv(c2, g2, a, st2, mask=True, below=c1, xbn=ctx.xbn1)
             else:
+                assert ctx.xbn1 is None, "BN-on-load forward needs the fused backward"
                 g2 = B.bn_bwd(c2, g2, st2)
                 B.conv_wgrad(c2, g2, a)
                 g1, st_g = B.conv_dgrad(c2, g2, mask=a, below=c1)

@@ -55,6 +55,8 @@ KNOBS = (
     Knob("fused_bn_bwd", "DPA_FUSED_BN_BWD", True, "BatchNorm backward formed in the fused backward's loader (=0 opts out)"),
     Knob("fused_w1", "DPA_FUSED_W1", False, "first conv's weight gradient in the pool-mode fused backward (slower at b256)"),
     Knob("fused_deconv", "DPA_NO_FUSED_DECONV", True, "full-resolution transposed conv: fused forward / backward"),
+    Knob("bn_on_load", "DPA_NO_BN_ON_LOAD", True, "DoubleConv with BatchNorm: the second conv forms relu(bn(z)) of the "
+         "first on load (forward and fused backward); the first conv's BN output is never stored"),
     Knob("dual_input", "DPA_NO_DUAL_INPUT", True, "32-channel level: skip and up half as two dense tensors read by the "
          "decoder conv (no concat buffer)"),
     # launch geometry / streams
@@ -111,6 +113,7 @@ class KernelConfig:
     fused_w1: bool = False
     fused_deconv: bool = True
     dual_input: bool = True
+    bn_on_load: bool = True
     side_priority: int = 0
     wgrad_stream_blocks: int = 2048
     wgrad_gemm_blocks: int = 768

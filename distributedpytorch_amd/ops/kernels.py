@@ -31,7 +31,7 @@ class IgemmArgs(ctypes.Structure):
                [("xbytes", ctypes.c_uint), ("pool", c_void_p), ("ldp", c_int), ("pcode", c_void_p), ("y2", c_void_p),
                 ("ldy2", c_int), ("split", c_int), ("hw", c_void_p), ("hb", c_void_p), ("tgt", c_void_p),
                 ("hslab", c_void_p), ("bnslab", c_void_p), ("korder", c_int), ("ximg", ctypes.c_uint),
-                ("hprob", c_void_p), ("x2", c_void_p)]
+                ("hprob", c_void_p), ("x2", c_void_p), ("xbn", c_void_p)]
 
 
 class WgradArgs(ctypes.Structure):
@@ -49,7 +49,8 @@ class BwdArgs(ctypes.Structure):
                [("tgt", c_void_p), ("hw", c_void_p), ("hb", c_void_p), ("dS", c_void_p), ("hslab", c_void_p)] + \
                [("pcode", c_void_p), ("dpool", c_void_p), ("ldp", c_int)] + \
                [("x1", c_void_p), ("slab1", c_void_p), ("bslab1", c_void_p), ("x1bytes", ctypes.c_uint)] + \
-               [("z", c_void_p), ("bncoef", c_void_p), ("bnslab", c_void_p), ("hprob", c_void_p), ("x2", c_void_p)]
+               [("z", c_void_p), ("bncoef", c_void_p), ("bnslab", c_void_p), ("hprob", c_void_p), ("x2", c_void_p),
+                                                                                      ("xbn", c_void_p)]
 
 
 class PackDesc(ctypes.Structure):
@@ -117,6 +118,9 @@ USE_FUSED_W1 = CFG.fused_w1
 # the 32-channel level without a concat buffer: dense skip + dense up half, read by the decoder conv's
 # row-streaming forward and fused backward through their dual input (x2)
 USE_DUAL_INPUT = CFG.dual_input
+# DoubleConv with BatchNorm at the 32/64-channel levels: conv2 reads conv1's pre-BN output z and forms
+# relu(bn(z)) in its loader (forward and fused backward) -- no normalise pass, no stored BN output
+USE_BN_ON_LOAD = CFG.bn_on_load
 
 # TIMING ABLATION ONLY (numerically wrong results): the listed kernel families are skipped so a bench
 # run measures what they cost end to end.  Never read from the environment: set_timing_ablation() is
@@ -150,7 +154,8 @@ def igemm(x: torch.Tensor, wpacked: torch.Tensor, y: torch.Tensor, *, Ngemm: int
           mask: Optional[torch.Tensor] = None, mode: int = 0, Cout: int = 0, accumulate: bool = False, cfg: int = 0,
           path: str = "auto", pool: Optional[torch.Tensor] = None, variant: int = 0,
           pcode: Optional[torch.Tensor] = None, y2: Optional[torch.Tensor] = None, split: int = 0, head=None,
-          bn_stats: Optional[list] = None, persistent: bool = True, x2: Optional[torch.Tensor] = None):
+          bn_stats: Optional[list] = None, persistent: bool = True, x2: Optional[torch.Tensor] = None,
+          xbn: Optional[torch.Tensor] = None):
     """Implicit-GEMM conv.  ``out_grid`` = (N, Ho, Wo) pixel grid of GEMM-M.
 
     ``path``: ``auto`` picks, for a conv3x3, the row-streaming kernel (Ngemm, Cs in {32, 64}), then the
@@ -171,7 +176,10 @@ def igemm(x: torch.Tensor, wpacked: torch.Tensor, y: torch.Tensor, *, Ngemm: int
     the backward passes it while side-stream weight gradients hold CUs, which a persistent grid
     sized for the whole chip would otherwise wait for.  ``x2``: dual input -- the conv input is the
     channel concat [x | x2] of two tensors of identical layout (32 channels each, ``Cs`` = 64), read
-    by the row-streaming kernel from both (a decoder conv over [skip | up] without a concat buffer)."""
+    by the row-streaming kernel from both (a decoder conv over [skip | up] without a concat buffer).
+    ``xbn`` (fp32 [2 Cs], :func:`bn_fwd` ``coef_out``): ``x`` is the pre-BatchNorm output z of the layer
+    below and the conv's input is relu(z * xbn[c] + xbn[Cs + c]), formed in the row-streaming loader
+    (BN-statistics epilogue launches only: a conv followed by BN, ``bn_stats`` given)."""
     N, Hs, Ws, Cx, ldx = _nhwc(x, "igemm.x")
     if x2 is not None:
         assert _nhwc(x2, "igemm.x2") == (N, Hs, Ws, Cx, ldx) and Cx == 32 and Cs == 64, "dual input: two [N,H,W,32]"
@@ -215,6 +223,9 @@ def igemm(x: torch.Tensor, wpacked: torch.Tensor, y: torch.Tensor, *, Ngemm: int
     if bn_stats is not None and USE_FUSED_BN and mode == 0 and pool is None and y2 is None and head is None \
             and not accumulate and not relu and path == "auto" and (mask is None or mch == Ngemm):
         bslab = torch.empty(N * -(-Ho // 16) * -(-Wo // 64) * 2 * Ngemm, dtype=torch.float32, device=y.device)
+    if xbn is not None:
+        assert bslab is not None and mask is None and x2 is None and Cs != 8, "BN-on-load: the BN-statistics stream conv"
+        assert xbn.dtype == torch.float32 and xbn.is_contiguous() and xbn.numel() == 2 * Cs
     hprob = None
     if head is not None:
         hw, hb, tgt = head[:3]
@@ -261,10 +272,15 @@ def igemm(x: torch.Tensor, wpacked: torch.Tensor, y: torch.Tensor, *, Ngemm: int
             rows = L.dpa_igemm_stream_blocks(ctypes.byref(a))
             if rows > 0 and rows * 2 * Ngemm <= bslab.numel():
                 a.bnslab = bslab.data_ptr()
-                if L.dpa_igemm_stream(ctypes.byref(a), c_int(0), st) == 0:
+                a.xbn = None if xbn is None else xbn.data_ptr()
+                err = L.dpa_igemm_stream(ctypes.byref(a), c_int(0), st)
+                if err == 0:
                     bn_stats.extend([bslab, rows])
                     return
-                a.bnslab = None
+                if xbn is not None:
+                    _check(err, "igemm_stream(BN-on-load)")
+                a.bnslab = a.xbn = None
+        assert xbn is None, "BN-on-load: only the row-streaming BN-statistics conv forms the input on load"
         # not fusable here: the BN pass computes the statistics (the same epilogue in the row-halo
         # kernel measured 4% slower end to end: its extra registers cost more than the pass it saves),
         # unless the row-block GEMM (below) takes the conv: its epilogue writes one slab row per tile
@@ -572,7 +588,8 @@ def bwd_pool_foldable(ci: int, co: int) -> bool:
 def conv_bwd_fused(g: Optional[torch.Tensor], x: torch.Tensor, wd: torch.Tensor, Kd: int, gw: torch.Tensor,
                    gb: Optional[torch.Tensor], *, mask: bool, dx: Optional[torch.Tensor] = None,
                    dx2: Optional[torch.Tensor] = None, split: int = 0, target_blocks: int = 0, head=None,
-                   pool=None, w1=None, bn=None, bn_stats: bool = False, x2: Optional[torch.Tensor] = None):
+                   pool=None, w1=None, bn=None, bn_stats: bool = False, x2: Optional[torch.Tensor] = None,
+                   xbn: Optional[torch.Tensor] = None):
     """Backward of ``y = conv3x3(x) (+bias)`` in one pass (csrc/bwd_stream.hip): returns
     ``dx = conv3x3^T(g)`` (times ``x > 0`` when ``mask``; with ``dx2``/``split`` the channels
     ``>= split`` go to ``dx2``) and ACCUMULATES the weight gradient into ``gw`` (PyTorch OIHW
@@ -603,7 +620,9 @@ def conv_bwd_fused(g: Optional[torch.Tensor], x: torch.Tensor, wd: torch.Tensor,
     function returns ``(dx, (slab, rows))``.
 
     ``x2``: dual input -- the conv input is [x | x2] (two [N,H,W,32] tensors of identical layout), as
-    :func:`igemm` ``x2``; the kernel's x loader reads both."""
+    :func:`igemm` ``x2``; the kernel's x loader reads both.  ``xbn`` (with ``bn`` and ``bn_stats``):
+    ``x`` is the pre-BatchNorm output z of the layer below and the kernel uses relu(z * xbn[c] +
+    xbn[CI + c]) as the conv input, dx mask and BN-statistics operand (:func:`igemm` ``xbn``)."""
     Nx, Hx, Wx, CI, ldx = _nhwc(x, "bwd.x")
     if x2 is not None:
         assert _nhwc(x2, "bwd.x2") == (Nx, Hx, Wx, CI, ldx) and CI == 32, "dual input: two [N,H,W,32]"
@@ -708,6 +727,9 @@ def conv_bwd_fused(g: Optional[torch.Tensor], x: torch.Tensor, wd: torch.Tensor,
         assert bn is not None and epi == 0, "BN statistics of the layer below: BN mode with the masked dx"
         bnslab = torch.empty(nblk * 2 * CI, dtype=torch.float32, device=x.device)
         a.bnslab = bnslab.data_ptr()
+    if xbn is not None:
+        assert bn_stats and xbn.dtype == torch.float32 and xbn.is_contiguous() and xbn.numel() == 2 * CI
+        a.xbn = xbn.data_ptr()
     _check(L.dpa_bwd_stream(ctypes.byref(a), c_int(CI), c_int(CO), c_int(epi), st), "bwd_stream")
     if hslab is not None:
         _check(L.dpa_head_grad_from_slab(_p(hslab), c_int(nblk), c_int(CO), _p(hslab[nblk * (CO + 1):]), _p(hgw),
@@ -886,17 +908,26 @@ def _fold_slab(slab: torch.Tensor, rows: int, K: int, max_rows: int = 512):
     return out, nout
 
 
-def bn_fwd(z: torch.Tensor, y: torch.Tensor, bn: torch.nn.BatchNorm2d, train: bool, relu: bool = True,
-           stats: Optional[list] = None, pool: Optional[torch.Tensor] = None, pcode: Optional[torch.Tensor] = None):
+def bn_fwd(z: torch.Tensor, y: Optional[torch.Tensor], bn: torch.nn.BatchNorm2d, train: bool, relu: bool = True,
+           stats: Optional[list] = None, pool: Optional[torch.Tensor] = None, pcode: Optional[torch.Tensor] = None,
+           coef_out: Optional[list] = None):
     """y = relu(BatchNorm2d(z)) (NHWC bf16; y may be a concat half).  Training: batch statistics,
     running stats updated (torch momentum semantics); returns ``saved`` = [mean, invstd] (fp32 [2C])
     for :func:`bn_bwd`.  Eval: running statistics, returns None.  ``stats`` = (slab, rows) partial
     sums the producing conv already computed (:func:`igemm` ``bn_stats``): no statistics pass.
     ``pool``/``pcode``: also the 2x2 max-pool of y and its window codes, in the same pass (even H, W;
-    otherwise a separate :func:`maxpool2`)."""
+    otherwise a separate :func:`maxpool2`).  ``y=None`` (with ``coef_out``, an empty list): no
+    normalise pass at all -- the statistics and running stats update as usual and ``coef_out``
+    receives the fp32 [2C] (scale, shift) with which a consumer forms relu(z * scale + shift) on load
+    (:func:`igemm` / :func:`conv_bwd_fused` ``xbn``)."""
     N, H, W, C, ldz = _nhwc(z, "bn.z")
-    Ny, Hy, Wy, Cy, ldy = _nhwc(y, "bn.y")
-    assert (Ny, Hy, Wy, Cy) == (N, H, W, C) and bn.num_features == C and bn.affine
+    if y is None:
+        assert coef_out is not None and pool is None and relu, "coefficients only: the consumer applies BN + ReLU"
+        ldy = 0
+    else:
+        Ny, Hy, Wy, Cy, ldy = _nhwc(y, "bn.y")
+        assert (Ny, Hy, Wy, Cy) == (N, H, W, C)
+    assert bn.num_features == C and bn.affine
     P = N * H * W
     L = _lib.lib()
     rows = L.dpa_bn_slab_rows(c_ll(P), c_int(C))
@@ -926,6 +957,8 @@ def bn_fwd(z: torch.Tensor, y: torch.Tensor, bn: torch.nn.BatchNorm2d, train: bo
         assert (Np, Hp, Wp, Cp) == (N, H // 2, W // 2, C)
         if pcode is not None:
             assert pcode.dtype == torch.uint8 and pcode.is_contiguous() and tuple(pcode.shape) == (N, H // 2, W // 2, C)
+    if coef_out is not None:
+        coef_out.append(coef)
     _check(L.dpa_bn_fwd(_p(z), c_int(ldz), _p(y), c_int(ldy), c_ll(P), c_int(C), _p(gamma), _p(beta),
                         ctypes.c_float(bn.eps), ctypes.c_float(mom), _p(rm), _p(rv), _p(slab) if use_batch else None,
                         _p(coef), _p(saved), c_int(int(use_batch)), c_int(int(relu)), c_int(pre_rows),

@@ -1,0 +1,144 @@
+"""BatchNorm applied on load (DoubleConv conv1 -> BN -> ReLU -> conv2 -> BN of the BN UNet, reference
+model/unet_parts.py:76-95 with batchnorm, modelsummary.txt:153-247): conv1 stops at its pre-BN output
+z, ``bn_fwd(z, None, ...)`` only computes the statistics and (scale, shift), and conv2 forms
+relu(z * scale + shift) in its loader -- the row-streaming forward (csrc/halo.hip, EPI 4) and the
+fused backward's BN mode 2 (csrc/bwd_stream.hip) -- with bn_apply's exact arithmetic.  So every result
+must equal the path that materialises y = relu(bn(z)) bitwise.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from test_hip_kernels import _pack_one
+
+pytestmark = pytest.mark.gpu
+
+
+def _bn(C):
+    bn = torch.nn.BatchNorm2d(C).cuda()
+    with torch.no_grad():
+        bn.weight.copy_(torch.linspace(0.6, 1.4, C))
+        bn.bias.copy_(torch.linspace(-0.3, 0.3, C))
+    return bn
+
+
+@pytest.mark.parametrize("N,H,W,C1,C2", [(2, 9, 128, 32, 32), (1, 7, 512, 32, 64), (2, 6, 256, 64, 64),
+                                         (1, 5, 96, 64, 32)])
+def test_stream_forward_bn_on_load(hip_lib, N, H, W, C1, C2):
+    from distributedpytorch_amd.ops import kernels as K
+    torch.manual_seed(3)
+    z = (torch.randn(N, H, W, C1) * 1.5 + 0.2).to(torch.bfloat16).cuda()
+    w = torch.randn(C2, C1, 3, 3) * 0.05
+    b = torch.randn(C2, device="cuda") * 0.1
+    wp, _, kf = _pack_one(0, w)
+    outs = []
+    for onload in (False, True):
+        bn = _bn(C1)
+        if onload:
+            coef = []
+            K.bn_fwd(z, None, bn, train=True, coef_out=coef)
+            xin, xbn = z, coef[0]
+        else:
+            xin, xbn = torch.empty_like(z), None
+            K.bn_fwd(z, xin, bn, train=True)
+        y = torch.empty(N, H, W, C2, dtype=torch.bfloat16, device="cuda")
+        st = []
+        K.igemm(xin, wp, y, Ngemm=C2, Kpad=kf, KH=3, KW=3, stride=1, pad=1, Cs=C1, out_grid=(N, H, W), bias=b,
+                relu=False, bn_stats=st, xbn=xbn)
+        torch.cuda.synchronize()
+        assert st, "the stream kernel's BN-statistics epilogue did not run"
+        outs.append((y, st[0][:st[1] * 2 * C2].clone(), bn.running_mean.clone(), bn.running_var.clone()))
+    (ya, sa, ma, va), (yb, sb, mb, vb) = outs
+    assert torch.equal(ya, yb) and torch.equal(sa, sb)
+    assert torch.equal(ma, mb) and torch.equal(va, vb)
+    # fp32 anchor: conv of relu(bn(z)) with the batch statistics of z
+    zf = z.float().cpu()
+    mean, var = zf.mean((0, 1, 2)), zf.var((0, 1, 2), unbiased=False)
+    bnc = _bn(C1).cpu()
+    yin = torch.relu((zf - mean) / torch.sqrt(var + bnc.eps) * bnc.weight.detach() + bnc.bias.detach())
+    ref = F.conv2d(yin.permute(0, 3, 1, 2), w.to(torch.bfloat16).float(), b.cpu(), padding=1).permute(0, 2, 3, 1)
+    err = ((yb.float().cpu() - ref).abs().max() / ref.abs().max()).item()
+    assert err < 2e-2
+
+
+@pytest.mark.parametrize("N,H,W,Cin,Cout", [(2, 5, 64, 32, 32), (1, 6, 128, 64, 64), (2, 4, 64, 32, 64),
+                                            (1, 5, 128, 64, 32)])
+def test_fused_backward_bn_on_load(hip_lib, N, H, W, Cin, Cout):
+    """Fused backward BN mode 2 with x = relu(bn(z_below)) formed on load == the same launch on the
+    materialised x: dx, weight / bias gradients, dgamma / dbeta and the layer-below BN partials."""
+    from distributedpytorch_amd.ops import kernels as K
+    torch.manual_seed(11)
+    zb = (torch.randn(N, H, W, Cin) * 1.2 - 0.1).to(torch.bfloat16).cuda()     # pre-BN output of the layer below
+    z = (torch.randn(N, H, W, Cout) * 1.5 + 0.2).to(torch.bfloat16).cuda()
+    w = torch.randn(Cout, Cin, 3, 3) * 0.05
+    packed, ng, kd = _pack_one(1, w)
+    res = []
+    for onload in (False, True):
+        bnb = _bn(Cin)
+        if onload:
+            coef = []
+            K.bn_fwd(zb, None, bnb, train=True, coef_out=coef)
+            x, xbn = zb, coef[0]
+        else:
+            x, xbn = torch.empty_like(zb), None
+            K.bn_fwd(zb, x, bnb, train=True)
+        bn = _bn(Cout)
+        y = torch.empty_like(z)
+        saved = K.bn_fwd(z, y, bn, train=True)
+        torch.manual_seed(12)
+        g = (torch.randn(N, H, W, Cout, device="cuda") * (y > 0)).to(torch.bfloat16)
+        dgam, dbet = torch.zeros(Cout, device="cuda"), torch.zeros(Cout, device="cuda")
+        gw, gb = torch.zeros(Cout * Cin * 9, device="cuda"), torch.zeros(Cout, device="cuda")
+        coef3 = K.bn_bwd_coef(g, z, saved, bn, dgam, dbet)
+        dx, (slab, rows) = K.conv_bwd_fused(g, x, packed, kd, gw, gb, mask=True, bn=(z, coef3), bn_stats=True, xbn=xbn)
+        torch.cuda.synchronize()
+        res.append((dx.float().cpu(), gw.cpu(), gb.cpu(), dgam.cpu(), dbet.cpu(), slab[:rows * 2 * Cin].cpu()))
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("model", ["unet-bn", "unet-bn-bilinear"])
+def test_unet_bn_step_on_load_equals_materialised(hip_lib, monkeypatch, model):
+    """A whole BN-UNet training step with BN-on-load == the step that stores every BN output (loss,
+    every gradient, the running statistics); the on-load path must actually be taken."""
+    from distributedpytorch_amd.compute import loss_from_partials, make_compute
+    from distributedpytorch_amd.data.synthetic import synthetic_batch
+    from distributedpytorch_amd.models.unet import build_model
+    from distributedpytorch_amd.optim import FlatParameterSpace
+    from distributedpytorch_amd.ops import kernels as K
+
+    torch.manual_seed(0)
+    net = build_model(model).cuda()
+    space = FlatParameterSpace(net)
+    comp = make_compute(net, backend="hip", dtype="bf16")
+    img, mask = synthetic_batch(2, 64, 256, 3, seed=5)
+    x, t = img.cuda(), mask.float().unsqueeze(1).cuda()
+    state0 = {k: v.clone() for k, v in net.state_dict().items() if "running" in k or "num_batches" in k}
+    used = []
+    real = K.igemm
+
+    def spy(*a, **kw):
+        used.append(kw.get("xbn") is not None)
+        return real(*a, **kw)
+
+    monkeypatch.setattr(K, "igemm", spy)
+
+    def run():
+        net.load_state_dict(state0, strict=False)
+        space.zero_grad()
+        used.clear()
+        S = comp.forward_partials(x, t)
+        loss = loss_from_partials(S, t.numel())
+        loss.backward()
+        torch.cuda.synchronize()
+        run_stats = {k: v.clone() for k, v in net.state_dict().items() if "running" in k}
+        return loss.item(), space.grad.clone(), run_stats, sum(used)
+
+    l1, g1, r1, n1 = run()
+    monkeypatch.setattr(K, "USE_BN_ON_LOAD", False)
+    l0, g0, r0, n0 = run()
+    assert n1 >= 4 and n0 == 0
+    assert l0 == l1
+    assert torch.allclose(g0, g1, rtol=1e-5, atol=1e-7 * g0.abs().max().item())
+    for k in r0:
+        assert torch.equal(r0[k], r1[k]), k

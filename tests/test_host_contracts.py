@@ -121,6 +121,25 @@ def test_dual_input_only_on_the_stream_kernels(L):
     assert L.dpa_bwd_stream(ctypes.byref(b), 64, 32, 0, None) == INVALID            # a plane is 32 channels
 
 
+def test_bn_on_load_only_in_bn_statistics_launches(L):
+    """IgemmArgs.xbn (BN + ReLU of the input formed on load) exists only in the row-streaming kernel's
+    BN-statistics forward epilogue; every other launch that would ignore it is refused.  BwdArgs.xbn
+    needs the BN mode with the layer-below statistics."""
+    for launch in (lambda a: L.dpa_igemm(ctypes.byref(a), 0, None), lambda a: L.dpa_igemm_halo(ctypes.byref(a), 0, None),
+                   lambda a: L.dpa_igemm_glds(ctypes.byref(a), 0, None), lambda a: L.dpa_igemm_stream(ctypes.byref(a), 0, None)):
+        a = _igemm_args()
+        a.xbn = 0x1000                      # no bnslab: not the BN-statistics epilogue
+        assert launch(a) == INVALID
+    for kw in (dict(mask=0x2000, mask_ch=32, ldm=32), dict(pool=0x2000, ldp=32, relu=1), dict(Cs=8, Kpad=96, ldx=8)):
+        a = _igemm_args(**kw)
+        a.xbn, a.bnslab = 0x1000, 0x3000
+        assert L.dpa_igemm_stream(ctypes.byref(a), 0, None) == INVALID, kw
+    from distributedpytorch_amd.ops import kernels as K
+    b = K.BwdArgs(ldg=32, ldx=32, ldy=32, Kd=288, N=1, H=64, W=64, rh=64, ipb=1)
+    b.xbn = 0x1000
+    assert L.dpa_bwd_stream(ctypes.byref(b), 32, 32, 0, None) == INVALID            # no BN mode
+
+
 def test_stream_block_count_matches_launch_geometry(L):
     # variant 1 (Cs = Ngemm = 32): 128-pixel strips, 32-row segments when there are >= 1024 of them
     a = _igemm_args(N=128, Ho=512, Wo=512, Hs=512, Ws=512)
