@@ -311,7 +311,10 @@ __global__ __launch_bounds__(64 * NW, 2) void bwd_stream_kernel(BwdArgs a) {
       }
     }
   };
-  auto rstore = [&](int slot, RowRegs& R, int ih) {
+  // register transforms of a loaded row (gradient formed on load, BN-on-load of x).  The row loop runs
+  // them right after the dx MFMAs, in the same scheduling region, so their VALU work overlaps the
+  // MFMAs instead of sitting between the epilogue and the ring store
+  auto rxform = [&](RowRegs& R, int ih) {
     if constexpr (POOL) {                       // (dskip, dpool, code) chunk -> gradient chunk
 #pragma unroll
       for (int j = 0; j < LG; ++j) {
@@ -380,9 +383,6 @@ __global__ __launch_bounds__(64 * NW, 2) void bwd_stream_kernel(BwdArgs a) {
         }
       }
     }
-#pragma unroll
-    for (int j = 0; j < LG; ++j)
-      if (gsto[j] >= 0) *reinterpret_cast<u32x4_t*>(Gring + slot * GSLOT + gsto[j]) = R.g[j];
     if constexpr (XBN) {                        // z chunk -> relu(bn(z)) chunk (padding stays zero)
       const bool rok = ih >= 0 && ih < a.H;
       if (xbn && rok) {
@@ -400,6 +400,11 @@ __global__ __launch_bounds__(64 * NW, 2) void bwd_stream_kernel(BwdArgs a) {
         }
       }
     }
+  };
+  auto rstore = [&](int slot, RowRegs& R, int ih) {
+#pragma unroll
+    for (int j = 0; j < LG; ++j)
+      if (gsto[j] >= 0) *reinterpret_cast<u32x4_t*>(Gring + slot * GSLOT + gsto[j]) = R.g[j];
 #pragma unroll
     for (int j = 0; j < LX; ++j)
       if (xsto[j] >= 0) *reinterpret_cast<u32x4_t*>(Xring + slot * XSLOT + xsto[j]) = R.x[j];
@@ -544,6 +549,7 @@ __global__ __launch_bounds__(64 * NW, 2) void bwd_stream_kernel(BwdArgs a) {
 #pragma unroll 1
       for (int j = 0; j < 3; ++j) {           // rows h0-1, h0, h0+1 -> slots 0..2
         rload(h0 - 1 + j, setA);
+        rxform(setA, h0 - 1 + j);
         rstore(j, setA, h0 - 1 + j);
       }
       if (nrows > 1) rload(h0 + 2, setA);      // in flight during row 0
@@ -581,6 +587,7 @@ __global__ __launch_bounds__(64 * NW, 2) void bwd_stream_kernel(BwdArgs a) {
                 acc[ic][ip] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ic], bfr[ip], acc[ic][ip], 0, 0, 0);
           }
       }
+      if (r + 1 < nrows) rxform(cur, h0 + r + 2);     // the row stored below (overlaps the MFMAs)
       // ---------------- dW += g[h]^T x[h+kh-1] (this wave: input-channel tile nt, pixel group pg)
 #pragma unroll
       for (int j = 0; j < KST; ++j) {

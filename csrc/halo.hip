@@ -568,12 +568,15 @@ __global__ __launch_bounds__(256 * WCS) void igemm_stream_kernel(IgemmArgs a) {
       R.v[j] = __builtin_amdgcn_raw_buffer_load_b128(lpl[j] ? x2r : xr, off, 0, 0);
     }
   };
-  auto rstore = [&](int slot, const RowRegs& R) {
+  // BN-on-load transform of a loaded row (registers only).  The row loop runs it right after its
+  // MFMAs, inside the same scheduling region, so the VALU work overlaps the MFMA drain instead of
+  // sitting between the epilogue and the ring store.
+  auto xform = [&](RowRegs& R) {
+    if constexpr (XBN) {
+      if (xbn && R.rok) {
 #pragma unroll
-    for (int j = 0; j < LR; ++j) {
-      u32x4_t v = R.v[j];
-      if constexpr (XBN) {
-        if (xbn && R.rok && lok[j]) {
+        for (int j = 0; j < LR; ++j) {
+          if (!lok[j]) continue;
           // chunk j's first channel: slice ks (plane for a dual input) * 32 + (c & 3) * 8
           const int c = tid + j * NT;
           const int cb = (dual ? (lpl[j] ? 32 : 0) : ((c >> 2) / HR) * 32) + (c & 3) * 8;
@@ -581,12 +584,17 @@ __global__ __launch_bounds__(256 * WCS) void igemm_stream_kernel(IgemmArgs a) {
           for (int k = 0; k < 4; ++k) {
             const float2 sc = *reinterpret_cast<const float2*>(xbc + cb + 2 * k);
             const float2 sh = *reinterpret_cast<const float2*>(xbc + CS + cb + 2 * k);
-            v[k] = pack_bf2(fmaxf(fmaf(lo_bf(v[k]), sc.x, sh.x), 0.f), fmaxf(fmaf(hi_bf(v[k]), sc.y, sh.y), 0.f));
+            R.v[j][k] = pack_bf2(fmaxf(fmaf(lo_bf(R.v[j][k]), sc.x, sh.x), 0.f),
+                                 fmaxf(fmaf(hi_bf(R.v[j][k]), sc.y, sh.y), 0.f));
           }
         }
       }
-      if (lsto[j] >= 0) *reinterpret_cast<u32x4_t*>(Ring + slot * SLOT + lsto[j]) = v;
     }
+  };
+  auto rstore = [&](int slot, const RowRegs& R) {
+#pragma unroll
+    for (int j = 0; j < LR; ++j)
+      if (lsto[j] >= 0) *reinterpret_cast<u32x4_t*>(Ring + slot * SLOT + lsto[j]) = R.v[j];
   };
   // ---- per-lane LDS fragment offsets and epilogue constants
   const int chunk = lane >> 4;
@@ -661,6 +669,7 @@ __global__ __launch_bounds__(256 * WCS) void igemm_stream_kernel(IgemmArgs a) {
 #pragma unroll 1
   for (int j = 0; j < 3; ++j) {
     rload(h0 - 1 + j, setA);
+    xform(setA);
     rstore(j, setA);
   }
   if (nrows > 1) rload(h0 + 2, setA);
@@ -713,6 +722,7 @@ __global__ __launch_bounds__(256 * WCS) void igemm_stream_kernel(IgemmArgs a) {
         }
       }
     }
+    if (r + 1 < nrows) xform(cur);      // BN-on-load of the row stored below (overlaps the MFMA drain)
     // epilogue for output row h0 + r: 32-bit buffer offsets = per-lane constant + uniform row base
 #pragma unroll
     for (int ip = 0; ip < TP; ++ip) {

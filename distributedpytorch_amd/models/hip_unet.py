@@ -216,7 +216,7 @@ class HipBlocks:
         return self.packed[c.off_d:c.off_d + c.Cin * c.Kd]
 
     # ------------------------------------------------------------------ primitive launches
-    def bn_on_load(self, c1: _Conv, c2: _Conv, W: int) -> bool:
+    def bn_on_load(self, c1: _Conv, c2: _Conv, H: int, W: int) -> bool:
         """DoubleConv conv1 -> BN -> ReLU -> conv2 -> BN at the 32/64-channel levels (training): conv1
         stops at its pre-BN output z (statistics from its epilogue, :meth:`conv_bn_z`) and conv2 forms
         relu(bn(z)) in its row-streaming loader, forward and fused backward (``xbn``).  The BN output
@@ -226,7 +226,8 @@ class HipBlocks:
         if c1.bn is None or c2.bn is None or not (c2.Cs == c2.Cin == c1.Cout and c2.Cin in (32, 64)
                                                   and c2.Cout in (32, 64)):
             return False
-        return self.fusable(c2, c1, W)
+        # the row-streaming conv binds one image per block: z's image within the 32-bit buffer range
+        return H * W * c2.Cin * 2 < K._MAX_BYTES and self.fusable(c2, c1, W)
 
     def conv_bn_z(self, c: _Conv, x: torch.Tensor, st: list):
         """Training conv + BatchNorm statistics without the normalise pass: returns (z, coef) with the
@@ -435,7 +436,8 @@ class HipBlocks:
         c1 = self.dec_convs[d - 1 - l][0]
         if not (c1.bn is None and c1.Cs == c1.Cin == 64 and self.enc_convs[l][1].Cout == 32):
             return False
-        return W >= 16 and H * W * 64 < 2 ** 31 - 1024 and self.fusable(c1, None, W)
+        # both kernels bind one image per block: each [H,W,32] image within the 32-bit buffer range
+        return W >= 16 and H * W * 32 * 2 < K._MAX_BYTES and self.fusable(c1, None, W)
 
     def conv_bwd_halves(self, c: _Conv, g: torch.Tensor, cat: torch.Tensor, C: int):
         """Backward of a conv over ``cat = [lo | hi]`` (C channels each) as two fused passes: each
@@ -703,7 +705,7 @@ class _EncFn(torch.autograd.Function):
         N, H, W = x.shape[:3]
         st1, st2 = [], []
         xbn1 = None
-        if B.bn_on_load(c1, c2, W):
+        if B.bn_on_load(c1, c2, H, W):
             a, xbn1 = B.conv_bn_z(c1, x, st1)         # a = conv1's pre-BN output; conv2 applies BN + ReLU
         else:
             a = B.conv_fwd(c1, x, st=st1)
@@ -848,7 +850,7 @@ class _DecFn(torch.autograd.Function):
         B.deconv_fwd(d, x, cat[..., C:] if up is None else up)
         st1, st2 = [], []
         xbn1 = None
-        if up is None and B.bn_on_load(c1, c2, w2):
+        if up is None and B.bn_on_load(c1, c2, h2, w2):
             a, xbn1 = B.conv_bn_z(c1, cat, st1)       # a = conv1's pre-BN output; conv2 applies BN + ReLU
         else:
             a = B.conv_fwd(c1, cat, st=st1, x2=up)

@@ -44,7 +44,10 @@ def main():
         model, (h, w) = t["model"], t["img"]
         cfg = PRESETS[model]
         mbs = sorted(int(k) for k in t["per_mb"])
-        configs = [(2, max(mbs))] if model == "unet" else [(8, max(mbs)), (8, 2 * max(mbs))]
+        # config 4: UNet 512^2 on 2 stages at the bench batch; config 5: UNet-XL 1024^2 on 8 stages at the
+        # single-GPU bench batch (16) and at the larger global batches the HBM allows (more microbatches:
+        # a smaller fill / drain bubble)
+        configs = [(2, max(mbs))] if model == "unet" else [(8, 16), (8, 32), (8, 64)]
         for S, batch in configs:
             kw = dict(link_gbs=a.link_gbs)
             t1 = single_device_ms(t, batch)
