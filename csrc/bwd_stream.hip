@@ -138,6 +138,7 @@ __global__ __launch_bounds__(64 * NW, 2) void bwd_stream_kernel(BwdArgs a) {
   __shared__ __attribute__((aligned(16))) char lds[WBYTES + 4 * GSLOT + 4 * XSLOT + W1BYTES];
   __shared__ __attribute__((aligned(16))) float bnc[BNL ? 3 * CO : 4];   // BN mode: the dz coefficients
   constexpr bool XBN = BNS;                     // x = relu(bn(z)) formed on load (a.xbn)
+  constexpr bool EARLY_XFORM = BNS && CI == 64;   // where the row loop runs the loader transforms (rxform)
   __shared__ __attribute__((aligned(16))) float xbc[XBN ? 2 * CI : 4];
   char* const Wimg = lds;
   char* const Gring = lds + WBYTES;
@@ -587,7 +588,11 @@ __global__ __launch_bounds__(64 * NW, 2) void bwd_stream_kernel(BwdArgs a) {
                 acc[ic][ip] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ic], bfr[ip], acc[ic][ip], 0, 0, 0);
           }
       }
-      if (r + 1 < nrows) rxform(cur, h0 + r + 2);     // the row stored below (overlaps the MFMAs)
+      // BN mode 2 at 64 input channels transforms the row stored below right after the dx MFMAs
+      // (overlapping them: 4.63 -> 3.75 ms per 64 -> 64 call at b256); the 32-channel and pool / head
+      // modes measured faster with the transform next to the ring store (profiles/*_r04_onload*.txt)
+      if constexpr (EARLY_XFORM)
+        if (r + 1 < nrows) rxform(cur, h0 + r + 2);
       // ---------------- dW += g[h]^T x[h+kh-1] (this wave: input-channel tile nt, pixel group pg)
 #pragma unroll
       for (int j = 0; j < KST; ++j) {
@@ -657,7 +662,10 @@ __global__ __launch_bounds__(64 * NW, 2) void bwd_stream_kernel(BwdArgs a) {
             __builtin_amdgcn_raw_buffer_store_b64(packed, yr, orow * yrowb + yoff[ip][ic], 0, 0);
         }
       __builtin_amdgcn_sched_barrier(0);
-      if (r + 1 < nrows) rstore((r + 3) & 3, cur, h0 + r + 2);
+      if (r + 1 < nrows) {
+        if constexpr (!EARLY_XFORM) rxform(cur, h0 + r + 2);
+        rstore((r + 3) & 3, cur, h0 + r + 2);
+      }
       __syncthreads();
     };
 #pragma unroll 1

@@ -1242,279 +1242,17 @@ __global__ __launch_bounds__(512) void igemm_pp2h_kernel(IgemmArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// Row-block GEMM with TWO MFMA phases per K-tile (cfg 16: 256 output channels, cfg 17: 128).
-// Same operands, LDS images, pixel row-block staging and K order as igemm_pp2h_kernel (bitwise-equal
-// output); what changes is the barrier structure.  pp2h splits every K-tile into four quadrant phases
-// (A half x B half): 8 MFMAs per wave between two barriers in the 128-channel form, whose PMC shows
-// 42 % MFMA issue with the rest in barrier skew and waits (profiles/pmc_b128_512_r03_final.txt).
-// Here a phase is one weight half against the wave's WHOLE pixel slice: phase 1 reads A half 0 and
-// all B fragments of the K-tile, phase 2 only A half 1 (B stays in registers) -- 16 MFMAs per phase at
-// 128 channels, 32 at 256, half the barriers per MFMA.  The two wave groups still ping-pong one barrier
-// apart.  Every sync_in first drains this wave's LDS reads (lgkmcnt(0)), so a region read in one phase
-// may be refilled by LDS-DMA in the next: weight half-tiles cycle through two K-tile buffers with
-// A1(s+1) issued in phase 1 of s and A0(s+2) in phase 2 of s.  Waits (per wave, its own DMA stream;
-// h = weight instructions per half-tile, b = pixel instructions per half-block: 3 in wave 0, else 2),
-// each retiring what the NEXT phase reads (cdna_hip_programming.md "Read a staged buffer one phase
-// AFTER the wait"), group g = K-tiles s = 3g .. 3g+2, next group's pixel halves B0 / B1 at t0 / t1:
-//   p1(s): issue A1(s+1) [+ B half], wait A1(s)    -> vmcnt(2h [+ b])
-//   p2(s): issue A0(s+2),            wait A0(s+1)  -> vmcnt(2h [+ b])  (t2: also retires B(g+1))
-// with the issues past the last K-tile dropped in the last group (counts below).
-template <int EP, int BC = 256, bool BNS = false>
-__global__ __launch_bounds__(512) void igemm_rb2_kernel(IgemmArgs a) {
-  static_assert(BC == 256 || BC == 128, "channel tile");
-  constexpr int BP = 256, WC = BC / 2, WP = 64, TC = WC / 16, TP = 4, RBY = 128;
-  constexpr int QA = WC / 2;                   // weight rows per wave and half
-  constexpr int NIC = QA / 16;                 // weight fragments per half
-  constexpr int AI = BC / 128;                 // weight DMA instructions per half-tile per wave
-  constexpr int ASTAGE = BC * RBY;             // weight K-tile image (32 / 16 KB)
-  constexpr int SEG = 34;                      // pixel rows per quadrant segment (32 + kw halo)
-  constexpr int BHALF = 4 * SEG * RBY;         // one pixel half-block (17 KB, 17 DMA instructions)
-  static_assert(2 * BHALF >= 4 * 2 * BC * 4, "BN sums staging fits one pixel group buffer");
-  __shared__ __attribute__((aligned(16))) char lds[2 * ASTAGE + 4 * BHALF];
-  char* const Bimg = lds + 2 * ASTAGE;
-
-  const int M = a.N * a.Ho * a.Wo;
-  const int W = a.Wo, H = a.Ho, HW = H * W;
-  const int nct = a.Ngemm / BC;
-  const int npt = M / BP;
-  const int bid = xcd_remap(blockIdx.x, npt * nct);
-  int pt, ct;
-  glds_tile(bid, npt, nct, pt, ct);
-  const int m0 = pt * BP, c0 = ct * BC;
-  const int img = m0 / HW, p0 = m0 - img * HW;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wc = wid & 1, wp = wid >> 1, grp = wid >> 2;
-  const int lr = lane >> 3;
-  const int lchunk = (lane & 7) ^ lr;
-  // weight half-tile h = rows {w*WC + h*QA + [0, QA)}; instruction i = j*8 + wid covers its rows 8i .. 8i+7
-  unsigned woff[2][AI];
-  int wdst[2][AI];
-#pragma unroll
-  for (int h = 0; h < 2; ++h)
-#pragma unroll
-    for (int j = 0; j < AI; ++j) {
-      const int i8 = 8 * (j * 8 + wid);
-      const int row = (i8 / QA) * WC + h * QA + i8 % QA;
-      wdst[h][j] = row * RBY;
-      woff[h][j] = (unsigned)(((c0 + row + lr) * a.Kpad) * 2 + lchunk * 16);
-    }
-  // pixel block DMA (as pp2h): instruction i of a half-block fills LDS rows 8i .. 8i+7; wave w issues
-  // i = w, 8 + w and wave 0 also i = 16
-  int bbase[2][3];
-  unsigned bvalid[2][3];
-#pragma unroll
-  for (int h = 0; h < 2; ++h)
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      const int i = j < 2 ? j * 8 + wid : 16;
-      const int q = 8 * i + lr;
-      const int sg = q / SEG, loc = q - sg * SEG;
-      const int pq = sg * 64 + h * 32;
-      const int r = (p0 + pq) / W, col = (p0 + pq) % W + loc - 1;
-      const bool cok = col >= 0 && col < W && (j < 2 || wid == 0);
-      unsigned vb = 0;
-#pragma unroll
-      for (int kh = 0; kh < 3; ++kh) {
-        const int ih = r + kh - 1;
-        if (cok && ih >= 0 && ih < H) vb |= 1u << kh;
-      }
-      bvalid[h][j] = vb;
-      bbase[h][j] = (((img * a.Hs + r - 1) * a.Ws + col) * a.ldx) * 2 + lchunk * 16;
-    }
-  const int rowB = W * a.ldx * 2;
-  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, 0, (int)a.xbytes, 0x00020000);
-  const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc((void*)a.w, 0, 0x7fffffff, 0x00020000);
-  const int S = a.Kpad / 64;                   // host: S >= 9 (Cs >= 64)
-  const int G = S / 3;
-
-  struct KC { int tap, ci; };
-  auto knext = [&](KC c) {
-    if (++c.tap == 9) { c.tap = 0; c.ci += 64; }
-    return c;
-  };
-  auto issueA = [&](int h, int buf, KC c) {
-    const unsigned wk = (unsigned)((c.tap * a.Cs + c.ci) * 2);
-    char* base = lds + buf * ASTAGE;
-#pragma unroll
-    for (int j = 0; j < AI; ++j) dma16(wrs, base + wdst[h][j], woff[h][j] + wk);
-  };
-  auto issueB = [&](int h, int gb, int kh, int ci) {
-    char* base = Bimg + (gb * 2 + h) * BHALF;
-    const int add = kh * rowB + ci * 2;
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const bool ok = (bvalid[h][j] >> kh) & 1u;
-      dma16(xr, base + (j * 8 + wid) * 1024, ok ? (unsigned)(bbase[h][j] + add) : 0x80000000u);
-    }
-    if (wid == 0) {
-      const bool ok = (bvalid[h][2] >> kh) & 1u;
-      dma16(xr, base + 16 * 1024, ok ? (unsigned)(bbase[h][2] + add) : 0x80000000u);
-    }
-  };
-  const bool w0 = wid == 0;
-
-  f32x4_t acc[TC][TP];
-#pragma unroll
-  for (int ic = 0; ic < TC; ++ic)
-#pragma unroll
-    for (int ip = 0; ip < TP; ++ip) acc[ic][ip] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-
-  constexpr bool PM = EP == 2 && BC == 128 && !BNS;
-  constexpr bool PB = EP == 1 && BC == 128 && !BNS;
-  float pbias[PB ? TC * 4 : 1];
-  if constexpr (PB) {
-    const int cb = c0 + wc * WC + 4 * (lane >> 4);
-#pragma unroll
-    for (int k = 0; k < TC * 4; ++k) pbias[k] = a.bias ? a.bias[cb + (k >> 2) * 16 + (k & 3)] : 0.f;
-  }
-  u32x2_t pmk[PM ? TP * TC : 1];
-  if constexpr (PM) {
-    const __amdgpu_buffer_rsrc_t mr = __builtin_amdgcn_make_buffer_rsrc((void*)a.mask, 0, 0x7fffffff, 0x00020000);
-    const int cb = c0 + wc * WC + 4 * (lane >> 4);
-#pragma unroll
-    for (int ip = 0; ip < TP; ++ip) {
-      const int m = m0 + wp * WP + ip * 16 + (lane & 15);
-      const unsigned mo = m < M ? (unsigned)m * (unsigned)a.ldm * 2u + (unsigned)cb * 2u : 0x80000000u;
-#pragma unroll
-      for (int ic = 0; ic < TC; ++ic) pmk[ip * TC + ic] = __builtin_amdgcn_raw_buffer_load_b64(mr, mo + ic * 32, 0, 0);
-    }
-  }
-
-  // prologue: A(0) both halves, pixel blocks of group 0, A0(1); wait for all but A0(1)
-  const KC k0{0, 0};
-  KC k1 = knext(k0);                           // K-tile of the next A1 issue (s + 1)
-  KC k2 = knext(k1);                           // K-tile of the next A0 issue (s + 2)
-  issueA(0, 0, k0);
-  issueA(1, 0, k0);
-  issueB(0, 0, 0, 0);
-  issueB(1, 0, 0, 0);
-  issueA(0, 1, k1);
-  wait_vm<AI>();
-  __builtin_amdgcn_sched_barrier(0);
-  __builtin_amdgcn_s_barrier();
-  if (grp) __builtin_amdgcn_s_barrier();       // the second half runs one barrier behind
-  __builtin_amdgcn_sched_barrier(0);
-
-  bf16x8_t af[NIC][2], bfr[TP][2];
-  auto readA = [&](const char* Wt, int h) {
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int ic = 0; ic < NIC; ++ic) {
-        const int row = wc * WC + h * QA + ic * 16 + (lane & 15);
-        const int chunk = kk * 4 + (lane >> 4);
-        af[ic][kk] = *reinterpret_cast<const bf16x8_t*>(Wt + row * RBY + ((chunk ^ (row & 7)) << 4));
-      }
-  };
-  // both pixel halves at kw: quadrant h, fragment ip -> bfr[2h + ip]
-  auto readB = [&](int gb, int kw) {
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const char* P = Bimg + (gb * 2 + h) * BHALF;
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-        for (int ip = 0; ip < 2; ++ip) {
-          const int row = wp * SEG + ip * 16 + (lane & 15) + kw;
-          const int chunk = kk * 4 + (lane >> 4);
-          bfr[h * 2 + ip][kk] = *reinterpret_cast<const bf16x8_t*>(P + row * RBY + ((chunk ^ (row & 7)) << 4));
-        }
-    }
-  };
-  auto mfma_half = [&](int qa) {
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int ic = 0; ic < NIC; ++ic)
-#pragma unroll
-        for (int ip = 0; ip < TP; ++ip)
-          acc[qa * NIC + ic][ip] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ic][kk], bfr[ip][kk], acc[qa * NIC + ic][ip], 0, 0, 0);
-  };
-  auto sync_in = [&]() {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's reads are done: the region may be refilled
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_setprio(1);
-  };
-  auto sync_out = [&]() {
-    __builtin_amdgcn_s_setprio(0);
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_sched_barrier(0);
-  };
-  // waits: "2 * AI" = two weight half-tiles, "+ 3 / + 2" = one pixel half-block (wave 0 / others)
-  auto wait_ab = [&]() { if (w0) wait_vm<2 * AI + 3>(); else wait_vm<2 * AI + 2>(); };
-
-  // one K-tile t of group buffer gb, weights in buffer bA (= (g + t) & 1).  NB: next group's pixel half
-  // issued in phase 1 (-1: none); I1 / I0: A1(s+1) / A0(s+2) exist; W1 / W2: vmcnt kinds of the two waits
-  // (0: 2h + b, 1: 2h, 2: h, 3: 0, -1: no wait)
-  auto ktile = [&](auto NBc, auto I1c, auto I0c, auto W1c, auto W2c, int gb, int bA, int kw, int kh2, int ci2) {
-    constexpr int NB = decltype(NBc)::value, W1 = decltype(W1c)::value, W2 = decltype(W2c)::value;
-    constexpr bool I1 = decltype(I1c)::value, I0 = decltype(I0c)::value;
-    const char* Wt = lds + bA * ASTAGE;
-    // ---- phase 1: A half 0, all of B
-    readB(gb, kw);
-    __builtin_amdgcn_sched_barrier(0);
-    readA(Wt, 0);
-    if constexpr (I1) { issueA(1, bA ^ 1, k1); k1 = knext(k1); }
-    if constexpr (NB >= 0) issueB(NB, gb ^ 1, kh2, ci2);
-    if constexpr (W1 == 0) wait_ab(); else if constexpr (W1 == 1) wait_vm<2 * AI>();
-    else if constexpr (W1 == 2) wait_vm<AI>(); else if constexpr (W1 == 3) wait_vm<0>();
-    sync_in();
-    mfma_half(0);
-    sync_out();
-    // ---- phase 2: A half 1 (B fragments reused)
-    readA(Wt, 1);
-    if constexpr (I0) { issueA(0, bA, k2); k2 = knext(k2); }
-    if constexpr (W2 == 0) wait_ab(); else if constexpr (W2 == 1) wait_vm<2 * AI>();
-    else if constexpr (W2 == 2) wait_vm<AI>(); else if constexpr (W2 == 3) wait_vm<0>();
-    sync_in();
-    mfma_half(1);
-    sync_out();
-  };
-  using F = std::false_type;
-  using T = std::true_type;
-
-  int kh = 0, ci = 0;
-#pragma unroll 1
-  for (int g = 0; g < G - 1; ++g) {
-    int kh2 = kh + 1, ci2 = ci;
-    if (kh2 == 3) { kh2 = 0; ci2 += 64; }
-    const int gb = g & 1, bA = g & 1;
-    ktile(std::integral_constant<int, 0>{}, T{}, T{}, std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{}, gb, bA, 0, kh2, ci2);
-    ktile(std::integral_constant<int, 1>{}, T{}, T{}, std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{}, gb, bA ^ 1, 1, kh2, ci2);
-    ktile(std::integral_constant<int, -1>{}, T{}, T{}, std::integral_constant<int, 1>{}, std::integral_constant<int, 1>{}, gb, bA, 2, kh2, ci2);
-    kh = kh2;
-    ci = ci2;
-  }
-  {
-    const int gb = (G - 1) & 1, bA = (G - 1) & 1;
-    ktile(std::integral_constant<int, -1>{}, T{}, T{}, std::integral_constant<int, 1>{}, std::integral_constant<int, 1>{}, gb, bA, 0, 0, 0);
-    ktile(std::integral_constant<int, -1>{}, T{}, F{}, std::integral_constant<int, 1>{}, std::integral_constant<int, 2>{}, gb, bA ^ 1, 1, 0, 0);
-    ktile(std::integral_constant<int, -1>{}, F{}, F{}, std::integral_constant<int, 3>{}, std::integral_constant<int, -1>{}, gb, bA, 2, 0, 0);
-  }
-  if (!grp) __builtin_amdgcn_s_barrier();      // balance the second half's extra barrier
-
-  if constexpr (BNS)
-    glds_epilogue_bns<TC, TP, WC, WP, EP>(a, acc, M, m0, c0, wc, wp, lane,
-                                          reinterpret_cast<float*>(Bimg + ((((G - 1) & 1) ^ 1) * 2) * BHALF));
-  else if constexpr (PM) glds_epilogue_fast<TC, TP, WC, WP, EP, true>(a, acc, M, m0, c0, wc, wp, lane, pmk);
-  else if constexpr (PB) glds_epilogue_fast<TC, TP, WC, WP, EP, false, true>(a, acc, M, m0, c0, wc, wp, lane, nullptr, pbias);
-  else if constexpr (EP != 0) glds_epilogue_fast<TC, TP, WC, WP, EP>(a, acc, M, m0, c0, wc, wp, lane);
-  else glds_epilogue<TC, TP, WC, WP>(a, acc, M, m0, c0, wc, wp, lane);
-}
-
-// ------------------------------------------------------------------------------------------------
-// Slice-staged implicit GEMM (cfg 18: 128 output channels x 512 pixels, cfg 19: 256 x 256), conv3x3
-// s1 p1 on tiles of R whole image rows (W in {32, 64, 128}; 256-channel form W <= 64).
+// Slice-staged implicit GEMM (cfg 18: 128 output channels x 512 pixels), conv3x3 s1 p1 on tiles of R
+// whole image rows (W in {32, 64, 128}).  The template also has a 256 x 256 form (BC = 256); measured
+// slower than igemm_pp2h_kernel<EP, 256> on every 256-channel layer (profiles/kbench_sl_b256_r04.txt),
+// it is not instantiated.
 //
-// Why: the row-block kernels (pp2h / rb2) stage the pixel operand once per (kernel row, 64-channel
-// slice) and the weights once per K-tile for every 256-pixel tile; at 128 output channels that is
-// 28 KB of LDS-DMA per 4.2 MFLOP K-tile (150 FLOP/B), and measured they run at ~2500 cycles per K-tile
-// whatever the barrier structure (2 vs 4 phases: rb2 == pp2h, profiles/kbench_rb2_b256_r04.txt) -- the
-// DMA traffic per FLOP, not the MFMA schedule, bounds them.  Here a tile's pixel operand is staged ONCE
+// Why: the row-block kernel (pp2h) stages the pixel operand once per (kernel row, 64-channel slice)
+// and the weights once per K-tile for every 256-pixel tile; at 128 output channels that is 28 KB of
+// LDS-DMA per 4.2 MFLOP K-tile (150 FLOP/B), and measured it runs at ~2500 cycles per K-tile whatever
+// the barrier structure (a two-phase variant with half the barriers measured bitwise-equal and
+// exactly as fast, profiles/kbench_rb2_b256_r04.txt; removed) -- the DMA traffic per FLOP, not the
+// MFMA schedule, bounds it.  Here a tile's pixel operand is staged ONCE
 // per 32-channel slice as an (R+2) x (W+2) image with its zero halo and all 9 taps read from it, and the
 // 128-channel tile covers 512 pixels: per 32-deep K-tile 8 KB of weights + 5.5 KB of pixels for
 // 4.2 MFLOP (310 FLOP/B, half the DMA instructions per MFMA of pp2h's 128-channel form).
@@ -1676,11 +1414,11 @@ __global__ __launch_bounds__(512) void igemm_sl_kernel(IgemmArgs a) {
 
 // slice-staged eligible: conv3x3 s1 p1 on one grid, K = 9 Cs unpadded, 32-channel slices, tiles of whole
 // rows of one image: W a power of two in [32, 128] (256-channel form: [32, 64])
-static inline bool sl_ok(const IgemmArgs& a, int BC) {
-  const int W = a.Wo, BP = BC == 128 ? 512 : 256;
+static inline bool sl_ok(const IgemmArgs& a) {
+  const int W = a.Wo;
   return a.mode == 0 && a.KH == 3 && a.KW == 3 && a.stride == 1 && a.pad == 1 && a.Hs == a.Ho && a.Ws == a.Wo &&
-         a.Kpad == 9 * a.Cs && (a.Cs % 32) == 0 && a.Ngemm % BC == 0 && (a.ldx & 7) == 0 &&
-         (W == 32 || W == 64 || (W == 128 && BC == 128)) && ((long)a.Ho * W) % BP == 0;
+         a.Kpad == 9 * a.Cs && (a.Cs % 32) == 0 && a.Ngemm % 128 == 0 && (a.ldx & 7) == 0 &&
+         (W == 32 || W == 64 || W == 128) && ((long)a.Ho * W) % 512 == 0;
 }
 
 // row-block staging eligible: conv3x3 s1 p1, slice-major K (Kpad == 9 Cs, Cs % 64 == 0), tiles = whole rows
@@ -1712,10 +1450,11 @@ static int launch_glds(const IgemmArgs& a, hipStream_t st) {
 //   14: 256 x 256 ping-pong: row-block pixel staging (igemm_pp2h_kernel) on whole-row tiles of 3x3 s1 p1
 //       convs, per-K-tile staging (igemm_pp2_kernel) otherwise
 //   15: 128 x 256 row-block ping-pong (igemm_pp2h_kernel<EP, 128>)
-//   16 / 17 (variant 65536 / 131072): the row-block GEMMs with two MFMA phases per K-tile (igemm_rb2_kernel)
-//   18 / 19 (variant 262144 / 524288): slice-staged 128 x 512 / 256 x 256 (igemm_sl_kernel)
+//   18 (variant 262144): slice-staged 128 x 512 (igemm_sl_kernel) -- the auto choice for 128-output-channel
+//       layers it takes (3-16 % faster than cfg 15 on every 128-channel 512^2-UNet layer,
+//       profiles/kbench_sl_b256_r04.txt), cfg 15 where it does not
 // Flags: +32 no persistent kernel in the auto choice (a side stream owns CUs), +2048 generic epilogue
-// (tests), +8192 cfg 14 without row blocks (tests), +16384 auto prefers the two-phase row-block kernels.
+// (tests), +8192 cfg 14 without row blocks (tests), +1048576 no slice-staged kernel in the auto choice.
 // Requires Cs % 64 == 0 (a K-step never straddles a tap; slice-staged: Cs % 32), Kpad % 64 == 0,
 // Ngemm % BC == 0.
 DPA_API int dpa_igemm_glds(const IgemmArgs* args, int cfg, hipStream_t st) {
@@ -1723,9 +1462,9 @@ DPA_API int dpa_igemm_glds(const IgemmArgs* args, int cfg, hipStream_t st) {
   if (cfg & 32) a.korder |= 2;          // no persistent kernel in the auto choice
   const bool no_fast_ep = cfg & 2048;   // the generic epilogue (tests)
   const bool no_rowblock = cfg & 8192;  // cfg 14 with per-K-tile pixel staging (tests)
-  const bool rb2 = cfg & 16384;         // auto: the two-phase row-block kernels (cfg 16 / 17) in place of 14 / 15
-  cfg = (cfg & 65536) ? 16 : (cfg & 131072) ? 17 : (cfg & 262144) ? 18 : (cfg & 524288) ? 19 : (cfg & 15);
-  const bool sl = cfg == 18 || cfg == 19;
+  const bool no_sl = cfg & 1048576;     // auto: no slice-staged kernel (A/B switch)
+  cfg = (cfg & 262144) ? 18 : (cfg & 15);
+  const bool sl = cfg == 18;
   if ((a.Cs & (sl ? 31 : 63)) || (a.Kpad & 63) || (a.ldx & 7) || (a.ldy & 3) || a.KH * a.KW > 32 || (a.korder & 1) || a.x2 || a.xbn)
     return (int)hipErrorInvalidValue;
   if (a.bnslab) {
@@ -1736,18 +1475,12 @@ DPA_API int dpa_igemm_glds(const IgemmArgs* args, int cfg, hipStream_t st) {
     if (no_fast_ep || no_rowblock || (ep != 1 && ep != 2) || (ep == 1 && a.relu) ||
         (ep == 2 && a.mask_ch != a.Ngemm) || M % 256)
       return (int)hipErrorInvalidValue;
-    if (cfg == 0) cfg = a.Ngemm % 256 == 0 ? (rb2 ? 16 : 14) : (rb2 ? 17 : 15);
-    const bool ok = (cfg == 14 || cfg == 16) ? (pp2h_ok(a) && a.Kpad >= 128) : (cfg == 15 || cfg == 17) ? pp2h128_ok(a) : false;
+    if (cfg == 0) cfg = a.Ngemm % 256 == 0 ? 14 : 15;
+    const bool ok = cfg == 14 ? (pp2h_ok(a) && a.Kpad >= 128) : cfg == 15 ? pp2h128_ok(a) : false;
     if (!ok) return (int)hipErrorInvalidValue;
-    const int BCt = (cfg == 14 || cfg == 16) ? 256 : 128;
+    const int BCt = cfg == 14 ? 256 : 128;
     const int grid = (int)(M / 256) * (a.Ngemm / BCt);
-    if (cfg == 16) {
-      if (ep == 1) hipLaunchKernelGGL((igemm_rb2_kernel<1, 256, true>), dim3(grid), dim3(512), 0, st, a);
-      else hipLaunchKernelGGL((igemm_rb2_kernel<2, 256, true>), dim3(grid), dim3(512), 0, st, a);
-    } else if (cfg == 17) {
-      if (ep == 1) hipLaunchKernelGGL((igemm_rb2_kernel<1, 128, true>), dim3(grid), dim3(512), 0, st, a);
-      else hipLaunchKernelGGL((igemm_rb2_kernel<2, 128, true>), dim3(grid), dim3(512), 0, st, a);
-    } else if (cfg == 14) {
+    if (cfg == 14) {
       if (ep == 1) hipLaunchKernelGGL((igemm_pp2h_kernel<1, 256, true>), dim3(grid), dim3(512), 0, st, a);
       else hipLaunchKernelGGL((igemm_pp2h_kernel<2, 256, true>), dim3(grid), dim3(512), 0, st, a);
     } else {
@@ -1769,12 +1502,16 @@ DPA_API int dpa_igemm_glds(const IgemmArgs* args, int cfg, hipStream_t st) {
     // steady-state kernel, 4-10 % faster than the 2-stage 256 x 256 tile on every deep layer and 1.38 vs
     // 1.18 PF on a plain 8192^3 GEMM (profiles/kbench_glds_pp2_b256_r03.txt)
     if (a.Ngemm % 256 == 0 && grid_of(256, 256) >= 512)
-      cfg = (a.Kpad <= 8 * 64 && !(a.korder & 2)) ? 8 : (rb2 && pp2h_ok(a)) ? 16 : 14;
+      cfg = (a.Kpad <= 8 * 64 && !(a.korder & 2)) ? 8 : 14;
+    // 128-output-channel layers on whole rows of <= 128 pixels: the slice-staged 128 x 512 kernel when
+    // its tiles fill every CU once
+    else if (a.Ngemm % 128 == 0 && !no_sl && !no_rowblock && sl_ok(a) && grid_of(128, 512) >= 256)
+      cfg = 18;
     // small grids (pipeline microbatches, small batches): the 128-channel row-block kernel when its
     // 128 x 256 tiles still fill every CU once -- it replaces the 3-stage 128 x 256 kernel (cfg 2) and,
     // at 256..511 of its tiles, the 128 x 128 one (cfg 4: twice the tiles at lower efficiency)
     else if (a.Ngemm % 128 == 0 && grid_of(128, 256) >= 256 && !no_rowblock && pp2h128_ok(a))
-      cfg = rb2 ? 17 : 15;
+      cfg = 15;
     else if (a.Ngemm % 128 == 0 && grid_of(128, 256) >= 512) cfg = 2;
     else if (a.Ngemm % 256 == 0 && grid_of(256, 128) >= 512) cfg = 1;
     else cfg = 4;
@@ -1810,40 +1547,13 @@ DPA_API int dpa_igemm_glds(const IgemmArgs* args, int cfg, hipStream_t st) {
       else hipLaunchKernelGGL((igemm_pp2h_kernel<0, 128>), dim3(grid), dim3(512), 0, st, a);
       return (int)hipGetLastError();
     }
-    case 16: {
-      if (!pp2h_ok(a) || a.Kpad < 9 * 64) break;
-      const int grid = (M / 256) * (a.Ngemm / 256);
-      if (ep == 1) hipLaunchKernelGGL((igemm_rb2_kernel<1, 256>), dim3(grid), dim3(512), 0, st, a);
-      else if (ep == 2) hipLaunchKernelGGL((igemm_rb2_kernel<2, 256>), dim3(grid), dim3(512), 0, st, a);
-      else if (ep == 3) hipLaunchKernelGGL((igemm_rb2_kernel<3, 256>), dim3(grid), dim3(512), 0, st, a);
-      else hipLaunchKernelGGL((igemm_rb2_kernel<0, 256>), dim3(grid), dim3(512), 0, st, a);
-      return (int)hipGetLastError();
-    }
-    case 17: {
-      if (!pp2h128_ok(a)) break;
-      const int grid = (M / 256) * (a.Ngemm / 128);
-      if (ep == 1) hipLaunchKernelGGL((igemm_rb2_kernel<1, 128>), dim3(grid), dim3(512), 0, st, a);
-      else if (ep == 2) hipLaunchKernelGGL((igemm_rb2_kernel<2, 128>), dim3(grid), dim3(512), 0, st, a);
-      else if (ep == 3) hipLaunchKernelGGL((igemm_rb2_kernel<3, 128>), dim3(grid), dim3(512), 0, st, a);
-      else hipLaunchKernelGGL((igemm_rb2_kernel<0, 128>), dim3(grid), dim3(512), 0, st, a);
-      return (int)hipGetLastError();
-    }
-    case 18:
-    case 19: {
-      const int BCt = cfg == 18 ? 128 : 256;
-      if (!sl_ok(a, BCt)) break;
-      const int grid = (M / (cfg == 18 ? 512 : 256)) * (a.Ngemm / BCt);
-      if (cfg == 18) {
-        if (ep == 1) hipLaunchKernelGGL((igemm_sl_kernel<1, 128>), dim3(grid), dim3(512), 0, st, a);
-        else if (ep == 2) hipLaunchKernelGGL((igemm_sl_kernel<2, 128>), dim3(grid), dim3(512), 0, st, a);
-        else if (ep == 3) hipLaunchKernelGGL((igemm_sl_kernel<3, 128>), dim3(grid), dim3(512), 0, st, a);
-        else hipLaunchKernelGGL((igemm_sl_kernel<0, 128>), dim3(grid), dim3(512), 0, st, a);
-      } else {
-        if (ep == 1) hipLaunchKernelGGL((igemm_sl_kernel<1, 256>), dim3(grid), dim3(512), 0, st, a);
-        else if (ep == 2) hipLaunchKernelGGL((igemm_sl_kernel<2, 256>), dim3(grid), dim3(512), 0, st, a);
-        else if (ep == 3) hipLaunchKernelGGL((igemm_sl_kernel<3, 256>), dim3(grid), dim3(512), 0, st, a);
-        else hipLaunchKernelGGL((igemm_sl_kernel<0, 256>), dim3(grid), dim3(512), 0, st, a);
-      }
+    case 18: {
+      if (!sl_ok(a)) break;
+      const int grid = (M / 512) * (a.Ngemm / 128);
+      if (ep == 1) hipLaunchKernelGGL((igemm_sl_kernel<1, 128>), dim3(grid), dim3(512), 0, st, a);
+      else if (ep == 2) hipLaunchKernelGGL((igemm_sl_kernel<2, 128>), dim3(grid), dim3(512), 0, st, a);
+      else if (ep == 3) hipLaunchKernelGGL((igemm_sl_kernel<3, 128>), dim3(grid), dim3(512), 0, st, a);
+      else hipLaunchKernelGGL((igemm_sl_kernel<0, 128>), dim3(grid), dim3(512), 0, st, a);
       return (int)hipGetLastError();
     }
     default: break;

@@ -41,7 +41,7 @@ KNOBS = (
     Knob("glds", "DPA_NO_GLDS", True, "LDS-DMA implicit GEMMs (csrc/igemm_glds.hip) for the deep layers"),
     Knob("glds128", "DPA_NO_GLDS128", True, "128-output-channel convs on the row-block GEMM instead of the row-halo conv"),
     Knob("glds_bn", "DPA_NO_GLDS_BN", True, "BatchNorm partial sums in the row-block GEMM epilogue"),
-    Knob("glds_rb2", "DPA_GLDS_RB2", False, "row-block GEMMs with two MFMA phases per K-tile (cfg 16/17)"),
+    Knob("glds_sl", "DPA_NO_GLDS_SL", True, "128-output-channel convs on rows <= 128 px: the slice-staged 128 x 512 GEMM (cfg 18)"),
     Knob("wgrad_gemm", "DPA_NO_WGRAD_GEMM", True, "deep weight gradients as a dense LDS-DMA GEMM (csrc/wgrad_gemm.hip)"),
     Knob("side_wgrad", "DPA_NO_SIDE_WGRAD", True, "weight gradients on a side HIP stream, overlapping the dgrad chain"),
     # fusions
@@ -99,7 +99,7 @@ class KernelConfig:
     glds: bool = True
     glds128: bool = True
     glds_bn: bool = True
-    glds_rb2: bool = False
+    glds_sl: bool = True
     wgrad_gemm: bool = True
     side_wgrad: bool = True
     fused_head: bool = True

@@ -91,8 +91,9 @@ CFG = _config.KernelConfig.from_env()
 USE_HALO = CFG.halo                    # row-halo kernels (csrc/halo.hip)
 USE_STREAM = CFG.stream                # row-streaming conv3x3 (weights resident, row ring)
 USE_GLDS = CFG.glds                    # LDS-DMA GEMMs (csrc/igemm_glds.hip)
-# row-block GEMMs with two MFMA phases per K-tile (igemm_rb2_kernel, cfg 16 / 17) instead of pp2h's four
-GLDS_RB2 = CFG.glds_rb2
+# 128-output-channel layers on rows of <= 128 pixels: the slice-staged 128 x 512 GEMM (cfg 18), 3-16 %
+# faster than the 128-channel row-block kernel (profiles/kbench_sl_b256_r04.txt)
+USE_GLDS_SL = CFG.glds_sl
 # 128-channel convs on the row-block ping-pong GEMM (cfg 15) instead of the row-halo conv: 10-15 % faster
 # on every 128-output-channel 3x3 conv / dgrad of the 512^2 UNet (profiles/kbench_glds_rowblock128_b256_r03.txt)
 USE_GLDS128 = CFG.glds128
@@ -328,14 +329,16 @@ def igemm(x: torch.Tensor, wpacked: torch.Tensor, y: torch.Tensor, *, Ngemm: int
         a = args(n0, n1, False)
         if gslab is not None:
             a.bnslab = gslab[n0 * Ho * Wo // 256 * 2 * Ngemm:].data_ptr()
-            if L.dpa_igemm_glds(ctypes.byref(a), c_int(16384 * GLDS_RB2 if variant == 0 else variant), st) == 0:
+            if L.dpa_igemm_glds(ctypes.byref(a), c_int(variant), st) == 0:
                 continue
             assert n0 == 0, "row-block BN statistics refused after the first chunk"
             a.bnslab, gslab = None, None
         if path == "glds" or (path == "auto" and glds_ok):
             no_pers = not persistent
-            auto_cfg = ((131072 if GLDS_RB2 else 15) if rb128 else
-                        32 * no_pers + 16384 * GLDS_RB2)
+            # 128 output channels: the slice-staged 128 x 512 kernel (cfg 18) on rows of <= 128 pixels,
+            # the 128-channel row-block kernel (15) otherwise; else the library's auto choice
+            sl = USE_GLDS_SL and Wo in (32, 64, 128) and (Ho * Wo) % 512 == 0 and Cs % 32 == 0
+            auto_cfg = (262144 if sl else 15) if rb128 else 32 * no_pers + (0 if USE_GLDS_SL else 1048576)
             err = L.dpa_igemm_glds(ctypes.byref(a), c_int(variant if path == "glds" else auto_cfg), st)
             if err == 0:
                 continue

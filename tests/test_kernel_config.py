@@ -29,13 +29,13 @@ def test_unknown_variables_do_not_change_dispatch():
     retired A/B knobs) builds the default kernel config and no timing ablation."""
     code = ("import json; from distributedpytorch_amd.ops import kernels as K; "
             "print(json.dumps({'nd': K.CFG.non_default(), 'ablate': sorted(K._ABLATE), "
-            "'rb2': K.GLDS_RB2, 'halo': K.USE_HALO}))")
+            "'sl': K.USE_GLDS_SL, 'halo': K.USE_HALO}))")
     env = dict(os.environ, DPA_ABLATE="glds,halo,bwd", DPA_WGRAD_ROWS="1", DPA_FUSED_DCONV1="1",
-               DPA_GLDS_TAP_MAJOR="1", DPA_GLDS_NO_PP="1", DPA_SOMETHING_NEW="1")
+               DPA_GLDS_TAP_MAJOR="1", DPA_GLDS_NO_PP="1", DPA_GLDS_RB2="1", DPA_SOMETHING_NEW="1")
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env, cwd=ROOT, timeout=120)
     assert r.returncode == 0, r.stderr[-2000:]
     out = json.loads(r.stdout.strip().splitlines()[-1])
-    assert out == {"nd": {}, "ablate": [], "rb2": False, "halo": True}
+    assert out == {"nd": {}, "ablate": [], "sl": True, "halo": True}
 
 
 def test_documented_switches_parse():

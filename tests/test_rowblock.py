@@ -1,14 +1,14 @@
-"""The row-block LDS-DMA GEMMs that carry the deep and 128-channel UNet levels (csrc/igemm_glds.hip):
-``igemm_pp2h_kernel`` (cfg 14 / 15: four quadrant phases per K-tile) and ``igemm_rb2_kernel``
-(cfg 16 / 17: two phases per K-tile), anchored DIRECTLY to a plain PyTorch fp32 convolution at real
-512^2-UNet layer shapes (64^2 / 32^2 / 128^2 grids, 256-pixel parts of 512- and 768-wide rows) for every
-specialised epilogue the model uses: forward bias + ReLU, dgrad with the ReLU-backward mask, the split
-dgrad of a concat input, and the BatchNorm partial sums of the forward and backward epilogues.
+"""The LDS-DMA GEMMs that carry the deep and 128-channel UNet levels (csrc/igemm_glds.hip):
+``igemm_pp2h_kernel`` (cfg 14 / 15: row-block staging, four quadrant phases per K-tile) and
+``igemm_sl_kernel`` (cfg 18: slice-staged 128 x 512 tiles, the default for 128-output-channel layers on
+rows of <= 128 pixels), anchored DIRECTLY to a plain PyTorch fp32 convolution at real 512^2-UNet layer
+shapes (64^2 / 32^2 / 128^2 grids, 256-pixel parts of 512- and 768-wide rows) for every specialised
+epilogue the model uses: forward bias + ReLU, dgrad with the ReLU-backward mask, the split dgrad of a
+concat input, and the BatchNorm partial sums of the forward and backward epilogues.
 
 Inputs are bf16-rounded (the kernels' storage type); the fp32 reference sees the same values, so what
 remains is the fp32 accumulation order and the bf16 rounding of the output (< 1e-2 of the output's
-max magnitude).  The two kernel families accumulate K in the same order, so they must also agree
-bitwise with each other.
+max magnitude).  The generic (pointer-math) epilogue must equal the specialised ones bitwise.
 """
 import pytest
 import torch
@@ -16,14 +16,12 @@ import torch.nn.functional as F
 
 pytestmark = pytest.mark.gpu
 
-RB2 = {256: 65536, 128: 131072}     # variant codes of the two-phase kernels (dpa_igemm_glds)
 PP2H = {256: 14, 128: 15}
-SL = {128: 262144, 256: 524288}     # slice-staged kernels (cfg 18: 128 x 512 tiles, cfg 19: 256 x 256)
+SL = 262144                          # slice-staged kernel variant code (cfg 18: 128 x 512 tiles)
 
 
-def _sl_ok(H, W, Ng, bc):
-    bp = 512 if bc == 128 else 256
-    return W in ((32, 64, 128) if bc == 128 else (32, 64)) and (H * W) % bp == 0 and Ng % bc == 0
+def _sl_ok(H, W, Ng):
+    return W in (32, 64, 128) and (H * W) % 512 == 0 and Ng % 128 == 0
 
 
 def _rel(a, b):
@@ -101,35 +99,30 @@ def test_rowblock_fp32_anchor(hip_lib, shape, kind):
     extra = _extra(kind, N, H, W, Ng, seed=Cs)
     exp = _expected(kind, ref, extra)
     bc = 256 if Ng % 256 == 0 else 128
-    outs = []
-    for v in (PP2H[bc], RB2[bc]):
-        y, y2, stats = _run(kind, x, w, N, H, W, Cs, Ng, v, extra)
+    v = PP2H[bc]
+    y, y2, stats = _run(kind, x, w, N, H, W, Cs, Ng, v, extra)
+    got = torch.cat([y, y2], dim=3) if kind == "split" else y
+    assert _rel(got.float().cpu(), exp) < 1e-2, (v, kind)
+    if kind.startswith("bn"):
+        assert stats, "the row-block epilogue did not take the BatchNorm sums"
+        slab, rows = stats
+        sums = slab.view(rows, 2, Ng).double().sum(0).cpu()
+        yd = y.double().cpu().reshape(-1, Ng)
+        s2 = (yd * yd) if kind == "bn_fwd" else (yd * extra["mask"].double().cpu().reshape(-1, Ng))
+        assert _rel(sums[0], yd.sum(0)) < 1e-4 and _rel(sums[1], s2.sum(0)) < 1e-4, (v, kind)
+    elif _sl_ok(H, W, Ng):            # slice-staged kernel: 32-channel K order, fp32 anchor
+        y, y2, _ = _run(kind, x, w, N, H, W, Cs, Ng, SL, extra)
         got = torch.cat([y, y2], dim=3) if kind == "split" else y
-        assert _rel(got.float().cpu(), exp) < 1e-2, (v, kind)
-        if kind.startswith("bn"):
-            assert stats, "the row-block epilogue did not take the BatchNorm sums"
-            slab, rows = stats
-            sums = slab.view(rows, 2, Ng).double().sum(0).cpu()
-            yd = y.double().cpu().reshape(-1, Ng)
-            s2 = (yd * yd) if kind == "bn_fwd" else (yd * extra["mask"].double().cpu().reshape(-1, Ng))
-            assert _rel(sums[0], yd.sum(0)) < 1e-4 and _rel(sums[1], s2.sum(0)) < 1e-4, (v, kind)
-        outs.append(got)
-    assert torch.equal(outs[0], outs[1]), "two-phase kernel != four-phase kernel (same K order)"
-    if not kind.startswith("bn"):
-        for bcs in (128, 256):       # slice-staged kernels: 32-channel K order, fp32 anchor only
-            if _sl_ok(H, W, Ng, bcs):
-                y, y2, _ = _run(kind, x, w, N, H, W, Cs, Ng, SL[bcs], extra)
-                got = torch.cat([y, y2], dim=3) if kind == "split" else y
-                assert _rel(got.float().cpu(), exp) < 1e-2, ("sl", bcs, kind)
+        assert _rel(got.float().cpu(), exp) < 1e-2, ("sl", kind)
 
 
 @pytest.mark.parametrize("N,H,W,Cs,Ng,kind", [(3, 30, 128, 64, 256, "dgrad"), (2, 70, 256, 64, 256, "fwd"),
                                                (16, 32, 32, 128, 256, "fwd"), (2, 9, 512, 64, 256, "dgrad"),
                                                (4, 128, 128, 128, 128, "fwd"), (3, 30, 256, 64, 128, "dgrad"),
                                                (2, 64, 64, 256, 384, "fwd"), (8, 32, 32, 64, 128, "dgrad")])
-def test_rb2_generic_epilogue_bitwise(hip_lib, N, H, W, Cs, Ng, kind):
-    """Partial last row groups, 8 / 2 / 1 rows per tile and the generic epilogue (variant + 2048): the
-    two-phase kernel == the four-phase kernel bitwise."""
+def test_rowblock_generic_epilogue_bitwise(hip_lib, N, H, W, Cs, Ng, kind):
+    """Partial last row groups, 8 / 2 / 1 rows per tile: the specialised epilogue == the generic
+    (pointer-math) epilogue (variant + 2048) bitwise, for the row-block and the slice-staged kernels."""
     from distributedpytorch_amd.ops import kernels as K
     torch.manual_seed(37)
     x = torch.randn(N, H, W, Cs, device="cuda").to(torch.bfloat16)
@@ -137,11 +130,13 @@ def test_rb2_generic_epilogue_bitwise(hip_lib, N, H, W, Cs, Ng, kind):
     extra = (dict(bias=torch.randn(Ng, device="cuda") * 0.1, relu=True) if kind == "fwd" else
              dict(mask=torch.randn(N, H, W, Ng, device="cuda").to(torch.bfloat16)))
     bc = 256 if Ng % 256 == 0 else 128
-    outs = []
-    for v in (PP2H[bc], RB2[bc], RB2[bc] + 2048):
-        y = torch.empty(N, H, W, Ng, device="cuda", dtype=torch.bfloat16)
-        K.igemm(x, w, y, Ngemm=Ng, Kpad=9 * Cs, KH=3, KW=3, stride=1, pad=1, Cs=Cs, out_grid=(N, H, W), path="glds",
-                variant=v, **extra)
-        outs.append(y)
-    torch.cuda.synchronize()
-    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[1], outs[2])
+    variants = [PP2H[bc]] + ([SL] if _sl_ok(H, W, Ng) else [])
+    for v in variants:
+        outs = []
+        for vv in (v, v + 2048):
+            y = torch.empty(N, H, W, Ng, device="cuda", dtype=torch.bfloat16)
+            K.igemm(x, w, y, Ngemm=Ng, Kpad=9 * Cs, KH=3, KW=3, stride=1, pad=1, Cs=Cs, out_grid=(N, H, W),
+                    path="glds", variant=vv, **extra)
+            outs.append(y)
+        torch.cuda.synchronize()
+        assert torch.equal(outs[0], outs[1]), v

@@ -2,6 +2,8 @@
 # Round-4 iteration: tests of the changed kernels, slice-staged GEMM timing, bench, per-block time tables.
 set -o pipefail
 cd "$(dirname "$0")/.." && export TMPDIR=/tmp && mkdir -p gpurun_out/sl gpurun_out/pipe
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_bn_on_load.py tests/test_bwd_fused.py > gpurun_out/sl/pytest.log 2>&1
+rc=$?; tail -2 gpurun_out/sl/pytest.log; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 300 python bench.py > gpurun_out/sl/bench.log 2>&1 || { echo bench failed; tail -3 gpurun_out/sl/bench.log; exit 1; }
 tail -1 gpurun_out/sl/bench.log | cut -c1-200
 timeout -k 10 300 python tools/kbench.py --batch 256 --paths "" --no-wgrad --gvar 14 15 262144 524288 --reps 7 --only "L2,L3,mid" > gpurun_out/sl/kbench.log 2>&1 || { echo kbench failed; tail gpurun_out/sl/kbench.log; exit 1; }
