@@ -50,6 +50,8 @@ def parse():
     ap.add_argument("--img", type=_hw, default=(512, 512),
                     help="image size: S (square) or HxW, e.g. 640x960 (the reference's default, utils/train_utils.py:26)")
     ap.add_argument("--backend", choices=["hip", "torch", "auto"], default="auto")
+    ap.add_argument("--dtype", choices=["bf16", "fp32"], default="bf16",
+                    help="compute / storage precision (fp32: the reference's precision, on the fp32 HIP engine)")
     ap.add_argument("--model", default="unet")
     ap.add_argument("--bucket-mb", type=float, default=8.0)
     ap.add_argument("--grad-comm-dtype", choices=["fp32", "bf16"], default="fp32",
@@ -137,7 +139,7 @@ def main():
         print(f"[bench] TIMING ABLATION {ablate}: results are numerically wrong", file=sys.stderr, flush=True)
     mp = a.parallelism == "mp"
     method = "MP" if mp else ("DDP" if world > 1 else "singleGPU")
-    cfg = TrainConfig(train_method=method, batch_size=a.batch, img_size=a.img, dtype="bf16",
+    cfg = TrainConfig(train_method=method, batch_size=a.batch, img_size=a.img, dtype=a.dtype,
                       backend=a.backend, model=a.model, bucket_mb=a.bucket_mb, lr=1e-4,
                       grad_comm_dtype=a.grad_comm_dtype, comm_overlap=a.comm_overlap,
                       microbatches=a.microbatches, stages=a.stages, mp_cut=a.mp_cut)
@@ -159,7 +161,7 @@ def main():
         strat = PipelineLocalStrategy(cfg, model.to(device), [device] * a.stages)
     else:
         strat = DDPStrategy(cfg, model, device) if world > 1 else SingleDevice(cfg, model, device)
-    backend = resolve_backend(a.backend, device)
+    backend = resolve_backend(a.backend, device, a.dtype, model)
 
     pool = []
     for i in range(a.pool):
@@ -234,7 +236,7 @@ def main():
     # cross-batch quotient of this run over stock-at-32 moves to vs_baseline_basis.
     vs = cross = None
     per_gpu_batch = a.batch if not mp else a.batch // max(1, world)
-    if STOCK_BASELINE_PER_GPU and not a.infer:
+    if STOCK_BASELINE_PER_GPU and not a.infer and a.dtype == "bf16":
         cross = round(value / (STOCK_BASELINE_PER_GPU * world), 4)
         vs = cross if (per_gpu_batch == STOCK_BASELINE_BATCH and not mp) else EQUAL_BATCH_RATIO_B32
     if mp:
@@ -253,7 +255,7 @@ def main():
                               "this_per_gpu_batch": per_gpu_batch,
                               "equal_batch_ratio_b32": EQUAL_BATCH_RATIO_B32,
                               "cross_batch_ratio": cross},
-        "dtype": "bf16",
+        "dtype": a.dtype,
         "data": "synthetic (GPU-generated images + ellipse masks), random-init weights",
         "config": {"model": f"{a.model} (reference 4-level UNet, base 32, {nparams} params)" if a.model == "unet"
                    else a.model, "global_batch": a.batch * (1 if mp else world),

@@ -1,0 +1,565 @@
+// fp32 training path (the reference's precision, utils/train_utils.py:60-61): fp32 storage, fp32 MFMA
+// (v_mfma_f32_16x16x4_f32, IEEE fp32 products, fp32 accumulation) for every conv-shaped product of the
+// UNet step, plus the fp32 elementwise ops around them.  The bf16 engine's kernels (halo.hip,
+// igemm_glds.hip, bwd_stream.hip ...) are bf16-specialised; this is a separate, deliberately simple
+// family -- correctness and precision first, the bf16 path is the fast one.
+//
+//   igemm_f32_kernel : implicit GEMM, NHWC fp32 (reference
+//                      model/unet_parts.py:10-12,51-54):
+//       conv3x3 forward  y[p][co] = relu?(b + sum_{tap,ci} x[p + off(tap)][ci] W[co][tap][ci])
+//       conv3x3 dgrad    dx[p][ci] = sum_{tap,co} g[p + off(tap)][co] Wflip[ci][tap][co]
+//       transposed conv forward (mode 1: 2x2/s2 scatter of n = (2i+j) Cout + co)
+//       transposed conv dgrad (KH = KW = 2, stride 2 gather)
+//     GEMM M = output pixels, N = output channels, K = taps x source channels (16-deep K-steps of
+//     float4 chunks that never straddle a tap: Cs % 4 == 0).  Register-staged, double-buffered LDS.
+//   wgrad_f32_kernel : dW[m][tap][n] = sum_p A[p][m] B[p*s + d(tap) - pad][n] (K3), split over pixel
+//                      ranges into fp32 slab rows [split][tap][M][Nc] that dpa_wgrad_reduce sums in a
+//                      fixed order; the bias gradient sum_p A[p][m] rides along (A = the output gradient).
+//   elementwise       : ReLU backward, 2x2 max-pool with window codes and its backward, the segmentation
+//                       head (1x1 conv + sigmoid + BCE/Dice partial sums) and its backward, NCHW -> NHWC4.
+//
+// MFMA operand order: the 16x16x4 f32 MFMA takes one K value per lane (lane group q = lane >> 4 holds
+// k = q).  Each lane reads a float4 of 4 consecutive K values of its row from LDS and issues 4 MFMAs
+// with elements 0..3: K is summed in the permuted order (4q + e) -- the same for both operands, so the
+// product is the same sum in another order (fp32 rounding differs from a sequential sum by ~1 ulp).
+#include "common.h"
+
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+
+struct F32ConvArgs {
+  const float* x;       // source [N][Hs][Ws][ldx]
+  const float* w;       // packed weights [Ngemm][Kpad] fp32, k = tap * Cs + ci (zero beyond KH*KW*Cs)
+  const float* bias;    // [Cout] or null
+  float* y;             // output (mode 0: [N][Ho][Wo][ldy]; mode 1: [N][2Ho][2Wo][ldy])
+  const float* mask;    // optional ReLU-backward mask on the output grid (y = 0 where mask <= 0)
+  int ldx, ldy, ldm, mask_ch;
+  int N, Ho, Wo, Hs, Ws, Cs;
+  int KH, KW, stride, pad;
+  int Ngemm, Kpad, mode, relu, accumulate, Cout;
+};
+
+struct F32WgradArgs {
+  const float* A;       // [N][Hg][Wg][lda]: M channels (the output gradient for a conv)
+  const float* B;       // [N][HB][WB][ldb]: Nc channels, read at (h*s + kh - pad, w*s + kw - pad)
+  float* slab;          // [splits][T][M][Nc]
+  float* bslab;         // [splits][M] (sum of A over the split's pixels) or null
+  int lda, ldb, N, Hg, Wg, HB, WB, M, Nc, s, pad, KH, KW;
+  long pix_per_split;   // pixels per split (multiple of 16)
+  int splits;
+};
+
+namespace {
+
+constexpr int F_BK = 16;             // K-step: 16 floats = 4 float4 chunks per LDS row (64 B)
+
+// conflict-free ds_read_b128 of 16 consecutive rows at one chunk: rows r and r + 4 land 4 dwords apart
+__device__ __forceinline__ int fswz(int row, int chunk) { return chunk ^ ((row >> 2) & 3); }
+
+__device__ __forceinline__ f32x4_t mfma4(const f32x4v& a, const f32x4v& b, f32x4_t c) {
+  c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0], b[0], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[1], b[1], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[2], b[2], c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[3], b[3], c, 0, 0, 0);
+  return c;
+}
+
+}  // namespace
+
+// BP pixels x BC channels per block, 4 waves (NWP along the pixels x NWC along the channels)
+template <int BP, int BC, int NWP>
+__global__ __launch_bounds__(256) void igemm_f32_kernel(F32ConvArgs a) {
+  constexpr int NWC = 4 / NWP, WP = BP / NWP, WC = BC / NWC, TP = WP / 16, TC = WC / 16;
+  static_assert(NWP * NWC == 4 && TP >= 1 && TC >= 1, "tile");
+  constexpr int RB = F_BK * 4;                       // LDS row bytes
+  constexpr int LP = BP * 4 / 256, LW = (BC * 4 + 255) / 256;
+  __shared__ __attribute__((aligned(16))) char lds[2][(BP + BC) * RB];
+
+  const int M = a.N * a.Ho * a.Wo;
+  const int nct = a.Ngemm / BC, npt = (M + BP - 1) / BP;
+  const int bid = xcd_remap(blockIdx.x, npt * nct);
+  const int pt = bid / nct, ct = bid - pt * nct;
+  const int m0 = pt * BP, c0 = ct * BC;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wp = wid / NWC, wc = wid - wp * NWC;
+  const int lchunk = tid & 3, lrow = tid >> 2;     // 64 rows x 4 chunks per pass
+  const int taps = a.KH * a.KW;
+
+  // per pixel row: (n, h0, w0) of tap (0, 0) and the in-image taps
+  int pn[LP], ph0[LP], pw0[LP];
+  unsigned tmask[LP];
+#pragma unroll
+  for (int i = 0; i < LP; ++i) {
+    const int m = m0 + lrow + i * 64;
+    const bool ok = m < M;
+    const int mm = ok ? m : 0;
+    const int hw = a.Ho * a.Wo;
+    pn[i] = mm / hw;
+    const int rem = mm - pn[i] * hw;
+    const int oh = rem / a.Wo, ow = rem - oh * a.Wo;
+    ph0[i] = oh * a.stride - a.pad;
+    pw0[i] = ow * a.stride - a.pad;
+    unsigned msk = 0;
+    for (int t = 0; t < taps; ++t) {
+      const int kh = t / a.KW, kw = t - kh * a.KW;
+      const int ih = ph0[i] + kh, iw = pw0[i] + kw;
+      if (ok && ih >= 0 && ih < a.Hs && iw >= 0 && iw < a.Ws) msk |= 1u << t;
+    }
+    tmask[i] = msk;
+  }
+  const int S = a.Kpad / F_BK;
+  f32x4v pr[LP], wr[LW];
+  auto gload = [&](int s) {
+    const int k0 = s * F_BK + lchunk * 4;
+    const int tap = k0 / a.Cs, ci = k0 - tap * a.Cs;
+    const int kh = tap / a.KW, kw = tap - kh * a.KW;
+#pragma unroll
+    for (int i = 0; i < LP; ++i) {
+      if (tap < taps && ((tmask[i] >> tap) & 1u)) {
+        const long off = ((long)(pn[i] * a.Hs + ph0[i] + kh) * a.Ws + pw0[i] + kw) * a.ldx + ci;
+        pr[i] = *reinterpret_cast<const f32x4v*>(a.x + off);
+      } else {
+        pr[i] = f32x4v{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < LW; ++i) {
+      const int r = lrow + i * 64;
+      if (r < BC) wr[i] = *reinterpret_cast<const f32x4v*>(a.w + (long)(c0 + r) * a.Kpad + s * F_BK + lchunk * 4);
+    }
+  };
+  auto lstore = [&](int buf) {
+    char* P = lds[buf];
+    char* Wt = lds[buf] + BP * RB;
+#pragma unroll
+    for (int i = 0; i < LP; ++i) {
+      const int r = lrow + i * 64;
+      *reinterpret_cast<f32x4v*>(P + r * RB + fswz(r, lchunk) * 16) = pr[i];
+    }
+#pragma unroll
+    for (int i = 0; i < LW; ++i) {
+      const int r = lrow + i * 64;
+      if (r < BC) *reinterpret_cast<f32x4v*>(Wt + r * RB + fswz(r, lchunk) * 16) = wr[i];
+    }
+  };
+
+  f32x4_t acc[TC][TP];
+#pragma unroll
+  for (int ic = 0; ic < TC; ++ic)
+#pragma unroll
+    for (int ip = 0; ip < TP; ++ip) acc[ic][ip] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  gload(0);
+  lstore(0);
+  __syncthreads();
+  const int q = lane >> 4;
+  for (int s = 0; s < S; ++s) {
+    const int buf = s & 1;
+    if (s + 1 < S) gload(s + 1);
+    const char* P = lds[buf];
+    const char* Wt = lds[buf] + BP * RB;
+    f32x4v af[TC], bfr[TP];
+#pragma unroll
+    for (int ic = 0; ic < TC; ++ic) {
+      const int row = wc * WC + ic * 16 + (lane & 15);
+      af[ic] = *reinterpret_cast<const f32x4v*>(Wt + row * RB + fswz(row, q) * 16);
+    }
+#pragma unroll
+    for (int ip = 0; ip < TP; ++ip) {
+      const int row = wp * WP + ip * 16 + (lane & 15);
+      bfr[ip] = *reinterpret_cast<const f32x4v*>(P + row * RB + fswz(row, q) * 16);
+    }
+#pragma unroll
+    for (int ic = 0; ic < TC; ++ic)
+#pragma unroll
+      for (int ip = 0; ip < TP; ++ip) acc[ic][ip] = mfma4(af[ic], bfr[ip], acc[ic][ip]);
+    if (s + 1 < S) lstore(buf ^ 1);
+    __syncthreads();
+  }
+
+  // epilogue: lane holds 4 consecutive GEMM columns (4 q + r) of pixel (lane & 15)
+#pragma unroll
+  for (int ip = 0; ip < TP; ++ip) {
+    const int m = m0 + wp * WP + ip * 16 + (lane & 15);
+    if (m >= M) continue;
+    long ybase;
+    if (a.mode == 0) {
+      ybase = (long)m * a.ldy;
+    } else {
+      const int hw = a.Ho * a.Wo;
+      const int n = m / hw, rem = m - n * hw, h = rem / a.Wo, w = rem - (rem / a.Wo) * a.Wo;
+      ybase = ((long)(n * 2 * a.Ho + 2 * h) * (2 * a.Wo) + 2 * w) * a.ldy;
+    }
+#pragma unroll
+    for (int ic = 0; ic < TC; ++ic) {
+      const int nidx = c0 + wc * WC + ic * 16 + 4 * q;
+      int co = nidx;
+      long off = ybase + nidx;
+      if (a.mode == 1) {
+        const int ij = nidx / a.Cout;
+        co = nidx - ij * a.Cout;
+        off = ybase + (long)((ij >> 1) * (2 * a.Wo) + (ij & 1)) * a.ldy + co;
+      }
+      f32x4v v = f32x4v{acc[ic][ip][0], acc[ic][ip][1], acc[ic][ip][2], acc[ic][ip][3]};
+      if (a.bias) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] += a.bias[co + r];
+      }
+      if (a.relu) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+      }
+      if (a.mask && co < a.mask_ch) {
+        const f32x4v mk = *reinterpret_cast<const f32x4v*>(a.mask + (long)m * a.ldm + co);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = mk[r] > 0.f ? v[r] : 0.f;
+      }
+      if (a.accumulate) v += *reinterpret_cast<const f32x4v*>(a.y + off);
+      *reinterpret_cast<f32x4v*>(a.y + off) = v;
+    }
+  }
+}
+
+// Weight gradient: 64 (A channels m) x 64 (columns tap * Nc + n) tile, K = 16 pixels per step; the
+// operands are K-strided in NHWC, so the loader transposes them into [row][16 px] LDS images.
+__global__ __launch_bounds__(256) void wgrad_f32_kernel(F32WgradArgs a) {
+  constexpr int RB = F_BK * 4;
+  __shared__ __attribute__((aligned(16))) float As[64 * F_BK], Bs[64 * F_BK];
+  __shared__ float bred[16][64];
+  const int T = a.KH * a.KW, Ncols = T * a.Nc;
+  const int nmt = (a.M + 63) / 64, nnt = (Ncols + 63) / 64, tiles = nmt * nnt;
+  const int bid = blockIdx.x;
+  const int split = bid / tiles, tile = bid - split * tiles;
+  const int mt = tile / nnt, nt = tile - mt * nnt;
+  const int m0 = mt * 64, n0 = nt * 64;
+  const long P = (long)a.N * a.Hg * a.Wg;
+  const long p0 = (long)split * a.pix_per_split;
+  const long p1 = p0 + a.pix_per_split < P ? p0 + a.pix_per_split : P;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wp = wid >> 1, wc = wid & 1;          // 2 x 2 waves of 32 x 32
+  const int lpx = tid >> 4, l4 = tid & 15;        // loader: pixel lpx of the step, chunk l4 of 16
+  // this thread's A chunk: channels m0 + 4 l4 ..; B chunk: column n0 + 4 l4 -> (tap, n)
+  const int am = m0 + 4 * l4;
+  const int bcol = n0 + 4 * l4;
+  const int btap = bcol / a.Nc, bn = bcol - btap * a.Nc;
+  const int bkh = btap / a.KW, bkw = btap - bkh * a.KW;
+  const bool aok = am < a.M, bok = bcol < Ncols;
+  const bool do_bias = a.bslab != nullptr && nt == 0;
+  f32x4v bsum = f32x4v{0.f, 0.f, 0.f, 0.f};
+
+  f32x4_t acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  const int q = lane >> 4;
+  for (long pb = p0; pb < p1; pb += F_BK) {
+    const long p = pb + lpx;
+    f32x4v va = f32x4v{0.f, 0.f, 0.f, 0.f}, vb = va;
+    if (p < p1) {
+      const int hw = a.Hg * a.Wg;
+      const int n = (int)(p / hw), rem = (int)(p - (long)n * hw), h = rem / a.Wg, w = rem - (rem / a.Wg) * a.Wg;
+      if (aok) va = *reinterpret_cast<const f32x4v*>(a.A + p * a.lda + am);
+      const int bh = h * a.s + bkh - a.pad, bw = w * a.s + bkw - a.pad;
+      if (bok && bh >= 0 && bh < a.HB && bw >= 0 && bw < a.WB)
+        vb = *reinterpret_cast<const f32x4v*>(a.B + ((long)(n * a.HB + bh) * a.WB + bw) * a.ldb + bn);
+    }
+    if (do_bias) bsum += va;
+    // transposed store: row (channel / column) r, pixel lpx; rows r .. r+3 of this chunk
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int r = 4 * l4 + e;
+      const int pc = lpx >> 2, pe = lpx & 3;
+      reinterpret_cast<float*>(reinterpret_cast<char*>(As) + r * RB + fswz(r, pc) * 16)[pe] = va[e];
+      reinterpret_cast<float*>(reinterpret_cast<char*>(Bs) + r * RB + fswz(r, pc) * 16)[pe] = vb[e];
+    }
+    __syncthreads();
+    f32x4v af[2], bfr[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int ra = wc * 32 + i * 16 + (lane & 15);
+      af[i] = *reinterpret_cast<const f32x4v*>(reinterpret_cast<const char*>(As) + ra * RB + fswz(ra, q) * 16);
+      const int rb = wp * 32 + i * 16 + (lane & 15);
+      bfr[i] = *reinterpret_cast<const f32x4v*>(reinterpret_cast<const char*>(Bs) + rb * RB + fswz(rb, q) * 16);
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = mfma4(af[i], bfr[j], acc[i][j]);
+    __syncthreads();
+  }
+  // slab[split][tap][m][n]: lane holds rows (m) 4 q + r of column (lane & 15)
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int col = n0 + wp * 32 + j * 16 + (lane & 15);
+    if (col >= Ncols) continue;
+    const int tap = col / a.Nc, n = col - tap * a.Nc;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wc * 32 + i * 16 + 4 * q + r;
+        if (m < a.M) a.slab[(((long)split * T + tap) * a.M + m) * a.Nc + n] = acc[i][j][r];
+      }
+  }
+  if (do_bias) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) bred[lpx][4 * l4 + e] = bsum[e];
+    __syncthreads();
+    if (tid < 64 && m0 + tid < a.M) {
+      float s = 0.f;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) s += bred[k][tid];
+      a.bslab[(long)split * a.M + m0 + tid] = s;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------ elementwise
+// y = g * (r > 0) over n floats (float4)
+__global__ __launch_bounds__(256) void relu_bwd_f32_kernel(const float* __restrict__ g, const float* __restrict__ r,
+                                                           float* __restrict__ y, long n4) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (long)gridDim.x * blockDim.x) {
+    const f32x4v gv = reinterpret_cast<const f32x4v*>(g)[i], rv = reinterpret_cast<const f32x4v*>(r)[i];
+    f32x4v o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = rv[e] > 0.f ? gv[e] : 0.f;
+    reinterpret_cast<f32x4v*>(y)[i] = o;
+  }
+}
+
+// 2x2/s2 max-pool (floor), NHWC dense C channels; code = argmax window position (first maximum,
+// window order tl, tr, bl, br -- torch max_pool2d's choice)
+__global__ __launch_bounds__(256) void maxpool2_f32_kernel(const float* __restrict__ x, float* __restrict__ y,
+                                                           unsigned char* __restrict__ code, int N, int H, int W, int C) {
+  const int Ho = H >> 1, Wo = W >> 1;
+  const long tot = (long)N * Ho * Wo * C;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < tot; i += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    const long pix = i / C;
+    const int wo = (int)(pix % Wo), ho = (int)((pix / Wo) % Ho), n = (int)(pix / ((long)Wo * Ho));
+    const float* b = x + (((long)n * H + 2 * ho) * W + 2 * wo) * C + c;
+    const float v0 = b[0], v1 = b[C], v2 = b[(long)W * C], v3 = b[(long)W * C + C];
+    float m = v0;
+    unsigned k = 0;
+    if (v1 > m) { m = v1; k = 1; }
+    if (v2 > m) { m = v2; k = 2; }
+    if (v3 > m) { m = v3; k = 3; }
+    y[i] = m;
+    code[i] = (unsigned char)k;
+  }
+}
+
+// dx[2h+i][2w+j][c] = (code == 2i+j) ? g[h][w][c] : 0 over the whole input grid (odd last row/col: 0)
+__global__ __launch_bounds__(256) void maxpool2_bwd_f32_kernel(const float* __restrict__ g, const unsigned char* __restrict__ code,
+                                                               float* __restrict__ dx, int N, int H, int W, int C) {
+  const int Ho = H >> 1, Wo = W >> 1;
+  const long tot = (long)N * H * W * C;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < tot; i += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C);
+    const long pix = i / C;
+    const int w = (int)(pix % W), h = (int)((pix / W) % H), n = (int)(pix / ((long)W * H));
+    const int ho = h >> 1, wo = w >> 1;
+    float v = 0.f;
+    if (ho < Ho && wo < Wo) {
+      const long o = (((long)n * Ho + ho) * Wo + wo) * C + c;
+      if (code[o] == (unsigned)((h & 1) * 2 + (w & 1))) v = g[o];
+    }
+    dx[i] = v;
+  }
+}
+
+// segmentation head forward: z = b + sum_c w[c] y[p][c], p = sigmoid(z); per-block partial sums of
+// [BCE(p, t), p * [t == 1], p, [t == 1]] (reference utils/utils.py:9-25, log clamped at -100 like
+// torch's BCELoss) -> slab[block][4]; optional probabilities out
+__global__ __launch_bounds__(256) void head_f32_kernel(const float* __restrict__ y, int C, const float* __restrict__ w,
+                                                       const float* __restrict__ b, const float* __restrict__ t, long P,
+                                                       float* __restrict__ slab, float* __restrict__ probs) {
+  __shared__ float red[4][256];
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < P; i += (long)gridDim.x * blockDim.x) {
+    float z = b[0];
+    for (int c = 0; c < C; ++c) z = fmaf(w[c], y[i * C + c], z);
+    const float p = 1.f / (1.f + expf(-z));
+    if (probs) probs[i] = p;
+    if (t) {
+      const float tt = t[i];
+      const float lp = fmaxf(logf(p), -100.f), l1p = fmaxf(logf(1.f - p), -100.f);
+      s0 += -(tt * lp + (1.f - tt) * l1p);
+      const float one = tt == 1.f ? 1.f : 0.f;
+      s1 += p * one;
+      s2 += p;
+      s3 += one;
+    }
+  }
+  if (!t) return;
+  red[0][threadIdx.x] = s0; red[1][threadIdx.x] = s1; red[2][threadIdx.x] = s2; red[3][threadIdx.x] = s3;
+  __syncthreads();
+  for (int k = 128; k > 0; k >>= 1) {
+    if ((int)threadIdx.x < k)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) red[j][threadIdx.x] += red[j][threadIdx.x + k];
+    __syncthreads();
+  }
+  if (threadIdx.x < 4) slab[blockIdx.x * 4 + threadIdx.x] = red[threadIdx.x][0];
+}
+
+// head backward: dL/dz per pixel from dS (gradient w.r.t. the four partial sums), torch's BCE backward
+// through the sigmoid (common.h head_dz, shared with the bf16 head kernels); gy[p][c] = dz w[c];
+// per-block partials of sum_p dz y[p][c] (C) and sum_p dz (1) -> slab[block][C + 1]
+template <int C>
+__global__ __launch_bounds__(256) void head_bwd_f32_kernel(const float* __restrict__ y, const float* __restrict__ w,
+                                                           const float* __restrict__ b, const float* __restrict__ t,
+                                                           const float* __restrict__ dS, long P, float* __restrict__ gy,
+                                                           float* __restrict__ slab) {
+  __shared__ float red[256];
+  float acc[C + 1];
+#pragma unroll
+  for (int c = 0; c <= C; ++c) acc[c] = 0.f;
+  const float d0 = dS[0], d1 = dS[1], d2 = dS[2];
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < P; i += (long)gridDim.x * blockDim.x) {
+    float z = b[0];
+#pragma unroll
+    for (int c = 0; c < C; ++c) z = fmaf(w[c], y[i * C + c], z);
+    const float p = 1.f / (1.f + expf(-z));
+    const float tt = t[i];
+    const float dz = head_dz(p, tt, tt == 1.f ? 1.f : 0.f, d0, d1, d2);
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      gy[i * C + c] = dz * w[c];
+      acc[c] = fmaf(dz, y[i * C + c], acc[c]);
+    }
+    acc[C] += dz;
+  }
+#pragma unroll
+  for (int c = 0; c <= C; ++c) {
+    red[threadIdx.x] = acc[c];
+    __syncthreads();
+    for (int k = 128; k > 0; k >>= 1) {
+      if ((int)threadIdx.x < k) red[threadIdx.x] += red[threadIdx.x + k];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) slab[(long)blockIdx.x * (C + 1) + c] = red[0];
+    __syncthreads();
+  }
+}
+
+// NCHW fp32 (C <= 4) -> NHWC fp32 with 4 channels (zero padded)
+__global__ __launch_bounds__(256) void nchw_to_nhwc4_f32_kernel(const float* __restrict__ x, float* __restrict__ y, int N,
+                                                                int C, long HW) {
+  const long tot = (long)N * HW;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < tot; i += (long)gridDim.x * blockDim.x) {
+    const long n = i / HW, p = i - n * HW;
+    f32x4v v = f32x4v{0.f, 0.f, 0.f, 0.f};
+    for (int c = 0; c < C; ++c) v[c] = x[(n * C + c) * HW + p];
+    reinterpret_cast<f32x4v*>(y)[i] = v;
+  }
+}
+
+// per-channel sums of an NHWC tensor into slab[block][C] (bias gradient of the transposed conv): block b
+// sums pixels b, b + gridDim.x, ... ; thread (c, r) takes channel c (+ 256 k for C > 256) of row group r
+__global__ __launch_bounds__(256) void channel_sum_f32_kernel(const float* __restrict__ g, long P, int C,
+                                                              float* __restrict__ slab) {
+  __shared__ float red[256];
+  const int R = C < 256 ? 256 / C : 1;               // host: C < 256 divides 256
+  const int r = threadIdx.x / (C < 256 ? C : 256);
+  for (int c = threadIdx.x % (C < 256 ? C : 256); c < C; c += 256) {
+    float s = 0.f;
+    for (long p = (long)blockIdx.x * R + r; p < P; p += (long)gridDim.x * R) s += g[p * C + c];
+    __syncthreads();
+    red[threadIdx.x] = s;
+    __syncthreads();
+    if (r == 0) {
+      for (int k = 1; k < R; ++k) s += red[k * C + c];
+      slab[(long)blockIdx.x * C + c] = s;
+    }
+  }
+}
+
+static unsigned egrid(long n) { return (unsigned)(n / 256 + 1 < 8192 ? n / 256 + 1 : 8192); }
+
+// Eligible: Cs % 4 == 0 (a float4 chunk never straddles a tap), Kpad % 16 == 0, Kpad >= KH*KW*Cs,
+// Ngemm % 32 == 0, 16-B aligned strides; mode 1 also Cout % 4 == 0.
+DPA_API int dpa_igemm_f32(const F32ConvArgs* args, hipStream_t st) {
+  const F32ConvArgs& a = *args;
+  if ((a.Cs & 3) || (a.Kpad % F_BK) || a.Kpad < a.KH * a.KW * a.Cs || (a.Ngemm & 31) || (a.ldx & 3) || (a.ldy & 3) ||
+      (a.mask && (a.ldm & 3)) || (a.mode == 1 && (a.Cout & 3)) || a.KH * a.KW > 32 || a.N < 1)
+    return (int)hipErrorInvalidValue;
+  const long M = (long)a.N * a.Ho * a.Wo;
+  if (a.Ngemm % 64 == 0) {
+    const long grid = ((M + 63) / 64) * (a.Ngemm / 64);
+    hipLaunchKernelGGL((igemm_f32_kernel<64, 64, 2>), dim3((unsigned)grid), dim3(256), 0, st, a);
+  } else {
+    const long grid = ((M + 63) / 64) * (a.Ngemm / 32);
+    hipLaunchKernelGGL((igemm_f32_kernel<64, 32, 4>), dim3((unsigned)grid), dim3(256), 0, st, a);
+  }
+  return (int)hipGetLastError();
+}
+
+// Eligible: M % 4 == 0, Nc % 4 == 0, lda / ldb % 4 == 0, pix_per_split % 16 == 0, splits covering all pixels.
+DPA_API int dpa_wgrad_f32(const F32WgradArgs* args, hipStream_t st) {
+  const F32WgradArgs& a = *args;
+  const long P = (long)a.N * a.Hg * a.Wg;
+  if ((a.M & 3) || (a.Nc & 3) || (a.lda & 3) || (a.ldb & 3) || a.pix_per_split < 16 || (a.pix_per_split % 16) ||
+      a.splits < 1 || (long)a.splits * a.pix_per_split < P || (long)(a.splits - 1) * a.pix_per_split >= P ||
+      a.KH * a.KW < 1)
+    return (int)hipErrorInvalidValue;
+  const int T = a.KH * a.KW;
+  const long tiles = (long)((a.M + 63) / 64) * ((T * a.Nc + 63) / 64);
+  hipLaunchKernelGGL(wgrad_f32_kernel, dim3((unsigned)(tiles * a.splits)), dim3(256), 0, st, a);
+  return (int)hipGetLastError();
+}
+
+DPA_API int dpa_relu_bwd_f32(const float* g, const float* r, float* y, long long n, hipStream_t st) {
+  if (n % 4) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(relu_bwd_f32_kernel, dim3(egrid(n / 4)), dim3(256), 0, st, g, r, y, (long)(n / 4));
+  return (int)hipGetLastError();
+}
+
+DPA_API int dpa_maxpool2_f32(const float* x, float* y, unsigned char* code, int N, int H, int W, int C, hipStream_t st) {
+  if (H < 2 || W < 2 || C < 1) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(maxpool2_f32_kernel, dim3(egrid((long)N * (H / 2) * (W / 2) * C)), dim3(256), 0, st, x, y, code, N, H,
+                     W, C);
+  return (int)hipGetLastError();
+}
+
+DPA_API int dpa_maxpool2_bwd_f32(const float* g, const unsigned char* code, float* dx, int N, int H, int W, int C,
+                                 hipStream_t st) {
+  if (H < 2 || W < 2 || C < 1) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(maxpool2_bwd_f32_kernel, dim3(egrid((long)N * H * W * C)), dim3(256), 0, st, g, code, dx, N, H, W, C);
+  return (int)hipGetLastError();
+}
+
+// head forward over P pixels of C channels: slab needs blocks * 4 floats (blocks = dpa_head_f32_blocks)
+DPA_API int dpa_head_f32_blocks(long long P) { return (int)(P / 256 + 1 < 1024 ? P / 256 + 1 : 1024); }
+
+DPA_API int dpa_head_f32(const float* y, int C, const float* w, const float* b, const float* t, long long P, float* slab,
+                         float* probs, hipStream_t st) {
+  if (C < 1) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(head_f32_kernel, dim3(dpa_head_f32_blocks(P)), dim3(256), 0, st, y, C, w, b, t, (long)P, slab, probs);
+  return (int)hipGetLastError();
+}
+
+DPA_API int dpa_head_bwd_f32(const float* y, int C, const float* w, const float* b, const float* t, const float* dS,
+                             long long P, float* gy, float* slab, hipStream_t st) {
+  const dim3 grid(dpa_head_f32_blocks(P));
+  switch (C) {
+    case 8: hipLaunchKernelGGL(head_bwd_f32_kernel<8>, grid, dim3(256), 0, st, y, w, b, t, dS, (long)P, gy, slab); break;
+    case 16: hipLaunchKernelGGL(head_bwd_f32_kernel<16>, grid, dim3(256), 0, st, y, w, b, t, dS, (long)P, gy, slab); break;
+    case 32: hipLaunchKernelGGL(head_bwd_f32_kernel<32>, grid, dim3(256), 0, st, y, w, b, t, dS, (long)P, gy, slab); break;
+    case 64: hipLaunchKernelGGL(head_bwd_f32_kernel<64>, grid, dim3(256), 0, st, y, w, b, t, dS, (long)P, gy, slab); break;
+    default: return (int)hipErrorInvalidValue;
+  }
+  return (int)hipGetLastError();
+}
+
+DPA_API int dpa_nchw_to_nhwc4_f32(const float* x, float* y, int N, int C, long long HW, hipStream_t st) {
+  if (C < 1 || C > 4) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(nchw_to_nhwc4_f32_kernel, dim3(egrid((long)N * HW)), dim3(256), 0, st, x, y, N, C, (long)HW);
+  return (int)hipGetLastError();
+}
+
+// slab rows = dpa_head_f32_blocks(P) (same grid policy)
+DPA_API int dpa_channel_sum_f32(const float* g, long long P, int C, float* slab, hipStream_t st) {
+  if (C < 1 || (C < 256 && 256 % C) || (C > 256 && C % 256)) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(channel_sum_f32_kernel, dim3(dpa_head_f32_blocks(P)), dim3(256), 0, st, g, (long)P, C, slab);
+  return (int)hipGetLastError();
+}

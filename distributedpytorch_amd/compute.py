@@ -59,28 +59,42 @@ class Compute:
         return run_segment(self.blocks, 0, n_blocks(self.depth), self.depth, {"x": x}, want="probs")["probs"]
 
 
-def resolve_backend(backend: str, device, dtype: str = "bf16") -> str:
-    """``auto`` -> the HIP engine on a GPU for bf16 compute; stock ops on CPU and for fp32 (the
-    reference's precision, utils/train_utils.py:60-61: the HIP kernels store bf16 activations, so an
-    fp32 run -- e.g. a parity run -- goes to the torch backend, which computes in fp32 on the GPU)."""
+def resolve_backend(backend: str, device, dtype: str = "bf16", model=None) -> str:
+    """``auto`` -> the HIP engines on a GPU, stock ops on CPU.  bf16: :class:`.models.hip_unet.HipBlocks`
+    (bf16 storage, fp32 accumulate); fp32 -- the reference's precision, utils/train_utils.py:60-61 --:
+    :class:`.models.hip_unet_f32.HipF32Blocks` (fp32 storage, fp32 MFMA) for the configurations it
+    supports (``model`` given: checked; no BatchNorm / bilinear, widths % 32), else the torch backend
+    (fp32 on the GPU) for ``auto`` and an error for an explicit ``hip``."""
     device = torch.device(device)
     if backend == "auto":
         if device.type != "cuda":
             return "torch"
-        if dtype != "bf16":
+        backend = "hip"
+        if dtype == "fp32" and model is not None and not _f32_supported(model):
             import logging
             logging.getLogger(__name__).info(
-                "dtype=%s: the HIP engine computes in bf16; using the torch backend (fp32 on %s)", dtype, device)
+                "dtype=fp32: this model configuration is not covered by the fp32 HIP engine; using the torch backend")
             return "torch"
-        return "hip"
-    if backend == "hip" and dtype != "bf16":
-        raise ValueError(f"--backend hip computes in bf16 (fp32 accumulate); --dtype {dtype} needs --backend torch/auto")
+        return backend
+    if backend == "hip" and dtype not in ("bf16", "fp32"):
+        raise ValueError(f"--backend hip computes in bf16 or fp32, not {dtype}")
+    if backend == "hip" and dtype == "fp32" and model is not None and not _f32_supported(model):
+        raise ValueError("--backend hip --dtype fp32: the fp32 engine covers the reference UNet family without "
+                         "BatchNorm / bilinear up-sampling and channel widths divisible by 32")
     return backend
+
+
+def _f32_supported(model) -> bool:
+    from .models.hip_unet_f32 import supported
+    return supported(model)
 
 
 def make_blocks(model, backend: str = "auto", dtype: str = "bf16", device=None, owned=None):
     dev = torch.device(device) if device is not None else next(model.parameters()).device
-    backend = resolve_backend(backend, dev, dtype)
+    backend = resolve_backend(backend, dev, dtype, model)
+    if backend == "hip" and dtype == "fp32":
+        from .models.hip_unet_f32 import HipF32Blocks
+        return HipF32Blocks(model, device=dev, owned=owned)
     if backend == "hip":
         from .models.hip_unet import HipBlocks
         return HipBlocks(model, dtype=dtype, device=dev, owned=owned)

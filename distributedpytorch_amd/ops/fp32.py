@@ -1,0 +1,239 @@
+"""Python wrappers of the fp32 kernel family (csrc/fp32.hip): the hand-written fp32 training path.
+
+Every wrapper checks the tensor contracts (dtype, NHWC strides, 16-B alignment) before it builds an
+argument block, and launches on the current stream of the output's device.  Weight packing is done
+with a few torch ops on the (small) fp32 parameter tensors; every activation-sized pass is a HIP kernel.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional, Tuple
+
+import torch
+
+from . import _lib
+
+c_int, c_ll, c_void_p = ctypes.c_int, ctypes.c_longlong, ctypes.c_void_p
+_MAX = 2 ** 31 - 1024          # per-launch element-offset range the host keeps (int pixel math)
+
+
+class F32ConvArgs(ctypes.Structure):
+    _fields_ = [("x", c_void_p), ("w", c_void_p), ("bias", c_void_p), ("y", c_void_p), ("mask", c_void_p)] + \
+               [(n, c_int) for n in ("ldx", "ldy", "ldm", "mask_ch", "N", "Ho", "Wo", "Hs", "Ws", "Cs", "KH", "KW",
+                                     "stride", "pad", "Ngemm", "Kpad", "mode", "relu", "accumulate", "Cout")]
+
+
+class F32WgradArgs(ctypes.Structure):
+    _fields_ = [("A", c_void_p), ("B", c_void_p), ("slab", c_void_p), ("bslab", c_void_p)] + \
+               [(n, c_int) for n in ("lda", "ldb", "N", "Hg", "Wg", "HB", "WB", "M", "Nc", "s", "pad", "KH", "KW")] + \
+               [("pix_per_split", ctypes.c_long), ("splits", c_int)]
+
+
+def _st(t: torch.Tensor):
+    return c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def _p(t: Optional[torch.Tensor]):
+    return None if t is None else c_void_p(t.data_ptr())
+
+
+def _check(err, name):
+    _lib.check(int(err), name)
+
+
+def nhwc(t: torch.Tensor, name: str) -> Tuple[int, int, int, int, int]:
+    """(N, H, W, C, ld) of an NHWC fp32 tensor (channel slice allowed: ld = W stride)."""
+    assert t.dtype == torch.float32 and t.dim() == 4 and t.is_cuda, f"{name}: need cuda fp32 NHWC, got {t.dtype} {tuple(t.shape)}"
+    N, H, W, C = t.shape
+    sN, sH, sW, sC = t.stride()
+    assert sC == 1 and sH == W * sW and (N == 1 or sN == H * sH), f"{name}: unsupported strides {t.stride()}"
+    assert sW % 4 == 0 and t.data_ptr() % 16 == 0, f"{name}: ld {sW} / pointer not 16-byte aligned"
+    return N, H, W, C, sW
+
+
+def round_up(x: int, m: int) -> int:
+    return (x + m - 1) // m * m
+
+
+# ---------------------------------------------------------------------------------------- packing
+def pack_conv_fwd(w: torch.Tensor, cs: int) -> Tuple[torch.Tensor, int]:
+    """Conv2d weight [Cout, Cin, 3, 3] -> [Cout][Kpad], k = tap * cs + ci (input channels padded to cs)."""
+    co, ci, kh, kw = w.shape
+    wp = torch.zeros(co, kh * kw, cs, dtype=torch.float32, device=w.device)
+    wp[:, :, :ci] = w.detach().permute(0, 2, 3, 1).reshape(co, kh * kw, ci)
+    kpad = round_up(kh * kw * cs, 16)
+    out = torch.zeros(co, kpad, dtype=torch.float32, device=w.device)
+    out[:, :kh * kw * cs] = wp.reshape(co, -1)
+    return out.contiguous(), kpad
+
+
+def pack_conv_dgrad(w: torch.Tensor) -> Tuple[torch.Tensor, int]:
+    """dx = conv3x3(g, flipped W^T): [Cin][Kpad], k = tap * Cout + co, tap of the flipped kernel."""
+    co, ci, kh, kw = w.shape
+    wd = w.detach().flip(2, 3).permute(1, 2, 3, 0).reshape(ci, kh * kw * co)
+    kpad = round_up(kh * kw * co, 16)
+    out = torch.zeros(ci, kpad, dtype=torch.float32, device=w.device)
+    out[:, :kh * kw * co] = wd
+    return out.contiguous(), kpad
+
+
+def pack_deconv_fwd(w: torch.Tensor) -> torch.Tensor:
+    """ConvTranspose2d weight [Cin, Cout, 2, 2] -> [4 Cout][Cin], row (2i + j) Cout + co."""
+    ci, co = w.shape[:2]
+    return w.detach().permute(2, 3, 1, 0).reshape(4 * co, ci).contiguous()
+
+
+def pack_deconv_dgrad(w: torch.Tensor) -> torch.Tensor:
+    """dx[h][w][ci] = sum_{i,j,co} g[2h+i][2w+j][co] W[ci][co][i][j]: [Cin][4 Cout], k = (2i + j) Cout + co."""
+    ci, co = w.shape[:2]
+    return w.detach().permute(0, 2, 3, 1).reshape(ci, 4 * co).contiguous()
+
+
+# ---------------------------------------------------------------------------------------- GEMMs
+def igemm(x: torch.Tensor, wp: torch.Tensor, y: torch.Tensor, *, Ngemm: int, Kpad: int, KH: int, KW: int,
+          stride: int, pad: int, Cs: int, out_grid, bias: Optional[torch.Tensor] = None, relu: bool = False,
+          mask: Optional[torch.Tensor] = None, mask_ch: int = 0, mode: int = 0, Cout: int = 0,
+          accumulate: bool = False) -> torch.Tensor:
+    """fp32 implicit GEMM (see csrc/fp32.hip igemm_f32_kernel); ``out_grid`` = (N, Ho, Wo) of GEMM-M."""
+    N, Hs, Ws, Cx, ldx = nhwc(x, "igemm_f32.x")
+    _, _, _, Cy, ldy = nhwc(y, "igemm_f32.y")
+    No, Ho, Wo = out_grid
+    assert No == N and Cs <= Cx and Cs % 4 == 0 and Kpad % 16 == 0 and Kpad >= KH * KW * Cs and Ngemm % 32 == 0
+    assert wp.dtype == torch.float32 and wp.is_contiguous() and wp.numel() >= Ngemm * Kpad
+    if mode == 0:
+        assert tuple(y.shape[:3]) == (N, Ho, Wo) and Cy >= Ngemm
+    else:
+        assert tuple(y.shape[:3]) == (N, 2 * Ho, 2 * Wo) and Cy >= Cout and Ngemm == 4 * Cout and Cout % 4 == 0
+    assert (Ho - 1) * stride + KH - 1 - pad <= Hs - 1 + pad and (Wo - 1) * stride + KW - 1 - pad <= Ws - 1 + pad
+    ldm = 0
+    if mask is not None:
+        Nm, Hm, Wm, Cm, ldm = nhwc(mask, "igemm_f32.mask")
+        assert (Nm, Hm, Wm) == (N, Ho, Wo) and mode == 0
+        mask_ch = mask_ch or min(Cm, Ngemm)
+    if bias is not None:
+        assert bias.dtype == torch.float32 and bias.is_contiguous() and bias.numel() >= (Cout or Ngemm)
+    L = _lib.lib()
+    st = _st(y)
+    per_img = max(Hs * Ws * ldx, (4 if mode else 1) * Ho * Wo * ldy)
+    step = max(1, _MAX // max(per_img, 1))
+    for n0 in range(0, N, step):
+        n1 = min(N, n0 + step)
+        a = F32ConvArgs(x[n0:n1].data_ptr(), wp.data_ptr(), None if bias is None else bias.data_ptr(), y[n0:n1].data_ptr(),
+                        None if mask is None else mask[n0:n1].data_ptr(), ldx, ldy, ldm, mask_ch, n1 - n0, Ho, Wo, Hs, Ws,
+                        Cs, KH, KW, stride, pad, Ngemm, Kpad, mode, int(relu), int(accumulate), Cout)
+        _check(L.dpa_igemm_f32(ctypes.byref(a), st), "igemm_f32")
+    return y
+
+
+def wgrad(A: torch.Tensor, B: torch.Tensor, gw: torch.Tensor, gb: Optional[torch.Tensor], *, KH: int, KW: int, s: int,
+          pad: int, target_blocks: int = 1024) -> None:
+    """gw[m][n][kh][kw] += sum_p A[p][m] B[p*s + (kh, kw) - pad][n] (OIHW with O = A's channels), gb[m] +=
+    sum_p A[p][m]; A is the pixel grid.  Split over pixel ranges into fp32 slabs, summed in a fixed order."""
+    N, Hg, Wg, M, lda = nhwc(A, "wgrad_f32.A")
+    NB, HB, WB, Nc, ldb = nhwc(B, "wgrad_f32.B")
+    assert NB == N and M % 4 == 0 and Nc % 4 == 0
+    assert gw.dtype == torch.float32 and gw.is_contiguous() and gw.numel() == M * Nc * KH * KW
+    assert gb is None or (gb.dtype == torch.float32 and gb.numel() == M)
+    T = KH * KW
+    P = N * Hg * Wg
+    tiles = -(-M // 64) * -(-(T * Nc) // 64)
+    splits = max(1, min(-(-target_blocks // tiles), -(-P // 4096)))
+    pps = round_up(-(-P // splits), 16)
+    splits = -(-P // pps)
+    slab = torch.empty(splits * T * M * Nc + (splits * M if gb is not None else 0), dtype=torch.float32, device=A.device)
+    bslab = slab[splits * T * M * Nc:] if gb is not None else None
+    a = F32WgradArgs(A.data_ptr(), B.data_ptr(), slab.data_ptr(), None if bslab is None else bslab.data_ptr(),
+                     lda, ldb, N, Hg, Wg, HB, WB, M, Nc, s, pad, KH, KW, pps, splits)
+    L = _lib.lib()
+    st = _st(A)
+    _check(L.dpa_wgrad_f32(ctypes.byref(a), st), "wgrad_f32")
+    _check(L.dpa_wgrad_reduce(_p(slab), _p(bslab), _p(gw), _p(gb), c_int(splits), c_int(T), c_int(M), c_int(Nc), c_int(Nc),
+                              c_int(0), st), "wgrad_reduce(f32)")
+
+
+# ---------------------------------------------------------------------------------------- elementwise
+def relu_bwd(g: torch.Tensor, r: torch.Tensor) -> torch.Tensor:
+    """g * (r > 0) (same shape, contiguous fp32)."""
+    assert g.dtype == r.dtype == torch.float32 and g.shape == r.shape and g.is_contiguous() and r.is_contiguous()
+    out = torch.empty_like(g)
+    _check(_lib.lib().dpa_relu_bwd_f32(_p(g), _p(r), _p(out), c_ll(g.numel()), _st(g)), "relu_bwd_f32")
+    return out
+
+
+def maxpool2(x: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    N, H, W, C, ld = nhwc(x, "maxpool2_f32.x")
+    assert ld == C and x.is_contiguous()
+    y = torch.empty(N, H // 2, W // 2, C, dtype=torch.float32, device=x.device)
+    code = torch.empty(N, H // 2, W // 2, C, dtype=torch.uint8, device=x.device)
+    _check(_lib.lib().dpa_maxpool2_f32(_p(x), _p(y), _p(code), c_int(N), c_int(H), c_int(W), c_int(C), _st(x)),
+           "maxpool2_f32")
+    return y, code
+
+
+def maxpool2_bwd(g: torch.Tensor, code: torch.Tensor, H: int, W: int) -> torch.Tensor:
+    N, Ho, Wo, C = g.shape
+    assert g.is_contiguous() and code.shape == g.shape and (Ho, Wo) == (H // 2, W // 2)
+    dx = torch.empty(N, H, W, C, dtype=torch.float32, device=g.device)
+    _check(_lib.lib().dpa_maxpool2_bwd_f32(_p(g), _p(code), _p(dx), c_int(N), c_int(H), c_int(W), c_int(C), _st(g)),
+           "maxpool2_bwd_f32")
+    return dx
+
+
+def head_fwd(y: torch.Tensor, w: torch.Tensor, b: torch.Tensor, t: Optional[torch.Tensor], want_probs: bool = False):
+    """Segmentation head on NHWC fp32 y: (S[4] partial sums or None, probabilities [P] or None)."""
+    N, H, W, C, ld = nhwc(y, "head_f32.y")
+    assert ld == C and y.is_contiguous()
+    P = N * H * W
+    L = _lib.lib()
+    blocks = L.dpa_head_f32_blocks(c_ll(P))
+    slab = torch.empty(blocks * 4, dtype=torch.float32, device=y.device)
+    probs = torch.empty(P, dtype=torch.float32, device=y.device) if want_probs else None
+    tf = None
+    if t is not None:
+        tf = t.reshape(-1).float().contiguous()
+        assert tf.numel() == P
+    w = w.detach().reshape(-1).float().contiguous()
+    b = b.detach().reshape(-1).float().contiguous()
+    _check(L.dpa_head_f32(_p(y), c_int(C), _p(w), _p(b), _p(tf), c_ll(P), _p(slab), _p(probs), _st(y)), "head_f32")
+    S = slab.view(blocks, 4).sum(0) if t is not None else None
+    return S, probs
+
+
+def head_bwd(y: torch.Tensor, w: torch.Tensor, b: torch.Tensor, t: torch.Tensor, dS: torch.Tensor):
+    """(dL/dy of the head -- NHWC fp32, NOT ReLU-masked --, segmap weight gradient [C], bias gradient [1])."""
+    N, H, W, C, ld = nhwc(y, "head_bwd_f32.y")
+    P = N * H * W
+    L = _lib.lib()
+    blocks = L.dpa_head_f32_blocks(c_ll(P))
+    gy = torch.empty_like(y)
+    slab = torch.empty(blocks * (C + 1), dtype=torch.float32, device=y.device)
+    tf = t.reshape(-1).float().contiguous()
+    dS = dS.reshape(-1).float().contiguous()
+    wv = w.detach().reshape(-1).float().contiguous()
+    bv = b.detach().reshape(-1).float().contiguous()
+    _check(L.dpa_head_bwd_f32(_p(y), c_int(C), _p(wv), _p(bv), _p(tf), _p(dS), c_ll(P), _p(gy), _p(slab), _st(y)),
+           "head_bwd_f32")
+    red = slab.view(blocks, C + 1).sum(0)
+    return gy, red[:C], red[C:]
+
+
+def input_nhwc4(x: torch.Tensor) -> torch.Tensor:
+    """NCHW fp32 (C <= 4) -> NHWC fp32 with 4 channels (zero padded)."""
+    assert x.dtype == torch.float32 and x.dim() == 4 and x.shape[1] <= 4
+    x = x.contiguous()
+    N, C, H, W = x.shape
+    y = torch.empty(N, H, W, 4, dtype=torch.float32, device=x.device)
+    _check(_lib.lib().dpa_nchw_to_nhwc4_f32(_p(x), _p(y), c_int(N), c_int(C), c_ll(H * W), _st(x)), "nchw_to_nhwc4_f32")
+    return y
+
+
+def channel_sum(g: torch.Tensor, out: torch.Tensor) -> None:
+    """out[c] += sum over pixels of NHWC fp32 g (dense)."""
+    N, H, W, C, ld = nhwc(g, "channel_sum_f32.g")
+    assert ld == C and g.is_contiguous()
+    P = N * H * W
+    L = _lib.lib()
+    blocks = L.dpa_head_f32_blocks(c_ll(P))
+    slab = torch.empty(blocks * C, dtype=torch.float32, device=g.device)
+    _check(L.dpa_channel_sum_f32(_p(g), c_ll(P), c_int(C), _p(slab), _st(g)), "channel_sum_f32")
+    out.view(-1).add_(slab.view(blocks, C).sum(0))

@@ -417,8 +417,10 @@ def train(cfg: TrainConfig):
     if cfg.load:
         load_model_state(model, cfg.load)
     strat = build_strategy(cfg, model)
-    log.info(f"strategy={strat.name} backend={resolve_backend(cfg.backend, strat.device, cfg.dtype)} device={strat.device}")
-    if resolve_backend(cfg.backend, strat.device, cfg.dtype) == "hip":
+    backend = resolve_backend(cfg.backend, strat.device, cfg.dtype, model)
+    log.info(f"strategy={strat.name} backend={backend}{'-fp32' if backend == 'hip' and cfg.dtype == 'fp32' else ''} "
+             f"device={strat.device}")
+    if backend == "hip" and cfg.dtype != "fp32":
         from .ops import kernels as _K
         log.info(_K.CFG.describe())        # the run's kernel switches, once (ops/config.py)
 

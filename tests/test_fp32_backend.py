@@ -1,6 +1,7 @@
-"""``--dtype fp32`` (the reference's precision, utils/train_utils.py:60-61) on a GPU: ``backend=auto``
-resolves to the torch backend instead of crashing in the bf16-only HIP engine; an explicit
-``--backend hip --dtype fp32`` is a clear error."""
+"""``--dtype fp32`` (the reference's precision, utils/train_utils.py:60-61): on a GPU ``backend=auto``
+resolves to the fp32 HIP engine (models/hip_unet_f32.py, csrc/fp32.hip) for the reference UNet family
+and to the torch backend for configurations it does not cover (BatchNorm / bilinear); an explicit
+``--backend hip --dtype fp32`` on an uncovered model is a clear error."""
 import os
 import subprocess
 import sys
@@ -8,17 +9,23 @@ import sys
 import pytest
 
 from distributedpytorch_amd.compute import resolve_backend
+from distributedpytorch_amd.models.unet import build_model
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def test_resolve_backend_fp32_picks_torch():
+def test_resolve_backend_fp32():
+    unet, bn, bil = build_model("unet"), build_model("unet-bn"), build_model("unet-bilinear")
     assert resolve_backend("auto", "cuda:0", "bf16") == "hip"
-    assert resolve_backend("auto", "cuda:0", "fp32") == "torch"
-    assert resolve_backend("auto", "cpu", "bf16") == "torch"
+    assert resolve_backend("auto", "cuda:0", "fp32") == "hip"
+    assert resolve_backend("auto", "cuda:0", "fp32", unet) == "hip"
+    assert resolve_backend("auto", "cuda:0", "fp32", bn) == "torch"
+    assert resolve_backend("auto", "cuda:0", "fp32", bil) == "torch"
+    assert resolve_backend("auto", "cpu", "fp32", unet) == "torch"
     assert resolve_backend("torch", "cuda:0", "fp32") == "torch"
-    with pytest.raises(ValueError, match="bf16"):
-        resolve_backend("hip", "cuda:0", "fp32")
+    assert resolve_backend("hip", "cuda:0", "fp32", unet) == "hip"
+    with pytest.raises(ValueError, match="fp32 engine"):
+        resolve_backend("hip", "cuda:0", "fp32", bn)
 
 
 @pytest.mark.gpu
@@ -29,4 +36,4 @@ def test_train_py_fp32_on_gpu(tmp_path):
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
     assert (tmp_path / "checkpoints" / "singleGPU.pth").exists()
     log = (tmp_path / "logs" / "singleGPU.log").read_text()
-    assert "backend=torch" in log, log[-2000:]
+    assert "backend=hip-fp32" in log, log[-2000:]
