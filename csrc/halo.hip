@@ -644,6 +644,10 @@ __global__ __launch_bounds__(256 * WCS) void igemm_stream_kernel(IgemmArgs a) {
   constexpr bool do_head = EPI == 3;
   float hwv[do_head ? TC : 1][4];
   float hsum[4] = {0.f, 0.f, 0.f, 0.f};
+  // the head's target of each output pixel of a row is loaded at the START of the row (issued before the
+  // row prefetch, like the mask): loaded in the epilogue its latency was exposed once per row
+  const __amdgpu_buffer_rsrc_t tgr = __builtin_amdgcn_make_buffer_rsrc((void*)(do_head ? a.tgt + opix : (const float*)a.y),
+                                                                       0, do_head ? a.Ho * a.Wo * 4 : 0, 0x00020000);
   if constexpr (do_head) {
 #pragma unroll
     for (int ic = 0; ic < TC; ++ic)
@@ -690,6 +694,14 @@ __global__ __launch_bounds__(256 * WCS) void igemm_stream_kernel(IgemmArgs a) {
         for (int ic = 0; ic < TC; ++ic)
           mk[ip][ic] = (wc * WCN + ic * 16 < a.mask_ch) ? __builtin_amdgcn_raw_buffer_load_b64(mr, mbase + ml[ip] + ic * 32, 0, 0)
                                              : u32x2_t{0x3f803f80u, 0x3f803f80u};
+    }
+    float ttp[do_head ? TP : 1];
+    if constexpr (do_head) {
+#pragma unroll
+      for (int ip = 0; ip < TP; ++ip) {
+        const unsigned px = (unsigned)((h0 + r) * a.Wo + w0 + wp * WP + ip * 16 + (lane & 15));
+        ttp[ip] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(tgr, (chunk == 0 && pv[ip]) ? px * 4u : 0x80000000u, 0, 0));
+      }
     }
     __builtin_amdgcn_sched_barrier(0);
     if (r + 2 < nrows) rload(h0 + r + 3, nxt);
@@ -806,7 +818,7 @@ __global__ __launch_bounds__(256 * WCS) void igemm_stream_kernel(IgemmArgs a) {
           const float z = hdot + a.hb[0];
           const float p = fast_sigmoid(z);
           if (a.hprob) a.hprob[pix] = p;
-          const float tt = a.tgt[pix];
+          const float tt = ttp[ip];
           const float lp = fmaxf(__logf(p), -100.f), l1p = fmaxf(__logf(1.f - p), -100.f);
           const float one = tt == 1.f ? 1.f : 0.f;
           hsum[0] -= tt * lp + (1.f - tt) * l1p;
