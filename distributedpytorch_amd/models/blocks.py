@@ -11,6 +11,13 @@ Backends implement ``enc/mid/dec/head_partials/head_probs`` (:class:`TorchBlocks
 kernels in :mod:`.hip_unet`).  :func:`run_segment` executes any contiguous block range on a dict of
 named tensors - ``x`` plus the skips ``skip{l}`` still to be consumed - which is exactly what a
 pipeline stage sends/receives; :func:`partition` balances block ranges over stages by FLOPs.
+
+Cuts may also fall INSIDE a DoubleConv block (a pipeline stage boundary between its two convs, for
+the time-balanced partitions of ``parallel/schedule.py``): a cut ``b + 0.5`` splits block ``b`` into
+its part ``a`` (encoder / mid: the first conv; decoder: transposed conv + crop + concat + first conv)
+and part ``b`` (the second conv; encoder: + max-pool), and the tensor crossing it is ``x`` = the first
+conv's output.  Backends provide ``enc_a/enc_b/mid_a/mid_b/dec_a/dec_b`` for those halves; a block
+whose both halves run in one segment still runs as ONE fused block.
 """
 from __future__ import annotations
 
@@ -52,15 +59,43 @@ def consumed(idx: int, depth: int) -> List[str]:
     return [skip_name(depth - 1 - i)] if kind == "dec" else []
 
 
-def boundary_names(cut: int, depth: int) -> List[str]:
-    """Tensors crossing a cut placed before block ``cut``: ``x`` + skips produced before, used after."""
+def boundary_names(cut: float, depth: int) -> List[str]:
+    """Tensors crossing a cut placed before block ``cut`` (or inside block ``cut - 0.5``): ``x`` + the
+    skips produced before it (at the END of encoder block l) and consumed after it (at the START of
+    their decoder block, by its part a)."""
     names = ["x"]
     for lvl in range(depth):
-        prod_idx = lvl
         cons_idx = depth + 1 + (depth - 1 - lvl)
-        if prod_idx < cut <= cons_idx:
+        if lvl + 1 <= cut <= cons_idx:
             names.append(skip_name(lvl))
     return names
+
+
+def splittable(idx: int, depth: int) -> bool:
+    """Blocks that may be cut between their two convs (all but the head)."""
+    return 0 <= idx < n_blocks(depth) - 1
+
+
+def segment_units(start: float, end: float, depth: int) -> List[Tuple[int, str]]:
+    """(block, part) units of the segment [start, end): part ``full`` for whole blocks, ``a`` / ``b``
+    for the halves at a fractional start / end (a cut ``b + 0.5`` lies inside block ``b``)."""
+    for c in (start, end):
+        f = c - int(c)
+        assert f in (0.0, 0.5) and (f == 0.0 or splittable(int(c), depth)), f"invalid cut {c}"
+    out = []
+    idx = int(start)
+    while idx < end:
+        lo = max(start, idx)
+        hi = min(end, idx + 1)
+        if lo == idx and hi == idx + 1:
+            out.append((idx, "full"))
+        elif lo == idx:
+            out.append((idx, "a"))
+        else:
+            assert hi == idx + 1, (start, end)
+            out.append((idx, "b"))
+        idx += 1
+    return out
 
 
 class TorchBlocks:
@@ -94,6 +129,32 @@ class TorchBlocks:
         with self.ctx():
             return self.model.decoder.level(i, x, skip)
 
+    # halves of a block cut between its two convs (pipeline stage boundaries inside a DoubleConv)
+    def enc_a(self, l: int, x):
+        with self.ctx():
+            return self.model.encoder.blocks()[l].half(x, "a")
+
+    def enc_b(self, l: int, x):
+        with self.ctx():
+            s = self.model.encoder.blocks()[l].half(x, "b")
+            return s, F.max_pool2d(s, 2, 2)
+
+    def mid_a(self, x):
+        with self.ctx():
+            return self.model.mid.half(x, "a")
+
+    def mid_b(self, x):
+        with self.ctx():
+            return self.model.mid.half(x, "b")
+
+    def dec_a(self, i: int, x, skip):
+        with self.ctx():
+            return self.model.decoder.level(i, x, skip, part="a")
+
+    def dec_b(self, i: int, x):
+        with self.ctx():
+            return self.model.decoder.blocks()[i].half(x, "b")
+
     def head_logits(self, x):
         with self.ctx():
             return self.model.segmap(x).float()
@@ -118,17 +179,25 @@ def run_segment(blocks, start: int, end: int, depth: int, env: Dict[str, torch.T
         blocks.expect_target(target)      # lets a backend fuse the head into the last decoder conv
     if start == 0:
         env["x"] = blocks.prep(env["x"])
-    for idx in range(start, end):
+    for idx, part in segment_units(start, end, depth):
         kind, i = block_kind(idx, depth)
-        with trace_range(f"{kind}{i}" if kind in ("enc", "dec") else kind):
+        tag = (f"{kind}{i}" if kind in ("enc", "dec") else kind) + ("" if part == "full" else part)
+        with trace_range(tag):
             if kind == "enc":
-                s, env["x"] = blocks.enc(i, env["x"])
-                env[skip_name(i)] = s
+                if part == "a":
+                    env["x"] = blocks.enc_a(i, env["x"])
+                else:
+                    s, env["x"] = blocks.enc(i, env["x"]) if part == "full" else blocks.enc_b(i, env["x"])
+                    env[skip_name(i)] = s
             elif kind == "mid":
-                env["x"] = blocks.mid(env["x"])
+                env["x"] = {"full": blocks.mid, "a": blocks.mid_a, "b": blocks.mid_b}[part](env["x"])
             elif kind == "dec":
-                name = skip_name(depth - 1 - i)
-                env["x"] = blocks.dec(i, env["x"], env.pop(name))
+                if part == "b":
+                    env["x"] = blocks.dec_b(i, env["x"])
+                else:
+                    name = skip_name(depth - 1 - i)
+                    fn = blocks.dec if part == "full" else blocks.dec_a
+                    env["x"] = fn(i, env["x"], env.pop(name))
             else:
                 x = env.pop("x")
                 if want == "partials":

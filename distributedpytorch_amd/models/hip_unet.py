@@ -622,6 +622,35 @@ class HipBlocks:
         self.ensure_packed()
         return _DecFn.apply(self.anchor, x, skip, self, i)
 
+    # halves of a block cut between its two convs (a pipeline stage boundary inside a DoubleConv,
+    # models/blocks.py): the tensor between them is the first conv's (BN+)ReLU output, materialised;
+    # the fusions that span the two convs (BN-on-load, the first conv's BN statistics from the second
+    # conv's dgrad epilogue) do not cross the cut
+    def enc_a(self, l: int, x):
+        self.ensure_packed()
+        return _ConvHalfFn.apply(self.anchor, x, self, self.enc_convs[l][0], l > 0, None)
+
+    def enc_b(self, l: int, a):
+        self.ensure_packed()
+        return _EncBFn.apply(self.anchor, a, self, l)
+
+    def mid_a(self, x):
+        self.ensure_packed()
+        return _ConvHalfFn.apply(self.anchor, x, self, self.mid_convs[0], True, None)
+
+    def mid_b(self, a):
+        self.ensure_packed()
+        return _ConvHalfFn.apply(self.anchor, a, self, self.mid_convs[1], True, self.mid_convs[0])
+
+    def dec_a(self, i: int, x, skip):
+        self.ensure_packed()
+        return _DecAFn.apply(self.anchor, x, skip, self, i)
+
+    def dec_b(self, i: int, a):
+        self.ensure_packed()
+        c1, c2 = self.dec_convs[i]
+        return _ConvHalfFn.apply(self.anchor, a, self, c2, True, c1)
+
     def expect_target(self, t):
         """The segment being run ends in the head: the last decoder conv may compute the head and the
         loss partial sums in its epilogue (one pass less over the full-resolution activation)."""
@@ -935,6 +964,164 @@ class _DecFn(torch.autograd.Function):
         B.join()
         ctx.st = None
         if ctx.crop is not None:     # gradient of the crop: zero outside the kept window
+            Hs, Ws, top, left = ctx.crop
+            full = torch.zeros(dskip.shape[0], Hs, Ws, C, dtype=dskip.dtype, device=dskip.device)
+            full[:, top:top + dskip.shape[1], left:left + dskip.shape[2]] = dskip
+            dskip = full
+        return None, _o(dx), _o(dskip), None, None
+
+
+class _ConvHalfFn(torch.autograd.Function):
+    """One conv (+BN) + ReLU of a split DoubleConv.  ``below``: the conv whose output ``x`` is (the
+    first conv, for a second half) -- x is then a ReLU output and the dgrad is masked by it; without
+    ``below`` (a first half) the dgrad is not masked (the pool backward / concat split upstream masks
+    it), and ``x_grad`` False skips it (the network input)."""
+
+    @staticmethod
+    def forward(ctx, anchor, x, B: "HipBlocks", c: _Conv, x_grad: bool, below):
+        x = _v(x)
+        st = []
+        y = B.conv_fwd(c, x, st=st)
+        ctx.B, ctx.c, ctx.below, ctx.x_grad = B, c, below, x_grad
+        ctx.st = st[0] if st else None
+        ctx.save_for_backward(x)
+        return _o(y)
+
+    @staticmethod
+    def backward(ctx, g):
+        B, c, below = ctx.B, ctx.c, ctx.below
+        (x,) = ctx.saved_tensors
+        g = _v(g)
+        W = g.shape[2]
+        mask = below is not None
+        if ctx.x_grad and B.fusable(c, below, W):
+            gx, _ = B.bwd_conv(c, g, x, ctx.st, mask=mask, below=below)
+        else:
+            g = B.bn_bwd(c, g, ctx.st)
+            B.conv_wgrad(c, g, x)
+            gx = None
+            if ctx.x_grad:
+                gx = B.conv_dgrad(c, g, mask=x if mask else None, below=below)
+                if below is not None:
+                    gx = gx[0]
+        B.ready([c.mod, c.bn])
+        B.join()
+        ctx.st = None
+        return None, (None if gx is None else _o(gx)), None, None, None, None
+
+
+class _EncBFn(torch.autograd.Function):
+    """Second half of an encoder block: conv2 (+BN) + ReLU + max-pool (fused when streaming)."""
+
+    @staticmethod
+    def forward(ctx, anchor, a, B: "HipBlocks", l: int):
+        c1, c2 = B.enc_convs[l]
+        a = _v(a)
+        N, H, W = a.shape[:3]
+        skip = torch.empty(N, H, W, c2.Cout, dtype=torch.bfloat16, device=a.device)   # dense: it may leave the stage
+        pooled = torch.empty(N, H // 2, W // 2, c2.Cout, dtype=torch.bfloat16, device=a.device)
+        code = (torch.empty(N, H // 2, W // 2, c2.Cout, dtype=torch.uint8, device=a.device)
+                if H % 2 == 0 and W % 2 == 0 else None)
+        st2 = []
+        B.conv_fwd(c2, a, skip, pool=pooled, pcode=code, st=st2)
+        ctx.B, ctx.l = B, l
+        ctx.st = st2[0] if st2 else None
+        ctx.has_code = code is not None
+        ctx.save_for_backward(a, skip, code if code is not None else skip)
+        return _o(skip), _o(pooled)
+
+    @staticmethod
+    def backward(ctx, dskip, dpooled):
+        B, l = ctx.B, ctx.l
+        a, skip, code = ctx.saved_tensors
+        c1, c2 = B.enc_convs[l]
+        C = c2.Cout
+        dpooled = (torch.zeros(a.shape[0], a.shape[1] // 2, a.shape[2] // 2, C, dtype=torch.bfloat16, device=a.device)
+                   if dpooled is None else _v(dpooled))
+        dskip = None if dskip is None else _v(dskip)
+        W = a.shape[2]
+        if (ctx.has_code and K.USE_FUSED_POOL_BWD and B.fusable(c2, c1, W, whole=True)
+                and K.bwd_pool_foldable(c2.Cin, c2.Cout)):
+            g1 = B.conv_bwd(c2, dskip, a, mask=True, pool=(code, dpooled))
+        else:
+            g2 = torch.empty(a.shape[:3] + (C,), dtype=torch.bfloat16, device=a.device)
+            if ctx.has_code:
+                K.pool_bwd_code(code, dskip, dpooled, g2)
+            else:
+                K.pool_bwd(skip, dskip, dpooled, g2)
+            if B.fusable(c2, c1, W):
+                g1, _ = B.bwd_conv(c2, g2, a, ctx.st, mask=True, below=c1)
+            else:
+                g2 = B.bn_bwd(c2, g2, ctx.st)
+                B.conv_wgrad(c2, g2, a)
+                g1, _ = B.conv_dgrad(c2, g2, mask=a, below=c1)
+        B.ready([c2.mod, c2.bn])
+        B.join()
+        ctx.st = None
+        return None, _o(g1), None, None
+
+
+class _DecAFn(torch.autograd.Function):
+    """First half of a decoder block: transposed conv, crop, concat (or the dual input), conv1 (+BN) + ReLU."""
+
+    @staticmethod
+    def forward(ctx, anchor, x, skip, B: "HipBlocks", i: int):
+        d = B.deconvs[i]
+        c1, c2 = B.dec_convs[i]
+        C = d.Cout
+        x = _v(x)
+        skip = _v(skip)
+        Ns, Hs, Ws, _ = skip.shape
+        h2, w2 = 2 * x.shape[1], 2 * x.shape[2]
+        ctx.crop = None
+        up = None
+        if (Hs, Ws) != (h2, w2):
+            top, left = int(round((Hs - h2) / 2.0)), int(round((Ws - w2) / 2.0))
+            cat = torch.empty(Ns, h2, w2, 2 * C, dtype=torch.bfloat16, device=x.device)
+            cat[..., :C].copy_(skip[:, top:top + h2, left:left + w2])
+            ctx.crop = (Hs, Ws, top, left)
+        elif skip.is_contiguous() and B.dual_level(len(B.deconvs) - 1 - i, h2, w2):
+            cat = skip
+            up = torch.empty(Ns, h2, w2, C, dtype=torch.bfloat16, device=x.device)
+        else:
+            cat = B.cat_for(skip)
+        B.deconv_fwd(d, x, cat[..., C:] if up is None else up)
+        st1 = []
+        a = B.conv_fwd(c1, cat, st=st1, x2=up)
+        ctx.B, ctx.i = B, i
+        ctx.st = st1[0] if st1 else None
+        ctx.dual = up is not None
+        ctx.save_for_backward(x, cat, up if up is not None else cat)
+        return _o(a)
+
+    @staticmethod
+    def backward(ctx, g1):
+        B, i = ctx.B, ctx.i
+        x, cat, up = ctx.saved_tensors
+        d = B.deconvs[i]
+        c1, c2 = B.dec_convs[i]
+        C = d.Cout
+        g1 = _v(g1)
+        W = g1.shape[2]
+        if ctx.dual:
+            (dskip, gup), _ = B.bwd_conv(c1, g1, cat, ctx.st, mask=False, split=C, x2=up)
+        elif B.fusable(c1, None, W):
+            (dskip, gup), _ = B.bwd_conv(c1, g1, cat, ctx.st, mask=False, split=C)
+        else:
+            g1 = B.bn_bwd(c1, g1, ctx.st)
+            if B.halves_fusable(c1, C, W):
+                dskip, gup = B.conv_bwd_halves(c1, g1, cat, C)
+            else:
+                B.conv_wgrad(c1, g1, cat)
+                dskip, gup = B.conv_dgrad_split(c1, g1, C)
+        B.ready([c1.mod, c1.bn])
+        if isinstance(d, _Up):
+            gup = K.up2_bwd(gup)
+        dx = B.deconv_bwd(d, gup, x)
+        B.ready([d.mod])
+        B.join()
+        ctx.st = None
+        if ctx.crop is not None:
             Hs, Ws, top, left = ctx.crop
             full = torch.zeros(dskip.shape[0], Hs, Ws, C, dtype=dskip.dtype, device=dskip.device)
             full[:, top:top + dskip.shape[1], left:left + dskip.shape[2]] = dskip

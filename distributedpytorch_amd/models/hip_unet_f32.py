@@ -184,17 +184,39 @@ class HipF32Blocks:
         return _o(self._conv(c2, self._conv(c1, _v(x))))
 
     def dec(self, i: int, x, skip):
+        # transposed conv, reference CenterCrop of the skip (model/unet_parts.py:58-74), concat with the
+        # skip first (:59), conv_block
+        return self.dec_b(i, self.dec_a(i, x, skip))
+
+    # halves of a block cut between its two convs (pipeline stage boundary inside a DoubleConv)
+    def enc_a(self, l: int, x):
+        c1 = self.model.encoder.blocks()[l].convs()[0]
+        return _o(self._conv(c1, _v(x), 4 if l == 0 else None))
+
+    def enc_b(self, l: int, a):
+        c2 = self.model.encoder.blocks()[l].convs()[1]
+        s = self._conv(c2, _v(a))
+        return _o(s), _o(_MaxPool.apply(s))
+
+    def mid_a(self, x):
+        return _o(self._conv(self.model.mid.convs()[0], _v(x)))
+
+    def mid_b(self, a):
+        return _o(self._conv(self.model.mid.convs()[1], _v(a)))
+
+    def dec_a(self, i: int, x, skip):
         d = self.model.decoder.ups()[i]
-        c1, c2 = self.model.decoder.blocks()[i].convs()
+        c1 = self.model.decoder.blocks()[i].convs()[0]
         up = _Deconv.apply(_v(x), d.weight, d.bias)
         sk = _v(skip)
         h2, w2 = up.shape[1:3]
         if tuple(sk.shape[1:3]) != (h2, w2):
-            # reference CenterCrop of the skip to the up-sampled size (model/unet_parts.py:58-74)
             top, left = int(round((sk.shape[1] - h2) / 2.0)), int(round((sk.shape[2] - w2) / 2.0))
             sk = sk[:, top:top + h2, left:left + w2]
-        cat = torch.cat([sk, up], dim=3)           # skip first (unet_parts.py:59)
-        return _o(self._conv(c2, self._conv(c1, cat)))
+        return _o(self._conv(c1, torch.cat([sk, up], dim=3)))
+
+    def dec_b(self, i: int, a):
+        return _o(self._conv(self.model.decoder.blocks()[i].convs()[1], _v(a)))
 
     def head_partials(self, x, t):
         seg = self.model.segmap

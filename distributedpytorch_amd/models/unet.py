@@ -102,6 +102,11 @@ class ConvBlock(nn.Module):
     def forward(self, x):
         return self.conv_block(x)
 
+    def half(self, x, part: str):
+        """Part ``a`` (first conv [+BN] + ReLU) or ``b`` (the second) -- a pipeline cut between the two."""
+        n = len(self.conv_block) // 2
+        return self.conv_block[:n](x) if part == "a" else self.conv_block[n:](x)
+
 
 class Encoder(nn.Module):
     def __init__(self, cfg: UNetConfig):
@@ -155,10 +160,11 @@ class Decoder(nn.Module):
     def ups(self) -> List[nn.Module]:
         return [getattr(self, f"deconv{i + 1}") for i in range(self.depth)]
 
-    def level(self, i: int, x, skip):
+    def level(self, i: int, x, skip, part: str = "full"):
         out = self.ups()[i](x)
         skip = center_crop(skip, out.shape[2], out.shape[3])
-        return self.blocks()[i](torch.cat((skip, out), dim=1))
+        cat = torch.cat((skip, out), dim=1)
+        return self.blocks()[i](cat) if part == "full" else self.blocks()[i].half(cat, "a")
 
     def forward(self, x, *skips):
         for i, skip in enumerate(skips):

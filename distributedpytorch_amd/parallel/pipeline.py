@@ -31,7 +31,7 @@ import torch
 import torch.distributed as dist
 
 from ..compute import loss_from_partials, make_blocks
-from ..models.blocks import boundary_names, block_kind, n_blocks, partition, run_segment, skip_name
+from ..models.blocks import boundary_names, block_kind, n_blocks, partition, run_segment, segment_units, skip_name
 from ..optim import FlatParameterSpace
 from ..utils.tracing import trace_range
 
@@ -55,35 +55,53 @@ def _block_param_prefixes(idx: int, depth: int) -> List[str]:
     return ["segmap."]
 
 
-def stage_param_names(model, start: int, end: int) -> List[str]:
+def _unit_param_prefixes(model, idx: int, part: str) -> List[str]:
+    """Parameter-name prefixes of block ``idx`` or of one of its halves (``a``: the first conv [+BN],
+    and the transposed conv of a decoder block; ``b``: the second conv [+BN])."""
     depth = model.cfg.depth
-    prefixes = [p for idx in range(start, end) for p in _block_param_prefixes(idx, depth)]
+    prefixes = _block_param_prefixes(idx, depth)
+    if part == "full":
+        return prefixes
+    kind, i = block_kind(idx, depth)
+    blk = {"enc": lambda: model.encoder.blocks()[i], "mid": lambda: model.mid,
+           "dec": lambda: model.decoder.blocks()[i]}[kind]()
+    n = len(blk.conv_block) // 2
+    layers = range(n) if part == "a" else range(n, 2 * n)
+    out = [f"{prefixes[0]}conv_block.{k}." for k in layers]
+    if kind == "dec" and part == "a":
+        out.append(prefixes[1])              # decoder.deconv{i+1}.
+    return out
+
+
+def _segment_prefixes(model, start: float, end: float) -> List[str]:
+    return [p for idx, part in segment_units(start, end, model.cfg.depth) for p in _unit_param_prefixes(model, idx, part)]
+
+
+def stage_param_names(model, start: float, end: float) -> List[str]:
+    prefixes = _segment_prefixes(model, start, end)
     return [n for n, _ in model.named_parameters() if any(n.startswith(p) for p in prefixes)]
 
 
-def stage_buffer_names(model, start: int, end: int) -> List[str]:
+def stage_buffer_names(model, start: float, end: float) -> List[str]:
     """Buffers (BatchNorm running statistics) of the blocks in ``[start, end)``."""
-    depth = model.cfg.depth
-    prefixes = [p for idx in range(start, end) for p in _block_param_prefixes(idx, depth)]
+    prefixes = _segment_prefixes(model, start, end)
     return [n for n, _ in model.named_buffers() if any(n.startswith(p) for p in prefixes)]
 
 
-def _tensor_producer(name: str, cut_start: int, cuts: Sequence[int], depth: int) -> int:
+def _tensor_producer(name: str, cut_start: float, cuts: Sequence[float], depth: int) -> int:
     """Stage that produces boundary tensor ``name`` entering the stage starting at ``cut_start``."""
     if name == "x":
-        return cuts.index(cut_start) - 1
+        return list(cuts).index(cut_start) - 1
     lvl = int(name[len("skip"):])
-    for s in range(len(cuts) - 1):
-        if cuts[s] <= lvl < cuts[s + 1]:
-            return s
-    raise ValueError(name)
+    return _stage_of_block(lvl + 0.5, cuts)      # a skip is produced by its encoder block's part b
 
 
-def _stage_of_block(idx: int, cuts: Sequence[int]) -> int:
+def _stage_of_block(pos: float, cuts: Sequence[float]) -> int:
+    """Stage whose segment contains position ``pos`` (a block index, or ``b + 0.5`` for part b)."""
     for s in range(len(cuts) - 1):
-        if cuts[s] <= idx < cuts[s + 1]:
+        if cuts[s] <= pos < cuts[s + 1]:
             return s
-    raise ValueError(idx)
+    raise ValueError(pos)
 
 
 def stage_io(cuts: Sequence[int], depth: int):
@@ -96,8 +114,8 @@ def stage_io(cuts: Sequence[int], depth: int):
         recv[s].append(("x", s - 1))
         send[s - 1].append(("x", s))
     for lvl in range(depth):
-        p = _stage_of_block(lvl, cuts)
-        c = _stage_of_block(depth + 1 + (depth - 1 - lvl), cuts)
+        p = _stage_of_block(lvl + 0.5, cuts)                      # produced by part b of enc block lvl
+        c = _stage_of_block(depth + 1 + (depth - 1 - lvl), cuts)  # consumed by part a of its decoder block
         if p != c:
             recv[c].append((skip_name(lvl), p))
             send[p].append((skip_name(lvl), c))
@@ -233,8 +251,14 @@ class GPipeDist:
             return infer_shapes(cfg, mb, h, w)[name]
         # "x" entering block `cut`: encoder levels floor-halve, the decoder doubles from the bottom
         cut = self.start
-        kind, i = block_kind(cut, self.depth)
+        kind, i = block_kind(int(cut), self.depth)
         hb, wb = h >> self.depth, w >> self.depth
+        if cut != int(cut):          # a cut inside a DoubleConv: x is its first conv's output
+            if kind == "enc":
+                return (mb, cfg.widths[i], h >> i, w >> i)
+            if kind == "mid":
+                return (mb, cfg.mid_width, hb, wb)
+            return (mb, cfg.widths[self.depth - 1 - i], hb << (i + 1), wb << (i + 1))
         if kind == "enc":
             return (mb, cfg.widths[i - 1], h >> i, w >> i)
         if kind == "mid":

@@ -119,6 +119,55 @@ def boundary_bytes(depth: int, widths: Sequence[int], mid_width: int, mb: int, h
     return out
 
 
+def unit_boundary_bytes(depth: int, widths: Sequence[int], mid_width: int, mb: int, h: int, w: int,
+                        dtype_bytes: int = 2) -> Dict[str, Tuple[int, int, int]]:
+    """:func:`boundary_bytes` in half-block UNIT space (unit 2b = part a of block b, 2b+1 = part b, the
+    head is the last unit): x leaves a block from its part b and enters the next block's part a, a skip
+    leaves its encoder block's part b and enters its decoder block's part a, and inside every block the
+    first conv's output goes from part a to part b."""
+    nb = 2 * depth + 2
+    out = {}
+    for name, (p, c, nbytes) in boundary_bytes(depth, widths, mid_width, mb, h, w, dtype_bytes).items():
+        out[name] = (2 * p + 1, 2 * c, nbytes)
+    H, W = h, w
+    for lvl, wd in enumerate(widths):                       # encoder first-conv outputs
+        out[f"a{lvl}"] = (2 * lvl, 2 * lvl + 1, mb * wd * H * W * dtype_bytes)
+        H, W = H // 2, W // 2
+    out[f"a{depth}"] = (2 * depth, 2 * depth + 1, mb * mid_width * H * W * dtype_bytes)
+    for i, wd in enumerate(reversed(widths)):               # decoder first-conv outputs
+        H, W = H * 2, W * 2
+        b = depth + 1 + i
+        out[f"a{b}"] = (2 * b, 2 * b + 1, mb * wd * H * W * dtype_bytes)
+    assert all(c <= 2 * (nb - 1) for _, c, _ in out.values())
+    return out
+
+
+def unit_table(table: dict) -> dict:
+    """The half-block UNIT view of a block-time table (``per_mb[..]["units"]``, tools/block_times.py):
+    every block but the head becomes two units (part a / part b of its DoubleConv), so partitions may
+    cut between the two convs.  Cuts found on it are unit indices; :func:`plan` reports them as block
+    positions (unit u -> u / 2: ``b + 0.5`` = inside block b)."""
+    t = dict(table)
+    t["per_mb"] = {mb: row["units"] for mb, row in table["per_mb"].items() if "units" in row}
+    if not t["per_mb"]:
+        raise ValueError("table has no half-block unit times (tools/block_times.py round 4+)")
+    nbk = len(next(iter(table["per_mb"].values()))["fwd"])
+    opt = table.get("opt_ms", [0.0] * nbk)
+    t["opt_ms"] = [v / 2 for v in opt[:-1] for _ in (0, 1)] + [opt[-1]]
+    t["unit_space"] = True
+    t["block_table"] = table            # the single-GPU step (efficiency basis) stays the whole-block one
+    return t
+
+
+def block_to_unit(pos: float, nblocks: int) -> int:
+    """Cut position in blocks (``b + 0.5`` = inside block b; ``nblocks`` = the end) -> unit index."""
+    return 2 * nblocks - 1 if pos == nblocks else int(round(2 * pos))
+
+
+def unit_to_block(u: int, nblocks: int):
+    return nblocks if u == 2 * nblocks - 1 else (u // 2 if u % 2 == 0 else u / 2)
+
+
 def stage_costs(table: dict, mb: int, M: int, cuts: Sequence[int], link_gbs: float = 100.0,
                 link_latency_ms: float = 0.015, defer: bool = True) -> List[StageCost]:
     """Stage costs of partition ``cuts`` at microbatch ``mb`` (M microbatches) from a block time table.
@@ -147,7 +196,8 @@ def stage_costs(table: dict, mb: int, M: int, cuts: Sequence[int], link_gbs: flo
             wg = 0.0
         opt = sum(table.get("opt_ms", [0.0] * len(row["fwd"]))[i] for i in blocks)
         costs.append(StageCost(f, b, max(wg, 0.0), opt))
-    for name, (pb, cb, nbytes) in boundary_bytes(depth, widths, mid_width, mb, h, w).items():
+    bfun = unit_boundary_bytes if table.get("unit_space") else boundary_bytes
+    for name, (pb, cb, nbytes) in bfun(depth, widths, mid_width, mb, h, w).items():
         if pb >= len(table["per_mb"][str(mb)]["fwd"]) or cb >= len(table["per_mb"][str(mb)]["fwd"]):
             continue
         ps, cs = _stage_of(pb, cuts), _stage_of(cb, cuts)
@@ -162,6 +212,8 @@ def stage_costs(table: dict, mb: int, M: int, cuts: Sequence[int], link_gbs: flo
 
 def single_device_ms(table: dict, batch: int) -> Optional[float]:
     """Measured single-stage step of the whole batch (sum of blocks + optimizer), if the table has it."""
+    if "block_table" in table:
+        table = table["block_table"]
     row = table["per_mb"].get(str(batch))
     if row is None:
         return None
@@ -189,12 +241,17 @@ def plan(table: dict, S: int, batch: int, cuts: Optional[Sequence[int]] = None, 
     partition, its simulated step, img/s and efficiency against the measured single-stage step."""
     out = []
     t1 = single_device_ms(table, batch)
+    units = bool(table.get("unit_space"))
+    nbk = len(next(iter(table["block_table"]["per_mb"].values()))["fwd"]) if units else None
     for M in sorted({batch // int(k) for k in table["per_mb"] if batch % int(k) == 0 and batch // int(k) >= 1}):
         mb = batch // M
         if cuts is None:
             c, tl = best_partition(table, S, mb, M, **kw)
         else:
-            c, tl = list(cuts), simulate(stage_costs(table, mb, M, cuts, **kw), M)
+            uc = [block_to_unit(p, nbk) for p in cuts] if units else list(cuts)
+            c, tl = list(cuts), simulate(stage_costs(table, mb, M, uc, **kw), M)
+        if units and cuts is None:
+            c = [unit_to_block(u, nbk) for u in c]          # unit index -> block position (b + 0.5: inside block b)
         r = {"stages": S, "microbatches": M, "mb": mb, "cuts": c, "step_ms": round(tl.step_ms, 3),
              "img_s": round(batch * 1000.0 / tl.step_ms, 1), "utilisation": round(tl.efficiency(), 3)}
         if t1 is not None:
@@ -228,8 +285,9 @@ def load_plan(model: str, h: int, w: int, stages: int, batch: int, path: str = N
     p = plans.get(plan_key(model, h, w, stages, batch))
     if p is None:
         return None
-    cuts = [int(c) for c in p["cuts"]]
+    cuts = [int(c) if float(c) == int(c) else float(c) for c in p["cuts"]]     # b + 0.5: a cut inside block b
     M = int(p["microbatches"])
-    if len(cuts) != stages + 1 or cuts[0] != 0 or any(b <= a for a, b in zip(cuts, cuts[1:])) or batch % M:
+    if (len(cuts) != stages + 1 or cuts[0] != 0 or any(b <= a for a, b in zip(cuts, cuts[1:])) or batch % M
+            or any(c * 2 != int(c * 2) for c in cuts)):
         raise ValueError(f"malformed pipeline plan {plan_key(model, h, w, stages, batch)}: {p}")
     return dict(p, cuts=cuts, microbatches=M)

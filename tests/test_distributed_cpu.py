@@ -113,14 +113,16 @@ def test_ddp_gloo_ranks(world, bucket_mb, comm, overlap):
             assert nb > 3 and in_bwd >= nb - 1
 
 
-def _pipe_worker(rank, world, port, microbatches, mode, q):
+def _pipe_worker(rank, world, port, microbatches, mode, q, model_name="unet-tiny"):
     _init(rank, world, port)
     from distributedpytorch_amd.parallel.pipeline import GPipeDist
     torch.manual_seed(0)
-    model = build_model("unet-tiny")
-    ref = build_model("unet-tiny")
+    model = build_model(model_name)
+    ref = build_model(model_name)
     ref.load_state_dict(model.state_dict())
-    pipe = GPipeDist(model, microbatches, backend="torch", dtype="fp32", img_hw=(32, 32), mode=mode)
+    cuts = list(mode) if isinstance(mode, (list, tuple)) else None
+    pipe = GPipeDist(model, microbatches, backend="torch", dtype="fp32", img_hw=(32, 32),
+                     mode="balanced" if cuts else mode, cuts=cuts)
     x, t = _data(4, seed=5)
     loss = pipe.train_step(x if pipe.is_first else None, t if pipe.is_last else None, 4, (32, 32))
     lref = bce_dice_from_probs(ref(x), t)
@@ -141,17 +143,26 @@ def _pipe_worker(rank, world, port, microbatches, mode, q):
     sd = pipe.gather_state_dict()
     sd_ok = True
     if rank == 0:
-        sd_ok = set(sd) == set(ref.state_dict()) and all(torch.equal(sd[k], v) for k, v in ref.state_dict().items())
+        # (BatchNorm running statistics: the reference model ran one more train-mode forward above)
+        sd_ok = set(sd) == set(ref.state_dict()) and all(torch.equal(sd[k], v) for k, v in ref.state_dict().items()
+                                                         if "running_" not in k and "num_batches" not in k)
     q.put((rank, None if loss is None else float(loss), float(lref), bad, nown, probs_ok, sd_ok))
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,mb,mode", [(2, 2, "reference"), (3, 4, "balanced")])
-def test_gpipe_gloo_matches_single_process(world, mb, mode):
+# cuts inside DoubleConv blocks (x.5: a stage boundary between a block's two convs): unet-tiny is
+# enc0 enc1 mid dec0 dec1 head; [0, 1.5, 3.5, 6] splits enc1 and dec0, [0, .5, 2.5, 4.5, 6] the first
+# encoder block, the bottleneck and the last decoder block; unet-tiny-bn adds BatchNorm + bilinear ups
+# (one microbatch: BatchNorm statistics over a microbatch are not the full batch's)
+@pytest.mark.parametrize("world,mb,mode,model_name", [(2, 2, "reference", "unet-tiny"), (3, 4, "balanced", "unet-tiny"),
+                                                      (3, 2, (0, 1.5, 3.5, 6), "unet-tiny"),
+                                                      (4, 2, (0, 0.5, 2.5, 4.5, 6), "unet-tiny"),
+                                                      (3, 1, (0, 1.5, 3.5, 6), "unet-tiny-bn")])
+def test_gpipe_gloo_matches_single_process(world, mb, mode, model_name):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_pipe_worker, args=(r, world, port, mb, mode, q)) for r in range(world)]
+    procs = [ctx.Process(target=_pipe_worker, args=(r, world, port, mb, mode, q, model_name)) for r in range(world)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=240) for _ in procs])
@@ -164,7 +175,7 @@ def test_gpipe_gloo_matches_single_process(world, mb, mode):
         assert probs_ok and sd_ok
         if rank == world - 1:
             assert abs(loss - lref) < 1e-5
-    assert total_own == len(build_model("unet-tiny").state_dict())   # each parameter owned by one stage
+    assert total_own == len(list(build_model(model_name).parameters()))   # each parameter owned by one stage
 
 
 def _ddp_bn_worker(rank, world, port, q):

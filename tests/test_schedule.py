@@ -122,3 +122,28 @@ def test_shipped_plans_are_well_formed():
         h, w = map(int, hw.split("x"))
         p = sch.load_plan(model, h, w, int(S), int(batch))
         assert p["cuts"][-1] == n_blocks(PRESETS[model].depth)
+
+
+def test_unit_space_cuts_inside_doubleconv():
+    """Half-block units: unit 2b / 2b+1 = part a / b of block b, the head the last unit; a partition
+    found on units is reported in block positions (b + 0.5 = a cut between block b's convs) and
+    evaluates to the same step when passed back as cuts; the boundary tensors follow the parts."""
+    from distributedpytorch_amd.parallel.schedule import (block_to_unit, unit_boundary_bytes, unit_table,
+                                                          unit_to_block)
+    nb = 6
+    for p in (0, 0.5, 1, 2.5, 5, 6):
+        assert unit_to_block(block_to_unit(p, nb), nb) == p
+    b = unit_boundary_bytes(2, [8, 16], 32, 1, 32, 32)
+    assert b["skip0"] == (1, 8, 8 * 32 * 32 * 2)          # enc0 part b -> dec1 (block 4) part a
+    assert b["x2"] == (5, 6, 32 * 8 * 8 * 2)               # mid part b -> dec0 part a
+    assert b["a2"] == (4, 5, 32 * 8 * 8 * 2)               # mid's first conv output
+    assert b["a4"] == (8, 9, 8 * 32 * 32 * 2)              # dec1's first conv output (full resolution)
+    t = _table()
+    for row in t["per_mb"].values():
+        row["units"] = {k: [v / 2 for v in row[k][:-1] for _ in (0, 1)] + [row[k][-1]] for k in ("fwd", "bwd", "bwd_nowgrad")}
+    ut = unit_table(t)
+    best = max(plan(ut, 2, 4, link_gbs=1e9), key=lambda r: r["img_s"])
+    again = plan(ut, 2, 4, cuts=best["cuts"], link_gbs=1e9)
+    assert [r["step_ms"] for r in again if r["microbatches"] == best["microbatches"]] == [best["step_ms"]]
+    whole = max(plan(t, 2, 4, link_gbs=1e9), key=lambda r: r["img_s"])
+    assert best["step_ms"] <= whole["step_ms"] + 1e-9     # finer cuts can only help the balance

@@ -8,7 +8,9 @@ backward it fuses) is run in isolation on copies of those inputs: forward, backw
 output gradients, and backward with the side-stream weight-gradient kernels skipped (timing
 ablation: the deferrable part of the backward is bwd - bwd_nowgrad).  Medians over --reps runs,
 CUDA events around each call.  The optimizer step (fused Adam over the flat buffer) is timed once
-and split over the blocks by parameter count.
+and split over the blocks by parameter count.  Every block except the head is also timed as its two
+halves (``units``: part a / part b of a DoubleConv cut between its convs, models/blocks.py) -- the
+conv-level stage boundaries of parallel/schedule.py.
 
     python tools/block_times.py --model unet --img 512 --mbs 8 16 32 64 128 256 --out profiles/block_times_unet_512_r04.json
 """
@@ -90,6 +92,7 @@ def main():
                     ins[idx] = {"x": env["x"], "skip": env[nm]}
                     env["x"] = B.dec(i, env["x"], env[nm])
         fwd, bwd, bwd_nw = [], [], []
+        ufwd, ubwd, ubwd_nw = [], [], []          # per half-block unit: (b, a), (b, b) for b < nb - 1, then head
         for idx in range(nb):
             kind, i = block_kind(idx, depth)
             if kind == "head":
@@ -141,7 +144,59 @@ def main():
                 K.set_timing_ablation(())
             print(f"mb {mb:4d} {table['blocks'][idx]:6s} fwd {fwd[-1]:8.3f} bwd {bwd[-1]:8.3f} "
                   f"bwd-wgrad {bwd_nw[-1]:8.3f} ms", flush=True)
-        table["per_mb"][str(mb)] = {"fwd": fwd, "bwd": bwd, "bwd_nowgrad": bwd_nw}
+            # the block's two halves (a pipeline cut between its convs, models/blocks.py): part a from the
+            # block input, part b from part a's output
+            with torch.no_grad():
+                if kind == "enc":
+                    a_out = B.enc_a(i, inp["x"])
+                elif kind == "mid":
+                    a_out = B.mid_a(inp["x"])
+                else:
+                    sk = inp["skip"]
+                    B._cats[sk.data_ptr()] = sk._base if sk._base is not None else sk
+                    a_out = B.dec_a(i, inp["x"], sk)
+            for part in ("a", "b"):
+                def run_part():
+                    if part == "b":
+                        xin = leaf(a_out)
+                        if kind == "enc":
+                            return B.enc_b(i, xin)
+                        return ((B.mid_b if kind == "mid" else (lambda v: B.dec_b(i, v)))(xin),)
+                    xin = leaf(inp["x"]) if idx > 0 else inp["x"]
+                    if kind == "enc":
+                        return (B.enc_a(i, xin),)
+                    if kind == "mid":
+                        return (B.mid_a(xin),)
+                    sk = inp["skip"]
+                    B._cats[sk.data_ptr()] = sk._base if sk._base is not None else sk
+                    return (B.dec_a(i, xin, leaf(sk)),)
+
+                def back_part(reps):
+                    ts = []
+                    for _ in range(reps):
+                        o = run_part()
+                        s_, e_ = ev(), ev()
+                        s_.record()
+                        torch.autograd.backward(o, [torch.randn_like(v) * 1e-3 for v in o])
+                        e_.record()
+                        torch.cuda.synchronize()
+                        ts.append(s_.elapsed_time(e_))
+                    ts.sort()
+                    return ts[len(ts) // 2]
+
+                ufwd.append(timed(lambda: run_part(), a.reps))
+                ubwd.append(back_part(a.reps))
+                K.set_timing_ablation({"wgrad"})
+                try:
+                    ubwd_nw.append(back_part(a.reps))
+                finally:
+                    K.set_timing_ablation(())
+                print(f"mb {mb:4d} {table['blocks'][idx]:6s}.{part} fwd {ufwd[-1]:8.3f} bwd {ubwd[-1]:8.3f} "
+                      f"bwd-wgrad {ubwd_nw[-1]:8.3f} ms", flush=True)
+            del a_out
+        ufwd.append(0.0), ubwd.append(0.0), ubwd_nw.append(0.0)     # the head unit (fused into the last block)
+        table["per_mb"][str(mb)] = {"fwd": fwd, "bwd": bwd, "bwd_nowgrad": bwd_nw,
+                                    "units": {"fwd": ufwd, "bwd": ubwd, "bwd_nowgrad": ubwd_nw}}
         del ins, env, x, m, t
         torch.cuda.empty_cache()
     # optimizer step, split over the blocks by parameter count

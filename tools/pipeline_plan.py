@@ -20,7 +20,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from distributedpytorch_amd.models.blocks import partition          # noqa: E402
 from distributedpytorch_amd.models.unet import PRESETS              # noqa: E402
-from distributedpytorch_amd.parallel.schedule import load_table, plan, single_device_ms  # noqa: E402
+from distributedpytorch_amd.parallel.schedule import load_table, plan, single_device_ms, unit_table  # noqa: E402
 
 
 def rows_for(table, S, batch, cuts, label, **kw):
@@ -60,13 +60,16 @@ def main():
                 allr += rows_for(t, S, batch, ref, "reference", **kw)
             allr += rows_for(t, S, batch, flop, "flop-balanced", **kw)
             allr += rows_for(t, S, batch, None, "time-balanced", **kw)
-            lines.append(f"{'partition':14s} {'M':>3s} {'mb':>4s} {'cuts':28s} {'step ms':>9s} {'img/s':>8s} "
+            if any("units" in row for row in t["per_mb"].values()):
+                # conv-level stage boundaries: cuts between the two convs of a DoubleConv (b + 0.5)
+                allr += rows_for(unit_table(t), S, batch, None, "time+conv-cut", **kw)
+            lines.append(f"{'partition':14s} {'M':>3s} {'mb':>4s} {'cuts':40s} {'step ms':>9s} {'img/s':>8s} "
                          f"{'util':>6s} {'eff':>6s}")
             for r in allr:
-                lines.append(f"{r['partition']:14s} {r['microbatches']:3d} {r['mb']:4d} {str(r['cuts']):28s} "
+                lines.append(f"{r['partition']:14s} {r['microbatches']:3d} {r['mb']:4d} {str(r['cuts']):40s} "
                              f"{r['step_ms']:9.2f} {r['img_s']:8.1f} {r['utilisation']:6.3f} "
                              f"{r.get('scaling_efficiency', float('nan')):6.3f}")
-            best = max((r for r in allr if r["partition"] == "time-balanced"), key=lambda r: r["img_s"])
+            best = max((r for r in allr if r["partition"] in ("time-balanced", "time+conv-cut")), key=lambda r: r["img_s"])
             lines.append(f"-> chosen: {best['partition']} cut {best['cuts']}, {best['microbatches']} microbatches "
                          f"({best['img_s']} img/s predicted)")
             lines.append("")
