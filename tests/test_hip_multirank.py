@@ -166,7 +166,9 @@ def _pipe_worker(rank, world, port, name, hw, M, cut, q):
         ref_sd = {k: v.detach().cpu() for k, v in ref.state_dict().items()}
         del sd
         model = model.cuda()
-        pipe = GPipeDist(model, M, backend="hip", dtype="bf16", img_hw=(hw, hw), mode=cut)
+        cuts = list(cut) if isinstance(cut, (list, tuple)) else None
+        pipe = GPipeDist(model, M, backend="hip", dtype="bf16", img_hw=(hw, hw), mode="balanced" if cuts else cut,
+                         cuts=cuts)
         pipe.space.zero_grad()
         loss = pipe.train_step(x if pipe.is_first else None, t if pipe.is_last else None, B, (hw, hw),
                                loss_scale=float(B))
@@ -197,7 +199,9 @@ def _pipe_worker(rank, world, port, name, hw, M, cut, q):
 @pytest.mark.timeout(420)
 @pytest.mark.parametrize("name,hw,world,M,cut", [("unet", 64, 2, 2, "reference"),
                                                  ("unet", 64, 4, 4, "balanced"),
-                                                 ("unet-xl", 64, 8, 4, "balanced")])
+                                                 ("unet-xl", 64, 8, 4, "balanced"),
+                                                 # stage boundaries inside DoubleConvs (half-block cuts)
+                                                 ("unet", 64, 4, 2, (0, 2.5, 5, 7.5, 10))])
 def test_gpipe_hip_matches_single_device(hip_lib, name, hw, world, M, cut):
     from distributedpytorch_amd.models.unet import build_model
     res = _run(_pipe_worker, world, name, hw, M, cut, timeout=360)

@@ -14,7 +14,7 @@ def _cos(a, b):
 
 
 @pytest.mark.parametrize("dtype,cuts,model_name", [("bf16", (0, 2.5, 7.5, 10), "unet"),
-                                                   ("bf16", (0, 0.5, 4.5, 9.5, 10), "unet"),
+                                                   ("bf16", (0, 0.5, 4.5, 8.5, 10), "unet"),
                                                    ("bf16", (0, 1.5, 5.5, 10), "unet-bn"),
                                                    ("fp32", (0, 0.5, 4.5, 8.5, 10), "unet")])
 def test_half_block_cuts_match_whole_blocks(hip_lib, dtype, cuts, model_name):
