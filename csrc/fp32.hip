@@ -52,8 +52,14 @@ namespace {
 
 constexpr int F_BK = 16;             // K-step: 16 floats = 4 float4 chunks per LDS row (64 B)
 
-// conflict-free ds_read_b128 of 16 consecutive rows at one chunk: rows r and r + 4 land 4 dwords apart
+// conflict-free ds_read_b128 of 16 consecutive rows at one chunk: 64-B rows (4 chunks) rotate the
+// chunk every 4 rows, 128-B rows (8 chunks) every 2 rows -- 16 distinct 16-B bank groups either way
 __device__ __forceinline__ int fswz(int row, int chunk) { return chunk ^ ((row >> 2) & 3); }
+template <int CPR>
+__device__ __forceinline__ int fswzk(int row, int chunk) {
+  if constexpr (CPR == 4) return chunk ^ ((row >> 2) & 3);
+  else return chunk ^ ((row >> 1) & 7);
+}
 
 __device__ __forceinline__ f32x4_t mfma4(const f32x4v& a, const f32x4v& b, f32x4_t c) {
   c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0], b[0], c, 0, 0, 0);
@@ -65,13 +71,15 @@ __device__ __forceinline__ f32x4_t mfma4(const f32x4v& a, const f32x4v& b, f32x4
 
 }  // namespace
 
-// BP pixels x BC channels per block, 4 waves (NWP along the pixels x NWC along the channels)
-template <int BP, int BC, int NWP>
+// BP pixels x BC channels per block, BK-deep K-steps, 4 waves (NWP along the pixels x NWC along the channels)
+template <int BP, int BC, int NWP, int BK>
 __global__ __launch_bounds__(256) void igemm_f32_kernel(F32ConvArgs a) {
   constexpr int NWC = 4 / NWP, WP = BP / NWP, WC = BC / NWC, TP = WP / 16, TC = WC / 16;
-  static_assert(NWP * NWC == 4 && TP >= 1 && TC >= 1, "tile");
-  constexpr int RB = F_BK * 4;                       // LDS row bytes
-  constexpr int LP = BP * 4 / 256, LW = (BC * 4 + 255) / 256;
+  static_assert(NWP * NWC == 4 && TP >= 1 && TC >= 1 && (BK == 16 || BK == 32), "tile");
+  constexpr int CPR = BK / 4, RPP = 256 / CPR;       // float4 chunks per LDS row, rows per loader pass
+  constexpr int RB = BK * 4;                         // LDS row bytes
+  constexpr int LP = BP / RPP, LW = (BC + RPP - 1) / RPP;
+  static_assert(BP % RPP == 0, "loader tiling");
   __shared__ __attribute__((aligned(16))) char lds[2][(BP + BC) * RB];
 
   const int M = a.N * a.Ho * a.Wo;
@@ -81,7 +89,7 @@ __global__ __launch_bounds__(256) void igemm_f32_kernel(F32ConvArgs a) {
   const int m0 = pt * BP, c0 = ct * BC;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wp = wid / NWC, wc = wid - wp * NWC;
-  const int lchunk = tid & 3, lrow = tid >> 2;     // 64 rows x 4 chunks per pass
+  const int lchunk = tid % CPR, lrow = tid / CPR;  // RPP rows x CPR chunks per pass
   const int taps = a.KH * a.KW;
 
   // per pixel row: (n, h0, w0) of tap (0, 0) and the in-image taps
@@ -89,7 +97,7 @@ __global__ __launch_bounds__(256) void igemm_f32_kernel(F32ConvArgs a) {
   unsigned tmask[LP];
 #pragma unroll
   for (int i = 0; i < LP; ++i) {
-    const int m = m0 + lrow + i * 64;
+    const int m = m0 + lrow + i * RPP;
     const bool ok = m < M;
     const int mm = ok ? m : 0;
     const int hw = a.Ho * a.Wo;
@@ -106,10 +114,10 @@ __global__ __launch_bounds__(256) void igemm_f32_kernel(F32ConvArgs a) {
     }
     tmask[i] = msk;
   }
-  const int S = a.Kpad / F_BK;
+  const int S = a.Kpad / BK;
   f32x4v pr[LP], wr[LW];
   auto gload = [&](int s) {
-    const int k0 = s * F_BK + lchunk * 4;
+    const int k0 = s * BK + lchunk * 4;
     const int tap = k0 / a.Cs, ci = k0 - tap * a.Cs;
     const int kh = tap / a.KW, kw = tap - kh * a.KW;
 #pragma unroll
@@ -123,8 +131,8 @@ __global__ __launch_bounds__(256) void igemm_f32_kernel(F32ConvArgs a) {
     }
 #pragma unroll
     for (int i = 0; i < LW; ++i) {
-      const int r = lrow + i * 64;
-      if (r < BC) wr[i] = *reinterpret_cast<const f32x4v*>(a.w + (long)(c0 + r) * a.Kpad + s * F_BK + lchunk * 4);
+      const int r = lrow + i * RPP;
+      if (r < BC) wr[i] = *reinterpret_cast<const f32x4v*>(a.w + (long)(c0 + r) * a.Kpad + s * BK + lchunk * 4);
     }
   };
   auto lstore = [&](int buf) {
@@ -132,13 +140,13 @@ __global__ __launch_bounds__(256) void igemm_f32_kernel(F32ConvArgs a) {
     char* Wt = lds[buf] + BP * RB;
 #pragma unroll
     for (int i = 0; i < LP; ++i) {
-      const int r = lrow + i * 64;
-      *reinterpret_cast<f32x4v*>(P + r * RB + fswz(r, lchunk) * 16) = pr[i];
+      const int r = lrow + i * RPP;
+      *reinterpret_cast<f32x4v*>(P + r * RB + fswzk<CPR>(r, lchunk) * 16) = pr[i];
     }
 #pragma unroll
     for (int i = 0; i < LW; ++i) {
-      const int r = lrow + i * 64;
-      if (r < BC) *reinterpret_cast<f32x4v*>(Wt + r * RB + fswz(r, lchunk) * 16) = wr[i];
+      const int r = lrow + i * RPP;
+      if (r < BC) *reinterpret_cast<f32x4v*>(Wt + r * RB + fswzk<CPR>(r, lchunk) * 16) = wr[i];
     }
   };
 
@@ -156,21 +164,25 @@ __global__ __launch_bounds__(256) void igemm_f32_kernel(F32ConvArgs a) {
     if (s + 1 < S) gload(s + 1);
     const char* P = lds[buf];
     const char* Wt = lds[buf] + BP * RB;
-    f32x4v af[TC], bfr[TP];
 #pragma unroll
-    for (int ic = 0; ic < TC; ++ic) {
-      const int row = wc * WC + ic * 16 + (lane & 15);
-      af[ic] = *reinterpret_cast<const f32x4v*>(Wt + row * RB + fswz(row, q) * 16);
+    for (int kk = 0; kk < BK / 16; ++kk) {
+      const int ch = kk * 4 + q;
+      f32x4v af[TC], bfr[TP];
+#pragma unroll
+      for (int ic = 0; ic < TC; ++ic) {
+        const int row = wc * WC + ic * 16 + (lane & 15);
+        af[ic] = *reinterpret_cast<const f32x4v*>(Wt + row * RB + fswzk<CPR>(row, ch) * 16);
+      }
+#pragma unroll
+      for (int ip = 0; ip < TP; ++ip) {
+        const int row = wp * WP + ip * 16 + (lane & 15);
+        bfr[ip] = *reinterpret_cast<const f32x4v*>(P + row * RB + fswzk<CPR>(row, ch) * 16);
+      }
+#pragma unroll
+      for (int ic = 0; ic < TC; ++ic)
+#pragma unroll
+        for (int ip = 0; ip < TP; ++ip) acc[ic][ip] = mfma4(af[ic], bfr[ip], acc[ic][ip]);
     }
-#pragma unroll
-    for (int ip = 0; ip < TP; ++ip) {
-      const int row = wp * WP + ip * 16 + (lane & 15);
-      bfr[ip] = *reinterpret_cast<const f32x4v*>(P + row * RB + fswz(row, q) * 16);
-    }
-#pragma unroll
-    for (int ic = 0; ic < TC; ++ic)
-#pragma unroll
-      for (int ip = 0; ip < TP; ++ip) acc[ic][ip] = mfma4(af[ic], bfr[ip], acc[ic][ip]);
     if (s + 1 < S) lstore(buf ^ 1);
     __syncthreads();
   }
@@ -478,18 +490,22 @@ static unsigned egrid(long n) { return (unsigned)(n / 256 + 1 < 8192 ? n / 256 +
 
 // Eligible: Cs % 4 == 0 (a float4 chunk never straddles a tap), Kpad % 16 == 0, Kpad >= KH*KW*Cs,
 // Ngemm % 32 == 0, 16-B aligned strides; mode 1 also Cout % 4 == 0.
+// Tiles: Ngemm % 64 == 0 -> 128 px x 64 ch, else 128 x 32; 32-deep K-steps when Kpad % 32 == 0.
 DPA_API int dpa_igemm_f32(const F32ConvArgs* args, hipStream_t st) {
   const F32ConvArgs& a = *args;
   if ((a.Cs & 3) || (a.Kpad % F_BK) || a.Kpad < a.KH * a.KW * a.Cs || (a.Ngemm & 31) || (a.ldx & 3) || (a.ldy & 3) ||
       (a.mask && (a.ldm & 3)) || (a.mode == 1 && (a.Cout & 3)) || a.KH * a.KW > 32 || a.N < 1)
     return (int)hipErrorInvalidValue;
   const long M = (long)a.N * a.Ho * a.Wo;
+  const bool k32 = a.Kpad % 32 == 0;
   if (a.Ngemm % 64 == 0) {
-    const long grid = ((M + 63) / 64) * (a.Ngemm / 64);
-    hipLaunchKernelGGL((igemm_f32_kernel<64, 64, 2>), dim3((unsigned)grid), dim3(256), 0, st, a);
+    const dim3 grid((unsigned)(((M + 127) / 128) * (a.Ngemm / 64)));
+    if (k32) hipLaunchKernelGGL((igemm_f32_kernel<128, 64, 2, 32>), grid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((igemm_f32_kernel<128, 64, 2, 16>), grid, dim3(256), 0, st, a);
   } else {
-    const long grid = ((M + 63) / 64) * (a.Ngemm / 32);
-    hipLaunchKernelGGL((igemm_f32_kernel<64, 32, 4>), dim3((unsigned)grid), dim3(256), 0, st, a);
+    const dim3 grid((unsigned)(((M + 127) / 128) * (a.Ngemm / 32)));
+    if (k32) hipLaunchKernelGGL((igemm_f32_kernel<128, 32, 4, 32>), grid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((igemm_f32_kernel<128, 32, 4, 16>), grid, dim3(256), 0, st, a);
   }
   return (int)hipGetLastError();
 }

@@ -3,7 +3,7 @@
 set -o pipefail
 cd "$(dirname "$0")/.." && export TMPDIR=/tmp && mkdir -p gpurun_out/split
 O=gpurun_out/split
-timeout -k 10 600 python -u -m pytest -x -q --timeout 180 --timeout-method thread tests/test_split_blocks.py tests/test_hip_multirank.py tests/test_bwd_fused.py tests/test_hip_kernels.py tests/test_hip_model.py > $O/pytest.log 2>&1
+timeout -k 10 600 python -u -m pytest -x -q --timeout 180 --timeout-method thread tests/test_split_blocks.py tests/test_fp32_engine.py tests/test_hip_multirank.py tests/test_bwd_fused.py tests/test_hip_kernels.py tests/test_hip_model.py > $O/pytest.log 2>&1
 rc=$?; tail -2 $O/pytest.log; [ $rc -ne 0 ] && exit $rc
 for i in 1 2; do
   timeout -k 10 300 python bench.py > $O/bench_$i.log 2>&1 || { echo "bench failed"; tail -3 $O/bench_$i.log; exit 1; }
