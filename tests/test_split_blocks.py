@@ -44,7 +44,13 @@ def test_half_block_cuts_match_whole_blocks(hip_lib, dtype, cuts, model_name):
     torch.cuda.synchronize()
     tol = 1e-5 if dtype == "fp32" else 2e-3
     assert abs(loss.item() - loss_ref.item()) < tol * max(1.0, abs(loss_ref.item()))
+    gmax = max(float(g.norm()) for g in g_ref.values())
     for n, p in model.named_parameters():
         assert p.grad is not None, n
+        if float(g_ref[n].norm()) < 1e-4 * gmax:
+            # a conv bias in front of a BatchNorm: its true gradient is zero (BN removes it), both runs
+            # hold rounding noise -- compare magnitudes, not directions
+            assert float(p.grad.norm()) < 1e-3 * gmax, n
+            continue
         c = _cos(p.grad, g_ref[n])
         assert c > (0.99999 if dtype == "fp32" else 0.999), (n, c)
