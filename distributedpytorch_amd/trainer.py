@@ -508,6 +508,8 @@ def train(cfg: TrainConfig):
                                     scheduler=scheduler, epoch=epoch, step=step)
             log.warning(f"stopped by signal {stop_signal} at step {step}; state saved to {last_path}")
             break
+        if strat.device.type == "cuda":
+            torch.cuda.synchronize(strat.device)    # epoch time = work done, not work enqueued
         ep_time = time.perf_counter() - t_ep
         steady_ips = steady.finish()
         bar.close()

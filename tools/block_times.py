@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--mbs", type=int, nargs="+", default=[8, 16, 32, 64, 128, 256])
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--blocks", nargs="*", default=None, help="time only these blocks (e.g. dec4), for profiling")
     a = ap.parse_args()
 
     from distributedpytorch_amd.compute import make_blocks
@@ -97,6 +98,10 @@ def main():
             kind, i = block_kind(idx, depth)
             if kind == "head":
                 fwd.append(0.0), bwd.append(0.0), bwd_nw.append(0.0)
+                continue
+            if a.blocks and table["blocks"][idx] not in a.blocks:
+                fwd.append(0.0), bwd.append(0.0), bwd_nw.append(0.0)
+                ufwd.extend([0.0, 0.0]), ubwd.extend([0.0, 0.0]), ubwd_nw.extend([0.0, 0.0])
                 continue
             inp = ins[idx]
             last = idx == nb - 2
