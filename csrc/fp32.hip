@@ -44,17 +44,17 @@ struct F32WgradArgs {
   float* slab;          // [splits][T][M][Nc]
   float* bslab;         // [splits][M] (sum of A over the split's pixels) or null
   int lda, ldb, N, Hg, Wg, HB, WB, M, Nc, s, pad, KH, KW;
-  long pix_per_split;   // pixels per split (multiple of 16)
+  long pix_per_split;   // pixels per split (multiple of 32; halo form: of 64, in stage order)
   int splits;
+  int halo;             // 1: the 3x3 / s1 / p1 form with the B halo staged per 2 x 32-pixel stage
 };
 
 namespace {
 
-constexpr int F_BK = 16;             // K-step: 16 floats = 4 float4 chunks per LDS row (64 B)
+constexpr int F_BK = 16;             // K-step granularity of the implicit GEMM (Kpad % 16 == 0)
 
 // conflict-free ds_read_b128 of 16 consecutive rows at one chunk: 64-B rows (4 chunks) rotate the
 // chunk every 4 rows, 128-B rows (8 chunks) every 2 rows -- 16 distinct 16-B bank groups either way
-__device__ __forceinline__ int fswz(int row, int chunk) { return chunk ^ ((row >> 2) & 3); }
 template <int CPR>
 __device__ __forceinline__ int fswzk(int row, int chunk) {
   if constexpr (CPR == 4) return chunk ^ ((row >> 2) & 3);
@@ -230,97 +230,247 @@ __global__ __launch_bounds__(256) void igemm_f32_kernel(F32ConvArgs a) {
   }
 }
 
-// Weight gradient: 64 (A channels m) x 64 (columns tap * Nc + n) tile, K = 16 pixels per step; the
-// operands are K-strided in NHWC, so the loader transposes them into [row][16 px] LDS images.
+// Weight gradient: dW[m][col] = sum_p A[p][m] B'[p][col], col = tap * Nc + n, B'[p][col] = B at pixel p's tap
+// position.  BM (A channels) x 128 (columns) per block, 4 waves (2 x 2 of 64 x 64 for BM = 128, else 1 x 4),
+// K = 32 pixels per stage.  The operands land in LDS in their natural [pixel][channel] order (float4
+// stores, rows padded by 16 floats so the four K lane groups of an MFMA operand read hit four distinct
+// 16-bank groups) and feed the MFMA as scalar reads -- no transpose; the next stage's global loads are
+// in registers while the current one computes (one barrier per stage).  The bias gradient sum_p A[p][m]
+// rides along in the blocks of column tile 0.
+template <int BM>
 __global__ __launch_bounds__(256) void wgrad_f32_kernel(F32WgradArgs a) {
-  constexpr int RB = F_BK * 4;
-  __shared__ __attribute__((aligned(16))) float As[64 * F_BK], Bs[64 * F_BK];
-  __shared__ float bred[16][64];
+  constexpr int BN = 128, BK = 32, PADF = 16;
+  constexpr int NWM = BM == 128 ? 2 : 1, NWN = 4 / NWM, WM = BM / NWM, WN = BN / NWN, TM = WM / 16, TN = WN / 16;
+  constexpr int SA = BM + PADF, SB = BN + PADF;                 // LDS row strides (floats), one row per pixel
+  constexpr int CPA = BM / 4, RPA = 256 / CPA, LA = BK / RPA;   // A loader: chunks per pixel, rows per pass, loads
+  constexpr int CPB = BN / 4, RPB = 256 / CPB, LB = BK / RPB;
+  static_assert(LA >= 1 && LB >= 1 && TM >= 1 && TN >= 1, "tile");
+  __shared__ __attribute__((aligned(16))) float As[2][BK * SA];
+  __shared__ __attribute__((aligned(16))) float Bs[2][BK * SB];
+
   const int T = a.KH * a.KW, Ncols = T * a.Nc;
-  const int nmt = (a.M + 63) / 64, nnt = (Ncols + 63) / 64, tiles = nmt * nnt;
-  const int bid = blockIdx.x;
+  const int nmt = a.M / BM, nnt = (Ncols + BN - 1) / BN, tiles = nmt * nnt;
+  const int bid = xcd_remap(blockIdx.x, tiles * a.splits);     // a split's tiles (same pixels) share an XCD's L2
   const int split = bid / tiles, tile = bid - split * tiles;
-  const int mt = tile / nnt, nt = tile - mt * nnt;
-  const int m0 = mt * 64, n0 = nt * 64;
-  const long P = (long)a.N * a.Hg * a.Wg;
-  const long p0 = (long)split * a.pix_per_split;
-  const long p1 = p0 + a.pix_per_split < P ? p0 + a.pix_per_split : P;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wp = wid >> 1, wc = wid & 1;          // 2 x 2 waves of 32 x 32
-  const int lpx = tid >> 4, l4 = tid & 15;        // loader: pixel lpx of the step, chunk l4 of 16
-  // this thread's A chunk: channels m0 + 4 l4 ..; B chunk: column n0 + 4 l4 -> (tap, n)
-  const int am = m0 + 4 * l4;
-  const int bcol = n0 + 4 * l4;
-  const int btap = bcol / a.Nc, bn = bcol - btap * a.Nc;
+  const int nt = tile / nmt, mt = tile - nt * nmt;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int P = a.N * a.Hg * a.Wg, hw = a.Hg * a.Wg;
+  const int p0 = (int)((long)split * a.pix_per_split);
+  const int p1 = p0 + (int)a.pix_per_split < P ? p0 + (int)a.pix_per_split : P;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, q = lane >> 4, l16 = lane & 15;
+  const int wm = wid / NWN, wn = wid - wm * NWN;
+  // loader chunks (fixed per thread): A channels m0 + 4 ca, B column n0 + 4 cb -> (tap, n)
+  const int ca = tid % CPA, ra = tid / CPA;
+  const int cb = tid % CPB, rb = tid / CPB;
+  const int bcol = n0 + 4 * cb;
+  const bool bok = bcol < Ncols;
+  const int btap = bok ? bcol / a.Nc : 0, bn = bcol - btap * a.Nc;
   const int bkh = btap / a.KW, bkw = btap - bkh * a.KW;
-  const bool aok = am < a.M, bok = bcol < Ncols;
   const bool do_bias = a.bslab != nullptr && nt == 0;
   f32x4v bsum = f32x4v{0.f, 0.f, 0.f, 0.f};
+  f32x4v va[LA], vb[LB];
 
-  f32x4_t acc[2][2];
+  auto gload = [&](int pb) {
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  const int q = lane >> 4;
-  for (long pb = p0; pb < p1; pb += F_BK) {
-    const long p = pb + lpx;
-    f32x4v va = f32x4v{0.f, 0.f, 0.f, 0.f}, vb = va;
-    if (p < p1) {
-      const int hw = a.Hg * a.Wg;
-      const int n = (int)(p / hw), rem = (int)(p - (long)n * hw), h = rem / a.Wg, w = rem - (rem / a.Wg) * a.Wg;
-      if (aok) va = *reinterpret_cast<const f32x4v*>(a.A + p * a.lda + am);
-      const int bh = h * a.s + bkh - a.pad, bw = w * a.s + bkw - a.pad;
-      if (bok && bh >= 0 && bh < a.HB && bw >= 0 && bw < a.WB)
-        vb = *reinterpret_cast<const f32x4v*>(a.B + ((long)(n * a.HB + bh) * a.WB + bw) * a.ldb + bn);
-    }
-    if (do_bias) bsum += va;
-    // transposed store: row (channel / column) r, pixel lpx; rows r .. r+3 of this chunk
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int r = 4 * l4 + e;
-      const int pc = lpx >> 2, pe = lpx & 3;
-      reinterpret_cast<float*>(reinterpret_cast<char*>(As) + r * RB + fswz(r, pc) * 16)[pe] = va[e];
-      reinterpret_cast<float*>(reinterpret_cast<char*>(Bs) + r * RB + fswz(r, pc) * 16)[pe] = vb[e];
-    }
-    __syncthreads();
-    f32x4v af[2], bfr[2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int ra = wc * 32 + i * 16 + (lane & 15);
-      af[i] = *reinterpret_cast<const f32x4v*>(reinterpret_cast<const char*>(As) + ra * RB + fswz(ra, q) * 16);
-      const int rb = wp * 32 + i * 16 + (lane & 15);
-      bfr[i] = *reinterpret_cast<const f32x4v*>(reinterpret_cast<const char*>(Bs) + rb * RB + fswz(rb, q) * 16);
+    for (int i = 0; i < LA; ++i) {
+      const int p = pb + ra + i * RPA;
+      va[i] = p < p1 ? *reinterpret_cast<const f32x4v*>(a.A + (long)p * a.lda + m0 + 4 * ca) : f32x4v{0.f, 0.f, 0.f, 0.f};
     }
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < LB; ++i) {
+      const int p = pb + rb + i * RPB;
+      vb[i] = f32x4v{0.f, 0.f, 0.f, 0.f};
+      if (bok && p < p1) {
+        const int n = p / hw, rem = p - n * hw, h = rem / a.Wg, w = rem - h * a.Wg;
+        const int bh = h * a.s + bkh - a.pad, bw = w * a.s + bkw - a.pad;
+        if (bh >= 0 && bh < a.HB && bw >= 0 && bw < a.WB)
+          vb[i] = *reinterpret_cast<const f32x4v*>(a.B + ((long)(n * a.HB + bh) * a.WB + bw) * a.ldb + bn);
+      }
+    }
+  };
+  auto lstore = [&](int buf) {
 #pragma unroll
-      for (int j = 0; j < 2; ++j) acc[i][j] = mfma4(af[i], bfr[j], acc[i][j]);
+    for (int i = 0; i < LA; ++i) {
+      *reinterpret_cast<f32x4v*>(&As[buf][(ra + i * RPA) * SA + 4 * ca]) = va[i];
+      if (do_bias) bsum += va[i];
+    }
+#pragma unroll
+    for (int i = 0; i < LB; ++i) *reinterpret_cast<f32x4v*>(&Bs[buf][(rb + i * RPB) * SB + 4 * cb]) = vb[i];
+  };
+
+  f32x4_t acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  const int S = (p1 - p0 + BK - 1) / BK;
+  gload(p0);
+  lstore(0);
+  __syncthreads();
+  for (int s = 0; s < S; ++s) {
+    const int buf = s & 1;
+    if (s + 1 < S) gload(p0 + (s + 1) * BK);
+    const float* Ab = As[buf] + wm * WM + l16;
+    const float* Bb = Bs[buf] + wn * WN + l16;
+#pragma unroll
+    for (int ks = 0; ks < BK / 4; ++ks) {
+      const int px = 4 * ks + q;                  // MFMA K index = lane group
+      float af[TM], bf[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[i] = Ab[px * SA + i * 16];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bf[j] = Bb[px * SB + j * 16];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bf[j], acc[i][j], 0, 0, 0);
+    }
+    if (s + 1 < S) lstore(buf ^ 1);
     __syncthreads();
   }
-  // slab[split][tap][m][n]: lane holds rows (m) 4 q + r of column (lane & 15)
+  // slab[split][tap][m][n]: lane holds rows (m) 4 q + r of column l16
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int col = n0 + wp * 32 + j * 16 + (lane & 15);
+  for (int j = 0; j < TN; ++j) {
+    const int col = n0 + wn * WN + j * 16 + l16;
     if (col >= Ncols) continue;
     const int tap = col / a.Nc, n = col - tap * a.Nc;
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int m = m0 + wc * 32 + i * 16 + 4 * q + r;
-        if (m < a.M) a.slab[(((long)split * T + tap) * a.M + m) * a.Nc + n] = acc[i][j][r];
+        const int m = m0 + wm * WM + i * 16 + 4 * q + r;
+        a.slab[(((long)split * T + tap) * a.M + m) * a.Nc + n] = acc[i][j][r];
       }
   }
-  if (do_bias) {
-#pragma unroll
-    for (int e = 0; e < 4; ++e) bred[lpx][4 * l4 + e] = bsum[e];
+  if (do_bias) {                                  // rows ra of the A loader -> sum over RPA row groups
+    float* red = As[0];
+    *reinterpret_cast<f32x4v*>(&red[ra * BM + 4 * ca]) = bsum;
     __syncthreads();
-    if (tid < 64 && m0 + tid < a.M) {
-      float s = 0.f;
+    if (tid < BM) {
+      float sum = 0.f;
 #pragma unroll
-      for (int k = 0; k < 16; ++k) s += bred[k][tid];
-      a.bslab[(long)split * a.M + m0 + tid] = s;
+      for (int k = 0; k < RPA; ++k) sum += red[k * BM + tid];
+      a.bslab[(long)split * a.M + m0 + tid] = sum;
+    }
+  }
+}
+
+// 3x3 / stride-1 / pad-1 weight gradient for the shallow levels (B channels NC = 32 / 64, A channels in
+// blocks of 32): a stage is a 2-row x 32-pixel patch; its B halo (4 rows x 34 pixels x NC) is staged in
+// LDS once and all 9 taps read from it, so B is fetched ~1.1x per pixel instead of once per tap-column
+// tile.  Block = 32 A channels x all 9 NC columns: (m-tile, n-tile) pairs over the 4 waves, each pair
+// with its 9 taps in registers.  Stages are enumerated (n, row pair, 32-px segment); a split is a
+// contiguous range of stages, reduced like the generic form.  Operands in natural [pixel][channel] LDS
+// order, scalar MFMA operand reads (row strides 48 / 80 floats: the 4 K lane groups hit 4 distinct
+// 16-bank groups), next stage's loads in registers during the current one.
+template <int NC>
+__global__ __launch_bounds__(256) void wgrad3_f32_kernel(F32WgradArgs a) {
+  constexpr int SR = 2, SW = 32, SP = SR * SW, HP = (SR + 2) * (SW + 2);   // stage pixels, halo pixels
+  constexpr int SA = 48, SB = 80;                                          // LDS row strides (floats)
+  constexpr int NT = NC / 16, PW = 2 * NT / 4;                             // n-tiles, (mt, nt) pairs per wave
+  constexpr int CB = NC / 4, LBI = (HP * CB + 255) / 256;                  // B chunks per pixel, loads per thread
+  static_assert(PW >= 1 && 2 * NT % 4 == 0, "tile");
+  __shared__ __attribute__((aligned(16))) float As[2][SP * SA];
+  __shared__ __attribute__((aligned(16))) float Bs[2][HP * SB];
+
+  const int nmb = a.M / 32;
+  const int bid = xcd_remap(blockIdx.x, nmb * a.splits);       // a split's m-blocks (same B halo) share an L2
+  const int split = bid / nmb, mb = bid - split * nmb;
+  const int m0 = mb * 32;
+  const int segs = a.Wg / SW, per_img = (a.Hg / SR) * segs;
+  const int nst = a.N * per_img;
+  const int sps = (int)(a.pix_per_split / SP);
+  const int st0 = split * sps, st1 = st0 + sps < nst ? st0 + sps : nst;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, q = lane >> 4, l16 = lane & 15;
+  const int mt = wid & 1, nt0 = (wid >> 1) * PW;
+  const int ca = tid & 7;                    // A loader: channel chunk (fixed per thread), pixel tid / 8 (+ 32)
+  const bool do_bias = a.bslab != nullptr;
+  f32x4v bsum = f32x4v{0.f, 0.f, 0.f, 0.f};
+  f32x4v va[2], vb[LBI];
+
+  auto gload = [&](int st) {
+    const int n = st / per_img, rem = st - n * per_img, hp = rem / segs;
+    const int h0 = hp * SR, w0 = (rem - hp * segs) * SW;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int px = (tid >> 3) + 32 * i;
+      const long pix = ((long)n * a.Hg + h0 + (px >> 5)) * a.Wg + w0 + (px & 31);
+      va[i] = *reinterpret_cast<const f32x4v*>(a.A + pix * a.lda + m0 + 4 * ca);
+    }
+#pragma unroll
+    for (int i = 0; i < LBI; ++i) {
+      const int idx = tid + 256 * i;
+      const int hpix = idx / CB, ch = idx - hpix * CB;
+      const int hr = hpix / (SW + 2), hc = hpix - hr * (SW + 2);
+      const int ih = h0 - 1 + hr, iw = w0 - 1 + hc;
+      vb[i] = f32x4v{0.f, 0.f, 0.f, 0.f};
+      if (hpix < HP && ih >= 0 && ih < a.HB && iw >= 0 && iw < a.WB)
+        vb[i] = *reinterpret_cast<const f32x4v*>(a.B + ((long)(n * a.HB + ih) * a.WB + iw) * a.ldb + 4 * ch);
+    }
+  };
+  auto lstore = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      *reinterpret_cast<f32x4v*>(&As[buf][((tid >> 3) + 32 * i) * SA + 4 * ca]) = va[i];
+      if (do_bias) bsum += va[i];
+    }
+#pragma unroll
+    for (int i = 0; i < LBI; ++i) {
+      const int idx = tid + 256 * i;
+      const int hpix = idx / CB, ch = idx - hpix * CB;
+      if (hpix < HP) *reinterpret_cast<f32x4v*>(&Bs[buf][hpix * SB + 4 * ch]) = vb[i];
+    }
+  };
+
+  f32x4_t acc[PW][9];
+#pragma unroll
+  for (int p = 0; p < PW; ++p)
+#pragma unroll
+    for (int t = 0; t < 9; ++t) acc[p][t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  if (st0 < st1) {
+    gload(st0);
+    lstore(0);
+  }
+  __syncthreads();
+  for (int st = st0; st < st1; ++st) {
+    const int buf = (st - st0) & 1;
+    if (st + 1 < st1) gload(st + 1);
+    const float* Ab = As[buf] + mt * 16 + l16;
+    const float* Bb = Bs[buf] + nt0 * 16 + l16;
+#pragma unroll 4
+    for (int ks = 0; ks < SP / 4; ++ks) {
+      const int px = 4 * ks + q, r = px >> 5, c = px & 31;      // MFMA K index = lane group
+      const float af = Ab[px * SA];
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int hp = (r + t / 3) * (SW + 2) + c + t % 3;
+#pragma unroll
+        for (int p = 0; p < PW; ++p)
+          acc[p][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(af, Bb[hp * SB + p * 16], acc[p][t], 0, 0, 0);
+      }
+    }
+    if (st + 1 < st1) lstore(buf ^ 1);
+    __syncthreads();
+  }
+  // slab[split][tap][m][n]: lane holds rows (m) 4 q + r of column l16
+#pragma unroll
+  for (int p = 0; p < PW; ++p)
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + mt * 16 + 4 * q + r, n = (nt0 + p) * 16 + l16;
+        a.slab[(((long)split * 9 + t) * a.M + m) * NC + n] = acc[p][t][r];
+      }
+  if (do_bias) {                             // 32 pixel groups x 32 channels
+    float* red = As[0];
+    *reinterpret_cast<f32x4v*>(&red[(tid >> 3) * 32 + 4 * ca]) = bsum;
+    __syncthreads();
+    if (tid < 32) {
+      float sum = 0.f;
+#pragma unroll
+      for (int k = 0; k < 32; ++k) sum += red[k * 32 + tid];
+      a.bslab[(long)split * a.M + m0 + tid] = sum;
     }
   }
 }
@@ -490,7 +640,8 @@ static unsigned egrid(long n) { return (unsigned)(n / 256 + 1 < 8192 ? n / 256 +
 
 // Eligible: Cs % 4 == 0 (a float4 chunk never straddles a tap), Kpad % 16 == 0, Kpad >= KH*KW*Cs,
 // Ngemm % 32 == 0, 16-B aligned strides; mode 1 also Cout % 4 == 0.
-// Tiles: Ngemm % 64 == 0 -> 128 px x 64 ch, else 128 x 32; 32-deep K-steps when Kpad % 32 == 0.
+// Tiles: 128 px x 128 ch (Ngemm % 128 == 0, 32-deep K-steps), 128 x 64 (Ngemm % 64 == 0), else 128 x 32;
+// 32-deep K-steps when Kpad % 32 == 0.
 DPA_API int dpa_igemm_f32(const F32ConvArgs* args, hipStream_t st) {
   const F32ConvArgs& a = *args;
   if ((a.Cs & 3) || (a.Kpad % F_BK) || a.Kpad < a.KH * a.KW * a.Cs || (a.Ngemm & 31) || (a.ldx & 3) || (a.ldy & 3) ||
@@ -498,7 +649,10 @@ DPA_API int dpa_igemm_f32(const F32ConvArgs* args, hipStream_t st) {
     return (int)hipErrorInvalidValue;
   const long M = (long)a.N * a.Ho * a.Wo;
   const bool k32 = a.Kpad % 32 == 0;
-  if (a.Ngemm % 64 == 0) {
+  if (a.Ngemm % 128 == 0 && k32) {
+    const dim3 grid((unsigned)(((M + 127) / 128) * (a.Ngemm / 128)));
+    hipLaunchKernelGGL((igemm_f32_kernel<128, 128, 2, 32>), grid, dim3(256), 0, st, a);
+  } else if (a.Ngemm % 64 == 0) {
     const dim3 grid((unsigned)(((M + 127) / 128) * (a.Ngemm / 64)));
     if (k32) hipLaunchKernelGGL((igemm_f32_kernel<128, 64, 2, 32>), grid, dim3(256), 0, st, a);
     else hipLaunchKernelGGL((igemm_f32_kernel<128, 64, 2, 16>), grid, dim3(256), 0, st, a);
@@ -510,17 +664,32 @@ DPA_API int dpa_igemm_f32(const F32ConvArgs* args, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
-// Eligible: M % 4 == 0, Nc % 4 == 0, lda / ldb % 4 == 0, pix_per_split % 16 == 0, splits covering all pixels.
+// Eligible: M % 32 == 0, Nc % 4 == 0, lda / ldb % 4 == 0, pix_per_split % 32 == 0, splits covering all
+// pixels.  BM = 128 / 64 / 32 A channels per tile (the largest dividing M).
+static int wgrad_f32_bm(int M) { return M % 128 == 0 ? 128 : M % 64 == 0 ? 64 : 32; }   // ops/fp32.py mirrors it
+
 DPA_API int dpa_wgrad_f32(const F32WgradArgs* args, hipStream_t st) {
   const F32WgradArgs& a = *args;
   const long P = (long)a.N * a.Hg * a.Wg;
-  if ((a.M & 3) || (a.Nc & 3) || (a.lda & 3) || (a.ldb & 3) || a.pix_per_split < 16 || (a.pix_per_split % 16) ||
+  if ((a.M & 31) || (a.Nc & 3) || (a.lda & 3) || (a.ldb & 3) || a.pix_per_split < 32 || (a.pix_per_split % 32) ||
       a.splits < 1 || (long)a.splits * a.pix_per_split < P || (long)(a.splits - 1) * a.pix_per_split >= P ||
-      a.KH * a.KW < 1)
+      a.KH * a.KW < 1 || P >= (1L << 31))
     return (int)hipErrorInvalidValue;
-  const int T = a.KH * a.KW;
-  const long tiles = (long)((a.M + 63) / 64) * ((T * a.Nc + 63) / 64);
-  hipLaunchKernelGGL(wgrad_f32_kernel, dim3((unsigned)(tiles * a.splits)), dim3(256), 0, st, a);
+  if (a.halo) {
+    if (a.KH != 3 || a.KW != 3 || a.s != 1 || a.pad != 1 || a.HB != a.Hg || a.WB != a.Wg || (a.Hg & 1) ||
+        (a.Wg % 32) || (a.pix_per_split % 64) || (a.Nc != 32 && a.Nc != 64))
+      return (int)hipErrorInvalidValue;
+    const dim3 grid((unsigned)((a.M / 32) * a.splits));
+    if (a.Nc == 32) hipLaunchKernelGGL(wgrad3_f32_kernel<32>, grid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL(wgrad3_f32_kernel<64>, grid, dim3(256), 0, st, a);
+    return (int)hipGetLastError();
+  }
+  const int T = a.KH * a.KW, bm = wgrad_f32_bm(a.M);
+  const long tiles = (long)(a.M / bm) * ((T * a.Nc + 127) / 128);
+  const dim3 grid((unsigned)(tiles * a.splits));
+  if (bm == 128) hipLaunchKernelGGL(wgrad_f32_kernel<128>, grid, dim3(256), 0, st, a);
+  else if (bm == 64) hipLaunchKernelGGL(wgrad_f32_kernel<64>, grid, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL(wgrad_f32_kernel<32>, grid, dim3(256), 0, st, a);
   return (int)hipGetLastError();
 }
 

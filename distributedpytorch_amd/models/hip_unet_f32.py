@@ -11,8 +11,9 @@ and weight in fp32 and runs every conv-shaped product on fp32 MFMA (v_mfma_f32_1
 * 2x2 max-pool with window codes and its backward, the segmentation head (1x1 conv + sigmoid +
   BCE / Dice partial sums, ``utils/utils.py:9-25``) and its backward, the NCHW -> NHWC input pass.
 
-Granularity is one autograd Function per op (simple, exact; the bf16 engine's cross-op fusions are
-not replicated: fp32 is the parity / precision path, bf16 the fast one).  Activations are NHWC
+Granularity is one autograd Function per op, except a DoubleConv's two convs (one Function: the inner
+ReLU backward is the mask epilogue of the second conv's dgrad); the bf16 engine's other cross-op fusions
+are not replicated (fp32 is the parity / precision path, bf16 the fast one).  Activations are NHWC
 tensors handed between blocks as logical-NCHW channels_last views, as in the bf16 engine.  Supported:
 the reference UNet family without BatchNorm and with transposed-conv up-sampling, channel widths
 divisible by 32 (other configurations take the stock torch path, ``compute.resolve_backend``).
@@ -52,18 +53,47 @@ def _dense(t: torch.Tensor) -> torch.Tensor:
     return t if t.is_contiguous() else t.contiguous()
 
 
+def _conv_fwd(x, weight, bias, cs: int):
+    """relu(conv3x3(x) + b), NHWC fp32; ``cs`` = channels of x the kernel reads (>= Cin, zero weights for
+    the padding channels of the network input)."""
+    N, H, W = x.shape[:3]
+    co = weight.shape[0]
+    wp, kpad = F32.pack_conv_fwd(weight, cs)
+    y = torch.empty(N, H, W, co, dtype=torch.float32, device=x.device)
+    F32.igemm(x, wp, y, Ngemm=co, Kpad=kpad, KH=3, KW=3, stride=1, pad=1, Cs=cs, out_grid=(N, H, W),
+              bias=bias.detach(), relu=True)
+    return y
+
+
+def _conv_dgrad(ge, weight, cs: int, mask=None):
+    """dL/dx of a conv3x3 from the pre-activation gradient ``ge``; ``mask`` = the input's own ReLU output
+    (its backward applied in the epilogue)."""
+    co, ci = weight.shape[:2]
+    N, H, W = ge.shape[:3]
+    wd, kd = F32.pack_conv_dgrad(weight)
+    ng = F32.round_up(cs, 32)          # GEMM-N multiple of 32: zero rows for the padding channels
+    if ng != ci:
+        wd = torch.cat([wd, wd.new_zeros(ng - ci, kd)]).contiguous()
+    gx = torch.empty(N, H, W, ng, dtype=torch.float32, device=ge.device)
+    F32.igemm(ge, wd, gx, Ngemm=ng, Kpad=kd, KH=3, KW=3, stride=1, pad=1, Cs=co, out_grid=(N, H, W), mask=mask)
+    return gx[..., :cs] if ng != cs else gx
+
+
+def _conv_wgrad(ge, x, weight, cs: int):
+    co, ci = weight.shape[:2]
+    gw = torch.zeros(co, cs, 3, 3, dtype=torch.float32, device=x.device)
+    gb = torch.zeros(co, dtype=torch.float32, device=x.device)
+    F32.wgrad(ge, x, gw, gb, KH=3, KW=3, s=1, pad=1)
+    return (gw if cs == ci else gw[:, :ci].contiguous()), gb
+
+
 class _ConvReLU(torch.autograd.Function):
-    """y = relu(conv3x3(x) + b), NHWC fp32; ``cs`` = channels of x the kernel reads (>= Cin, zero weights
-    for the padding channels of the network input)."""
+    """y = relu(conv3x3(x) + b), NHWC fp32 (one conv: the halves of a DoubleConv cut by a pipeline stage
+    boundary)."""
 
     @staticmethod
     def forward(ctx, x, weight, bias, cs: int):
-        N, H, W = x.shape[:3]
-        co = weight.shape[0]
-        wp, kpad = F32.pack_conv_fwd(weight, cs)
-        y = torch.empty(N, H, W, co, dtype=torch.float32, device=x.device)
-        F32.igemm(x, wp, y, Ngemm=co, Kpad=kpad, KH=3, KW=3, stride=1, pad=1, Cs=cs, out_grid=(N, H, W),
-                  bias=bias.detach(), relu=True)
+        y = _conv_fwd(x, weight, bias, cs)
         ctx.cs = cs
         ctx.save_for_backward(x, weight, y)
         return y
@@ -71,22 +101,34 @@ class _ConvReLU(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gy):
         x, weight, y = ctx.saved_tensors
-        co, ci = weight.shape[:2]
-        N, H, W = x.shape[:3]
         ge = F32.relu_bwd(_dense(gy), y)
-        gx = None
-        if ctx.needs_input_grad[0]:
-            wd, kd = F32.pack_conv_dgrad(weight)
-            ng = F32.round_up(ctx.cs, 32)          # GEMM-N multiple of 32: zero rows for the padding channels
-            if ng != ci:
-                wd = torch.cat([wd, wd.new_zeros(ng - ci, kd)]).contiguous()
-            gx = torch.empty(N, H, W, ng, dtype=torch.float32, device=x.device)
-            F32.igemm(ge, wd, gx, Ngemm=ng, Kpad=kd, KH=3, KW=3, stride=1, pad=1, Cs=co, out_grid=(N, H, W))
-            gx = gx[..., :ctx.cs]
-        gw = torch.zeros(co, ctx.cs, 3, 3, dtype=torch.float32, device=x.device)
-        gb = torch.zeros(co, dtype=torch.float32, device=x.device)
-        F32.wgrad(ge, x, gw, gb, KH=3, KW=3, s=1, pad=1)
-        return gx, gw[:, :ci].contiguous(), gb, None
+        gx = _conv_dgrad(ge, weight, ctx.cs) if ctx.needs_input_grad[0] else None
+        gw, gb = _conv_wgrad(ge, x, weight, ctx.cs)
+        return gx, gw, gb, None
+
+
+class _DoubleConvReLU(torch.autograd.Function):
+    """relu(conv2(relu(conv1(x)))) (reference DoubleConv without BatchNorm, model/unet_parts.py:7-15) as one
+    Function: the inner ReLU's backward is the mask epilogue of conv2's dgrad, so the inner gradient is
+    written once, already masked."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2, cs: int):
+        a = _conv_fwd(x, w1, b1, cs)
+        y = _conv_fwd(a, w2, b2, a.shape[3])
+        ctx.cs = cs
+        ctx.save_for_backward(x, w1, a, w2, y)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w1, a, w2, y = ctx.saved_tensors
+        ge2 = F32.relu_bwd(_dense(gy), y)
+        ge1 = _conv_dgrad(ge2, w2, a.shape[3], mask=a)
+        gw2, gb2 = _conv_wgrad(ge2, a, w2, a.shape[3])
+        gx = _conv_dgrad(ge1, w1, ctx.cs) if ctx.needs_input_grad[0] else None
+        gw1, gb1 = _conv_wgrad(ge1, x, w1, ctx.cs)
+        return gx, gw1, gb1, gw2, gb2, None
 
 
 class _Deconv(torch.autograd.Function):
@@ -172,21 +214,23 @@ class HipF32Blocks:
     def _conv(self, conv, x, cs=None):
         return _ConvReLU.apply(x, conv.weight, conv.bias, cs or x.shape[3])
 
+    def _double(self, c1, c2, x, cs=None):
+        return _DoubleConvReLU.apply(x, c1.weight, c1.bias, c2.weight, c2.bias, cs or x.shape[3])
+
     def enc(self, l: int, x):
         c1, c2 = self.model.encoder.blocks()[l].convs()
-        x = _v(x)
-        a = self._conv(c1, x, 4 if l == 0 else None)
-        s = self._conv(c2, a)
+        s = self._double(c1, c2, _v(x), 4 if l == 0 else None)
         return _o(s), _o(_MaxPool.apply(s))
 
     def mid(self, x):
         c1, c2 = self.model.mid.convs()
-        return _o(self._conv(c2, self._conv(c1, _v(x))))
+        return _o(self._double(c1, c2, _v(x)))
 
     def dec(self, i: int, x, skip):
         # transposed conv, reference CenterCrop of the skip (model/unet_parts.py:58-74), concat with the
         # skip first (:59), conv_block
-        return self.dec_b(i, self.dec_a(i, x, skip))
+        c1, c2 = self.model.decoder.blocks()[i].convs()
+        return _o(self._double(c1, c2, self._up_cat(i, x, skip)))
 
     # halves of a block cut between its two convs (pipeline stage boundary inside a DoubleConv)
     def enc_a(self, l: int, x):
@@ -204,16 +248,19 @@ class HipF32Blocks:
     def mid_b(self, a):
         return _o(self._conv(self.model.mid.convs()[1], _v(a)))
 
-    def dec_a(self, i: int, x, skip):
+    def _up_cat(self, i: int, x, skip):
         d = self.model.decoder.ups()[i]
-        c1 = self.model.decoder.blocks()[i].convs()[0]
         up = _Deconv.apply(_v(x), d.weight, d.bias)
         sk = _v(skip)
         h2, w2 = up.shape[1:3]
         if tuple(sk.shape[1:3]) != (h2, w2):
             top, left = int(round((sk.shape[1] - h2) / 2.0)), int(round((sk.shape[2] - w2) / 2.0))
             sk = sk[:, top:top + h2, left:left + w2]
-        return _o(self._conv(c1, torch.cat([sk, up], dim=3)))
+        return torch.cat([sk, up], dim=3)
+
+    def dec_a(self, i: int, x, skip):
+        c1 = self.model.decoder.blocks()[i].convs()[0]
+        return _o(self._conv(c1, self._up_cat(i, x, skip)))
 
     def dec_b(self, i: int, a):
         return _o(self._conv(self.model.decoder.blocks()[i].convs()[1], _v(a)))

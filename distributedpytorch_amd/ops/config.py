@@ -59,6 +59,8 @@ KNOBS = (
          "first on load (forward and fused backward); the first conv's BN output is never stored"),
     Knob("dual_input", "DPA_NO_DUAL_INPUT", True, "32-channel level: skip and up half as two dense tensors read by the "
          "decoder conv (no concat buffer)"),
+    Knob("f32_wgrad_halo", "DPA_NO_F32_WGRAD_HALO", True, "fp32 engine: 3x3 weight gradients over 32 / 64 input channels "
+         "stage the input halo once per 2 x 32-pixel patch (csrc/fp32.hip wgrad3_f32_kernel)"),
     # launch geometry / streams
     Knob("side_priority", "DPA_SIDE_PRIORITY", 0, "HIP priority of the weight-gradient side stream (torch convention)"),
     Knob("wgrad_stream_blocks", "DPA_WGRAD_STREAM_BLOCKS", 2048, "target workgroups of a row-streaming weight gradient"),
@@ -114,6 +116,7 @@ class KernelConfig:
     fused_deconv: bool = True
     dual_input: bool = True
     bn_on_load: bool = True
+    f32_wgrad_halo: bool = True
     side_priority: int = 0
     wgrad_stream_blocks: int = 2048
     wgrad_gemm_blocks: int = 768

@@ -12,6 +12,7 @@ from typing import Optional, Tuple
 import torch
 
 from . import _lib
+from . import config as _config
 
 c_int, c_ll, c_void_p = ctypes.c_int, ctypes.c_longlong, ctypes.c_void_p
 _MAX = 2 ** 31 - 1024          # per-launch element-offset range the host keeps (int pixel math)
@@ -23,10 +24,13 @@ class F32ConvArgs(ctypes.Structure):
                                      "stride", "pad", "Ngemm", "Kpad", "mode", "relu", "accumulate", "Cout")]
 
 
+USE_WGRAD_HALO = _config.KernelConfig.from_env().f32_wgrad_halo   # 3x3 weight gradients with the input halo staged
+
+
 class F32WgradArgs(ctypes.Structure):
     _fields_ = [("A", c_void_p), ("B", c_void_p), ("slab", c_void_p), ("bslab", c_void_p)] + \
                [(n, c_int) for n in ("lda", "ldb", "N", "Hg", "Wg", "HB", "WB", "M", "Nc", "s", "pad", "KH", "KW")] + \
-               [("pix_per_split", ctypes.c_long), ("splits", c_int)]
+               [("pix_per_split", ctypes.c_long), ("splits", c_int), ("halo", c_int)]
 
 
 def _st(t: torch.Tensor):
@@ -131,19 +135,29 @@ def wgrad(A: torch.Tensor, B: torch.Tensor, gw: torch.Tensor, gb: Optional[torch
     sum_p A[p][m]; A is the pixel grid.  Split over pixel ranges into fp32 slabs, summed in a fixed order."""
     N, Hg, Wg, M, lda = nhwc(A, "wgrad_f32.A")
     NB, HB, WB, Nc, ldb = nhwc(B, "wgrad_f32.B")
-    assert NB == N and M % 4 == 0 and Nc % 4 == 0
+    assert NB == N and M % 32 == 0 and Nc % 4 == 0
     assert gw.dtype == torch.float32 and gw.is_contiguous() and gw.numel() == M * Nc * KH * KW
     assert gb is None or (gb.dtype == torch.float32 and gb.numel() == M)
     T = KH * KW
     P = N * Hg * Wg
-    tiles = -(-M // 64) * -(-(T * Nc) // 64)
-    splits = max(1, min(-(-target_blocks // tiles), -(-P // 4096)))
-    pps = round_up(-(-P // splits), 16)
-    splits = -(-P // pps)
+    halo = int(USE_WGRAD_HALO and (KH, KW, s, pad) == (3, 3, 1, 1) and (HB, WB) == (Hg, Wg) and Hg % 2 == 0
+               and Wg % 32 == 0 and Nc in (32, 64))
+    if halo:       # stages of 2 rows x 32 pixels, all 9 taps of 32 A channels per block
+        nst = N * (Hg // 2) * (Wg // 32)
+        splits = max(1, min(nst, -(-target_blocks // (M // 32))))
+        sps = -(-nst // splits)
+        splits = -(-nst // sps)
+        pps = 64 * sps
+    else:
+        bm = 128 if M % 128 == 0 else 64 if M % 64 == 0 else 32          # csrc/fp32.hip wgrad_f32_bm
+        tiles = (M // bm) * -(-(T * Nc) // 128)
+        splits = max(1, min(-(-target_blocks // tiles), -(-P // 1024)))
+        pps = round_up(-(-P // splits), 32)
+        splits = -(-P // pps)
     slab = torch.empty(splits * T * M * Nc + (splits * M if gb is not None else 0), dtype=torch.float32, device=A.device)
     bslab = slab[splits * T * M * Nc:] if gb is not None else None
     a = F32WgradArgs(A.data_ptr(), B.data_ptr(), slab.data_ptr(), None if bslab is None else bslab.data_ptr(),
-                     lda, ldb, N, Hg, Wg, HB, WB, M, Nc, s, pad, KH, KW, pps, splits)
+                     lda, ldb, N, Hg, Wg, HB, WB, M, Nc, s, pad, KH, KW, pps, splits, halo)
     L = _lib.lib()
     st = _st(A)
     _check(L.dpa_wgrad_f32(ctypes.byref(a), st), "wgrad_f32")

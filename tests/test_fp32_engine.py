@@ -15,6 +15,7 @@ def _rel(a, b):
 
 
 @pytest.mark.parametrize("N,H,W,Cin,Cout,cs", [(2, 16, 24, 32, 32, 32), (1, 9, 13, 64, 96, 64), (2, 8, 8, 3, 32, 4),
+                                               (2, 32, 40, 128, 128, 128), (1, 20, 18, 64, 256, 64),
                                                (3, 12, 10, 96, 64, 96)])
 def test_conv_relu_fwd_bwd(hip_lib, N, H, W, Cin, Cout, cs):
     from distributedpytorch_amd.models.hip_unet_f32 import _ConvReLU
@@ -34,6 +35,54 @@ def test_conv_relu_fwd_bwd(hip_lib, N, H, W, Cin, Cout, cs):
     gx, gw, gb = torch.autograd.grad(y, (xn, w, b), g.permute(0, 2, 3, 1).contiguous())
     assert _rel(gw, gw_ref) < 1e-5 and _rel(gb, gb_ref) < 1e-5
     assert _rel(gx[..., :Cin].permute(0, 3, 1, 2), gx_ref) < 1e-5
+
+
+@pytest.mark.parametrize("N,H,W,Nc,M", [(2, 8, 64, 32, 32), (1, 6, 32, 64, 96), (3, 2, 96, 64, 64), (1, 4, 32, 32, 64)])
+def test_wgrad_halo_form(hip_lib, N, H, W, Nc, M):
+    """3x3 weight gradient with the input halo staged per 2 x 32-pixel patch (wgrad3_f32_kernel) and the
+    generic tap-column form, both vs torch fp32 (weight and bias gradient)."""
+    from distributedpytorch_amd.ops import fp32 as F32
+    torch.manual_seed(Nc + M + H)
+    x = torch.randn(N, Nc, H, W, device="cuda")
+    g = torch.randn(N, M, H, W, device="cuda")
+    gw_ref = torch.nn.grad.conv2d_weight(x, (M, Nc, 3, 3), g, padding=1)
+    gb_ref = g.sum((0, 2, 3))
+    A, B = g.permute(0, 2, 3, 1).contiguous(), x.permute(0, 2, 3, 1).contiguous()
+    old = F32.USE_WGRAD_HALO
+    try:
+        for halo in (True, False):
+            F32.USE_WGRAD_HALO = halo
+            gw = torch.zeros(M, Nc, 3, 3, device="cuda")
+            gb = torch.zeros(M, device="cuda")
+            F32.wgrad(A, B, gw, gb, KH=3, KW=3, s=1, pad=1)
+            assert _rel(gw, gw_ref) < 1e-5 and _rel(gb, gb_ref) < 1e-5, halo
+    finally:
+        F32.USE_WGRAD_HALO = old
+
+
+@pytest.mark.parametrize("N,H,W,Cin,Cmid,Cout,cs", [(2, 12, 20, 3, 32, 32, 4), (1, 16, 16, 128, 64, 64, 128)])
+def test_double_conv_fwd_bwd(hip_lib, N, H, W, Cin, Cmid, Cout, cs):
+    """The fused DoubleConv Function (inner ReLU backward as conv2's dgrad mask epilogue) vs torch fp32."""
+    from distributedpytorch_amd.models.hip_unet_f32 import _DoubleConvReLU
+    torch.manual_seed(Cin + Cmid)
+    xr = torch.randn(N, Cin, H, W, device="cuda")
+    w1 = (torch.randn(Cmid, Cin, 3, 3, device="cuda") / (9 * Cin) ** 0.5).requires_grad_(True)
+    b1 = (torch.randn(Cmid, device="cuda") * 0.1).requires_grad_(True)
+    w2 = (torch.randn(Cout, Cmid, 3, 3, device="cuda") / (9 * Cmid) ** 0.5).requires_grad_(True)
+    b2 = (torch.randn(Cout, device="cuda") * 0.1).requires_grad_(True)
+    ref_x = xr.clone().requires_grad_(True)
+    ref = torch.relu(F.conv2d(torch.relu(F.conv2d(ref_x, w1, b1, padding=1)), w2, b2, padding=1))
+    g = torch.randn_like(ref)
+    refs = torch.autograd.grad(ref, (ref_x, w1, b1, w2, b2), g)
+    xn = torch.zeros(N, H, W, cs, device="cuda")
+    xn[..., :Cin] = xr.permute(0, 2, 3, 1)
+    xn.requires_grad_(True)
+    y = _DoubleConvReLU.apply(xn, w1, b1, w2, b2, cs)
+    assert _rel(y.permute(0, 3, 1, 2), ref) < 1e-5
+    gx, gw1, gb1, gw2, gb2 = torch.autograd.grad(y, (xn, w1, b1, w2, b2), g.permute(0, 2, 3, 1).contiguous())
+    assert _rel(gx[..., :Cin].permute(0, 3, 1, 2), refs[0]) < 1e-5
+    for got, want in zip((gw1, gb1, gw2, gb2), refs[1:]):
+        assert _rel(got, want) < 1e-5
 
 
 @pytest.mark.parametrize("N,h,w,Cin,Cout", [(2, 8, 12, 64, 32), (1, 5, 7, 128, 64), (2, 4, 4, 512, 256)])

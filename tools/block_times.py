@@ -65,8 +65,20 @@ def main():
         ts.sort()
         return ts[len(ts) // 2]
 
+    # the HIP engine's Functions hang off an anchor leaf and write weight gradients into the flat buffer
+    params = [p for p in model.parameters() if p.requires_grad] + ([B.anchor] if hasattr(B, "anchor") else [])
+    acc = []        # the leaves whose .grad is accumulated: parameters and the block input
+
     def leaf(t):
         return t.detach().requires_grad_(True)
+
+    def xleaf(t):
+        # the block input's gradient is accumulated (a stage boundary receives it); a skip is not: within a
+        # stage the encoder consumes the decoder's strided skip gradient directly, and materialising it
+        # into a leaf's .grad (a layout-changing copy of the concat-buffer view) is not engine work
+        v = leaf(t)
+        acc[:] = params + [v]
+        return v
 
     table = {"model": a.model, "img": [a.img, a.img], "depth": depth, "widths": list(model.cfg.widths),
              "mid_width": model.cfg.mid_width, "blocks": [f"{k}{i}" if k in ("enc", "dec") else k
@@ -107,7 +119,8 @@ def main():
             last = idx == nb - 2
 
             def run():
-                xin = leaf(inp["x"]) if idx > 0 else inp["x"]
+                acc[:] = params
+                xin = xleaf(inp["x"]) if idx > 0 else inp["x"]
                 if kind == "enc":
                     return B.enc(i, xin)
                 if kind == "mid":
@@ -128,7 +141,7 @@ def main():
                 s_, e_ = ev(), ev()
                 s_.record()
                 torch.autograd.backward(o, [torch.ones_like(v) if v.dim() == 1 else
-                                            torch.randn_like(v) * 1e-3 for v in o])
+                                            torch.randn_like(v) * 1e-3 for v in o], inputs=acc)
                 e_.record()
                 return s_, e_
 
@@ -162,12 +175,13 @@ def main():
                     a_out = B.dec_a(i, inp["x"], sk)
             for part in ("a", "b"):
                 def run_part():
+                    acc[:] = params
                     if part == "b":
-                        xin = leaf(a_out)
+                        xin = xleaf(a_out)
                         if kind == "enc":
                             return B.enc_b(i, xin)
                         return ((B.mid_b if kind == "mid" else (lambda v: B.dec_b(i, v)))(xin),)
-                    xin = leaf(inp["x"]) if idx > 0 else inp["x"]
+                    xin = xleaf(inp["x"]) if idx > 0 else inp["x"]
                     if kind == "enc":
                         return (B.enc_a(i, xin),)
                     if kind == "mid":
@@ -182,7 +196,7 @@ def main():
                         o = run_part()
                         s_, e_ = ev(), ev()
                         s_.record()
-                        torch.autograd.backward(o, [torch.randn_like(v) * 1e-3 for v in o])
+                        torch.autograd.backward(o, [torch.randn_like(v) * 1e-3 for v in o], inputs=acc)
                         e_.record()
                         torch.cuda.synchronize()
                         ts.append(s_.elapsed_time(e_))

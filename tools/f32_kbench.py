@@ -1,0 +1,101 @@
+#!/usr/bin/env python3
+"""Per-layer timing of the fp32 engine's GEMM kernels (csrc/fp32.hip) on the UNet at one batch: conv3x3
+forward, dgrad and weight gradient, transposed-conv forward / dgrad / weight gradient; achieved TFLOP/s
+against the 157 TFLOP/s fp32-MFMA peak.
+
+    python tools/f32_kbench.py --batch 16 --img 512
+"""
+import argparse
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=16)
+    ap.add_argument("--img", type=int, default=512)
+    ap.add_argument("--model", default="unet")
+    ap.add_argument("--reps", type=int, default=5)
+    a = ap.parse_args()
+    from distributedpytorch_amd.models import hip_unet_f32 as E
+    from distributedpytorch_amd.models.unet import build_model
+    from distributedpytorch_amd.ops import fp32 as F32
+    dev = torch.device("cuda:0")
+    cfg = build_model(a.model).cfg
+    N, S = a.batch, a.img
+    convs, deconvs = [], []
+    w = list(cfg.widths)
+    cin, h = 3, S
+    for l, c in enumerate(w):
+        convs.append((f"enc{l}.c1", h, cin, c)), convs.append((f"enc{l}.c2", h, c, c))
+        cin, h = c, h // 2
+    convs.append(("mid.c1", h, cin, cfg.mid_width)), convs.append(("mid.c2", h, cfg.mid_width, cfg.mid_width))
+    cin = cfg.mid_width
+    for i, c in enumerate(reversed(w)):
+        deconvs.append((f"dec{i}.up", h, cin, c))
+        h *= 2
+        convs.append((f"dec{i}.c1", h, 2 * c, c)), convs.append((f"dec{i}.c2", h, c, c))
+        cin = c
+
+    def t(fn):
+        fn()
+        torch.cuda.synchronize()
+        ts = []
+        for _ in range(a.reps):
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            fn()
+            e.record()
+            torch.cuda.synchronize()
+            ts.append(s.elapsed_time(e))
+        return sorted(ts)[len(ts) // 2]
+
+    tot = {"fwd": 0.0, "dgrad": 0.0, "wgrad": 0.0}
+    print(f"{'layer':10s} {'HxW':>9s} {'ci':>4s} {'co':>4s} | {'fwd ms':>7s} {'TF/s':>6s} | {'dgrad':>7s} {'TF/s':>6s} | "
+          f"{'wgrad':>7s} {'TF/s':>6s}")
+    for name, hh, ci, co in convs:
+        cs = 4 if ci == 3 else ci
+        x = torch.randn(N, hh, hh, cs, device=dev)
+        wt = torch.randn(co, ci, 3, 3, device=dev) * 0.05
+        b = torch.zeros(co, device=dev)
+        ge = torch.randn(N, hh, hh, co, device=dev)
+        fl = 2.0 * N * hh * hh * co * ci * 9
+        tf = t(lambda: E._conv_fwd(x, wt, b, cs))
+        td = t(lambda: E._conv_dgrad(ge, wt, cs)) if ci != 3 else 0.0
+        tw = t(lambda: E._conv_wgrad(ge, x, wt, cs))
+        tot["fwd"] += tf
+        tot["dgrad"] += td
+        tot["wgrad"] += tw
+        print(f"{name:10s} {hh:4d}x{hh:<4d} {ci:4d} {co:4d} | {tf:7.3f} {fl / tf / 1e9:6.1f} | {td:7.3f} "
+              f"{(fl / td / 1e9 if td else 0):6.1f} | {tw:7.3f} {fl / tw / 1e9:6.1f}", flush=True)
+        del x, ge
+    for name, hh, ci, co in deconvs:
+        x = torch.randn(N, hh, hh, ci, device=dev)
+        wt = torch.randn(ci, co, 2, 2, device=dev) * 0.05
+        b = torch.zeros(co, device=dev)
+        gy = torch.randn(N, 2 * hh, 2 * hh, co, device=dev)
+        fl = 2.0 * N * hh * hh * ci * co * 4
+        y = torch.empty(N, 2 * hh, 2 * hh, co, device=dev)
+        wf = F32.pack_deconv_fwd(wt)
+        tf = t(lambda: F32.igemm(x, wf, y, Ngemm=4 * co, Kpad=ci, KH=1, KW=1, stride=1, pad=0, Cs=ci,
+                                 out_grid=(N, hh, hh), bias=b, mode=1, Cout=co))
+        gx = torch.empty(N, hh, hh, ci, device=dev)
+        wd = F32.pack_deconv_dgrad(wt)
+        td = t(lambda: F32.igemm(gy, wd, gx, Ngemm=ci, Kpad=4 * co, KH=2, KW=2, stride=2, pad=0, Cs=co,
+                                 out_grid=(N, hh, hh)))
+        gw = torch.zeros(ci, co, 2, 2, device=dev)
+        tw = t(lambda: F32.wgrad(x, gy, gw, None, KH=2, KW=2, s=2, pad=0))
+        tot["fwd"] += tf
+        tot["dgrad"] += td
+        tot["wgrad"] += tw
+        print(f"{name:10s} {hh:4d}x{hh:<4d} {ci:4d} {co:4d} | {tf:7.3f} {fl / tf / 1e9:6.1f} | {td:7.3f} "
+              f"{fl / td / 1e9:6.1f} | {tw:7.3f} {fl / tw / 1e9:6.1f}", flush=True)
+    print("totals ms: " + ", ".join(f"{k} {v:.2f}" for k, v in tot.items()))
+
+
+if __name__ == "__main__":
+    main()
