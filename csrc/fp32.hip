@@ -232,21 +232,20 @@ __global__ __launch_bounds__(256) void igemm_f32_kernel(F32ConvArgs a) {
 
 // Weight gradient: dW[m][col] = sum_p A[p][m] B'[p][col], col = tap * Nc + n, B'[p][col] = B at pixel p's tap
 // position.  BM (A channels) x 128 (columns) per block, 4 waves (2 x 2 of 64 x 64 for BM = 128, else 1 x 4),
-// K = 32 pixels per stage.  The operands land in LDS in their natural [pixel][channel] order (float4
-// stores, rows padded by 16 floats so the four K lane groups of an MFMA operand read hit four distinct
-// 16-bank groups) and feed the MFMA as scalar reads -- no transpose; the next stage's global loads are
-// in registers while the current one computes (one barrier per stage).  The bias gradient sum_p A[p][m]
-// rides along in the blocks of column tile 0.
+// K = 32 pixels per stage.  LDS holds both operands K-contiguous ([channel / column][32 px], 128-B rows,
+// fswzk<8> swizzle), as the conv kernel does, so an MFMA operand is one ds_read_b128 per 4 MFMAs (K in
+// the permuted 4q + e order, the same for both operands).  The loader transposes in registers: a thread
+// loads a 4-pixel x 4-channel micro-block (4 float4, channel-contiguous in NHWC) and writes it as 4
+// float4 rows of 4 pixels.  Next stage's loads in registers during the current one; one barrier per
+// stage.  The bias gradient sum_p A[p][m] rides along in the blocks of column tile 0.
 template <int BM>
 __global__ __launch_bounds__(256) void wgrad_f32_kernel(F32WgradArgs a) {
-  constexpr int BN = 128, BK = 32, PADF = 16;
+  constexpr int BN = 128, BK = 32, RB = BK * 4;                 // LDS row bytes (8 chunks of 4 px)
   constexpr int NWM = BM == 128 ? 2 : 1, NWN = 4 / NWM, WM = BM / NWM, WN = BN / NWN, TM = WM / 16, TN = WN / 16;
-  constexpr int SA = BM + PADF, SB = BN + PADF;                 // LDS row strides (floats), one row per pixel
-  constexpr int CPA = BM / 4, RPA = 256 / CPA, LA = BK / RPA;   // A loader: chunks per pixel, rows per pass, loads
-  constexpr int CPB = BN / 4, RPB = 256 / CPB, LB = BK / RPB;
-  static_assert(LA >= 1 && LB >= 1 && TM >= 1 && TN >= 1, "tile");
-  __shared__ __attribute__((aligned(16))) float As[2][BK * SA];
-  __shared__ __attribute__((aligned(16))) float Bs[2][BK * SB];
+  constexpr int QA = BM / 4, UA = QA * (BK / 4);                // A micro-blocks (4 ch x 4 px) per stage
+  constexpr int QB = BN / 4;                                    // B: 32 x 8 = 256 micro-blocks, one per thread
+  static_assert(TM >= 1 && TN >= 1 && UA <= 256 && QB * (BK / 4) == 256, "tile");
+  __shared__ __attribute__((aligned(16))) char lds[2][(BM + BN) * RB];
 
   const int T = a.KH * a.KW, Ncols = T * a.Nc;
   const int nmt = a.M / BM, nnt = (Ncols + BN - 1) / BN, tiles = nmt * nnt;
@@ -259,43 +258,58 @@ __global__ __launch_bounds__(256) void wgrad_f32_kernel(F32WgradArgs a) {
   const int p1 = p0 + (int)a.pix_per_split < P ? p0 + (int)a.pix_per_split : P;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, q = lane >> 4, l16 = lane & 15;
   const int wm = wid / NWN, wn = wid - wm * NWN;
-  // loader chunks (fixed per thread): A channels m0 + 4 ca, B column n0 + 4 cb -> (tap, n)
-  const int ca = tid % CPA, ra = tid / CPA;
-  const int cb = tid % CPB, rb = tid / CPB;
-  const int bcol = n0 + 4 * cb;
+  // loader micro-blocks: A channels m0 + 4 qa, pixels 4 pa ..; B columns n0 + 4 qb -> (tap, n), pixels 4 pb ..
+  const bool has_a = tid < UA;
+  const int qa = tid % QA, pa = tid / QA;
+  const int qb = tid % QB, pbq = tid / QB;
+  const int bcol = n0 + 4 * qb;
   const bool bok = bcol < Ncols;
   const int btap = bok ? bcol / a.Nc : 0, bn = bcol - btap * a.Nc;
   const int bkh = btap / a.KW, bkw = btap - bkh * a.KW;
   const bool do_bias = a.bslab != nullptr && nt == 0;
   f32x4v bsum = f32x4v{0.f, 0.f, 0.f, 0.f};
-  f32x4v va[LA], vb[LB];
+  f32x4v va[4], vb[4];
 
   auto gload = [&](int pb) {
 #pragma unroll
-    for (int i = 0; i < LA; ++i) {
-      const int p = pb + ra + i * RPA;
-      va[i] = p < p1 ? *reinterpret_cast<const f32x4v*>(a.A + (long)p * a.lda + m0 + 4 * ca) : f32x4v{0.f, 0.f, 0.f, 0.f};
+    for (int e = 0; e < 4; ++e) {
+      const int p = pb + 4 * pa + e;
+      va[e] = has_a && p < p1 ? *reinterpret_cast<const f32x4v*>(a.A + (long)p * a.lda + m0 + 4 * qa)
+                              : f32x4v{0.f, 0.f, 0.f, 0.f};
     }
+    // (n, h, w) of the quad's first pixel, then stepped one pixel at a time (one division per quad)
+    const int pq0 = pb + 4 * pbq;
+    int n = pq0 / hw, h = (pq0 - n * hw) / a.Wg, w = pq0 - n * hw - h * a.Wg;
 #pragma unroll
-    for (int i = 0; i < LB; ++i) {
-      const int p = pb + rb + i * RPB;
-      vb[i] = f32x4v{0.f, 0.f, 0.f, 0.f};
-      if (bok && p < p1) {
-        const int n = p / hw, rem = p - n * hw, h = rem / a.Wg, w = rem - h * a.Wg;
+    for (int e = 0; e < 4; ++e) {
+      vb[e] = f32x4v{0.f, 0.f, 0.f, 0.f};
+      if (bok && pq0 + e < p1) {
         const int bh = h * a.s + bkh - a.pad, bw = w * a.s + bkw - a.pad;
         if (bh >= 0 && bh < a.HB && bw >= 0 && bw < a.WB)
-          vb[i] = *reinterpret_cast<const f32x4v*>(a.B + ((long)(n * a.HB + bh) * a.WB + bw) * a.ldb + bn);
+          vb[e] = *reinterpret_cast<const f32x4v*>(a.B + ((long)(n * a.HB + bh) * a.WB + bw) * a.ldb + bn);
+      }
+      if (++w == a.Wg) {
+        w = 0;
+        if (++h == a.Hg) h = 0, ++n;
       }
     }
   };
   auto lstore = [&](int buf) {
+    char* As = lds[buf];
+    char* Bs = lds[buf] + BM * RB;
+    if (has_a) {
 #pragma unroll
-    for (int i = 0; i < LA; ++i) {
-      *reinterpret_cast<f32x4v*>(&As[buf][(ra + i * RPA) * SA + 4 * ca]) = va[i];
-      if (do_bias) bsum += va[i];
+      for (int j = 0; j < 4; ++j) {
+        const int r = 4 * qa + j;
+        *reinterpret_cast<f32x4v*>(As + r * RB + fswzk<8>(r, pa) * 16) = f32x4v{va[0][j], va[1][j], va[2][j], va[3][j]};
+      }
+      if (do_bias) bsum += va[0] + va[1] + va[2] + va[3];
     }
 #pragma unroll
-    for (int i = 0; i < LB; ++i) *reinterpret_cast<f32x4v*>(&Bs[buf][(rb + i * RPB) * SB + 4 * cb]) = vb[i];
+    for (int j = 0; j < 4; ++j) {
+      const int r = 4 * qb + j;
+      *reinterpret_cast<f32x4v*>(Bs + r * RB + fswzk<8>(r, pbq) * 16) = f32x4v{vb[0][j], vb[1][j], vb[2][j], vb[3][j]};
+    }
   };
 
   f32x4_t acc[TM][TN];
@@ -310,20 +324,26 @@ __global__ __launch_bounds__(256) void wgrad_f32_kernel(F32WgradArgs a) {
   for (int s = 0; s < S; ++s) {
     const int buf = s & 1;
     if (s + 1 < S) gload(p0 + (s + 1) * BK);
-    const float* Ab = As[buf] + wm * WM + l16;
-    const float* Bb = Bs[buf] + wn * WN + l16;
+    const char* As = lds[buf];
+    const char* Bs = lds[buf] + BM * RB;
 #pragma unroll
-    for (int ks = 0; ks < BK / 4; ++ks) {
-      const int px = 4 * ks + q;                  // MFMA K index = lane group
-      float af[TM], bf[TN];
+    for (int kb = 0; kb < BK / 16; ++kb) {
+      const int ch = 4 * kb + q;
+      f32x4v af[TM], bf[TN];
 #pragma unroll
-      for (int i = 0; i < TM; ++i) af[i] = Ab[px * SA + i * 16];
+      for (int i = 0; i < TM; ++i) {
+        const int r = wm * WM + i * 16 + l16;
+        af[i] = *reinterpret_cast<const f32x4v*>(As + r * RB + fswzk<8>(r, ch) * 16);
+      }
 #pragma unroll
-      for (int j = 0; j < TN; ++j) bf[j] = Bb[px * SB + j * 16];
+      for (int j = 0; j < TN; ++j) {
+        const int r = wn * WN + j * 16 + l16;
+        bf[j] = *reinterpret_cast<const f32x4v*>(Bs + r * RB + fswzk<8>(r, ch) * 16);
+      }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bf[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < TN; ++j) acc[i][j] = mfma4(af[i], bf[j], acc[i][j]);
     }
     if (s + 1 < S) lstore(buf ^ 1);
     __syncthreads();
@@ -342,36 +362,36 @@ __global__ __launch_bounds__(256) void wgrad_f32_kernel(F32WgradArgs a) {
         a.slab[(((long)split * T + tap) * a.M + m) * a.Nc + n] = acc[i][j][r];
       }
   }
-  if (do_bias) {                                  // rows ra of the A loader -> sum over RPA row groups
-    float* red = As[0];
-    *reinterpret_cast<f32x4v*>(&red[ra * BM + 4 * ca]) = bsum;
+  if (do_bias) {                                  // A micro-block rows pa -> sum over the 8 pixel quads
+    float* red = reinterpret_cast<float*>(lds[0]);
+    if (has_a) *reinterpret_cast<f32x4v*>(&red[pa * BM + 4 * qa]) = bsum;
     __syncthreads();
     if (tid < BM) {
       float sum = 0.f;
 #pragma unroll
-      for (int k = 0; k < RPA; ++k) sum += red[k * BM + tid];
+      for (int k = 0; k < BK / 4; ++k) sum += red[k * BM + tid];
       a.bslab[(long)split * a.M + m0 + tid] = sum;
     }
   }
 }
 
 // 3x3 / stride-1 / pad-1 weight gradient for the shallow levels (B channels NC = 32 / 64, A channels in
-// blocks of 32): a stage is a 2-row x 32-pixel patch; its B halo (4 rows x 34 pixels x NC) is staged in
-// LDS once and all 9 taps read from it, so B is fetched ~1.1x per pixel instead of once per tap-column
-// tile.  Block = 32 A channels x all 9 NC columns: (m-tile, n-tile) pairs over the 4 waves, each pair
-// with its 9 taps in registers.  Stages are enumerated (n, row pair, 32-px segment); a split is a
-// contiguous range of stages, reduced like the generic form.  Operands in natural [pixel][channel] LDS
-// order, scalar MFMA operand reads (row strides 48 / 80 floats: the 4 K lane groups hit 4 distinct
-// 16-bank groups), next stage's loads in registers during the current one.
+// blocks of 32): a stage is a 2-row x 32-pixel patch; its B halo (4 rows x 34 pixels x NC) is fetched
+// once and stored K-contiguous in three column-shifted copies ([kw][halo row][n][32 px], one per kernel
+// column, so every tap's operand is an aligned float4 of 4 pixels), and all 9 taps read from it: B is
+// fetched ~1.2x per pixel instead of once per tap-column tile.  Block = 32 A channels x all 9 NC columns:
+// (m-tile, n-tile) pairs over the 4 waves, each pair with its 9 taps in registers; one ds_read_b128 per 4
+// MFMAs as in the generic form.  Single LDS buffer, the next stage's loads in registers during the
+// current one.  Stages are enumerated (n, row pair, 32-px segment); a split is a contiguous range of
+// stages, reduced like the generic form.
 template <int NC>
 __global__ __launch_bounds__(256) void wgrad3_f32_kernel(F32WgradArgs a) {
-  constexpr int SR = 2, SW = 32, SP = SR * SW, HP = (SR + 2) * (SW + 2);   // stage pixels, halo pixels
-  constexpr int SA = 48, SB = 80;                                          // LDS row strides (floats)
-  constexpr int NT = NC / 16, PW = 2 * NT / 4;                             // n-tiles, (mt, nt) pairs per wave
-  constexpr int CB = NC / 4, LBI = (HP * CB + 255) / 256;                  // B chunks per pixel, loads per thread
-  static_assert(PW >= 1 && 2 * NT % 4 == 0, "tile");
-  __shared__ __attribute__((aligned(16))) float As[2][SP * SA];
-  __shared__ __attribute__((aligned(16))) float Bs[2][HP * SB];
+  constexpr int SR = 2, SW = 32, RB = 128;                      // stage rows, pixels per row, LDS row bytes
+  constexpr int NT = NC / 16, PW = 2 * NT / 4;                  // n-tiles, (mt, nt) pairs per wave
+  constexpr int QN = NC / 4, UB = (SR + 2) * 8 * QN, LBI = UB / 256;   // B micro-blocks (4 ch x 4 shifted px)
+  static_assert(PW >= 1 && 2 * NT % 4 == 0 && UB % 256 == 0, "tile");
+  constexpr int AROWS = SR * 32, BROWS = 3 * (SR + 2) * NC;     // A rows (r, m); B rows (kw, hr, n)
+  __shared__ __attribute__((aligned(16))) char lds[(AROWS + BROWS) * RB];
 
   const int nmb = a.M / 32;
   const int bid = xcd_remap(blockIdx.x, nmb * a.splits);       // a split's m-blocks (same B halo) share an L2
@@ -379,46 +399,59 @@ __global__ __launch_bounds__(256) void wgrad3_f32_kernel(F32WgradArgs a) {
   const int m0 = mb * 32;
   const int segs = a.Wg / SW, per_img = (a.Hg / SR) * segs;
   const int nst = a.N * per_img;
-  const int sps = (int)(a.pix_per_split / SP);
+  const int sps = (int)(a.pix_per_split / (SR * SW));
   const int st0 = split * sps, st1 = st0 + sps < nst ? st0 + sps : nst;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, q = lane >> 4, l16 = lane & 15;
   const int mt = wid & 1, nt0 = (wid >> 1) * PW;
-  const int ca = tid & 7;                    // A loader: channel chunk (fixed per thread), pixel tid / 8 (+ 32)
+  // A micro-blocks (threads < 128): channels m0 + 4 qa, pixel quad pq (row pq / 8, chunk pq % 8)
+  const bool has_a = tid < 128;
+  const int qa = tid & 7, pq = (tid >> 3) & 15;
   const bool do_bias = a.bslab != nullptr;
   f32x4v bsum = f32x4v{0.f, 0.f, 0.f, 0.f};
-  f32x4v va[2], vb[LBI];
+  f32x4v va[4], vb[LBI][6];
 
   auto gload = [&](int st) {
     const int n = st / per_img, rem = st - n * per_img, hp = rem / segs;
     const int h0 = hp * SR, w0 = (rem - hp * segs) * SW;
+    if (has_a) {
+      const long pix = ((long)n * a.Hg + h0 + (pq >> 3)) * a.Wg + w0 + 4 * (pq & 7);
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int px = (tid >> 3) + 32 * i;
-      const long pix = ((long)n * a.Hg + h0 + (px >> 5)) * a.Wg + w0 + (px & 31);
-      va[i] = *reinterpret_cast<const f32x4v*>(a.A + pix * a.lda + m0 + 4 * ca);
+      for (int e = 0; e < 4; ++e) va[e] = *reinterpret_cast<const f32x4v*>(a.A + (pix + e) * a.lda + m0 + 4 * qa);
     }
 #pragma unroll
     for (int i = 0; i < LBI; ++i) {
-      const int idx = tid + 256 * i;
-      const int hpix = idx / CB, ch = idx - hpix * CB;
-      const int hr = hpix / (SW + 2), hc = hpix - hr * (SW + 2);
-      const int ih = h0 - 1 + hr, iw = w0 - 1 + hc;
-      vb[i] = f32x4v{0.f, 0.f, 0.f, 0.f};
-      if (hpix < HP && ih >= 0 && ih < a.HB && iw >= 0 && iw < a.WB)
-        vb[i] = *reinterpret_cast<const f32x4v*>(a.B + ((long)(n * a.HB + ih) * a.WB + iw) * a.ldb + 4 * ch);
+      const int u = tid + 256 * i, nq = u % QN, rest = u / QN, hr = rest >> 3, j = rest & 7;
+      const int ih = h0 - 1 + hr;
+#pragma unroll
+      for (int e = 0; e < 6; ++e) {
+        const int iw = w0 - 1 + 4 * j + e;
+        vb[i][e] = f32x4v{0.f, 0.f, 0.f, 0.f};
+        if (ih >= 0 && ih < a.HB && iw >= 0 && iw < a.WB)
+          vb[i][e] = *reinterpret_cast<const f32x4v*>(a.B + ((long)(n * a.HB + ih) * a.WB + iw) * a.ldb + 4 * nq);
+      }
     }
   };
-  auto lstore = [&](int buf) {
+  auto lstore = [&]() {
+    if (has_a) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      *reinterpret_cast<f32x4v*>(&As[buf][((tid >> 3) + 32 * i) * SA + 4 * ca]) = va[i];
-      if (do_bias) bsum += va[i];
+      for (int c = 0; c < 4; ++c) {
+        const int r = (pq >> 3) * 32 + 4 * qa + c;
+        *reinterpret_cast<f32x4v*>(lds + r * RB + fswzk<8>(r, pq & 7) * 16) = f32x4v{va[0][c], va[1][c], va[2][c], va[3][c]};
+      }
+      if (do_bias) bsum += va[0] + va[1] + va[2] + va[3];
     }
+    char* Bs = lds + AROWS * RB;
 #pragma unroll
     for (int i = 0; i < LBI; ++i) {
-      const int idx = tid + 256 * i;
-      const int hpix = idx / CB, ch = idx - hpix * CB;
-      if (hpix < HP) *reinterpret_cast<f32x4v*>(&Bs[buf][hpix * SB + 4 * ch]) = vb[i];
+      const int u = tid + 256 * i, nq = u % QN, rest = u / QN, hr = rest >> 3, j = rest & 7;
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const int r = (kw * (SR + 2) + hr) * NC + 4 * nq + c;
+          *reinterpret_cast<f32x4v*>(Bs + r * RB + fswzk<8>(r, j) * 16) =
+              f32x4v{vb[i][kw][c], vb[i][kw + 1][c], vb[i][kw + 2][c], vb[i][kw + 3][c]};
+        }
     }
   };
 
@@ -427,29 +460,28 @@ __global__ __launch_bounds__(256) void wgrad3_f32_kernel(F32WgradArgs a) {
   for (int p = 0; p < PW; ++p)
 #pragma unroll
     for (int t = 0; t < 9; ++t) acc[p][t] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  if (st0 < st1) {
-    gload(st0);
-    lstore(0);
-  }
-  __syncthreads();
+  if (st0 < st1) gload(st0);
   for (int st = st0; st < st1; ++st) {
-    const int buf = (st - st0) & 1;
+    lstore();
+    __syncthreads();
     if (st + 1 < st1) gload(st + 1);
-    const float* Ab = As[buf] + mt * 16 + l16;
-    const float* Bb = Bs[buf] + nt0 * 16 + l16;
-#pragma unroll 4
-    for (int ks = 0; ks < SP / 4; ++ks) {
-      const int px = 4 * ks + q, r = px >> 5, c = px & 31;      // MFMA K index = lane group
-      const float af = Ab[px * SA];
+    const char* Bs = lds + AROWS * RB;
 #pragma unroll
-      for (int t = 0; t < 9; ++t) {
-        const int hp = (r + t / 3) * (SW + 2) + c + t % 3;
+    for (int r = 0; r < SR; ++r)
 #pragma unroll
-        for (int p = 0; p < PW; ++p)
-          acc[p][t] = __builtin_amdgcn_mfma_f32_16x16x4f32(af, Bb[hp * SB + p * 16], acc[p][t], 0, 0, 0);
+      for (int cb = 0; cb < 2; ++cb) {
+        const int ch = 4 * cb + q;
+        const int ra = r * 32 + mt * 16 + l16;
+        const f32x4v af = *reinterpret_cast<const f32x4v*>(lds + ra * RB + fswzk<8>(ra, ch) * 16);
+#pragma unroll
+        for (int t = 0; t < 9; ++t)
+#pragma unroll
+          for (int p = 0; p < PW; ++p) {
+            const int rb = ((t % 3) * (SR + 2) + r + t / 3) * NC + (nt0 + p) * 16 + l16;
+            const f32x4v bf = *reinterpret_cast<const f32x4v*>(Bs + rb * RB + fswzk<8>(rb, ch) * 16);
+            acc[p][t] = mfma4(af, bf, acc[p][t]);
+          }
       }
-    }
-    if (st + 1 < st1) lstore(buf ^ 1);
     __syncthreads();
   }
   // slab[split][tap][m][n]: lane holds rows (m) 4 q + r of column l16
@@ -462,14 +494,14 @@ __global__ __launch_bounds__(256) void wgrad3_f32_kernel(F32WgradArgs a) {
         const int m = m0 + mt * 16 + 4 * q + r, n = (nt0 + p) * 16 + l16;
         a.slab[(((long)split * 9 + t) * a.M + m) * NC + n] = acc[p][t][r];
       }
-  if (do_bias) {                             // 32 pixel groups x 32 channels
-    float* red = As[0];
-    *reinterpret_cast<f32x4v*>(&red[(tid >> 3) * 32 + 4 * ca]) = bsum;
+  if (do_bias) {                             // 16 pixel quads x 32 channels
+    float* red = reinterpret_cast<float*>(lds);
+    if (has_a) *reinterpret_cast<f32x4v*>(&red[pq * 32 + 4 * qa]) = bsum;
     __syncthreads();
     if (tid < 32) {
       float sum = 0.f;
 #pragma unroll
-      for (int k = 0; k < 32; ++k) sum += red[k * 32 + tid];
+      for (int k = 0; k < 16; ++k) sum += red[k * 32 + tid];
       a.bslab[(long)split * a.M + m0 + tid] = sum;
     }
   }
@@ -640,8 +672,8 @@ static unsigned egrid(long n) { return (unsigned)(n / 256 + 1 < 8192 ? n / 256 +
 
 // Eligible: Cs % 4 == 0 (a float4 chunk never straddles a tap), Kpad % 16 == 0, Kpad >= KH*KW*Cs,
 // Ngemm % 32 == 0, 16-B aligned strides; mode 1 also Cout % 4 == 0.
-// Tiles: 128 px x 128 ch (Ngemm % 128 == 0, 32-deep K-steps), 128 x 64 (Ngemm % 64 == 0), else 128 x 32;
-// 32-deep K-steps when Kpad % 32 == 0.
+// Tiles (32-deep K-steps when Kpad % 32 == 0): Ngemm % 128 == 0 -> 128 px x 128 ch (K32); Ngemm % 64 == 0 ->
+// 128 x 64; else 128 x 32.  (256-pixel tiles for Ngemm 32 / 64 measured 5-17 % slower: 72-80 KB of LDS.)
 DPA_API int dpa_igemm_f32(const F32ConvArgs* args, hipStream_t st) {
   const F32ConvArgs& a = *args;
   if ((a.Cs & 3) || (a.Kpad % F_BK) || a.Kpad < a.KH * a.KW * a.Cs || (a.Ngemm & 31) || (a.ldx & 3) || (a.ldy & 3) ||

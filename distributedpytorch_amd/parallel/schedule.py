@@ -181,20 +181,30 @@ def stage_costs(table: dict, mb: int, M: int, cuts: Sequence[int], link_gbs: flo
     row = table["per_mb"][str(mb)]
     big = table["per_mb"].get(str(mb * M))
     S = len(cuts) - 1
+    unit_space = bool(table.get("unit_space"))
+    if unit_space:       # a block whose two halves share a stage costs its measured whole-block time
+        bt = table["block_table"]
+        brow, bbig = bt["per_mb"][str(mb)], bt["per_mb"].get(str(mb * M))
+        nbk = len(brow["fwd"])
     costs = []
     for s in range(S):
-        blocks = range(cuts[s], cuts[s + 1])
-        f = sum(row["fwd"][b] for b in blocks)
-        if defer:
-            b = sum(row["bwd_nowgrad"][i] for i in blocks)
-            if big is not None:
-                wg = sum(big["bwd"][i] - big["bwd_nowgrad"][i] for i in blocks)
+        items, u = [], cuts[s]
+        while u < cuts[s + 1]:
+            if unit_space and u % 2 == 0 and u + 1 < cuts[s + 1] and u // 2 < nbk - 1:
+                items.append((brow, bbig, u // 2))
+                u += 2
             else:
-                wg = M * sum(row["bwd"][i] - row["bwd_nowgrad"][i] for i in blocks)
+                items.append((row, big, u))
+                u += 1
+        f = sum(r["fwd"][i] for r, _, i in items)
+        if defer:
+            b = sum(r["bwd_nowgrad"][i] for r, _, i in items)
+            wg = sum((bg["bwd"][i] - bg["bwd_nowgrad"][i]) if bg is not None else M * (r["bwd"][i] - r["bwd_nowgrad"][i])
+                     for r, bg, i in items)
         else:
-            b = sum(row["bwd"][i] for i in blocks)
+            b = sum(r["bwd"][i] for r, _, i in items)
             wg = 0.0
-        opt = sum(table.get("opt_ms", [0.0] * len(row["fwd"]))[i] for i in blocks)
+        opt = sum(table.get("opt_ms", [0.0] * len(row["fwd"]))[i] for i in range(cuts[s], cuts[s + 1]))
         costs.append(StageCost(f, b, max(wg, 0.0), opt))
     bfun = unit_boundary_bytes if table.get("unit_space") else boundary_bytes
     for name, (pb, cb, nbytes) in bfun(depth, widths, mid_width, mb, h, w).items():

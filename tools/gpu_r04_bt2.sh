@@ -8,4 +8,4 @@ timeout -k 10 600 python -u tools/block_times.py --model unet --img 512 --mbs 8 
 tail -2 $O/bt_unet.log
 timeout -k 10 600 python -u tools/block_times.py --model unet-xl --img 1024 --mbs 1 2 4 8 16 --out $O/block_times_unetxl_1024.json > $O/bt_xl.log 2>&1 || { echo bt xl failed; tail $O/bt_xl.log; exit 1; }
 tail -2 $O/bt_xl.log
-bash tools/gpu_r04_knobs.sh
+[ -z "$SKIP_KNOBS" ] && bash tools/gpu_r04_knobs.sh; true
