@@ -241,12 +241,19 @@ def test_conv_bn_stats_fused_in_stream_epilogue(hip_lib, N, H, W, Cin, Cout):
         y = torch.empty_like(z)
         saved = K.bn_fwd(z, y, bn, train=True, stats=stats)
         torch.cuda.synchronize()
-        outs.append((y.float().cpu(), saved.cpu(), bn.running_mean.cpu(), bn.running_var.cpu()))
-    (y1, s1, m1, v1), (y0, s0, m0, v0) = outs
-    # the sums are taken in a different order: at most a bf16 rounding flip apart
+        # each path's statistics are exact for the z it produced (fp64 reference over that z)
+        zd = z.double().reshape(-1, Cout).cpu()
+        mean, var = zd.mean(0), zd.var(0, unbiased=False)
+        assert torch.allclose(saved.cpu()[:Cout].double(), mean, rtol=1e-5, atol=1e-6)
+        assert torch.allclose(saved.cpu()[Cout:].double(), (var + bn.eps).rsqrt(), rtol=1e-3, atol=1e-6)
+        outs.append((y.float().cpu(), saved.cpu(), bn.running_mean.cpu(), bn.running_var.cpu(), float(zd.abs().max())))
+    (y1, s1, m1, v1, _), (y0, s0, m0, v0, zmax) = outs
+    # the fused and unfused paths may run different conv kernels (accumulation order): their z are at most
+    # bf16 rounding flips apart, which move a mean over few pixels by ~ulp(|z|) / P
+    tol = 2.0 ** -7 * zmax / (N * H * W) * 4
     assert _rel(y1, y0) < 1e-2
-    assert torch.allclose(s1, s0, rtol=1e-5, atol=1e-6) and torch.allclose(m1, m0, rtol=1e-5, atol=1e-6)
-    assert torch.allclose(v1, v0, rtol=1e-5, atol=1e-6)
+    assert torch.allclose(s1, s0, rtol=1e-3, atol=tol) and torch.allclose(m1, m0, rtol=1e-3, atol=tol)
+    assert torch.allclose(v1, v0, rtol=1e-3, atol=tol)
     y_ref = F.relu(bn_ref(F.conv2d(x, w, b, padding=1))).permute(0, 2, 3, 1)
     assert _rel(y1, y_ref) < 3e-2
 
