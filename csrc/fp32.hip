@@ -561,6 +561,39 @@ __global__ __launch_bounds__(256) void maxpool2_bwd_f32_kernel(const float* __re
   }
 }
 
+// encoder DoubleConv output gradient in one pass: ge = (y > 0) * (gs + [code == window position] gp) --
+// the skip gradient (gs, pixel stride lds, may be null), the max-pool backward and the ReLU backward
+// that autograd would run as three passes (scatter, add, mask); NHWC fp32, 4 channels per thread
+__global__ __launch_bounds__(256) void enc_out_bwd_f32_kernel(const float* __restrict__ gs, int lds,
+                                                              const float* __restrict__ gp,
+                                                              const unsigned char* __restrict__ code,
+                                                              const float* __restrict__ y, float* __restrict__ ge,
+                                                              int N, int H, int W, int C) {
+  const int Ho = H >> 1, Wo = W >> 1, C4 = C >> 2;
+  const long tot = (long)N * H * W * C4;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < tot; i += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C4) * 4;
+    const long pix = i / C4;
+    const int w = (int)(pix % W), h = (int)((pix / W) % H), n = (int)(pix / ((long)W * H));
+    f32x4v v = gs ? *reinterpret_cast<const f32x4v*>(gs + pix * lds + c) : f32x4v{0.f, 0.f, 0.f, 0.f};
+    const int ho = h >> 1, wo = w >> 1;
+    if (gp && ho < Ho && wo < Wo) {
+      const long o = (((long)n * Ho + ho) * Wo + wo) * C + c;
+      const f32x4v g = *reinterpret_cast<const f32x4v*>(gp + o);
+      const unsigned k = (unsigned)((h & 1) * 2 + (w & 1));
+      const uchar4 cd = *reinterpret_cast<const uchar4*>(code + o);
+      v[0] += cd.x == k ? g[0] : 0.f;
+      v[1] += cd.y == k ? g[1] : 0.f;
+      v[2] += cd.z == k ? g[2] : 0.f;
+      v[3] += cd.w == k ? g[3] : 0.f;
+    }
+    const f32x4v yv = *reinterpret_cast<const f32x4v*>(y + pix * C + c);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = yv[e] > 0.f ? v[e] : 0.f;
+    *reinterpret_cast<f32x4v*>(ge + pix * C + c) = v;
+  }
+}
+
 // segmentation head forward: z = b + sum_c w[c] y[p][c], p = sigmoid(z); per-block partial sums of
 // [BCE(p, t), p * [t == 1], p, [t == 1]] (reference utils/utils.py:9-25, log clamped at -100 like
 // torch's BCELoss) -> slab[block][4]; optional probabilities out
@@ -650,14 +683,14 @@ __global__ __launch_bounds__(256) void nchw_to_nhwc4_f32_kernel(const float* __r
 
 // per-channel sums of an NHWC tensor into slab[block][C] (bias gradient of the transposed conv): block b
 // sums pixels b, b + gridDim.x, ... ; thread (c, r) takes channel c (+ 256 k for C > 256) of row group r
-__global__ __launch_bounds__(256) void channel_sum_f32_kernel(const float* __restrict__ g, long P, int C,
+__global__ __launch_bounds__(256) void channel_sum_f32_kernel(const float* __restrict__ g, long P, int C, int ld,
                                                               float* __restrict__ slab) {
   __shared__ float red[256];
   const int R = C < 256 ? 256 / C : 1;               // host: C < 256 divides 256
   const int r = threadIdx.x / (C < 256 ? C : 256);
   for (int c = threadIdx.x % (C < 256 ? C : 256); c < C; c += 256) {
     float s = 0.f;
-    for (long p = (long)blockIdx.x * R + r; p < P; p += (long)gridDim.x * R) s += g[p * C + c];
+    for (long p = (long)blockIdx.x * R + r; p < P; p += (long)gridDim.x * R) s += g[p * ld + c];
     __syncthreads();
     red[threadIdx.x] = s;
     __syncthreads();
@@ -745,6 +778,14 @@ DPA_API int dpa_maxpool2_bwd_f32(const float* g, const unsigned char* code, floa
   return (int)hipGetLastError();
 }
 
+DPA_API int dpa_enc_out_bwd_f32(const float* gs, int lds, const float* gp, const unsigned char* code, const float* y,
+                                float* ge, int N, int H, int W, int C, hipStream_t st) {
+  if (H < 1 || W < 1 || (C & 3) || (gs && (lds & 3)) || (gp && (H < 2 || W < 2))) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(enc_out_bwd_f32_kernel, dim3(egrid((long)N * H * W * (C / 4))), dim3(256), 0, st, gs, lds, gp, code, y,
+                     ge, N, H, W, C);
+  return (int)hipGetLastError();
+}
+
 // head forward over P pixels of C channels: slab needs blocks * 4 floats (blocks = dpa_head_f32_blocks)
 DPA_API int dpa_head_f32_blocks(long long P) { return (int)(P / 256 + 1 < 1024 ? P / 256 + 1 : 1024); }
 
@@ -775,8 +816,8 @@ DPA_API int dpa_nchw_to_nhwc4_f32(const float* x, float* y, int N, int C, long l
 }
 
 // slab rows = dpa_head_f32_blocks(P) (same grid policy)
-DPA_API int dpa_channel_sum_f32(const float* g, long long P, int C, float* slab, hipStream_t st) {
+DPA_API int dpa_channel_sum_f32(const float* g, long long P, int C, int ld, float* slab, hipStream_t st) {
   if (C < 1 || (C < 256 && 256 % C) || (C > 256 && C % 256)) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(channel_sum_f32_kernel, dim3(dpa_head_f32_blocks(P)), dim3(256), 0, st, g, (long)P, C, slab);
+  hipLaunchKernelGGL(channel_sum_f32_kernel, dim3(dpa_head_f32_blocks(P)), dim3(256), 0, st, g, (long)P, C, ld, slab);
   return (int)hipGetLastError();
 }

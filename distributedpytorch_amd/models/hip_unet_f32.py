@@ -131,6 +131,33 @@ class _DoubleConvReLU(torch.autograd.Function):
         return gx, gw1, gb1, gw2, gb2, None
 
 
+class _EncBlock(torch.autograd.Function):
+    """Encoder block: DoubleConv + 2x2 max-pool (reference Encoder, model/unet_parts.py:20-40) -> (skip, pooled).
+    Backward: the skip gradient, the pool backward and the last ReLU backward form the second conv's
+    pre-activation gradient in one pass (F32.enc_out_bwd); the inner ReLU as in :class:`_DoubleConvReLU`."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2, cs: int):
+        a = _conv_fwd(x, w1, b1, cs)
+        y = _conv_fwd(a, w2, b2, a.shape[3])
+        pooled, code = F32.maxpool2(y)
+        ctx.cs = cs
+        ctx.save_for_backward(x, w1, a, w2, y, code)
+        return y, pooled
+
+    @staticmethod
+    def backward(ctx, gs, gp):
+        x, w1, a, w2, y, code = ctx.saved_tensors
+        if gs is not None and not F32.nhwc_ok(gs):
+            gs = gs.contiguous()
+        ge2 = F32.enc_out_bwd(gs, None if gp is None else _dense(gp), code, y)
+        ge1 = _conv_dgrad(ge2, w2, a.shape[3], mask=a)
+        gw2, gb2 = _conv_wgrad(ge2, a, w2, a.shape[3])
+        gx = _conv_dgrad(ge1, w1, ctx.cs) if ctx.needs_input_grad[0] else None
+        gw1, gb1 = _conv_wgrad(ge1, x, w1, ctx.cs)
+        return gx, gw1, gb1, gw2, gb2, None
+
+
 class _Deconv(torch.autograd.Function):
     """y = ConvTranspose2d(k2, s2)(x) + b, NHWC fp32 (reference model/unet_parts.py:51-54)."""
 
@@ -160,6 +187,43 @@ class _Deconv(torch.autograd.Function):
         gb = torch.zeros(co, dtype=torch.float32, device=x.device)
         F32.channel_sum(gy, gb)
         return gx, gw, gb
+
+
+class _UpCat(torch.autograd.Function):
+    """[skip ‖ ConvTranspose2d(k2, s2)(x) + b] in one NHWC buffer (reference concat order, skip first,
+    model/unet_parts.py:58-59): the transposed conv's scatter epilogue stores straight into the upper
+    channel half; the backward reads both gradient halves in place (no split copies)."""
+
+    @staticmethod
+    def forward(ctx, x, skip, weight, bias):
+        N, h, w, ci = x.shape
+        co, C = weight.shape[1], skip.shape[3]
+        buf = torch.empty(N, 2 * h, 2 * w, C + co, dtype=torch.float32, device=x.device)
+        buf[..., :C].copy_(skip)
+        F32.igemm(x, F32.pack_deconv_fwd(weight), buf[..., C:], Ngemm=4 * co, Kpad=ci, KH=1, KW=1, stride=1, pad=0,
+                  Cs=ci, out_grid=(N, h, w), bias=bias.detach(), mode=1, Cout=co)
+        ctx.C = C
+        ctx.save_for_backward(x, weight)
+        return buf
+
+    @staticmethod
+    def backward(ctx, gbuf):
+        x, weight = ctx.saved_tensors
+        N, h, w, ci = x.shape
+        co, C = weight.shape[1], ctx.C
+        if not F32.nhwc_ok(gbuf):
+            gbuf = gbuf.contiguous()
+        gs, gy = gbuf[..., :C], gbuf[..., C:]
+        gx = None
+        if ctx.needs_input_grad[0]:
+            gx = torch.empty(N, h, w, ci, dtype=torch.float32, device=x.device)
+            F32.igemm(gy, F32.pack_deconv_dgrad(weight), gx, Ngemm=ci, Kpad=4 * co, KH=2, KW=2, stride=2, pad=0, Cs=co,
+                      out_grid=(N, h, w))
+        gw = torch.zeros(ci, co, 2, 2, dtype=torch.float32, device=x.device)
+        F32.wgrad(x, gy, gw, None, KH=2, KW=2, s=2, pad=0)
+        gb = torch.zeros(co, dtype=torch.float32, device=x.device)
+        F32.channel_sum(gy, gb)
+        return gx, gs, gw, gb
 
 
 class _MaxPool(torch.autograd.Function):
@@ -219,8 +283,9 @@ class HipF32Blocks:
 
     def enc(self, l: int, x):
         c1, c2 = self.model.encoder.blocks()[l].convs()
-        s = self._double(c1, c2, _v(x), 4 if l == 0 else None)
-        return _o(s), _o(_MaxPool.apply(s))
+        xv = _v(x)
+        s, p = _EncBlock.apply(xv, c1.weight, c1.bias, c2.weight, c2.bias, 4 if l == 0 else xv.shape[3])
+        return _o(s), _o(p)
 
     def mid(self, x):
         c1, c2 = self.model.mid.convs()
@@ -250,8 +315,10 @@ class HipF32Blocks:
 
     def _up_cat(self, i: int, x, skip):
         d = self.model.decoder.ups()[i]
-        up = _Deconv.apply(_v(x), d.weight, d.bias)
-        sk = _v(skip)
+        xv, sk = _v(x), _v(skip)
+        if tuple(sk.shape[1:3]) == (2 * xv.shape[1], 2 * xv.shape[2]) and sk.shape[3] % 4 == 0:
+            return _UpCat.apply(xv, sk, d.weight, d.bias)
+        up = _Deconv.apply(xv, d.weight, d.bias)
         h2, w2 = up.shape[1:3]
         if tuple(sk.shape[1:3]) != (h2, w2):
             top, left = int(round((sk.shape[1] - h2) / 2.0)), int(round((sk.shape[2] - w2) / 2.0))

@@ -55,6 +55,15 @@ def nhwc(t: torch.Tensor, name: str) -> Tuple[int, int, int, int, int]:
     return N, H, W, C, sW
 
 
+def nhwc_ok(t: torch.Tensor) -> bool:
+    """True when :func:`nhwc` accepts ``t`` (dense or channel-sliced NHWC, 16-byte aligned)."""
+    try:
+        nhwc(t, "")
+        return True
+    except AssertionError:
+        return False
+
+
 def round_up(x: int, m: int) -> int:
     return (x + m - 1) // m * m
 
@@ -193,6 +202,23 @@ def maxpool2_bwd(g: torch.Tensor, code: torch.Tensor, H: int, W: int) -> torch.T
     return dx
 
 
+def enc_out_bwd(gs: Optional[torch.Tensor], gp: Optional[torch.Tensor], code: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+    """(y > 0) * (gs + maxpool2_bwd(gp, code)) in one pass: the gradient entering an encoder DoubleConv's
+    last ReLU from its skip output (``gs``: NHWC, channel slice allowed) and its pooled output (``gp``)."""
+    N, H, W, C, ld = nhwc(y, "enc_out_bwd_f32.y")
+    assert ld == C and y.is_contiguous() and C % 4 == 0
+    lds = 0
+    if gs is not None:
+        assert tuple(gs.shape) == (N, H, W, C)
+        _, _, _, _, lds = nhwc(gs, "enc_out_bwd_f32.gs")
+    if gp is not None:
+        assert gp.is_contiguous() and code.shape == gp.shape and tuple(gp.shape) == (N, H // 2, W // 2, C)
+    ge = torch.empty_like(y)
+    _check(_lib.lib().dpa_enc_out_bwd_f32(_p(gs), c_int(lds), _p(gp), _p(code), _p(y), _p(ge), c_int(N), c_int(H),
+                                         c_int(W), c_int(C), _st(y)), "enc_out_bwd_f32")
+    return ge
+
+
 def head_fwd(y: torch.Tensor, w: torch.Tensor, b: torch.Tensor, t: Optional[torch.Tensor], want_probs: bool = False):
     """Segmentation head on NHWC fp32 y: (S[4] partial sums or None, probabilities [P] or None)."""
     N, H, W, C, ld = nhwc(y, "head_f32.y")
@@ -242,12 +268,11 @@ def input_nhwc4(x: torch.Tensor) -> torch.Tensor:
 
 
 def channel_sum(g: torch.Tensor, out: torch.Tensor) -> None:
-    """out[c] += sum over pixels of NHWC fp32 g (dense)."""
+    """out[c] += sum over pixels of NHWC fp32 g (channel slice allowed)."""
     N, H, W, C, ld = nhwc(g, "channel_sum_f32.g")
-    assert ld == C and g.is_contiguous()
     P = N * H * W
     L = _lib.lib()
     blocks = L.dpa_head_f32_blocks(c_ll(P))
     slab = torch.empty(blocks * C, dtype=torch.float32, device=g.device)
-    _check(L.dpa_channel_sum_f32(_p(g), c_ll(P), c_int(C), _p(slab), _st(g)), "channel_sum_f32")
+    _check(L.dpa_channel_sum_f32(_p(g), c_ll(P), c_int(C), c_int(ld), _p(slab), _st(g)), "channel_sum_f32")
     out.view(-1).add_(slab.view(blocks, C).sum(0))

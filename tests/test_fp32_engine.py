@@ -37,6 +37,51 @@ def test_conv_relu_fwd_bwd(hip_lib, N, H, W, Cin, Cout, cs):
     assert _rel(gx[..., :Cin].permute(0, 3, 1, 2), gx_ref) < 1e-5
 
 
+@pytest.mark.parametrize("N,h,w,Cin,Cout,C", [(2, 8, 12, 64, 32, 32), (1, 4, 4, 512, 256, 256)])
+def test_up_cat(hip_lib, N, h, w, Cin, Cout, C):
+    """[skip ‖ ConvTranspose2d(x)] in one buffer (deconv epilogue into the upper half) vs torch, forward and
+    every gradient (the two gradient halves are read in place)."""
+    from distributedpytorch_amd.models.hip_unet_f32 import _UpCat
+    torch.manual_seed(Cin + C)
+    x = torch.randn(N, Cin, h, w, device="cuda").requires_grad_(True)
+    sk = torch.randn(N, C, 2 * h, 2 * w, device="cuda").requires_grad_(True)
+    wt = (torch.randn(Cin, Cout, 2, 2, device="cuda") / Cin ** 0.5).requires_grad_(True)
+    b = (torch.randn(Cout, device="cuda") * 0.1).requires_grad_(True)
+    ref = torch.cat([sk, F.conv_transpose2d(x, wt, b, stride=2)], dim=1)
+    g = torch.randn_like(ref)
+    refs = torch.autograd.grad(ref, (x, sk, wt, b), g)
+    xn = x.detach().permute(0, 2, 3, 1).contiguous().requires_grad_(True)
+    skn = sk.detach().permute(0, 2, 3, 1).contiguous().requires_grad_(True)
+    y = _UpCat.apply(xn, skn, wt, b)
+    assert _rel(y.permute(0, 3, 1, 2), ref) < 1e-5
+    gx, gsk, gw, gb = torch.autograd.grad(y, (xn, skn, wt, b), g.permute(0, 2, 3, 1).contiguous())
+    assert _rel(gx.permute(0, 3, 1, 2), refs[0]) < 1e-5 and _rel(gsk.permute(0, 3, 1, 2), refs[1]) == 0.0
+    assert _rel(gw, refs[2]) < 1e-5 and _rel(gb, refs[3]) < 1e-5
+
+
+@pytest.mark.parametrize("N,H,W,C,strided", [(2, 6, 8, 32, True), (1, 7, 9, 64, False), (3, 4, 4, 4, True)])
+def test_enc_out_bwd(hip_lib, N, H, W, C, strided):
+    """(y > 0) * (skip grad + max-pool backward) in one pass vs autograd of relu -> (identity, max_pool2d)."""
+    from distributedpytorch_amd.ops import fp32 as F32
+    torch.manual_seed(N * H + C)
+    z = torch.randn(N, C, H, W, device="cuda", requires_grad=True)
+    y = torch.relu(z)
+    p = F.max_pool2d(y, 2)
+    gs = torch.randn_like(y)
+    gp = torch.randn_like(p)
+    (gz_ref,) = torch.autograd.grad((y, p), (z,), (gs, gp))
+    yn = y.detach().permute(0, 2, 3, 1).contiguous()
+    pn, code = F32.maxpool2(yn)
+    assert _rel(pn.permute(0, 3, 1, 2), p) == 0.0
+    gsn = gs.permute(0, 2, 3, 1).contiguous()
+    if strided:       # the skip gradient as a channel slice of a wider buffer (cat backward)
+        wide = torch.randn(N, H, W, 2 * C, device="cuda")
+        wide[..., :C] = gsn
+        gsn = wide[..., :C]
+    ge = F32.enc_out_bwd(gsn, gp.permute(0, 2, 3, 1).contiguous(), code, yn)
+    assert _rel(ge.permute(0, 3, 1, 2), gz_ref) < 1e-6
+
+
 @pytest.mark.parametrize("N,H,W,Nc,M", [(2, 8, 64, 32, 32), (1, 6, 32, 64, 96), (3, 2, 96, 64, 64), (1, 4, 32, 32, 64)])
 def test_wgrad_halo_form(hip_lib, N, H, W, Nc, M):
     """3x3 weight gradient with the input halo staged per 2 x 32-pixel patch (wgrad3_f32_kernel) and the
