@@ -716,7 +716,10 @@ DPA_API int dpa_igemm_f32(const F32ConvArgs* args, hipStream_t st) {
   const bool k32 = a.Kpad % 32 == 0;
   if (a.Ngemm % 128 == 0 && k32) {
     const dim3 grid((unsigned)(((M + 127) / 128) * (a.Ngemm / 128)));
-    hipLaunchKernelGGL((igemm_f32_kernel<128, 128, 2, 32>), grid, dim3(256), 0, st, a);
+    // 16-deep K-steps (32 KB of LDS, 3 waves / SIMD) measured faster for a single 128-wide GEMM-N tile and
+    // the transposed conv's scatter; 32-deep for the wider layers (profiles/f32_kbench_b16_512_r04.txt)
+    if (a.Ngemm == 128 || a.mode == 1) hipLaunchKernelGGL((igemm_f32_kernel<128, 128, 2, 16>), grid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((igemm_f32_kernel<128, 128, 2, 32>), grid, dim3(256), 0, st, a);
   } else if (a.Ngemm % 64 == 0) {
     const dim3 grid((unsigned)(((M + 127) / 128) * (a.Ngemm / 64)));
     if (k32) hipLaunchKernelGGL((igemm_f32_kernel<128, 64, 2, 32>), grid, dim3(256), 0, st, a);
