@@ -147,3 +147,23 @@ def test_unit_space_cuts_inside_doubleconv():
     assert [r["step_ms"] for r in again if r["microbatches"] == best["microbatches"]] == [best["step_ms"]]
     whole = max(plan(t, 2, 4, link_gbs=1e9), key=lambda r: r["img_s"])
     assert best["step_ms"] <= whole["step_ms"] + 1e-9     # finer cuts can only help the balance
+
+
+def test_unit_space_prices_uncut_blocks_whole():
+    """A block whose two halves share a stage costs its measured whole-block time; only a block that a
+    cut splits is priced from its half-block units (the halves lose the block's fusions, so their sum
+    is larger than the whole)."""
+    from distributedpytorch_amd.parallel.schedule import unit_table
+    t = _table()
+    for row in t["per_mb"].values():       # halves 30 % dearer than the whole block
+        row["units"] = {k: [0.65 * v for v in row[k][:-1] for _ in (0, 1)] + [row[k][-1]]
+                        for k in ("fwd", "bwd", "bwd_nowgrad")}
+    ut = unit_table(t)
+    whole = stage_costs(t, 1, 4, [0, 3, 6], defer=False)
+    units = stage_costs(ut, 1, 4, [0, 6, 11], defer=False)           # the same partition in unit space
+    assert [c.fwd for c in units] == pytest.approx([c.fwd for c in whole])
+    assert [c.bwd for c in units] == pytest.approx([c.bwd for c in whole])
+    split = stage_costs(ut, 1, 4, [0, 5, 11], defer=False)           # cut inside block 2 (2.5)
+    f = t["per_mb"]["1"]["fwd"]
+    assert split[0].fwd == pytest.approx(f[0] + f[1] + 0.65 * f[2])
+    assert split[1].fwd == pytest.approx(0.65 * f[2] + f[3] + f[4] + f[5])
