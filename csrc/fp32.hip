@@ -61,6 +61,10 @@ __device__ __forceinline__ int fswzk(int row, int chunk) {
   else return chunk ^ ((row >> 1) & 7);
 }
 
+// weight-gradient operand rows: additionally XOR row bits 4..6, so the loader's rotated 4-row micro-block
+// stores (rows 4q + (j + q) % 4 across a 16-lane group) are conflict-free as well as the 16-row reads
+__device__ __forceinline__ int wswz(int row, int chunk) { return chunk ^ (((row >> 1) ^ (row >> 4)) & 7); }
+
 __device__ __forceinline__ f32x4_t mfma4(const f32x4v& a, const f32x4v& b, f32x4_t c) {
   c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0], b[0], c, 0, 0, 0);
   c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[1], b[1], c, 0, 0, 0);
@@ -294,21 +298,28 @@ __global__ __launch_bounds__(256) void wgrad_f32_kernel(F32WgradArgs a) {
       }
     }
   };
+  // column jj of a 4 x 4 micro-block (selects, no dynamic register indexing)
+  auto colv = [](const f32x4v (&v)[4], int jj) {
+    f32x4v o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = jj == 0 ? v[e][0] : jj == 1 ? v[e][1] : jj == 2 ? v[e][2] : v[e][3];
+    return o;
+  };
   auto lstore = [&](int buf) {
     char* As = lds[buf];
     char* Bs = lds[buf] + BM * RB;
     if (has_a) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int r = 4 * qa + j;
-        *reinterpret_cast<f32x4v*>(As + r * RB + fswzk<8>(r, pa) * 16) = f32x4v{va[0][j], va[1][j], va[2][j], va[3][j]};
+      for (int j = 0; j < 4; ++j) {           // rotated by the channel quad: both row parities per store
+        const int jj = (j + qa) & 3, r = 4 * qa + jj;
+        *reinterpret_cast<f32x4v*>(As + r * RB + wswz(r, pa) * 16) = colv(va, jj);
       }
       if (do_bias) bsum += va[0] + va[1] + va[2] + va[3];
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int r = 4 * qb + j;
-      *reinterpret_cast<f32x4v*>(Bs + r * RB + fswzk<8>(r, pbq) * 16) = f32x4v{vb[0][j], vb[1][j], vb[2][j], vb[3][j]};
+      const int jj = (j + qb) & 3, r = 4 * qb + jj;
+      *reinterpret_cast<f32x4v*>(Bs + r * RB + wswz(r, pbq) * 16) = colv(vb, jj);
     }
   };
 
@@ -333,12 +344,12 @@ __global__ __launch_bounds__(256) void wgrad_f32_kernel(F32WgradArgs a) {
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         const int r = wm * WM + i * 16 + l16;
-        af[i] = *reinterpret_cast<const f32x4v*>(As + r * RB + fswzk<8>(r, ch) * 16);
+        af[i] = *reinterpret_cast<const f32x4v*>(As + r * RB + wswz(r, ch) * 16);
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int r = wn * WN + j * 16 + l16;
-        bf[j] = *reinterpret_cast<const f32x4v*>(Bs + r * RB + fswzk<8>(r, ch) * 16);
+        bf[j] = *reinterpret_cast<const f32x4v*>(Bs + r * RB + wswz(r, ch) * 16);
       }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
@@ -706,7 +717,8 @@ static unsigned egrid(long n) { return (unsigned)(n / 256 + 1 < 8192 ? n / 256 +
 // Eligible: Cs % 4 == 0 (a float4 chunk never straddles a tap), Kpad % 16 == 0, Kpad >= KH*KW*Cs,
 // Ngemm % 32 == 0, 16-B aligned strides; mode 1 also Cout % 4 == 0.
 // Tiles (32-deep K-steps when Kpad % 32 == 0): Ngemm % 128 == 0 -> 128 px x 128 ch (K32); Ngemm % 64 == 0 ->
-// 128 x 64; else 128 x 32.  (256-pixel tiles for Ngemm 32 / 64 measured 5-17 % slower: 72-80 KB of LDS.)
+// 128 x 64; else 128 x 32; Ngemm 64 over <= 64 / Ngemm 32 over 32 input channels: 256 x Ngemm with 16-deep
+// K-steps (the 32-deep 256-pixel form measured 5-17 % slower: 72-80 KB of LDS).
 DPA_API int dpa_igemm_f32(const F32ConvArgs* args, hipStream_t st) {
   const F32ConvArgs& a = *args;
   if ((a.Cs & 3) || (a.Kpad % F_BK) || a.Kpad < a.KH * a.KW * a.Cs || (a.Ngemm & 31) || (a.ldx & 3) || (a.ldy & 3) ||
@@ -714,7 +726,12 @@ DPA_API int dpa_igemm_f32(const F32ConvArgs* args, hipStream_t st) {
     return (int)hipErrorInvalidValue;
   const long M = (long)a.N * a.Ho * a.Wo;
   const bool k32 = a.Kpad % 32 == 0;
-  if (a.Ngemm % 128 == 0 && k32) {
+  if (k32 && a.mode == 0 && ((a.Ngemm == 64 && a.Cs <= 64) || (a.Ngemm == 32 && a.Cs == 32))) {
+    // narrow GEMM-N over few input channels: 256-pixel tiles, 16-deep K-steps (36-40 KB LDS)
+    const dim3 grid((unsigned)((M + 255) / 256));
+    if (a.Ngemm == 64) hipLaunchKernelGGL((igemm_f32_kernel<256, 64, 4, 16>), grid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((igemm_f32_kernel<256, 32, 4, 16>), grid, dim3(256), 0, st, a);
+  } else if (a.Ngemm % 128 == 0 && k32) {
     const dim3 grid((unsigned)(((M + 127) / 128) * (a.Ngemm / 128)));
     // 16-deep K-steps (32 KB of LDS, 3 waves / SIMD) measured faster for a single 128-wide GEMM-N tile and
     // the transposed conv's scatter; 32-deep for the wider layers (profiles/f32_kbench_b16_512_r04.txt)
