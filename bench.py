@@ -67,13 +67,13 @@ def parse():
                          "(one batch of --batch images split into --microbatches, strong scaling); with one "
                          "process, mp runs --stages stages on cuda:0 (pipeline rehearsal)")
     ap.add_argument("--microbatches", type=int, default=0,
-                    help="mp microbatches (0: the measured pipeline plan's count for this model / image / stages "
-                         "/ batch, parallel/plans.json; 8 without one)")
+                    help="mp microbatches (0: the pipeline plan's count for this model / image / stages / batch, "
+                         "parallel/plans.json; without one 2 for the reference cut, 8 otherwise)")
     ap.add_argument("--stages", type=int, default=2, help="mp with one process: stages on the local device")
-    ap.add_argument("--mp-cut", choices=["auto", "reference", "balanced", "time"], default="auto",
-                    help="mp stage boundaries (auto: the time-balanced plan from measured block times when "
-                         "parallel/plans.json has one for this configuration, else the reference "
-                         "encoder|decoder cut for 2 stages and the FLOP-balanced cut otherwise)")
+    ap.add_argument("--mp-cut", choices=["auto", "reference", "balanced", "v", "time"], default="auto",
+                    help="mp stage placement (auto: the link-aware plan from measured block times when "
+                         "parallel/plans.json has one for this configuration, else the skip-local mirrored "
+                         "V placement; reference: the reference's encoder|decoder cut)")
     ap.add_argument("--timing-ablation", default="",
                     help="MEASUREMENT ONLY, numerically wrong: skip these kernel families (comma list of "
                          "stream,halo,glds,wgrad,wgrad_deep,bwd,deconv) to see what they cost; the JSON line is "
@@ -146,13 +146,9 @@ def main():
     mp_info = None
     if mp:
         from distributedpytorch_amd.config import mp_plan
-        mode, cuts, M = mp_plan(cfg, world if world > 1 else a.stages, default_microbatches=8)
-        cfg.microbatches = M
-        mp_info = {"cut_mode": mode, "microbatches": M}
-        if mode == "time":
-            from distributedpytorch_amd.parallel.schedule import load_plan
-            pl = load_plan(a.model, a.img[0], a.img[1], world if world > 1 else a.stages, a.batch)
-            mp_info.update(predicted_img_s=pl.get("predicted_img_s"), predicted_efficiency=pl.get("predicted_efficiency"))
+        mpp = mp_plan(cfg, world if world > 1 else a.stages)
+        mp_info = {"cut_mode": mpp.mode, "placement": str(mpp.placement), "microbatches": mpp.microbatches,
+                   "policy": mpp.policy, **mpp.info}
     model = build_model(a.model)
     nparams = count_params(model)
     if mp and world > 1:
@@ -219,10 +215,10 @@ def main():
         allr = [torch.zeros(1, dtype=torch.float64, device=device) for _ in range(world)]
         dist.all_gather(allr, torch.tensor([mine], dtype=torch.float64, device=device))
         rank_ms = [round(float(v.item()), 3) for v in allr]
-    if mp and world > 1:  # the loss lives on the last pipeline stage; rank 0 prints it
+    if mp and world > 1:  # the loss lives on the head pipeline stage; rank 0 prints it
         lt = (loss.detach().float().reshape(1) if loss is not None
               else torch.zeros(1, device=device))
-        dist.broadcast(lt, src=world - 1)
+        dist.broadcast(lt, src=strat.pipe.head_rank)
         loss = lt
     final_loss = float(loss.item()) if loss is not None else float("nan")
 
@@ -262,7 +258,7 @@ def main():
                    "per_gpu_batch": a.batch if not mp else a.batch // max(1, world),
                    "seq_len": a.img[0] * a.img[1], "image_hw": list(a.img),
                    "parallelism": par, "backend": backend,
-                   "mp_cut": (strat.pipe.cuts if mp else None), "mp_plan": mp_info, "bucket_mb": a.bucket_mb,
+                   "mp_cut": (str(strat.pipe.pl) if mp else None), "mp_plan": mp_info, "bucket_mb": a.bucket_mb,
                    "grad_comm_dtype": a.grad_comm_dtype, "comm_overlap": a.comm_overlap,
                    "hip_graph": graphed is not None},
         "final_loss": round(final_loss, 5) if final_loss == final_loss else None, "warmup_s": round(warm_s, 2),

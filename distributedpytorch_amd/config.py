@@ -42,7 +42,7 @@ class TrainConfig:
     device: Optional[str] = None
     stages: int = 2                                  # pipeline stages for -t MP
     microbatches: int = 0                            # 0: the measured plan's count, else 2 (reference split_size=B/2)
-    mp_cut: str = "auto"                             # MP stage cut: reference | balanced | time | auto (see mp_plan)
+    mp_cut: str = "auto"                             # MP placement: reference | balanced | v | time | auto (mp_plan)
     bucket_mb: float = 8.0                           # DDP/DP all-reduce bucket size (MiB of fp32 grads)
     grad_comm_dtype: str = "fp32"                    # DDP gradient all-reduce wire dtype: fp32 | bf16
     comm_overlap: bool = True                        # DDP/DP: launch gradient buckets during the backward
@@ -98,11 +98,12 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--device", type=str, default=None)
     p.add_argument("--stages", type=int, default=2)
     p.add_argument("--microbatches", type=int, default=0,
-                   help="MP microbatches (0: the measured pipeline plan's count, else 2 as the reference)")
-    p.add_argument("--mp-cut", choices=["auto", "reference", "balanced", "time"], default="auto",
-                   help="MP stage boundaries: reference = encoder+mid | decoder+head (2 stages, ~34|62 GFLOP "
-                        "per image at 512^2); balanced = FLOP-balanced contiguous blocks; auto = reference for 2 "
-                        "stages, balanced otherwise")
+                   help="MP microbatches (0: the pipeline plan's count; else 2 for the reference cut, 8 otherwise)")
+    p.add_argument("--mp-cut", choices=["auto", "reference", "balanced", "v", "time"], default="auto",
+                   help="MP stage placement: reference = encoder+mid | decoder+head (2 stages; all skips cross "
+                        "the cut); balanced = FLOP-balanced contiguous blocks; v = mirrored, skip-local (stage s "
+                        "owns encoder level s and decoder level s); time = the measured-time plan in "
+                        "parallel/plans.json; auto = time when planned, else v")
     p.add_argument("--bucket-mb", type=float, default=8.0)
     p.add_argument("--grad-comm-dtype", choices=["fp32", "bf16"], default="fp32",
                    help="DDP: all-reduce gradient buckets in bf16 (half the bytes) instead of fp32")
@@ -151,30 +152,68 @@ def parse_args(argv=None) -> TrainConfig:
 
 
 def mp_cut_mode(cfg: "TrainConfig", stages: int) -> str:
-    return mp_plan(cfg, stages)[0]
+    return mp_plan(cfg, stages).mode
 
 
-def mp_plan(cfg: "TrainConfig", stages: int, default_microbatches: int = 2):
-    """(cut mode, cuts or None, microbatches) of an MP run.
+@dataclass
+class MPPlan:
+    """How an MP run is laid out: the stage placement, microbatch count and per-stage op order."""
+    mode: str                           # reference | balanced | v | time
+    placement: object                   # parallel.placement.Placement
+    microbatches: int
+    orders: Optional[list] = None       # per-stage static op order (None: derived from FLOP costs)
+    policy: str = "feed"
+    info: dict = field(default_factory=dict)
 
-    ``time`` / ``auto``: the time-balanced cut and microbatch count that tools/pipeline_plan.py chose
-    from MEASURED per-block times with the GPipe schedule simulator (parallel/schedule.py; plans in
-    parallel/plans.json, keyed by model, image, stages and global batch).  Without a plan for the
-    configuration, ``auto`` falls back to the reference encoder|decoder cut for 2 stages
-    (unet_model.py:14-20) and the FLOP-balanced cut otherwise, ``time`` to the FLOP-balanced cut.
-    An explicit ``--microbatches`` always wins."""
+
+def mp_plan(cfg: "TrainConfig", stages: int) -> MPPlan:
+    """Placement, microbatch count and op order of an MP run (``--mp-cut``):
+
+    * ``reference``: the reference cut, encoder+mid | decoder+head (unet_model.py:14-20; 2 stages):
+      all four skips cross the cut, 31 MiB per image at 512^2 bf16 -- link-bound on xGMI;
+    * ``balanced``: FLOP-balanced contiguous block ranges;
+    * ``v``: the skip-local mirrored placement (stage s owns encoder level(s) s and the same decoder
+      level(s); parallel/placement.py), FLOP-balanced;
+    * ``time``: the placement, microbatch count and op order tools/pipeline_plan.py chose from MEASURED
+      per-block times with the link-queueing schedule model (parallel/plans.json, keyed by model,
+      image, stages and global batch);
+    * ``auto`` (default): ``time`` when plans.json has the configuration, else ``v``.
+
+    Microbatches: ``--microbatches`` when given, else the plan's, else 2 for the reference cut (the
+    reference's split_size = B/2) and 8 otherwise (reduced to a divisor of the batch)."""
+    import math
+    from .models.blocks import n_blocks, partition
+    from .models.unet import build_model
+    from .parallel.placement import Placement, v_partition
     from .parallel.schedule import load_plan
+    mcfg = build_model(cfg.model).cfg
+    h, w = cfg.img_size
     mode = cfg.mp_cut
     plan = None
     if mode in ("auto", "time"):
-        h, w = cfg.img_size
-        plan = load_plan(cfg.model, h, w, stages, cfg.batch_size)
-        if plan is None:
-            mode = "reference" if (mode == "auto" and stages == 2) else "balanced"
-        else:
+        plan = load_plan(cfg.model, h, w, stages, cfg.batch_size, depth=mcfg.depth)
+        if plan is not None:
             mode = "time"
-    M = cfg.microbatches or (plan["microbatches"] if plan else default_microbatches)
-    return mode, (plan["cuts"] if plan else None), M
+        else:
+            mode = "v" if stages > 1 else "balanced"
+    if stages == 1:
+        pl = Placement.contiguous([0, n_blocks(mcfg.depth)])
+    elif mode == "time":
+        pl = plan["placement"]
+    elif mode == "reference":
+        pl = Placement.contiguous(partition(mcfg, stages, h, w, mode="reference"))
+    elif mode == "balanced":
+        pl = Placement.contiguous(partition(mcfg, stages, h, w, mode="balanced"))
+    elif mode == "v":
+        pl = v_partition(mcfg, stages, h, w)
+    else:
+        raise ValueError(f"unknown --mp-cut {mode!r}")
+    M = cfg.microbatches or (plan["microbatches"] if plan else (2 if mode == "reference" else 8))
+    if not cfg.microbatches and cfg.batch_size % M:
+        M = math.gcd(M, cfg.batch_size)
+    orders = plan.get("orders") if plan is not None and M == plan["microbatches"] else None
+    info = {k: plan[k] for k in ("predicted_img_s", "predicted_efficiency", "rehearsal_img_s") if plan and k in plan}
+    return MPPlan(mode, pl, M, orders, (plan or {}).get("policy", "feed"), info)
 
 
 def dist_env():

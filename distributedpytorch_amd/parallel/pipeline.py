@@ -5,20 +5,24 @@ Reference: a hand-written 2-stage, 2-microbatch pipeline inside ``UNet.forward``
 cuda:1, the bottleneck and all four skips copied with ``.to('cuda:1')`` per microbatch, overlap
 only from async launch order, backward via plain autograd.
 
-Here, generalised to N stages x M microbatches (GPipe: all forwards, then all backwards):
+Here, generalised to N stages x M microbatches (GPipe: all forwards, then all backwards) over a
+:class:`.placement.Placement`: the reference's encoder|decoder cut (``--mp-cut reference``), any
+contiguous partition, or the mirrored V placement in which stage s owns encoder level(s) s on the way
+down and the same decoder level(s) on the way up, so skips never leave their GPU and each stage has
+two segments (half the fill / drain bubble).  The reference cut moves 31 MiB per image across one
+xGMI link at 512^2 bf16 (all four skips), which makes it link-bound (parallel/schedule.py);
+the V placement moves 6 MiB.
 
-* :class:`GPipeDist` - one process per GPU (torchrun), the MI355X-native form.  Each rank owns one
-  contiguous block range (:func:`..models.blocks.partition`, FLOP-balanced, or the reference cut).
-  Activations AND skip tensors go *directly* from producer to consumer stage with RCCL
-  ``isend/irecv`` (one xGMI hop on the fully connected MI355X mesh - skips never relay through
-  intermediate stages), sent in the compute dtype (bf16: half the reference's bytes).  P2P runs on
-  RCCL's per-peer streams, so transfers overlap with the next microbatch's compute; receives are
-  posted one microbatch ahead.  The last stage sums the per-microbatch loss partial sums, which
-  gives exactly the reference's full-batch loss (global Dice), then back-propagates microbatch by
-  microbatch so gradients start flowing upstream immediately.
+* :class:`GPipeDist` - one process per GPU (torchrun), the MI355X-native form.  Activations AND skip
+  tensors go *directly* from producer to consumer segment with RCCL ``isend/irecv`` (one xGMI hop on
+  the fully connected MI355X mesh), in the compute dtype (bf16: half the reference's bytes), on one
+  communicator per sending segment; every receive of a phase is posted before its first op computes,
+  so transfers overlap compute.  The head stage sums the per-microbatch loss partial sums, which gives
+  exactly the reference's full-batch loss (global Dice), then back-propagates op by op so gradients
+  start flowing upstream immediately.
 * :class:`GPipeLocal` - single process, N local devices (the reference's own form, kept for
-  ``python train.py -t MP`` without torchrun): stages issued in wavefront order so stage s works
-  on microbatch m while stage s+1 works on microbatch m-1; cross-device copies are peer copies.
+  ``python train.py -t MP`` without torchrun): segments issued in wavefront order; cross-device
+  copies are peer copies.
 
 Both are numerically transparent: pipelined forward == plain forward (SURVEY §3.4 probe7), checked
 by the tests against a single-device run.
@@ -31,9 +35,11 @@ import torch
 import torch.distributed as dist
 
 from ..compute import loss_from_partials, make_blocks
-from ..models.blocks import boundary_names, block_kind, n_blocks, partition, run_segment, segment_units, skip_name
+from ..models.blocks import block_kind, partition, run_segment, segment_units, skip_name
 from ..optim import FlatParameterSpace
 from ..utils.tracing import trace_range
+from .placement import Placement, channel_members, flop_orders, remote_groups, seg_io
+from .placement import stage_io as _stage_io
 
 
 def _debug_point(device):
@@ -88,49 +94,30 @@ def stage_buffer_names(model, start: float, end: float) -> List[str]:
     return [n for n, _ in model.named_buffers() if any(n.startswith(p) for p in prefixes)]
 
 
-def _tensor_producer(name: str, cut_start: float, cuts: Sequence[float], depth: int) -> int:
-    """Stage that produces boundary tensor ``name`` entering the stage starting at ``cut_start``."""
-    if name == "x":
-        return list(cuts).index(cut_start) - 1
-    lvl = int(name[len("skip"):])
-    return _stage_of_block(lvl + 0.5, cuts)      # a skip is produced by its encoder block's part b
+def placement_param_names(model, pl: Placement, stage: int) -> List[str]:
+    """Parameters of every segment stage ``stage`` owns under placement ``pl``."""
+    out = []
+    for j in pl.segments(stage):
+        out += stage_param_names(model, *pl.seg_range(j))
+    return out
 
 
-def _stage_of_block(pos: float, cuts: Sequence[float]) -> int:
-    """Stage whose segment contains position ``pos`` (a block index, or ``b + 0.5`` for part b)."""
-    for s in range(len(cuts) - 1):
-        if cuts[s] <= pos < cuts[s + 1]:
-            return s
-    raise ValueError(pos)
+def placement_buffer_names(model, pl: Placement, stage: int) -> List[str]:
+    out = []
+    for j in pl.segments(stage):
+        out += stage_buffer_names(model, *pl.seg_range(j))
+    return out
 
 
-def stage_io(cuts: Sequence[int], depth: int):
-    """Per stage: ``recv`` list of (name, src_stage) and ``send`` list of (name, dst_stage)."""
-    S = len(cuts) - 1
-    recv = [[] for _ in range(S)]
-    send = [[] for _ in range(S)]
-    for s in range(1, S):
-        # x comes from the previous stage
-        recv[s].append(("x", s - 1))
-        send[s - 1].append(("x", s))
-    for lvl in range(depth):
-        p = _stage_of_block(lvl + 0.5, cuts)                      # produced by part b of enc block lvl
-        c = _stage_of_block(depth + 1 + (depth - 1 - lvl), cuts)  # consumed by part a of its decoder block
-        if p != c:
-            recv[c].append((skip_name(lvl), p))
-            send[p].append((skip_name(lvl), c))
-    return recv, send
-
-
-def sender_groups(recv_spec, send_spec) -> List[List[int]]:
-    """Members of each stage's sender communicator: the stage, the stages it sends activations to
-    (forward) and the stages it sends gradients to (backward: its producers), sorted."""
-    S = len(send_spec)
-    return [sorted({s} | {d for _, d in send_spec[s]} | {p for _, p in recv_spec[s]}) for s in range(S)]
+def stage_io(cuts, depth: int):
+    """Per stage: ``recv`` list of (name, src_stage) and ``send`` list of (name, dst_stage) for a
+    contiguous cut list or a :class:`.placement.Placement`."""
+    pl = cuts if isinstance(cuts, Placement) else Placement.contiguous(cuts)
+    return _stage_io(pl, depth)
 
 
 def infer_shapes(cfg, microbatch: int, h: int, w: int) -> Dict[str, tuple]:
-    """Shapes (NCHW) of every boundary tensor for one microbatch, by arithmetic (no tracing)."""
+    """Shapes (NCHW) of every skip tensor for one microbatch, by arithmetic (no tracing)."""
     shapes = {}
     H, W = h, w
     for lvl, wd in enumerate(cfg.widths):
@@ -139,50 +126,68 @@ def infer_shapes(cfg, microbatch: int, h: int, w: int) -> Dict[str, tuple]:
     return shapes
 
 
-class _Stage:
-    def __init__(self, model, blocks, start, end, depth):
-        self.model, self.blocks, self.start, self.end, self.depth = model, blocks, start, end, depth
+class _Capture(torch.autograd.Function):
+    """Boundary of a segment's input: forward is the identity (same storage, so the HIP engine still
+    finds a skip's concat buffer by address), backward stores the incoming gradient under ``key`` in
+    ``box`` as produced -- no ``AccumulateGrad`` on a detached leaf, which would copy a strided
+    skip gradient (a 64-of-128-channel view of the decoder's dgrad output) into a fresh dense ``.grad``."""
 
-    def forward(self, env, target=None, want="partials"):
-        return run_segment(self.blocks, self.start, self.end, self.depth, env, target, want)
+    @staticmethod
+    def forward(ctx, anchor, t, box, key):
+        ctx.box, ctx.key = box, key
+        return t.detach()
+
+    @staticmethod
+    def backward(ctx, g):
+        ctx.box[ctx.key] = g
+        return None, None, None, None
 
 
 class GPipeDist:
-    """Multi-process GPipe over a process group whose size == number of stages.
+    """Multi-process GPipe over a process group whose size == number of stages, on any
+    :class:`.placement.Placement` (contiguous block ranges, or the mirrored V placement where stage s
+    owns encoder levels on the way down and the same decoder levels on the way up).
 
     Communication (RCCL over xGMI, or gloo on CPU):
-    * one communicator PER SENDING STAGE (:func:`sender_groups`): stage s sends only on its own
-      group G[s] = {s} + its consumers + its producers, and receives from p only on G[p].  torch
-      puts every coalesced P2P op of a group on that group's single RCCL stream in issue order, so
-      with one shared group a pre-posted receive would hold back the same rank's later send (a
-      middle stage could not hand microbatch m downstream before m+1 arrived from upstream); with
-      sender groups no rank ever both sends and receives on one group, so sends never queue behind
-      its own receives (checked op by op in ``tests/test_pipeline_p2p_order.py``);
-    * the tensors of one microbatch that go to the same group are posted as ONE
-      ``batch_isend_irecv`` group (RCCL group call: the x and skip transfers start together);
-    * forward receives for microbatch m+1 and backward gradient receives for microbatch m-1 are
-      posted before microbatch m computes, so transfer latency hides behind compute;
-    * every group's communicator is created at construction (a 1-element exchange from its sender
-      to every member), so the lazy RCCL communicator setup never lands inside a training step;
+    * one communicator PER SEGMENT (:func:`.placement.channel_members`): segment j's owner is its only
+      sender (activations to the stages of j's consumer segments, gradients to the stages of j's
+      producer segments); a rank receives a segment's messages only on that segment's communicator.
+      torch puts every P2P op of a group on that group's single RCCL stream in issue order, so no send
+      can ever queue behind the same rank's pre-posted receive (``tests/test_pipeline_p2p_order.py``),
+      and each (segment, stage) message stream is matched in microbatch order;
+    * the tensors one op sends to one stage go as ONE ``batch_isend_irecv`` group (x and skips
+      together); a skip goes straight from its encoder segment to its decoder segment (one hop);
+      segments of one stage hand tensors over locally (no copy);
+    * every receive of the step is posted before the first op computes (forward: at the start;
+      backward: when the loss is known), so transfers land while earlier ops compute;
+    * each stage issues its ops in the static order of :func:`.placement.stage_orders` (the list
+      scheduler of the schedule model; a plan can carry the order it simulated);
+    * every communicator is created at construction (a 1-element exchange from its sender to every
+      member), so the lazy RCCL setup never lands inside a training step;
     * a skip that leaves this stage is written by the encoder conv into a dense tensor (HIP engine
       ``dense_skips``) and sent as is; activations travel in the compute dtype (bf16).
     """
 
     def __init__(self, model, microbatches: int, backend: str = "auto", dtype: str = "bf16",
-                 group=None, cuts: Optional[List[int]] = None, img_hw=(512, 512), mode: str = "balanced",
-                 warm: bool = True):
+                 group=None, cuts: Optional[List[float]] = None, img_hw=(512, 512), mode: str = "balanced",
+                 warm: bool = True, placement: Optional[Placement] = None, policy: str = "feed",
+                 orders: Optional[List[dict]] = None):
         self.group = group
         self.rank = dist.get_rank(group)
         self.S = dist.get_world_size(group)
         self.M = microbatches
         self.model = model
         self.depth = model.cfg.depth
-        self.cuts = cuts or partition(model.cfg, self.S, img_hw[0], img_hw[1], mode=mode)
-        assert len(self.cuts) == self.S + 1
-        self.start, self.end = self.cuts[self.rank], self.cuts[self.rank + 1]
-        self.recv_spec, self.send_spec = stage_io(self.cuts, self.depth)
+        if placement is None:
+            placement = Placement.contiguous(cuts or partition(model.cfg, self.S, img_hw[0], img_hw[1], mode=mode))
+        self.pl = placement.validate(self.depth)
+        assert self.pl.S == self.S, f"placement has {self.pl.S} stages, the group {self.S} ranks"
+        self.cuts = list(self.pl.cuts)
+        self.segs = self.pl.segments(self.rank)
+        self.ins, self.outs = seg_io(self.pl, self.depth)
+        self.recv_spec, self.send_spec = _stage_io(self.pl, self.depth)
         self.device = next(model.parameters()).device
-        names = set(stage_param_names(model, self.start, self.end))
+        names = set(placement_param_names(model, self.pl, self.rank))
         own = [(n, p) for n, p in model.named_parameters() if n in names]
         for n, p in model.named_parameters():
             if n not in names:
@@ -195,62 +200,70 @@ class GPipeDist:
         if hasattr(self.blocks, "dense_skips"):
             self.blocks.dense_skips = {int(n[len("skip"):]) for n, _ in self.send_spec[self.rank]
                                        if n.startswith("skip")}
-        self.stage = _Stage(model, self.blocks, self.start, self.end, self.depth)
         self.comm_dtype = torch.bfloat16 if (dtype == "bf16" and self.device.type == "cuda") else torch.float32
-        self.is_first = self.rank == 0
-        self.is_last = self.rank == self.S - 1
+        self.first_rank = self.pl.owner[0]
+        self.head_rank = self.pl.owner[self.pl.head_seg]
+        self.is_first = self.rank == self.first_rank
+        self.is_last = self.rank == self.head_rank
+        self.policy = policy
+        h, w = img_hw
+        self.orders = (orders or flop_orders(self.pl, model.cfg, microbatches, h, w, policy))[self.rank]
+        assert sorted(self.orders["fwd"]) == sorted(j for j in self.segs for _ in range(microbatches))
         self._glob = lambda s: dist.get_global_rank(group, s) if group is not None else s
         self._host_staged = self.device.type == "cuda" and dist.get_backend(group) != "nccl"
-        self.peers = sorted({p for _, p in self.recv_spec[self.rank]} | {p for _, p in self.send_spec[self.rank]})
-        # per-sender communicators: stage s sends only on groups[s], receives from p only on groups[p]
-        self.members = sender_groups(self.recv_spec, self.send_spec)
+        self._anchor = torch.zeros((), device=self.device, requires_grad=True)
+        # one communicator per segment with a remote edge; its owner is the only sender
+        self.members = channel_members(self.pl, self.depth)
         self.groups: Dict[int, object] = {}
         world_pipeline = group is None or dist.get_world_size(group) == dist.get_world_size()
-        for s in range(self.S):
-            ranks = [self._glob(r) for r in self.members[s]]
+        for j in range(self.pl.K):
+            ranks = [self._glob(r) for r in self.members[j]]
             if len(ranks) < 2:
                 continue
             if world_pipeline:      # every rank of the job calls new_group, members or not
                 g = dist.new_group(ranks)
-            elif self.rank in self.members[s]:   # pipeline inside a bigger job: members only, in order
+            elif self.rank in self.members[j]:   # pipeline inside a bigger job: members only, in order
                 g = dist.new_group(ranks, use_local_synchronization=True)
             else:
                 continue
-            if self.rank in self.members[s]:
-                self.groups[s] = g
-        self.op_log: Optional[list] = None   # tests: [(sender group, "send"/"recv", peer stage)] per posted op
+            if self.rank in self.members[j]:
+                self.groups[j] = g
+        # messages: per segment, its remote edges grouped by the other end's stage
+        self.fwd_msgs = [remote_groups(self.pl, self.outs[j], self.pl.owner[j]) for j in range(self.pl.K)]
+        self.bwd_msgs = [remote_groups(self.pl, self.ins[j], self.pl.owner[j]) for j in range(self.pl.K)]
+        self.op_log: Optional[list] = None   # tests: [(segment channel, "send"/"recv", peer stage)] per posted op
         if warm:
             self.warm_up()
 
     def warm_up(self):
-        """One tiny exchange on every group this stage belongs to (its sender to each member), in
-        stage order on every rank: creates the RCCL communicators now instead of inside the first
+        """One tiny exchange on every communicator this stage belongs to (its sender to each member), in
+        segment order on every rank: creates the RCCL communicators now instead of inside the first
         timed step, and every group's first operation involves all of its members."""
         dev = "cpu" if self._host_staged else self.device
-        for s in sorted(self.groups):
-            g = self.groups[s]
-            others = [r for r in self.members[s] if r != s]
-            ops, keep = [], []
-            if s == self.rank:
-                out = torch.full((1,), float(self.rank), dtype=self.comm_dtype, device=dev)
+        for j in sorted(self.groups):
+            g = self.groups[j]
+            sender = self.pl.owner[j]
+            others = [r for r in self.members[j] if r != sender]
+            keep = []
+            if sender == self.rank:
+                out = torch.full((1,), float(j), dtype=self.comm_dtype, device=dev)
                 keep.append(out)
                 ops = [dist.P2POp(dist.isend, out, self._glob(r), g) for r in others]
             else:
                 inp = torch.empty(1, dtype=self.comm_dtype, device=dev)
                 keep.append(inp)
-                ops = [dist.P2POp(dist.irecv, inp, self._glob(s), g)]
-            for w in dist.batch_isend_irecv(ops):
-                w.wait()
-            if s != self.rank:
-                assert int(keep[0].float().item()) == s, f"stage {self.rank}: sender {s} answered {keep[0].item()}"
+                ops = [dist.P2POp(dist.irecv, inp, self._glob(sender), g)]
+            for wk in dist.batch_isend_irecv(ops):
+                wk.wait()
+            if sender != self.rank:
+                assert int(keep[0].float().item()) == j, f"stage {self.rank}: channel {j} answered {keep[0].item()}"
 
     # shapes of the boundary tensors for this microbatch size
-    def _shape(self, name, mb, h, w):
+    def _shape(self, name, mb, h, w, cut):
+        """Logical NCHW shape of tensor ``name`` entering the segment that starts at ``cut``."""
         cfg = self.model.cfg
         if name.startswith("skip"):
             return infer_shapes(cfg, mb, h, w)[name]
-        # "x" entering block `cut`: encoder levels floor-halve, the decoder doubles from the bottom
-        cut = self.start
         kind, i = block_kind(int(cut), self.depth)
         hb, wb = h >> self.depth, w >> self.depth
         if cut != int(cut):          # a cut inside a DoubleConv: x is its first conv's output
@@ -289,152 +302,205 @@ class GPipeDist:
             return t.permute(0, 2, 3, 1).reshape(-1)
         return t.reshape(-1)
 
-    def _post(self, sends=(), recvs=()):
-        """One grouped P2P launch: ``sends`` = [(tensor, dst)], ``recvs`` = [(flat buffer, src)].
-        Returns a :class:`_Transfer` whose ``wait()`` completes it (and keeps the send buffers alive).
+    def _post(self, sends=(), recvs=(), channel: int = None):
+        """One grouped P2P launch on segment ``channel``'s communicator: ``sends`` = [(tensor, dst
+        stage)] (this rank owns the segment), or ``recvs`` = [(flat buffer, src stage)] (the segment's
+        owner sends).  Returns a :class:`_Transfer` whose ``wait()`` completes it.
 
         RCCL moves device memory directly (ordered after the producing kernels on the current
         stream).  gloo (CPU tests; the one-GPU rehearsal of this path, ranks sharing cuda:0) is
         host-staged explicitly: a device buffer is copied to host memory before the send and from
         it after the receive completes."""
-        by_group: Dict[int, list] = {}
-        keep, copies = [], []
-        for t, dst in sends:                      # all on this stage's own sender group
+        g = self.groups[channel]
+        ops, keep, copies = [], [], []
+        for t, dst in sends:
             buf = self._wire(t)
             if self._host_staged:
                 buf = buf.to("cpu")                   # synchronous: the producing kernels have finished
             keep.append(buf)
-            by_group.setdefault(self.rank, []).append(dist.P2POp(dist.isend, buf, self._glob(dst), self.groups[self.rank]))
-            self._log(self.rank, "send", dst)
-        for flat, src in recvs:                   # on the SENDER's group
+            ops.append(dist.P2POp(dist.isend, buf, self._glob(dst), g))
+            self._log(channel, "send", dst)
+        for flat, src in recvs:
             if self._host_staged:
                 host = torch.empty(flat.shape, dtype=flat.dtype)
                 copies.append((host, flat))
                 flat = host
-            by_group.setdefault(src, []).append(dist.P2POp(dist.irecv, flat, self._glob(src), self.groups[src]))
-            self._log(src, "recv", src)
-        works = []
-        for g in sorted(by_group):
-            works.extend(dist.batch_isend_irecv(by_group[g]))
-        return _Transfer(works, keep, copies)
+            ops.append(dist.P2POp(dist.irecv, flat, self._glob(src), g))
+            self._log(channel, "recv", src)
+        return _Transfer(dist.batch_isend_irecv(ops) if ops else [], keep, copies)
 
-    def _log(self, group_sender: int, kind: str, peer: int):
+    def _log(self, channel: int, kind: str, peer: int):
         if self.op_log is not None:
-            self.op_log.append((group_sender, kind, peer))
+            self.op_log.append((channel, kind, peer))
 
-    def _irecv(self, mb, h, w):
-        bufs, recvs = {}, []
-        for name, src in self.recv_spec[self.rank]:
-            t, flat = self._empty_wire(self._shape(name, mb, h, w))
-            recvs.append((flat, src))
-            bufs[name] = t
-        return bufs, self._post(recvs=recvs)
-
-    def _irecv_grads(self, outs: Dict[str, torch.Tensor]):
-        grads, recvs = [], []
-        for name, dst in self.send_spec[self.rank]:
-            g, flat = self._empty_wire(tuple(outs[name].shape))
-            recvs.append((flat, dst))
-            grads.append(g)
-        return grads, self._post(recvs=recvs)
+    def _cap(self, t, box, key):
+        # detached: the producer's graph (another segment of this stage) must not be reached from here
+        return _Capture.apply(self._anchor, t.detach(), box, key)
 
     def train_step(self, images: Optional[torch.Tensor], targets: Optional[torch.Tensor], batch: int,
                    hw, dice: bool = True, loss_scale: float = 1.0):
-        """One GPipe step. Returns the (full-batch) loss on the last stage, None elsewhere."""
+        """One GPipe step. Returns the (full-batch) loss on the head stage, None elsewhere."""
         h, w = hw
-        M = self.M
+        M, pl, me = self.M, self.pl, self.rank
         assert batch % M == 0, f"batch {batch} must be divisible by microbatches {M}"
         mb = batch // M
-        xs = images.chunk(M) if self.is_first else [None] * M
-        ts = targets.chunk(M) if self.is_last else [None] * M
-        saved_in, saved_out, pending = [], [], []
-        partials = []
-        nxt = self._irecv(mb, h, w) if not self.is_first else None
-        for m in range(M):
-            if self.is_first:
-                env = {"x": xs[m]}
-                leaves = {}
-            else:
-                bufs, xfer = nxt
-                xfer.wait()
-                if m + 1 < M:
-                    nxt = self._irecv(mb, h, w)        # microbatch m+1 lands while m computes
-                leaves = {k: v.detach().requires_grad_(True) for k, v in bufs.items()}
-                env = dict(leaves)
-            with trace_range(f"stage{self.rank}_fwd_mb{m}"):
-                out = self.stage.forward(env, ts[m], "partials")
+        head = pl.head_seg
+        xs = images.chunk(M) if self.is_first else None
+        ts = targets.chunk(M) if self.is_last else None
+        # every forward receive of the step: message (producer segment p, microbatch m) to this stage
+        frx = {}
+        for p in range(pl.K):
+            edges = self.fwd_msgs[p].get(me)
+            if not edges:
+                continue
+            for m in range(M):
+                bufs, recvs = {}, []
+                for name, c in edges:
+                    t, flat = self._empty_wire(self._shape(name, mb, h, w, pl.cuts[c]))
+                    bufs[name] = t
+                    recvs.append((flat, pl.owner[p]))
+                frx[(p, m)] = (bufs, self._post(recvs=recvs, channel=p))
+        caps: Dict[tuple, Optional[torch.Tensor]] = {}      # (consumer segment, m, name) -> input gradient
+        fout: Dict[tuple, Dict[str, torch.Tensor]] = {}      # (segment, m) -> its outputs
+        partials: List[Optional[torch.Tensor]] = [None] * M
+        pending = []
+        nxt = {j: 0 for j in self.segs}
+        for j in self.orders["fwd"]:
+            m = nxt[j]
+            nxt[j] += 1
+            env = {}
+            for name, p in self.ins[j]:
+                if pl.owner[p] == me:
+                    t = fout[(p, m)][name]
+                else:
+                    bufs, xfer = frx[(p, m)]
+                    xfer.wait()
+                    t = bufs[name]
+                env[name] = self._cap(t, caps, (j, m, name))
+            if j == 0:
+                env["x"] = xs[m]
+            a, b = pl.seg_range(j)
+            with trace_range(f"stage{me}_fwd_seg{j}_mb{m}"):
+                out = run_segment(self.blocks, a, b, self.depth, env, ts[m] if j == head else None, "partials")
             _debug_point(self.device)
-            saved_in.append(leaves)
-            if self.is_last:
-                partials.append(out["partials"])
-                saved_out.append({})
-            else:
-                sends = {name: out[name] for name, _ in self.send_spec[self.rank]}
-                pending.append(self._post(sends=[(sends[n], d) for n, d in self.send_spec[self.rank]]))
-                saved_out.append(sends)
+            if j == head:
+                partials[m] = out["partials"]
+                continue
+            fout[(j, m)] = {name: out[name] for name, _ in self.outs[j]}
+            for d, edges in self.fwd_msgs[j].items():
+                pending.append(self._post(sends=[(out[name], d) for name, _ in edges], channel=j))
+        frx = None
 
-        # ---------------- backward (microbatches in reverse order) ----------------
-        loss = None
+        # ---------------- backward (each segment's microbatches in reverse order) ----------------
+        loss = dP = None
         if self.is_last:
             P = torch.stack([p.detach() for p in partials]).requires_grad_(True)
             loss = loss_from_partials(P.sum(0), targets.numel(), dice)
             (loss * loss_scale).backward()
             dP = P.grad
-        gnxt = self._irecv_grads(saved_out[M - 1]) if not self.is_last else None
+        brx = {}           # gradient messages (consumer segment c, microbatch m) to this stage
+        for c in range(pl.K):
+            edges = self.bwd_msgs[c].get(me)
+            if not edges:
+                continue
+            for m in reversed(range(M)):
+                bufs, recvs = {}, []
+                for name, p in edges:
+                    g, flat = self._empty_wire(tuple(fout[(p, m)][name].shape))
+                    bufs[name] = g
+                    recvs.append((flat, pl.owner[c]))
+                brx[(c, m)] = (bufs, self._post(recvs=recvs, channel=c))
         if hasattr(self.blocks, "open_defer_window"):
             self.blocks.open_defer_window()     # the microbatches' weight gradients: one launch per layer
-        for m in reversed(range(M)):
-            rng = trace_range(f"stage{self.rank}_bwd_mb{m}")
-            rng.__enter__()
-            if self.is_last:
-                torch.autograd.backward(partials[m], dP[m])
-            else:
-                grads, xfer = gnxt
-                xfer.wait()
-                if m > 0:
-                    gnxt = self._irecv_grads(saved_out[m - 1])   # gradients of m-1 land while m runs
-                outs = [saved_out[m][name] for name, _ in self.send_spec[self.rank]]
-                torch.autograd.backward(outs, [g.to(o.dtype) for o, g in zip(outs, grads)])
-            rng.__exit__(None, None, None)
+        nxt = {j: M - 1 for j in self.segs}
+        for j in self.orders["bwd"]:
+            m = nxt[j]
+            nxt[j] -= 1
+            with trace_range(f"stage{me}_bwd_seg{j}_mb{m}"):
+                if j == head:
+                    torch.autograd.backward(partials[m], dP[m])
+                    partials[m] = None
+                else:
+                    outs, grads = [], []
+                    for name, c in self.outs[j]:
+                        o = fout[(j, m)][name]
+                        if pl.owner[c] == me:
+                            assert (c, m, name) in caps, f"segment {c} mb {m} backward must precede segment {j}'s"
+                            g = caps.pop((c, m, name))
+                        else:
+                            bufs, xfer = brx[(c, m)]
+                            xfer.wait()
+                            g = bufs[name]
+                        if g is not None and o.requires_grad:
+                            outs.append(o)
+                            grads.append(g.to(o.dtype))
+                    if outs:
+                        torch.autograd.backward(outs, grads)
+                    fout[(j, m)] = None
             _debug_point(self.device)
-            if not self.is_first:
-                gsends = []
-                for name, src in self.recv_spec[self.rank]:
-                    gr = saved_in[m][name].grad
-                    if gr is None:
-                        gr = torch.zeros_like(saved_in[m][name])
-                    gsends.append((gr, src))
-                pending.append(self._post(sends=gsends))
-            saved_in[m] = saved_out[m] = None
+            for d, edges in self.bwd_msgs[j].items():
+                gs = []
+                for name, _ in edges:
+                    g = caps.pop((j, m, name), None)
+                    gs.append(g if g is not None else torch.zeros(self._shape(name, mb, h, w, pl.cuts[j]),
+                                                                   dtype=self.comm_dtype, device=self.device))
+                pending.append(self._post(sends=[(g, d) for g in gs], channel=j))
+            for name, p in self.ins[j]:            # local producers read theirs from caps; nothing else left
+                if pl.owner[p] != me:
+                    caps.pop((j, m, name), None)
         if hasattr(self.blocks, "close_defer_window"):
             self.blocks.close_defer_window()
         for xfer in pending:
+            xfer.wait()
+        for _, (_, xfer) in brx.items():
             xfer.wait()
         return loss
 
     @torch.no_grad()
     def eval_probs(self, images, batch, hw):
-        """Inference through the pipeline (one microbatch = whole batch); probs on the last stage."""
+        """Inference through the pipeline (one microbatch = whole batch); probs on the head stage."""
         h, w = hw
-        if self.is_first:
-            env = {"x": images}
-        else:
-            bufs, xfer = self._irecv(batch, h, w)
-            xfer.wait()
-            env = dict(bufs)
-        out = self.stage.forward(env, None, "probs")
-        if not self.is_last:
-            self._post(sends=[(out[n], d) for n, d in self.send_spec[self.rank]]).wait()
-        return out.get("probs")
+        pl, me = self.pl, self.rank
+        fout, sent, probs = {}, [], None
+        got = {}                                   # producer segment -> its (one) message to this stage
+        for j in range(pl.K):                      # chain order on every rank: no circular wait
+            if pl.owner[j] != me:
+                continue
+            env = {}
+            for name, p in self.ins[j]:
+                if pl.owner[p] == me:
+                    env[name] = fout[p][name]
+                    continue
+                if p not in got:
+                    edges = self.fwd_msgs[p][me]
+                    bufs, recvs = {}, []
+                    for n2, c in edges:
+                        t, flat = self._empty_wire(self._shape(n2, batch, h, w, pl.cuts[c]))
+                        bufs[n2] = t
+                        recvs.append((flat, pl.owner[p]))
+                    self._post(recvs=recvs, channel=p).wait()
+                    got[p] = bufs
+                env[name] = got[p][name]
+            if j == 0:
+                env["x"] = images
+            a, b = pl.seg_range(j)
+            out = run_segment(self.blocks, a, b, self.depth, env, None, "probs" if j == pl.head_seg else "partials")
+            if j == pl.head_seg:
+                probs = out["probs"]
+                continue
+            fout[j] = out
+            for d, edges in self.fwd_msgs[j].items():
+                sent.append(self._post(sends=[(out[n], d) for n, _ in edges], channel=j))
+        for x in sent:
+            x.wait()
+        return probs
 
     def gather_state_dict(self):
         """Full model state dict on stage 0 (other stages send their parameters and buffers)."""
         params = {**dict(self.model.named_parameters()), **dict(self.model.named_buffers())}
-        all_cuts = self.cuts
         sd = {}
         for s in range(self.S):
-            snames = (stage_param_names(self.model, all_cuts[s], all_cuts[s + 1])
-                      + stage_buffer_names(self.model, all_cuts[s], all_cuts[s + 1]))
+            snames = placement_param_names(self.model, self.pl, s) + placement_buffer_names(self.model, self.pl, s)
             for n in snames:
                 if s == 0:
                     if self.rank == 0:
@@ -468,29 +534,35 @@ class _Transfer:
 
 
 class GPipeLocal:
-    """Single-process pipeline over local devices (reference MP form, N stages x M microbatches)."""
+    """Single-process pipeline over local devices (reference MP form, N stages x M microbatches) on any
+    :class:`.placement.Placement`: segment j runs on ``devices[owner[j]]``."""
 
     def __init__(self, model, devices: Sequence, microbatches: int, backend: str = "auto", dtype: str = "bf16",
-                 cuts: Optional[List[int]] = None, img_hw=(512, 512), mode: str = "balanced"):
+                 cuts: Optional[List[float]] = None, img_hw=(512, 512), mode: str = "balanced",
+                 placement: Optional[Placement] = None):
         self.devices = [torch.device(d) for d in devices]
         self.S = len(self.devices)
         self.M = microbatches
         self.model = model
         self.depth = model.cfg.depth
-        self.cuts = cuts or partition(model.cfg, self.S, img_hw[0], img_hw[1], mode=mode)
-        # place each block's parameters on its stage's device
+        if placement is None:
+            placement = Placement.contiguous(cuts or partition(model.cfg, self.S, img_hw[0], img_hw[1], mode=mode))
+        self.pl = placement.validate(self.depth)
+        assert self.pl.S == self.S, f"placement has {self.pl.S} stages for {self.S} devices"
+        self.cuts = list(self.pl.cuts)
+        # place each segment's parameters on its stage's device
         for s in range(self.S):
-            for n in stage_param_names(model, self.cuts[s], self.cuts[s + 1]):
+            for n in placement_param_names(model, self.pl, s):
                 mod_name, _, pname = n.rpartition(".")
                 mod = model.get_submodule(mod_name)
                 setattr(mod, pname, torch.nn.Parameter(getattr(mod, pname).detach().to(self.devices[s])))
-            for n in stage_buffer_names(model, self.cuts[s], self.cuts[s + 1]):
+            for n in placement_buffer_names(model, self.pl, s):
                 mod_name, _, bname = n.rpartition(".")
                 mod = model.get_submodule(mod_name)
                 setattr(mod, bname, getattr(mod, bname).to(self.devices[s]))
         self.spaces = []
         for s in range(self.S):
-            names = set(stage_param_names(model, self.cuts[s], self.cuts[s + 1]))
+            names = set(placement_param_names(model, self.pl, s))
             own = [(n, p) for n, p in model.named_parameters() if n in names]
             self.spaces.append(FlatParameterSpace(own, device=self.devices[s]))
         # each stage's engine packs only its own layers' weights (stages sharing a device would
@@ -505,7 +577,7 @@ class GPipeLocal:
         # skips between stages: engines on the SAME device share one concat-buffer registry (the decoder
         # stage finds the encoder's concat buffer: zero-copy, as in a single-stage run); a skip that
         # changes device is written dense by its producer (one peer copy into the consumer's buffer)
-        _, send = stage_io(self.cuts, self.depth)
+        _, send = _stage_io(self.pl, self.depth)
         first = {}
         for s, b in enumerate(self.stage_blocks):
             if hasattr(b, "_cats"):
@@ -518,61 +590,69 @@ class GPipeLocal:
             if hasattr(b, "dense_skips"):
                 b.dense_skips = {int(n[len("skip"):]) for n, dst in send[s]
                                  if n.startswith("skip") and self.devices[dst] != self.devices[s]}
+        self.ins, _ = seg_io(self.pl, self.depth)
 
-    def _run(self, s, env, target, want):
-        dev = self.devices[s]
+    def _run(self, j, env, target, want):
+        dev = self.devices[self.pl.owner[j]]
         env = {k: v.to(dev, non_blocking=True) for k, v in env.items()}
         if target is not None:
             target = target.to(dev, non_blocking=True)
         ctx = torch.cuda.device(dev) if dev.type == "cuda" else _Null()
+        a, b = self.pl.seg_range(j)
         with ctx:
-            out = run_segment(self.stage_blocks[s], self.cuts[s], self.cuts[s + 1], self.depth, env, target, want)
+            out = run_segment(self.stage_blocks[self.pl.owner[j]], a, b, self.depth, env, target, want)
         _debug_point(dev)
         return out
 
+    def _wave(self, images, targets, want):
+        """Microbatches through the segments in wavefront order: at tick k, segments K-1..0 run
+        microbatch k-j (later segments issued first, like unet_model.py:33-44, so a downstream device
+        never waits behind upstream launches).  Returns the head outputs per microbatch."""
+        K, head = self.pl.K, self.pl.head_seg
+        xs = images.chunk(self.M)
+        M = len(xs)
+        ts = targets.chunk(M) if targets is not None else [None] * M
+        outs = {}
+        res = [None] * M
+        for k in range(M + K - 1):
+            for j in reversed(range(K)):
+                m = k - j
+                if not 0 <= m < M:
+                    continue
+                env = {name: outs[(p, m)][name] for name, p in self.ins[j]}
+                if j == 0:
+                    env["x"] = xs[m]
+                out = self._run(j, env, ts[m] if j == head else None, want if j == head else "partials")
+                if j == head:
+                    res[m] = out[want]
+                else:
+                    outs[(j, m)] = out
+        return res
+
     def forward_partials(self, images, targets):
-        M, S = self.M, self.S
-        xs, ts = images.chunk(M), targets.chunk(M)
-        envs = [{"x": x} for x in xs]
-        partials = [None] * M
-        # wavefront order: at tick k, stages S-1..0 run microbatch k-s (later stages issued first,
-        # like unet_model.py:33-44, so the downstream device never waits behind upstream launches)
-        for k in range(M + S - 1):
-            for s in reversed(range(S)):
-                m = k - s
-                if 0 <= m < M:
-                    out = self._run(s, envs[m], ts[m] if s == S - 1 else None, "partials")
-                    if s == S - 1:
-                        partials[m] = out["partials"].to(self.devices[0])
-                    else:
-                        envs[m] = out
-        return sum(partials)
+        return sum(p.to(self.devices[0]) for p in self._wave(images, targets, "partials"))
 
     def forward_loss(self, images, targets, dice=True):
         return loss_from_partials(self.forward_partials(images, targets), targets.numel(), dice)
 
     @torch.no_grad()
     def probs(self, images):
-        env = {"x": images}
-        for s in range(self.S):
-            env = self._run(s, env, None, "probs" if s == self.S - 1 else "partials")
-        return env["probs"].to(self.devices[0])
+        pl = self.pl
+        outs = {}
+        for j in range(pl.K):
+            env = {name: outs[p][name] for name, p in self.ins[j]}
+            if j == 0:
+                env["x"] = images
+            out = self._run(j, env, None, "probs" if j == pl.head_seg else "partials")
+            if j == pl.head_seg:
+                return out["probs"].to(self.devices[0])
+            outs[j] = out
 
     def forward_probs(self, images):
         """Differentiable pipelined forward to the probability map (``UNet(pipe=True).forward``):
         microbatches in wavefront order, outputs concatenated on the first device (reference
         ``torch.cat(ret).to('cuda:0')``, unet_model.py:53)."""
-        M, S = self.M, self.S
-        envs = [{"x": x} for x in images.chunk(M)]
-        outs = [None] * len(envs)
-        for k in range(len(envs) + S - 1):
-            for s in reversed(range(S)):
-                m = k - s
-                if 0 <= m < len(envs):
-                    envs[m] = self._run(s, envs[m], None, "probs" if s == S - 1 else "partials")
-                    if s == S - 1:
-                        outs[m] = envs[m]["probs"].to(self.devices[0])
-        return torch.cat(outs)
+        return torch.cat([p.to(self.devices[0]) for p in self._wave(images, None, "probs")])
 
 
 class _Null:

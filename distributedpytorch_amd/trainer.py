@@ -249,9 +249,9 @@ class PipelineLocalStrategy(Strategy):
     def __init__(self, cfg, model, devices):
         super().__init__(cfg)
         H, W = cfg.img_size
-        mode, cuts, M = mp_plan(cfg, len(devices))
-        self.pipe = GPipeLocal(model, devices, M, cfg.backend, cfg.dtype, img_hw=(H, W),
-                               mode="balanced" if mode == "time" else mode, cuts=cuts)
+        self.plan = mp_plan(cfg, len(devices))
+        self.pipe = GPipeLocal(model, devices, self.plan.microbatches, cfg.backend, cfg.dtype, img_hw=(H, W),
+                               placement=self.plan.placement)
         self.model = model
         self.device = self.pipe.devices[0]
         self.optimizer = FusedAdam(self.pipe.spaces, lr=cfg.lr, weight_decay=cfg.weight_decay)
@@ -279,10 +279,10 @@ class PipelineDistStrategy(Strategy):
         self.device = torch.device(device)
         self.model = model.to(self.device)
         H, W = cfg.img_size
-        mode, cuts, M = mp_plan(cfg, self.world)
-        self.pipe = GPipeDist(self.model, M, cfg.backend, cfg.dtype, img_hw=(H, W),
-                              mode="balanced" if mode == "time" else mode, cuts=cuts)
-        self.is_main = self.pipe.is_last  # the last stage owns the loss; rank 0 saves
+        self.plan = mp_plan(cfg, self.world)
+        self.pipe = GPipeDist(self.model, self.plan.microbatches, cfg.backend, cfg.dtype, img_hw=(H, W),
+                              placement=self.plan.placement, policy=self.plan.policy, orders=self.plan.orders)
+        self.is_main = self.pipe.is_last  # the head stage owns the loss; rank 0 saves
         self.optimizer = FusedAdam(self.pipe.space, lr=cfg.lr, weight_decay=cfg.weight_decay)
 
     def train_step(self, images, targets):

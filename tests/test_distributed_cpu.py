@@ -4,7 +4,8 @@
   scheduler decision is the same on every rank (reference defect A5); rank-0-only checkpoint with
   the reference ``module.`` prefix.
 * GPipe over process groups: loss and every gradient equal a single-process run of the full batch
-  (reference MP probe7 equivalence), for the reference 2-stage cut and a balanced 3-stage cut.
+  (reference MP probe7 equivalence), for the reference 2-stage cut, balanced contiguous cuts (up to 8
+  stages), half-block cuts and the mirrored V placements (2 / 3 / 4 / 8 stages).
 """
 import os
 import socket
@@ -120,9 +121,15 @@ def _pipe_worker(rank, world, port, microbatches, mode, q, model_name="unet-tiny
     model = build_model(model_name)
     ref = build_model(model_name)
     ref.load_state_dict(model.state_dict())
+    from distributedpytorch_amd.parallel.placement import parse_placement, v_partition
     cuts = list(mode) if isinstance(mode, (list, tuple)) else None
+    placement = None
+    if mode == "v":
+        placement = v_partition(model.cfg, world, 32, 32)
+    elif isinstance(mode, str) and (":" in mode or "@" in mode):
+        placement = parse_placement(mode)
     pipe = GPipeDist(model, microbatches, backend="torch", dtype="fp32", img_hw=(32, 32),
-                     mode="balanced" if cuts else mode, cuts=cuts)
+                     mode="balanced" if (cuts or placement) else mode, cuts=cuts, placement=placement)
     x, t = _data(4, seed=5)
     loss = pipe.train_step(x if pipe.is_first else None, t if pipe.is_last else None, 4, (32, 32))
     lref = bce_dice_from_probs(ref(x), t)
@@ -146,7 +153,7 @@ def _pipe_worker(rank, world, port, microbatches, mode, q, model_name="unet-tiny
         # (BatchNorm running statistics: the reference model ran one more train-mode forward above)
         sd_ok = set(sd) == set(ref.state_dict()) and all(torch.equal(sd[k], v) for k, v in ref.state_dict().items()
                                                          if "running_" not in k and "num_batches" not in k)
-    q.put((rank, None if loss is None else float(loss), float(lref), bad, nown, probs_ok, sd_ok))
+    q.put((rank, None if loss is None else float(loss), float(lref), bad, nown, probs_ok, sd_ok, pipe.is_last))
     dist.destroy_process_group()
 
 
@@ -154,10 +161,25 @@ def _pipe_worker(rank, world, port, microbatches, mode, q, model_name="unet-tiny
 # enc0 enc1 mid dec0 dec1 head; [0, 1.5, 3.5, 6] splits enc1 and dec0, [0, .5, 2.5, 4.5, 6] the first
 # encoder block, the bottleneck and the last decoder block; unet-tiny-bn adds BatchNorm + bilinear ups
 # (one microbatch: BatchNorm statistics over a microbatch are not the full batch's)
+# V placements (parallel/placement.py): stage s owns encoder level(s) s and the same decoder level(s); the
+# head stage is stage 0.  "v:0,1,3,6" keeps mid with enc1 on stage 1, so skip1 crosses 1 -> 0 with x;
+# "v:0,1,2,5,8,10" (unet-tiny4) sends skips 2 and 3 from stage 2 to stage 1 in one message while skip 1 is
+# handed over locally between stage 1's two segments; "0,1,5,8,10@0,1,0,1" is not a V at all (stage 1
+# owns enc1..mid and the last decoder + head): two segments of one stage feed the other stage on
+# separate communicators
 @pytest.mark.parametrize("world,mb,mode,model_name", [(2, 2, "reference", "unet-tiny"), (3, 4, "balanced", "unet-tiny"),
                                                       (3, 2, (0, 1.5, 3.5, 6), "unet-tiny"),
                                                       (4, 2, (0, 0.5, 2.5, 4.5, 6), "unet-tiny"),
-                                                      (3, 1, (0, 1.5, 3.5, 6), "unet-tiny-bn")])
+                                                      (3, 1, (0, 1.5, 3.5, 6), "unet-tiny-bn"),
+                                                      (2, 4, "v", "unet-tiny"),
+                                                      (2, 2, "v:0,1.5,3.5,6", "unet-tiny"),
+                                                      (2, 2, "v:0,1,3,6", "unet-tiny"),
+                                                      (3, 2, "v:0,1,2,5,8,10", "unet-tiny4"),
+                                                      (2, 4, "0,1,5,8,10@0,1,0,1", "unet-tiny4"),
+                                                      (4, 4, "v", "unet-tiny4"),
+                                                      (2, 1, "v", "unet-tiny-bn"),
+                                                      (8, 2, "v", "unet-tiny4"),
+                                                      (8, 2, "balanced", "unet-tiny4")])
 def test_gpipe_gloo_matches_single_process(world, mb, mode, model_name):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -165,15 +187,16 @@ def test_gpipe_gloo_matches_single_process(world, mb, mode, model_name):
     procs = [ctx.Process(target=_pipe_worker, args=(r, world, port, mb, mode, q, model_name)) for r in range(world)]
     for p in procs:
         p.start()
-    res = sorted([q.get(timeout=240) for _ in procs])
+    res = sorted([q.get(timeout=300) for _ in procs], key=lambda r: r[0])
     for p in procs:
         p.join(timeout=60)
     total_own = 0
-    for rank, loss, lref, bad, nown, probs_ok, sd_ok in res:
+    assert sum(r[-1] for r in res) == 1                # exactly one head stage
+    for rank, loss, lref, bad, nown, probs_ok, sd_ok, is_head in res:
         assert not bad, f"rank {rank}: grads differ for {bad}"
         total_own += nown
         assert probs_ok and sd_ok
-        if rank == world - 1:
+        if is_head:
             assert abs(loss - lref) < 1e-5
     assert total_own == len(list(build_model(model_name).parameters()))   # each parameter owned by one stage
 

@@ -166,9 +166,15 @@ def _pipe_worker(rank, world, port, name, hw, M, cut, q):
         ref_sd = {k: v.detach().cpu() for k, v in ref.state_dict().items()}
         del sd
         model = model.cuda()
+        from distributedpytorch_amd.parallel.placement import parse_placement, v_partition
         cuts = list(cut) if isinstance(cut, (list, tuple)) else None
-        pipe = GPipeDist(model, M, backend="hip", dtype="bf16", img_hw=(hw, hw), mode="balanced" if cuts else cut,
-                         cuts=cuts)
+        pl = None
+        if cut == "v":
+            pl = v_partition(model.cfg, world, hw, hw)
+        elif isinstance(cut, str) and ":" in cut:
+            pl = parse_placement(cut)
+        pipe = GPipeDist(model, M, backend="hip", dtype="bf16", img_hw=(hw, hw),
+                         mode="balanced" if (cuts or pl) else cut, cuts=cuts, placement=pl)
         pipe.space.zero_grad()
         loss = pipe.train_step(x if pipe.is_first else None, t if pipe.is_last else None, B, (hw, hw),
                                loss_scale=float(B))
@@ -187,10 +193,10 @@ def _pipe_worker(rank, world, port, name, hw, M, cut, q):
         sd_ok = True
         if rank == 0:
             sd_ok = set(gsd) == set(ref_sd) and all(torch.equal(gsd[k].cpu(), v) for k, v in ref_sd.items())
-        q.put((rank, pipe.cuts, lrel, bad, n_own, sd_ok, None))
+        q.put((rank, str(pipe.pl), lrel, bad, n_own, sd_ok, pipe.is_last, None))
     except Exception as e:
         import traceback
-        q.put((rank, None, None, [], 0, False, repr(e) + traceback.format_exc()[-2000:]))
+        q.put((rank, None, None, [], 0, False, False, repr(e) + traceback.format_exc()[-2000:]))
     finally:
         if dist.is_initialized():
             dist.destroy_process_group()
@@ -201,14 +207,22 @@ def _pipe_worker(rank, world, port, name, hw, M, cut, q):
                                                  ("unet", 64, 4, 4, "balanced"),
                                                  ("unet-xl", 64, 8, 4, "balanced"),
                                                  # stage boundaries inside DoubleConvs (half-block cuts)
-                                                 ("unet", 64, 4, 2, (0, 2.5, 5, 7.5, 10))])
+                                                 ("unet", 64, 4, 2, (0, 2.5, 5, 7.5, 10)),
+                                                 # mirrored V placements: skips handed over between a stage's
+                                                 # own segments (zero-copy concat buffer), head on stage 0
+                                                 ("unet", 64, 2, 4, "v"),
+                                                 ("unet", 64, 4, 2, "v"),
+                                                 ("unet-xl", 64, 8, 2, "v"),
+                                                 ("unet", 64, 2, 2, "v:0,1.5,7.5,10"),
+                                                 ("unet", 64, 3, 2, "v:0,1,2,5,8,10")])
 def test_gpipe_hip_matches_single_device(hip_lib, name, hw, world, M, cut):
     from distributedpytorch_amd.models.unet import build_model
     res = _run(_pipe_worker, world, name, hw, M, cut, timeout=360)
     n_total = sum(r[4] for r in res)
     assert n_total == len(list(build_model(name).parameters())), "every parameter owned by exactly one stage"
-    for rank, cuts, lrel, bad, n_own, sd_ok, _ in res:
-        assert not bad, f"stage {rank} (cuts {cuts}): gradient cosine too low {bad}"
+    assert sum(r[6] for r in res) == 1, "exactly one head stage"
+    for rank, cuts, lrel, bad, n_own, sd_ok, is_head, _ in res:
+        assert not bad, f"stage {rank} ({cuts}): gradient cosine too low {bad}"
         assert sd_ok, "gather_state_dict differs from the model"
-        if rank == world - 1:
+        if is_head:
             assert lrel is not None and lrel < 1e-3, f"loss rel err {lrel}"

@@ -33,15 +33,19 @@ def _single(model, x, t):
     return loss.detach(), {n: p.grad.detach().clone() for n, p in model.named_parameters()}
 
 
-def test_pipeline_local_hip_matches_single(hip_lib):
+@pytest.mark.parametrize("cut", ["reference", "v"])
+def test_pipeline_local_hip_matches_single(hip_lib, cut):
     from distributedpytorch_amd.models.unet import build_model
     from distributedpytorch_amd.parallel.pipeline import GPipeLocal
+    from distributedpytorch_amd.parallel.placement import Placement
     torch.manual_seed(0)
     a, b = build_model("unet"), build_model("unet")
     b.load_state_dict(a.state_dict())
     x, t = _batch()
     l_ref, g_ref = _single(b.cuda(), x, t)
-    pipe = GPipeLocal(a, ["cuda:0", "cuda:0"], 2, backend="hip", dtype="bf16", img_hw=(64, 64), mode="reference")
+    pl = Placement.mirrored([0, 2, 7, 10]) if cut == "v" else None
+    pipe = GPipeLocal(a, ["cuda:0", "cuda:0"], 2, backend="hip", dtype="bf16", img_hw=(64, 64), mode="reference",
+                      placement=pl)
     for s in pipe.spaces:
         s.zero_grad()
     loss = pipe.forward_loss(x, t)

@@ -4,11 +4,12 @@ torch coalesces every ``batch_isend_irecv`` of a process group onto that group's
 communicator and stream, in issue order.  If one rank both received and sent on one group, a receive
 it pre-posted for microbatch m+1 would hold back its send of microbatch m (a middle stage could
 not hand m downstream before m+1 arrived from upstream).  ``GPipeDist`` therefore gives every
-sending stage its own group (``sender_groups``): these tests record each rank's posted operations
-per group and assert that on every group a rank only sends (its own group) or only receives (any
-other group) -- so no send can follow an unmatched receive on one stream -- and that the pipelined
-step still equals a single-process step of the full batch (reference ``model/unet_model.py:33-44``
-issues the downstream stage first for the same reason).
+sending SEGMENT its own group (``channel_members``; its owner stage is the only sender): these tests
+record each rank's posted operations per group and assert that on every group a rank only sends (a
+segment it owns) or only receives from the segment's owner -- so no send can follow an unmatched
+receive on one stream -- and that the pipelined step still equals a single-process step of the full
+batch (reference ``model/unet_model.py:33-44`` issues the downstream stage first for the same reason),
+for contiguous and mirrored (V) placements.
 """
 import os
 import socket
@@ -30,7 +31,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, microbatches, q):
+def _worker(rank, world, port, microbatches, q, kind="balanced"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
     torch.set_num_threads(1)
@@ -41,7 +42,10 @@ def _worker(rank, world, port, microbatches, q):
         model = build_model("unet-tiny4")
         ref = build_model("unet-tiny4")
         ref.load_state_dict(model.state_dict())
-        pipe = GPipeDist(model, microbatches, backend="torch", dtype="fp32", img_hw=(32, 32), mode="balanced")
+        from distributedpytorch_amd.parallel.placement import v_partition
+        pl = v_partition(model.cfg, world, 32, 32) if kind == "v" else None
+        pipe = GPipeDist(model, microbatches, backend="torch", dtype="fp32", img_hw=(32, 32), mode="balanced",
+                         placement=pl)
         g = torch.Generator().manual_seed(5)
         x = torch.rand(4, 3, 32, 32, generator=g)
         t = (torch.rand(4, 1, 32, 32, generator=g) > 0.5).float()
@@ -52,18 +56,19 @@ def _worker(rank, world, port, microbatches, q):
         refp = dict(ref.named_parameters())
         bad = [n for n, p in model.named_parameters()
                if p.requires_grad and p.grad is not None and not torch.allclose(p.grad, refp[n].grad, atol=1e-5)]
-        q.put((rank, pipe.op_log, pipe.members, pipe.cuts, None if loss is None else float(loss), float(lref), bad))
+        q.put((rank, pipe.op_log, pipe.members, list(pipe.pl.owner), None if loss is None else float(loss),
+               float(lref), bad, pipe.is_last))
     except Exception as e:   # surface the failure instead of a queue timeout
-        q.put((rank, repr(e), None, None, None, None, None))
+        q.put((rank, repr(e), None, None, None, None, None, None))
     finally:
         dist.destroy_process_group()
 
 
-def _run(world, microbatches):
+def _run(world, microbatches, kind="balanced"):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, microbatches, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, microbatches, q, kind)) for r in range(world)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=300) for _ in procs], key=lambda r: r[0])
@@ -72,45 +77,45 @@ def _run(world, microbatches):
     return res
 
 
-@pytest.mark.parametrize("world", [4, 8])
-def test_no_send_behind_own_receive(world):
-    res = _run(world, microbatches=4)
-    for rank, log, members, cuts, loss, lref, bad in res:
+@pytest.mark.parametrize("world,kind", [(4, "balanced"), (8, "balanced"), (4, "v"), (8, "v")])
+def test_no_send_behind_own_receive(world, kind):
+    res = _run(world, microbatches=4, kind=kind)
+    for rank, log, members, owner, loss, lref, bad, is_head in res:
         assert isinstance(log, list), f"rank {rank} failed: {log}"
         assert log, f"rank {rank} posted nothing"
         groups = {}
-        for grp, kind, peer in log:
-            assert rank in members[grp], f"rank {rank} used group {grp} it is not a member of"
-            groups.setdefault(grp, []).append((kind, peer))
-        for grp, ops in groups.items():
+        for ch, k, peer in log:
+            assert rank in members[ch], f"rank {rank} used channel {ch} it is not a member of"
+            groups.setdefault(ch, []).append((k, peer))
+        for ch, ops in groups.items():
             kinds = {k for k, _ in ops}
-            if grp == rank:
-                assert kinds == {"send"}, f"rank {rank}: its own group carries {kinds}"
+            if owner[ch] == rank:
+                assert kinds == {"send"}, f"rank {rank}: its own channel {ch} carries {kinds}"
             else:
-                assert kinds == {"recv"} and all(p == grp for _, p in ops), \
-                    f"rank {rank}: group {grp} carries {ops}"
+                assert kinds == {"recv"} and all(p == owner[ch] for _, p in ops), \
+                    f"rank {rank}: channel {ch} carries {ops}"
             # the VERDICT's property, stated directly: no send after a receive on one group
             seen_recv = False
             for k, _ in ops:
-                assert not (k == "send" and seen_recv), f"rank {rank}: send queued behind a receive on group {grp}"
+                assert not (k == "send" and seen_recv), f"rank {rank}: send queued behind a receive on channel {ch}"
                 seen_recv |= k == "recv"
         assert not bad, f"rank {rank}: gradients differ for {bad}"
-        if rank == world - 1:
+        if is_head:
             assert abs(loss - lref) < 1e-5, (loss, lref)
-    # every stage sends: activations downstream (all but the last), gradients upstream (all but the first)
+    # every stage sends: activations downstream, gradients upstream
     assert all(any(k == "send" for _, k, _ in r[1]) for r in res)
 
 
 def test_sender_groups_cover_every_edge():
-    from distributedpytorch_amd.parallel.pipeline import sender_groups, stage_io
     from distributedpytorch_amd.models.blocks import partition
+    from distributedpytorch_amd.parallel.placement import Placement, channel_members, seg_io, v_partition
     cfg = build_model("unet-tiny4").cfg
     for S in (2, 3, 4, 8):
-        cuts = partition(cfg, S, 64, 64, mode="balanced")
-        recv, send = stage_io(cuts, cfg.depth)
-        members = sender_groups(recv, send)
-        for s in range(S):
-            for _, d in send[s]:          # forward activation s -> d rides group s
-                assert d in members[s]
-            for _, p in recv[s]:          # backward gradient s -> p rides group s
-                assert p in members[s]
+        for pl in (Placement.contiguous(partition(cfg, S, 64, 64, mode="balanced")), v_partition(cfg, S, 64, 64)):
+            ins, outs = seg_io(pl, cfg.depth)
+            members = channel_members(pl, cfg.depth)
+            for j in range(pl.K):
+                for _, c in outs[j]:      # forward activation j -> c rides channel j
+                    assert pl.owner[c] in members[j]
+                for _, p in ins[j]:       # backward gradient j -> p rides channel j
+                    assert pl.owner[p] in members[j]

@@ -1,13 +1,18 @@
 #!/usr/bin/env python3
-"""Pipeline plan from measured per-block times (tools/block_times.py) and the GPipe schedule model
-(distributedpytorch_amd/parallel/schedule.py): for BASELINE configs 4 (UNet 512^2, 2 stages) and 5
-(UNet-XL 1024^2, 8 stages) the simulated step, img/s and efficiency of
+"""Pipeline plans from measured per-block times (tools/block_times.py) and the link-queueing GPipe
+schedule model (distributedpytorch_amd/parallel/schedule.py).
 
-  * the reference cut (encoder+mid | decoder+head) / the FLOP-balanced cut the engine used so far, and
-  * the time-balanced cut the simulator finds,
+For BASELINE config 4 (UNet 512^2, 2 stages) and config 5 (UNet-XL 1024^2, 8 stages), at every
+microbatch count the table supports and at two effective xGMI rates per directed peer link (100 and
+64 GB/s), the simulated step, img/s, efficiency and busiest-link load of
 
-at every microbatch count the table supports; writes a text table and the chosen defaults
-(distributedpytorch_amd/parallel/plans.json, read by bench.py / the trainer for ``--mp-cut auto``).
+  * the reference cut (encoder+mid | decoder+head, 2 stages) and the FLOP-balanced contiguous cut,
+  * the best contiguous placement the search finds (half-block cuts allowed),
+  * the best mirrored V placement (stage s owns encoder level(s) s and the same decoder level(s)),
+
+then writes a text table and the chosen plans (distributedpytorch_amd/parallel/plans.json, read by
+``--mp-cut auto|time``): placement, microbatch count, op-order policy and the per-stage op order the
+simulation used (the engine issues exactly that order).
 
     python tools/pipeline_plan.py profiles/block_times_unet_512_r04.json profiles/block_times_unetxl_1024_r04.json
 """
@@ -20,62 +25,82 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from distributedpytorch_amd.models.blocks import partition          # noqa: E402
 from distributedpytorch_amd.models.unet import PRESETS              # noqa: E402
-from distributedpytorch_amd.parallel.schedule import load_table, plan, single_device_ms, unit_table  # noqa: E402
+from distributedpytorch_amd.parallel.placement import Placement, describe, v_partition  # noqa: E402
+from distributedpytorch_amd.parallel.schedule import (evaluate_placement, load_table, search,  # noqa: E402
+                                                      simulate_table, single_device_ms, unit_table)
 
 
-def rows_for(table, S, batch, cuts, label, **kw):
-    out = []
-    for r in plan(table, S, batch, cuts=cuts, **kw):
-        r["partition"] = label
-        out.append(r)
-    return out
+def fmt(r, label):
+    return (f"{label:16s} {r['microbatches']:3d} {r['mb']:4d} {str(r['cuts']):52s} {r['policy']:7s} "
+            f"{r['step_ms']:9.2f} {r['img_s']:8.1f} {r.get('scaling_efficiency', float('nan')):6.3f} "
+            f"{r['max_link_gb']:7.2f} {r['max_link_busy_ms']:8.1f}")
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("tables", nargs="+")
-    ap.add_argument("--link-gbs", type=float, default=100.0, help="effective xGMI GB/s per peer pair")
-    ap.add_argument("--out", default="profiles/pipeline_plan_r04.txt")
+    ap.add_argument("--links", default="100,64", help="effective GB/s per directed xGMI peer link (first: the plan's)")
+    ap.add_argument("--out", default="profiles/pipeline_plan_r05.txt")
     ap.add_argument("--plans", default="distributedpytorch_amd/parallel/plans.json")
     a = ap.parse_args()
+    links = [float(v) for v in a.links.split(",")]
     lines, plans = [], {}
     for path in a.tables:
         t = load_table(path)
+        ut = unit_table(t) if any("units" in row for row in t["per_mb"].values()) else t
         model, (h, w) = t["model"], t["img"]
         cfg = PRESETS[model]
         mbs = sorted(int(k) for k in t["per_mb"])
-        # config 4: UNet 512^2 on 2 stages at the bench batch; config 5: UNet-XL 1024^2 on 8 stages at the
-        # single-GPU bench batch (16) and at the larger global batches the HBM allows (more microbatches:
-        # a smaller fill / drain bubble)
-        configs = [(2, max(mbs))] if model == "unet" else [(8, 16), (8, 32), (8, 64)]
+        configs = [(2, max(mbs)), (4, max(mbs))] if model == "unet" else [(8, 16), (8, 32), (8, 64)]
         for S, batch in configs:
-            kw = dict(link_gbs=a.link_gbs)
             t1 = single_device_ms(t, batch)
-            lines.append(f"## {model} {h}x{w}, {S} stages, global batch {batch} "
-                         f"(single-GPU step {'%.1f ms' % t1 if t1 else 'n/a'})")
-            ref = partition(cfg, S, h, w, mode="reference") if S == 2 else None
-            flop = partition(cfg, S, h, w, mode="balanced")
-            allr = []
-            if ref is not None:
-                allr += rows_for(t, S, batch, ref, "reference", **kw)
-            allr += rows_for(t, S, batch, flop, "flop-balanced", **kw)
-            allr += rows_for(t, S, batch, None, "time-balanced", **kw)
-            if any("units" in row for row in t["per_mb"].values()):
-                # conv-level stage boundaries: cuts between the two convs of a DoubleConv (b + 0.5)
-                allr += rows_for(unit_table(t), S, batch, None, "time+conv-cut", **kw)
-            lines.append(f"{'partition':14s} {'M':>3s} {'mb':>4s} {'cuts':40s} {'step ms':>9s} {'img/s':>8s} "
-                         f"{'util':>6s} {'eff':>6s}")
-            for r in allr:
-                lines.append(f"{r['partition']:14s} {r['microbatches']:3d} {r['mb']:4d} {str(r['cuts']):40s} "
-                             f"{r['step_ms']:9.2f} {r['img_s']:8.1f} {r['utilisation']:6.3f} "
-                             f"{r.get('scaling_efficiency', float('nan')):6.3f}")
-            best = max((r for r in allr if r["partition"] in ("time-balanced", "time+conv-cut")), key=lambda r: r["img_s"])
-            lines.append(f"-> chosen: {best['partition']} cut {best['cuts']}, {best['microbatches']} microbatches "
-                         f"({best['img_s']} img/s predicted)")
+            best_v = None
+            for gbs in links:
+                kw = dict(link_gbs=gbs)
+                lines.append(f"## {model} {h}x{w}, {S} stages, global batch {batch}, xGMI {gbs:g} GB/s per directed link "
+                             f"(single-GPU step {'%.1f ms' % t1 if t1 else 'n/a'})")
+                lines.append(f"{'placement':16s} {'M':>3s} {'mb':>4s} {'cuts':52s} {'policy':7s} {'step ms':>9s} "
+                             f"{'img/s':>8s} {'eff':>6s} {'link GB':>7s} {'link ms':>8s}")
+                fixed = []
+                if S == 2:
+                    fixed.append(("reference", Placement.contiguous(partition(cfg, S, h, w, mode="reference"))))
+                fixed.append(("flop-contig", Placement.contiguous(partition(cfg, S, h, w, mode="balanced"))))
+                fixed.append(("flop-v", v_partition(cfg, S, h, w)))
+                for label, pl in fixed:
+                    for pol in ("feed", "further"):
+                        for r in evaluate_placement(ut, pl, batch, policy=pol, **kw):
+                            lines.append(fmt(r, label))
+                cont = search(ut, S, batch, "contiguous", **kw)
+                for r in cont:
+                    lines.append(fmt(r, "search-contig"))
+                vv = search(ut, S, batch, "v", **kw)
+                for r in vv:
+                    lines.append(fmt(r, "search-v"))
+                bc = max(cont, key=lambda r: r["img_s"])
+                bv = max(vv, key=lambda r: r["img_s"])
+                lines.append(f"-> best contiguous {bc['cuts']} M={bc['microbatches']}: {bc['img_s']} img/s "
+                             f"(eff {bc.get('scaling_efficiency')}); best V {bv['cuts']} M={bv['microbatches']}: "
+                             f"{bv['img_s']} img/s (eff {bv.get('scaling_efficiency')})")
+                lines.append("")
+                if gbs == links[0]:
+                    best_v = bv
+                else:          # the chosen plan re-simulated at the slower link
+                    pl = Placement(best_v["cuts"], best_v["owner"])
+                    r = evaluate_placement(ut, pl, batch, Ms=[best_v["microbatches"]], policy=best_v["policy"], **kw)[0]
+                    best_v.setdefault("at_slow_link", {})[f"{gbs:g}"] = {
+                        "img_s": r["img_s"], "efficiency": r.get("scaling_efficiency")}
+            pl = Placement(best_v["cuts"], best_v["owner"])
+            M = best_v["microbatches"]
+            tl = simulate_table(ut, pl, batch // M, M, policy=best_v["policy"], link_gbs=links[0])
+            lines.append(f"-> chosen for {model} {S} stages b{batch}: {pl} M={M} policy {best_v['policy']}: "
+                         f"{best_v['img_s']} img/s predicted at {links[0]:g} GB/s; " + "; ".join(describe(pl, cfg.depth)))
             lines.append("")
-            plans[f"{model}:{h}x{w}:{S}:{batch}"] = {"cuts": best["cuts"], "microbatches": best["microbatches"],
-                                                     "predicted_img_s": best["img_s"],
-                                                     "predicted_efficiency": best.get("scaling_efficiency")}
+            plans[f"{model}:{h}x{w}:{S}:{batch}"] = {
+                "cuts": best_v["cuts"], "owner": best_v["owner"], "placement": pl.kind, "microbatches": M,
+                "policy": best_v["policy"], "orders": tl.orders,
+                "predicted_img_s": best_v["img_s"], "predicted_efficiency": best_v.get("scaling_efficiency"),
+                "link_gbs": links[0], "at_slow_link": best_v.get("at_slow_link", {}),
+                "source": os.path.basename(path)}
     txt = "\n".join(lines)
     print(txt)
     if a.out:
