@@ -168,11 +168,12 @@ class TorchBlocks:
 
 
 def run_segment(blocks, start: int, end: int, depth: int, env: Dict[str, torch.Tensor],
-                target: torch.Tensor = None, want: str = "partials") -> Dict[str, torch.Tensor]:
+                target: torch.Tensor = None, want: str = "partials", emit=None) -> Dict[str, torch.Tensor]:
     """Run blocks ``[start, end)`` on ``env`` (mutated copy returned).
 
     If the head block is included the result holds ``partials`` (training, needs ``target``) or
-    ``probs`` (inference) instead of ``x``.
+    ``probs`` (inference) instead of ``x``.  ``emit(name, tensor)`` is called as soon as an encoder
+    level's skip exists (a pipeline stage starts sending it while its deeper levels compute).
     """
     env = dict(env)
     if want == "partials" and end == n_blocks(depth) and hasattr(blocks, "expect_target"):
@@ -189,6 +190,8 @@ def run_segment(blocks, start: int, end: int, depth: int, env: Dict[str, torch.T
                 else:
                     s, env["x"] = blocks.enc(i, env["x"]) if part == "full" else blocks.enc_b(i, env["x"])
                     env[skip_name(i)] = s
+                    if emit is not None:
+                        emit(skip_name(i), s)
             elif kind == "mid":
                 env["x"] = {"full": blocks.mid, "a": blocks.mid_a, "b": blocks.mid_b}[part](env["x"])
             elif kind == "dec":

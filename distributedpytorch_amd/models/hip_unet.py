@@ -154,6 +154,8 @@ class HipBlocks:
         # bytes, the layer that crossed it launches over the microbatches it has (a partial merge)
         self.defer_cap_bytes = 8 << 30
         self._deferred_bytes = 0
+        self.n_multi_launches = 0     # merged weight-gradient launches so far (tests / tools/defer_mem.py)
+        self.peak_deferred_bytes = 0
 
     # ------------------------------------------------------------------ weight packing
     def _build_packing(self):
@@ -469,12 +471,16 @@ class HipBlocks:
             ent[1].append(g)
             ent[2].append(x)
             self._deferred_bytes += _nbytes(g) + _nbytes(x)
-            if len(ent[1]) >= self.defer_wgrad or self._deferred_bytes > self.defer_cap_bytes:
-                # every microbatch of this layer is in (or the deferral hit its memory cap): launch now,
-                # so it overlaps the rest of the backward
-                del self._deferred[id(c)]
-                self._deferred_bytes -= sum(_nbytes(t) for t in ent[1] + ent[2])
-                self._launch_multi(c, ent[1], ent[2])
+            self.peak_deferred_bytes = max(self.peak_deferred_bytes, self._deferred_bytes)
+            if len(ent[1]) >= self.defer_wgrad:
+                # every microbatch of this layer is in: launch now, so it overlaps the rest of the backward
+                self._launch_deferred(id(c))
+            # memory cap: launch the layers holding the most deferred bytes until the total is
+            # back under the cap -- not only the one that crossed it, which would leave the others over the
+            # cap and turn every later weight gradient into a per-microbatch launch
+            while self._deferred_bytes > self.defer_cap_bytes and self._deferred:
+                self._launch_deferred(max(self._deferred, key=lambda k: sum(
+                    _nbytes(t) for t in self._deferred[k][1] + self._deferred[k][2])))
             if not self._defer_window and not self._flush_queued:
                 # end of this backward: leftovers, the merged stream's join, the readiness announcements
                 torch.autograd.Variable._execution_engine.queue_callback(self.flush_wgrad)
@@ -556,6 +562,12 @@ class HipBlocks:
         self._defer_window = False
         self.flush_wgrad()
 
+    def _launch_deferred(self, key):
+        c, gs, xs = self._deferred.pop(key)
+        self._deferred_bytes -= sum(_nbytes(t) for t in gs + xs)
+        self.n_multi_launches += 1
+        self._launch_multi(c, gs, xs)
+
     def _launch_multi(self, c, gs, xs):
         """One weight-gradient launch over the deferred microbatches of conv ``c``, on a stream of its
         own: the per-block joins (side stream) must not wait for it, only flush_wgrad does."""
@@ -580,10 +592,9 @@ class HipBlocks:
         """Run the deferred weight gradients still waiting for microbatches (one launch per layer over
         the ones that arrived), join the side stream, announce the gradients."""
         self._flush_queued = False
-        deferred, self._deferred = self._deferred, {}
+        for key in list(self._deferred):
+            self._launch_deferred(key)
         self._deferred_bytes = 0
-        for c, gs, xs in deferred.values():
-            self._launch_multi(c, gs, xs)
         if self._keep2:
             torch.cuda.current_stream(self.device).wait_stream(self.side2)
             self._keep2 = []

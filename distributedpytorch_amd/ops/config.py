@@ -80,6 +80,11 @@ RUNTIME_ENV = {
     "DPA_ARCH": "tools/build_hip.py: --offload-arch (default gfx950)",
 }
 
+# variables earlier rounds read and that now do nothing: setting one is warned about, not ignored silently
+REMOVED_ENV = {
+    "DPA_DP_OVERLAP": "removed in round 3: use --no-comm-overlap (DDP / DP) for one reduction after the backward",
+}
+
 # the DPA_NO_* switches turn a default-on feature off; the others carry their value
 _NEGATED = {k.env for k in KNOBS if k.env.startswith("DPA_NO_")}
 
@@ -148,13 +153,21 @@ def allowed_env() -> Dict[str, str]:
     """Every DPA_* variable the package reads, with its meaning."""
     out = {k.env: k.doc for k in KNOBS}
     out.update(RUNTIME_ENV)
+    out.update({k: "(no effect) " + v for k, v in REMOVED_ENV.items()})
     return out
 
 
 _logged = [False]
 
 
+def removed_in_env(env: Mapping[str, str] = None) -> Dict[str, str]:
+    env = os.environ if env is None else env
+    return {k: v for k, v in REMOVED_ENV.items() if k in env}
+
+
 def log_once(cfg: KernelConfig) -> None:
     if not _logged[0]:
         _logged[0] = True
         log.info(cfg.describe())
+        for k, why in removed_in_env().items():
+            log.warning("%s is set but has no effect: %s", k, why)

@@ -380,15 +380,31 @@ class GPipeDist:
             if j == 0:
                 env["x"] = xs[m]
             a, b = pl.seg_range(j)
+            # a skip leaving this stage is sent the moment its encoder level finishes, while
+            # the deeper levels compute; per destination the tensors go in the message's (sorted) order,
+            # which is the production order (skips by level, x last), so the receiver's one grouped
+            # receive matches the sender's separate sends
+            sent = {d: 0 for d in self.fwd_msgs[j]}
+
+            def emit(name, t, j=j):
+                for d, edges in self.fwd_msgs[j].items():
+                    k = sent[d]
+                    if k < len(edges) and edges[k][0] == name:
+                        pending.append(self._post(sends=[(t, d)], channel=j))
+                        sent[d] = k + 1
+
             with trace_range(f"stage{me}_fwd_seg{j}_mb{m}"):
-                out = run_segment(self.blocks, a, b, self.depth, env, ts[m] if j == head else None, "partials")
+                out = run_segment(self.blocks, a, b, self.depth, env, ts[m] if j == head else None, "partials",
+                                  emit=emit if self.fwd_msgs[j] else None)
             _debug_point(self.device)
             if j == head:
                 partials[m] = out["partials"]
                 continue
             fout[(j, m)] = {name: out[name] for name, _ in self.outs[j]}
             for d, edges in self.fwd_msgs[j].items():
-                pending.append(self._post(sends=[(out[name], d) for name, _ in edges], channel=j))
+                rest = edges[sent[d]:]
+                if rest:
+                    pending.append(self._post(sends=[(out[name], d) for name, _ in rest], channel=j))
         frx = None
 
         # ---------------- backward (each segment's microbatches in reverse order) ----------------

@@ -411,6 +411,9 @@ def train(cfg: TrainConfig):
     _setup_logging(cfg, rank)
     log.info("UNet for Carvana Image Masking (Segmentation)")
     log.info(f"config: {cfg.to_dict()}")
+    from .ops.config import removed_in_env
+    for k, why in removed_in_env().items():
+        log.warning(f"{k} is set but has no effect: {why}")
     model = build_model(cfg.model)
     if cfg.checkpoint is not None:
         load_model_state(model, os.path.join(cfg.out_dir, "checkpoints", f"{cfg.checkpoint}.pth"))

@@ -55,7 +55,7 @@ def main(argv=None):
     ap.add_argument("--model", default="unet")
     ap.add_argument("--backend", default="auto", choices=["auto", "hip", "torch"])
     ap.add_argument("--dtype", default=None, choices=["bf16", "fp32"],
-                    help="compute dtype (default bf16 on a GPU, fp32 on CPU; fp32 selects the torch backend)")
+                    help="compute dtype (default bf16 on a GPU, fp32 on CPU; on a GPU fp32 runs the fp32 HIP engine)")
     ap.add_argument("--seed", "-s", type=int, default=42)
     a = ap.parse_args(argv)
     H, W = (a.img_size[0], a.img_size[-1])

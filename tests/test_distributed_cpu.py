@@ -247,3 +247,65 @@ def test_pipeline_wire_roundtrip(layout):
     assert flat.dim() == 1 and flat.is_contiguous()
     flat.copy_(wire)
     assert torch.equal(r, t) and r.is_contiguous(memory_format=layout)
+
+
+def _ddp_train_worker(rank, world, port, out, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    try:
+        from distributedpytorch_amd.config import parse_args
+        from distributedpytorch_amd.trainer import train
+        args = ["--synthetic", "--synthetic-len", str(8 * world), "-v", "25", "--img-size", "32", "--model",
+                "unet-tiny", "--backend", "torch", "--dtype", "fp32", "-b", "2", "--log-every", "1", "--lr", "1e-3",
+                "-t", "DDP", "-e", "2", "--bucket-mb", "0.004", "--out-dir", out]
+        r = train(parse_args(args))
+        st = r["strategy"]
+        flat = st.space.data.detach().clone()
+        allp = [torch.zeros_like(flat) for _ in range(world)]
+        dist.all_gather(allp, flat)
+        log = torch.tensor([b for b, _, _ in st.reducer.last_launch_log], dtype=torch.int64)
+        logs = [torch.zeros_like(log) for _ in range(world)]
+        dist.all_gather(logs, log)
+        in_bwd = sum(1 for _, _, fin in st.reducer.last_launch_log if not fin)
+        lr = torch.tensor([st.optimizer.param_groups[0]["lr"]])
+        lrs = [torch.zeros_like(lr) for _ in range(world)]
+        dist.all_gather(lrs, lr)
+        q.put((rank, r["step"], all(torch.equal(allp[0], p) for p in allp), [l.tolist() for l in logs],
+               len(st.reducer.buckets), in_bwd, [float(v) for v in lrs], None))
+    except Exception as e:   # surface the failure instead of a queue timeout
+        import traceback
+        q.put((rank, -1, False, None, 0, 0, None, repr(e) + traceback.format_exc()[-1500:]))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def test_ddp_trainer_eight_ranks(tmp_path):
+    """The whole DDP training loop (train.py -t DDP) at world 8 on gloo: replicas bit-identical after two
+    epochs; every rank launched the same bucket sequence 0..n-1, all but the last during the backward;
+    the plateau scheduler's LR identical on all ranks (A5); rank 0 alone wrote checkpoints/DDP.pth with
+    the reference ``module.`` keys and the loss pickles."""
+    world = 8
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ddp_train_worker, args=(r, world, port, str(tmp_path), q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=400) for _ in procs], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+    errs = [(r[0], r[-1]) for r in res if r[-1] is not None]
+    assert not errs, errs
+    nb = res[0][4]
+    assert nb > 3
+    for rank, steps, same, logs, _, in_bwd, lrs, _ in res:
+        assert steps > 0 and same, f"rank {rank}: replicas diverged"
+        assert all(l == list(range(nb)) for l in logs), f"bucket order differs across ranks: {logs}"
+        assert in_bwd >= nb - 1
+        assert len(set(lrs)) == 1, lrs
+    sd = torch.load(tmp_path / "checkpoints" / "DDP.pth", map_location="cpu", weights_only=True)
+    assert sd and all(k.startswith("module.") for k in sd)
+    assert set(k[len("module."):] for k in sd) == set(build_model("unet-tiny").state_dict())
+    assert (tmp_path / "loss" / "DDP" / "train_loss.pkl").exists() and (tmp_path / "loss" / "DDP" / "val_loss.pkl").exists()

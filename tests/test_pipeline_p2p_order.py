@@ -44,8 +44,8 @@ def _worker(rank, world, port, microbatches, q, kind="balanced"):
         ref.load_state_dict(model.state_dict())
         from distributedpytorch_amd.parallel.placement import v_partition
         pl = v_partition(model.cfg, world, 32, 32) if kind == "v" else None
-        pipe = GPipeDist(model, microbatches, backend="torch", dtype="fp32", img_hw=(32, 32), mode="balanced",
-                         placement=pl)
+        pipe = GPipeDist(model, microbatches, backend="torch", dtype="fp32", img_hw=(32, 32),
+                         mode="reference" if kind == "reference" else "balanced", placement=pl)
         g = torch.Generator().manual_seed(5)
         x = torch.rand(4, 3, 32, 32, generator=g)
         t = (torch.rand(4, 1, 32, 32, generator=g) > 0.5).float()
@@ -119,3 +119,17 @@ def test_sender_groups_cover_every_edge():
                     assert pl.owner[c] in members[j]
                 for _, p in ins[j]:       # backward gradient j -> p rides channel j
                     assert pl.owner[p] in members[j]
+
+
+def test_skips_sent_as_their_encoder_level_finishes():
+    """Reference cut (encoder+mid | decoder+head): stage 0 posts each skip the moment its encoder level
+    finishes and the bottleneck last -- five sends per microbatch, skips in level order -- and the
+    decoder stage's single grouped receive per microbatch still matches them (loss and gradients equal
+    the single-process step)."""
+    res = _run(2, microbatches=2, kind="reference")
+    (r0, log0, *_), (r1, log1, _, _, loss, lref, bad, is_head) = res
+    assert isinstance(log0, list) and isinstance(log1, list), (log0, log1)
+    fwd_sends = [e for e in log0 if e[1] == "send"]
+    assert len(fwd_sends) == 2 * 5
+    assert sum(1 for e in log1 if e[1] == "recv" and e[0] == 0) == 2 * 5    # one batch of 5 per microbatch
+    assert is_head and abs(loss - lref) < 1e-5 and not bad
