@@ -47,6 +47,7 @@ struct F32WgradArgs {
   long pix_per_split;   // pixels per split (multiple of 32; halo form: of 64, in stage order)
   int splits;
   int halo;             // 1: the 3x3 / s1 / p1 form with the B halo staged per 2 x 32-pixel stage
+  int big;              // 1: allow the 256 x 256 tile (M % 256 == 0, >= 256 columns)
 };
 
 namespace {
@@ -235,20 +236,23 @@ __global__ __launch_bounds__(256) void igemm_f32_kernel(F32ConvArgs a) {
 }
 
 // Weight gradient: dW[m][col] = sum_p A[p][m] B'[p][col], col = tap * Nc + n, B'[p][col] = B at pixel p's tap
-// position.  BM (A channels) x 128 (columns) per block, 4 waves (2 x 2 of 64 x 64 for BM = 128, else 1 x 4),
+// position.  BM (A channels) x BN (columns) per block, 2 BN threads: BN = 128 -> 4 waves (2 x 2 of 64 x 64
+// for BM = 128, else 1 x 4); BN = 256 -> 8 waves (2 x 4; 128 x 64 each for BM = 256: the deep layers, half
+// the staged operand bytes per FLOP of the 128 x 128 tile, one block of 128 KB LDS per CU).
 // K = 32 pixels per stage.  LDS holds both operands K-contiguous ([channel / column][32 px], 128-B rows,
 // fswzk<8> swizzle), as the conv kernel does, so an MFMA operand is one ds_read_b128 per 4 MFMAs (K in
 // the permuted 4q + e order, the same for both operands).  The loader transposes in registers: a thread
 // loads a 4-pixel x 4-channel micro-block (4 float4, channel-contiguous in NHWC) and writes it as 4
 // float4 rows of 4 pixels.  Next stage's loads in registers during the current one; one barrier per
 // stage.  The bias gradient sum_p A[p][m] rides along in the blocks of column tile 0.
-template <int BM>
-__global__ __launch_bounds__(256) void wgrad_f32_kernel(F32WgradArgs a) {
-  constexpr int BN = 128, BK = 32, RB = BK * 4;                 // LDS row bytes (8 chunks of 4 px)
-  constexpr int NWM = BM == 128 ? 2 : 1, NWN = 4 / NWM, WM = BM / NWM, WN = BN / NWN, TM = WM / 16, TN = WN / 16;
+template <int BM, int BN>
+__global__ __launch_bounds__(2 * BN) void wgrad_f32_kernel(F32WgradArgs a) {
+  constexpr int BK = 32, RB = BK * 4;                           // LDS row bytes (8 chunks of 4 px)
+  constexpr int NT = 2 * BN, NW = NT / 64;                      // one B micro-block per thread per stage
+  constexpr int NWM = BM >= 128 ? 2 : 1, NWN = NW / NWM, WM = BM / NWM, WN = BN / NWN, TM = WM / 16, TN = WN / 16;
   constexpr int QA = BM / 4, UA = QA * (BK / 4);                // A micro-blocks (4 ch x 4 px) per stage
-  constexpr int QB = BN / 4;                                    // B: 32 x 8 = 256 micro-blocks, one per thread
-  static_assert(TM >= 1 && TN >= 1 && UA <= 256 && QB * (BK / 4) == 256, "tile");
+  constexpr int QB = BN / 4;                                    // B: BN/4 x 8 micro-blocks
+  static_assert(TM >= 1 && TN >= 1 && UA <= NT && QB * (BK / 4) == NT, "tile");
   __shared__ __attribute__((aligned(16))) char lds[2][(BM + BN) * RB];
 
   const int T = a.KH * a.KW, Ncols = T * a.Nc;
@@ -751,7 +755,11 @@ DPA_API int dpa_igemm_f32(const F32ConvArgs* args, hipStream_t st) {
 
 // Eligible: M % 32 == 0, Nc % 4 == 0, lda / ldb % 4 == 0, pix_per_split % 32 == 0, splits covering all
 // pixels.  BM = 128 / 64 / 32 A channels per tile (the largest dividing M).
-static int wgrad_f32_bm(int M) { return M % 128 == 0 ? 128 : M % 64 == 0 ? 64 : 32; }   // ops/fp32.py mirrors it
+// block tile rows (A channels); 256 -> the 256 x 256 8-wave tile (deep layers, opt-in by the host's `big`)
+static int wgrad_f32_bm(int M, int Ncols, int big) {   // ops/fp32.py wgrad_f32_tile mirrors it
+  if (big && M == 256 && Ncols >= 9 * 256) return 256;
+  return M % 128 == 0 ? 128 : M % 64 == 0 ? 64 : 32;
+}
 
 DPA_API int dpa_wgrad_f32(const F32WgradArgs* args, hipStream_t st) {
   const F32WgradArgs& a = *args;
@@ -769,12 +777,13 @@ DPA_API int dpa_wgrad_f32(const F32WgradArgs* args, hipStream_t st) {
     else hipLaunchKernelGGL(wgrad3_f32_kernel<64>, grid, dim3(256), 0, st, a);
     return (int)hipGetLastError();
   }
-  const int T = a.KH * a.KW, bm = wgrad_f32_bm(a.M);
-  const long tiles = (long)(a.M / bm) * ((T * a.Nc + 127) / 128);
+  const int T = a.KH * a.KW, bm = wgrad_f32_bm(a.M, T * a.Nc, a.big), bn = bm == 256 ? 256 : 128;
+  const long tiles = (long)(a.M / bm) * ((T * a.Nc + bn - 1) / bn);
   const dim3 grid((unsigned)(tiles * a.splits));
-  if (bm == 128) hipLaunchKernelGGL(wgrad_f32_kernel<128>, grid, dim3(256), 0, st, a);
-  else if (bm == 64) hipLaunchKernelGGL(wgrad_f32_kernel<64>, grid, dim3(256), 0, st, a);
-  else hipLaunchKernelGGL(wgrad_f32_kernel<32>, grid, dim3(256), 0, st, a);
+  if (bm == 256) hipLaunchKernelGGL((wgrad_f32_kernel<256, 256>), grid, dim3(512), 0, st, a);
+  else if (bm == 128) hipLaunchKernelGGL((wgrad_f32_kernel<128, 128>), grid, dim3(256), 0, st, a);
+  else if (bm == 64) hipLaunchKernelGGL((wgrad_f32_kernel<64, 128>), grid, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((wgrad_f32_kernel<32, 128>), grid, dim3(256), 0, st, a);
   return (int)hipGetLastError();
 }
 

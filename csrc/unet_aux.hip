@@ -10,6 +10,8 @@
 #include "common.h"
 #include "conv_args.h"
 
+#include <type_traits>
+
 // ------------------------------------------------------------------------------ input conversion
 __global__ __launch_bounds__(256) void nchw3_to_nhwc8_kernel(const float* __restrict__ x, bf16_t* __restrict__ y, int B,
                                                              int C, int HW) {
@@ -220,8 +222,8 @@ struct PackDesc {
   long long dst;   // element offset in the packed bf16 buffer
   int mode, Cout, Cin, Cs, Ngemm, Kpad;
 };
-__global__ __launch_bounds__(256) void pack_kernel(bf16_t* __restrict__ packed,
-                                                   const PackDesc* __restrict__ descs) {
+template <typename OutT>
+__global__ __launch_bounds__(256) void pack_kernel(OutT* __restrict__ packed, const PackDesc* __restrict__ descs) {
   const PackDesc d = descs[blockIdx.y];
   const long tot = (long)d.Ngemm * d.Kpad;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < tot; i += (long)gridDim.x * blockDim.x) {
@@ -233,7 +235,7 @@ __global__ __launch_bounds__(256) void pack_kernel(bf16_t* __restrict__ packed,
       if (tap < 9 && ci < d.Cin) v = W[((long)n * d.Cin + ci) * 9 + tap];
     } else if (d.mode == 1) {
       const int tap = k / d.Cout, co = k - tap * d.Cout;
-      if (tap < 9) v = W[((long)co * d.Cin + n) * 9 + (8 - tap)];
+      if (tap < 9 && n < d.Cin) v = W[((long)co * d.Cin + n) * 9 + (8 - tap)];
     } else if (d.mode == 2) {
       const int ij = n / d.Cout, co = n - ij * d.Cout;
       if (k < d.Cin) v = W[((long)k * d.Cout + co) * 4 + ij];
@@ -245,7 +247,8 @@ __global__ __launch_bounds__(256) void pack_kernel(bf16_t* __restrict__ packed,
     } else {
       if (k < d.Cout) v = W[(long)k * d.Cin + n];
     }
-    packed[d.dst + i] = f2bf(v);
+    if constexpr (std::is_same<OutT, float>::value) packed[d.dst + i] = v;
+    else packed[d.dst + i] = f2bf(v);
   }
 }
 DPA_API int dpa_pack_weights(const float* flat, bf16_t* packed, const void* descs, int ndesc, long long max_elems,
@@ -253,7 +256,15 @@ DPA_API int dpa_pack_weights(const float* flat, bf16_t* packed, const void* desc
   if (ndesc <= 0) return 0;
   dim3 grid(dpa_grid(max_elems, 256, 1024), ndesc);
   (void)flat;
-  hipLaunchKernelGGL(pack_kernel, grid, dim3(256), 0, st, packed, reinterpret_cast<const PackDesc*>(descs));
+  hipLaunchKernelGGL(pack_kernel<bf16_t>, grid, dim3(256), 0, st, packed, reinterpret_cast<const PackDesc*>(descs));
+  return (int)hipGetLastError();
+}
+// the fp32 engine's packed weights (models/hip_unet_f32.py): the same layouts, fp32 values; mode 1 rows
+// n >= Cin (GEMM-N padded to a multiple of 32) are zero
+DPA_API int dpa_pack_weights_f32(float* packed, const void* descs, int ndesc, long long max_elems, hipStream_t st) {
+  if (ndesc <= 0) return 0;
+  dim3 grid(dpa_grid(max_elems, 256, 1024), ndesc);
+  hipLaunchKernelGGL(pack_kernel<float>, grid, dim3(256), 0, st, packed, reinterpret_cast<const PackDesc*>(descs));
   return (int)hipGetLastError();
 }
 

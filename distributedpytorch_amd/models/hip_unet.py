@@ -196,9 +196,10 @@ class HipBlocks:
                 d.off_f = add(2, d.mod.weight, d.Cout, d.Cin, d.Cin, 4 * d.Cout, d.Kf)
                 d.off_d = add(3, d.mod.weight, d.Cout, d.Cin, d.Cout, d.Cin, d.Kd)
         self.packed = torch.zeros(max(off, 64), dtype=torch.bfloat16, device=self.device)
-        raw = (K.PackDesc * len(descs))(*descs)
-        host = torch.frombuffer(bytearray(bytes(raw)), dtype=torch.uint8)
-        self.descs_dev = host.to(self.device)
+        raw = bytes((K.PackDesc * len(descs))(*descs))
+        # (a pipeline stage may own no conv at all, e.g. only the head: an empty table, no pack launch)
+        self.descs_dev = (torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(self.device) if raw
+                          else torch.zeros(0, dtype=torch.uint8, device=self.device))
         self.ndesc = len(descs)
         self.max_elems = max_elems
         self.spaces = list(spaces.values())

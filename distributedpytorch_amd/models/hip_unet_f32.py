@@ -11,9 +11,11 @@ and weight in fp32 and runs every conv-shaped product on fp32 MFMA (v_mfma_f32_1
 * 2x2 max-pool with window codes and its backward, the segmentation head (1x1 conv + sigmoid +
   BCE / Dice partial sums, ``utils/utils.py:9-25``) and its backward, the NCHW -> NHWC input pass.
 
-Granularity is one autograd Function per op, except a DoubleConv's two convs (one Function: the inner
-ReLU backward is the mask epilogue of the second conv's dgrad); the bf16 engine's other cross-op fusions
-are not replicated (fp32 is the parity / precision path, bf16 the fast one).  Activations are NHWC
+Granularity is one autograd Function per block (a DoubleConv's two convs are one Function: the inner ReLU
+backward is the mask epilogue of the second conv's dgrad).  As in the bf16 engine, parameters are not
+autograd inputs: every layer's GEMM weight layouts are packed by one batched kernel per parameter update
+(``ensure_packed``), and the weight / bias gradients are reduced straight into the flat fp32 gradient
+buffer, each block announcing its finished parameters (``ready``: DDP buckets overlap the backward).  Activations are NHWC
 tensors handed between blocks as logical-NCHW channels_last views, as in the bf16 engine.  Supported:
 the reference UNet family without BatchNorm and with transposed-conv up-sampling, channel widths
 divisible by 32 (other configurations take the stock torch path, ``compute.resolve_backend``).
@@ -53,38 +55,58 @@ def _dense(t: torch.Tensor) -> torch.Tensor:
     return t if t.is_contiguous() else t.contiguous()
 
 
-def _conv_fwd(x, weight, bias, cs: int):
-    """relu(conv3x3(x) + b), NHWC fp32; ``cs`` = channels of x the kernel reads (>= Cin, zero weights for
-    the padding channels of the network input)."""
+def _grad(p: torch.nn.Parameter) -> torch.Tensor:
+    """The parameter's gradient view in the flat fp32 buffer (optim.FlatParameterSpace): the engine's
+    weight-gradient reductions accumulate straight into it (no zero-filled temporaries, no autograd add)."""
+    if p.grad is None:
+        p.grad = torch.zeros_like(p)
+    g = p.grad
+    assert g.dtype == torch.float32 and g.is_contiguous()
+    return g
+
+
+class _L:
+    """Packing bookkeeping of one conv3x3 / transposed-conv layer: offsets of its forward and dgrad GEMM
+    weights in the engine's packed fp32 buffer."""
+
+    def __init__(self, mod, kind: str, cs: int = 0):
+        self.mod, self.kind = mod, kind
+        if kind == "conv":
+            self.Cout, self.Cin = mod.out_channels, mod.in_channels
+            self.Cs = cs or self.Cin
+            self.Kf = F32.round_up(9 * self.Cs, 16)
+            self.Nd = F32.round_up(self.Cin, 32)          # dgrad GEMM-N (zero rows for padding channels)
+            self.Kd = F32.round_up(9 * self.Cout, 16)
+        else:                                             # ConvTranspose2d(k2, s2): weight [Cin, Cout, 2, 2]
+            self.Cin, self.Cout = mod.in_channels, mod.out_channels
+            self.Cs = self.Cin
+            self.Kf, self.Nd, self.Kd = self.Cin, self.Cin, 4 * self.Cout
+        self.off_f = self.off_d = -1
+
+
+def _conv_fwd(B, c: _L, x):
+    """relu(conv3x3(x) + b), NHWC fp32; x has ``c.Cs`` channels (>= Cin: zero weights for the padding
+    channels of the network input)."""
     N, H, W = x.shape[:3]
-    co = weight.shape[0]
-    wp, kpad = F32.pack_conv_fwd(weight, cs)
-    y = torch.empty(N, H, W, co, dtype=torch.float32, device=x.device)
-    F32.igemm(x, wp, y, Ngemm=co, Kpad=kpad, KH=3, KW=3, stride=1, pad=1, Cs=cs, out_grid=(N, H, W),
-              bias=bias.detach(), relu=True)
+    y = torch.empty(N, H, W, c.Cout, dtype=torch.float32, device=x.device)
+    F32.igemm(x, B.wf(c), y, Ngemm=c.Cout, Kpad=c.Kf, KH=3, KW=3, stride=1, pad=1, Cs=c.Cs, out_grid=(N, H, W),
+              bias=c.mod.bias.detach(), relu=True)
     return y
 
 
-def _conv_dgrad(ge, weight, cs: int, mask=None):
+def _conv_dgrad(B, c: _L, ge, mask=None):
     """dL/dx of a conv3x3 from the pre-activation gradient ``ge``; ``mask`` = the input's own ReLU output
     (its backward applied in the epilogue)."""
-    co, ci = weight.shape[:2]
     N, H, W = ge.shape[:3]
-    wd, kd = F32.pack_conv_dgrad(weight)
-    ng = F32.round_up(cs, 32)          # GEMM-N multiple of 32: zero rows for the padding channels
-    if ng != ci:
-        wd = torch.cat([wd, wd.new_zeros(ng - ci, kd)]).contiguous()
-    gx = torch.empty(N, H, W, ng, dtype=torch.float32, device=ge.device)
-    F32.igemm(ge, wd, gx, Ngemm=ng, Kpad=kd, KH=3, KW=3, stride=1, pad=1, Cs=co, out_grid=(N, H, W), mask=mask)
-    return gx[..., :cs] if ng != cs else gx
+    gx = torch.empty(N, H, W, c.Nd, dtype=torch.float32, device=ge.device)
+    F32.igemm(ge, B.wd(c), gx, Ngemm=c.Nd, Kpad=c.Kd, KH=3, KW=3, stride=1, pad=1, Cs=c.Cout, out_grid=(N, H, W),
+              mask=mask)
+    return gx[..., :c.Cs] if c.Nd != c.Cs else gx
 
 
-def _conv_wgrad(ge, x, weight, cs: int):
-    co, ci = weight.shape[:2]
-    gw = torch.zeros(co, cs, 3, 3, dtype=torch.float32, device=x.device)
-    gb = torch.zeros(co, dtype=torch.float32, device=x.device)
-    F32.wgrad(ge, x, gw, gb, KH=3, KW=3, s=1, pad=1)
-    return (gw if cs == ci else gw[:, :ci].contiguous()), gb
+def _conv_wgrad(B, c: _L, ge, x):
+    gw, gb = _grad(c.mod.weight), _grad(c.mod.bias)
+    B.side_launch(lambda: F32.wgrad(ge, x, gw, gb, KH=3, KW=3, s=1, pad=1, nreal=c.Cin), ge, x)
 
 
 class _ConvReLU(torch.autograd.Function):
@@ -92,19 +114,22 @@ class _ConvReLU(torch.autograd.Function):
     boundary)."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, cs: int):
-        y = _conv_fwd(x, weight, bias, cs)
-        ctx.cs = cs
-        ctx.save_for_backward(x, weight, y)
+    def forward(ctx, anchor, x, B, c):
+        y = _conv_fwd(B, c, x)
+        ctx.B, ctx.c = B, c
+        ctx.save_for_backward(x, y)
         return y
 
     @staticmethod
     def backward(ctx, gy):
-        x, weight, y = ctx.saved_tensors
+        x, y = ctx.saved_tensors
+        B, c = ctx.B, ctx.c
         ge = F32.relu_bwd(_dense(gy), y)
-        gx = _conv_dgrad(ge, weight, ctx.cs) if ctx.needs_input_grad[0] else None
-        gw, gb = _conv_wgrad(ge, x, weight, ctx.cs)
-        return gx, gw, gb, None
+        _conv_wgrad(B, c, ge, x)
+        gx = _conv_dgrad(B, c, ge) if ctx.needs_input_grad[1] else None
+        B.join()
+        B.ready([c.mod])
+        return None, gx, None, None
 
 
 class _DoubleConvReLU(torch.autograd.Function):
@@ -113,22 +138,25 @@ class _DoubleConvReLU(torch.autograd.Function):
     written once, already masked."""
 
     @staticmethod
-    def forward(ctx, x, w1, b1, w2, b2, cs: int):
-        a = _conv_fwd(x, w1, b1, cs)
-        y = _conv_fwd(a, w2, b2, a.shape[3])
-        ctx.cs = cs
-        ctx.save_for_backward(x, w1, a, w2, y)
+    def forward(ctx, anchor, x, B, c1, c2):
+        a = _conv_fwd(B, c1, x)
+        y = _conv_fwd(B, c2, a)
+        ctx.B, ctx.c = B, (c1, c2)
+        ctx.save_for_backward(x, a, y)
         return y
 
     @staticmethod
     def backward(ctx, gy):
-        x, w1, a, w2, y = ctx.saved_tensors
+        x, a, y = ctx.saved_tensors
+        B, (c1, c2) = ctx.B, ctx.c
         ge2 = F32.relu_bwd(_dense(gy), y)
-        ge1 = _conv_dgrad(ge2, w2, a.shape[3], mask=a)
-        gw2, gb2 = _conv_wgrad(ge2, a, w2, a.shape[3])
-        gx = _conv_dgrad(ge1, w1, ctx.cs) if ctx.needs_input_grad[0] else None
-        gw1, gb1 = _conv_wgrad(ge1, x, w1, ctx.cs)
-        return gx, gw1, gb1, gw2, gb2, None
+        _conv_wgrad(B, c2, ge2, a)                 # side stream: overlaps the dgrad chain
+        ge1 = _conv_dgrad(B, c2, ge2, mask=a)
+        _conv_wgrad(B, c1, ge1, x)
+        gx = _conv_dgrad(B, c1, ge1) if ctx.needs_input_grad[1] else None
+        B.join()
+        B.ready([c2.mod, c1.mod])
+        return None, gx, None, None, None
 
 
 class _EncBlock(torch.autograd.Function):
@@ -137,56 +165,65 @@ class _EncBlock(torch.autograd.Function):
     pre-activation gradient in one pass (F32.enc_out_bwd); the inner ReLU as in :class:`_DoubleConvReLU`."""
 
     @staticmethod
-    def forward(ctx, x, w1, b1, w2, b2, cs: int):
-        a = _conv_fwd(x, w1, b1, cs)
-        y = _conv_fwd(a, w2, b2, a.shape[3])
+    def forward(ctx, anchor, x, B, c1, c2):
+        a = _conv_fwd(B, c1, x)
+        y = _conv_fwd(B, c2, a)
         pooled, code = F32.maxpool2(y)
-        ctx.cs = cs
-        ctx.save_for_backward(x, w1, a, w2, y, code)
+        ctx.B, ctx.c = B, (c1, c2)
+        ctx.save_for_backward(x, a, y, code)
         return y, pooled
 
     @staticmethod
     def backward(ctx, gs, gp):
-        x, w1, a, w2, y, code = ctx.saved_tensors
+        x, a, y, code = ctx.saved_tensors
+        B, (c1, c2) = ctx.B, ctx.c
         if gs is not None and not F32.nhwc_ok(gs):
             gs = gs.contiguous()
         ge2 = F32.enc_out_bwd(gs, None if gp is None else _dense(gp), code, y)
-        ge1 = _conv_dgrad(ge2, w2, a.shape[3], mask=a)
-        gw2, gb2 = _conv_wgrad(ge2, a, w2, a.shape[3])
-        gx = _conv_dgrad(ge1, w1, ctx.cs) if ctx.needs_input_grad[0] else None
-        gw1, gb1 = _conv_wgrad(ge1, x, w1, ctx.cs)
-        return gx, gw1, gb1, gw2, gb2, None
+        _conv_wgrad(B, c2, ge2, a)
+        ge1 = _conv_dgrad(B, c2, ge2, mask=a)
+        _conv_wgrad(B, c1, ge1, x)
+        gx = _conv_dgrad(B, c1, ge1) if ctx.needs_input_grad[1] else None
+        B.join()
+        B.ready([c2.mod, c1.mod])
+        return None, gx, None, None, None
+
+
+def _deconv_bwd(B, d: _L, x, gy, need_dx: bool):
+    N, h, w, ci = x.shape
+    gw, gb = _grad(d.mod.weight), _grad(d.mod.bias)
+
+    def wgrad():
+        F32.wgrad(x, gy, gw, None, KH=2, KW=2, s=2, pad=0)
+        F32.channel_sum(gy, gb)
+
+    B.side_launch(wgrad, x, gy)
+    gx = None
+    if need_dx:
+        gx = torch.empty(N, h, w, ci, dtype=torch.float32, device=x.device)
+        F32.igemm(gy, B.wd(d), gx, Ngemm=ci, Kpad=d.Kd, KH=2, KW=2, stride=2, pad=0, Cs=d.Cout, out_grid=(N, h, w))
+    B.join()
+    B.ready([d.mod])
+    return gx
 
 
 class _Deconv(torch.autograd.Function):
     """y = ConvTranspose2d(k2, s2)(x) + b, NHWC fp32 (reference model/unet_parts.py:51-54)."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias):
+    def forward(ctx, anchor, x, B, d):
         N, h, w, ci = x.shape
-        co = weight.shape[1]
-        y = torch.empty(N, 2 * h, 2 * w, co, dtype=torch.float32, device=x.device)
-        F32.igemm(x, F32.pack_deconv_fwd(weight), y, Ngemm=4 * co, Kpad=ci, KH=1, KW=1, stride=1, pad=0, Cs=ci,
-                  out_grid=(N, h, w), bias=bias.detach(), mode=1, Cout=co)
-        ctx.save_for_backward(x, weight)
+        y = torch.empty(N, 2 * h, 2 * w, d.Cout, dtype=torch.float32, device=x.device)
+        F32.igemm(x, B.wf(d), y, Ngemm=4 * d.Cout, Kpad=d.Kf, KH=1, KW=1, stride=1, pad=0, Cs=ci,
+                  out_grid=(N, h, w), bias=d.mod.bias.detach(), mode=1, Cout=d.Cout)
+        ctx.B, ctx.d = B, d
+        ctx.save_for_backward(x)
         return y
 
     @staticmethod
     def backward(ctx, gy):
-        x, weight = ctx.saved_tensors
-        N, h, w, ci = x.shape
-        co = weight.shape[1]
-        gy = _dense(gy)
-        gx = None
-        if ctx.needs_input_grad[0]:
-            gx = torch.empty(N, h, w, ci, dtype=torch.float32, device=x.device)
-            F32.igemm(gy, F32.pack_deconv_dgrad(weight), gx, Ngemm=ci, Kpad=4 * co, KH=2, KW=2, stride=2, pad=0, Cs=co,
-                      out_grid=(N, h, w))
-        gw = torch.zeros(ci, co, 2, 2, dtype=torch.float32, device=x.device)
-        F32.wgrad(x, gy, gw, None, KH=2, KW=2, s=2, pad=0)
-        gb = torch.zeros(co, dtype=torch.float32, device=x.device)
-        F32.channel_sum(gy, gb)
-        return gx, gw, gb
+        (x,) = ctx.saved_tensors
+        return None, _deconv_bwd(ctx.B, ctx.d, x, _dense(gy), ctx.needs_input_grad[1]), None, None
 
 
 class _UpCat(torch.autograd.Function):
@@ -195,35 +232,26 @@ class _UpCat(torch.autograd.Function):
     channel half; the backward reads both gradient halves in place (no split copies)."""
 
     @staticmethod
-    def forward(ctx, x, skip, weight, bias):
+    def forward(ctx, anchor, x, skip, B, d):
         N, h, w, ci = x.shape
-        co, C = weight.shape[1], skip.shape[3]
-        buf = torch.empty(N, 2 * h, 2 * w, C + co, dtype=torch.float32, device=x.device)
+        C = skip.shape[3]
+        buf = torch.empty(N, 2 * h, 2 * w, C + d.Cout, dtype=torch.float32, device=x.device)
         buf[..., :C].copy_(skip)
-        F32.igemm(x, F32.pack_deconv_fwd(weight), buf[..., C:], Ngemm=4 * co, Kpad=ci, KH=1, KW=1, stride=1, pad=0,
-                  Cs=ci, out_grid=(N, h, w), bias=bias.detach(), mode=1, Cout=co)
-        ctx.C = C
-        ctx.save_for_backward(x, weight)
+        F32.igemm(x, B.wf(d), buf[..., C:], Ngemm=4 * d.Cout, Kpad=d.Kf, KH=1, KW=1, stride=1, pad=0,
+                  Cs=ci, out_grid=(N, h, w), bias=d.mod.bias.detach(), mode=1, Cout=d.Cout)
+        ctx.C, ctx.B, ctx.d = C, B, d
+        ctx.save_for_backward(x)
         return buf
 
     @staticmethod
     def backward(ctx, gbuf):
-        x, weight = ctx.saved_tensors
-        N, h, w, ci = x.shape
-        co, C = weight.shape[1], ctx.C
+        (x,) = ctx.saved_tensors
+        C = ctx.C
         if not F32.nhwc_ok(gbuf):
             gbuf = gbuf.contiguous()
         gs, gy = gbuf[..., :C], gbuf[..., C:]
-        gx = None
-        if ctx.needs_input_grad[0]:
-            gx = torch.empty(N, h, w, ci, dtype=torch.float32, device=x.device)
-            F32.igemm(gy, F32.pack_deconv_dgrad(weight), gx, Ngemm=ci, Kpad=4 * co, KH=2, KW=2, stride=2, pad=0, Cs=co,
-                      out_grid=(N, h, w))
-        gw = torch.zeros(ci, co, 2, 2, dtype=torch.float32, device=x.device)
-        F32.wgrad(x, gy, gw, None, KH=2, KW=2, s=2, pad=0)
-        gb = torch.zeros(co, dtype=torch.float32, device=x.device)
-        F32.channel_sum(gy, gb)
-        return gx, gs, gw, gb
+        gx = _deconv_bwd(ctx.B, ctx.d, x, gy, ctx.needs_input_grad[1])
+        return None, gx, gs, None, None
 
 
 class _MaxPool(torch.autograd.Function):
@@ -244,30 +272,144 @@ class _HeadLoss(torch.autograd.Function):
     """Partial sums S[4] of the reference loss from the last decoder output (1x1 conv + sigmoid)."""
 
     @staticmethod
-    def forward(ctx, y, weight, bias, t):
-        S, _ = F32.head_fwd(y, weight, bias, t)
-        ctx.save_for_backward(y, weight, bias, t)
+    def forward(ctx, anchor, y, B, t):
+        seg = B.model.segmap
+        S, _ = F32.head_fwd(y, seg.weight, seg.bias, t)
+        ctx.B = B
+        ctx.save_for_backward(y, t)
         return S
 
     @staticmethod
     def backward(ctx, dS):
-        y, weight, bias, t = ctx.saved_tensors
-        gy, gw, gb = F32.head_bwd(y, weight, bias, t, dS)
-        return gy, gw.view_as(weight), gb.view_as(bias), None
+        y, t = ctx.saved_tensors
+        seg = ctx.B.model.segmap
+        gy, _, _ = F32.head_bwd(y, seg.weight, seg.bias, t, dS, _grad(seg.weight).view(-1), _grad(seg.bias))
+        ctx.B.ready([seg])
+        return None, gy, None, None
 
 
-class HipF32Blocks:
+class F32Engine:
+    """Packed fp32 GEMM weights of a set of layers plus the readiness announcements: the state the
+    block Functions use (``wf`` / ``wd`` / ``ready``).  :class:`HipF32Blocks` is the UNet's engine; the
+    tests build one over single layers."""
+
+    def __init__(self, layers, device, owned=None):
+        self.device = torch.device(device)
+        self._owned = owned
+        # parameters enter no autograd graph: the Functions take this leaf so their outputs require grad,
+        # and write the parameter gradients into the flat buffer themselves
+        self.anchor = torch.zeros(1, device=self.device, requires_grad=True)
+        self._build_packing(layers)
+        self._packed_version = None
+        # weight gradients on a second HIP stream (as in the bf16 engine): nothing in the backward reads
+        # them, so they overlap the dgrad chain; a block's end joins the streams, then announces
+        from ..ops import kernels as K
+        self.side = torch.cuda.Stream(device=self.device, priority=K.SIDE_PRIORITY) if K.SIDE_WGRAD else None
+        self._keep = []
+
+    def side_launch(self, fn, *keep):
+        """Run ``fn`` (weight-gradient launches reading ``keep``) on the side stream; the operands stay
+        referenced until :meth:`join`, so the caching allocator cannot hand their memory to the compute
+        stream while the side stream still reads it."""
+        if self.side is None:
+            fn()
+            return
+        self.side.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(self.side):
+            fn()
+        self._keep.extend(keep)
+
+    def join(self):
+        if self.side is not None and self._keep:
+            torch.cuda.current_stream(self.device).wait_stream(self.side)
+            self._keep = []
+
+    def _build_packing(self, layers):
+        """One descriptor per (layer, layout) of the layers on this device (a pipeline stage packs only its
+        own); ONE batched kernel re-packs them whenever a parameter changed (``space.version``)."""
+        from ..ops import kernels as K
+        descs, off, max_elems, spaces = [], 0, 0, {}
+
+        def add(mode, w, cout, cin, cs, ngemm, kpad):
+            nonlocal off, max_elems
+            assert w.dtype == torch.float32 and w.is_contiguous()
+            descs.append(K.PackDesc(w.data_ptr(), off, mode, cout, cin, cs, ngemm, kpad))
+            sp = getattr(w, "_dpa_space", None)
+            if sp is not None:
+                spaces[id(sp)] = sp
+            start = off
+            off = F32.round_up(off + ngemm * kpad, 64)
+            max_elems = max(max_elems, ngemm * kpad)
+            return start
+
+        for c in layers:
+            if c.mod.weight.device != self.device or (self._owned is not None and id(c.mod.weight) not in self._owned):
+                continue
+            if c.kind == "conv":
+                c.off_f = add(0, c.mod.weight, c.Cout, c.Cin, c.Cs, c.Cout, c.Kf)
+                c.off_d = add(1, c.mod.weight, c.Cout, c.Cin, c.Cout, c.Nd, c.Kd)
+            else:
+                c.off_f = add(2, c.mod.weight, c.Cout, c.Cin, c.Cin, 4 * c.Cout, c.Kf)
+                c.off_d = add(3, c.mod.weight, c.Cout, c.Cin, c.Cout, c.Cin, c.Kd)
+        self.packed = torch.zeros(max(off, 64), dtype=torch.float32, device=self.device)
+        raw = bytes((K.PackDesc * len(descs))(*descs))
+        # (a pipeline stage may own no conv at all, e.g. only the head: an empty table, no pack launch)
+        self.descs_dev = (torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(self.device) if raw
+                          else torch.zeros(0, dtype=torch.uint8, device=self.device))
+        self.ndesc, self.max_elems = len(descs), max_elems
+        self.spaces = list(spaces.values())
+
+    def ensure_packed(self):
+        """Re-pack when a parameter changed (without a flat parameter space: every call)."""
+        v = sum(s.version for s in self.spaces)
+        if self._packed_version != v or not self.spaces:
+            F32.pack_weights(self.packed, self.descs_dev, self.ndesc, self.max_elems)
+            self._packed_version = v
+
+    def wf(self, c: _L) -> torch.Tensor:
+        assert c.off_f >= 0, "layer not packed on this engine's device"
+        n = (4 * c.Cout if c.kind == "deconv" else c.Cout) * c.Kf
+        return self.packed[c.off_f:c.off_f + n]
+
+    def wd(self, c: _L) -> torch.Tensor:
+        assert c.off_d >= 0, "layer not packed on this engine's device"
+        return self.packed[c.off_d:c.off_d + c.Nd * c.Kd]
+
+    def ready(self, mods):
+        """Announce finished parameter gradients (DDP buckets start while the backward runs)."""
+        by_space = {}
+        for m in mods:
+            for p in (m.weight, m.bias):
+                sp = getattr(p, "_dpa_space", None)
+                if sp is not None:
+                    by_space.setdefault(id(sp), (sp, []))[1].append(p)
+        for sp, ps in by_space.values():
+            sp.notify_ready(ps)
+
+
+class HipF32Blocks(F32Engine):
     """Block backend (models.blocks protocol) of the fp32 engine."""
 
     name = "hip"
 
     def __init__(self, model, device=None, owned=None):
+        from ..optim import FlatParameterSpace
         self.model = model
-        self.device = torch.device(device) if device is not None else next(model.parameters()).device
-        assert self.device.type == "cuda", "HipF32Blocks needs a GPU"
+        device = torch.device(device) if device is not None else next(model.parameters()).device
+        assert device.type == "cuda", "HipF32Blocks needs a GPU"
         assert supported(model), "fp32 HIP engine: reference UNet family without BatchNorm / bilinear, widths % 32 == 0"
         self.dense_skips = set()
+        if not any(hasattr(p, "_dpa_space") for p in model.parameters()):
+            FlatParameterSpace(model, device=device)     # standalone use: flatten here
+        self.encc = [[_L(c, "conv", 4 if (l == 0 and j == 0) else 0) for j, c in enumerate(b.convs())]
+                     for l, b in enumerate(model.encoder.blocks())]
+        self.midc = [_L(c, "conv") for c in model.mid.convs()]
+        self.decc = [[_L(c, "conv") for c in b.convs()] for b in model.decoder.blocks()]
+        self.ups = [_L(m, "deconv") for m in model.decoder.ups()]
+        layers = [c for cs in self.encc for c in cs] + self.midc + [c for cs in self.decc for c in cs] + self.ups
+        super().__init__(layers, device, owned)
 
+    # ------------------------------------------------------------------ block API
     def prep(self, x):
         if x.dim() == 4 and x.shape[1] <= 4 and x.dtype == torch.float32 and x.stride(1) != 1:
             return _o(F32.input_nhwc4(x))
@@ -275,50 +417,49 @@ class HipF32Blocks:
             return x          # already converted
         return _o(F32.input_nhwc4(x.float()))
 
-    def _conv(self, conv, x, cs=None):
-        return _ConvReLU.apply(x, conv.weight, conv.bias, cs or x.shape[3])
+    def _conv(self, c, x):
+        self.ensure_packed()
+        return _ConvReLU.apply(self.anchor, x, self, c)
 
-    def _double(self, c1, c2, x, cs=None):
-        return _DoubleConvReLU.apply(x, c1.weight, c1.bias, c2.weight, c2.bias, cs or x.shape[3])
+    def _double(self, c1, c2, x):
+        self.ensure_packed()
+        return _DoubleConvReLU.apply(self.anchor, x, self, c1, c2)
 
     def enc(self, l: int, x):
-        c1, c2 = self.model.encoder.blocks()[l].convs()
-        xv = _v(x)
-        s, p = _EncBlock.apply(xv, c1.weight, c1.bias, c2.weight, c2.bias, 4 if l == 0 else xv.shape[3])
+        self.ensure_packed()
+        c1, c2 = self.encc[l]
+        s, p = _EncBlock.apply(self.anchor, _v(x), self, c1, c2)
         return _o(s), _o(p)
 
     def mid(self, x):
-        c1, c2 = self.model.mid.convs()
-        return _o(self._double(c1, c2, _v(x)))
+        return _o(self._double(*self.midc, _v(x)))
 
     def dec(self, i: int, x, skip):
         # transposed conv, reference CenterCrop of the skip (model/unet_parts.py:58-74), concat with the
         # skip first (:59), conv_block
-        c1, c2 = self.model.decoder.blocks()[i].convs()
-        return _o(self._double(c1, c2, self._up_cat(i, x, skip)))
+        return _o(self._double(*self.decc[i], self._up_cat(i, x, skip)))
 
     # halves of a block cut between its two convs (pipeline stage boundary inside a DoubleConv)
     def enc_a(self, l: int, x):
-        c1 = self.model.encoder.blocks()[l].convs()[0]
-        return _o(self._conv(c1, _v(x), 4 if l == 0 else None))
+        return _o(self._conv(self.encc[l][0], _v(x)))
 
     def enc_b(self, l: int, a):
-        c2 = self.model.encoder.blocks()[l].convs()[1]
-        s = self._conv(c2, _v(a))
+        s = self._conv(self.encc[l][1], _v(a))
         return _o(s), _o(_MaxPool.apply(s))
 
     def mid_a(self, x):
-        return _o(self._conv(self.model.mid.convs()[0], _v(x)))
+        return _o(self._conv(self.midc[0], _v(x)))
 
     def mid_b(self, a):
-        return _o(self._conv(self.model.mid.convs()[1], _v(a)))
+        return _o(self._conv(self.midc[1], _v(a)))
 
     def _up_cat(self, i: int, x, skip):
-        d = self.model.decoder.ups()[i]
+        self.ensure_packed()
+        d = self.ups[i]
         xv, sk = _v(x), _v(skip)
         if tuple(sk.shape[1:3]) == (2 * xv.shape[1], 2 * xv.shape[2]) and sk.shape[3] % 4 == 0:
-            return _UpCat.apply(xv, sk, d.weight, d.bias)
-        up = _Deconv.apply(xv, d.weight, d.bias)
+            return _UpCat.apply(self.anchor, xv, sk, self, d)
+        up = _Deconv.apply(self.anchor, xv, self, d)
         h2, w2 = up.shape[1:3]
         if tuple(sk.shape[1:3]) != (h2, w2):
             top, left = int(round((sk.shape[1] - h2) / 2.0)), int(round((sk.shape[2] - w2) / 2.0))
@@ -326,15 +467,13 @@ class HipF32Blocks:
         return torch.cat([sk, up], dim=3)
 
     def dec_a(self, i: int, x, skip):
-        c1 = self.model.decoder.blocks()[i].convs()[0]
-        return _o(self._conv(c1, self._up_cat(i, x, skip)))
+        return _o(self._conv(self.decc[i][0], self._up_cat(i, x, skip)))
 
     def dec_b(self, i: int, a):
-        return _o(self._conv(self.model.decoder.blocks()[i].convs()[1], _v(a)))
+        return _o(self._conv(self.decc[i][1], _v(a)))
 
     def head_partials(self, x, t):
-        seg = self.model.segmap
-        return _HeadLoss.apply(_dense(_v(x)), seg.weight, seg.bias, t.float().contiguous())
+        return _HeadLoss.apply(self.anchor, _dense(_v(x)), self, t.float().contiguous())
 
     @torch.no_grad()
     def head_probs(self, x):

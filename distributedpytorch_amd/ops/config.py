@@ -61,6 +61,8 @@ KNOBS = (
          "decoder conv (no concat buffer)"),
     Knob("f32_wgrad_halo", "DPA_NO_F32_WGRAD_HALO", True, "fp32 engine: 3x3 weight gradients over 32 / 64 input channels "
          "stage the input halo once per 2 x 32-pixel patch (csrc/fp32.hip wgrad3_f32_kernel)"),
+    Knob("f32_wgrad_big", "DPA_NO_F32_WGRAD_BIG", True, "fp32 engine: 256 x 256 8-wave weight-gradient tiles for the "
+         "256-output-channel layers over >= 256 inputs instead of 128 x 128"),
     # launch geometry / streams
     Knob("side_priority", "DPA_SIDE_PRIORITY", 0, "HIP priority of the weight-gradient side stream (torch convention)"),
     Knob("wgrad_stream_blocks", "DPA_WGRAD_STREAM_BLOCKS", 2048, "target workgroups of a row-streaming weight gradient"),
@@ -122,6 +124,7 @@ class KernelConfig:
     dual_input: bool = True
     bn_on_load: bool = True
     f32_wgrad_halo: bool = True
+    f32_wgrad_big: bool = True
     side_priority: int = 0
     wgrad_stream_blocks: int = 2048
     wgrad_gemm_blocks: int = 768

@@ -1,8 +1,10 @@
 """Python wrappers of the fp32 kernel family (csrc/fp32.hip): the hand-written fp32 training path.
 
 Every wrapper checks the tensor contracts (dtype, NHWC strides, 16-B alignment) before it builds an
-argument block, and launches on the current stream of the output's device.  Weight packing is done
-with a few torch ops on the (small) fp32 parameter tensors; every activation-sized pass is a HIP kernel.
+argument block, and launches on the current stream of the output's device.  Weights are packed into
+their GEMM layouts by ONE batched kernel per parameter update (:func:`pack_weights`, the bf16 engine's
+descriptor table with fp32 output); the ``pack_*`` torch forms below are the reference layouts the
+tests compare it with.  Weight / bias gradients are reduced straight into the flat fp32 gradient buffer.
 """
 from __future__ import annotations
 
@@ -25,12 +27,23 @@ class F32ConvArgs(ctypes.Structure):
 
 
 USE_WGRAD_HALO = _config.KernelConfig.from_env().f32_wgrad_halo   # 3x3 weight gradients with the input halo staged
+USE_WGRAD_BIG = _config.KernelConfig.from_env().f32_wgrad_big     # 256 x 256 8-wave weight-gradient tiles (deep layers)
+
+
+def wgrad_f32_tile(M: int, Ncols: int, big: bool):
+    """(rows, columns) of the weight-gradient block tile (csrc/fp32.hip wgrad_f32_bm).  The 256 x 256 tile
+    pays for 256 output channels over >= 256 input channels (b16, 512^2: enc3.c2 / dec0.c1 / dec0.c2
+    +5-9 %); with 512 outputs at 32^2 or 128 inputs its grid is too small (-3..-16 %,
+    profiles/f32_kbench_b16_512_r05.txt)."""
+    if big and M == 256 and Ncols >= 9 * 256:
+        return 256, 256
+    return (128 if M % 128 == 0 else 64 if M % 64 == 0 else 32), 128
 
 
 class F32WgradArgs(ctypes.Structure):
     _fields_ = [("A", c_void_p), ("B", c_void_p), ("slab", c_void_p), ("bslab", c_void_p)] + \
                [(n, c_int) for n in ("lda", "ldb", "N", "Hg", "Wg", "HB", "WB", "M", "Nc", "s", "pad", "KH", "KW")] + \
-               [("pix_per_split", ctypes.c_long), ("splits", c_int), ("halo", c_int)]
+               [("pix_per_split", ctypes.c_long), ("splits", c_int), ("halo", c_int), ("big", c_int)]
 
 
 def _st(t: torch.Tensor):
@@ -138,14 +151,24 @@ def igemm(x: torch.Tensor, wp: torch.Tensor, y: torch.Tensor, *, Ngemm: int, Kpa
     return y
 
 
+def pack_weights(packed: torch.Tensor, descs_dev: torch.Tensor, ndesc: int, max_elems: int) -> None:
+    """Every layer's GEMM weight layouts in one launch (csrc/unet_aux.hip pack_kernel<float>; descriptors
+    as ``ops.kernels.PackDesc``: mode 0 conv fwd, 1 conv dgrad, 2 / 3 transposed conv fwd / dgrad)."""
+    assert packed.dtype == torch.float32 and packed.is_contiguous()
+    _check(_lib.lib().dpa_pack_weights_f32(_p(packed), _p(descs_dev), c_int(ndesc), c_ll(max_elems), _st(packed)),
+           "pack_weights_f32")
+
+
 def wgrad(A: torch.Tensor, B: torch.Tensor, gw: torch.Tensor, gb: Optional[torch.Tensor], *, KH: int, KW: int, s: int,
-          pad: int, target_blocks: int = 1024) -> None:
+          pad: int, target_blocks: int = 1024, nreal: int = 0) -> None:
     """gw[m][n][kh][kw] += sum_p A[p][m] B[p*s + (kh, kw) - pad][n] (OIHW with O = A's channels), gb[m] +=
-    sum_p A[p][m]; A is the pixel grid.  Split over pixel ranges into fp32 slabs, summed in a fixed order."""
+    sum_p A[p][m]; A is the pixel grid.  Split over pixel ranges into fp32 slabs, summed in a fixed order.
+    ``nreal``: channels of B that gw holds (the first layer's zero padding channels are dropped)."""
     N, Hg, Wg, M, lda = nhwc(A, "wgrad_f32.A")
     NB, HB, WB, Nc, ldb = nhwc(B, "wgrad_f32.B")
-    assert NB == N and M % 32 == 0 and Nc % 4 == 0
-    assert gw.dtype == torch.float32 and gw.is_contiguous() and gw.numel() == M * Nc * KH * KW
+    nreal = nreal or Nc
+    assert NB == N and M % 32 == 0 and Nc % 4 == 0 and nreal <= Nc
+    assert gw.dtype == torch.float32 and gw.is_contiguous() and gw.numel() == M * nreal * KH * KW
     assert gb is None or (gb.dtype == torch.float32 and gb.numel() == M)
     T = KH * KW
     P = N * Hg * Wg
@@ -158,20 +181,20 @@ def wgrad(A: torch.Tensor, B: torch.Tensor, gw: torch.Tensor, gb: Optional[torch
         splits = -(-nst // sps)
         pps = 64 * sps
     else:
-        bm = 128 if M % 128 == 0 else 64 if M % 64 == 0 else 32          # csrc/fp32.hip wgrad_f32_bm
-        tiles = (M // bm) * -(-(T * Nc) // 128)
+        bm, bn = wgrad_f32_tile(M, T * Nc, USE_WGRAD_BIG)
+        tiles = (M // bm) * -(-(T * Nc) // bn)
         splits = max(1, min(-(-target_blocks // tiles), -(-P // 1024)))
         pps = round_up(-(-P // splits), 32)
         splits = -(-P // pps)
     slab = torch.empty(splits * T * M * Nc + (splits * M if gb is not None else 0), dtype=torch.float32, device=A.device)
     bslab = slab[splits * T * M * Nc:] if gb is not None else None
     a = F32WgradArgs(A.data_ptr(), B.data_ptr(), slab.data_ptr(), None if bslab is None else bslab.data_ptr(),
-                     lda, ldb, N, Hg, Wg, HB, WB, M, Nc, s, pad, KH, KW, pps, splits, halo)
+                     lda, ldb, N, Hg, Wg, HB, WB, M, Nc, s, pad, KH, KW, pps, splits, halo, int(USE_WGRAD_BIG))
     L = _lib.lib()
     st = _st(A)
     _check(L.dpa_wgrad_f32(ctypes.byref(a), st), "wgrad_f32")
-    _check(L.dpa_wgrad_reduce(_p(slab), _p(bslab), _p(gw), _p(gb), c_int(splits), c_int(T), c_int(M), c_int(Nc), c_int(Nc),
-                              c_int(0), st), "wgrad_reduce(f32)")
+    _check(L.dpa_wgrad_reduce(_p(slab), _p(bslab), _p(gw), _p(gb), c_int(splits), c_int(T), c_int(M), c_int(Nc),
+                              c_int(nreal), c_int(0), st), "wgrad_reduce(f32)")
 
 
 # ---------------------------------------------------------------------------------------- elementwise
@@ -239,8 +262,11 @@ def head_fwd(y: torch.Tensor, w: torch.Tensor, b: torch.Tensor, t: Optional[torc
     return S, probs
 
 
-def head_bwd(y: torch.Tensor, w: torch.Tensor, b: torch.Tensor, t: torch.Tensor, dS: torch.Tensor):
-    """(dL/dy of the head -- NHWC fp32, NOT ReLU-masked --, segmap weight gradient [C], bias gradient [1])."""
+def head_bwd(y: torch.Tensor, w: torch.Tensor, b: torch.Tensor, t: torch.Tensor, dS: torch.Tensor,
+             gw: Optional[torch.Tensor] = None, gb: Optional[torch.Tensor] = None):
+    """(dL/dy of the head -- NHWC fp32, NOT ReLU-masked --, segmap weight gradient [C], bias gradient [1]).
+    With ``gw`` / ``gb`` (the flat gradient buffer's views, adjacent: weight then bias) the parameter
+    gradients are reduced into them in place and returned as those views."""
     N, H, W, C, ld = nhwc(y, "head_bwd_f32.y")
     P = N * H * W
     L = _lib.lib()
@@ -251,9 +277,19 @@ def head_bwd(y: torch.Tensor, w: torch.Tensor, b: torch.Tensor, t: torch.Tensor,
     dS = dS.reshape(-1).float().contiguous()
     wv = w.detach().reshape(-1).float().contiguous()
     bv = b.detach().reshape(-1).float().contiguous()
-    _check(L.dpa_head_bwd_f32(_p(y), c_int(C), _p(wv), _p(bv), _p(tf), _p(dS), c_ll(P), _p(gy), _p(slab), _st(y)),
+    st = _st(y)
+    _check(L.dpa_head_bwd_f32(_p(y), c_int(C), _p(wv), _p(bv), _p(tf), _p(dS), c_ll(P), _p(gy), _p(slab), st),
            "head_bwd_f32")
+    if (gw is not None and gb is not None and gw.is_contiguous() and gw.numel() == C and gb.numel() == 1
+            and gb.data_ptr() == gw.data_ptr() + 4 * C):
+        _check(L.dpa_wgrad_reduce_cfg(None, _p(slab), None, _p(gw), c_int(blocks), c_int(0), c_int(C + 1), c_int(1),
+                                      c_int(1), c_int(0), c_int(0), st), "head_bwd_f32(reduce)")
+        return gy, gw, gb
     red = slab.view(blocks, C + 1).sum(0)
+    if gw is not None:
+        gw.view(-1).add_(red[:C])
+        gb.view(-1).add_(red[C:])
+        return gy, gw, gb
     return gy, red[:C], red[C:]
 
 
@@ -268,11 +304,15 @@ def input_nhwc4(x: torch.Tensor) -> torch.Tensor:
 
 
 def channel_sum(g: torch.Tensor, out: torch.Tensor) -> None:
-    """out[c] += sum over pixels of NHWC fp32 g (channel slice allowed)."""
+    """out[c] += sum over pixels of NHWC fp32 g (channel slice allowed): per-block partial sums, then the
+    fixed-order slab reduction of the weight gradients (bias rows only) straight into ``out``."""
     N, H, W, C, ld = nhwc(g, "channel_sum_f32.g")
+    assert out.dtype == torch.float32 and out.is_contiguous() and out.numel() == C
     P = N * H * W
     L = _lib.lib()
     blocks = L.dpa_head_f32_blocks(c_ll(P))
     slab = torch.empty(blocks * C, dtype=torch.float32, device=g.device)
-    _check(L.dpa_channel_sum_f32(_p(g), c_ll(P), c_int(C), c_int(ld), _p(slab), _st(g)), "channel_sum_f32")
-    out.view(-1).add_(slab.view(blocks, C).sum(0))
+    st = _st(g)
+    _check(L.dpa_channel_sum_f32(_p(g), c_ll(P), c_int(C), c_int(ld), _p(slab), st), "channel_sum_f32")
+    _check(L.dpa_wgrad_reduce_cfg(None, _p(slab), None, _p(out), c_int(blocks), c_int(0), c_int(C), c_int(1), c_int(1),
+                                  c_int(0), c_int(0), st), "channel_sum_f32(reduce)")

@@ -14,11 +14,58 @@ def _rel(a, b):
     return ((a - b).abs().max() / b.abs().max().clamp_min(1e-30)).item()
 
 
+def _conv(w, b):
+    """A Conv2d carrying the given weights (the engine reads them through its packed buffer)."""
+    m = torch.nn.Conv2d(w.shape[1], w.shape[0], 3, padding=1).cuda()
+    with torch.no_grad():
+        m.weight.copy_(w)
+        m.bias.copy_(b)
+    return m
+
+
+def _deconv(w, b):
+    m = torch.nn.ConvTranspose2d(w.shape[0], w.shape[1], 2, stride=2).cuda()
+    with torch.no_grad():
+        m.weight.copy_(w)
+        m.bias.copy_(b)
+    return m
+
+
+def _engine(*layers):
+    """fp32 engine over single layers: weights packed by the batched pack kernel, gradients reduced in place
+    into each module's .grad (the flat-buffer views in a real model)."""
+    from distributedpytorch_amd.models.hip_unet_f32 import F32Engine
+    eng = F32Engine(list(layers), "cuda:0")
+    eng.ensure_packed()
+    return eng
+
+
+def test_pack_kernel_matches_torch_layouts(hip_lib):
+    """The batched fp32 pack kernel reproduces the reference packing of every layout (conv forward with
+    padded input channels, flipped conv dgrad, transposed-conv forward and dgrad)."""
+    from distributedpytorch_amd.models.hip_unet_f32 import _L
+    from distributedpytorch_amd.ops import fp32 as F32
+    torch.manual_seed(5)
+    c0 = _conv(torch.randn(32, 3, 3, 3, device="cuda"), torch.randn(32, device="cuda"))
+    c1 = _conv(torch.randn(64, 96, 3, 3, device="cuda"), torch.randn(64, device="cuda"))
+    d = _deconv(torch.randn(128, 64, 2, 2, device="cuda"), torch.randn(64, device="cuda"))
+    L0, L1, LD = _L(c0, "conv", 4), _L(c1, "conv"), _L(d, "deconv")
+    eng = _engine(L0, L1, LD)
+    wp, kp = F32.pack_conv_fwd(c0.weight, 4)
+    assert kp == L0.Kf and torch.equal(eng.wf(L0).view(32, kp), wp)
+    wp, kp = F32.pack_conv_fwd(c1.weight, 96)
+    assert torch.equal(eng.wf(L1).view(64, kp), wp)
+    wd, kd = F32.pack_conv_dgrad(c1.weight)
+    assert kd == L1.Kd and torch.equal(eng.wd(L1).view(96, kd), wd)
+    assert torch.equal(eng.wf(LD).view(256, 128), F32.pack_deconv_fwd(d.weight))
+    assert torch.equal(eng.wd(LD).view(128, 256), F32.pack_deconv_dgrad(d.weight))
+
+
 @pytest.mark.parametrize("N,H,W,Cin,Cout,cs", [(2, 16, 24, 32, 32, 32), (1, 9, 13, 64, 96, 64), (2, 8, 8, 3, 32, 4),
                                                (2, 32, 40, 128, 128, 128), (1, 20, 18, 64, 256, 64),
                                                (3, 12, 10, 96, 64, 96)])
 def test_conv_relu_fwd_bwd(hip_lib, N, H, W, Cin, Cout, cs):
-    from distributedpytorch_amd.models.hip_unet_f32 import _ConvReLU
+    from distributedpytorch_amd.models.hip_unet_f32 import _ConvReLU, _L
     torch.manual_seed(Cin + Cout)
     xr = torch.randn(N, Cin, H, W, device="cuda")
     w = (torch.randn(Cout, Cin, 3, 3, device="cuda") / (9 * Cin) ** 0.5).requires_grad_(True)
@@ -30,9 +77,13 @@ def test_conv_relu_fwd_bwd(hip_lib, N, H, W, Cin, Cout, cs):
     xn = torch.zeros(N, H, W, cs, device="cuda")
     xn[..., :Cin] = xr.permute(0, 2, 3, 1)
     xn.requires_grad_(True)
-    y = _ConvReLU.apply(xn, w, b, cs)
+    m = _conv(w.detach(), b.detach())
+    layer = _L(m, "conv", cs)
+    eng = _engine(layer)
+    y = _ConvReLU.apply(eng.anchor, xn, eng, layer)
     assert _rel(y.permute(0, 3, 1, 2), ref) < 1e-5
-    gx, gw, gb = torch.autograd.grad(y, (xn, w, b), g.permute(0, 2, 3, 1).contiguous())
+    (gx,) = torch.autograd.grad(y, (xn,), g.permute(0, 2, 3, 1).contiguous())
+    gw, gb = m.weight.grad, m.bias.grad
     assert _rel(gw, gw_ref) < 1e-5 and _rel(gb, gb_ref) < 1e-5
     assert _rel(gx[..., :Cin].permute(0, 3, 1, 2), gx_ref) < 1e-5
 
@@ -41,7 +92,7 @@ def test_conv_relu_fwd_bwd(hip_lib, N, H, W, Cin, Cout, cs):
 def test_up_cat(hip_lib, N, h, w, Cin, Cout, C):
     """[skip ‖ ConvTranspose2d(x)] in one buffer (deconv epilogue into the upper half) vs torch, forward and
     every gradient (the two gradient halves are read in place)."""
-    from distributedpytorch_amd.models.hip_unet_f32 import _UpCat
+    from distributedpytorch_amd.models.hip_unet_f32 import _L, _UpCat
     torch.manual_seed(Cin + C)
     x = torch.randn(N, Cin, h, w, device="cuda").requires_grad_(True)
     sk = torch.randn(N, C, 2 * h, 2 * w, device="cuda").requires_grad_(True)
@@ -52,9 +103,13 @@ def test_up_cat(hip_lib, N, h, w, Cin, Cout, C):
     refs = torch.autograd.grad(ref, (x, sk, wt, b), g)
     xn = x.detach().permute(0, 2, 3, 1).contiguous().requires_grad_(True)
     skn = sk.detach().permute(0, 2, 3, 1).contiguous().requires_grad_(True)
-    y = _UpCat.apply(xn, skn, wt, b)
+    m = _deconv(wt.detach(), b.detach())
+    layer = _L(m, "deconv")
+    eng = _engine(layer)
+    y = _UpCat.apply(eng.anchor, xn, skn, eng, layer)
     assert _rel(y.permute(0, 3, 1, 2), ref) < 1e-5
-    gx, gsk, gw, gb = torch.autograd.grad(y, (xn, skn, wt, b), g.permute(0, 2, 3, 1).contiguous())
+    gx, gsk = torch.autograd.grad(y, (xn, skn), g.permute(0, 2, 3, 1).contiguous())
+    gw, gb = m.weight.grad, m.bias.grad
     assert _rel(gx.permute(0, 3, 1, 2), refs[0]) < 1e-5 and _rel(gsk.permute(0, 3, 1, 2), refs[1]) == 0.0
     assert _rel(gw, refs[2]) < 1e-5 and _rel(gb, refs[3]) < 1e-5
 
@@ -105,10 +160,34 @@ def test_wgrad_halo_form(hip_lib, N, H, W, Nc, M):
         F32.USE_WGRAD_HALO = old
 
 
+@pytest.mark.parametrize("N,H,W,Nc,M", [(2, 8, 16, 256, 256), (1, 8, 8, 512, 256), (3, 4, 4, 512, 256),
+                                        (2, 6, 10, 320, 256)])
+def test_wgrad_big_tile(hip_lib, N, H, W, Nc, M):
+    """The 256 x 256 8-wave weight-gradient tile (DPA_F32_WGRAD_BIG, deep layers) vs torch fp32, with a
+    ragged last column tile (9 Nc not a multiple of 256) and ragged pixel splits."""
+    from distributedpytorch_amd.ops import fp32 as F32
+    torch.manual_seed(Nc + M)
+    x = torch.randn(N, Nc, H, W, device="cuda")
+    g = torch.randn(N, M, H, W, device="cuda")
+    gw_ref = torch.nn.grad.conv2d_weight(x, (M, Nc, 3, 3), g, padding=1)
+    gb_ref = g.sum((0, 2, 3))
+    A, B = g.permute(0, 2, 3, 1).contiguous(), x.permute(0, 2, 3, 1).contiguous()
+    old = F32.USE_WGRAD_BIG
+    try:
+        F32.USE_WGRAD_BIG = True
+        assert F32.wgrad_f32_tile(M, 9 * Nc, True) == (256, 256)
+        gw = torch.zeros(M, Nc, 3, 3, device="cuda")
+        gb = torch.zeros(M, device="cuda")
+        F32.wgrad(A, B, gw, gb, KH=3, KW=3, s=1, pad=1, target_blocks=7)
+        assert _rel(gw, gw_ref) < 1e-5 and _rel(gb, gb_ref) < 1e-5
+    finally:
+        F32.USE_WGRAD_BIG = old
+
+
 @pytest.mark.parametrize("N,H,W,Cin,Cmid,Cout,cs", [(2, 12, 20, 3, 32, 32, 4), (1, 16, 16, 128, 64, 64, 128)])
 def test_double_conv_fwd_bwd(hip_lib, N, H, W, Cin, Cmid, Cout, cs):
     """The fused DoubleConv Function (inner ReLU backward as conv2's dgrad mask epilogue) vs torch fp32."""
-    from distributedpytorch_amd.models.hip_unet_f32 import _DoubleConvReLU
+    from distributedpytorch_amd.models.hip_unet_f32 import _DoubleConvReLU, _L
     torch.manual_seed(Cin + Cmid)
     xr = torch.randn(N, Cin, H, W, device="cuda")
     w1 = (torch.randn(Cmid, Cin, 3, 3, device="cuda") / (9 * Cin) ** 0.5).requires_grad_(True)
@@ -122,9 +201,13 @@ def test_double_conv_fwd_bwd(hip_lib, N, H, W, Cin, Cmid, Cout, cs):
     xn = torch.zeros(N, H, W, cs, device="cuda")
     xn[..., :Cin] = xr.permute(0, 2, 3, 1)
     xn.requires_grad_(True)
-    y = _DoubleConvReLU.apply(xn, w1, b1, w2, b2, cs)
+    m1, m2 = _conv(w1.detach(), b1.detach()), _conv(w2.detach(), b2.detach())
+    l1, l2 = _L(m1, "conv", cs), _L(m2, "conv")
+    eng = _engine(l1, l2)
+    y = _DoubleConvReLU.apply(eng.anchor, xn, eng, l1, l2)
     assert _rel(y.permute(0, 3, 1, 2), ref) < 1e-5
-    gx, gw1, gb1, gw2, gb2 = torch.autograd.grad(y, (xn, w1, b1, w2, b2), g.permute(0, 2, 3, 1).contiguous())
+    (gx,) = torch.autograd.grad(y, (xn,), g.permute(0, 2, 3, 1).contiguous())
+    gw1, gb1, gw2, gb2 = m1.weight.grad, m1.bias.grad, m2.weight.grad, m2.bias.grad
     assert _rel(gx[..., :Cin].permute(0, 3, 1, 2), refs[0]) < 1e-5
     for got, want in zip((gw1, gb1, gw2, gb2), refs[1:]):
         assert _rel(got, want) < 1e-5
@@ -132,7 +215,7 @@ def test_double_conv_fwd_bwd(hip_lib, N, H, W, Cin, Cmid, Cout, cs):
 
 @pytest.mark.parametrize("N,h,w,Cin,Cout", [(2, 8, 12, 64, 32), (1, 5, 7, 128, 64), (2, 4, 4, 512, 256)])
 def test_deconv_fwd_bwd(hip_lib, N, h, w, Cin, Cout):
-    from distributedpytorch_amd.models.hip_unet_f32 import _Deconv
+    from distributedpytorch_amd.models.hip_unet_f32 import _Deconv, _L
     torch.manual_seed(Cin)
     x = torch.randn(N, Cin, h, w, device="cuda").requires_grad_(True)
     wt = (torch.randn(Cin, Cout, 2, 2, device="cuda") / Cin ** 0.5).requires_grad_(True)
@@ -141,9 +224,13 @@ def test_deconv_fwd_bwd(hip_lib, N, h, w, Cin, Cout):
     g = torch.randn_like(ref)
     gx_ref, gw_ref, gb_ref = torch.autograd.grad(ref, (x, wt, b), g)
     xn = x.detach().permute(0, 2, 3, 1).contiguous().requires_grad_(True)
-    y = _Deconv.apply(xn, wt, b)
+    m = _deconv(wt.detach(), b.detach())
+    layer = _L(m, "deconv")
+    eng = _engine(layer)
+    y = _Deconv.apply(eng.anchor, xn, eng, layer)
     assert _rel(y.permute(0, 3, 1, 2), ref) < 1e-5
-    gx, gw, gb = torch.autograd.grad(y, (xn, wt, b), g.permute(0, 2, 3, 1).contiguous())
+    (gx,) = torch.autograd.grad(y, (xn,), g.permute(0, 2, 3, 1).contiguous())
+    gw, gb = m.weight.grad, m.bias.grad
     assert _rel(gx.permute(0, 3, 1, 2), gx_ref) < 1e-5 and _rel(gw, gw_ref) < 1e-5 and _rel(gb, gb_ref) < 1e-5
 
 
@@ -169,9 +256,17 @@ def test_pool_and_head(hip_lib):
     dS = torch.tensor([0.3, -1.2, 0.7, 0.1], device="cuda")
     g_ref = torch.autograd.grad(S_ref, (yv, hw, hb), dS)
     yn = yv.detach().permute(0, 2, 3, 1).contiguous().requires_grad_(True)
-    S = _HeadLoss.apply(yn, hw, hb, t)
+    import types
+    seg = torch.nn.Conv2d(32, 1, 1).cuda()
+    with torch.no_grad():
+        seg.weight.copy_(hw)
+        seg.bias.copy_(hb)
+    eng = _engine()
+    eng.model = types.SimpleNamespace(segmap=seg)
+    S = _HeadLoss.apply(eng.anchor, yn, eng, t)
     assert _rel(S, S_ref) < 1e-5
-    gy, ghw, ghb = torch.autograd.grad(S, (yn, hw, hb), dS)
+    (gy,) = torch.autograd.grad(S, (yn,), dS)
+    ghw, ghb = seg.weight.grad, seg.bias.grad
     assert _rel(gy.permute(0, 3, 1, 2), g_ref[0]) < 1e-4 and _rel(ghw, g_ref[1]) < 1e-4 and _rel(ghb, g_ref[2]) < 1e-4
 
 

@@ -6,7 +6,8 @@ the real HIP kernels (the wire is the only difference from an RCCL run):
 * DDP (reference ``utils/train_utils.py:195-225``): the bucketed all-reduce of gradients the HIP
   backward announces block by block (``notify_ready``) equals the mean of per-rank single-device
   HIP gradients (fp32 wire exact, bf16 wire within bf16 rounding), rank 1's different init is
-  replaced by rank 0's, and replicas stay bitwise identical over 3 optimizer steps.
+  replaced by rank 0's, and replicas stay bitwise identical over 3 optimizer steps -- on the bf16
+  engine and on the fp32 engine (the reference's precision).
 * GPipe (reference ``model/unet_model.py:24-53``): a pipelined step equals the single-device HIP
   step of the same batch -- loss within 1e-3 relative, every parameter gradient cosine > 0.999,
   ``gather_state_dict`` exact -- for the reference 2-stage cut, a FLOP-balanced 4-stage cut and the
@@ -57,7 +58,7 @@ def _gather_cpu(t, world):
     return out
 
 
-def _ddp_worker(rank, world, port, comm, q):
+def _ddp_worker(rank, world, port, comm, dtype, q):
     import torch.distributed as dist
     try:
         _init(rank, world, port)
@@ -69,12 +70,12 @@ def _ddp_worker(rank, world, port, comm, q):
         if rank == 1:                      # DDP must replace this with rank 0's parameters
             for p in model.parameters():
                 p.data.mul_(1.5)
-        cfg = TrainConfig(train_method="DDP", backend="hip", dtype="bf16", lr=1e-3, bucket_mb=1.0,
+        cfg = TrainConfig(train_method="DDP", backend="hip", dtype=dtype, lr=1e-3, bucket_mb=1.0,
                           grad_comm_dtype=comm)
         st = DDPStrategy(cfg, model, torch.device("cuda:0"))
         ref = build_model("unet")
         ref.load_state_dict(st.model.state_dict())
-        sd = SingleDevice(TrainConfig(backend="hip", lr=1e-3), ref, "cuda:0")
+        sd = SingleDevice(TrainConfig(backend="hip", dtype=dtype, lr=1e-3), ref, "cuda:0")
         x, t = _batch(4, 64, seed=100 + rank)
         sd.optimizer.zero_grad()
         (sd.forward_loss(x, t) * 4).backward()
@@ -134,9 +135,12 @@ def _run(worker, world, *args, timeout=240):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("world,comm", [(2, "fp32"), (2, "bf16"), (4, "fp32")])
-def test_ddp_hip_allreduce_equals_mean_of_rank_grads(hip_lib, world, comm):
-    res = _run(_ddp_worker, world, comm)
+@pytest.mark.parametrize("world,comm,dtype", [(2, "fp32", "bf16"), (2, "bf16", "bf16"), (4, "fp32", "bf16"),
+                                              # the reference's own precision: the fp32 HIP engine under DDP
+                                              # (utils/train_utils.py:170-248 trains fp32)
+                                              (2, "fp32", "fp32"), (4, "fp32", "fp32")])
+def test_ddp_hip_allreduce_equals_mean_of_rank_grads(hip_lib, world, comm, dtype):
+    res = _run(_ddp_worker, world, comm, dtype)
     for rank, ok, err, same, nb, _ in res:
         assert nb >= 4, f"expected several buckets at 1 MiB, got {nb}"
         assert ok, f"rank {rank}: reduced grads != mean of per-rank grads (max rel err {err:.2e})"

@@ -3,7 +3,7 @@
 forward, dgrad and weight gradient, transposed-conv forward / dgrad / weight gradient; achieved TFLOP/s
 against the 157 TFLOP/s fp32-MFMA peak.
 
-    python tools/f32_kbench.py --batch 16 --img 512
+    python tools/f32_kbench.py --batch 16 --img 512 [--wgrad-big both]
 """
 import argparse
 import os
@@ -20,6 +20,8 @@ def main():
     ap.add_argument("--img", type=int, default=512)
     ap.add_argument("--model", default="unet")
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--wgrad-big", choices=["off", "on", "both"], default="off",
+                    help="time the conv weight gradients with the 256 x 256 tile too (deep layers)")
     a = ap.parse_args()
     from distributedpytorch_amd.models import hip_unet_f32 as E
     from distributedpytorch_amd.models.unet import build_model
@@ -60,18 +62,27 @@ def main():
     for name, hh, ci, co in convs:
         cs = 4 if ci == 3 else ci
         x = torch.randn(N, hh, hh, cs, device=dev)
-        wt = torch.randn(co, ci, 3, 3, device=dev) * 0.05
-        b = torch.zeros(co, device=dev)
+        m = torch.nn.Conv2d(ci, co, 3, padding=1).to(dev)
+        layer = E._L(m, "conv", cs)
+        eng = E.F32Engine([layer], dev)
+        eng.side = None                      # time the kernels themselves, on the current stream
+        eng.ensure_packed()
         ge = torch.randn(N, hh, hh, co, device=dev)
         fl = 2.0 * N * hh * hh * co * ci * 9
-        tf = t(lambda: E._conv_fwd(x, wt, b, cs))
-        td = t(lambda: E._conv_dgrad(ge, wt, cs)) if ci != 3 else 0.0
-        tw = t(lambda: E._conv_wgrad(ge, x, wt, cs))
+        tf = t(lambda: E._conv_fwd(eng, layer, x))
+        td = t(lambda: E._conv_dgrad(eng, layer, ge)) if ci != 3 else 0.0
+        modes = {"off": [False], "on": [True], "both": [False, True]}[a.wgrad_big]
+        tws = []
+        for big in modes:
+            F32.USE_WGRAD_BIG = big
+            tws.append(t(lambda: E._conv_wgrad(eng, layer, ge, x)))
+        tw = tws[-1]
         tot["fwd"] += tf
         tot["dgrad"] += td
         tot["wgrad"] += tw
+        extra = "" if len(tws) == 1 else f" (128x128 tile: {tws[0]:7.3f} {fl / tws[0] / 1e9:6.1f})"
         print(f"{name:10s} {hh:4d}x{hh:<4d} {ci:4d} {co:4d} | {tf:7.3f} {fl / tf / 1e9:6.1f} | {td:7.3f} "
-              f"{(fl / td / 1e9 if td else 0):6.1f} | {tw:7.3f} {fl / tw / 1e9:6.1f}", flush=True)
+              f"{(fl / td / 1e9 if td else 0):6.1f} | {tw:7.3f} {fl / tw / 1e9:6.1f}{extra}", flush=True)
         del x, ge
     for name, hh, ci, co in deconvs:
         x = torch.randn(N, hh, hh, ci, device=dev)
