@@ -36,6 +36,7 @@ struct F32ConvArgs {
   int N, Ho, Wo, Hs, Ws, Cs;
   int KH, KW, stride, pad;
   int Ngemm, Kpad, mode, relu, accumulate, Cout;
+  int wide;             // 1: the 256-pixel 8-wave tile for GEMM-N % 128 == 0 (ops/fp32.py IGEMM_WIDE)
 };
 
 struct F32WgradArgs {
@@ -76,12 +77,13 @@ __device__ __forceinline__ f32x4_t mfma4(const f32x4v& a, const f32x4v& b, f32x4
 
 }  // namespace
 
-// BP pixels x BC channels per block, BK-deep K-steps, 4 waves (NWP along the pixels x NWC along the channels)
-template <int BP, int BC, int NWP, int BK>
-__global__ __launch_bounds__(256) void igemm_f32_kernel(F32ConvArgs a) {
-  constexpr int NWC = 4 / NWP, WP = BP / NWP, WC = BC / NWC, TP = WP / 16, TC = WC / 16;
-  static_assert(NWP * NWC == 4 && TP >= 1 && TC >= 1 && (BK == 16 || BK == 32), "tile");
-  constexpr int CPR = BK / 4, RPP = 256 / CPR;       // float4 chunks per LDS row, rows per loader pass
+// BP pixels x BC channels per block, BK-deep K-steps, NW waves (NWP along the pixels x NWC along the channels);
+// NW = 8 with BP = 256: twice the MFMA work per barrier and per staged weight row (the deep layers)
+template <int BP, int BC, int NWP, int BK, int NW = 4>
+__global__ __launch_bounds__(64 * NW) void igemm_f32_kernel(F32ConvArgs a) {
+  constexpr int NWC = NW / NWP, WP = BP / NWP, WC = BC / NWC, TP = WP / 16, TC = WC / 16;
+  static_assert(NWP * NWC == NW && TP >= 1 && TC >= 1 && (BK == 16 || BK == 32), "tile");
+  constexpr int CPR = BK / 4, RPP = 64 * NW / CPR;   // float4 chunks per LDS row, rows per loader pass
   constexpr int RB = BK * 4;                         // LDS row bytes
   constexpr int LP = BP / RPP, LW = (BC + RPP - 1) / RPP;
   static_assert(BP % RPP == 0, "loader tiling");
@@ -537,7 +539,7 @@ __global__ __launch_bounds__(256) void relu_bwd_f32_kernel(const float* __restri
 
 // 2x2/s2 max-pool (floor), NHWC dense C channels; code = argmax window position (first maximum,
 // window order tl, tr, bl, br -- torch max_pool2d's choice)
-__global__ __launch_bounds__(256) void maxpool2_f32_kernel(const float* __restrict__ x, float* __restrict__ y,
+__global__ __launch_bounds__(256) void maxpool2_f32_kernel(const float* __restrict__ x, int ldx, float* __restrict__ y,
                                                            unsigned char* __restrict__ code, int N, int H, int W, int C) {
   const int Ho = H >> 1, Wo = W >> 1;
   const long tot = (long)N * Ho * Wo * C;
@@ -545,8 +547,8 @@ __global__ __launch_bounds__(256) void maxpool2_f32_kernel(const float* __restri
     const int c = (int)(i % C);
     const long pix = i / C;
     const int wo = (int)(pix % Wo), ho = (int)((pix / Wo) % Ho), n = (int)(pix / ((long)Wo * Ho));
-    const float* b = x + (((long)n * H + 2 * ho) * W + 2 * wo) * C + c;
-    const float v0 = b[0], v1 = b[C], v2 = b[(long)W * C], v3 = b[(long)W * C + C];
+    const float* b = x + (((long)n * H + 2 * ho) * W + 2 * wo) * ldx + c;
+    const float v0 = b[0], v1 = b[ldx], v2 = b[(long)W * ldx], v3 = b[(long)W * ldx + ldx];
     float m = v0;
     unsigned k = 0;
     if (v1 > m) { m = v1; k = 1; }
@@ -582,7 +584,7 @@ __global__ __launch_bounds__(256) void maxpool2_bwd_f32_kernel(const float* __re
 __global__ __launch_bounds__(256) void enc_out_bwd_f32_kernel(const float* __restrict__ gs, int lds,
                                                               const float* __restrict__ gp,
                                                               const unsigned char* __restrict__ code,
-                                                              const float* __restrict__ y, float* __restrict__ ge,
+                                                              const float* __restrict__ y, int ldy, float* __restrict__ ge,
                                                               int N, int H, int W, int C) {
   const int Ho = H >> 1, Wo = W >> 1, C4 = C >> 2;
   const long tot = (long)N * H * W * C4;
@@ -602,7 +604,7 @@ __global__ __launch_bounds__(256) void enc_out_bwd_f32_kernel(const float* __res
       v[2] += cd.z == k ? g[2] : 0.f;
       v[3] += cd.w == k ? g[3] : 0.f;
     }
-    const f32x4v yv = *reinterpret_cast<const f32x4v*>(y + pix * C + c);
+    const f32x4v yv = *reinterpret_cast<const f32x4v*>(y + pix * ldy + c);
 #pragma unroll
     for (int e = 0; e < 4; ++e) v[e] = yv[e] > 0.f ? v[e] : 0.f;
     *reinterpret_cast<f32x4v*>(ge + pix * C + c) = v;
@@ -735,6 +737,12 @@ DPA_API int dpa_igemm_f32(const F32ConvArgs* args, hipStream_t st) {
     const dim3 grid((unsigned)((M + 255) / 256));
     if (a.Ngemm == 64) hipLaunchKernelGGL((igemm_f32_kernel<256, 64, 4, 16>), grid, dim3(256), 0, st, a);
     else hipLaunchKernelGGL((igemm_f32_kernel<256, 32, 4, 16>), grid, dim3(256), 0, st, a);
+  } else if (a.Ngemm % 128 == 0 && k32 && a.wide && ((M + 255) / 256) * (a.Ngemm / 128) >= 512) {
+    // one 96 KB block of 8 waves per CU: only with >= 2 blocks per CU of work (a 32^2 deep layer at b16 has
+    // 256 and runs 30 % slower on it, profiles/f32_kbench_b16_512_r05_wide.txt)
+    const dim3 grid((unsigned)(((M + 255) / 256) * (a.Ngemm / 128)));
+    if (a.Ngemm == 128 || a.mode == 1) hipLaunchKernelGGL((igemm_f32_kernel<256, 128, 4, 16, 8>), grid, dim3(512), 0, st, a);
+    else hipLaunchKernelGGL((igemm_f32_kernel<256, 128, 4, 32, 8>), grid, dim3(512), 0, st, a);
   } else if (a.Ngemm % 128 == 0 && k32) {
     const dim3 grid((unsigned)(((M + 127) / 128) * (a.Ngemm / 128)));
     // 16-deep K-steps (32 KB of LDS, 3 waves / SIMD) measured faster for a single 128-wide GEMM-N tile and
@@ -793,9 +801,11 @@ DPA_API int dpa_relu_bwd_f32(const float* g, const float* r, float* y, long long
   return (int)hipGetLastError();
 }
 
-DPA_API int dpa_maxpool2_f32(const float* x, float* y, unsigned char* code, int N, int H, int W, int C, hipStream_t st) {
+DPA_API int dpa_maxpool2_f32(const float* x, int ldx, float* y, unsigned char* code, int N, int H, int W, int C,
+                             hipStream_t st) {
   if (H < 2 || W < 2 || C < 1) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(maxpool2_f32_kernel, dim3(egrid((long)N * (H / 2) * (W / 2) * C)), dim3(256), 0, st, x, y, code, N, H,
+  if (ldx < C) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(maxpool2_f32_kernel, dim3(egrid((long)N * (H / 2) * (W / 2) * C)), dim3(256), 0, st, x, ldx, y, code, N, H,
                      W, C);
   return (int)hipGetLastError();
 }
@@ -808,10 +818,11 @@ DPA_API int dpa_maxpool2_bwd_f32(const float* g, const unsigned char* code, floa
 }
 
 DPA_API int dpa_enc_out_bwd_f32(const float* gs, int lds, const float* gp, const unsigned char* code, const float* y,
-                                float* ge, int N, int H, int W, int C, hipStream_t st) {
-  if (H < 1 || W < 1 || (C & 3) || (gs && (lds & 3)) || (gp && (H < 2 || W < 2))) return (int)hipErrorInvalidValue;
+                                int ldy, float* ge, int N, int H, int W, int C, hipStream_t st) {
+  if (H < 1 || W < 1 || (C & 3) || (gs && (lds & 3)) || (ldy & 3) || ldy < C || (gp && (H < 2 || W < 2)))
+    return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(enc_out_bwd_f32_kernel, dim3(egrid((long)N * H * W * (C / 4))), dim3(256), 0, st, gs, lds, gp, code, y,
-                     ge, N, H, W, C);
+                     ldy, ge, N, H, W, C);
   return (int)hipGetLastError();
 }
 

@@ -434,6 +434,12 @@ DPA_API int dpa_head_grad_from_slab(const float* slab, int nblk, int C, float* t
   return (int)hipGetLastError();
 }
 
+// zero-fill (the flat gradient buffer before a step): a DMA-engine memset, no compute kernel
+DPA_API int dpa_zero(void* p, long long nbytes, hipStream_t st) {
+  if (nbytes < 0) return (int)hipErrorInvalidValue;
+  return (int)hipMemsetAsync(p, 0, (size_t)nbytes, st);
+}
+
 DPA_API int dpa_slab_sum(const float* slab, int nblk, int K, float* out, hipStream_t st) {
   hipLaunchKernelGGL(slab_sum_kernel, dim3(K), dim3(256), 0, st, slab, nblk, K, out, 0);
   return (int)hipGetLastError();

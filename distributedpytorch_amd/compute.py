@@ -64,7 +64,12 @@ def resolve_backend(backend: str, device, dtype: str = "bf16", model=None) -> st
     (bf16 storage, fp32 accumulate); fp32 -- the reference's precision, utils/train_utils.py:60-61 --:
     :class:`.models.hip_unet_f32.HipF32Blocks` (fp32 storage, fp32 MFMA) for the configurations it
     supports (``model`` given: checked; no BatchNorm / bilinear, widths % 32), else the torch backend
-    (fp32 on the GPU) for ``auto`` and an error for an explicit ``hip``."""
+    (fp32 on the GPU) for ``auto`` and an error for an explicit ``hip``.
+
+    The fp32 choice is deliberate even where stock MIOpen's steady state is close (b16, 512^2: 305 img/s
+    for this engine after round 5 vs 313 for MIOpen): MIOpen's first iteration spends minutes
+    compiling and searching solvers (449 s at b16; the b64 search did not finish in 600 s), while the HIP
+    engine has no warm-up, and it is the path the fp32 multi-rank (DDP) tests cover."""
     device = torch.device(device)
     if backend == "auto":
         if device.type != "cuda":

@@ -798,6 +798,23 @@ class _EncFn(torch.autograd.Function):
             B.join()
             ctx.st = None
             return None, None, None, None
+        N = a.shape[0]
+        chunks = K.ENC0_CHUNKS if (pool_fold and not ctx.x_needs_grad and c1.bn is None and dskip is not None
+                                   and B.side is not None and B.defer_wgrad <= 1) else 1
+        if chunks > 1 and N >= chunks:
+            # the first level: conv1 needs only its weight gradient, which reads conv2's whole input gradient
+            # -- launched after the last fused backward it would run alone at the end of the step (1.1 ms
+            # at b256).  Image chunks: conv1's weight gradient of chunk i (side stream) overlaps the fused
+            # backward of chunk i + 1, leaving only the last chunk's exposed
+            bounds = [N * i // chunks for i in range(chunks + 1)]
+            for n0, n1 in zip(bounds, bounds[1:]):
+                g1c = B.conv_bwd(c2, dskip[n0:n1], a[n0:n1], mask=True, pool=(code[n0:n1], dpooled[n0:n1]))
+                B.conv_wgrad(c1, g1c, x[n0:n1])
+            B.ready([c2.mod, c2.bn])
+            B.ready([c1.mod, c1.bn])
+            B.join()
+            ctx.st = None
+            return None, None, None, None
         if pool_fold:
             # max-pool backward folded into the conv's fused backward: the gradient is formed from
             # (skip gradient, pooled gradient, window codes) on load and never stored

@@ -22,6 +22,7 @@ divisible by 32 (other configurations take the stock torch path, ``compute.resol
 """
 from __future__ import annotations
 
+import weakref
 from typing import Optional
 
 import torch
@@ -84,11 +85,12 @@ class _L:
         self.off_f = self.off_d = -1
 
 
-def _conv_fwd(B, c: _L, x):
+def _conv_fwd(B, c: _L, x, y=None):
     """relu(conv3x3(x) + b), NHWC fp32; x has ``c.Cs`` channels (>= Cin: zero weights for the padding
-    channels of the network input)."""
+    channels of the network input); ``y``: the output (a channel slice allowed), else a new tensor."""
     N, H, W = x.shape[:3]
-    y = torch.empty(N, H, W, c.Cout, dtype=torch.float32, device=x.device)
+    if y is None:
+        y = torch.empty(N, H, W, c.Cout, dtype=torch.float32, device=x.device)
     F32.igemm(x, B.wf(c), y, Ngemm=c.Cout, Kpad=c.Kf, KH=3, KW=3, stride=1, pad=1, Cs=c.Cs, out_grid=(N, H, W),
               bias=c.mod.bias.detach(), relu=True)
     return y
@@ -161,22 +163,33 @@ class _DoubleConvReLU(torch.autograd.Function):
 
 class _EncBlock(torch.autograd.Function):
     """Encoder block: DoubleConv + 2x2 max-pool (reference Encoder, model/unet_parts.py:20-40) -> (skip, pooled).
-    Backward: the skip gradient, the pool backward and the last ReLU backward form the second conv's
-    pre-activation gradient in one pass (F32.enc_out_bwd); the inner ReLU as in :class:`_DoubleConvReLU`."""
+    The second conv writes the skip straight into the first half of the decoder's [N,H,W,2C] concat buffer
+    (registered with the engine by address; a skip leaving this pipeline stage stays dense), so the
+    reference's torch.cat (unet_parts.py:59) costs no copy.  Backward: the skip gradient, the pool backward
+    and the last ReLU backward form the second conv's pre-activation gradient in one pass
+    (F32.enc_out_bwd); the inner ReLU as in :class:`_DoubleConvReLU`."""
 
     @staticmethod
-    def forward(ctx, anchor, x, B, c1, c2):
+    def forward(ctx, anchor, x, B, c1, c2, dense: bool):
+        N, H, W = x.shape[:3]
         a = _conv_fwd(B, c1, x)
-        y = _conv_fwd(B, c2, a)
+        if dense:
+            own = y = torch.empty(N, H, W, c2.Cout, dtype=torch.float32, device=x.device)
+        else:
+            own = B.new_cat(N, H, W, c2.Cout)
+            y = own[..., :c2.Cout]
+        _conv_fwd(B, c2, a, y)
         pooled, code = F32.maxpool2(y)
-        ctx.B, ctx.c = B, (c1, c2)
-        ctx.save_for_backward(x, a, y, code)
+        ctx.B, ctx.c, ctx.C = B, (c1, c2), c2.Cout
+        # the concat buffer itself is saved: it keeps the engine's weak registry entry alive for the decoder
+        ctx.save_for_backward(x, a, own, code)
         return y, pooled
 
     @staticmethod
     def backward(ctx, gs, gp):
-        x, a, y, code = ctx.saved_tensors
+        x, a, own, code = ctx.saved_tensors
         B, (c1, c2) = ctx.B, ctx.c
+        y = own[..., :ctx.C]
         if gs is not None and not F32.nhwc_ok(gs):
             gs = gs.contiguous()
         ge2 = F32.enc_out_bwd(gs, None if gp is None else _dense(gp), code, y)
@@ -186,7 +199,7 @@ class _EncBlock(torch.autograd.Function):
         gx = _conv_dgrad(B, c1, ge1) if ctx.needs_input_grad[1] else None
         B.join()
         B.ready([c2.mod, c1.mod])
-        return None, gx, None, None, None
+        return None, gx, None, None, None, None
 
 
 def _deconv_bwd(B, d: _L, x, gy, need_dx: bool):
@@ -228,15 +241,15 @@ class _Deconv(torch.autograd.Function):
 
 class _UpCat(torch.autograd.Function):
     """[skip ‖ ConvTranspose2d(k2, s2)(x) + b] in one NHWC buffer (reference concat order, skip first,
-    model/unet_parts.py:58-59): the transposed conv's scatter epilogue stores straight into the upper
-    channel half; the backward reads both gradient halves in place (no split copies)."""
+    model/unet_parts.py:58-59): the skip is already in the buffer's first half when this engine's encoder
+    wrote it (one copy otherwise: a skip received from another pipeline stage); the transposed conv's
+    scatter epilogue stores straight into the upper half; the backward reads both gradient halves in place."""
 
     @staticmethod
     def forward(ctx, anchor, x, skip, B, d):
         N, h, w, ci = x.shape
         C = skip.shape[3]
-        buf = torch.empty(N, 2 * h, 2 * w, C + d.Cout, dtype=torch.float32, device=x.device)
-        buf[..., :C].copy_(skip)
+        buf = B.cat_for(skip, C + d.Cout)
         F32.igemm(x, B.wf(d), buf[..., C:], Ngemm=4 * d.Cout, Kpad=d.Kf, KH=1, KW=1, stride=1, pad=0,
                   Cs=ci, out_grid=(N, h, w), bias=d.mod.bias.detach(), mode=1, Cout=d.Cout)
         ctx.C, ctx.B, ctx.d = C, B, d
@@ -306,6 +319,26 @@ class F32Engine:
         from ..ops import kernels as K
         self.side = torch.cuda.Stream(device=self.device, priority=K.SIDE_PRIORITY) if K.SIDE_WGRAD else None
         self._keep = []
+        # concat buffers by the address of their first half (weak: a buffer whose skip another engine consumes
+        # is not kept alive by this map)
+        self._cats = weakref.WeakValueDictionary()
+        self.dense_skips = set()
+
+    def new_cat(self, N, H, W, C):
+        cat = torch.empty(N, H, W, 2 * C, dtype=torch.float32, device=self.device)
+        self._cats[cat.data_ptr()] = cat
+        return cat
+
+    def cat_for(self, skip: torch.Tensor, width: int) -> torch.Tensor:
+        """[N,H,W,width] concat buffer whose first skip.shape[3] channels hold ``skip``: the encoder's own
+        buffer when ``skip`` is its first half (zero-copy), else a new one with the skip copied in."""
+        N, H, W, C = skip.shape
+        cat = self._cats.pop(skip.data_ptr(), None)
+        if cat is not None and tuple(cat.shape) == (N, H, W, width) and skip.stride(2) == width:
+            return cat
+        cat = torch.empty(N, H, W, width, dtype=torch.float32, device=self.device)
+        cat[..., :C].copy_(skip)
+        return cat
 
     def side_launch(self, fn, *keep):
         """Run ``fn`` (weight-gradient launches reading ``keep``) on the side stream; the operands stay
@@ -398,7 +431,6 @@ class HipF32Blocks(F32Engine):
         device = torch.device(device) if device is not None else next(model.parameters()).device
         assert device.type == "cuda", "HipF32Blocks needs a GPU"
         assert supported(model), "fp32 HIP engine: reference UNet family without BatchNorm / bilinear, widths % 32 == 0"
-        self.dense_skips = set()
         if not any(hasattr(p, "_dpa_space") for p in model.parameters()):
             FlatParameterSpace(model, device=device)     # standalone use: flatten here
         self.encc = [[_L(c, "conv", 4 if (l == 0 and j == 0) else 0) for j, c in enumerate(b.convs())]
@@ -428,7 +460,7 @@ class HipF32Blocks(F32Engine):
     def enc(self, l: int, x):
         self.ensure_packed()
         c1, c2 = self.encc[l]
-        s, p = _EncBlock.apply(self.anchor, _v(x), self, c1, c2)
+        s, p = _EncBlock.apply(self.anchor, _v(x), self, c1, c2, l in self.dense_skips)
         return _o(s), _o(p)
 
     def mid(self, x):

@@ -63,12 +63,16 @@ KNOBS = (
          "stage the input halo once per 2 x 32-pixel patch (csrc/fp32.hip wgrad3_f32_kernel)"),
     Knob("f32_wgrad_big", "DPA_NO_F32_WGRAD_BIG", True, "fp32 engine: 256 x 256 8-wave weight-gradient tiles for the "
          "256-output-channel layers over >= 256 inputs instead of 128 x 128"),
+    Knob("f32_igemm_wide", "DPA_NO_F32_IGEMM_WIDE", True, "fp32 engine: 256-pixel x 128-channel 8-wave conv / dgrad "
+         "tiles for GEMM-N % 128 == 0 when the grid has >= 512 of them (the 128 x 128 4-wave tile otherwise)"),
     # launch geometry / streams
     Knob("side_priority", "DPA_SIDE_PRIORITY", 0, "HIP priority of the weight-gradient side stream (torch convention)"),
     Knob("wgrad_stream_blocks", "DPA_WGRAD_STREAM_BLOCKS", 2048, "target workgroups of a row-streaming weight gradient"),
     Knob("wgrad_gemm_blocks", "DPA_WGRAD_GEMM_BLOCKS", 768, "target workgroups of a dense-GEMM weight gradient"),
     Knob("bwd_blocks", "DPA_BWD_BLOCKS", 1024, "minimum workgroups of a fused backward launch"),
     Knob("bwd_blocks_small", "DPA_BWD_BLOCKS_SMALL", 512, "the same for launches over < 2^25 pixels"),
+    Knob("enc0_chunks", "DPA_ENC0_CHUNKS", 4, "first encoder level backward in this many image chunks, so the first "
+         "conv's side-stream weight gradient of one chunk overlaps the next chunk's fused backward (1 = off)"),
 )
 
 # process / launcher environment (not kernel dispatch): documented here so the allow-list is complete
@@ -125,11 +129,13 @@ class KernelConfig:
     bn_on_load: bool = True
     f32_wgrad_halo: bool = True
     f32_wgrad_big: bool = True
+    f32_igemm_wide: bool = True
     side_priority: int = 0
     wgrad_stream_blocks: int = 2048
     wgrad_gemm_blocks: int = 768
     bwd_blocks: int = 1024
     bwd_blocks_small: int = 512
+    enc0_chunks: int = 4
     bwd_blocks_set: bool = False          # DPA_BWD_BLOCKS given explicitly: applies to every launch
 
     @classmethod

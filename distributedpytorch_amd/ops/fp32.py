@@ -23,11 +23,12 @@ _MAX = 2 ** 31 - 1024          # per-launch element-offset range the host keeps 
 class F32ConvArgs(ctypes.Structure):
     _fields_ = [("x", c_void_p), ("w", c_void_p), ("bias", c_void_p), ("y", c_void_p), ("mask", c_void_p)] + \
                [(n, c_int) for n in ("ldx", "ldy", "ldm", "mask_ch", "N", "Ho", "Wo", "Hs", "Ws", "Cs", "KH", "KW",
-                                     "stride", "pad", "Ngemm", "Kpad", "mode", "relu", "accumulate", "Cout")]
+                                     "stride", "pad", "Ngemm", "Kpad", "mode", "relu", "accumulate", "Cout", "wide")]
 
 
 USE_WGRAD_HALO = _config.KernelConfig.from_env().f32_wgrad_halo   # 3x3 weight gradients with the input halo staged
 USE_WGRAD_BIG = _config.KernelConfig.from_env().f32_wgrad_big     # 256 x 256 8-wave weight-gradient tiles (deep layers)
+IGEMM_WIDE = _config.KernelConfig.from_env().f32_igemm_wide      # 256-pixel 8-wave conv / dgrad tiles for GEMM-N % 128 == 0
 
 
 def wgrad_f32_tile(M: int, Ncols: int, big: bool):
@@ -146,7 +147,7 @@ def igemm(x: torch.Tensor, wp: torch.Tensor, y: torch.Tensor, *, Ngemm: int, Kpa
         n1 = min(N, n0 + step)
         a = F32ConvArgs(x[n0:n1].data_ptr(), wp.data_ptr(), None if bias is None else bias.data_ptr(), y[n0:n1].data_ptr(),
                         None if mask is None else mask[n0:n1].data_ptr(), ldx, ldy, ldm, mask_ch, n1 - n0, Ho, Wo, Hs, Ws,
-                        Cs, KH, KW, stride, pad, Ngemm, Kpad, mode, int(relu), int(accumulate), Cout)
+                        Cs, KH, KW, stride, pad, Ngemm, Kpad, mode, int(relu), int(accumulate), Cout, int(IGEMM_WIDE))
         _check(L.dpa_igemm_f32(ctypes.byref(a), st), "igemm_f32")
     return y
 
@@ -207,11 +208,11 @@ def relu_bwd(g: torch.Tensor, r: torch.Tensor) -> torch.Tensor:
 
 
 def maxpool2(x: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """2x2 max-pool + window codes of NHWC fp32 x (a channel slice allowed: the skip half of a concat buffer)."""
     N, H, W, C, ld = nhwc(x, "maxpool2_f32.x")
-    assert ld == C and x.is_contiguous()
     y = torch.empty(N, H // 2, W // 2, C, dtype=torch.float32, device=x.device)
     code = torch.empty(N, H // 2, W // 2, C, dtype=torch.uint8, device=x.device)
-    _check(_lib.lib().dpa_maxpool2_f32(_p(x), _p(y), _p(code), c_int(N), c_int(H), c_int(W), c_int(C), _st(x)),
+    _check(_lib.lib().dpa_maxpool2_f32(_p(x), c_int(ld), _p(y), _p(code), c_int(N), c_int(H), c_int(W), c_int(C), _st(x)),
            "maxpool2_f32")
     return y, code
 
@@ -228,17 +229,17 @@ def maxpool2_bwd(g: torch.Tensor, code: torch.Tensor, H: int, W: int) -> torch.T
 def enc_out_bwd(gs: Optional[torch.Tensor], gp: Optional[torch.Tensor], code: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
     """(y > 0) * (gs + maxpool2_bwd(gp, code)) in one pass: the gradient entering an encoder DoubleConv's
     last ReLU from its skip output (``gs``: NHWC, channel slice allowed) and its pooled output (``gp``)."""
-    N, H, W, C, ld = nhwc(y, "enc_out_bwd_f32.y")
-    assert ld == C and y.is_contiguous() and C % 4 == 0
+    N, H, W, C, ldy = nhwc(y, "enc_out_bwd_f32.y")
+    assert C % 4 == 0
     lds = 0
     if gs is not None:
         assert tuple(gs.shape) == (N, H, W, C)
         _, _, _, _, lds = nhwc(gs, "enc_out_bwd_f32.gs")
     if gp is not None:
         assert gp.is_contiguous() and code.shape == gp.shape and tuple(gp.shape) == (N, H // 2, W // 2, C)
-    ge = torch.empty_like(y)
-    _check(_lib.lib().dpa_enc_out_bwd_f32(_p(gs), c_int(lds), _p(gp), _p(code), _p(y), _p(ge), c_int(N), c_int(H),
-                                         c_int(W), c_int(C), _st(y)), "enc_out_bwd_f32")
+    ge = torch.empty(N, H, W, C, dtype=torch.float32, device=y.device)
+    _check(_lib.lib().dpa_enc_out_bwd_f32(_p(gs), c_int(lds), _p(gp), _p(code), _p(y), c_int(ldy), _p(ge), c_int(N),
+                                         c_int(H), c_int(W), c_int(C), _st(y)), "enc_out_bwd_f32")
     return ge
 
 
@@ -257,8 +258,12 @@ def head_fwd(y: torch.Tensor, w: torch.Tensor, b: torch.Tensor, t: Optional[torc
         assert tf.numel() == P
     w = w.detach().reshape(-1).float().contiguous()
     b = b.detach().reshape(-1).float().contiguous()
-    _check(L.dpa_head_f32(_p(y), c_int(C), _p(w), _p(b), _p(tf), c_ll(P), _p(slab), _p(probs), _st(y)), "head_f32")
-    S = slab.view(blocks, 4).sum(0) if t is not None else None
+    st = _st(y)
+    _check(L.dpa_head_f32(_p(y), c_int(C), _p(w), _p(b), _p(tf), c_ll(P), _p(slab), _p(probs), st), "head_f32")
+    S = None
+    if t is not None:
+        S = torch.empty(4, dtype=torch.float32, device=y.device)
+        _check(L.dpa_slab_sum(_p(slab), c_int(blocks), c_int(4), _p(S), st), "head_f32(slab_sum)")
     return S, probs
 
 

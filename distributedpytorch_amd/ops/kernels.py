@@ -100,6 +100,7 @@ USE_GLDS128 = CFG.glds128
 USE_GLDS_BN = CFG.glds_bn              # BatchNorm partial sums in the row-block GEMM epilogue
 SIDE_WGRAD = CFG.side_wgrad            # weight gradients on a side stream (models/hip_unet.py)
 SIDE_PRIORITY = CFG.side_priority      # its HIP priority (torch convention: lower = higher, 0 = default)
+ENC0_CHUNKS = CFG.enc0_chunks          # first-level backward in image chunks (models/hip_unet.py _EncFn)
 WGRAD_STREAM_CFG = 0                   # row-streaming weight-gradient tile override (kbench A/B; 0 = auto)
 HALO_CFG = 0                           # row-halo conv tile override (kbench A/B; 0 = auto)
 USE_FUSED_HEAD = CFG.fused_head        # segmentation head + loss partials in the last decoder conv
@@ -1068,3 +1069,23 @@ class _LossFromPartials(torch.autograd.Function):
 
 def loss_from_partials(S: torch.Tensor, n: int, dice: bool = True) -> torch.Tensor:
     return _LossFromPartials.apply(S.contiguous(), n, dice)
+
+
+def zero_(t: torch.Tensor) -> torch.Tensor:
+    """In-place zero of a dense device tensor by hipMemsetAsync on the current stream (no compute kernel)."""
+    assert t.is_cuda and t.is_contiguous()
+    _check(_lib.lib().dpa_zero(_p(t), c_ll(t.numel() * t.element_size()), _stream(t)), "zero")
+    return t
+
+
+_SEEDS = {}
+
+
+def backward_scaled(loss: torch.Tensor, scale: float) -> None:
+    """``(loss * scale).backward()`` without the two elementwise launches: the backward is seeded with a
+    cached device scalar (one per device and scale value), which the loss op's HIP backward consumes."""
+    key = (loss.device, float(scale))
+    seed = _SEEDS.get(key)
+    if seed is None:
+        seed = _SEEDS[key] = torch.full((), float(scale), dtype=loss.dtype, device=loss.device)
+    torch.autograd.backward(loss, seed)

@@ -24,6 +24,11 @@ import torch.distributed as dist
 import torch.nn as nn
 
 
+def _hip_available() -> bool:
+    from .ops import _lib
+    return _lib.available()
+
+
 class FlatParameterSpace:
     """Make every parameter/grad of ``module`` a view into one flat fp32 buffer (backward order)."""
 
@@ -88,7 +93,11 @@ class FlatParameterSpace:
         return self.offsets[i], self.offsets[i + 1]
 
     def zero_grad(self):
-        self.grad.zero_()
+        if self.grad.is_cuda and _hip_available():
+            from .ops.kernels import zero_
+            zero_(self.grad)                 # a DMA memset: no compute kernel in the step
+        else:
+            self.grad.zero_()
         # autograd may have replaced .grad with a fresh tensor (e.g. after set_to_none); re-bind
         for p, o, n in zip(self.params, self.offsets, self.numels):
             if p.grad is None or p.grad.data_ptr() != self.grad[o:o + n].data_ptr():

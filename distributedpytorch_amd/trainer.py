@@ -99,6 +99,16 @@ def _loss_scale(cfg, batch):
     return float(batch) if cfg.loss_scale_by_batch else 1.0
 
 
+def _backward(loss, scale: float):
+    """``(loss * scale).backward()`` (reference utils/train_utils.py:69, A11); on a GPU with the HIP loss op
+    the scale seeds the backward instead of costing two elementwise launches."""
+    if loss.is_cuda and loss.grad_fn is not None and type(loss.grad_fn).__name__.startswith("_LossFromPartials"):
+        from .ops.kernels import backward_scaled
+        backward_scaled(loss, scale)
+    else:
+        (loss * scale).backward()
+
+
 class SingleDevice(Strategy):
     name = "singleGPU"
 
@@ -117,7 +127,7 @@ class SingleDevice(Strategy):
     def train_step(self, images, targets):
         self.optimizer.zero_grad()
         loss = self.forward_loss(images, targets)
-        (loss * _loss_scale(self.cfg, images.shape[0])).backward()
+        _backward(loss, _loss_scale(self.cfg, images.shape[0]))
         self.optimizer.step()
         return loss.detach()
 
@@ -163,7 +173,7 @@ class DDPStrategy(SingleDevice):
     def train_step(self, images, targets):
         self.optimizer.zero_grad()
         loss = self.forward_loss(images, targets)
-        (loss * _loss_scale(self.cfg, images.shape[0])).backward()
+        _backward(loss, _loss_scale(self.cfg, images.shape[0]))
         self.reducer.finish()
         self.optimizer.step()
         return loss.detach()
@@ -231,7 +241,7 @@ class DPStrategy(Strategy):
     def train_step(self, images, targets):
         self.optimizer.zero_grad()
         loss = self.dp.forward_loss(images, targets)
-        (loss * _loss_scale(self.cfg, images.shape[0])).backward()
+        _backward(loss, _loss_scale(self.cfg, images.shape[0]))
         self.dp.all_reduce_grads()
         self.optimizer.step()
         return loss.detach()
@@ -259,7 +269,7 @@ class PipelineLocalStrategy(Strategy):
     def train_step(self, images, targets):
         self.optimizer.zero_grad()
         loss = self.pipe.forward_loss(images, targets)
-        (loss * _loss_scale(self.cfg, images.shape[0])).backward()
+        _backward(loss, _loss_scale(self.cfg, images.shape[0]))
         self.optimizer.step()
         return loss.detach()
 

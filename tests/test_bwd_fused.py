@@ -234,3 +234,36 @@ def test_conv_bwd_fused_batchnorm_modes(hip_lib, N, H, W, Cin, Cout, epi):
         xs = x.float().cpu()
         assert _rel(sums[0], dxa.sum((0, 1, 2))) < 1e-3
         assert _rel(sums[1], (dxa * xs).sum((0, 1, 2))) < 1e-3
+
+
+@pytest.mark.parametrize("chunks", [2, 4])
+def test_first_level_backward_in_image_chunks(hip_lib, chunks):
+    """DPA_ENC0_CHUNKS: the first encoder level's fused (pool-folded) backward and the first conv's
+    side-stream weight gradient run per image chunk; every gradient equals the one-launch backward up to
+    fp32 summation order (the weight gradients are reduced per chunk)."""
+    from distributedpytorch_amd.config import TrainConfig
+    from distributedpytorch_amd.models.unet import build_model
+    from distributedpytorch_amd.ops import kernels as K
+    from distributedpytorch_amd.trainer import SingleDevice
+    from distributedpytorch_amd.data.synthetic import synthetic_batch
+    torch.manual_seed(0)
+    model = build_model("unet")
+    st = SingleDevice(TrainConfig(backend="hip", lr=1e-3), model, "cuda:0")
+    img, mask = synthetic_batch(8, 128, 128, 3, seed=4)
+    x, t = img.cuda(), mask.float().unsqueeze(1).cuda()
+    grads = []
+    old = K.ENC0_CHUNKS
+    try:
+        for c in (1, chunks):
+            K.ENC0_CHUNKS = c
+            st.optimizer.zero_grad()
+            (st.forward_loss(x, t) * 8).backward()
+            torch.cuda.synchronize()
+            grads.append(st.space.grad.detach().clone())
+    finally:
+        K.ENC0_CHUNKS = old
+    g0, g1 = grads
+    for i, n in enumerate(st.space.names):
+        o0, o1 = st.space.slice_of(i)
+        a, b = g0[o0:o1].double(), g1[o0:o1].double()
+        assert ((a - b).abs().max() / a.abs().max().clamp_min(1e-30)).item() < 1e-4, n

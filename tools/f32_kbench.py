@@ -22,6 +22,8 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--wgrad-big", choices=["off", "on", "both"], default="off",
                     help="time the conv weight gradients with the 256 x 256 tile too (deep layers)")
+    ap.add_argument("--igemm-wide", choices=["off", "on", "both"], default="off",
+                    help="time the conv forward / dgrad with the 256-pixel 8-wave tile too")
     a = ap.parse_args()
     from distributedpytorch_amd.models import hip_unet_f32 as E
     from distributedpytorch_amd.models.unet import build_model
@@ -69,8 +71,13 @@ def main():
         eng.ensure_packed()
         ge = torch.randn(N, hh, hh, co, device=dev)
         fl = 2.0 * N * hh * hh * co * ci * 9
-        tf = t(lambda: E._conv_fwd(eng, layer, x))
-        td = t(lambda: E._conv_dgrad(eng, layer, ge)) if ci != 3 else 0.0
+        wmodes = {"off": [False], "on": [True], "both": [False, True]}[a.igemm_wide]
+        tfs, tds = [], []
+        for wide in wmodes:
+            F32.IGEMM_WIDE = wide
+            tfs.append(t(lambda: E._conv_fwd(eng, layer, x)))
+            tds.append(t(lambda: E._conv_dgrad(eng, layer, ge)) if ci != 3 else 0.0)
+        tf, td = tfs[-1], tds[-1]
         modes = {"off": [False], "on": [True], "both": [False, True]}[a.wgrad_big]
         tws = []
         for big in modes:
@@ -81,6 +88,8 @@ def main():
         tot["dgrad"] += td
         tot["wgrad"] += tw
         extra = "" if len(tws) == 1 else f" (128x128 tile: {tws[0]:7.3f} {fl / tws[0] / 1e9:6.1f})"
+        if len(tfs) > 1:
+            extra += f" [4-wave fwd {tfs[0]:7.3f} dgrad {tds[0]:7.3f}]"
         print(f"{name:10s} {hh:4d}x{hh:<4d} {ci:4d} {co:4d} | {tf:7.3f} {fl / tf / 1e9:6.1f} | {td:7.3f} "
               f"{(fl / td / 1e9 if td else 0):6.1f} | {tw:7.3f} {fl / tw / 1e9:6.1f}{extra}", flush=True)
         del x, ge
