@@ -49,6 +49,7 @@ struct F32WgradArgs {
   int splits;
   int halo;             // 1: the 3x3 / s1 / p1 form with the B halo staged per 2 x 32-pixel stage
   int big;              // 1: allow the 256 x 256 tile (M % 256 == 0, >= 256 columns)
+  int px;               // 1: pixel-major LDS images (no loader transpose), PX form of wgrad_f32_kernel
 };
 
 namespace {
@@ -247,7 +248,13 @@ __global__ __launch_bounds__(64 * NW) void igemm_f32_kernel(F32ConvArgs a) {
 // loads a 4-pixel x 4-channel micro-block (4 float4, channel-contiguous in NHWC) and writes it as 4
 // float4 rows of 4 pixels.  Next stage's loads in registers during the current one; one barrier per
 // stage.  The bias gradient sum_p A[p][m] rides along in the blocks of column tile 0.
-template <int BM, int BN>
+//
+// PX = true: the same GEMM with PIXEL-major LDS images ([32 px][BM + 4] / [32 px][BN + 4] floats, channels
+// contiguous as in NHWC): the loader stores each thread's float4s as they were loaded (no register
+// transpose), and an MFMA operand is 4 ds_read_b32 of one channel column (rows 4q + e; the +4-float row
+// pad puts rows 4 apart 16 banks apart: conflict-free halves).  Same MFMA sequence per accumulator -> the
+// same result bit for bit.
+template <int BM, int BN, bool PX = false>
 __global__ __launch_bounds__(2 * BN) void wgrad_f32_kernel(F32WgradArgs a) {
   constexpr int BK = 32, RB = BK * 4;                           // LDS row bytes (8 chunks of 4 px)
   constexpr int NT = 2 * BN, NW = NT / 64;                      // one B micro-block per thread per stage
@@ -255,7 +262,9 @@ __global__ __launch_bounds__(2 * BN) void wgrad_f32_kernel(F32WgradArgs a) {
   constexpr int QA = BM / 4, UA = QA * (BK / 4);                // A micro-blocks (4 ch x 4 px) per stage
   constexpr int QB = BN / 4;                                    // B: BN/4 x 8 micro-blocks
   static_assert(TM >= 1 && TN >= 1 && UA <= NT && QB * (BK / 4) == NT, "tile");
-  __shared__ __attribute__((aligned(16))) char lds[2][(BM + BN) * RB];
+  constexpr int SA = BM + 4, SB = BN + 4;                       // PX: floats per pixel row
+  constexpr int STAGE = PX ? BK * (SA + SB) * 4 : (BM + BN) * RB;
+  __shared__ __attribute__((aligned(16))) char lds[2][STAGE];
 
   const int T = a.KH * a.KW, Ncols = T * a.Nc;
   const int nmt = a.M / BM, nnt = (Ncols + BN - 1) / BN, tiles = nmt * nnt;
@@ -312,6 +321,18 @@ __global__ __launch_bounds__(2 * BN) void wgrad_f32_kernel(F32WgradArgs a) {
     return o;
   };
   auto lstore = [&](int buf) {
+    if constexpr (PX) {
+      float* As = reinterpret_cast<float*>(lds[buf]);
+      float* Bs = As + BK * SA;
+      if (has_a) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) *reinterpret_cast<f32x4v*>(As + (4 * pa + e) * SA + 4 * qa) = va[e];
+        if (do_bias) bsum += va[0] + va[1] + va[2] + va[3];
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) *reinterpret_cast<f32x4v*>(Bs + (4 * pbq + e) * SB + 4 * qb) = vb[e];
+      return;
+    }
     char* As = lds[buf];
     char* Bs = lds[buf] + BM * RB;
     if (has_a) {
@@ -341,6 +362,28 @@ __global__ __launch_bounds__(2 * BN) void wgrad_f32_kernel(F32WgradArgs a) {
   for (int s = 0; s < S; ++s) {
     const int buf = s & 1;
     if (s + 1 < S) gload(p0 + (s + 1) * BK);
+    if constexpr (PX) {
+      const float* As = reinterpret_cast<const float*>(lds[buf]) + wm * WM + l16;
+      const float* Bs = reinterpret_cast<const float*>(lds[buf]) + BK * SA + wn * WN + l16;
+#pragma unroll
+      for (int kb = 0; kb < BK / 16; ++kb)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int row = 16 * kb + 4 * q + e;
+          float av[TM], bv[TN];
+#pragma unroll
+          for (int i = 0; i < TM; ++i) av[i] = As[row * SA + i * 16];
+#pragma unroll
+          for (int j = 0; j < TN; ++j) bv[j] = Bs[row * SB + j * 16];
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i], bv[j], acc[i][j], 0, 0, 0);
+        }
+      if (s + 1 < S) lstore(buf ^ 1);
+      __syncthreads();
+      continue;
+    }
     const char* As = lds[buf];
     const char* Bs = lds[buf] + BM * RB;
 #pragma unroll
@@ -788,6 +831,13 @@ DPA_API int dpa_wgrad_f32(const F32WgradArgs* args, hipStream_t st) {
   const int T = a.KH * a.KW, bm = wgrad_f32_bm(a.M, T * a.Nc, a.big), bn = bm == 256 ? 256 : 128;
   const long tiles = (long)(a.M / bm) * ((T * a.Nc + bn - 1) / bn);
   const dim3 grid((unsigned)(tiles * a.splits));
+  if (a.px) {
+    if (bm == 256) hipLaunchKernelGGL((wgrad_f32_kernel<256, 256, true>), grid, dim3(512), 0, st, a);
+    else if (bm == 128) hipLaunchKernelGGL((wgrad_f32_kernel<128, 128, true>), grid, dim3(256), 0, st, a);
+    else if (bm == 64) hipLaunchKernelGGL((wgrad_f32_kernel<64, 128, true>), grid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((wgrad_f32_kernel<32, 128, true>), grid, dim3(256), 0, st, a);
+    return (int)hipGetLastError();
+  }
   if (bm == 256) hipLaunchKernelGGL((wgrad_f32_kernel<256, 256>), grid, dim3(512), 0, st, a);
   else if (bm == 128) hipLaunchKernelGGL((wgrad_f32_kernel<128, 128>), grid, dim3(256), 0, st, a);
   else if (bm == 64) hipLaunchKernelGGL((wgrad_f32_kernel<64, 128>), grid, dim3(256), 0, st, a);

@@ -65,6 +65,9 @@ KNOBS = (
          "256-output-channel layers over >= 256 inputs instead of 128 x 128"),
     Knob("f32_igemm_wide", "DPA_NO_F32_IGEMM_WIDE", True, "fp32 engine: 256-pixel x 128-channel 8-wave conv / dgrad "
          "tiles for GEMM-N % 128 == 0 when the grid has >= 512 of them (the 128 x 128 4-wave tile otherwise)"),
+    Knob("f32_wgrad_px", "DPA_NO_F32_WGRAD_PX", True, "fp32 engine: weight-gradient operands staged pixel-major "
+         "(no loader transpose; ds_read_b32 operand columns) -- same result bit for bit, 19.9 vs 20.2 ms of "
+         "weight gradients at b16 512^2 (profiles/f32_kbench_b16_512_r05_px.txt)"),
     # launch geometry / streams
     Knob("side_priority", "DPA_SIDE_PRIORITY", 0, "HIP priority of the weight-gradient side stream (torch convention)"),
     Knob("wgrad_stream_blocks", "DPA_WGRAD_STREAM_BLOCKS", 2048, "target workgroups of a row-streaming weight gradient"),
@@ -130,6 +133,7 @@ class KernelConfig:
     f32_wgrad_halo: bool = True
     f32_wgrad_big: bool = True
     f32_igemm_wide: bool = True
+    f32_wgrad_px: bool = True
     side_priority: int = 0
     wgrad_stream_blocks: int = 2048
     wgrad_gemm_blocks: int = 768

@@ -29,6 +29,7 @@ class F32ConvArgs(ctypes.Structure):
 USE_WGRAD_HALO = _config.KernelConfig.from_env().f32_wgrad_halo   # 3x3 weight gradients with the input halo staged
 USE_WGRAD_BIG = _config.KernelConfig.from_env().f32_wgrad_big     # 256 x 256 8-wave weight-gradient tiles (deep layers)
 IGEMM_WIDE = _config.KernelConfig.from_env().f32_igemm_wide      # 256-pixel 8-wave conv / dgrad tiles for GEMM-N % 128 == 0
+WGRAD_PX = _config.KernelConfig.from_env().f32_wgrad_px          # pixel-major LDS weight-gradient operands
 
 
 def wgrad_f32_tile(M: int, Ncols: int, big: bool):
@@ -44,7 +45,7 @@ def wgrad_f32_tile(M: int, Ncols: int, big: bool):
 class F32WgradArgs(ctypes.Structure):
     _fields_ = [("A", c_void_p), ("B", c_void_p), ("slab", c_void_p), ("bslab", c_void_p)] + \
                [(n, c_int) for n in ("lda", "ldb", "N", "Hg", "Wg", "HB", "WB", "M", "Nc", "s", "pad", "KH", "KW")] + \
-               [("pix_per_split", ctypes.c_long), ("splits", c_int), ("halo", c_int), ("big", c_int)]
+               [("pix_per_split", ctypes.c_long), ("splits", c_int), ("halo", c_int), ("big", c_int), ("px", c_int)]
 
 
 def _st(t: torch.Tensor):
@@ -190,7 +191,8 @@ def wgrad(A: torch.Tensor, B: torch.Tensor, gw: torch.Tensor, gb: Optional[torch
     slab = torch.empty(splits * T * M * Nc + (splits * M if gb is not None else 0), dtype=torch.float32, device=A.device)
     bslab = slab[splits * T * M * Nc:] if gb is not None else None
     a = F32WgradArgs(A.data_ptr(), B.data_ptr(), slab.data_ptr(), None if bslab is None else bslab.data_ptr(),
-                     lda, ldb, N, Hg, Wg, HB, WB, M, Nc, s, pad, KH, KW, pps, splits, halo, int(USE_WGRAD_BIG))
+                     lda, ldb, N, Hg, Wg, HB, WB, M, Nc, s, pad, KH, KW, pps, splits, halo, int(USE_WGRAD_BIG),
+                     int(WGRAD_PX))
     L = _lib.lib()
     st = _st(A)
     _check(L.dpa_wgrad_f32(ctypes.byref(a), st), "wgrad_f32")

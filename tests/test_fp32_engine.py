@@ -184,6 +184,34 @@ def test_wgrad_big_tile(hip_lib, N, H, W, Nc, M):
         F32.USE_WGRAD_BIG = old
 
 
+@pytest.mark.parametrize("N,H,W,Nc,M,big", [(2, 8, 16, 64, 128, False), (1, 6, 10, 32, 64, False),
+                                            (2, 5, 7, 96, 32, False), (1, 8, 8, 512, 256, True)])
+def test_wgrad_pixel_major_form(hip_lib, N, H, W, Nc, M, big):
+    """The pixel-major weight-gradient form (default; DPA_NO_F32_WGRAD_PX=1 opts out: no loader transpose, ds_read_b32 operand
+    columns) issues the same MFMA sequence per accumulator: bit-equal to the transposing form, and within
+    fp32 rounding of torch."""
+    from distributedpytorch_amd.ops import fp32 as F32
+    torch.manual_seed(Nc + M + W)
+    x = torch.randn(N, Nc, H, W, device="cuda")
+    g = torch.randn(N, M, H, W, device="cuda")
+    gw_ref = torch.nn.grad.conv2d_weight(x, (M, Nc, 3, 3), g, padding=1)
+    A, B = g.permute(0, 2, 3, 1).contiguous(), x.permute(0, 2, 3, 1).contiguous()
+    old = (F32.WGRAD_PX, F32.USE_WGRAD_HALO, F32.USE_WGRAD_BIG)
+    outs = []
+    try:
+        F32.USE_WGRAD_HALO, F32.USE_WGRAD_BIG = False, big
+        for px in (False, True):
+            F32.WGRAD_PX = px
+            gw = torch.zeros(M, Nc, 3, 3, device="cuda")
+            gb = torch.zeros(M, device="cuda")
+            F32.wgrad(A, B, gw, gb, KH=3, KW=3, s=1, pad=1, target_blocks=13)
+            outs.append((gw, gb))
+    finally:
+        F32.WGRAD_PX, F32.USE_WGRAD_HALO, F32.USE_WGRAD_BIG = old
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    assert _rel(outs[1][0], gw_ref) < 1e-5
+
+
 @pytest.mark.parametrize("N,H,W,Cin,Cmid,Cout,cs", [(2, 12, 20, 3, 32, 32, 4), (1, 16, 16, 128, 64, 64, 128)])
 def test_double_conv_fwd_bwd(hip_lib, N, H, W, Cin, Cmid, Cout, cs):
     """The fused DoubleConv Function (inner ReLU backward as conv2's dgrad mask epilogue) vs torch fp32."""

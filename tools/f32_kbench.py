@@ -24,6 +24,8 @@ def main():
                     help="time the conv weight gradients with the 256 x 256 tile too (deep layers)")
     ap.add_argument("--igemm-wide", choices=["off", "on", "both"], default="off",
                     help="time the conv forward / dgrad with the 256-pixel 8-wave tile too")
+    ap.add_argument("--wgrad-px", choices=["off", "on", "both"], default="off",
+                    help="time the generic weight gradients with the pixel-major LDS form too")
     a = ap.parse_args()
     from distributedpytorch_amd.models import hip_unet_f32 as E
     from distributedpytorch_amd.models.unet import build_model
@@ -79,15 +81,19 @@ def main():
             tds.append(t(lambda: E._conv_dgrad(eng, layer, ge)) if ci != 3 else 0.0)
         tf, td = tfs[-1], tds[-1]
         modes = {"off": [False], "on": [True], "both": [False, True]}[a.wgrad_big]
+        pxm = {"off": [False], "on": [True], "both": [False, True]}[a.wgrad_px]
+        if len(pxm) > 1:
+            modes = [F32.USE_WGRAD_BIG] * 2
         tws = []
-        for big in modes:
+        for k, big in enumerate(modes):
             F32.USE_WGRAD_BIG = big
+            F32.WGRAD_PX = pxm[min(k, len(pxm) - 1)]
             tws.append(t(lambda: E._conv_wgrad(eng, layer, ge, x)))
         tw = tws[-1]
         tot["fwd"] += tf
         tot["dgrad"] += td
         tot["wgrad"] += tw
-        extra = "" if len(tws) == 1 else f" (128x128 tile: {tws[0]:7.3f} {fl / tws[0] / 1e9:6.1f})"
+        extra = "" if len(tws) == 1 else f" (other form: {tws[0]:7.3f} {fl / tws[0] / 1e9:6.1f})"
         if len(tfs) > 1:
             extra += f" [4-wave fwd {tfs[0]:7.3f} dgrad {tds[0]:7.3f}]"
         print(f"{name:10s} {hh:4d}x{hh:<4d} {ci:4d} {co:4d} | {tf:7.3f} {fl / tf / 1e9:6.1f} | {td:7.3f} "

@@ -107,6 +107,15 @@ def main():
         with open(a.out, "w") as f:
             f.write(txt + "\n")
     if a.plans:
+        old = {}
+        if os.path.exists(a.plans):
+            with open(a.plans) as f:
+                old = json.load(f)
+        for key, row in plans.items():      # measured rehearsals stay with a plan whose placement is unchanged
+            prev = old.get(key, {})
+            if "measured" in prev and prev.get("cuts") == row["cuts"] and prev.get("owner") == row["owner"] \
+                    and prev.get("microbatches") == row["microbatches"]:
+                row["measured"] = prev["measured"]
         with open(a.plans, "w") as f:
             json.dump(plans, f, indent=1)
 
