@@ -37,6 +37,7 @@ struct F32ConvArgs {
   int KH, KW, stride, pad;
   int Ngemm, Kpad, mode, relu, accumulate, Cout;
   int wide;             // 1: the 256-pixel 8-wave tile for GEMM-N % 128 == 0 (ops/fp32.py IGEMM_WIDE)
+  int halo;             // 1: 3x3 / s1 / p1 convs with GEMM-N == 32 (or 64, 2): conv3_halo_f32_kernel
 };
 
 struct F32WgradArgs {
@@ -47,7 +48,8 @@ struct F32WgradArgs {
   int lda, ldb, N, Hg, Wg, HB, WB, M, Nc, s, pad, KH, KW;
   long pix_per_split;   // pixels per split (multiple of 32; halo form: of 64, in stage order)
   int splits;
-  int halo;             // 1: the 3x3 / s1 / p1 form with the B halo staged per 2 x 32-pixel stage
+  int halo;             // 1: the 3x3 / s1 / p1 form with the B halo staged per 2 x 32-pixel stage; 2: 64 columns as 2 x 32;
+                        //    3: the first layer's 4-channel form (wgrad_c4_f32_kernel)
   int big;              // 1: allow the 256 x 256 tile (M % 256 == 0, >= 256 columns)
   int px;               // 1: pixel-major LDS images (no loader transpose), PX form of wgrad_f32_kernel
 };
@@ -229,6 +231,114 @@ __global__ __launch_bounds__(64 * NW) void igemm_f32_kernel(F32ConvArgs a) {
       }
       if (a.mask && co < a.mask_ch) {
         const f32x4v mk = *reinterpret_cast<const f32x4v*>(a.mask + (long)m * a.ldm + co);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = mk[r] > 0.f ? v[r] : 0.f;
+      }
+      if (a.accumulate) v += *reinterpret_cast<const f32x4v*>(a.y + off);
+      *reinterpret_cast<f32x4v*>(a.y + off) = v;
+    }
+  }
+}
+
+// 3x3 / stride 1 / pad 1 conv over 32-channel input slices with a narrow GEMM-N (32 output columns per
+// block): the implicit GEMM above re-fetches every input pixel once per tap (9x) for only 32 output
+// channels -- 16 FLOP per byte through L1 / L2, the bound of the 32-channel full-resolution layers
+// (70-86 TF/s, profiles/f32_kbench_b16_512_r05_px.txt).  Here a block stages the 10 x 34 input halo of its
+// 8 x 32 output pixels once per 32-channel slice ([pixel][32 ch], 128-B rows, chunk ^ (pixel & 7) so 8
+// consecutive pixels at any tap shift read distinct bank groups) together with the slice's 9 taps of
+// weights ([tap][n][32 k], fswzk<8>), and every tap reads its operands from LDS: 80 KB per block (2 per
+// CU), ~4x fewer fetched bytes per FLOP.  Wave w computes output rows 2w, 2w + 1 (4 pixel tiles x 2
+// channel tiles).  K runs tap-major within a slice in 16-deep slabs, the permuted 4q + e order as above.
+// Same epilogue (bias / ReLU / mask / accumulate) as igemm_f32_kernel, mode 0.
+__global__ __launch_bounds__(256) void conv3_halo_f32_kernel(F32ConvArgs a) {
+  constexpr int BR = 8, BW = 32, HR = BR + 2, HW = BW + 2, HP = HR * HW, RB = 128;
+  __shared__ __attribute__((aligned(16))) char lds[(HP + 9 * 32) * RB];
+  char* Hs = lds;
+  char* Ws = lds + HP * RB;
+  const int nct = a.Ngemm / 32, nwt = a.Wo / BW, nht = a.Ho / BR;
+  const int total = a.N * nht * nwt * nct;
+  const int bid = xcd_remap(blockIdx.x, total);
+  const int ct = bid % nct, pt = bid / nct;
+  const int n = pt / (nht * nwt), rem = pt - n * (nht * nwt), hb = rem / nwt, wb = rem - hb * nwt;
+  const int h0 = hb * BR, w0 = wb * BW, c0 = ct * 32;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, q = lane >> 4, l16 = lane & 15;
+
+  f32x4_t acc[2][4];
+#pragma unroll
+  for (int ic = 0; ic < 2; ++ic)
+#pragma unroll
+    for (int ip = 0; ip < 4; ++ip) acc[ic][ip] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  for (int cs = 0; cs < a.Cs; cs += 32) {
+    if (cs) __syncthreads();
+    // halo slice: HP pixels x 8 chunks, chunk-fastest across threads
+    constexpr int HI = (HP * 8 + 255) / 256;
+    f32x4v hv[HI];
+#pragma unroll
+    for (int i = 0; i < HI; ++i) {          // all loads in flight before the first store
+      const int u = tid + 256 * i, p = u >> 3, c = u & 7, hr = p / HW, hc = p - hr * HW;
+      const int ih = h0 - 1 + hr, iw = w0 - 1 + hc;
+      hv[i] = f32x4v{0.f, 0.f, 0.f, 0.f};
+      if (u < HP * 8 && ih >= 0 && ih < a.Hs && iw >= 0 && iw < a.Ws)
+        hv[i] = *reinterpret_cast<const f32x4v*>(a.x + ((long)(n * a.Hs + ih) * a.Ws + iw) * a.ldx + cs + 4 * c);
+    }
+#pragma unroll
+    for (int i = 0; i < HI; ++i) {
+      const int u = tid + 256 * i, p = u >> 3, c = u & 7;
+      if (u < HP * 8) *reinterpret_cast<f32x4v*>(Hs + p * RB + ((c ^ (p & 7)) << 4)) = hv[i];
+    }
+    // weights of the slice: row (tap, n) = the packed row c0 + n at k = tap * Cs + cs
+#pragma unroll
+    for (int i = 0; i < 9; ++i) {
+      const int u = tid + 256 * i, row = u >> 3, c = u & 7, tap = row >> 5, nn = row & 31;
+      *reinterpret_cast<f32x4v*>(Ws + row * RB + fswzk<8>(row, c) * 16) =
+          *reinterpret_cast<const f32x4v*>(a.w + (long)(c0 + nn) * a.Kpad + tap * a.Cs + cs + 4 * c);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      const int kh = tap / 3, kw = tap - 3 * kh;
+#pragma unroll
+      for (int sl = 0; sl < 2; ++sl) {
+        const int ch = 4 * sl + q;
+        f32x4v af[2], bf[4];
+#pragma unroll
+        for (int ic = 0; ic < 2; ++ic) {
+          const int row = tap * 32 + ic * 16 + l16;
+          af[ic] = *reinterpret_cast<const f32x4v*>(Ws + row * RB + fswzk<8>(row, ch) * 16);
+        }
+#pragma unroll
+        for (int ip = 0; ip < 4; ++ip) {
+          const int p = (2 * wid + (ip >> 1) + kh) * HW + 16 * (ip & 1) + l16 + kw;
+          bf[ip] = *reinterpret_cast<const f32x4v*>(Hs + p * RB + ((ch ^ (p & 7)) << 4));
+        }
+#pragma unroll
+        for (int ic = 0; ic < 2; ++ic)
+#pragma unroll
+          for (int ip = 0; ip < 4; ++ip) acc[ic][ip] = mfma4(af[ic], bf[ip], acc[ic][ip]);
+      }
+    }
+  }
+
+  // epilogue: lane holds 4 consecutive output channels (4 q + r) of pixel l16 of each pixel tile
+#pragma unroll
+  for (int ip = 0; ip < 4; ++ip) {
+    const long m = ((long)n * a.Ho + h0 + 2 * wid + (ip >> 1)) * a.Wo + w0 + 16 * (ip & 1) + l16;
+#pragma unroll
+    for (int ic = 0; ic < 2; ++ic) {
+      const int co = c0 + ic * 16 + 4 * q;
+      const long off = m * a.ldy + co;
+      f32x4v v = f32x4v{acc[ic][ip][0], acc[ic][ip][1], acc[ic][ip][2], acc[ic][ip][3]};
+      if (a.bias) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] += a.bias[co + r];
+      }
+      if (a.relu) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+      }
+      if (a.mask && co < a.mask_ch) {
+        const f32x4v mk = *reinterpret_cast<const f32x4v*>(a.mask + m * a.ldm + co);
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] = mk[r] > 0.f ? v[r] : 0.f;
       }
@@ -453,10 +563,10 @@ __global__ __launch_bounds__(256) void wgrad3_f32_kernel(F32WgradArgs a) {
   constexpr int AROWS = SR * 32, BROWS = 3 * (SR + 2) * NC;     // A rows (r, m); B rows (kw, hr, n)
   __shared__ __attribute__((aligned(16))) char lds[(AROWS + BROWS) * RB];
 
-  const int nmb = a.M / 32;
-  const int bid = xcd_remap(blockIdx.x, nmb * a.splits);       // a split's m-blocks (same B halo) share an L2
-  const int split = bid / nmb, mb = bid - split * nmb;
-  const int m0 = mb * 32;
+  const int nmb = a.M / 32, nnb = a.Nc / NC, per_split = nmb * nnb;   // nnb = 2: 64 B channels as two 32-column halves
+  const int bid = xcd_remap(blockIdx.x, per_split * a.splits);  // a split's blocks (same B halo) share an L2
+  const int split = bid / per_split, rb0 = bid - split * per_split, nb = rb0 / nmb, mb = rb0 - nb * nmb;
+  const int m0 = mb * 32, n0 = nb * NC;
   const int segs = a.Wg / SW, per_img = (a.Hg / SR) * segs;
   const int nst = a.N * per_img;
   const int sps = (int)(a.pix_per_split / (SR * SW));
@@ -466,7 +576,7 @@ __global__ __launch_bounds__(256) void wgrad3_f32_kernel(F32WgradArgs a) {
   // A micro-blocks (threads < 128): channels m0 + 4 qa, pixel quad pq (row pq / 8, chunk pq % 8)
   const bool has_a = tid < 128;
   const int qa = tid & 7, pq = (tid >> 3) & 15;
-  const bool do_bias = a.bslab != nullptr;
+  const bool do_bias = a.bslab != nullptr && nb == 0;
   f32x4v bsum = f32x4v{0.f, 0.f, 0.f, 0.f};
   f32x4v va[4], vb[LBI][6];
 
@@ -487,7 +597,7 @@ __global__ __launch_bounds__(256) void wgrad3_f32_kernel(F32WgradArgs a) {
         const int iw = w0 - 1 + 4 * j + e;
         vb[i][e] = f32x4v{0.f, 0.f, 0.f, 0.f};
         if (ih >= 0 && ih < a.HB && iw >= 0 && iw < a.WB)
-          vb[i][e] = *reinterpret_cast<const f32x4v*>(a.B + ((long)(n * a.HB + ih) * a.WB + iw) * a.ldb + 4 * nq);
+          vb[i][e] = *reinterpret_cast<const f32x4v*>(a.B + ((long)(n * a.HB + ih) * a.WB + iw) * a.ldb + n0 + 4 * nq);
       }
     }
   };
@@ -552,7 +662,7 @@ __global__ __launch_bounds__(256) void wgrad3_f32_kernel(F32WgradArgs a) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int m = m0 + mt * 16 + 4 * q + r, n = (nt0 + p) * 16 + l16;
-        a.slab[(((long)split * 9 + t) * a.M + m) * NC + n] = acc[p][t][r];
+        a.slab[(((long)split * 9 + t) * a.M + m) * a.Nc + n0 + n] = acc[p][t][r];
       }
   if (do_bias) {                             // 16 pixel quads x 32 channels
     float* red = reinterpret_cast<float*>(lds);
@@ -564,6 +674,80 @@ __global__ __launch_bounds__(256) void wgrad3_f32_kernel(F32WgradArgs a) {
       for (int k = 0; k < 16; ++k) sum += red[k * 32 + tid];
       a.bslab[(long)split * a.M + m0 + tid] = sum;
     }
+  }
+}
+
+// First-layer weight gradient (3x3 / s1 / p1, 4 input channels -- the 3-channel image padded --, 32 output
+// channels): 36 GEMM columns, so the 128-column tile of wgrad_f32_kernel is 72 % padding (0.57 ms at b16,
+// 512^2, 13 TF/s).  Here the MFMA columns are (tap, channel) pairs plus one column of ones (the bias
+// gradient), 3 n-tiles of 16, and both operands come straight from global memory: lane (q, l16) reads the
+// output-gradient channel l16 of pixel 4 ks + q (64 B per 16 lanes) and the input value of its column at
+// that pixel's tap position (L1 / L2 hits: the input is 16 B per pixel).  A wave walks 64-pixel row
+// segments of its block's range; the 4 waves' sums meet in LDS in a fixed order and the block writes one
+// slab row [9][32][4] (+ the bias row) for dpa_wgrad_reduce.
+__global__ __launch_bounds__(256) void wgrad_c4_f32_kernel(F32WgradArgs a) {
+  __shared__ float red[4][24][64];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, q = lane >> 4, l16 = lane & 15;
+  const int segs = a.Wg / 64, units = a.N * a.Hg * segs;
+  const int upb = (int)(a.pix_per_split / 64);
+  const int u0 = blockIdx.x * upb, u1 = u0 + upb < units ? u0 + upb : units;
+  // this lane's column of each n-tile: (tap offset, channel) or the ones column (36) or padding
+  int dh[3], dw[3], cc[3], kind[3];
+#pragma unroll
+  for (int nt = 0; nt < 3; ++nt) {
+    const int j = nt * 16 + l16, tap = j >> 2;
+    kind[nt] = j < 36 ? 0 : j == 36 ? 1 : 2;
+    dh[nt] = tap / 3 - 1;
+    dw[nt] = tap % 3 - 1;
+    cc[nt] = j & 3;
+  }
+  f32x4_t acc[2][3];
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < 3; ++nt) acc[mt][nt] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  for (int u = u0 + wid; u < u1; u += 4) {
+    const int n = u / (a.Hg * segs), rem = u - n * (a.Hg * segs), h = rem / segs, w0 = (rem - h * segs) * 64;
+    const float* Ar = a.A + ((long)(n * a.Hg + h) * a.Wg + w0) * a.lda;
+    float av[16][2], bv[16][3];
+#pragma unroll
+    for (int ks = 0; ks < 16; ++ks) {
+      const int w = w0 + 4 * ks + q;
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt) av[ks][mt] = Ar[(long)(4 * ks + q) * a.lda + mt * 16 + l16];
+#pragma unroll
+      for (int nt = 0; nt < 3; ++nt) {
+        const int ih = h + dh[nt], iw = w + dw[nt];
+        float v = kind[nt] == 1 ? 1.f : 0.f;
+        if (kind[nt] == 0 && ih >= 0 && ih < a.HB && iw >= 0 && iw < a.WB)
+          v = a.B[((long)(n * a.HB + ih) * a.WB + iw) * a.ldb + cc[nt]];
+        bv[ks][nt] = v;
+      }
+    }
+#pragma unroll
+    for (int ks = 0; ks < 16; ++ks)
+#pragma unroll
+      for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < 3; ++nt)
+          acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[ks][mt], bv[ks][nt], acc[mt][nt], 0, 0, 0);
+  }
+#pragma unroll
+  for (int mt = 0; mt < 2; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < 3; ++nt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) red[wid][(mt * 3 + nt) * 4 + r][lane] = acc[mt][nt][r];
+  __syncthreads();
+  // thread: lane L, 6 of the 24 (mt, nt, r) values; lane L of those holds rows 4 q + r, column l16
+  const int L = lane, qq = L >> 4, col = L & 15;
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    const int e = wid * 6 + i, mt = e / 12, nt = (e / 4) % 3, r = e & 3;
+    const float v = ((red[0][e][L] + red[1][e][L]) + red[2][e][L]) + red[3][e][L];
+    const int m = mt * 16 + 4 * qq + r, j = nt * 16 + col;
+    if (j < 36) a.slab[(((long)blockIdx.x * 9 + (j >> 2)) * 32 + m) * 4 + (j & 3)] = v;
+    else if (j == 36 && a.bslab) a.bslab[(long)blockIdx.x * 32 + m] = v;
   }
 }
 
@@ -775,6 +959,13 @@ DPA_API int dpa_igemm_f32(const F32ConvArgs* args, hipStream_t st) {
     return (int)hipErrorInvalidValue;
   const long M = (long)a.N * a.Ho * a.Wo;
   const bool k32 = a.Kpad % 32 == 0;
+  if (a.halo && a.mode == 0 && a.KH == 3 && a.KW == 3 && a.stride == 1 && a.pad == 1 && a.Hs == a.Ho &&
+      a.Ws == a.Wo && a.Ho % 8 == 0 && a.Wo % 32 == 0 && a.Cs % 32 == 0 && a.Kpad >= 9 * a.Cs &&
+      (a.Ngemm == 32 || (a.halo == 2 && a.Ngemm == 64))) {
+    const dim3 grid((unsigned)(M / 256 * (a.Ngemm / 32)));
+    hipLaunchKernelGGL(conv3_halo_f32_kernel, grid, dim3(256), 0, st, a);
+    return (int)hipGetLastError();
+  }
   if (k32 && a.mode == 0 && ((a.Ngemm == 64 && a.Cs <= 64) || (a.Ngemm == 32 && a.Cs == 32))) {
     // narrow GEMM-N over few input channels: 256-pixel tiles, 16-deep K-steps (36-40 KB LDS)
     const dim3 grid((unsigned)((M + 255) / 256));
@@ -819,12 +1010,22 @@ DPA_API int dpa_wgrad_f32(const F32WgradArgs* args, hipStream_t st) {
       a.splits < 1 || (long)a.splits * a.pix_per_split < P || (long)(a.splits - 1) * a.pix_per_split >= P ||
       a.KH * a.KW < 1 || P >= (1L << 31))
     return (int)hipErrorInvalidValue;
+  if (a.halo == 3) {      // first layer: 4 input channels, 32 outputs, 64-pixel row segments per split unit
+    if (a.KH != 3 || a.KW != 3 || a.s != 1 || a.pad != 1 || a.HB != a.Hg || a.WB != a.Wg || a.Nc != 4 || a.M != 32 ||
+        (a.Wg % 64) || (a.pix_per_split % 64))
+      return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL(wgrad_c4_f32_kernel, dim3((unsigned)a.splits), dim3(256), 0, st, a);
+    return (int)hipGetLastError();
+  }
   if (a.halo) {
     if (a.KH != 3 || a.KW != 3 || a.s != 1 || a.pad != 1 || a.HB != a.Hg || a.WB != a.Wg || (a.Hg & 1) ||
         (a.Wg % 32) || (a.pix_per_split % 64) || (a.Nc != 32 && a.Nc != 64))
       return (int)hipErrorInvalidValue;
-    const dim3 grid((unsigned)((a.M / 32) * a.splits));
-    if (a.Nc == 32) hipLaunchKernelGGL(wgrad3_f32_kernel<32>, grid, dim3(256), 0, st, a);
+    // halo == 2 with 64 columns: the 32-column kernel over each half (56 KB of LDS, 2 blocks per CU, vs one
+    // 104 KB block of the 64-column form)
+    const bool halves = a.Nc == 64 && a.halo == 2;
+    const dim3 grid((unsigned)((a.M / 32) * (halves ? 2 : 1) * a.splits));
+    if (a.Nc == 32 || halves) hipLaunchKernelGGL(wgrad3_f32_kernel<32>, grid, dim3(256), 0, st, a);
     else hipLaunchKernelGGL(wgrad3_f32_kernel<64>, grid, dim3(256), 0, st, a);
     return (int)hipGetLastError();
   }

@@ -68,6 +68,15 @@ KNOBS = (
     Knob("f32_wgrad_px", "DPA_NO_F32_WGRAD_PX", True, "fp32 engine: weight-gradient operands staged pixel-major "
          "(no loader transpose; ds_read_b32 operand columns) -- same result bit for bit, 19.9 vs 20.2 ms of "
          "weight gradients at b16 512^2 (profiles/f32_kbench_b16_512_r05_px.txt)"),
+    Knob("f32_wgrad3_halves", "DPA_NO_F32_WGRAD3_HALVES", True, "fp32 engine: the halo weight gradient over 64 input "
+         "channels as two 32-column blocks (56 KB, 2 blocks per CU) instead of one 104 KB 64-column block: 0.88 vs "
+         "1.16 ms at enc1.c2, 312 -> 321 img/s at b16 (profiles/f32_kbench_b16_512_r05_halves.txt)"),
+    Knob("f32_wgrad_c4", "DPA_NO_F32_WGRAD_C4", True, "fp32 engine: the first conv's weight gradient (4 padded input "
+         "channels, 32 outputs) with 48 MFMA columns straight from global memory instead of a 128-column tile "
+         "(0.27 vs 0.58 ms at b16 512^2, profiles/f32_kbench_b16_512_r05_halo.txt)"),
+    Knob("f32_conv_halo", "DPA_F32_CONV_HALO", 2, "fp32 engine: 3x3 conv / dgrad with GEMM-N 32 (1; 2: also 64; 0: off) "
+         "over 32-channel input slices staged once per 8 x 32 output pixels with the halo (csrc/fp32.hip "
+         "conv3_halo_f32_kernel) instead of per tap: enc0.c2 forward 0.89 vs 1.07 ms, dec3.c1 1.42 vs 1.71 ms"),
     # launch geometry / streams
     Knob("side_priority", "DPA_SIDE_PRIORITY", 0, "HIP priority of the weight-gradient side stream (torch convention)"),
     Knob("wgrad_stream_blocks", "DPA_WGRAD_STREAM_BLOCKS", 2048, "target workgroups of a row-streaming weight gradient"),
@@ -134,6 +143,9 @@ class KernelConfig:
     f32_wgrad_big: bool = True
     f32_igemm_wide: bool = True
     f32_wgrad_px: bool = True
+    f32_wgrad3_halves: bool = True
+    f32_conv_halo: int = 2
+    f32_wgrad_c4: bool = True
     side_priority: int = 0
     wgrad_stream_blocks: int = 2048
     wgrad_gemm_blocks: int = 768

@@ -23,13 +23,16 @@ _MAX = 2 ** 31 - 1024          # per-launch element-offset range the host keeps 
 class F32ConvArgs(ctypes.Structure):
     _fields_ = [("x", c_void_p), ("w", c_void_p), ("bias", c_void_p), ("y", c_void_p), ("mask", c_void_p)] + \
                [(n, c_int) for n in ("ldx", "ldy", "ldm", "mask_ch", "N", "Ho", "Wo", "Hs", "Ws", "Cs", "KH", "KW",
-                                     "stride", "pad", "Ngemm", "Kpad", "mode", "relu", "accumulate", "Cout", "wide")]
+                                     "stride", "pad", "Ngemm", "Kpad", "mode", "relu", "accumulate", "Cout", "wide", "halo")]
 
 
 USE_WGRAD_HALO = _config.KernelConfig.from_env().f32_wgrad_halo   # 3x3 weight gradients with the input halo staged
 USE_WGRAD_BIG = _config.KernelConfig.from_env().f32_wgrad_big     # 256 x 256 8-wave weight-gradient tiles (deep layers)
 IGEMM_WIDE = _config.KernelConfig.from_env().f32_igemm_wide      # 256-pixel 8-wave conv / dgrad tiles for GEMM-N % 128 == 0
 WGRAD_PX = _config.KernelConfig.from_env().f32_wgrad_px          # pixel-major LDS weight-gradient operands
+WGRAD3_HALVES = _config.KernelConfig.from_env().f32_wgrad3_halves  # 64-input-channel halo weight gradients as 2 x 32
+WGRAD_C4 = _config.KernelConfig.from_env().f32_wgrad_c4          # first layer's weight gradient: 4-channel form
+CONV_HALO = _config.KernelConfig.from_env().f32_conv_halo         # 3x3 convs with GEMM-N 32 (1) / also 64 (2): halo-staged
 
 
 def wgrad_f32_tile(M: int, Ncols: int, big: bool):
@@ -148,7 +151,8 @@ def igemm(x: torch.Tensor, wp: torch.Tensor, y: torch.Tensor, *, Ngemm: int, Kpa
         n1 = min(N, n0 + step)
         a = F32ConvArgs(x[n0:n1].data_ptr(), wp.data_ptr(), None if bias is None else bias.data_ptr(), y[n0:n1].data_ptr(),
                         None if mask is None else mask[n0:n1].data_ptr(), ldx, ldy, ldm, mask_ch, n1 - n0, Ho, Wo, Hs, Ws,
-                        Cs, KH, KW, stride, pad, Ngemm, Kpad, mode, int(relu), int(accumulate), Cout, int(IGEMM_WIDE))
+                        Cs, KH, KW, stride, pad, Ngemm, Kpad, mode, int(relu), int(accumulate), Cout, int(IGEMM_WIDE),
+                        CONV_HALO)
         _check(L.dpa_igemm_f32(ctypes.byref(a), st), "igemm_f32")
     return y
 
@@ -176,9 +180,18 @@ def wgrad(A: torch.Tensor, B: torch.Tensor, gw: torch.Tensor, gb: Optional[torch
     P = N * Hg * Wg
     halo = int(USE_WGRAD_HALO and (KH, KW, s, pad) == (3, 3, 1, 1) and (HB, WB) == (Hg, Wg) and Hg % 2 == 0
                and Wg % 32 == 0 and Nc in (32, 64))
-    if halo:       # stages of 2 rows x 32 pixels, all 9 taps of 32 A channels per block
+    if (WGRAD_C4 and (KH, KW, s, pad) == (3, 3, 1, 1) and (HB, WB) == (Hg, Wg) and Nc == 4 and M == 32
+            and Wg % 64 == 0):
+        halo = 3   # first layer: 64-pixel row segments, <= 512 blocks (splits)
+        units = N * Hg * (Wg // 64)
+        upb = -(-units // min(512, units))
+        splits = -(-units // upb)
+        pps = 64 * upb
+    elif halo:     # stages of 2 rows x 32 pixels, all 9 taps of 32 A channels per block
+        if Nc == 64 and WGRAD3_HALVES:
+            halo = 2   # each block: one 32-column half of B
         nst = N * (Hg // 2) * (Wg // 32)
-        splits = max(1, min(nst, -(-target_blocks // (M // 32))))
+        splits = max(1, min(nst, -(-target_blocks // ((M // 32) * halo))))
         sps = -(-nst // splits)
         splits = -(-nst // sps)
         pps = 64 * sps

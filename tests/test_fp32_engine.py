@@ -88,6 +88,41 @@ def test_conv_relu_fwd_bwd(hip_lib, N, H, W, Cin, Cout, cs):
     assert _rel(gx[..., :Cin].permute(0, 3, 1, 2), gx_ref) < 1e-5
 
 
+@pytest.mark.parametrize("N,H,W,Cin,Cout", [(2, 16, 64, 32, 32), (1, 8, 32, 64, 32), (2, 8, 32, 32, 64),
+                                           (1, 16, 32, 64, 64), (1, 8, 64, 96, 64)])
+def test_conv_halo_form(hip_lib, N, H, W, Cin, Cout):
+    """3x3 conv forward and input gradient through the halo-staged narrow kernel (conv3_halo_f32_kernel:
+    GEMM-N 32, or 64 with DPA_F32_CONV_HALO=2; 32-channel input slices) against torch fp32, and against
+    the per-tap implicit GEMM."""
+    from distributedpytorch_amd.models.hip_unet_f32 import _ConvReLU, _L
+    from distributedpytorch_amd.ops import fp32 as F32
+    torch.manual_seed(Cin * Cout + W)
+    xr = torch.randn(N, Cin, H, W, device="cuda")
+    w = torch.randn(Cout, Cin, 3, 3, device="cuda") / (9 * Cin) ** 0.5
+    b = torch.randn(Cout, device="cuda") * 0.1
+    ref_x = xr.clone().requires_grad_(True)
+    ref = torch.relu(F.conv2d(ref_x, w, b, padding=1))
+    g = torch.randn_like(ref)
+    (gx_ref,) = torch.autograd.grad(ref, (ref_x,), g)
+    outs = []
+    old = F32.CONV_HALO
+    try:
+        for mode in (0, 2):
+            F32.CONV_HALO = mode
+            xn = xr.permute(0, 2, 3, 1).contiguous().requires_grad_(True)
+            m = _conv(w, b)
+            layer = _L(m, "conv", Cin)
+            eng = _engine(layer)
+            y = _ConvReLU.apply(eng.anchor, xn, eng, layer)
+            (gx,) = torch.autograd.grad(y, (xn,), g.permute(0, 2, 3, 1).contiguous())
+            assert _rel(y.permute(0, 3, 1, 2), ref) < 1e-5, mode
+            assert _rel(gx.permute(0, 3, 1, 2), gx_ref) < 1e-5, mode
+            outs.append(y)
+    finally:
+        F32.CONV_HALO = old
+    assert _rel(outs[1], outs[0]) < 1e-5
+
+
 @pytest.mark.parametrize("N,h,w,Cin,Cout,C", [(2, 8, 12, 64, 32, 32), (1, 4, 4, 512, 256, 256)])
 def test_up_cat(hip_lib, N, h, w, Cin, Cout, C):
     """[skip ‖ ConvTranspose2d(x)] in one buffer (deconv epilogue into the upper half) vs torch, forward and
@@ -139,8 +174,9 @@ def test_enc_out_bwd(hip_lib, N, H, W, C, strided):
 
 @pytest.mark.parametrize("N,H,W,Nc,M", [(2, 8, 64, 32, 32), (1, 6, 32, 64, 96), (3, 2, 96, 64, 64), (1, 4, 32, 32, 64)])
 def test_wgrad_halo_form(hip_lib, N, H, W, Nc, M):
-    """3x3 weight gradient with the input halo staged per 2 x 32-pixel patch (wgrad3_f32_kernel) and the
-    generic tap-column form, both vs torch fp32 (weight and bias gradient)."""
+    """3x3 weight gradient with the input halo staged per 2 x 32-pixel patch (wgrad3_f32_kernel; 64 input
+    channels also as two 32-column halves) and the generic tap-column form, all vs torch fp32 (weight and
+    bias gradient)."""
     from distributedpytorch_amd.ops import fp32 as F32
     torch.manual_seed(Nc + M + H)
     x = torch.randn(N, Nc, H, W, device="cuda")
@@ -148,16 +184,40 @@ def test_wgrad_halo_form(hip_lib, N, H, W, Nc, M):
     gw_ref = torch.nn.grad.conv2d_weight(x, (M, Nc, 3, 3), g, padding=1)
     gb_ref = g.sum((0, 2, 3))
     A, B = g.permute(0, 2, 3, 1).contiguous(), x.permute(0, 2, 3, 1).contiguous()
-    old = F32.USE_WGRAD_HALO
+    old = (F32.USE_WGRAD_HALO, F32.WGRAD3_HALVES)
     try:
-        for halo in (True, False):
-            F32.USE_WGRAD_HALO = halo
+        for halo, halves in ((True, False), (True, True), (False, False)):
+            F32.USE_WGRAD_HALO, F32.WGRAD3_HALVES = halo, halves
             gw = torch.zeros(M, Nc, 3, 3, device="cuda")
             gb = torch.zeros(M, device="cuda")
             F32.wgrad(A, B, gw, gb, KH=3, KW=3, s=1, pad=1)
-            assert _rel(gw, gw_ref) < 1e-5 and _rel(gb, gb_ref) < 1e-5, halo
+            assert _rel(gw, gw_ref) < 1e-5 and _rel(gb, gb_ref) < 1e-5, (halo, halves)
     finally:
-        F32.USE_WGRAD_HALO = old
+        F32.USE_WGRAD_HALO, F32.WGRAD3_HALVES = old
+
+
+@pytest.mark.parametrize("N,H,W", [(2, 6, 64), (1, 4, 128), (3, 5, 192)])
+def test_wgrad_first_layer_form(hip_lib, N, H, W):
+    """The first conv's weight gradient (3 image channels padded to 4, 32 outputs) through the 4-channel
+    form (wgrad_c4_f32_kernel: (tap, channel) MFMA columns plus a ones column for the bias) and through
+    the generic tile, vs torch fp32; the padding channel's gradient is dropped."""
+    from distributedpytorch_amd.ops import fp32 as F32
+    torch.manual_seed(N * H + W)
+    x4 = torch.randn(N, 4, H, W, device="cuda")
+    g = torch.randn(N, 32, H, W, device="cuda")
+    gw_ref = torch.nn.grad.conv2d_weight(x4[:, :3], (32, 3, 3, 3), g, padding=1)
+    gb_ref = g.sum((0, 2, 3))
+    A, B = g.permute(0, 2, 3, 1).contiguous(), x4.permute(0, 2, 3, 1).contiguous()
+    old = F32.WGRAD_C4
+    try:
+        for c4 in (True, False):
+            F32.WGRAD_C4 = c4
+            gw = torch.zeros(32, 3, 3, 3, device="cuda")
+            gb = torch.zeros(32, device="cuda")
+            F32.wgrad(A, B, gw, gb, KH=3, KW=3, s=1, pad=1, nreal=3)
+            assert _rel(gw, gw_ref) < 1e-5 and _rel(gb, gb_ref) < 1e-5, c4
+    finally:
+        F32.WGRAD_C4 = old
 
 
 @pytest.mark.parametrize("N,H,W,Nc,M", [(2, 8, 16, 256, 256), (1, 8, 8, 512, 256), (3, 4, 4, 512, 256),

@@ -14,18 +14,28 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
+def _modes(opt, current):
+    return {"default": [current], "off": [False], "on": [True], "both": [False, True]}[opt]
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=16)
     ap.add_argument("--img", type=int, default=512)
     ap.add_argument("--model", default="unet")
     ap.add_argument("--reps", type=int, default=5)
-    ap.add_argument("--wgrad-big", choices=["off", "on", "both"], default="off",
+    ap.add_argument("--wgrad-big", choices=["default", "off", "on", "both"], default="default",
                     help="time the conv weight gradients with the 256 x 256 tile too (deep layers)")
-    ap.add_argument("--igemm-wide", choices=["off", "on", "both"], default="off",
+    ap.add_argument("--igemm-wide", choices=["default", "off", "on", "both"], default="default",
                     help="time the conv forward / dgrad with the 256-pixel 8-wave tile too")
-    ap.add_argument("--wgrad-px", choices=["off", "on", "both"], default="off",
+    ap.add_argument("--wgrad-px", choices=["default", "off", "on", "both"], default="default",
                     help="time the generic weight gradients with the pixel-major LDS form too")
+    ap.add_argument("--conv-halo", default="default",
+                    help="comma list of DPA_F32_CONV_HALO modes to time the conv forward / dgrad with (last printed first)")
+    ap.add_argument("--wgrad-c4", choices=["default", "off", "on", "both"], default="default",
+                    help="time the first conv's weight gradient with the 4-channel form too")
+    ap.add_argument("--wgrad3-halves", choices=["default", "off", "on", "both"], default="default",
+                    help="time the 64-input-channel halo weight gradients as two 32-column halves too")
     a = ap.parse_args()
     from distributedpytorch_amd.models import hip_unet_f32 as E
     from distributedpytorch_amd.models.unet import build_model
@@ -73,21 +83,29 @@ def main():
         eng.ensure_packed()
         ge = torch.randn(N, hh, hh, co, device=dev)
         fl = 2.0 * N * hh * hh * co * ci * 9
-        wmodes = {"off": [False], "on": [True], "both": [False, True]}[a.igemm_wide]
+        wmodes = _modes(a.igemm_wide, F32.IGEMM_WIDE)
+        hmodes = [F32.CONV_HALO] if a.conv_halo == "default" else [int(v) for v in a.conv_halo.split(",")]
+        if len(hmodes) > 1:
+            wmodes = [F32.IGEMM_WIDE] * len(hmodes)
         tfs, tds = [], []
-        for wide in wmodes:
+        for k, wide in enumerate(wmodes):
             F32.IGEMM_WIDE = wide
+            F32.CONV_HALO = hmodes[min(k, len(hmodes) - 1)]
             tfs.append(t(lambda: E._conv_fwd(eng, layer, x)))
             tds.append(t(lambda: E._conv_dgrad(eng, layer, ge)) if ci != 3 else 0.0)
         tf, td = tfs[-1], tds[-1]
-        modes = {"off": [False], "on": [True], "both": [False, True]}[a.wgrad_big]
-        pxm = {"off": [False], "on": [True], "both": [False, True]}[a.wgrad_px]
-        if len(pxm) > 1:
+        modes = _modes(a.wgrad_big, F32.USE_WGRAD_BIG)
+        pxm = _modes(a.wgrad_px, F32.WGRAD_PX)
+        hvm = _modes(a.wgrad3_halves, F32.WGRAD3_HALVES)
+        c4m = _modes(a.wgrad_c4, F32.WGRAD_C4)
+        if len(pxm) > 1 or len(hvm) > 1 or len(c4m) > 1:
             modes = [F32.USE_WGRAD_BIG] * 2
         tws = []
         for k, big in enumerate(modes):
             F32.USE_WGRAD_BIG = big
             F32.WGRAD_PX = pxm[min(k, len(pxm) - 1)]
+            F32.WGRAD3_HALVES = hvm[min(k, len(hvm) - 1)]
+            F32.WGRAD_C4 = c4m[min(k, len(c4m) - 1)]
             tws.append(t(lambda: E._conv_wgrad(eng, layer, ge, x)))
         tw = tws[-1]
         tot["fwd"] += tf
@@ -95,7 +113,7 @@ def main():
         tot["wgrad"] += tw
         extra = "" if len(tws) == 1 else f" (other form: {tws[0]:7.3f} {fl / tws[0] / 1e9:6.1f})"
         if len(tfs) > 1:
-            extra += f" [4-wave fwd {tfs[0]:7.3f} dgrad {tds[0]:7.3f}]"
+            extra += f" [other fwd {tfs[0]:7.3f} dgrad {tds[0]:7.3f}]"
         print(f"{name:10s} {hh:4d}x{hh:<4d} {ci:4d} {co:4d} | {tf:7.3f} {fl / tf / 1e9:6.1f} | {td:7.3f} "
               f"{(fl / td / 1e9 if td else 0):6.1f} | {tw:7.3f} {fl / tw / 1e9:6.1f}{extra}", flush=True)
         del x, ge
