@@ -37,6 +37,17 @@ def main():
         busy = sum((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3 for r in step)
         print(f"last step: wall {wall:.1f} us, kernels busy {busy:.1f} us ({100 * busy / wall:.1f}%), "
               f"{len(step)} dispatches")
+        # the GPU idle time: wall not covered by any kernel (launch gaps, host syncs), and the largest gaps
+        ivs = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in step)
+        cov, gaps, end = 0, [], ivs[0][0]
+        for s0, e0 in ivs:
+            if s0 > end:
+                gaps.append(((s0 - end) / 1e3, (end - t0) / 1e3))
+            cov += max(0, e0 - max(s0, end))
+            end = max(end, e0)
+        idle = sum(g for g, _ in gaps)
+        print(f"idle (no kernel running): {idle:.1f} us ({100 * idle / wall:.1f}% of the step) in {len(gaps)} gaps; "
+              "largest: " + ", ".join(f"{g:.0f} us at {t:.0f}" for g, t in sorted(gaps, reverse=True)[:5]))
         if a.timeline:
             for r in step:
                 d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
