@@ -118,10 +118,14 @@ def main():
     device = torch.device(f"cuda:{local}")
     if world > 1:
         backend = os.environ.get("DPA_DIST_BACKEND", "nccl")
+        # a collective that never completes (a rank lost, a link down) errors out after 10 minutes
+        # instead of hanging the job; no step of this bench legitimately waits that long
+        import datetime
+        tmo = datetime.timedelta(seconds=600)
         if backend == "nccl":
-            dist.init_process_group("nccl", init_method="env://", device_id=device)
+            dist.init_process_group("nccl", init_method="env://", device_id=device, timeout=tmo)
         else:
-            dist.init_process_group(backend, init_method="env://")
+            dist.init_process_group(backend, init_method="env://", timeout=tmo)
 
     from distributedpytorch_amd.config import TrainConfig
     from distributedpytorch_amd.data.synthetic import synthetic_batch
