@@ -145,8 +145,12 @@ def _extent_bytes(N, H, W, C, ld):
 
 
 def _image_chunks(N: int, per_image_bytes: int):
-    """Split a batch so every launch addresses < 2 GiB per tensor (buffer-descriptor range)."""
+    """Split a batch so every launch addresses < 2 GiB per tensor (buffer-descriptor range), in equal
+    chunks: 255 + 1 images would leave a one-image launch that cannot fill the chip (~35 us for ~5 us
+    of work, several per step at b256)."""
     per = max(1, _MAX_BYTES // max(per_image_bytes, 1))
+    n = -(-N // per)
+    per = -(-N // n)
     return [(i, min(N, i + per)) for i in range(0, N, per)]
 
 
