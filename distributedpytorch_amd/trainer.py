@@ -766,9 +766,10 @@ def evaluate(strat: Strategy, val_loader, cfg: Optional[TrainConfig] = None):
         t = tot.to(strat.device) if strat.device.type == "cuda" else tot
         tot = strat.reduce_eval(t).cpu()
     elif strat.name == "MP" and isinstance(strat, PipelineDistStrategy):
-        # the last stage holds the outputs; share the result with every stage
+        # the head stage holds the outputs (the last stage for a contiguous placement, stage 0 for a
+        # mirrored one); share the result with every stage
         t = tot.to(strat.device) if strat.device.type == "cuda" else tot
-        dist.broadcast(t, src=strat.world - 1)
+        dist.broadcast(t, src=strat.pipe.head_rank)
         tot = t.cpu()
     if tot[2] == 0:
         return float("nan"), float("nan")

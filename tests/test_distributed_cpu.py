@@ -309,3 +309,57 @@ def test_ddp_trainer_eight_ranks(tmp_path):
     assert sd and all(k.startswith("module.") for k in sd)
     assert set(k[len("module."):] for k in sd) == set(build_model("unet-tiny").state_dict())
     assert (tmp_path / "loss" / "DDP" / "train_loss.pkl").exists() and (tmp_path / "loss" / "DDP" / "val_loss.pkl").exists()
+
+
+def _mp_train_worker(rank, world, port, out, cut, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    try:
+        from distributedpytorch_amd.config import parse_args
+        from distributedpytorch_amd.trainer import train
+        args = ["--synthetic", "--synthetic-len", "16", "-v", "25", "--img-size", "32", "--model", "unet-tiny",
+                "--backend", "torch", "--dtype", "fp32", "-b", "4", "--log-every", "1", "--lr", "1e-3", "-t", "MP",
+                "-e", "2", "--mp-cut", cut, "--out-dir", out]
+        r = train(parse_args(args))
+        st = r["strategy"]
+        lr = torch.tensor([st.optimizer.param_groups[0]["lr"]])
+        lrs = [torch.zeros_like(lr) for _ in range(world)]
+        dist.all_gather(lrs, lr)
+        q.put((rank, r["step"], str(st.pipe.pl), st.pipe.head_rank, [float(v) for v in lrs], None))
+    except Exception as e:
+        import traceback
+        q.put((rank, -1, None, None, None, repr(e) + traceback.format_exc()[-1500:]))
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("cut", ["v", "reference"])
+def test_mp_trainer_two_ranks(tmp_path, cut):
+    """The whole -t MP training loop at world 2 on gloo, for the mirrored (V) placement -- head and loss
+    on stage 0 -- and the reference encoder|decoder cut (head on the last stage): finite validation loss
+    shared with every stage (the broadcast comes from the head stage), the plateau LR identical on both
+    ranks, the gathered checkpoint with every reference key written once by rank 0."""
+    import pickle  # noqa: F401  (the loss pickles are only checked for existence)
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_mp_train_worker, args=(r, world, port, str(tmp_path), cut, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=400) for _ in procs], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+    errs = [(r[0], r[-1]) for r in res if r[-1] is not None]
+    assert not errs, errs
+    assert res[0][3] == (0 if cut == "v" else 1), res[0][2]
+    for rank, steps, _, _, lrs, _ in res:
+        assert steps > 0 and len(set(lrs)) == 1, (rank, lrs)
+    sd = torch.load(tmp_path / "checkpoints" / "MP.pth", map_location="cpu", weights_only=True)
+    assert set(sd) == set(build_model("unet-tiny").state_dict())
+    import json
+    rows = [json.loads(l) for l in open(tmp_path / "logs" / "MP.jsonl")]
+    vals = [r["val_loss"] for r in rows if "val_loss" in r]
+    assert vals and all(v == v and abs(v) < 1e3 for v in vals), vals
