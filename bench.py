@@ -70,6 +70,9 @@ def parse():
                     help="mp microbatches (0: the pipeline plan's count for this model / image / stages / batch, "
                          "parallel/plans.json; without one 2 for the reference cut, 8 otherwise)")
     ap.add_argument("--stages", type=int, default=2, help="mp with one process: stages on the local device")
+    ap.add_argument("--mp-replicas", type=int, default=1,
+                    help="mp over N ranks: R pipelines of N/R stages, data-parallel across them (each pipeline "
+                         "trains its own --batch images)")
     ap.add_argument("--mp-cut", choices=["auto", "reference", "balanced", "v", "time"], default="auto",
                     help="mp stage placement (auto: the link-aware plan from measured block times when "
                          "parallel/plans.json has one for this configuration, else the skip-local mirrored "
@@ -146,11 +149,11 @@ def main():
     cfg = TrainConfig(train_method=method, batch_size=a.batch, img_size=a.img, dtype=a.dtype,
                       backend=a.backend, model=a.model, bucket_mb=a.bucket_mb, lr=1e-4,
                       grad_comm_dtype=a.grad_comm_dtype, comm_overlap=a.comm_overlap,
-                      microbatches=a.microbatches, stages=a.stages, mp_cut=a.mp_cut)
+                      microbatches=a.microbatches, stages=a.stages, mp_cut=a.mp_cut, mp_replicas=a.mp_replicas)
     mp_info = None
     if mp:
         from distributedpytorch_amd.config import mp_plan
-        mpp = mp_plan(cfg, world if world > 1 else a.stages)
+        mpp = mp_plan(cfg, world // max(1, a.mp_replicas) if world > 1 else a.stages)
         mp_info = {"cut_mode": mpp.mode, "placement": str(mpp.placement), "microbatches": mpp.microbatches,
                    "policy": mpp.policy, **mpp.info}
     model = build_model(a.model)
@@ -226,8 +229,11 @@ def main():
         loss = lt
     final_loss = float(loss.item()) if loss is not None else float("nan")
 
-    # dp: every rank trains its own --batch images (weak scaling); mp: the N ranks share one batch
-    imgs = a.batch * (1 if mp else world) * a.steps
+    # dp: every rank trains its own --batch images (weak scaling); mp: the ranks of a pipeline share one
+    # batch, each of the --mp-replicas pipelines trains its own
+    R = max(1, a.mp_replicas) if mp and world > 1 else 1
+    S = world // R if mp and world > 1 else (a.stages if mp else 1)
+    imgs = a.batch * (R if mp else world) * a.steps
     value = imgs / elapsed
     ms = 1000.0 * elapsed / a.steps
     # vs_baseline: like for like only, i.e. null unless stock PyTorch-ROCm was measured at THIS per-GPU
@@ -235,19 +241,19 @@ def main():
     # 1080 s, so there is no like-for-like number).  The batch-32 equal-batch ratio and this run's
     # quotient over stock-at-32 stay in vs_baseline_basis as context.
     vs = cross = None
-    per_gpu_batch = a.batch if not mp else a.batch // max(1, world)
+    per_gpu_batch = a.batch if not mp else a.batch // max(1, S)
     if STOCK_BASELINE_PER_GPU and not a.infer and a.dtype == "bf16":
         cross = round(value / (STOCK_BASELINE_PER_GPU * world), 4)
         if per_gpu_batch == STOCK_BASELINE_BATCH and not mp and a.img == (512, 512) and a.model == "unet":
             vs = cross
     if mp:
-        par = f"mp{world if world > 1 else a.stages}x{strat.pipe.M}mb" + ("" if world > 1 else "-1gpu")
+        par = f"mp{S}x{strat.pipe.M}mb" + ("" if world > 1 else "-1gpu") + (f"-dp{R}" if R > 1 else "")
     else:
         par = f"dp{world}"
     out = {
         "metric": BASELINE_METRIC if not a.infer else "images/sec inference UNet 512x512 bf16 (eval forward)", "value": round(value, 2), "unit": "images/s", "n_gpus": world,
         "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
-        "scaling": "strong" if mp else "weak", "vs_baseline": vs,
+        "scaling": "strong" if (mp and R == 1) else "weak", "vs_baseline": vs,
         # context only: stock PyTorch-ROCm (MIOpen, bf16 autocast) was measured at batch 32; the
         # equal-batch ratio there and this run over stock-at-32 (cross_batch_ratio, different batches
         # unless --batch 32)
@@ -260,8 +266,8 @@ def main():
         "dtype": a.dtype,
         "data": "synthetic (GPU-generated images + ellipse masks), random-init weights",
         "config": {"model": f"{a.model} (reference 4-level UNet, base 32, {nparams} params)" if a.model == "unet"
-                   else a.model, "global_batch": a.batch * (1 if mp else world),
-                   "per_gpu_batch": a.batch if not mp else a.batch // max(1, world),
+                   else a.model, "global_batch": a.batch * (R if mp else world),
+                   "per_gpu_batch": per_gpu_batch,
                    "seq_len": a.img[0] * a.img[1], "image_hw": list(a.img),
                    "parallelism": par, "backend": backend,
                    "mp_cut": (str(strat.pipe.pl) if mp else None), "mp_plan": mp_info, "bucket_mb": a.bucket_mb,

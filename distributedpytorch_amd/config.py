@@ -43,6 +43,7 @@ class TrainConfig:
     stages: int = 2                                  # pipeline stages for -t MP
     microbatches: int = 0                            # 0: the measured plan's count, else 2 (reference split_size=B/2)
     mp_cut: str = "auto"                             # MP placement: reference | balanced | v | time | auto (mp_plan)
+    mp_replicas: int = 1                             # MP: R pipelines of world/R stages, data-parallel across them
     bucket_mb: float = 8.0                           # DDP/DP all-reduce bucket size (MiB of fp32 grads)
     grad_comm_dtype: str = "fp32"                    # DDP gradient all-reduce wire dtype: fp32 | bf16
     comm_overlap: bool = True                        # DDP/DP: launch gradient buckets during the backward
@@ -104,6 +105,9 @@ def build_parser() -> argparse.ArgumentParser:
                         "the cut); balanced = FLOP-balanced contiguous blocks; v = mirrored, skip-local (stage s "
                         "owns encoder level s and decoder level s); time = the measured-time plan in "
                         "parallel/plans.json; auto = time when planned, else v")
+    p.add_argument("--mp-replicas", type=int, default=1,
+                   help="-t MP over N ranks: R pipelines of N/R stages each (ranks r*N/R .. (r+1)*N/R - 1), every "
+                        "pipeline on its own data shard, stage gradients averaged across the R pipelines")
     p.add_argument("--bucket-mb", type=float, default=8.0)
     p.add_argument("--grad-comm-dtype", choices=["fp32", "bf16"], default="fp32",
                    help="DDP: all-reduce gradient buckets in bf16 (half the bytes) instead of fp32")
@@ -143,7 +147,8 @@ def parse_args(argv=None) -> TrainConfig:
         batch_size=a.batch_size, checkpoint=a.checkpoint, seed=a.seed, img_size=img_size,
         dtype=a.dtype, backend=a.backend, model=a.model, synthetic=a.synthetic,
         synthetic_len=a.synthetic_len, device_data=a.device_data, data_dir=a.data_dir, out_dir=a.out_dir, device=a.device,
-        stages=a.stages, microbatches=a.microbatches, mp_cut=a.mp_cut, bucket_mb=a.bucket_mb, grad_comm_dtype=a.grad_comm_dtype,
+        stages=a.stages, microbatches=a.microbatches, mp_cut=a.mp_cut, mp_replicas=a.mp_replicas, bucket_mb=a.bucket_mb,
+        grad_comm_dtype=a.grad_comm_dtype,
         comm_overlap=a.comm_overlap, global_dice=a.global_dice,
         loss_scale_by_batch=a.loss_scale_by_batch, max_steps=a.max_steps, num_workers=a.num_workers,
         log_every=a.log_every, resume=a.resume, profile=a.profile, trace_ranges=a.trace_ranges, cuda_graph=a.cuda_graph,

@@ -289,17 +289,41 @@ class PipelineDistStrategy(Strategy):
         self.device = torch.device(device)
         self.model = model.to(self.device)
         H, W = cfg.img_size
-        self.plan = mp_plan(cfg, self.world)
+        # R pipelines of S stages (--mp-replicas): pipeline r = ranks r*S .. r*S + S - 1, stage s of every
+        # pipeline in one data-parallel group; R = 1 is the plain pipeline over the whole job
+        R = max(1, int(cfg.mp_replicas or 1))
+        if self.world % R:
+            raise ValueError(f"--mp-replicas {R} does not divide the {self.world} ranks")
+        S = self.world // R
+        self.replicas, self.stages = R, S
+        self.replica, self.stage = divmod(self.rank, S)
+        pipe_group = self.dp_group = None
+        if R > 1:   # every rank creates every group, in the same order
+            pgs = [dist.new_group(list(range(r * S, (r + 1) * S))) for r in range(R)]
+            dgs = [dist.new_group([s + k * S for k in range(R)]) for s in range(S)]
+            pipe_group, self.dp_group = pgs[self.replica], dgs[self.stage]
+        self.plan = mp_plan(cfg, S)
         self.pipe = GPipeDist(self.model, self.plan.microbatches, cfg.backend, cfg.dtype, img_hw=(H, W),
-                              placement=self.plan.placement, policy=self.plan.policy, orders=self.plan.orders)
-        self.is_main = self.pipe.is_last  # the head stage owns the loss; rank 0 saves
+                              placement=self.plan.placement, policy=self.plan.policy, orders=self.plan.orders,
+                              group=pipe_group)
+        # the head stage owns the loss (pipeline 0's logs); rank 0 saves
+        self.is_main = self.pipe.is_last and self.replica == 0
         self.optimizer = FusedAdam(self.pipe.space, lr=cfg.lr, weight_decay=cfg.weight_decay)
+        if R > 1:   # every pipeline starts from pipeline 0's parameters (stage s: global rank s)
+            dist.broadcast(self.pipe.space.data, src=self.stage, group=self.dp_group)
+            self.pipe.space.touch()
 
     def train_step(self, images, targets):
         self.optimizer.zero_grad()
         B = images.shape[0]
         loss = self.pipe.train_step(images, targets, B, self.cfg.img_size,
                                     loss_scale=_loss_scale(self.cfg, B))
+        if self.replicas > 1:
+            # data parallel across the pipelines: each stage's flat gradient averaged over its R copies
+            # (one all-reduce per stage per step, DDP semantics: the mean of the per-pipeline losses' grads)
+            g = self.pipe.space.grad
+            dist.all_reduce(g, group=self.dp_group)
+            g.mul_(1.0 / self.replicas)
         self.optimizer.step()
         return None if loss is None else loss.detach()
 
@@ -319,13 +343,14 @@ class PipelineDistStrategy(Strategy):
         mine = self.optimizer.state_dict()
         out = [None] * self.world if self.rank == 0 else None
         dist.gather_object(mine, out, dst=0)
-        return {"stages": out} if self.rank == 0 else None
+        # pipelines hold identical optimizer states (same averaged gradients): pipeline 0's are kept
+        return {"stages": out[:self.stages]} if self.rank == 0 else None
 
     def load_optimizer_state_dict(self, sd):
-        if "stages" in sd and len(sd["stages"]) != self.world:
+        if "stages" in sd and len(sd["stages"]) != self.stages:
             raise ValueError(f"checkpoint holds optimizer state for {len(sd['stages'])} pipeline stages, "
-                             f"this run has {self.world}")
-        self.optimizer.load_state_dict(sd["stages"][self.rank] if "stages" in sd else sd)
+                             f"this run has {self.stages}")
+        self.optimizer.load_state_dict(sd["stages"][self.stage] if "stages" in sd else sd)
 
     def barrier(self):
         dist.barrier()
@@ -438,8 +463,11 @@ def train(cfg: TrainConfig):
         log.info(_K.CFG.describe())        # the run's kernel switches, once (ops/config.py)
 
     train_set, val_set = build_datasets(cfg, strat.device)
-    dp_ranks = world if strat.name == "DDP" else 1
-    dp_rank = strat.rank if strat.name == "DDP" else 0
+    # data shards: DDP ranks, or the pipelines of a replicated -t MP (every stage of one pipeline reads the
+    # same shard; only its first / head stage uses it)
+    mp_dist = isinstance(strat, PipelineDistStrategy)
+    dp_ranks = world if strat.name == "DDP" else (strat.replicas if mp_dist else 1)
+    dp_rank = strat.rank if strat.name == "DDP" else (strat.replica if mp_dist else 0)
     if isinstance(_base_dataset(train_set), DeviceSyntheticSegmentation):
         train_loader, val_loader, sampler = device_loaders(
             train_set, val_set, cfg.batch_size, rank=dp_rank, world_size=dp_ranks, seed=cfg.seed,
@@ -530,9 +558,8 @@ def train(cfg: TrainConfig):
         curves.add_val(step, time.time() - t_start, val_loss)
         plateau_step(scheduler, val_loss)
         metrics.log(kind="epoch", epoch=epoch, step=step, val_loss=val_loss, val_dice=val_dice,
-                    img_per_s=n_img * max(1, strat.world if strat.name == "DDP" else 1) / max(ep_time, 1e-9),
-                    img_per_s_steady=(None if steady_ips is None
-                                      else steady_ips * max(1, strat.world if strat.name == "DDP" else 1)),
+                    img_per_s=n_img * dp_ranks / max(ep_time, 1e-9),
+                    img_per_s_steady=(None if steady_ips is None else steady_ips * dp_ranks),
                     peak_mem_gb=(torch.cuda.max_memory_allocated(strat.device) / 2 ** 30
                                  if strat.device.type == "cuda" else 0.0))
         if strat.is_main:
@@ -766,10 +793,10 @@ def evaluate(strat: Strategy, val_loader, cfg: Optional[TrainConfig] = None):
         t = tot.to(strat.device) if strat.device.type == "cuda" else tot
         tot = strat.reduce_eval(t).cpu()
     elif strat.name == "MP" and isinstance(strat, PipelineDistStrategy):
-        # the head stage holds the outputs (the last stage for a contiguous placement, stage 0 for a
-        # mirrored one); share the result with every stage
+        # each pipeline's head stage holds its shard's sums (the last stage for a contiguous placement,
+        # stage 0 for a mirrored one), every other rank zeros: the sum over the job is the total, on all
         t = tot.to(strat.device) if strat.device.type == "cuda" else tot
-        dist.broadcast(t, src=strat.pipe.head_rank)
+        dist.all_reduce(t)
         tot = t.cpu()
     if tot[2] == 0:
         return float("nan"), float("nan")

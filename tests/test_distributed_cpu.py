@@ -363,3 +363,73 @@ def test_mp_trainer_two_ranks(tmp_path, cut):
     rows = [json.loads(l) for l in open(tmp_path / "logs" / "MP.jsonl")]
     vals = [r["val_loss"] for r in rows if "val_loss" in r]
     assert vals and all(v == v and abs(v) < 1e3 for v in vals), vals
+
+
+def _hybrid_worker(rank, world, port, replicas, mode, q):
+    _init(rank, world, port)
+    from distributedpytorch_amd.config import TrainConfig
+    from distributedpytorch_amd.trainer import PipelineDistStrategy
+    torch.manual_seed(0)
+    model = build_model("unet-tiny")
+    ref = build_model("unet-tiny")
+    ref.load_state_dict(model.state_dict())
+    S = world // replicas
+    if rank >= S:   # other pipelines start from different weights: pipeline 0's must be broadcast
+        for p in model.parameters():
+            p.data.add_(0.5)
+    cfg = TrainConfig(train_method="MP", backend="torch", dtype="fp32", lr=1e-3, mp_replicas=replicas,
+                      mp_cut=mode, microbatches=2, img_size=(32, 32), model="unet-tiny", batch_size=4)
+    try:
+        st = PipelineDistStrategy(cfg, model, "cpu")
+    except Exception as e:      # surface the failure instead of a queue timeout
+        q.put((rank, -1, -1, repr(e), False, False, False))
+        raise
+    r = st.replica
+    x, t = _data(4, seed=50 + r)
+    st.train_step(x, t)
+    # expected: the mean over the pipelines of the plain full-batch gradient (loss x batch, A11)
+    grads = []
+    for k in range(replicas):
+        ref.zero_grad()
+        xk, tk = _data(4, seed=50 + k)
+        (bce_dice_from_probs(ref(xk), tk) * 4).backward()
+        rp = dict(ref.named_parameters())
+        grads.append(torch.cat([rp[n].grad.reshape(-1) for n in st.pipe.space.names]))
+    expect = sum(grads) / replicas
+    ok_grad = torch.allclose(st.pipe.space.grad, expect, atol=1e-5, rtol=1e-4)
+    for i in range(2):
+        st.train_step(*_data(4, seed=200 + 10 * i + r))
+    params = st.pipe.space.data.clone()
+    # the same stage of every pipeline holds the same parameters
+    same = []
+    if st.dp_group is not None:
+        allp = [torch.zeros_like(params) for _ in range(replicas)]
+        dist.all_gather(allp, params, group=st.dp_group)
+        same = [torch.equal(allp[0], p) for p in allp]
+    q.put((rank, st.replica, st.stage, ok_grad, all(same), st.pipe.is_last, st.is_main))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,replicas,mode", [(4, 2, "v"), (4, 2, "reference"), (6, 3, "v"), (4, 4, "balanced")])
+def test_pipeline_replicas_data_parallel(world, replicas, mode):
+    """-t MP with --mp-replicas R: R pipelines of world/R stages (ranks r*S .. r*S+S-1), each on its own
+    batch; every stage's gradient equals the mean over the pipelines of the plain full-batch gradients,
+    pipeline 0's initial parameters reach every pipeline, and the same stage of all pipelines stays
+    bit-identical across optimizer steps (R = world: plain data parallelism through the pipeline code)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_hybrid_worker, args=(r, world, port, replicas, mode, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=300) for _ in procs], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+    S = world // replicas
+    for rank, rep, stage, ok_grad, same, _, _ in res:
+        assert isinstance(ok_grad, bool), ok_grad
+        assert (rep, stage) == divmod(rank, S)
+        assert ok_grad, f"rank {rank}: stage gradient != mean of the pipelines' gradients"
+        assert same, f"rank {rank}: stage parameters differ across pipelines"
+    assert sum(r[-2] for r in res) == replicas          # one head stage per pipeline
+    assert sum(r[-1] for r in res) == 1                 # one main (logging) rank: pipeline 0's head
