@@ -36,6 +36,52 @@ def fmt(r, label):
             f"{r['max_link_gb']:7.2f} {r['max_link_busy_ms']:8.1f}")
 
 
+def hybrid_tables(paths, link_gbs):
+    """--mp-replicas: R pipelines of S stages on G = R x S GPUs at a fixed global batch B (each pipeline
+    B / R images).  Step = the best V pipeline of S stages at B / R (simulated, links queued) + the
+    data-parallel all-reduce of the largest stage's fp32 gradients over R GPUs, not overlapped (ring:
+    2 (R-1)/R x bytes at the link rate); S = 1 is plain data parallelism."""
+    from distributedpytorch_amd.models.unet import build_model
+    from distributedpytorch_amd.parallel.pipeline import placement_param_names
+    out = []
+    for path in paths:
+        t = load_table(path)
+        ut = unit_table(t) if any("units" in row for row in t["per_mb"].values()) else t
+        model_name, (h, w) = t["model"], t["img"]
+        model = build_model(model_name)
+        numel = {n: p.numel() for n, p in model.named_parameters()}
+        G, batches = (2, [256]) if model_name == "unet" else (8, [16, 32, 64])
+        for B in batches:
+            t1 = single_device_ms(t, B)
+            out.append(f"## {model_name} {h}x{w}: {G} GPUs as R pipelines x S stages, global batch {B}, "
+                       f"{link_gbs:g} GB/s links (single GPU: {t1:.1f} ms)")
+            out.append(f"{'S':>2s} {'R':>2s} {'b/pipe':>6s} {'M':>3s} {'pipe ms':>8s} {'ar ms':>6s} {'step ms':>8s} "
+                       f"{'img/s':>8s} {'eff':>6s}  placement")
+            for S in [d for d in range(1, G + 1) if G % d == 0]:
+                R = G // S
+                if B % R:
+                    continue
+                b = B // R
+                if S == 1:
+                    tp, M, pl_s, stage_bytes = single_device_ms(t, b), 1, "whole model", 4 * sum(numel.values())
+                    if tp is None:
+                        continue
+                else:
+                    rows = search(ut, S, b, "v", link_gbs=link_gbs)
+                    if not rows:
+                        continue
+                    best = max(rows, key=lambda r: r["img_s"])
+                    pl = Placement(best["cuts"], best["owner"])
+                    tp, M, pl_s = 1000.0 * b / best["img_s"], best["microbatches"], str(pl)
+                    stage_bytes = max(4 * sum(numel[n] for n in placement_param_names(model, pl, s)) for s in range(S))
+                tar = 2 * (R - 1) / R * stage_bytes / (link_gbs * 1e6) if R > 1 else 0.0
+                step = tp + tar
+                out.append(f"{S:2d} {R:2d} {b:6d} {M:3d} {tp:8.2f} {tar:6.2f} {step:8.2f} {1000 * B / step:8.1f} "
+                           f"{t1 / (G * step):6.3f}  {pl_s}")
+            out.append("")
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("tables", nargs="+")
@@ -101,6 +147,7 @@ def main():
                 "predicted_img_s": best_v["img_s"], "predicted_efficiency": best_v.get("scaling_efficiency"),
                 "link_gbs": links[0], "at_slow_link": best_v.get("at_slow_link", {}),
                 "source": os.path.basename(path)}
+    lines += hybrid_tables(a.tables, links[0])
     txt = "\n".join(lines)
     print(txt)
     if a.out:
