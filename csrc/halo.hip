@@ -875,7 +875,9 @@ __global__ __launch_bounds__(256 * WCS) void igemm_stream_kernel(IgemmArgs a) {
 // First layer (Cin = 3 padded to 8): K = 9 taps x 8 channels.  A 32-deep MFMA k-step covers 4 taps,
 // one per 16-lane group, so each lane reads its tap's 16 bytes straight from the row ring at pixel
 // (p + kw) of slot (r + kh): no im2col, 3 k-steps (taps 9..11 have zero weights).
-template <int BP, int RH>
+// BNS: the conv is followed by BatchNorm (bias, no ReLU): also sum y, sum y^2 of the stored bf16 output per
+// block -> a.bnslab[block][2][32], as igemm_stream_kernel's EPI 4 (no statistics pass over the 512^2 output)
+template <int BP, int RH, bool BNS = false>
 __global__ __launch_bounds__(256) void igemm_stream8_kernel(IgemmArgs a) {
   constexpr int NG = 32, HR = BP + 2, SLOT = HR * 16;
   constexpr int WP = BP / 4, TP = WP / 16, TC = NG / 16;
@@ -923,10 +925,19 @@ __global__ __launch_bounds__(256) void igemm_stream8_kernel(IgemmArgs a) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) bias[ic][e] = a.bias ? a.bias[ic * 16 + 4 * chunk + e] : 0.f;
   unsigned yl[TP];
+  float pz[TP];                 // 1 for pixels inside the row (the statistics skip a ragged strip's tail)
 #pragma unroll
   for (int ip = 0; ip < TP; ++ip) {
     const int pl = w0 + wp * WP + ip * 16 + (lane & 15);
     yl[ip] = pl < a.Wo ? (unsigned)((pl * a.ldy + 4 * chunk) * 2) : 0x80000000u;   // ragged strip: dropped
+    pz[ip] = pl < a.Wo ? 1.f : 0.f;
+  }
+  float bsum[BNS ? TC : 1][4], bsq[BNS ? TC : 1][4];
+  if constexpr (BNS) {
+#pragma unroll
+    for (int ic = 0; ic < TC; ++ic)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) bsum[ic][e] = bsq[ic][e] = 0.f;
   }
 #pragma unroll 1
   for (int j = 0; j < 3; ++j) {
@@ -974,18 +985,57 @@ __global__ __launch_bounds__(256) void igemm_stream8_kernel(IgemmArgs a) {
         if (a.relu) {
           v0 = relu_f(v0); v1 = relu_f(v1); v2 = relu_f(v2); v3 = relu_f(v3);
         }
-        __builtin_amdgcn_raw_buffer_store_b64(u32x2_t{pack_bf2(v0, v1), pack_bf2(v2, v3)}, yr, ybase + yl[ip] + ic * 32, 0, 0);
+        const u32x2_t packed = u32x2_t{pack_bf2(v0, v1), pack_bf2(v2, v3)};
+        __builtin_amdgcn_raw_buffer_store_b64(packed, yr, ybase + yl[ip] + ic * 32, 0, 0);
+        if constexpr (BNS) {     // statistics of the STORED bf16 values
+          const float q[4] = {pz[ip] * lo_bf(packed.x), pz[ip] * hi_bf(packed.x), pz[ip] * lo_bf(packed.y),
+                              pz[ip] * hi_bf(packed.y)};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            bsum[ic][e] += q[e];
+            bsq[ic][e] = fmaf(q[e], q[e], bsq[ic][e]);
+          }
+        }
       }
     __builtin_amdgcn_sched_barrier(0);
     if (r + 1 < nrows) rstore((r + 3) & 3);
     __syncthreads();
+  }
+  if constexpr (BNS) {
+    // lanes l ^ 1..15 hold the same channels of other pixels: butterfly over the 16, then the 4 waves in a
+    // fixed order -> one deterministic slab row per block
+    __shared__ float bred[4][2 * NG];
+#pragma unroll
+    for (int ic = 0; ic < TC; ++ic)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float sv = bsum[ic][e], qv = bsq[ic][e];
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          sv += __shfl_xor(sv, o, 64);
+          qv += __shfl_xor(qv, o, 64);
+        }
+        if ((lane & 15) == 0) {
+          const int c = ic * 16 + 4 * chunk + e;
+          bred[wp][c] = sv;
+          bred[wp][NG + c] = qv;
+        }
+      }
+    __syncthreads();
+    for (int k = tid; k < 2 * NG; k += 256)
+      a.bnslab[(long)blockIdx.x * 2 * NG + k] = (bred[0][k] + bred[1][k]) + (bred[2][k] + bred[3][k]);
   }
 }
 
 template <int BP, int RH>
 static int launch_igemm_stream8(const IgemmArgs& a, hipStream_t st) {
   const int grid = a.N * ((a.Ho + RH - 1) / RH) * ((a.Wo + BP - 1) / BP);
-  hipLaunchKernelGGL((igemm_stream8_kernel<BP, RH>), dim3(grid), dim3(256), 0, st, a);
+  if (a.bnslab) {   // conv followed by BatchNorm: statistics in the epilogue (bias only, plain store)
+    if (a.relu || a.mask || a.accumulate || a.y2 || a.hslab) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL((igemm_stream8_kernel<BP, RH, true>), dim3(grid), dim3(256), 0, st, a);
+  } else {
+    hipLaunchKernelGGL((igemm_stream8_kernel<BP, RH>), dim3(grid), dim3(256), 0, st, a);
+  }
   return (int)hipGetLastError();
 }
 
@@ -1043,6 +1093,7 @@ static int stream_auto_variant(const IgemmArgs& a) {
 // blocks the streaming launch of `a` (variant 0) uses -- rows of the fused head's slab
 DPA_API int dpa_igemm_stream_blocks(const IgemmArgs* args) {
   const IgemmArgs& a = *args;
+  if (a.Cs == 8 && a.Ngemm == 32) return a.N * ((a.Ho + 31) / 32) * ((a.Wo + 127) / 128);   // igemm_stream8<128, 32>
   const int variant = stream_auto_variant(a);
   const int bp = (variant == 1 || variant == 3) ? 128 : 64;
   const int strips = (a.Wo + bp - 1) / bp;

@@ -79,12 +79,22 @@ DPA_API int dpa_maxpool2(const bf16_t* x, int ldx, bf16_t* y, int ldy, int N, in
 // window.  A wave covers 64/CC consecutive windows of one pooled row: each of its loads/stores
 // touches full 64-B runs of the two full-resolution rows.
 //   g[p][c] = (dskip[p][c] + (argmax(window)[c] == q(p) ? dpool[window][c] : 0)) * mask_q(p)[c]
+// BNS: the pooled tensor y (= the skip) is a BatchNorm+ReLU output: also the BN backward's partial sums of the
+// STORED bf16 g, sum g[c] and sum g[c] * y[c], per block -> bnslab[block][2][C] (no statistics pass over g, z).
+// A thread's channel chunk is fixed (256 % C/8 == 0 for C <= 512), so per-thread sums reduce per chunk.
+template <bool BNS = false>
 __global__ __launch_bounds__(256) void pool_bwd_code_kernel(const unsigned char* __restrict__ code,
                                                             const bf16_t* __restrict__ dskip, int ldd,
                                                             const bf16_t* __restrict__ dpool, int ldp,
-                                                            bf16_t* __restrict__ g, int ldg, int N, int H, int W, int C) {
+                                                            bf16_t* __restrict__ g, int ldg, int N, int H, int W, int C,
+                                                            const bf16_t* __restrict__ y, int ldy, float* __restrict__ bnslab) {
   const int CC = C >> 3, Ho = H >> 1, Wo = W >> 1;
   const unsigned tot = (unsigned)N * Ho * Wo * CC;
+  float sg[BNS ? 8 : 1], sgy[BNS ? 8 : 1];
+  if constexpr (BNS) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) sg[k] = sgy[k] = 0.f;
+  }
   for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < tot; i += gridDim.x * blockDim.x) {
     const unsigned cc = i % CC, win = i / CC;
     const unsigned ow = win % Wo, noh = win / Wo;          // noh = n * Ho + oh
@@ -92,10 +102,14 @@ __global__ __launch_bounds__(256) void pool_bwd_code_kernel(const unsigned char*
     const size_t pix[4] = {p00, p00 + 1, p00 + W, p00 + W + 1};
     const uint2 cw = *reinterpret_cast<const uint2*>(code + (size_t)win * C + cc * 8);
     const uint4 dp = *reinterpret_cast<const uint4*>(dpool + (size_t)win * ldp + cc * 8);
-    uint4 ds[4];
+    uint4 ds[4], yv[BNS ? 4 : 1];
 #pragma unroll
     for (int q = 0; q < 4; ++q)
       ds[q] = dskip ? *reinterpret_cast<const uint4*>(dskip + pix[q] * ldd + cc * 8) : make_uint4(0u, 0u, 0u, 0u);
+    if constexpr (BNS) {      // issued with the other loads: 8 independent 16-B loads in flight per lane
+#pragma unroll
+      for (int q = 0; q < 4; ++q) yv[q] = *reinterpret_cast<const uint4*>(y + pix[q] * ldy + cc * 8);
+    }
     const unsigned* pd = &dp.x;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -112,16 +126,56 @@ __global__ __launch_bounds__(256) void pool_bwd_code_kernel(const unsigned char*
         o[k] = pack_bf2(lo, hi);
       }
       *reinterpret_cast<uint4*>(g + pix[q] * ldg + cc * 8) = make_uint4(o[0], o[1], o[2], o[3]);
+      if constexpr (BNS) {
+        const unsigned* py = &yv[q].x;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float g0 = lo_bf(o[k]), g1 = hi_bf(o[k]);
+          sg[2 * k] += g0;
+          sg[2 * k + 1] += g1;
+          sgy[2 * k] = fmaf(g0, lo_bf(py[k]), sgy[2 * k]);
+          sgy[2 * k + 1] = fmaf(g1, hi_bf(py[k]), sgy[2 * k + 1]);
+        }
+      }
+    }
+  }
+  if constexpr (BNS) {
+    // thread t holds chunk t % CC; the 256 / CC threads of a chunk are summed in thread order
+    __shared__ float red[256][17];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      red[threadIdx.x][k] = sg[k];
+      red[threadIdx.x][8 + k] = sgy[k];
+    }
+    __syncthreads();
+    for (int j = threadIdx.x; j < 2 * C; j += 256) {
+      const int which = j / C, c = j - which * C, chunk = c >> 3, k = c & 7;
+      float acc = 0.f;
+      for (int t = chunk; t < 256; t += CC) acc += red[t][8 * which + k];
+      bnslab[(long)blockIdx.x * 2 * C + j] = acc;
     }
   }
 }
+// blocks of a launch (rows of its BN slab): dpa_pool_bwd_code_blocks
+DPA_API int dpa_pool_bwd_code_blocks(int N, int H, int W, int C) {
+  return dpa_grid((long)N * (H / 2) * (W / 2) * (C / 8), 256, 16384);
+}
+
+// y / bnslab (or null): the BatchNorm partial sums of g against y (pool_bwd_code_kernel BNS), C <= 512
 DPA_API int dpa_pool_bwd_code(const unsigned char* code, const bf16_t* dskip, int ldd, const bf16_t* dpool, int ldp,
-                              bf16_t* g, int ldg, int N, int H, int W, int C, hipStream_t st) {
+                              bf16_t* g, int ldg, int N, int H, int W, int C, const bf16_t* y, int ldy, float* bnslab,
+                              hipStream_t st) {
   if ((C & 7) || (ldd & 7) || (ldp & 7) || (ldg & 7) || (H & 1) || (W & 1)) return (int)hipErrorInvalidValue;
+  if (bnslab && (!y || (ldy & 7) || C > 512)) return (int)hipErrorInvalidValue;
   const long tot = (long)N * (H / 2) * (W / 2) * (C / 8);
   if ((long)N * H * W * (C / 8) >= (1l << 31)) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(pool_bwd_code_kernel, dim3(dpa_grid(tot, 256, 16384)), dim3(256), 0, st, code, dskip, ldd, dpool, ldp, g,
-                     ldg, N, H, W, C);
+  const dim3 grid(dpa_pool_bwd_code_blocks(N, H, W, C));
+  if (bnslab)
+    hipLaunchKernelGGL(pool_bwd_code_kernel<true>, grid, dim3(256), 0, st, code, dskip, ldd, dpool, ldp, g, ldg, N, H, W, C,
+                       y, ldy, bnslab);
+  else
+    hipLaunchKernelGGL(pool_bwd_code_kernel<false>, grid, dim3(256), 0, st, code, dskip, ldd, dpool, ldp, g, ldg, N, H, W, C,
+                       y, ldy, bnslab);
   return (int)hipGetLastError();
 }
 
@@ -356,15 +410,23 @@ DPA_API int dpa_head_fwd(const bf16_t* y, int ldy, int C, const float* w, const 
 //   dp = dS0 * (p-t)/max(p(1-p),1e-12) + dS1*[t==1] + dS2 ;  dz = dp * p * (1-p)
 //   gy[p][c] = dz * w[c] * (y[p][c] > 0)      (ReLU backward of the last decoder conv)
 //   dw[c] += dz * y[p][c] ;  db += dz          (block partials -> slab [grid][C+1])
-template <int C>
+// BNS: the last decoder conv is followed by BatchNorm + ReLU (y = its output): also the BN backward's partial
+// sums of the STORED bf16 gradient, sum gy[c] and sum gy[c] * y[c], per block -> bnslab[block][2][C] (the
+// conv epilogues' EPI 5 convention), so the BN backward needs no statistics pass over (gy, z)
+template <int C, bool BNS = false>
 __global__ __launch_bounds__(256) void head_bwd_kernel(const bf16_t* __restrict__ y, int ldy, const float* __restrict__ w,
                                                        const float* __restrict__ b, const float* __restrict__ t,
                                                        const float* __restrict__ dS, bf16_t* __restrict__ gy, int ldg,
-                                                       float* __restrict__ slab, long P) {
+                                                       float* __restrict__ slab, long P, float* __restrict__ bnslab) {
   __shared__ float red[4];
   float wv[C], dw[C];
+  float sg[BNS ? C : 1], sgy[BNS ? C : 1];
 #pragma unroll
   for (int c = 0; c < C; ++c) { wv[c] = w[c]; dw[c] = 0.f; }
+  if constexpr (BNS) {
+#pragma unroll
+    for (int c = 0; c < C; ++c) sg[c] = sgy[c] = 0.f;
+  }
   const float bias = b[0];
   const float d0 = dS[0], d1 = dS[1], d2 = dS[2];
   float db = 0.f;
@@ -387,6 +449,13 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const bf16_t* __restrict_
       const float g0 = v[c] > 0.f ? dz * wv[c] : 0.f;
       const float g1 = v[c + 1] > 0.f ? dz * wv[c + 1] : 0.f;
       o[c / 2] = pack_bf2(g0, g1);
+      if constexpr (BNS) {
+        const float q0 = lo_bf(o[c / 2]), q1 = hi_bf(o[c / 2]);
+        sg[c] += q0;
+        sg[c + 1] += q1;
+        sgy[c] = fmaf(q0, v[c], sgy[c]);
+        sgy[c + 1] = fmaf(q1, v[c + 1], sgy[c + 1]);
+      }
     }
 #pragma unroll
     for (int k = 0; k < C / 8; ++k)
@@ -400,6 +469,16 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const bf16_t* __restrict_
   }
   const float s = block_sum_256(db, red);
   if (threadIdx.x == 0) out[C] = s;
+  if constexpr (BNS) {
+    float* bo = bnslab + (long)blockIdx.x * 2 * C;
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      const float a0 = block_sum_256(sg[c], red);
+      if (threadIdx.x == 0) bo[c] = a0;
+      const float a1 = block_sum_256(sgy[c], red);
+      if (threadIdx.x == 0) bo[C + c] = a1;
+    }
+  }
 }
 
 // gw: segmap weight grad [C] (+=), gb: bias grad [1] (+=); contiguous in the flat buffer is not assumed.
@@ -409,17 +488,21 @@ __global__ void head_grad_finish(const float* __restrict__ tmp, float* __restric
   if (c == C) gb[0] += tmp[C];
 }
 
+// bnslab (or null): [head_grid(P)][2][C] BatchNorm backward partial sums of gy (head_bwd_kernel BNS), C = 32 / 64
 DPA_API int dpa_head_bwd(const bf16_t* y, int ldy, int C, const float* w, const float* b, const float* t, const float* dS,
-                         bf16_t* gy, int ldg, float* slab, float* tmp, float* gw, float* gb, long long P, hipStream_t st) {
+                         bf16_t* gy, int ldg, float* slab, float* tmp, float* gw, float* gb, long long P, float* bnslab,
+                         hipStream_t st) {
   const int grid = head_grid(P);
-  if ((ldy & 7) || (ldg & 7)) return (int)hipErrorInvalidValue;
+  if ((ldy & 7) || (ldg & 7) || (bnslab && C != 32 && C != 64)) return (int)hipErrorInvalidValue;
+#define DPA_HB(Cv, BN) hipLaunchKernelGGL((head_bwd_kernel<Cv, BN>), dim3(grid), dim3(256), 0, st, y, ldy, w, b, t, dS, gy, ldg, slab, (long)P, bnslab)
   switch (C) {
-    case 8: hipLaunchKernelGGL(head_bwd_kernel<8>, dim3(grid), dim3(256), 0, st, y, ldy, w, b, t, dS, gy, ldg, slab, (long)P); break;
-    case 16: hipLaunchKernelGGL(head_bwd_kernel<16>, dim3(grid), dim3(256), 0, st, y, ldy, w, b, t, dS, gy, ldg, slab, (long)P); break;
-    case 32: hipLaunchKernelGGL(head_bwd_kernel<32>, dim3(grid), dim3(256), 0, st, y, ldy, w, b, t, dS, gy, ldg, slab, (long)P); break;
-    case 64: hipLaunchKernelGGL(head_bwd_kernel<64>, dim3(grid), dim3(256), 0, st, y, ldy, w, b, t, dS, gy, ldg, slab, (long)P); break;
+    case 8: DPA_HB(8, false); break;
+    case 16: DPA_HB(16, false); break;
+    case 32: if (bnslab) DPA_HB(32, true); else DPA_HB(32, false); break;
+    case 64: if (bnslab) DPA_HB(64, true); else DPA_HB(64, false); break;
     default: return (int)hipErrorInvalidValue;
   }
+#undef DPA_HB
   hipLaunchKernelGGL(slab_sum_kernel, dim3(C + 1), dim3(256), 0, st, slab, grid, C + 1, tmp, 0);
   hipLaunchKernelGGL(head_grad_finish, dim3(1), dim3(128), 0, st, tmp, gw, gb, C);
   return (int)hipGetLastError();

@@ -137,6 +137,7 @@ class HipBlocks:
         self.dense_skips = set()
         self._fusable = {}
         self._head_pending = None   # (placeholder grad, y, target, dS): head backward deferred to the decoder
+        self._head_bn_stats = None  # (gy, BN partial sums) from the head backward for the last decoder BN
         # pipeline microbatches: the side-stream conv weight gradients of every microbatch are deferred
         # and run as ONE launch per layer over all microbatches' images (K.wgrad_multi) -- one split-K
         # slab set and reduction per step instead of one per microbatch.  Flushed at the end of the
@@ -821,15 +822,19 @@ class _EncFn(torch.autograd.Function):
             g1, st_g = B.conv_bwd(c2, dskip, a, mask=True, pool=(code, dpooled)), None
         else:
             g2 = torch.empty(a.shape[:3] + (C,), dtype=torch.bfloat16, device=a.device)
+            # a BatchNorm after conv2 (skip = its ReLU output): the pool backward also writes that BN's backward
+            # partial sums (sum g, sum g*skip) -- no statistics pass over (g, z)
+            g_stats = [] if (c2.bn is not None and ctx.has_code) else None
             if ctx.has_code:
-                K.pool_bwd_code(code, dskip, dpooled, g2)
+                K.pool_bwd_code(code, dskip, dpooled, g2, y=skip, bn_stats=g_stats)
             else:
                 K.pool_bwd(skip, dskip, dpooled, g2)
+            g_stats = g_stats or None
             if B.fusable(c2, c1, W):
-                g1, st_g = B.bwd_conv(c2, g2, a, st2, mask=True, below=c1, xbn=ctx.xbn1)
+                g1, st_g = B.bwd_conv(c2, g2, a, st2, mask=True, below=c1, xbn=ctx.xbn1, stats=g_stats)
             else:
                 assert ctx.xbn1 is None, "BN-on-load forward needs the fused backward"
-                g2 = B.bn_bwd(c2, g2, st2)
+                g2 = B.bn_bwd(c2, g2, st2, stats=g_stats)
                 B.conv_wgrad(c2, g2, a)              # side stream: overlaps the dgrad chain
                 g1, st_g = B.conv_dgrad(c2, g2, mask=a, below=c1)
         ctx.xbn1 = None
@@ -955,6 +960,9 @@ class _DecFn(torch.autograd.Function):
             B.ready([seg])
         else:
             g2 = _v(g2)
+            hb, B._head_bn_stats = B._head_bn_stats, None
+            head_stats = hb[1] if (hb is not None and g2.data_ptr() == hb[0].data_ptr()
+                                   and g2.stride() == hb[0].stride()) else None
             if pend is not None:
                 # the head's deferred gradient reached us in another form (summed with another
                 # gradient, or materialised by a hook): form it now and add it, never drop it
@@ -966,10 +974,10 @@ class _DecFn(torch.autograd.Function):
                 g2 = (gy.float() + g2.float()).to(torch.bfloat16).contiguous()
             W = g2.shape[2]
             if B.fusable(c2, c1, W):
-                g1, st_g = B.bwd_conv(c2, g2, a, st2, mask=True, below=c1, xbn=ctx.xbn1)
+                g1, st_g = B.bwd_conv(c2, g2, a, st2, mask=True, below=c1, xbn=ctx.xbn1, stats=head_stats)
             else:
                 assert ctx.xbn1 is None, "BN-on-load forward needs the fused backward"
-                g2 = B.bn_bwd(c2, g2, st2)
+                g2 = B.bn_bwd(c2, g2, st2, stats=head_stats)
                 B.conv_wgrad(c2, g2, a)
                 g1, st_g = B.conv_dgrad(c2, g2, mask=a, below=c1)
         B.ready([c2.mod, c2.bn])
@@ -1163,6 +1171,7 @@ class _HeadFn(torch.autograd.Function):
     def forward(ctx, anchor, y, t, B: HipBlocks):
         seg = B.model.segmap
         y = _v(y)
+        B._head_bn_stats = None              # a previous step's unconsumed hand-over (holds gy) goes now
         cache, B._head_cache = B._head_cache, None
         if cache is not None and cache[0] == y.data_ptr() and cache[1] == t.data_ptr():
             S = cache[2]                     # computed by the last decoder conv's epilogue
@@ -1187,6 +1196,11 @@ class _HeadFn(torch.autograd.Function):
             B._head_pending = (ph, y, t.reshape(-1), dS, ctx.hprob)
             ctx.hprob = None
             return None, ph, None, None
-        gy = K.head_bwd(y, seg.weight, seg.bias, t, dS, _grad(seg.weight).view(-1), _grad(seg.bias))
+        # a BatchNorm after the last decoder conv: the head backward also writes that BN's backward partial
+        # sums (sum gy, sum gy*y), handed to the decoder's backward with gy (no statistics pass over gy, z)
+        stats = [] if B.dec_convs[-1][1].bn is not None else None
+        gy = K.head_bwd(y, seg.weight, seg.bias, t, dS, _grad(seg.weight).view(-1), _grad(seg.bias), bn_stats=stats)
         B.ready([seg])
+        if stats:
+            B._head_bn_stats = (gy, stats)
         return None, _o(gy), None, None

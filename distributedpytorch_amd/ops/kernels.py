@@ -274,7 +274,7 @@ def igemm(x: torch.Tensor, wpacked: torch.Tensor, y: torch.Tensor, *, Ngemm: int
         return S
     done = False
     if bslab is not None:
-        if a is not None and conv3 and stream_ok and USE_STREAM and Cs != 8:
+        if a is not None and conv3 and stream_ok and USE_STREAM and (Cs != 8 or xbn is None):
             rows = L.dpa_igemm_stream_blocks(ctypes.byref(a))
             if rows > 0 and rows * 2 * Ngemm <= bslab.numel():
                 a.bnslab = bslab.data_ptr()
@@ -771,8 +771,11 @@ def maxpool2(x: torch.Tensor, y: torch.Tensor, code: Optional[torch.Tensor] = No
                                    _p(code), _stream(x)), "maxpool2")
 
 
-def pool_bwd_code(code: torch.Tensor, dskip: Optional[torch.Tensor], dpool: torch.Tensor, g: torch.Tensor):
-    """Max-pool backward + skip-gradient add + ReLU mask from the forward's window codes."""
+def pool_bwd_code(code: torch.Tensor, dskip: Optional[torch.Tensor], dpool: torch.Tensor, g: torch.Tensor,
+                  y: Optional[torch.Tensor] = None, bn_stats: Optional[list] = None):
+    """Max-pool backward + skip-gradient add + ReLU mask from the forward's window codes.  ``y`` + ``bn_stats``
+    (an empty list): y (the pooled tensor) is a BatchNorm+ReLU output and the list receives (slab [blocks][2][C],
+    blocks) of sum g, sum g*y -- the BN backward's partial sums (:func:`bn_bwd` ``stats``)."""
     N, H, W, C, ldg = _nhwc(g, "pool_bwd_code.g")
     assert code.dtype == torch.uint8 and tuple(code.shape) == (N, H // 2, W // 2, C) and code.is_contiguous()
     ldd = 8
@@ -781,8 +784,18 @@ def pool_bwd_code(code: torch.Tensor, dskip: Optional[torch.Tensor], dpool: torc
         assert (Nd, Hd, Wd, Cd) == (N, H, W, C)
     Np, Hp, Wp, Cp, ldp = _nhwc(dpool, "pool_bwd_code.dpool")
     assert (Np, Hp, Wp, Cp) == (N, H // 2, W // 2, C)
-    _check(_lib.lib().dpa_pool_bwd_code(_p(code), _p(dskip), c_int(ldd), _p(dpool), c_int(ldp), _p(g), c_int(ldg),
-                                        c_int(N), c_int(H), c_int(W), c_int(C), _stream(g)), "pool_bwd_code")
+    L = _lib.lib()
+    ldy, bnslab = 0, None
+    if bn_stats is not None and y is not None:
+        Ny, Hy, Wy, Cy, ldy = _nhwc(y, "pool_bwd_code.y")
+        assert (Ny, Hy, Wy, Cy) == (N, H, W, C)
+        rows = L.dpa_pool_bwd_code_blocks(c_int(N), c_int(H), c_int(W), c_int(C))
+        bnslab = torch.empty(rows * 2 * C, dtype=torch.float32, device=g.device)
+    _check(L.dpa_pool_bwd_code(_p(code), _p(dskip), c_int(ldd), _p(dpool), c_int(ldp), _p(g), c_int(ldg),
+                               c_int(N), c_int(H), c_int(W), c_int(C), _p(y if bnslab is not None else None), c_int(ldy),
+                               _p(bnslab), _stream(g)), "pool_bwd_code")
+    if bnslab is not None:
+        bn_stats.extend([bnslab, rows])
 
 
 def pool_bwd(skip: torch.Tensor, dskip: Optional[torch.Tensor], dpool: torch.Tensor, g: torch.Tensor):
@@ -825,18 +838,25 @@ def head_fwd(y: torch.Tensor, w: torch.Tensor, b: torch.Tensor, t: Optional[torc
 
 
 def head_bwd(y: torch.Tensor, w: torch.Tensor, b: torch.Tensor, t: torch.Tensor, dS: torch.Tensor,
-             gw: torch.Tensor, gb: torch.Tensor) -> torch.Tensor:
+             gw: torch.Tensor, gb: torch.Tensor, bn_stats: Optional[list] = None) -> torch.Tensor:
+    """Segmentation-head backward: returns gy = dL/dy (ReLU-masked by y).  ``bn_stats`` (an empty list):
+    y is a BatchNorm+ReLU output and the list receives (slab [blocks][2][C], blocks) of sum gy, sum gy*y,
+    the BN backward's partial sums (:func:`bn_bwd` ``stats``) -- no statistics pass over (gy, z)."""
     N, H, W, C, ldy = _nhwc(y, "head_bwd.y")
     P = N * H * W
     L = _lib.lib()
     nblk = L.dpa_head_slab_blocks(c_ll(P))
     gy = torch.empty(N, H, W, C, dtype=torch.bfloat16, device=y.device)
-    slab = torch.empty(nblk * (C + 1) + C + 1, dtype=torch.float32, device=y.device)
-    tmp = slab[nblk * (C + 1):]
+    want = bn_stats is not None and C in (32, 64)
+    slab = torch.empty(nblk * (C + 1) + C + 1 + (nblk * 2 * C if want else 0), dtype=torch.float32, device=y.device)
+    tmp = slab[nblk * (C + 1):nblk * (C + 1) + C + 1]
+    bnslab = slab[nblk * (C + 1) + C + 1:] if want else None
     dS = dS.float().contiguous()
     assert gw.is_contiguous() and gw.numel() == C and gb.numel() == 1
     _check(L.dpa_head_bwd(_p(y), c_int(ldy), c_int(C), _p(w.reshape(-1).contiguous()), _p(b), _p(t), _p(dS), _p(gy),
-                          c_int(C), _p(slab), _p(tmp), _p(gw), _p(gb), c_ll(P), _stream(y)), "head_bwd")
+                          c_int(C), _p(slab), _p(tmp), _p(gw), _p(gb), c_ll(P), _p(bnslab), _stream(y)), "head_bwd")
+    if want:
+        bn_stats.extend([bnslab, nblk])
     return gy
 
 

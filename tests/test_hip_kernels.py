@@ -362,6 +362,16 @@ def test_head_loss_fwd_bwd(hip_lib):
     assert _rel(gb.cpu(), br.grad) < 1e-3
     assert _rel(_nchw(gy), yr.grad * (y > 0)) < 1e-2
     assert _rel(probs.cpu(), torch.sigmoid(F.conv2d(y, w, b))[:, 0]) < 1e-5
+    # with a BatchNorm before the head: the same gy, plus the BN backward's partial sums of the stored gy
+    stats = []
+    gy2 = K.head_bwd(_nhwc(y), wc, bc, tc, Sc.grad, torch.zeros(C, device="cuda"), torch.zeros(1, device="cuda"),
+                     bn_stats=stats)
+    torch.cuda.synchronize()
+    assert torch.equal(gy2, gy) and stats
+    slab, rows = stats
+    sums = slab.view(rows, 2, C).double().sum(0).cpu()
+    g64, y64 = gy.double().cpu().reshape(-1, C), _nhwc(y).double().cpu().reshape(-1, C)
+    assert _rel(sums[0], g64.sum(0)) < 1e-4 and _rel(sums[1], (g64 * y64).sum(0)) < 1e-4
 
 
 def test_input_conversion(hip_lib):
@@ -441,6 +451,16 @@ def test_pool_codes_backward(hip_lib, N, H, W, C, fused):
     K.pool_bwd_code(code, dskip, dpool, g)
     torch.cuda.synchronize()
     assert torch.equal(g, g_ref)
+    # with a BatchNorm behind the pooled tensor: the same g, plus sum g and sum g*skip per channel
+    stats = []
+    g2 = torch.empty_like(g_ref)
+    K.pool_bwd_code(code, dskip, dpool, g2, y=skip, bn_stats=stats)
+    torch.cuda.synchronize()
+    assert torch.equal(g2, g_ref) and stats
+    slab, rows = stats
+    sums = slab.view(rows, 2, C).double().sum(0).cpu()
+    gd, yd = g2.double().cpu().reshape(-1, C), skip.double().cpu().reshape(-1, C)
+    assert _rel(sums[0], gd.sum(0)) < 1e-4 and _rel(sums[1], (gd * yd).sum(0)) < 1e-4
 
 
 def test_stream_pool_codes_match_maxpool(hip_lib):

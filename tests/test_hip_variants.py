@@ -206,6 +206,34 @@ def test_hip_unet_variants_match_torch_fp32(hip_lib, variant):
     assert (p - p_ref).abs().max().item() < 5e-2
 
 
+@pytest.mark.parametrize("N,H,W", [(2, 40, 256), (1, 33, 200)])
+def test_first_conv_bn_stats_in_stream8_epilogue(hip_lib, N, H, W):
+    """The first conv (RGB padded to 8 channels, igemm_stream8_kernel) followed by BatchNorm: its epilogue
+    writes the batch sums (sum z, sum z^2 of the stored bf16 output, ragged last strip masked) -- they
+    equal the fp64 sums over the z it wrote, and the output equals the plain launch bitwise."""
+    from distributedpytorch_amd.ops import kernels as K
+    torch.manual_seed(5)
+    x8 = torch.zeros(N, H, W, 8)
+    x8[..., :3] = torch.rand(N, H, W, 3)
+    xh = x8.to(torch.bfloat16).cuda()
+    packed = (torch.randn(32, 96) * 0.2)
+    packed[:, 72:] = 0
+    packed = packed.to(torch.bfloat16).cuda().reshape(-1)
+    b = (torch.randn(32) * 0.1).cuda()
+    z0 = torch.empty(N, H, W, 32, dtype=torch.bfloat16, device="cuda")
+    K.igemm(xh, packed, z0, Ngemm=32, Kpad=96, KH=3, KW=3, stride=1, pad=1, Cs=8, out_grid=(N, H, W), bias=b, relu=False)
+    z1 = torch.empty_like(z0)
+    stats = []
+    K.igemm(xh, packed, z1, Ngemm=32, Kpad=96, KH=3, KW=3, stride=1, pad=1, Cs=8, out_grid=(N, H, W), bias=b, relu=False,
+            bn_stats=stats)
+    torch.cuda.synchronize()
+    assert torch.equal(z0, z1) and len(stats) == 2
+    slab, rows = stats
+    sums = slab[:rows * 64].view(rows, 2, 32).double().sum(0).cpu()
+    zd = z1.double().reshape(-1, 32).cpu()
+    assert _rel(sums[0], zd.sum(0)) < 1e-5 and _rel(sums[1], (zd * zd).sum(0)) < 1e-5
+
+
 @pytest.mark.parametrize("N,H,W,Cin,Cout", [(2, 5, 128, 32, 32), (1, 7, 64, 64, 32), (2, 6, 128, 32, 64),
                                             (1, 33, 64, 64, 64),
                                             # deep layers: the row-block GEMM's epilogue (256 / 128 channels)
