@@ -17,12 +17,14 @@
 // (dgrad B operand: pixel rows, k contiguous) and as ds_read_b64_tr_b16 pixel-fragments (wgrad).
 #include "conv_args.h"
 
-template <int CIN, int COUT>
+// BNS: x is a BatchNorm+ReLU output (the decoder conv's below): also that BN's backward partial sums of the
+// STORED masked dx, sum dx[ci] and sum dx[ci] * x[ci], per block -> bnslab[block][2][CIN] (no statistics pass)
+template <int CIN, int COUT, bool BNS = false>
 __global__ __launch_bounds__(512) void deconv_bwd_kernel(const bf16_t* __restrict__ g, int ldg, const bf16_t* __restrict__ x,
                                                         int ldx, const bf16_t* __restrict__ wd, bf16_t* __restrict__ dx,
                                                         int lddx, float* __restrict__ slab, float* __restrict__ bslab,
                                                         int N, int h, int w, int tiles_per_block, unsigned gbytes,
-                                                        unsigned xbytes) {
+                                                        unsigned xbytes, float* __restrict__ bnslab) {
   constexpr int P = 64;                       // low-resolution pixels per tile
   constexpr int K4 = 4 * COUT;                // dgrad K / wgrad N
   constexpr int RBX = CIN * 2, RBG = K4 * 2;  // LDS row bytes
@@ -122,6 +124,11 @@ __global__ __launch_bounds__(512) void deconv_bwd_kernel(const bf16_t* __restric
     for (int j = 0; j < TN; ++j) accw[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   const int bcol = tid % K4, brg = tid / K4;
   float bsum = 0.f;
+  float bns[BNS ? 4 : 1], bnq[BNS ? 4 : 1];
+  if constexpr (BNS) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) bns[e] = bnq[e] = 0.f;
+  }
 
   if (t0 < t1) {
     gload(t0);
@@ -153,9 +160,18 @@ __global__ __launch_bounds__(512) void deconv_bwd_kernel(const bf16_t* __restric
       const float v2 = lo_bf(mk.y) > 0.f ? acc[2] : 0.f;
       const float v3 = hi_bf(mk.y) > 0.f ? acc[3] : 0.f;
       const int m = m0 + prow;
+      const u32x2_t pk = u32x2_t{pack_bf2(v0, v1), pack_bf2(v2, v3)};
       if (m < M)
-        __builtin_amdgcn_raw_buffer_store_b64(u32x2_t{pack_bf2(v0, v1), pack_bf2(v2, v3)}, dr,
-                                              (unsigned)((m * lddx + ci) * 2), 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b64(pk, dr, (unsigned)((m * lddx + ci) * 2), 0, 0);
+      if constexpr (BNS) {     // pixels past M: x was loaded as zeros, so their dx is zero too
+        const float q[4] = {lo_bf(pk.x), hi_bf(pk.x), lo_bf(pk.y), hi_bf(pk.y)};
+        const float xv[4] = {lo_bf(mk.x), hi_bf(mk.x), lo_bf(mk.y), hi_bf(mk.y)};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          bns[e] += q[e];
+          bnq[e] = fmaf(q[e], xv[e], bnq[e]);
+        }
+      }
     }
     // ---- wgrad: accw[ci][k] += sum_px x[px][ci] * g[px][k]
 #pragma unroll
@@ -208,24 +224,55 @@ __global__ __launch_bounds__(512) void deconv_bwd_kernel(const bf16_t* __restric
       bslab[(long)split * COUT + tid] = s;
     }
   }
+  if constexpr (BNS) {
+    // lanes l ^ 1..15 hold the same 4 channels of other pixels: butterfly, then the NPG pixel-group waves
+    // of a channel group in a fixed order
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        bns[e] += __shfl_xor(bns[e], o, 64);
+        bnq[e] += __shfl_xor(bnq[e], o, 64);
+      }
+    __syncthreads();                                          // the bias reduction's LDS reads are done
+    float* bred = reinterpret_cast<float*>(lds);              // [NPG][2][CIN]
+    if ((lane & 15) == 0) {
+      const int ci = ci0 + 4 * (lane >> 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        bred[(pg * 2) * CIN + ci + e] = bns[e];
+        bred[(pg * 2 + 1) * CIN + ci + e] = bnq[e];
+      }
+    }
+    __syncthreads();
+    if (tid < 2 * CIN) {
+      float acc = 0.f;
+#pragma unroll
+      for (int q = 0; q < NPG; ++q) acc += bred[q * 2 * CIN + tid];
+      bnslab[(long)split * 2 * CIN + tid] = acc;
+    }
+  }
 }
 
+// bnslab (or null): [splits][2][Cin] BatchNorm backward partial sums of the stored dx (deconv_bwd_kernel BNS)
 DPA_API int dpa_deconv_bwd(const bf16_t* g, int ldg, const bf16_t* x, int ldx, const bf16_t* wd, bf16_t* dx, int lddx,
                            float* slab, float* bslab, int N, int h, int w, int Cin, int Cout, int splits,
-                           unsigned gbytes, unsigned xbytes, hipStream_t st) {
+                           unsigned gbytes, unsigned xbytes, float* bnslab, hipStream_t st) {
   if ((ldg & 7) || (ldx & 7) || (lddx & 3) || splits < 1) return (int)hipErrorInvalidValue;
   const long M = (long)N * h * w;
   const int ntiles = (int)((M + 63) / 64);
   const int tpb = (ntiles + splits - 1) / splits;
   if ((long)(splits - 1) * tpb >= ntiles) return (int)hipErrorInvalidValue;   // every split owns >= 1 tile
-  if (Cin == 64 && Cout == 32)
-    hipLaunchKernelGGL((deconv_bwd_kernel<64, 32>), dim3(splits), dim3(512), 0, st, g, ldg, x, ldx, wd, dx, lddx, slab, bslab,
-                       N, h, w, tpb, gbytes, xbytes);
-  else if (Cin == 128 && Cout == 64)
-    hipLaunchKernelGGL((deconv_bwd_kernel<128, 64>), dim3(splits), dim3(512), 0, st, g, ldg, x, ldx, wd, dx, lddx, slab,
-                       bslab, N, h, w, tpb, gbytes, xbytes);
-  else
+#define DPA_DB(CI, CO, BN) hipLaunchKernelGGL((deconv_bwd_kernel<CI, CO, BN>), dim3(splits), dim3(512), 0, st, g, ldg, x, ldx, \
+                                              wd, dx, lddx, slab, bslab, N, h, w, tpb, gbytes, xbytes, bnslab)
+  if (Cin == 64 && Cout == 32) {
+    if (bnslab) DPA_DB(64, 32, true); else DPA_DB(64, 32, false);
+  } else if (Cin == 128 && Cout == 64) {
+    if (bnslab) DPA_DB(128, 64, true); else DPA_DB(128, 64, false);
+  } else {
     return (int)hipErrorInvalidValue;
+  }
+#undef DPA_DB
   return (int)hipGetLastError();
 }
 

@@ -137,7 +137,9 @@ class HipBlocks:
         self.dense_skips = set()
         self._fusable = {}
         self._head_pending = None   # (placeholder grad, y, target, dS): head backward deferred to the decoder
-        self._head_bn_stats = None  # (gy, BN partial sums) from the head backward for the last decoder BN
+        # gradients whose producer also wrote the consumer BatchNorm's backward partial sums (the head and
+        # the fused transposed-conv backward): data_ptr -> (shape, stride, (slab, rows)); see take_stats
+        self._stats_hand = {}
         # pipeline microbatches: the side-stream conv weight gradients of every microbatch are deferred
         # and run as ONE launch per layer over all microbatches' images (K.wgrad_multi) -- one split-K
         # slab set and reduction per step instead of one per microbatch.  Flushed at the end of the
@@ -253,6 +255,8 @@ class HipBlocks:
         then one statistics pass + one normalise/ReLU pass; ``st`` receives (z, saved) for the backward.
         ``x2``: dual input, the conv reads [x | x2] (:meth:`dual_level`).  ``xbn``: ``x`` is the layer
         below's pre-BN output and the conv reads relu(bn(x)) (:meth:`bn_on_load`)."""
+        if self._stats_hand:                 # a forward: last backward's unconsumed hand-overs go
+            self._stats_hand.clear()
         N, H, W = x.shape[:3]
         if y is None:
             y = torch.empty(N, H, W, c.Cout, dtype=torch.bfloat16, device=x.device)
@@ -302,6 +306,20 @@ class HipBlocks:
         K.pack_weights(packed, descs, 1, c.Cout * c.Kf)
         self._fold_cache[id(c)] = (key, packed, bias)
         return packed, bias
+
+    def hand_stats(self, g: torch.Tensor, stats):
+        """``g`` (about to be returned to autograd) comes with the partial sums (sum g, sum g*y) of the
+        BatchNorm whose output y it is the gradient of: the consumer's backward takes them (take_stats).
+        The entry holds ``g`` itself, so its memory cannot be reused by another tensor that would then
+        match; entries left unconsumed (e.g. a gradient sent to another pipeline stage) are dropped at the
+        next forward (conv_fwd)."""
+        if stats:
+            self._stats_hand[g.data_ptr()] = (g, stats)
+
+    def take_stats(self, g: torch.Tensor):
+        """The partial sums handed over with this very tensor (same storage, shape and strides), or None."""
+        e = self._stats_hand.pop(g.data_ptr(), None)
+        return e[1] if e is not None and e[0].shape == g.shape and e[0].stride() == g.stride() else None
 
     def bn_bwd(self, c: _Conv, g: torch.Tensor, st, stats: list = None):
         """gradient w.r.t. the conv output: identity without BN, BatchNorm backward with it (``stats``:
@@ -543,7 +561,13 @@ class HipBlocks:
         both in one pass over (gup, x) (csrc/deconv.hip).  Elsewhere the weight gradient goes to the
         side stream first, then the dgrad runs on the compute stream."""
         if isinstance(d, _Deconv) and K.USE_FUSED_DECONV and (d.Cin, d.Cout) in K.DECONV_BWD_SHAPES:
-            return K.deconv_bwd_fused(gup, x, self.wd(d), _grad(d.mod.weight).view(-1), _grad(d.mod.bias))
+            # x is the BatchNorm+ReLU output of the level below (a BN model): its BN's backward partial sums
+            # come from this kernel's dx epilogue
+            stats = [] if (self.enc_convs[0][1].bn is not None and K.BN_SUMS_DECONV) else None
+            dx = K.deconv_bwd_fused(gup, x, self.wd(d), _grad(d.mod.weight).view(-1), _grad(d.mod.bias),
+                                    bn_stats=stats)
+            self.hand_stats(dx, stats)
+            return dx
         self.deconv_wgrad(d, gup, x)
         return self.deconv_dgrad(d, gup, x)
 
@@ -824,7 +848,7 @@ class _EncFn(torch.autograd.Function):
             g2 = torch.empty(a.shape[:3] + (C,), dtype=torch.bfloat16, device=a.device)
             # a BatchNorm after conv2 (skip = its ReLU output): the pool backward also writes that BN's backward
             # partial sums (sum g, sum g*skip) -- no statistics pass over (g, z)
-            g_stats = [] if (c2.bn is not None and ctx.has_code) else None
+            g_stats = [] if (c2.bn is not None and ctx.has_code and K.BN_SUMS_POOL) else None
             if ctx.has_code:
                 K.pool_bwd_code(code, dskip, dpooled, g2, y=skip, bn_stats=g_stats)
             else:
@@ -871,7 +895,8 @@ class _MidFn(torch.autograd.Function):
         x, a = ctx.saved_tensors
         st1, st2 = ctx.st
         c1, c2 = B.mid_convs
-        g2 = B.bn_bwd(c2, _v(g2), st2)
+        g2 = _v(g2)
+        g2 = B.bn_bwd(c2, g2, st2, stats=B.take_stats(g2))
         B.conv_wgrad(c2, g2, a)
         g1, st_g = B.conv_dgrad(c2, g2, mask=a, below=c1)
         B.ready([c2.mod, c2.bn])
@@ -960,9 +985,7 @@ class _DecFn(torch.autograd.Function):
             B.ready([seg])
         else:
             g2 = _v(g2)
-            hb, B._head_bn_stats = B._head_bn_stats, None
-            head_stats = hb[1] if (hb is not None and g2.data_ptr() == hb[0].data_ptr()
-                                   and g2.stride() == hb[0].stride()) else None
+            head_stats = B.take_stats(g2)    # from the head's or the next level's transposed-conv backward
             if pend is not None:
                 # the head's deferred gradient reached us in another form (summed with another
                 # gradient, or materialised by a hook): form it now and add it, never drop it
@@ -1171,7 +1194,7 @@ class _HeadFn(torch.autograd.Function):
     def forward(ctx, anchor, y, t, B: HipBlocks):
         seg = B.model.segmap
         y = _v(y)
-        B._head_bn_stats = None              # a previous step's unconsumed hand-over (holds gy) goes now
+        B._stats_hand.clear()                # a previous step's unconsumed hand-overs go now
         cache, B._head_cache = B._head_cache, None
         if cache is not None and cache[0] == y.data_ptr() and cache[1] == t.data_ptr():
             S = cache[2]                     # computed by the last decoder conv's epilogue
@@ -1201,6 +1224,5 @@ class _HeadFn(torch.autograd.Function):
         stats = [] if B.dec_convs[-1][1].bn is not None else None
         gy = K.head_bwd(y, seg.weight, seg.bias, t, dS, _grad(seg.weight).view(-1), _grad(seg.bias), bn_stats=stats)
         B.ready([seg])
-        if stats:
-            B._head_bn_stats = (gy, stats)
+        B.hand_stats(gy, stats)
         return None, _o(gy), None, None

@@ -71,6 +71,10 @@ KNOBS = (
     Knob("f32_wgrad3_halves", "DPA_NO_F32_WGRAD3_HALVES", True, "fp32 engine: the halo weight gradient over 64 input "
          "channels as two 32-column blocks (56 KB, 2 blocks per CU) instead of one 104 KB 64-column block: 0.88 vs "
          "1.16 ms at enc1.c2, 312 -> 321 img/s at b16 (profiles/f32_kbench_b16_512_r05_halves.txt)"),
+    Knob("bn_sums_pool", "DPA_NO_BN_SUMS_POOL", True, "BatchNorm UNet: the encoder BN's backward partial sums from the "
+         "max-pool backward (reads the skip once more) instead of a statistics pass over (g, z)"),
+    Knob("bn_sums_deconv", "DPA_NO_BN_SUMS_DECONV", True, "BatchNorm UNet: the decoder BN's backward partial sums from the "
+         "fused transposed-conv backward's dx epilogue instead of a statistics pass"),
     Knob("f32_wgrad_c4", "DPA_NO_F32_WGRAD_C4", True, "fp32 engine: the first conv's weight gradient (4 padded input "
          "channels, 32 outputs) with 48 MFMA columns straight from global memory instead of a 128-column tile "
          "(0.27 vs 0.58 ms at b16 512^2, profiles/f32_kbench_b16_512_r05_halo.txt)"),
@@ -145,6 +149,8 @@ class KernelConfig:
     f32_wgrad_px: bool = True
     f32_wgrad3_halves: bool = True
     f32_conv_halo: int = 2
+    bn_sums_pool: bool = True
+    bn_sums_deconv: bool = True
     f32_wgrad_c4: bool = True
     side_priority: int = 0
     wgrad_stream_blocks: int = 2048

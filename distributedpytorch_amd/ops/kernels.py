@@ -94,6 +94,8 @@ USE_GLDS = CFG.glds                    # LDS-DMA GEMMs (csrc/igemm_glds.hip)
 # 128-output-channel layers on rows of <= 128 pixels: the slice-staged 128 x 512 GEMM (cfg 18), 3-16 %
 # faster than the 128-channel row-block kernel (profiles/kbench_sl_b256_r04.txt)
 USE_GLDS_SL = CFG.glds_sl
+BN_SUMS_POOL = CFG.bn_sums_pool        # BN backward partial sums from the pool backward (models/hip_unet.py)
+BN_SUMS_DECONV = CFG.bn_sums_deconv    # ... from the fused transposed-conv backward
 # 128-channel convs on the row-block ping-pong GEMM (cfg 15) instead of the row-halo conv: 10-15 % faster
 # on every 128-output-channel 3x3 conv / dgrad of the 512^2 UNet (profiles/kbench_glds_rowblock128_b256_r03.txt)
 USE_GLDS128 = CFG.glds128
@@ -866,9 +868,11 @@ DECONV_BWD_SHAPES = ((64, 32), (128, 64))
 
 
 def deconv_bwd_fused(gup: torch.Tensor, x: torch.Tensor, wd: torch.Tensor, gw: torch.Tensor,
-                     gb: Optional[torch.Tensor]) -> torch.Tensor:
+                     gb: Optional[torch.Tensor], bn_stats: Optional[list] = None) -> torch.Tensor:
     """ConvTranspose2d(k2, s2) dgrad (ReLU-masked by x) AND weight/bias gradient in one pass over
-    (gup, x) (csrc/deconv.hip); gw [Cin*Cout*4] / gb [Cout] accumulate.  Returns dx [N,h,w,Cin]."""
+    (gup, x) (csrc/deconv.hip); gw [Cin*Cout*4] / gb [Cout] accumulate.  Returns dx [N,h,w,Cin].
+    ``bn_stats`` (an empty list): x is a BatchNorm+ReLU output; the list receives (slab [rows][2][Cin],
+    rows) of sum dx, sum dx*x -- that BN's backward partial sums (:func:`bn_bwd` ``stats``)."""
     N, H2, W2, Cout, ldg = _nhwc(gup, "deconv_bwd.g")
     Nx, h, w, Cin, ldx = _nhwc(x, "deconv_bwd.x")
     assert Nx == N and (H2, W2) == (2 * h, 2 * w) and (Cin, Cout) in DECONV_BWD_SHAPES
@@ -879,20 +883,28 @@ def deconv_bwd_fused(gup: torch.Tensor, x: torch.Tensor, wd: torch.Tensor, gw: t
         return dx
     L = _lib.lib()
     st = _stream(x)
+    bn_parts = []
     for n0, n1 in _image_chunks(N, max(H2 * W2 * ldg, h * w * ldx) * 2):
         nb = n1 - n0
         ntiles = -(-nb * h * w // 64)
         splits = min(ntiles, 512 if Cin == 64 else 256)
         tpb = -(-ntiles // splits)
         splits = -(-ntiles // tpb)
-        slab = torch.empty(splits * 4 * Cout * Cin + splits * Cout, dtype=torch.float32, device=x.device)
-        bslab = slab[splits * 4 * Cout * Cin:] if gb is not None else None
+        bnn = splits * 2 * Cin if bn_stats is not None else 0
+        slab = torch.empty(splits * 4 * Cout * Cin + splits * Cout + bnn, dtype=torch.float32, device=x.device)
+        bslab = slab[splits * 4 * Cout * Cin:splits * 4 * Cout * Cin + splits * Cout] if gb is not None else None
+        bnslab = slab[splits * 4 * Cout * Cin + splits * Cout:] if bnn else None
+        if bnslab is not None:
+            bn_parts.append((bnslab, splits))
         _check(L.dpa_deconv_bwd(_p(gup[n0:n1]), c_int(ldg), _p(x[n0:n1]), c_int(ldx), _p(wd), _p(dx[n0:n1]), c_int(Cin),
                                 _p(slab), _p(bslab), c_int(nb), c_int(h), c_int(w), c_int(Cin), c_int(Cout),
                                 c_int(splits), ctypes.c_uint(_extent_bytes(nb, H2, W2, Cout, ldg)),
-                                ctypes.c_uint(_extent_bytes(nb, h, w, Cin, ldx)), st), "deconv_bwd")
+                                ctypes.c_uint(_extent_bytes(nb, h, w, Cin, ldx)), _p(bnslab), st), "deconv_bwd")
         _check(L.dpa_wgrad_reduce(_p(slab), _p(bslab), _p(gw), _p(gb), c_int(splits), c_int(4), c_int(Cout), c_int(Cin),
                                   c_int(Cin), c_int(1), st), "wgrad_reduce")
+    if bn_parts:
+        rows = sum(r for _, r in bn_parts)
+        bn_stats.extend([bn_parts[0][0] if len(bn_parts) == 1 else torch.cat([t for t, _ in bn_parts]), rows])
     return dx
 
 

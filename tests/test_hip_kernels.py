@@ -309,6 +309,15 @@ def test_deconv_bwd_fused(hip_lib, N, h, w, Cin, Cout, strided):
     assert _rel(_nchw(dx), xr.grad * (x > 0)) < 1e-2
     assert _rel(gw.cpu() - 0.5, wr.grad) < 1e-2
     assert _rel(gb.cpu() - 0.5, br.grad) < 1e-2
+    # x a BatchNorm+ReLU output: the same dx, plus sum dx and sum dx*x per input channel from the epilogue
+    stats = []
+    dx2 = K.deconv_bwd_fused(g_in, _nhwc(x), wd, torch.zeros_like(gw).view(-1), torch.zeros_like(gb), bn_stats=stats)
+    torch.cuda.synchronize()
+    assert torch.equal(dx2, dx) and stats
+    slab, rows = stats
+    sums = slab.view(rows, 2, Cin).double().sum(0).cpu()
+    dd, xd = dx.double().cpu().reshape(-1, Cin), _nhwc(x).double().cpu().reshape(-1, Cin)
+    assert _rel(sums[0], dd.sum(0)) < 1e-4 and _rel(sums[1], (dd * xd).sum(0)) < 1e-4
 
 
 @pytest.mark.parametrize("N,H,W,C", [(2, 16, 16, 32), (1, 9, 11, 64)])
