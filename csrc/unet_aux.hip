@@ -82,18 +82,29 @@ DPA_API int dpa_maxpool2(const bf16_t* x, int ldx, bf16_t* y, int ldy, int N, in
 // BNS: the pooled tensor y (= the skip) is a BatchNorm+ReLU output: also the BN backward's partial sums of the
 // STORED bf16 g, sum g[c] and sum g[c] * y[c], per block -> bnslab[block][2][C] (no statistics pass over g, z).
 // A thread's channel chunk is fixed (256 % C/8 == 0 for C <= 512), so per-thread sums reduce per chunk.
-template <bool BNS = false>
+// ZBN (with BNS): `y` holds the BN input z (dense) and y = relu(z * coef[c] + coef[C + c]) is formed on load
+// with bn_apply_pool_kernel's arithmetic -- the skip y itself may be a strided concat half (ldy = 2C), z is not.
+template <bool BNS = false, bool ZBN = false>
 __global__ __launch_bounds__(256) void pool_bwd_code_kernel(const unsigned char* __restrict__ code,
                                                             const bf16_t* __restrict__ dskip, int ldd,
                                                             const bf16_t* __restrict__ dpool, int ldp,
                                                             bf16_t* __restrict__ g, int ldg, int N, int H, int W, int C,
-                                                            const bf16_t* __restrict__ y, int ldy, float* __restrict__ bnslab) {
+                                                            const bf16_t* __restrict__ y, int ldy, float* __restrict__ bnslab,
+                                                            const float* __restrict__ coef) {
   const int CC = C >> 3, Ho = H >> 1, Wo = W >> 1;
   const unsigned tot = (unsigned)N * Ho * Wo * CC;
-  float sg[BNS ? 8 : 1], sgy[BNS ? 8 : 1];
+  float sg[BNS ? 8 : 1], sgy[BNS ? 8 : 1], zsc[ZBN ? 8 : 1], zsh[ZBN ? 8 : 1];
   if constexpr (BNS) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) sg[k] = sgy[k] = 0.f;
+  }
+  if constexpr (ZBN) {        // this thread's channel chunk is fixed (see below)
+    const int c0 = (int)((blockIdx.x * blockDim.x + threadIdx.x) % (unsigned)CC) * 8;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      zsc[k] = coef[c0 + k];
+      zsh[k] = coef[C + c0 + k];
+    }
   }
   for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < tot; i += gridDim.x * blockDim.x) {
     const unsigned cc = i % CC, win = i / CC;
@@ -131,10 +142,14 @@ __global__ __launch_bounds__(256) void pool_bwd_code_kernel(const unsigned char*
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           const float g0 = lo_bf(o[k]), g1 = hi_bf(o[k]);
+          unsigned yk = py[k];
+          if constexpr (ZBN)
+            yk = pack_bf2(fmaxf(fmaf(lo_bf(yk), zsc[2 * k], zsh[2 * k]), 0.f),
+                          fmaxf(fmaf(hi_bf(yk), zsc[2 * k + 1], zsh[2 * k + 1]), 0.f));
           sg[2 * k] += g0;
           sg[2 * k + 1] += g1;
-          sgy[2 * k] = fmaf(g0, lo_bf(py[k]), sgy[2 * k]);
-          sgy[2 * k + 1] = fmaf(g1, hi_bf(py[k]), sgy[2 * k + 1]);
+          sgy[2 * k] = fmaf(g0, lo_bf(yk), sgy[2 * k]);
+          sgy[2 * k + 1] = fmaf(g1, hi_bf(yk), sgy[2 * k + 1]);
         }
       }
     }
@@ -161,21 +176,26 @@ DPA_API int dpa_pool_bwd_code_blocks(int N, int H, int W, int C) {
   return dpa_grid((long)N * (H / 2) * (W / 2) * (C / 8), 256, 16384);
 }
 
-// y / bnslab (or null): the BatchNorm partial sums of g against y (pool_bwd_code_kernel BNS), C <= 512
+// y / bnslab (or null): the BatchNorm partial sums of g against y (pool_bwd_code_kernel BNS), C <= 512;
+// coef (or null, needs bnslab): y is the BN input z, relu(bn(z)) formed on load (ZBN)
 DPA_API int dpa_pool_bwd_code(const unsigned char* code, const bf16_t* dskip, int ldd, const bf16_t* dpool, int ldp,
                               bf16_t* g, int ldg, int N, int H, int W, int C, const bf16_t* y, int ldy, float* bnslab,
-                              hipStream_t st) {
+                              const float* coef, hipStream_t st) {
   if ((C & 7) || (ldd & 7) || (ldp & 7) || (ldg & 7) || (H & 1) || (W & 1)) return (int)hipErrorInvalidValue;
   if (bnslab && (!y || (ldy & 7) || C > 512)) return (int)hipErrorInvalidValue;
+  if (coef && !bnslab) return (int)hipErrorInvalidValue;
   const long tot = (long)N * (H / 2) * (W / 2) * (C / 8);
   if ((long)N * H * W * (C / 8) >= (1l << 31)) return (int)hipErrorInvalidValue;
   const dim3 grid(dpa_pool_bwd_code_blocks(N, H, W, C));
-  if (bnslab)
-    hipLaunchKernelGGL(pool_bwd_code_kernel<true>, grid, dim3(256), 0, st, code, dskip, ldd, dpool, ldp, g, ldg, N, H, W, C,
-                       y, ldy, bnslab);
+#define DPA_PB(BN, ZB) hipLaunchKernelGGL((pool_bwd_code_kernel<BN, ZB>), grid, dim3(256), 0, st, code, dskip, ldd, dpool, ldp, g, ldg, N, H, W, C, y, ldy, bnslab, coef)
+  if (coef)
+    DPA_PB(true, true);
+  else if (bnslab)
+    DPA_PB(true, false);
   else
-    hipLaunchKernelGGL(pool_bwd_code_kernel<false>, grid, dim3(256), 0, st, code, dskip, ldd, dpool, ldp, g, ldg, N, H, W, C,
-                       y, ldy, bnslab);
+    DPA_PB(false, false);
+#undef DPA_PB
+  (void)tot;
   return (int)hipGetLastError();
 }
 
@@ -338,19 +358,39 @@ __device__ __forceinline__ void load_row(const bf16_t* y, float* v) {
   }
 }
 
-template <int C>
+// ZBN: the row holds the last decoder conv's pre-BN output z and y = relu(bn(z)) is formed on load with
+// bn_apply_kernel's arithmetic (fp32 fma, ReLU, bf16 rounding), so y is never stored: coef = [scale C | shift C]
+template <int C, bool ZBN>
+__device__ __forceinline__ void load_row_bn(const bf16_t* y, const float* sc, const float* sh, float* v) {
+  load_row<C>(y, v);
+  if constexpr (ZBN) {
+#pragma unroll
+    for (int c = 0; c < C; c += 2) {
+      const unsigned o = pack_bf2(fmaxf(fmaf(v[c], sc[c], sh[c]), 0.f), fmaxf(fmaf(v[c + 1], sc[c + 1], sh[c + 1]), 0.f));
+      v[c] = lo_bf(o);
+      v[c + 1] = hi_bf(o);
+    }
+  }
+}
+
+template <int C, bool ZBN = false>
 __global__ __launch_bounds__(256) void head_fwd_kernel(const bf16_t* __restrict__ y, int ldy, const float* __restrict__ w,
                                                        const float* __restrict__ b, const float* __restrict__ t,
-                                                       float* __restrict__ slab, float* __restrict__ probs, long P) {
+                                                       float* __restrict__ slab, float* __restrict__ probs, long P,
+                                                       const float* __restrict__ coef) {
   __shared__ float red[4];
-  float wv[C];
+  float wv[C], sc[ZBN ? C : 1], sh[ZBN ? C : 1];
 #pragma unroll
   for (int c = 0; c < C; ++c) wv[c] = w[c];
+  if constexpr (ZBN) {
+#pragma unroll
+    for (int c = 0; c < C; ++c) { sc[c] = coef[c]; sh[c] = coef[C + c]; }
+  }
   const float bias = b[0];
   float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < P; i += (long)gridDim.x * blockDim.x) {
     float v[C];
-    load_row<C>(y + i * ldy, v);
+    load_row_bn<C, ZBN>(y + i * ldy, sc, sh, v);
     float z = bias;
 #pragma unroll
     for (int c = 0; c < C; ++c) z = fmaf(v[c], wv[c], z);
@@ -390,17 +430,21 @@ __global__ __launch_bounds__(256) void slab_sum_kernel(const float* __restrict__
 
 static int head_grid(long P) { return dpa_grid(P, 256, 2048); }
 
+// coef (or null): y is the pre-BN output z of a BatchNorm+ReLU layer, y = relu(z * coef[c] + coef[C + c])
+// formed on load (head_fwd_kernel ZBN), C = 32 / 64
 DPA_API int dpa_head_fwd(const bf16_t* y, int ldy, int C, const float* w, const float* b, const float* t, float* slab,
-                         float* S, float* probs, long long P, hipStream_t st) {
+                         float* S, float* probs, long long P, const float* coef, hipStream_t st) {
   const int grid = head_grid(P);
-  if (ldy & 7) return (int)hipErrorInvalidValue;
+  if ((ldy & 7) || (coef && C != 32 && C != 64)) return (int)hipErrorInvalidValue;
+#define DPA_HF(Cv, ZB) hipLaunchKernelGGL((head_fwd_kernel<Cv, ZB>), dim3(grid), dim3(256), 0, st, y, ldy, w, b, t, slab, probs, (long)P, coef)
   switch (C) {
-    case 8: hipLaunchKernelGGL(head_fwd_kernel<8>, dim3(grid), dim3(256), 0, st, y, ldy, w, b, t, slab, probs, (long)P); break;
-    case 16: hipLaunchKernelGGL(head_fwd_kernel<16>, dim3(grid), dim3(256), 0, st, y, ldy, w, b, t, slab, probs, (long)P); break;
-    case 32: hipLaunchKernelGGL(head_fwd_kernel<32>, dim3(grid), dim3(256), 0, st, y, ldy, w, b, t, slab, probs, (long)P); break;
-    case 64: hipLaunchKernelGGL(head_fwd_kernel<64>, dim3(grid), dim3(256), 0, st, y, ldy, w, b, t, slab, probs, (long)P); break;
+    case 8: DPA_HF(8, false); break;
+    case 16: DPA_HF(16, false); break;
+    case 32: if (coef) DPA_HF(32, true); else DPA_HF(32, false); break;
+    case 64: if (coef) DPA_HF(64, true); else DPA_HF(64, false); break;
     default: return (int)hipErrorInvalidValue;
   }
+#undef DPA_HF
   if (slab && S) hipLaunchKernelGGL(slab_sum_kernel, dim3(4), dim3(256), 0, st, slab, grid, 4, S, 0);
   return (int)hipGetLastError();
 }
@@ -413,13 +457,18 @@ DPA_API int dpa_head_fwd(const bf16_t* y, int ldy, int C, const float* w, const 
 // BNS: the last decoder conv is followed by BatchNorm + ReLU (y = its output): also the BN backward's partial
 // sums of the STORED bf16 gradient, sum gy[c] and sum gy[c] * y[c], per block -> bnslab[block][2][C] (the
 // conv epilogues' EPI 5 convention), so the BN backward needs no statistics pass over (gy, z)
-template <int C, bool BNS = false>
+template <int C, bool BNS = false, bool ZBN = false>
 __global__ __launch_bounds__(256) void head_bwd_kernel(const bf16_t* __restrict__ y, int ldy, const float* __restrict__ w,
                                                        const float* __restrict__ b, const float* __restrict__ t,
                                                        const float* __restrict__ dS, bf16_t* __restrict__ gy, int ldg,
-                                                       float* __restrict__ slab, long P, float* __restrict__ bnslab) {
+                                                       float* __restrict__ slab, long P, float* __restrict__ bnslab,
+                                                       const float* __restrict__ coef) {
   __shared__ float red[4];
-  float wv[C], dw[C];
+  float wv[C], dw[C], sc[ZBN ? C : 1], sh[ZBN ? C : 1];
+  if constexpr (ZBN) {
+#pragma unroll
+    for (int c = 0; c < C; ++c) { sc[c] = coef[c]; sh[c] = coef[C + c]; }
+  }
   float sg[BNS ? C : 1], sgy[BNS ? C : 1];
 #pragma unroll
   for (int c = 0; c < C; ++c) { wv[c] = w[c]; dw[c] = 0.f; }
@@ -432,7 +481,7 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const bf16_t* __restrict_
   float db = 0.f;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < P; i += (long)gridDim.x * blockDim.x) {
     float v[C];
-    load_row<C>(y + i * ldy, v);
+    load_row_bn<C, ZBN>(y + i * ldy, sc, sh, v);
     float z = bias;
 #pragma unroll
     for (int c = 0; c < C; ++c) z = fmaf(v[c], wv[c], z);
@@ -489,17 +538,18 @@ __global__ void head_grad_finish(const float* __restrict__ tmp, float* __restric
 }
 
 // bnslab (or null): [head_grid(P)][2][C] BatchNorm backward partial sums of gy (head_bwd_kernel BNS), C = 32 / 64
+// coef (or null, needs bnslab): y is the pre-BN z, y = relu(bn(z)) formed on load as in dpa_head_fwd
 DPA_API int dpa_head_bwd(const bf16_t* y, int ldy, int C, const float* w, const float* b, const float* t, const float* dS,
                          bf16_t* gy, int ldg, float* slab, float* tmp, float* gw, float* gb, long long P, float* bnslab,
-                         hipStream_t st) {
+                         const float* coef, hipStream_t st) {
   const int grid = head_grid(P);
-  if ((ldy & 7) || (ldg & 7) || (bnslab && C != 32 && C != 64)) return (int)hipErrorInvalidValue;
-#define DPA_HB(Cv, BN) hipLaunchKernelGGL((head_bwd_kernel<Cv, BN>), dim3(grid), dim3(256), 0, st, y, ldy, w, b, t, dS, gy, ldg, slab, (long)P, bnslab)
+  if ((ldy & 7) || (ldg & 7) || (bnslab && C != 32 && C != 64) || (coef && !bnslab)) return (int)hipErrorInvalidValue;
+#define DPA_HB(Cv, BN, ZB) hipLaunchKernelGGL((head_bwd_kernel<Cv, BN, ZB>), dim3(grid), dim3(256), 0, st, y, ldy, w, b, t, dS, gy, ldg, slab, (long)P, bnslab, coef)
   switch (C) {
-    case 8: DPA_HB(8, false); break;
-    case 16: DPA_HB(16, false); break;
-    case 32: if (bnslab) DPA_HB(32, true); else DPA_HB(32, false); break;
-    case 64: if (bnslab) DPA_HB(64, true); else DPA_HB(64, false); break;
+    case 8: DPA_HB(8, false, false); break;
+    case 16: DPA_HB(16, false, false); break;
+    case 32: if (coef) DPA_HB(32, true, true); else if (bnslab) DPA_HB(32, true, false); else DPA_HB(32, false, false); break;
+    case 64: if (coef) DPA_HB(64, true, true); else if (bnslab) DPA_HB(64, true, false); else DPA_HB(64, false, false); break;
     default: return (int)hipErrorInvalidValue;
   }
 #undef DPA_HB

@@ -240,7 +240,7 @@ DPA_API int dpa_wgrad(const WgradArgs* args, int kind, int cfg, hipStream_t st) 
 // streams per element), partial sums combined through LDS in a fixed order -> deterministic.
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ slab, const float* __restrict__ bslab,
                                                            float* __restrict__ gw, float* __restrict__ gb, int splits, int T,
-                                                           int M, int Nc, int Nreal, int mode) {
+                                                           int M, int Nc, int Nreal, int mode, int rmul) {
   __shared__ float part[8][33];
   const long tot = (long)T * M * Nc;
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
@@ -250,7 +250,7 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
     const long idx = isb ? (b - nblk_w) * 32 + tx : b * 32 + tx;
     const long lim = isb ? M : tot;
     const float* src = isb ? bslab : slab;
-    const long stride = isb ? M : tot;
+    const long stride = (isb ? M : tot) * rmul;
     float s = 0.f;
     if (idx < lim) {
 #pragma unroll 8
@@ -287,7 +287,7 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
 template <int G>
 __global__ __launch_bounds__(256) void wgrad_reduce4_kernel(const float* __restrict__ slab, const float* __restrict__ bslab,
                                                             float* __restrict__ gw, float* __restrict__ gb, int splits,
-                                                            int T, int M, int Nc, int Nreal, int mode) {
+                                                            int T, int M, int Nc, int Nreal, int mode, int rmul) {
   constexpr int Q = 256 / G;                   // quads per block
   __shared__ f32x4_t part[G][Q];
   const long totq = (long)T * M * Nc / 4, mq = bslab ? M / 4 : 0;
@@ -299,7 +299,7 @@ __global__ __launch_bounds__(256) void wgrad_reduce4_kernel(const float* __restr
     const long qi = isb ? q - totq : q;
     const bool ok = isb ? qi < mq : true;
     const float* src = isb ? bslab : slab;
-    const long stride = isb ? M : totq * 4;
+    const long stride = (isb ? M : totq * 4) * rmul;
     f32x4_t s = f32x4_t{0.f, 0.f, 0.f, 0.f};
     if (ok) {
 #pragma unroll 4
@@ -338,7 +338,8 @@ __global__ __launch_bounds__(256) void wgrad_reduce4_kernel(const float* __restr
 // contiguous run of 64*T floats.  Blocks past the weight tiles sum the bias slab, 64 channels each.
 __global__ __launch_bounds__(256) void wgrad_reduce_tile_kernel(const float* __restrict__ slab,
                                                                 const float* __restrict__ bslab, float* __restrict__ gw,
-                                                                float* __restrict__ gb, int splits, int T, int M, int Nc) {
+                                                                float* __restrict__ gb, int splits, int T, int M, int Nc,
+                                                                int rmul) {
   __shared__ float part[4][9][64];
   __shared__ float out[64 * 9];
   const long tot = (long)T * M * Nc;
@@ -352,7 +353,7 @@ __global__ __launch_bounds__(256) void wgrad_reduce_tile_kernel(const float* __r
         const float* src = slab + ((long)t * M + m) * Nc + n0 + n;
         float acc = 0.f;
 #pragma unroll 4
-        for (int k = grp; k < splits; k += 4) acc += src[(long)k * tot];
+        for (int k = grp; k < splits; k += 4) acc += src[(long)k * rmul * tot];
         part[grp][t][n] = acc;
       }
       __syncthreads();
@@ -368,7 +369,7 @@ __global__ __launch_bounds__(256) void wgrad_reduce_tile_kernel(const float* __r
       const int m0 = (int)(b - ntile) * 64;
       float acc = 0.f;
       if (m0 + n < M)
-        for (int k = grp; k < splits; k += 4) acc += bslab[(long)k * M + m0 + n];
+        for (int k = grp; k < splits; k += 4) acc += bslab[(long)k * rmul * M + m0 + n];
       part[grp][0][n] = acc;
       __syncthreads();
       if (grp == 0 && m0 + n < M) gb[m0 + n] += ((part[0][0][n] + part[1][0][n]) + part[2][0][n]) + part[3][0][n];
@@ -377,12 +378,46 @@ __global__ __launch_bounds__(256) void wgrad_reduce_tile_kernel(const float* __r
   }
 }
 
+// Few elements over thousands of splits (the first conv's [9][32][8] weight gradient from a row-streaming
+// kernel with one slab row per block): the kernels above give each element ONE block-column of threads,
+// so a 2304-element slab is summed by 73 blocks walking 16k rows -- 0.9 ms, latency bound.  Stage 1 sums
+// groups of R consecutive rows IN PLACE into the group's first row (one thread per element, coalesced,
+// (elements / 256) x groups blocks); the reduce kernels then walk every R-th row (rmul).  Fixed order.
+__global__ __launch_bounds__(256) void wgrad_presum_kernel(float* __restrict__ slab, float* __restrict__ bslab, int splits,
+                                                           long tot, int M, int R) {
+  const long e = (long)blockIdx.x * 256 + threadIdx.x;
+  const bool isb = e >= tot;
+  if (e >= tot + (bslab ? M : 0)) return;
+  float* src = isb ? bslab + (e - tot) : slab + e;
+  const long stride = isb ? M : tot;
+  const int r0 = blockIdx.y * R, r1 = min(splits, r0 + R);
+  float s = 0.f;
+#pragma unroll 8
+  for (int k = r0; k < r1; ++k) s += src[(long)k * stride];
+  src[(long)r0 * stride] = s;
+}
+
+static int WGRAD_PRESUM = 1;        // DPA_NO_WGRAD_PRESUM=1 -> 0 (set at library load, ops/_lib.py)
+DPA_API void dpa_wgrad_set_presum(int on) { WGRAD_PRESUM = on; }
+
 // g: -1 auto, 0 the 32-element kernel, > 0 the quad kernel with g split groups, -2 the tiled kernel
-// (tools/kbench_reduce.py)
-DPA_API int dpa_wgrad_reduce_cfg(const float* slab, const float* bslab, float* gw, float* gb, int splits, int T, int M,
+// (tools/kbench_reduce.py).  The slabs are scratch: the presum stage (many splits, few elements) writes them.
+DPA_API int dpa_wgrad_reduce_cfg(const float* slab_in, const float* bslab_in, float* gw, float* gb, int splits, int T, int M,
                                  int Nc, int Nreal, int mode, int g, hipStream_t st) {
   const long tot = (long)T * M * Nc;
+  float* slab = const_cast<float*>(slab_in);
+  float* bslab = const_cast<float*>(bslab_in);
   const bool tile_ok = mode == 0 && Nreal == Nc && Nc % 64 == 0 && T <= 9;
+  int rmul = 1;
+  if (WGRAD_PRESUM && splits >= 1024 && tot <= 65536) {
+    constexpr int R = 32;
+    const long el = tot + (bslab ? M : 0);
+    const unsigned groups = (unsigned)((splits + R - 1) / R);
+    hipLaunchKernelGGL(wgrad_presum_kernel, dim3((unsigned)((el + 255) / 256), groups), dim3(256), 0, st, slab, bslab, splits,
+                       tot, M, R);
+    splits = (int)groups;
+    rmul = R;
+  }
   if (g == -1) {
     // measured on the UNet / UNet-XL slab shapes (profiles/kbench_reduce_r02.txt): tiled for few
     // splits, quad kernel with 4-8 groups for a moderate count, the 32-element kernel for thousands
@@ -395,7 +430,7 @@ DPA_API int dpa_wgrad_reduce_cfg(const float* slab, const float* bslab, float* g
     if (!tile_ok) return (int)hipErrorInvalidValue;
     const long nb = (long)M * (Nc / 64) + (bslab ? (M + 63) / 64 : 0);
     hipLaunchKernelGGL(wgrad_reduce_tile_kernel, dim3((unsigned)(nb < 16384 ? nb : 16384)), dim3(256), 0, st, slab, bslab,
-                       gw, gb, splits, T, M, Nc);
+                       gw, gb, splits, T, M, Nc, rmul);
     return (int)hipGetLastError();
   }
   if (g != 0 && tot % 4 == 0 && M % 4 == 0 && ((size_t)slab & 15) == 0 && (!bslab || ((size_t)bslab & 15) == 0)) {
@@ -405,14 +440,14 @@ DPA_API int dpa_wgrad_reduce_cfg(const float* slab, const float* bslab, float* g
     const long nb = (quads + (256 / G) - 1) / (256 / G);
     const dim3 grid((unsigned)(nb < 8192 ? nb : 8192));
 #define DPA_RED4(Gv) \
-    if (G == Gv) { hipLaunchKernelGGL(wgrad_reduce4_kernel<Gv>, grid, dim3(256), 0, st, slab, bslab, gw, gb, splits, T, M, Nc, Nreal, mode); return (int)hipGetLastError(); }
+    if (G == Gv) { hipLaunchKernelGGL(wgrad_reduce4_kernel<Gv>, grid, dim3(256), 0, st, slab, bslab, gw, gb, splits, T, M, Nc, Nreal, mode, rmul); return (int)hipGetLastError(); }
     DPA_RED4(1) DPA_RED4(2) DPA_RED4(4) DPA_RED4(8) DPA_RED4(16) DPA_RED4(32) DPA_RED4(64)
 #undef DPA_RED4
     return (int)hipErrorInvalidValue;
   }
   const long nb = (tot + 31) / 32 + (bslab ? (M + 31) / 32 : 0);
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)(nb < 8192 ? nb : 8192)), dim3(256), 0, st, slab, bslab, gw, gb,
-                     splits, T, M, Nc, Nreal, mode);
+                     splits, T, M, Nc, Nreal, mode, rmul);
   return (int)hipGetLastError();
 }
 

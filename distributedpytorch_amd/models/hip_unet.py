@@ -235,24 +235,25 @@ class HipBlocks:
         # the row-streaming conv binds one image per block: z's image within the 32-bit buffer range
         return H * W * c2.Cin * 2 < K._MAX_BYTES and self.fusable(c2, c1, W)
 
-    def conv_bn_z(self, c: _Conv, x: torch.Tensor, st: list):
+    def conv_bn_z(self, c: _Conv, x: torch.Tensor, st: list, xbn: torch.Tensor = None):
         """Training conv + BatchNorm statistics without the normalise pass: returns (z, coef) with the
-        consumer's on-load transform relu(z * coef[c] + coef[C + c]); ``st`` receives (z, saved)."""
+        consumer's on-load transform relu(z * coef[c] + coef[C + c]); ``st`` receives (z, saved, coef).
+        ``xbn``: x is itself a pre-BN output, read as relu(bn(x)) (:meth:`conv_fwd`)."""
         N, H, W = x.shape[:3]
         z = torch.empty(N, H, W, c.Cout, dtype=torch.bfloat16, device=x.device)
         self._bn_stats_version += 1
         stats = []
         K.igemm(x, self.wf(c), z, Ngemm=c.Cout, Kpad=c.Kf, KH=3, KW=3, stride=1, pad=1, Cs=c.Cs, out_grid=(N, H, W),
-                bias=c.mod.bias, relu=False, bn_stats=stats)
+                bias=c.mod.bias, relu=False, bn_stats=stats, xbn=xbn)
         coef = []
         saved = K.bn_fwd(z, None, c.bn, train=True, stats=stats, coef_out=coef)
-        st.append((z, saved))
+        st.append((z, saved, coef[0]))
         return z, coef[0]
 
     def conv_fwd(self, c: _Conv, x: torch.Tensor, y: torch.Tensor = None, pool: torch.Tensor = None,
                  pcode: torch.Tensor = None, st: list = None, x2: torch.Tensor = None, xbn: torch.Tensor = None):
         """relu(conv(x)) -> y (and its 2x2 max-pool + window codes).  BN variant: the conv writes z,
-        then one statistics pass + one normalise/ReLU pass; ``st`` receives (z, saved) for the backward.
+        then one statistics pass + one normalise/ReLU pass; ``st`` receives (z, saved, coef) for the backward.
         ``x2``: dual input, the conv reads [x | x2] (:meth:`dual_level`).  ``xbn``: ``x`` is the layer
         below's pre-BN output and the conv reads relu(bn(x)) (:meth:`bn_on_load`)."""
         if self._stats_hand:                 # a forward: last backward's unconsumed hand-overs go
@@ -279,9 +280,10 @@ class HipBlocks:
         stats = [] if self.model.training else None    # batch statistics from the conv epilogue
         K.igemm(x, self.wf(c), z, Ngemm=c.Cout, Kpad=c.Kf, KH=3, KW=3, stride=1, pad=1, Cs=c.Cs, out_grid=(N, H, W),
                 bias=c.mod.bias, relu=False, bn_stats=stats, xbn=xbn)
-        saved = K.bn_fwd(z, y, c.bn, train=self.model.training, stats=stats, pool=pool, pcode=pcode)
+        coef = [] if self.model.training else None     # (scale, shift): consumers may re-form y from z
+        saved = K.bn_fwd(z, y, c.bn, train=self.model.training, stats=stats, pool=pool, pcode=pcode, coef_out=coef)
         if st is not None:
-            st.append((z, saved))
+            st.append((z, saved, coef[0] if coef else None))
         return y
 
     @torch.no_grad()
@@ -326,7 +328,7 @@ class HipBlocks:
         the (sum g, sum g*y) partials the dgrad producing g computed in its epilogue, if any)."""
         if c.bn is None:
             return g
-        z, saved = st
+        z, saved = st[:2]
         return K.bn_bwd(g, z, saved, c.bn, _grad(c.bn.weight), _grad(c.bn.bias), stats=stats)
 
     def conv_dgrad(self, c: _Conv, g: torch.Tensor, mask: torch.Tensor = None, out: torch.Tensor = None,
@@ -420,7 +422,7 @@ class HipBlocks:
         gw, gb = _grad(c.mod.weight).view(-1), _grad(c.mod.bias)
         bn = None
         if c.bn is not None:
-            z, saved = st
+            z, saved = st[:2]
             bn = (z, K.bn_bwd_coef(g, z, saved, c.bn, _grad(c.bn.weight), _grad(c.bn.bias), stats=stats))
         want = below is not None and below.bn is not None
         dx2 = None
@@ -850,7 +852,9 @@ class _EncFn(torch.autograd.Function):
             # partial sums (sum g, sum g*skip) -- no statistics pass over (g, z)
             g_stats = [] if (c2.bn is not None and ctx.has_code and K.BN_SUMS_POOL) else None
             if ctx.has_code:
-                K.pool_bwd_code(code, dskip, dpooled, g2, y=skip, bn_stats=g_stats)
+                # the sums read y = relu(bn(z)) re-formed from the dense z (the skip is a strided concat half)
+                zc = (st2[0], st2[2]) if (g_stats is not None and K.BN_SUMS_POOL_Z and st2[2] is not None) else (skip, None)
+                K.pool_bwd_code(code, dskip, dpooled, g2, y=zc[0], bn_stats=g_stats, coef=zc[1])
             else:
                 K.pool_bwd(skip, dskip, dpooled, g2)
             g_stats = g_stats or None
@@ -861,6 +865,9 @@ class _EncFn(torch.autograd.Function):
                 g2 = B.bn_bwd(c2, g2, st2, stats=g_stats)
                 B.conv_wgrad(c2, g2, a)              # side stream: overlaps the dgrad chain
                 g1, st_g = B.conv_dgrad(c2, g2, mask=a, below=c1)
+            g2 = None                    # dead: freed before conv1's backward allocates
+        st2 = None                       # conv2's BN input z, likewise
+        ctx.st = (st1, None)
         ctx.xbn1 = None
         B.ready([c2.mod, c2.bn])
         if ctx.x_needs_grad and B.fusable(c1, None, W):
@@ -955,6 +962,13 @@ class _DecFn(torch.autograd.Function):
                         out_grid=(N, H, W), bias=c2.mod.bias, relu=True,
                         head=(seg.weight.view(-1), seg.bias, tgt, hprob))
             B._head_cache = (y.data_ptr(), tgt.data_ptr(), S, hprob)
+        elif (tgt is not None and c2.bn is not None and K.BN_HEAD_ON_LOAD and B.model.training and seg.out_channels == 1
+              and tgt.numel() == N * H * W and c2.Cout in (32, 64)):
+            # BatchNorm model: the head reads relu(bn(z)) on load (forward and backward), so the last decoder
+            # conv's BN output is never written: the returned tensor is z, which _HeadFn recognises
+            y, coef = B.conv_bn_z(c2, a, st2, xbn=xbn1)
+            S, _ = K.head_fwd(y, seg.weight, seg.bias, tgt, coef=coef)
+            B._head_cache = (y.data_ptr(), tgt.data_ptr(), S, None, coef)
         else:
             y = B.conv_fwd(c2, a, st=st2, xbn=xbn1)
         ctx.xbn1 = xbn1
@@ -973,7 +987,24 @@ class _DecFn(torch.autograd.Function):
         c1, c2 = B.dec_convs[i]
         C = d.Cout
         pend = B._head_pending
-        if pend is not None and g2.data_ptr() == pend[0].data_ptr() and g2.stride() == pend[0].stride():
+        formed = False
+        if (pend is not None and len(pend) > 5 and g2.data_ptr() == pend[0].data_ptr()
+                and g2.stride() == pend[0].stride()):
+            # BatchNorm model, head on load: its gradient (and that BN's backward partial sums) is formed here
+            # from (z, coef) rather than in _HeadFn.backward, so the full-resolution gy is a local that dies
+            # after this conv's backward instead of an autograd buffer held to the end of this function
+            B._head_pending = None
+            _, z2, t, dS, _, coef = pend
+            pend = None
+            seg = B.model.segmap
+            hs = []
+            g2 = K.head_bwd(z2, seg.weight, seg.bias, t, dS, _grad(seg.weight).view(-1), _grad(seg.bias), bn_stats=hs,
+                            coef=coef)
+            B.ready([seg])
+            head_stats, formed = hs or None, True
+            del z2
+        if (pend is not None and len(pend) == 5 and g2.data_ptr() == pend[0].data_ptr()
+                and g2.stride() == pend[0].stride()):
             # the head's gradient was deferred (_HeadFn.backward): it is formed from y inside this
             # conv's fused backward instead of being materialised (saves a write + read of it)
             B._head_pending = None
@@ -984,17 +1015,21 @@ class _DecFn(torch.autograd.Function):
                                                              _grad(seg.weight).view(-1), _grad(seg.bias), hprob)), None
             B.ready([seg])
         else:
-            g2 = _v(g2)
-            head_stats = B.take_stats(g2)    # from the head's or the next level's transposed-conv backward
+            if not formed:
+                g2 = _v(g2)
+                head_stats = B.take_stats(g2)    # from the head's or the next level's transposed-conv backward
             if pend is not None:
                 # the head's deferred gradient reached us in another form (summed with another
                 # gradient, or materialised by a hook): form it now and add it, never drop it
                 B._head_pending = None
-                ph, y, t, dS, _ = pend
+                ph, y, t, dS = pend[:4]
+                coef = pend[5] if len(pend) > 5 else None      # BN head on load: y is the BN input z
                 seg = B.model.segmap
-                gy = K.head_bwd(y, seg.weight, seg.bias, t, dS, _grad(seg.weight).view(-1), _grad(seg.bias))
+                gy = K.head_bwd(y, seg.weight, seg.bias, t, dS, _grad(seg.weight).view(-1), _grad(seg.bias),
+                                bn_stats=[] if coef is not None else None, coef=coef)
                 B.ready([seg])
                 g2 = (gy.float() + g2.float()).to(torch.bfloat16).contiguous()
+                head_stats = None            # partial sums of the summed gradient: the BN backward forms them
             W = g2.shape[2]
             if B.fusable(c2, c1, W):
                 g1, st_g = B.bwd_conv(c2, g2, a, st2, mask=True, below=c1, xbn=ctx.xbn1, stats=head_stats)
@@ -1004,6 +1039,10 @@ class _DecFn(torch.autograd.Function):
                 B.conv_wgrad(c2, g2, a)
                 g1, st_g = B.conv_dgrad(c2, g2, mask=a, below=c1)
         B.ready([c2.mod, c2.bn])
+        # dead from here: the gradient and conv2's saved BN input z (the step's peak is reached just below, in
+        # conv1's backward at full resolution; autograd would hold them to the end of this function)
+        g2 = st2 = None
+        ctx.st = (st1, None)
         if ctx.dual:
             # the forward checked fusable() (dual_level): the fused backward reads [skip | up] too
             (dskip, gup), _ = B.bwd_conv(c1, g1, cat, st1, mask=False, stats=st_g, split=C, x2=up)
@@ -1017,6 +1056,7 @@ class _DecFn(torch.autograd.Function):
                 B.conv_wgrad(c1, g1, cat)
                 dskip, gup = B.conv_dgrad_split(c1, g1, C)
         B.ready([c1.mod, c1.bn])
+        g1 = None
         if isinstance(d, _Up):
             gup = K.up2_bwd(gup)          # to the projection's (low) resolution
         dx = B.deconv_bwd(d, gup, x)
@@ -1196,13 +1236,16 @@ class _HeadFn(torch.autograd.Function):
         y = _v(y)
         B._stats_hand.clear()                # a previous step's unconsumed hand-overs go now
         cache, B._head_cache = B._head_cache, None
-        if cache is not None and cache[0] == y.data_ptr() and cache[1] == t.data_ptr():
+        hit = cache is not None and cache[0] == y.data_ptr() and cache[1] == t.data_ptr()
+        if hit:
             S = cache[2]                     # computed by the last decoder conv's epilogue
         else:
             S, _ = K.head_fwd(y, seg.weight, seg.bias, t)
         ctx.B = B
+        # BN model with the head formed on load: y is the last BN's input z, relu(bn(z)) = relu(z*coef[:C]+coef[C:])
+        ctx.coef = cache[4] if hit and len(cache) > 4 else None
         # fused forward => y is this engine's last decoder conv output and its backward runs next
-        ctx.fold = cache is not None and cache[0] == y.data_ptr() and B.head_bwd_foldable(y.shape[2])
+        ctx.fold = hit and ctx.coef is None and B.head_bwd_foldable(y.shape[2])
         ctx.hprob = cache[3] if ctx.fold else None      # the forward's probabilities, for the folded backward
         ctx.save_for_backward(y, t)
         return S.clone()
@@ -1221,8 +1264,15 @@ class _HeadFn(torch.autograd.Function):
             return None, ph, None, None
         # a BatchNorm after the last decoder conv: the head backward also writes that BN's backward partial
         # sums (sum gy, sum gy*y), handed to the decoder's backward with gy (no statistics pass over gy, z)
+        coef, ctx.coef = ctx.coef, None
+        if coef is not None and t.is_contiguous() and K.BN_HEAD_DEFER:
+            # BN head on load: defer to the decoder's backward (see _DecFn.backward), like the fold above
+            ph = torch.zeros((), dtype=y.dtype, device=y.device).expand(y.shape[0], y.shape[3], y.shape[1], y.shape[2])
+            B._head_pending = (ph, y, t.reshape(-1), dS, None, coef)
+            return None, ph, None, None
         stats = [] if B.dec_convs[-1][1].bn is not None else None
-        gy = K.head_bwd(y, seg.weight, seg.bias, t, dS, _grad(seg.weight).view(-1), _grad(seg.bias), bn_stats=stats)
+        gy = K.head_bwd(y, seg.weight, seg.bias, t, dS, _grad(seg.weight).view(-1), _grad(seg.bias), bn_stats=stats,
+                        coef=coef)
         B.ready([seg])
         B.hand_stats(gy, stats)
         return None, _o(gy), None, None

@@ -75,6 +75,15 @@ KNOBS = (
          "max-pool backward (reads the skip once more) instead of a statistics pass over (g, z)"),
     Knob("bn_sums_deconv", "DPA_NO_BN_SUMS_DECONV", True, "BatchNorm UNet: the decoder BN's backward partial sums from the "
          "fused transposed-conv backward's dx epilogue instead of a statistics pass"),
+    Knob("bn_sums_pool_z", "DPA_NO_BN_SUMS_POOL_Z", True, "BatchNorm UNet: the pool backward's BN partial sums read the "
+         "dense pre-BN z and re-form relu(bn(z)) instead of reading the skip (a strided concat half)"),
+    Knob("wgrad_presum", "DPA_NO_WGRAD_PRESUM", True, "split-K weight-gradient reduction over >= 1024 slab rows of a "
+         "small weight: rows summed in groups of 32 in place first (the first conv's [9][32][8] gradient: one "
+         "block column per element walked 16k rows, 0.9 ms)"),
+    Knob("bn_head_defer", "DPA_NO_BN_HEAD_DEFER", True, "BatchNorm UNet, head on load: the head backward runs inside the "
+         "last decoder level's backward, so its full-resolution gradient is freed there (peak HBM)"),
+    Knob("bn_head_on_load", "DPA_NO_BN_HEAD_ON_LOAD", True, "BatchNorm UNet: the segmentation head forms the last decoder "
+         "BN's output relu(bn(z)) on load in its forward and backward, so that full-resolution tensor is never written"),
     Knob("f32_wgrad_c4", "DPA_NO_F32_WGRAD_C4", True, "fp32 engine: the first conv's weight gradient (4 padded input "
          "channels, 32 outputs) with 48 MFMA columns straight from global memory instead of a 128-column tile "
          "(0.27 vs 0.58 ms at b16 512^2, profiles/f32_kbench_b16_512_r05_halo.txt)"),
@@ -151,6 +160,10 @@ class KernelConfig:
     f32_conv_halo: int = 2
     bn_sums_pool: bool = True
     bn_sums_deconv: bool = True
+    bn_sums_pool_z: bool = True
+    bn_head_on_load: bool = True
+    bn_head_defer: bool = True
+    wgrad_presum: bool = True
     f32_wgrad_c4: bool = True
     side_priority: int = 0
     wgrad_stream_blocks: int = 2048

@@ -96,6 +96,9 @@ USE_GLDS = CFG.glds                    # LDS-DMA GEMMs (csrc/igemm_glds.hip)
 USE_GLDS_SL = CFG.glds_sl
 BN_SUMS_POOL = CFG.bn_sums_pool        # BN backward partial sums from the pool backward (models/hip_unet.py)
 BN_SUMS_DECONV = CFG.bn_sums_deconv    # ... from the fused transposed-conv backward
+BN_SUMS_POOL_Z = CFG.bn_sums_pool_z    # ... reading the dense z (relu(bn(z)) re-formed) instead of the skip
+BN_HEAD_ON_LOAD = CFG.bn_head_on_load  # the head reads the last decoder BN's input z (relu(bn(z)) on load)
+BN_HEAD_DEFER = CFG.bn_head_defer      # ... with its backward deferred into the decoder's (memory)
 # 128-channel convs on the row-block ping-pong GEMM (cfg 15) instead of the row-halo conv: 10-15 % faster
 # on every 128-output-channel 3x3 conv / dgrad of the 512^2 UNet (profiles/kbench_glds_rowblock128_b256_r03.txt)
 USE_GLDS128 = CFG.glds128
@@ -774,10 +777,12 @@ def maxpool2(x: torch.Tensor, y: torch.Tensor, code: Optional[torch.Tensor] = No
 
 
 def pool_bwd_code(code: torch.Tensor, dskip: Optional[torch.Tensor], dpool: torch.Tensor, g: torch.Tensor,
-                  y: Optional[torch.Tensor] = None, bn_stats: Optional[list] = None):
+                  y: Optional[torch.Tensor] = None, bn_stats: Optional[list] = None, coef: Optional[torch.Tensor] = None):
     """Max-pool backward + skip-gradient add + ReLU mask from the forward's window codes.  ``y`` + ``bn_stats``
     (an empty list): y (the pooled tensor) is a BatchNorm+ReLU output and the list receives (slab [blocks][2][C],
-    blocks) of sum g, sum g*y -- the BN backward's partial sums (:func:`bn_bwd` ``stats``)."""
+    blocks) of sum g, sum g*y -- the BN backward's partial sums (:func:`bn_bwd` ``stats``).  ``coef`` (fp32
+    [scale C | shift C]): ``y`` is that BN's input z and relu(bn(z)) is formed on load (z is dense where the
+    skip y may be a concat half)."""
     N, H, W, C, ldg = _nhwc(g, "pool_bwd_code.g")
     assert code.dtype == torch.uint8 and tuple(code.shape) == (N, H // 2, W // 2, C) and code.is_contiguous()
     ldd = 8
@@ -793,9 +798,13 @@ def pool_bwd_code(code: torch.Tensor, dskip: Optional[torch.Tensor], dpool: torc
         assert (Ny, Hy, Wy, Cy) == (N, H, W, C)
         rows = L.dpa_pool_bwd_code_blocks(c_int(N), c_int(H), c_int(W), c_int(C))
         bnslab = torch.empty(rows * 2 * C, dtype=torch.float32, device=g.device)
+        if coef is not None:
+            assert coef.dtype == torch.float32 and coef.is_contiguous() and coef.numel() == 2 * C
+    else:
+        coef = None
     _check(L.dpa_pool_bwd_code(_p(code), _p(dskip), c_int(ldd), _p(dpool), c_int(ldp), _p(g), c_int(ldg),
                                c_int(N), c_int(H), c_int(W), c_int(C), _p(y if bnslab is not None else None), c_int(ldy),
-                               _p(bnslab), _stream(g)), "pool_bwd_code")
+                               _p(bnslab), _p(coef), _stream(g)), "pool_bwd_code")
     if bnslab is not None:
         bn_stats.extend([bnslab, rows])
 
@@ -821,9 +830,13 @@ def pack_weights(packed: torch.Tensor, descs_dev: torch.Tensor, ndesc: int, max_
                                        _stream(packed)), "pack_weights")
 
 
-def head_fwd(y: torch.Tensor, w: torch.Tensor, b: torch.Tensor, t: Optional[torch.Tensor], want_probs: bool = False):
-    """-> (S[4] fp32 or None, probs[N,H,W] fp32 or None)."""
+def head_fwd(y: torch.Tensor, w: torch.Tensor, b: torch.Tensor, t: Optional[torch.Tensor], want_probs: bool = False,
+             coef: Optional[torch.Tensor] = None):
+    """-> (S[4] fp32 or None, probs[N,H,W] fp32 or None).  ``coef`` ([scale C | shift C] fp32, bn_fwd's
+    ``coef_out``): ``y`` is the pre-BN output z of a BatchNorm+ReLU layer and relu(bn(z)) is formed on load."""
     N, H, W, C, ldy = _nhwc(y, "head.y")
+    if coef is not None:
+        assert C in (32, 64) and coef.dtype == torch.float32 and coef.is_contiguous() and coef.numel() == 2 * C
     P = N * H * W
     L = _lib.lib()
     nblk = L.dpa_head_slab_blocks(c_ll(P))
@@ -835,16 +848,20 @@ def head_fwd(y: torch.Tensor, w: torch.Tensor, b: torch.Tensor, t: Optional[torc
     probs = torch.empty(N, H, W, dtype=torch.float32, device=y.device) if want_probs else None
     wf = w.reshape(-1).contiguous()
     _check(L.dpa_head_fwd(_p(y), c_int(ldy), c_int(C), _p(wf), _p(b), _p(t), _p(slab), _p(S), _p(probs), c_ll(P),
-                          _stream(y)), "head_fwd")
+                          _p(coef), _stream(y)), "head_fwd")
     return S, probs
 
 
 def head_bwd(y: torch.Tensor, w: torch.Tensor, b: torch.Tensor, t: torch.Tensor, dS: torch.Tensor,
-             gw: torch.Tensor, gb: torch.Tensor, bn_stats: Optional[list] = None) -> torch.Tensor:
+             gw: torch.Tensor, gb: torch.Tensor, bn_stats: Optional[list] = None,
+             coef: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Segmentation-head backward: returns gy = dL/dy (ReLU-masked by y).  ``bn_stats`` (an empty list):
     y is a BatchNorm+ReLU output and the list receives (slab [blocks][2][C], blocks) of sum gy, sum gy*y,
-    the BN backward's partial sums (:func:`bn_bwd` ``stats``) -- no statistics pass over (gy, z)."""
+    the BN backward's partial sums (:func:`bn_bwd` ``stats``) -- no statistics pass over (gy, z).
+    ``coef`` (with ``bn_stats``): ``y`` is that BN's input z, y = relu(bn(z)) formed on load (:func:`head_fwd`)."""
     N, H, W, C, ldy = _nhwc(y, "head_bwd.y")
+    if coef is not None:
+        assert bn_stats is not None and C in (32, 64) and coef.dtype == torch.float32 and coef.numel() == 2 * C
     P = N * H * W
     L = _lib.lib()
     nblk = L.dpa_head_slab_blocks(c_ll(P))
@@ -856,7 +873,8 @@ def head_bwd(y: torch.Tensor, w: torch.Tensor, b: torch.Tensor, t: torch.Tensor,
     dS = dS.float().contiguous()
     assert gw.is_contiguous() and gw.numel() == C and gb.numel() == 1
     _check(L.dpa_head_bwd(_p(y), c_int(ldy), c_int(C), _p(w.reshape(-1).contiguous()), _p(b), _p(t), _p(dS), _p(gy),
-                          c_int(C), _p(slab), _p(tmp), _p(gw), _p(gb), c_ll(P), _p(bnslab), _stream(y)), "head_bwd")
+                          c_int(C), _p(slab), _p(tmp), _p(gw), _p(gb), c_ll(P), _p(bnslab), _p(coef), _stream(y)),
+           "head_bwd")
     if want:
         bn_stats.extend([bnslab, nblk])
     return gy

@@ -142,3 +142,58 @@ def test_unet_bn_step_on_load_equals_materialised(hip_lib, monkeypatch, model):
     assert torch.allclose(g0, g1, rtol=1e-5, atol=1e-7 * g0.abs().max().item())
     for k in r0:
         assert torch.equal(r0[k], r1[k]), k
+
+
+@pytest.mark.parametrize("model", ["unet-bn", "unet-bn-bilinear"])
+def test_unet_bn_head_on_load_equals_materialised(hip_lib, monkeypatch, model):
+    """The head reading the last decoder BN's input z (relu(bn(z)) formed on load, forward and backward)
+    == the step that writes that BN output and runs the head over it; the on-load path must be taken."""
+    from distributedpytorch_amd.compute import loss_from_partials, make_compute
+    from distributedpytorch_amd.data.synthetic import synthetic_batch
+    from distributedpytorch_amd.models.unet import build_model
+    from distributedpytorch_amd.optim import FlatParameterSpace
+    from distributedpytorch_amd.ops import kernels as K
+
+    torch.manual_seed(0)
+    net = build_model(model).cuda()
+    space = FlatParameterSpace(net)
+    comp = make_compute(net, backend="hip", dtype="bf16")
+    img, mask = synthetic_batch(2, 64, 256, 3, seed=6)
+    x, t = img.cuda(), mask.float().unsqueeze(1).cuda()
+    state0 = {k: v.clone() for k, v in net.state_dict().items() if "running" in k or "num_batches" in k}
+    used = []
+    real_f, real_b = K.head_fwd, K.head_bwd
+
+    def spy_f(*a, **kw):
+        used.append(kw.get("coef") is not None)
+        return real_f(*a, **kw)
+
+    def spy_b(*a, **kw):
+        used.append(kw.get("coef") is not None)
+        return real_b(*a, **kw)
+
+    monkeypatch.setattr(K, "head_fwd", spy_f)
+    monkeypatch.setattr(K, "head_bwd", spy_b)
+
+    def run():
+        net.load_state_dict(state0, strict=False)
+        space.zero_grad()
+        used.clear()
+        S = comp.forward_partials(x, t)
+        loss = loss_from_partials(S, t.numel())
+        loss.backward()
+        torch.cuda.synchronize()
+        run_stats = {k: v.clone() for k, v in net.state_dict().items() if "running" in k}
+        return loss.item(), space.grad.clone(), run_stats, sum(used)
+
+    l1, g1, r1, n1 = run()
+    monkeypatch.setattr(K, "BN_HEAD_DEFER", False)     # head backward in _HeadFn instead of the decoder's
+    l2, g2, r2, n2 = run()
+    assert n2 == 2 and l2 == l1 and torch.equal(g2, g1)
+    monkeypatch.setattr(K, "BN_HEAD_ON_LOAD", False)
+    l0, g0, r0, n0 = run()
+    assert n1 == 2 and n0 == 0
+    assert abs(l0 - l1) <= 1e-6 * abs(l0)
+    assert torch.allclose(g0, g1, rtol=1e-3, atol=1e-4 * g0.abs().max().item())
+    for k in r0:
+        assert torch.equal(r0[k], r1[k]), k

@@ -381,6 +381,24 @@ def test_head_loss_fwd_bwd(hip_lib):
     sums = slab.view(rows, 2, C).double().sum(0).cpu()
     g64, y64 = gy.double().cpu().reshape(-1, C), _nhwc(y).double().cpu().reshape(-1, C)
     assert _rel(sums[0], g64.sum(0)) < 1e-4 and _rel(sums[1], (g64 * y64).sum(0)) < 1e-4
+    # the head reading the BN input z with y = relu(bn(z)) formed on load (forward and backward)
+    z = _bf(torch.randn(N, C, H, W))
+    coef = torch.cat([torch.rand(C) + 0.5, torch.randn(C) * 0.3]).cuda()
+    yz = _bf(F.relu(z * coef[:C].cpu().view(1, C, 1, 1) + coef[C:].cpu().view(1, C, 1, 1)))
+    Sy, _ = K.head_fwd(_nhwc(yz), wc, bc, tc)
+    Sz, _ = K.head_fwd(_nhwc(z), wc, bc, tc, coef=coef)
+    torch.cuda.synchronize()
+    assert _rel(Sz.cpu(), Sy.cpu()) < 1e-4
+    sy, sz = [], []
+    gyy = K.head_bwd(_nhwc(yz), wc, bc, tc, Sc.grad, torch.zeros(C, device="cuda"), torch.zeros(1, device="cuda"),
+                     bn_stats=sy)
+    gwz, gbz = torch.zeros(C, device="cuda"), torch.zeros(1, device="cuda")
+    gyz = K.head_bwd(_nhwc(z), wc, bc, tc, Sc.grad, gwz, gbz, bn_stats=sz, coef=coef)
+    torch.cuda.synchronize()
+    assert _rel(_nchw(gyz), _nchw(gyy)) < 1e-3
+    a0 = sy[0].view(sy[1], 2, C).double().sum(0)
+    a1 = sz[0].view(sz[1], 2, C).double().sum(0)
+    assert _rel(a1.cpu(), a0.cpu()) < 1e-3
 
 
 def test_input_conversion(hip_lib):
@@ -470,6 +488,18 @@ def test_pool_codes_backward(hip_lib, N, H, W, C, fused):
     sums = slab.view(rows, 2, C).double().sum(0).cpu()
     gd, yd = g2.double().cpu().reshape(-1, C), skip.double().cpu().reshape(-1, C)
     assert _rel(sums[0], gd.sum(0)) < 1e-4 and _rel(sums[1], (gd * yd).sum(0)) < 1e-4
+    # the sums against y = relu(bn(z)) re-formed on load from a dense z
+    z = torch.randn(N, H, W, C, device="cuda").to(torch.bfloat16)
+    coef = torch.cat([torch.rand(C) + 0.5, torch.randn(C) * 0.3]).cuda()
+    yz = torch.relu(z.float() * coef[:C] + coef[C:]).to(torch.bfloat16)
+    sz = []
+    g3 = torch.empty_like(g_ref)
+    K.pool_bwd_code(code, dskip, dpool, g3, y=z, bn_stats=sz, coef=coef)
+    torch.cuda.synchronize()
+    assert torch.equal(g3, g_ref) and sz
+    sums = sz[0].view(sz[1], 2, C).double().sum(0).cpu()
+    yd = yz.double().cpu().reshape(-1, C)
+    assert _rel(sums[0], gd.sum(0)) < 1e-4 and _rel(sums[1], (gd * yd).sum(0)) < 1e-3
 
 
 def test_stream_pool_codes_match_maxpool(hip_lib):
@@ -717,3 +747,23 @@ def test_glds_rowblock_128(hip_lib, N, H, W, Cs, Ng, kind):
     ref = (torch.relu(ref + extra["bias"].cpu()) if kind == "fwd" else ref * (extra["mask"].float().cpu() > 0))
     for v, y in zip((2, 15), outs[:2]):
         assert _rel(y.float().cpu(), ref) < 1e-2, (v, kind)
+
+
+@pytest.mark.parametrize("splits,T,M,Nc,Nreal", [(3000, 9, 32, 8, 3), (1500, 9, 32, 32, 32), (40, 9, 32, 8, 8)])
+def test_wgrad_reduce_many_splits(hip_lib, splits, T, M, Nc, Nreal):
+    """Split-K slab reduction into the OIHW gradient (accumulating), including the in-place presum stage
+    taken for thousands of splits over a small weight: == the fp64 sum of the slab rows."""
+    from ctypes import c_int
+    from distributedpytorch_amd.ops import kernels as K
+    torch.manual_seed(3)
+    slab = torch.randn(splits, T, M, Nc, device="cuda")
+    bslab = torch.randn(splits, M, device="cuda")
+    ref_w = slab.double().sum(0)[..., :Nreal].permute(1, 2, 0).cpu()          # [M][Nreal][T]
+    ref_b = bslab.double().sum(0).cpu()
+    gw = torch.ones(M * Nreal * T, device="cuda")
+    gb = torch.ones(M, device="cuda")
+    K._check(K._lib.lib().dpa_wgrad_reduce(K._p(slab), K._p(bslab), K._p(gw), K._p(gb), c_int(splits), c_int(T), c_int(M),
+                                           c_int(Nc), c_int(Nreal), c_int(0), K._stream(gw)), "wgrad_reduce")
+    torch.cuda.synchronize()
+    assert _rel(gw.cpu().double().view(M, Nreal, T) - 1.0, ref_w) < 1e-5
+    assert _rel(gb.cpu().double() - 1.0, ref_b) < 1e-5

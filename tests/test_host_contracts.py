@@ -185,7 +185,7 @@ def test_elementwise_launchers_reject(L):
     n = None
     i = ctypes.c_int
     assert L.dpa_maxpool2(n, i(12), n, i(12), i(1), i(8), i(8), i(12), n, n) == INVALID            # C % 8
-    assert L.dpa_pool_bwd_code(n, n, i(8), n, i(8), n, i(8), i(1), i(7), i(8), i(8), n, i(0), n, n) == INVALID  # odd H
+    assert L.dpa_pool_bwd_code(n, n, i(8), n, i(8), n, i(8), i(1), i(7), i(8), i(8), n, i(0), n, n, n) == INVALID  # odd H
     assert L.dpa_up2_fwd(n, i(8), n, i(8), i(1), i(0), i(4), i(8), n) == INVALID                   # h < 1
     assert L.dpa_up2_bwd(n, i(8), n, i(8), i(1), i(4), i(4), i(12), n) == INVALID                  # C % 8
     assert L.dpa_slab_fold(n, i(0), i(64), i(8), n, n) == INVALID
