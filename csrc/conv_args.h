@@ -91,6 +91,10 @@ struct WgradArgs {
   // atab[n] / btab[n] instead of A / B + n * image size -- one weight-gradient launch over the images
   // of several tensors of the same per-image layout (the microbatches of a pipeline stage)
   const bf16_t* const* atab; const bf16_t* const* btab;
+  // BatchNorm backward on load of A (wgrad_stream, the first conv): A is the ReLU-masked gradient g of a
+  // BN output and the GEMM row operand is dz = abn[m] g + abn[M + m] z + abn[2M + m] with z = az (the BN
+  // input, A's layout) -- bn_bwd_apply's formula; zero outside the image.  Null: A as is.
+  const bf16_t* az; const float* abn;
 };
 
 // 16-B LDS-DMA: lane l's bytes land at lds + 16*l.  (Wrapped in a __device__ function: used

@@ -1159,7 +1159,7 @@ __device__ __forceinline__ bf16x8_t tr_pair_off(const char* base, int off0, int 
   return __builtin_bit_cast(bf16x8_t, v);
 }
 
-template <int BM, int BN, int BP, int RH>
+template <int BM, int BN, int BP, int RH, bool ABN = false>
 __global__ __launch_bounds__(192) void wgrad_stream_kernel(WgradArgs a, int ipb) {
   constexpr int NT = 192;
   constexpr int HR = BP + 2;
@@ -1170,6 +1170,7 @@ __global__ __launch_bounds__(192) void wgrad_stream_kernel(WgradArgs a, int ipb)
   constexpr int TM = BM / 16, TN = BN / 16;
   __shared__ __attribute__((aligned(16))) char lds[2 * IMGA + 4 * SLOTB];
   __shared__ float bred[BM];
+  __shared__ float abc[ABN ? 3 * BM : 4];       // ABN: this tile's dz coefficients [3][BM]
   char* const Aimg = lds;
   char* const Ring = lds + 2 * IMGA;
 
@@ -1189,12 +1190,16 @@ __global__ __launch_bounds__(192) void wgrad_stream_kernel(WgradArgs a, int ipb)
   const bool do_bias = a.bslab != nullptr && nt == 0;
   // one image at a time: 64-bit image bases (rebound per image below), 32-bit offsets inside it;
   // a.abytes / a.bbytes are the extents of ONE image here, so one launch covers any batch
-  __amdgpu_buffer_rsrc_t ar, br;
+  __amdgpu_buffer_rsrc_t ar, br, zr;
 
   // per-thread loader constants
   unsigned aoff[LA], boff[LB];
   int asto[LA], bsto[LB];
   bool bok[LB];
+  if constexpr (ABN) {
+    for (int i = tid; i < 3 * BM; i += NT) abc[i] = a.abn[(i / BM) * a.M + m0 + i % BM];
+    __syncthreads();
+  }
 #pragma unroll
   for (int j = 0; j < LA; ++j) {
     const int c = tid + j * NT, px = c / CPRA, cc = c - px * CPRA;
@@ -1211,12 +1216,33 @@ __global__ __launch_bounds__(192) void wgrad_stream_kernel(WgradArgs a, int ipb)
     bsto[j] = c < CHB ? px * RBB + ((cc ^ swz_kk<RBB>(px)) << 4) : -1;
   }
   const unsigned arow = (unsigned)(a.WA * a.lda * 2), brow = (unsigned)(a.WB * a.ldb * 2);
-  u32x4_t ra[LA], rb[LB];
+  u32x4_t ra[LA], rb[LB], rz[ABN ? LA : 1];
   int n = ig * ipb;
   auto load_a = [&](int h) {
     const unsigned base = (unsigned)h * arow;
 #pragma unroll
     for (int j = 0; j < LA; ++j) ra[j] = __builtin_amdgcn_raw_buffer_load_b128(ar, asto[j] >= 0 ? base + aoff[j] : 0x80000000u, 0, 0);
+    if constexpr (ABN) {
+#pragma unroll
+      for (int j = 0; j < LA; ++j) rz[j] = __builtin_amdgcn_raw_buffer_load_b128(zr, asto[j] >= 0 ? base + aoff[j] : 0x80000000u, 0, 0);
+    }
+  };
+  // ABN: (g, z) chunk -> dz chunk; pixels past the row stay zero (they add nothing to dW / db)
+  auto xform_a = [&]() {
+    if constexpr (ABN) {
+#pragma unroll
+      for (int j = 0; j < LA; ++j) {
+        const int c = tid + j * NT, cb = (c % CPRA) * 8;
+        const bool ok = asto[j] >= 0 && aoff[j] != 0x80000000u;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int ch = cb + 2 * e;
+          const float v0 = fmaf(abc[ch], lo_bf(ra[j][e]), fmaf(abc[BM + ch], lo_bf(rz[j][e]), abc[2 * BM + ch]));
+          const float v1 = fmaf(abc[ch + 1], hi_bf(ra[j][e]), fmaf(abc[BM + ch + 1], hi_bf(rz[j][e]), abc[2 * BM + ch + 1]));
+          ra[j][e] = ok ? pack_bf2(v0, v1) : 0u;
+        }
+      }
+    }
   };
   auto load_b = [&](int ih) {
     const bool rok = ih >= 0 && ih < a.HB;
@@ -1264,6 +1290,7 @@ __global__ __launch_bounds__(192) void wgrad_stream_kernel(WgradArgs a, int ipb)
   for (int im = 0; im < nimg; ++im, ++n) {
   ar = __builtin_amdgcn_make_buffer_rsrc((void*)(a.atab ? a.atab[n] : a.A + (long)n * a.HA * a.WA * a.lda), 0, (int)a.abytes, 0x00020000);
   br = __builtin_amdgcn_make_buffer_rsrc((void*)(a.btab ? a.btab[n] : a.B + (long)n * a.HB * a.WB * a.ldb), 0, (int)a.bbytes, 0x00020000);
+  if constexpr (ABN) zr = __builtin_amdgcn_make_buffer_rsrc((void*)(a.az + (long)n * a.HA * a.WA * a.lda), 0, (int)a.abytes, 0x00020000);
   // prologue: input rows h0-1, h0, h0+1 -> ring slots 0..2; gradient row h0 -> A buffer 0
   if (nrows > 0) {
 #pragma unroll 1
@@ -1272,6 +1299,7 @@ __global__ __launch_bounds__(192) void wgrad_stream_kernel(WgradArgs a, int ipb)
       store_b(j);
     }
     load_a(h0);
+    xform_a();
     store_a(0);
   }
   __syncthreads();
@@ -1316,6 +1344,7 @@ __global__ __launch_bounds__(192) void wgrad_stream_kernel(WgradArgs a, int ipb)
     }
     __builtin_amdgcn_sched_barrier(0);
     if (more) {
+      xform_a();
       store_a((r + 1) & 1);
       store_b((r + 3) & 3);
     }
@@ -1349,10 +1378,10 @@ __global__ __launch_bounds__(192) void wgrad_stream_kernel(WgradArgs a, int ipb)
   }
 }
 
-template <int BM, int BN, int BP, int RH>
+template <int BM, int BN, int BP, int RH, bool ABN = false>
 static int launch_wgrad_stream(const WgradArgs& a, int ipb, hipStream_t st) {
   const int tiles = (a.M / BM) * ((a.Nc + BN - 1) / BN);
-  hipLaunchKernelGGL((wgrad_stream_kernel<BM, BN, BP, RH>), dim3(tiles * a.splits), dim3(192), 0, st, a, ipb);
+  hipLaunchKernelGGL((wgrad_stream_kernel<BM, BN, BP, RH, ABN>), dim3(tiles * a.splits), dim3(192), 0, st, a, ipb);
   return (int)hipGetLastError();
 }
 
@@ -1367,6 +1396,14 @@ DPA_API int dpa_wgrad_stream(const WgradArgs* args, int cfg, int bp, int rh, int
       a.HB != a.Hg || a.WB != a.Wg || a.Wg < 8 ||
       a.splits != ((a.N + ipb - 1) / ipb) * ((a.Hg + rh - 1) / rh) * ((a.Wg + bp - 1) / bp))
     return (int)hipErrorInvalidValue;
+  // BatchNorm backward on load of the gradient: the first layer's tile only (the other 32/64-channel
+  // layers of a BN model take the fused backward, csrc/bwd_stream.hip, which does the same on load)
+  if (a.abn != nullptr || a.az != nullptr) {
+    if (!(a.abn && a.az) || a.atab || cfg != 4 || a.Nc != 8 || a.M % 32 || bp != 64) return (int)hipErrorInvalidValue;
+    if (rh == 64) return launch_wgrad_stream<32, 16, 64, 64, true>(a, ipb, st);
+    if (rh == 32) return launch_wgrad_stream<32, 16, 64, 32, true>(a, ipb, st);
+    return (int)hipErrorInvalidValue;
+  }
 #define DPA_WS(C, BMv, BNv, BPv, RHv)                                                              \
   if (cfg == C && bp == BPv && rh == RHv && a.M % BMv == 0 && a.Nc % BNv == 0) return launch_wgrad_stream<BMv, BNv, BPv, RHv>(a, ipb, st);
   DPA_WS(1, 32, 32, 64, 64)

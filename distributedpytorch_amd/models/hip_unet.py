@@ -485,8 +485,15 @@ class HipBlocks:
         return (K.USE_FUSED_HEAD_BWD and c2.Cin == 32 and c2.Cout == 32 and self.model.segmap.out_channels == 1
                 and self.fusable(c2, c1, W, whole=True))
 
-    def conv_wgrad(self, c: _Conv, g: torch.Tensor, x: torch.Tensor):
+    def conv_wgrad(self, c: _Conv, g: torch.Tensor, x: torch.Tensor, gbn=None):
+        """Weight + bias gradient of ``c`` (side stream).  ``gbn`` = (z, coef3): ``g`` is the gradient of
+        c's BatchNorm+ReLU output and dz is formed on load (:func:`K.wgrad` ``abn``; first conv only)."""
         N, H, W = g.shape[:3]
+        if gbn is not None:
+            gw, gb = _grad(c.mod.weight), _grad(c.mod.bias)
+            self._side_launch(lambda: K.wgrad(g, x, kind=0, grid=(N, H, W), M=c.Cout, Nc=c.Cs, s=1, pad=1, KW=3,
+                                              gw=gw.view(-1), gb=gb, Nreal=c.Cin, abn=gbn), g, x, *gbn)
+            return
         if self.defer_wgrad > 1 and K.wgrad_multi_eligible(c.Cout, c.Cs, W):
             self._release_done()
             ent = self._deferred.setdefault(id(c), (c, [], []))
@@ -873,6 +880,14 @@ class _EncFn(torch.autograd.Function):
         if ctx.x_needs_grad and B.fusable(c1, None, W):
             # the pool backward below applies the ReLU mask
             gx, _ = B.bwd_conv(c1, g1, x, st1, mask=False, stats=st_g)
+        elif (not ctx.x_needs_grad and c1.bn is not None and K.BN_WGRAD_ON_LOAD and B.defer_wgrad <= 1
+              and K.wgrad_bn_eligible(c1.Cout, c1.Cs, W) and g1.is_contiguous() and st1[0].is_contiguous()):
+            # the first conv (no input gradient): its BN backward is formed in the weight gradient's loader from
+            # per-channel coefficients -- the full-resolution dz pass (write + read) never happens
+            z1, saved1 = st1[:2]
+            coef3 = K.bn_bwd_coef(g1, z1, saved1, c1.bn, _grad(c1.bn.weight), _grad(c1.bn.bias), stats=st_g)
+            B.conv_wgrad(c1, g1, x, gbn=(z1, coef3))
+            gx = None
         else:
             g1 = B.bn_bwd(c1, g1, st1, stats=st_g)
             B.conv_wgrad(c1, g1, x)

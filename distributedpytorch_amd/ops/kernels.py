@@ -38,7 +38,8 @@ class WgradArgs(ctypes.Structure):
     _fields_ = [("A", c_void_p), ("B", c_void_p), ("slab", c_void_p), ("bslab", c_void_p)] + \
                [(n, c_int) for n in ("lda", "ldb", "N", "Hg", "Wg", "HA", "WA", "HB", "WB", "M", "Nc", "s", "pad",
                                      "KW", "pix_per_split", "splits")] + \
-               [("abytes", ctypes.c_uint), ("bbytes", ctypes.c_uint), ("atab", c_void_p), ("btab", c_void_p)]
+               [("abytes", ctypes.c_uint), ("bbytes", ctypes.c_uint), ("atab", c_void_p), ("btab", c_void_p),
+                ("az", c_void_p), ("abn", c_void_p)]
 
 
 class BwdArgs(ctypes.Structure):
@@ -98,6 +99,7 @@ BN_SUMS_POOL = CFG.bn_sums_pool        # BN backward partial sums from the pool 
 BN_SUMS_DECONV = CFG.bn_sums_deconv    # ... from the fused transposed-conv backward
 BN_SUMS_POOL_Z = CFG.bn_sums_pool_z    # ... reading the dense z (relu(bn(z)) re-formed) instead of the skip
 BN_HEAD_ON_LOAD = CFG.bn_head_on_load  # the head reads the last decoder BN's input z (relu(bn(z)) on load)
+BN_WGRAD_ON_LOAD = CFG.bn_wgrad_on_load  # the first conv's BN backward in its weight gradient's loader
 BN_HEAD_DEFER = CFG.bn_head_defer      # ... with its backward deferred into the decoder's (memory)
 # 128-channel convs on the row-block ping-pong GEMM (cfg 15) instead of the row-halo conv: 10-15 % faster
 # on every 128-output-channel 3x3 conv / dgrad of the 512^2 UNet (profiles/kbench_glds_rowblock128_b256_r03.txt)
@@ -374,14 +376,26 @@ def wgrad_splits(P: int, tiles: int, target_blocks: int = 1024, min_pix: int = 5
     return splits, pps
 
 
+def wgrad_bn_eligible(M: int, Nc: int, W: int) -> bool:
+    """Can :func:`wgrad` form a BatchNorm backward on load of its gradient (``abn``)?  The first conv
+    (8-padded RGB input) on the row-streaming kernel."""
+    return USE_STREAM and Nc == 8 and M % 32 == 0 and W >= 8 and "wgrad" not in _ABLATE
+
+
 def wgrad(A: torch.Tensor, B: torch.Tensor, *, kind: int, grid, M: int, Nc: int, s: int, pad: int, KW: int,
           gw: torch.Tensor, gb: Optional[torch.Tensor], Nreal: int, cfg: int = 0, target_blocks: int = 1024,
-          path: str = "auto"):
+          path: str = "auto", abn=None):
     """Weight (+bias) gradient of a conv3x3 (kind 0), transposed conv 2x2/s2 (kind 1) or conv1x1
     (kind 2); accumulates into gw/gb.
 
     ``path``: ``auto`` = row-streaming kernel when W % 64 == 0, else row-halo (W % 32 == 0), else the
-    generic per-tap gather kernel; ``stream`` / ``halo`` / ``generic`` force one."""
+    generic per-tap gather kernel; ``stream`` / ``halo`` / ``generic`` force one.
+    ``abn`` = (z, coef3): ``A`` is the ReLU-masked gradient of a BatchNorm output whose input is ``z``; the
+    GEMM uses dz = coef3[m] A + coef3[M + m] z + coef3[2M + m] formed on load (:func:`bn_bwd_coef`), so the
+    dz pass over HBM never happens (:func:`wgrad_bn_eligible` shapes)."""
+    if abn is not None:
+        assert kind == 0 and cfg == 0 and path in ("auto", "stream") and wgrad_bn_eligible(M, Nc, grid[2])
+        return _wgrad_stream(A, B, grid=grid, M=M, Nc=Nc, gw=gw, gb=gb, Nreal=Nreal, abn=abn)
     if _ABLATE and ("wgrad" in _ABLATE or ("wgrad_deep" in _ABLATE and (M >= 128 or Nc >= 128))):
         return
     if (path == "gemm" or (path == "auto" and wgrad_gemm_eligible(M, Nc, grid))) and kind == 0 and cfg == 0 \
@@ -527,7 +541,7 @@ def wgrad_multi(As, Bs, *, M: int, Nc: int, gw: torch.Tensor, gb: Optional[torch
     return _wgrad_stream(As[0], Bs[0], grid=(N, H, W), M=M, Nc=Nc, gw=gw, gb=gb, Nreal=Nreal, tabs=tabs)
 
 
-def _wgrad_stream(A, B, *, grid, M, Nc, gw, gb, Nreal, tabs=None):
+def _wgrad_stream(A, B, *, grid, M, Nc, gw, gb, Nreal, tabs=None, abn=None):
     NA, HA, WA, CA, lda = _nhwc(A, "wgrad.A")
     NB, HB, WB, CB, ldb = _nhwc(B, "wgrad.B")
     N, Hg, Wg = grid
@@ -564,6 +578,11 @@ def _wgrad_stream(A, B, *, grid, M, Nc, gw, gb, Nreal, tabs=None):
                   _extent_bytes(1, HB, WB, CB, ldb))
     if tabs is not None:
         a.atab, a.btab = tabs[0].data_ptr(), tabs[1].data_ptr()
+    if abn is not None:
+        z, coef3 = abn
+        assert tabs is None and z.dtype == torch.bfloat16 and z.shape == A.shape and z.stride() == A.stride()
+        assert coef3.dtype == torch.float32 and coef3.is_contiguous() and coef3.numel() == 3 * M and CA == M
+        a.az, a.abn = z.data_ptr(), coef3.data_ptr()
     _check(L.dpa_wgrad_stream(ctypes.byref(a), c_int(hcfg), c_int(bp), c_int(rh), c_int(ipb), st), "wgrad_stream")
     _check(L.dpa_wgrad_reduce(_p(slab), _p(bslab), _p(gw), _p(gb), c_int(splits), c_int(9), c_int(M), c_int(Nc),
                               c_int(Nreal), c_int(0), st), "wgrad_reduce")

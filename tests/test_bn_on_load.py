@@ -197,3 +197,88 @@ def test_unet_bn_head_on_load_equals_materialised(hip_lib, monkeypatch, model):
     assert torch.allclose(g0, g1, rtol=1e-3, atol=1e-4 * g0.abs().max().item())
     for k in r0:
         assert torch.equal(r0[k], r1[k]), k
+
+
+def test_first_conv_wgrad_bn_on_load(hip_lib):
+    """The first conv's weight gradient forming dz = a g + b z + c on load (K.wgrad ``abn``) == bn_bwd's dz
+    pass followed by the plain weight gradient, bit for bit (same dz bf16 values, same kernel and order)."""
+    from distributedpytorch_amd.ops import kernels as K
+    torch.manual_seed(11)
+    N, H, W, C = 2, 40, 128, 32
+    x8 = torch.zeros(N, H, W, 8, dtype=torch.bfloat16, device="cuda")
+    x8[..., :3] = torch.randn(N, H, W, 3, device="cuda").to(torch.bfloat16)
+    z = (torch.randn(N, H, W, C, device="cuda") * 1.3 + 0.2).to(torch.bfloat16)
+    g = torch.randn(N, H, W, C, device="cuda").to(torch.bfloat16)
+    res = []
+    for on_load in (False, True):
+        torch.manual_seed(12)
+        bn = torch.nn.BatchNorm2d(C).cuda()
+        with torch.no_grad():
+            bn.weight.uniform_(0.5, 1.5)
+            bn.bias.uniform_(-0.5, 0.5)
+        y = torch.empty_like(z)
+        saved = K.bn_fwd(z, y, bn, train=True)
+        gm = torch.where(y > 0, g, torch.zeros_like(g))          # the ReLU-masked gradient of the BN output
+        dgam, dbet = torch.zeros(C, device="cuda"), torch.zeros(C, device="cuda")
+        gw, gb = torch.zeros(C * 3 * 9, device="cuda"), torch.zeros(C, device="cuda")
+        if on_load:
+            coef3 = K.bn_bwd_coef(gm, z, saved, bn, dgam, dbet)
+            K.wgrad(gm, x8, kind=0, grid=(N, H, W), M=C, Nc=8, s=1, pad=1, KW=3, gw=gw, gb=gb, Nreal=3,
+                    abn=(z, coef3))
+        else:
+            dz = K.bn_bwd(gm, z, saved, bn, dgam, dbet)
+            K.wgrad(dz, x8, kind=0, grid=(N, H, W), M=C, Nc=8, s=1, pad=1, KW=3, gw=gw, gb=gb, Nreal=3, path="stream")
+        torch.cuda.synchronize()
+        res.append((gw.cpu(), gb.cpu(), dgam.cpu(), dbet.cpu()))
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
+    # anchored: fp32 PyTorch weight gradient of the same dz
+    dz = K.bn_bwd(gm, z, saved, bn, torch.zeros(C, device="cuda"), torch.zeros(C, device="cuda")).float()
+    xr = x8[..., :3].float().permute(0, 3, 1, 2).requires_grad_(False)
+    wr = torch.zeros(C, 3, 3, 3, device="cuda", requires_grad=True)
+    out = torch.nn.functional.conv2d(xr, wr, padding=1)
+    out.backward(dz.permute(0, 3, 1, 2))
+    ref = wr.grad.reshape(-1).cpu()
+    assert (res[1][0] - ref).norm() / ref.norm() < 1e-2
+
+
+def test_unet_bn_step_first_conv_wgrad_on_load_equals_materialised(hip_lib, monkeypatch):
+    """A whole BN-UNet step with the first conv's BN backward in its weight-gradient loader == the step with
+    the dz pass, bit for bit (loss, gradients, running statistics); the on-load path must be taken."""
+    from distributedpytorch_amd.compute import loss_from_partials, make_compute
+    from distributedpytorch_amd.data.synthetic import synthetic_batch
+    from distributedpytorch_amd.models.unet import build_model
+    from distributedpytorch_amd.optim import FlatParameterSpace
+    from distributedpytorch_amd.ops import kernels as K
+
+    torch.manual_seed(0)
+    net = build_model("unet-bn").cuda()
+    space = FlatParameterSpace(net)
+    comp = make_compute(net, backend="hip", dtype="bf16")
+    img, mask = synthetic_batch(2, 64, 256, 3, seed=7)
+    x, t = img.cuda(), mask.float().unsqueeze(1).cuda()
+    state0 = {k: v.clone() for k, v in net.state_dict().items() if "running" in k or "num_batches" in k}
+    used = []
+    real = K.wgrad
+
+    def spy(*a, **kw):
+        used.append(kw.get("abn") is not None)
+        return real(*a, **kw)
+
+    monkeypatch.setattr(K, "wgrad", spy)
+
+    def run():
+        net.load_state_dict(state0, strict=False)
+        space.zero_grad()
+        used.clear()
+        S = comp.forward_partials(x, t)
+        loss = loss_from_partials(S, t.numel())
+        loss.backward()
+        torch.cuda.synchronize()
+        return loss.item(), space.grad.clone(), sum(used)
+
+    l1, g1, n1 = run()
+    monkeypatch.setattr(K, "BN_WGRAD_ON_LOAD", False)
+    l0, g0, n0 = run()
+    assert n1 == 1 and n0 == 0
+    assert l0 == l1 and torch.equal(g0, g1)
