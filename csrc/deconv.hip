@@ -19,12 +19,16 @@
 
 // BNS: x is a BatchNorm+ReLU output (the decoder conv's below): also that BN's backward partial sums of the
 // STORED masked dx, sum dx[ci] and sum dx[ci] * x[ci], per block -> bnslab[block][2][CIN] (no statistics pass)
-template <int CIN, int COUT, bool BNS = false>
+// XBN: x holds the layer below's pre-BN output z and x = relu(z * xbn[c] + xbn[CIN + c]) is formed when the
+// staged chunk goes to LDS (bn_apply's arithmetic; pixels past the batch stay zero) -- that BN output is
+// never written in the forward (deconv_fwd_kernel XBN)
+template <int CIN, int COUT, bool BNS = false, bool XBN = false>
 __global__ __launch_bounds__(512) void deconv_bwd_kernel(const bf16_t* __restrict__ g, int ldg, const bf16_t* __restrict__ x,
                                                         int ldx, const bf16_t* __restrict__ wd, bf16_t* __restrict__ dx,
                                                         int lddx, float* __restrict__ slab, float* __restrict__ bslab,
                                                         int N, int h, int w, int tiles_per_block, unsigned gbytes,
-                                                        unsigned xbytes, float* __restrict__ bnslab) {
+                                                        unsigned xbytes, float* __restrict__ bnslab,
+                                                        const float* __restrict__ xbn) {
   constexpr int P = 64;                       // low-resolution pixels per tile
   constexpr int K4 = 4 * COUT;                // dgrad K / wgrad N
   constexpr int RBX = CIN * 2, RBG = K4 * 2;  // LDS row bytes
@@ -38,6 +42,7 @@ __global__ __launch_bounds__(512) void deconv_bwd_kernel(const bf16_t* __restric
   constexpr int NRG = 512 / K4;               // bias-gradient row groups
   static_assert(NCG * NPG == 8 && TPX >= 1 && NRG >= 1 && 512 % K4 == 0, "tiling");
   __shared__ __attribute__((aligned(16))) char lds[P * (RBX + RBG)];
+  __shared__ float xbc[XBN ? 2 * CIN : 4];
   char* const ximg = lds;
   char* const gimg = lds + P * RBX;
 
@@ -45,6 +50,10 @@ __global__ __launch_bounds__(512) void deconv_bwd_kernel(const bf16_t* __restric
   const int M = N * h * w;
   const int ntiles = (M + P - 1) / P;
   const int split = blockIdx.x;
+  if constexpr (XBN) {
+    for (int i = tid; i < 2 * CIN; i += 512) xbc[i] = xbn[i];
+    __syncthreads();
+  }
   const int t0 = split * tiles_per_block;
   const int t1 = min(ntiles, t0 + tiles_per_block);
   const __amdgpu_buffer_rsrc_t gr = __builtin_amdgcn_make_buffer_rsrc((void*)g, 0, (int)gbytes, 0x00020000);
@@ -94,10 +103,20 @@ __global__ __launch_bounds__(512) void deconv_bwd_kernel(const bf16_t* __restric
       }
     }
   };
-  auto lstore = [&]() {
+  auto lstore = [&](int t) {
 #pragma unroll
     for (int j = 0; j < L; ++j) {
       if (lsto[j] < 0) continue;
+      if (XBN && !isg[j]) {
+        const bool ok = t * P + cpix[j] < M;
+        const int cb = cofs[j] * 8;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float v0 = fmaxf(fmaf(lo_bf(reg[j][e]), xbc[cb + 2 * e], xbc[CIN + cb + 2 * e]), 0.f);
+          const float v1 = fmaxf(fmaf(hi_bf(reg[j][e]), xbc[cb + 2 * e + 1], xbc[CIN + cb + 2 * e + 1]), 0.f);
+          reg[j][e] = ok ? pack_bf2(v0, v1) : 0u;
+        }
+      }
       char* dst = isg[j] ? gimg + lsto[j] : ximg + (lsto[j] - P * RBG);
       *reinterpret_cast<u32x4_t*>(dst) = reg[j];
     }
@@ -132,7 +151,7 @@ __global__ __launch_bounds__(512) void deconv_bwd_kernel(const bf16_t* __restric
 
   if (t0 < t1) {
     gload(t0);
-    lstore();
+    lstore(t0);
   }
   __syncthreads();
 #pragma unroll 1
@@ -195,7 +214,7 @@ __global__ __launch_bounds__(512) void deconv_bwd_kernel(const bf16_t* __restric
     __builtin_amdgcn_sched_barrier(0);
     __syncthreads();
     if (more) {
-      lstore();
+      lstore(t + 1);
       __syncthreads();
     }
   }
@@ -254,21 +273,23 @@ __global__ __launch_bounds__(512) void deconv_bwd_kernel(const bf16_t* __restric
   }
 }
 
-// bnslab (or null): [splits][2][Cin] BatchNorm backward partial sums of the stored dx (deconv_bwd_kernel BNS)
+// bnslab (or null): [splits][2][Cin] BatchNorm backward partial sums of the stored dx (deconv_bwd_kernel BNS);
+// xbn (or null, needs bnslab): x is the pre-BN z, x = relu(bn(z)) formed on load (XBN)
 DPA_API int dpa_deconv_bwd(const bf16_t* g, int ldg, const bf16_t* x, int ldx, const bf16_t* wd, bf16_t* dx, int lddx,
                            float* slab, float* bslab, int N, int h, int w, int Cin, int Cout, int splits,
-                           unsigned gbytes, unsigned xbytes, float* bnslab, hipStream_t st) {
+                           unsigned gbytes, unsigned xbytes, float* bnslab, const float* xbn, hipStream_t st) {
+  if (xbn && !bnslab) return (int)hipErrorInvalidValue;
   if ((ldg & 7) || (ldx & 7) || (lddx & 3) || splits < 1) return (int)hipErrorInvalidValue;
   const long M = (long)N * h * w;
   const int ntiles = (int)((M + 63) / 64);
   const int tpb = (ntiles + splits - 1) / splits;
   if ((long)(splits - 1) * tpb >= ntiles) return (int)hipErrorInvalidValue;   // every split owns >= 1 tile
-#define DPA_DB(CI, CO, BN) hipLaunchKernelGGL((deconv_bwd_kernel<CI, CO, BN>), dim3(splits), dim3(512), 0, st, g, ldg, x, ldx, \
-                                              wd, dx, lddx, slab, bslab, N, h, w, tpb, gbytes, xbytes, bnslab)
+#define DPA_DB(CI, CO, BN, XB) hipLaunchKernelGGL((deconv_bwd_kernel<CI, CO, BN, XB>), dim3(splits), dim3(512), 0, st, g, ldg, x, \
+                                                  ldx, wd, dx, lddx, slab, bslab, N, h, w, tpb, gbytes, xbytes, bnslab, xbn)
   if (Cin == 64 && Cout == 32) {
-    if (bnslab) DPA_DB(64, 32, true); else DPA_DB(64, 32, false);
+    if (xbn) DPA_DB(64, 32, true, true); else if (bnslab) DPA_DB(64, 32, true, false); else DPA_DB(64, 32, false, false);
   } else if (Cin == 128 && Cout == 64) {
-    if (bnslab) DPA_DB(128, 64, true); else DPA_DB(128, 64, false);
+    if (xbn) DPA_DB(128, 64, true, true); else if (bnslab) DPA_DB(128, 64, true, false); else DPA_DB(128, 64, false, false);
   } else {
     return (int)hipErrorInvalidValue;
   }
@@ -283,10 +304,12 @@ DPA_API int dpa_deconv_bwd(const bf16_t* g, int ldg, const bf16_t* x, int ldx, c
 // ([(2i+j)*Cout + co][ci], 4*Cout x Cin) in VGPRs (wave w owns rows w*4*Cout/8 ..), and the output
 // tile staged in LDS so the global stores are whole 16-B chunks ordered along each output row
 // (the MFMA layout alone would give 8-B pieces scattered over four sub-pixel rows).
-template <int CIN, int COUT>
+// XBN: x is the layer below's pre-BN output z, relu(bn(z)) formed when the staged chunk goes to LDS
+template <int CIN, int COUT, bool XBN = false>
 __global__ __launch_bounds__(512) void deconv_fwd_kernel(const bf16_t* __restrict__ x, int ldx, const bf16_t* __restrict__ wf,
                                                         const float* __restrict__ bias, bf16_t* __restrict__ y, int ldy,
-                                                        int N, int h, int w, int tiles_per_block, unsigned xbytes) {
+                                                        int N, int h, int w, int tiles_per_block, unsigned xbytes,
+                                                        const float* __restrict__ xbn) {
   constexpr int P = 64;
   constexpr int K4 = 4 * COUT;                 // GEMM N (output sub-pixel x channel)
   constexpr int RBX = CIN * 2, RBO = K4 * 2;
@@ -300,6 +323,7 @@ __global__ __launch_bounds__(512) void deconv_fwd_kernel(const bf16_t* __restric
   constexpr int LO = (CO + 511) / 512;
   static_assert(NT_W >= 1 && CX % 512 == 0 && CO % 512 == 0, "tiling");
   __shared__ __attribute__((aligned(16))) char lds[P * (RBX + RBO)];
+  __shared__ float xbc[XBN ? 2 * CIN : 4];
   char* const ximg = lds;
   char* const oimg = lds + P * RBX;
 
@@ -341,9 +365,19 @@ __global__ __launch_bounds__(512) void deconv_fwd_kernel(const bf16_t* __restric
 #pragma unroll
     for (int j = 0; j < LX; ++j) {
       const int c = tid + j * 512, p = c / CPX, xc = c - p * CPX;
+      if constexpr (XBN) {   // pixels past the batch: relu(shift), never stored (outputs are per pixel)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          reg[j][e] = pack_bf2(fmaxf(fmaf(lo_bf(reg[j][e]), xbc[xc * 8 + 2 * e], xbc[CIN + xc * 8 + 2 * e]), 0.f),
+                               fmaxf(fmaf(hi_bf(reg[j][e]), xbc[xc * 8 + 2 * e + 1], xbc[CIN + xc * 8 + 2 * e + 1]), 0.f));
+      }
       *reinterpret_cast<u32x4_t*>(ximg + p * RBX + ((xc ^ swz_kk<RBX>(p)) << 4)) = reg[j];
     }
   };
+  if constexpr (XBN) {
+    for (int i = tid; i < 2 * CIN; i += 512) xbc[i] = xbn[i];
+    __syncthreads();
+  }
 
   if (t0 < t1) {
     gload(t0);
@@ -401,18 +435,23 @@ __global__ __launch_bounds__(512) void deconv_fwd_kernel(const bf16_t* __restric
   }
 }
 
+// xbn (or null): x is the pre-BN z of a BatchNorm+ReLU layer, x = relu(z * xbn[c] + xbn[Cin + c]) (XBN)
 DPA_API int dpa_deconv_fwd(const bf16_t* x, int ldx, const bf16_t* wf, const float* bias, bf16_t* y, int ldy, int N, int h,
-                           int w, int Cin, int Cout, int blocks, unsigned xbytes, hipStream_t st) {
+                           int w, int Cin, int Cout, int blocks, unsigned xbytes, const float* xbn, hipStream_t st) {
   if ((ldx & 7) || (ldy & 7) || blocks < 1) return (int)hipErrorInvalidValue;
   const long M = (long)N * h * w;
   const int ntiles = (int)((M + 63) / 64);
   const int tpb = (ntiles + blocks - 1) / blocks;
   const int grid = (ntiles + tpb - 1) / tpb;
-  if (Cin == 64 && Cout == 32)
-    hipLaunchKernelGGL((deconv_fwd_kernel<64, 32>), dim3(grid), dim3(512), 0, st, x, ldx, wf, bias, y, ldy, N, h, w, tpb, xbytes);
-  else if (Cin == 128 && Cout == 64)
-    hipLaunchKernelGGL((deconv_fwd_kernel<128, 64>), dim3(grid), dim3(512), 0, st, x, ldx, wf, bias, y, ldy, N, h, w, tpb, xbytes);
-  else
+#define DPA_DF(CI, CO, XB) hipLaunchKernelGGL((deconv_fwd_kernel<CI, CO, XB>), dim3(grid), dim3(512), 0, st, x, ldx, wf, bias, y, ldy, \
+                                              N, h, w, tpb, xbytes, xbn)
+  if (Cin == 64 && Cout == 32) {
+    if (xbn) DPA_DF(64, 32, true); else DPA_DF(64, 32, false);
+  } else if (Cin == 128 && Cout == 64) {
+    if (xbn) DPA_DF(128, 64, true); else DPA_DF(128, 64, false);
+  } else {
     return (int)hipErrorInvalidValue;
+  }
+#undef DPA_DF
   return (int)hipGetLastError();
 }

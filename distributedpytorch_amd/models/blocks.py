@@ -180,8 +180,15 @@ def run_segment(blocks, start: int, end: int, depth: int, env: Dict[str, torch.T
         blocks.expect_target(target)      # lets a backend fuse the head into the last decoder conv
     if start == 0:
         env["x"] = blocks.prep(env["x"])
-    for idx, part in segment_units(start, end, depth):
+    units = segment_units(start, end, depth)
+    for u, (idx, part) in enumerate(units):
         kind, i = block_kind(idx, depth)
+        if kind == "dec" and hasattr(blocks, "next_dec_local"):
+            # the next unit is a whole decoder block of this same segment: a backend may hand it its input in
+            # an internal form (models/hip_unet.py: a BatchNorm's input z, normalised on load)
+            nxt = units[u + 1] if u + 1 < len(units) else None
+            blocks.next_dec_local = (part == "full" and nxt is not None and nxt[1] == "full"
+                                     and block_kind(nxt[0], depth)[0] == "dec")
         tag = (f"{kind}{i}" if kind in ("enc", "dec") else kind) + ("" if part == "full" else part)
         with trace_range(tag):
             if kind == "enc":

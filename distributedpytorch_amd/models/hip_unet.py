@@ -140,6 +140,10 @@ class HipBlocks:
         # gradients whose producer also wrote the consumer BatchNorm's backward partial sums (the head and
         # the fused transposed-conv backward): data_ptr -> (shape, stride, (slab, rows)); see take_stats
         self._stats_hand = {}
+        # decoder outputs handed to the next decoder block as their BatchNorm input z (run_segment sets
+        # next_dec_local when that block follows in the same segment): z data_ptr -> (z, coef)
+        self.next_dec_local = False
+        self._zx = {}
         # pipeline microbatches: the side-stream conv weight gradients of every microbatch are deferred
         # and run as ONE launch per layer over all microbatches' images (K.wgrad_multi) -- one split-K
         # slab set and reduction per step instead of one per microbatch.  Flushed at the end of the
@@ -530,8 +534,12 @@ class HipBlocks:
         if pending:
             self._notify(pending)
 
-    def deconv_fwd(self, d: _Deconv, x: torch.Tensor, out: torch.Tensor):
+    def deconv_fwd(self, d: _Deconv, x: torch.Tensor, out: torch.Tensor, xbn: torch.Tensor = None):
+        """``xbn``: ``x`` is the level below's BatchNorm input z, read as relu(bn(z)) (fused shapes only)."""
         N, h, w = x.shape[:3]
+        if xbn is not None:
+            K.deconv_fwd_fused(x, self.wf(d), d.mod.bias, out, xbn=xbn)
+            return
         if isinstance(d, _Up):
             low = torch.empty(N, h, w, d.Cout, dtype=torch.bfloat16, device=x.device)
             K.igemm(x, self.wf(d), low, Ngemm=d.Cout, Kpad=d.Kf, KH=1, KW=1, stride=1, pad=0, Cs=d.Cin,
@@ -565,16 +573,16 @@ class HipBlocks:
         self._side_launch(lambda: K.wgrad(gup, x, kind=1, grid=(N, h, w), M=d.Cout, Nc=d.Cin, s=2, pad=0, KW=2,
                                           gw=gw, gb=gb, Nreal=d.Cin), gup, x)
 
-    def deconv_bwd(self, d, gup: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
+    def deconv_bwd(self, d, gup: torch.Tensor, x: torch.Tensor, xbn: torch.Tensor = None) -> torch.Tensor:
         """dgrad + weight gradient of the up-path layer; the full-resolution transposed convs run
         both in one pass over (gup, x) (csrc/deconv.hip).  Elsewhere the weight gradient goes to the
-        side stream first, then the dgrad runs on the compute stream."""
+        side stream first, then the dgrad runs on the compute stream.  ``xbn``: as :meth:`deconv_fwd`."""
         if isinstance(d, _Deconv) and K.USE_FUSED_DECONV and (d.Cin, d.Cout) in K.DECONV_BWD_SHAPES:
             # x is the BatchNorm+ReLU output of the level below (a BN model): its BN's backward partial sums
             # come from this kernel's dx epilogue
-            stats = [] if (self.enc_convs[0][1].bn is not None and K.BN_SUMS_DECONV) else None
+            stats = [] if (xbn is not None or (self.enc_convs[0][1].bn is not None and K.BN_SUMS_DECONV)) else None
             dx = K.deconv_bwd_fused(gup, x, self.wd(d), _grad(d.mod.weight).view(-1), _grad(d.mod.bias),
-                                    bn_stats=stats)
+                                    bn_stats=stats, xbn=xbn)
             self.hand_stats(dx, stats)
             return dx
         self.deconv_wgrad(d, gup, x)
@@ -652,6 +660,7 @@ class HipBlocks:
 
     # ------------------------------------------------------------------ block API
     def prep(self, x: torch.Tensor) -> torch.Tensor:
+        self._zx.clear()
         if x.dtype == torch.bfloat16 and x.dim() == 4 and x.shape[1] == 8:
             return x   # already converted (logical NCHW8, channels_last)
         return _o(K.input_nhwc8(x.float()))
@@ -939,6 +948,11 @@ class _DecFn(torch.autograd.Function):
         C = d.Cout
         x = _v(x)
         skip = _v(skip)
+        # x may be the previous decoder block's BatchNorm input z (see below): the transposed conv reads
+        # relu(bn(z)) on load, forward and backward
+        zx = B._zx.pop(x.data_ptr(), None)
+        dxbn = zx[1] if (zx is not None and zx[0].shape == x.shape and zx[0].stride() == x.stride()) else None
+        local_next, B.next_dec_local = B.next_dec_local, False
         Ns, Hs, Ws, _ = skip.shape
         h2, w2 = 2 * x.shape[1], 2 * x.shape[2]
         ctx.crop = None
@@ -957,7 +971,7 @@ class _DecFn(torch.autograd.Function):
         else:
             cat = B.cat_for(skip)
             up = None
-        B.deconv_fwd(d, x, cat[..., C:] if up is None else up)
+        B.deconv_fwd(d, x, cat[..., C:] if up is None else up, xbn=dxbn)
         st1, st2 = [], []
         xbn1 = None
         if up is None and B.bn_on_load(c1, c2, h2, w2):
@@ -977,6 +991,14 @@ class _DecFn(torch.autograd.Function):
                         out_grid=(N, H, W), bias=c2.mod.bias, relu=True,
                         head=(seg.weight.view(-1), seg.bias, tgt, hprob))
             B._head_cache = (y.data_ptr(), tgt.data_ptr(), S, hprob)
+        elif (local_next and tgt is None and c2.bn is not None and K.BN_DECONV_ON_LOAD and B.model.training
+              and i + 1 < len(B.deconvs) and isinstance(B.deconvs[i + 1], _Deconv) and K.USE_FUSED_DECONV
+              and (B.deconvs[i + 1].Cin, B.deconvs[i + 1].Cout) in K.DECONV_BWD_SHAPES
+              and B.deconvs[i + 1].Cin == c2.Cout):
+            # BatchNorm model: the next decoder block's transposed conv reads relu(bn(z)) on load (forward and
+            # backward), so this BN output is never written; the returned tensor is z, recognised there
+            y, coef = B.conv_bn_z(c2, a, st2, xbn=xbn1)
+            B._zx[y.data_ptr()] = (y, coef)
         elif (tgt is not None and c2.bn is not None and K.BN_HEAD_ON_LOAD and B.model.training and seg.out_channels == 1
               and tgt.numel() == N * H * W and c2.Cout in (32, 64)):
             # BatchNorm model: the head reads relu(bn(z)) on load (forward and backward), so the last decoder
@@ -987,6 +1009,7 @@ class _DecFn(torch.autograd.Function):
         else:
             y = B.conv_fwd(c2, a, st=st2, xbn=xbn1)
         ctx.xbn1 = xbn1
+        ctx.dxbn = dxbn
         ctx.B, ctx.i = B, i
         ctx.st = (st1[0] if st1 else None, st2[0] if st2 else None)
         ctx.dual = up is not None
@@ -1074,7 +1097,8 @@ class _DecFn(torch.autograd.Function):
         g1 = None
         if isinstance(d, _Up):
             gup = K.up2_bwd(gup)          # to the projection's (low) resolution
-        dx = B.deconv_bwd(d, gup, x)
+        dx = B.deconv_bwd(d, gup, x, xbn=ctx.dxbn)
+        ctx.dxbn = None
         B.ready([d.mod])
         B.join()
         ctx.st = None

@@ -82,6 +82,8 @@ KNOBS = (
          "block column per element walked 16k rows, 0.9 ms)"),
     Knob("bn_wgrad_on_load", "DPA_NO_BN_WGRAD_ON_LOAD", True, "BatchNorm UNet: the first conv's BN backward formed "
          "in its weight gradient's loader (dz = a g + b z + c) instead of a dz pass over HBM"),
+    Knob("bn_deconv_on_load", "DPA_NO_BN_DECONV_ON_LOAD", True, "BatchNorm UNet: a decoder block's output BN is "
+         "applied on load by the next block's fused transposed conv (forward and backward), never written"),
     Knob("bn_head_defer", "DPA_NO_BN_HEAD_DEFER", True, "BatchNorm UNet, head on load: the head backward runs inside the "
          "last decoder level's backward, so its full-resolution gradient is freed there (peak HBM)"),
     Knob("bn_head_on_load", "DPA_NO_BN_HEAD_ON_LOAD", True, "BatchNorm UNet: the segmentation head forms the last decoder "
@@ -167,6 +169,7 @@ class KernelConfig:
     bn_head_defer: bool = True
     wgrad_presum: bool = True
     bn_wgrad_on_load: bool = True
+    bn_deconv_on_load: bool = True
     f32_wgrad_c4: bool = True
     side_priority: int = 0
     wgrad_stream_blocks: int = 2048

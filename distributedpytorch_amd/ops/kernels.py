@@ -100,6 +100,7 @@ BN_SUMS_DECONV = CFG.bn_sums_deconv    # ... from the fused transposed-conv back
 BN_SUMS_POOL_Z = CFG.bn_sums_pool_z    # ... reading the dense z (relu(bn(z)) re-formed) instead of the skip
 BN_HEAD_ON_LOAD = CFG.bn_head_on_load  # the head reads the last decoder BN's input z (relu(bn(z)) on load)
 BN_WGRAD_ON_LOAD = CFG.bn_wgrad_on_load  # the first conv's BN backward in its weight gradient's loader
+BN_DECONV_ON_LOAD = CFG.bn_deconv_on_load  # a decoder block's output BN applied by the next transposed conv
 BN_HEAD_DEFER = CFG.bn_head_defer      # ... with its backward deferred into the decoder's (memory)
 # 128-channel convs on the row-block ping-pong GEMM (cfg 15) instead of the row-halo conv: 10-15 % faster
 # on every 128-output-channel 3x3 conv / dgrad of the 512^2 UNet (profiles/kbench_glds_rowblock128_b256_r03.txt)
@@ -905,11 +906,15 @@ DECONV_BWD_SHAPES = ((64, 32), (128, 64))
 
 
 def deconv_bwd_fused(gup: torch.Tensor, x: torch.Tensor, wd: torch.Tensor, gw: torch.Tensor,
-                     gb: Optional[torch.Tensor], bn_stats: Optional[list] = None) -> torch.Tensor:
+                     gb: Optional[torch.Tensor], bn_stats: Optional[list] = None,
+                     xbn: Optional[torch.Tensor] = None) -> torch.Tensor:
     """ConvTranspose2d(k2, s2) dgrad (ReLU-masked by x) AND weight/bias gradient in one pass over
     (gup, x) (csrc/deconv.hip); gw [Cin*Cout*4] / gb [Cout] accumulate.  Returns dx [N,h,w,Cin].
     ``bn_stats`` (an empty list): x is a BatchNorm+ReLU output; the list receives (slab [rows][2][Cin],
-    rows) of sum dx, sum dx*x -- that BN's backward partial sums (:func:`bn_bwd` ``stats``)."""
+    rows) of sum dx, sum dx*x -- that BN's backward partial sums (:func:`bn_bwd` ``stats``).
+    ``xbn`` (with ``bn_stats``; fp32 [scale Cin | shift Cin]): ``x`` is that BN's input z, relu(bn(z)) on load."""
+    if xbn is not None:
+        assert bn_stats is not None and xbn.dtype == torch.float32 and xbn.is_contiguous()
     N, H2, W2, Cout, ldg = _nhwc(gup, "deconv_bwd.g")
     Nx, h, w, Cin, ldx = _nhwc(x, "deconv_bwd.x")
     assert Nx == N and (H2, W2) == (2 * h, 2 * w) and (Cin, Cout) in DECONV_BWD_SHAPES
@@ -936,7 +941,7 @@ def deconv_bwd_fused(gup: torch.Tensor, x: torch.Tensor, wd: torch.Tensor, gw: t
         _check(L.dpa_deconv_bwd(_p(gup[n0:n1]), c_int(ldg), _p(x[n0:n1]), c_int(ldx), _p(wd), _p(dx[n0:n1]), c_int(Cin),
                                 _p(slab), _p(bslab), c_int(nb), c_int(h), c_int(w), c_int(Cin), c_int(Cout),
                                 c_int(splits), ctypes.c_uint(_extent_bytes(nb, H2, W2, Cout, ldg)),
-                                ctypes.c_uint(_extent_bytes(nb, h, w, Cin, ldx)), _p(bnslab), st), "deconv_bwd")
+                                ctypes.c_uint(_extent_bytes(nb, h, w, Cin, ldx)), _p(bnslab), _p(xbn), st), "deconv_bwd")
         _check(L.dpa_wgrad_reduce(_p(slab), _p(bslab), _p(gw), _p(gb), c_int(splits), c_int(4), c_int(Cout), c_int(Cin),
                                   c_int(Cin), c_int(1), st), "wgrad_reduce")
     if bn_parts:
@@ -945,10 +950,14 @@ def deconv_bwd_fused(gup: torch.Tensor, x: torch.Tensor, wd: torch.Tensor, gw: t
     return dx
 
 
-def deconv_fwd_fused(x: torch.Tensor, wf: torch.Tensor, bias: Optional[torch.Tensor], y: torch.Tensor):
+def deconv_fwd_fused(x: torch.Tensor, wf: torch.Tensor, bias: Optional[torch.Tensor], y: torch.Tensor,
+                     xbn: Optional[torch.Tensor] = None):
     """ConvTranspose2d(k2, s2) forward of the full-resolution up-convs (csrc/deconv.hip) into ``y``
-    (the decoder concat buffer's second half), whole-chunk stores along each output row."""
+    (the decoder concat buffer's second half), whole-chunk stores along each output row.  ``xbn`` (fp32
+    [scale Cin | shift Cin]): ``x`` is the pre-BN output z of a BatchNorm+ReLU layer, read as relu(bn(z))."""
     N, h, w, Cin, ldx = _nhwc(x, "deconv_fwd.x")
+    if xbn is not None:
+        assert xbn.dtype == torch.float32 and xbn.is_contiguous() and xbn.numel() == 2 * Cin
     Ny, H2, W2, Cy, ldy = _nhwc(y, "deconv_fwd.y")
     Cout = Cy
     assert Ny == N and (H2, W2) == (2 * h, 2 * w) and (Cin, Cout) in DECONV_BWD_SHAPES
@@ -963,7 +972,7 @@ def deconv_fwd_fused(x: torch.Tensor, wf: torch.Tensor, bias: Optional[torch.Ten
         nb = n1 - n0
         _check(L.dpa_deconv_fwd(_p(x[n0:n1]), c_int(ldx), _p(wf), _p(bias), _p(y[n0:n1]), c_int(ldy), c_int(nb), c_int(h),
                                 c_int(w), c_int(Cin), c_int(Cout), c_int(1024 if Cin == 64 else 512),
-                                ctypes.c_uint(_extent_bytes(nb, h, w, Cin, ldx)), st), "deconv_fwd")
+                                ctypes.c_uint(_extent_bytes(nb, h, w, Cin, ldx)), _p(xbn), st), "deconv_fwd")
 
 
 # ------------------------------------------------------------------------------------- BN / bilinear

@@ -282,3 +282,49 @@ def test_unet_bn_step_first_conv_wgrad_on_load_equals_materialised(hip_lib, monk
     l0, g0, n0 = run()
     assert n1 == 1 and n0 == 0
     assert l0 == l1 and torch.equal(g0, g1)
+
+
+@pytest.mark.parametrize("model", ["unet-bn", "unet-bn64"])
+def test_unet_bn_step_deconv_on_load_equals_materialised(hip_lib, monkeypatch, model):
+    """Decoder outputs handed to the next block's transposed conv as their BN input z (relu(bn(z)) on load,
+    forward and backward) == the step that writes those BN outputs, bit for bit; the path must be taken."""
+    from distributedpytorch_amd.compute import loss_from_partials, make_compute
+    from distributedpytorch_amd.data.synthetic import synthetic_batch
+    from distributedpytorch_amd.models.unet import build_model
+    from distributedpytorch_amd.optim import FlatParameterSpace
+    from distributedpytorch_amd.ops import kernels as K
+
+    torch.manual_seed(0)
+    net = build_model(model).cuda()
+    space = FlatParameterSpace(net)
+    comp = make_compute(net, backend="hip", dtype="bf16")
+    img, mask = synthetic_batch(2, 64, 256, 3, seed=8)
+    x, t = img.cuda(), mask.float().unsqueeze(1).cuda()
+    state0 = {k: v.clone() for k, v in net.state_dict().items() if "running" in k or "num_batches" in k}
+    used = []
+    real = K.deconv_fwd_fused
+
+    def spy(*a, **kw):
+        used.append(kw.get("xbn") is not None)
+        return real(*a, **kw)
+
+    monkeypatch.setattr(K, "deconv_fwd_fused", spy)
+
+    def run():
+        net.load_state_dict(state0, strict=False)
+        space.zero_grad()
+        used.clear()
+        S = comp.forward_partials(x, t)
+        loss = loss_from_partials(S, t.numel())
+        loss.backward()
+        torch.cuda.synchronize()
+        run_stats = {k: v.clone() for k, v in net.state_dict().items() if "running" in k}
+        return loss.item(), space.grad.clone(), run_stats, sum(used)
+
+    l1, g1, r1, n1 = run()
+    monkeypatch.setattr(K, "BN_DECONV_ON_LOAD", False)
+    l0, g0, r0, n0 = run()
+    assert n1 >= 1 and n0 == 0
+    assert l0 == l1 and torch.equal(g0, g1)
+    for k in r0:
+        assert torch.equal(r0[k], r1[k]), k

@@ -320,6 +320,40 @@ def test_deconv_bwd_fused(hip_lib, N, h, w, Cin, Cout, strided):
     assert _rel(sums[0], dd.sum(0)) < 1e-4 and _rel(sums[1], (dd * xd).sum(0)) < 1e-4
 
 
+@pytest.mark.parametrize("N,h,w,Cin,Cout", [(2, 5, 7, 64, 32), (2, 33, 31, 128, 64)])
+def test_deconv_bn_on_load(hip_lib, N, h, w, Cin, Cout):
+    """Transposed conv forward / fused backward reading a BatchNorm input z with relu(bn(z)) formed on load
+    == the same kernels over the BN output materialised by bn_fwd, bit for bit (incl. the BN sums)."""
+    from distributedpytorch_amd.ops import kernels as K
+    torch.manual_seed(8)
+    z = (torch.randn(N, h, w, Cin, device="cuda") * 1.4 - 0.2).to(torch.bfloat16)
+    bn = torch.nn.BatchNorm2d(Cin).cuda()
+    with torch.no_grad():
+        bn.weight.uniform_(-1.0, 1.5)          # negative scales too
+        bn.bias.uniform_(-0.5, 0.5)
+    y = torch.empty_like(z)
+    coef = []
+    K.bn_fwd(z, y, bn, train=True, coef_out=coef)
+    coef = coef[0]
+    wt = torch.randn(Cin, Cout, 2, 2) / Cin ** 0.5
+    wf, _, _ = _pack_one(2, wt)
+    wd, _, _ = _pack_one(3, wt)
+    b = torch.randn(Cout).cuda()
+    outs = []
+    for src, xbn in ((y, None), (z, coef)):
+        cat = torch.zeros(N, 2 * h, 2 * w, 2 * Cout, dtype=torch.bfloat16, device="cuda")
+        K.deconv_fwd_fused(src, wf, b, cat[..., Cout:], xbn=xbn)
+        gup = torch.randn(N, 2 * h, 2 * w, Cout, generator=torch.Generator().manual_seed(3)).cuda().to(torch.bfloat16)
+        gw = torch.zeros(Cin * Cout * 4, device="cuda")
+        gb = torch.zeros(Cout, device="cuda")
+        stats = []
+        dx = K.deconv_bwd_fused(gup, src, wd, gw, gb, bn_stats=stats, xbn=xbn)
+        torch.cuda.synchronize()
+        outs.append((cat, dx, gw, gb, stats[0][:stats[1] * 2 * Cin]))
+    for a, c in zip(*outs):
+        assert torch.equal(a, c)
+
+
 @pytest.mark.parametrize("N,H,W,C", [(2, 16, 16, 32), (1, 9, 11, 64)])
 def test_maxpool_and_backward(hip_lib, N, H, W, C):
     from distributedpytorch_amd.ops import kernels as K

@@ -190,9 +190,9 @@ def test_elementwise_launchers_reject(L):
     assert L.dpa_up2_bwd(n, i(8), n, i(8), i(1), i(4), i(4), i(12), n) == INVALID                  # C % 8
     assert L.dpa_slab_fold(n, i(0), i(64), i(8), n, n) == INVALID
     assert L.dpa_deconv_bwd(n, i(64), n, i(64), n, n, i(64), n, n, i(1), i(8), i(8), i(64), i(32), i(0),
-                            ctypes.c_uint(0), ctypes.c_uint(0), n, n) == INVALID                    # splits < 1
+                            ctypes.c_uint(0), ctypes.c_uint(0), n, n, n) == INVALID                 # splits < 1
     assert L.dpa_deconv_fwd(n, i(60), n, n, n, i(64), i(1), i(8), i(8), i(64), i(32), i(1), ctypes.c_uint(0),
-                            n) == INVALID                                                           # ldx % 8
+                            n, n) == INVALID                                                        # ldx % 8
 
 
 def test_bn_shapes(L):
