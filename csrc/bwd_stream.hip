@@ -137,7 +137,9 @@ __global__ __launch_bounds__(64 * NW, 2) void bwd_stream_kernel(BwdArgs a) {
   constexpr int BCH = BP * 4 * KSO, LBI = (BCH + NT - 1) / NT;   // bias: chunks of the g row's BP pixels
   __shared__ __attribute__((aligned(16))) char lds[WBYTES + 4 * GSLOT + 4 * XSLOT + W1BYTES];
   __shared__ __attribute__((aligned(16))) float bnc[BNL ? 3 * CO : 4];   // BN mode: the dz coefficients
-  constexpr bool XBN = BNS;                     // x = relu(bn(z)) formed on load (a.xbn)
+  // x = relu(bn(z)) formed on load (a.xbn): BN mode 2, and mode 1 with a dual input (x only, not x2 --
+  // the decoder conv over [skip | up] whose skip is the encoder BN's input z)
+  constexpr bool XBN = BNL;
   constexpr bool EARLY_XFORM = BNS && CI == 64;   // where the row loop runs the loader transforms (rxform)
   __shared__ __attribute__((aligned(16))) float xbc[XBN ? 2 * CI : 4];
   char* const Wimg = lds;
@@ -389,8 +391,8 @@ __global__ __launch_bounds__(64 * NW, 2) void bwd_stream_kernel(BwdArgs a) {
       if (xbn && rok) {
 #pragma unroll
         for (int j = 0; j < LX; ++j) {
-          if (!xok[j]) continue;
-          const int cb = dual ? (xpl[j] ? 32 : 0) + (tid & 3) * 8 : (tid % (CI / 8)) * 8;
+          if (!xok[j] || (dual && xpl[j])) continue;
+          const int cb = dual ? (tid & 3) * 8 : (tid % (CI / 8)) * 8;
 #pragma unroll
           for (int k = 0; k < 4; ++k) {
             const float2 sc = *reinterpret_cast<const float2*>(xbc + cb + 2 * k);
@@ -821,7 +823,7 @@ DPA_API int dpa_bwd_stream(const BwdArgs* args, int ci, int co, int epi, hipStre
   if (!bwd_cfg(ci, co, &bp, &nw) || (fused_mode && a.W % bp) || a.W < 16 || (a.ldg & 7) || (a.ldx & 7) || (a.ldy & 3) ||
       a.rh < 1 || a.ipb < 1 ||
       a.Kd < 9 * co || (epi == 1 && (a.y2 == nullptr || (a.ldy2 & 3) || a.split % 16 || a.split <= 0 || a.split >= ci)) ||
-      (a.x2 && (ci != 64 || a.ldx < 32 || fused_mode)) || (a.xbn && (a.z == nullptr || a.bnslab == nullptr)))
+      (a.x2 && (ci != 64 || a.ldx < 32 || fused_mode)) || (a.xbn && (a.z == nullptr || (a.bnslab == nullptr && a.x2 == nullptr))))
     return (int)hipErrorInvalidValue;
   // BN modes: the gradient source is plain (no pool / head / first-conv fold); statistics for the
   // layer below only with the masked dx

@@ -542,7 +542,8 @@ __global__ __launch_bounds__(256 * WCS) void igemm_stream_kernel(IgemmArgs a) {
   const unsigned rowbytes_x = (unsigned)(a.Ws * a.ldx * 2);
   // BN-on-load (EPI 4, a.xbn): the input is the PRE-BatchNorm output z of the layer below and the
   // loader stores y = relu(z * xbn[c] + xbn[CS + c]) into the ring -- bn_apply's exact arithmetic,
-  // so the layer below never writes y (its BN+ReLU pass over HBM disappears); padding stays zero
+  // so the layer below never writes y (its BN+ReLU pass over HBM disappears); padding stays zero.
+  // With a dual input only x (channels < 32) is a BN input; x2 is stored as loaded
   constexpr bool XBN = EPI == 4;
   __shared__ float xbc[XBN ? 2 * CS : 1];
   const bool xbn = XBN && a.xbn != nullptr;
@@ -576,7 +577,7 @@ __global__ __launch_bounds__(256 * WCS) void igemm_stream_kernel(IgemmArgs a) {
       if (xbn && R.rok) {
 #pragma unroll
         for (int j = 0; j < LR; ++j) {
-          if (!lok[j]) continue;
+          if (!lok[j] || lpl[j]) continue;     // dual input: x2 (plane 1) is read as is
           // chunk j's first channel: slice ks (plane for a dual input) * 32 + (c & 3) * 8
           const int c = tid + j * NT;
           const int cb = (dual ? (lpl[j] ? 32 : 0) : ((c >> 2) / HR) * 32) + (c & 3) * 8;

@@ -236,7 +236,7 @@ __global__ __launch_bounds__(256) void bn_apply_pool_kernel(const bf16_t* __rest
         v[q][2 * e] = lo_bf(o[e]);
         v[q][2 * e + 1] = hi_bf(o[e]);
       }
-      *reinterpret_cast<uint4*>(y + pix[q] * ldy + c0) = make_uint4(o[0], o[1], o[2], o[3]);
+      if (y) *reinterpret_cast<uint4*>(y + pix[q] * ldy + c0) = make_uint4(o[0], o[1], o[2], o[3]);
     }
     unsigned o[4], cd[2] = {0u, 0u};
 #pragma unroll
@@ -320,8 +320,10 @@ DPA_API int dpa_bn_fwd(const bf16_t* z, int ldz, bf16_t* y, int ldy, long long P
     hipLaunchKernelGGL(bn_finalize_kernel, dim3(C), dim3(256), 0, st, (const float*)nullptr, 0, C, (long)P, gamma, beta, eps,
                        momentum, rmean, rvar, coef, saved);
   }
-  // coefficients only (y == pool == null): the consumer applies the BN + ReLU on load (IgemmArgs::xbn)
+  // coefficients only (y == pool == null): the consumer applies the BN + ReLU on load (IgemmArgs::xbn);
+  // y == null with pool: only the pooled tensor and its window codes (the consumers of y read z on load)
   if (y == nullptr && pool == nullptr) return (int)hipGetLastError();
+  if (y == nullptr && !(pool && relu)) return (int)hipErrorInvalidValue;
   if (pool) {
     const long tot = (long)P / 4 * (C / 8);
     hipLaunchKernelGGL(bn_apply_pool_kernel, dim3(dpa_grid(tot, 256, 16384)), dim3(256), 0, st, z, ldz, y, ldy, pool, ldp,

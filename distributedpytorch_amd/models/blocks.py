@@ -181,6 +181,8 @@ def run_segment(blocks, start: int, end: int, depth: int, env: Dict[str, torch.T
     if start == 0:
         env["x"] = blocks.prep(env["x"])
     units = segment_units(start, end, depth)
+    if hasattr(blocks, "skip_z_ok"):
+        blocks.skip_z_ok = emit is None     # a pipeline stage may send its skips: they must be plain tensors
     for u, (idx, part) in enumerate(units):
         kind, i = block_kind(idx, depth)
         if kind == "dec" and hasattr(blocks, "next_dec_local"):

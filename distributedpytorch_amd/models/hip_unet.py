@@ -143,6 +143,7 @@ class HipBlocks:
         # decoder outputs handed to the next decoder block as their BatchNorm input z (run_segment sets
         # next_dec_local when that block follows in the same segment): z data_ptr -> (z, coef)
         self.next_dec_local = False
+        self.skip_z_ok = False
         self._zx = {}
         # pipeline microbatches: the side-stream conv weight gradients of every microbatch are deferred
         # and run as ONE launch per layer over all microbatches' images (K.wgrad_multi) -- one split-K
@@ -239,10 +240,25 @@ class HipBlocks:
         # the row-streaming conv binds one image per block: z's image within the 32-bit buffer range
         return H * W * c2.Cin * 2 < K._MAX_BYTES and self.fusable(c2, c1, W)
 
-    def conv_bn_z(self, c: _Conv, x: torch.Tensor, st: list, xbn: torch.Tensor = None):
+    def conv_bn_z(self, c: _Conv, x: torch.Tensor, st: list, xbn: torch.Tensor = None, x2: torch.Tensor = None):
         """Training conv + BatchNorm statistics without the normalise pass: returns (z, coef) with the
         consumer's on-load transform relu(z * coef[c] + coef[C + c]); ``st`` receives (z, saved, coef).
-        ``xbn``: x is itself a pre-BN output, read as relu(bn(x)) (:meth:`conv_fwd`)."""
+        ``xbn``: x is itself a pre-BN output, read as relu(bn(x)) (:meth:`conv_fwd`); ``x2``: dual input."""
+        N, H, W = x.shape[:3]
+        z = torch.empty(N, H, W, c.Cout, dtype=torch.bfloat16, device=x.device)
+        self._bn_stats_version += 1
+        stats = []
+        K.igemm(x, self.wf(c), z, Ngemm=c.Cout, Kpad=c.Kf, KH=3, KW=3, stride=1, pad=1, Cs=c.Cs, out_grid=(N, H, W),
+                bias=c.mod.bias, relu=False, bn_stats=stats, xbn=xbn, x2=x2)
+        coef = []
+        saved = K.bn_fwd(z, None, c.bn, train=True, stats=stats, coef_out=coef)
+        st.append((z, saved, coef[0]))
+        return z, coef[0]
+
+    def conv_bn_z_pool(self, c: _Conv, x: torch.Tensor, st: list, pool: torch.Tensor, pcode: torch.Tensor,
+                       xbn: torch.Tensor = None):
+        """:meth:`conv_bn_z` that also writes the 2x2 max-pool of relu(bn(z)) and its window codes (one
+        normalise pass over z that stores only the pooled quarter): returns (z, coef)."""
         N, H, W = x.shape[:3]
         z = torch.empty(N, H, W, c.Cout, dtype=torch.bfloat16, device=x.device)
         self._bn_stats_version += 1
@@ -250,7 +266,7 @@ class HipBlocks:
         K.igemm(x, self.wf(c), z, Ngemm=c.Cout, Kpad=c.Kf, KH=3, KW=3, stride=1, pad=1, Cs=c.Cs, out_grid=(N, H, W),
                 bias=c.mod.bias, relu=False, bn_stats=stats, xbn=xbn)
         coef = []
-        saved = K.bn_fwd(z, None, c.bn, train=True, stats=stats, coef_out=coef)
+        saved = K.bn_fwd(z, None, c.bn, train=True, stats=stats, pool=pool, pcode=pcode, coef_out=coef)
         st.append((z, saved, coef[0]))
         return z, coef[0]
 
@@ -269,7 +285,7 @@ class HipBlocks:
             K.igemm(x, self.wf(c), y, Ngemm=c.Cout, Kpad=c.Kf, KH=3, KW=3, stride=1, pad=1, Cs=c.Cs,
                     out_grid=(N, H, W), bias=c.mod.bias, relu=True, pool=pool, pcode=pcode, x2=x2)
             return y
-        assert x2 is None, "dual input: convs without BatchNorm"
+        assert x2 is None or self.model.training, "dual input with BatchNorm: training forward (dual_level)"
         assert xbn is None or self.model.training, "BN-on-load: training forward"
         if not self.model.training and K.FOLD_BN_EVAL and c.bn.track_running_stats and c.bn.running_mean is not None:
             # inference: BatchNorm with running statistics is a per-channel affine map -> folded into
@@ -283,7 +299,7 @@ class HipBlocks:
             self._bn_stats_version += 1                 # running statistics move (eval fold cache)
         stats = [] if self.model.training else None    # batch statistics from the conv epilogue
         K.igemm(x, self.wf(c), z, Ngemm=c.Cout, Kpad=c.Kf, KH=3, KW=3, stride=1, pad=1, Cs=c.Cs, out_grid=(N, H, W),
-                bias=c.mod.bias, relu=False, bn_stats=stats, xbn=xbn)
+                bias=c.mod.bias, relu=False, bn_stats=stats, xbn=xbn, x2=x2)
         coef = [] if self.model.training else None     # (scale, shift): consumers may re-form y from z
         saved = K.bn_fwd(z, y, c.bn, train=self.model.training, stats=stats, pool=pool, pcode=pcode, coef_out=coef)
         if st is not None:
@@ -441,7 +457,8 @@ class HipBlocks:
         """A conv over a concat of two C-channel halves whose fused backward does not exist at 2C input
         channels but does at C (the 256^2 decoder conv 128 -> 64): conv(cat) = conv_lo(skip) +
         conv_hi(up), so its backward is two fused passes, one per half."""
-        if not (K.USE_FUSED_HALVES and c.bn is None and c.Cs == c.Cin == 2 * C):
+        if not (K.USE_FUSED_HALVES and (c.bn is None or (K.BN_HALVES and K.USE_FUSED_BN_BWD))
+                and c.Cs == c.Cin == 2 * C):
             return False
         key = ("halves", C, c.Cout, W)
         ok = self._fusable.get(key)
@@ -462,24 +479,27 @@ class HipBlocks:
         if not 0 <= l < d:
             return False
         c1 = self.dec_convs[d - 1 - l][0]
-        if not (c1.bn is None and c1.Cs == c1.Cin == 64 and self.enc_convs[l][1].Cout == 32):
+        if not ((c1.bn is None or (K.BN_DUAL and self.model.training)) and c1.Cs == c1.Cin == 64
+                and self.enc_convs[l][1].Cout == 32):
             return False
         # both kernels bind one image per block: each [H,W,32] image within the 32-bit buffer range
         return W >= 16 and H * W * 32 * 2 < K._MAX_BYTES and self.fusable(c1, None, W)
 
-    def conv_bwd_halves(self, c: _Conv, g: torch.Tensor, cat: torch.Tensor, C: int):
+    def conv_bwd_halves(self, c: _Conv, g: torch.Tensor, cat: torch.Tensor, C: int, bn=None):
         """Backward of a conv over ``cat = [lo | hi]`` (C channels each) as two fused passes: each
         writes its half's dense input gradient and its half of the weight gradient (the dgrad rows of
         the packed weights and the input-channel columns of dW belonging to that half); the bias
         gradient comes with the first.  Replaces one 2C-channel dgrad + a side-stream weight gradient
-        that together did ~1.7x the work at a third of the MFMA rate (profiles/kbench_halo_b256_r02.txt)."""
+        that together did ~1.7x the work at a third of the MFMA rate (profiles/kbench_halo_b256_r02.txt).
+        ``bn`` = (z, coef3): the conv is followed by BatchNorm + ReLU and ``g`` is the gradient of its
+        output; both passes form dz on load (:func:`K.conv_bwd_fused` ``bn``)."""
         gw, gb = _grad(c.mod.weight).view(c.Cout, c.Cin, 9), _grad(c.mod.bias)
         wd = self.wd(c)
         outs = []
         for h in range(2):
             part = torch.zeros(c.Cout * C * 9, dtype=torch.float32, device=g.device)
             outs.append(K.conv_bwd_fused(g, cat[..., h * C:(h + 1) * C], wd[h * C * c.Kd:(h + 1) * C * c.Kd], c.Kd,
-                                         part, gb if h == 0 else None, mask=False))
+                                         part, gb if h == 0 else None, mask=False, bn=bn))
             gw[:, h * C:(h + 1) * C].add_(part.view(c.Cout, C, 9))
         return outs[0], outs[1]
 
@@ -803,7 +823,15 @@ class _EncFn(torch.autograd.Function):
         # window codes (argmax + ReLU masks) for the backward: it then never re-reads the skip
         code = (torch.empty(N, H // 2, W // 2, c2.Cout, dtype=torch.uint8, device=x.device)
                 if H % 2 == 0 and W % 2 == 0 else None)
-        B.conv_fwd(c2, a, skip, pool=pooled, pcode=code, st=st2, xbn=xbn1)   # pool fused into the conv epilogue when streaming
+        if (cat is None and code is not None and c2.bn is not None and K.BN_SKIP_Z and B.skip_z_ok
+                and B.model.training and K.BN_SUMS_POOL and K.BN_SUMS_POOL_Z and l not in B.dense_skips
+                and B.dual_level(l, H, W) and B.bn_on_load(*B.dec_convs[len(B.dec_convs) - 1 - l], H, W)):
+            # the skip's consumer (the decoder conv's dual input) forms relu(bn(z)) on load: the skip IS z and
+            # the BN pass writes only the pooled quarter + codes (the full-resolution y is never stored)
+            skip, coef2 = B.conv_bn_z_pool(c2, a, st2, pooled, code, xbn=xbn1)
+            B._zx[skip.data_ptr()] = (skip, coef2)
+        else:
+            B.conv_fwd(c2, a, skip, pool=pooled, pcode=code, st=st2, xbn=xbn1)   # pool fused into the conv epilogue when streaming
         ctx.B, ctx.l = B, l
         ctx.xbn1 = xbn1
         ctx.x_needs_grad = l > 0
@@ -952,6 +980,7 @@ class _DecFn(torch.autograd.Function):
         # relu(bn(z)) on load, forward and backward
         zx = B._zx.pop(x.data_ptr(), None)
         dxbn = zx[1] if (zx is not None and zx[0].shape == x.shape and zx[0].stride() == x.stride()) else None
+        skip_xbn = None
         local_next, B.next_dec_local = B.next_dec_local, False
         Ns, Hs, Ws, _ = skip.shape
         h2, w2 = 2 * x.shape[1], 2 * x.shape[2]
@@ -968,14 +997,23 @@ class _DecFn(torch.autograd.Function):
             # dual input: skip and up stay two dense tensors, the conv reads both (no concat buffer)
             cat = skip
             up = torch.empty(Ns, h2, w2, C, dtype=torch.bfloat16, device=x.device)
+            sz = B._zx.pop(skip.data_ptr(), None)
+            if sz is not None and sz[0].shape == skip.shape and sz[0].stride() == skip.stride():
+                # the skip is the encoder BN's input z: conv1 reads relu(bn(z)) for its first 32 channels
+                skip_xbn = torch.zeros(4 * C, dtype=torch.float32, device=x.device)
+                skip_xbn[:C].copy_(sz[1][:C])
+                skip_xbn[2 * C:3 * C].copy_(sz[1][C:])
         else:
             cat = B.cat_for(skip)
             up = None
         B.deconv_fwd(d, x, cat[..., C:] if up is None else up, xbn=dxbn)
         st1, st2 = [], []
         xbn1 = None
-        if up is None and B.bn_on_load(c1, c2, h2, w2):
-            a, xbn1 = B.conv_bn_z(c1, cat, st1)       # a = conv1's pre-BN output; conv2 applies BN + ReLU
+        if skip_xbn is not None:
+            assert B.bn_on_load(c1, c2, h2, w2), "skip kept as z: the decoder conv must be a BN-statistics stream conv"
+        if B.bn_on_load(c1, c2, h2, w2):
+            # a = conv1's pre-BN output; conv2 applies BN + ReLU
+            a, xbn1 = B.conv_bn_z(c1, cat, st1, x2=up, xbn=skip_xbn)
         else:
             a = B.conv_fwd(c1, cat, st=st1, x2=up)
         N, H, W = a.shape[:3]
@@ -1010,6 +1048,7 @@ class _DecFn(torch.autograd.Function):
             y = B.conv_fwd(c2, a, st=st2, xbn=xbn1)
         ctx.xbn1 = xbn1
         ctx.dxbn = dxbn
+        ctx.skip_xbn = skip_xbn
         ctx.B, ctx.i = B, i
         ctx.st = (st1[0] if st1 else None, st2[0] if st2 else None)
         ctx.dual = up is not None
@@ -1083,9 +1122,16 @@ class _DecFn(torch.autograd.Function):
         ctx.st = (st1, None)
         if ctx.dual:
             # the forward checked fusable() (dual_level): the fused backward reads [skip | up] too
-            (dskip, gup), _ = B.bwd_conv(c1, g1, cat, st1, mask=False, stats=st_g, split=C, x2=up)
+            (dskip, gup), _ = B.bwd_conv(c1, g1, cat, st1, mask=False, stats=st_g, split=C, x2=up, xbn=ctx.skip_xbn)
+            ctx.skip_xbn = None
         elif B.fusable(c1, None, W):
             (dskip, gup), _ = B.bwd_conv(c1, g1, cat, st1, mask=False, stats=st_g, split=C)
+        elif c1.bn is not None and B.halves_fusable(c1, C, W) and g1.stride() == st1[0].stride():
+            # BatchNorm conv over a 2C-channel concat: one fused pass per half, each forming the BN backward
+            # on load (the dz pass, the split dgrad GEMM and the side-stream weight gradient all go)
+            z1, saved1 = st1[:2]
+            coef3 = K.bn_bwd_coef(g1, z1, saved1, c1.bn, _grad(c1.bn.weight), _grad(c1.bn.bias), stats=st_g)
+            dskip, gup = B.conv_bwd_halves(c1, g1, cat, C, bn=(z1, coef3))
         else:
             g1 = B.bn_bwd(c1, g1, st1, stats=st_g)
             if B.halves_fusable(c1, C, W):

@@ -84,6 +84,12 @@ KNOBS = (
          "in its weight gradient's loader (dz = a g + b z + c) instead of a dz pass over HBM"),
     Knob("bn_deconv_on_load", "DPA_NO_BN_DECONV_ON_LOAD", True, "BatchNorm UNet: a decoder block's output BN is "
          "applied on load by the next block's fused transposed conv (forward and backward), never written"),
+    Knob("bn_dual", "DPA_NO_BN_DUAL", True, "BatchNorm UNet (training): the full-resolution skip and up-sampled "
+         "halves stay two dense tensors (dual input, as in the plain UNet) instead of a concat buffer"),
+    Knob("bn_halves", "DPA_NO_BN_HALVES", True, "BatchNorm UNet: the 256^2 decoder conv over the 128-channel concat "
+         "takes the two-pass fused backward (BN backward on load) instead of dz pass + split dgrad + weight gradient"),
+    Knob("bn_skip_z", "DPA_NO_BN_SKIP_Z", True, "BatchNorm UNet: at a dual-input level the encoder's skip is its BN "
+         "input z (only the pooled tensor is normalised); the decoder conv forms relu(bn(z)) on load"),
     Knob("bn_head_defer", "DPA_NO_BN_HEAD_DEFER", True, "BatchNorm UNet, head on load: the head backward runs inside the "
          "last decoder level's backward, so its full-resolution gradient is freed there (peak HBM)"),
     Knob("bn_head_on_load", "DPA_NO_BN_HEAD_ON_LOAD", True, "BatchNorm UNet: the segmentation head forms the last decoder "
@@ -170,6 +176,9 @@ class KernelConfig:
     wgrad_presum: bool = True
     bn_wgrad_on_load: bool = True
     bn_deconv_on_load: bool = True
+    bn_dual: bool = True
+    bn_halves: bool = True
+    bn_skip_z: bool = True
     f32_wgrad_c4: bool = True
     side_priority: int = 0
     wgrad_stream_blocks: int = 2048

@@ -101,6 +101,9 @@ BN_SUMS_POOL_Z = CFG.bn_sums_pool_z    # ... reading the dense z (relu(bn(z)) re
 BN_HEAD_ON_LOAD = CFG.bn_head_on_load  # the head reads the last decoder BN's input z (relu(bn(z)) on load)
 BN_WGRAD_ON_LOAD = CFG.bn_wgrad_on_load  # the first conv's BN backward in its weight gradient's loader
 BN_DECONV_ON_LOAD = CFG.bn_deconv_on_load  # a decoder block's output BN applied by the next transposed conv
+BN_DUAL = CFG.bn_dual                  # BN model: dual-input (no concat buffer) full-resolution decoder level
+BN_HALVES = CFG.bn_halves              # BN model: two-pass fused backward of the concat-input decoder conv
+BN_SKIP_Z = CFG.bn_skip_z              # BN model: the dual-level skip kept as its BN input z
 BN_HEAD_DEFER = CFG.bn_head_defer      # ... with its backward deferred into the decoder's (memory)
 # 128-channel convs on the row-block ping-pong GEMM (cfg 15) instead of the row-halo conv: 10-15 % faster
 # on every 128-output-channel 3x3 conv / dgrad of the 512^2 UNet (profiles/kbench_glds_rowblock128_b256_r03.txt)
@@ -238,7 +241,8 @@ def igemm(x: torch.Tensor, wpacked: torch.Tensor, y: torch.Tensor, *, Ngemm: int
             and not accumulate and not relu and path == "auto" and (mask is None or mch == Ngemm):
         bslab = torch.empty(N * -(-Ho // 16) * -(-Wo // 64) * 2 * Ngemm, dtype=torch.float32, device=y.device)
     if xbn is not None:
-        assert bslab is not None and mask is None and x2 is None and Cs != 8, "BN-on-load: the BN-statistics stream conv"
+        # with a dual input only x (channels < 32) is formed on load: xbn [scale 64 | shift 64], entries < 32 used
+        assert bslab is not None and mask is None and Cs != 8, "BN-on-load: the BN-statistics stream conv"
         assert xbn.dtype == torch.float32 and xbn.is_contiguous() and xbn.numel() == 2 * Cs
     hprob = None
     if head is not None:
@@ -761,7 +765,8 @@ def conv_bwd_fused(g: Optional[torch.Tensor], x: torch.Tensor, wd: torch.Tensor,
         bnslab = torch.empty(nblk * 2 * CI, dtype=torch.float32, device=x.device)
         a.bnslab = bnslab.data_ptr()
     if xbn is not None:
-        assert bn_stats and xbn.dtype == torch.float32 and xbn.is_contiguous() and xbn.numel() == 2 * CI
+        assert (bn_stats or (bn is not None and x2 is not None)) and xbn.dtype == torch.float32
+        assert xbn.is_contiguous() and xbn.numel() == 2 * CI
         a.xbn = xbn.data_ptr()
     _check(L.dpa_bwd_stream(ctypes.byref(a), c_int(CI), c_int(CO), c_int(epi), st), "bwd_stream")
     if hslab is not None:
@@ -1008,7 +1013,9 @@ def bn_fwd(z: torch.Tensor, y: Optional[torch.Tensor], bn: torch.nn.BatchNorm2d,
     (:func:`igemm` / :func:`conv_bwd_fused` ``xbn``)."""
     N, H, W, C, ldz = _nhwc(z, "bn.z")
     if y is None:
-        assert coef_out is not None and pool is None and relu, "coefficients only: the consumer applies BN + ReLU"
+        # coefficients only, or (pool) only the pooled tensor + codes: the consumers of y read z on load
+        assert coef_out is not None and relu and (pool is None or (pcode is not None and H % 2 == 0 and W % 2 == 0)), \
+            "no y: the consumer applies BN + ReLU"
         ldy = 0
     else:
         Ny, Hy, Wy, Cy, ldy = _nhwc(y, "bn.y")
