@@ -72,6 +72,11 @@ struct BwdArgs {
   // pre-BN output z and the loader forms relu(z * xbn[c] + xbn[CI + c]) (the forward's bn_apply
   // arithmetic) -- the BN output is never stored in the forward
   const float* xbn;
+  // HEAD + BN mode (the last decoder conv is followed by BatchNorm + ReLU and then the head): `g` is the
+  // conv's pre-BN output z (the BN input, also `z`) and the head gradient of y = relu(z * ybn[c] +
+  // ybn[CO + c]) is formed on load (p from hprob), then the BN backward (bncoef) -- neither the BN output
+  // nor the head gradient is ever stored.  The segmap gradients come from the statistics pass before.
+  const float* ybn;
 };
 
 // 8 consecutive k (pixel rows roff+8g .. +7) of 16 channels starting at col0, from an nk image
@@ -100,8 +105,9 @@ __device__ __forceinline__ bf16x8_t tr_pair(const char* base, int off0, int off1
   return __builtin_bit_cast(bf16x8_t, v);
 }
 
+// (head + BN mode: one 8-wave block per CU -- its registers do not fit two 4-wave blocks without spilling)
 template <int BP, int CI, int CO, int NW, int PG, int EPI, bool HEAD, bool POOL, bool W1, int BNM>
-__global__ __launch_bounds__(64 * NW, 2) void bwd_stream_kernel(BwdArgs a) {
+__global__ __launch_bounds__(64 * NW, (HEAD && BNM) ? 1 : 2) void bwd_stream_kernel(BwdArgs a) {
   constexpr int NT = 64 * NW;
   constexpr int HR = BP + 2;                   // ring row: BP pixels + 1 halo pixel each side
   constexpr int KSO = CO / 32;                 // 32-channel slices of g
@@ -122,7 +128,8 @@ __global__ __launch_bounds__(64 * NW, 2) void bwd_stream_kernel(BwdArgs a) {
   static_assert(!W1 || (POOL && CI == 32 && CO == 32 && EPI == 0 && BP % 32 == 0), "W1 mode");
   // BNM: 0 none, 1 BatchNorm backward on load, 2 that + the layer below's BN statistics from dx
   constexpr bool BNL = BNM >= 1, BNS = BNM == 2;
-  static_assert(!BNM || !(HEAD || POOL || W1), "BN mode: plain gradient source");
+  static_assert(!BNM || !(POOL || W1), "BN mode: plain or head gradient source");
+  static_assert(!(HEAD && BNM == 1), "head + BN: with the layer below's BN statistics (mode 2)");
   static_assert(!BNS || EPI == 0, "BN statistics of the layer below need the masked dx");
   // W1: x1 row ring (5 slots: the delayed dW1 step still reads row h-2 while row h+2 is stored),
   // dx row double buffer [BP][32] (nk, swz_nk<32>), per-wave tiles of the 32 x (9 taps x 8) dW1
@@ -137,6 +144,8 @@ __global__ __launch_bounds__(64 * NW, 2) void bwd_stream_kernel(BwdArgs a) {
   constexpr int BCH = BP * 4 * KSO, LBI = (BCH + NT - 1) / NT;   // bias: chunks of the g row's BP pixels
   __shared__ __attribute__((aligned(16))) char lds[WBYTES + 4 * GSLOT + 4 * XSLOT + W1BYTES];
   __shared__ __attribute__((aligned(16))) float bnc[BNL ? 3 * CO : 4];   // BN mode: the dz coefficients
+  constexpr bool HBN = HEAD && BNL;             // head gradient of relu(bn(z)) formed on load, then dz
+  __shared__ __attribute__((aligned(16))) float ybc[HBN ? 3 * CO : 4];   // HBN: [scale | shift | segmap w]
   // x = relu(bn(z)) formed on load (a.xbn): BN mode 2, and mode 1 with a dual input (x only, not x2 --
   // the decoder conv over [skip | up] whose skip is the encoder BN's input z)
   constexpr bool XBN = BNL;
@@ -193,6 +202,8 @@ __global__ __launch_bounds__(64 * NW, 2) void bwd_stream_kernel(BwdArgs a) {
   const bool xbn = XBN && a.xbn != nullptr;
   if constexpr (BNL) {
     for (int i = tid; i < 3 * CO; i += NT) bnc[i] = a.bncoef[i];
+    if constexpr (HBN)       // (the segmap weights in LDS too: registers are the limit of this mode)
+      for (int i = tid; i < 3 * CO; i += NT) ybc[i] = i < 2 * CO ? a.ybn[i] : a.hw[i - 2 * CO];
     if (xbn)
       for (int i = tid; i < 2 * CI; i += NT) xbc[i] = a.xbn[i];
     __syncthreads();
@@ -258,7 +269,7 @@ __global__ __launch_bounds__(64 * NW, 2) void bwd_stream_kernel(BwdArgs a) {
   if constexpr (HEAD) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      hwv[e] = a.hw[(tid & 3) * 8 + e];
+      hwv[e] = HBN ? 0.f : a.hw[(tid & 3) * 8 + e];
       hdw[e] = 0.f;
     }
     hd0 = a.dS[0]; hd1 = a.dS[1]; hd2 = a.dS[2];
@@ -285,9 +296,11 @@ __global__ __launch_bounds__(64 * NW, 2) void bwd_stream_kernel(BwdArgs a) {
   auto rload = [&](int ih, RowRegs& R) {
     const bool rok = ih >= 0 && ih < a.H;                     // wave-uniform
     const unsigned gb = (unsigned)ih * growb, xb = (unsigned)ih * xrowb;
+    if constexpr (!HBN) {                      // HEAD + BN: the gradient is formed from z (R.z) alone
 #pragma unroll
-    for (int j = 0; j < LG; ++j)
-      R.g[j] = __builtin_amdgcn_raw_buffer_load_b128(gr, (rok && gok[j]) ? gb + goff[j] : 0x80000000u, 0, 0);
+      for (int j = 0; j < LG; ++j)
+        R.g[j] = __builtin_amdgcn_raw_buffer_load_b128(gr, (rok && gok[j]) ? gb + goff[j] : 0x80000000u, 0, 0);
+    }
 #pragma unroll
     for (int j = 0; j < LX; ++j)
       R.x[j] = __builtin_amdgcn_raw_buffer_load_b128(xpl[j] ? x2r : xr, (rok && xok[j]) ? xb + xoff[j] : 0x80000000u, 0, 0);
@@ -338,6 +351,28 @@ __global__ __launch_bounds__(64 * NW, 2) void bwd_stream_kernel(BwdArgs a) {
         R.g[j] = u32x4_t{o[0], o[1], o[2], o[3]};
       }
     }
+    if constexpr (HBN) {                        // z chunk -> head gradient of y = relu(bn(z)) (into R.g)
+#pragma unroll
+      for (int j = 0; j < LG; ++j) {
+        if (!glive[j]) continue;
+        const int cb = (tid & 3) * 8;
+        const float p = __uint_as_float(R.p[j]);
+        const float tt = __uint_as_float(R.t[j]);
+        const float dz = head_dz(p, tt, tt == 1.f ? 1.f : 0.f, hd0, hd1, hd2);
+        unsigned o[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float2 sc = *reinterpret_cast<const float2*>(ybc + cb + 2 * e);
+          const float2 sh = *reinterpret_cast<const float2*>(ybc + CO + cb + 2 * e);
+          // y as the forward's BN pass would have stored it (bf16); ReLU mask y > 0
+          const unsigned yq = pack_bf2(fmaxf(fmaf(lo_bf(R.z[j][e]), sc.x, sh.x), 0.f),
+                                       fmaxf(fmaf(hi_bf(R.z[j][e]), sc.y, sh.y), 0.f));
+          const float2 hw2 = *reinterpret_cast<const float2*>(ybc + 2 * CO + cb + 2 * e);
+          o[e] = pack_bf2(lo_bf(yq) > 0.f ? dz * hw2.x : 0.f, hi_bf(yq) > 0.f ? dz * hw2.y : 0.f);
+        }
+        R.g[j] = u32x4_t{o[0], o[1], o[2], o[3]};
+      }
+    }
     if constexpr (BNL) {                        // (g, z) chunk -> conv-output gradient chunk
       const bool rok = ih >= 0 && ih < a.H;
 #pragma unroll
@@ -359,7 +394,7 @@ __global__ __launch_bounds__(64 * NW, 2) void bwd_stream_kernel(BwdArgs a) {
         R.g[j] = u32x4_t{o[0], o[1], o[2], o[3]};
       }
     }
-    if constexpr (HEAD) {                       // y chunk -> gradient chunk (+ segmap gradient partials)
+    if constexpr (HEAD && !HBN) {               // y chunk -> gradient chunk (+ segmap gradient partials)
       const bool rowv = ih >= h0 && ih < h0 + nrows;
 #pragma unroll
       for (int j = 0; j < LG; ++j) {
@@ -743,7 +778,7 @@ __global__ __launch_bounds__(64 * NW, 2) void bwd_stream_kernel(BwdArgs a) {
       a.bslab[((long)split_id * PG + q) * CO + cch] = s;
     }
   }
-  if constexpr (HEAD) {
+  if constexpr (HEAD && !HBN) {
     // segmap gradient partials: per thread 8 channels (cc = tid & 3) + dz sum; fixed-order reduction
     __syncthreads();
     float* hp = reinterpret_cast<float*>(lds);
@@ -849,6 +884,13 @@ DPA_API int dpa_bwd_stream(const BwdArgs* args, int ci, int co, int epi, hipStre
       return launch_bwd_stream<64, 32, 32, W1_NW, 2, 0, false, true, true>(a, st);
     }
     return launch_bwd_stream<64, 32, 32, 4, 2, 0, false, true>(a, st);
+  }
+  if (a.ybn != nullptr) {     // head + BN: the last decoder conv 32 -> 32 of a BN model (its BN statistics
+    // and the segmap gradients from the head statistics pass; the layer below's BN sums from dx)
+    if (ci == 32 && co == 32 && epi == 0 && bn && a.bnslab && a.tgt && a.hw && a.hb && a.dS && a.hprob && !a.hslab &&
+        !a.pcode && !a.x1 && a.W % 64 == 0)
+      return launch_bwd_stream<64, 32, 32, 8, 2, 0, true, false, false, 2>(a, st);
+    return (int)hipErrorInvalidValue;
   }
   if (a.hslab != nullptr) {                        // fused head backward: last decoder conv 32 -> 32
     if (ci == 32 && co == 32 && epi == 0 && a.tgt && a.hw && a.hb && a.dS && a.hprob)

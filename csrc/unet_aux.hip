@@ -506,9 +506,11 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const bf16_t* __restrict_
         sgy[c + 1] = fmaf(q1, v[c + 1], sgy[c + 1]);
       }
     }
+    if (gy) {                  // null: statistics pass (the gradient is formed again on load by its consumer)
 #pragma unroll
-    for (int k = 0; k < C / 8; ++k)
-      *reinterpret_cast<uint4*>(gy + i * ldg + 8 * k) = make_uint4(o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]);
+      for (int k = 0; k < C / 8; ++k)
+        *reinterpret_cast<uint4*>(gy + i * ldg + 8 * k) = make_uint4(o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]);
+    }
   }
   float* out = slab + (long)blockIdx.x * (C + 1);
 #pragma unroll
@@ -538,12 +540,15 @@ __global__ void head_grad_finish(const float* __restrict__ tmp, float* __restric
 }
 
 // bnslab (or null): [head_grid(P)][2][C] BatchNorm backward partial sums of gy (head_bwd_kernel BNS), C = 32 / 64
-// coef (or null, needs bnslab): y is the pre-BN z, y = relu(bn(z)) formed on load as in dpa_head_fwd
+// coef (or null, needs bnslab): y is the pre-BN z, y = relu(bn(z)) formed on load as in dpa_head_fwd;
+// gy (or null, needs bnslab): null = only the segmap gradients and the BN partial sums (the fused conv
+// backward's head + BN mode forms the gradient itself, csrc/bwd_stream.hip)
 DPA_API int dpa_head_bwd(const bf16_t* y, int ldy, int C, const float* w, const float* b, const float* t, const float* dS,
                          bf16_t* gy, int ldg, float* slab, float* tmp, float* gw, float* gb, long long P, float* bnslab,
                          const float* coef, hipStream_t st) {
   const int grid = head_grid(P);
-  if ((ldy & 7) || (ldg & 7) || (bnslab && C != 32 && C != 64) || (coef && !bnslab)) return (int)hipErrorInvalidValue;
+  if ((ldy & 7) || (ldg & 7) || (bnslab && C != 32 && C != 64) || (coef && !bnslab) || (!gy && !bnslab))
+    return (int)hipErrorInvalidValue;
 #define DPA_HB(Cv, BN, ZB) hipLaunchKernelGGL((head_bwd_kernel<Cv, BN, ZB>), dim3(grid), dim3(256), 0, st, y, ldy, w, b, t, dS, gy, ldg, slab, (long)P, bnslab, coef)
   switch (C) {
     case 8: DPA_HB(8, false, false); break;

@@ -453,6 +453,20 @@ class HipBlocks:
                                x2=x2, xbn=xbn)
         return res if want else (res, None)
 
+    def bwd_conv_head_bn(self, c: _Conv, z: torch.Tensor, x: torch.Tensor, st, t, dS, hprob, ycoef, *,
+                         xbn: torch.Tensor = None, stats: list = None):
+        """Fused backward of the last decoder conv of a BN model with the head folded in: ``z`` is its BN
+        input (= st[0]), ``ycoef`` that BN's forward (scale, shift); the kernel forms the head gradient of
+        relu(bn(z)) from ``hprob`` / ``t`` / ``dS`` and the BN backward (partial sums ``stats`` from the head
+        statistics pass) on load.  Returns (dx, BN partial sums of the layer below)."""
+        gw, gb = _grad(c.mod.weight).view(-1), _grad(c.mod.bias)
+        z = st[0]                          # the saved BN input (the head's copy of it is the same storage)
+        coef3 = K.bn_bwd_coef(z, z, st[1], c.bn, _grad(c.bn.weight), _grad(c.bn.bias), stats=stats)
+        seg = self.model.segmap
+        return K.conv_bwd_fused(z, x, self.wd(c), c.Kd, gw, gb, mask=True,
+                                head=(t, seg.weight, seg.bias, dS, None, None, hprob), bn=(z, coef3), bn_stats=True,
+                                xbn=xbn, ybn=ycoef)
+
     def halves_fusable(self, c: _Conv, C: int, W: int) -> bool:
         """A conv over a concat of two C-channel halves whose fused backward does not exist at 2C input
         channels but does at C (the 256^2 decoder conv 128 -> 64): conv(cat) = conv_lo(skip) +
@@ -1042,8 +1056,9 @@ class _DecFn(torch.autograd.Function):
             # BatchNorm model: the head reads relu(bn(z)) on load (forward and backward), so the last decoder
             # conv's BN output is never written: the returned tensor is z, which _HeadFn recognises
             y, coef = B.conv_bn_z(c2, a, st2, xbn=xbn1)
-            S, _ = K.head_fwd(y, seg.weight, seg.bias, tgt, coef=coef)
-            B._head_cache = (y.data_ptr(), tgt.data_ptr(), S, None, coef)
+            # the per-pixel probability is kept for the head backward folded into conv2's (K.BN_HEAD_FOLD)
+            S, probs = K.head_fwd(y, seg.weight, seg.bias, tgt, coef=coef, want_probs=K.BN_HEAD_FOLD)
+            B._head_cache = (y.data_ptr(), tgt.data_ptr(), S, None if probs is None else probs.view(-1), coef)
         else:
             y = B.conv_fwd(c2, a, st=st2, xbn=xbn1)
         ctx.xbn1 = xbn1
@@ -1064,23 +1079,38 @@ class _DecFn(torch.autograd.Function):
         c1, c2 = B.dec_convs[i]
         C = d.Cout
         pend = B._head_pending
-        formed = False
+        formed = folded = False
         if (pend is not None and len(pend) > 5 and g2.data_ptr() == pend[0].data_ptr()
                 and g2.stride() == pend[0].stride()):
             # BatchNorm model, head on load: its gradient (and that BN's backward partial sums) is formed here
             # from (z, coef) rather than in _HeadFn.backward, so the full-resolution gy is a local that dies
             # after this conv's backward instead of an autograd buffer held to the end of this function
             B._head_pending = None
-            _, z2, t, dS, _, coef = pend
+            _, z2, t, dS, hprob, coef = pend
             pend = None
             seg = B.model.segmap
             hs = []
-            g2 = K.head_bwd(z2, seg.weight, seg.bias, t, dS, _grad(seg.weight).view(-1), _grad(seg.bias), bn_stats=hs,
-                            coef=coef)
-            B.ready([seg])
-            head_stats, formed = hs or None, True
+            W = z2.shape[2]
+            if (hprob is not None and K.BN_HEAD_FOLD and c1.bn is not None and c2.Cin == c2.Cout == 32
+                    and B.fusable(c2, c1, W) and W % 64 == 0
+                    and z2.is_contiguous() and st2[0].data_ptr() == z2.data_ptr() and st2[0].stride() == z2.stride()):
+                # head + BN folded into conv2's fused backward: a statistics pass (the segmap gradients and the
+                # BN's partial sums), then the kernel forms gy from z and the stored probability and dz from gy
+                # on load -- the head gradient is never stored
+                K.head_bwd(z2, seg.weight, seg.bias, t, dS, _grad(seg.weight).view(-1), _grad(seg.bias), bn_stats=hs,
+                           coef=coef, store=False)
+                B.ready([seg])
+                g1, st_g = B.bwd_conv_head_bn(c2, z2, a, st2, t, dS, hprob, coef, xbn=ctx.xbn1, stats=hs)
+                folded = True
+            else:
+                g2 = K.head_bwd(z2, seg.weight, seg.bias, t, dS, _grad(seg.weight).view(-1), _grad(seg.bias),
+                                bn_stats=hs, coef=coef)
+                B.ready([seg])
+                head_stats, formed = hs or None, True
             del z2
-        if (pend is not None and len(pend) == 5 and g2.data_ptr() == pend[0].data_ptr()
+        if folded:
+            pass
+        elif (pend is not None and len(pend) == 5 and g2.data_ptr() == pend[0].data_ptr()
                 and g2.stride() == pend[0].stride()):
             # the head's gradient was deferred (_HeadFn.backward): it is formed from y inside this
             # conv's fused backward instead of being materialised (saves a write + read of it)
@@ -1331,7 +1361,8 @@ class _HeadFn(torch.autograd.Function):
         ctx.coef = cache[4] if hit and len(cache) > 4 else None
         # fused forward => y is this engine's last decoder conv output and its backward runs next
         ctx.fold = hit and ctx.coef is None and B.head_bwd_foldable(y.shape[2])
-        ctx.hprob = cache[3] if ctx.fold else None      # the forward's probabilities, for the folded backward
+        # the forward's probabilities, for the folded backward (plain, or BN head on load)
+        ctx.hprob = cache[3] if (ctx.fold or ctx.coef is not None) else None
         ctx.save_for_backward(y, t)
         return S.clone()
 
@@ -1353,7 +1384,8 @@ class _HeadFn(torch.autograd.Function):
         if coef is not None and t.is_contiguous() and K.BN_HEAD_DEFER:
             # BN head on load: defer to the decoder's backward (see _DecFn.backward), like the fold above
             ph = torch.zeros((), dtype=y.dtype, device=y.device).expand(y.shape[0], y.shape[3], y.shape[1], y.shape[2])
-            B._head_pending = (ph, y, t.reshape(-1), dS, None, coef)
+            B._head_pending = (ph, y, t.reshape(-1), dS, ctx.hprob, coef)
+            ctx.hprob = None
             return None, ph, None, None
         stats = [] if B.dec_convs[-1][1].bn is not None else None
         gy = K.head_bwd(y, seg.weight, seg.bias, t, dS, _grad(seg.weight).view(-1), _grad(seg.bias), bn_stats=stats,

@@ -90,6 +90,9 @@ KNOBS = (
          "takes the two-pass fused backward (BN backward on load) instead of dz pass + split dgrad + weight gradient"),
     Knob("bn_skip_z", "DPA_NO_BN_SKIP_Z", True, "BatchNorm UNet: at a dual-input level the encoder's skip is its BN "
          "input z (only the pooled tensor is normalised); the decoder conv forms relu(bn(z)) on load"),
+    Knob("bn_head_fold", "DPA_BN_HEAD_FOLD", False, "BatchNorm UNet: the head backward folded into the last decoder "
+         "conv's fused backward (a statistics pass, then gy and dz formed on load; the head gradient is never stored). "
+         "Off: measured 1.1-1.3 % slower end to end on one box (profiles/bn_knobs_ab_r05.txt, box G)"),
     Knob("bn_head_defer", "DPA_NO_BN_HEAD_DEFER", True, "BatchNorm UNet, head on load: the head backward runs inside the "
          "last decoder level's backward, so its full-resolution gradient is freed there (peak HBM)"),
     Knob("bn_head_on_load", "DPA_NO_BN_HEAD_ON_LOAD", True, "BatchNorm UNet: the segmentation head forms the last decoder "
@@ -179,6 +182,7 @@ class KernelConfig:
     bn_dual: bool = True
     bn_halves: bool = True
     bn_skip_z: bool = True
+    bn_head_fold: bool = False
     f32_wgrad_c4: bool = True
     side_priority: int = 0
     wgrad_stream_blocks: int = 2048

@@ -51,7 +51,7 @@ class BwdArgs(ctypes.Structure):
                [("pcode", c_void_p), ("dpool", c_void_p), ("ldp", c_int)] + \
                [("x1", c_void_p), ("slab1", c_void_p), ("bslab1", c_void_p), ("x1bytes", ctypes.c_uint)] + \
                [("z", c_void_p), ("bncoef", c_void_p), ("bnslab", c_void_p), ("hprob", c_void_p), ("x2", c_void_p),
-                                                                                      ("xbn", c_void_p)]
+                                                                                      ("xbn", c_void_p), ("ybn", c_void_p)]
 
 
 class PackDesc(ctypes.Structure):
@@ -104,6 +104,7 @@ BN_DECONV_ON_LOAD = CFG.bn_deconv_on_load  # a decoder block's output BN applied
 BN_DUAL = CFG.bn_dual                  # BN model: dual-input (no concat buffer) full-resolution decoder level
 BN_HALVES = CFG.bn_halves              # BN model: two-pass fused backward of the concat-input decoder conv
 BN_SKIP_Z = CFG.bn_skip_z              # BN model: the dual-level skip kept as its BN input z
+BN_HEAD_FOLD = CFG.bn_head_fold        # BN model: head backward folded into the last conv's fused backward
 BN_HEAD_DEFER = CFG.bn_head_defer      # ... with its backward deferred into the decoder's (memory)
 # 128-channel convs on the row-block ping-pong GEMM (cfg 15) instead of the row-halo conv: 10-15 % faster
 # on every 128-output-channel 3x3 conv / dgrad of the 512^2 UNet (profiles/kbench_glds_rowblock128_b256_r03.txt)
@@ -626,7 +627,7 @@ def conv_bwd_fused(g: Optional[torch.Tensor], x: torch.Tensor, wd: torch.Tensor,
                    gb: Optional[torch.Tensor], *, mask: bool, dx: Optional[torch.Tensor] = None,
                    dx2: Optional[torch.Tensor] = None, split: int = 0, target_blocks: int = 0, head=None,
                    pool=None, w1=None, bn=None, bn_stats: bool = False, x2: Optional[torch.Tensor] = None,
-                   xbn: Optional[torch.Tensor] = None):
+                   xbn: Optional[torch.Tensor] = None, ybn: Optional[torch.Tensor] = None):
     """Backward of ``y = conv3x3(x) (+bias)`` in one pass (csrc/bwd_stream.hip): returns
     ``dx = conv3x3^T(g)`` (times ``x > 0`` when ``mask``; with ``dx2``/``split`` the channels
     ``>= split`` go to ``dx2``) and ACCUMULATES the weight gradient into ``gw`` (PyTorch OIHW
@@ -746,16 +747,23 @@ def conv_bwd_fused(g: Optional[torch.Tensor], x: torch.Tensor, wd: torch.Tensor,
         assert tgt.dtype == torch.float32 and tgt.is_contiguous() and tgt.numel() == N * H * W
         assert hprob.dtype == torch.float32 and hprob.is_contiguous() and hprob.numel() == N * H * W
         assert hw.dtype == torch.float32 and hw.numel() == CO and hb.numel() == 1
-        assert hgw.is_contiguous() and hgw.numel() == CO and hgb.numel() == 1
         dS = dS.float().contiguous()
-        hslab = torch.empty(nblk * (CO + 1) + CO + 1, dtype=torch.float32, device=x.device)
         hw = hw.reshape(-1).contiguous()
-        a.tgt, a.hw, a.hb, a.dS, a.hslab = tgt.data_ptr(), hw.data_ptr(), hb.data_ptr(), dS.data_ptr(), hslab.data_ptr()
+        a.tgt, a.hw, a.hb, a.dS = tgt.data_ptr(), hw.data_ptr(), hb.data_ptr(), dS.data_ptr()
         a.hprob = hprob.data_ptr()
+        if ybn is not None:
+            # head + BN: g is the BN input z; the segmap gradients came from the head statistics pass
+            assert bn is not None and bn_stats and bn[0].data_ptr() == g.data_ptr(), "head + BN: g is z, with BN sums"
+            assert ybn.dtype == torch.float32 and ybn.is_contiguous() and ybn.numel() == 2 * CO
+            a.ybn = ybn.data_ptr()
+        else:
+            assert hgw.is_contiguous() and hgw.numel() == CO and hgb.numel() == 1
+            hslab = torch.empty(nblk * (CO + 1) + CO + 1, dtype=torch.float32, device=x.device)
+            a.hslab = hslab.data_ptr()
     bnslab = None
     if bn is not None:
         z, coef3 = bn
-        assert head is None and pool is None and w1 is None, "BN mode: plain gradient source"
+        assert (head is None or ybn is not None) and pool is None and w1 is None, "BN mode: plain or head gradient source"
         Nz, Hz, Wz, Cz, ldz = _nhwc(z, "bwd.z")
         assert (Nz, Hz, Wz, Cz) == (N, H, W, CO) and ldz == ldg, "BN mode: z laid out like g"
         assert coef3.dtype == torch.float32 and coef3.is_contiguous() and coef3.numel() == 3 * CO
@@ -879,18 +887,21 @@ def head_fwd(y: torch.Tensor, w: torch.Tensor, b: torch.Tensor, t: Optional[torc
 
 def head_bwd(y: torch.Tensor, w: torch.Tensor, b: torch.Tensor, t: torch.Tensor, dS: torch.Tensor,
              gw: torch.Tensor, gb: torch.Tensor, bn_stats: Optional[list] = None,
-             coef: Optional[torch.Tensor] = None) -> torch.Tensor:
+             coef: Optional[torch.Tensor] = None, store: bool = True) -> Optional[torch.Tensor]:
     """Segmentation-head backward: returns gy = dL/dy (ReLU-masked by y).  ``bn_stats`` (an empty list):
     y is a BatchNorm+ReLU output and the list receives (slab [blocks][2][C], blocks) of sum gy, sum gy*y,
     the BN backward's partial sums (:func:`bn_bwd` ``stats``) -- no statistics pass over (gy, z).
-    ``coef`` (with ``bn_stats``): ``y`` is that BN's input z, y = relu(bn(z)) formed on load (:func:`head_fwd`)."""
+    ``coef`` (with ``bn_stats``): ``y`` is that BN's input z, y = relu(bn(z)) formed on load (:func:`head_fwd`).
+    ``store`` False (with ``bn_stats``): only the segmap gradients and the BN partial sums, returns None (the
+    fused conv backward's head + BN mode forms gy itself, :func:`conv_bwd_fused` ``ybn``)."""
     N, H, W, C, ldy = _nhwc(y, "head_bwd.y")
     if coef is not None:
         assert bn_stats is not None and C in (32, 64) and coef.dtype == torch.float32 and coef.numel() == 2 * C
     P = N * H * W
     L = _lib.lib()
     nblk = L.dpa_head_slab_blocks(c_ll(P))
-    gy = torch.empty(N, H, W, C, dtype=torch.bfloat16, device=y.device)
+    assert store or bn_stats is not None
+    gy = torch.empty(N, H, W, C, dtype=torch.bfloat16, device=y.device) if store else None
     want = bn_stats is not None and C in (32, 64)
     slab = torch.empty(nblk * (C + 1) + C + 1 + (nblk * 2 * C if want else 0), dtype=torch.float32, device=y.device)
     tmp = slab[nblk * (C + 1):nblk * (C + 1) + C + 1]

@@ -443,3 +443,12 @@ def test_unet_bn_step_skip_as_z(hip_lib, monkeypatch):
     conv forms relu(bn(z)) on load, forward and backward) == the step that writes the skip, bit for bit."""
     _knob_step_equal(monkeypatch, "unet-bn", "BN_SKIP_Z", "bn_fwd",
                      lambda a, kw: a[1] is None and kw.get("pool") is not None, seed=11, exact=True)
+
+
+def test_unet_bn_step_head_folded(hip_lib, monkeypatch):
+    """The BN model's head backward folded into the last decoder conv's fused backward (statistics pass, then
+    gy and dz formed on load from z and the stored probability) == head_bwd + BN-mode fused backward."""
+    from distributedpytorch_amd.ops import kernels as K
+    monkeypatch.setattr(K, "BN_HEAD_FOLD", True)        # off by default (measured slower end to end)
+    _knob_step_equal(monkeypatch, "unet-bn", "BN_HEAD_FOLD", "conv_bwd_fused",
+                     lambda a, kw: kw.get("ybn") is not None, seed=12, exact=True)
