@@ -28,10 +28,17 @@ Fusions across block boundaries: the last decoder conv computes the segmentation
 partial sums in its epilogue when the segment ends in the head (``expect_target``); the
 full-resolution transposed convs run their dgrad and weight gradient in one pass.
 
-Variants (north-star DoubleConv / Up): a conv followed by BatchNorm writes its raw output z, then
-``bn_fwd`` (statistics + normalise + ReLU) produces the activation; the backward runs ``bn_bwd``
-on the masked gradient before the conv's dgrad/wgrad.  The bilinear Up path runs its 1x1
-projection at the low resolution and up-samples into the concat half (``_Up``).
+Variants (north-star DoubleConv / Up): a conv followed by BatchNorm writes its raw output z with the
+batch statistics from its epilogue; the BN output relu(bn(z)) is materialised (``bn_fwd``) only where
+its consumer is an LDS-DMA GEMM.  Every other consumer forms it on load from z and the per-channel
+(scale, shift): the second conv of a 32/64-channel DoubleConv (``bn_on_load``), the next decoder block's
+transposed conv (``_zx`` hand-over, forward and backward), the dual-input decoder conv for a skip kept as
+z, and the segmentation head (forward and backward).  Backward: the BN's partial sums (sum g, sum g*y)
+come from whichever kernel produces g (dx epilogues, the head / max-pool / transposed-conv backwards;
+``hand_stats`` / ``take_stats``), and dz = a g + b z + c is formed in the consumer's loader (fused conv
+backward, the first conv's weight gradient) -- a separate ``bn_bwd`` pass remains only in front of the
+deep GEMMs.  The bilinear Up path runs its 1x1 projection at the low resolution and up-samples into the
+concat half (``_Up``).
 """
 from __future__ import annotations
 
