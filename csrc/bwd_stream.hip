@@ -149,7 +149,9 @@ __global__ __launch_bounds__(64 * NW, (HEAD && BNM) ? 1 : 2) void bwd_stream_ker
   // x = relu(bn(z)) formed on load (a.xbn): BN mode 2, and mode 1 with a dual input (x only, not x2 --
   // the decoder conv over [skip | up] whose skip is the encoder BN's input z)
   constexpr bool XBN = BNL;
-  constexpr bool EARLY_XFORM = BNS && CI == 64;   // where the row loop runs the loader transforms (rxform)
+  // where the row loop runs the loader transforms (rxform): in the BN modes at 64 input channels right after
+  // the dx MFMAs (mode 1 too: 2258 / 2274 vs 2253 / 2265 img/s for the BN UNet on one box)
+  constexpr bool EARLY_XFORM = BNL && CI == 64;
   __shared__ __attribute__((aligned(16))) float xbc[XBN ? 2 * CI : 4];
   char* const Wimg = lds;
   char* const Gring = lds + WBYTES;
