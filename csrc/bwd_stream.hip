@@ -206,8 +206,8 @@ __global__ __launch_bounds__(64 * NW, (HEAD && BNM) ? 1 : 2) void bwd_stream_ker
     for (int i = tid; i < 3 * CO; i += NT) bnc[i] = a.bncoef[i];
     if constexpr (HBN)       // (the segmap weights in LDS too: registers are the limit of this mode)
       for (int i = tid; i < 3 * CO; i += NT) ybc[i] = i < 2 * CO ? a.ybn[i] : a.hw[i - 2 * CO];
-    if (xbn)
-      for (int i = tid; i < 2 * CI; i += NT) xbc[i] = a.xbn[i];
+    if (xbn)   // dual input: x's coefficients only, [scale 32 | shift 32] -> xbc[0, 32) and xbc[CI, CI + 32)
+      for (int i = tid; i < (dual ? 64 : 2 * CI); i += NT) xbc[dual && i >= 32 ? CI + i - 32 : i] = a.xbn[i];
     __syncthreads();
   }
   // ---- loader constants

@@ -549,7 +549,8 @@ __global__ __launch_bounds__(256 * WCS) void igemm_stream_kernel(IgemmArgs a) {
   const bool xbn = XBN && a.xbn != nullptr;
   if constexpr (XBN) {
     if (xbn) {
-      for (int i = tid; i < 2 * CS; i += NT) xbc[i] = a.xbn[i];
+      // a dual input's coefficients cover x only: [scale 32 | shift 32] -> xbc[0, 32) and xbc[CS, CS + 32)
+      for (int i = tid; i < (dual ? 64 : 2 * CS); i += NT) xbc[dual && i >= 32 ? CS + i - 32 : i] = a.xbn[i];
       __syncthreads();
     }
   }

@@ -1021,9 +1021,7 @@ class _DecFn(torch.autograd.Function):
             sz = B._zx.pop(skip.data_ptr(), None)
             if sz is not None and sz[0].shape == skip.shape and sz[0].stride() == skip.stride():
                 # the skip is the encoder BN's input z: conv1 reads relu(bn(z)) for its first 32 channels
-                skip_xbn = torch.zeros(4 * C, dtype=torch.float32, device=x.device)
-                skip_xbn[:C].copy_(sz[1][:C])
-                skip_xbn[2 * C:3 * C].copy_(sz[1][C:])
+                skip_xbn = sz[1]
         else:
             cat = B.cat_for(skip)
             up = None

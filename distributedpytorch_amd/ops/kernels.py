@@ -242,9 +242,9 @@ def igemm(x: torch.Tensor, wpacked: torch.Tensor, y: torch.Tensor, *, Ngemm: int
             and not accumulate and not relu and path == "auto" and (mask is None or mch == Ngemm):
         bslab = torch.empty(N * -(-Ho // 16) * -(-Wo // 64) * 2 * Ngemm, dtype=torch.float32, device=y.device)
     if xbn is not None:
-        # with a dual input only x (channels < 32) is formed on load: xbn [scale 64 | shift 64], entries < 32 used
+        # with a dual input only x (channels < 32) is formed on load: xbn = [scale 32 | shift 32]
         assert bslab is not None and mask is None and Cs != 8, "BN-on-load: the BN-statistics stream conv"
-        assert xbn.dtype == torch.float32 and xbn.is_contiguous() and xbn.numel() == 2 * Cs
+        assert xbn.dtype == torch.float32 and xbn.is_contiguous() and xbn.numel() == (64 if x2 is not None else 2 * Cs)
     hprob = None
     if head is not None:
         hw, hb, tgt = head[:3]
@@ -774,7 +774,7 @@ def conv_bwd_fused(g: Optional[torch.Tensor], x: torch.Tensor, wd: torch.Tensor,
         a.bnslab = bnslab.data_ptr()
     if xbn is not None:
         assert (bn_stats or (bn is not None and x2 is not None)) and xbn.dtype == torch.float32
-        assert xbn.is_contiguous() and xbn.numel() == 2 * CI
+        assert xbn.is_contiguous() and xbn.numel() == (64 if x2 is not None else 2 * CI)   # dual: x's only
         a.xbn = xbn.data_ptr()
     _check(L.dpa_bwd_stream(ctypes.byref(a), c_int(CI), c_int(CO), c_int(epi), st), "bwd_stream")
     if hslab is not None:
