@@ -149,9 +149,11 @@ __global__ __launch_bounds__(64 * NW, (HEAD && BNM) ? 1 : 2) void bwd_stream_ker
   // x = relu(bn(z)) formed on load (a.xbn): BN mode 2, and mode 1 with a dual input (x only, not x2 --
   // the decoder conv over [skip | up] whose skip is the encoder BN's input z)
   constexpr bool XBN = BNL;
-  // where the row loop runs the loader transforms (rxform): in the BN modes at 64 input channels right after
-  // the dx MFMAs (mode 1 too: 2258 / 2274 vs 2253 / 2265 img/s for the BN UNet on one box)
-  constexpr bool EARLY_XFORM = BNL && CI == 64;
+  // where the row loop runs the loader transforms (rxform): in BN mode 2 at 64 input channels right after the
+  // dx MFMAs.  Mode 1 keeps them next to the ring store: early, the dual-input split kernel (64 -> 32,
+  // EPI 1) took 8.37 vs 7.77 ms per b256 step and the halves kernel 5.97 vs 6.01 (kernel traces,
+  // profiles/bn_mode1_early_vs_late_r05.txt; the end-to-end A/B, +0.3 %, was within noise)
+  constexpr bool EARLY_XFORM = BNS && CI == 64;
   __shared__ __attribute__((aligned(16))) float xbc[XBN ? 2 * CI : 4];
   char* const Wimg = lds;
   char* const Gring = lds + WBYTES;
