@@ -48,10 +48,23 @@ def test_train_stops_on_signal_and_resumes(tmp_path):
     args = ["-e", "200", "-b", "2", "--synthetic", "--synthetic-len", "16", "--img-size", "32",
             "--model", "unet-tiny", "--backend", "torch", "--dtype", "fp32", "--out-dir", str(tmp_path),
             "--log-every", "1", "--watchdog", "300", "--debug-sync"]
-    t = threading.Timer(1.5, lambda: os.kill(os.getpid(), signal.SIGUSR1))
+    done = threading.Event()
+
+    def fire():
+        # only once train() has installed its handler (SIGUSR1's default action would end the process -- under
+        # a loaded machine the 1.5 s of a fixed timer can pass before that), then a few steps later
+        deadline = time.monotonic() + 120
+        while signal.getsignal(signal.SIGUSR1) in (signal.SIG_DFL, None) and time.monotonic() < deadline:
+            if done.wait(0.05):
+                return
+        if not done.wait(1.0):
+            os.kill(os.getpid(), signal.SIGUSR1)
+
+    t = threading.Thread(target=fire, daemon=True)
     t.start()
     out = train(parse_args(args))
-    t.cancel()
+    done.set()
+    t.join()
     assert out.get("stopped_by_signal") == signal.SIGUSR1
     assert os.path.exists(tmp_path / "checkpoints" / "singleGPU_last.pt")
     stopped = out["step"]
