@@ -25,8 +25,12 @@ static __device__ __forceinline__ unsigned short f2bf(float f) {
   __hip_bfloat16 b = __float2bfloat16(f);
   return *reinterpret_cast<unsigned short*>(&b);
 }
+// two f32 -> one bf16 pair, round-to-nearest-even: ONE v_cvt_pk_bf16_f32 (two scalar casts compile to two
+// of them plus a v_or_b32_sdwa -- three VALU per pair in every epilogue and loader transform)
+typedef __attribute__((ext_vector_type(2))) float f32x2_t;
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
 static __device__ __forceinline__ unsigned int pack_bf2(float lo, float hi) {
-  return (unsigned int)f2bf(lo) | ((unsigned int)f2bf(hi) << 16);
+  return __builtin_bit_cast(unsigned int, __builtin_convertvector(f32x2_t{lo, hi}, bf16x2_t));
 }
 static __device__ __forceinline__ float lo_bf(unsigned int u) { return __uint_as_float(u << 16); }
 static __device__ __forceinline__ float hi_bf(unsigned int u) { return __uint_as_float(u & 0xffff0000u); }
