@@ -109,8 +109,9 @@ KNOBS = (
     Knob("wgrad_gemm_blocks", "DPA_WGRAD_GEMM_BLOCKS", 768, "target workgroups of a dense-GEMM weight gradient"),
     Knob("bwd_blocks", "DPA_BWD_BLOCKS", 1024, "minimum workgroups of a fused backward launch"),
     Knob("bwd_blocks_small", "DPA_BWD_BLOCKS_SMALL", 512, "the same for launches over < 2^25 pixels"),
-    Knob("enc0_chunks", "DPA_ENC0_CHUNKS", 4, "first encoder level backward in this many image chunks, so the first "
-         "conv's side-stream weight gradient of one chunk overlaps the next chunk's fused backward (1 = off)"),
+    Knob("enc0_chunks", "DPA_ENC0_CHUNKS", 8, "first encoder level backward in this many image chunks, so the first "
+         "conv's side-stream weight gradient of one chunk overlaps the next chunk's fused backward (1 = off); 8 vs "
+         "4: step wall 86.02 / 85.98 vs 86.61 / 86.04 ms in kernel traces at b256 (profiles/enc0_chunks_r05.txt)"),
 )
 
 # process / launcher environment (not kernel dispatch): documented here so the allow-list is complete
@@ -189,7 +190,7 @@ class KernelConfig:
     wgrad_gemm_blocks: int = 768
     bwd_blocks: int = 1024
     bwd_blocks_small: int = 512
-    enc0_chunks: int = 4
+    enc0_chunks: int = 8
     bwd_blocks_set: bool = False          # DPA_BWD_BLOCKS given explicitly: applies to every launch
 
     @classmethod
