@@ -30,9 +30,6 @@ BASELINE_METRIC = "images/sec (whole node) UNet 512x512 bf16 at 1/2/4/8 MI355X; 
 # so vs_baseline compares against the batch-32 rate; the reference publishes no number.
 STOCK_BASELINE_PER_GPU = 909.62
 STOCK_BASELINE_BATCH = 32
-# this framework at the SAME per-GPU batch 32, same box and session as the stock run
-# (profiles/bench_b32_640x960_r03_end.txt: 2680 img/s; round 2: 2383) -> the equal-batch ratio
-EQUAL_BATCH_RATIO_B32 = round(2679.87 / 909.62, 3)
 
 
 def _hw(s: str):
@@ -62,10 +59,18 @@ def parse():
     ap.add_argument("--pool", type=int, default=2, help="distinct synthetic batches cycled")
     ap.add_argument("--out", default=None, help="also append the JSON line to this file")
     ap.add_argument("--graph", action="store_true", help="N=1: replay the step from a captured HIP graph")
-    ap.add_argument("--parallelism", choices=["dp", "mp"], default="dp",
+    ap.add_argument("--parallelism", choices=["dp", "mp", "dp1proc"], default="dp",
                     help="dp: one replica per GPU, RCCL all-reduce (weak scaling); mp: GPipe over the N ranks "
                          "(one batch of --batch images split into --microbatches, strong scaling); with one "
-                         "process, mp runs --stages stages on cuda:0 (pipeline rehearsal)")
+                         "process, mp runs --stages stages on cuda:0 (pipeline rehearsal); dp1proc: -t DP, one "
+                         "process driving --replicas replicas (one host thread each, native RCCL clique, "
+                         "--batch images per replica; replicas beyond the visible GPUs share them: a host-"
+                         "issue rehearsal)")
+    ap.add_argument("--replicas", type=int, default=0,
+                    help="dp1proc: replicas (0: one per visible GPU)")
+    ap.add_argument("--comm-probe", action="store_true",
+                    help="N=1 dp: after the timed steps, run steps that launch an RCCL-bucket stand-in at each "
+                         "DDP bucket-ready point and report how long it waited for CUs (utils/comm_probe.py)")
     ap.add_argument("--microbatches", type=int, default=0,
                     help="mp microbatches (0: the pipeline plan's count for this model / image / stages / batch, "
                          "parallel/plans.json; without one 2 for the reference cut, 8 otherwise)")
@@ -134,7 +139,8 @@ def main():
     from distributedpytorch_amd.data.synthetic import synthetic_batch
     from distributedpytorch_amd.models.summary import layer_table
     from distributedpytorch_amd.models.unet import PRESETS, build_model, count_params
-    from distributedpytorch_amd.trainer import DDPStrategy, PipelineDistStrategy, PipelineLocalStrategy, SingleDevice
+    from distributedpytorch_amd.trainer import (DDPStrategy, DPStrategy, PipelineDistStrategy, PipelineLocalStrategy,
+                                                SingleDevice)
     from distributedpytorch_amd.compute import resolve_backend
     from distributedpytorch_amd.utils import set_seed
 
@@ -145,7 +151,9 @@ def main():
         K.set_timing_ablation(ablate)
         print(f"[bench] TIMING ABLATION {ablate}: results are numerically wrong", file=sys.stderr, flush=True)
     mp = a.parallelism == "mp"
-    method = "MP" if mp else ("DDP" if world > 1 else "singleGPU")
+    dp1 = a.parallelism == "dp1proc"
+    assert not (dp1 and world > 1), "dp1proc is one process"
+    method = "MP" if mp else ("DP" if dp1 else ("DDP" if world > 1 else "singleGPU"))
     cfg = TrainConfig(train_method=method, batch_size=a.batch, img_size=a.img, dtype=a.dtype,
                       backend=a.backend, model=a.model, bucket_mb=a.bucket_mb, lr=1e-4,
                       grad_comm_dtype=a.grad_comm_dtype, comm_overlap=a.comm_overlap,
@@ -158,7 +166,14 @@ def main():
                    "policy": mpp.policy, **mpp.info}
     model = build_model(a.model)
     nparams = count_params(model)
-    if mp and world > 1:
+    n_rep = 1
+    if dp1:
+        ngpu = torch.cuda.device_count()
+        n_rep = a.replicas or ngpu
+        devs = [torch.device(f"cuda:{i % ngpu}") for i in range(n_rep)]
+        strat = DPStrategy(cfg, model.to(devs[0]), devs)
+        same_dev = len({d.index for d in devs}) < n_rep
+    elif mp and world > 1:
         strat = PipelineDistStrategy(cfg, model, device)
     elif mp:
         strat = PipelineLocalStrategy(cfg, model.to(device), [device] * a.stages)
@@ -168,7 +183,8 @@ def main():
 
     pool = []
     for i in range(a.pool):
-        img, mask = synthetic_batch(a.batch, a.img[0], a.img[1], 3, seed=1000 * rank + i, device=device)
+        # dp1proc: the global batch on cuda:0, scattered to the replicas inside the step (reference -t DP)
+        img, mask = synthetic_batch(a.batch * n_rep, a.img[0], a.img[1], 3, seed=1000 * rank + i, device=device)
         pool.append((img, mask.float().unsqueeze(1)))
 
     graphed = None
@@ -201,11 +217,14 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    evs = [torch.cuda.Event(enable_timing=True) for _ in range(a.steps + 1)] if world > 1 else None
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(a.steps + 1)] if (world > 1 or dp1) else None
     if evs:
         evs[0].record()
+    host_s = 0.0          # host time inside the step calls: the launch/issue cost (asynchronous kernels)
     for i in range(a.steps):
+        h0 = time.perf_counter()
         loss = step(a.warmup + i)
+        host_s += time.perf_counter() - h0
         if evs:
             evs[i + 1].record()
     if world > 1:
@@ -233,7 +252,7 @@ def main():
     # batch, each of the --mp-replicas pipelines trains its own
     R = max(1, a.mp_replicas) if mp and world > 1 else 1
     S = world // R if mp and world > 1 else (a.stages if mp else 1)
-    imgs = a.batch * (R if mp else world) * a.steps
+    imgs = a.batch * (R if mp else world * n_rep) * a.steps
     value = imgs / elapsed
     ms = 1000.0 * elapsed / a.steps
     # vs_baseline: like for like only, i.e. null unless stock PyTorch-ROCm was measured at THIS per-GPU
@@ -242,12 +261,18 @@ def main():
     # quotient over stock-at-32 stay in vs_baseline_basis as context.
     vs = cross = None
     per_gpu_batch = a.batch if not mp else a.batch // max(1, S)
-    if STOCK_BASELINE_PER_GPU and not a.infer and a.dtype == "bf16":
-        cross = round(value / (STOCK_BASELINE_PER_GPU * world), 4)
-        if per_gpu_batch == STOCK_BASELINE_BATCH and not mp and a.img == (512, 512) and a.model == "unet":
+    # like for like only: one real GPU, the stock run's config (a multi-rank or replica run would compare
+    # against N x the single-GPU stock rate, and stock DDP / DP were never measured)
+    same_device_ranks = os.environ.get("DPA_SAME_DEVICE", "0") == "1"
+    if STOCK_BASELINE_PER_GPU and not a.infer and a.dtype == "bf16" and world == 1 and not dp1 and not mp:
+        cross = round(value / STOCK_BASELINE_PER_GPU, 4)
+        if (per_gpu_batch == STOCK_BASELINE_BATCH and a.img == (512, 512) and a.model == "unet"
+                and not same_device_ranks and a.backend != "torch"):
             vs = cross
     if mp:
         par = f"mp{S}x{strat.pipe.M}mb" + ("" if world > 1 else "-1gpu") + (f"-dp{R}" if R > 1 else "")
+    elif dp1:
+        par = f"dp1proc{n_rep}" + ("-shared-gpu" if same_dev else "")
     else:
         par = f"dp{world}"
     out = {
@@ -258,15 +283,15 @@ def main():
         # equal-batch ratio there and this run over stock-at-32 (cross_batch_ratio, different batches
         # unless --batch 32)
         "vs_baseline_basis": {"kind": ("stock_measured_at_this_batch" if vs is not None else
-                                       "null: stock not measurable at this batch (MIOpen find > 1080 s at b256)"),
+                                       "null: stock PyTorch-ROCm measured only on one GPU at batch 32 (its MIOpen "
+                                       "find did not finish in 1080 s at b256)"),
                               "stock_per_gpu_img_s": STOCK_BASELINE_PER_GPU, "stock_per_gpu_batch": STOCK_BASELINE_BATCH,
                               "this_per_gpu_batch": per_gpu_batch,
-                              "equal_batch_ratio_b32": EQUAL_BATCH_RATIO_B32,
                               "cross_batch_ratio": cross},
         "dtype": a.dtype,
         "data": "synthetic (GPU-generated images + ellipse masks), random-init weights",
         "config": {"model": f"{a.model} (reference 4-level UNet, base 32, {nparams} params)" if a.model == "unet"
-                   else a.model, "global_batch": a.batch * (R if mp else world),
+                   else a.model, "global_batch": a.batch * (R if mp else world * n_rep),
                    "per_gpu_batch": per_gpu_batch,
                    "seq_len": a.img[0] * a.img[1], "image_hw": list(a.img),
                    "parallelism": par, "backend": backend,
@@ -274,12 +299,31 @@ def main():
                    "grad_comm_dtype": a.grad_comm_dtype, "comm_overlap": a.comm_overlap,
                    "hip_graph": graphed is not None},
         "final_loss": round(final_loss, 5) if final_loss == final_loss else None, "warmup_s": round(warm_s, 2),
+        "host_ms_per_step": round(1000.0 * host_s / a.steps, 3),
         "peak_mem_gb": round(torch.cuda.max_memory_allocated(device) / 2 ** 30, 2),
         # the run's non-default kernel switches (ops/config.py; empty = the shipped dispatch)
         "kernel_config": {k: v for k, v in K.CFG.non_default().items()},
     }
     if ablate:
         out["INVALID_timing_ablation"] = ablate
+    if dp1:
+        # host issue (one thread per replica + the autograd walk) vs device time per step: above 1 the step
+        # is host-bound and more replicas per process would not scale
+        dev_ms = sum(evs[i].elapsed_time(evs[i + 1]) for i in range(a.steps)) / a.steps
+        out["dp1proc"] = {"replicas": n_rep, "devices": sorted({d.index for d in devs}),
+                          "native_clique": strat.dp.comm is not None, "device_ms_per_step_dev0": round(dev_ms, 3),
+                          "host_ms_per_step": out["host_ms_per_step"],
+                          "host_over_device": round(out["host_ms_per_step"] / max(dev_ms, 1e-9), 3)}
+    if a.comm_probe:
+        assert world == 1 and not mp and not dp1 and hasattr(strat, "space")
+        from distributedpytorch_amd.utils.comm_probe import CommProbe
+        probe = CommProbe(strat.space, bucket_mb=a.bucket_mb)
+        res = None
+        for i in range(3):      # outside the timed region: each probed step synchronises
+            probe.start_step()
+            step(i)
+            res = probe.finish_step()
+        out["comm_probe"] = res
     if not a.infer and a.model in PRESETS:
         # achieved model FLOP rate: forward FLOPs (analytic layer table) x 3 for forward + dgrad + wgrad
         fwd_gflop = sum(r[3] for r in layer_table(PRESETS[a.model], a.img[0], a.img[1]))

@@ -617,3 +617,26 @@ DPA_API int dpa_loss_grad(const float* g, const float* coef, float scale, float*
   hipLaunchKernelGGL(loss_grad_kernel, dim3(1), dim3(64), 0, st, g, coef, scale, dS);
   return (int)hipGetLastError();
 }
+
+// ---- communication-slot probe (VERDICT r5 #3c): a stand-in for an RCCL all-reduce bucket launched while
+// the backward's one-workgroup-per-CU GEMMs hold the CUs.  RCCL's ring kernels run a few workgroups
+// (one per channel) that stream the bucket through L2/HBM; this kernel has that geometry -- `blocks`
+// workgroups of 256 threads copying `n` float4 -- and each workgroup's lanes stamp the constant 100 MHz
+// clock when the workgroup starts and when it ends (stamp[2 * block + {0, 1}], vector stores), so the host
+// can separate "waited for a CU" from "ran slowly beside the GEMMs".
+__global__ __launch_bounds__(256) void comm_probe_kernel(const float4* __restrict__ src, float4* __restrict__ dst,
+                                                         long n, unsigned long long* __restrict__ stamp) {
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  const int lane = threadIdx.x & 63;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) dst[i] = src[i];
+  __syncthreads();
+  const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+  if (threadIdx.x < 64 && lane < 2) stamp[2 * blockIdx.x + lane] = lane == 0 ? t0 : t1;
+}
+DPA_API int dpa_comm_probe(const void* src, void* dst, long long n16, int blocks, unsigned long long* stamp,
+                           hipStream_t st) {
+  if (blocks < 1 || blocks > 1024 || n16 < 0) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(comm_probe_kernel, dim3(blocks), dim3(256), 0, st, (const float4*)src, (float4*)dst, (long)n16,
+                     stamp);
+  return (int)hipGetLastError();
+}

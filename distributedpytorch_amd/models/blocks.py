@@ -181,8 +181,15 @@ def run_segment(blocks, start: int, end: int, depth: int, env: Dict[str, torch.T
     if start == 0:
         env["x"] = blocks.prep(env["x"])
     units = segment_units(start, end, depth)
-    if hasattr(blocks, "skip_z_ok"):
-        blocks.skip_z_ok = emit is None     # a pipeline stage may send its skips: they must be plain tensors
+    if hasattr(blocks, "skip_z_levels"):
+        # a backend may keep a skip in an internal form (models/hip_unet.py: a BatchNorm's input z, normalised
+        # by its consumer on load) only when that consumer runs inside THIS call: the hand-over is keyed in the
+        # engine and reset by prep(), so a skip consumed by another segment (a pipeline's other stage, the
+        # second segment of a mirrored placement, the next microbatch's prep in between) must stay plain
+        enc_here = {i for idx, part in units for k, i in [block_kind(idx, depth)] if k == "enc" and part != "a"}
+        dec_here = {depth - 1 - i for idx, part in units for k, i in [block_kind(idx, depth)]
+                    if k == "dec" and part != "b"}
+        blocks.skip_z_levels = (enc_here & dec_here) - set(getattr(blocks, "dense_skips", ()))
     for u, (idx, part) in enumerate(units):
         kind, i = block_kind(idx, depth)
         if kind == "dec" and hasattr(blocks, "next_dec_local"):

@@ -149,8 +149,10 @@ class HipBlocks:
         self._stats_hand = {}
         # decoder outputs handed to the next decoder block as their BatchNorm input z (run_segment sets
         # next_dec_local when that block follows in the same segment): z data_ptr -> (z, coef)
+        # skip_z_levels: encoder levels whose skip may be kept as that BN's input z (run_segment: the
+        # consuming decoder level runs in the same call and the skip is not sent)
         self.next_dec_local = False
-        self.skip_z_ok = False
+        self.skip_z_levels = set()
         self._zx = {}
         # pipeline microbatches: the side-stream conv weight gradients of every microbatch are deferred
         # and run as ONE launch per layer over all microbatches' images (K.wgrad_multi) -- one split-K
@@ -162,6 +164,10 @@ class HipBlocks:
         self._deferred = {}
         self._deferred_ready = []
         self._flush_queued = False
+        # early_ready (set by a strategy whose reducer listens): per-module announcement as soon as the last
+        # microbatch's contribution is issued, instead of all at flush_wgrad
+        self.early_ready = False
+        self._ready_count, self._seen_mods, self._announced = {}, {}, set()
         self.side2 = None             # stream of the merged (all-microbatch) weight-gradient launches
         self._keep2 = []              # (event after the launch, its operands): released once the event is done
         # memory bound of the deferral: a layer's deferred gradients and inputs stay alive
@@ -631,12 +637,42 @@ class HipBlocks:
 
     def ready(self, mods):
         if self.defer_wgrad > 1 and (self._deferred or self._defer_window or self._flush_queued):
-            self._deferred_ready.extend(mods)   # final only after flush_wgrad
+            if not self.early_ready:
+                self._deferred_ready.extend(mods)   # final only after flush_wgrad
+                return
+            # a data-parallel reducer listens (pipelines x replicas): announce a module as soon as its last
+            # microbatch's contribution is issued -- its buckets' all-reduces then overlap the rest of the
+            # stage's backward instead of following it
+            final = []
+            for m in mods:
+                if m is None or id(m) in self._announced:
+                    continue
+                n = self._ready_count.get(id(m), 0) + 1
+                self._ready_count[id(m)] = n
+                self._seen_mods[id(m)] = m
+                if n >= self.defer_wgrad and not any(e[0].mod is m for e in self._deferred.values()):
+                    final.append(m)
+            if final:
+                self._announce_now(final)
             return
         if self._side_pending:          # some of these gradients may still be in flight on the side stream
             self._ready_pending.extend(mods)
             return
         self._notify(mods)
+
+    def _announce_now(self, mods):
+        """Announce final gradients produced on any of this engine's streams: the announcement (and the
+        collective a listener launches from it) is issued on the merged-launch stream after it has caught up
+        with the compute and side streams -- the compute stream itself never waits."""
+        for m in mods:
+            self._announced.add(id(m))
+        if self.side2 is None:
+            self.side2 = torch.cuda.Stream(device=self.device, priority=K.SIDE_PRIORITY)
+        self.side2.wait_stream(torch.cuda.current_stream(self.device))
+        if self.side is not None:
+            self.side2.wait_stream(self.side)
+        with torch.cuda.stream(self.side2):
+            self._notify(mods)
 
     def open_defer_window(self):
         """Pipeline stage backward over several microbatches begins: defer until close_defer_window()."""
@@ -684,6 +720,10 @@ class HipBlocks:
             self._keep2 = []
         self.join()
         mods, self._deferred_ready = self._deferred_ready, []
+        if self.early_ready:
+            # the modules not yet announced (a layer whose merged launch waited for the flush)
+            mods = [m for k, m in self._seen_mods.items() if k not in self._announced]
+            self._ready_count, self._seen_mods, self._announced = {}, {}, set()
         if mods:
             self._notify(mods)
 
@@ -844,7 +884,7 @@ class _EncFn(torch.autograd.Function):
         # window codes (argmax + ReLU masks) for the backward: it then never re-reads the skip
         code = (torch.empty(N, H // 2, W // 2, c2.Cout, dtype=torch.uint8, device=x.device)
                 if H % 2 == 0 and W % 2 == 0 else None)
-        if (cat is None and code is not None and c2.bn is not None and K.BN_SKIP_Z and B.skip_z_ok
+        if (cat is None and code is not None and c2.bn is not None and K.BN_SKIP_Z and l in B.skip_z_levels
                 and B.model.training and K.BN_SUMS_POOL and K.BN_SUMS_POOL_Z and l not in B.dense_skips
                 and B.dual_level(l, H, W) and B.bn_on_load(*B.dec_convs[len(B.dec_convs) - 1 - l], H, W)):
             # the skip's consumer (the decoder conv's dual input) forms relu(bn(z)) on load: the skip IS z and

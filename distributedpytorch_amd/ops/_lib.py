@@ -58,7 +58,7 @@ def _declare(L):
                  "dpa_igemm_stream_blocks", "dpa_slab_fold", "dpa_bwd_stream", "dpa_head_grad_from_slab", "dpa_bwd_stream_pool_ok",
                  "dpa_wgrad_reduce_cfg", "dpa_igemm_f32", "dpa_wgrad_f32", "dpa_relu_bwd_f32", "dpa_maxpool2_f32",
                  "dpa_maxpool2_bwd_f32", "dpa_head_f32_blocks", "dpa_head_f32", "dpa_head_bwd_f32", "dpa_nchw_to_nhwc4_f32",
-                 "dpa_channel_sum_f32", "dpa_enc_out_bwd_f32", "dpa_pack_weights_f32", "dpa_zero"):
+                 "dpa_channel_sum_f32", "dpa_enc_out_bwd_f32", "dpa_pack_weights_f32", "dpa_zero", "dpa_comm_probe"):
         getattr(L, name).restype = ctypes.c_int
     L.dpa_head_slab_blocks.restype = ctypes.c_int
     L.dpa_head_slab_blocks.argtypes = [ctypes.c_longlong]

@@ -1189,3 +1189,14 @@ def backward_scaled(loss: torch.Tensor, scale: float) -> None:
     if seed is None:
         seed = _SEEDS[key] = torch.full((), float(scale), dtype=loss.dtype, device=loss.device)
     torch.autograd.backward(loss, seed)
+
+
+def comm_probe(src: torch.Tensor, dst: torch.Tensor, stamp: torch.Tensor, blocks: int = 32):
+    """RCCL-bucket stand-in (csrc/unet_aux.hip ``comm_probe_kernel``): ``blocks`` workgroups copy ``src``
+    into ``dst`` (16-B aligned, same byte size) on the CURRENT stream; ``stamp`` (int64, >= 2 * blocks) gets
+    each workgroup's start / end on the GPU's constant 100 MHz clock."""
+    nb = src.numel() * src.element_size()
+    assert nb % 16 == 0 and dst.numel() * dst.element_size() == nb and stamp.numel() >= 2 * blocks
+    assert stamp.dtype == torch.int64 and src.is_cuda and dst.is_cuda and stamp.is_cuda
+    _check(_lib.lib().dpa_comm_probe(_p(src), _p(dst), c_ll(nb // 16), c_int(blocks), _p(stamp),
+                                     c_void_p(torch.cuda.current_stream(src.device).cuda_stream)), "comm_probe")

@@ -59,8 +59,11 @@ def bucket_plan(space: FlatParameterSpace, bucket_mb: float = 8.0, first_bucket_
 class BucketedAllReduce:
     def __init__(self, space: FlatParameterSpace, bucket_mb: float = 8.0, first_bucket_mb: float = 1.0,
                  group=None, average: bool = True, scale: float = 1.0, comm_dtype: str = "fp32",
-                 overlap: bool = True):
+                 overlap: bool = True, per_param: int = 1):
         self.space = space
+        # announcements that make one parameter's gradient final: 1, or the microbatch count for autograd
+        # hooks that fire once per microbatch (a pipeline stage on the torch backend)
+        self.per_param = max(1, int(per_param))
         self.overlap = bool(overlap)
         # "bf16": each bucket travels as bf16 (half the xGMI bytes; torch's bf16_compress_hook
         # semantics: pre-scaled, reduced in bf16, written back into the fp32 flat buffer)
@@ -100,7 +103,7 @@ class BucketedAllReduce:
         if getattr(self, "launch_log", None):
             self.last_launch_log = self.launch_log
         self.pending = list(self.expected)
-        self.seen = [False] * len(self.bucket_of)
+        self.seen = [0] * len(self.bucket_of)
         self.n_ready = 0
         self.next_launch = 0
         self.works = []
@@ -112,9 +115,11 @@ class BucketedAllReduce:
     def mark_ready(self, param_index: int):
         # a parameter announced twice in one step (an autograd hook AND notify_ready, or a double
         # notify) would otherwise drive its bucket's count below zero and stall it until finish()
-        assert not self.seen[param_index], \
-            f"gradient of parameter {param_index} ({self.space.names[param_index]}) announced twice in one step"
-        self.seen[param_index] = True
+        assert self.seen[param_index] < self.per_param, \
+            f"gradient of parameter {param_index} ({self.space.names[param_index]}) announced too often in one step"
+        self.seen[param_index] += 1
+        if self.seen[param_index] < self.per_param:
+            return
         self.n_ready += 1
         b = self.bucket_of[param_index]
         self.pending[b] -= 1

@@ -31,7 +31,7 @@ from .models.unet import build_model
 from .optim import FlatParameterSpace, FusedAdam, make_plateau, plateau_step
 from .parallel.ddp import BucketedAllReduce, broadcast_parameters, sync_buffers
 from .parallel.dp import ReplicatedDataParallel
-from .parallel.pipeline import GPipeDist, GPipeLocal
+from .parallel.pipeline import GPipeDist, GPipeLocal, placement_buffer_names
 from .utils import LossCurves, MetricsLogger, load_model_state, save_model, set_seed
 from .utils.checkpoint import load_training_state, save_training_state
 from .utils.resilience import ShutdownGuard, StepWatchdog, check_finite, comm_env_defaults
@@ -309,21 +309,54 @@ class PipelineDistStrategy(Strategy):
         # the head stage owns the loss (pipeline 0's logs); rank 0 saves
         self.is_main = self.pipe.is_last and self.replica == 0
         self.optimizer = FusedAdam(self.pipe.space, lr=cfg.lr, weight_decay=cfg.weight_decay)
+        self.reducer = None
         if R > 1:   # every pipeline starts from pipeline 0's parameters (stage s: global rank s)
             dist.broadcast(self.pipe.space.data, src=self.stage, group=self.dp_group)
             self.pipe.space.touch()
+            self.sync_stage_buffers()
+            # data parallel across the pipelines: each stage's flat gradient averaged over its R copies in
+            # buckets launched as soon as their gradients are final -- during the stage's last microbatch's
+            # backward (the pipeline drain), not after it.  The HIP engine announces a layer once its last
+            # microbatch's contribution is issued (``early_ready``: the merged weight-gradient launch + the
+            # bucket's all-reduce ordered on its side stream); the torch backend's autograd hooks fire once
+            # per microbatch, so a parameter is final at its M-th.
+            blocks = self.pipe.blocks
+            per_param = 1
+            if hasattr(blocks, "early_ready"):
+                blocks.early_ready = True
+            else:
+                per_param = self.plan.microbatches
+            self.reducer = BucketedAllReduce(self.pipe.space, bucket_mb=cfg.bucket_mb, group=self.dp_group,
+                                             comm_dtype=cfg.grad_comm_dtype, overlap=cfg.comm_overlap,
+                                             per_param=per_param).register_hooks()
+
+    def sync_stage_buffers(self):
+        """Pipeline 0's stage buffers (BatchNorm running statistics) to every replica of the stage: torch
+        DDP's ``broadcast_buffers`` across the pipelines, so validation and the checkpoint (pipeline 0's)
+        describe one model."""
+        if self.replicas <= 1:
+            return
+        bufs = dict(self.model.named_buffers())
+        for n in placement_buffer_names(self.model, self.pipe.pl, self.stage):
+            b = bufs[n]
+            if self.pipe._host_staged:
+                h = b.cpu()
+                dist.broadcast(h, src=self.stage, group=self.dp_group)
+                b.copy_(h)
+            else:
+                dist.broadcast(b, src=self.stage, group=self.dp_group)
+
+    def before_eval(self):
+        self.sync_stage_buffers()
 
     def train_step(self, images, targets):
         self.optimizer.zero_grad()
         B = images.shape[0]
         loss = self.pipe.train_step(images, targets, B, self.cfg.img_size,
                                     loss_scale=_loss_scale(self.cfg, B))
-        if self.replicas > 1:
-            # data parallel across the pipelines: each stage's flat gradient averaged over its R copies
-            # (one all-reduce per stage per step, DDP semantics: the mean of the per-pipeline losses' grads)
-            g = self.pipe.space.grad
-            dist.all_reduce(g, group=self.dp_group)
-            g.mul_(1.0 / self.replicas)
+        if self.reducer is not None:
+            # DDP semantics: the mean over the pipelines of each pipeline's gradient
+            self.reducer.finish()
         self.optimizer.step()
         return None if loss is None else loss.detach()
 
@@ -335,6 +368,9 @@ class PipelineDistStrategy(Strategy):
         return loss_from_partials(_partials(p, targets), targets.numel()), dice_score(p, targets)
 
     def state_dict(self):
+        self.sync_stage_buffers()
+        if self.replica != 0:
+            return None        # replicas hold pipeline 0's state; only pipeline 0 gathers (rank 0 saves)
         return self.pipe.gather_state_dict()
 
     def optimizer_state_dict(self):

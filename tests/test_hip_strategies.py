@@ -275,3 +275,39 @@ def test_dp_bucket_reducer_native_clique(hip_lib):
     torch.cuda.synchronize()
     assert torch.equal(sp.grad, ref)
     assert red.exposed_comm_ms() >= 0
+
+
+def _bench(extra, timeout=300):
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--steps", "3", "--warmup", "1"] + extra,
+                       capture_output=True, text=True, timeout=timeout, cwd=root)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    return json.loads(lines[0])
+
+
+def test_bench_dp1proc_replicas_share_one_gpu(hip_lib):
+    """VERDICT r5 #3a: ``-t DP`` has a bench path (DPStrategy, one process, a host thread per replica); on one
+    GPU its replicas share cuda:0 (host-issue rehearsal, Python-sum reduction instead of the RCCL clique)."""
+    out = _bench(["--parallelism", "dp1proc", "--replicas", "2", "--batch", "4", "--img", "128"])
+    assert out["config"]["parallelism"].startswith("dp1proc2") and out["config"]["global_batch"] == 8
+    assert abs(out["value"] - 8 * 1000.0 / out["ms_per_step"]) < 0.02 * out["value"]
+    d = out["dp1proc"]
+    assert d["replicas"] == 2 and d["host_ms_per_step"] > 0 and d["device_ms_per_step_dev0"] > 0
+    assert out["vs_baseline"] is None
+
+
+def test_bench_comm_probe_reports_every_bucket(hip_lib):
+    """VERDICT r5 #3c: the RCCL-bucket stand-in launched at each bucket-ready point of the backward
+    (utils/comm_probe.py) reports its wait for CUs next to its idle time, for every DDP bucket."""
+    out = _bench(["--batch", "8", "--img", "256", "--comm-probe", "--bucket-mb", "1"])
+    cp = out["comm_probe"]
+    assert cp["unlaunched"] == 0 and len(cp["buckets"]) >= 2
+    for b in cp["buckets"]:
+        assert b["total_us"] > 0 and b["run_us"] > 0 and b["idle"]["run_us"] > 0
+        assert 0 <= b["ready_at_us"] <= cp["step_us"]
