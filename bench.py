@@ -78,7 +78,7 @@ def parse():
     ap.add_argument("--mp-replicas", type=int, default=1,
                     help="mp over N ranks: R pipelines of N/R stages, data-parallel across them (each pipeline "
                          "trains its own --batch images)")
-    ap.add_argument("--mp-cut", choices=["auto", "reference", "balanced", "v", "time"], default="auto",
+    ap.add_argument("--mp-cut", choices=["auto", "reference", "balanced", "v", "time", "spatial"], default="auto",
                     help="mp stage placement (auto: the link-aware plan from measured block times when "
                          "parallel/plans.json has one for this configuration, else the skip-local mirrored "
                          "V placement; reference: the reference's encoder|decoder cut)")
@@ -184,7 +184,9 @@ def main():
     pool = []
     for i in range(a.pool):
         # dp1proc: the global batch on cuda:0, scattered to the replicas inside the step (reference -t DP)
-        img, mask = synthetic_batch(a.batch * n_rep, a.img[0], a.img[1], 3, seed=1000 * rank + i, device=device)
+        # mp: the ranks of one pipeline share a batch (a row-split plan reads every rank's rows of it)
+        data_rank = rank // max(1, world // max(1, a.mp_replicas)) if (mp and world > 1) else rank
+        img, mask = synthetic_batch(a.batch * n_rep, a.img[0], a.img[1], 3, seed=1000 * data_rank + i, device=device)
         pool.append((img, mask.float().unsqueeze(1)))
 
     graphed = None
@@ -295,7 +297,8 @@ def main():
                    "per_gpu_batch": per_gpu_batch,
                    "seq_len": a.img[0] * a.img[1], "image_hw": list(a.img),
                    "parallelism": par, "backend": backend,
-                   "mp_cut": (str(strat.pipe.pl) if mp else None), "mp_plan": mp_info, "bucket_mb": a.bucket_mb,
+                   "mp_cut": (str(getattr(strat.pipe, "pl", None) or strat.pipe.plan) if mp else None),
+                   "mp_plan": mp_info, "bucket_mb": a.bucket_mb,
                    "grad_comm_dtype": a.grad_comm_dtype, "comm_overlap": a.comm_overlap,
                    "hip_graph": graphed is not None},
         "final_loss": round(final_loss, 5) if final_loss == final_loss else None, "warmup_s": round(warm_s, 2),

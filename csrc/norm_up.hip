@@ -473,3 +473,232 @@ DPA_API int dpa_up2_bwd(const bf16_t* g, int ldg, bf16_t* dx, int lddx, int N, i
   hipLaunchKernelGGL(up2_bwd_kernel, dim3(dpa_grid(tot, 256, 16384)), dim3(256), 0, st, g, ldg, dx, lddx, N, h, w, C);
   return (int)hipGetLastError();
 }
+
+// ------------------------------------------------------------------------------ fp32 forms
+// The fp32 engine (models/hip_unet_f32.py: the reference's precision, utils/train_utils.py:60-61) for the
+// BatchNorm and bilinear variants: the same statistics / finalize kernels above (the slab is fp32 either
+// way), fp32 NHWC activations read and written 4 channels (16 B) per lane.
+template <int MODE>
+__global__ __launch_bounds__(256) void bn_partial_f32_kernel(const float* __restrict__ a, int lda, const float* __restrict__ z,
+                                                             int ldz, const float* __restrict__ saved, long P, int C, int G,
+                                                             float* __restrict__ slab) {
+  __shared__ float red[256 * 8];
+  const int tid = threadIdx.x;
+  const int R = 256 / G;
+  const int g = tid % G, r = tid / G;
+  const int c0 = (blockIdx.y * G + g) * 4;
+  float s[4], q[4], mu[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    s[k] = 0.f;
+    q[k] = 0.f;
+    mu[k] = MODE ? saved[c0 + k] : 0.f;
+  }
+  for (long p = (long)blockIdx.x * R + r; p < P; p += (long)gridDim.x * R) {
+    const float4 u = *reinterpret_cast<const float4*>(a + p * lda + c0);
+    const float v[4] = {u.x, u.y, u.z, u.w};
+    if (MODE == 0) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        s[k] += v[k];
+        q[k] = fmaf(v[k], v[k], q[k]);
+      }
+    } else {
+      const float4 w = *reinterpret_cast<const float4*>(z + p * ldz + c0);
+      const float zz[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        s[k] += v[k];
+        q[k] = fmaf(v[k], zz[k] - mu[k], q[k]);
+      }
+    }
+  }
+  float* row = red + r * (G * 8) + g * 8;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    row[k] = s[k];
+    row[4 + k] = q[k];
+  }
+  __syncthreads();
+  for (int j = tid; j < G * 8; j += 256) {
+    float acc = 0.f;
+    for (int rr = 0; rr < R; ++rr) acc += red[rr * G * 8 + j];
+    const int gg = j >> 3, k = j & 7;
+    const int c = (blockIdx.y * G + gg) * 4 + (k & 3);
+    slab[(long)blockIdx.x * 2 * C + (k >> 2) * C + c] = acc;
+  }
+}
+
+// y = relu?(z*coef[c] + coef[C+c])
+__global__ __launch_bounds__(256) void bn_apply_f32_kernel(const float* __restrict__ z, int ldz, float* __restrict__ y, int ldy,
+                                                           const float* __restrict__ coef, long P, int C, int relu) {
+  const int CC = C >> 2;
+  const long tot = P * CC;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < tot; i += (long)gridDim.x * blockDim.x) {
+    const int c0 = (int)(i % CC) * 4;
+    const long p = i / CC;
+    const float4 u = *reinterpret_cast<const float4*>(z + p * ldz + c0);
+    float v[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      v[k] = fmaf(v[k], coef[c0 + k], coef[C + c0 + k]);
+      if (relu) v[k] = fmaxf(v[k], 0.f);
+    }
+    *reinterpret_cast<float4*>(y + p * ldy + c0) = make_float4(v[0], v[1], v[2], v[3]);
+  }
+}
+
+// dz = coef3[c]*g + coef3[C+c]*z + coef3[2C+c]
+__global__ __launch_bounds__(256) void bn_bwd_apply_f32_kernel(const float* __restrict__ g, int ldg, const float* __restrict__ z,
+                                                               int ldz, const float* __restrict__ coef3, float* __restrict__ dz,
+                                                               int lddz, long P, int C) {
+  const int CC = C >> 2;
+  const long tot = P * CC;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < tot; i += (long)gridDim.x * blockDim.x) {
+    const int c0 = (int)(i % CC) * 4;
+    const long p = i / CC;
+    const float4 ug = *reinterpret_cast<const float4*>(g + p * ldg + c0);
+    const float4 uz = *reinterpret_cast<const float4*>(z + p * ldz + c0);
+    const float gv[4] = {ug.x, ug.y, ug.z, ug.w}, zv[4] = {uz.x, uz.y, uz.z, uz.w};
+    float o[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      o[k] = fmaf(coef3[c0 + k], gv[k], fmaf(coef3[C + c0 + k], zv[k], coef3[2 * C + c0 + k]));
+    *reinterpret_cast<float4*>(dz + p * lddz + c0) = make_float4(o[0], o[1], o[2], o[3]);
+  }
+}
+
+static bool bn_shape_f32(long P, int C, int& G, dim3& grid) {
+  if (C <= 0 || (C & 3) || P <= 0) return false;
+  const int CG = C / 4;
+  G = 1;
+  while (G * 2 <= 32 && CG % (G * 2) == 0) G *= 2;
+  const int R = 256 / G;
+  long nbx = (P + R - 1) / R;
+  if (nbx > 512) nbx = 512;
+  grid = dim3((unsigned)nbx, (unsigned)(CG / G));
+  return true;
+}
+
+DPA_API int dpa_bn_slab_rows_f32(long long P, int C) {
+  int G;
+  dim3 grid;
+  return bn_shape_f32(P, C, G, grid) ? (int)grid.x : 0;
+}
+
+// BN(+ReLU) forward, fp32: train -> batch statistics (saved = mean, invstd; running stats updated), eval ->
+// running statistics; then y = relu?(bn(z))
+DPA_API int dpa_bn_fwd_f32(const float* z, int ldz, float* y, int ldy, long long P, int C, const float* gamma,
+                           const float* beta, float eps, float momentum, float* rmean, float* rvar, float* slab, float* coef,
+                           float* saved, int train, int relu, hipStream_t st) {
+  int G;
+  dim3 grid;
+  if (!bn_shape_f32(P, C, G, grid) || (ldz & 3) || (ldy & 3)) return (int)hipErrorInvalidValue;
+  if (train) {
+    hipLaunchKernelGGL(bn_partial_f32_kernel<0>, grid, dim3(256), 0, st, z, ldz, (const float*)nullptr, 0,
+                       (const float*)nullptr, (long)P, C, G, slab);
+    hipLaunchKernelGGL(bn_finalize_kernel, dim3(C), dim3(256), 0, st, slab, (int)grid.x, C, (long)P, gamma, beta, eps,
+                       momentum, rmean, rvar, coef, saved);
+  } else {
+    hipLaunchKernelGGL(bn_finalize_kernel, dim3(C), dim3(256), 0, st, (const float*)nullptr, 0, C, (long)P, gamma, beta, eps,
+                       momentum, rmean, rvar, coef, saved);
+  }
+  const long tot = (long)P * (C / 4);
+  hipLaunchKernelGGL(bn_apply_f32_kernel, dim3(dpa_grid(tot, 256, 16384)), dim3(256), 0, st, z, ldz, y, ldy, coef, (long)P, C,
+                     relu);
+  return (int)hipGetLastError();
+}
+
+// BN backward, fp32: g = dL/d(bn output) with the ReLU mask applied -> dz; dgamma / dbeta accumulated
+DPA_API int dpa_bn_bwd_f32(const float* g, int ldg, const float* z, int ldz, float* dz, int lddz, long long P, int C,
+                           const float* gamma, const float* saved, float* slab, float* coef3, float* dgamma, float* dbeta,
+                           hipStream_t st) {
+  int G;
+  dim3 grid;
+  if (!bn_shape_f32(P, C, G, grid) || (ldg & 3) || (ldz & 3) || (lddz & 3)) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(bn_partial_f32_kernel<1>, grid, dim3(256), 0, st, g, ldg, z, ldz, saved, (long)P, C, G, slab);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(256), 0, st, slab, (int)grid.x, C, (long)P, gamma, saved, coef3,
+                     dgamma, dbeta, (const float*)nullptr, 0);
+  const long tot = (long)P * (C / 4);
+  hipLaunchKernelGGL(bn_bwd_apply_f32_kernel, dim3(dpa_grid(tot, 256, 16384)), dim3(256), 0, st, g, ldg, z, ldz, coef3, dz,
+                     lddz, (long)P, C);
+  return (int)hipGetLastError();
+}
+
+// bilinear x2 (align_corners=False), fp32 NHWC, 4 channels per lane
+__global__ __launch_bounds__(256) void up2_fwd_f32_kernel(const float* __restrict__ x, int ldx, float* __restrict__ y, int ldy,
+                                                          int N, int h, int w, int C) {
+  const int CC = C >> 2, Ho = 2 * h, Wo = 2 * w;
+  const long tot = (long)N * Ho * Wo * CC;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < tot; i += (long)gridDim.x * blockDim.x) {
+    const int cc = (int)(i % CC);
+    const long op = i / CC;
+    const int ow = (int)(op % Wo);
+    const long t = op / Wo;
+    const int oh = (int)(t % Ho);
+    const int n = (int)(t / Ho);
+    int h0, h1, w0, w1;
+    float lh, lw;
+    up_src(oh, h, h0, h1, lh);
+    up_src(ow, w, w0, w1, lw);
+    const long base = (long)n * h * w;
+    const float* xc = x + cc * 4;
+    const float4 a = *reinterpret_cast<const float4*>(xc + (base + (long)h0 * w + w0) * ldx);
+    const float4 b = *reinterpret_cast<const float4*>(xc + (base + (long)h0 * w + w1) * ldx);
+    const float4 c = *reinterpret_cast<const float4*>(xc + (base + (long)h1 * w + w0) * ldx);
+    const float4 d = *reinterpret_cast<const float4*>(xc + (base + (long)h1 * w + w1) * ldx);
+    const float h0l = 1.f - lh, w0l = 1.f - lw;
+    float4 o;
+    o.x = h0l * (w0l * a.x + lw * b.x) + lh * (w0l * c.x + lw * d.x);
+    o.y = h0l * (w0l * a.y + lw * b.y) + lh * (w0l * c.y + lw * d.y);
+    o.z = h0l * (w0l * a.z + lw * b.z) + lh * (w0l * c.z + lw * d.z);
+    o.w = h0l * (w0l * a.w + lw * b.w) + lh * (w0l * c.w + lw * d.w);
+    *reinterpret_cast<float4*>(y + op * ldy + cc * 4) = o;
+  }
+}
+
+__global__ __launch_bounds__(256) void up2_bwd_f32_kernel(const float* __restrict__ g, int ldg, float* __restrict__ dx, int lddx,
+                                                          int N, int h, int w, int C) {
+  const int CC = C >> 2, Ho = 2 * h, Wo = 2 * w;
+  const long tot = (long)N * h * w * CC;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < tot; i += (long)gridDim.x * blockDim.x) {
+    const int cc = (int)(i % CC);
+    const long ip = i / CC;
+    const int iw = (int)(ip % w);
+    const long t = ip / w;
+    const int ih = (int)(t % h);
+    const int n = (int)(t / h);
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    const int oh0 = max(2 * ih - 2, 0), oh1 = min(2 * ih + 2, Ho - 1);
+    const int ow0 = max(2 * iw - 2, 0), ow1 = min(2 * iw + 2, Wo - 1);
+    for (int oh = oh0; oh <= oh1; ++oh) {
+      const float wh = up_weight(oh, h, ih);
+      if (wh == 0.f) continue;
+      for (int ow = ow0; ow <= ow1; ++ow) {
+        const float ww = up_weight(ow, w, iw);
+        if (ww == 0.f) continue;
+        const float wt = wh * ww;
+        const float4 u = *reinterpret_cast<const float4*>(g + (((long)n * Ho + oh) * Wo + ow) * ldg + cc * 4);
+        acc[0] = fmaf(wt, u.x, acc[0]);
+        acc[1] = fmaf(wt, u.y, acc[1]);
+        acc[2] = fmaf(wt, u.z, acc[2]);
+        acc[3] = fmaf(wt, u.w, acc[3]);
+      }
+    }
+    *reinterpret_cast<float4*>(dx + ip * lddx + cc * 4) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+  }
+}
+
+DPA_API int dpa_up2_fwd_f32(const float* x, int ldx, float* y, int ldy, int N, int h, int w, int C, hipStream_t st) {
+  if ((C & 3) || (ldx & 3) || (ldy & 3) || h < 1 || w < 1) return (int)hipErrorInvalidValue;
+  const long tot = (long)N * 4 * h * w * (C / 4);
+  hipLaunchKernelGGL(up2_fwd_f32_kernel, dim3(dpa_grid(tot, 256, 16384)), dim3(256), 0, st, x, ldx, y, ldy, N, h, w, C);
+  return (int)hipGetLastError();
+}
+
+DPA_API int dpa_up2_bwd_f32(const float* g, int ldg, float* dx, int lddx, int N, int h, int w, int C, hipStream_t st) {
+  if ((C & 3) || (ldg & 3) || (lddx & 3) || h < 1 || w < 1) return (int)hipErrorInvalidValue;
+  const long tot = (long)N * h * w * (C / 4);
+  hipLaunchKernelGGL(up2_bwd_f32_kernel, dim3(dpa_grid(tot, 256, 16384)), dim3(256), 0, st, g, ldg, dx, lddx, N, h, w, C);
+  return (int)hipGetLastError();
+}

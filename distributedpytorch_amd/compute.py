@@ -63,13 +63,12 @@ def resolve_backend(backend: str, device, dtype: str = "bf16", model=None) -> st
     """``auto`` -> the HIP engines on a GPU, stock ops on CPU.  bf16: :class:`.models.hip_unet.HipBlocks`
     (bf16 storage, fp32 accumulate); fp32 -- the reference's precision, utils/train_utils.py:60-61 --:
     :class:`.models.hip_unet_f32.HipF32Blocks` (fp32 storage, fp32 MFMA) for the configurations it
-    supports (``model`` given: checked; no BatchNorm / bilinear, widths % 32), else the torch backend
-    (fp32 on the GPU) for ``auto`` and an error for an explicit ``hip``.
+    supports (``model`` given: checked; the reference family incl. the BN / bilinear variants, widths % 32),
+    else the torch backend (fp32 on the GPU) for ``auto`` and an error for an explicit ``hip``.
 
-    The fp32 choice is deliberate even where stock MIOpen's steady state is close (b16, 512^2: 305 img/s
-    for this engine after round 5 vs 313 for MIOpen): MIOpen's first iteration spends minutes
-    compiling and searching solvers (449 s at b16; the b64 search did not finish in 600 s), while the HIP
-    engine has no warm-up, and it is the path the fp32 multi-rank (DDP) tests cover."""
+    Stock MIOpen fp32 against this engine, same box, interleaved runs: profiles/fp32_vs_stock_same_box_r06.jsonl
+    (BASELINE.md "Round 6"); MIOpen's first iteration also spends minutes compiling and searching solvers
+    (449 s at b16; the b64 search did not finish in 600 s), while the HIP engine has no warm-up."""
     device = torch.device(device)
     if backend == "auto":
         if device.type != "cuda":
@@ -84,8 +83,8 @@ def resolve_backend(backend: str, device, dtype: str = "bf16", model=None) -> st
     if backend == "hip" and dtype not in ("bf16", "fp32"):
         raise ValueError(f"--backend hip computes in bf16 or fp32, not {dtype}")
     if backend == "hip" and dtype == "fp32" and model is not None and not _f32_supported(model):
-        raise ValueError("--backend hip --dtype fp32: the fp32 engine covers the reference UNet family without "
-                         "BatchNorm / bilinear up-sampling and channel widths divisible by 32")
+        raise ValueError("--backend hip --dtype fp32: the fp32 engine covers the reference UNet family (with the "
+                         "BatchNorm / bilinear variants) at channel widths divisible by 32")
     return backend
 
 

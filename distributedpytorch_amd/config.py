@@ -100,7 +100,7 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--stages", type=int, default=2)
     p.add_argument("--microbatches", type=int, default=0,
                    help="MP microbatches (0: the pipeline plan's count; else 2 for the reference cut, 8 otherwise)")
-    p.add_argument("--mp-cut", choices=["auto", "reference", "balanced", "v", "time"], default="auto",
+    p.add_argument("--mp-cut", choices=["auto", "reference", "balanced", "v", "time", "spatial"], default="auto",
                    help="MP stage placement: reference = encoder+mid | decoder+head (2 stages; all skips cross "
                         "the cut); balanced = FLOP-balanced contiguous blocks; v = mirrored, skip-local (stage s "
                         "owns encoder level s and decoder level s); time = the measured-time plan in "
@@ -182,6 +182,9 @@ def mp_plan(cfg: "TrainConfig", stages: int) -> MPPlan:
     * ``time``: the placement, microbatch count and op order tools/pipeline_plan.py chose from MEASURED
       per-block times with the link-queueing schedule model (parallel/plans.json, keyed by model,
       image, stages and global batch);
+    * ``spatial``: the top level(s) split by image ROWS over all stages and the inner chain pipelined
+      (parallel/spatial.py; plans.json's row-split plan when it has one, else a FLOP-balanced one): for deep
+      pipelines at high resolution, where whole full-resolution tensors cost more link time than compute;
     * ``auto`` (default): ``time`` when plans.json has the configuration, else ``v``.
 
     Microbatches: ``--microbatches`` when given, else the plan's, else 2 for the reference cut (the
@@ -195,11 +198,13 @@ def mp_plan(cfg: "TrainConfig", stages: int) -> MPPlan:
     h, w = cfg.img_size
     mode = cfg.mp_cut
     plan = None
-    if mode in ("auto", "time"):
+    if mode in ("auto", "time", "spatial"):
         plan = load_plan(cfg.model, h, w, stages, cfg.batch_size, depth=mcfg.depth)
+        if mode == "spatial" and plan is not None and not plan.get("spatial"):
+            plan = None
         if plan is not None:
             mode = "time"
-        else:
+        elif mode != "spatial":
             mode = "v" if stages > 1 else "balanced"
     if stages == 1:
         pl = Placement.contiguous([0, n_blocks(mcfg.depth)])
@@ -211,9 +216,14 @@ def mp_plan(cfg: "TrainConfig", stages: int) -> MPPlan:
         pl = Placement.contiguous(partition(mcfg, stages, h, w, mode="balanced"))
     elif mode == "v":
         pl = v_partition(mcfg, stages, h, w)
+    elif mode == "spatial":
+        from .parallel.spatial import default_plan
+        pl = default_plan(mcfg, stages, h, w)
     else:
         raise ValueError(f"unknown --mp-cut {mode!r}")
     M = cfg.microbatches or (plan["microbatches"] if plan else (2 if mode == "reference" else 8))
+    if plan is not None and plan.get("spatial"):
+        mode = "spatial"
     if not cfg.microbatches and cfg.batch_size % M:
         M = math.gcd(M, cfg.batch_size)
     orders = plan.get("orders") if plan is not None and M == plan["microbatches"] else None

@@ -9,7 +9,10 @@ and weight in fp32 and runs every conv-shaped product on fp32 MFMA (v_mfma_f32_1
 * ConvTranspose2d(k2, s2) forward (GEMM + 2x2 scatter), dgrad (stride-2 gather GEMM) and weight /
   bias gradient;
 * 2x2 max-pool with window codes and its backward, the segmentation head (1x1 conv + sigmoid +
-  BCE / Dice partial sums, ``utils/utils.py:9-25``) and its backward, the NCHW -> NHWC input pass.
+  BCE / Dice partial sums, ``utils/utils.py:9-25``) and its backward, the NCHW -> NHWC input pass;
+* the north-star variants (``model/modelsummary.txt:153-247``): Conv2d+BatchNorm+ReLU DoubleConvs (fp32 batch
+  statistics, apply and backward kernels, csrc/norm_up.hip) and the bilinear Up path (x2 up-sampling
+  kernels; its 1x1 projection is a plain GEMM at the low resolution).
 
 Granularity is one autograd Function per block (a DoubleConv's two convs are one Function: the inner ReLU
 backward is the mask epilogue of the second conv's dgrad).  As in the bf16 engine, parameters are not
@@ -17,7 +20,7 @@ autograd inputs: every layer's GEMM weight layouts are packed by one batched ker
 (``ensure_packed``), and the weight / bias gradients are reduced straight into the flat fp32 gradient
 buffer, each block announcing its finished parameters (``ready``: DDP buckets overlap the backward).  Activations are NHWC
 tensors handed between blocks as logical-NCHW channels_last views, as in the bf16 engine.  Supported:
-the reference UNet family without BatchNorm and with transposed-conv up-sampling, channel widths
+the reference UNet family with or without BatchNorm, transposed-conv or bilinear up-sampling, channel widths
 divisible by 32 (other configurations take the stock torch path, ``compute.resolve_backend``).
 """
 from __future__ import annotations
@@ -32,13 +35,13 @@ from .unet import Up
 
 
 def supported(model) -> bool:
-    cfg = model.cfg
-    if getattr(cfg, "batchnorm", False) or any(isinstance(m, Up) for m in model.decoder.ups()):
-        return False
+    """The reference UNet family, with or without BatchNorm (Conv2d+BN+ReLU DoubleConv) and with transposed-
+    conv or bilinear up-sampling, channel widths divisible by 32."""
     convs = [c for b in model.encoder.blocks() for c in b.convs()] + list(model.mid.convs()) + \
             [c for b in model.decoder.blocks() for c in b.convs()]
+    ups_ok = all(isinstance(m, Up) or m.out_channels % 32 == 0 for m in model.decoder.ups())
     return all(c.out_channels % 32 == 0 for c in convs) and model.encoder.blocks()[0].convs()[0].in_channels <= 4 \
-        and model.segmap.out_channels == 1 and model.segmap.in_channels in (8, 16, 32, 64)
+        and model.segmap.out_channels == 1 and model.segmap.in_channels in (8, 16, 32, 64) and ups_ok
 
 
 def _v(t: torch.Tensor) -> torch.Tensor:
@@ -70,14 +73,17 @@ class _L:
     """Packing bookkeeping of one conv3x3 / transposed-conv layer: offsets of its forward and dgrad GEMM
     weights in the engine's packed fp32 buffer."""
 
-    def __init__(self, mod, kind: str, cs: int = 0):
-        self.mod, self.kind = mod, kind
+    def __init__(self, mod, kind: str, cs: int = 0, bn=None):
+        self.mod, self.kind, self.bn = mod, kind, bn
         if kind == "conv":
             self.Cout, self.Cin = mod.out_channels, mod.in_channels
             self.Cs = cs or self.Cin
             self.Kf = F32.round_up(9 * self.Cs, 16)
             self.Nd = F32.round_up(self.Cin, 32)          # dgrad GEMM-N (zero rows for padding channels)
             self.Kd = F32.round_up(9 * self.Cout, 16)
+        elif kind == "up":                                # bilinear Up: 1x1 projection (models/unet.py Up)
+            self.Cin, self.Cout = mod.proj.in_channels, mod.proj.out_channels
+            self.Cs, self.Kf, self.Nd, self.Kd = self.Cin, self.Cin, self.Cin, self.Cout
         else:                                             # ConvTranspose2d(k2, s2): weight [Cin, Cout, 2, 2]
             self.Cin, self.Cout = mod.in_channels, mod.out_channels
             self.Cs = self.Cin
@@ -85,15 +91,29 @@ class _L:
         self.off_f = self.off_d = -1
 
 
-def _conv_fwd(B, c: _L, x, y=None):
+def _conv_fwd(B, c: _L, x, y=None, relu: bool = True):
     """relu(conv3x3(x) + b), NHWC fp32; x has ``c.Cs`` channels (>= Cin: zero weights for the padding
-    channels of the network input); ``y``: the output (a channel slice allowed), else a new tensor."""
+    channels of the network input); ``y``: the output (a channel slice allowed), else a new tensor.
+    ``relu=False``: the pre-BatchNorm output z."""
     N, H, W = x.shape[:3]
     if y is None:
         y = torch.empty(N, H, W, c.Cout, dtype=torch.float32, device=x.device)
     F32.igemm(x, B.wf(c), y, Ngemm=c.Cout, Kpad=c.Kf, KH=3, KW=3, stride=1, pad=1, Cs=c.Cs, out_grid=(N, H, W),
-              bias=c.mod.bias.detach(), relu=True)
+              bias=c.mod.bias.detach(), relu=relu)
     return y
+
+
+def _conv_bn_fwd(B, c: _L, x, y=None):
+    """relu(bn(conv3x3(x) + b)): returns (y, z, saved) -- z the conv output, saved the BN batch statistics
+    (None in eval mode: running statistics)."""
+    z = _conv_fwd(B, c, x, relu=False)
+    y, saved = F32.bn_fwd(z, c.bn, B.model.training, relu=True, y=y)
+    return y, z, saved
+
+
+def _bn_bwd(c: _L, g, z, saved):
+    """dL/dz from g = dL/d(relu(bn(z))) with the ReLU mask already applied."""
+    return F32.bn_bwd(_dense(g), z, saved, c.bn, _grad(c.bn.weight), _grad(c.bn.bias))
 
 
 def _conv_dgrad(B, c: _L, ge, mask=None):
@@ -200,6 +220,114 @@ class _EncBlock(torch.autograd.Function):
         B.join()
         B.ready([c2.mod, c1.mod])
         return None, gx, None, None, None, None
+
+
+class _DoubleConvBN(torch.autograd.Function):
+    """relu(bn2(conv2(relu(bn1(conv1(x)))))) -- the north-star DoubleConv = Conv2d+BN+ReLU twice
+    (model/modelsummary.txt:153-247), training (batch statistics) or eval (running statistics).  Backward: the
+    outer ReLU mask, BN2's backward, conv2's dgrad with the inner ReLU as its mask epilogue, BN1's backward,
+    conv1's dgrad; weight gradients on the side stream."""
+
+    @staticmethod
+    def forward(ctx, anchor, x, B, c1, c2):
+        y1, z1, s1 = _conv_bn_fwd(B, c1, x)
+        y2, z2, s2 = _conv_bn_fwd(B, c2, y1)
+        ctx.B, ctx.c = B, (c1, c2)
+        ctx.st = (s1, s2)
+        ctx.save_for_backward(x, z1, y1, z2, y2)
+        return y2
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, z1, y1, z2, y2 = ctx.saved_tensors
+        B, (c1, c2) = ctx.B, ctx.c
+        s1, s2 = ctx.st
+        dz2 = _bn_bwd(c2, F32.relu_bwd(_dense(gy), y2), z2, s2)
+        _conv_wgrad(B, c2, dz2, y1)
+        g1 = _conv_dgrad(B, c2, dz2, mask=y1)
+        dz1 = _bn_bwd(c1, g1, z1, s1)
+        _conv_wgrad(B, c1, dz1, x)
+        gx = _conv_dgrad(B, c1, dz1) if ctx.needs_input_grad[1] else None
+        B.join()
+        B.ready([c2.mod, c2.bn, c1.mod, c1.bn])
+        ctx.st = None
+        return None, gx, None, None, None
+
+
+class _ConvBN(torch.autograd.Function):
+    """relu(bn(conv3x3(x))) -- one half of a BN DoubleConv cut by a pipeline stage boundary."""
+
+    @staticmethod
+    def forward(ctx, anchor, x, B, c):
+        y, z, s = _conv_bn_fwd(B, c, x)
+        ctx.B, ctx.c, ctx.st = B, c, s
+        ctx.save_for_backward(x, z, y)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, z, y = ctx.saved_tensors
+        B, c = ctx.B, ctx.c
+        dz = _bn_bwd(c, F32.relu_bwd(_dense(gy), y), z, ctx.st)
+        _conv_wgrad(B, c, dz, x)
+        gx = _conv_dgrad(B, c, dz) if ctx.needs_input_grad[1] else None
+        B.join()
+        B.ready([c.mod, c.bn])
+        ctx.st = None
+        return None, gx, None, None
+
+
+class _EncBlockBN(torch.autograd.Function):
+    """Encoder block of the BN model: DoubleConv(+BN) + 2x2 max-pool -> (skip, pooled); the skip written into
+    the decoder's concat buffer as in :class:`_EncBlock`; backward forms the last ReLU's masked gradient from
+    the skip gradient and the pool backward in one pass (F32.enc_out_bwd), then the two BN + conv backwards."""
+
+    @staticmethod
+    def forward(ctx, anchor, x, B, c1, c2, dense: bool):
+        N, H, W = x.shape[:3]
+        y1, z1, s1 = _conv_bn_fwd(B, c1, x)
+        if dense:
+            own = y = torch.empty(N, H, W, c2.Cout, dtype=torch.float32, device=x.device)
+        else:
+            own = B.new_cat(N, H, W, c2.Cout)
+            y = own[..., :c2.Cout]
+        _, z2, s2 = _conv_bn_fwd(B, c2, y1, y=y)
+        pooled, code = F32.maxpool2(y)
+        ctx.B, ctx.c, ctx.C, ctx.st = B, (c1, c2), c2.Cout, (s1, s2)
+        ctx.save_for_backward(x, z1, y1, z2, own, code)
+        return y, pooled
+
+    @staticmethod
+    def backward(ctx, gs, gp):
+        x, z1, y1, z2, own, code = ctx.saved_tensors
+        B, (c1, c2) = ctx.B, ctx.c
+        s1, s2 = ctx.st
+        y = own[..., :ctx.C]
+        if gs is not None and not F32.nhwc_ok(gs):
+            gs = gs.contiguous()
+        g2 = F32.enc_out_bwd(gs, None if gp is None else _dense(gp), code, y)
+        dz2 = _bn_bwd(c2, g2, z2, s2)
+        _conv_wgrad(B, c2, dz2, y1)
+        g1 = _conv_dgrad(B, c2, dz2, mask=y1)
+        dz1 = _bn_bwd(c1, g1, z1, s1)
+        _conv_wgrad(B, c1, dz1, x)
+        gx = _conv_dgrad(B, c1, dz1) if ctx.needs_input_grad[1] else None
+        B.join()
+        B.ready([c2.mod, c2.bn, c1.mod, c1.bn])
+        ctx.st = None
+        return None, gx, None, None, None, None
+
+
+class _Up2(torch.autograd.Function):
+    """Bilinear x2 up-sampling, align_corners=False (the variant ``Up``: models/unet.py), NHWC fp32."""
+
+    @staticmethod
+    def forward(ctx, x):
+        return F32.up2_fwd(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        return F32.up2_bwd(_dense(g))
 
 
 def _deconv_bwd(B, d: _L, x, gy, need_dx: bool):
@@ -378,6 +506,8 @@ class F32Engine:
         for c in layers:
             if c.mod.weight.device != self.device or (self._owned is not None and id(c.mod.weight) not in self._owned):
                 continue
+            if c.kind == "up":                # bilinear Up: its 1x1 projection is a plain GEMM (torch.mm)
+                continue
             if c.kind == "conv":
                 c.off_f = add(0, c.mod.weight, c.Cout, c.Cin, c.Cs, c.Cout, c.Kf)
                 c.off_d = add(1, c.mod.weight, c.Cout, c.Cin, c.Cout, c.Nd, c.Kd)
@@ -412,6 +542,8 @@ class F32Engine:
         """Announce finished parameter gradients (DDP buckets start while the backward runs)."""
         by_space = {}
         for m in mods:
+            if m is None:
+                continue
             for p in (m.weight, m.bias):
                 sp = getattr(p, "_dpa_space", None)
                 if sp is not None:
@@ -430,14 +562,18 @@ class HipF32Blocks(F32Engine):
         self.model = model
         device = torch.device(device) if device is not None else next(model.parameters()).device
         assert device.type == "cuda", "HipF32Blocks needs a GPU"
-        assert supported(model), "fp32 HIP engine: reference UNet family without BatchNorm / bilinear, widths % 32 == 0"
+        assert supported(model), "fp32 HIP engine: reference UNet family (BN / bilinear variants too), widths % 32 == 0"
         if not any(hasattr(p, "_dpa_space") for p in model.parameters()):
             FlatParameterSpace(model, device=device)     # standalone use: flatten here
-        self.encc = [[_L(c, "conv", 4 if (l == 0 and j == 0) else 0) for j, c in enumerate(b.convs())]
-                     for l, b in enumerate(model.encoder.blocks())]
-        self.midc = [_L(c, "conv") for c in model.mid.convs()]
-        self.decc = [[_L(c, "conv") for c in b.convs()] for b in model.decoder.blocks()]
-        self.ups = [_L(m, "deconv") for m in model.decoder.ups()]
+
+        def convs(b, first=False):
+            bns = b.bns() if getattr(b, "batchnorm", False) else [None, None]
+            return [_L(c, "conv", 4 if (first and j == 0) else 0, bn=bn) for j, (c, bn) in enumerate(zip(b.convs(), bns))]
+
+        self.encc = [convs(b, l == 0) for l, b in enumerate(model.encoder.blocks())]
+        self.midc = convs(model.mid)
+        self.decc = [convs(b) for b in model.decoder.blocks()]
+        self.ups = [_L(m, "up" if isinstance(m, Up) else "deconv") for m in model.decoder.ups()]
         layers = [c for cs in self.encc for c in cs] + self.midc + [c for cs in self.decc for c in cs] + self.ups
         super().__init__(layers, device, owned)
 
@@ -451,16 +587,21 @@ class HipF32Blocks(F32Engine):
 
     def _conv(self, c, x):
         self.ensure_packed()
+        if c.bn is not None:
+            return _ConvBN.apply(self.anchor, x, self, c)
         return _ConvReLU.apply(self.anchor, x, self, c)
 
     def _double(self, c1, c2, x):
         self.ensure_packed()
+        if c1.bn is not None:
+            return _DoubleConvBN.apply(self.anchor, x, self, c1, c2)
         return _DoubleConvReLU.apply(self.anchor, x, self, c1, c2)
 
     def enc(self, l: int, x):
         self.ensure_packed()
         c1, c2 = self.encc[l]
-        s, p = _EncBlock.apply(self.anchor, _v(x), self, c1, c2, l in self.dense_skips)
+        fn = _EncBlockBN if c1.bn is not None else _EncBlock
+        s, p = fn.apply(self.anchor, _v(x), self, c1, c2, l in self.dense_skips)
         return _o(s), _o(p)
 
     def mid(self, x):
@@ -489,9 +630,17 @@ class HipF32Blocks(F32Engine):
         self.ensure_packed()
         d = self.ups[i]
         xv, sk = _v(x), _v(skip)
-        if tuple(sk.shape[1:3]) == (2 * xv.shape[1], 2 * xv.shape[2]) and sk.shape[3] % 4 == 0:
+        if d.kind == "up":
+            # bilinear Up: proj(up2(x)) == up2(proj(x)) (the interpolation weights sum to 1 and act per channel):
+            # the 1x1 projection runs at the low resolution as a plain GEMM, then the up-sampling kernel
+            N, h, w, ci = xv.shape
+            wt = d.mod.proj.weight.view(d.mod.proj.out_channels, ci)
+            low = torch.addmm(d.mod.proj.bias, _dense(xv).reshape(-1, ci), wt.t()).view(N, h, w, -1)
+            up = _Up2.apply(low)
+        elif tuple(sk.shape[1:3]) == (2 * xv.shape[1], 2 * xv.shape[2]) and sk.shape[3] % 4 == 0:
             return _UpCat.apply(self.anchor, xv, sk, self, d)
-        up = _Deconv.apply(self.anchor, xv, self, d)
+        else:
+            up = _Deconv.apply(self.anchor, xv, self, d)
         h2, w2 = up.shape[1:3]
         if tuple(sk.shape[1:3]) != (h2, w2):
             top, left = int(round((sk.shape[1] - h2) / 2.0)), int(round((sk.shape[2] - w2) / 2.0))

@@ -336,3 +336,80 @@ def channel_sum(g: torch.Tensor, out: torch.Tensor) -> None:
     _check(L.dpa_channel_sum_f32(_p(g), c_ll(P), c_int(C), c_int(ld), _p(slab), st), "channel_sum_f32")
     _check(L.dpa_wgrad_reduce_cfg(None, _p(slab), None, _p(out), c_int(blocks), c_int(0), c_int(C), c_int(1), c_int(1),
                                   c_int(0), c_int(0), st), "channel_sum_f32(reduce)")
+
+
+# ---------------------------------------------------------------------------------------- BN / bilinear
+def _declare_norm():
+    L = _lib.lib()
+    for name in ("dpa_bn_fwd_f32", "dpa_bn_bwd_f32", "dpa_up2_fwd_f32", "dpa_up2_bwd_f32"):
+        getattr(L, name).restype = ctypes.c_int
+    L.dpa_bn_slab_rows_f32.restype = ctypes.c_int
+    L.dpa_bn_slab_rows_f32.argtypes = [ctypes.c_longlong, ctypes.c_int]
+    return L
+
+
+def bn_fwd(z: torch.Tensor, bn: torch.nn.BatchNorm2d, train: bool, relu: bool = True,
+           y: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+    """y = relu(BatchNorm2d(z)), NHWC fp32 (csrc/norm_up.hip fp32 forms; torch.nn.BatchNorm2d semantics:
+    biased batch variance to normalise, unbiased for running_var, ``momentum`` update).  Returns (y, saved):
+    saved = [mean, invstd] for :func:`bn_bwd` in training, None in eval (running statistics)."""
+    L = _declare_norm()
+    N, H, W, C, ldz = nhwc(z, "bn_fwd_f32.z")
+    if y is None:
+        y = torch.empty(N, H, W, C, dtype=torch.float32, device=z.device)
+    _, _, _, _, ldy = nhwc(y, "bn_fwd_f32.y")
+    P = N * H * W
+    rows = L.dpa_bn_slab_rows_f32(P, C)
+    slab = torch.empty(max(rows, 1) * 2 * C, dtype=torch.float32, device=z.device)
+    coef = torch.empty(2 * C, dtype=torch.float32, device=z.device)
+    saved = torch.empty(2 * C, dtype=torch.float32, device=z.device) if train else None
+    track = train and bn.track_running_stats and bn.running_mean is not None
+    if train and bn.num_batches_tracked is not None:
+        bn.num_batches_tracked.add_(1)
+    mom = bn.momentum if bn.momentum is not None else 0.1
+    _check(L.dpa_bn_fwd_f32(_p(z), c_int(ldz), _p(y), c_int(ldy), c_ll(P), c_int(C), _p(bn.weight.detach()),
+                            _p(bn.bias.detach()), ctypes.c_float(bn.eps), ctypes.c_float(mom),
+                            _p(bn.running_mean) if (track or not train) else None,
+                            _p(bn.running_var) if (track or not train) else None, _p(slab), _p(coef), _p(saved),
+                            c_int(1 if train else 0), c_int(1 if relu else 0), _st(z)), "bn_fwd_f32")
+    return y, saved
+
+
+def bn_bwd(g: torch.Tensor, z: torch.Tensor, saved: torch.Tensor, bn: torch.nn.BatchNorm2d,
+           dgamma: Optional[torch.Tensor], dbeta: Optional[torch.Tensor]) -> torch.Tensor:
+    """dz from g = dL/d(BN output) with the ReLU mask applied; dgamma / dbeta += (the flat fp32 gradients)."""
+    L = _declare_norm()
+    N, H, W, C, ldg = nhwc(g, "bn_bwd_f32.g")
+    _, _, _, _, ldz = nhwc(z, "bn_bwd_f32.z")
+    P = N * H * W
+    rows = L.dpa_bn_slab_rows_f32(P, C)
+    slab = torch.empty(max(rows, 1) * 2 * C, dtype=torch.float32, device=g.device)
+    coef3 = torch.empty(3 * C, dtype=torch.float32, device=g.device)
+    dz = torch.empty(N, H, W, C, dtype=torch.float32, device=g.device)
+    _check(L.dpa_bn_bwd_f32(_p(g), c_int(ldg), _p(z), c_int(ldz), _p(dz), c_int(C), c_ll(P), c_int(C),
+                            _p(bn.weight.detach()), _p(saved), _p(slab), _p(coef3), _p(dgamma), _p(dbeta), _st(g)),
+           "bn_bwd_f32")
+    return dz
+
+
+def up2_fwd(x: torch.Tensor, y: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Bilinear x2 up-sampling (align_corners=False) of NHWC fp32 x (into ``y``: a concat half allowed)."""
+    L = _declare_norm()
+    N, h, w, C, ldx = nhwc(x, "up2_f32.x")
+    if y is None:
+        y = torch.empty(N, 2 * h, 2 * w, C, dtype=torch.float32, device=x.device)
+    Ny, Hy, Wy, Cy, ldy = nhwc(y, "up2_f32.y")
+    assert (Ny, Hy, Wy, Cy) == (N, 2 * h, 2 * w, C)
+    _check(L.dpa_up2_fwd_f32(_p(x), c_int(ldx), _p(y), c_int(ldy), c_int(N), c_int(h), c_int(w), c_int(C), _st(x)),
+           "up2_fwd_f32")
+    return y
+
+
+def up2_bwd(g: torch.Tensor) -> torch.Tensor:
+    L = _declare_norm()
+    N, H, W, C, ldg = nhwc(g, "up2_bwd_f32.g")
+    assert H % 2 == 0 and W % 2 == 0
+    dx = torch.empty(N, H // 2, W // 2, C, dtype=torch.float32, device=g.device)
+    _check(L.dpa_up2_bwd_f32(_p(g), c_int(ldg), _p(dx), c_int(C), c_int(N), c_int(H // 2), c_int(W // 2), c_int(C),
+                             _st(g)), "up2_bwd_f32")
+    return dx

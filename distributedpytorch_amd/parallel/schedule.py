@@ -573,7 +573,11 @@ def load_plan(model: str, h: int, w: int, stages: int, batch: int, path: str = N
         from ..models.unet import PRESETS
         depth = PRESETS[model].depth if model in PRESETS else None
     try:
-        pl = Placement.from_plan(p)
+        if p.get("spatial"):                     # row-split top levels (parallel/spatial.py)
+            from .spatial import SpatialPlan
+            pl = SpatialPlan.from_plan(p)
+        else:
+            pl = Placement.from_plan(p)
         if depth is not None:
             pl.validate(depth)
         M = int(p["microbatches"])

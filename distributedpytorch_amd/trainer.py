@@ -260,8 +260,15 @@ class PipelineLocalStrategy(Strategy):
         super().__init__(cfg)
         H, W = cfg.img_size
         self.plan = mp_plan(cfg, len(devices))
+        pl = self.plan.placement
+        if self.plan.mode == "spatial":
+            # row-split plans need one process per stage (parallel/spatial_pipe.py): the single-process form
+            # runs the FLOP-balanced skip-local V placement instead
+            from .parallel.placement import v_partition
+            log.warning("MP: the row-split plan needs torchrun (one process per stage); running the V placement")
+            pl = v_partition(model.cfg, len(devices), H, W)
         self.pipe = GPipeLocal(model, devices, self.plan.microbatches, cfg.backend, cfg.dtype, img_hw=(H, W),
-                               placement=self.plan.placement)
+                               placement=pl)
         self.model = model
         self.device = self.pipe.devices[0]
         self.optimizer = FusedAdam(self.pipe.spaces, lr=cfg.lr, weight_decay=cfg.weight_decay)
@@ -303,9 +310,17 @@ class PipelineDistStrategy(Strategy):
             dgs = [dist.new_group([s + k * S for k in range(R)]) for s in range(S)]
             pipe_group, self.dp_group = pgs[self.replica], dgs[self.stage]
         self.plan = mp_plan(cfg, S)
-        self.pipe = GPipeDist(self.model, self.plan.microbatches, cfg.backend, cfg.dtype, img_hw=(H, W),
-                              placement=self.plan.placement, policy=self.plan.policy, orders=self.plan.orders,
-                              group=pipe_group)
+        self.spatial = self.plan.mode == "spatial"
+        if self.spatial:
+            # top level(s) split by image rows over every stage (parallel/spatial_pipe.py): every rank reads
+            # its rows of the same batch
+            from .parallel.spatial_pipe import SpatialGPipe
+            self.pipe = SpatialGPipe(self.model, self.plan.placement, self.plan.microbatches, cfg.backend, cfg.dtype,
+                                     group=pipe_group, img_hw=(H, W))
+        else:
+            self.pipe = GPipeDist(self.model, self.plan.microbatches, cfg.backend, cfg.dtype, img_hw=(H, W),
+                                  placement=self.plan.placement, policy=self.plan.policy, orders=self.plan.orders,
+                                  group=pipe_group)
         # the head stage owns the loss (pipeline 0's logs); rank 0 saves
         self.is_main = self.pipe.is_last and self.replica == 0
         self.optimizer = FusedAdam(self.pipe.space, lr=cfg.lr, weight_decay=cfg.weight_decay)
@@ -326,15 +341,18 @@ class PipelineDistStrategy(Strategy):
                 blocks.early_ready = True
             else:
                 per_param = self.plan.microbatches
+            # (row-split pipelines all-reduce their split levels' gradients inside the step: the replicas'
+            # all-reduce follows it as one collective instead of racing it bucket by bucket)
             self.reducer = BucketedAllReduce(self.pipe.space, bucket_mb=cfg.bucket_mb, group=self.dp_group,
-                                             comm_dtype=cfg.grad_comm_dtype, overlap=cfg.comm_overlap,
+                                             comm_dtype=cfg.grad_comm_dtype,
+                                             overlap=cfg.comm_overlap and not self.spatial,
                                              per_param=per_param).register_hooks()
 
     def sync_stage_buffers(self):
         """Pipeline 0's stage buffers (BatchNorm running statistics) to every replica of the stage: torch
         DDP's ``broadcast_buffers`` across the pipelines, so validation and the checkpoint (pipeline 0's)
         describe one model."""
-        if self.replicas <= 1:
+        if self.replicas <= 1 or self.spatial:        # row-split plans exclude BatchNorm models
             return
         bufs = dict(self.model.named_buffers())
         for n in placement_buffer_names(self.model, self.pipe.pl, self.stage):
@@ -363,8 +381,8 @@ class PipelineDistStrategy(Strategy):
     @torch.no_grad()
     def eval_batch(self, images, targets):
         p = self.pipe.eval_probs(images, images.shape[0], self.cfg.img_size)
-        if p is None:
-            return None
+        if p is None or (self.spatial and not self.pipe.is_last):
+            return None             # (row-split: every stage holds the gathered probabilities; stage 0 counts)
         return loss_from_partials(_partials(p, targets), targets.numel()), dice_score(p, targets)
 
     def state_dict(self):

@@ -455,3 +455,109 @@ def test_pipeline_replicas_data_parallel(world, replicas, mode, model_name):
         assert same, f"rank {rank}: stage parameters differ across pipelines"
     assert sum(r[-2] for r in res) == replicas          # one head stage per pipeline
     assert sum(r[-1] for r in res) == 1                 # one main (logging) rank: pipeline 0's head
+
+
+def _spatial_worker(rank, world, port, plan_kw, M, q):
+    _init(rank, world, port)
+    from distributedpytorch_amd.parallel.spatial import SpatialPlan
+    from distributedpytorch_amd.parallel.spatial_pipe import SpatialGPipe
+    torch.manual_seed(0)
+    model = build_model("unet-tiny4")
+    ref = build_model("unet-tiny4")
+    ref.load_state_dict(model.state_dict())
+    plan = SpatialPlan(**plan_kw)
+    try:
+        pipe = SpatialGPipe(model, plan, M, backend="torch", dtype="fp32", img_hw=(64, 64))
+        x, t = _data(4, seed=11, hw=64)
+        loss = pipe.train_step(x, t, 4, (64, 64))
+    except Exception as e:
+        import traceback
+        q.put((rank, repr(e) + traceback.format_exc(), None, None, None, None))
+        raise
+    lref = bce_dice_from_probs(ref(x), t)
+    lref.backward()
+    refp = dict(ref.named_parameters())
+    bad = [n for n, p in model.named_parameters()
+           if p.requires_grad and not torch.allclose(p.grad, refp[n].grad, atol=2e-5, rtol=1e-4)]
+    nown = sum(1 for p in model.parameters() if p.requires_grad)
+    probs = pipe.eval_probs(x, 4, (64, 64))
+    with torch.no_grad():
+        probs_ok = bool(torch.allclose(probs, ref(x), atol=1e-5))
+    sd = pipe.gather_state_dict()
+    sd_ok = rank != 0 or (set(sd) == set(ref.state_dict())
+                          and all(torch.equal(sd[k], v) for k, v in ref.state_dict().items()))
+    q.put((rank, None, float(loss), float(lref), bad, (nown, probs_ok, sd_ok)))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,plan_kw,M", [
+    (2, dict(S=2, inner_cuts=(1, 3, 6, 8), inner_owner=(0, 1, 0), L=1), 2),              # inner V
+    (2, dict(S=2, inner_cuts=(1, 4, 8), inner_owner=(0, 1), L=1, bounds=(0, 24, 64)), 1),  # uneven rows
+    (4, dict(S=4, inner_cuts=(2, 3, 3.5, 4, 5, 5.5, 6, 7), inner_owner=(0, 1, 2, 3, 2, 1, 0), L=2), 2),
+    (8, dict(S=8, inner_cuts=(1, 1.5, 2, 3, 4, 5, 6, 7, 8), inner_owner=tuple(range(8)), L=1), 2),
+])
+def test_spatial_pipeline_matches_single_process(world, plan_kw, M):
+    """Row-split top levels (parallel/spatial.py, spatial_pipe.py): every stage runs the split levels on its
+    own image rows (halo rows recomputed, never exchanged), the inner chain is pipelined; loss, every
+    parameter gradient (split levels after their all-reduce), the probabilities and the gathered state dict
+    equal a single-process run of the full batch -- at 2, 4 and 8 stages, 1 and 2 split levels, inner V and
+    contiguous chains and uneven row slices."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_spatial_worker, args=(r, world, port, plan_kw, M, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=300) for _ in procs], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+    for rank, err, loss, lref, bad, extra in res:
+        assert err is None, f"rank {rank}: {err}"
+        assert abs(loss - lref) < 1e-5, (rank, loss, lref)
+        assert not bad, f"rank {rank}: grads differ for {bad}"
+        nown, probs_ok, sd_ok = extra
+        assert probs_ok and sd_ok, (rank, probs_ok, sd_ok)
+
+
+def _spatial_trainer_worker(rank, world, port, q):
+    _init(rank, world, port)
+    from distributedpytorch_amd.config import TrainConfig
+    from distributedpytorch_amd.trainer import PipelineDistStrategy
+    torch.manual_seed(0)
+    model = build_model("unet-tiny4")
+    ref = build_model("unet-tiny4")
+    ref.load_state_dict(model.state_dict())
+    cfg = TrainConfig(train_method="MP", backend="torch", dtype="fp32", lr=1e-3, mp_cut="spatial", microbatches=2,
+                      img_size=(64, 64), model="unet-tiny4", batch_size=4)
+    try:
+        st = PipelineDistStrategy(cfg, model, "cpu")
+        x, t = _data(4, seed=3, hw=64)
+        loss = st.train_step(x, t)
+        ev = st.eval_batch(x, t)
+        sd = st.state_dict()
+        res = (st.plan.mode, float(loss), ev is not None, sd is not None, st.is_main)
+    except Exception as e:
+        import traceback
+        res = (repr(e) + traceback.format_exc(),)
+    q.put((rank, res))
+    dist.destroy_process_group()
+
+
+def test_spatial_plan_through_mp_strategy():
+    """``-t MP --mp-cut spatial``: the FLOP-balanced row-split plan (parallel/spatial.py ``default_plan``)
+    drives PipelineDistStrategy: a training step, validation counted once (stage 0), rank 0's state dict."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_spatial_trainer_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=300) for _ in procs], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+    for rank, r in res:
+        assert len(r) == 5, r[0]
+        mode, loss, has_eval, has_sd, main = r
+        assert mode == "spatial" and loss == loss
+        assert has_eval == (rank == 0) and has_sd == (rank == 0) and main == (rank == 0)
+    assert res[0][1][1] == res[1][1][1]            # every stage holds the same full-batch loss

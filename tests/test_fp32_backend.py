@@ -1,7 +1,8 @@
 """``--dtype fp32`` (the reference's precision, utils/train_utils.py:60-61): on a GPU ``backend=auto``
-resolves to the fp32 HIP engine (models/hip_unet_f32.py, csrc/fp32.hip) for the reference UNet family
-and to the torch backend for configurations it does not cover (BatchNorm / bilinear); an explicit
-``--backend hip --dtype fp32`` on an uncovered model is a clear error."""
+resolves to the fp32 HIP engine (models/hip_unet_f32.py, csrc/fp32.hip) for the reference UNet family and
+its BatchNorm / bilinear variants (round 6), and to the torch backend for configurations it does not cover
+(channel widths not divisible by 32); an explicit ``--backend hip --dtype fp32`` on an uncovered model is a
+clear error."""
 import os
 import subprocess
 import sys
@@ -15,17 +16,19 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def test_resolve_backend_fp32():
-    unet, bn, bil = build_model("unet"), build_model("unet-bn"), build_model("unet-bilinear")
+    unet, bn, bil = build_model("unet"), build_model("unet-bn"), build_model("unet-bn-bilinear")
+    tiny = build_model("unet-tiny")                     # base 8: widths not divisible by 32
     assert resolve_backend("auto", "cuda:0", "bf16") == "hip"
     assert resolve_backend("auto", "cuda:0", "fp32") == "hip"
     assert resolve_backend("auto", "cuda:0", "fp32", unet) == "hip"
-    assert resolve_backend("auto", "cuda:0", "fp32", bn) == "torch"
-    assert resolve_backend("auto", "cuda:0", "fp32", bil) == "torch"
+    assert resolve_backend("auto", "cuda:0", "fp32", bn) == "hip"
+    assert resolve_backend("auto", "cuda:0", "fp32", bil) == "hip"
+    assert resolve_backend("auto", "cuda:0", "fp32", tiny) == "torch"
     assert resolve_backend("auto", "cpu", "fp32", unet) == "torch"
     assert resolve_backend("torch", "cuda:0", "fp32") == "torch"
     assert resolve_backend("hip", "cuda:0", "fp32", unet) == "hip"
     with pytest.raises(ValueError, match="fp32 engine"):
-        resolve_backend("hip", "cuda:0", "fp32", bn)
+        resolve_backend("hip", "cuda:0", "fp32", tiny)
 
 
 @pytest.mark.gpu

@@ -212,7 +212,9 @@ def test_bench_json_contract(hip_lib, extra):
 
 
 @pytest.mark.parametrize("extra", [[], ["--grad-comm-dtype", "bf16"], ["--no-comm-overlap"],
-                                   ["--parallelism", "mp", "--microbatches", "2"]])
+                                   ["--parallelism", "mp", "--microbatches", "2"],
+                                   # row-split top level (parallel/spatial_pipe.py) through bench.py
+                                   ["--parallelism", "mp", "--microbatches", "2", "--mp-cut", "spatial"]])
 def test_bench_two_ranks_same_device(hip_lib, extra):
     """Rehearsal of the multi-rank bench path on one GPU: torchrun with 2 ranks sharing cuda:0 over
     gloo (DPA_SAME_DEVICE=1) - DDP bucketed all-reduce of HIP-engine gradients, and GPipe send/recv of
@@ -243,6 +245,8 @@ def test_bench_two_ranks_same_device(hip_lib, extra):
     rm = out["rank_ms_per_step"]
     assert len(rm["per_rank"]) == 2 and 0 < rm["min"] <= rm["max"]
     assert out["config"]["comm_overlap"] == ("--no-comm-overlap" not in extra)
+    if "spatial" in extra:
+        assert out["config"]["mp_plan"]["cut_mode"] == "spatial" and "spatial" in out["config"]["mp_cut"]
     if not mp_run:  # DDP: the reducer timed the stall on outstanding all-reduce buckets, on every rank
         assert out["exposed_comm_ms_last_step"] is not None and out["exposed_comm_ms_last_step"] >= 0
         assert 0 <= out["exposed_comm_ms"]["min"] <= out["exposed_comm_ms"]["max"]

@@ -254,3 +254,74 @@ def test_shipped_plans_are_well_formed():
             assert len(p["orders"]) == pl.S
             c = [SegCost(1.0, 2.0)] * pl.K
             simulate_placement(pl, PRESETS[model].depth, p["microbatches"], c, orders=p["orders"])
+
+
+def _unet_table():
+    from distributedpytorch_amd.parallel.schedule import load_table, unit_table
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    return unit_table(load_table(os.path.join(root, "profiles", "block_times_unetxl_1024_r04.json")))
+
+
+def test_graph_simulator_reproduces_placement_simulator():
+    """The op-graph scheduler of the row-split model (parallel/spatial.py simulate_graph) is the placement
+    scheduler on a general graph: a whole-level placement expressed as a graph, with the deferred weight
+    gradients after the last op as in simulate_placement, gives the identical timeline."""
+    from distributedpytorch_amd.parallel.schedule import placement_costs, simulate_placement
+    from distributedpytorch_amd.parallel.spatial import GNode, placement_graph, simulate_graph
+    t = _unet_table()
+    for pl, M in ((Placement.mirrored([0, 1, 2, 3, 3.5, 4, 4.5, 5, 6, 6.5, 7, 7.5, 8, 9, 10, 12]), 8),
+                  (Placement.contiguous([0, 2, 4, 5.5, 6.5, 8, 9, 10, 12]), 4)):
+        costs, wg, op, eb = placement_costs(t, pl, 16 // M, M)
+        a = simulate_placement(pl, t["depth"], M, costs, eb, wg, op)
+        nodes, opt = placement_graph(t, pl, 16, M)
+        nodes = [GNode(n.name, n.stage, n.fwd, n.bwd, n.ins, n.head) for n in nodes]    # wgrad at the end
+        b = simulate_graph(nodes, pl.S, M, wg, opt)
+        assert abs(a.step_ms - b.step_ms) < 1e-9 and a.stage_end == pytest.approx(b.stage_end)
+        assert a.orders == b.orders
+
+
+def test_row_split_geometry_is_exact_and_covering():
+    """parallel/spatial.py row_plan: own rows partition the image; every split level runs on rows whose
+    two 3x3 convs are exact (two rows inside each non-border edge) on what its consumers read; decoder rows
+    even-aligned so the transposed conv's output rows map exactly."""
+    from distributedpytorch_amd.parallel.spatial import row_plan
+    for H, S, L, bounds in ((1024, 8, 1, None), (1024, 8, 2, None), (64, 4, 2, None), (64, 2, 1, (0, 24, 64)),
+                            (1024, 8, 2, (0, 132 - 4, 332, 512, 664, 788, 864, 948, 1024))):
+        rp = row_plan(H, S, L, bounds)
+        assert rp[0].own[0] == 0 and rp[-1].own[1] == H
+        assert all(a.own[1] == b.own[0] for a, b in zip(rp, rp[1:]))
+        for sl in rp:
+            for l in range(L):
+                Hl = H >> l
+                ex = lambda r: (r[0] + (2 if r[0] > 0 else 0), r[1] - (2 if r[1] < Hl else 0))   # noqa: E731
+                e = ex(sl.enc_in[l])
+                assert e[0] <= sl.dec_in[l][0] and sl.dec_in[l][1] <= e[1]          # the skip rows are exact
+                d = ex(sl.dec_in[l])
+                need = sl.own if l == 0 else sl.up_src(l - 1)
+                assert d[0] <= need[0] and need[1] <= d[1]                          # consumer's rows exact
+                assert sl.dec_in[l][0] % 2 == 0 and (sl.dec_in[l][1] % 2 == 0 or sl.dec_in[l][1] == Hl)
+                assert sl.enc_in[l][0] % 2 == 0
+                if l + 1 < L:
+                    nxt = sl.enc_in[l + 1]
+                    assert e[0] <= 2 * nxt[0] and 2 * nxt[1] <= e[1]
+            assert ex(sl.enc_in[L - 1])[0] <= 2 * sl.send[0] and 2 * sl.send[1] <= ex(sl.enc_in[L - 1])[1]
+            assert sl.up_src(L - 1) == sl.recv
+
+
+def test_shipped_row_split_plan_predicts_half_efficiency():
+    """Config 5 (UNet-XL 1024^2, 8 stages, b16): the plan tools/pipeline_plan.py ships re-simulates to its
+    recorded prediction, >= 0.5 scaling efficiency with the link queues on, and beats the
+    best whole-level V placement on the same model."""
+    from distributedpytorch_amd.parallel.schedule import PLANS_PATH, single_device_ms
+    from distributedpytorch_amd.parallel.spatial import SpatialPlan, simulate_placement_graph, simulate_spatial
+    with open(PLANS_PATH) as f:
+        p = json.load(f)["unet-xl:1024x1024:8:16"]
+    assert p.get("spatial"), p
+    t = _unet_table()
+    plan = SpatialPlan.from_plan(p).validate(5)
+    tl = simulate_spatial(t, plan, 16, p["microbatches"], policy=p["policy"])
+    eff = single_device_ms(t, 16) / tl.step_ms / 8
+    assert abs(16000.0 / tl.step_ms - p["predicted_img_s"]) < 0.5 and eff >= 0.5
+    v = p["v_alternative"]
+    tv = simulate_placement_graph(t, Placement(tuple(v["cuts"]), tuple(v["owner"])), 16, v["microbatches"])
+    assert tv.step_ms > tl.step_ms

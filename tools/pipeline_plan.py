@@ -28,6 +28,8 @@ from distributedpytorch_amd.models.unet import PRESETS              # noqa: E402
 from distributedpytorch_amd.parallel.placement import Placement, describe, v_partition  # noqa: E402
 from distributedpytorch_amd.parallel.schedule import (evaluate_placement, load_table, search,  # noqa: E402
                                                       simulate_table, single_device_ms, unit_table)
+from distributedpytorch_amd.parallel.spatial import (SpatialPlan, search_spatial,  # noqa: E402
+                                                     simulate_placement_graph, simulate_spatial)
 
 
 def fmt(r, label):
@@ -86,7 +88,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("tables", nargs="+")
     ap.add_argument("--links", default="100,64", help="effective GB/s per directed xGMI peer link (first: the plan's)")
-    ap.add_argument("--out", default="profiles/pipeline_plan_r05.txt")
+    ap.add_argument("--out", default="profiles/pipeline_plan_r06.txt")
     ap.add_argument("--plans", default="distributedpytorch_amd/parallel/plans.json")
     a = ap.parse_args()
     links = [float(v) for v in a.links.split(",")]
@@ -138,15 +140,47 @@ def main():
             pl = Placement(best_v["cuts"], best_v["owner"])
             M = best_v["microbatches"]
             tl = simulate_table(ut, pl, batch // M, M, policy=best_v["policy"], link_gbs=links[0])
-            lines.append(f"-> chosen for {model} {S} stages b{batch}: {pl} M={M} policy {best_v['policy']}: "
-                         f"{best_v['img_s']} img/s predicted at {links[0]:g} GB/s; " + "; ".join(describe(pl, cfg.depth)))
-            lines.append("")
-            plans[f"{model}:{h}x{w}:{S}:{batch}"] = {
+            row = {
                 "cuts": best_v["cuts"], "owner": best_v["owner"], "placement": pl.kind, "microbatches": M,
                 "policy": best_v["policy"], "orders": tl.orders,
                 "predicted_img_s": best_v["img_s"], "predicted_efficiency": best_v.get("scaling_efficiency"),
                 "link_gbs": links[0], "at_slow_link": best_v.get("at_slow_link", {}),
                 "source": os.path.basename(path)}
+            chosen = f"{pl} M={M} policy {best_v['policy']}: {best_v['img_s']} img/s predicted at {links[0]:g} GB/s; " \
+                + "; ".join(describe(pl, cfg.depth))
+            if model != "unet" and not cfg.batchnorm and S >= 4:
+                # row-split top levels (parallel/spatial.py) against the best whole-level V, both on the op-graph
+                # model (deferred weight gradients in the drain's idle time)
+                tv = simulate_placement_graph(ut, pl, batch, M, policy=best_v["policy"], link_gbs=links[0])
+                v_img = round(batch * 1000.0 / tv.step_ms, 1)
+                lines.append(f"## {model} {h}x{w}, {S} stages, b{batch}: row-split top levels vs the V above "
+                             f"(op-graph model; V {pl} M={M}: {v_img} img/s, eff {t1 / tv.step_ms / S:.3f})")
+                sp = search_spatial(ut, S, batch, link_gbs=links[0], top=6)
+                for r in sp:
+                    lines.append(f"spatial L={r['split_levels']} M={r['microbatches']:3d} mb={r['mb']:3d} inner "
+                                 f"{r['inner_cuts']}@{r['inner_owner']} rows {r['row_bounds']} {r['policy']:7s} "
+                                 f"{r['step_ms']:8.2f} ms {r['img_s']:8.1f} img/s eff {r.get('scaling_efficiency')} "
+                                 f"link {r['max_link_gb']:.2f} GB / {r['max_link_busy_ms']:.1f} ms")
+                bs = max(sp, key=lambda r: r["img_s"]) if sp else None
+                if bs is not None and bs["img_s"] > v_img:
+                    sp_pl = SpatialPlan.from_plan(bs)
+                    for gbs in links[1:]:
+                        t2 = simulate_spatial(ut, sp_pl, batch, bs["microbatches"], policy=bs["policy"], link_gbs=gbs)
+                        bs.setdefault("at_slow_link", {})[f"{gbs:g}"] = {
+                            "img_s": round(batch * 1000.0 / t2.step_ms, 1),
+                            "efficiency": round(t1 / t2.step_ms / S, 3)}
+                    row = {**sp_pl.to_plan(), "placement": "spatial", "microbatches": bs["microbatches"],
+                           "policy": bs["policy"], "predicted_img_s": bs["img_s"],
+                           "predicted_efficiency": bs.get("scaling_efficiency"), "link_gbs": links[0],
+                           "at_slow_link": bs.get("at_slow_link", {}), "source": os.path.basename(path),
+                           "v_alternative": {"cuts": best_v["cuts"], "owner": best_v["owner"], "microbatches": M,
+                                             "img_s_graph_model": v_img}}
+                    chosen = f"{sp_pl} M={bs['microbatches']} policy {bs['policy']}: {bs['img_s']} img/s predicted " \
+                             f"(eff {bs.get('scaling_efficiency')}) at {links[0]:g} GB/s (V: {v_img})"
+                lines.append("")
+            lines.append(f"-> chosen for {model} {S} stages b{batch}: {chosen}")
+            lines.append("")
+            plans[f"{model}:{h}x{w}:{S}:{batch}"] = row
     lines += hybrid_tables(a.tables, links[0])
     txt = "\n".join(lines)
     print(txt)
