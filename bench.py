@@ -58,7 +58,9 @@ def parse():
                          "bucket by bucket during it")
     ap.add_argument("--pool", type=int, default=2, help="distinct synthetic batches cycled")
     ap.add_argument("--out", default=None, help="also append the JSON line to this file")
-    ap.add_argument("--graph", action="store_true", help="N=1: replay the step from a captured HIP graph")
+    ap.add_argument("--graph", action="store_true",
+                    help="N=1: replay the step from a captured HIP graph; dp1proc: each replica's forward and "
+                         "backward from HIP graphs (trainer.GraphedDP)")
     ap.add_argument("--parallelism", choices=["dp", "mp", "dp1proc"], default="dp",
                     help="dp: one replica per GPU, RCCL all-reduce (weak scaling); mp: GPipe over the N ranks "
                          "(one batch of --batch images split into --microbatches, strong scaling); with one "
@@ -68,6 +70,9 @@ def parse():
                          "issue rehearsal)")
     ap.add_argument("--replicas", type=int, default=0,
                     help="dp1proc: replicas (0: one per visible GPU)")
+    ap.add_argument("--reserve-cus", type=int, default=0,
+                    help="run the step's compute (and the engine's side streams) on CU-masked streams that leave this "
+                         "many CUs free for communication kernels (RCCL buckets; measured with --comm-probe)")
     ap.add_argument("--comm-probe", action="store_true",
                     help="N=1 dp: after the timed steps, run steps that launch an RCCL-bucket stand-in at each "
                          "DDP bucket-ready point and report how long it waited for CUs (utils/comm_probe.py)")
@@ -189,8 +194,23 @@ def main():
         img, mask = synthetic_batch(a.batch * n_rep, a.img[0], a.img[1], 3, seed=1000 * data_rank + i, device=device)
         pool.append((img, mask.float().unsqueeze(1)))
 
+    masked = None
+    if a.reserve_cus:
+        masked = K.cu_masked_stream(device, a.reserve_cus)
+        masked.wait_stream(torch.cuda.current_stream(device))
+        eng = getattr(getattr(strat, "compute", None), "blocks", None)
+        if eng is not None and getattr(eng, "side", None) is not None:
+            eng.side = K.cu_masked_stream(device, a.reserve_cus)
+            if hasattr(eng, "side2"):
+                eng.side2 = K.cu_masked_stream(device, a.reserve_cus)
+        torch.cuda.set_stream(masked)
+        print(f"[bench] compute on CU-masked streams: {masked.cus} CUs, {a.reserve_cus} reserved", file=sys.stderr)
+
     graphed = None
-    if a.graph and world == 1 and not mp:
+    if a.graph and dp1:
+        from distributedpytorch_amd.trainer import GraphedDP
+        graphed = GraphedDP(strat, *pool[0])
+    elif a.graph and world == 1 and not mp:
         from distributedpytorch_amd.trainer import GraphedStep
         graphed = GraphedStep(strat, *pool[0])
 
@@ -300,7 +320,7 @@ def main():
                    "mp_cut": (str(getattr(strat.pipe, "pl", None) or strat.pipe.plan) if mp else None),
                    "mp_plan": mp_info, "bucket_mb": a.bucket_mb,
                    "grad_comm_dtype": a.grad_comm_dtype, "comm_overlap": a.comm_overlap,
-                   "hip_graph": graphed is not None},
+                   "hip_graph": graphed is not None, "reserve_cus": a.reserve_cus},
         "final_loss": round(final_loss, 5) if final_loss == final_loss else None, "warmup_s": round(warm_s, 2),
         "host_ms_per_step": round(1000.0 * host_s / a.steps, 3),
         "peak_mem_gb": round(torch.cuda.max_memory_allocated(device) / 2 ** 30, 2),

@@ -10,7 +10,10 @@
 #include "common.h"
 #include "conv_args.h"
 
+#include <hip/hip_ext.h>
+
 #include <type_traits>
+#include <vector>
 
 // ------------------------------------------------------------------------------ input conversion
 __global__ __launch_bounds__(256) void nchw3_to_nhwc8_kernel(const float* __restrict__ x, bf16_t* __restrict__ y, int B,
@@ -639,4 +642,32 @@ DPA_API int dpa_comm_probe(const void* src, void* dst, long long n16, int blocks
   hipLaunchKernelGGL(comm_probe_kernel, dim3(blocks), dim3(256), 0, st, (const float4*)src, (float4*)dst, (long)n16,
                      stamp);
   return (int)hipGetLastError();
+}
+
+// A compute stream restricted to all CUs but `reserve` of them (hipExtStreamCreateWithCUMask), spread evenly
+// over the CU index range: the backward's one-workgroup-per-CU GEMMs then always leave CUs on which an RCCL
+// bucket's kernels start at once (VERDICT r5 #3c; the measured trade-off: BASELINE.md round 6).
+DPA_API int dpa_stream_create_cumask(int device, int reserve, void** out) {
+  hipError_t e = hipSetDevice(device);
+  if (e != hipSuccess) return (int)e;
+  hipDeviceProp_t prop;
+  e = hipGetDeviceProperties(&prop, device);
+  if (e != hipSuccess) return (int)e;
+  const int n = prop.multiProcessorCount;
+  if (reserve < 0 || reserve >= n) return (int)hipErrorInvalidValue;
+  std::vector<uint32_t> mask((n + 31) / 32, 0u);
+  const int every = reserve > 0 ? n / reserve : n + 1;
+  int kept = 0;
+  for (int i = 0; i < n; ++i) {
+    const bool res = reserve > 0 && (i % every) == every - 1 && (i / every) < reserve;
+    if (!res) {
+      mask[i / 32] |= 1u << (i % 32);
+      ++kept;
+    }
+  }
+  hipStream_t s;
+  e = hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data());
+  if (e != hipSuccess) return (int)e;
+  *out = (void*)s;
+  return kept;      // >= 0: the number of CUs the stream may use
 }

@@ -504,9 +504,9 @@ class F32Engine:
             return start
 
         for c in layers:
-            if c.mod.weight.device != self.device or (self._owned is not None and id(c.mod.weight) not in self._owned):
+            if c.kind == "up":                # bilinear Up: its 1x1 projection is a plain GEMM (torch.addmm)
                 continue
-            if c.kind == "up":                # bilinear Up: its 1x1 projection is a plain GEMM (torch.mm)
+            if c.mod.weight.device != self.device or (self._owned is not None and id(c.mod.weight) not in self._owned):
                 continue
             if c.kind == "conv":
                 c.off_f = add(0, c.mod.weight, c.Cout, c.Cin, c.Cs, c.Cout, c.Kf)

@@ -1200,3 +1200,19 @@ def comm_probe(src: torch.Tensor, dst: torch.Tensor, stamp: torch.Tensor, blocks
     assert stamp.dtype == torch.int64 and src.is_cuda and dst.is_cuda and stamp.is_cuda
     _check(_lib.lib().dpa_comm_probe(_p(src), _p(dst), c_ll(nb // 16), c_int(blocks), _p(stamp),
                                      c_void_p(torch.cuda.current_stream(src.device).cuda_stream)), "comm_probe")
+
+
+def cu_masked_stream(device, reserve: int) -> torch.cuda.ExternalStream:
+    """A HIP stream of ``device`` whose kernels may use every CU but ``reserve`` (spread over the CU index
+    range): compute on it always leaves CUs free for another stream's kernels (an RCCL bucket's).  Returns a
+    torch ExternalStream (the stream lives for the process)."""
+    dev = torch.device(device)
+    L = _lib.lib()
+    L.dpa_stream_create_cumask.restype = c_int
+    out = c_void_p()
+    kept = L.dpa_stream_create_cumask(c_int(dev.index or 0), c_int(int(reserve)), ctypes.byref(out))
+    if kept < 0 or out.value is None:
+        raise RuntimeError(f"hipExtStreamCreateWithCUMask failed ({kept})")
+    s = torch.cuda.ExternalStream(out.value, device=dev)
+    s.cus = kept
+    return s

@@ -585,4 +585,5 @@ def load_plan(model: str, h: int, w: int, stages: int, batch: int, path: str = N
             raise ValueError(f"{pl.S} stages / {M} microbatches")
     except (ValueError, KeyError, TypeError) as e:
         raise ValueError(f"malformed pipeline plan {key}: {p} ({e})") from e
-    return dict(p, placement=pl, cuts=list(pl.cuts), microbatches=M)
+    cuts = list(pl.cuts) if hasattr(pl, "cuts") else list(pl.inner_cuts)
+    return dict(p, placement=pl, cuts=cuts, microbatches=M)

@@ -456,9 +456,10 @@ class SpatialGPipe:
         loss = loss_from_partials(P.sum(0), targets.numel(), dice)
         (loss * loss_scale).backward()
         dP = P.grad
-        # ---- every backward receive
+        # ---- every backward receive, posted in the order the senders send: microbatches M-1 .. 0 (a
+        # communicator matches one sender's messages to a receiver in order)
         brx = {}
-        for m in range(M):
+        for m in reversed(range(M)):
             if me == self.last:
                 for s in range(S):
                     if s != me:

@@ -724,6 +724,98 @@ class GraphedStep:
         return self.loss.clone()
 
 
+class GraphedDP:
+    """``-t DP`` with every replica's forward and backward replayed from HIP graphs (VERDICT r5 #3b).
+
+    One process drives all replicas: eagerly that is ~140 kernel launches plus the Python autograd walk per
+    replica under one GIL -- measured on one GPU with 8 replicas at 32 images each, 60.6 ms of host issue per
+    step against 11.9 ms of device time per replica (``bench.py --parallelism dp1proc``, BASELINE.md round
+    6), so 8 real GPUs would wait on the host.  Here each replica's forward (weight packing, blocks, fused
+    loss partial sums) and its backward are two graphs captured once; a step is, per replica, two replays
+    and a few copies, plus the cross-replica coupling done eagerly between them: the reference's global
+    BCE - log Dice needs the SUM of all replicas' partial sums before any backward (dL/dS is then the same
+    seed for every replica), and the gradient sum runs after the backward graphs as one reduction (the
+    native RCCL clique; the bucketed overlap would have to live inside one replica's graph) before Adam.
+    Capture needs one eager warm-up (lazy allocations); it changes no parameter (no optimizer step)."""
+
+    @staticmethod
+    def supported(strat) -> bool:
+        return type(strat) is DPStrategy and strat.device.type == "cuda"
+
+    def __init__(self, strat, images, targets):
+        self.strat = strat
+        dp = strat.dp
+        if dp.reducer is not None:
+            dp.reducer.overlap = False          # one reduction after the backward graphs (see above)
+            n = len(dp.spaces[0].numels)
+            dp.reducer.buckets, dp.reducer.bucket_of = [(0, dp.spaces[0].offsets[-1], 0, n)], [0] * n
+            dp.reducer.expected = [n * len(dp.spaces)]
+            dp.reducer.reset()
+        self.devices = dp.devices
+        self.xs = [x.detach().clone() for x in dp.scatter(images)]
+        self.ts = [t.detach().clone() for t in dp.scatter(targets)]
+        self.n = targets.numel()
+        bufs = [{k: v.clone() for k, v in r.named_buffers()} for r in dp.replicas]
+        # eager warm-up: lazy allocations, packed weights, kernel caches (no optimizer step)
+        for sp in dp.spaces:
+            sp.zero_grad()
+        loss = dp.forward_loss(images, targets)
+        _backward(loss, _loss_scale(strat.cfg, images.shape[0]))
+        dp.all_reduce_grads()
+        torch.cuda.synchronize()
+        self.S, self.dS, self.fwd, self.bwd = [], [], [], []
+        for r, (comp, d) in enumerate(zip(dp.computes, self.devices)):
+            with torch.cuda.device(d):
+                dp.spaces[r].touch()            # the captured forward repacks the weights every replay
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    S = comp.forward_partials(self.xs[r], self.ts[r])
+                self.fwd.append(g)
+                self.S.append(S)
+                self.dS.append(torch.zeros_like(S))
+        for r, d in enumerate(self.devices):
+            with torch.cuda.device(d):
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, pool=self.fwd[r].pool()):
+                    torch.autograd.backward(self.S[r], self.dS[r])
+                self.bwd.append(g)
+        if dp.reducer is not None:
+            dp.reducer.reset()                  # the captures announced gradients: nothing was reduced
+        torch.cuda.synchronize()
+        with torch.no_grad():                   # BatchNorm running statistics as before the captures
+            for rep, b in zip(dp.replicas, bufs):
+                for k, v in rep.named_buffers():
+                    v.copy_(b[k])
+        log.info(f"DP: captured forward + backward graphs of {len(self.devices)} replicas")
+
+    def matches(self, images, targets) -> bool:
+        return images.shape[0] == sum(x.shape[0] for x in self.xs) and images.shape[1:] == self.xs[0].shape[1:]
+
+    def __call__(self, images, targets):
+        strat, dp = self.strat, self.strat.dp
+        strat.optimizer.zero_grad()
+        for x, xs in zip(dp.scatter(images), self.xs):
+            xs.copy_(x, non_blocking=True)
+        for t, ts in zip(dp.scatter(targets), self.ts):
+            ts.copy_(t, non_blocking=True)
+        for r, d in enumerate(self.devices):
+            with torch.cuda.device(d):
+                self.fwd[r].replay()
+        d0 = self.devices[0]
+        St = sum(S.to(d0) for S in self.S).detach().requires_grad_(True)
+        loss = loss_from_partials(St, self.n)
+        _backward(loss, _loss_scale(strat.cfg, images.shape[0]))
+        for r, d in enumerate(self.devices):
+            with torch.cuda.device(d):
+                self.dS[r].copy_(St.grad.to(d), non_blocking=True)
+                self.bwd[r].replay()
+        dp.all_reduce_grads()
+        strat.optimizer.step()
+        for sp in dp.spaces:
+            sp.touch()
+        return loss.detach()
+
+
 class _Profiler:
     """``--profile``: torch.profiler (CPU + HIP kernel activity via roctracer) over steps 3..7 of the
     run; writes a Chrome trace ``logs/<method>_rank<r>_trace.json`` and a per-kernel table

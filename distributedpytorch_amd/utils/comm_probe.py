@@ -79,8 +79,9 @@ class CommProbe:
         k = len(self.buckets)
         launched = self.next_launch
         for b in range(launched):
-            self._launch(b, slot=k + b)
-            torch.cuda.synchronize(self.device)
+            for _ in range(2):              # the second run is the baseline (the first pays launch warm-up)
+                self._launch(b, slot=k + b)
+                torch.cuda.synchronize(self.device)
         st = self.stamp.cpu()
         step_us = self.ev_step[0].elapsed_time(self.ev_step[1]) * 1e3
 

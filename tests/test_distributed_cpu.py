@@ -477,8 +477,9 @@ def _spatial_worker(rank, world, port, plan_kw, M, q):
     lref = bce_dice_from_probs(ref(x), t)
     lref.backward()
     refp = dict(ref.named_parameters())
+    # relative to each gradient's own scale (an absolute bound hid swapped microbatches once)
     bad = [n for n, p in model.named_parameters()
-           if p.requires_grad and not torch.allclose(p.grad, refp[n].grad, atol=2e-5, rtol=1e-4)]
+           if p.requires_grad and float((p.grad - refp[n].grad).abs().max()) > 1e-4 * float(refp[n].grad.abs().max())]
     nown = sum(1 for p in model.parameters() if p.requires_grad)
     probs = pipe.eval_probs(x, 4, (64, 64))
     with torch.no_grad():

@@ -194,8 +194,8 @@ def main():
                 old = json.load(f)
         for key, row in plans.items():      # measured rehearsals stay with a plan whose placement is unchanged
             prev = old.get(key, {})
-            if "measured" in prev and prev.get("cuts") == row["cuts"] and prev.get("owner") == row["owner"] \
-                    and prev.get("microbatches") == row["microbatches"]:
+            if "measured" in prev and prev.get("cuts") == row.get("cuts") and prev.get("owner") == row.get("owner") \
+                    and prev.get("inner_cuts") == row.get("inner_cuts") and prev.get("microbatches") == row["microbatches"]:
                 row["measured"] = prev["measured"]
         with open(a.plans, "w") as f:
             json.dump(plans, f, indent=1)
