@@ -762,9 +762,6 @@ __global__ __launch_bounds__(512) void igemm_pp2_kernel(IgemmArgs a) {
   __builtin_amdgcn_sched_barrier(0);
   __builtin_amdgcn_s_barrier();
   if (grp) __builtin_amdgcn_s_barrier();       // the second half runs one barrier behind
-#ifdef DPA_PRIO_STATIC
-  if (grp) __builtin_amdgcn_s_setprio(1);      // experiment: static priority for the second half
-#endif
   __builtin_amdgcn_sched_barrier(0);
 
   bf16x8_t af[4][2], bfr[2][2][2];
@@ -802,14 +799,10 @@ __global__ __launch_bounds__(512) void igemm_pp2_kernel(IgemmArgs a) {
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-#ifndef DPA_PRIO_STATIC
     __builtin_amdgcn_s_setprio(1);
-#endif
   };
   auto sync_out = [&]() {
-#ifndef DPA_PRIO_STATIC
     __builtin_amdgcn_s_setprio(0);
-#endif
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
@@ -1070,9 +1063,6 @@ __global__ __launch_bounds__(512) void igemm_pp2h_kernel(IgemmArgs a) {
   __builtin_amdgcn_sched_barrier(0);
   __builtin_amdgcn_s_barrier();
   if (grp) __builtin_amdgcn_s_barrier();       // the second half runs one barrier behind
-#ifdef DPA_PRIO_STATIC
-  if (grp) __builtin_amdgcn_s_setprio(1);      // experiment: static priority for the second half
-#endif
   __builtin_amdgcn_sched_barrier(0);
 
   bf16x8_t af[NIC][2], bfr[2][2][2];
@@ -1112,14 +1102,10 @@ __global__ __launch_bounds__(512) void igemm_pp2h_kernel(IgemmArgs a) {
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-#ifndef DPA_PRIO_STATIC
     __builtin_amdgcn_s_setprio(1);
-#endif
   };
   auto sync_out = [&]() {
-#ifndef DPA_PRIO_STATIC
     __builtin_amdgcn_s_setprio(0);
-#endif
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);

@@ -164,9 +164,6 @@ __global__ __launch_bounds__(512) void wgrad_gemm_kernel(WgradArgs a) {
   __builtin_amdgcn_sched_barrier(0);
   __builtin_amdgcn_s_barrier();
   if (grp) __builtin_amdgcn_s_barrier();       // the second half runs one barrier behind
-#ifdef DPA_PRIO_STATIC
-  if (grp) __builtin_amdgcn_s_setprio(1);      // experiment: static priority for the second half
-#endif
   __builtin_amdgcn_sched_barrier(0);
 
   // per-lane LDS byte offsets of the transposed fragment reads (conv_args.h tr_frag's addressing) inside
@@ -258,14 +255,10 @@ __global__ __launch_bounds__(512) void wgrad_gemm_kernel(WgradArgs a) {
     __builtin_amdgcn_s_barrier();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this phase's asm fragment reads
     __builtin_amdgcn_sched_barrier(0);
-#ifndef DPA_PRIO_STATIC
     __builtin_amdgcn_s_setprio(1);
-#endif
   };
   auto sync_out = [&]() {
-#ifndef DPA_PRIO_STATIC
     __builtin_amdgcn_s_setprio(0);
-#endif
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);

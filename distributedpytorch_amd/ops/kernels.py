@@ -404,6 +404,9 @@ def wgrad(A: torch.Tensor, B: torch.Tensor, *, kind: int, grid, M: int, Nc: int,
         return _wgrad_stream(A, B, grid=grid, M=M, Nc=Nc, gw=gw, gb=gb, Nreal=Nreal, abn=abn)
     if _ABLATE and ("wgrad" in _ABLATE or ("wgrad_deep" in _ABLATE and (M >= 128 or Nc >= 128))):
         return
+    if (path == "band" or (path == "auto" and wgrad_band_eligible(M, Nc, grid))) and kind == 0 and cfg == 0 \
+            and A.shape[1:3] == B.shape[1:3] == tuple(grid[1:]):
+        return _wgrad_band(A, B, grid=grid, M=M, Nc=Nc, gw=gw, gb=gb, Nreal=Nreal)
     if (path == "gemm" or (path == "auto" and wgrad_gemm_eligible(M, Nc, grid))) and kind == 0 and cfg == 0 \
             and A.shape[1:3] == B.shape[1:3] == tuple(grid[1:]):
         return _wgrad_gemm(A, B, grid=grid, M=M, Nc=Nc, gw=gw, gb=gb, Nreal=Nreal)
@@ -515,6 +518,69 @@ def _wgrad_gemm(A, B, *, grid, M, Nc, gw, gb, Nreal, blocks: int = 0, tabs=None,
                               c_int(Nreal), c_int(0), st), "wgrad_reduce(gemm)")
 
 
+# deep-layer weight gradients with the input band staged once for all nine taps (csrc/wgrad_band.hip):
+# 256 output channels x (9 taps x 32 input channels) per workgroup; DPA_NO_WGRAD_BAND=1 -> wgrad_gemm
+USE_WGRAD_BAND = CFG.wgrad_band
+
+
+def wgrad_band_eligible(M: int, Nc: int, grid) -> bool:
+    N, H, W = grid
+    return USE_WGRAD_BAND and M % 256 == 0 and Nc % 32 == 0 and W in (32, 64) and H % (64 // W) == 0
+
+
+def wgrad_band_ips(N: int, H: int, W: int, M: int, Nc: int, group: int = 0, cus: int = 256,
+                   min_blocks: int = 512) -> int:
+    """Images per split of a band launch: the fewest rounds of workgroups over the CUs (one 140-KB workgroup
+    per CU) times the work per workgroup, plus the fp32 slab traffic of the split-K partials; at least
+    ``min_blocks`` workgroups when the batch allows (room to interleave with the other stream's kernels).
+    ``group``: splits stay inside ``group``-image tensors (per-image tables)."""
+    tiles = (M // 256) * (Nc // 32)
+    steps = H * W // 64
+    t_step, bw = 1.6e-6, 4e12                     # ~60 % MFMA per K-step (9.4 MFLOP); slab write + read
+    best = None
+    for ips in range(1, N + 1):
+        if group and group % ips:
+            continue
+        splits = -(-N // ips)
+        blocks = splits * tiles
+        cost = -(-blocks // cus) * ips * steps * t_step + splits * 9 * M * Nc * 8 / bw
+        key = (blocks < min(min_blocks, N * tiles), cost)
+        if best is None or key < best[0]:
+            best = (key, ips)
+    return best[1]
+
+
+def _wgrad_band(A, B, *, grid, M, Nc, gw, gb, Nreal, tabs=None, group: int = 0, ips: int = 0):
+    """conv3x3 weight (+bias) gradient of the deep layers (64^2 / 32^2 grids, Cout % 256 == 0): one
+    workgroup per (group of images, 256 output channels x 32 input channels x 9 taps); split-K slabs over
+    the image groups, reduced by dpa_wgrad_reduce (same slab layout as :func:`_wgrad_gemm`)."""
+    NA, HA, WA, CA, lda = _nhwc(A, "wgrad_band.A")
+    NB, HB, WB, CB, ldb = _nhwc(B, "wgrad_band.B")
+    N, Hg, Wg = grid
+    assert (HA, WA) == (Hg, Wg) == (HB, WB) and CA >= M and CB >= Nc
+    assert (NA == NB == N) or (tabs is not None and tabs[0].numel() == tabs[1].numel() == N and group > 0
+                               and N % group == 0)
+    assert gw.dtype == torch.float32 and gw.is_contiguous() and gw.numel() == M * Nreal * 9
+    ips = ips or wgrad_band_ips(N, Hg, Wg, M, Nc, group if tabs is not None else 0)
+    ips = max(1, min(ips, (_MAX_BYTES - 1) // (Hg * Wg * max(lda, ldb) * 2)))
+    if tabs is not None:
+        while group % ips:        # a split never straddles two tensors
+            ips -= 1
+    splits = -(-N // ips)
+    slab = torch.empty(splits * 9 * M * Nc + splits * M, dtype=torch.float32, device=A.device)
+    bslab = slab[splits * 9 * M * Nc:] if gb is not None else None
+    a = WgradArgs(A.data_ptr(), B.data_ptr(), slab.data_ptr(), None if bslab is None else bslab.data_ptr(), lda, ldb,
+                  N, Hg, Wg, HA, WA, HB, WB, M, Nc, 1, 1, 3, ips, splits, ips * Hg * Wg * lda * 2,
+                  ips * Hg * Wg * ldb * 2)
+    if tabs is not None:
+        a.atab, a.btab = tabs[0].data_ptr(), tabs[1].data_ptr()
+    L = _lib.lib()
+    st = _stream(A)
+    _check(L.dpa_wgrad_band(ctypes.byref(a), st), "wgrad_band")
+    _check(L.dpa_wgrad_reduce(_p(slab), _p(bslab), _p(gw), _p(gb), c_int(splits), c_int(9), c_int(M), c_int(Nc),
+                              c_int(Nreal), c_int(0), st), "wgrad_reduce(band)")
+
+
 def _image_table(ts, C_min: int, name: str):
     """Device array of per-image base pointers over the images of tensors ``ts`` (same H, W, ld)."""
     ptrs, geo = [], None
@@ -541,6 +607,9 @@ def wgrad_multi(As, Bs, *, M: int, Nc: int, gw: torch.Tensor, gb: Optional[torch
     # splits cannot straddle two microbatch tensors: with few-image microbatches at the deepest levels
     # (UNet-XL, 2 images of 32x32) that means short splits and a slab set several times the batch's
     # dW -- keep the gemm path for >= 64 K-steps per split (profiles/pipeline_rehearsal_r03.txt)
+    if wgrad_band_eligible(M, Nc, (N, H, W)) and len(sizes) == 1:
+        return _wgrad_band(As[0], Bs[0], grid=(N, H, W), M=M, Nc=Nc, gw=gw, gb=gb, Nreal=Nreal, tabs=tabs,
+                           group=sizes.pop())
     if wgrad_gemm_eligible(M, Nc, (N, H, W)) and len(sizes) == 1 and min(sizes) * (H * W // 64) >= 64:
         return _wgrad_gemm(As[0], Bs[0], grid=(N, H, W), M=M, Nc=Nc, gw=gw, gb=gb, Nreal=Nreal, tabs=tabs,
                            group=sizes.pop())

@@ -223,7 +223,11 @@ def test_deconv_dgrad_from_concat(hip_lib, N, h, w, Cin, Cout):
     # deep layers as a dense 256x256 LDS-DMA GEMM (csrc/wgrad_gemm.hip): partial last column tile
     # (9 x 128 = 1152, 9 x 64 = 576 columns), 32-wide rows (two rows per K-step), several channel tiles
     (2, 4, 64, 128, 256, None, "gemm"), (3, 6, 32, 256, 256, None, "gemm"), (1, 2, 128, 64, 512, None, "gemm"),
-    (2, 5, 64, 512, 256, None, "gemm")])
+    (2, 5, 64, 512, 256, None, "gemm"),
+    # deep layers with the input band staged once for all 9 taps (csrc/wgrad_band.hip): 64-wide rows (one row
+    # per K-step), 32-wide rows (two), several channel and output-channel tiles, one-image batches
+    (2, 4, 64, 128, 256, None, "band"), (3, 6, 32, 256, 256, None, "band"), (2, 5, 64, 512, 256, None, "band"),
+    (1, 2, 32, 64, 512, None, "band"), (3, 2, 64, 32, 256, None, "band"), (1, 1, 64, 32, 256, None, "band")])
 def test_conv3x3_wgrad(hip_lib, N, H, W, Cin, Cout, cin_pad, path):
     from distributedpytorch_amd.ops import kernels as K
     torch.manual_seed(4)
@@ -698,6 +702,36 @@ def test_wgrad_gemm_image_groups(hip_lib, blocks):
     torch.cuda.synchronize()
     assert _rel(gw.cpu().view(Cout, Cin, 3, 3), wr.grad) < 1e-2, blocks
     assert _rel(gb.cpu(), br.grad) < 1e-2, blocks
+
+
+@pytest.mark.parametrize("N,H,W,Cin,Cout,ips", [
+    (8, 64, 64, 256, 256, 0), (8, 64, 64, 512, 256, 3), (8, 64, 64, 128, 256, 8), (16, 32, 32, 512, 512, 0),
+    (16, 32, 32, 256, 512, 5), (5, 32, 32, 64, 256, 1)])
+def test_wgrad_band_real_shapes(hip_lib, N, H, W, Cin, Cout, ips):
+    """csrc/wgrad_band.hip at the UNet's deep-layer shapes (64^2 x 128/256/512 -> 256, 32^2 -> 512) and image
+    groups of 1 .. N (ragged last split): fp32-anchored -- torch fp32 conv2d backward on the same bf16
+    operands; and equal (fp32 summation-order level) to the dense-GEMM path it replaces."""
+    from distributedpytorch_amd.ops import kernels as K
+    torch.manual_seed(23)
+    x = torch.randn(N, Cin, H, W, device="cuda").to(torch.bfloat16)
+    g = torch.randn(N, Cout, H, W, device="cuda").to(torch.bfloat16)
+    # fp32 reference as 9 shifted fp32 GEMMs (no MIOpen algorithm search at these sizes)
+    xh, gh = x.permute(0, 2, 3, 1).contiguous(), g.permute(0, 2, 3, 1).contiguous()
+    xp = F.pad(xh.float(), (0, 0, 1, 1, 1, 1))
+    g2 = gh.float().reshape(-1, Cout).t()
+    ref = torch.stack([g2 @ xp[:, kh:kh + H, kw:kw + W].reshape(-1, Cin) for kh in range(3) for kw in range(3)], -1)
+    ref = ref.view(Cout, Cin, 3, 3)
+    bref = g2.sum(1)
+    gw = torch.zeros(Cout * Cin * 9, device="cuda")
+    gb = torch.zeros(Cout, device="cuda")
+    K._wgrad_band(gh, xh, grid=(N, H, W), M=Cout, Nc=Cin, gw=gw, gb=gb, Nreal=Cin, ips=ips)
+    gw2 = torch.zeros(Cout * Cin * 9, device="cuda")
+    gb2 = torch.zeros(Cout, device="cuda")
+    K._wgrad_gemm(gh, xh, grid=(N, H, W), M=Cout, Nc=Cin, gw=gw2, gb=gb2, Nreal=Cin)
+    torch.cuda.synchronize()
+    assert _rel(gw.view(Cout, Cin, 3, 3), ref) < 1e-4
+    assert _rel(gb, bref) < 1e-4
+    assert _rel(gw, gw2) < 1e-5 and _rel(gb, gb2) < 1e-5
 
 
 @pytest.mark.parametrize("M,Nc,H,W,mb,nmb", [(256, 256, 4, 64, 3, 3), (256, 128, 3, 32, 2, 4), (512, 64, 2, 64, 4, 2),

@@ -50,7 +50,7 @@ def _wgrad_args(**kw):
 def test_library_exports_and_version(L):
     assert L.dpa_version() > 0
     for name in ("dpa_igemm", "dpa_igemm_glds", "dpa_igemm_halo", "dpa_igemm_stream", "dpa_wgrad", "dpa_wgrad_halo",
-                 "dpa_wgrad_stream", "dpa_wgrad_gemm", "dpa_wgrad_reduce", "dpa_deconv_fwd", "dpa_deconv_bwd", "dpa_maxpool2",
+                 "dpa_wgrad_stream", "dpa_wgrad_gemm", "dpa_wgrad_band", "dpa_wgrad_reduce", "dpa_deconv_fwd", "dpa_deconv_bwd", "dpa_maxpool2",
                  "dpa_pool_bwd", "dpa_pool_bwd_code", "dpa_head_fwd", "dpa_head_bwd", "dpa_bn_fwd", "dpa_bn_bwd",
                  "dpa_up2_fwd", "dpa_up2_bwd", "dpa_adam_flat", "dpa_adam_flat_dev", "dpa_pack_weights",
                  "dpa_slab_fold", "dpa_loss_finish", "dpa_loss_grad"):
@@ -179,6 +179,23 @@ def test_wgrad_gemm_rejects(L, kw):
     assert L.dpa_wgrad_gemm(ctypes.byref(_wgrad_args(**base)), None) != INVALID     # the valid case passes
     base.update(kw)
     assert L.dpa_wgrad_gemm(ctypes.byref(_wgrad_args(**base)), None) == INVALID
+
+
+@pytest.mark.parametrize("kw", [dict(M=128), dict(Nc=48), dict(Nc=16, ldb=16), dict(Wg=128, WA=128, WB=128),
+                                dict(Hg=3, HA=3, HB=3, Wg=32, WA=32, WB=32), dict(KW=2), dict(pad=0), dict(HB=32),
+                                dict(splits=2), dict(pix_per_split=0), dict(lda=260), dict(abytes=1024),
+                                dict(N=0), dict(atab=1)])
+def test_wgrad_band_rejects(L, kw):
+    """csrc/wgrad_band.hip: M % 256, Nc % 32, W in {32, 64}, H % (64 / W), 3x3 s1 p1 on one grid, split count =
+    ceil(N / images per split), 16-B strides, both or neither per-image table, 32-bit split extents (a
+    one-K-step split is valid here: no peeled tail)."""
+    base = dict(M=256, Nc=64, lda=256, ldb=64, pix_per_split=1, splits=1,
+                abytes=64 * 64 * 256 * 2, bbytes=64 * 64 * 64 * 2)
+    assert L.dpa_wgrad_band(ctypes.byref(_wgrad_args(**base)), None) != INVALID     # the valid case passes
+    one_step = dict(base, Hg=1, HA=1, HB=1)
+    assert L.dpa_wgrad_band(ctypes.byref(_wgrad_args(**one_step)), None) != INVALID
+    base.update(kw)
+    assert L.dpa_wgrad_band(ctypes.byref(_wgrad_args(**base)), None) == INVALID
 
 
 def test_elementwise_launchers_reject(L):

@@ -10,6 +10,7 @@
 #   smoke                  __graft_entry__.smoke()
 #   bench[:N]              python bench.py $BENCH_ARGS, N times (default 1), JSON lines -> $O/bench.jsonl
 #   run:NAME|ARGS          python bench.py ARGS -> $O/NAME.log (the JSON line also -> $O/bench.jsonl)
+#   envrun:NAME|VAR=V ..|ARGS  the same with extra environment (e.g. DPA_LIB_PATH=build/ab/X/libdpa_hip.so)
 #   prof:NAME|ARGS         rocprofv3 --kernel-trace --stats of bench.py ARGS -> $O/NAME/, summary NAME.txt
 #   pmc:NAME|COUNTERS|ARGS rocprofv3 --pmc COUNTERS (one pass) of bench.py ARGS -> $O/NAME/
 #   py:NAME|SCRIPT ARGS    python SCRIPT ARGS -> $O/NAME.log (tools that need the GPU)
@@ -50,6 +51,10 @@ for task in "$@"; do
     run)
       name=${arg%%|*}; args=${arg#*|}
       step "$name" timeout -k 10 $LIMIT python bench.py $args --out "$O/bench.jsonl" > "$O/$name.log" 2>&1
+      tail -1 "$O/$name.log" | cut -c1-260 ;;
+    envrun)
+      name=${arg%%|*}; rest=${arg#*|}; vars=${rest%%|*}; args=${rest#*|}
+      step "$name" env $vars timeout -k 10 $LIMIT python bench.py $args --out "$O/bench.jsonl" > "$O/$name.log" 2>&1
       tail -1 "$O/$name.log" | cut -c1-260 ;;
     prof)
       name=${arg%%|*}; args=${arg#*|}
