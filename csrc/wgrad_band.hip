@@ -303,6 +303,251 @@ __global__ __launch_bounds__(512) void wgrad_band_kernel(WgradArgs a) {
   else run(std::integral_constant<int, 0>{});
 }
 
+// ------------------------------------------------------------------------------------------------
+// 128-output-channel form (the 128^2 level of the reference UNet -- enc.conv3, dec.conv2 -- and any grid with
+// W % 64 == 0): 128 co x (9 taps x 64 ci) = 128 x 576 per workgroup; a K-step = 64 pixels of ONE image row
+// (w0 = 0, 64, ...).  The band is 3 rows x 72 pixels x 64 channels (128-B pixel rows): band pixel c <-> image
+// column w0 - 1 + c, nine 1-KB DMA instructions per row whose lanes outside the image read zeros (per-lane
+// range check) -- at interior strips the halo columns are real pixels.  16 KB A + 27 KB B per 9.4 MFLOP.
+// Waves: 2 (64 output channels) x 4 (16-channel quarter j of the 64, all nine taps): every wave's taps are
+// compile-time and its quarter is an XOR of the fragment address (chunk bits 1-2, which the swizzle
+// commutes with).  Splits are ranges of K-steps (pix_per_split pixels, a multiple of 64): a split may start
+// inside an image (256 K-steps per 128^2 image).
+namespace {
+constexpr int B1_RB = 128;                       // B pixel row: 64 input channels
+constexpr int B1_SP = 80;                        // LDS pixel rows per band row (72 used)
+constexpr int B1_BYTES = 3 * B1_SP * B1_RB;      // 30720
+constexpr int A1_RB = 256;                       // A pixel row: 128 gradient channels
+constexpr int A1_BYTES = 64 * A1_RB;             // 16384
+constexpr int S1 = A1_BYTES + B1_BYTES;          // 47104 per K-step buffer
+constexpr int NBI1 = 4;                          // 27 band instructions over 8 waves (5 zero-fill dummies)
+constexpr int LDS1 = NBUF * S1 + 1024;
+}  // namespace
+
+__global__ __launch_bounds__(512) void wgrad_band128_kernel(WgradArgs a) {
+  __shared__ __attribute__((aligned(1024))) char lds[LDS1];
+
+  const int H = a.Hg, W = a.Wg, HW = H * W;
+  const int spi = HW / 64;                                     // K-steps per image
+  const long stot = (long)a.N * spi;
+  const int sps = a.pix_per_split / 64;                        // K-steps per split
+  const int nct = a.Nc / 64, tiles = (a.M / 128) * nct;
+  const int bid = xcd_remap(blockIdx.x, tiles * a.splits);
+  const int split = bid / tiles, tile = bid - split * tiles;   // a split's tiles share an XCD's L2
+  const int mt = tile / nct, ct = tile - mt * nct;
+  const int m0 = mt * 128, ci0 = ct * 64;
+  const long gs0 = (long)split * sps;                          // the split's first K-step
+  const int S = (int)min((long)sps, stot - gs0);
+  const int n0 = (int)(gs0 / spi), ls0 = (int)(gs0 - (long)n0 * spi);
+  const bool do_bias = a.bslab != nullptr && ct == 0;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int cg = wid & 1, jq = wid >> 1, grp = wid >> 2;      // channel group, channel quarter, ping-pong half
+
+  // buffers from the split's first image; per-image tables: the host keeps a split inside one tensor and
+  // passes its extent (abytes / bbytes), else everything up to the batch's end (clamped to 31 bits)
+  const unsigned arec = a.atab ? a.abytes : (unsigned)min((long)(a.N - n0) * HW * a.lda * 2, 0x7fffffffL);
+  const unsigned brec = a.btab ? a.bbytes : (unsigned)min((long)(a.N - n0) * HW * a.ldb * 2, 0x7fffffffL);
+  const __amdgpu_buffer_rsrc_t ar = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(a.atab ? a.atab[n0] : a.A + (long)n0 * HW * a.lda), 0, (int)arec, 0x00020000);
+  const __amdgpu_buffer_rsrc_t br = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(a.btab ? a.btab[n0] : a.B + (long)n0 * HW * a.ldb), 0, (int)brec, 0x00020000);
+
+  // ---- DMA constants.  A: [64 px][128 ch], 16 instructions of 1 KB (4 pixel rows x 16 chunks); wave w
+  // issues instruction kk*8 + w of half kk; lane l: pixel row 4 ins + (l >> 4), slot l & 15 <- chunk
+  // (l & 15) ^ swz_kk<256>(row).
+  const int arow = 4 * wid + (lane >> 4);
+  const unsigned laneA = (unsigned)((arow * a.lda + m0 + (((lane & 15) ^ swz_kk<A1_RB>(arow)) * 8)) * 2);
+  const unsigned stepA = (unsigned)(64 * a.lda * 2), halfA = (unsigned)(32 * a.lda * 2);
+  // B: band row r, 8-pixel block ib (instruction i = 9 r + ib); lane l: band pixel c = 8 ib + (l >> 3), slot
+  // l & 7 <- chunk (l & 7) ^ swz_kk<128>(LDS row); source relative to the K-step's first pixel (h0, w0)
+  int laneB[NBI1], bDst[NBI1], bRow[NBI1], bCol[NBI1];
+#pragma unroll
+  for (int jj = 0; jj < NBI1; ++jj) {
+    const int i = wid + 8 * jj;
+    const bool real = i < 27;
+    const int r = real ? i / 9 : 0, ib = real ? i - 9 * r : 0;
+    const int c = 8 * ib + (lane >> 3);
+    const int lr = r * B1_SP + c;
+    laneB[jj] = (((r - 1) * W + (c - 1)) * a.ldb + ci0 + (((lane & 7) ^ swz_kk<B1_RB>(lr)) * 8)) * 2;
+    bDst[jj] = real ? A1_BYTES + (r * B1_SP + 8 * ib) * B1_RB : -1;
+    bRow[jj] = r;
+    bCol[jj] = 8 * ib - 1;                                     // + (lane >> 3): image column - w0
+  }
+  const int l3 = lane >> 3;
+  const unsigned stepB = (unsigned)(64 * a.ldb * 2);
+
+  auto issueA = [&](int kk, int bf, int s, int lsq) {          // lsq: K-step index relative to image n0
+    const bool ok = s < S;
+    dma16(ar, lds + bf * S1 + kk * (A1_BYTES / 2) + wid * 1024,
+          ok ? (unsigned)lsq * stepA + laneA + (unsigned)kk * halfA : 0x80000000u);
+  };
+  auto issueB = [&](int bf, int s, int lsq, int h0, int w0) {
+#pragma unroll
+    for (int jj = 0; jj < NBI1; ++jj) {
+      const int h = h0 - 1 + bRow[jj], w = w0 + bCol[jj] + l3;
+      const bool ok = s < S && bDst[jj] >= 0 && h >= 0 && h < H && w >= 0 && w < W;
+      const int o = (int)((unsigned)lsq * stepB) + laneB[jj];
+      dma16(br, bDst[jj] >= 0 ? lds + bf * S1 + bDst[jj] : lds + NBUF * S1, ok ? (unsigned)o : 0x80000000u);
+    }
+  };
+  // image row / column of the K-step ls (relative to image n0)
+  auto coords = [&](int ls, int& h0, int& w0) {
+    const int t = ls % spi;
+    h0 = (t * 64) / W;
+    w0 = t * 64 - h0 * W;
+  };
+
+  int h0, w0;
+  coords(ls0, h0, w0);
+  issueA(0, 0, 0, ls0);
+  issueA(1, 0, 0, ls0);
+  issueB(0, 0, ls0, h0, w0);
+  coords(ls0 + 1, h0, w0);
+  issueA(0, 1, 1, ls0 + 1);
+  issueA(1, 1, 1, ls0 + 1);
+  issueB(1, 1, ls0 + 1, h0, w0);
+  wait_vm<2 + NBI1>();                                         // step 0 landed (step 1 may be in flight)
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  if (grp) __builtin_amdgcn_s_barrier();                       // the second half runs one barrier behind
+  __builtin_amdgcn_sched_barrier(0);
+
+  // fragment read offsets (tr_frag addressing; lane (g, q, p) reads k rows 8g + q + 4h, 4 columns at 4p):
+  // A fragment 0 of the wave's 64 channels (fragment ic: ^ ic * 32); B with the wave's quarter folded in
+  const unsigned lds0 = (unsigned)(size_t)LDS_PTR(char, lds);
+  unsigned aoff[2], boff[3][2];
+  {
+    const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int r = 8 * g + q + 4 * h;
+      const int col = cg * 64 + 4 * p;
+      aoff[h] = (unsigned)(r * A1_RB + (((col >> 3) ^ swz_kk<A1_RB>(r)) << 4) + (col & 7) * 2);
+#pragma unroll
+      for (int kw = 0; kw < 3; ++kw) {
+        const int rr = r + kw, cb = jq * 16 + 4 * p;         // band rows start at multiples of 16 LDS rows
+        boff[kw][h] = (unsigned)(A1_BYTES + rr * B1_RB + (((cb >> 3) ^ swz_kk<B1_RB>(rr)) << 4) + (cb & 7) * 2);
+      }
+    }
+  }
+
+  typedef __attribute__((ext_vector_type(8))) short s16x8_t;
+  const s16x8_t ones_s = {0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80};   // bf16 1.0
+  const bf16x8_t ones = __builtin_bit_cast(bf16x8_t, ones_s);
+
+  f32x4_t acc[4][9];
+#pragma unroll
+  for (int ic = 0; ic < 4; ++ic)
+#pragma unroll
+    for (int f = 0; f < 9; ++f) acc[ic][f] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  f32x4_t bacc[2] = {f32x4_t{0.f, 0.f, 0.f, 0.f}, f32x4_t{0.f, 0.f, 0.f, 0.f}};
+  s16x4_t ra[4][2], rb[9][2];
+
+  auto reads = [&](unsigned stage, auto KKc) {
+    constexpr int KK = decltype(KKc)::value;
+#define DPA_BAND1_B(f)                                                                         \
+  {                                                                                            \
+    constexpr int kh = (f) / 3, kw = (f) % 3;                                                  \
+    constexpr int O = (kh * B1_SP + KK * 32) * B1_RB;                                          \
+    rb[f][0] = trld<O>(boff[kw][0] + stage);                                                   \
+    rb[f][1] = trld<O>(boff[kw][1] + stage);                                                   \
+  }
+    DPA_BAND1_B(0) DPA_BAND1_B(1) DPA_BAND1_B(2) DPA_BAND1_B(3) DPA_BAND1_B(4)
+    DPA_BAND1_B(5) DPA_BAND1_B(6) DPA_BAND1_B(7) DPA_BAND1_B(8)
+#undef DPA_BAND1_B
+    constexpr int OA = KK * 32 * A1_RB;
+    const unsigned a0 = aoff[0] + stage, a1 = aoff[1] + stage;
+#pragma unroll
+    for (int ic = 0; ic < 4; ++ic) {
+      ra[ic][0] = trld<OA>(a0 ^ (ic * 32u));
+      ra[ic][1] = trld<OA>(a1 ^ (ic * 32u));
+    }
+  };
+  auto mfmas = [&]() {
+    bf16x8_t af[4];
+#pragma unroll
+    for (int ic = 0; ic < 4; ++ic) af[ic] = tr_join(ra[ic][0], ra[ic][1]);
+#pragma unroll
+    for (int f = 0; f < 9; ++f) {
+      const bf16x8_t bf = tr_join(rb[f][0], rb[f][1]);
+#pragma unroll
+      for (int ic = 0; ic < 4; ++ic)
+        acc[ic][f] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ic], bf, acc[ic][f], 0, 0, 0);
+    }
+    if (do_bias) {                                             // quarters 0 / 1 sum fragments 0-1 / 2-3
+      if (jq == 0) {
+        bacc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0], ones, bacc[0], 0, 0, 0);
+        bacc[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1], ones, bacc[1], 0, 0, 0);
+      } else if (jq == 1) {
+        bacc[0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[2], ones, bacc[0], 0, 0, 0);
+        bacc[1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[3], ones, bacc[1], 0, 0, 0);
+      }
+    }
+  };
+  auto sync_in = [&]() {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+  };
+  auto sync_out = [&]() {
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  int lsq = ls0 + 2;                                           // the step being issued (s + 2), rel. to image n0
+  coords(lsq, h0, w0);
+  int cur = 0, iss = 2;
+  for (int s = 0; s < S; ++s) {
+    const unsigned stage = lds0 + (unsigned)(cur * S1);
+    reads(stage, std::integral_constant<int, 0>{});
+    issueA(0, iss, s + 2, lsq);
+    sync_in();
+    mfmas();
+    sync_out();
+    reads(stage, std::integral_constant<int, 1>{});
+    issueA(1, iss, s + 2, lsq);
+    issueB(iss, s + 2, lsq, h0, w0);
+    wait_vm<2 + NBI1>();                                       // A(s + 1), B(s + 1) of this wave landed
+    sync_in();
+    mfmas();
+    sync_out();
+    cur = cur == NBUF - 1 ? 0 : cur + 1;
+    iss = iss == NBUF - 1 ? 0 : iss + 1;
+    ++lsq;
+    w0 += 64;
+    if (w0 == W) {
+      w0 = 0;
+      if (++h0 == H) h0 = 0;
+    }
+  }
+  wait_vm<0>();                                                // no DMA may land after the workgroup ends
+  if (!grp) __builtin_amdgcn_s_barrier();                      // balance the second half's extra barrier
+
+  // ---- epilogue: acc[ic][f]: co = m0 + cg*64 + ic*16 + 4 (lane >> 4) + r, tap f, ci = ci0 + jq*16 + (lane & 15)
+  const int ci = ci0 + jq * 16 + (lane & 15);
+#pragma unroll
+  for (int f = 0; f < 9; ++f) {
+    float* dst = a.slab + (((long)split * 9 + f) * a.M + m0 + cg * 64 + 4 * (lane >> 4)) * a.Nc + ci;
+#pragma unroll
+    for (int ic = 0; ic < 4; ++ic)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) dst[(long)(ic * 16 + r) * a.Nc] = acc[ic][f][r];
+  }
+  if (do_bias && jq < 2 && (lane & 15) == 0) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        a.bslab[(long)split * a.M + m0 + cg * 64 + (2 * jq + i) * 16 + 4 * (lane >> 4) + r] = bacc[i][r];
+  }
+}
+
 // Eligible: conv3x3 s1 p1 (A = the output gradient, B = the layer input, same pixel grid), W in {32, 64},
 // H % (64 / W) == 0, M % 256 == 0, Nc % 32 == 0, 16-B aligned channel strides; per-image tables as
 // wgrad_gemm.hip (every split's images consecutive images of one tensor); pix_per_split = images per split
@@ -322,5 +567,25 @@ DPA_API int dpa_wgrad_band(const WgradArgs* args, hipStream_t st) {
     hipLaunchKernelGGL(wgrad_band_kernel<64>, dim3(tiles * a.splits), dim3(512), 0, st, a);
   else
     hipLaunchKernelGGL(wgrad_band_kernel<32>, dim3(tiles * a.splits), dim3(512), 0, st, a);
+  return (int)hipGetLastError();
+}
+
+// Eligible: conv3x3 s1 p1 on one grid, W % 64 == 0, M % 128 == 0, Nc % 64 == 0, 16-B aligned channel strides;
+// pix_per_split = pixels per split (a positive multiple of 64), splits = ceil(N H W / pix_per_split); a split's
+// span from its first image addressable with 32-bit offsets; per-image tables: whole-image splits
+// (pix_per_split % (H W) == 0) inside one tensor, abytes / bbytes = a split's extent.
+DPA_API int dpa_wgrad_band128(const WgradArgs* args, hipStream_t st) {
+  const WgradArgs& a = *args;
+  const long HW = (long)a.Hg * a.Wg, pps = a.pix_per_split;
+  if ((a.M % 128) || a.M < 128 || (a.Nc % 64) || a.Nc < 64 || (a.lda & 7) || (a.ldb & 7) || a.s != 1 ||
+      a.pad != 1 || a.KW != 3 || a.HA != a.Hg || a.WA != a.Wg || a.HB != a.Hg || a.WB != a.Wg || a.Wg < 64 ||
+      (a.Wg % 64) || a.Hg < 1 || a.N < 1 || (!a.atab != !a.btab) || pps < 64 || (pps % 64) ||
+      a.splits != ((long)a.N * HW + pps - 1) / pps || a.lda < a.M || a.ldb < a.Nc ||
+      (pps + 2 * HW) * a.lda * 2 >= (1L << 31) || (pps + 2 * HW) * a.ldb * 2 >= (1L << 31))
+    return (int)hipErrorInvalidValue;
+  if (a.atab && ((pps % HW) || pps * a.lda * 2 > (long)a.abytes || pps * a.ldb * 2 > (long)a.bbytes))
+    return (int)hipErrorInvalidValue;
+  const int tiles = (a.M / 128) * (a.Nc / 64);
+  hipLaunchKernelGGL(wgrad_band128_kernel, dim3(tiles * a.splits), dim3(512), 0, st, a);
   return (int)hipGetLastError();
 }

@@ -407,6 +407,9 @@ def wgrad(A: torch.Tensor, B: torch.Tensor, *, kind: int, grid, M: int, Nc: int,
     if (path == "band" or (path == "auto" and wgrad_band_eligible(M, Nc, grid))) and kind == 0 and cfg == 0 \
             and A.shape[1:3] == B.shape[1:3] == tuple(grid[1:]):
         return _wgrad_band(A, B, grid=grid, M=M, Nc=Nc, gw=gw, gb=gb, Nreal=Nreal)
+    if (path == "band128" or (path == "auto" and wgrad_band128_eligible(M, Nc, grid))) and kind == 0 and cfg == 0 \
+            and A.shape[1:3] == B.shape[1:3] == tuple(grid[1:]):
+        return _wgrad_band128(A, B, grid=grid, M=M, Nc=Nc, gw=gw, gb=gb, Nreal=Nreal)
     if (path == "gemm" or (path == "auto" and wgrad_gemm_eligible(M, Nc, grid))) and kind == 0 and cfg == 0 \
             and A.shape[1:3] == B.shape[1:3] == tuple(grid[1:]):
         return _wgrad_gemm(A, B, grid=grid, M=M, Nc=Nc, gw=gw, gb=gb, Nreal=Nreal)
@@ -550,6 +553,69 @@ def wgrad_band_ips(N: int, H: int, W: int, M: int, Nc: int, group: int = 0, cus:
     return best[1]
 
 
+def wgrad_band128_eligible(M: int, Nc: int, grid) -> bool:
+    """The 128-output-channel band kernel (csrc/wgrad_band.hip wgrad_band128_kernel): W % 64 == 0 grids
+    the 256-channel form does not take (the 128^2 level of the UNet)."""
+    N, H, W = grid
+    return (USE_WGRAD_BAND and M % 128 == 0 and Nc % 64 == 0 and W % 64 == 0 and W >= 64
+            and not wgrad_band_eligible(M, Nc, grid))
+
+
+def wgrad_band128_steps(N: int, H: int, W: int, M: int, Nc: int, group: int = 0, cus: int = 256,
+                        min_blocks: int = 512) -> int:
+    """K-steps (64 pixels) per split of a 128-channel band launch: whole images or an image's 1/2 .. 1/32
+    (splits may start inside an image); the cost model of :func:`wgrad_band_ips`.  ``group``: whole-image
+    splits inside ``group``-image tensors."""
+    tiles = (M // 128) * (Nc // 64)
+    spi = H * W // 64
+    total = N * spi
+    cands = {spi * i for i in range(1, N + 1) if not group or group % i == 0}
+    if not group:
+        cands |= {spi // k for k in (2, 4, 8, 16, 32) if spi % k == 0}
+    t_step, bw = 1.6e-6, 4e12
+    best = None
+    for sps in sorted(cands):
+        splits = -(-total // sps)
+        blocks = splits * tiles
+        cost = -(-blocks // cus) * sps * t_step + splits * 9 * M * Nc * 8 / bw
+        key = (blocks < min(min_blocks, total * tiles), cost)
+        if best is None or key < best[0]:
+            best = (key, sps)
+    return best[1]
+
+
+def _wgrad_band128(A, B, *, grid, M, Nc, gw, gb, Nreal, tabs=None, group: int = 0, steps: int = 0):
+    """conv3x3 weight (+bias) gradient of 128-output-channel tiles on W % 64 == 0 grids: one workgroup per
+    (range of 64-pixel K-steps, 128 output channels x 64 input channels x 9 taps); split-K slabs reduced by
+    dpa_wgrad_reduce (same slab layout as :func:`_wgrad_gemm`)."""
+    NA, HA, WA, CA, lda = _nhwc(A, "wgrad_band128.A")
+    NB, HB, WB, CB, ldb = _nhwc(B, "wgrad_band128.B")
+    N, Hg, Wg = grid
+    assert (HA, WA) == (Hg, Wg) == (HB, WB) and CA >= M and CB >= Nc
+    assert (NA == NB == N) or (tabs is not None and tabs[0].numel() == tabs[1].numel() == N and group > 0
+                               and N % group == 0)
+    assert gw.dtype == torch.float32 and gw.is_contiguous() and gw.numel() == M * Nreal * 9
+    HW = Hg * Wg
+    sps = steps or wgrad_band128_steps(N, Hg, Wg, M, Nc, group if tabs is not None else 0)
+    # 32-bit offsets over a split's span from its first image
+    while sps > 1 and (sps * 64 + 2 * HW) * max(lda, ldb) * 2 >= 2 ** 31:
+        sps = sps - HW // 64 if sps > HW // 64 else sps // 2
+    pps = sps * 64
+    splits = -(-N * HW // pps)
+    slab = torch.empty(splits * 9 * M * Nc + splits * M, dtype=torch.float32, device=A.device)
+    bslab = slab[splits * 9 * M * Nc:] if gb is not None else None
+    a = WgradArgs(A.data_ptr(), B.data_ptr(), slab.data_ptr(), None if bslab is None else bslab.data_ptr(), lda, ldb,
+                  N, Hg, Wg, HA, WA, HB, WB, M, Nc, 1, 1, 3, pps, splits, pps * lda * 2, pps * ldb * 2)
+    if tabs is not None:
+        assert pps % HW == 0 and group % (pps // HW) == 0
+        a.atab, a.btab = tabs[0].data_ptr(), tabs[1].data_ptr()
+    L = _lib.lib()
+    st = _stream(A)
+    _check(L.dpa_wgrad_band128(ctypes.byref(a), st), "wgrad_band128")
+    _check(L.dpa_wgrad_reduce(_p(slab), _p(bslab), _p(gw), _p(gb), c_int(splits), c_int(9), c_int(M), c_int(Nc),
+                              c_int(Nreal), c_int(0), st), "wgrad_reduce(band128)")
+
+
 def _wgrad_band(A, B, *, grid, M, Nc, gw, gb, Nreal, tabs=None, group: int = 0, ips: int = 0):
     """conv3x3 weight (+bias) gradient of the deep layers (64^2 / 32^2 grids, Cout % 256 == 0): one
     workgroup per (group of images, 256 output channels x 32 input channels x 9 taps); split-K slabs over
@@ -610,6 +676,9 @@ def wgrad_multi(As, Bs, *, M: int, Nc: int, gw: torch.Tensor, gb: Optional[torch
     if wgrad_band_eligible(M, Nc, (N, H, W)) and len(sizes) == 1:
         return _wgrad_band(As[0], Bs[0], grid=(N, H, W), M=M, Nc=Nc, gw=gw, gb=gb, Nreal=Nreal, tabs=tabs,
                            group=sizes.pop())
+    if wgrad_band128_eligible(M, Nc, (N, H, W)) and len(sizes) == 1:
+        return _wgrad_band128(As[0], Bs[0], grid=(N, H, W), M=M, Nc=Nc, gw=gw, gb=gb, Nreal=Nreal, tabs=tabs,
+                              group=sizes.pop())
     if wgrad_gemm_eligible(M, Nc, (N, H, W)) and len(sizes) == 1 and min(sizes) * (H * W // 64) >= 64:
         return _wgrad_gemm(As[0], Bs[0], grid=(N, H, W), M=M, Nc=Nc, gw=gw, gb=gb, Nreal=Nreal, tabs=tabs,
                            group=sizes.pop())

@@ -227,7 +227,10 @@ def test_deconv_dgrad_from_concat(hip_lib, N, h, w, Cin, Cout):
     # deep layers with the input band staged once for all 9 taps (csrc/wgrad_band.hip): 64-wide rows (one row
     # per K-step), 32-wide rows (two), several channel and output-channel tiles, one-image batches
     (2, 4, 64, 128, 256, None, "band"), (3, 6, 32, 256, 256, None, "band"), (2, 5, 64, 512, 256, None, "band"),
-    (1, 2, 32, 64, 512, None, "band"), (3, 2, 64, 32, 256, None, "band"), (1, 1, 64, 32, 256, None, "band")])
+    (1, 2, 32, 64, 512, None, "band"), (3, 2, 64, 32, 256, None, "band"), (1, 1, 64, 32, 256, None, "band"),
+    # its 128-output-channel form (W % 64 == 0: K-steps are 64-pixel strips of one row, real halo columns)
+    (2, 4, 128, 64, 128, None, "band128"), (1, 3, 192, 128, 128, None, "band128"), (2, 2, 64, 256, 128, None, "band128"),
+    (1, 5, 128, 64, 256, None, "band128"), (2, 1, 64, 64, 128, None, "band128")])
 def test_conv3x3_wgrad(hip_lib, N, H, W, Cin, Cout, cin_pad, path):
     from distributedpytorch_amd.ops import kernels as K
     torch.manual_seed(4)
@@ -732,6 +735,29 @@ def test_wgrad_band_real_shapes(hip_lib, N, H, W, Cin, Cout, ips):
     assert _rel(gw.view(Cout, Cin, 3, 3), ref) < 1e-4
     assert _rel(gb, bref) < 1e-4
     assert _rel(gw, gw2) < 1e-5 and _rel(gb, gb2) < 1e-5
+
+
+@pytest.mark.parametrize("N,H,W,Cin,Cout,steps", [
+    (8, 128, 128, 64, 128, 0), (8, 128, 128, 128, 128, 16), (8, 128, 128, 256, 128, 256), (3, 128, 128, 128, 128, 96),
+    (4, 64, 64, 128, 128, 0), (2, 256, 256, 64, 128, 0)])
+def test_wgrad_band128_real_shapes(hip_lib, N, H, W, Cin, Cout, steps):
+    """csrc/wgrad_band.hip's 128-channel kernel at the UNet's 128^2 layer shapes (64/128/256 -> 128) with
+    splits of whole images, of part of an image (16 K-steps = 8 rows) and straddling images (96 K-steps of
+    256): fp32-anchored (nine shifted fp32 GEMMs on the same bf16 operands)."""
+    from distributedpytorch_amd.ops import kernels as K
+    torch.manual_seed(29)
+    x = torch.randn(N, Cin, H, W, device="cuda").to(torch.bfloat16)
+    g = torch.randn(N, Cout, H, W, device="cuda").to(torch.bfloat16)
+    xh, gh = x.permute(0, 2, 3, 1).contiguous(), g.permute(0, 2, 3, 1).contiguous()
+    xp = F.pad(xh.float(), (0, 0, 1, 1, 1, 1))
+    g2 = gh.float().reshape(-1, Cout).t()
+    ref = torch.stack([g2 @ xp[:, kh:kh + H, kw:kw + W].reshape(-1, Cin) for kh in range(3) for kw in range(3)], -1)
+    gw = torch.zeros(Cout * Cin * 9, device="cuda")
+    gb = torch.zeros(Cout, device="cuda")
+    K._wgrad_band128(gh, xh, grid=(N, H, W), M=Cout, Nc=Cin, gw=gw, gb=gb, Nreal=Cin, steps=steps)
+    torch.cuda.synchronize()
+    assert _rel(gw.view(Cout, Cin, 9), ref) < 1e-4
+    assert _rel(gb, g2.sum(1)) < 1e-4
 
 
 @pytest.mark.parametrize("M,Nc,H,W,mb,nmb", [(256, 256, 4, 64, 3, 3), (256, 128, 3, 32, 2, 4), (512, 64, 2, 64, 4, 2),

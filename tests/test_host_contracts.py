@@ -50,7 +50,7 @@ def _wgrad_args(**kw):
 def test_library_exports_and_version(L):
     assert L.dpa_version() > 0
     for name in ("dpa_igemm", "dpa_igemm_glds", "dpa_igemm_halo", "dpa_igemm_stream", "dpa_wgrad", "dpa_wgrad_halo",
-                 "dpa_wgrad_stream", "dpa_wgrad_gemm", "dpa_wgrad_band", "dpa_wgrad_reduce", "dpa_deconv_fwd", "dpa_deconv_bwd", "dpa_maxpool2",
+                 "dpa_wgrad_stream", "dpa_wgrad_gemm", "dpa_wgrad_band", "dpa_wgrad_band128", "dpa_wgrad_reduce", "dpa_deconv_fwd", "dpa_deconv_bwd", "dpa_maxpool2",
                  "dpa_pool_bwd", "dpa_pool_bwd_code", "dpa_head_fwd", "dpa_head_bwd", "dpa_bn_fwd", "dpa_bn_bwd",
                  "dpa_up2_fwd", "dpa_up2_bwd", "dpa_adam_flat", "dpa_adam_flat_dev", "dpa_pack_weights",
                  "dpa_slab_fold", "dpa_loss_finish", "dpa_loss_grad"):
@@ -196,6 +196,22 @@ def test_wgrad_band_rejects(L, kw):
     assert L.dpa_wgrad_band(ctypes.byref(_wgrad_args(**one_step)), None) != INVALID
     base.update(kw)
     assert L.dpa_wgrad_band(ctypes.byref(_wgrad_args(**base)), None) == INVALID
+
+
+@pytest.mark.parametrize("kw", [dict(M=64, lda=64), dict(Nc=32, ldb=32), dict(Wg=96, WA=96, WB=96), dict(KW=2),
+                                dict(HB=32), dict(splits=2), dict(pix_per_split=96), dict(pix_per_split=0),
+                                dict(lda=132), dict(atab=1), dict(atab=1, btab=1, pix_per_split=64 * 32)])
+def test_wgrad_band128_rejects(L, kw):
+    """csrc/wgrad_band.hip 128-channel form: M % 128, Nc % 64, W % 64, 3x3 s1 p1 on one grid, pixels per
+    split a multiple of 64 and splits = ceil(N H W / it), both or neither per-image table, whole-image splits
+    with tables."""
+    base = dict(M=128, Nc=64, lda=128, ldb=64, pix_per_split=64 * 64, splits=1, Hg=64, Wg=64, HA=64, WA=64,
+                HB=64, WB=64)
+    assert L.dpa_wgrad_band128(ctypes.byref(_wgrad_args(**base)), None) != INVALID     # the valid case passes
+    assert L.dpa_wgrad_band128(ctypes.byref(_wgrad_args(**dict(base, pix_per_split=64 * 16, splits=4))),
+                               None) != INVALID                                         # splits inside an image
+    base.update(kw)
+    assert L.dpa_wgrad_band128(ctypes.byref(_wgrad_args(**base)), None) == INVALID
 
 
 def test_elementwise_launchers_reject(L):
