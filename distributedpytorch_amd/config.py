@@ -123,7 +123,9 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--profile", action="store_true", help="torch.profiler trace of a few steps")
     p.add_argument("--trace-ranges", action="store_true",
                    help="roctx ranges around blocks, pipeline transfers and all-reduce buckets (rocprofv3 --marker-trace)")
-    p.add_argument("--cuda-graph", action="store_true", help="capture the training step in a HIP graph")
+    p.add_argument("--cuda-graph", action="store_true",
+                   help="capture the training step in a HIP graph (singleGPU: the whole step; -t DP: each "
+                        "replica's forward and backward)")
     p.add_argument("--debug-sync", action="store_true",
                    help="synchronise after every HIP kernel and pipeline stage op (race / fault triage)")
     p.add_argument("--watchdog", type=float, default=0.0,

@@ -123,6 +123,7 @@ RUNTIME_ENV = {
     "DPA_SAME_DEVICE": "multi-rank rehearsal: every rank on cuda:0 (tests, one-GPU boxes)",
     "DPA_DIST_BACKEND": "process-group backend override (gloo for the one-GPU rehearsal)",
     "DPA_DP_NATIVE_COMM": "-t DP: the native single-process RCCL clique (=0: torch collectives)",
+    "DPA_DP_REPLICAS": "-t DP rehearsal: this many replicas over the visible GPUs round-robin (one-GPU boxes)",
     "DPA_ARCH": "tools/build_hip.py: --offload-arch (default gfx950)",
 }
 

@@ -70,8 +70,8 @@ class ReplicatedDataParallel:
     def _parallel(self, fn, args_per_dev):
         if len(self.devices) == 1 or not self.devices[0].type == "cuda":
             return [fn(i, *a) for i, a in enumerate(args_per_dev)]
-        out = [None] * len(self.devices)
-        err = [None] * len(self.devices)
+        out = [None] * len(args_per_dev)
+        err = [None] * len(args_per_dev)
 
         def run(i, a):
             try:
@@ -91,12 +91,18 @@ class ReplicatedDataParallel:
         return out
 
     def scatter(self, x: torch.Tensor) -> List[torch.Tensor]:
+        """torch.nn.DataParallel's split: ceil(B / n) images per replica, so a batch smaller than the
+        replica count (a short last or validation batch) feeds only the first replicas."""
         chunks = x.chunk(len(self.devices), dim=0)
-        assert len(chunks) == len(self.devices), "batch smaller than the number of devices"
         return [c.to(d, non_blocking=True) for c, d in zip(chunks, self.devices)]
 
     def forward_loss(self, images: torch.Tensor, targets: torch.Tensor, dice: bool = True):
         xs, ts = self.scatter(images), self.scatter(targets)
+        if len(xs) < len(self.devices) and self.reducer is not None and torch.is_grad_enabled():
+            # replicas without images this step: their (zeroed) gradients are final now
+            for k in range(len(xs), len(self.devices)):
+                for i in range(len(self.spaces[k].numels)):
+                    self.reducer.mark_ready(i, k)
         parts = self._parallel(lambda i, x, t: self.computes[i].forward_partials(x, t), list(zip(xs, ts)))
         d0 = self.devices[0]
         S = sum(p.to(d0) for p in parts)

@@ -440,6 +440,9 @@ def build_strategy(cfg: TrainConfig, model) -> Strategy:
         return SingleDevice(cfg, model, dev)
     if m == "DP":
         devs = _devices_for(cfg)
+        reps = int(os.environ.get("DPA_DP_REPLICAS", "0") or 0)
+        if reps > 0:                  # rehearsal: replicas round-robin over the visible devices
+            devs = [devs[i % len(devs)] for i in range(reps)]
         if torch.cuda.is_available():
             assert len(devs) >= 2, f"Requires at least 2 GPUs to run, but got {len(devs)}"
         return DPStrategy(cfg, model, devs)
@@ -547,7 +550,9 @@ def train(cfg: TrainConfig):
     guard = ShutdownGuard()
     dog = StepWatchdog(cfg.watchdog) if cfg.watchdog > 0 else None
     graphed = None
-    if cfg.cuda_graph and not GraphedStep.supported(strat):
+    # --cuda-graph: the whole singleGPU step, or every -t DP replica's forward / backward (GraphedDP)
+    graph_cls = next((c for c in (GraphedStep, GraphedDP) if c.supported(strat)), None)
+    if cfg.cuda_graph and graph_cls is None:
         log.warning(f"--cuda-graph: not supported for {strat.name} on {strat.device}; running eagerly")
     stop_signal = None
     for epoch in range(start_epoch, cfg.epochs):
@@ -560,8 +565,8 @@ def train(cfg: TrainConfig):
             steady.tick(images.shape[0])
             if prof is not None:
                 prof.before(step)
-            if cfg.cuda_graph and graphed is None and GraphedStep.supported(strat):
-                graphed = GraphedStep(strat, images, targets)
+            if cfg.cuda_graph and graphed is None and graph_cls is not None:
+                graphed = graph_cls(strat, images, targets)
             if graphed is not None and graphed.matches(images, targets):
                 loss = graphed(images, targets)
             else:
@@ -736,7 +741,9 @@ class GraphedDP:
     BCE - log Dice needs the SUM of all replicas' partial sums before any backward (dL/dS is then the same
     seed for every replica), and the gradient sum runs after the backward graphs as one reduction (the
     native RCCL clique; the bucketed overlap would have to live inside one replica's graph) before Adam.
-    Capture needs one eager warm-up (lazy allocations); it changes no parameter (no optimizer step)."""
+    Capture needs one eager warm-up (lazy allocations); it changes no parameter (no optimizer step).
+    Measured (profiles/session6_graph_reserve_prio_r06.txt, 8 replicas x 8 images on one GPU): host issue
+    46.1 -> 20.3 ms per step, 1370 -> 1827 img/s.  ``train.py -t DP --cuda-graph`` / ``bench.py --graph``."""
 
     @staticmethod
     def supported(strat) -> bool:

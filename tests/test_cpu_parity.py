@@ -144,6 +144,30 @@ def test_dp_strategy_cpu_matches_full_batch():
         assert torch.equal(p, q)
 
 
+@pytest.mark.parametrize("n_img", [1, 2])
+def test_dp_batch_smaller_than_replicas(n_img):
+    """torch.nn.DataParallel semantics for a short batch (a last or validation batch of fewer images than
+    replicas): only the first replicas get images, the idle replicas' zero gradients join the bucketed sum,
+    and the step equals the full-batch reference; eval probabilities cover the batch."""
+    from distributedpytorch_amd.config import TrainConfig
+    from distributedpytorch_amd.trainer import DPStrategy
+    torch.manual_seed(3)
+    a, b = build_model("unet-tiny"), build_model("unet-tiny")
+    b.load_state_dict(a.state_dict())
+    x = torch.rand(n_img, 3, 32, 32)
+    t = (torch.rand(n_img, 1, 32, 32) > 0.5).float()
+    st = DPStrategy(TrainConfig(backend="torch", lr=1e-3, dtype="fp32", bucket_mb=0.002), a, ["cpu"] * 3)
+    l1 = st.train_step(x, t)
+    l2 = _ref_step(b, x, t)
+    assert torch.allclose(l1, l2, atol=1e-6)
+    for (n, p), (_, q) in zip(st.model.named_parameters(), b.named_parameters()):
+        assert torch.allclose(p, q, atol=1e-5), n
+    for r in st.dp.replicas[1:]:
+        for p, q in zip(st.dp.replicas[0].parameters(), r.parameters()):
+            assert torch.equal(p, q)
+    assert st.dp.probs(x).shape[0] == n_img
+
+
 @pytest.mark.parametrize("stages,mb", [(2, 2), (3, 4)])
 def test_local_pipeline_matches_plain_forward(stages, mb):
     """Reference probe7: pipelined forward == plain forward, grads agree."""

@@ -5,6 +5,7 @@ The pipeline splits the batch into microbatches and sums their loss partials on 
 DataParallel); both must match a single-device step of the same batch with the same kernels.
 """
 import gc
+import os
 
 import pytest
 import torch
@@ -127,6 +128,22 @@ def test_graphed_dp_matches_eager_dp(hip_lib, model_name):
     assert float((p1 - p0).abs().max()) <= 1e-6 * float(p0.abs().max())
     for k in b0:
         assert torch.allclose(b1[k].float(), b0[k].float(), rtol=1e-5, atol=1e-6), k
+
+
+def test_train_py_dp_cuda_graph(hip_lib, tmp_path):
+    """``train.py -t DP --cuda-graph`` runs the replicas from captured graphs (trainer.GraphedDP) end to end:
+    training, validation and the checkpoint."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, os.path.join(root, "train.py"), "-t", "DP", "--cuda-graph", "--synthetic",
+           "--synthetic-len", "16", "--img-size", "128", "-e", "1", "-b", "4", "--out-dir", str(tmp_path)]
+    env = dict(os.environ, DPA_DP_REPLICAS="2")           # two replicas on the box's one GPU
+    r = subprocess.run(cmd, cwd=root, capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    logs = "".join(p.read_text() for p in (tmp_path / "logs").glob("*.log"))
+    assert "captured forward + backward graphs" in logs, logs[-2000:]
+    assert list((tmp_path / "checkpoints").glob("*.pth"))
 
 
 def test_train_step_loss_decreases(hip_lib):
