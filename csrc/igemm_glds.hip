@@ -1412,6 +1412,188 @@ __global__ __launch_bounds__(512) void igemm_sl_kernel(IgemmArgs a) {
   else glds_epilogue<TC, TP, WC, WP>(a, acc, M, m0, c0, wc, wp, lane);
 }
 
+// ds_read_b128 as inline asm with an immediate offset (see igemm_slp_kernel)
+template <int OFF = 0>
+__device__ __forceinline__ bf16x8_t lds_read128_i(unsigned addr) {
+  bf16x8_t v;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "n"(OFF) : "memory");
+  return v;
+}
+
+// Slice-staged kernel on the ping-pong schedule (cfg 18's default since round 6; the kernel above stays as
+// DPA_NO_SLPP=1).  Same tile, slice images and fragments as igemm_sl_kernel<EP, 128>, but the K loop is
+// one phase per tap -- 12 fragment reads, then 32 MFMAs per wave -- with the two wave halves one barrier
+// apart (one half issues its MFMAs while the other reads its fragments and issues DMA), instead of three
+// taps per step ending in vmcnt(0) + __syncthreads with every wave waiting at once (35-45 % MFMA,
+// profiles/pmc_b128_512_r05_end.txt).  Weights are staged per tap: a ring of six 8-KB tap buffers, the
+// tap of phase g + 4 issued at phase g (into the buffer phase g - 2 read: two phases, i.e. both halves,
+// past its last read), so each has ~3 phases to land; the next slice's image is issued in slots 1-4 of
+// the 9 phases of the current slice (2 instructions per wave per phase, zero-fill dummies past the
+// image) into the other image buffer.  Every wave issues the same DMA count per phase, so the waits are
+// compile-time vmcnt values (slice loop unrolled by its 9 phases).
+template <int EP>
+__global__ __launch_bounds__(512) void igemm_slp_kernel(IgemmArgs a) {
+  constexpr int BC = 128, TC = 8, TP = 4, WC = 128, WP = 64, BP = 512, RB = 64;
+  constexpr int TAPB = BC * RB;                      // one tap's weights: 8 KB
+  constexpr int PIMG = 49 * 1024;                    // largest (R+2)(W+2) image, whole DMA instructions
+  constexpr int MI = 7;                              // pixel DMA slots per wave per image (8 x 7 >= 49)
+  __shared__ __attribute__((aligned(1024))) char lds[6 * TAPB + 2 * PIMG + 1024];
+  char* const Pimg = lds + 6 * TAPB;
+  char* const dump = lds + 6 * TAPB + 2 * PIMG;
+
+  const int W = a.Wo, H = a.Ho, HW = H * W;
+  const int lw = 31 - __builtin_clz(W);             // W is a power of two (host)
+  const int R = BP >> lw;                            // image rows per tile
+  const int W2 = W + 2;
+  const int NPX = (R + 2) * W2;                      // pixels of the slice image
+  const int NPI = (NPX + 15) >> 4;                   // DMA instructions per image
+  const int M = a.N * HW;
+  const int nct = a.Ngemm / BC, npt = M / BP;
+  const int bid = xcd_remap(blockIdx.x, npt * nct);
+  int pt, ct;
+  glds_tile(bid, npt, nct, pt, ct);
+  const int m0 = pt * BP, c0 = ct * BC;
+  const int img = m0 / HW, r0 = (m0 - img * HW) >> lw;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wp = wid, grp = wid >> 2;
+  const int lq = lane >> 2, lc = lane & 3;
+
+  // tap-weight DMA: 8 instructions of 16 rows; wave w -> rows 16 w + lq
+  const int wrow = 16 * wid + lq;
+  const unsigned wsrc = (unsigned)(((c0 + wrow) * a.Kpad) * 2 + ((lc ^ swz64(wrow)) << 4));
+  // pixel DMA: image instruction i = wid + 8 m covers image pixels 16 i + lq (flattened (R+2) x (W+2))
+  unsigned psrc[MI];
+  unsigned pvalid = 0;
+#pragma unroll
+  for (int m = 0; m < MI; ++m) {
+    const int P = 16 * (wid + 8 * m) + lq;
+    const int rr = P / W2, cc = P - rr * W2;
+    const int row = r0 - 1 + rr, col = cc - 1;
+    const bool ok = P < NPX && row >= 0 && row < H && col >= 0 && col < W;
+    pvalid |= (ok ? 1u : 0u) << m;
+    psrc[m] = (unsigned)((((img * a.Hs + row) * a.Ws + col) * a.ldx) * 2 + ((lc ^ swz64(P)) << 4));
+  }
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, 0, (int)a.xbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc((void*)a.w, 0, 0x7fffffff, 0x00020000);
+
+  const int NSL = a.Cs / 32, NPH = NSL * 9;          // slices, phases (slice-major, then kh, then kw)
+  // the weights of phase g (tap (g % 9) / 3, (g % 9) % 3 of slice g / 9) into ring buffer g % 6
+  auto issueW = [&](int g) {
+    const int sl = g / 9, t = g - 9 * sl;
+    const bool ok = g < NPH;
+    dma16(wrs, lds + (g % 6) * TAPB + wid * 1024, ok ? wsrc + (unsigned)((t * a.Cs + sl * 32) * 2) : 0x80000000u);
+  };
+  // pixel slot m of slice sl's image into image buffer sl & 1 (dummies past the image / the slices)
+  auto issueP = [&](int sl, int m) {
+    const bool real = m < MI && wid + 8 * m < NPI;
+    const int mm = m < MI ? m : 0;
+    const bool ok = real && sl < NSL && ((pvalid >> mm) & 1u);
+    char* dst = real ? Pimg + (sl & 1) * PIMG + (wid + 8 * m) * 1024 : dump;
+    dma16(xr, dst, ok ? psrc[mm] + (unsigned)(sl * 64) : 0x80000000u);
+  };
+
+  // fragment addresses: A row = ic*16 + (lane & 15); B output pixel q -> image pixel base
+  const int chunk = lane >> 4;
+  int pb[TP];
+#pragma unroll
+  for (int ip = 0; ip < TP; ++ip) {
+    const int q = wp * WP + ip * 16 + (lane & 15);
+    pb[ip] = (q >> lw) * W2 + (q & (W - 1));
+  }
+  f32x4_t acc[TC][TP];
+#pragma unroll
+  for (int ic = 0; ic < TC; ++ic)
+#pragma unroll
+    for (int ip = 0; ip < TP; ++ip) acc[ic][ip] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  // prologue: slice 0's image (MI slots) and the weights of phases 0-3
+#pragma unroll
+  for (int m = 0; m < MI; ++m) issueP(0, m);
+  issueW(0);
+  issueW(1);
+  issueW(2);
+  issueW(3);
+  wait_vm<3>();                                      // image 0 and phase 0's weights landed
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  if (grp) __builtin_amdgcn_s_barrier();             // the second half runs one barrier behind
+  __builtin_amdgcn_sched_barrier(0);
+
+  auto sync_in = [&]() {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this phase's fragment reads
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+  };
+  auto sync_out = [&]() {
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  bf16x8_t af[TC], bf[TP];
+  // fragment reads as inline asm: a plain LDS load makes hipcc wait vmcnt(0) first while any LDS-DMA is in
+  // flight (it cannot tell the load from the DMA destination); sync_in waits lgkmcnt(0) itself
+  const unsigned lds0 = (unsigned)(size_t)LDS_PTR(char, lds);
+  const unsigned aoff = (unsigned)((lane & 15) * RB + ((chunk ^ swz64(lane & 15)) << 4));   // + ic * 16 rows
+  // phase Q (compile-time position in the slice) of slice sl
+  auto phase = [&](int sl, auto Qc) {
+    constexpr int Q = decltype(Qc)::value, KH = Q / 3, KW = Q % 3;
+    const int g = 9 * sl + Q;
+    const unsigned wa = lds0 + (unsigned)((g % 6) * TAPB) + aoff;
+    const unsigned pbase = lds0 + (unsigned)(6 * TAPB + (sl & 1) * PIMG);
+#pragma unroll
+    for (int ic = 0; ic < TC; ++ic) af[ic] = lds_read128_i(wa + (unsigned)(ic * 16 * RB));
+    const int poff = KH * W2 + KW;
+#pragma unroll
+    for (int ip = 0; ip < TP; ++ip) {
+      int pq = pb[ip];
+      asm volatile("" : "+v"(pq));                   // per-phase address math (not 36 hoisted registers)
+      const int P = pq + poff;
+      bf[ip] = lds_read128_i(pbase + (unsigned)(P * RB + ((chunk ^ swz64(P)) << 4)));
+    }
+    issueW(g + 4);
+    if constexpr (Q >= 1 && Q <= 4) {
+      issueP(sl + 1, 2 * (Q - 1));
+      issueP(sl + 1, 2 * (Q - 1) + 1);
+    }
+    // outstanding after W(g + 1): W(g + 2 .. g + 4) and the image slots of phases g - 3 .. g
+    constexpr int P0 = (Q >= 1 && Q <= 4) ? 2 : 0, P1 = (Q - 1 >= 1 && Q - 1 <= 4) ? 2 : 0;
+    constexpr int P2 = (Q - 2 >= 1 && Q - 2 <= 4) ? 2 : 0, P3 = (Q - 3 >= 1 && Q - 3 <= 4) ? 2 : 0;
+    wait_vm<3 + P0 + P1 + P2 + P3>();
+    sync_in();
+#pragma unroll
+    for (int ic = 0; ic < TC; ++ic)
+#pragma unroll
+      for (int ip = 0; ip < TP; ++ip)
+        acc[ic][ip] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ic], bf[ip], acc[ic][ip], 0, 0, 0);
+    sync_out();
+  };
+#pragma unroll 1
+  for (int sl = 0; sl < NSL; ++sl) {
+    phase(sl, std::integral_constant<int, 0>{});
+    phase(sl, std::integral_constant<int, 1>{});
+    phase(sl, std::integral_constant<int, 2>{});
+    phase(sl, std::integral_constant<int, 3>{});
+    phase(sl, std::integral_constant<int, 4>{});
+    phase(sl, std::integral_constant<int, 5>{});
+    phase(sl, std::integral_constant<int, 6>{});
+    phase(sl, std::integral_constant<int, 7>{});
+    phase(sl, std::integral_constant<int, 8>{});
+  }
+  wait_vm<0>();                                      // no DMA may land after the workgroup ends
+  if (!grp) __builtin_amdgcn_s_barrier();            // balance the second half's extra barrier
+
+  if constexpr (EP != 0) glds_epilogue_fast<TC, TP, WC, WP, EP>(a, acc, M, m0, c0, 0, wp, lane);
+  else glds_epilogue<TC, TP, WC, WP>(a, acc, M, m0, c0, 0, wp, lane);
+}
+
+static int SL_PINGPONG = 1;         // DPA_NO_SLPP=1 -> 0 (set at library load, ops/_lib.py)
+DPA_API void dpa_igemm_set_slpp(int on) { SL_PINGPONG = on; }
+
 // slice-staged eligible: conv3x3 s1 p1 on one grid, K = 9 Cs unpadded, 32-channel slices, tiles of whole
 // rows of one image: W a power of two in [32, 128] (256-channel form: [32, 64])
 static inline bool sl_ok(const IgemmArgs& a) {
@@ -1550,6 +1732,7 @@ DPA_API int dpa_igemm_glds(const IgemmArgs* args, int cfg, hipStream_t st) {
     case 18: {
       if (!sl_ok(a)) break;
       const int grid = (M / 512) * (a.Ngemm / 128);
+      if (SL_PINGPONG) DPA_EP_LAUNCH(igemm_slp_kernel, grid);
       if (ep == 1) hipLaunchKernelGGL((igemm_sl_kernel<1, 128>), dim3(grid), dim3(512), 0, st, a);
       else if (ep == 2) hipLaunchKernelGGL((igemm_sl_kernel<2, 128>), dim3(grid), dim3(512), 0, st, a);
       else if (ep == 3) hipLaunchKernelGGL((igemm_sl_kernel<3, 128>), dim3(grid), dim3(512), 0, st, a);

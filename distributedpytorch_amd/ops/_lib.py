@@ -68,7 +68,9 @@ def _declare(L):
     L.dpa_bwd_stream_geom.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
     L.dpa_error_string.restype = ctypes.c_char_p
     from .config import KernelConfig
-    L.dpa_wgrad_set_presum(ctypes.c_int(int(KernelConfig.from_env().wgrad_presum)))
+    kc = KernelConfig.from_env()
+    L.dpa_wgrad_set_presum(ctypes.c_int(int(kc.wgrad_presum)))
+    L.dpa_igemm_set_slpp(ctypes.c_int(int(kc.slpp)))
 
 
 def check(err: int, name: str):

@@ -140,3 +140,36 @@ def test_rowblock_generic_epilogue_bitwise(hip_lib, N, H, W, Cs, Ng, kind):
             outs.append(y)
         torch.cuda.synchronize()
         assert torch.equal(outs[0], outs[1]), v
+
+
+@pytest.mark.parametrize("N,H,W,Cs,Ng,kind", [(2, 128, 128, 128, 128, "fwd"), (2, 128, 128, 256, 128, "dgrad"),
+                                               (2, 64, 64, 256, 128, "dgrad"), (3, 32, 32, 64, 128, "fwd"),
+                                               (2, 128, 128, 64, 256, "fwd"), (1, 16, 128, 32, 128, "dgrad")])
+def test_slice_staged_pingpong_bitwise(hip_lib, N, H, W, Cs, Ng, kind):
+    """igemm_slp_kernel (the ping-pong schedule of the slice-staged 128 x 512 tile, one phase per tap) runs
+    the same MFMA sequence on every accumulator as igemm_sl_kernel (three taps per barrier step): bitwise
+    equal outputs, one slice to eight, 4 / 8 / 16 image rows per tile, two channel tiles."""
+    import ctypes
+    from distributedpytorch_amd.ops import _lib
+    from distributedpytorch_amd.ops import kernels as K
+    torch.manual_seed(41)
+    x = torch.randn(N, H, W, Cs, device="cuda").to(torch.bfloat16)
+    w = (torch.randn(Ng, 9 * Cs, device="cuda") / (9 * Cs) ** 0.5).to(torch.bfloat16)
+    extra = (dict(bias=torch.randn(Ng, device="cuda") * 0.1, relu=True) if kind == "fwd" else
+             dict(mask=torch.randn(N, H, W, Ng, device="cuda").to(torch.bfloat16)))
+    L = _lib.lib()
+    outs = []
+    try:
+        for on in (1, 0):
+            L.dpa_igemm_set_slpp(ctypes.c_int(on))
+            y = torch.empty(N, H, W, Ng, device="cuda", dtype=torch.bfloat16)
+            K.igemm(x, w, y, Ngemm=Ng, Kpad=9 * Cs, KH=3, KW=3, stride=1, pad=1, Cs=Cs, out_grid=(N, H, W),
+                    path="glds", variant=SL, **extra)
+            torch.cuda.synchronize()
+            outs.append(y)
+    finally:
+        L.dpa_igemm_set_slpp(ctypes.c_int(int(K.CFG.slpp)))
+    assert torch.equal(outs[0], outs[1])
+    ref = _ref_conv(x.float().cpu().permute(0, 3, 1, 2),
+                    w.float().cpu().view(Ng, 9, Cs).permute(0, 2, 1).reshape(Ng, Cs, 3, 3))
+    assert _rel(outs[0].float().cpu(), _expected(kind, ref, extra)) < 1e-2
