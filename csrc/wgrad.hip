@@ -383,6 +383,9 @@ __global__ __launch_bounds__(256) void wgrad_reduce_tile_kernel(const float* __r
 // so a 2304-element slab is summed by 73 blocks walking 16k rows -- 0.9 ms, latency bound.  Stage 1 sums
 // groups of R consecutive rows IN PLACE into the group's first row (one thread per element, coalesced,
 // (elements / 256) x groups blocks); the reduce kernels then walk every R-th row (rmul).  Fixed order.
+// gridDim.y < groups: each block walks groups blockIdx.y, + gridDim.y, ... (the same per-group sums): beside
+// a busy kernel on the other stream, thousands of 256-thread blocks wait for dispatch far longer than
+// they run (0.44 ms vs 6 us alone for the first conv's slab, profiles/hip_b256_512_summary_r06.txt)
 __global__ __launch_bounds__(256) void wgrad_presum_kernel(float* __restrict__ slab, float* __restrict__ bslab, int splits,
                                                            long tot, int M, int R) {
   const long e = (long)blockIdx.x * 256 + threadIdx.x;
@@ -390,15 +393,20 @@ __global__ __launch_bounds__(256) void wgrad_presum_kernel(float* __restrict__ s
   if (e >= tot + (bslab ? M : 0)) return;
   float* src = isb ? bslab + (e - tot) : slab + e;
   const long stride = isb ? M : tot;
-  const int r0 = blockIdx.y * R, r1 = min(splits, r0 + R);
-  float s = 0.f;
+  const int groups = (splits + R - 1) / R;
+  for (int gi = blockIdx.y; gi < groups; gi += gridDim.y) {
+    const int r0 = gi * R, r1 = min(splits, r0 + R);
+    float s = 0.f;
 #pragma unroll 8
-  for (int k = r0; k < r1; ++k) s += src[(long)k * stride];
-  src[(long)r0 * stride] = s;
+    for (int k = r0; k < r1; ++k) s += src[(long)k * stride];
+    src[(long)r0 * stride] = s;
+  }
 }
 
 static int WGRAD_PRESUM = 1;        // DPA_NO_WGRAD_PRESUM=1 -> 0 (set at library load, ops/_lib.py)
+static int WGRAD_PRESUM_Y = 0;      // DPA_WGRAD_PRESUM_Y: cap on the presum grid's group dimension (0 = one block per group)
 DPA_API void dpa_wgrad_set_presum(int on) { WGRAD_PRESUM = on; }
+DPA_API void dpa_wgrad_set_presum_y(int y) { WGRAD_PRESUM_Y = y; }
 
 // g: -1 auto, 0 the 32-element kernel, > 0 the quad kernel with g split groups, -2 the tiled kernel
 // (tools/kbench_reduce.py).  The slabs are scratch: the presum stage (many splits, few elements) writes them.
@@ -413,7 +421,8 @@ DPA_API int dpa_wgrad_reduce_cfg(const float* slab_in, const float* bslab_in, fl
     constexpr int R = 32;
     const long el = tot + (bslab ? M : 0);
     const unsigned groups = (unsigned)((splits + R - 1) / R);
-    hipLaunchKernelGGL(wgrad_presum_kernel, dim3((unsigned)((el + 255) / 256), groups), dim3(256), 0, st, slab, bslab, splits,
+    const unsigned gy = WGRAD_PRESUM_Y > 0 && (unsigned)WGRAD_PRESUM_Y < groups ? (unsigned)WGRAD_PRESUM_Y : groups;
+    hipLaunchKernelGGL(wgrad_presum_kernel, dim3((unsigned)((el + 255) / 256), gy), dim3(256), 0, st, slab, bslab, splits,
                        tot, M, R);
     splits = (int)groups;
     rmul = R;

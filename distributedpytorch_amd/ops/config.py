@@ -43,6 +43,7 @@ KNOBS = (
     Knob("glds_bn", "DPA_NO_GLDS_BN", True, "BatchNorm partial sums in the row-block GEMM epilogue"),
     Knob("glds_sl", "DPA_NO_GLDS_SL", True, "128-output-channel convs on rows <= 128 px: the slice-staged 128 x 512 GEMM (cfg 18)"),
     Knob("wgrad_gemm", "DPA_NO_WGRAD_GEMM", True, "deep weight gradients as a dense LDS-DMA GEMM (csrc/wgrad_gemm.hip)"),
+    Knob("wgrad_presum_y", "DPA_WGRAD_PRESUM_Y", 0, "cap on the in-place presum grid's group blocks (0 = one block per 32-row group)"),
     Knob("slpp", "DPA_NO_SLPP", True, "128-output-channel slice-staged convs on the ping-pong schedule (csrc/igemm_glds.hip igemm_slp_kernel)"),
     Knob("wgrad_band", "DPA_NO_WGRAD_BAND", True, "deep weight gradients with the input band staged once for all 9 taps (csrc/wgrad_band.hip)"),
     Knob("side_wgrad", "DPA_NO_SIDE_WGRAD", True, "weight gradients on a side HIP stream, overlapping the dgrad chain"),
@@ -158,6 +159,7 @@ class KernelConfig:
     wgrad_gemm: bool = True
     wgrad_band: bool = True
     slpp: bool = True
+    wgrad_presum_y: int = 0
     side_wgrad: bool = True
     fused_head: bool = True
     fused_bn: bool = True
