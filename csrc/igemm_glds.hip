@@ -1431,12 +1431,17 @@ __device__ __forceinline__ bf16x8_t lds_read128_i(unsigned addr) {
 // the 9 phases of the current slice (2 instructions per wave per phase, zero-fill dummies past the
 // image) into the other image buffer.  Every wave issues the same DMA count per phase, so the waits are
 // compile-time vmcnt values (slice loop unrolled by its 9 phases).
-template <int EP>
+template <int EP, int BC>
 __global__ __launch_bounds__(512) void igemm_slp_kernel(IgemmArgs a) {
-  constexpr int BC = 128, TC = 8, TP = 4, WC = 128, WP = 64, BP = 512, RB = 64;
-  constexpr int TAPB = BC * RB;                      // one tap's weights: 8 KB
-  constexpr int PIMG = 49 * 1024;                    // largest (R+2)(W+2) image, whole DMA instructions
-  constexpr int MI = 7;                              // pixel DMA slots per wave per image (8 x 7 >= 49)
+  static_assert(BC == 128 || BC == 256, "channel tile");
+  constexpr int TC = 8, TP = 4, WC = 128, WP = 64, RB = 64;
+  constexpr int NCW = BC / 128, BP = 8 / NCW * WP;   // 1 x 8 waves, 512 pixels / 2 x 4 waves, 256 pixels
+  constexpr int TAPB = BC * RB;                      // one tap's weights: 8 / 16 KB
+  constexpr int NWW = BC / 128;                      // weight DMA instructions per wave per phase
+  // largest (R+2)(W+2) image in whole DMA instructions: 128 channels W <= 128 (R >= 4), 256 channels W <= 64
+  constexpr int PIMG = BC == 128 ? 49 * 1024 : 25 * 1024;
+  constexpr int MI = BC == 128 ? 7 : 4;              // pixel DMA slots per wave per image (8 x MI >= PIMG / 1 KB)
+  constexpr int NPQ = (MI + 1) / 2;                  // phases 1 .. NPQ of a slice issue 2 slots each
   __shared__ __attribute__((aligned(1024))) char lds[6 * TAPB + 2 * PIMG + 1024];
   char* const Pimg = lds + 6 * TAPB;
   char* const dump = lds + 6 * TAPB + 2 * PIMG;
@@ -1456,12 +1461,16 @@ __global__ __launch_bounds__(512) void igemm_slp_kernel(IgemmArgs a) {
   const int img = m0 / HW, r0 = (m0 - img * HW) >> lw;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wp = wid, grp = wid >> 2;
+  const int wc = wid % NCW, wp = wid / NCW, grp = wid >> 2;
   const int lq = lane >> 2, lc = lane & 3;
 
-  // tap-weight DMA: 8 instructions of 16 rows; wave w -> rows 16 w + lq
-  const int wrow = 16 * wid + lq;
-  const unsigned wsrc = (unsigned)(((c0 + wrow) * a.Kpad) * 2 + ((lc ^ swz64(wrow)) << 4));
+  // tap-weight DMA: BC / 16 instructions of 16 rows; wave w -> rows 16 (w + 8 v) + lq
+  unsigned wsrc[NWW];
+#pragma unroll
+  for (int v = 0; v < NWW; ++v) {
+    const int wrow = 16 * (wid + 8 * v) + lq;
+    wsrc[v] = (unsigned)(((c0 + wrow) * a.Kpad) * 2 + ((lc ^ swz64(wrow)) << 4));
+  }
   // pixel DMA: image instruction i = wid + 8 m covers image pixels 16 i + lq (flattened (R+2) x (W+2))
   unsigned psrc[MI];
   unsigned pvalid = 0;
@@ -1482,7 +1491,10 @@ __global__ __launch_bounds__(512) void igemm_slp_kernel(IgemmArgs a) {
   auto issueW = [&](int g) {
     const int sl = g / 9, t = g - 9 * sl;
     const bool ok = g < NPH;
-    dma16(wrs, lds + (g % 6) * TAPB + wid * 1024, ok ? wsrc + (unsigned)((t * a.Cs + sl * 32) * 2) : 0x80000000u);
+#pragma unroll
+    for (int v = 0; v < NWW; ++v)
+      dma16(wrs, lds + (g % 6) * TAPB + (wid + 8 * v) * 1024,
+            ok ? wsrc[v] + (unsigned)((t * a.Cs + sl * 32) * 2) : 0x80000000u);
   };
   // pixel slot m of slice sl's image into image buffer sl & 1 (dummies past the image / the slices)
   auto issueP = [&](int sl, int m) {
@@ -1507,14 +1519,14 @@ __global__ __launch_bounds__(512) void igemm_slp_kernel(IgemmArgs a) {
 #pragma unroll
     for (int ip = 0; ip < TP; ++ip) acc[ic][ip] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  // prologue: slice 0's image (MI slots) and the weights of phases 0-3
+  // prologue: slice 0's image (2 NPQ slots) and the weights of phases 0-3
 #pragma unroll
-  for (int m = 0; m < MI; ++m) issueP(0, m);
+  for (int m = 0; m < 2 * NPQ; ++m) issueP(0, m);
   issueW(0);
   issueW(1);
   issueW(2);
   issueW(3);
-  wait_vm<3>();                                      // image 0 and phase 0's weights landed
+  wait_vm<3 * NWW>();                                // image 0 and phase 0's weights landed
   __builtin_amdgcn_sched_barrier(0);
   __builtin_amdgcn_s_barrier();
   if (grp) __builtin_amdgcn_s_barrier();             // the second half runs one barrier behind
@@ -1538,7 +1550,7 @@ __global__ __launch_bounds__(512) void igemm_slp_kernel(IgemmArgs a) {
   // fragment reads as inline asm: a plain LDS load makes hipcc wait vmcnt(0) first while any LDS-DMA is in
   // flight (it cannot tell the load from the DMA destination); sync_in waits lgkmcnt(0) itself
   const unsigned lds0 = (unsigned)(size_t)LDS_PTR(char, lds);
-  const unsigned aoff = (unsigned)((lane & 15) * RB + ((chunk ^ swz64(lane & 15)) << 4));   // + ic * 16 rows
+  const unsigned aoff = (unsigned)((wc * WC + (lane & 15)) * RB + ((chunk ^ swz64(lane & 15)) << 4));   // + ic * 16 rows
   // phase Q (compile-time position in the slice) of slice sl
   auto phase = [&](int sl, auto Qc) {
     constexpr int Q = decltype(Qc)::value, KH = Q / 3, KW = Q % 3;
@@ -1556,14 +1568,14 @@ __global__ __launch_bounds__(512) void igemm_slp_kernel(IgemmArgs a) {
       bf[ip] = lds_read128_i(pbase + (unsigned)(P * RB + ((chunk ^ swz64(P)) << 4)));
     }
     issueW(g + 4);
-    if constexpr (Q >= 1 && Q <= 4) {
+    if constexpr (Q >= 1 && Q <= NPQ) {
       issueP(sl + 1, 2 * (Q - 1));
       issueP(sl + 1, 2 * (Q - 1) + 1);
     }
     // outstanding after W(g + 1): W(g + 2 .. g + 4) and the image slots of phases g - 3 .. g
-    constexpr int P0 = (Q >= 1 && Q <= 4) ? 2 : 0, P1 = (Q - 1 >= 1 && Q - 1 <= 4) ? 2 : 0;
-    constexpr int P2 = (Q - 2 >= 1 && Q - 2 <= 4) ? 2 : 0, P3 = (Q - 3 >= 1 && Q - 3 <= 4) ? 2 : 0;
-    wait_vm<3 + P0 + P1 + P2 + P3>();
+    constexpr int P0 = (Q >= 1 && Q <= NPQ) ? 2 : 0, P1 = (Q - 1 >= 1 && Q - 1 <= NPQ) ? 2 : 0;
+    constexpr int P2 = (Q - 2 >= 1 && Q - 2 <= NPQ) ? 2 : 0, P3 = (Q - 3 >= 1 && Q - 3 <= NPQ) ? 2 : 0;
+    wait_vm<3 * NWW + P0 + P1 + P2 + P3>();
     sync_in();
 #pragma unroll
     for (int ic = 0; ic < TC; ++ic)
@@ -1587,12 +1599,22 @@ __global__ __launch_bounds__(512) void igemm_slp_kernel(IgemmArgs a) {
   wait_vm<0>();                                      // no DMA may land after the workgroup ends
   if (!grp) __builtin_amdgcn_s_barrier();            // balance the second half's extra barrier
 
-  if constexpr (EP != 0) glds_epilogue_fast<TC, TP, WC, WP, EP>(a, acc, M, m0, c0, 0, wp, lane);
-  else glds_epilogue<TC, TP, WC, WP>(a, acc, M, m0, c0, 0, wp, lane);
+  if constexpr (EP != 0) glds_epilogue_fast<TC, TP, WC, WP, EP>(a, acc, M, m0, c0, wc, wp, lane);
+  else glds_epilogue<TC, TP, WC, WP>(a, acc, M, m0, c0, wc, wp, lane);
 }
 
 static int SL_PINGPONG = 1;         // DPA_NO_SLPP=1 -> 0 (set at library load, ops/_lib.py)
+static int SLP256 = 0;              // DPA_SLP256=1: 256-channel convs on W <= 64 take igemm_slp_kernel<EP, 256>
 DPA_API void dpa_igemm_set_slpp(int on) { SL_PINGPONG = on; }
+DPA_API void dpa_igemm_set_slp256(int on) { SLP256 = on; }
+
+// 256-channel slice-staged ping-pong eligible: W in {32, 64}, whole 256-pixel tiles, Cs % 32, unpadded K
+static inline bool slp256_ok(const IgemmArgs& a) {
+  const int W = a.Wo;
+  return a.mode == 0 && a.KH == 3 && a.KW == 3 && a.stride == 1 && a.pad == 1 && a.Hs == a.Ho && a.Ws == a.Wo &&
+         a.Kpad == 9 * a.Cs && (a.Cs % 32) == 0 && a.Ngemm % 256 == 0 && (a.ldx & 7) == 0 && (W == 32 || W == 64) &&
+         ((long)a.Ho * W) % 256 == 0;
+}
 
 // slice-staged eligible: conv3x3 s1 p1 on one grid, K = 9 Cs unpadded, 32-channel slices, tiles of whole
 // rows of one image: W a power of two in [32, 128] (256-channel form: [32, 64])
@@ -1700,6 +1722,15 @@ DPA_API int dpa_igemm_glds(const IgemmArgs* args, int cfg, hipStream_t st) {
   }
   const int ep = no_fast_ep ? 0 : glds_ep_kind(a);
   // launch kernel template K<EP> with the specialised epilogue of this launch
+// the same for K<EP, BCv>
+#define DPA_EP_LAUNCH2(K, BCv, grid)                                                               \
+  do {                                                                                             \
+    if (ep == 1) hipLaunchKernelGGL((K<1, BCv>), dim3(grid), dim3(512), 0, st, a);                 \
+    else if (ep == 2) hipLaunchKernelGGL((K<2, BCv>), dim3(grid), dim3(512), 0, st, a);            \
+    else if (ep == 3) hipLaunchKernelGGL((K<3, BCv>), dim3(grid), dim3(512), 0, st, a);            \
+    else hipLaunchKernelGGL((K<0, BCv>), dim3(grid), dim3(512), 0, st, a);                         \
+    return (int)hipGetLastError();                                                                 \
+  } while (0)
 #define DPA_EP_LAUNCH(K, grid)                                                                     \
   do {                                                                                             \
     if (ep == 1) hipLaunchKernelGGL((K<1>), dim3(grid), dim3(512), 0, st, a);                      \
@@ -1717,6 +1748,7 @@ DPA_API int dpa_igemm_glds(const IgemmArgs* args, int cfg, hipStream_t st) {
     case 14: {
       if (a.Ngemm % 256 || a.Kpad < 128) break;     // the steady loop + peeled tail need S >= 2
       const int grid = ((M + 255) / 256) * (a.Ngemm / 256);
+      if (SLP256 && !no_rowblock && slp256_ok(a)) DPA_EP_LAUNCH2(igemm_slp_kernel, 256, grid);
       if (!no_rowblock && pp2h_ok(a)) DPA_EP_LAUNCH(igemm_pp2h_kernel, grid);
       DPA_EP_LAUNCH(igemm_pp2_kernel, grid);
     }
@@ -1732,7 +1764,7 @@ DPA_API int dpa_igemm_glds(const IgemmArgs* args, int cfg, hipStream_t st) {
     case 18: {
       if (!sl_ok(a)) break;
       const int grid = (M / 512) * (a.Ngemm / 128);
-      if (SL_PINGPONG) DPA_EP_LAUNCH(igemm_slp_kernel, grid);
+      if (SL_PINGPONG) DPA_EP_LAUNCH2(igemm_slp_kernel, 128, grid);
       if (ep == 1) hipLaunchKernelGGL((igemm_sl_kernel<1, 128>), dim3(grid), dim3(512), 0, st, a);
       else if (ep == 2) hipLaunchKernelGGL((igemm_sl_kernel<2, 128>), dim3(grid), dim3(512), 0, st, a);
       else if (ep == 3) hipLaunchKernelGGL((igemm_sl_kernel<3, 128>), dim3(grid), dim3(512), 0, st, a);
@@ -1742,5 +1774,6 @@ DPA_API int dpa_igemm_glds(const IgemmArgs* args, int cfg, hipStream_t st) {
     default: break;
   }
 #undef DPA_EP_LAUNCH
+#undef DPA_EP_LAUNCH2
   return (int)hipErrorInvalidValue;
 }

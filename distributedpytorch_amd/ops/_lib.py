@@ -71,6 +71,7 @@ def _declare(L):
     kc = KernelConfig.from_env()
     L.dpa_wgrad_set_presum(ctypes.c_int(int(kc.wgrad_presum)))
     L.dpa_igemm_set_slpp(ctypes.c_int(int(kc.slpp)))
+    L.dpa_igemm_set_slp256(ctypes.c_int(int(kc.slp256)))
     L.dpa_wgrad_set_presum_y(ctypes.c_int(int(kc.wgrad_presum_y)))
 
 

@@ -44,6 +44,7 @@ KNOBS = (
     Knob("glds_sl", "DPA_NO_GLDS_SL", True, "128-output-channel convs on rows <= 128 px: the slice-staged 128 x 512 GEMM (cfg 18)"),
     Knob("wgrad_gemm", "DPA_NO_WGRAD_GEMM", True, "deep weight gradients as a dense LDS-DMA GEMM (csrc/wgrad_gemm.hip)"),
     Knob("wgrad_presum_y", "DPA_WGRAD_PRESUM_Y", 0, "cap on the in-place presum grid's group blocks (0 = one block per 32-row group)"),
+    Knob("slp256", "DPA_SLP256", False, "256-channel convs on 32/64-wide grids as slice-staged ping-pong (igemm_slp_kernel<EP, 256>) instead of the row-block kernel"),
     Knob("slpp", "DPA_NO_SLPP", True, "128-output-channel slice-staged convs on the ping-pong schedule (csrc/igemm_glds.hip igemm_slp_kernel)"),
     Knob("wgrad_band", "DPA_NO_WGRAD_BAND", True, "deep weight gradients with the input band staged once for all 9 taps (csrc/wgrad_band.hip)"),
     Knob("side_wgrad", "DPA_NO_SIDE_WGRAD", True, "weight gradients on a side HIP stream, overlapping the dgrad chain"),
@@ -159,6 +160,7 @@ class KernelConfig:
     wgrad_gemm: bool = True
     wgrad_band: bool = True
     slpp: bool = True
+    slp256: bool = False
     wgrad_presum_y: int = 0
     side_wgrad: bool = True
     fused_head: bool = True

@@ -173,3 +173,27 @@ def test_slice_staged_pingpong_bitwise(hip_lib, N, H, W, Cs, Ng, kind):
     ref = _ref_conv(x.float().cpu().permute(0, 3, 1, 2),
                     w.float().cpu().view(Ng, 9, Cs).permute(0, 2, 1).reshape(Ng, Cs, 3, 3))
     assert _rel(outs[0].float().cpu(), _expected(kind, ref, extra)) < 1e-2
+
+
+@pytest.mark.parametrize("kind", ["fwd", "dgrad", "split"])
+@pytest.mark.parametrize("shape", [(2, 64, 64, 256, 256), (2, 32, 32, 512, 512), (2, 64, 64, 512, 256),
+                                   (3, 32, 32, 256, 512)])
+def test_slp256_fp32_anchor(hip_lib, shape, kind):
+    """igemm_slp_kernel<EP, 256> (DPA_SLP256: the 256-channel convs of the 64^2 / 32^2 levels as slice-staged
+    ping-pong instead of the row-block kernel) at real layer shapes for the forward, the masked dgrad and the
+    split dgrad epilogues: within bf16 output rounding of the fp32 convolution, like the row-block kernel."""
+    import ctypes
+    from distributedpytorch_amd.ops import _lib
+    from distributedpytorch_amd.ops import kernels as K
+    N, H, W, Cs, Ng = shape
+    x, w, xc, wconv = _operands(N, H, W, Cs, Ng, seed=43 + Cs)
+    exp = _expected(kind, _ref_conv(xc, wconv), _extra(kind, N, H, W, Ng, seed=Cs))
+    L = _lib.lib()
+    try:
+        for on in (1, 0):
+            L.dpa_igemm_set_slp256(ctypes.c_int(on))
+            y, y2, _ = _run(kind, x, w, N, H, W, Cs, Ng, PP2H[256], _extra(kind, N, H, W, Ng, seed=Cs))
+            got = torch.cat([y, y2], dim=3) if kind == "split" else y
+            assert _rel(got.float().cpu(), exp) < 1e-2, (on, kind)
+    finally:
+        L.dpa_igemm_set_slp256(ctypes.c_int(int(K.CFG.slp256)))
