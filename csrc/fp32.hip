@@ -873,45 +873,96 @@ __global__ __launch_bounds__(256) void head_f32_kernel(const float* __restrict__
   if (threadIdx.x < 4) slab[blockIdx.x * 4 + threadIdx.x] = red[threadIdx.x][0];
 }
 
-// head backward: dL/dz per pixel from dS (gradient w.r.t. the four partial sums), torch's BCE backward
-// through the sigmoid (common.h head_dz, shared with the bf16 head kernels); gy[p][c] = dz w[c];
-// per-block partials of sum_p dz y[p][c] (C) and sum_p dz (1) -> slab[block][C + 1]
+// The same head forward with L = C / 4 lanes per pixel, each loading one float4 of the pixel's row: a wave
+// reads 64 / L whole rows per instruction (coalesced 1-KB runs at C = 32) instead of 64 lanes each walking
+// its own row one float at a time (0.41 ms for 2.5 M pixels of 32 channels,
+// profiles/hip_fp32_b4_640x960_summary_r06.txt).  z's channel sum: lane partials, then an xor tree over
+// the pixel's lanes; the loss terms from lane 0 of each pixel (the formulas above).
 template <int C>
-__global__ __launch_bounds__(256) void head_bwd_f32_kernel(const float* __restrict__ y, const float* __restrict__ w,
+__global__ __launch_bounds__(256) void head_f32_vec_kernel(const float* __restrict__ y, const float* __restrict__ w,
                                                            const float* __restrict__ b, const float* __restrict__ t,
-                                                           const float* __restrict__ dS, long P, float* __restrict__ gy,
-                                                           float* __restrict__ slab) {
-  __shared__ float red[256];
-  float acc[C + 1];
+                                                           long P, float* __restrict__ slab, float* __restrict__ probs) {
+  constexpr int L = C / 4, PPB = 256 / L;          // lanes per pixel, pixels per block iteration
+  __shared__ float red[4][256];
+  const int sub = threadIdx.x % L;
+  const f32x4v wv = *reinterpret_cast<const f32x4v*>(w + 4 * sub);
+  const float bb = b[0];
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  for (long i = (long)blockIdx.x * PPB + threadIdx.x / L; i < P; i += (long)gridDim.x * PPB) {
+    const f32x4v v = *reinterpret_cast<const f32x4v*>(y + i * C + 4 * sub);
+    float z = fmaf(wv[3], v[3], fmaf(wv[2], v[2], fmaf(wv[1], v[1], wv[0] * v[0])));
 #pragma unroll
-  for (int c = 0; c <= C; ++c) acc[c] = 0.f;
-  const float d0 = dS[0], d1 = dS[1], d2 = dS[2];
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < P; i += (long)gridDim.x * blockDim.x) {
-    float z = b[0];
+    for (int o = L / 2; o > 0; o >>= 1) z += __shfl_xor(z, o, 64);
+    z += bb;
+    if (sub == 0) {
+      const float p = 1.f / (1.f + expf(-z));
+      if (probs) probs[i] = p;
+      if (t) {
+        const float tt = t[i];
+        const float lp = fmaxf(logf(p), -100.f), l1p = fmaxf(logf(1.f - p), -100.f);
+        s0 += -(tt * lp + (1.f - tt) * l1p);
+        const float one = tt == 1.f ? 1.f : 0.f;
+        s1 += p * one;
+        s2 += p;
+        s3 += one;
+      }
+    }
+  }
+  if (!t) return;
+  red[0][threadIdx.x] = s0; red[1][threadIdx.x] = s1; red[2][threadIdx.x] = s2; red[3][threadIdx.x] = s3;
+  __syncthreads();
+  for (int k = 128; k > 0; k >>= 1) {
+    if ((int)threadIdx.x < k)
 #pragma unroll
-    for (int c = 0; c < C; ++c) z = fmaf(w[c], y[i * C + c], z);
+      for (int j = 0; j < 4; ++j) red[j][threadIdx.x] += red[j][threadIdx.x + k];
+    __syncthreads();
+  }
+  if (threadIdx.x < 4) slab[blockIdx.x * 4 + threadIdx.x] = red[threadIdx.x][0];
+}
+
+// head backward: dL/dz per pixel from dS (gradient w.r.t. the four partial sums), torch's BCE backward through
+// the sigmoid (common.h head_dz, shared with the bf16 head kernels); gy[p][c] = dz w[c]; per-block partials of
+// sum_p dz y[p][c] (C) and sum_p dz (1) -> slab[block][C + 1].  L = C / 4 lanes per pixel (float4 loads of y
+// and stores of gy, as above); every lane
+// of a pixel forms dz itself; channel partials of dz y in the 4 channels a lane owns, reduced per block in
+// LDS in a fixed order (rows = the block's pixel slots), the bias partial (dz) from lane 0 of each pixel.
+template <int C>
+__global__ __launch_bounds__(256) void head_bwd_f32_vec_kernel(const float* __restrict__ y, const float* __restrict__ w,
+                                                               const float* __restrict__ b, const float* __restrict__ t,
+                                                               const float* __restrict__ dS, long P, float* __restrict__ gy,
+                                                               float* __restrict__ slab) {
+  constexpr int L = C / 4, PPB = 256 / L;
+  __shared__ float red[PPB][C + 1];
+  const int sub = threadIdx.x % L, slot = threadIdx.x / L;
+  const f32x4v wv = *reinterpret_cast<const f32x4v*>(w + 4 * sub);
+  const float bb = b[0], d0 = dS[0], d1 = dS[1], d2 = dS[2];
+  f32x4v acc = f32x4v{0.f, 0.f, 0.f, 0.f};
+  float accb = 0.f;
+  for (long i = (long)blockIdx.x * PPB + slot; i < P; i += (long)gridDim.x * PPB) {
+    const f32x4v v = *reinterpret_cast<const f32x4v*>(y + i * C + 4 * sub);
+    float z = fmaf(wv[3], v[3], fmaf(wv[2], v[2], fmaf(wv[1], v[1], wv[0] * v[0])));
+#pragma unroll
+    for (int o = L / 2; o > 0; o >>= 1) z += __shfl_xor(z, o, 64);
+    z += bb;
     const float p = 1.f / (1.f + expf(-z));
     const float tt = t[i];
     const float dz = head_dz(p, tt, tt == 1.f ? 1.f : 0.f, d0, d1, d2);
+    *reinterpret_cast<f32x4v*>(gy + i * C + 4 * sub) = dz * wv;
 #pragma unroll
-    for (int c = 0; c < C; ++c) {
-      gy[i * C + c] = dz * w[c];
-      acc[c] = fmaf(dz, y[i * C + c], acc[c]);
-    }
-    acc[C] += dz;
+    for (int r = 0; r < 4; ++r) acc[r] = fmaf(dz, v[r], acc[r]);
+    accb += dz;
   }
 #pragma unroll
-  for (int c = 0; c <= C; ++c) {
-    red[threadIdx.x] = acc[c];
-    __syncthreads();
-    for (int k = 128; k > 0; k >>= 1) {
-      if ((int)threadIdx.x < k) red[threadIdx.x] += red[threadIdx.x + k];
-      __syncthreads();
-    }
-    if (threadIdx.x == 0) slab[(long)blockIdx.x * (C + 1) + c] = red[0];
-    __syncthreads();
+  for (int r = 0; r < 4; ++r) red[slot][4 * sub + r] = acc[r];
+  if (sub == 0) red[slot][C] = accb;
+  __syncthreads();
+  if ((int)threadIdx.x <= C) {
+    float s = 0.f;
+    for (int k = 0; k < PPB; ++k) s += red[k][threadIdx.x];
+    slab[(long)blockIdx.x * (C + 1) + threadIdx.x] = s;
   }
 }
+
 
 // NCHW fp32 (C <= 4) -> NHWC fp32 with 4 channels (zero padded)
 __global__ __launch_bounds__(256) void nchw_to_nhwc4_f32_kernel(const float* __restrict__ x, float* __restrict__ y, int N,
@@ -1083,7 +1134,14 @@ DPA_API int dpa_head_f32_blocks(long long P) { return (int)(P / 256 + 1 < 1024 ?
 DPA_API int dpa_head_f32(const float* y, int C, const float* w, const float* b, const float* t, long long P, float* slab,
                          float* probs, hipStream_t st) {
   if (C < 1) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(head_f32_kernel, dim3(dpa_head_f32_blocks(P)), dim3(256), 0, st, y, C, w, b, t, (long)P, slab, probs);
+  const dim3 grid(dpa_head_f32_blocks(P));
+  switch (C) {
+    case 8: hipLaunchKernelGGL(head_f32_vec_kernel<8>, grid, dim3(256), 0, st, y, w, b, t, (long)P, slab, probs); break;
+    case 16: hipLaunchKernelGGL(head_f32_vec_kernel<16>, grid, dim3(256), 0, st, y, w, b, t, (long)P, slab, probs); break;
+    case 32: hipLaunchKernelGGL(head_f32_vec_kernel<32>, grid, dim3(256), 0, st, y, w, b, t, (long)P, slab, probs); break;
+    case 64: hipLaunchKernelGGL(head_f32_vec_kernel<64>, grid, dim3(256), 0, st, y, w, b, t, (long)P, slab, probs); break;
+    default: hipLaunchKernelGGL(head_f32_kernel, grid, dim3(256), 0, st, y, C, w, b, t, (long)P, slab, probs);
+  }
   return (int)hipGetLastError();
 }
 
@@ -1091,10 +1149,10 @@ DPA_API int dpa_head_bwd_f32(const float* y, int C, const float* w, const float*
                              long long P, float* gy, float* slab, hipStream_t st) {
   const dim3 grid(dpa_head_f32_blocks(P));
   switch (C) {
-    case 8: hipLaunchKernelGGL(head_bwd_f32_kernel<8>, grid, dim3(256), 0, st, y, w, b, t, dS, (long)P, gy, slab); break;
-    case 16: hipLaunchKernelGGL(head_bwd_f32_kernel<16>, grid, dim3(256), 0, st, y, w, b, t, dS, (long)P, gy, slab); break;
-    case 32: hipLaunchKernelGGL(head_bwd_f32_kernel<32>, grid, dim3(256), 0, st, y, w, b, t, dS, (long)P, gy, slab); break;
-    case 64: hipLaunchKernelGGL(head_bwd_f32_kernel<64>, grid, dim3(256), 0, st, y, w, b, t, dS, (long)P, gy, slab); break;
+    case 8: hipLaunchKernelGGL(head_bwd_f32_vec_kernel<8>, grid, dim3(256), 0, st, y, w, b, t, dS, (long)P, gy, slab); break;
+    case 16: hipLaunchKernelGGL(head_bwd_f32_vec_kernel<16>, grid, dim3(256), 0, st, y, w, b, t, dS, (long)P, gy, slab); break;
+    case 32: hipLaunchKernelGGL(head_bwd_f32_vec_kernel<32>, grid, dim3(256), 0, st, y, w, b, t, dS, (long)P, gy, slab); break;
+    case 64: hipLaunchKernelGGL(head_bwd_f32_vec_kernel<64>, grid, dim3(256), 0, st, y, w, b, t, dS, (long)P, gy, slab); break;
     default: return (int)hipErrorInvalidValue;
   }
   return (int)hipGetLastError();
