@@ -926,11 +926,13 @@ __global__ __launch_bounds__(256) void head_f32_vec_kernel(const float* __restri
 // and stores of gy, as above); every lane
 // of a pixel forms dz itself; channel partials of dz y in the 4 channels a lane owns, reduced per block in
 // LDS in a fixed order (rows = the block's pixel slots), the bias partial (dz) from lane 0 of each pixel.
+// relu: gy is also ReLU-backward masked by y > 0 (y = the last decoder block's ReLU output, so its ReLU
+// backward pass over the full-resolution gradient disappears; the parameter partials use dz as before).
 template <int C>
 __global__ __launch_bounds__(256) void head_bwd_f32_vec_kernel(const float* __restrict__ y, const float* __restrict__ w,
                                                                const float* __restrict__ b, const float* __restrict__ t,
                                                                const float* __restrict__ dS, long P, float* __restrict__ gy,
-                                                               float* __restrict__ slab) {
+                                                               float* __restrict__ slab, int relu) {
   constexpr int L = C / 4, PPB = 256 / L;
   __shared__ float red[PPB][C + 1];
   const int sub = threadIdx.x % L, slot = threadIdx.x / L;
@@ -947,7 +949,12 @@ __global__ __launch_bounds__(256) void head_bwd_f32_vec_kernel(const float* __re
     const float p = 1.f / (1.f + expf(-z));
     const float tt = t[i];
     const float dz = head_dz(p, tt, tt == 1.f ? 1.f : 0.f, d0, d1, d2);
-    *reinterpret_cast<f32x4v*>(gy + i * C + 4 * sub) = dz * wv;
+    f32x4v o = dz * wv;
+    if (relu) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[r] = v[r] > 0.f ? o[r] : 0.f;
+    }
+    *reinterpret_cast<f32x4v*>(gy + i * C + 4 * sub) = o;
 #pragma unroll
     for (int r = 0; r < 4; ++r) acc[r] = fmaf(dz, v[r], acc[r]);
     accb += dz;
@@ -1146,13 +1153,13 @@ DPA_API int dpa_head_f32(const float* y, int C, const float* w, const float* b, 
 }
 
 DPA_API int dpa_head_bwd_f32(const float* y, int C, const float* w, const float* b, const float* t, const float* dS,
-                             long long P, float* gy, float* slab, hipStream_t st) {
+                             long long P, float* gy, float* slab, int relu, hipStream_t st) {
   const dim3 grid(dpa_head_f32_blocks(P));
   switch (C) {
-    case 8: hipLaunchKernelGGL(head_bwd_f32_vec_kernel<8>, grid, dim3(256), 0, st, y, w, b, t, dS, (long)P, gy, slab); break;
-    case 16: hipLaunchKernelGGL(head_bwd_f32_vec_kernel<16>, grid, dim3(256), 0, st, y, w, b, t, dS, (long)P, gy, slab); break;
-    case 32: hipLaunchKernelGGL(head_bwd_f32_vec_kernel<32>, grid, dim3(256), 0, st, y, w, b, t, dS, (long)P, gy, slab); break;
-    case 64: hipLaunchKernelGGL(head_bwd_f32_vec_kernel<64>, grid, dim3(256), 0, st, y, w, b, t, dS, (long)P, gy, slab); break;
+    case 8: hipLaunchKernelGGL(head_bwd_f32_vec_kernel<8>, grid, dim3(256), 0, st, y, w, b, t, dS, (long)P, gy, slab, relu); break;
+    case 16: hipLaunchKernelGGL(head_bwd_f32_vec_kernel<16>, grid, dim3(256), 0, st, y, w, b, t, dS, (long)P, gy, slab, relu); break;
+    case 32: hipLaunchKernelGGL(head_bwd_f32_vec_kernel<32>, grid, dim3(256), 0, st, y, w, b, t, dS, (long)P, gy, slab, relu); break;
+    case 64: hipLaunchKernelGGL(head_bwd_f32_vec_kernel<64>, grid, dim3(256), 0, st, y, w, b, t, dS, (long)P, gy, slab, relu); break;
     default: return (int)hipErrorInvalidValue;
   }
   return (int)hipGetLastError();

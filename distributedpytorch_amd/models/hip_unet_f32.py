@@ -131,6 +131,14 @@ def _conv_wgrad(B, c: _L, ge, x):
     B.side_launch(lambda: F32.wgrad(ge, x, gw, gb, KH=3, KW=3, s=1, pad=1, nreal=c.Cin), ge, x)
 
 
+def _relu_masked(gy: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+    """ReLU backward of a block output y: a no-op for a gradient the head backward already masked by y > 0
+    (the tensor carries ``_dpa_relu_masked``; any autograd accumulation returns a fresh, unmarked tensor)."""
+    if getattr(gy, "_dpa_relu_masked", False):
+        return gy
+    return F32.relu_bwd(_dense(gy), y)
+
+
 class _ConvReLU(torch.autograd.Function):
     """y = relu(conv3x3(x) + b), NHWC fp32 (one conv: the halves of a DoubleConv cut by a pipeline stage
     boundary)."""
@@ -146,7 +154,7 @@ class _ConvReLU(torch.autograd.Function):
     def backward(ctx, gy):
         x, y = ctx.saved_tensors
         B, c = ctx.B, ctx.c
-        ge = F32.relu_bwd(_dense(gy), y)
+        ge = _relu_masked(gy, y)
         _conv_wgrad(B, c, ge, x)
         gx = _conv_dgrad(B, c, ge) if ctx.needs_input_grad[1] else None
         B.join()
@@ -171,7 +179,7 @@ class _DoubleConvReLU(torch.autograd.Function):
     def backward(ctx, gy):
         x, a, y = ctx.saved_tensors
         B, (c1, c2) = ctx.B, ctx.c
-        ge2 = F32.relu_bwd(_dense(gy), y)
+        ge2 = _relu_masked(gy, y)
         _conv_wgrad(B, c2, ge2, a)                 # side stream: overlaps the dgrad chain
         ge1 = _conv_dgrad(B, c2, ge2, mask=a)
         _conv_wgrad(B, c1, ge1, x)
@@ -242,7 +250,7 @@ class _DoubleConvBN(torch.autograd.Function):
         x, z1, y1, z2, y2 = ctx.saved_tensors
         B, (c1, c2) = ctx.B, ctx.c
         s1, s2 = ctx.st
-        dz2 = _bn_bwd(c2, F32.relu_bwd(_dense(gy), y2), z2, s2)
+        dz2 = _bn_bwd(c2, _relu_masked(gy, y2), z2, s2)
         _conv_wgrad(B, c2, dz2, y1)
         g1 = _conv_dgrad(B, c2, dz2, mask=y1)
         dz1 = _bn_bwd(c1, g1, z1, s1)
@@ -268,7 +276,7 @@ class _ConvBN(torch.autograd.Function):
     def backward(ctx, gy):
         x, z, y = ctx.saved_tensors
         B, c = ctx.B, ctx.c
-        dz = _bn_bwd(c, F32.relu_bwd(_dense(gy), y), z, ctx.st)
+        dz = _bn_bwd(c, _relu_masked(gy, y), z, ctx.st)
         _conv_wgrad(B, c, dz, x)
         gx = _conv_dgrad(B, c, dz) if ctx.needs_input_grad[1] else None
         B.join()
@@ -424,7 +432,11 @@ class _HeadLoss(torch.autograd.Function):
     def backward(ctx, dS):
         y, t = ctx.saved_tensors
         seg = ctx.B.model.segmap
-        gy, _, _ = F32.head_bwd(y, seg.weight, seg.bias, t, dS, _grad(seg.weight).view(-1), _grad(seg.bias))
+        # y is the last decoder block's ReLU output: its ReLU backward rides in the head backward, and the
+        # block skips its relu_bwd pass for a gradient marked this way (_relu_masked)
+        gy, _, _ = F32.head_bwd(y, seg.weight, seg.bias, t, dS, _grad(seg.weight).view(-1), _grad(seg.bias),
+                                relu=True)
+        gy._dpa_relu_masked = True
         ctx.B.ready([seg])
         return None, gy, None, None
 

@@ -283,8 +283,9 @@ def head_fwd(y: torch.Tensor, w: torch.Tensor, b: torch.Tensor, t: Optional[torc
 
 
 def head_bwd(y: torch.Tensor, w: torch.Tensor, b: torch.Tensor, t: torch.Tensor, dS: torch.Tensor,
-             gw: Optional[torch.Tensor] = None, gb: Optional[torch.Tensor] = None):
-    """(dL/dy of the head -- NHWC fp32, NOT ReLU-masked --, segmap weight gradient [C], bias gradient [1]).
+             gw: Optional[torch.Tensor] = None, gb: Optional[torch.Tensor] = None, relu: bool = False):
+    """(dL/dy of the head -- NHWC fp32, ReLU-backward masked by y > 0 with ``relu`` (y is then the last decoder
+    block's ReLU output) --, segmap weight gradient [C], bias gradient [1]).
     With ``gw`` / ``gb`` (the flat gradient buffer's views, adjacent: weight then bias) the parameter
     gradients are reduced into them in place and returned as those views."""
     N, H, W, C, ld = nhwc(y, "head_bwd_f32.y")
@@ -298,7 +299,7 @@ def head_bwd(y: torch.Tensor, w: torch.Tensor, b: torch.Tensor, t: torch.Tensor,
     wv = w.detach().reshape(-1).float().contiguous()
     bv = b.detach().reshape(-1).float().contiguous()
     st = _st(y)
-    _check(L.dpa_head_bwd_f32(_p(y), c_int(C), _p(wv), _p(bv), _p(tf), _p(dS), c_ll(P), _p(gy), _p(slab), st),
+    _check(L.dpa_head_bwd_f32(_p(y), c_int(C), _p(wv), _p(bv), _p(tf), _p(dS), c_ll(P), _p(gy), _p(slab), c_int(int(relu)), st),
            "head_bwd_f32")
     if (gw is not None and gb is not None and gw.is_contiguous() and gw.numel() == C and gb.numel() == 1
             and gb.data_ptr() == gw.data_ptr() + 4 * C):
