@@ -335,15 +335,17 @@ def test_pool_and_head(hip_lib):
     assert torch.equal(y.permute(0, 3, 1, 2), ref)
     (gx,) = torch.autograd.grad(y, (xn,), g.permute(0, 2, 3, 1).contiguous())
     assert torch.equal(gx.permute(0, 3, 1, 2), gx_ref)
-    # head: 1x1 conv + sigmoid + loss partial sums, and its backward
+    # head: 1x1 conv + sigmoid + loss partial sums, and its backward.  Its input is always a block's ReLU
+    # output (the engine folds that ReLU's backward into the head backward), so the reference is the head
+    # composed with that ReLU
     yv = torch.randn(2, 32, 16, 16, device="cuda").requires_grad_(True)
     hw = (torch.randn(1, 32, 1, 1, device="cuda") * 0.2).requires_grad_(True)
     hb = torch.randn(1, device="cuda").requires_grad_(True)
     t = (torch.rand(2, 1, 16, 16, device="cuda") > 0.5).float()
-    S_ref = loss_partials_from_probs(torch.sigmoid(F.conv2d(yv, hw, hb)), t)
+    S_ref = loss_partials_from_probs(torch.sigmoid(F.conv2d(torch.relu(yv), hw, hb)), t)
     dS = torch.tensor([0.3, -1.2, 0.7, 0.1], device="cuda")
     g_ref = torch.autograd.grad(S_ref, (yv, hw, hb), dS)
-    yn = yv.detach().permute(0, 2, 3, 1).contiguous().requires_grad_(True)
+    yn = torch.relu(yv.detach()).permute(0, 2, 3, 1).contiguous().requires_grad_(True)
     import types
     seg = torch.nn.Conv2d(32, 1, 1).cuda()
     with torch.no_grad():
