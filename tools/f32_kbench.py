@@ -21,7 +21,7 @@ def _modes(opt, current):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=16)
-    ap.add_argument("--img", type=int, default=512)
+    ap.add_argument("--img", default="512", help="H or HxW (e.g. 640x960, the reference default)")
     ap.add_argument("--model", default="unet")
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--wgrad-big", choices=["default", "off", "on", "both"], default="default",
@@ -42,19 +42,20 @@ def main():
     from distributedpytorch_amd.ops import fp32 as F32
     dev = torch.device("cuda:0")
     cfg = build_model(a.model).cfg
-    N, S = a.batch, a.img
+    N = a.batch
+    H0, W0 = (int(v) for v in a.img.split("x")) if "x" in a.img else (int(a.img), int(a.img))
     convs, deconvs = [], []
     w = list(cfg.widths)
-    cin, h = 3, S
+    cin, h, wd = 3, H0, W0
     for l, c in enumerate(w):
-        convs.append((f"enc{l}.c1", h, cin, c)), convs.append((f"enc{l}.c2", h, c, c))
-        cin, h = c, h // 2
-    convs.append(("mid.c1", h, cin, cfg.mid_width)), convs.append(("mid.c2", h, cfg.mid_width, cfg.mid_width))
+        convs.append((f"enc{l}.c1", (h, wd), cin, c)), convs.append((f"enc{l}.c2", (h, wd), c, c))
+        cin, h, wd = c, h // 2, wd // 2
+    convs.append(("mid.c1", (h, wd), cin, cfg.mid_width)), convs.append(("mid.c2", (h, wd), cfg.mid_width, cfg.mid_width))
     cin = cfg.mid_width
     for i, c in enumerate(reversed(w)):
-        deconvs.append((f"dec{i}.up", h, cin, c))
-        h *= 2
-        convs.append((f"dec{i}.c1", h, 2 * c, c)), convs.append((f"dec{i}.c2", h, c, c))
+        deconvs.append((f"dec{i}.up", (h, wd), cin, c))
+        h, wd = h * 2, wd * 2
+        convs.append((f"dec{i}.c1", (h, wd), 2 * c, c)), convs.append((f"dec{i}.c2", (h, wd), c, c))
         cin = c
 
     def t(fn):
@@ -73,16 +74,16 @@ def main():
     tot = {"fwd": 0.0, "dgrad": 0.0, "wgrad": 0.0}
     print(f"{'layer':10s} {'HxW':>9s} {'ci':>4s} {'co':>4s} | {'fwd ms':>7s} {'TF/s':>6s} | {'dgrad':>7s} {'TF/s':>6s} | "
           f"{'wgrad':>7s} {'TF/s':>6s}")
-    for name, hh, ci, co in convs:
+    for name, (hh, ww), ci, co in convs:
         cs = 4 if ci == 3 else ci
-        x = torch.randn(N, hh, hh, cs, device=dev)
+        x = torch.randn(N, hh, ww, cs, device=dev)
         m = torch.nn.Conv2d(ci, co, 3, padding=1).to(dev)
         layer = E._L(m, "conv", cs)
         eng = E.F32Engine([layer], dev)
         eng.side = None                      # time the kernels themselves, on the current stream
         eng.ensure_packed()
-        ge = torch.randn(N, hh, hh, co, device=dev)
-        fl = 2.0 * N * hh * hh * co * ci * 9
+        ge = torch.randn(N, hh, ww, co, device=dev)
+        fl = 2.0 * N * hh * ww * co * ci * 9
         wmodes = _modes(a.igemm_wide, F32.IGEMM_WIDE)
         hmodes = [F32.CONV_HALO] if a.conv_halo == "default" else [int(v) for v in a.conv_halo.split(",")]
         if len(hmodes) > 1:
@@ -114,29 +115,29 @@ def main():
         extra = "" if len(tws) == 1 else f" (other form: {tws[0]:7.3f} {fl / tws[0] / 1e9:6.1f})"
         if len(tfs) > 1:
             extra += f" [other fwd {tfs[0]:7.3f} dgrad {tds[0]:7.3f}]"
-        print(f"{name:10s} {hh:4d}x{hh:<4d} {ci:4d} {co:4d} | {tf:7.3f} {fl / tf / 1e9:6.1f} | {td:7.3f} "
+        print(f"{name:10s} {hh:4d}x{ww:<4d} {ci:4d} {co:4d} | {tf:7.3f} {fl / tf / 1e9:6.1f} | {td:7.3f} "
               f"{(fl / td / 1e9 if td else 0):6.1f} | {tw:7.3f} {fl / tw / 1e9:6.1f}{extra}", flush=True)
         del x, ge
-    for name, hh, ci, co in deconvs:
-        x = torch.randn(N, hh, hh, ci, device=dev)
+    for name, (hh, ww), ci, co in deconvs:
+        x = torch.randn(N, hh, ww, ci, device=dev)
         wt = torch.randn(ci, co, 2, 2, device=dev) * 0.05
         b = torch.zeros(co, device=dev)
-        gy = torch.randn(N, 2 * hh, 2 * hh, co, device=dev)
-        fl = 2.0 * N * hh * hh * ci * co * 4
-        y = torch.empty(N, 2 * hh, 2 * hh, co, device=dev)
+        gy = torch.randn(N, 2 * hh, 2 * ww, co, device=dev)
+        fl = 2.0 * N * hh * ww * ci * co * 4
+        y = torch.empty(N, 2 * hh, 2 * ww, co, device=dev)
         wf = F32.pack_deconv_fwd(wt)
         tf = t(lambda: F32.igemm(x, wf, y, Ngemm=4 * co, Kpad=ci, KH=1, KW=1, stride=1, pad=0, Cs=ci,
-                                 out_grid=(N, hh, hh), bias=b, mode=1, Cout=co))
-        gx = torch.empty(N, hh, hh, ci, device=dev)
+                                 out_grid=(N, hh, ww), bias=b, mode=1, Cout=co))
+        gx = torch.empty(N, hh, ww, ci, device=dev)
         wd = F32.pack_deconv_dgrad(wt)
         td = t(lambda: F32.igemm(gy, wd, gx, Ngemm=ci, Kpad=4 * co, KH=2, KW=2, stride=2, pad=0, Cs=co,
-                                 out_grid=(N, hh, hh)))
+                                 out_grid=(N, hh, ww)))
         gw = torch.zeros(ci, co, 2, 2, device=dev)
         tw = t(lambda: F32.wgrad(x, gy, gw, None, KH=2, KW=2, s=2, pad=0))
         tot["fwd"] += tf
         tot["dgrad"] += td
         tot["wgrad"] += tw
-        print(f"{name:10s} {hh:4d}x{hh:<4d} {ci:4d} {co:4d} | {tf:7.3f} {fl / tf / 1e9:6.1f} | {td:7.3f} "
+        print(f"{name:10s} {hh:4d}x{ww:<4d} {ci:4d} {co:4d} | {tf:7.3f} {fl / tf / 1e9:6.1f} | {td:7.3f} "
               f"{fl / td / 1e9:6.1f} | {tw:7.3f} {fl / tw / 1e9:6.1f}", flush=True)
     print("totals ms: " + ", ".join(f"{k} {v:.2f}" for k, v in tot.items()))
 
