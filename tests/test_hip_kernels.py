@@ -217,9 +217,10 @@ def test_deconv_dgrad_from_concat(hip_lib, N, h, w, Cin, Cout):
     # ragged rows (partial last strip: out-of-row gradient pixels read as zeros)
     (1, 5, 240, 128, 64, None, "stream"), (2, 3, 120, 64, 128, None, "stream"), (1, 4, 60, 128, 128, None, "stream"),
     (2, 5, 200, 3, 32, 8, "stream"), (1, 3, 480, 64, 64, None, "stream"),
-    # deep layers on the LDS-DMA row pipeline (128 x 64 x 9-tap tiles; ragged strips, row segments)
-    (2, 5, 64, 128, 128, None, "rows"), (1, 7, 120, 64, 128, None, "rows"), (2, 4, 128, 256, 256, None, "rows"),
-    (1, 3, 48, 64, 256, None, "rows"), (1, 66, 64, 128, 128, None, "rows"), (2, 9, 100, 192, 128, None, "rows"),
+    # deep-layer shapes through the automatic choice (band128 on W % 64 grids, the row-streaming kernel on ragged
+    # widths: odd row counts, W = 120 / 48 / 100, 192 input channels)
+    (2, 5, 64, 128, 128, None, "auto"), (1, 7, 120, 64, 128, None, "auto"), (2, 4, 128, 256, 256, None, "auto"),
+    (1, 3, 48, 64, 256, None, "auto"), (1, 66, 64, 128, 128, None, "auto"), (2, 9, 100, 192, 128, None, "auto"),
     # deep layers as a dense 256x256 LDS-DMA GEMM (csrc/wgrad_gemm.hip): partial last column tile
     # (9 x 128 = 1152, 9 x 64 = 576 columns), 32-wide rows (two rows per K-step), several channel tiles
     (2, 4, 64, 128, 256, None, "gemm"), (3, 6, 32, 256, 256, None, "gemm"), (1, 2, 128, 64, 512, None, "gemm"),

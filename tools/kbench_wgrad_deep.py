@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
-"""Deep-layer conv3x3 weight gradients at the bench batch: the row-streaming, LDS-DMA row-pipeline and
-dense-GEMM (csrc/wgrad_gemm.hip) paths interleaved in one process, plus the max deviation of each
-from the gemm path's result.  Usage: python tools/kbench_wgrad_deep.py [--batch 256] [--img 512]"""
+"""Deep-layer conv3x3 weight gradients at the bench batch: the row-streaming (csrc/halo.hip), dense-GEMM
+(csrc/wgrad_gemm.hip) and band-staged (csrc/wgrad_band.hip: 256- and 128-output-channel forms) paths
+interleaved in one process, plus the max deviation of each from the gemm path's result (accuracy against
+fp32: tools/wgrad_check.py).  Usage: python tools/kbench_wgrad_deep.py [--batch 256] [--img 512]"""
 import argparse
 import os
 import sys
@@ -18,7 +19,7 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--img", type=int, default=512)
     ap.add_argument("--reps", type=int, default=5)
-    ap.add_argument("--paths", default="stream,rows,gemm")
+    ap.add_argument("--paths", default="stream,gemm,band,band128")
     ap.add_argument("--only", default="", help="comma-separated layer-name substrings")
     a = ap.parse_args()
     B, S = a.batch, a.img
