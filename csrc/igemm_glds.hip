@@ -1431,17 +1431,27 @@ __device__ __forceinline__ bf16x8_t lds_read128_i(unsigned addr) {
 // the 9 phases of the current slice (2 instructions per wave per phase, zero-fill dummies past the
 // image) into the other image buffer.  Every wave issues the same DMA count per phase, so the waits are
 // compile-time vmcnt values (slice loop unrolled by its 9 phases).
+//
+// BC = 64 (round 6, the 64-output-channel convs the row-halo kernel took: 256^2 128 -> 64 forward, 128^2 dgrads
+// into 64 channels): 8 waves of 64 channels x 64 pixels (16 MFMAs per phase), 512-pixel tiles of whole rows
+// up to W = 256 (R = 2: a 4 x 258-pixel image, 65 KB per buffer); the 4-KB tap weights are 4 DMA
+// instructions, so waves 4-7 issue a zero-fill dummy into the dump area (uniform vmcnt); the next slice's
+// image goes out 3 slots per phase in phases 1-3.
 template <int EP, int BC>
 __global__ __launch_bounds__(512) void igemm_slp_kernel(IgemmArgs a) {
-  static_assert(BC == 128 || BC == 256, "channel tile");
-  constexpr int TC = 8, TP = 4, WC = 128, WP = 64, RB = 64;
-  constexpr int NCW = BC / 128, BP = 8 / NCW * WP;   // 1 x 8 waves, 512 pixels / 2 x 4 waves, 256 pixels
-  constexpr int TAPB = BC * RB;                      // one tap's weights: 8 / 16 KB
-  constexpr int NWW = BC / 128;                      // weight DMA instructions per wave per phase
-  // largest (R+2)(W+2) image in whole DMA instructions: 128 channels W <= 128 (R >= 4), 256 channels W <= 64
-  constexpr int PIMG = BC == 128 ? 49 * 1024 : 25 * 1024;
-  constexpr int MI = BC == 128 ? 7 : 4;              // pixel DMA slots per wave per image (8 x MI >= PIMG / 1 KB)
-  constexpr int NPQ = (MI + 1) / 2;                  // phases 1 .. NPQ of a slice issue 2 slots each
+  static_assert(BC == 64 || BC == 128 || BC == 256, "channel tile");
+  constexpr int WC = BC == 64 ? 64 : 128, TC = WC / 16, TP = 4, WP = 64, RB = 64;
+  constexpr int NCW = BC / WC, BP = 8 / NCW * WP;    // 1 x 8 waves, 512 pixels / 2 x 4 waves, 256 pixels
+  constexpr int TAPB = BC * RB;                      // one tap's weights: 4 / 8 / 16 KB
+  constexpr int NWW = BC == 64 ? 1 : BC / 128;       // weight DMA instructions per wave per phase
+  // largest (R+2)(W+2) image in whole DMA instructions: 64 channels W <= 256 (R >= 2), 128 channels W <= 128
+  // (R >= 4), 256 channels W <= 64
+  constexpr int PIMG = BC == 64 ? 65 * 1024 : BC == 128 ? 49 * 1024 : 25 * 1024;
+  constexpr int MI = BC == 64 ? 9 : BC == 128 ? 7 : 4;   // pixel DMA slots per wave per image (8 x MI >= PIMG / 1 KB)
+  constexpr int SPP = BC == 64 ? 3 : 2;              // image slots issued per phase
+  constexpr int NPQ = (MI + SPP - 1) / SPP;          // phases 1 .. NPQ of a slice issue them
+  // phase 8's wait allows the slots of phases 5 .. 8 outstanding: the next image must be out by phase 4
+  static_assert(NPQ <= 4, "image issue window");
   __shared__ __attribute__((aligned(1024))) char lds[6 * TAPB + 2 * PIMG + 1024];
   char* const Pimg = lds + 6 * TAPB;
   char* const dump = lds + 6 * TAPB + 2 * PIMG;
@@ -1490,10 +1500,11 @@ __global__ __launch_bounds__(512) void igemm_slp_kernel(IgemmArgs a) {
   // the weights of phase g (tap (g % 9) / 3, (g % 9) % 3 of slice g / 9) into ring buffer g % 6
   auto issueW = [&](int g) {
     const int sl = g / 9, t = g - 9 * sl;
-    const bool ok = g < NPH;
+    const bool real = BC != 64 || wid < 4;             // BC 64: waves 4-7 issue a dummy (wave-uniform)
+    const bool ok = g < NPH && real;
 #pragma unroll
     for (int v = 0; v < NWW; ++v)
-      dma16(wrs, lds + (g % 6) * TAPB + (wid + 8 * v) * 1024,
+      dma16(wrs, real ? lds + (g % 6) * TAPB + (wid + 8 * v) * 1024 : dump,
             ok ? wsrc[v] + (unsigned)((t * a.Cs + sl * 32) * 2) : 0x80000000u);
   };
   // pixel slot m of slice sl's image into image buffer sl & 1 (dummies past the image / the slices)
@@ -1519,9 +1530,9 @@ __global__ __launch_bounds__(512) void igemm_slp_kernel(IgemmArgs a) {
 #pragma unroll
     for (int ip = 0; ip < TP; ++ip) acc[ic][ip] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  // prologue: slice 0's image (2 NPQ slots) and the weights of phases 0-3
+  // prologue: slice 0's image (SPP NPQ slots) and the weights of phases 0-3
 #pragma unroll
-  for (int m = 0; m < 2 * NPQ; ++m) issueP(0, m);
+  for (int m = 0; m < SPP * NPQ; ++m) issueP(0, m);
   issueW(0);
   issueW(1);
   issueW(2);
@@ -1569,12 +1580,12 @@ __global__ __launch_bounds__(512) void igemm_slp_kernel(IgemmArgs a) {
     }
     issueW(g + 4);
     if constexpr (Q >= 1 && Q <= NPQ) {
-      issueP(sl + 1, 2 * (Q - 1));
-      issueP(sl + 1, 2 * (Q - 1) + 1);
+#pragma unroll
+      for (int u = 0; u < SPP; ++u) issueP(sl + 1, SPP * (Q - 1) + u);
     }
     // outstanding after W(g + 1): W(g + 2 .. g + 4) and the image slots of phases g - 3 .. g
-    constexpr int P0 = (Q >= 1 && Q <= NPQ) ? 2 : 0, P1 = (Q - 1 >= 1 && Q - 1 <= NPQ) ? 2 : 0;
-    constexpr int P2 = (Q - 2 >= 1 && Q - 2 <= NPQ) ? 2 : 0, P3 = (Q - 3 >= 1 && Q - 3 <= NPQ) ? 2 : 0;
+    constexpr int P0 = (Q >= 1 && Q <= NPQ) ? SPP : 0, P1 = (Q - 1 >= 1 && Q - 1 <= NPQ) ? SPP : 0;
+    constexpr int P2 = (Q - 2 >= 1 && Q - 2 <= NPQ) ? SPP : 0, P3 = (Q - 3 >= 1 && Q - 3 <= NPQ) ? SPP : 0;
     wait_vm<3 * NWW + P0 + P1 + P2 + P3>();
     sync_in();
 #pragma unroll
@@ -1614,6 +1625,14 @@ static inline bool slp256_ok(const IgemmArgs& a) {
   return a.mode == 0 && a.KH == 3 && a.KW == 3 && a.stride == 1 && a.pad == 1 && a.Hs == a.Ho && a.Ws == a.Wo &&
          a.Kpad == 9 * a.Cs && (a.Cs % 32) == 0 && a.Ngemm % 256 == 0 && (a.ldx & 7) == 0 && (W == 32 || W == 64) &&
          ((long)a.Ho * W) % 256 == 0;
+}
+
+// 64-channel slice-staged ping-pong eligible (cfg 19): W a power of two in [32, 256], whole 512-pixel tiles
+static inline bool slp64_ok(const IgemmArgs& a) {
+  const int W = a.Wo;
+  return a.mode == 0 && a.KH == 3 && a.KW == 3 && a.stride == 1 && a.pad == 1 && a.Hs == a.Ho && a.Ws == a.Wo &&
+         a.Kpad == 9 * a.Cs && (a.Cs % 32) == 0 && a.Ngemm % 64 == 0 && (a.ldx & 7) == 0 &&
+         (W == 32 || W == 64 || W == 128 || W == 256) && ((long)a.Ho * W) % 512 == 0;
 }
 
 // slice-staged eligible: conv3x3 s1 p1 on one grid, K = 9 Cs unpadded, 32-channel slices, tiles of whole
@@ -1657,6 +1676,7 @@ static int launch_glds(const IgemmArgs& a, hipStream_t st) {
 //   18 (variant 262144): slice-staged 128 x 512 (igemm_sl_kernel) -- the auto choice for 128-output-channel
 //       layers it takes (3-16 % faster than cfg 15 on every 128-channel 512^2-UNet layer,
 //       profiles/kbench_sl_b256_r04.txt), cfg 15 where it does not
+//   19 (variant 524288): slice-staged ping-pong 64 x 512 (igemm_slp_kernel<EP, 64>), W <= 256
 // Flags: +32 no persistent kernel in the auto choice (a side stream owns CUs), +2048 generic epilogue
 // (tests), +8192 cfg 14 without row blocks (tests), +1048576 no slice-staged kernel in the auto choice.
 // Requires Cs % 64 == 0 (a K-step never straddles a tap; slice-staged: Cs % 32), Kpad % 64 == 0,
@@ -1667,8 +1687,8 @@ DPA_API int dpa_igemm_glds(const IgemmArgs* args, int cfg, hipStream_t st) {
   const bool no_fast_ep = cfg & 2048;   // the generic epilogue (tests)
   const bool no_rowblock = cfg & 8192;  // cfg 14 with per-K-tile pixel staging (tests)
   const bool no_sl = cfg & 1048576;     // auto: no slice-staged kernel (A/B switch)
-  cfg = (cfg & 262144) ? 18 : (cfg & 15);
-  const bool sl = cfg == 18;
+  cfg = (cfg & 262144) ? 18 : (cfg & 524288) ? 19 : (cfg & 15);
+  const bool sl = cfg == 18 || cfg == 19;
   if ((a.Cs & (sl ? 31 : 63)) || (a.Kpad & 63) || (a.ldx & 7) || (a.ldy & 3) || a.KH * a.KW > 32 || (a.korder & 1) || a.x2 || a.xbn)
     return (int)hipErrorInvalidValue;
   if (a.bnslab) {
@@ -1770,6 +1790,11 @@ DPA_API int dpa_igemm_glds(const IgemmArgs* args, int cfg, hipStream_t st) {
       else if (ep == 3) hipLaunchKernelGGL((igemm_sl_kernel<3, 128>), dim3(grid), dim3(512), 0, st, a);
       else hipLaunchKernelGGL((igemm_sl_kernel<0, 128>), dim3(grid), dim3(512), 0, st, a);
       return (int)hipGetLastError();
+    }
+    case 19: {
+      if (!slp64_ok(a)) break;
+      const int grid = (M / 512) * (a.Ngemm / 64);
+      DPA_EP_LAUNCH2(igemm_slp_kernel, 64, grid);
     }
     default: break;
   }

@@ -46,6 +46,11 @@ KNOBS = (
     Knob("wgrad_presum_y", "DPA_WGRAD_PRESUM_Y", 0, "cap on the in-place presum grid's group blocks (0 = one block per 32-row group)"),
     Knob("slp256", "DPA_SLP256", False, "256-channel convs on 32/64-wide grids as slice-staged ping-pong (igemm_slp_kernel<EP, 256>) instead of the row-block kernel"),
     Knob("slpp", "DPA_NO_SLPP", True, "128-output-channel slice-staged convs on the ping-pong schedule (csrc/igemm_glds.hip igemm_slp_kernel)"),
+    Knob("halo_cfg", "DPA_HALO_CFG", 0, "row-halo conv tile override (csrc/halo.hip dpa_igemm_halo cfg; 0 = auto)"),
+    Knob("slp64", "DPA_SLP64", False, "64-output-channel convs over >= 64 input channels on rows <= 256 px: slice-staged "
+         "ping-pong 64 x 512 (igemm_slp_kernel<EP, 64>, cfg 19) instead of the row-halo conv. Off: bitwise equal but "
+         "slower at b256 (3619 vs 3113 us at 256^2 128 -> 64, 1015 vs 875 us at the 128^2 dgrad; 16 MFMAs per phase do "
+         "not cover the phase barriers, profiles/kbench_slp64_halo_r06.txt)"),
     Knob("wgrad_band", "DPA_NO_WGRAD_BAND", True, "deep weight gradients with the input band staged once for all 9 taps (csrc/wgrad_band.hip)"),
     Knob("side_wgrad", "DPA_NO_SIDE_WGRAD", True, "weight gradients on a side HIP stream, overlapping the dgrad chain"),
     # fusions
@@ -161,6 +166,8 @@ class KernelConfig:
     wgrad_band: bool = True
     slpp: bool = True
     slp256: bool = False
+    slp64: bool = False
+    halo_cfg: int = 0
     wgrad_presum_y: int = 0
     side_wgrad: bool = True
     fused_head: bool = True

@@ -95,6 +95,9 @@ USE_GLDS = CFG.glds                    # LDS-DMA GEMMs (csrc/igemm_glds.hip)
 # 128-output-channel layers on rows of <= 128 pixels: the slice-staged 128 x 512 GEMM (cfg 18), 3-16 %
 # faster than the 128-channel row-block kernel (profiles/kbench_sl_b256_r04.txt)
 USE_GLDS_SL = CFG.glds_sl
+# 64-output-channel convs over >= 64 input channels (the 256^2 decoder conv 128 -> 64, the 128^2 dgrads into 64
+# channels): the slice-staged ping-pong 64 x 512 GEMM (cfg 19) instead of the row-halo conv
+USE_SLP64 = CFG.slp64
 BN_SUMS_POOL = CFG.bn_sums_pool        # BN backward partial sums from the pool backward (models/hip_unet.py)
 BN_SUMS_DECONV = CFG.bn_sums_deconv    # ... from the fused transposed-conv backward
 BN_SUMS_POOL_Z = CFG.bn_sums_pool_z    # ... reading the dense z (relu(bn(z)) re-formed) instead of the skip
@@ -114,7 +117,7 @@ SIDE_WGRAD = CFG.side_wgrad            # weight gradients on a side stream (mode
 SIDE_PRIORITY = CFG.side_priority      # its HIP priority (torch convention: lower = higher, 0 = default)
 ENC0_CHUNKS = CFG.enc0_chunks          # first-level backward in image chunks (models/hip_unet.py _EncFn)
 WGRAD_STREAM_CFG = 0                   # row-streaming weight-gradient tile override (kbench A/B; 0 = auto)
-HALO_CFG = 0                           # row-halo conv tile override (kbench A/B; 0 = auto)
+HALO_CFG = CFG.halo_cfg                # row-halo conv tile override (A/B; 0 = auto)
 USE_FUSED_HEAD = CFG.fused_head        # segmentation head + loss partials in the last decoder conv
 USE_FUSED_BN = CFG.fused_bn            # BatchNorm statistics in the producing streaming conv
 FOLD_BN_EVAL = CFG.fold_bn_eval        # eval-mode BatchNorm folded into the conv weights
@@ -330,7 +333,12 @@ def igemm(x: torch.Tensor, wpacked: torch.Tensor, y: torch.Tensor, *, Ngemm: int
     rb128 = (path == "auto" and USE_GLDS128 and USE_GLDS and conv3 and pad == 1 and
              (Hs, Ws) == (Ho, Wo) and Kpad == 9 * Cs and Cs % 64 == 0 and (Wo in (32, 64, 128) or Wo % 256 == 0) and
              (Ho * Wo) % 256 == 0 and Ngemm % 128 == 0 and Ngemm % 256 != 0)
-    if a is not None and not rb128 and (path == "halo" or (path == "auto" and USE_HALO and conv3 and Cs % 32 == 0 and Ngemm <= 128)):
+    # 64 output channels from >= 64 (not the row-streaming shapes): whole-row 512-pixel tiles, slice-major K
+    slp64 = (path == "auto" and USE_SLP64 and USE_GLDS and conv3 and pad == 1 and (Hs, Ws) == (Ho, Wo) and
+             Kpad == 9 * Cs and Cs % 32 == 0 and Cs >= 64 and Ngemm == 64 and Wo in (32, 64, 128, 256) and
+             (Ho * Wo) % 512 == 0 and xbn is None)
+    if (a is not None and not rb128 and not slp64 and
+            (path == "halo" or (path == "auto" and USE_HALO and conv3 and Cs % 32 == 0 and Ngemm <= 128))):
         err = L.dpa_igemm_halo(ctypes.byref(a), c_int(variant if path == "halo" else HALO_CFG), st)
         if err == 0:
             done = True
@@ -351,6 +359,9 @@ def igemm(x: torch.Tensor, wpacked: torch.Tensor, y: torch.Tensor, *, Ngemm: int
                 continue
             assert n0 == 0, "row-block BN statistics refused after the first chunk"
             a.bnslab, gslab = None, None
+        if slp64:
+            _check(L.dpa_igemm_glds(ctypes.byref(a), c_int(524288), st), "igemm_slp<64>")
+            continue
         if path == "glds" or (path == "auto" and glds_ok):
             no_pers = not persistent
             # 128 output channels: the slice-staged 128 x 512 kernel (cfg 18) on rows of <= 128 pixels,

@@ -620,10 +620,11 @@ def test_stream_conv_fused_head(hip_lib, N, H, W):
     (2, 5, 128, 64, 128, 4), (1, 4, 128, 128, 64, 4), (2, 3, 128, 32, 64, 5), (1, 7, 256, 256, 128, 4),
     (2, 5, 128, 64, 128, 2), (2, 5, 128, 64, 128, 6), (1, 3, 128, 128, 128, 7), (2, 4, 256, 128, 256, 6),
     (2, 5, 128, 64, 128, 8), (1, 4, 128, 128, 64, 8), (2, 3, 128, 32, 64, 9), (1, 7, 256, 256, 128, 8),
-    (1, 3, 128, 128, 128, 10), (2, 5, 256, 32, 32, 9)])
+    (1, 3, 128, 128, 128, 10), (2, 5, 256, 32, 32, 9), (2, 5, 128, 128, 64, 11), (1, 5, 128, 64, 64, 12),
+    (1, 7, 256, 128, 64, 13), (2, 6, 128, 64, 128, 13), (1, 3, 256, 128, 64, 14)])
 def test_conv3x3_halo_two_rows(hip_lib, N, H, W, Cin, Cout, hcfg):
-    """Row-halo conv with two output rows per block (one weight staging per slice for both; odd
-    heights -> the last block's second row is masked): forward with bias+ReLU and masked dgrad."""
+    """Row-halo conv with two (three, four) output rows per block (one weight staging per slice for all;
+    heights not a multiple -> the last block's extra rows are masked): forward with bias+ReLU and masked dgrad."""
     from distributedpytorch_amd.ops import kernels as K
     torch.manual_seed(9)
     x = _bf(F.relu(torch.randn(N, Cin, H, W)))
@@ -639,7 +640,7 @@ def test_conv3x3_halo_two_rows(hip_lib, N, H, W, Cin, Cout, hcfg):
     F.conv2d(xr, w, padding=1).backward(g)
     packed_d, ngd, kpd = _pack_one(1, w)
     dx = torch.empty(N, H, W, Cin, dtype=torch.bfloat16, device="cuda")
-    bc = {2: 64, 4: 64, 5: 32, 6: 128, 7: 128, 8: 64, 9: 32, 10: 128}[hcfg]   # output-channel tile
+    bc = {2: 64, 4: 64, 5: 32, 6: 128, 7: 128, 8: 64, 9: 32, 10: 128, 11: 64, 12: 64, 13: 64, 14: 64}[hcfg]   # output-channel tile
     if Cin % bc == 0:
         K.igemm(_nhwc(g), packed_d, dx, Ngemm=ngd, Kpad=kpd, KH=3, KW=3, stride=1, pad=1, Cs=Cout,
                 out_grid=(N, H, W), mask=_nhwc(x), path="halo", variant=hcfg)

@@ -197,3 +197,32 @@ def test_slp256_fp32_anchor(hip_lib, shape, kind):
             assert _rel(got.float().cpu(), exp) < 1e-2, (on, kind)
     finally:
         L.dpa_igemm_set_slp256(ctypes.c_int(int(K.CFG.slp256)))
+
+
+@pytest.mark.parametrize("N,H,W,Cs,kind", [(2, 256, 256, 128, "fwd"), (2, 128, 128, 128, "dgrad"),
+                                           (2, 64, 64, 256, "fwd"), (3, 32, 32, 64, "dgrad")])
+def test_slp64_bitwise_vs_halo(hip_lib, N, H, W, Cs, kind):
+    """igemm_slp_kernel<EP, 64> (cfg 19, DPA_SLP64: the 64-output-channel convs as slice-staged ping-pong,
+    waves 4-7 issuing dummy weight DMAs, the next image 3 slots per phase) runs each accumulator's MFMAs in the
+    row-halo kernel's order (slice, then tap): bitwise equal to row-halo cfg 4 where that takes the shape, and
+    within bf16 rounding of the fp32 convolution; 2-8 image rows per 512-pixel tile."""
+    from distributedpytorch_amd.ops import kernels as K
+    Ng = 64
+    torch.manual_seed(47 + Cs + W)
+    x = torch.randn(N, H, W, Cs, device="cuda").to(torch.bfloat16)
+    w = (torch.randn(Ng, 9 * Cs, device="cuda") / (9 * Cs) ** 0.5).to(torch.bfloat16)
+    extra = (dict(bias=torch.randn(Ng, device="cuda") * 0.1, relu=True) if kind == "fwd" else
+             dict(mask=torch.randn(N, H, W, Ng, device="cuda").to(torch.bfloat16)))
+    y = torch.empty(N, H, W, Ng, device="cuda", dtype=torch.bfloat16)
+    K.igemm(x, w, y, Ngemm=Ng, Kpad=9 * Cs, KH=3, KW=3, stride=1, pad=1, Cs=Cs, out_grid=(N, H, W),
+            path="glds", variant=524288, **extra)
+    torch.cuda.synchronize()
+    if W % 128 == 0:
+        yh = torch.empty_like(y)
+        K.igemm(x, w, yh, Ngemm=Ng, Kpad=9 * Cs, KH=3, KW=3, stride=1, pad=1, Cs=Cs, out_grid=(N, H, W),
+                path="halo", variant=4, **extra)
+        torch.cuda.synchronize()
+        assert torch.equal(y, yh)
+    ref = _ref_conv(x.float().cpu().permute(0, 3, 1, 2),
+                    w.float().cpu().view(Ng, 9, Cs).permute(0, 2, 1).reshape(Ng, Cs, 3, 3))
+    assert _rel(y.float().cpu(), _expected(kind, ref, extra)) < 1e-2
