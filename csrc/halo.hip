@@ -279,10 +279,6 @@ DPA_API int dpa_igemm_halo(const IgemmArgs* args, int cfg, hipStream_t st) {
     if (a.Ngemm == 32 && tiles_ok(a.Wo, 256)) cfg = 1;
     // two output rows per block: 20-25% faster than one row on every 512^2 UNet shape
     // (profiles/kbench_b32_512.txt halo.c4/c5 vs c2/c3)
-    // 64 output channels on 256-pixel rows: 4 rows x 8 waves per staging of the weights, 4-5 % faster than
-    // cfg 4 at 256^2 128 -> 64 (2972 vs 3113 us at b256, profiles/kbench_slp64_halo_r06.txt); cfg 4 stays
-    // at 128^2 (892 vs 875 us)
-    else if (a.Ngemm == 64 && a.Wo % 256 == 0) cfg = 13;
     else if (a.Ngemm % 64 == 0 && a.Ngemm <= 128 && tiles_ok(a.Wo, 128)) cfg = 4;
     else if (a.Ngemm % 32 == 0 && a.Ngemm <= 64 && tiles_ok(a.Wo, 128)) cfg = 5;
     else return (int)hipErrorInvalidValue;
@@ -298,6 +294,8 @@ DPA_API int dpa_igemm_halo(const IgemmArgs* args, int cfg, hipStream_t st) {
     case 8: if (!tiles_ok(a.Wo, 128) || a.Ngemm % 64) break; return launch_igemm_halo<128, 64, 64, 32, 2, true>(a, st);
     case 9: if (!tiles_ok(a.Wo, 128) || a.Ngemm % 32) break; return launch_igemm_halo<128, 32, 32, 32, 2, true>(a, st);
     case 10: if (!tiles_ok(a.Wo, 128) || a.Ngemm % 128) break; return launch_igemm_halo<128, 128, 32, 64, 2, true>(a, st);
+    // (cfg 13 is 4-5 % faster than cfg 4 alone at 256^2 128 -> 64, 2972 vs 3113 us at b256, but the step is 0.4 %
+    // slower with it: 3158 / 3165 vs 3171 / 3183 img/s on one box, profiles/kbench_slp64_halo_r06.txt -- not auto)
     // more output rows per staging of the weight slice (the weights are half of the staged bytes at 64
     // output channels): 3 rows x 4 waves / 8 waves (two blocks per CU), 4 rows x 8 waves, 256 x 2 rows x 8 waves
     case 11: if (!tiles_ok(a.Wo, 128) || a.Ngemm % 64) break; return launch_igemm_halo<128, 64, 64, 32, 3>(a, st);
