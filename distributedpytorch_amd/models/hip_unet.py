@@ -425,13 +425,15 @@ class HipBlocks:
             ok = self._fusable[key] = K.bwd_fused_eligible(c.Cin, c.Cout, W, whole=whole)
         return ok
 
-    def conv_bwd(self, c: _Conv, g, x: torch.Tensor, mask: bool, split: int = 0, head=None, pool=None, first=None):
+    def conv_bwd(self, c: _Conv, g, x: torch.Tensor, mask: bool, split: int = 0, head=None, pool=None, first=None,
+                 sink=None):
         """Fused backward of ``c``: returns dx (ReLU-masked by ``x`` when ``mask``; with ``split`` the
         two dense halves of a concat gradient) and accumulates the weight and bias gradients.
         ``head``: ``g`` is the conv output and the segmentation-head backward is folded in; ``pool``:
         ``g`` is the skip gradient and the max-pool backward is folded in; ``first`` = (conv c1, its
         input x1): ``x = relu(c1(x1))`` and x1 needs no gradient, so dx is consumed in-kernel by
-        c1's weight/bias gradient and never stored (returns None)."""
+        c1's weight/bias gradient and never stored (returns None).  ``sink`` (:class:`K.SlabSink`): the weight
+        gradient slab rows go there, reduced by the sink's owner."""
         if first is not None:
             c1, x1 = first
             w1 = (x1, _grad(c1.mod.weight).view(-1), _grad(c1.mod.bias))
@@ -442,7 +444,7 @@ class HipBlocks:
             N, H, W = x.shape[:3]
             hi = torch.empty(N, H, W, c.Cin - split, dtype=torch.bfloat16, device=x.device)
             return K.conv_bwd_fused(g, x, self.wd(c), c.Kd, gw, gb, mask=False, dx2=hi, split=split)
-        return K.conv_bwd_fused(g, x, self.wd(c), c.Kd, gw, gb, mask=mask, head=head, pool=pool)
+        return K.conv_bwd_fused(g, x, self.wd(c), c.Kd, gw, gb, mask=mask, head=head, pool=pool, sink=sink)
 
     def bwd_conv(self, c: _Conv, g: torch.Tensor, x: torch.Tensor, st, *, mask: bool, below: _Conv = None,
                  stats: list = None, split: int = 0, x2: torch.Tensor = None, xbn: torch.Tensor = None):
@@ -536,10 +538,16 @@ class HipBlocks:
         return (K.USE_FUSED_HEAD_BWD and c2.Cin == 32 and c2.Cout == 32 and self.model.segmap.out_channels == 1
                 and self.fusable(c2, c1, W, whole=True))
 
-    def conv_wgrad(self, c: _Conv, g: torch.Tensor, x: torch.Tensor, gbn=None):
+    def conv_wgrad(self, c: _Conv, g: torch.Tensor, x: torch.Tensor, gbn=None, sink=None):
         """Weight + bias gradient of ``c`` (side stream).  ``gbn`` = (z, coef3): ``g`` is the gradient of
-        c's BatchNorm+ReLU output and dz is formed on load (:func:`K.wgrad` ``abn``; first conv only)."""
+        c's BatchNorm+ReLU output and dz is formed on load (:func:`K.wgrad` ``abn``; first conv only).
+        ``sink`` (:class:`K.SlabSink`): slab rows only; the caller reduces (:meth:`sink_reduce`)."""
         N, H, W = g.shape[:3]
+        if sink is not None:
+            gw, gb = _grad(c.mod.weight), _grad(c.mod.bias)
+            self._side_launch(lambda: K.wgrad(g, x, kind=0, grid=(N, H, W), M=c.Cout, Nc=c.Cs, s=1, pad=1, KW=3,
+                                              gw=gw.view(-1), gb=gb, Nreal=c.Cin, sink=sink), g, x)
+            return
         if gbn is not None:
             gw, gb = _grad(c.mod.weight), _grad(c.mod.bias)
             self._side_launch(lambda: K.wgrad(g, x, kind=0, grid=(N, H, W), M=c.Cout, Nc=c.Cs, s=1, pad=1, KW=3,
@@ -569,6 +577,10 @@ class HipBlocks:
         gw, gb = _grad(c.mod.weight), _grad(c.mod.bias)
         self._side_launch(lambda: K.wgrad(g, x, kind=0, grid=(N, H, W), M=c.Cout, Nc=c.Cs, s=1, pad=1, KW=3,
                                           gw=gw.view(-1), gb=gb, Nreal=c.Cin), g, x)
+
+    def sink_reduce(self, sink):
+        """Reduce a side-stream :class:`K.SlabSink` on the side stream (after every launch that fed it)."""
+        self._side_launch(sink.reduce)
 
     def join(self):
         """End of a block's backward: the compute stream waits for the side-stream weight gradients,
@@ -939,9 +951,23 @@ class _EncFn(torch.autograd.Function):
             # at b256).  Image chunks: conv1's weight gradient of chunk i (side stream) overlaps the fused
             # backward of chunk i + 1, leaving only the last chunk's exposed
             bounds = [N * i // chunks for i in range(chunks + 1)]
+            H = a.shape[1]
+            sink2 = sink1 = None
+            if K.CHUNK_SINK and K.wgrad_multi_eligible(c1.Cout, c1.Cs, W) and not K._ABLATE:
+                # one weight-gradient reduction per conv after the chunks instead of one per chunk per stream
+                # (each a presum + reduce; the side stream's waited ~0.45 ms for dispatch behind the next
+                # chunk's fused backward)
+                sizes = [n1 - n0 for n0, n1 in zip(bounds, bounds[1:])]
+                sink2 = K.SlabSink(sum(K.bwd_fused_rows(n, H, W, c2.Cin, c2.Cout) for n in sizes), c2.Cout, c2.Cin,
+                                   _grad(c2.mod.weight).view(-1), _grad(c2.mod.bias), c2.Cin)
+                sink1 = K.SlabSink(sum(K.wgrad_stream_rows(n, H, W, c1.Cout, c1.Cs) for n in sizes), c1.Cout, c1.Cs,
+                                   _grad(c1.mod.weight).view(-1), _grad(c1.mod.bias), c1.Cin)
             for n0, n1 in zip(bounds, bounds[1:]):
-                g1c = B.conv_bwd(c2, dskip[n0:n1], a[n0:n1], mask=True, pool=(code[n0:n1], dpooled[n0:n1]))
-                B.conv_wgrad(c1, g1c, x[n0:n1])
+                g1c = B.conv_bwd(c2, dskip[n0:n1], a[n0:n1], mask=True, pool=(code[n0:n1], dpooled[n0:n1]), sink=sink2)
+                B.conv_wgrad(c1, g1c, x[n0:n1], sink=sink1)
+            if sink2 is not None:
+                sink2.reduce()
+                B.sink_reduce(sink1)
             B.ready([c2.mod, c2.bn])
             B.ready([c1.mod, c1.bn])
             B.join()

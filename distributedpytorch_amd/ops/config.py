@@ -118,6 +118,8 @@ KNOBS = (
     Knob("wgrad_gemm_blocks", "DPA_WGRAD_GEMM_BLOCKS", 768, "target workgroups of a dense-GEMM weight gradient"),
     Knob("bwd_blocks", "DPA_BWD_BLOCKS", 1024, "minimum workgroups of a fused backward launch"),
     Knob("bwd_blocks_small", "DPA_BWD_BLOCKS_SMALL", 512, "the same for launches over < 2^25 pixels"),
+    Knob("chunk_sink", "DPA_NO_CHUNK_SINK", True, "first-level image chunks: each conv's weight-gradient slab rows "
+         "of all chunks in one buffer, reduced once after the chunks (kernels.SlabSink) instead of per chunk"),
     Knob("enc0_chunks", "DPA_ENC0_CHUNKS", 8, "first encoder level backward in this many image chunks, so the first "
          "conv's side-stream weight gradient of one chunk overlaps the next chunk's fused backward (1 = off); 8 vs "
          "4: step wall 86.02 / 85.98 vs 86.61 / 86.04 ms in kernel traces at b256 (profiles/enc0_chunks_r05.txt)"),
@@ -167,6 +169,7 @@ class KernelConfig:
     slpp: bool = True
     slp256: bool = False
     slp64: bool = False
+    chunk_sink: bool = True
     halo_cfg: int = 0
     wgrad_presum_y: int = 0
     side_wgrad: bool = True

@@ -116,6 +116,7 @@ USE_GLDS_BN = CFG.glds_bn              # BatchNorm partial sums in the row-block
 SIDE_WGRAD = CFG.side_wgrad            # weight gradients on a side stream (models/hip_unet.py)
 SIDE_PRIORITY = CFG.side_priority      # its HIP priority (torch convention: lower = higher, 0 = default)
 ENC0_CHUNKS = CFG.enc0_chunks          # first-level backward in image chunks (models/hip_unet.py _EncFn)
+CHUNK_SINK = CFG.chunk_sink            # ... with one weight-gradient reduction per conv after the chunks (SlabSink)
 WGRAD_STREAM_CFG = 0                   # row-streaming weight-gradient tile override (kbench A/B; 0 = auto)
 HALO_CFG = CFG.halo_cfg                # row-halo conv tile override (A/B; 0 = auto)
 USE_FUSED_HEAD = CFG.fused_head        # segmentation head + loss partials in the last decoder conv
@@ -401,7 +402,7 @@ def wgrad_bn_eligible(M: int, Nc: int, W: int) -> bool:
 
 def wgrad(A: torch.Tensor, B: torch.Tensor, *, kind: int, grid, M: int, Nc: int, s: int, pad: int, KW: int,
           gw: torch.Tensor, gb: Optional[torch.Tensor], Nreal: int, cfg: int = 0, target_blocks: int = 1024,
-          path: str = "auto", abn=None):
+          path: str = "auto", abn=None, sink: Optional["SlabSink"] = None):
     """Weight (+bias) gradient of a conv3x3 (kind 0), transposed conv 2x2/s2 (kind 1) or conv1x1
     (kind 2); accumulates into gw/gb.
 
@@ -409,7 +410,14 @@ def wgrad(A: torch.Tensor, B: torch.Tensor, *, kind: int, grid, M: int, Nc: int,
     generic per-tap gather kernel; ``stream`` / ``halo`` / ``generic`` force one.
     ``abn`` = (z, coef3): ``A`` is the ReLU-masked gradient of a BatchNorm output whose input is ``z``; the
     GEMM uses dz = coef3[m] A + coef3[M + m] z + coef3[2M + m] formed on load (:func:`bn_bwd_coef`), so the
-    dz pass over HBM never happens (:func:`wgrad_bn_eligible` shapes)."""
+    dz pass over HBM never happens (:func:`wgrad_bn_eligible` shapes).  ``sink`` (:class:`SlabSink`): the
+    row-streaming kernel writes its slab rows there and the reduction is left to the sink (row-streaming
+    shapes only: :func:`wgrad_multi_eligible`)."""
+    if sink is not None:
+        assert abn is None and kind == 0 and cfg == 0 and path == "auto" and not _ABLATE
+        assert wgrad_multi_eligible(M, Nc, grid[2]) and not wgrad_band_eligible(M, Nc, grid) and \
+            not wgrad_band128_eligible(M, Nc, grid) and not wgrad_gemm_eligible(M, Nc, grid), "sink: stream shapes"
+        return _wgrad_stream(A, B, grid=grid, M=M, Nc=Nc, gw=gw, gb=gb, Nreal=Nreal, sink=sink)
     if abn is not None:
         assert kind == 0 and cfg == 0 and path in ("auto", "stream") and wgrad_bn_eligible(M, Nc, grid[2])
         return _wgrad_stream(A, B, grid=grid, M=M, Nc=Nc, gw=gw, gb=gb, Nreal=Nreal, abn=abn)
@@ -696,13 +704,8 @@ def wgrad_multi(As, Bs, *, M: int, Nc: int, gw: torch.Tensor, gb: Optional[torch
     return _wgrad_stream(As[0], Bs[0], grid=(N, H, W), M=M, Nc=Nc, gw=gw, gb=gb, Nreal=Nreal, tabs=tabs)
 
 
-def _wgrad_stream(A, B, *, grid, M, Nc, gw, gb, Nreal, tabs=None, abn=None):
-    NA, HA, WA, CA, lda = _nhwc(A, "wgrad.A")
-    NB, HB, WB, CB, ldb = _nhwc(B, "wgrad.B")
-    N, Hg, Wg = grid
-    assert (HA, WA) == (Hg, Wg) == (HB, WB) and CA >= M and CB >= Nc
-    assert (NA == NB == N) or (tabs is not None and tabs[0].numel() == tabs[1].numel() == N)
-    assert gw.dtype == torch.float32 and gw.is_contiguous() and gw.numel() == M * Nreal * 9
+def _wgrad_stream_geom(N: int, Hg: int, Wg: int, M: int, Nc: int):
+    """(tile cfg, strip width, rows per split, images per split, slab rows) of a row-streaming weight gradient."""
     if Nc == 8:            # first layer (RGB padded to 8 channels): 32x16 tile, half the columns zero
         hcfg = 4
     elif WGRAD_STREAM_CFG in (1, 2, 3) and not (WGRAD_STREAM_CFG == 2 and M % 64) and not (WGRAD_STREAM_CFG == 3 and Nc % 64):
@@ -711,8 +714,6 @@ def _wgrad_stream(A, B, *, grid, M, Nc, gw, gb, Nreal, tabs=None, abn=None):
         hcfg = 2 if M % 64 == 0 else (3 if Nc % 64 == 0 else 1)
     bm, bn = {1: (32, 32), 2: (64, 32), 3: (32, 64), 4: (32, 16)}[hcfg]
     tiles = (M // bm) * (-(-Nc // bn))
-    L = _lib.lib()
-    st = _stream(A)
     nb = N
     # one launch for the whole batch: the kernel binds one image at a time (per-image extents below).
     # Strip width: 64 pixels unless 32-pixel strips waste less of a ragged row (the first layer's
@@ -726,8 +727,25 @@ def _wgrad_stream(A, B, *, grid, M, Nc, gw, gb, Nreal, tabs=None, abn=None):
     # slab reduction otherwise grows linearly with the batch
     ipb = max(1, (nb * per_img * tiles) // WGRAD_STREAM_BLOCKS)
     splits = -(-nb // ipb) * per_img
-    slab = torch.empty(splits * 9 * M * Nc + splits * M, dtype=torch.float32, device=A.device)
-    bslab = slab[splits * 9 * M * Nc:] if gb is not None else None
+    return hcfg, bp, rh, ipb, splits
+
+
+def _wgrad_stream(A, B, *, grid, M, Nc, gw, gb, Nreal, tabs=None, abn=None, sink=None):
+    NA, HA, WA, CA, lda = _nhwc(A, "wgrad.A")
+    NB, HB, WB, CB, ldb = _nhwc(B, "wgrad.B")
+    N, Hg, Wg = grid
+    assert (HA, WA) == (Hg, Wg) == (HB, WB) and CA >= M and CB >= Nc
+    assert (NA == NB == N) or (tabs is not None and tabs[0].numel() == tabs[1].numel() == N)
+    assert gw.dtype == torch.float32 and gw.is_contiguous() and gw.numel() == M * Nreal * 9
+    hcfg, bp, rh, ipb, splits = _wgrad_stream_geom(N, Hg, Wg, M, Nc)
+    L = _lib.lib()
+    st = _stream(A)
+    nb = N
+    if sink is not None:
+        slab, bslab = sink.take(splits, M, Nc, gb is not None)
+    else:
+        slab = torch.empty(splits * 9 * M * Nc + splits * M, dtype=torch.float32, device=A.device)
+        bslab = slab[splits * 9 * M * Nc:] if gb is not None else None
     a = WgradArgs(A.data_ptr(), B.data_ptr(), slab.data_ptr(), None if bslab is None else bslab.data_ptr(), lda, ldb,
                   nb, Hg, Wg, HA, WA, HB, WB, M, Nc, 1, 1, 3, 0, splits, _extent_bytes(1, HA, WA, CA, lda),
                   _extent_bytes(1, HB, WB, CB, ldb))
@@ -739,8 +757,52 @@ def _wgrad_stream(A, B, *, grid, M, Nc, gw, gb, Nreal, tabs=None, abn=None):
         assert coef3.dtype == torch.float32 and coef3.is_contiguous() and coef3.numel() == 3 * M and CA == M
         a.az, a.abn = z.data_ptr(), coef3.data_ptr()
     _check(L.dpa_wgrad_stream(ctypes.byref(a), c_int(hcfg), c_int(bp), c_int(rh), c_int(ipb), st), "wgrad_stream")
-    _check(L.dpa_wgrad_reduce(_p(slab), _p(bslab), _p(gw), _p(gb), c_int(splits), c_int(9), c_int(M), c_int(Nc),
-                              c_int(Nreal), c_int(0), st), "wgrad_reduce")
+    if sink is None:
+        _check(L.dpa_wgrad_reduce(_p(slab), _p(bslab), _p(gw), _p(gb), c_int(splits), c_int(9), c_int(M), c_int(Nc),
+                                  c_int(Nreal), c_int(0), st), "wgrad_reduce")
+
+
+def wgrad_stream_rows(N: int, H: int, W: int, M: int, Nc: int) -> int:
+    """Slab rows one :func:`wgrad` launch on the row-streaming kernel writes (:class:`SlabSink` sizing)."""
+    return _wgrad_stream_geom(N, H, W, M, Nc)[4]
+
+
+class SlabSink:
+    """The split-K weight-gradient slab rows of SEVERAL launches for one layer in one buffer, summed by a
+    single dpa_wgrad_reduce (fixed row order) instead of one per launch.  The first encoder level's backward
+    runs in image chunks (models/hip_unet.py ``_EncFn``) so each chunk's side-stream weight gradient overlaps
+    the next chunk's fused backward; per chunk both streams then paid a presum + reduce, the side one waiting
+    ~0.45 ms for dispatch behind the fused backward (profiles/hip_b256_512_summary_r06.txt).  The buffer is
+    allocated at the first :meth:`take`, in the stream context of that launch (so it lives in that stream's
+    pool), and :meth:`reduce` runs on the same stream."""
+
+    def __init__(self, rows: int, M: int, Nc: int, gw: torch.Tensor, gb: Optional[torch.Tensor], Nreal: int):
+        assert gw.dtype == torch.float32 and gw.is_contiguous() and gw.numel() == M * Nreal * 9
+        self.rows, self.M, self.Nc, self.Nreal, self.gw, self.gb = rows, M, Nc, Nreal, gw, gb
+        self.buf = None
+        self.used = 0
+
+    def take(self, n: int, M: int, Nc: int, bias: bool):
+        assert (M, Nc, bias) == (self.M, self.Nc, self.gb is not None), "slab sink: another layer's shape"
+        assert self.used + n <= self.rows, "slab sink: more rows than sized for"
+        if self.buf is None:
+            self.buf = torch.empty(self.rows * 9 * M * Nc + (self.rows * M if bias else 0), dtype=torch.float32,
+                                   device=self.gw.device)
+        slab = self.buf[self.used * 9 * M * Nc:]
+        bslab = self.buf[self.rows * 9 * M * Nc + self.used * M:] if bias else None
+        self.used += n
+        return slab, bslab
+
+    def reduce(self):
+        """Sum every row taken into gw / gb (on the current stream) and release the buffer."""
+        if self.buf is None:
+            return
+        M, Nc = self.M, self.Nc
+        bslab = self.buf[self.rows * 9 * M * Nc:] if self.gb is not None else None
+        _check(_lib.lib().dpa_wgrad_reduce(_p(self.buf), _p(bslab), _p(self.gw), _p(self.gb), c_int(self.used), c_int(9),
+                                           c_int(M), c_int(Nc), c_int(self.Nreal), c_int(0),
+                                           _stream(self.gw)), "wgrad_reduce(sink)")
+        self.buf = None
 
 
 # ------------------------------------------------------------------------------- fused conv backward
@@ -772,11 +834,31 @@ def bwd_pool_foldable(ci: int, co: int) -> bool:
     return bool(_lib.lib().dpa_bwd_stream_pool_ok(c_int(ci), c_int(co)))
 
 
+def _bwd_rows(N: int, H: int, W: int, bp: int, target_blocks: int = 0):
+    """(rows per block, blocks) of a fused-backward launch: whole image columns per block; the rows are split
+    only when the batch gives too few blocks."""
+    strips = -(-W // bp)
+    if not target_blocks:
+        target_blocks = BWD_BLOCKS if (_BWD_BLOCKS_SET or N * H * W >= BWD_SMALL_PIXELS) else BWD_BLOCKS_SMALL
+    segs = max(1, min(H, -(-target_blocks // max(1, N * strips))))
+    rh = -(-H // segs)
+    return rh, N * strips * (-(-H // rh))
+
+
+def bwd_fused_rows(N: int, H: int, W: int, CI: int, CO: int) -> int:
+    """Slab rows one :func:`conv_bwd_fused` launch writes (:class:`SlabSink` sizing)."""
+    bp = ctypes.c_int(0)
+    pg = _lib.lib().dpa_bwd_stream_geom(c_int(CI), c_int(CO), ctypes.byref(bp))
+    assert pg > 0
+    return _bwd_rows(N, H, W, bp.value)[1] * pg
+
+
 def conv_bwd_fused(g: Optional[torch.Tensor], x: torch.Tensor, wd: torch.Tensor, Kd: int, gw: torch.Tensor,
                    gb: Optional[torch.Tensor], *, mask: bool, dx: Optional[torch.Tensor] = None,
                    dx2: Optional[torch.Tensor] = None, split: int = 0, target_blocks: int = 0, head=None,
                    pool=None, w1=None, bn=None, bn_stats: bool = False, x2: Optional[torch.Tensor] = None,
-                   xbn: Optional[torch.Tensor] = None, ybn: Optional[torch.Tensor] = None):
+                   xbn: Optional[torch.Tensor] = None, ybn: Optional[torch.Tensor] = None,
+                   sink: Optional["SlabSink"] = None):
     """Backward of ``y = conv3x3(x) (+bias)`` in one pass (csrc/bwd_stream.hip): returns
     ``dx = conv3x3^T(g)`` (times ``x > 0`` when ``mask``; with ``dx2``/``split`` the channels
     ``>= split`` go to ``dx2``) and ACCUMULATES the weight gradient into ``gw`` (PyTorch OIHW
@@ -809,7 +891,9 @@ def conv_bwd_fused(g: Optional[torch.Tensor], x: torch.Tensor, wd: torch.Tensor,
     ``x2``: dual input -- the conv input is [x | x2] (two [N,H,W,32] tensors of identical layout), as
     :func:`igemm` ``x2``; the kernel's x loader reads both.  ``xbn`` (with ``bn`` and ``bn_stats``):
     ``x`` is the pre-BatchNorm output z of the layer below and the kernel uses relu(z * xbn[c] +
-    xbn[CI + c]) as the conv input, dx mask and BN-statistics operand (:func:`igemm` ``xbn``)."""
+    xbn[CI + c]) as the conv input, dx mask and BN-statistics operand (:func:`igemm` ``xbn``).
+    ``sink`` (:class:`SlabSink`): the weight / bias gradient slab rows go there and the sink reduces them
+    later (not with ``w1`` or ``head``)."""
     Nx, Hx, Wx, CI, ldx = _nhwc(x, "bwd.x")
     if x2 is not None:
         assert _nhwc(x2, "bwd.x2") == (Nx, Hx, Wx, CI, ldx) and CI == 32, "dual input: two [N,H,W,32]"
@@ -854,16 +938,14 @@ def conv_bwd_fused(g: Optional[torch.Tensor], x: torch.Tensor, wd: torch.Tensor,
         assert C1 >= CI
         ldy2, epi = 0, (0 if mask else 2)
     assert dx is None or tuple(dx.shape[:3]) == (N, H, W)
-    strips = -(-W // bp.value)
-    # whole image columns per block; split the rows only when the batch gives too few blocks
-    if not target_blocks:
-        target_blocks = BWD_BLOCKS if (_BWD_BLOCKS_SET or N * H * W >= BWD_SMALL_PIXELS) else BWD_BLOCKS_SMALL
-    segs = max(1, min(H, -(-target_blocks // max(1, N * strips))))
-    rh = -(-H // segs)
-    nblk = N * strips * (-(-H // rh))
-    slab = torch.empty(nblk * pg * 9 * CO * CI + (nblk * pg * CO if gb is not None else 0), dtype=torch.float32,
-                       device=x.device)
-    bslab = slab[nblk * pg * 9 * CO * CI:] if gb is not None else None
+    rh, nblk = _bwd_rows(N, H, W, bp.value, target_blocks)
+    if sink is not None:
+        assert w1 is None and head is None, "slab sink: plain / split / pool / BN modes"
+        slab, bslab = sink.take(nblk * pg, CO, CI, gb is not None)
+    else:
+        slab = torch.empty(nblk * pg * 9 * CO * CI + (nblk * pg * CO if gb is not None else 0), dtype=torch.float32,
+                           device=x.device)
+        bslab = slab[nblk * pg * 9 * CO * CI:] if gb is not None else None
     a = BwdArgs(None if g is None else g.data_ptr(), x.data_ptr(), wd.data_ptr(), None if dx is None else dx.data_ptr(),
                 None if dx2 is None else dx2.data_ptr(),
                 slab.data_ptr(), None if bslab is None else bslab.data_ptr(), ldg, ldx, ldy, ldy2, split, Kd,
@@ -929,8 +1011,9 @@ def conv_bwd_fused(g: Optional[torch.Tensor], x: torch.Tensor, wd: torch.Tensor,
     if hslab is not None:
         _check(L.dpa_head_grad_from_slab(_p(hslab), c_int(nblk), c_int(CO), _p(hslab[nblk * (CO + 1):]), _p(hgw),
                                          _p(hgb), st), "head_grad_from_slab")
-    _check(L.dpa_wgrad_reduce(_p(slab), _p(bslab), _p(gw), _p(gb), c_int(nblk * pg), c_int(9), c_int(CO), c_int(CI),
-                              c_int(CI), c_int(0), st), "wgrad_reduce(bwd_stream)")
+    if sink is None:
+        _check(L.dpa_wgrad_reduce(_p(slab), _p(bslab), _p(gw), _p(gb), c_int(nblk * pg), c_int(9), c_int(CO), c_int(CI),
+                                  c_int(CI), c_int(0), st), "wgrad_reduce(bwd_stream)")
     if slab1 is not None:
         _check(L.dpa_wgrad_reduce(_p(slab1), _p(slab1[nblk * 9 * CI * 8:]), _p(gw1), _p(gb1), c_int(nblk),
                                   c_int(9), c_int(CI), c_int(8), c_int(creal), c_int(0), st), "wgrad_reduce(bwd_stream.w1)")

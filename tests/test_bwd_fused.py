@@ -236,11 +236,13 @@ def test_conv_bwd_fused_batchnorm_modes(hip_lib, N, H, W, Cin, Cout, epi):
         assert _rel(sums[1], (dxa * xs).sum((0, 1, 2))) < 1e-3
 
 
+@pytest.mark.parametrize("sink", [True, False])
 @pytest.mark.parametrize("chunks", [2, 4])
-def test_first_level_backward_in_image_chunks(hip_lib, chunks):
+def test_first_level_backward_in_image_chunks(hip_lib, chunks, sink):
     """DPA_ENC0_CHUNKS: the first encoder level's fused (pool-folded) backward and the first conv's
     side-stream weight gradient run per image chunk; every gradient equals the one-launch backward up to
-    fp32 summation order (the weight gradients are reduced per chunk)."""
+    fp32 summation order -- with the slab rows of all chunks reduced once per conv (kernels.SlabSink,
+    DPA_NO_CHUNK_SINK=0) or per chunk."""
     from distributedpytorch_amd.config import TrainConfig
     from distributedpytorch_amd.models.unet import build_model
     from distributedpytorch_amd.ops import kernels as K
@@ -252,7 +254,8 @@ def test_first_level_backward_in_image_chunks(hip_lib, chunks):
     img, mask = synthetic_batch(8, 128, 128, 3, seed=4)
     x, t = img.cuda(), mask.float().unsqueeze(1).cuda()
     grads = []
-    old = K.ENC0_CHUNKS
+    old, old_sink = K.ENC0_CHUNKS, K.CHUNK_SINK
+    K.CHUNK_SINK = sink
     try:
         for c in (1, chunks):
             K.ENC0_CHUNKS = c
@@ -261,7 +264,7 @@ def test_first_level_backward_in_image_chunks(hip_lib, chunks):
             torch.cuda.synchronize()
             grads.append(st.space.grad.detach().clone())
     finally:
-        K.ENC0_CHUNKS = old
+        K.ENC0_CHUNKS, K.CHUNK_SINK = old, old_sink
     g0, g1 = grads
     for i, n in enumerate(st.space.names):
         o0, o1 = st.space.slice_of(i)
