@@ -299,9 +299,46 @@ struct PackDesc {
   long long dst;   // element offset in the packed bf16 buffer
   int mode, Cout, Cin, Cs, Ngemm, Kpad;
 };
+// Conv2d modes 0 / 1 go one thread per (GEMM row, channel) over all 9 taps: the thread reads the 9 contiguous
+// taps W[co][ci][0..8] (36 B; consecutive lanes read consecutive 36-B runs in mode 0) and writes 9 packed values,
+// each store coalesced across lanes (consecutive channels).  The per-element form below gathered mode 1 with a
+// Cin*36-B lane stride (one cache line per element): 1.08 ms per UNet-XL step for ~0.25 GB of weights.
+// 32-bit index math throughout (the host checks Ngemm * Kpad < 2^31).
+template <typename OutT>
+__device__ __forceinline__ void pack_store(OutT* p, long idx, float v) {
+  if constexpr (std::is_same<OutT, float>::value) p[idx] = v;
+  else p[idx] = f2bf(v);
+}
 template <typename OutT>
 __global__ __launch_bounds__(256) void pack_kernel(OutT* __restrict__ packed, const PackDesc* __restrict__ descs) {
   const PackDesc d = descs[blockIdx.y];
+  const unsigned stride = gridDim.x * blockDim.x, t0 = blockIdx.x * blockDim.x + threadIdx.x;
+  if (d.mode == 0 || d.mode == 1) {
+    const float* W = reinterpret_cast<const float*>(d.src);
+    OutT* dst = packed + d.dst;
+    const int C = d.mode == 0 ? d.Cs : d.Cout;      // channels per tap in the packed row
+    const unsigned rows = (unsigned)d.Ngemm * (unsigned)C;
+    for (unsigned i = t0; i < rows; i += stride) {
+      const unsigned n = i / (unsigned)C, c = i - n * (unsigned)C;
+      float w[9];
+      // mode 0: row n = co, channel c = ci (ci >= Cin: first-layer padding); mode 1: row n = ci (n >= Cin:
+      // GEMM-N padding), channel c = co, taps flipped
+      const bool ok = d.mode == 0 ? (int)c < d.Cin : (int)n < d.Cin;
+      const float* src = W + (d.mode == 0 ? ((long)n * d.Cin + c) * 9 : ((long)c * d.Cin + n) * 9);
+#pragma unroll
+      for (int t = 0; t < 9; ++t) w[t] = ok ? src[t] : 0.f;
+      const long row = (long)n * d.Kpad;
+#pragma unroll
+      for (int t = 0; t < 9; ++t) pack_store(dst, row + t * C + c, d.mode == 0 ? w[t] : w[8 - t]);
+    }
+    // K padding columns [9 C, Kpad) of every row
+    const unsigned padw = (unsigned)(d.Kpad - 9 * C), npad = (unsigned)d.Ngemm * padw;
+    for (unsigned i = t0; i < npad; i += stride) {
+      const unsigned n = i / padw, k = 9 * C + (i - n * padw);
+      pack_store(dst, (long)n * d.Kpad + k, 0.f);
+    }
+    return;
+  }
   const long tot = (long)d.Ngemm * d.Kpad;
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < tot; i += (long)gridDim.x * blockDim.x) {
     const int n = (int)(i / d.Kpad), k = (int)(i - (long)n * d.Kpad);
@@ -331,6 +368,7 @@ __global__ __launch_bounds__(256) void pack_kernel(OutT* __restrict__ packed, co
 DPA_API int dpa_pack_weights(const float* flat, bf16_t* packed, const void* descs, int ndesc, long long max_elems,
                              hipStream_t st) {
   if (ndesc <= 0) return 0;
+  if (max_elems >= (1ll << 31)) return (int)hipErrorInvalidValue;   // 32-bit index math
   dim3 grid(dpa_grid(max_elems, 256, 1024), ndesc);
   (void)flat;
   hipLaunchKernelGGL(pack_kernel<bf16_t>, grid, dim3(256), 0, st, packed, reinterpret_cast<const PackDesc*>(descs));
@@ -340,6 +378,7 @@ DPA_API int dpa_pack_weights(const float* flat, bf16_t* packed, const void* desc
 // n >= Cin (GEMM-N padded to a multiple of 32) are zero
 DPA_API int dpa_pack_weights_f32(float* packed, const void* descs, int ndesc, long long max_elems, hipStream_t st) {
   if (ndesc <= 0) return 0;
+  if (max_elems >= (1ll << 31)) return (int)hipErrorInvalidValue;   // 32-bit index math
   dim3 grid(dpa_grid(max_elems, 256, 1024), ndesc);
   hipLaunchKernelGGL(pack_kernel<float>, grid, dim3(256), 0, st, packed, reinterpret_cast<const PackDesc*>(descs));
   return (int)hipGetLastError();

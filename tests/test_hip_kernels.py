@@ -53,6 +53,23 @@ def _pack_one(mode, w, cin_pad=None):
     return packed, ngemm, kpad
 
 
+@pytest.mark.parametrize("Cout,Cin,cs", [(32, 3, 8), (64, 32, 32), (96, 160, 160), (256, 512, 512)])
+def test_pack_weights_conv_layouts(hip_lib, Cout, Cin, cs):
+    """The weight pack kernel's conv3x3 forward (mode 0) and dgrad (mode 1) layouts, bit for bit against a torch
+    construction: dst[co][tap*Cs + ci] = W[co][ci][tap] (ci >= Cin zero) and dst[ci][tap*Cout + co] =
+    W[co][ci][8 - tap]; K padding columns zero."""
+    torch.manual_seed(5)
+    w = torch.randn(Cout, Cin, 3, 3)
+    p0, ng0, kp0 = _pack_one(0, w, cs)
+    r0 = torch.zeros(Cout, kp0)
+    r0[:, :9 * cs].view(Cout, 9, cs)[:, :, :Cin] = w.reshape(Cout, Cin, 9).permute(0, 2, 1)
+    assert torch.equal(p0.view(ng0, kp0).cpu(), r0.to(torch.bfloat16))
+    p1, ng1, kp1 = _pack_one(1, w)
+    r1 = torch.zeros(Cin, kp1)
+    r1[:, :9 * Cout].view(Cin, 9, Cout)[:] = w.reshape(Cout, Cin, 9).flip(2).permute(1, 2, 0)
+    assert torch.equal(p1.view(ng1, kp1).cpu(), r1.to(torch.bfloat16))
+
+
 @pytest.mark.parametrize("N,H,W,Cin,Cout,cfg", [
     (2, 17, 23, 3, 32, 0),      # first layer: 3 -> padded 8 input channels, partial tiles
     (2, 16, 16, 32, 64, 0),
