@@ -887,9 +887,11 @@ __global__ __launch_bounds__(256 * WCS) void igemm_stream_kernel(IgemmArgs a) {
 // (p + kw) of slot (r + kh): no im2col, 3 k-steps (taps 9..11 have zero weights).
 // BNS: the conv is followed by BatchNorm (bias, no ReLU): also sum y, sum y^2 of the stored bf16 output per
 // block -> a.bnslab[block][2][32], as igemm_stream_kernel's EPI 4 (no statistics pass over the 512^2 output)
-template <int BP, int RH, bool BNS = false>
+// NG = 64: the UNet-XL first conv (3 -> 64), the same schedule with twice the output tiles per wave.
+template <int BP, int RH, bool BNS = false, int NG = 32>
 __global__ __launch_bounds__(256) void igemm_stream8_kernel(IgemmArgs a) {
-  constexpr int NG = 32, HR = BP + 2, SLOT = HR * 16;
+  static_assert(NG == 32 || NG == 64, "output channels");
+  constexpr int HR = BP + 2, SLOT = HR * 16;
   constexpr int WP = BP / 4, TP = WP / 16, TC = NG / 16;
   __shared__ __attribute__((aligned(16))) char lds[3 * NG * 64 + 4 * SLOT];
   char* const Wimg = lds;
@@ -1037,14 +1039,14 @@ __global__ __launch_bounds__(256) void igemm_stream8_kernel(IgemmArgs a) {
   }
 }
 
-template <int BP, int RH>
+template <int BP, int RH, int NG>
 static int launch_igemm_stream8(const IgemmArgs& a, hipStream_t st) {
   const int grid = a.N * ((a.Ho + RH - 1) / RH) * ((a.Wo + BP - 1) / BP);
   if (a.bnslab) {   // conv followed by BatchNorm: statistics in the epilogue (bias only, plain store)
     if (a.relu || a.mask || a.accumulate || a.y2 || a.hslab) return (int)hipErrorInvalidValue;
-    hipLaunchKernelGGL((igemm_stream8_kernel<BP, RH, true>), dim3(grid), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((igemm_stream8_kernel<BP, RH, true, NG>), dim3(grid), dim3(256), 0, st, a);
   } else {
-    hipLaunchKernelGGL((igemm_stream8_kernel<BP, RH>), dim3(grid), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((igemm_stream8_kernel<BP, RH, false, NG>), dim3(grid), dim3(256), 0, st, a);
   }
   return (int)hipGetLastError();
 }
@@ -1103,7 +1105,7 @@ static int stream_auto_variant(const IgemmArgs& a) {
 // blocks the streaming launch of `a` (variant 0) uses -- rows of the fused head's slab
 DPA_API int dpa_igemm_stream_blocks(const IgemmArgs* args) {
   const IgemmArgs& a = *args;
-  if (a.Cs == 8 && a.Ngemm == 32) return a.N * ((a.Ho + 31) / 32) * ((a.Wo + 127) / 128);   // igemm_stream8<128, 32>
+  if (a.Cs == 8 && (a.Ngemm == 32 || a.Ngemm == 64)) return a.N * ((a.Ho + 31) / 32) * ((a.Wo + 127) / 128);   // igemm_stream8<128, 32>
   const int variant = stream_auto_variant(a);
   const int bp = (variant == 1 || variant == 3) ? 128 : 64;
   const int strips = (a.Wo + bp - 1) / bp;
@@ -1124,7 +1126,9 @@ DPA_API int dpa_igemm_stream(const IgemmArgs* args, int variant, hipStream_t st)
       (a.pool && ((a.ldp & 3) || (a.Wo & 1) || !a.relu)) || (a.x2 && (a.Cs != 64 || a.ldx < 32)) ||
       (a.xbn && (a.bnslab == nullptr || a.mask || a.pool || a.hslab || a.Cs == 8)))     // BN-on-load: the EPI 4 kernels only
     return (int)hipErrorInvalidValue;
-  if (a.Cs == 8 && a.Ngemm == 32 && !a.pool) return launch_igemm_stream8<128, 32>(a, st);
+  if (a.Cs == 8 && a.Ngemm == 32 && !a.pool) return launch_igemm_stream8<128, 32, 32>(a, st);
+  if (a.Cs == 8 && a.Ngemm == 64 && !a.pool && !a.hslab && !a.mask && !a.accumulate && !a.y2 && !a.x2)
+    return launch_igemm_stream8<128, 32, 64>(a, st);
   if (variant == 0) variant = stream_auto_variant(a);
   const int bp = (variant == 1 || variant == 3) ? 128 : 64;
   const long blocks32 = (long)a.N * ((a.Ho + 31) / 32) * ((a.Wo + bp - 1) / bp);

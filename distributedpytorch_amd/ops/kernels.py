@@ -274,7 +274,7 @@ def igemm(x: torch.Tensor, wpacked: torch.Tensor, y: torch.Tensor, *, Ngemm: int
         return a
 
     conv3 = mode == 0 and KH == 3 and stride == 1 and cfg == 0
-    stream_ok = (Ngemm in (32, 64) and Cs in (32, 64)) or (Ngemm == 32 and Cs == 8 and pool is None)
+    stream_ok = (Ngemm in (32, 64) and Cs in (32, 64)) or (Ngemm in (32, 64) and Cs == 8 and pool is None)
     # ---- per-image kernels (row-streaming, row-halo): each block binds one image, so ONE launch
     # covers the whole batch (no 2 GiB chunks, no chunk tails)
     per_image_ok = Hs * Ws * ldx * 2 < _MAX_BYTES

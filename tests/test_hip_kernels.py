@@ -92,6 +92,7 @@ def test_pack_weights_conv_layouts(hip_lib, Cout, Cin, cs):
     (2, 2, 128, 64, 128, "auto"),
     (2, 5, 128, 3, 32, "stream"),          # first layer (8 padded channels) streaming kernel
     (1, 34, 256, 3, 32, "auto"),
+    (2, 5, 128, 3, 64, "stream"), (1, 35, 256, 3, 64, "auto"), (1, 5, 200, 3, 64, "stream"),   # UNet-XL first conv
     # ragged rows (640x960 widths 480 / 240 / 120 and others): a partial last strip / tile
     (2, 5, 96, 32, 32, "stream"), (1, 6, 240, 64, 64, "stream"), (1, 4, 480, 32, 64, "auto"),
     (1, 4, 240, 64, 128, "halo"), (2, 3, 120, 128, 128, "halo"), (1, 3, 480, 64, 32, "halo"),
