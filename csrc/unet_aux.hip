@@ -620,6 +620,45 @@ DPA_API int dpa_zero(void* p, long long nbytes, hipStream_t st) {
   return (int)hipMemsetAsync(p, 0, (size_t)nbytes, st);
 }
 
+// Per-channel sums of a bf16 NHWC tensor (P pixels, C channels at row stride ld), ADDED to out[C]: the bias
+// gradient of a transposed conv whose weight gradient runs on the dense GEMM (wgrad_gemm.hip up mode, which
+// has no bias column).  Thread t owns the 8-channel chunk t % (C / 8) (C / 8 divides 256), so per-thread sums
+// reduce per chunk in thread order in LDS; one slab row per block, then slab_sum_kernel (fixed order).
+__global__ __launch_bounds__(256) void chan_sum_bf16_kernel(const bf16_t* __restrict__ g, long P, int C, int ld,
+                                                            float* __restrict__ slab) {
+  const int CC = C >> 3;
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const long tot = P * CC;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < tot; i += (long)gridDim.x * 256) {
+    const long px = i / CC;
+    const int cc = (int)(i - px * CC);
+    const uint4 v = *reinterpret_cast<const uint4*>(g + px * ld + cc * 8);
+    const unsigned* u = &v.x;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      s[2 * k] += lo_bf(u[k]);
+      s[2 * k + 1] += hi_bf(u[k]);
+    }
+  }
+  __shared__ float red[256][9];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) red[threadIdx.x][k] = s[k];
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += 256) {
+    const int chunk = c >> 3, k = c & 7;
+    float t = 0.f;
+    for (int th = chunk; th < 256; th += CC) t += red[th][k];
+    slab[(long)blockIdx.x * C + c] = t;
+  }
+}
+DPA_API int dpa_chan_sum_bf16(const bf16_t* g, long long P, int C, int ld, float* slab, int nblk, float* out,
+                              hipStream_t st) {
+  if ((C & 7) || (ld & 7) || C > 2048 || (256 % (C / 8)) || nblk < 1) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(chan_sum_bf16_kernel, dim3(nblk), dim3(256), 0, st, g, (long)P, C, ld, slab);
+  hipLaunchKernelGGL(slab_sum_kernel, dim3(C), dim3(256), 0, st, slab, nblk, C, out, 1);
+  return (int)hipGetLastError();
+}
+
 DPA_API int dpa_slab_sum(const float* slab, int nblk, int K, float* out, hipStream_t st) {
   hipLaunchKernelGGL(slab_sum_kernel, dim3(K), dim3(256), 0, st, slab, nblk, K, out, 0);
   return (int)hipGetLastError();

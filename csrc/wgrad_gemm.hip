@@ -55,7 +55,7 @@ __device__ __forceinline__ bf16x8_t tr_join(s16x4_t v0, s16x4_t v1) {
 // are consecutive pixels of the split's contiguous images) and its (h, w) for the zero-padding masks
 struct WKC {
   unsigned oa, ob;
-  int h, w;
+  int h, w, n;            // n: image inside the split (the transposed-conv mode's B addressing)
 };
 
 }  // namespace
@@ -64,7 +64,12 @@ __global__ __launch_bounds__(512) void wgrad_gemm_kernel(WgradArgs a) {
   __shared__ __attribute__((aligned(16))) char lds[2 * WG_STAGE];
 
   const int H = a.Hg, W = a.Wg, HW = H * W;
-  const int Ncols = 9 * a.Nc;
+  // up mode (KW == 2): the weight gradient of a transposed conv k2 s2, dW[ci][tap][co] = sum_p x[p][ci] *
+  // g[2p + (i, j)][co] -- A = the layer input x on the low-resolution grid, B = the output gradient on the
+  // 2x grid, 4 taps at (2h + i, 2w + j); no padding
+  const bool up = a.KW == 2;
+  const int T = up ? 4 : 9;
+  const int Ncols = T * a.Nc;
   const int nmt = a.M / 256, nnt = (Ncols + 255) / 256, tiles = nmt * nnt;
   const int bid = xcd_remap(blockIdx.x, tiles * a.splits);
   const int split = bid / tiles, tile = bid - split * tiles;   // a split's tiles share an XCD's L2
@@ -87,7 +92,7 @@ __global__ __launch_bounds__(512) void wgrad_gemm_kernel(WgradArgs a) {
   const __amdgpu_buffer_rsrc_t ar = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(a.atab ? a.atab[nimg0] : a.A + (long)nimg0 * HW * a.lda), 0, (int)a.abytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t br = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(a.btab ? a.btab[nimg0] : a.B + (long)nimg0 * HW * a.ldb), 0, (int)a.bbytes, 0x00020000);
+      (void*)(a.btab ? a.btab[nimg0] : a.B + (long)nimg0 * (up ? 4 : 1) * HW * a.ldb), 0, (int)a.bbytes, 0x00020000);
 
   // ---- per-lane DMA constants.  Half-tile image = 16 instructions of 1 KB (4 pixel rows x 16
   // chunks); wave wid issues instructions wid and 8 + wid.  Lane l: pixel row r = 4 ins + (l >> 4),
@@ -110,7 +115,8 @@ __global__ __launch_bounds__(512) void wgrad_gemm_kernel(WgradArgs a) {
       colok[h][j] = col < Ncols;
       dh[h][j] = lh + kh - 1;
       dw[h][j] = lw + kw - 1;
-      laneB[h][j] = (unsigned)((((lh + kh - 1) * W + (lw + kw - 1)) * a.ldb + ci) * 2);
+      laneB[h][j] = up ? (unsigned)((((2 * lh + (tap >> 1)) * 2 * W + 2 * lw + (tap & 1)) * a.ldb + ci) * 2)
+                       : (unsigned)((((lh + kh - 1) * W + (lw + kw - 1)) * a.ldb + ci) * 2);
     }
   }
   const unsigned rowA = (unsigned)(64 * a.lda * 2), rowB = (unsigned)(64 * a.ldb * 2);   // bytes per K-step
@@ -124,7 +130,10 @@ __global__ __launch_bounds__(512) void wgrad_gemm_kernel(WgradArgs a) {
     } else {
       c.h += 64 / W;
     }
-    if (c.h == H) c.h = 0;
+    if (c.h == H) {
+      c.h = 0;
+      ++c.n;
+    }
     return c;
   };
   auto issueA = [&](int h, int buf, WKC c) {
@@ -134,6 +143,12 @@ __global__ __launch_bounds__(512) void wgrad_gemm_kernel(WgradArgs a) {
   };
   auto issueB = [&](int h, int buf, WKC c) {
     char* base = lds + buf * WG_STAGE + (2 + h) * WG_HALF;
+    if (up) {
+      const unsigned ob = (unsigned)((((c.n * 2 * H + 2 * c.h) * 2 * W) + 2 * c.w) * a.ldb * 2);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) dma16(br, base + (j * 8 + wid) * 1024, colok[h][j] ? ob + laneB[h][j] : 0x80000000u);
+      return;
+    }
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int hh = c.h + dh[h][j], ww = c.w + dw[h][j];
@@ -152,7 +167,7 @@ __global__ __launch_bounds__(512) void wgrad_gemm_kernel(WgradArgs a) {
   const s16x8_t ones_s = {0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80};   // bf16 1.0
   const bf16x8_t ones = __builtin_bit_cast(bf16x8_t, ones_s);
 
-  WKC k0{0u, 0u, 0, 0};
+  WKC k0{0u, 0u, 0, 0, 0};
   WKC k1 = knext(k0);
   issueA(0, 0, k0);
   issueB(0, 0, k0);
@@ -375,7 +390,7 @@ __global__ __launch_bounds__(512) void wgrad_gemm_kernel(WgradArgs a) {
       const int col = n0 + qb * 128 + wp * 32 + ip * 16 + (lane & 15);
       if (col >= Ncols) continue;
       const int tap = col / a.Nc, ci = col - tap * a.Nc;
-      float* dst = a.slab + (((long)split * 9 + tap) * a.M + m0 + wc * 64 + 4 * (lane >> 4)) * a.Nc + ci;
+      float* dst = a.slab + (((long)split * T + tap) * a.M + m0 + wc * 64 + 4 * (lane >> 4)) * a.Nc + ci;
 #pragma unroll
       for (int qa = 0; qa < 2; ++qa)
 #pragma unroll
@@ -401,6 +416,20 @@ __global__ __launch_bounds__(512) void wgrad_gemm_kernel(WgradArgs a) {
 DPA_API int dpa_wgrad_gemm(const WgradArgs* args, hipStream_t st) {
   const WgradArgs& a = *args;
   const int ips = a.pix_per_split;
+  if (a.KW == 2) {
+    // transposed conv k2 s2 (up mode): A = x [N][Hg][Wg][lda] (M = its channels), B = the output gradient
+    // [N][2Hg][2Wg][ldb]; columns (tap, co), 4 taps; no bias from this kernel (bslab must be null)
+    if ((a.M % 256) || ((4 * a.Nc) % 256) || (a.Nc % 8) || (a.lda & 7) || (a.ldb & 7) || a.s != 2 || a.pad != 0 ||
+        a.bslab != nullptr || a.atab || a.btab || a.HA != a.Hg || a.WA != a.Wg || a.HB != 2 * a.Hg ||
+        a.WB != 2 * a.Wg || (a.Wg % 64 && (a.Wg > 64 || 64 % a.Wg)) || ((a.Hg * a.Wg) % 64) || ips < 1 ||
+        a.splits != (a.N + ips - 1) / ips || (long)ips * a.Hg * a.Wg / 64 < 2 ||
+        (long)((a.N - 1) % ips + 1) * a.Hg * a.Wg / 64 < 2 || a.lda < a.M || a.ldb < a.Nc ||
+        (long)ips * a.Hg * a.Wg * a.lda * 2 > (long)a.abytes || (long)ips * 4 * a.Hg * a.Wg * a.ldb * 2 > (long)a.bbytes)
+      return (int)hipErrorInvalidValue;
+    const int tiles = (a.M / 256) * (4 * a.Nc / 256);
+    hipLaunchKernelGGL(wgrad_gemm_kernel, dim3(tiles * a.splits), dim3(512), 0, st, a);
+    return (int)hipGetLastError();
+  }
   if ((a.M % 256) || (a.Nc % 8) || (a.lda & 7) || (a.ldb & 7) || a.s != 1 || a.pad != 1 || a.KW != 3 ||
       a.HA != a.Hg || a.WA != a.Wg || a.HB != a.Hg || a.WB != a.Wg || (a.Wg % 64 && a.Wg != 32) ||
       ((a.Hg * a.Wg) % 64) || (!a.atab != !a.btab) || ips < 1 || a.splits != (a.N + ips - 1) / ips ||

@@ -51,7 +51,7 @@ def lib():
 
 def _declare(L):
     for name in ("dpa_version", "dpa_igemm", "dpa_wgrad", "dpa_wgrad_reduce", "dpa_input_nhwc8", "dpa_maxpool2",
-                 "dpa_pool_bwd", "dpa_pool_bwd_code_blocks", "dpa_pack_weights", "dpa_head_fwd", "dpa_head_bwd", "dpa_adam_flat",
+                 "dpa_pool_bwd", "dpa_pool_bwd_code_blocks", "dpa_chan_sum_bf16", "dpa_pack_weights", "dpa_head_fwd", "dpa_head_bwd", "dpa_adam_flat",
                  "dpa_igemm_halo", "dpa_wgrad_halo", "dpa_igemm_stream", "dpa_wgrad_stream", "dpa_wgrad_gemm", "dpa_wgrad_band", "dpa_wgrad_band128", "dpa_adam_flat_dev", "dpa_igemm_glds",
                  "dpa_loss_finish", "dpa_loss_grad", "dpa_pool_bwd_code", "dpa_bn_fwd", "dpa_bn_bwd", "dpa_bn_bwd_coef",
                  "dpa_up2_fwd", "dpa_up2_bwd", "dpa_deconv_bwd", "dpa_deconv_fwd", "dpa_slab_sum",

@@ -51,6 +51,8 @@ KNOBS = (
          "ping-pong 64 x 512 (igemm_slp_kernel<EP, 64>, cfg 19) instead of the row-halo conv. Off: bitwise equal but "
          "slower at b256 (3619 vs 3113 us at 256^2 128 -> 64, 1015 vs 875 us at the 128^2 dgrad; 16 MFMAs per phase do "
          "not cover the phase barriers, profiles/kbench_slp64_halo_r06.txt)"),
+    Knob("wgrad_up", "DPA_NO_WGRAD_UP", True, "transposed-conv weight gradients (Cin % 256 == 0) on the dense LDS-DMA GEMM "
+         "(csrc/wgrad_gemm.hip up mode) instead of the register-staged split-K kernel"),
     Knob("wgrad_band", "DPA_NO_WGRAD_BAND", True, "deep weight gradients with the input band staged once for all 9 taps (csrc/wgrad_band.hip)"),
     Knob("side_wgrad", "DPA_NO_SIDE_WGRAD", True, "weight gradients on a side HIP stream, overlapping the dgrad chain"),
     # fusions
@@ -169,6 +171,7 @@ class KernelConfig:
     slpp: bool = True
     slp256: bool = False
     slp64: bool = False
+    wgrad_up: bool = True
     chunk_sink: bool = True
     halo_cfg: int = 0
     wgrad_presum_y: int = 0

@@ -432,6 +432,9 @@ def wgrad(A: torch.Tensor, B: torch.Tensor, *, kind: int, grid, M: int, Nc: int,
     if (path == "gemm" or (path == "auto" and wgrad_gemm_eligible(M, Nc, grid))) and kind == 0 and cfg == 0 \
             and A.shape[1:3] == B.shape[1:3] == tuple(grid[1:]):
         return _wgrad_gemm(A, B, grid=grid, M=M, Nc=Nc, gw=gw, gb=gb, Nreal=Nreal)
+    if (path == "up" or (path == "auto" and wgrad_up_eligible(M, Nc, grid))) and kind == 1 and cfg == 0 \
+            and A.shape[1:3] == (2 * grid[1], 2 * grid[2]) and Nreal == Nc:
+        return _wgrad_up(A, B, grid=grid, M=M, Nc=Nc, gw=gw, gb=gb, Nreal=Nreal)
     if path in ("auto", "stream") and kind == 0 and cfg == 0 and (USE_STREAM or path == "stream") \
             and grid[2] >= 8 and M % 32 == 0 and (Nc % 32 == 0 or Nc == 8):
         return _wgrad_stream(A, B, grid=grid, M=M, Nc=Nc, gw=gw, gb=gb, Nreal=Nreal)
@@ -538,6 +541,54 @@ def _wgrad_gemm(A, B, *, grid, M, Nc, gw, gb, Nreal, blocks: int = 0, tabs=None,
     _check(L.dpa_wgrad_gemm(ctypes.byref(a), st), "wgrad_gemm")
     _check(L.dpa_wgrad_reduce(_p(slab), _p(bslab), _p(gw), _p(gb), c_int(splits), c_int(9), c_int(M), c_int(Nc),
                               c_int(Nreal), c_int(0), st), "wgrad_reduce(gemm)")
+
+
+# transposed-conv (k2 s2) weight gradients on the dense LDS-DMA GEMM (csrc/wgrad_gemm.hip up mode) instead of the
+# register-staged split-K kernel; DPA_NO_WGRAD_UP=1 falls back
+USE_WGRAD_UP = CFG.wgrad_up
+
+
+def wgrad_up_eligible(Cout: int, Cin: int, grid) -> bool:
+    """Can the transposed conv Cin -> Cout on the low-resolution ``grid`` take :func:`_wgrad_up`?"""
+    N, h, w = grid
+    spi = h * w // 64
+    # one workgroup per (image, tile) at most: with fewer than 128 of them the split-K kernel is faster
+    # (UNet-XL 1024^2 b16, 256 -> 128: 32 workgroups, 409 vs 209 us; profiles/kbench_deconv_wgrad_up_r06.txt)
+    tiles = (Cin // 256) * (4 * Cout // 256) if Cin % 256 == 0 and (4 * Cout) % 256 == 0 else 0
+    return (USE_WGRAD_UP and tiles > 0 and N * tiles >= 128 and Cout % 8 == 0 and (h * w) % 64 == 0
+            and (w % 64 == 0 or (w < 64 and 64 % w == 0)) and spi >= 2)
+
+
+def _wgrad_up(A, B, *, grid, M, Nc, gw, gb, Nreal):
+    """Weight (+bias) gradient of a transposed conv k2 s2 (``A`` = output gradient [N, 2h, 2w, >= M], M = Cout;
+    ``B`` = layer input [N, h, w, >= Nc], Nc = Cin) as the dense GEMM dW[ci][tap][co] = sum_p x[p][ci] *
+    g[2p + tap][co] (wgrad_gemm.hip up mode: the input is the GEMM's A operand, the gradient the 4-tap B
+    operand); slab rows [split][tap][Cin][Cout] reduced straight into the ConvTranspose2d layout.  The bias
+    gradient (no bias column in that kernel) is a per-channel sum of the gradient (dpa_chan_sum_bf16)."""
+    NA, HA, WA, CA, lda = _nhwc(A, "wgrad_up.A")
+    NB, HB, WB, CB, ldb = _nhwc(B, "wgrad_up.B")
+    N, h, w = grid
+    assert NA == NB == N and (HA, WA) == (2 * h, 2 * w) and (HB, WB) == (h, w) and CA >= M and CB >= Nc
+    assert Nreal == Nc and gw.dtype == torch.float32 and gw.is_contiguous() and gw.numel() == M * Nc * 4
+    tiles = (Nc // 256) * (4 * M // 256)
+    spi = h * w // 64
+    ips = max(1, -(-N * tiles // WGRAD_GEMM_BLOCKS), -(-2 // spi))
+    ips = max(1, min(ips, _MAX_BYTES // (4 * h * w * max(lda, ldb) * 2)))
+    splits = -(-N // ips)
+    slab = torch.empty(splits * 4 * Nc * M, dtype=torch.float32, device=A.device)
+    a = WgradArgs(B.data_ptr(), A.data_ptr(), slab.data_ptr(), None, ldb, lda, N, h, w, h, w, 2 * h, 2 * w, Nc, M,
+                  2, 0, 2, ips, splits, ips * h * w * ldb * 2, ips * 4 * h * w * lda * 2)
+    L = _lib.lib()
+    st = _stream(A)
+    _check(L.dpa_wgrad_gemm(ctypes.byref(a), st), "wgrad_gemm(up)")
+    _check(L.dpa_wgrad_reduce(_p(slab), None, _p(gw), None, c_int(splits), c_int(4), c_int(Nc), c_int(M), c_int(M),
+                              c_int(0), st), "wgrad_reduce(up)")
+    if gb is not None:
+        P = N * 4 * h * w
+        nblk = max(1, min(1024, P * (M // 8) // 4096))
+        part = torch.empty(nblk * M, dtype=torch.float32, device=A.device)
+        _check(L.dpa_chan_sum_bf16(_p(A), ctypes.c_longlong(P), c_int(M), c_int(lda), _p(part), c_int(nblk), _p(gb),
+                                   st), "chan_sum_bf16")
 
 
 # deep-layer weight gradients with the input band staged once for all nine taps (csrc/wgrad_band.hip):

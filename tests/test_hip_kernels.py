@@ -881,3 +881,30 @@ def test_wgrad_reduce_many_splits(hip_lib, splits, T, M, Nc, Nreal):
     torch.cuda.synchronize()
     assert _rel(gw.cpu().double().view(M, Nreal, T) - 1.0, ref_w) < 1e-5
     assert _rel(gb.cpu().double() - 1.0, ref_b) < 1e-5
+
+
+@pytest.mark.parametrize("N,h,w,Cin,Cout,half", [(64, 32, 32, 256, 128, True), (16, 16, 64, 512, 256, False),
+                                                  (128, 16, 16, 256, 64, True), (8, 8, 32, 1024, 512, False)])
+def test_wgrad_up_matches_split_k(hip_lib, N, h, w, Cin, Cout, half):
+    """Transposed-conv weight + bias gradient on the dense GEMM (wgrad_gemm.hip up mode: x as the A operand,
+    the gradient as a 4-tap B operand at (2h + i, 2w + j), no padding; bias from dpa_chan_sum_bf16) equals the
+    split-K kernel's (cfg 14) up to fp32 summation order, with the gradient a concat half (ld = 2 Cout) or dense."""
+    from distributedpytorch_amd.ops import kernels as K
+    torch.manual_seed(11)
+    x = torch.randn(N, h, w, Cin, device="cuda").to(torch.bfloat16)
+    full = torch.randn(N, 2 * h, 2 * w, 2 * Cout if half else Cout, device="cuda").to(torch.bfloat16)
+    g = full[..., Cout:] if half else full
+    assert K.wgrad_up_eligible(Cout, Cin, (N, h, w))
+    outs = []
+    for cfg in (0, 14):
+        gw = torch.randn(Cin * Cout * 4, device="cuda")          # accumulates: start from the same values
+        gb = torch.randn(Cout, device="cuda")
+        gw0, gb0 = gw.clone(), gb.clone()
+        K.wgrad(g, x, kind=1, grid=(N, h, w), M=Cout, Nc=Cin, s=2, pad=0, KW=2, gw=gw, gb=gb, Nreal=Cin, cfg=cfg)
+        torch.cuda.synchronize()
+        outs.append((gw - gw0, gb - gb0))
+    (dw, db), (rw, rb) = outs
+    ref = torch.einsum("nhwc,nhiwjo->coij", x.float(), g.float().view(N, h, 2, w, 2, Cout)).reshape(-1)
+    assert ((dw - ref).abs().max() / ref.abs().max()).item() < 1e-4
+    assert ((dw - rw).abs().max() / rw.abs().max()).item() < 1e-4
+    assert ((db - rb).abs().max() / rb.abs().max()).item() < 1e-4
